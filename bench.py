@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Headline benchmark: LightGBMClassifier boosting throughput on a Higgs-shape
+synthetic dataset (11M rows x 28 float features per GPU), 1..8 MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1
+it is launched under torch.distributed.run with one rank per GPU. One step =
+one boosting iteration (gradients -> 31-leaf tree -> score update) over the
+full training matrix at the reference's defaults (numLeaves 31, maxBin 255,
+learningRate 0.1, minDataInLeaf 20, binary objective). W untimed warmup
+iterations, then exactly K timed iterations bracketed by barrier + device
+synchronize; time is the max over ranks. ``value`` = total rows x K / seconds
+(whole job). Data is synthetic (no datasets are downloadable here); per-GPU
+work is fixed as N grows (weak scaling): N=8 trains on 88M rows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rows/sec LightGBMClassifier 11M×28 Higgs-shape synthetic; 1/2/4/8 MI355X"
+
+
+def higgs_like(n: int, f: int, seed: int):
+    """Higgs-shape synthetic: 21 'low-level' heavy-tailed kinematic features
+    and 7 'high-level' nonlinear combinations; label from a noisy nonlinear
+    score (roughly balanced, AUC ceiling well below 1 like HIGGS)."""
+    rng = np.random.default_rng(seed)
+    low = f - 7 if f > 7 else f
+    X = np.empty((n, f), dtype=np.float32)
+    X[:, :low] = rng.standard_normal((n, low), dtype=np.float32)
+    X[:, 0:low:3] = np.abs(X[:, 0:low:3]) * 1.5  # pt-like, positive
+    for j in range(low, f):
+        a, b = (j * 7) % low, (j * 11 + 3) % low
+        X[:, j] = np.sqrt(X[:, a] ** 2 + X[:, b] ** 2 + 1.0) + 0.1 * rng.standard_normal(n, dtype=np.float32)
+    s = (0.8 * X[:, 0] - 0.6 * X[:, 1] * X[:, 2] + 0.5 * np.sin(X[:, 3] * 2) + 0.4 * X[:, low] - 0.3 * X[:, low + 1]
+         + 0.25 * (X[:, 4] > 0.5)) if f > 7 else X[:, 0]
+    s = s - np.median(s)
+    y = (s + 1.2 * rng.standard_normal(n, dtype=np.float32) > 0).astype(np.float32)
+    return X, y
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=11_000_000, help="rows per GPU (weak scaling)")
+    ap.add_argument("--features", type=int, default=28)
+    ap.add_argument("--leaves", type=int, default=31)
+    ap.add_argument("--device", default="gpu")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = args.device == "gpu" and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+    from synapseml_amd.parallel import distributed as D
+
+    if world > 1:
+        D.init_from_env("nccl" if use_gpu else "gloo")
+    from synapseml_amd.ops import native
+
+    g = native.gbdt()
+    t_setup = time.perf_counter()
+    X, y = higgs_like(args.rows, args.features, seed=1234 + rank)
+    params = (f"objective=binary num_iterations={args.warmup + args.steps} learning_rate=0.1 "
+              f"num_leaves={args.leaves} max_bin=255 min_data_in_leaf=20 bin_construct_sample_cnt=200000 "
+              f"device_type={'gpu' if use_gpu else 'cpu'} num_machines={world} tree_learner=data metric=auc")
+    names = [f"f{i}" for i in range(args.features)]
+    # shared bin boundaries: rank 0 samples, broadcasts the serialized reference
+    ser = None
+    if rank == 0:
+        rng = np.random.default_rng(1)
+        idx = np.sort(rng.choice(args.rows, size=min(200_000, args.rows), replace=False))
+        ser = bytes(g.DatasetReference.from_sample(X[idx].astype(np.float64), args.rows * world, params, names)
+                    .serialize())
+    ser = D.broadcast_object(ser, 0)
+    ref = g.DatasetReference.deserialize(ser)
+    ds = g.Dataset(ref, args.rows)
+    chunk = 1 << 20
+    for s in range(0, args.rows, chunk):
+        ds.push_dense(X[s: s + chunk], s)
+    ds.set_label(y)
+    n_hold = min(200_000, args.rows)
+    X_hold, y_hold = X[:n_hold].astype(np.float64), y[:n_hold]
+    del X
+    comm = D.gbdt_comm(use_gpu) if world > 1 else None
+    booster = g.Booster(ds, params, comm)
+    setup_s = time.perf_counter() - t_setup
+
+    def sync():
+        booster.synchronize()
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        booster.update()
+    sync()
+    D.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        booster.update()
+    sync()
+    D.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    el = np.array([elapsed], dtype=np.float64)
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor(el, device="cuda" if use_gpu else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # sanity: holdout AUC of the trained model (outside the timed region)
+    auc = None
+    if rank == 0:
+        try:
+            from sklearn.metrics import roc_auc_score
+
+            p = booster.predict(X_hold, 0, 0, -1)[:, 0]
+            auc = float(roc_auc_score(y_hold, p))
+        except Exception:  # pragma: no cover
+            auc = None
+    total_rows = args.rows * world
+    value = total_rows * args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "rows/s (row-iterations per second, whole job)",
+            "n_gpus": world if use_gpu else 0,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32 gradients / fp64 histogram sums (reference LightGBM: fp32 grads, fp64 hist)",
+            "data": "synthetic Higgs-shape (21 heavy-tailed + 7 derived float features), random labels w/ noise",
+            "config": {
+                "model": "LightGBMClassifier(binary, numLeaves=%d, maxBin=255, lr=0.1, minDataInLeaf=20)" % args.leaves,
+                "global_batch": total_rows,
+                "seq_len": args.features,
+                "parallelism": f"dp{world}",
+                "rows_per_gpu": args.rows,
+                "backend": booster.backend,
+                "train_auc_sample": auc,
+                "setup_s": round(setup_s, 2),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,64 @@
+// Training backends: where histograms, split search, row partitioning and
+// score updates run. The CPU backend is the oracle / no-GPU path (SURVEY §7.0
+// D4); the HIP backend keeps the binned matrix, gradients, scores and the
+// whole leaf-wise growth loop resident on the MI355X.
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "comm.h"
+#include "config.h"
+#include "dataset.h"
+#include "objective.h"
+#include "split_math.h"
+#include "tree.h"
+
+namespace sml {
+
+struct TrainStats {
+  double hist_ms = 0, split_ms = 0, partition_ms = 0, grad_ms = 0, score_ms = 0, comm_ms = 0;
+  int64_t trees = 0;
+};
+
+class TrainBackend {
+ public:
+  virtual ~TrainBackend() = default;
+  virtual std::string Name() const = 0;
+  virtual void Init(const Dataset* data, const Config& cfg, int num_tree_per_iter) = 0;
+  virtual void SetScores(const std::vector<double>& s) = 0;  // class-major n*K
+  virtual void GetScores(std::vector<double>* s) = 0;
+  virtual void AddBias(int k, double b) = 0;
+  virtual void ScaleScore(int k, double s) = 0;
+  virtual void ComputeGradients(const Objective& obj) = 0;
+  virtual void SetGradients(const float* g, const float* h) = 0;  // class-major n*K
+  virtual void GetGradients(std::vector<float>* g, std::vector<float>* h) = 0;
+  // Restrict training rows (bagging/GOSS). nullptr = all rows.
+  virtual void SetBag(const std::vector<int32_t>* rows) = 0;
+  virtual Tree TrainTree(int k, const std::vector<char>& feature_mask) = 0;
+  // score[k] += scale * tree(row) for every training row
+  virtual void UpdateScore(const Tree& t, int k, double scale) = 0;
+  // Leaf index of every training row for `t` (renew / DART helpers).
+  virtual void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) = 0;
+  virtual void Synchronize() {}
+  void SetComm(Comm* c) { comm_ = c; }
+  Comm* comm() const { return comm_; }
+  TrainStats stats;
+
+ protected:
+  Comm* comm_ = nullptr;
+};
+
+std::unique_ptr<TrainBackend> MakeCpuBackend();
+// Defined in the HIP translation unit; returns nullptr if no device.
+std::unique_ptr<TrainBackend> MakeGpuBackend(int device_id);
+bool GpuAvailable();
+
+// Host reference of the split search (K5): best split of one feature given its
+// histogram. Used by the CPU backend and by tests that compare the device.
+void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinMapper& m,
+                          int feature_inner, double sum_g, double sum_h, int64_t cnt,
+                          const SplitParams& sp, SplitResult* best);
+SplitParams MakeSplitParams(const Config& cfg);
+
+}  // namespace sml

@@ -1,0 +1,377 @@
+// CPU training backend: OpenMP histogram construction + host split search.
+// It is the numerical oracle for the HIP kernels and the runtime for hosts
+// without an MI355X (BASELINE config 1, "local[2] CPU plumbing").
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <stdexcept>
+
+#include "backend.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace sml {
+
+SplitParams MakeSplitParams(const Config& c) {
+  SplitParams p;
+  p.lambda_l1 = c.lambda_l1; p.lambda_l2 = c.lambda_l2; p.max_delta_step = c.max_delta_step;
+  p.min_gain_to_split = c.min_gain_to_split; p.min_sum_hessian = c.min_sum_hessian_in_leaf;
+  p.min_data_in_leaf = c.min_data_in_leaf; p.num_leaves = c.num_leaves; p.max_depth = c.max_depth;
+  p.cat_l2 = c.cat_l2; p.cat_smooth = c.cat_smooth; p.max_cat_threshold = c.max_cat_threshold;
+  p.max_cat_to_onehot = c.max_cat_to_onehot; p.min_data_per_group = c.min_data_per_group;
+  return p;
+}
+
+static void ConsiderSplit(double gl, double hl, double gr, double hr, int64_t cl, int64_t cr,
+                          double parent_gain, const SplitParams& sp, double l2, int feature,
+                          uint32_t thr, int default_left, SplitResult* best) {
+  if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
+  if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
+  const double gain = LeafGain(gl, hl, sp.lambda_l1, l2, sp.max_delta_step) +
+                      LeafGain(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+  const double shift = parent_gain + sp.min_gain_to_split;
+  if (!(gain > shift)) return;
+  const double sg = gain - shift;
+  if (best->feature >= 0 && !SplitBetter(sg, feature, thr, best->gain, best->feature, best->threshold)) return;
+  best->gain = sg;
+  best->feature = feature;
+  best->threshold = thr;
+  best->default_left = default_left;
+  best->is_cat = 0;
+  best->left_g = gl; best->left_h = hl; best->right_g = gr; best->right_h = hr;
+  best->left_cnt = cl; best->right_cnt = cr;
+  best->left_out = LeafOutput(gl, hl, sp.lambda_l1, l2, sp.max_delta_step);
+  best->right_out = LeafOutput(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+}
+
+void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinMapper& m,
+                          int fi, double G, double H, int64_t cnt, const SplitParams& sp,
+                          SplitResult* best) {
+  const double cnt_factor = cnt / std::max(H, kEpsilon);
+  const double parent_gain = LeafGain(G, H, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
+  if (m.is_categorical) {
+    // one-vs-rest for few categories, otherwise sorted-by-ratio prefix search
+    const int other = nb - 1;
+    const double l2 = sp.lambda_l2 + sp.cat_l2;
+    const double cat_parent = LeafGain(G, H, sp.lambda_l1, l2, sp.max_delta_step);
+    SplitResult local = *best;
+    bool found = false;
+    auto try_set = [&](const std::vector<int>& left_bins, double gl, double hl) {
+      const double gr = G - gl, hr = H - hl;
+      const int64_t cl = EstimateCount(hl, cnt_factor), cr = cnt - cl;
+      if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
+      if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
+      if (static_cast<int>(left_bins.size()) > 1 && (cl < sp.min_data_per_group || cr < sp.min_data_per_group)) return;
+      const double gain = LeafGain(gl, hl, sp.lambda_l1, l2, sp.max_delta_step) +
+                          LeafGain(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+      const double shift = cat_parent + sp.min_gain_to_split;
+      if (!(gain > shift)) return;
+      const double sg = gain - shift;
+      if (local.feature >= 0 && !SplitBetter(sg, fi, static_cast<uint32_t>(left_bins.size()), local.gain, local.feature, local.threshold)) return;
+      local.gain = sg; local.feature = fi; local.threshold = static_cast<uint32_t>(left_bins.size());
+      local.default_left = 0; local.is_cat = 1;
+      std::memset(local.cat_bits, 0, sizeof(local.cat_bits));
+      for (int b : left_bins) local.cat_bits[b / 32] |= 1u << (b % 32);
+      local.left_g = gl; local.left_h = hl; local.right_g = gr; local.right_h = hr;
+      local.left_cnt = cl; local.right_cnt = cr;
+      local.left_out = LeafOutput(gl, hl, sp.lambda_l1, l2, sp.max_delta_step);
+      local.right_out = LeafOutput(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+      found = true;
+    };
+    if (nb <= sp.max_cat_to_onehot + 1) {
+      for (int b = 0; b < other; ++b) try_set({b}, hg[b], hh[b]);
+    } else {
+      std::vector<int> idx;
+      for (int b = 0; b < other; ++b)
+        if (EstimateCount(hh[b], cnt_factor) >= sp.cat_smooth) idx.push_back(b);
+      std::stable_sort(idx.begin(), idx.end(), [&](int a, int c) {
+        return hg[a] / (hh[a] + sp.cat_smooth) < hg[c] / (hh[c] + sp.cat_smooth);
+      });
+      const int maxk = std::min<int>(sp.max_cat_threshold, (static_cast<int>(idx.size()) + 1) / 2);
+      for (int dir = 0; dir < 2; ++dir) {
+        std::vector<int> left;
+        double gl = 0, hl = 0;
+        for (int k = 0; k < static_cast<int>(idx.size()) && k < maxk; ++k) {
+          int b = dir == 0 ? idx[k] : idx[idx.size() - 1 - k];
+          left.push_back(b);
+          gl += hg[b]; hl += hh[b];
+          try_set(left, gl, hl);
+        }
+      }
+    }
+    if (found) *best = local;
+    return;
+  }
+  const int mt = m.missing_type;
+  const int nan_bin = (mt == kMissingNaN) ? nb - 1 : -1;
+  const int zero_bin = (mt == kMissingZero) ? m.default_bin : -1;
+  double mg = 0, mh = 0;  // missing bin sums
+  if (nan_bin >= 0) { mg = hg[nan_bin]; mh = hh[nan_bin]; }
+  if (zero_bin >= 0) { mg = hg[zero_bin]; mh = hh[zero_bin]; }
+  const int last = (nan_bin >= 0) ? nb - 2 : nb - 1;  // last ordered bin
+  double gl = 0, hl = 0;
+  for (int t = 0; t < last; ++t) {
+    if (t != zero_bin) { gl += hg[t]; hl += hh[t]; }
+    if (mt == kMissingNone) {
+      const int64_t cl = EstimateCount(hl, cnt_factor);
+      ConsiderSplit(gl, hl, G - gl, H - hl, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 1, best);
+    } else {
+      // missing -> right
+      {
+        const int64_t cl = EstimateCount(hl, cnt_factor);
+        ConsiderSplit(gl, hl, G - gl, H - hl, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 0, best);
+      }
+      // missing -> left
+      {
+        const double g2 = gl + mg, h2 = hl + mh;
+        const int64_t cl = EstimateCount(h2, cnt_factor);
+        ConsiderSplit(g2, h2, G - g2, H - h2, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 1, best);
+      }
+    }
+  }
+}
+
+namespace {
+
+struct LeafInfo {
+  int64_t begin = 0, count = 0;  // local row range
+  int64_t gcount = 0;            // global row count (all ranks)
+  double sum_g = 0, sum_h = 0;
+  int depth = 0;
+  SplitResult best;
+  bool has_best = false;
+};
+
+class CpuBackend : public TrainBackend {
+ public:
+  std::string Name() const override { return "cpu"; }
+  void Init(const Dataset* d, const Config& cfg, int K) override {
+    data_ = d; cfg_ = cfg; K_ = K; n_ = d->num_data;
+    sp_ = MakeSplitParams(cfg);
+    score_.assign(static_cast<size_t>(n_) * K, 0.0);
+    g_.assign(static_cast<size_t>(n_) * K, 0.f);
+    h_.assign(static_cast<size_t>(n_) * K, 0.f);
+    F_ = d->ref.num_inner();
+    nthreads_ = 1;
+#ifdef _OPENMP
+    nthreads_ = cfg.num_threads > 0 ? cfg.num_threads : omp_get_max_threads();
+#endif
+  }
+  void SetScores(const std::vector<double>& s) override { score_ = s; }
+  void GetScores(std::vector<double>* s) override { *s = score_; }
+  void AddBias(int k, double b) override {
+    for (int64_t i = 0; i < n_; ++i) score_[k * n_ + i] += b;
+  }
+  void ScaleScore(int k, double sc) override {
+    for (int64_t i = 0; i < n_; ++i) score_[k * n_ + i] *= sc;
+  }
+  void ComputeGradients(const Objective& obj) override { obj.GetGradients(score_.data(), g_.data(), h_.data()); }
+  void SetGradients(const float* g, const float* h) override {
+    std::memcpy(g_.data(), g, sizeof(float) * g_.size());
+    std::memcpy(h_.data(), h, sizeof(float) * h_.size());
+  }
+  void GetGradients(std::vector<float>* g, std::vector<float>* h) override { *g = g_; *h = h_; }
+  void SetBag(const std::vector<int32_t>* rows) override {
+    if (rows) { bag_ = *rows; use_bag_ = true; } else { bag_.clear(); use_bag_ = false; }
+  }
+
+  void BuildHist(int k, const LeafInfo& leaf, const std::vector<char>& fmask, std::vector<double>* hist) {
+    const int stride = 256 * 2;
+    hist->assign(static_cast<size_t>(F_) * stride, 0.0);
+    const float* g = g_.data() + static_cast<size_t>(k) * n_;
+    const float* h = h_.data() + static_cast<size_t>(k) * n_;
+    const int64_t cnt = leaf.count;
+    const int nt = std::max<int>(1, std::min<int64_t>(nthreads_, cnt / 4096 + 1));
+    std::vector<std::vector<double>> local(nt, std::vector<double>(hist->size(), 0.0));
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (int t = 0; t < nt; ++t) {
+      double* hl = local[t].data();
+      int64_t b = leaf.begin + cnt * t / nt, e = leaf.begin + cnt * (t + 1) / nt;
+      for (int64_t p = b; p < e; ++p) {
+        const int64_t r = idx_[p];
+        const uint8_t* row = &data_->bins[r * data_->row_stride];
+        const double gv = g[r], hv = h[r];
+        for (int f = 0; f < F_; ++f) {
+          if (!fmask[f]) continue;
+          double* c = hl + f * stride + row[f] * 2;
+          c[0] += gv; c[1] += hv;
+        }
+      }
+    }
+    for (int t = 0; t < nt; ++t)
+      for (size_t i = 0; i < hist->size(); ++i) (*hist)[i] += local[t][i];
+    if (comm_ && comm_->world() > 1) {
+      hist->push_back(static_cast<double>(leaf.count));
+      comm_->AllReduceHost(hist->data(), static_cast<int64_t>(hist->size()));
+      last_gcount_ = static_cast<int64_t>(hist->back());
+      hist->pop_back();
+    } else {
+      last_gcount_ = leaf.count;
+    }
+  }
+
+  void FindBest(const std::vector<double>& hist, LeafInfo* leaf, const std::vector<char>& fmask) {
+    SplitResult best{};
+    best.feature = -1;
+    best.gain = -std::numeric_limits<double>::infinity();
+    if (leaf->gcount >= 2 * sp_.min_data_in_leaf && (sp_.max_depth <= 0 || leaf->depth < sp_.max_depth)) {
+      std::vector<SplitResult> per(F_);
+      std::vector<double> tg(256), th(256);
+#pragma omp parallel for schedule(dynamic) firstprivate(tg, th)
+      for (int f = 0; f < F_; ++f) {
+        per[f].feature = -1;
+        per[f].gain = -std::numeric_limits<double>::infinity();
+        if (!fmask[f]) continue;
+        const BinMapper& m = data_->ref.mappers[data_->ref.used_features[f]];
+        for (int b = 0; b < m.num_bin; ++b) { tg[b] = hist[f * 512 + b * 2]; th[b] = hist[f * 512 + b * 2 + 1]; }
+        FindBestSplitFeature(tg.data(), th.data(), m.num_bin, m, f, leaf->sum_g, leaf->sum_h, leaf->gcount, sp_, &per[f]);
+      }
+      for (int f = 0; f < F_; ++f) {
+        if (per[f].feature < 0) continue;
+        if (best.feature < 0 || SplitBetter(per[f].gain, per[f].feature, per[f].threshold, best.gain, best.feature, best.threshold))
+          best = per[f];
+      }
+    }
+    leaf->best = best;
+    leaf->has_best = best.feature >= 0;
+  }
+
+  bool GoesLeft(const SplitResult& s, const uint8_t* row) const {
+    const uint32_t b = row[s.feature];
+    if (s.is_cat) return (s.cat_bits[b / 32] >> (b % 32)) & 1u;
+    const BinMapper& m = data_->ref.mappers[data_->ref.used_features[s.feature]];
+    if ((m.missing_type == kMissingZero && b == static_cast<uint32_t>(m.default_bin)) ||
+        (m.missing_type == kMissingNaN && b == static_cast<uint32_t>(m.num_bin - 1)))
+      return s.default_left != 0;
+    return b <= s.threshold;
+  }
+
+  Tree TrainTree(int k, const std::vector<char>& fmask_in) override {
+    std::vector<char> fmask = fmask_in;
+    if (static_cast<int>(fmask.size()) != F_) fmask.assign(F_, 1);
+    const int L = std::max(2, cfg_.num_leaves);
+    Tree tree(L);
+    // root
+    if (use_bag_) { idx_.assign(bag_.begin(), bag_.end()); }
+    else { idx_.resize(n_); std::iota(idx_.begin(), idx_.end(), 0); }
+    std::vector<LeafInfo> leaves(L);
+    std::vector<std::vector<double>> hists(L);
+    const float* g = g_.data() + static_cast<size_t>(k) * n_;
+    const float* h = h_.data() + static_cast<size_t>(k) * n_;
+    leaves[0].begin = 0; leaves[0].count = static_cast<int64_t>(idx_.size());
+    double G = 0, H = 0;
+#pragma omp parallel for reduction(+ : G, H)
+    for (int64_t p = 0; p < leaves[0].count; ++p) { G += g[idx_[p]]; H += h[idx_[p]]; }
+    {
+      double st[3] = {G, H, static_cast<double>(leaves[0].count)};
+      if (comm_) comm_->AllReduceHost(st, 3);
+      G = st[0]; H = st[1]; leaves[0].gcount = static_cast<int64_t>(st[2]);
+    }
+    leaves[0].sum_g = G; leaves[0].sum_h = H;
+    tree.leaf_value[0] = LeafOutput(G, H, sp_.lambda_l1, sp_.lambda_l2, sp_.max_delta_step);
+    tree.leaf_count[0] = leaves[0].gcount;
+    tree.leaf_weight[0] = H;
+    BuildHist(k, leaves[0], fmask, &hists[0]);
+    FindBest(hists[0], &leaves[0], fmask);
+    std::vector<int64_t> tmp;
+    for (int s = 1; s < L; ++s) {
+      int bl = -1;
+      for (int l = 0; l < tree.num_leaves; ++l) {
+        if (!leaves[l].has_best) continue;
+        if (bl < 0 || leaves[l].best.gain > leaves[bl].best.gain) bl = l;
+      }
+      if (bl < 0 || leaves[bl].best.gain <= 0) break;
+      const SplitResult sr = leaves[bl].best;
+      LeafInfo& P = leaves[bl];
+      // stable partition of the leaf's rows
+      tmp.resize(P.count);
+      int64_t nl = 0;
+      for (int64_t p = 0; p < P.count; ++p) {
+        const int64_t r = idx_[P.begin + p];
+        if (GoesLeft(sr, &data_->bins[r * data_->row_stride])) idx_[P.begin + nl++] = r; else tmp[p - nl] = r;
+      }
+      std::memcpy(&idx_[P.begin + nl], tmp.data(), sizeof(int64_t) * (P.count - nl));
+      const int fr = data_->ref.used_features[sr.feature];
+      const BinMapper& m = data_->ref.mappers[fr];
+      int right;
+      if (sr.is_cat) {
+        std::vector<uint32_t> binbits(8, 0), valbits;
+        int maxcat = 0;
+        for (int b = 0; b < m.num_bin - 1; ++b)
+          if ((sr.cat_bits[b / 32] >> (b % 32)) & 1u) { binbits[b / 32] |= 1u << (b % 32); maxcat = std::max(maxcat, m.bin2cat[b]); }
+        valbits.assign(maxcat / 32 + 1, 0);
+        for (int b = 0; b < m.num_bin - 1; ++b)
+          if ((sr.cat_bits[b / 32] >> (b % 32)) & 1u) valbits[m.bin2cat[b] / 32] |= 1u << (m.bin2cat[b] % 32);
+        right = tree.SplitCategorical(bl, sr.feature, fr, binbits, valbits, sr.left_out, sr.right_out,
+                                      sr.left_cnt, sr.right_cnt, sr.left_h, sr.right_h, sr.gain);
+      } else {
+        right = tree.Split(bl, sr.feature, fr, sr.threshold, m.BinToValue(sr.threshold), sr.default_left != 0,
+                           m.missing_type, sr.left_out, sr.right_out, sr.left_cnt, sr.right_cnt, sr.left_h, sr.right_h, sr.gain);
+      }
+      LeafInfo& Lf = leaves[bl];
+      LeafInfo& R = leaves[right];
+      const int depth = P.depth + 1;
+      R.begin = P.begin + nl; R.count = P.count - nl; R.sum_g = sr.right_g; R.sum_h = sr.right_h; R.depth = depth;
+      Lf.count = nl; Lf.sum_g = sr.left_g; Lf.sum_h = sr.left_h; Lf.depth = depth;
+      // smaller child (by the globally consistent estimate) gets a fresh
+      // histogram, the larger = parent - smaller
+      const int64_t pg = P.gcount;
+      const bool left_small = sr.left_cnt <= sr.right_cnt;
+      int small = left_small ? bl : right, large = left_small ? right : bl;
+      std::vector<double> parent = std::move(hists[bl]);
+      BuildHist(k, leaves[small], fmask, &hists[small]);
+      leaves[small].gcount = last_gcount_;
+      leaves[large].gcount = pg - last_gcount_;
+      hists[large].resize(parent.size());
+      for (size_t i = 0; i < parent.size(); ++i) hists[large][i] = parent[i] - hists[small][i];
+      FindBest(hists[bl], &leaves[bl], fmask);
+      FindBest(hists[right], &leaves[right], fmask);
+    }
+    // exact (global) leaf counts
+    for (int l = 0; l < tree.num_leaves; ++l) tree.leaf_count[l] = leaves[l].gcount;
+    return tree;
+  }
+
+  void UpdateScore(const Tree& t, int k, double scale) override {
+    double* s = score_.data() + static_cast<size_t>(k) * n_;
+    if (t.num_leaves <= 1) {
+      for (int64_t i = 0; i < n_; ++i) s[i] += scale * t.leaf_value[0];
+      return;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n_; ++i) {
+      int l = t.GetLeafByBins(&data_->bins[i * data_->row_stride], data_->ref.mappers, data_->ref.used_features);
+      s[i] += scale * t.leaf_value[l];
+    }
+  }
+
+  void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) override {
+    leaf->resize(n_);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n_; ++i)
+      (*leaf)[i] = t.GetLeafByBins(&data_->bins[i * data_->row_stride], data_->ref.mappers, data_->ref.used_features);
+  }
+
+ private:
+  const Dataset* data_ = nullptr;
+  Config cfg_;
+  SplitParams sp_{};
+  int K_ = 1, F_ = 0, nthreads_ = 1;
+  int64_t n_ = 0;
+  std::vector<double> score_;
+  std::vector<float> g_, h_;
+  std::vector<int64_t> idx_;
+  std::vector<int32_t> bag_;
+  bool use_bag_ = false;
+  int64_t last_gcount_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<TrainBackend> MakeCpuBackend() { return std::unique_ptr<TrainBackend>(new CpuBackend()); }
+
+}  // namespace sml

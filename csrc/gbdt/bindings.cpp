@@ -1,0 +1,256 @@
+// pybind11 module `synapseml_amd._gbdt`: Python surface of the native GBDT
+// engine (dataset / booster / collectives). Replaces the reference's SWIG
+// lightgbmlib bindings (lightgbm/.../swig/SwigUtils.scala) with zero-copy
+// numpy buffers instead of per-element setItem calls (SURVEY §3.1 hot loop 1).
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <stdexcept>
+
+#include "backend.h"
+#include "booster.h"
+#include "comm.h"
+#include "dataset.h"
+#include "predictor.h"
+
+namespace py = pybind11;
+using namespace sml;
+
+namespace {
+
+using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
+using F32 = py::array_t<float, py::array::c_style | py::array::forcecast>;
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+
+struct PyDataset {
+  std::shared_ptr<Dataset> d;
+};
+
+struct PyComm {
+  std::shared_ptr<Comm> c;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_gbdt, m) {
+  m.doc() = "MI355X-native gradient boosting engine (HIP kernels + RCCL)";
+  m.def("gpu_available", &GpuAvailable);
+
+  py::class_<DatasetReference, std::shared_ptr<DatasetReference>>(m, "DatasetReference")
+      .def_static("from_sample",
+                  [](F64 sample, int64_t total_rows, const std::string& params, std::vector<std::string> names) {
+                    auto b = sample.request();
+                    if (b.ndim != 2) throw std::runtime_error("sample must be 2-D");
+                    Config cfg = Config::Parse(params);
+                    py::gil_scoped_release rel;
+                    return std::make_shared<DatasetReference>(DatasetReference::FromSample(
+                        static_cast<const double*>(b.ptr), b.shape[0], static_cast<int>(b.shape[1]), total_rows, cfg, names));
+                  })
+      .def_static("from_sampled_columns",
+                  [](std::vector<std::vector<double>> cols, int64_t total, const std::string& params,
+                     std::vector<std::string> names) {
+                    Config cfg = Config::Parse(params);
+                    return std::make_shared<DatasetReference>(DatasetReference::FromSampledColumns(cols, total, cfg, names));
+                  })
+      .def("serialize", [](const DatasetReference& r) { return py::bytes(r.Serialize()); })
+      .def_static("deserialize", [](py::bytes b) { return std::make_shared<DatasetReference>(DatasetReference::Deserialize(b)); })
+      .def_property_readonly("num_total_features", [](const DatasetReference& r) { return r.num_total_features; })
+      .def_property_readonly("num_used_features", [](const DatasetReference& r) { return r.num_inner(); })
+      .def_property_readonly("feature_names", [](const DatasetReference& r) { return r.feature_names; })
+      .def("feature_infos", [](const DatasetReference& r) {
+        std::vector<std::string> v;
+        for (auto& mm : r.mappers) v.push_back(mm.FeatureInfo());
+        return v;
+      })
+      .def("num_bins", [](const DatasetReference& r) {
+        std::vector<int> v;
+        for (auto& mm : r.mappers) v.push_back(mm.num_bin);
+        return v;
+      })
+      .def("upper_bounds", [](const DatasetReference& r, int f) { return r.mappers.at(f).upper_bounds; })
+      .def("value_to_bin", [](const DatasetReference& r, int f, double v) { return r.mappers.at(f).ValueToBin(v); });
+
+  py::class_<PyDataset>(m, "Dataset")
+      .def(py::init([](std::shared_ptr<DatasetReference> ref, int64_t n) {
+        PyDataset p;
+        p.d = std::make_shared<Dataset>();
+        p.d->Init(*ref, n);
+        return p;
+      }))
+      .def("push_dense",
+           [](PyDataset& p, py::array X, int64_t start) {
+             auto b = X.request();
+             if (b.ndim != 2) throw std::runtime_error("rows must be 2-D");
+             if (start < 0 || start + b.shape[0] > p.d->num_data) throw std::runtime_error("push_dense out of range");
+             if (b.format == py::format_descriptor<float>::format()) {
+               F32 a = py::cast<F32>(X);
+               py::gil_scoped_release rel;
+               p.d->PushDenseF32(a.data(), a.shape(0), static_cast<int>(a.shape(1)), start);
+             } else {
+               F64 a = py::cast<F64>(X);
+               py::gil_scoped_release rel;
+               p.d->PushDense(a.data(), a.shape(0), static_cast<int>(a.shape(1)), start);
+             }
+           })
+      .def("push_csr",
+           [](PyDataset& p, I64 indptr, I32 indices, F64 values, int64_t start) {
+             const int64_t nrows = indptr.shape(0) - 1;
+             if (start < 0 || start + nrows > p.d->num_data) throw std::runtime_error("push_csr out of range");
+             py::gil_scoped_release rel;
+             p.d->PushCSR(indptr.data(), indices.data(), values.data(), nrows, start);
+           })
+      .def("set_label", [](PyDataset& p, F32 y) {
+        if (y.size() != p.d->num_data) throw std::runtime_error("label size mismatch");
+        p.d->label.assign(y.data(), y.data() + y.size());
+      })
+      .def("set_weight", [](PyDataset& p, F32 w) {
+        if (w.size() != p.d->num_data) throw std::runtime_error("weight size mismatch");
+        p.d->weight.assign(w.data(), w.data() + w.size());
+      })
+      .def("set_init_score", [](PyDataset& p, F64 s) { p.d->init_score.assign(s.data(), s.data() + s.size()); })
+      .def("set_group", [](PyDataset& p, I32 sizes) {
+        std::vector<int32_t> v(sizes.data(), sizes.data() + sizes.size());
+        p.d->SetQueryFromGroupSizes(v);
+      })
+      .def_property_readonly("num_data", [](const PyDataset& p) { return p.d->num_data; })
+      .def_property_readonly("num_features", [](const PyDataset& p) { return p.d->ref.num_total_features; })
+      .def("get_label", [](const PyDataset& p) { return py::array_t<float>(p.d->label.size(), p.d->label.data()); })
+      .def("get_bins", [](const PyDataset& p) {
+        return py::array_t<uint8_t>({p.d->num_data, static_cast<int64_t>(p.d->row_stride)}, p.d->bins.data());
+      });
+
+  py::class_<PyComm>(m, "Comm")
+      .def_property_readonly("rank", [](const PyComm& c) { return c.c->rank(); })
+      .def_property_readonly("world", [](const PyComm& c) { return c.c->world(); })
+      .def("allreduce_host", [](PyComm& c, py::array_t<double> a) {
+        auto b = a.request();
+        c.c->AllReduceHost(static_cast<double*>(b.ptr), b.size);
+      });
+  m.def("host_comm", [](int rank, int world, std::function<void(py::array_t<double>)> fn) {
+    PyComm c;
+    c.c = std::make_shared<HostComm>(rank, world, [fn](double* buf, int64_t n) {
+      py::gil_scoped_acquire acq;
+      py::array_t<double> a({n}, {sizeof(double)}, buf, py::none());
+      fn(a);
+    });
+    return c;
+  });
+  m.def("rccl_unique_id", []() { return py::bytes(RcclGetUniqueId()); });
+  m.def("rccl_comm", [](py::bytes uid, int rank, int world, int device) {
+    PyComm c;
+    c.c.reset(NewRcclComm(std::string(uid), rank, world, device));
+    return c;
+  });
+
+  py::class_<Booster, std::shared_ptr<Booster>>(m, "Booster")
+      .def(py::init([](PyDataset& d, const std::string& params, py::object comm) {
+             Comm* c = nullptr;
+             std::shared_ptr<Comm> keep;
+             if (!comm.is_none()) { keep = comm.cast<PyComm&>().c; c = keep.get(); }
+             py::gil_scoped_release rel;
+             auto b = std::make_shared<Booster>(d.d, params, c);
+             return b;
+           }),
+           py::arg("train"), py::arg("params"), py::arg("comm") = py::none(), py::keep_alive<1, 4>())
+      .def_static("from_model_string", [](const std::string& s) { return std::shared_ptr<Booster>(Booster::FromModelString(s)); })
+      .def("add_valid", [](Booster& b, PyDataset& d, const std::string& name) { b.AddValidData(d.d, name); })
+      .def("merge", &Booster::MergeFrom)
+      .def("reset_parameter", &Booster::ResetParameter)
+      .def("update",
+           [](Booster& b, py::object g, py::object h) {
+             if (g.is_none()) { py::gil_scoped_release rel; return b.TrainOneIter(); }
+             F32 ga = py::cast<F32>(g), ha = py::cast<F32>(h);
+             py::gil_scoped_release rel;
+             return b.TrainOneIter(ga.data(), ha.data());
+           },
+           py::arg("grad") = py::none(), py::arg("hess") = py::none())
+      .def("rollback_one_iter", &Booster::RollbackOneIter)
+      .def("eval", &Booster::Eval)
+      .def("eval_names", &Booster::EvalNames)
+      .def("truncate", &Booster::Truncate)
+      .def("synchronize", [](Booster& b) { py::gil_scoped_release rel; b.Synchronize(); })
+      .def("train_scores", [](Booster& b) {
+        std::vector<double> s;
+        b.GetTrainScores(&s);
+        return py::array_t<double>(s.size(), s.data());
+      })
+      .def("valid_scores", [](const Booster& b, int i) {
+        std::vector<double> s;
+        b.GetPredictForValid(i, &s);
+        return py::array_t<double>(s.size(), s.data());
+      })
+      .def("save_model_string", &Booster::SaveModelToString, py::arg("start_iteration") = 0,
+           py::arg("num_iteration") = -1, py::arg("importance_type") = 0)
+      .def("dump_model", &Booster::DumpModel, py::arg("start_iteration") = 0, py::arg("num_iteration") = -1)
+      .def("predict",
+           [](const Booster& b, F64 X, int type, int start, int num) {
+             if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
+             const int64_t n = X.shape(0);
+             const int osz = b.PredictOutputSize(type, start, num);
+             py::array_t<double> out({n, static_cast<int64_t>(osz)});
+             double* o = out.mutable_data();
+             const double* x = X.data();
+             const int nc = static_cast<int>(X.shape(1));
+             {
+               py::gil_scoped_release rel;
+               b.Predict(x, n, nc, type, start, num, o);
+             }
+             return out;
+           },
+           py::arg("X"), py::arg("predict_type") = 0, py::arg("start_iteration") = 0, py::arg("num_iteration") = -1)
+      .def("feature_importance", &Booster::FeatureImportance, py::arg("num_iteration") = -1, py::arg("importance_type") = 0)
+      .def_property_readonly("num_classes", &Booster::NumClasses)
+      .def_property_readonly("num_model_per_iteration", &Booster::NumModelPerIteration)
+      .def_property_readonly("num_features", &Booster::NumFeatures)
+      .def_property_readonly("num_total_model", &Booster::NumTotalModel)
+      .def_property_readonly("current_iteration", &Booster::CurrentIteration)
+      .def_property_readonly("feature_names", &Booster::FeatureNames)
+      .def_property_readonly("backend", &Booster::BackendName)
+      .def("stats", [](Booster& b) {
+        py::dict d;
+        TrainStats* s = b.stats();
+        if (s) {
+          d["grad_ms"] = s->grad_ms; d["hist_ms"] = s->hist_ms; d["split_ms"] = s->split_ms;
+          d["partition_ms"] = s->partition_ms; d["score_ms"] = s->score_ms; d["comm_ms"] = s->comm_ms;
+          d["trees"] = s->trees;
+        }
+        return d;
+      });
+
+  py::class_<GpuPredictor, std::shared_ptr<GpuPredictor>>(m, "GpuPredictor")
+      .def(py::init([](const Booster& b, int start, int num, int device) {
+             return std::make_shared<GpuPredictor>(b, start, num, device);
+           }),
+           py::arg("booster"), py::arg("start_iteration") = 0, py::arg("num_iteration") = -1, py::arg("device") = -1,
+           py::keep_alive<1, 2>())
+      .def("predict",
+           [](GpuPredictor& p, F64 X, bool normal) {
+             const int64_t n = X.shape(0);
+             py::array_t<double> out({n, static_cast<int64_t>(p.NumOutputs())});
+             double* o = out.mutable_data();
+             const double* x = X.data();
+             const int nc = static_cast<int>(X.shape(1));
+             {
+               py::gil_scoped_release rel;
+               p.Predict(x, n, nc, normal, o);
+             }
+             return out;
+           },
+           py::arg("X"), py::arg("normal") = false)
+      .def("predict_leaf", [](GpuPredictor& p, F64 X) {
+        const int64_t n = X.shape(0);
+        py::array_t<int32_t> out({n, static_cast<int64_t>(p.NumTrees())});
+        int32_t* o = out.mutable_data();
+        const double* x = X.data();
+        const int nc = static_cast<int>(X.shape(1));
+        {
+          py::gil_scoped_release rel;
+          p.PredictLeaf(x, n, nc, o);
+        }
+        return out;
+      });
+}

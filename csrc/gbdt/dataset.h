@@ -1,0 +1,111 @@
+// Binned training dataset (native component N1 of SURVEY.md §2.3).
+//
+// Reference behaviour being reproduced: the reference builds LightGBM bin
+// mappers from a driver-side row sample (lightgbm/.../dataset/
+// ReferenceDatasetUtils.scala:14-71, LGBM_DatasetCreateFromSampledColumn),
+// serialises them to bytes (":52") and lets every executor push rows into a
+// Dataset initialised from that reference (":73-97", StreamingPartitionTask
+// .scala:202-277). Here the bin matrix is a row-major uint8 array padded to a
+// multiple of 4 features, so a HIP kernel can fetch 4 feature bins per dword
+// and a gathered row (leaf index lists) is one contiguous 4*k byte segment.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <limits>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "config.h"
+
+namespace sml {
+
+constexpr double kZeroThreshold = 1e-35;
+enum MissingType : int { kMissingNone = 0, kMissingZero = 1, kMissingNaN = 2 };
+
+struct BinMapper {
+  int num_bin = 1;
+  int missing_type = kMissingNone;
+  bool is_categorical = false;
+  bool is_trivial = true;
+  int default_bin = 0;   // bin that holds 0.0
+  double min_val = 0.0, max_val = 0.0;
+  std::vector<double> upper_bounds;  // numerical: one per non-NaN bin, last = +inf
+  std::vector<int> bin2cat;          // categorical: bin -> category value
+  std::unordered_map<int, int> cat2bin;
+
+  // values: sampled feature values (zeros may be omitted: total_sample_cnt
+  // counts them implicitly, exactly like LightGBM's sampled-column API).
+  void FindBin(std::vector<double> values, size_t total_sample_cnt, int max_bin,
+               int min_data_in_bin, bool categorical, bool use_missing, bool zero_as_missing);
+  inline uint32_t ValueToBin(double v) const {
+    if (is_categorical) {
+      if (std::isnan(v) || v < 0) return static_cast<uint32_t>(num_bin - 1);
+      auto it = cat2bin.find(static_cast<int>(v));
+      return it == cat2bin.end() ? static_cast<uint32_t>(num_bin - 1) : static_cast<uint32_t>(it->second);
+    }
+    if (std::isnan(v)) {
+      if (missing_type == kMissingNaN) return static_cast<uint32_t>(num_bin - 1);
+      v = 0.0;
+    }
+    // smallest i with v <= upper_bounds[i]
+    int lo = 0, hi = static_cast<int>(upper_bounds.size()) - 1;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (v <= upper_bounds[mid]) hi = mid; else lo = mid + 1;
+    }
+    return static_cast<uint32_t>(lo);
+  }
+  double BinToValue(uint32_t bin) const {  // split threshold for "bin <= t"
+    return upper_bounds[bin];
+  }
+  std::string FeatureInfo() const;
+  void Serialize(std::string* out) const;
+  const char* Deserialize(const char* p);
+};
+
+// Bin boundaries for all columns: what the reference calls the "reference
+// dataset" (serialisable, broadcast to executors).
+struct DatasetReference {
+  int num_total_features = 0;
+  std::vector<BinMapper> mappers;          // one per column
+  std::vector<int> used_features;          // inner index -> column index
+  std::vector<int> real_to_inner;          // column -> inner (or -1)
+  std::vector<std::string> feature_names;
+  std::string Serialize() const;
+  static DatasetReference Deserialize(const std::string& bytes);
+  // Build from a row-major sample (n_sample x num_cols) of doubles.
+  static DatasetReference FromSample(const double* sample, int64_t n_sample, int num_cols,
+                                     int64_t total_rows, const Config& cfg,
+                                     const std::vector<std::string>& names);
+  // Build from a column-wise sample with explicit non-zero values per column
+  // (LGBM_DatasetCreateFromSampledColumn semantics).
+  static DatasetReference FromSampledColumns(const std::vector<std::vector<double>>& cols,
+                                             int64_t total_sample_cnt, const Config& cfg,
+                                             const std::vector<std::string>& names);
+  int num_inner() const { return static_cast<int>(used_features.size()); }
+  int row_stride() const { return ((num_inner() + 3) / 4) * 4; }
+};
+
+struct Dataset {
+  DatasetReference ref;
+  int64_t num_data = 0;
+  int row_stride = 4;                 // bytes per row in `bins`
+  std::vector<uint8_t> bins;          // num_data * row_stride
+  std::vector<float> label;
+  std::vector<float> weight;          // empty = unweighted
+  std::vector<double> init_score;     // empty or num_data * num_tree_per_iteration
+  std::vector<int32_t> query_boundaries;  // ranking: size num_queries+1
+
+  void Init(const DatasetReference& r, int64_t n);
+  // Push a block of dense rows (row-major, num_cols doubles each) at `start`.
+  void PushDense(const double* rows, int64_t nrows, int num_cols, int64_t start);
+  void PushDenseF32(const float* rows, int64_t nrows, int num_cols, int64_t start);
+  // Push CSR rows at `start` (indptr has nrows+1 entries).
+  void PushCSR(const int64_t* indptr, const int32_t* indices, const double* values,
+               int64_t nrows, int64_t start);
+  void SetQueryFromGroupSizes(const std::vector<int32_t>& sizes);
+  inline uint8_t Bin(int64_t row, int inner) const { return bins[row * row_stride + inner]; }
+};
+
+}  // namespace sml

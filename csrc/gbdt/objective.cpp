@@ -1,0 +1,455 @@
+#include "objective.h"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <sstream>
+#include <stdexcept>
+
+namespace sml {
+
+std::string Objective::Canonical(const std::string& name) { return name; }
+
+Objective::Objective(const Config& cfg) : name_(cfg.objective) {
+  p_.num_class = cfg.num_class;
+  p_.sigmoid = cfg.sigmoid;
+  p_.alpha = cfg.alpha;
+  p_.fair_c = cfg.fair_c;
+  p_.poisson_max_delta_step = cfg.poisson_max_delta_step;
+  p_.tweedie_rho = cfg.tweedie_variance_power;
+  p_.pos_weight = 1.0;
+  p_.neg_weight = 1.0;
+  boost_from_average_ = cfg.boost_from_average;
+  label_gain_ = cfg.label_gain;
+  max_position_ = cfg.max_position;
+  lambdarank_norm_ = cfg.lambdarank_norm;
+  const std::string& o = cfg.objective;
+  if (o == "binary") p_.kind = kObjBinary;
+  else if (o == "multiclass") p_.kind = kObjMulticlass;
+  else if (o == "multiclassova") p_.kind = kObjMulticlassOVA;
+  else if (o == "regression") p_.kind = kObjRegression;
+  else if (o == "regression_l1") p_.kind = kObjL1;
+  else if (o == "huber") p_.kind = kObjHuber;
+  else if (o == "fair") p_.kind = kObjFair;
+  else if (o == "poisson") p_.kind = kObjPoisson;
+  else if (o == "quantile") p_.kind = kObjQuantile;
+  else if (o == "mape") p_.kind = kObjMape;
+  else if (o == "gamma") p_.kind = kObjGamma;
+  else if (o == "tweedie") p_.kind = kObjTweedie;
+  else if (o == "cross_entropy") p_.kind = kObjCrossEntropy;
+  else if (o == "lambdarank" || o == "rank_xendcg") p_.kind = kObjLambdarank;
+  else if (o == "custom" || o == "none" || o == "null") p_.kind = kObjCustom;
+  else throw std::runtime_error("unsupported objective: " + o);
+  num_tree_per_iter_ = (p_.kind == kObjMulticlass || p_.kind == kObjMulticlassOVA) ? cfg.num_class : 1;
+  if (p_.kind == kObjBinary) {
+    if (cfg.scale_pos_weight != 1.0) p_.pos_weight = cfg.scale_pos_weight;
+  }
+  unbalance_ = cfg.is_unbalance;
+}
+
+void Objective::Init(const Dataset& d) {
+  Init(d.label.data(), d.weight.empty() ? nullptr : d.weight.data(), d.num_data, d.query_boundaries);
+}
+
+void Objective::Init(const float* label, const float* weight, int64_t n, const std::vector<int32_t>& qb) {
+  label_ = label; weight_ = weight; n_ = n; qb_ = qb;
+  if (p_.kind == kObjBinary && unbalance_) {
+    int64_t pos = 0, neg = 0;
+    for (int64_t i = 0; i < n; ++i) (label[i] > 0 ? pos : neg)++;
+    if (pos > 0 && neg > 0) {
+      if (pos > neg) { p_.pos_weight = 1.0; p_.neg_weight = static_cast<double>(pos) / neg; }
+      else { p_.pos_weight = static_cast<double>(neg) / pos; p_.neg_weight = 1.0; }
+    }
+  }
+  if (p_.kind == kObjLambdarank) {
+    if (qb_.size() < 2) throw std::runtime_error("lambdarank requires query/group information");
+    inv_max_dcg_.assign(qb_.size() - 1, 0.0);
+    for (size_t q = 0; q + 1 < qb_.size(); ++q) {
+      std::vector<int> labs;
+      for (int32_t i = qb_[q]; i < qb_[q + 1]; ++i) labs.push_back(static_cast<int>(label[i]));
+      std::sort(labs.begin(), labs.end(), std::greater<int>());
+      double dcg = 0;
+      for (int k = 0; k < static_cast<int>(labs.size()) && k < max_position_; ++k)
+        dcg += label_gain_[std::min<int>(labs[k], static_cast<int>(label_gain_.size()) - 1)] / std::log2(2.0 + k);
+      inv_max_dcg_[q] = dcg > 0 ? 1.0 / dcg : 0.0;
+    }
+  }
+}
+
+void Objective::GetGradients(const double* score, float* g, float* h) const {
+  if (p_.kind == kObjLambdarank) { LambdarankGradients(score, g, h); return; }
+  if (p_.kind == kObjCustom) throw std::runtime_error("custom objective: gradients must be supplied");
+  if (p_.kind == kObjMulticlass) {
+    const int K = p_.num_class;
+    const double factor = K / (K - 1.0);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n_; ++i) {
+      double mx = -1e300;
+      for (int k = 0; k < K; ++k) mx = std::max(mx, score[k * n_ + i]);
+      double sum = 0;
+      std::vector<double> e(K);
+      for (int k = 0; k < K; ++k) { e[k] = std::exp(score[k * n_ + i] - mx); sum += e[k]; }
+      const double w = weight_ ? weight_[i] : 1.0;
+      const int y = static_cast<int>(label_[i]);
+      for (int k = 0; k < K; ++k) {
+        const double p = e[k] / sum;
+        g[k * n_ + i] = static_cast<float>(((k == y) ? p - 1.0 : p) * w);
+        h[k * n_ + i] = static_cast<float>(factor * p * (1.0 - p) * w);
+      }
+    }
+    return;
+  }
+  if (p_.kind == kObjMulticlassOVA) {
+    for (int k = 0; k < p_.num_class; ++k) {
+#pragma omp parallel for schedule(static)
+      for (int64_t i = 0; i < n_; ++i) {
+        const double y = static_cast<int>(label_[i]) == k ? 1.0 : 0.0;
+        PointGradient(p_, score[k * n_ + i], y, weight_ ? weight_[i] : 1.0, &g[k * n_ + i], &h[k * n_ + i]);
+      }
+    }
+    return;
+  }
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n_; ++i)
+    PointGradient(p_, score[i], label_[i], weight_ ? weight_[i] : 1.0, &g[i], &h[i]);
+}
+
+void Objective::LambdarankGradients(const double* score, float* g, float* h) const {
+  const double sig = p_.sigmoid;
+  const int nq = static_cast<int>(qb_.size()) - 1;
+#pragma omp parallel for schedule(dynamic)
+  for (int q = 0; q < nq; ++q) {
+    const int b = qb_[q], cnt = qb_[q + 1] - qb_[q];
+    std::vector<double> lam(cnt, 0.0), hes(cnt, 0.0);
+    std::vector<int> order(cnt);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return score[b + a] > score[b + c]; });
+    const double best = cnt ? score[b + order[0]] : 0, worst = cnt ? score[b + order[cnt - 1]] : 0;
+    double sum_l = 0;
+    const double imd = inv_max_dcg_[q];
+    for (int i = 0; i < cnt - 1 && i < max_position_; ++i) {
+      for (int j = i + 1; j < cnt; ++j) {
+        const int li = static_cast<int>(label_[b + order[i]]), lj = static_cast<int>(label_[b + order[j]]);
+        if (li == lj) continue;
+        int hr = i, lr = j;
+        if (li < lj) std::swap(hr, lr);
+        const int hi = order[hr], lo = order[lr];
+        const int lh = static_cast<int>(label_[b + hi]), ll = static_cast<int>(label_[b + lo]);
+        const double gap = label_gain_[std::min<size_t>(lh, label_gain_.size() - 1)] -
+                           label_gain_[std::min<size_t>(ll, label_gain_.size() - 1)];
+        const double pd = std::fabs(1.0 / std::log2(2.0 + hr) - 1.0 / std::log2(2.0 + lr));
+        const double ds = score[b + hi] - score[b + lo];
+        double dn = gap * pd * imd;
+        if (lambdarank_norm_ && best != worst) dn /= (0.01 + std::fabs(ds));
+        double pl = 1.0 / (1.0 + std::exp(sig * ds));
+        double ph = pl * (1.0 - pl);
+        pl *= -sig * dn;
+        ph *= sig * sig * dn;
+        lam[lo] -= pl; hes[lo] += ph;
+        lam[hi] += pl; hes[hi] += ph;
+        sum_l -= 2 * pl;
+      }
+    }
+    double nf = 1.0;
+    if (lambdarank_norm_ && sum_l > 0) nf = std::log2(1 + sum_l) / sum_l;
+    for (int i = 0; i < cnt; ++i) {
+      const double w = weight_ ? weight_[b + i] : 1.0;
+      g[b + i] = static_cast<float>(lam[i] * nf * w);
+      h[b + i] = static_cast<float>(hes[i] * nf * w);
+    }
+  }
+}
+
+namespace {
+double WeightedPercentile(std::vector<std::pair<double, double>> v, double alpha) {
+  // v: (value, weight)
+  if (v.empty()) return 0.0;
+  std::sort(v.begin(), v.end());
+  double tot = 0;
+  for (auto& p : v) tot += p.second;
+  double thr = alpha * tot, acc = 0;
+  for (size_t i = 0; i < v.size(); ++i) {
+    acc += v[i].second;
+    if (acc >= thr) {
+      if (i + 1 < v.size() && std::fabs(acc - thr) < 1e-12 * std::max(1.0, tot)) return (v[i].first + v[i + 1].first) / 2;
+      return v[i].first;
+    }
+  }
+  return v.back().first;
+}
+}  // namespace
+
+double Objective::BoostFromScore(int class_id) const {
+  if (!boost_from_average_) return 0.0;
+  const int64_t n = n_;
+  auto W = [&](int64_t i) { return weight_ ? static_cast<double>(weight_[i]) : 1.0; };
+  switch (p_.kind) {
+    case kObjBinary:
+    case kObjMulticlassOVA:
+    case kObjCrossEntropy: {
+      double sl = 0, sw = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        double y = p_.kind == kObjMulticlassOVA ? (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0)
+                                               : (p_.kind == kObjBinary ? (label_[i] > 0 ? 1.0 : 0.0) : label_[i]);
+        sl += y * W(i); sw += W(i);
+      }
+      double pavg = sw > 0 ? sl / sw : 0.5;
+      pavg = std::min(std::max(pavg, kEpsilon), 1.0 - kEpsilon);
+      double init = std::log(pavg / (1.0 - pavg));
+      if (p_.kind != kObjCrossEntropy) init /= p_.sigmoid;
+      return init;
+    }
+    case kObjMulticlass: {
+      double sl = 0, sw = 0;
+      for (int64_t i = 0; i < n; ++i) { sl += (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0) * W(i); sw += W(i); }
+      double p = sw > 0 ? sl / sw : 1.0 / p_.num_class;
+      return std::log(std::max(kEpsilon, p));
+    }
+    case kObjRegression:
+    case kObjHuber:
+    case kObjFair: {
+      double s = 0, sw = 0;
+      for (int64_t i = 0; i < n; ++i) { s += label_[i] * W(i); sw += W(i); }
+      return sw > 0 ? s / sw : 0.0;
+    }
+    case kObjPoisson:
+    case kObjGamma:
+    case kObjTweedie: {
+      double s = 0, sw = 0;
+      for (int64_t i = 0; i < n; ++i) { s += label_[i] * W(i); sw += W(i); }
+      double m = sw > 0 ? s / sw : 1.0;
+      return std::log(std::max(m, kEpsilon));
+    }
+    case kObjL1:
+    case kObjQuantile: {
+      std::vector<std::pair<double, double>> v(n);
+      for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i)};
+      return WeightedPercentile(std::move(v), p_.kind == kObjL1 ? 0.5 : p_.alpha);
+    }
+    case kObjMape: {
+      std::vector<std::pair<double, double>> v(n);
+      for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i) / std::max(1.0, std::fabs(static_cast<double>(label_[i])))};
+      return WeightedPercentile(std::move(v), 0.5);
+    }
+    default: return 0.0;
+  }
+}
+
+double Objective::RenewLeafOutput(const double* score, const int64_t* rows, int64_t cnt) const {
+  std::vector<std::pair<double, double>> v(cnt);
+  for (int64_t k = 0; k < cnt; ++k) {
+    int64_t i = rows[k];
+    double w = weight_ ? weight_[i] : 1.0;
+    if (p_.kind == kObjMape) w /= std::max(1.0, std::fabs(static_cast<double>(label_[i])));
+    v[k] = {label_[i] - score[i], w};
+  }
+  return WeightedPercentile(std::move(v), p_.kind == kObjQuantile ? p_.alpha : 0.5);
+}
+
+void Objective::ConvertOutput(const double* raw, double* out) const {
+  switch (p_.kind) {
+    case kObjBinary: out[0] = 1.0 / (1.0 + std::exp(-p_.sigmoid * raw[0])); break;
+    case kObjCrossEntropy: out[0] = 1.0 / (1.0 + std::exp(-raw[0])); break;
+    case kObjMulticlass: {
+      double mx = raw[0];
+      for (int k = 1; k < p_.num_class; ++k) mx = std::max(mx, raw[k]);
+      double s = 0;
+      for (int k = 0; k < p_.num_class; ++k) { out[k] = std::exp(raw[k] - mx); s += out[k]; }
+      for (int k = 0; k < p_.num_class; ++k) out[k] /= s;
+      break;
+    }
+    case kObjMulticlassOVA:
+      for (int k = 0; k < p_.num_class; ++k) out[k] = 1.0 / (1.0 + std::exp(-p_.sigmoid * raw[k]));
+      break;
+    case kObjPoisson: case kObjGamma: case kObjTweedie: out[0] = std::exp(raw[0]); break;
+    default: for (int k = 0; k < num_tree_per_iter_; ++k) out[k] = raw[k];
+  }
+}
+
+std::string Objective::ToString() const {
+  std::ostringstream o;
+  o << name_;
+  if (p_.kind == kObjBinary) o << " sigmoid:" << p_.sigmoid;
+  if (p_.kind == kObjMulticlass) o << " num_class:" << p_.num_class;
+  if (p_.kind == kObjMulticlassOVA) o << " num_class:" << p_.num_class << " sigmoid:" << p_.sigmoid;
+  if (p_.kind == kObjQuantile || p_.kind == kObjHuber) o << " alpha:" << p_.alpha;
+  if (p_.kind == kObjFair) o << " fair_c:" << p_.fair_c;
+  if (p_.kind == kObjTweedie) o << " tweedie_variance_power:" << p_.tweedie_rho;
+  return o.str();
+}
+
+std::string Objective::DefaultMetric() const {
+  switch (p_.kind) {
+    case kObjBinary: return "binary_logloss";
+    case kObjMulticlass: case kObjMulticlassOVA: return "multi_logloss";
+    case kObjL1: return "l1";
+    case kObjHuber: return "huber";
+    case kObjFair: return "fair";
+    case kObjPoisson: return "poisson";
+    case kObjQuantile: return "quantile";
+    case kObjMape: return "mape";
+    case kObjGamma: return "gamma";
+    case kObjTweedie: return "tweedie";
+    case kObjCrossEntropy: return "cross_entropy";
+    case kObjLambdarank: return "ndcg";
+    case kObjCustom: return "";
+    default: return "l2";
+  }
+}
+
+// ---------------------------------------------------------------------------
+bool MetricHigherBetter(const std::string& name) {
+  return name.rfind("auc", 0) == 0 || name.rfind("ndcg", 0) == 0 || name.rfind("map", 0) == 0 ||
+         name.rfind("average_precision", 0) == 0;
+}
+
+namespace {
+double AUC(const double* s, const float* y, const float* w, int64_t n) {
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return s[a] > s[b]; });
+  double tp = 0, fp = 0, area = 0, tp_prev = 0, fp_prev = 0;
+  for (int64_t k = 0; k < n; ++k) {
+    int64_t i = idx[k];
+    double wi = w ? w[i] : 1.0;
+    if (y[i] > 0) tp += wi; else fp += wi;
+    if (k + 1 == n || s[idx[k + 1]] != s[i]) {
+      area += (fp - fp_prev) * (tp + tp_prev) / 2.0;
+      tp_prev = tp; fp_prev = fp;
+    }
+  }
+  if (tp == 0 || fp == 0) return 1.0;
+  return area / (tp * fp);
+}
+double AveragePrecision(const double* s, const float* y, const float* w, int64_t n) {
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return s[a] > s[b]; });
+  double tp = 0, fp = 0, ap = 0, tot_pos = 0, prev_recall = 0;
+  for (int64_t i = 0; i < n; ++i) if (y[i] > 0) tot_pos += w ? w[i] : 1.0;
+  if (tot_pos == 0) return 1.0;
+  for (int64_t k = 0; k < n; ++k) {
+    int64_t i = idx[k];
+    double wi = w ? w[i] : 1.0;
+    if (y[i] > 0) tp += wi; else fp += wi;
+    if (k + 1 == n || s[idx[k + 1]] != s[i]) {
+      double recall = tp / tot_pos, prec = tp / (tp + fp);
+      ap += (recall - prev_recall) * prec;
+      prev_recall = recall;
+    }
+  }
+  return ap;
+}
+}  // namespace
+
+double EvalMetric(const std::string& name_in, const Objective& obj, const double* score,
+                  const float* label, const float* weight, int64_t n, int num_class,
+                  const std::vector<int32_t>& qb, const std::vector<double>& label_gain) {
+  std::string name = name_in;
+  int at = -1;
+  auto pos = name.find('@');
+  if (pos != std::string::npos) { at = std::stoi(name.substr(pos + 1)); name = name.substr(0, pos); }
+  const int nout = obj.NumModelPerIteration();
+  double sw = 0;
+  for (int64_t i = 0; i < n; ++i) sw += weight ? weight[i] : 1.0;
+  auto W = [&](int64_t i) { return weight ? static_cast<double>(weight[i]) : 1.0; };
+  std::vector<double> raw(nout), out(nout);
+  auto conv = [&](int64_t i) {
+    for (int k = 0; k < nout; ++k) raw[k] = score[k * n + i];
+    obj.ConvertOutput(raw.data(), out.data());
+  };
+  if (name == "auc") return AUC(score, label, weight, n);
+  if (name == "average_precision") return AveragePrecision(score, label, weight, n);
+  if (name == "binary_logloss" || name == "cross_entropy" || name == "xentropy") {
+    double s = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      conv(i);
+      double p = std::min(std::max(out[0], kEpsilon), 1.0 - kEpsilon);
+      double y = label[i] > 0 ? (name == "binary_logloss" ? 1.0 : label[i]) : 0.0;
+      s += -(y * std::log(p) + (1 - y) * std::log(1 - p)) * W(i);
+    }
+    return s / sw;
+  }
+  if (name == "binary_error") {
+    double s = 0;
+    for (int64_t i = 0; i < n; ++i) { conv(i); s += ((out[0] > 0.5) != (label[i] > 0)) * W(i); }
+    return s / sw;
+  }
+  if (name == "multi_logloss" || name == "multi_error") {
+    double s = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      conv(i);
+      int y = static_cast<int>(label[i]);
+      if (name == "multi_logloss") {
+        s += -std::log(std::max(out[y], kEpsilon)) * W(i);
+      } else {
+        int am = static_cast<int>(std::max_element(out.begin(), out.end()) - out.begin());
+        int top_k = at > 0 ? at : 1;
+        int rank = 0;
+        for (int k = 0; k < num_class; ++k) if (out[k] > out[y]) ++rank;
+        (void)am;
+        s += (rank >= top_k) * W(i);
+      }
+    }
+    return s / sw;
+  }
+  if (name == "ndcg" || name == "map") {
+    const int nq = static_cast<int>(qb.size()) - 1;
+    const int k = at > 0 ? at : 5;
+    double tot = 0;
+    for (int q = 0; q < nq; ++q) {
+      const int b = qb[q], cnt = qb[q + 1] - qb[q];
+      std::vector<int> ord(cnt);
+      std::iota(ord.begin(), ord.end(), 0);
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int c) { return score[b + a] > score[b + c]; });
+      if (name == "ndcg") {
+        std::vector<int> labs;
+        for (int i = 0; i < cnt; ++i) labs.push_back(static_cast<int>(label[b + i]));
+        std::vector<int> sl = labs;
+        std::sort(sl.begin(), sl.end(), std::greater<int>());
+        double dcg = 0, idcg = 0;
+        for (int i = 0; i < std::min(k, cnt); ++i) {
+          dcg += label_gain[std::min<size_t>(labs[ord[i]], label_gain.size() - 1)] / std::log2(2.0 + i);
+          idcg += label_gain[std::min<size_t>(sl[i], label_gain.size() - 1)] / std::log2(2.0 + i);
+        }
+        tot += idcg > 0 ? dcg / idcg : 1.0;
+      } else {
+        double hits = 0, ap = 0;
+        int npos = 0;
+        for (int i = 0; i < cnt; ++i) if (label[b + i] > 0.5) ++npos;
+        for (int i = 0; i < std::min(k, cnt); ++i) {
+          if (label[b + ord[i]] > 0.5) { hits += 1; ap += hits / (i + 1.0); }
+        }
+        tot += npos > 0 ? ap / std::min(k, npos) : 1.0;
+      }
+    }
+    return nq > 0 ? tot / nq : 0.0;
+  }
+  // regression family on converted outputs
+  const ObjParams& p = obj.params();
+  double s = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    conv(i);
+    const double y = label[i], f = out[0], d = f - y;
+    double v = 0;
+    if (name == "l2" || name == "mse" || name == "rmse" || name == "l2_root" || name == "regression") v = d * d;
+    else if (name == "l1" || name == "mae") v = std::fabs(d);
+    else if (name == "quantile") v = d >= 0 ? (1 - p.alpha) * d : -p.alpha * d;
+    else if (name == "huber") v = std::fabs(d) <= p.alpha ? 0.5 * d * d : p.alpha * (std::fabs(d) - 0.5 * p.alpha);
+    else if (name == "fair") { double x = std::fabs(d), c = p.fair_c; v = c * x - c * c * std::log1p(x / c); }
+    else if (name == "poisson") { double e = std::max(f, 1e-10); v = e - y * std::log(e); }
+    else if (name == "mape") v = std::fabs(d) / std::max(1.0, std::fabs(y));
+    else if (name == "gamma") { double e = std::max(f, 1e-10); double psi = 1.0, theta = -1.0 / e; v = -((y * theta - std::log(-1.0 / theta)) / psi); }
+    else if (name == "gamma_deviance") { double e = std::max(f, 1e-10), r = y / e; v = 2.0 * (r - std::log(std::max(r, 1e-10)) - 1.0); }
+    else if (name == "tweedie") {
+      double rho = p.tweedie_rho, e = std::max(f, 1e-10);
+      v = -y * std::exp((1 - rho) * std::log(e)) / (1 - rho) + std::exp((2 - rho) * std::log(e)) / (2 - rho);
+    } else throw std::runtime_error("unknown metric: " + name_in);
+    s += v * W(i);
+  }
+  s /= sw;
+  if (name == "rmse" || name == "l2_root") s = std::sqrt(s);
+  return s;
+}
+
+}  // namespace sml

@@ -1,0 +1,78 @@
+// Split-gain / leaf-output formulas shared by the CPU learner and the HIP
+// split-search kernel (K5 in SURVEY.md §2.4). Semantics follow LightGBM's
+// FeatureHistogram: L1 soft-threshold, L2 shrink, max_delta_step clamp, and
+// data counts estimated from hessian sums (cnt_factor = n / sum_hessian).
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define SML_HD __host__ __device__ __forceinline__
+#else
+#define SML_HD inline
+#endif
+
+namespace sml {
+
+constexpr double kEpsilon = 1e-15;
+
+struct SplitParams {
+  double lambda_l1, lambda_l2, max_delta_step, min_gain_to_split, min_sum_hessian;
+  int min_data_in_leaf;
+  int num_leaves, max_depth;
+  // categorical
+  double cat_l2, cat_smooth;
+  int max_cat_threshold, max_cat_to_onehot, min_data_per_group;
+};
+
+SML_HD double ThresholdL1(double s, double l1) {
+  double reg = fabs(s) - l1;
+  if (reg < 0) reg = 0;
+  return (s > 0 ? 1.0 : (s < 0 ? -1.0 : 0.0)) * reg;
+}
+
+SML_HD double LeafOutput(double g, double h, double l1, double l2, double max_delta_step) {
+  double out = -ThresholdL1(g, l1) / (h + l2);
+  if (max_delta_step > 0 && fabs(out) > max_delta_step) out = (out > 0 ? 1.0 : -1.0) * max_delta_step;
+  return out;
+}
+
+SML_HD double LeafGainGivenOutput(double g, double h, double l1, double l2, double out) {
+  const double sg = ThresholdL1(g, l1);
+  return -(2.0 * sg * out + (h + l2) * out * out);
+}
+
+SML_HD double LeafGain(double g, double h, double l1, double l2, double max_delta_step) {
+  if (max_delta_step <= 0) {
+    const double sg = ThresholdL1(g, l1);
+    return sg * sg / (h + l2);
+  }
+  return LeafGainGivenOutput(g, h, l1, l2, LeafOutput(g, h, l1, l2, max_delta_step));
+}
+
+SML_HD int64_t EstimateCount(double h, double cnt_factor) {
+  return static_cast<int64_t>(h * cnt_factor + 0.5);
+}
+
+// Best split of one leaf (host-side result record; the device kernel writes
+// the same fields into a POD of identical layout).
+struct SplitResult {
+  double gain;         // split gain minus parent gain (LightGBM's "split_gain")
+  double left_g, left_h, right_g, right_h;
+  double left_out, right_out;
+  int64_t left_cnt, right_cnt;
+  int feature;         // inner feature index, -1 = no split
+  uint32_t threshold;  // bin threshold (numerical) or number of categories (categorical)
+  int default_left;
+  int is_cat;
+  uint32_t cat_bits[8];  // categorical: bins that go left (256 bins max)
+};
+
+SML_HD bool SplitBetter(double gain_a, int feat_a, uint32_t thr_a, double gain_b, int feat_b, uint32_t thr_b) {
+  // deterministic ordering: larger gain, then smaller feature, then smaller threshold
+  if (gain_a != gain_b) return gain_a > gain_b;
+  if (feat_a != feat_b) return feat_a < feat_b;
+  return thr_a < thr_b;
+}
+
+}  // namespace sml

@@ -1,0 +1,51 @@
+"""Structured usage logging (reference: core/.../logging/SynapseMLLogging.scala
+:19-172 and the Python SynapseMLLogger). One JSON payload per constructor /
+fit / transform with uid, class, method, library version, column count,
+execution seconds and error. Emitted on the ``synapseml_amd`` logger at DEBUG;
+nothing is sent anywhere (no telemetry endpoint)."""
+from __future__ import annotations
+
+import json
+import logging
+import time
+import traceback
+
+LIBRARY_NAME = "synapseml_amd"
+LIBRARY_VERSION = "0.1.0"
+PROTOCOL_VERSION = "0.0.1"
+
+logger = logging.getLogger(LIBRARY_NAME)
+
+
+def payload(stage, method: str, num_cols=None, seconds=None, error=None) -> dict:
+    p = {
+        "modelUid": getattr(stage, "uid", None),
+        "className": type(stage).__name__,
+        "method": method,
+        "libraryVersion": LIBRARY_VERSION,
+        "libraryName": LIBRARY_NAME,
+        "protocolVersion": PROTOCOL_VERSION,
+    }
+    if num_cols is not None:
+        p["dfInfo"] = {"input": {"numCols": num_cols}}
+    if seconds is not None:
+        p["executionSeconds"] = seconds
+    if error is not None:
+        p["errorType"] = type(error).__name__
+        p["errorMessage"] = str(error)
+    return p
+
+
+def log_verb(stage, method: str, fn, df=None):
+    t0 = time.perf_counter()
+    ncols = len(df.columns) if df is not None and hasattr(df, "columns") else None
+    try:
+        out = fn()
+    except Exception as e:
+        if logger.isEnabledFor(logging.DEBUG):
+            logger.debug(json.dumps(payload(stage, method, ncols, time.perf_counter() - t0, e)))
+            logger.debug(traceback.format_exc())
+        raise
+    if logger.isEnabledFor(logging.DEBUG):
+        logger.debug(json.dumps(payload(stage, method, ncols, time.perf_counter() - t0)))
+    return out

@@ -1,0 +1,444 @@
+"""Distributed LightGBM-style training driver (reference:
+lightgbm/.../LightGBMBase.scala, BasePartitionTask.scala, TrainUtils.scala).
+
+Flow of one ``fit``: optional sequential batches (``numBatches``, :45-60) ->
+per batch: column preparation, validation split, categorical slots, bin
+boundaries from a row sample (``samplingMode`` global/subset/fixed, or a cached
+``referenceDataset``), native Dataset construction, booster creation (+ merge
+of ``modelString`` for continued training), the iteration loop with delegate
+hooks, learning-rate resets, custom objective, train/valid evaluation and early
+stopping (TrainUtils.scala:98-169), and truncation to the best iteration.
+
+Data parallel: when a process group with world > 1 is active each rank holds
+its partition; rank 0's sample defines the shared bin boundaries (broadcast,
+C8 in SURVEY §2.5) and histograms are allreduced over RCCL inside the engine.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import List, Optional
+
+import numpy as np
+
+from ..core.dataframe import DataFrame
+from ..core.linalg import SparseVector, as_csr, as_matrix
+from ..core.pipeline import Estimator
+from ..core.utils import ParamsStringBuilder
+from ..ops import native
+from ..parallel import distributed as D
+from .booster import LightGBMBooster
+from .params import LightGBMParams
+
+log = logging.getLogger("synapseml_amd.lightgbm")
+
+
+class InstrumentationMeasures(dict):
+    """Per-phase wall-clock timings (reference: LightGBMPerformance.scala:11-183)."""
+
+    def mark(self, name: str, value_ms: float) -> None:
+        self[name] = self.get(name, 0.0) + value_ms
+
+
+def _features(df: DataFrame, col: str, matrix_type: str):
+    c = df[col]
+    if isinstance(c, np.ndarray) and c.ndim == 2:
+        if matrix_type == "sparse":
+            return "sparse", as_csr(c)
+        return "dense", np.ascontiguousarray(c, dtype=np.float64)
+    sparse = matrix_type == "sparse" or (matrix_type == "auto" and any(isinstance(v, SparseVector) for v in c[:10]))
+    if sparse:
+        return "sparse", as_csr(c)
+    return "dense", as_matrix(c)
+
+
+def _slice_features(kind, data, idx):
+    if kind == "dense":
+        return data[idx]
+    indptr, indices, values, width = data
+    rows = np.nonzero(idx)[0] if idx.dtype == bool else idx
+    new_ptr = [0]
+    ii, vv = [], []
+    for r in rows:
+        a, b = indptr[r], indptr[r + 1]
+        ii.append(indices[a:b])
+        vv.append(values[a:b])
+        new_ptr.append(new_ptr[-1] + (b - a))
+    return (np.asarray(new_ptr, np.int64), np.concatenate(ii).astype(np.int32) if ii else np.zeros(0, np.int32),
+            np.concatenate(vv) if vv else np.zeros(0), width)
+
+
+def _num_rows(kind, data) -> int:
+    return data.shape[0] if kind == "dense" else len(data[0]) - 1
+
+
+def _num_cols(kind, data) -> int:
+    return data.shape[1] if kind == "dense" else data[3]
+
+
+def _sample_dense(kind, data, idx) -> np.ndarray:
+    if kind == "dense":
+        return np.ascontiguousarray(data[idx])
+    indptr, indices, values, width = data
+    out = np.zeros((len(idx), width))
+    for i, r in enumerate(idx):
+        a, b = indptr[r], indptr[r + 1]
+        out[i, indices[a:b]] = values[a:b]
+    return out
+
+
+class LightGBMBase(Estimator, LightGBMParams):
+    _objective_default = "regression"
+
+    def _init_state(self) -> None:
+        self._measures: List[InstrumentationMeasures] = []
+
+    # ------------------------------------------------------------- public helpers
+    def getPerformanceMeasures(self) -> List[InstrumentationMeasures]:  # noqa: N802
+        return list(getattr(self, "_measures", []))
+
+    # ------------------------------------------------------------- hooks
+    def _is_classification(self) -> bool:
+        return False
+
+    def _num_class(self, df: DataFrame) -> int:
+        return 1
+
+    def _extra_params(self, sb: ParamsStringBuilder, num_class: int) -> None:
+        pass
+
+    def _make_model(self, booster: LightGBMBooster, num_class: int):
+        raise NotImplementedError
+
+    def _group_col(self) -> Optional[str]:
+        return None
+
+    # ------------------------------------------------------------- params string
+    def _categorical_indexes(self, df: DataFrame, num_cols: int) -> List[int]:
+        idx = set(self.getCategoricalSlotIndexes() or [])
+        names = self.getCategoricalSlotNames() or []
+        slot_names = self._slot_names(df, num_cols)
+        for n in names:
+            if n in slot_names:
+                idx.add(slot_names.index(n))
+        md = df.metadata(self.getFeaturesCol())
+        for i, attr in enumerate(md.get("ml_attr", {}).get("attrs", {}).get("nominal", [])):
+            if "idx" in attr:
+                idx.add(int(attr["idx"]))
+        for i in md.get("categorical_slots", []):
+            idx.add(int(i))
+        return sorted(i for i in idx if 0 <= i < num_cols)
+
+    def _slot_names(self, df: DataFrame, num_cols: int) -> List[str]:
+        names = list(self.getSlotNames() or [])
+        if not names:
+            md = df.metadata(self.getFeaturesCol())
+            names = list(md.get("slot_names", []))
+        if len(names) != num_cols:
+            names = [f"Column_{i}" for i in range(num_cols)]
+        for n in names:
+            if any(ch in n for ch in '",:[]{}'):
+                raise ValueError(f"Invalid slot name {n!r}: slot names cannot contain \" , : [ ] {{ }}")
+        return names
+
+    def _train_params(self, num_class: int, cat_idx: List[int], num_machines: int) -> str:
+        sb = ParamsStringBuilder()
+        sb.append(self.getPassThroughArgs())
+        sb.appendParamValueIfNotThere("is_pre_partition", "True")
+        sb.appendParamValueIfNotThere("boosting_type", self.getBoostingType())
+        sb.appendParamValueIfNotThere("tree_learner", "data" if self.getParallelism() == "data_parallel" else
+                                      ("voting" if self.getParallelism() == "voting_parallel" else self.getParallelism()))
+        sb.appendParamValueIfNotThere("top_k", self.getTopK())
+        sb.appendParamValueIfNotThere("num_leaves", self.getNumLeaves())
+        sb.appendParamValueIfNotThere("max_bin", self.getMaxBin())
+        sb.appendParamValueIfNotThere("bin_construct_sample_cnt", self.getBinSampleCount())
+        sb.appendParamValueIfNotThere("min_data_in_bin", self.getMinDataPerBin())
+        sb.appendParamValueIfNotThere("bagging_fraction", self.getBaggingFraction())
+        sb.appendParamValueIfNotThere("pos_bagging_fraction", self.getPosBaggingFraction())
+        sb.appendParamValueIfNotThere("neg_bagging_fraction", self.getNegBaggingFraction())
+        sb.appendParamValueIfNotThere("bagging_freq", self.getBaggingFreq())
+        sb.appendParamValueIfNotThere("feature_fraction", self.getFeatureFraction())
+        sb.appendParamValueIfNotThere("feature_fraction_bynode", self.getFeatureFractionByNode())
+        sb.appendParamValueIfNotThere("max_depth", self.getMaxDepth())
+        sb.appendParamValueIfNotThere("min_sum_hessian_in_leaf", self.getMinSumHessianInLeaf())
+        sb.appendParamValueIfNotThere("lambda_l1", self.getLambdaL1())
+        sb.appendParamValueIfNotThere("lambda_l2", self.getLambdaL2())
+        metric = self.getMetric()
+        sb.appendParamValueIfNotThere("metric", metric if metric else None)
+        sb.appendParamValueIfNotThere("min_gain_to_split", self.getMinGainToSplit())
+        sb.appendParamValueIfNotThere("max_delta_step", self.getMaxDeltaStep())
+        sb.appendParamValueIfNotThere("min_data_in_leaf", self.getMinDataInLeaf())
+        sb.appendParamValueIfNotThere("num_iterations", self.getNumIterations())
+        sb.appendParamValueIfNotThere("learning_rate", self.getLearningRate())
+        sb.appendParamValueIfNotThere("num_machines", num_machines)
+        sb.appendParamValueIfNotThere("verbosity", self.getVerbosity())
+        sb.appendParamValueIfNotThere("early_stopping_round", self.getEarlyStoppingRound())
+        sb.appendParamListIfNotThere("categorical_feature", cat_idx)
+        sb.appendParamListIfNotThere("max_bin_by_feature", self.getMaxBinByFeature())
+        sb.appendParamValueIfNotThere("top_rate", self.getTopRate())
+        sb.appendParamValueIfNotThere("other_rate", self.getOtherRate())
+        sb.appendParamListIfNotThere("monotone_constraints", self.getMonotoneConstraints())
+        sb.appendParamValueIfNotThere("monotone_constraints_method", self.getMonotoneConstraintsMethod())
+        sb.appendParamValueIfNotThere("monotone_penalty", self.getMonotonePenalty())
+        # dataset
+        sb.appendParamValueIfNotThere("is_enable_sparse", self.getIsEnableSparse())
+        sb.appendParamValueIfNotThere("use_missing", self.getUseMissing())
+        sb.appendParamValueIfNotThere("zero_as_missing", self.getZeroAsMissing())
+        if self.getBoostingType() == "dart":
+            sb.appendParamValueIfNotThere("drop_rate", self.getDropRate())
+            sb.appendParamValueIfNotThere("max_drop", self.getMaxDrop())
+            sb.appendParamValueIfNotThere("skip_drop", self.getSkipDrop())
+            sb.appendParamValueIfNotThere("xgboost_dart_mode", self.getXGBoostDartMode())
+            sb.appendParamValueIfNotThere("uniform_drop", self.getUniformDrop())
+        # objective
+        sb.appendParamValueIfNotThere("objective", "custom" if self.getFobj() is not None else self.getObjective())
+        # execution
+        sb.appendParamValueIfNotThere("num_threads", self.getNumThreads())
+        sb.appendParamValueIfNotThere("device_type", self.getDeviceType())
+        # seeds
+        sb.appendParamValueIfNotThere("seed", self.getSeed())
+        sb.appendParamValueIfNotThere("deterministic", self.getDeterministic())
+        sb.appendParamValueIfNotThere("bagging_seed", self.getBaggingSeed())
+        sb.appendParamValueIfNotThere("feature_fraction_seed", self.getFeatureFractionSeed())
+        sb.appendParamValueIfNotThere("extra_seed", self.getExtraSeed())
+        sb.appendParamValueIfNotThere("drop_seed", self.getDropSeed())
+        sb.appendParamValueIfNotThere("data_random_seed", self.getDataRandomSeed())
+        sb.appendParamValueIfNotThere("objective_seed", self.getObjectiveSeed())
+        # categorical
+        sb.appendParamValueIfNotThere("min_data_per_group", self.getMinDataPerGroup())
+        sb.appendParamValueIfNotThere("max_cat_threshold", self.getMaxCatThreshold())
+        sb.appendParamValueIfNotThere("cat_l2", self.getCatl2())
+        sb.appendParamValueIfNotThere("cat_smooth", self.getCatSmooth())
+        sb.appendParamValueIfNotThere("max_cat_to_onehot", self.getMaxCatToOnehot())
+        self._extra_params(sb, num_class)
+        return sb.result
+
+    # ------------------------------------------------------------- fit
+    def _fit(self, df: DataFrame):
+        self._measures = []
+        nb = self.getNumBatches()
+        batches = df.randomSplit([1.0] * nb, seed=self.getSeed() or 0) if nb and nb > 0 else [df]
+        model_str = self.getModelString() or None
+        booster = None
+        num_class = self._num_class(df)
+        delegate = self.getDelegate()
+        for bi, batch in enumerate(batches):
+            if delegate is not None:
+                delegate.beforeTrainBatch(bi, log, batch, booster)
+            booster = self._train_batch(batch, model_str, bi, num_class)
+            model_str = booster.modelStr
+            if delegate is not None:
+                delegate.afterTrainBatch(bi, log, batch, booster)
+        return self._make_model(booster, num_class)
+
+    def _prepare(self, df: DataFrame):
+        """Column extraction; ranker rows are grouped contiguously."""
+        gcol = self._group_col()
+        if gcol:
+            g = df[gcol]
+            codes = {}
+            ids = np.asarray([codes.setdefault(v, len(codes)) for v in g.tolist()], dtype=np.int64)
+            order = np.argsort(ids, kind="stable")
+            df = df._take_rows(order)
+        return df
+
+    def _train_batch(self, df: DataFrame, model_str: Optional[str], batch_index: int, num_class: int):
+        m = InstrumentationMeasures()
+        t_start = time.perf_counter()
+        g = native.gbdt()
+        df = self._prepare(df)
+        vcol = self.getValidationIndicatorCol()
+        valid_df = None
+        if vcol and vcol in df:
+            vmask = np.asarray(df[vcol], dtype=bool)
+            valid_df = df.filter(vmask)
+            df = df.filter(~vmask)
+        kind, data = _features(df, self.getFeaturesCol(), self.getMatrixType())
+        n = _num_rows(kind, data)
+        ncols = _num_cols(kind, data)
+        world = D.world_size()
+        if world > 1:
+            ncols = max(D.all_gather_object(ncols))
+        cat_idx = self._categorical_indexes(df, ncols)
+        names = self._slot_names(df, ncols)
+        params = self._train_params(num_class, cat_idx, world)
+        use_gpu = self.getDeviceType() == "gpu" and native.gpu_available()
+        # --- bin boundaries (reference dataset)
+        t0 = time.perf_counter()
+        ref_bytes = self.getReferenceDataset()
+        if ref_bytes:
+            ref = g.DatasetReference.deserialize(bytes(ref_bytes))
+        else:
+            sample = None
+            if D.rank() == 0 or world == 1:
+                sample = self._sample_rows(kind, data, n)
+            if world > 1:
+                # "global" sampling gathers a proportional sample from every rank
+                if self.getSamplingMode() == "global":
+                    parts = D.all_gather_object(self._sample_rows(kind, data, n, share=1.0 / world))
+                    sample = np.concatenate([p for p in parts if p is not None and len(p)], axis=0)
+                ser = None
+                if D.rank() == 0:
+                    tot = n * world
+                    ser = bytes(g.DatasetReference.from_sample(sample, tot, params, names).serialize())
+                ser = D.broadcast_object(ser, 0)
+                ref = g.DatasetReference.deserialize(ser)
+            else:
+                ref = g.DatasetReference.from_sample(sample, n, params, names)
+            self._last_reference = bytes(ref.serialize())
+        m.mark("sampling_ms", (time.perf_counter() - t0) * 1e3)
+        # --- datasets
+        delegate = self.getDelegate()
+        if delegate is not None:
+            delegate.beforeGenerateTrainDataset(batch_index, D.rank(), None, df.schema, log, params)
+        t0 = time.perf_counter()
+        train = self._build_dataset(g, ref, df, kind, data, n, num_class)
+        m.mark("dataset_creation_ms", (time.perf_counter() - t0) * 1e3)
+        if delegate is not None:
+            delegate.afterGenerateTrainDataset(batch_index, D.rank(), None, df.schema, log, params)
+        valid = None
+        if valid_df is not None and len(valid_df) > 0:
+            if delegate is not None:
+                delegate.beforeGenerateValidDataset(batch_index, D.rank(), None, df.schema, log, params)
+            t0 = time.perf_counter()
+            vk, vd = _features(valid_df, self.getFeaturesCol(), self.getMatrixType())
+            valid = self._build_dataset(g, ref, valid_df, vk, vd, _num_rows(vk, vd), num_class)
+            m.mark("validation_dataset_creation_ms", (time.perf_counter() - t0) * 1e3)
+            if delegate is not None:
+                delegate.afterGenerateValidDataset(batch_index, D.rank(), None, df.schema, log, params)
+        # --- booster
+        t0 = time.perf_counter()
+        comm = D.gbdt_comm(use_gpu) if world > 1 else None
+        nb = g.Booster(train, params, comm)
+        if model_str:
+            nb.merge(g.Booster.from_model_string(model_str))
+        if valid is not None:
+            nb.add_valid(valid, "valid")
+        m.mark("booster_init_ms", (time.perf_counter() - t0) * 1e3)
+        prior_iters = nb.current_iteration
+        best = self._iterate(nb, valid is not None, batch_index, m, n, num_class)
+        if best is not None and best >= 0:
+            # keep iterations up to and including the best one (BasePartitionTask.scala:450-457)
+            nb.truncate(prior_iters + best + 1)
+        m.mark("total_ms", (time.perf_counter() - t_start) * 1e3)
+        m["backend"] = nb.backend
+        m["native_stats"] = nb.stats()
+        self._measures.append(m)
+        booster = LightGBMBooster(native_booster=nb, best_iteration=best if best is not None else -1)
+        return booster
+
+    def _sample_rows(self, kind, data, n, share: float = 1.0):
+        cnt = int(min(n, max(1, int(self.getBinSampleCount() * share))))
+        rng = np.random.default_rng(self.getDataRandomSeed())
+        mode = self.getSamplingMode()
+        if n == 0:
+            return np.zeros((0, _num_cols(kind, data)))
+        if mode == "fixed":
+            idx = np.arange(cnt)
+        elif mode == "subset":
+            sub = min(n, self.getSamplingSubsetSize())
+            idx = np.sort(rng.choice(sub, size=min(cnt, sub), replace=False))
+        else:
+            idx = np.sort(rng.choice(n, size=cnt, replace=False))
+        return _sample_dense(kind, data, idx)
+
+    def _build_dataset(self, g, ref, df: DataFrame, kind, data, n, num_class):
+        ds = g.Dataset(ref, n)
+        if kind == "dense":
+            chunk = 1 << 20
+            for s in range(0, n, chunk):
+                ds.push_dense(data[s: s + chunk], s)
+        else:
+            indptr, indices, values, _ = data
+            ds.push_csr(indptr, indices, values, 0)
+        ds.set_label(self._labels(df))
+        wcol = self.getWeightCol()
+        if wcol and wcol in df:
+            ds.set_weight(np.asarray(df[wcol], dtype=np.float32))
+        icol = self.getInitScoreCol()
+        if icol and icol in df:
+            s = df[icol]
+            if isinstance(s, np.ndarray) and s.ndim == 2:
+                arr = np.ascontiguousarray(s.T, dtype=np.float64).ravel()  # class-major
+            elif s.dtype == object:
+                arr = np.ascontiguousarray(as_matrix(s).T).ravel()
+            else:
+                arr = np.asarray(s, dtype=np.float64)
+            ds.set_init_score(arr)
+        gcol = self._group_col()
+        if gcol and gcol in df:
+            vals = df[gcol].tolist()
+            sizes = []
+            prev = object()
+            for v in vals:
+                if sizes and v == prev:
+                    sizes[-1] += 1
+                else:
+                    sizes.append(1)
+                    prev = v
+            ds.set_group(np.asarray(sizes, dtype=np.int32))
+        return ds
+
+    def _labels(self, df: DataFrame) -> np.ndarray:
+        return np.asarray(df[self.getLabelCol()], dtype=np.float32)
+
+    def _iterate(self, nb, has_valid: bool, batch_index: int, m: InstrumentationMeasures, n: int, num_class: int):
+        delegate = self.getDelegate()
+        fobj = self.getFobj()
+        lr = self.getLearningRate()
+        es = self.getEarlyStoppingRound()
+        tol = self.getImprovementTolerance()
+        names = nb.eval_names()
+        best_score = [None] * len(names)
+        best_iter = [0] * len(names)
+        best_result = None
+        provide_train = self.getIsProvideTrainingMetric()
+        t0 = time.perf_counter()
+        num_iter = self.getNumIterations()
+        it = 0
+        finished = False
+        while not finished and it < num_iter:
+            if delegate is not None:
+                delegate.beforeTrainIteration(batch_index, D.rank(), it, log, None, nb, has_valid)
+                new_lr = delegate.getLearningRate(batch_index, D.rank(), it, log, None, lr)
+                if new_lr != lr:
+                    nb.reset_parameter(f"learning_rate={new_lr}")
+                    lr = new_lr
+            try:
+                if fobj is not None:
+                    K = nb.num_model_per_iteration
+                    preds = nb.train_scores().reshape(K, -1).T if K > 1 else nb.train_scores()
+                    grad, hess = fobj(preds, None)
+                    grad = np.asarray(grad, dtype=np.float32)
+                    hess = np.asarray(hess, dtype=np.float32)
+                    if K > 1 and grad.ndim == 2:
+                        grad = np.ascontiguousarray(grad.T).ravel()
+                        hess = np.ascontiguousarray(hess.T).ravel()
+                    finished = nb.update(grad, hess)
+                else:
+                    finished = nb.update()
+            except RuntimeError as e:  # early termination (TrainUtils.scala:89-95)
+                log.warning("training stopped early on this task: %s", e)
+                finished = True
+            train_res = dict(nb.eval(0)) if provide_train and not finished else None
+            valid_res = None
+            if has_valid and not finished:
+                res = nb.eval(1)
+                valid_res = dict(res)
+                for i, (name, score) in enumerate(res):
+                    higher = name.startswith(("auc", "ndcg@", "map@", "average_precision"))
+                    better = (best_score[i] is None or
+                              ((score - best_score[i] > tol) if higher else (score - best_score[i] < tol)))
+                    if better:
+                        best_score[i] = score
+                        best_iter[i] = it
+                    elif es > 0 and it - best_iter[i] >= es:
+                        finished = True
+                        best_result = best_iter[i]
+            if delegate is not None:
+                delegate.afterTrainIteration(batch_index, D.rank(), it, log, None, nb, has_valid, finished,
+                                             train_res, valid_res)
+            it += 1
+        nb.synchronize()
+        m.mark("training_iterations_ms", (time.perf_counter() - t0) * 1e3)
+        return best_result

@@ -1,0 +1,145 @@
+"""Process-group helpers: one process per GPU, ``torch.distributed`` for the
+control plane, RCCL (backend "nccl" on ROCm) or native RCCL communicators for
+the data plane.
+
+This is the MI355X replacement of the reference's coordination layer
+(SURVEY §2.7/§5.8): the driver rendezvous of lightgbm/.../NetworkManager.scala
+becomes the torchrun/TCPStore rendezvous (rank, world size, master address),
+and LightGBM's socket linkers / VW's spanning tree / Horovod become RCCL
+collectives over xGMI.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, List, Optional
+
+import numpy as np
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+
+        return dist if dist.is_available() else None
+    except Exception:  # pragma: no cover
+        return None
+
+
+def is_initialized() -> bool:
+    d = _dist()
+    return bool(d and d.is_initialized())
+
+
+def rank() -> int:
+    d = _dist()
+    return d.get_rank() if d and d.is_initialized() else 0
+
+
+def world_size() -> int:
+    d = _dist()
+    return d.get_world_size() if d and d.is_initialized() else 1
+
+
+def local_rank() -> int:
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def backend() -> Optional[str]:
+    d = _dist()
+    return d.get_backend() if d and d.is_initialized() else None
+
+
+def init_from_env(backend_name: Optional[str] = None, timeout_s: float = 1200.0) -> bool:
+    """Initialise the default process group from torchrun-style env vars."""
+    d = _dist()
+    if d is None or d.is_initialized():
+        return bool(d and d.is_initialized())
+    if "RANK" not in os.environ or "WORLD_SIZE" not in os.environ:
+        return False
+    import datetime
+
+    import torch
+
+    if backend_name is None:
+        backend_name = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend_name == "nccl":
+        torch.cuda.set_device(local_rank())
+    d.init_process_group(backend=backend_name, timeout=datetime.timedelta(seconds=timeout_s))
+    return True
+
+
+def barrier() -> None:
+    if is_initialized():
+        d = _dist()
+        if backend() == "nccl":
+            import torch
+
+            d.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            d.barrier()
+
+
+def broadcast_object(obj: Any, src: int = 0) -> Any:
+    if not is_initialized() or world_size() == 1:
+        return obj
+    d = _dist()
+    lst = [obj]
+    d.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def all_gather_object(obj: Any) -> List[Any]:
+    if not is_initialized() or world_size() == 1:
+        return [obj]
+    d = _dist()
+    out = [None] * world_size()
+    d.all_gather_object(out, obj)
+    return out
+
+
+def allreduce_numpy(a: np.ndarray) -> None:
+    """In-place sum of a float64 host array over the default group."""
+    if not is_initialized() or world_size() == 1:
+        return
+    import torch
+
+    d = _dist()
+    if backend() == "nccl":
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{torch.cuda.current_device()}")
+        d.all_reduce(t)
+        a[...] = t.cpu().numpy()
+    else:
+        t = torch.from_numpy(a)  # shares memory with `a`
+        d.all_reduce(t)
+
+
+_comm_cache: dict = {}
+
+
+def gbdt_comm(use_gpu: bool):
+    """Communicator for the native GBDT engine, or None when world == 1.
+
+    GPU runs get a native RCCL communicator whose ncclUniqueId is broadcast
+    over the control plane, so histogram allreduces are enqueued on the
+    engine's own HIP stream with no Python round trip; CPU runs get a host
+    communicator that reduces through the default (gloo) group.
+    """
+    if world_size() <= 1:
+        return None
+    from ..ops import native
+
+    g = native.gbdt()
+    key = ("rccl" if use_gpu else "host", world_size())
+    if key in _comm_cache:
+        return _comm_cache[key]
+    if use_gpu:
+        uid = g.rccl_unique_id() if rank() == 0 else None
+        uid = broadcast_object(uid, 0)
+        import torch
+
+        dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
+        c = g.rccl_comm(uid, rank(), world_size(), dev)
+    else:
+        c = g.host_comm(rank(), world_size(), lambda arr: allreduce_numpy(arr))
+    _comm_cache[key] = c
+    return c

@@ -1,0 +1,123 @@
+"""HIP backend vs the CPU oracle (same binned data, same params)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n=60000, f=12, seed=0, nan_frac=0.0, cat=False):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, f))
+    if cat:
+        X[:, 0] = rng.integers(0, 12, size=n)
+    if nan_frac:
+        m = rng.random((n, f)) < nan_frac
+        m[:, 0] = False
+        X[m] = np.nan
+    s = X[:, 0] * (0.2 if cat else 1.0) + np.nan_to_num(X[:, 1]) * np.nan_to_num(X[:, 2]) + 0.5 * np.sin(np.nan_to_num(X[:, 3]))
+    if cat:
+        s += (X[:, 0] % 3 == 1) * 1.5
+    y = (s + 0.5 * rng.standard_normal(n) > 0).astype(np.float32)
+    return X, y
+
+
+def _train(X, y, params, iters):
+    from synapseml_amd.ops import native
+
+    g = native.gbdt()
+    ref = g.DatasetReference.from_sample(X[:50000], len(X), params, [f"f{i}" for i in range(X.shape[1])])
+    ds = g.Dataset(ref, len(X))
+    ds.push_dense(X, 0)
+    ds.set_label(y)
+    b = g.Booster(ds, params, None)
+    for _ in range(iters):
+        b.update()
+    return b
+
+
+@pytest.mark.parametrize("extra", ["", "lambda_l1=0.5 lambda_l2=1.0 min_data_in_leaf=50", "max_depth=4 num_leaves=15"])
+def test_gpu_trees_match_cpu(extra):
+    from sklearn.metrics import roc_auc_score
+
+    X, y = _data()
+    base = f"objective=binary num_leaves=31 learning_rate=0.1 {extra}"
+    bc = _train(X, y, base + " device_type=cpu", 5)
+    bg = _train(X, y, base + " device_type=gpu", 5)
+    assert bg.backend == "hip"
+    mc, mg = bc.save_model_string(), bg.save_model_string()
+    # the first tree must be identical in structure (same splits)
+    t0c = mc.split("Tree=0")[1].split("Tree=1")[0]
+    t0g = mg.split("Tree=0")[1].split("Tree=1")[0]
+    line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")][0]
+    assert line(t0c, "split_feature") == line(t0g, "split_feature")
+    assert line(t0c, "threshold") == line(t0g, "threshold")
+    lc = np.array(line(t0c, "leaf_value").split("=")[1].split(), float)
+    lg = np.array(line(t0g, "leaf_value").split("=")[1].split(), float)
+    np.testing.assert_allclose(lc, lg, rtol=1e-4, atol=1e-6)
+    pc = bc.predict(X, 0, 0, -1)[:, 0]
+    pg = bg.predict(X, 0, 0, -1)[:, 0]
+    assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 2e-3
+    # training scores kept on the device equal the model's own predictions
+    np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
+
+
+def test_gpu_missing_and_categorical():
+    from sklearn.metrics import roc_auc_score
+
+    X, y = _data(nan_frac=0.1, cat=True)
+    p = "objective=binary num_leaves=31 categorical_feature=0"
+    bc = _train(X, y, p + " device_type=cpu", 8)
+    bg = _train(X, y, p + " device_type=gpu", 8)
+    assert bg.backend == "hip"
+    pc = bc.predict(X, 1, 0, -1)[:, 0]
+    pg = bg.predict(X, 1, 0, -1)[:, 0]
+    assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 5e-3
+    np.testing.assert_allclose(bg.train_scores(), bg.predict(X, 0, 0, -1)[:, 0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("obj", ["regression", "multiclass num_class=3", "poisson"])
+def test_gpu_objectives(obj):
+    X, y = _data(n=30000)
+    if obj.startswith("multiclass"):
+        y = (np.digitize(X[:, 0] + X[:, 1], [-0.5, 0.5])).astype(np.float32)
+    elif obj == "poisson":
+        y = np.random.default_rng(1).poisson(np.exp(0.3 * X[:, 0])).astype(np.float32)
+    else:
+        y = (X[:, 0] * 2 + X[:, 1] ** 2).astype(np.float32)
+    bc = _train(X, y, f"objective={obj} device_type=cpu", 5)
+    bg = _train(X, y, f"objective={obj} device_type=gpu", 5)
+    pc = bc.predict(X, 1, 0, -1)
+    pg = bg.predict(X, 1, 0, -1)
+    assert np.corrcoef(pc.ravel(), pg.ravel())[0, 1] > 0.999
+
+
+def test_gpu_bagging_goss_rf():
+    X, y = _data(n=40000)
+    for extra in ["bagging_fraction=0.7 bagging_freq=1", "boosting=goss", "boosting=rf bagging_fraction=0.6 bagging_freq=1"]:
+        bg = _train(X, y, f"objective=binary device_type=gpu {extra}", 12)
+        s = bg.train_scores()
+        p = bg.predict(X, 0, 0, -1)[:, 0]
+        np.testing.assert_allclose(s, p, rtol=1e-5, atol=1e-5)
+
+
+def test_gpu_predictor_matches_cpu_predict():
+    from synapseml_amd.ops import native
+
+    X, y = _data(n=50000, nan_frac=0.05)
+    b = _train(X, y, "objective=binary device_type=gpu", 10)
+    gp = native.gbdt().GpuPredictor(b, 0, -1, -1)
+    np.testing.assert_allclose(gp.predict(X, False), b.predict(X, 0, 0, -1), rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(gp.predict(X, True), b.predict(X, 1, 0, -1), rtol=1e-10, atol=1e-10)
+    np.testing.assert_array_equal(gp.predict_leaf(X), b.predict(X, 2, 0, -1).astype(np.int32))
+
+
+def test_classifier_api_on_gpu():
+    from synapseml_amd.core import DataFrame
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    X, y = _data(n=30000)
+    df = DataFrame({"features": X, "label": y.astype(float)})
+    m = LightGBMClassifier(numIterations=10).fit(df)
+    assert m.getLightGBMBooster().native.backend == "hip"
+    out = m.transform(df)
+    assert out["probability"].shape == (30000, 2)

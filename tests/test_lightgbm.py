@@ -1,0 +1,274 @@
+"""LightGBM API behaviour on the CPU backend (reference test strategy:
+lightgbm/src/test/.../split5/VerifyLightGBMClassifierStream.scala and
+split2/VerifyLightGBMRegressorStream.scala / VerifyLightGBMRankerStream.scala)."""
+import numpy as np
+import pytest
+from sklearn.metrics import roc_auc_score
+
+from synapseml_amd.core import DataFrame, SparseVector
+from synapseml_amd.lightgbm import (LightGBMClassificationModel, LightGBMClassifier, LightGBMDelegate,
+                                    LightGBMRanker, LightGBMRegressionModel, LightGBMRegressor)
+
+
+def binary_df(n=4000, f=10, seed=0, parts=2):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, f))
+    y = (X[:, 0] + X[:, 1] * X[:, 2] + 0.3 * rng.standard_normal(n) > 0).astype(float)
+    return DataFrame({"features": X, "label": y}, num_partitions=parts), X, y
+
+
+def clf(**kw):
+    kw.setdefault("deviceType", "cpu")
+    kw.setdefault("numIterations", 30)
+    return LightGBMClassifier(**kw)
+
+
+def test_binary_auc_matches_sklearn_histgb():
+    from sklearn.ensemble import HistGradientBoostingClassifier
+
+    df, X, y = binary_df()
+    m = clf(numIterations=50).fit(df)
+    out = m.transform(df)
+    prob = out["probability"]
+    np.testing.assert_allclose(prob.sum(1), 1.0)  # LightGBMTestUtils.scala:60-68
+    auc = roc_auc_score(y, prob[:, 1])
+    sk = HistGradientBoostingClassifier(max_iter=50, max_leaf_nodes=31, learning_rate=0.1, max_bins=255,
+                                        early_stopping=False, min_samples_leaf=20).fit(X, y)
+    auc_sk = roc_auc_score(y, sk.predict_proba(X)[:, 1])
+    assert abs(auc - auc_sk) < 0.01, (auc, auc_sk)
+    raw = out["rawPrediction"]
+    np.testing.assert_allclose(raw[:, 0], -raw[:, 1])
+    np.testing.assert_array_equal(out["prediction"], (prob[:, 1] > 0.5).astype(float))
+
+
+def test_multiclass_and_importances_and_shap():
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((3000, 6))
+    y = np.digitize(X[:, 0] + 0.5 * X[:, 1], [-0.7, 0.7]).astype(float)
+    df = DataFrame({"features": X, "label": y})
+    m = clf(objective="multiclass", numIterations=20, featuresShapCol="shap", leafPredictionCol="leaf").fit(df)
+    out = m.transform(df)
+    assert out["probability"].shape == (3000, 3)
+    np.testing.assert_allclose(out["probability"].sum(1), 1.0, rtol=1e-9)
+    assert (out["prediction"] == y).mean() > 0.9
+    assert out["shap"].shape == (3000, (6 + 1) * 3)          # LightGBMTestUtils.scala:81-93
+    assert out["leaf"].shape == (3000, m.getBoosterNumTotalModel())
+    # SHAP additivity per class block
+    raw = out["rawPrediction"]
+    sh = out["shap"].reshape(3000, 3, 7).sum(2)
+    np.testing.assert_allclose(sh, raw, atol=1e-8)
+    imp_s = m.getFeatureImportances("split")
+    imp_g = m.getFeatureImportances("gain")
+    assert len(imp_s) == 6 and np.argmax(imp_g) in (0, 1)
+
+
+def test_model_text_save_load_and_params_section(tmp_path):
+    df, X, y = binary_df()
+    m = clf(numIterations=10, lambdaL1=0.1, isEnableSparse=False, useMissing=False, zeroAsMissing=True,
+            slotNames=[f"Age_years{i}" if i == 0 else f"c{i}" for i in range(10)]).fit(df)
+    s = m.getNativeModel()
+    for needle in ["[lambda_l1: 0.1]", "is_enable_sparse: 0", "use_missing: 0", "zero_as_missing: 1", "Age_years"]:
+        assert needle in s, needle
+    p = str(tmp_path / "native.txt")
+    m.saveNativeModel(p)
+    m2 = LightGBMClassificationModel.loadNativeModelFromFile(p)
+    np.testing.assert_allclose(m2.transform(df)["probability"], m.transform(df)["probability"])
+    m3 = LightGBMClassificationModel.loadNativeModelFromString(s)
+    assert m3.numClasses == 2
+    d = str(tmp_path / "stage")
+    m.save(d)
+    m4 = LightGBMClassificationModel.load(d)
+    np.testing.assert_allclose(m4.transform(df)["rawPrediction"], m.transform(df)["rawPrediction"])
+    assert "tree_info" in m.getLightGBMBooster().dumpModel()
+
+
+def test_pass_through_args_win():
+    df, _, _ = binary_df()
+    m = clf(numIterations=5, numLeaves=31, passThroughArgs="num_leaves=4 min_data_in_leaf=5").fit(df)
+    s = m.getNativeModel()
+    assert "[num_leaves: 4]" in s and "[min_data_in_leaf: 5]" in s
+    assert all(int(l.split("=")[1]) <= 4 for l in s.splitlines() if l.startswith("num_leaves="))
+
+
+def test_early_stopping_truncates_to_best_iteration():
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((3000, 5))
+    y = (X[:, 0] + rng.standard_normal(3000) > 0).astype(float)
+    val = rng.random(3000) < 0.3
+    df = DataFrame({"features": X, "label": y, "isVal": val})
+    m = clf(numIterations=200, earlyStoppingRound=5, validationIndicatorCol="isVal", metric="auc",
+            learningRate=0.3).fit(df)
+    best = m.getBoosterBestIteration()
+    assert 0 <= best < 199
+    assert m.getBoosterNumTotalIterations() == best + 1
+
+
+def test_num_batches_and_continued_training():
+    df, X, y = binary_df()
+    m1 = clf(numIterations=5, numBatches=2).fit(df)
+    assert m1.getBoosterNumTotalIterations() == 10
+    m2 = clf(numIterations=5, modelString=m1.getNativeModel()).fit(df)
+    assert m2.getBoosterNumTotalIterations() == 15
+    a1 = roc_auc_score(y, m1.transform(df)["probability"][:, 1])
+    a2 = roc_auc_score(y, m2.transform(df)["probability"][:, 1])
+    assert a2 >= a1 - 1e-3
+
+
+def test_custom_objective_improves():
+    df, X, y = binary_df()
+
+    def fobj(preds, _data):
+        p = 1.0 / (1.0 + np.exp(-preds))
+        return p - y, p * (1 - p)
+
+    m = clf(numIterations=20, fobj=fobj).fit(df)
+    raw = m.transform(df)["rawPrediction"][:, 1]
+    assert roc_auc_score(y, raw) > 0.85
+
+
+def test_delegate_learning_rate_schedule():
+    calls = []
+
+    class D(LightGBMDelegate):
+        def getLearningRate(self, batchIndex, partitionId, curIters, log, trainParams, previousLearningRate):
+            calls.append(curIters)
+            return 0.5 if curIters < 2 else 0.05
+
+    df, _, _ = binary_df()
+    m = clf(numIterations=5, delegate=D()).fit(df)
+    assert calls == [0, 1, 2, 3, 4]
+    assert m.getBoosterNumTotalIterations() == 5
+
+
+def test_seed_deterministic_reproducible():
+    df, X, y = binary_df()
+    aucs = set()
+    for _ in range(3):
+        m = clf(numIterations=10, seed=1, deterministic=True, baggingFraction=0.8, baggingFreq=1,
+                featureFraction=0.8).fit(df)
+        aucs.add(round(roc_auc_score(y, m.transform(df)["probability"][:, 1]), 12))
+    assert len(aucs) == 1
+
+
+@pytest.mark.parametrize("boosting", ["gbdt", "rf", "dart", "goss"])
+def test_boosting_types(boosting):
+    df, X, y = binary_df()
+    extra = dict(baggingFraction=0.7, baggingFreq=1) if boosting == "rf" else {}
+    m = clf(numIterations=20, boostingType=boosting, **extra).fit(df)
+    assert roc_auc_score(y, m.transform(df)["probability"][:, 1]) > 0.85
+
+
+def test_weights_categorical_sparse_and_missing():
+    rng = np.random.default_rng(3)
+    n = 3000
+    cat = rng.integers(0, 8, n)
+    x1 = rng.standard_normal(n)
+    x1[rng.random(n) < 0.1] = np.nan
+    y = ((cat % 3 == 0) ^ (np.nan_to_num(x1) > 0.5)).astype(float)
+    X = np.stack([cat, x1, rng.standard_normal(n)], 1)
+    df = DataFrame({"features": X, "label": y, "w": rng.random(n) + 0.5})
+    m = clf(numIterations=30, categoricalSlotIndexes=[0], weightCol="w").fit(df)
+    assert "num_cat=" in m.getNativeModel()
+    assert roc_auc_score(y, m.transform(df)["probability"][:, 1]) > 0.95
+    sp = np.empty(n, dtype=object)
+    for i in range(n):
+        nz = np.nonzero(np.nan_to_num(X[i]))[0]
+        sp[i] = SparseVector(3, nz, X[i, nz])
+    m2 = clf(numIterations=10).fit(DataFrame({"features": sp, "label": y}))
+    assert m2.transform(DataFrame({"features": sp, "label": y}))["probability"].shape == (n, 2)
+
+
+def test_predict_disable_shape_check():
+    df, X, y = binary_df(f=3)
+    m = clf(numIterations=5).fit(df)
+    wide = DataFrame({"features": np.concatenate([X, np.zeros((len(X), 12))], 1)})
+    with pytest.raises(ValueError):
+        m.transform(wide)
+    m.setPredictDisableShapeCheck(True)
+    assert m.transform(wide)["probability"].shape[0] == len(X)
+
+
+def test_iteration_controls_at_predict_time():
+    df, X, y = binary_df()
+    m = clf(numIterations=20).fit(df)
+    full = m.transform(df)["rawPrediction"][:, 1]
+    m.setNumIterations(5)
+    part = m.transform(df)["rawPrediction"][:, 1]
+    assert not np.allclose(full, part)
+    m.setNumIterations(-1).setStartIteration(0)
+    np.testing.assert_allclose(m.transform(df)["rawPrediction"][:, 1], full)
+
+
+def test_init_score_and_empty_partition():
+    df, X, y = binary_df()
+    df2 = df.withColumn("init", np.zeros(len(X)) + 0.5)
+    m = clf(numIterations=5, initScoreCol="init").fit(df2)
+    assert m.getBoosterNumTotalIterations() == 5
+    # an empty partition must not hang (VerifyLightGBMClassifierStream.scala:449-461)
+    df3 = df.filter(np.arange(len(X)) >= 2000)  # first partition now empty
+    m3 = clf(numIterations=5).fit(df3)
+    assert m3.getBoosterNumTotalIterations() == 5
+
+
+def test_sampling_modes_and_reference_dataset_reuse():
+    df, X, y = binary_df()
+    for mode in ["global", "subset", "fixed"]:
+        est = clf(numIterations=3, samplingMode=mode, binSampleCount=1000)
+        est.fit(df)
+    est = clf(numIterations=3)
+    est.fit(df)
+    ref = est._last_reference
+    m = clf(numIterations=3, referenceDataset=ref).fit(df)
+    assert m.getBoosterNumTotalIterations() == 3
+    meas = est.getPerformanceMeasures()
+    assert meas and meas[0]["training_iterations_ms"] > 0 and "sampling_ms" in meas[0]
+
+
+@pytest.mark.parametrize("objective", ["regression", "regression_l1", "huber", "fair", "poisson", "quantile",
+                                       "mape", "gamma", "tweedie"])
+def test_regression_objectives(objective):
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((2000, 5))
+    y = np.exp(0.5 * X[:, 0] + 0.2 * X[:, 1]) * (1 + 0.05 * rng.random(2000))
+    df = DataFrame({"features": X, "label": y})
+    m = LightGBMRegressor(deviceType="cpu", numIterations=40, objective=objective).fit(df)
+    pred = m.transform(df)["prediction"]
+    assert np.corrcoef(pred, y)[0, 1] > 0.8
+
+
+def test_regressor_save_load_and_tweedie_param(tmp_path):
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((1000, 4))
+    y = np.abs(X[:, 0]) + 0.1
+    df = DataFrame({"features": X, "label": y})
+    m = LightGBMRegressor(deviceType="cpu", numIterations=10, objective="tweedie", tweedieVariancePower=1.3).fit(df)
+    assert "tweedie_variance_power:1.3" in m.getNativeModel()
+    p = str(tmp_path / "r")
+    m.save(p)
+    np.testing.assert_allclose(LightGBMRegressionModel.load(p).transform(df)["prediction"],
+                               m.transform(df)["prediction"])
+
+
+def test_ranker_lambdarank_ndcg():
+    rng = np.random.default_rng(6)
+    nq, per = 200, 10
+    X = rng.standard_normal((nq * per, 5))
+    rel = np.clip(np.round(X[:, 0] + 0.5 * X[:, 1] + 1.5 + 0.3 * rng.standard_normal(nq * per)), 0, 4)
+    groups = np.repeat([f"q{i}" for i in range(nq)], per)
+    perm = rng.permutation(nq * per)  # interleave groups: the estimator must regroup
+    df = DataFrame({"features": X[perm], "label": rel[perm], "group": groups[perm]})
+    m = LightGBMRanker(deviceType="cpu", numIterations=30, groupCol="group", evalAt=[5]).fit(df)
+    pred = m.transform(df)["prediction"]
+    # NDCG@5 averaged over queries
+    from collections import defaultdict
+
+    by = defaultdict(list)
+    for g, p, r in zip(df["group"], pred, df["label"]):
+        by[g].append((p, r))
+    nd = []
+    for items in by.values():
+        order = sorted(items, key=lambda t: -t[0])
+        gains = [(2 ** r - 1) / np.log2(i + 2) for i, (_, r) in enumerate(order[:5])]
+        ideal = [(2 ** r - 1) / np.log2(i + 2) for i, r in enumerate(sorted([r for _, r in items], reverse=True)[:5])]
+        nd.append(sum(gains) / sum(ideal) if sum(ideal) > 0 else 1.0)
+    assert np.mean(nd) > 0.85
