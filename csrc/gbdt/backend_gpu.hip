@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -158,59 +159,167 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 
 // ---------------------------------------------------------------- K3
 // One block = one contiguous chunk of the leaf's row segment x one group of 32
-// features. Rows' bins are fetched as dwords (4 features), gradients as float2
+// features. A thread owns whole rows: the 32 bins of its feature group are two
+// dwordx4 loads (rows are padded to 16 B), the gradient pair one float2 load
 // from the ordered copy (or the physical arrays for an unpartitioned root).
+// kHistUnroll rows are fetched before any is accumulated so every wave keeps
+// several gathers in flight (the loop is latency-bound otherwise); the adds go
+// to LDS-privatised histograms with ds_add_f32, one row per lane, so the lanes
+// of a wave hit the same feature at random bins (bank = (feature + bin) % 32
+// thanks to the 257-float row pitch).
+constexpr int kHistUnroll = 4;
+
+// Accumulation modes (selected per backend, SML_HIST_MODE overrides):
+//  0: two ds_add_f32 per (row, feature)
+//  1: fixed point, g and h packed in one 64-bit word -> one ds_add_u64; h >= 0
+//     lives in the low 32 bits (never carries), g in the high 32 (two's
+//     complement wraps exactly). Integer adds are order independent, so the
+//     histogram is bitwise deterministic.
+//  2: fixed point, two ds_add_u32
+// Fixed-point scales are chosen per launch from the block's row count and the
+// tree's max |g|, max h so no block sum can overflow (>= 16 bits per value at
+// the root, ~20 bits for typical leaves).
+__device__ __forceinline__ uint32_t word_of(const uint4& b, int j) {
+  return j < 4 ? b.x : (j < 8 ? b.y : (j < 12 ? b.z : b.w));
+}
+
+template <int MODE>
+__device__ __forceinline__ void hist_add(void* lds, int j, uint32_t bin, float2 v, int32_t gq, uint32_t hq,
+                                         unsigned long long packed) {
+  if (MODE == 0) {
+    float* shg = static_cast<float*>(lds);
+    float* shh = shg + kFeatPerGroup * kHistStride;
+    atomicAdd(&shg[j * kHistStride + bin], v.x);
+    atomicAdd(&shh[j * kHistStride + bin], v.y);
+  } else if (MODE == 1) {
+    unsigned long long* sh = static_cast<unsigned long long*>(lds);
+    atomicAdd(&sh[j * kHistStride + bin], packed);
+  } else {
+    uint32_t* shg = static_cast<uint32_t*>(lds);
+    uint32_t* shh = shg + kFeatPerGroup * kHistStride;
+    atomicAdd(&shg[j * kHistStride + bin], static_cast<uint32_t>(gq));
+    atomicAdd(&shh[j * kHistStride + bin], hq);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void hist_accumulate(void* lds, const uint4& b0, const uint4& b1, float2 v, int Fg,
+                                                float sg, float sh) {
+  int32_t gq = 0;
+  uint32_t hq = 0;
+  unsigned long long packed = 0;
+  if (MODE != 0) {
+    gq = __float2int_rn(v.x * sg);
+    hq = static_cast<uint32_t>(__float2uint_rn(fmaxf(v.y, 0.f) * sh));
+    packed = (static_cast<unsigned long long>(static_cast<uint32_t>(gq)) << 32) | hq;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (j < Fg) hist_add<MODE>(lds, j, (word_of(b0, j) >> (8 * (j & 3))) & 255u, v, gq, hq, packed);
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (j + 16 < Fg) hist_add<MODE>(lds, j + 16, (word_of(b1, j) >> (8 * (j & 3))) & 255u, v, gq, hq, packed);
+  }
+}
+
+template <int MODE>
 __global__ __launch_bounds__(kHistThreads) void hist_kernel(
-    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint32_t* __restrict__ bins,
-    int W, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
+    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
+    int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
     const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
-    const float* __restrict__ h, float2* __restrict__ slab) {
+    const float* __restrict__ h, const float* __restrict__ ghmax, float2* __restrict__ slab) {
   if (st->done) return;
   const DLeaf L = HistSeg(st, leaves);
   const int count = L.count;
   const int nb_active = max(1, min(kMaxHistBlocks, ceil_div_i(count, kMinRowsPerHistBlock)));
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ float sh[2 * kFeatPerGroup * kHistStride];
+  constexpr int kWordBytes = MODE == 1 ? 8 : 4;
+  constexpr int kArrays = MODE == 1 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kArrays * kFeatPerGroup * kHistStride * kWordBytes];
+  void* lds = lds_raw;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 2 * kFeatPerGroup * kHistStride; i += kHistThreads) sh[i] = 0.f;
+  {
+    uint32_t* z = reinterpret_cast<uint32_t*>(lds_raw);
+    for (int i = tid; i < kArrays * kFeatPerGroup * kHistStride * kWordBytes / 4; i += kHistThreads) z[i] = 0u;
+  }
   __syncthreads();
   const int grp = blockIdx.y;
-  const int Wg = min(kFeatPerGroup / 4, W - grp * (kFeatPerGroup / 4));
   const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
+  const int col = grp * 2;            // first uint4 of this group in a row
+  const bool two = Fg > 16;
   const int chunk = ceil_div_i(count, nb_active);
   const int p0 = L.begin + blockIdx.x * chunk;
   const int p1 = min(L.begin + count, p0 + chunk);
-  const int32_t* perm = L.buf == 0 ? perm0 : perm1;
-  const float2* ogh = L.buf == 0 ? ogh0 : ogh1;
+  // fixed-point scales (unused in MODE 0)
+  float sg = 0.f, shs = 0.f;
+  if (MODE != 0) {
+    const float gmax = fmaxf(ghmax[0], 1e-30f), hmax = fmaxf(ghmax[1], 1e-30f);
+    const float rows = static_cast<float>(max(1, chunk));
+    sg = 2.0e9f / (rows * gmax);
+    shs = (MODE == 1 ? 4.0e9f : 2.0e9f) / (rows * hmax);
+  }
+  const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
+  const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
   const bool phys = L.buf < 0;
-  if (p1 > p0) {
-    const int items = (p1 - p0) * Wg;
-    for (int it = tid; it < items; it += kHistThreads) {
-      const int q = it / Wg;
-      const int w = it - q * Wg;
-      const int pos = p0 + q;
-      int r;
-      float2 v;
-      if (phys) { r = pos; v = make_float2(g[r], h[r]); }
-      else { r = perm[pos]; v = ogh[pos]; }
-      const uint32_t b4 = bins[static_cast<size_t>(r) * W + grp * (kFeatPerGroup / 4) + w];
+  for (int base = p0 + tid; base < p1; base += kHistThreads * kHistUnroll) {
+    int r[kHistUnroll];
+    bool ok[kHistUnroll];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = w * 4 + j;
-        if (f < Fg) {
-          const uint32_t b = (b4 >> (8 * j)) & 255u;
-          atomicAdd(&sh[f * kHistStride + b], v.x);
-          atomicAdd(&sh[kFeatPerGroup * kHistStride + f * kHistStride + b], v.y);
-        }
-      }
+    for (int u = 0; u < kHistUnroll; ++u) {
+      const int pos = base + u * kHistThreads;
+      ok[u] = pos < p1;
+      r[u] = ok[u] ? (phys ? pos : perm[pos]) : 0;
     }
+    uint4 b0[kHistUnroll], b1[kHistUnroll];
+    float2 v[kHistUnroll];
+#pragma unroll
+    for (int u = 0; u < kHistUnroll; ++u) {
+      const int pos = base + u * kHistThreads;
+      const size_t rb = static_cast<size_t>(r[u]) * W4 + col;
+      b0[u] = bins4[rb];
+      b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
+      v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : (ok[u] ? ogh[pos] : make_float2(0.f, 0.f));
+    }
+#pragma unroll
+    for (int u = 0; u < kHistUnroll; ++u)
+      if (ok[u]) hist_accumulate<MODE>(lds, b0[u], b1[u], v[u], Fg, sg, shs);
   }
   __syncthreads();
   float2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
   for (int i = tid; i < Fg * kBinsPerFeature; i += kHistThreads) {
     const int f = i >> 8, b = i & 255;
-    out[(grp * kFeatPerGroup + f) * kBinsPerFeature + b] =
-        make_float2(sh[f * kHistStride + b], sh[kFeatPerGroup * kHistStride + f * kHistStride + b]);
+    float2 o;
+    if (MODE == 0) {
+      const float* shg = reinterpret_cast<const float*>(lds_raw);
+      o = make_float2(shg[f * kHistStride + b], shg[kFeatPerGroup * kHistStride + f * kHistStride + b]);
+    } else if (MODE == 1) {
+      const unsigned long long w = reinterpret_cast<const unsigned long long*>(lds_raw)[f * kHistStride + b];
+      o = make_float2(static_cast<float>(static_cast<double>(static_cast<int32_t>(w >> 32)) / sg),
+                      static_cast<float>(static_cast<double>(static_cast<uint32_t>(w)) / shs));
+    } else {
+      const uint32_t* shg = reinterpret_cast<const uint32_t*>(lds_raw);
+      o = make_float2(static_cast<float>(static_cast<double>(static_cast<int32_t>(shg[f * kHistStride + b])) / sg),
+                      static_cast<float>(static_cast<double>(shg[kFeatPerGroup * kHistStride + f * kHistStride + b]) / shs));
+    }
+    out[(grp * kFeatPerGroup + f) * kBinsPerFeature + b] = o;
+  }
+}
+
+// max |g|, max h of one class (fixed-point scales of the histogram kernel)
+__global__ void ghmax_kernel(const float* __restrict__ g, const float* __restrict__ h, int64_t n,
+                             unsigned int* __restrict__ out_bits) {
+  float mg = 0.f, mh = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    mg = fmaxf(mg, fabsf(g[i]));
+    mh = fmaxf(mh, fabsf(h[i]));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { mg = fmaxf(mg, __shfl_xor(mg, off, 64)); mh = fmaxf(mh, __shfl_xor(mh, off, 64)); }
+  if ((threadIdx.x & 63) == 0) {
+    // non-negative floats order like their bit patterns
+    atomicMax(&out_bits[0], __float_as_uint(mg));
+    atomicMax(&out_bits[1], __float_as_uint(mh));
   }
 }
 
@@ -421,6 +530,9 @@ __global__ __launch_bounds__(256) void find_split_kernel(
   if (lane == 63) { wsum_g[wid] = vg; wsum_h[wid] = vh; }
   __syncthreads();
   for (int w = 0; w < wid; ++w) { vg += wsum_g[w]; vh += wsum_h[w]; }
+  __shared__ double pref_g[256], pref_h[256];
+  pref_g[tid] = vg;
+  pref_h[tid] = vh;
   const double cnt_factor = cnt / fmax(H, kEpsilon);
   const double parent_gain = LeafGain(G, H, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
   const double shift = parent_gain + sp.min_gain_to_split;
@@ -458,9 +570,8 @@ __global__ __launch_bounds__(256) void find_split_kernel(
     if (b.gain == -INFINITY) {
       r.feature = -1; r.gain = -INFINITY;
     } else {
-      // recompute the winning prefix (serial, cheap) for exact sums
-      double gl = 0, hl = 0;
-      for (int t = 0; t <= b.thr; ++t) if (t != zero_bin && t != nan_bin) { gl += sg_[t]; hl += shh_[t]; }
+      // the winning prefix, exactly as the candidate saw it
+      double gl = pref_g[b.thr], hl = pref_h[b.thr];
       if (mt != kMissingNone && b.dl) { gl += mg; hl += mh; }
       const double gr = G - gl, hr = H - hl;
       r.feature = f; r.gain = b.gain; r.threshold = static_cast<uint32_t>(b.thr); r.default_left = b.dl;
@@ -476,72 +587,108 @@ __global__ __launch_bounds__(256) void find_split_kernel(
 }
 
 // ---------------------------------------------------------------- choose + tree bookkeeping
-// One block. Reduces the per-feature results of the new leaves, then picks the
-// next leaf to split (max gain), records the split in the device tree and sets
-// up the partition of that leaf.
+// One block. Wave c reduces the per-feature results of new leaf c (lanes
+// stride over features), all threads then reduce the leaves' best gains, and
+// thread 0 records the chosen split in the device tree and sets up the
+// partition of that leaf. Every global read on the serial path is independent
+// so the bookkeeping costs a few memory latencies, not one per leaf/feature.
+struct KeyG {
+  double gain;
+  int a, b;  // tie-breakers (smaller wins)
+};
+
+__device__ __forceinline__ bool KeyBetter(const KeyG& x, const KeyG& y) {
+  if (x.gain != y.gain) return x.gain > y.gain;
+  if (x.a != y.a) return x.a < y.a;
+  return x.b < y.b;
+}
+
+__device__ __forceinline__ KeyG WaveArgmax(KeyG k) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    KeyG o;
+    o.gain = __shfl_xor(k.gain, off, 64);
+    o.a = __shfl_xor(k.a, off, 64);
+    o.b = __shfl_xor(k.b, off, 64);
+    if (KeyBetter(o, k)) k = o;
+  }
+  return k;
+}
+
 __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DLeaf* __restrict__ leaves,
-                                                     SplitResult* __restrict__ lbest,
+                                                     SplitResult* __restrict__ lbest, double* __restrict__ lgain,
                                                      const SplitResult* __restrict__ fbest, int F, DTree t,
-                                                     const int32_t* __restrict__ feat_missing,
                                                      const double* __restrict__ count_slot) {
   if (st->done) return;
-  const int tid = threadIdx.x;
-  __shared__ int sh_best_child[2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ int sh_best_f[2];
+  __shared__ KeyG wk[4];
   const bool root = st->phase == 0;
   const int nchild = root ? 1 : 2;
-  // per-child argmax over features (thread 0/1 serially; F is small)
-  if (tid < nchild) {
-    int bi = -1;
-    for (int f = 0; f < F; ++f) {
-      const SplitResult& r = fbest[tid * F + f];
+  const int small_leaf = st->small_leaf, large_leaf = st->large_leaf;
+  if (wid < nchild) {
+    KeyG k{-INFINITY, 1 << 30, 1 << 30};
+    for (int f = lane; f < F; f += 64) {
+      const SplitResult& r = fbest[wid * F + f];
       if (r.feature < 0) continue;
-      if (bi < 0 || SplitBetter(r.gain, r.feature, r.threshold, fbest[tid * F + bi].gain, fbest[tid * F + bi].feature,
-                                fbest[tid * F + bi].threshold))
-        bi = f;
+      KeyG c{r.gain, r.feature, static_cast<int>(r.threshold)};
+      if (KeyBetter(c, k)) { k = c; k.b = (static_cast<int>(r.threshold) & 0xFFFF) | (f << 16); }
     }
-    sh_best_child[tid] = bi;
+    k = WaveArgmax(k);
+    if (lane == 0) sh_best_f[wid] = k.gain == -INFINITY ? -1 : (k.b >> 16);
   }
   __syncthreads();
-  if (tid != 0) return;
-  // store leaf bests + global counts
-  if (root) {
-    const int bi = sh_best_child[0];
-    if (bi >= 0) lbest[0] = fbest[bi]; else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; }
-    t.lval[0] = 0.0;
-    t.lcount[0] = leaves[0].gcount;
-    t.lweight[0] = leaves[0].sum_h;
-    t.lparent[0] = -1;
-    t.ldepth[0] = 0;
-  } else {
-    const int64_t small_cnt = static_cast<int64_t>(*count_slot);
-    const int s = st->small_leaf, l = st->large_leaf;
-    const int64_t parent_cnt = leaves[l].gcount;  // choose stored parent count here
-    {
+  if (tid == 0) {
+    if (root) {
+      const int bi = sh_best_f[0];
+      if (bi >= 0) { lbest[0] = fbest[bi]; lgain[0] = fbest[bi].gain; }
+      else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; lgain[0] = -INFINITY; }
+      t.lval[0] = 0.0;
+      t.lcount[0] = leaves[0].gcount;
+      t.lweight[0] = leaves[0].sum_h;
+      t.lparent[0] = -1;
+      t.ldepth[0] = 0;
+    } else {
+      const int64_t small_cnt = static_cast<int64_t>(*count_slot);
+      const int64_t parent_cnt = leaves[large_leaf].gcount;  // stored by the previous choose
       const int ob = st->pbuf == 0 ? 1 : 0;
       DLeaf& Lc = leaves[st->split_leaf];
       DLeaf& Rc = leaves[st->new_leaf];
       Lc.begin = st->pbegin; Lc.count = st->ptotal; Lc.buf = ob;
       Rc.begin = st->pbegin + st->ptotal; Rc.count = st->pcount - st->ptotal; Rc.buf = ob;
-    }
-    leaves[s].gcount = small_cnt;
-    leaves[l].gcount = parent_cnt - small_cnt;
-    t.lcount[s] = leaves[s].gcount;
-    t.lcount[l] = leaves[l].gcount;
-    for (int c = 0; c < 2; ++c) {
-      const int leaf = c == 0 ? s : l;
-      const int bi = sh_best_child[c];
-      if (bi >= 0) lbest[leaf] = fbest[c * F + bi]; else { lbest[leaf].feature = -1; lbest[leaf].gain = -INFINITY; }
+      leaves[small_leaf].gcount = small_cnt;
+      leaves[large_leaf].gcount = parent_cnt - small_cnt;
+      t.lcount[small_leaf] = small_cnt;
+      t.lcount[large_leaf] = parent_cnt - small_cnt;
+      for (int c = 0; c < 2; ++c) {
+        const int leaf = c == 0 ? small_leaf : large_leaf;
+        const int bi = sh_best_f[c];
+        if (bi >= 0) { lbest[leaf] = fbest[c * F + bi]; lgain[leaf] = fbest[c * F + bi].gain; }
+        else { lbest[leaf].feature = -1; lbest[leaf].gain = -INFINITY; lgain[leaf] = -INFINITY; }
+      }
     }
   }
-  // pick the next leaf
+  __syncthreads();
   const int nl = st->num_leaves;
-  if (nl >= st->max_leaves) { st->done = 1; return; }
-  int bl = -1;
-  for (int i = 0; i < nl; ++i) {
-    if (lbest[i].feature < 0) continue;
-    if (bl < 0 || lbest[i].gain > lbest[bl].gain) bl = i;
+  if (nl >= st->max_leaves) {
+    if (tid == 0) st->done = 1;
+    return;
   }
-  if (bl < 0 || !(lbest[bl].gain > 0.0)) { st->done = 1; return; }
+  // argmax over leaves (ties -> smaller leaf id)
+  KeyG k{-INFINITY, 1 << 30, 0};
+  for (int i = tid; i < nl; i += 256) {
+    const double gi = lgain[i];
+    KeyG c{gi, i, 0};
+    if (gi > -INFINITY && KeyBetter(c, k)) k = c;
+  }
+  k = WaveArgmax(k);
+  if (lane == 0) wk[wid] = k;
+  __syncthreads();
+  if (tid != 0) return;
+  KeyG best = wk[0];
+  for (int w = 1; w < 4; ++w) if (KeyBetter(wk[w], best)) best = wk[w];
+  const int bl = best.gain == -INFINITY ? -1 : best.a;
+  if (bl < 0 || !(best.gain > 0.0)) { st->done = 1; return; }
   const SplitResult sr = lbest[bl];
   const int node = nl - 1;
   const int parent = t.lparent[bl];
@@ -565,7 +712,6 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
   t.lcount[bl] = sr.left_cnt; t.lcount[nl] = sr.right_cnt;
   const int depth = t.ldepth[bl] + 1;
   t.ldepth[bl] = depth; t.ldepth[nl] = depth;
-  // leaf records for the children (segments are filled by the partition)
   const DLeaf P = leaves[bl];
   DLeaf Lc = P, Rc = P;
   Lc.depth = depth; Rc.depth = depth;
@@ -579,6 +725,8 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
   if (left_small) { Rc.gcount = P.gcount; } else { Lc.gcount = P.gcount; }
   leaves[bl] = Lc;
   leaves[nl] = Rc;
+  lgain[bl] = -INFINITY;
+  lgain[nl] = -INFINITY;
   st->pbegin = P.begin; st->pcount = P.count; st->pbuf = P.buf; st->ptotal = 0;
   st->split_leaf = bl;
   st->new_leaf = nl;
@@ -586,20 +734,22 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
   st->large_leaf = left_small ? nl : bl;
   st->num_leaves = nl + 1;
   st->phase = 1;
-  (void)feat_missing;
 }
 
 // ---------------------------------------------------------------- K6
-__device__ __forceinline__ bool RowGoesLeft(const uint8_t* bins8, int S, int r, const SplitResult& sr, FeatMeta fm) {
+// Decisions read the column-major copy: the lanes of a wave touch one byte
+// column (contiguous for the physical root, increasing for partitioned leaves)
+// instead of one 32-B row each.
+__device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int r, const SplitResult& sr, FeatMeta fm) {
   const int f = sr.feature;
-  const uint32_t b = bins8[static_cast<size_t>(r) * S + f];
+  const uint32_t b = cbins[static_cast<size_t>(f) * n + r];
   return DeviceGoesLeft(b, fm.num_bin[f], fm.missing[f], fm.default_bin[f], sr.is_cat, sr.threshold,
                         sr.default_left, sr.cat_bits);
 }
 
 __global__ __launch_bounds__(kPartThreads) void part_count_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const SplitResult* __restrict__ lbest,
-    const uint8_t* __restrict__ bins8, int S, const int32_t* __restrict__ perm0,
+    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, FeatMeta fm, int32_t* __restrict__ counts) {
   if (st->done) return;
   DLeaf P;
@@ -614,7 +764,7 @@ __global__ __launch_bounds__(kPartThreads) void part_count_kernel(
   int c = 0;
   for (int p = p0 + threadIdx.x; p < p1; p += kPartThreads) {
     const int r = P.buf < 0 ? p : perm[p];
-    c += RowGoesLeft(bins8, S, r, sr, fm) ? 1 : 0;
+    c += RowGoesLeft(cbins, n, r, sr, fm) ? 1 : 0;
   }
   __shared__ int sc[kPartThreads / 64];
 #pragma unroll
@@ -630,7 +780,7 @@ __global__ __launch_bounds__(kPartThreads) void part_count_kernel(
 
 __global__ __launch_bounds__(kPartThreads) void part_scatter_kernel(
     DState* __restrict__ st, const DLeaf* __restrict__ leaves, const SplitResult* __restrict__ lbest,
-    const uint8_t* __restrict__ bins8, int S, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
+    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
     const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0,
     int32_t* __restrict__ wperm1, float2* __restrict__ wogh0, float2* __restrict__ wogh1,
     const float* __restrict__ g, const float* __restrict__ h, FeatMeta fm, const int32_t* __restrict__ counts) {
@@ -679,7 +829,7 @@ __global__ __launch_bounds__(kPartThreads) void part_scatter_kernel(
     if (valid) {
       if (P.buf < 0) { r = p; v = make_float2(g[r], h[r]); }
       else { r = perm[p]; v = ogh[p]; }
-      left = RowGoesLeft(bins8, S, r, sr, fm);
+      left = RowGoesLeft(cbins, n, r, sr, fm);
     }
     const unsigned long long bl = __ballot(valid && left);
     const unsigned long long bv = __ballot(valid);
@@ -710,34 +860,43 @@ __global__ __launch_bounds__(kPartThreads) void part_scatter_kernel(
 }
 
 // ---------------------------------------------------------------- K7
+// Node = one int4 {feature | missing<<16 | default_left<<18 | is_cat<<19,
+// threshold bin, left, right}: a single 16-B load per level; bins come from the
+// column-major copy so a wave's loads of one level are coalesced.
 struct DevTreeView {
-  const int32_t* feat;
-  const uint32_t* thr;
-  const int32_t* flags;  // bit0 cat, bit1 default_left, bits2-3 missing
-  const int32_t* left;
-  const int32_t* right;
+  const int4* nodes;
   const uint32_t* cat_bits;  // 8 words per node
   const double* lval;
   int num_leaves;
 };
 
-__global__ void score_kernel(DevTreeView tv, const uint8_t* __restrict__ bins8, int S, int64_t n,
-                             FeatMeta fm, double scale, double* __restrict__ score, int32_t* __restrict__ leaf_out) {
+__global__ void score_kernel(DevTreeView tv, const uint8_t* __restrict__ cbins, int64_t n, FeatMeta fm,
+                             double scale, double* __restrict__ score, int32_t* __restrict__ leaf_out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int node = 0;
     if (tv.num_leaves > 1) {
-      const uint8_t* row = bins8 + i * S;
       for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
-        const int f = tv.feat[node];
-        const int fl = tv.flags[node];
-        const bool left = DeviceGoesLeft(row[f], fm.num_bin[f], (fl >> 2) & 3, fm.default_bin[f], fl & 1,
-                                         tv.thr[node], (fl >> 1) & 1, tv.cat_bits + node * 8);
-        node = left ? tv.left[node] : tv.right[node];
+        const int4 nd = tv.nodes[node];
+        const int f = nd.x & 0xFFFF;
+        const int mt = (nd.x >> 16) & 3, dl = (nd.x >> 18) & 1, ic = (nd.x >> 19) & 1;
+        const uint32_t b = cbins[static_cast<size_t>(f) * n + i];
+        const bool left = DeviceGoesLeft(b, fm.num_bin[f], mt, fm.default_bin[f], ic, static_cast<uint32_t>(nd.y), dl,
+                                         tv.cat_bits + node * 8);
+        node = left ? nd.z : nd.w;
       }
       node = node < 0 ? ~node : 0;  // a malformed tree cannot loop forever
     }
     if (score) score[i] += scale * tv.lval[node];
     if (leaf_out) leaf_out[i] = node;
+  }
+}
+
+// row-major -> column-major bin copy (once per dataset)
+__global__ void transpose_bins_kernel(const uint8_t* __restrict__ bins, int S, int F, int64_t n,
+                                      uint8_t* __restrict__ cbins) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* row = bins + i * S;
+    for (int f = 0; f < F; ++f) cbins[static_cast<size_t>(f) * n + i] = row[f];
   }
 }
 
@@ -764,6 +923,9 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipGetDevice(&dev_));
     SML_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     sp_ = MakeSplitParams(cfg);
+    hist_mode_ = 1;  // packed fixed point (deterministic); SML_HIST_MODE=0 selects float atomics
+    if (const char* e = std::getenv("SML_HIST_MODE")) hist_mode_ = std::atoi(e);
+    ghmax_.alloc(2);
     F_ = d->ref.num_inner();
     S_ = d->row_stride;
     W_ = S_ / 4;
@@ -772,6 +934,10 @@ class GpuBackend : public TrainBackend {
     FG_ = (F_ + kFeatPerGroup - 1) / kFeatPerGroup;
     bins_.alloc(static_cast<size_t>(n_) * S_);
     SML_HIP_CHECK(hipMemcpyAsync(bins_.get(), d->bins.data(), static_cast<size_t>(n_) * S_, hipMemcpyHostToDevice, stream_));
+    cbins_.alloc(static_cast<size_t>(n_) * std::max(1, F_));
+    hipLaunchKernelGGL(transpose_bins_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, bins_.get(), S_, F_, n_,
+                       cbins_.get());
+    SML_HIP_CHECK(hipGetLastError());
     label_.alloc(n_);
     SML_HIP_CHECK(hipMemcpyAsync(label_.get(), d->label.data(), sizeof(float) * n_, hipMemcpyHostToDevice, stream_));
     if (!d->weight.empty()) {
@@ -788,6 +954,7 @@ class GpuBackend : public TrainBackend {
     count_slot_.alloc(1);
     fbest_.alloc(2 * F_);
     lbest_.alloc(L_);
+    lgain_.alloc(L_);
     leaves_.alloc(L_);
     state_.alloc(1);
     counts_.alloc(kMaxPartBlocks);
@@ -820,8 +987,8 @@ class GpuBackend : public TrainBackend {
     dt_.gain = td; dt_.ival = td + NI; dt_.iweight = td + 2 * NI; dt_.lval = td + 3 * NI; dt_.lweight = td + 3 * NI + L_;
     dt_.icount = tree_l_.get(); dt_.lcount = tree_l_.get() + NI;
     // score-update tree (uploaded from host trees)
-    up_i_.alloc(static_cast<size_t>(NI) * 4 + 4);
-    up_u_.alloc(static_cast<size_t>(NI) * 9 + 4);
+    up_nodes_.alloc(static_cast<size_t>(NI) + 1);
+    up_u_.alloc(static_cast<size_t>(NI) * 8 + 8);
     up_d_.alloc(L_ + 4);
     leaf_idx_.alloc(n_);
     SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
@@ -898,6 +1065,12 @@ class GpuBackend : public TrainBackend {
                          g, h, perm_[0].get(), ogh_[0].get());
       SML_HIP_CHECK(hipGetLastError());
     }
+    if (hist_mode_ != 0) {
+      SML_HIP_CHECK(hipMemsetAsync(ghmax_.get(), 0, 2 * sizeof(unsigned int), stream_));
+      hipLaunchKernelGGL(ghmax_kernel, dim3(GridFor(n_) < 2048 ? GridFor(n_) : 2048), dim3(256), 0, stream_, g, h, n_,
+                         ghmax_.get());
+      SML_HIP_CHECK(hipGetLastError());
+    }
     hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_.get(), leaves_.get(), root_count, root_buf, L_);
     SML_HIP_CHECK(hipGetLastError());
     // root histogram + split search
@@ -906,10 +1079,10 @@ class GpuBackend : public TrainBackend {
     for (int s = 1; s < L_; ++s) {
       // partition the chosen leaf, histogram its smaller child, search both
       hipLaunchKernelGGL(part_count_kernel, dim3(kMaxPartBlocks), dim3(kPartThreads), 0, stream_, state_.get(),
-                         leaves_.get(), lbest_.get(), bins_.get(), S_, perm_[0].get(), perm_[1].get(), fm_, counts_.get());
+                         leaves_.get(), lbest_.get(), cbins_.get(), n_, perm_[0].get(), perm_[1].get(), fm_, counts_.get());
       SML_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL(part_scatter_kernel, dim3(kMaxPartBlocks), dim3(kPartThreads), 0, stream_, state_.get(),
-                         leaves_.get(), lbest_.get(), bins_.get(), S_, perm_[0].get(), perm_[1].get(), ogh_[0].get(),
+                         leaves_.get(), lbest_.get(), cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(),
                          ogh_[1].get(), perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_,
                          counts_.get());
       SML_HIP_CHECK(hipGetLastError());
@@ -923,14 +1096,14 @@ class GpuBackend : public TrainBackend {
 
   void UpdateScore(const Tree& t, int k, double scale) override {
     DevTreeView tv = UploadTree(t);
-    hipLaunchKernelGGL(score_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, tv, bins_.get(), S_, n_, fm_, scale,
+    hipLaunchKernelGGL(score_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, tv, cbins_.get(), n_, fm_, scale,
                        score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
     SML_HIP_CHECK(hipGetLastError());
   }
 
   void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) override {
     DevTreeView tv = UploadTree(t);
-    hipLaunchKernelGGL(score_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, tv, bins_.get(), S_, n_, fm_, 0.0,
+    hipLaunchKernelGGL(score_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, tv, cbins_.get(), n_, fm_, 0.0,
                        static_cast<double*>(nullptr), leaf_idx_.get());
     SML_HIP_CHECK(hipGetLastError());
     leaf->resize(n_);
@@ -948,9 +1121,14 @@ class GpuBackend : public TrainBackend {
   }
 
   void EnqueueHistogram(const float* g, const float* h) {
-    hipLaunchKernelGGL(hist_kernel, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_.get(),
-                       leaves_.get(), reinterpret_cast<const uint32_t*>(bins_.get()), W_, F_, perm_[0].get(),
-                       perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, slab_.get());
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_.get(), leaves_.get(),
+                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(), perm_[1].get(),
+                         ogh_[0].get(), ogh_[1].get(), g, h, reinterpret_cast<const float*>(ghmax_.get()), slab_.get());
+    };
+    if (hist_mode_ == 1) launch(hist_kernel<1>);
+    else if (hist_mode_ == 2) launch(hist_kernel<2>);
+    else launch(hist_kernel<0>);
     SML_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + 255) / 256, kReduceSplit), dim3(256), 0, stream_, state_.get(),
                        leaves_.get(), slab_.get(), E_, part_.get(), count_slot_.get());
@@ -974,7 +1152,7 @@ class GpuBackend : public TrainBackend {
                        E_, count_slot_.get(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
     SML_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, state_.get(), leaves_.get(), lbest_.get(),
-                       fbest_.get(), F_, dt_, fm_.missing, count_slot_.get());
+                       lgain_.get(), fbest_.get(), F_, dt_, count_slot_.get());
     SML_HIP_CHECK(hipGetLastError());
   }
 
@@ -1045,37 +1223,34 @@ class GpuBackend : public TrainBackend {
 
   DevTreeView UploadTree(const Tree& t) {
     const int NI = std::max(1, t.num_leaves - 1);
-    const size_t need_i = static_cast<size_t>(NI) * 4, need_u = static_cast<size_t>(NI) * 9, need_d = t.num_leaves;
-    if (need_i > up_i_.n) up_i_.alloc(need_i);
+    const size_t need_n = static_cast<size_t>(NI), need_u = static_cast<size_t>(NI) * 8, need_d = t.num_leaves;
+    if (need_n > up_nodes_.n) up_nodes_.alloc(need_n);
     if (need_u > up_u_.n) up_u_.alloc(need_u);
     if (need_d > up_d_.n) up_d_.alloc(need_d);
-    // stage everything in the pinned buffer, then 3 async copies
-    const size_t bytes = need_i * 4 + need_u * 4 + need_d * 8;
+    const size_t bytes = need_n * 16 + need_u * 4 + need_d * 8;
     if (bytes > kPinnedBytes) throw std::runtime_error("tree too large for staging buffer");
     SML_HIP_CHECK(hipStreamSynchronize(stream_));  // pinned buffer reuse
-    int32_t* pi = static_cast<int32_t*>(pinned_);
-    uint32_t* pu = reinterpret_cast<uint32_t*>(pi + need_i);
-    double* pd = reinterpret_cast<double*>(pu + need_u + (need_u & 1));
+    int4* pn = static_cast<int4*>(pinned_);
+    uint32_t* pu = reinterpret_cast<uint32_t*>(pn + need_n);
+    double* pd = reinterpret_cast<double*>(pu + need_u);
     for (int node = 0; node < t.num_leaves - 1; ++node) {
-      pi[node] = t.split_feature_inner[node];
-      pi[NI + node] = static_cast<int32_t>(t.decision_type[node]);
-      pi[2 * NI + node] = t.left_child[node];
-      pi[3 * NI + node] = t.right_child[node];
-      pu[node] = t.threshold_in_bin[node];
-      for (int w = 0; w < 8; ++w) pu[NI + node * 8 + w] = 0;
-      if (t.decision_type[node] & 1) {
+      const int8_t dt = t.decision_type[node];
+      const int mt = (dt >> 2) & 3, dl = (dt >> 1) & 1, ic = dt & 1;
+      pn[node] = make_int4(t.split_feature_inner[node] | (mt << 16) | (dl << 18) | (ic << 19),
+                           static_cast<int>(t.threshold_in_bin[node]), t.left_child[node], t.right_child[node]);
+      for (int w = 0; w < 8; ++w) pu[node * 8 + w] = 0;
+      if (ic) {
         int ci = static_cast<int>(t.threshold_in_bin[node]);
-        int s = t.cat_boundaries_inner[ci], e = t.cat_boundaries_inner[ci + 1];
-        for (int w = 0; w < 8 && s + w < e; ++w) pu[NI + node * 8 + w] = t.cat_threshold_inner[s + w];
+        int s0 = t.cat_boundaries_inner[ci], e0 = t.cat_boundaries_inner[ci + 1];
+        for (int w = 0; w < 8 && s0 + w < e0; ++w) pu[node * 8 + w] = t.cat_threshold_inner[s0 + w];
       }
     }
     for (int l = 0; l < t.num_leaves; ++l) pd[l] = t.leaf_value[l];
-    SML_HIP_CHECK(hipMemcpyAsync(up_i_.get(), pi, need_i * 4, hipMemcpyHostToDevice, stream_));
+    SML_HIP_CHECK(hipMemcpyAsync(up_nodes_.get(), pn, need_n * 16, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipMemcpyAsync(up_u_.get(), pu, need_u * 4, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipMemcpyAsync(up_d_.get(), pd, need_d * 8, hipMemcpyHostToDevice, stream_));
     DevTreeView tv;
-    tv.feat = up_i_.get(); tv.flags = up_i_.get() + NI; tv.left = up_i_.get() + 2 * NI; tv.right = up_i_.get() + 3 * NI;
-    tv.thr = up_u_.get(); tv.cat_bits = up_u_.get() + NI; tv.lval = up_d_.get(); tv.num_leaves = t.num_leaves;
+    tv.nodes = up_nodes_.get(); tv.cat_bits = up_u_.get(); tv.lval = up_d_.get(); tv.num_leaves = t.num_leaves;
     return tv;
   }
 
@@ -1088,24 +1263,26 @@ class GpuBackend : public TrainBackend {
   int K_ = 1, F_ = 0, S_ = 4, W_ = 1, E_ = 0, L_ = 2, FG_ = 1;
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
-  DevBuf<uint8_t> bins_;
+  DevBuf<uint8_t> bins_, cbins_;
   DevBuf<float> label_, weight_, g_, h_;
   DevBuf<double> score_;
   DevBuf<int32_t> perm_[2];
   DevBuf<float2> ogh_[2];
   DevBuf<float2> slab_;
   DevBuf<double2> part_, hist_pool_;
-  DevBuf<double> count_slot_;
+  DevBuf<double> count_slot_, lgain_;
   DevBuf<SplitResult> fbest_, lbest_;
   DevBuf<DLeaf> leaves_;
   DevBuf<DState> state_;
   DevBuf<int32_t> counts_, meta_i_, bag_;
   DevBuf<int8_t> mask_;
+  DevBuf<unsigned int> ghmax_;
+  int hist_mode_ = 1;
   DevBuf<int32_t> tree_i_;
   DevBuf<uint32_t> tree_u_;
   DevBuf<double> tree_d_;
   DevBuf<int64_t> tree_l_;
-  DevBuf<int32_t> up_i_;
+  DevBuf<int4> up_nodes_;
   DevBuf<uint32_t> up_u_;
   DevBuf<double> up_d_;
   DevBuf<int32_t> leaf_idx_;

@@ -284,7 +284,7 @@ DatasetReference DatasetReference::FromSample(const double* sample, int64_t n_sa
 void Dataset::Init(const DatasetReference& r, int64_t n) {
   ref = r;
   num_data = n;
-  row_stride = std::max(4, r.row_stride());
+  row_stride = r.row_stride();
   bins.assign(static_cast<size_t>(n) * row_stride, 0);
   // rows that are never pushed hold every feature's zero bin
   std::vector<uint8_t> zrow(row_stride, 0);

@@ -9,6 +9,7 @@
 // multiple of 4 features, so a HIP kernel can fetch 4 feature bins per dword
 // and a gathered row (leaf index lists) is one contiguous 4*k byte segment.
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <limits>
@@ -84,7 +85,9 @@ struct DatasetReference {
                                              int64_t total_sample_cnt, const Config& cfg,
                                              const std::vector<std::string>& names);
   int num_inner() const { return static_cast<int>(used_features.size()); }
-  int row_stride() const { return ((num_inner() + 3) / 4) * 4; }
+  // rows are padded to 16 bytes so the HIP histogram kernel fetches 16
+  // feature bins per dwordx4 load
+  int row_stride() const { return std::max(16, ((num_inner() + 15) / 16) * 16); }
 };
 
 struct Dataset {

@@ -1,0 +1,288 @@
+// pybind11 module `synapseml_amd._vw`: VW-style learner + hashing + GPU SGD.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+
+#include "vw_core.h"
+#include "vw_gpu.h"
+
+namespace py = pybind11;
+using namespace smlvw;
+
+namespace {
+using F32 = py::array_t<float, py::array::c_style | py::array::forcecast>;
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+using U32 = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>;
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+
+// One namespace block of a batch: CSR over examples.
+struct Block {
+  unsigned char ns;
+  I64 indptr;
+  U32 idx;
+  F32 val;
+};
+
+std::vector<Block> ToBlocks(py::list blocks) {
+  std::vector<Block> out;
+  for (auto item : blocks) {
+    py::tuple t = item.cast<py::tuple>();
+    std::string ns = t[0].cast<std::string>();
+    out.push_back(Block{static_cast<unsigned char>(ns.empty() ? ' ' : ns[0]), py::cast<I64>(t[1]), py::cast<U32>(t[2]),
+                        py::cast<F32>(t[3])});
+  }
+  return out;
+}
+
+void FillExample(Example* ex, const std::vector<Block>& blocks, int64_t row) {
+  ex->ns.clear();
+  for (const auto& b : blocks) {
+    const int64_t s = b.indptr.data()[row], e = b.indptr.data()[row + 1];
+    if (e <= s) continue;
+    Namespace& n = ex->Get(b.ns);
+    for (int64_t p = s; p < e; ++p) n.f.push_back(Feature{b.val.data()[p], b.idx.data()[p]});
+  }
+}
+
+struct NcclHandle {
+  ncclComm_t c = nullptr;
+  int world = 1;
+  ~NcclHandle() { if (c) ncclCommDestroy(c); }
+};
+}  // namespace
+
+PYBIND11_MODULE(_vw, m) {
+  m.doc() = "Vowpal Wabbit-style hashed online learning (C++ core + HIP hogwild SGD)";
+  m.def("murmur3", [](py::bytes b, uint32_t seed) {
+    std::string s = b;
+    return Murmur3(s.data(), s.size(), seed);
+  });
+  m.def("hash_string", [](const std::string& s, uint32_t seed) { return HashString(s, seed); });
+  m.def("murmur_batch", [](const std::vector<std::string>& strs, uint32_t seed, const std::string& prefix) {
+    py::array_t<uint32_t> out(strs.size());
+    auto o = out.mutable_data();
+    for (size_t i = 0; i < strs.size(); ++i) {
+      std::string s = prefix + strs[i];
+      o[i] = Murmur3(s.data(), s.size(), seed);
+    }
+    return out;
+  }, py::arg("strings"), py::arg("seed"), py::arg("prefix") = "");
+  m.def("gpu_available", &VwGpuAvailable);
+
+  py::class_<VW, std::shared_ptr<VW>>(m, "VW")
+      .def(py::init([](const std::string& args, py::object model) {
+             if (model.is_none()) return std::make_shared<VW>(args);
+             std::string b = model.cast<py::bytes>();
+             return std::make_shared<VW>(args, &b);
+           }),
+           py::arg("args"), py::arg("model") = py::none())
+      .def("learn_batch",
+           [](VW& vw, py::list blocks, F32 labels, py::object weights, py::object multiclass, py::object costs,
+              bool learn) {
+             auto bl = ToBlocks(blocks);
+             const int64_t n = labels.size();
+             py::array_t<float> preds(n);
+             float* pr = preds.mutable_data();
+             const float* w = weights.is_none() ? nullptr : py::cast<F32>(weights).data();
+             I32 mc = multiclass.is_none() ? I32() : py::cast<I32>(multiclass);
+             std::vector<std::vector<std::pair<int, float>>> cs;
+             if (!costs.is_none()) cs = costs.cast<std::vector<std::vector<std::pair<int, float>>>>();
+             std::vector<std::vector<float>> scores;
+             Example ex;
+             {
+               for (int64_t i = 0; i < n; ++i) {
+                 FillExample(&ex, bl, i);
+                 ex.l = Label();
+                 ex.l.label = labels.data()[i];
+                 ex.l.has_label = true;
+                 ex.l.weight = w ? w[i] : 1.f;
+                 if (!multiclass.is_none()) ex.l.multiclass = mc.data()[i];
+                 if (!cs.empty()) ex.l.costs = cs[i];
+                 if (learn) vw.Learn(ex); else vw.Predict(ex);
+                 pr[i] = ex.pred;
+                 if (!ex.scores.empty()) scores.push_back(ex.scores);
+               }
+             }
+             return py::make_tuple(preds, scores);
+           },
+           py::arg("blocks"), py::arg("labels"), py::arg("weights") = py::none(), py::arg("multiclass") = py::none(),
+           py::arg("costs") = py::none(), py::arg("learn") = true)
+      .def("learn_cb",
+           [](VW& vw, py::list shared_blocks, py::list action_blocks, I64 action_indptr, I32 chosen, F32 cost, F32 prob,
+              bool learn) {
+             // shared_blocks: CSR over rows; action_blocks: CSR over all actions;
+             // action_indptr: row -> [first action, last action)
+             auto sb = ToBlocks(shared_blocks);
+             auto ab = ToBlocks(action_blocks);
+             const int64_t n = action_indptr.size() - 1;
+             py::list out;
+             for (int64_t i = 0; i < n; ++i) {
+               std::vector<Example> exs;
+               Example sh;
+               FillExample(&sh, sb, i);
+               sh.l.cb_shared = true;
+               exs.push_back(std::move(sh));
+               const int64_t a0 = action_indptr.data()[i], a1 = action_indptr.data()[i + 1];
+               for (int64_t a = a0; a < a1; ++a) {
+                 Example ax;
+                 FillExample(&ax, ab, a);
+                 if (chosen.data()[i] - 1 == a - a0) {
+                   ax.l.cb_has = true;
+                   ax.l.cb_action = chosen.data()[i];
+                   ax.l.cb_cost = cost.data()[i];
+                   ax.l.cb_prob = prob.data()[i];
+                 }
+                 exs.push_back(std::move(ax));
+               }
+               if (learn) vw.LearnMulti(exs); else vw.PredictMulti(exs);
+               py::list probs;
+               if (exs.size() > 1)
+                 for (auto& ap : exs[1].action_probs) probs.append(py::make_tuple(ap.first, ap.second));
+               out.append(probs);
+             }
+             return out;
+           },
+           py::arg("shared_blocks"), py::arg("action_blocks"), py::arg("action_indptr"), py::arg("chosen"),
+           py::arg("cost"), py::arg("prob"), py::arg("learn") = true)
+      .def("learn_text",
+           [](VW& vw, const std::vector<std::string>& lines, bool learn) {
+             py::array_t<float> preds(lines.size());
+             float* pr = preds.mutable_data();
+             for (size_t i = 0; i < lines.size(); ++i) {
+               Example ex = vw.ParseLine(lines[i]);
+               if (learn) vw.Learn(ex); else vw.Predict(ex);
+               pr[i] = ex.pred;
+             }
+             return preds;
+           },
+           py::arg("lines"), py::arg("learn") = true)
+      .def("learn_text_multi",
+           [](VW& vw, const std::vector<std::string>& lines, bool learn) {
+             std::vector<Example> exs;
+             for (auto& l : lines) exs.push_back(vw.ParseLine(l));
+             if (learn) vw.LearnMulti(exs); else vw.PredictMulti(exs);
+             py::list probs;
+             size_t head = (!exs.empty() && exs[0].l.cb_shared) ? 1 : 0;
+             if (exs.size() > head)
+               for (auto& ap : exs[head].action_probs) probs.append(py::make_tuple(ap.first, ap.second));
+             return probs;
+           },
+           py::arg("lines"), py::arg("learn") = true)
+      .def("end_pass", &VW::EndPass)
+      .def("perform_remaining_passes", &VW::PerformRemainingPasses)
+      .def("save_model", [](const VW& vw) { return py::bytes(vw.SaveModel()); })
+      .def("readable_model", &VW::ReadableModel)
+      .def("output_prediction_type", &VW::OutputPredictionType)
+      .def_property_readonly("args", &VW::args)
+      .def_property_readonly("num_bits", &VW::num_bits)
+      .def_property_readonly("hash_seed", &VW::HashSeed)
+      .def("set_allreduce",
+           [](VW& vw, int world, std::function<void(py::array_t<float>)> fn) {
+             vw.world_size = world;
+             vw.SetAllReduce([fn](float* buf, size_t n) {
+               py::gil_scoped_acquire acq;
+               py::array_t<float> a({static_cast<py::ssize_t>(n)}, {sizeof(float)}, buf, py::none());
+               fn(a);
+             });
+           })
+      .def("stats", [](const VW& vw) {
+        const Stats& s = vw.stats();
+        py::dict d;
+        d["numberOfExamplesPerPass"] = s.examples;
+        d["weightedExampleSum"] = s.weighted_examples;
+        d["weightedLabelSum"] = s.weighted_labels;
+        d["averageLoss"] = s.weighted_examples > 0 ? s.sum_loss / s.weighted_examples : 0.0;
+        d["bestConstant"] = s.weighted_examples > 0 ? s.weighted_labels / s.weighted_examples : 0.0;
+        d["totalNumberOfFeatures"] = s.total_features;
+        d["passes"] = s.passes;
+        d["ipsEstimate"] = s.examples > 0 ? s.cb_ips_num / s.examples : 0.0;
+        d["snipsEstimate"] = s.cb_snips_den > 0 ? s.cb_ips_num / s.cb_snips_den : 0.0;
+        return d;
+      })
+      .def("weights", [](VW& vw) {
+        const uint64_t n = vw.NumWeights() / vw.stride();
+        py::array_t<float> out(n);
+        float* o = out.mutable_data();
+        for (uint64_t i = 0; i < n; ++i) o[i] = vw.weights()[i * vw.stride()];
+        return out;
+      });
+  m.def("merge_models", [](std::vector<std::shared_ptr<VW>> ms) {
+    std::vector<const VW*> v;
+    for (auto& p : ms) v.push_back(p.get());
+    return std::shared_ptr<VW>(VW::Merge(v));
+  });
+
+  py::class_<NcclHandle, std::shared_ptr<NcclHandle>>(m, "NcclComm");
+  m.def("nccl_unique_id", []() {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+    return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+  });
+  m.def("nccl_comm", [](py::bytes uid, int rank, int world) {
+    std::string s = uid;
+    ncclUniqueId id;
+    std::memcpy(&id, s.data(), sizeof(id));
+    auto h = std::make_shared<NcclHandle>();
+    if (ncclCommInitRank(&h->c, world, id, rank) != ncclSuccess) throw std::runtime_error("ncclCommInitRank failed");
+    h->world = world;
+    return h;
+  });
+
+  py::class_<GpuSgdConfig>(m, "GpuSgdConfig")
+      .def(py::init<>())
+      .def_readwrite("bits", &GpuSgdConfig::bits)
+      .def_readwrite("lr", &GpuSgdConfig::lr)
+      .def_readwrite("power_t", &GpuSgdConfig::power_t)
+      .def_readwrite("l2", &GpuSgdConfig::l2)
+      .def_readwrite("loss", &GpuSgdConfig::loss)
+      .def_readwrite("adaptive", &GpuSgdConfig::adaptive);
+  py::class_<GpuSgd, std::shared_ptr<GpuSgd>>(m, "GpuSgd")
+      .def(py::init([](const GpuSgdConfig& c, int dev) { return std::make_shared<GpuSgd>(c, dev); }),
+           py::arg("config"), py::arg("device") = -1)
+      .def("learn",
+           [](GpuSgd& g, I64 indptr, U32 idx, F32 val, F32 labels, py::object weights, int batch) {
+             const int64_t n = indptr.size() - 1;
+             py::array_t<float> preds(n);
+             const float* w = weights.is_none() ? nullptr : py::cast<F32>(weights).data();
+             float* pr = preds.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               g.Learn(indptr.data(), idx.data(), val.data(), labels.data(), w, n, batch, pr);
+             }
+             return preds;
+           },
+           py::arg("indptr"), py::arg("indices"), py::arg("values"), py::arg("labels"), py::arg("weights") = py::none(),
+           py::arg("batch") = 1024)
+      .def("predict",
+           [](GpuSgd& g, I64 indptr, U32 idx, F32 val) {
+             const int64_t n = indptr.size() - 1;
+             py::array_t<float> out(n);
+             float* o = out.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               g.Predict(indptr.data(), idx.data(), val.data(), n, o);
+             }
+             return out;
+           })
+      .def("allreduce_average", [](GpuSgd& g, std::shared_ptr<NcclHandle> h) {
+        py::gil_scoped_release rel;
+        g.AllReduceAverage(h->c, h->world);
+      })
+      .def("weights", [](const GpuSgd& g) {
+        py::array_t<float> out(g.NumWeights());
+        g.CopyWeights(out.mutable_data());
+        return out;
+      })
+      .def("set_weights", [](GpuSgd& g, F32 w) {
+        if (static_cast<uint64_t>(w.size()) != g.NumWeights()) throw std::runtime_error("size mismatch");
+        g.SetWeights(w.data());
+      })
+      .def_property_readonly("examples", &GpuSgd::examples)
+      .def_property_readonly("sum_loss", &GpuSgd::sum_loss);
+}

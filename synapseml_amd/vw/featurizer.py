@@ -1,0 +1,186 @@
+"""Hashing featurizers (reference: vw/.../VowpalWabbitFeaturizer.scala,
+featurizer/*.scala, VowpalWabbitInteractions.scala,
+VowpalWabbitMurmurWithPrefix.scala). Feature index = mask & murmur3(colName +
+value, murmur3(outputCol, seed)); numeric columns hash the column name and keep
+the value; zero values are dropped; duplicates are summed (sumCollisions)."""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+
+from ..core.contracts import HasInputCols, HasOutputCol
+from ..core.dataframe import DataFrame
+from ..core.linalg import DenseVector, SparseVector
+from ..core.params import Param, TypeConverters as T
+from ..core.pipeline import Transformer
+from ..ops import native
+
+
+def _vw():
+    return native.load("_vw")
+
+
+def murmur_hash(s: str, seed: int) -> int:
+    """VW murmur3_32 of the UTF-8 bytes of ``s`` (signed like the JVM int)."""
+    h = int(_vw().murmur3(s.encode("utf-8"), seed & 0xFFFFFFFF))
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+class VowpalWabbitMurmurWithPrefix:
+    """Murmur hashing with a fixed string prefix (VowpalWabbitMurmurWithPrefix.scala:15-79)."""
+
+    def __init__(self, prefix: str):
+        self.prefix = prefix
+
+    def hash(self, value: str, seed: int) -> int:
+        return murmur_hash(self.prefix + value, seed)
+
+
+def sort_and_distinct(indices: np.ndarray, values: np.ndarray, sum_collisions: bool = True):
+    """VectorUtils.sortAndDistinct: sort by index, merge duplicates."""
+    if len(indices) == 0:
+        return indices.astype(np.int32), values.astype(np.float64)
+    order = np.argsort(indices, kind="stable")
+    idx = indices[order]
+    val = values[order]
+    uniq, first = np.unique(idx, return_index=True)
+    if sum_collisions:
+        sums = np.add.reduceat(val, first)
+    else:
+        sums = val[first]
+    return uniq.astype(np.int32), sums.astype(np.float64)
+
+
+class HasNumBits(Transformer):
+    numBits = Param("Number of bits used to mask", 30, T.toInt)
+
+
+class VowpalWabbitFeaturizer(HasNumBits, HasInputCols, HasOutputCol):
+    seed = Param("Hash seed", 0, T.toInt)
+    stringSplitInputCols = Param("Input cols that should be split at word boundaries", [], T.toListString)
+    sumCollisions = Param("Sums collisions if true, otherwise removes them", True, T.toBoolean)
+    prefixStringsWithColumnName = Param("Prefix string features with column name", True, T.toBoolean)
+    preserveOrderNumBits = Param("Number of bits used to preserve the feature order", 0, T.toInt)
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self._setDefault(outputCol="features", inputCols=[])
+
+    def _all_cols(self) -> List[str]:
+        return list(self.getInputCols() or []) + list(self.getStringSplitInputCols() or [])
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        nb, po = self.getNumBits(), self.getPreserveOrderNumBits()
+        if nb + po > 30:
+            raise ValueError(f"Number of bits used for hashing ({nb}) and for order preserving ({po}) must be <= 30")
+        for c in self._all_cols():
+            if c not in df:
+                raise ValueError(f"missing input column {c}")
+        mask = (1 << nb) - 1
+        ns_hash = murmur_hash(self.getOutputCol(), self.getSeed()) & 0xFFFFFFFF
+        vw = _vw()
+        prefix_on = self.getPrefixStringsWithColumnName()
+        split_cols = set(self.getStringSplitInputCols() or [])
+        n = df.count()
+        per_row_idx: List[List[np.ndarray]] = [[] for _ in range(n)]
+        per_row_val: List[List[np.ndarray]] = [[] for _ in range(n)]
+
+        def add(i, idx, val):
+            per_row_idx[i].append(np.asarray(idx, dtype=np.int64))
+            per_row_val[i].append(np.asarray(val, dtype=np.float64))
+
+        for c in self._all_cols():
+            col = df[c]
+            pre = c if prefix_on else ""
+            if isinstance(col, np.ndarray) and col.ndim == 2:  # dense vector column
+                width = col.shape[1]
+                idx = np.arange(width, dtype=np.int64) & mask if width >= mask + 1 else np.arange(width)
+                for i in range(n):
+                    add(i, idx, col[i])
+                continue
+            if col.dtype.kind in "biuf":
+                if col.dtype.kind == "b":
+                    h = int(vw.murmur3(c.encode(), ns_hash)) & mask
+                    for i in np.nonzero(col)[0]:
+                        add(int(i), [h], [1.0])
+                else:
+                    h = int(vw.murmur3(c.encode(), ns_hash)) & mask
+                    vals = col.astype(np.float64)
+                    for i in np.nonzero(vals)[0]:
+                        add(int(i), [h], [vals[i]])
+                continue
+            # object columns: strings, string lists, maps, vectors
+            for i, v in enumerate(col.tolist()):
+                if v is None:
+                    continue
+                if isinstance(v, str):
+                    toks = v.split() if c in split_cols else [v]
+                    hs = vw.murmur_batch(toks, ns_hash, pre) & mask
+                    add(i, hs, np.ones(len(toks)))
+                elif isinstance(v, (list, tuple)) and (not v or isinstance(v[0], str)):
+                    hs = vw.murmur_batch([str(t) for t in v], ns_hash, pre) & mask
+                    add(i, hs, np.ones(len(v)))
+                elif isinstance(v, dict):
+                    keys = [str(k) for k in v.keys()]
+                    vals = np.asarray([float(x) if not isinstance(x, str) else 1.0 for x in v.values()])
+                    if any(isinstance(x, str) for x in v.values()):
+                        keys = [f"{k}{x}" if isinstance(x, str) else k for k, x in v.items()]
+                    hs = vw.murmur_batch(keys, ns_hash, c) & mask
+                    nz = vals != 0
+                    add(i, hs[nz], vals[nz])
+                elif isinstance(v, SparseVector):
+                    add(i, v.indices.astype(np.int64) & mask if v.size >= mask + 1 else v.indices, v.values)
+                elif isinstance(v, (DenseVector, np.ndarray, list, tuple)):
+                    a = np.asarray(v, dtype=np.float64)
+                    add(i, np.arange(len(a)), a)
+                elif isinstance(v, (bool, np.bool_)):
+                    if v:
+                        add(i, [int(vw.murmur3(c.encode(), ns_hash)) & mask], [1.0])
+                else:
+                    fv = float(v)
+                    if fv != 0:
+                        add(i, [int(vw.murmur3(c.encode(), ns_hash)) & mask], [fv])
+        size = (1 << 30) if po > 0 else (1 << nb)
+        out = np.empty(n, dtype=object)
+        for i in range(n):
+            idx = np.concatenate(per_row_idx[i]) if per_row_idx[i] else np.zeros(0, np.int64)
+            val = np.concatenate(per_row_val[i]) if per_row_val[i] else np.zeros(0)
+            if po > 0:
+                if len(idx) > (1 << po):
+                    raise ValueError(f"Too many features {len(idx)} for preserveOrderNumBits={po}")
+                idx = idx | (np.arange(len(idx), dtype=np.int64) << (30 - po))
+            si, sv = sort_and_distinct(idx, val, self.getSumCollisions())
+            out[i] = SparseVector(size, si, sv)
+        return df.withColumn(self.getOutputCol(), out)
+
+
+class VowpalWabbitInteractions(HasNumBits, HasInputCols, HasOutputCol):
+    """Quadratic (and higher) feature crosses of sparse vectors for non-VW
+    learners (VowpalWabbitInteractions.scala): index = mask & (h1 * FNV ^ h2)."""
+
+    sumCollisions = Param("Sums collisions if true, otherwise removes them", True, T.toBoolean)
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        mask = (1 << self.getNumBits()) - 1
+        fnv = 16777619
+        cols = [df[c] for c in self.getInputCols()]
+        n = df.count()
+        out = np.empty(n, dtype=object)
+
+        def as_sparse(v):
+            if isinstance(v, SparseVector):
+                return v.indices.astype(np.int64), v.values
+            a = np.asarray(v, dtype=np.float64)
+            nz = np.nonzero(a)[0]
+            return nz.astype(np.int64), a[nz]
+
+        for i in range(n):
+            idx, val = as_sparse(cols[0][i])
+            for c in cols[1:]:
+                i2, v2 = as_sparse(c[i])
+                idx = ((idx[:, None] * fnv) ^ i2[None, :]).ravel() & mask
+                val = (val[:, None] * v2[None, :]).ravel()
+            si, sv = sort_and_distinct(idx, val, self.getSumCollisions())
+            out[i] = SparseVector(1 << self.getNumBits(), si, sv)
+        return df.withColumn(self.getOutputCol(), out)

@@ -1,0 +1,419 @@
+"""Vowpal Wabbit-style estimators and models (reference: vw/.../
+VowpalWabbitBase.scala, VowpalWabbitBaseLearner.scala, VowpalWabbitBaseSpark
+.scala, VowpalWabbitClassifier.scala, VowpalWabbitRegressor.scala,
+VowpalWabbitGeneric.scala, VowpalWabbitContextualBandit.scala,
+VowpalWabbitBaseProgressive.scala).
+
+Training: every partition/rank owns a native learner built from the VW
+command line (passThroughArgs first, then the typed params); rows are
+marshalled in columnar batches (no per-row JNI calls); at pass boundaries (and
+``numSyncsPerPass`` times within a pass) the weight tables are averaged across
+ranks with an allreduce (RCCL/gloo replaces VW's spanning tree,
+VowpalWabbitClusterUtil.scala); rank 0's model is returned. ``splitCol``
+training broadcasts the model per split and averages (mergeModels).
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional
+
+import numpy as np
+
+from ..core.contracts import (HasFeaturesCol, HasLabelCol, HasPredictionCol, HasProbabilityCol,
+                              HasRawPredictionCol, HasWeightCol)
+from ..core.dataframe import DataFrame
+from ..core.linalg import DenseVector, SparseVector
+from ..core.params import Param, TypeConverters as T
+from ..core.pipeline import Estimator, Model, Transformer
+from ..core.utils import ParamsStringBuilder, StopWatch
+from ..ops import native
+from ..parallel import distributed as D
+from .featurizer import murmur_hash
+
+
+def _vw():
+    return native.load("_vw")
+
+
+class VowpalWabbitBaseParams(HasFeaturesCol):
+    passThroughArgs = Param("VW command line arguments passed", "", T.toString)
+    additionalFeatures = Param("Additional feature columns", [], T.toListString)
+    hashSeed = Param("Seed used for hashing", 0, T.toInt)
+    numBits = Param("Number of bits used", 18, T.toInt)
+    learningRate = Param("Learning rate", None, T.toFloat)
+    powerT = Param("t power value", None, T.toFloat)
+    l1 = Param("l_1 lambda", None, T.toFloat)
+    l2 = Param("l_2 lambda", None, T.toFloat)
+    interactions = Param("Interaction terms as specified by -q", [], T.toListString)
+    ignoreNamespaces = Param("Namespaces to be ignored (first letter only)", None, T.toString)
+    initialModel = Param("Initial model to start from", None, complex=True)
+    numPasses = Param("Number of passes over the data", 1, T.toInt)
+    numSyncsPerPass = Param("Number of times weights should be synchronized within each pass", 0, T.toInt)
+    useBarrierExecutionMode = Param("Use barrier execution mode, on by default.", True, T.toBoolean)
+    splitCol = Param("The column to split on for inter-pass sync", None, T.toString)
+    splitColValues = Param("Sorted values to use to select each split to train on", None)
+    predictionIdCol = Param("The ID column returned for predictions", None, T.toString)
+    deviceType = Param("cpu (exact sequential VW semantics) or gpu (hogwild mini-batch SGD on the MI355X)", "cpu",
+                       T.toString)
+    gpuBatchSize = Param("Mini-batch size of the GPU learner", 1024, T.toInt)
+
+
+def build_args(est, extra: Optional[ParamsStringBuilder] = None) -> str:
+    sb = ParamsStringBuilder(prefix="--", delimiter=" ")
+    sb.append(est.getPassThroughArgs())
+    sb.appendParamValueIfNotThere("hash_seed", est.getHashSeed())
+    if "-b " not in (" " + sb.result + " "):
+        sb.appendParamValueIfNotThere("bit_precision", est.getNumBits())
+    if " -l " not in (" " + sb.result + " "):
+        sb.appendParamValueIfNotThere("learning_rate", est.getLearningRate())
+    sb.appendParamValueIfNotThere("power_t", est.getPowerT())
+    sb.appendParamValueIfNotThere("l1", est.getL1())
+    sb.appendParamValueIfNotThere("l2", est.getL2())
+    sb.appendParamValueIfNotThere("ignore", est.getIgnoreNamespaces())
+    for q in est.getInteractions() or []:
+        if f"-q {q}" not in sb.result and f"--quadratic {q}" not in sb.result:
+            sb.append(f"-q {q}")
+    if extra is not None:
+        sb.append(extra.result)
+    sb.appendParamFlagIfNotThere("no_stdin")
+    if est.getNumPasses() > 1:
+        sb.appendParamValueIfNotThere("passes", est.getNumPasses())
+        sb.appendParamFlagIfNotThere("holdout_off")
+    return sb.result
+
+
+def namespace_blocks(df: DataFrame, cols: List[str], hash_seed: int):
+    """Columns -> [(featureGroup, indptr, indices, values)] for the native
+    batch API. Dense vector columns get index = murmur(col, seed) + i, sparse
+    vectors keep their (already hashed) indices (VowpalWabbitUtil.scala:11-40)."""
+    blocks = []
+    n = df.count()
+    for c in cols:
+        col = df[c]
+        ns_hash = murmur_hash(c, hash_seed) & 0xFFFFFFFF
+        group = c[0]
+        if isinstance(col, np.ndarray) and col.ndim == 2:
+            width = col.shape[1]
+            nz = col != 0
+            indptr = np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64)
+            rr, cc = np.nonzero(nz)
+            idx = ((cc.astype(np.uint64) + ns_hash) & 0xFFFFFFFF).astype(np.uint32)
+            blocks.append((group, indptr, idx, col[rr, cc].astype(np.float32)))
+            continue
+        indptr = [0]
+        ii, vv = [], []
+        for v in col.tolist():
+            if isinstance(v, SparseVector):
+                ii.append(v.indices.astype(np.uint32))
+                vv.append(v.values.astype(np.float32))
+                indptr.append(indptr[-1] + len(v.indices))
+            else:
+                a = np.asarray(v.toArray() if isinstance(v, DenseVector) else v, dtype=np.float64)
+                nzi = np.nonzero(a)[0]
+                ii.append(((nzi.astype(np.uint64) + ns_hash) & 0xFFFFFFFF).astype(np.uint32))
+                vv.append(a[nzi].astype(np.float32))
+                indptr.append(indptr[-1] + len(nzi))
+        blocks.append((group, np.asarray(indptr, np.int64),
+                       np.concatenate(ii).astype(np.uint32) if ii else np.zeros(0, np.uint32),
+                       np.concatenate(vv).astype(np.float32) if vv else np.zeros(0, np.float32)))
+    assert all(len(b[1]) == n + 1 for b in blocks)
+    return blocks
+
+
+def _block_slice(blocks, a: int, b: int):
+    out = []
+    for g, ip, ii, vv in blocks:
+        s, e = ip[a], ip[b]
+        out.append((g, (ip[a:b + 1] - s).astype(np.int64), ii[s:e], vv[s:e]))
+    return out
+
+
+def _host_allreduce_f32(arr: np.ndarray) -> None:
+    if D.world_size() <= 1:
+        return
+    import torch
+
+    t = torch.from_numpy(arr)
+    if D.backend() == "nccl":
+        tt = t.cuda()
+        D._dist().all_reduce(tt)
+        arr[...] = tt.cpu().numpy()
+    else:
+        D._dist().all_reduce(t)
+
+
+class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
+    model = Param("The VW model bytes", None, complex=True)
+    performanceStatistics = Param("Training statistics", None, complex=True)
+    testArgs = Param("Additional arguments passed to VW at test time", "", T.toString)
+    vwArgs = Param("Arguments the model was trained with", "", T.toString)
+
+    def _native_model(self):
+        cache = getattr(self, "_vw_cache", None)
+        key = (id(self.getModel()), self.getTestArgs())
+        if cache is None or cache[0] != key:
+            m = _vw().VW(self.getVwArgs() + " --testonly " + (self.getTestArgs() or ""), self.getModel())
+            self._vw_cache = (key, m)
+        return self._vw_cache[1]
+
+    def getPerformanceStatistics(self) -> DataFrame:  # noqa: N802
+        return self.getOrDefault("performanceStatistics")
+
+    def getReadableModel(self) -> str:  # noqa: N802
+        return self._native_model().readable_model()
+
+    def saveNativeModel(self, path: str) -> None:  # noqa: N802
+        with open(path, "wb") as f:
+            f.write(self.getModel())
+
+    def _predict_raw(self, df: DataFrame, multiclass: bool = False):
+        vw = self._native_model()
+        cols = [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or [])
+        blocks = namespace_blocks(df, cols, self.getHashSeed())
+        n = df.count()
+        preds, scores = vw.learn_batch(blocks, np.zeros(n, np.float32), None, None, None, False)
+        return np.asarray(preds, dtype=np.float64), scores
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        raw, _ = self._predict_raw(df)
+        return df.withColumn(self.getPredictionCol(), raw)
+
+
+class VowpalWabbitBase(Estimator, VowpalWabbitBaseParams, HasLabelCol, HasWeightCol, HasPredictionCol):
+    _model_cls = VowpalWabbitModelBase
+
+    def _extra_args(self) -> Optional[ParamsStringBuilder]:
+        return None
+
+    def _labels(self, df: DataFrame):
+        return np.asarray(df[self.getLabelCol()], dtype=np.float32), None, None
+
+    def _train_partition(self, df: DataFrame, args: str, model_bytes=None):
+        vw = _vw().VW(args, model_bytes)
+        world = D.world_size()
+        if world > 1:
+            vw.set_allreduce(world, _host_allreduce_f32)
+        total = StopWatch()
+        ingest = StopWatch()
+        learn = StopWatch()
+        multipass = StopWatch()
+        total.start()
+        cols = [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or [])
+        blocks = ingest.measure(lambda: namespace_blocks(df, cols, self.getHashSeed()))
+        labels, multiclass, costs = self._labels(df)
+        wcol = self.getWeightCol()
+        weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
+        n = df.count()
+        syncs = self.getNumSyncsPerPass()
+        # every rank must fire the same number of syncs (VowpalWabbitSyncSchedule.scala:36-72)
+        if syncs > 0 and world > 1:
+            max_n = max(D.all_gather_object(n))
+        else:
+            max_n = n
+        splits = [int(max_n * (k + 1) / (syncs + 1)) for k in range(syncs)] if syncs > 0 else []
+        start = 0
+        for s in splits + [None]:
+            end = n if s is None else min(n, s)
+            if end > start:
+                learn.measure(lambda: vw.learn_batch(
+                    _block_slice(blocks, start, end), labels[start:end],
+                    None if weights is None else weights[start:end],
+                    None if multiclass is None else multiclass[start:end],
+                    None if costs is None else costs[start:end], True))
+            start = max(start, end)
+            if s is not None and world > 1:
+                vw.end_pass()
+        if self.getNumPasses() > 1:
+            multipass.measure(vw.perform_remaining_passes)
+        elif world > 1:
+            vw.end_pass()
+        total.pause()
+        stats = vw.stats()
+        stats.update(timeTotalNs=total.elapsed_ns, timeNativeIngestNs=ingest.elapsed_ns, timeLearnNs=learn.elapsed_ns,
+                     timeMultipassNs=multipass.elapsed_ns)
+        return vw, stats
+
+    def _stats_df(self, vw, stats: dict) -> DataFrame:
+        tot = max(1, stats["timeTotalNs"])
+        row = {"partitionId": D.rank(), "arguments": vw.args, "learningRate": float(self.getLearningRate() or 0.5),
+               "powerT": float(self.getPowerT() or 0.5), "hashSeed": vw.hash_seed, "numBits": vw.num_bits}
+        row.update({k: v for k, v in stats.items()})
+        for k in ["timeNativeIngestNs", "timeLearnNs", "timeMultipassNs"]:
+            row[k.replace("Ns", "Percentage")] = stats[k] / tot
+        return DataFrame({k: [v] for k, v in row.items()})
+
+    def _fit(self, df: DataFrame):
+        args = build_args(self, self._extra_args())
+        init = self.getInitialModel()
+        if self.getSplitCol():
+            vw, stats = self._train_splits(df, args, init)
+        else:
+            vw, stats = self._train_partition(df, args, init)
+        m = self._model_cls()
+        self._copyValues(m)
+        m.set("model", bytes(vw.save_model()))
+        m.set("vwArgs", args)
+        m.set("performanceStatistics", self._stats_df(vw, stats))
+        self._post_fit(m)
+        return m
+
+    def _post_fit(self, model) -> None:
+        pass
+
+    def _train_splits(self, df: DataFrame, args: str, init):
+        """Spark-coordinated path (VowpalWabbitBaseLearner.scala:307-354): per
+        split value train every partition from the current model, then average."""
+        col = df[self.getSplitCol()]
+        values = self.getSplitColValues() or sorted(set(col.tolist()))
+        model = init
+        vw = stats = None
+        for v in values:
+            part = df.filter(col == v)
+            models = []
+            for p in part.partitions():
+                if p.count() == 0:
+                    continue
+                vw, stats = self._train_partition(p, args, model)
+                models.append(vw)
+            if models:
+                vw = _vw().merge_models(models) if len(models) > 1 else models[0]
+                model = bytes(vw.save_model())
+        return vw, stats
+
+    def parallelFit(self, df: DataFrame, paramMaps: list):  # noqa: N802
+        """Fit one model per param map (VowpalWabbitPythonBase.parallelFit)."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(max_workers=min(8, len(paramMaps) or 1)) as ex:
+            return list(ex.map(lambda pm: self.copy(pm).fit(df), paramMaps))
+
+
+# ============================================================ regressor
+class VowpalWabbitRegressionModel(VowpalWabbitModelBase, HasRawPredictionCol):
+    def _transform(self, df: DataFrame) -> DataFrame:
+        raw, _ = self._predict_raw(df)
+        return df.withColumn(self.getRawPredictionCol(), raw).withColumn(self.getPredictionCol(), raw)
+
+
+class VowpalWabbitRegressor(VowpalWabbitBase):
+    _model_cls = VowpalWabbitRegressionModel
+
+
+# ============================================================ classifier
+class VowpalWabbitClassificationModel(VowpalWabbitModelBase, HasRawPredictionCol, HasProbabilityCol):
+    numClassesModel = Param("Number of classes.", 2, T.toInt)
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        raw, scores = self._predict_raw(df)
+        if self.getNumClassesModel() == 2:
+            if "--link logistic" in self.getVwArgs():
+                p = raw
+            else:
+                p = 1.0 / (1.0 + np.exp(-raw))
+            prob = np.stack([1 - p, p], 1)
+            return (df.withColumn(self.getRawPredictionCol(), raw).withColumn(self.getProbabilityCol(), prob)
+                    .withColumn(self.getPredictionCol(), (p > 0.5).astype(np.float64)))
+        if scores and "--probabilities" in self.getVwArgs():
+            probs = np.asarray(scores, dtype=np.float64)
+            return (df.withColumn(self.getRawPredictionCol(), probs).withColumn(self.getProbabilityCol(), probs)
+                    .withColumn(self.getPredictionCol(), np.argmax(probs, 1).astype(np.float64)))
+        return df.withColumn(self.getRawPredictionCol(), raw).withColumn(self.getPredictionCol(), raw)
+
+
+class VowpalWabbitClassifier(VowpalWabbitBase, HasRawPredictionCol, HasProbabilityCol):
+    _model_cls = VowpalWabbitClassificationModel
+    labelConversion = Param("Convert 0/1 Spark ML style labels to -1/1 VW style labels.", False, T.toBoolean)
+    numClasses = Param("Number of classes. Defaults to binary. Needs to match oaa/csoaa.", 2, T.toInt)
+
+    def _labels(self, df: DataFrame):
+        y = np.asarray(df[self.getLabelCol()], dtype=np.float64)
+        if self.getNumClasses() != 2:
+            return y.astype(np.float32), y.astype(np.int32), None
+        if self.getLabelConversion():
+            y = y * 2 - 1
+        return y.astype(np.float32), None, None
+
+    def _post_fit(self, model) -> None:
+        model.set("numClassesModel", self.getNumClasses())
+
+
+# ============================================================ generic (VW text format)
+class VowpalWabbitGenericModel(Model, HasPredictionCol):
+    model = Param("The VW model bytes", None, complex=True)
+    vwArgs = Param("Arguments the model was trained with", "", T.toString)
+    inputCol = Param("Column with examples in VW text format", "value", T.toString)
+    testArgs = Param("Additional test-time arguments", "", T.toString)
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        vw = _vw().VW(self.getVwArgs() + " --testonly " + self.getTestArgs(), self.getModel())
+        preds = vw.learn_text([str(s) for s in df[self.getInputCol()].tolist()], False)
+        return df.withColumn(self.getPredictionCol(), np.asarray(preds, np.float64))
+
+    def getReadableModel(self) -> str:  # noqa: N802
+        return _vw().VW(self.getVwArgs(), self.getModel()).readable_model()
+
+
+class VowpalWabbitGeneric(Estimator, HasPredictionCol):
+    """Learn from VW-format strings (VowpalWabbitGeneric.scala:19-131)."""
+
+    passThroughArgs = Param("VW command line arguments passed", "", T.toString)
+    inputCol = Param("Column with examples in VW text format", "value", T.toString)
+    numPasses = Param("Number of passes over the data", 1, T.toInt)
+    initialModel = Param("Initial model to start from", None, complex=True)
+
+    def _fit(self, df: DataFrame):
+        args = self.getPassThroughArgs() + (f" --passes {self.getNumPasses()}" if self.getNumPasses() > 1 else "")
+        vw = _vw().VW(args, self.getInitialModel())
+        if D.world_size() > 1:
+            vw.set_allreduce(D.world_size(), _host_allreduce_f32)
+        lines = [str(s) for s in df[self.getInputCol()].tolist()]
+        if "--cb" in args:
+            # multi-line examples separated by empty lines
+            group: List[str] = []
+            for l in lines + [""]:
+                if l.strip():
+                    group.append(l)
+                elif group:
+                    vw.learn_text_multi(group, True)
+                    group = []
+        else:
+            vw.learn_text(lines, True)
+        if self.getNumPasses() > 1:
+            vw.perform_remaining_passes()
+        elif D.world_size() > 1:
+            vw.end_pass()
+        m = VowpalWabbitGenericModel()
+        m.set("model", bytes(vw.save_model()))
+        m.set("vwArgs", args)
+        m.set("inputCol", self.getInputCol())
+        m.set("predictionCol", self.getPredictionCol())
+        return m
+
+
+class VowpalWabbitGenericProgressive(Transformer, HasPredictionCol):
+    """Online 1-step-ahead predictions while learning (VowpalWabbitGenericProgressive.scala)."""
+
+    passThroughArgs = Param("VW command line arguments passed", "", T.toString)
+    inputCol = Param("Column with examples in VW text format", "value", T.toString)
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        out = []
+        for part in df.partitions():
+            vw = _vw().VW(self.getPassThroughArgs())
+            out.append(np.asarray(vw.learn_text([str(s) for s in part[self.getInputCol()].tolist()], True), np.float64))
+        return df.withColumn(self.getPredictionCol(), np.concatenate(out) if out else np.zeros(0))
+
+
+class VowpalWabbitProgressive(Transformer, VowpalWabbitBaseParams, HasLabelCol, HasPredictionCol):
+    """Progressive validation over Spark-vector features (VowpalWabbitBaseProgressive.scala)."""
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        args = build_args(self)
+        out = []
+        for part in df.partitions():
+            vw = _vw().VW(args)
+            cols = [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or [])
+            blocks = namespace_blocks(part, cols, self.getHashSeed())
+            preds, _ = vw.learn_batch(blocks, np.asarray(part[self.getLabelCol()], np.float32), None, None, None, True)
+            out.append(np.asarray(preds, np.float64))
+        return df.withColumn(self.getPredictionCol(), np.concatenate(out) if out else np.zeros(0))

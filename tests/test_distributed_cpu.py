@@ -1,0 +1,48 @@
+"""Data-parallel training across 2 processes (gloo) must match one process on
+the union of the shards when both use the same bin boundaries."""
+import numpy as np
+import pytest
+
+from synapseml_amd.core import DataFrame
+from synapseml_amd.lightgbm import LightGBMClassifier, LightGBMRegressor
+from synapseml_amd.parallel.runtime import distributed_fit, run_partitions
+
+
+def _allreduce_task(part, rank, world):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(part.count())])
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def test_run_partitions_rendezvous():
+    df = DataFrame({"x": np.arange(10.0)}, num_partitions=4)
+    res = run_partitions(_allreduce_task, df, num_workers=2)
+    assert res == [10.0, 10.0]
+
+
+@pytest.mark.parametrize("est_cls", [LightGBMClassifier, LightGBMRegressor])
+def test_data_parallel_matches_single_process(est_cls):
+    rng = np.random.default_rng(0)
+    n = 6000
+    X = rng.standard_normal((n, 8))
+    y = (X[:, 0] + X[:, 1] * X[:, 2] > 0).astype(float)
+    if est_cls is LightGBMRegressor:
+        y = X[:, 0] * 2 + X[:, 1] ** 2
+    df = DataFrame({"features": X, "label": y}, num_partitions=2)
+    base = est_cls(deviceType="cpu", numIterations=8, numThreads=1)
+    base.fit(df)
+    ref = base._last_reference
+    single = est_cls(deviceType="cpu", numIterations=8, numThreads=1, referenceDataset=ref).fit(df)
+    dist_model = distributed_fit(est_cls(deviceType="cpu", numIterations=8, numThreads=1, referenceDataset=ref), df,
+                                 num_workers=2)
+    col = "probability" if est_cls is LightGBMClassifier else "prediction"
+    a = single.transform(df)[col]
+    b = dist_model.transform(df)[col]
+    np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
+    def splits(m):
+        return [l for l in m.getNativeModel().splitlines() if l.startswith(("split_feature=", "threshold="))]
+
+    assert splits(single) == splits(dist_model)
