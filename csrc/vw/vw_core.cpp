@@ -232,7 +232,7 @@ void VW::Update(const Example& ex, uint64_t offset, float pred, float label, flo
     }
     float rate = 1.f;
     if (adaptive_) rate = w[1] > 0.f ? 1.f / std::sqrt(w[1]) : 0.f;
-    if (normalized_) { const float inv = 1.f / w[2]; rate *= adaptive_ ? inv * inv : inv * inv; }
+    if (normalized_) { const float inv = 1.f / w[2]; rate *= adaptive_ ? inv : inv * inv; }
     spare_.push_back(rate);
     pred_per_update += x2 * rate;
   });
@@ -241,7 +241,11 @@ void VW::Update(const Example& ex, uint64_t offset, float pred, float label, flo
   total_weight_ += importance;
   sum_norm_x_ += importance * norm_x;
   double eta = lr_;
-  if (normalized_) eta *= sum_norm_x_ > 0 ? total_weight_ / sum_norm_x_ : 1.0;
+  if (normalized_ && sum_norm_x_ > 0) {
+    // average feature-norm multiplier (sqrt under adaptive, as for the per-feature decay)
+    const double avg_norm = total_weight_ / sum_norm_x_;
+    eta *= adaptive_ ? std::sqrt(avg_norm) : avg_norm;
+  }
   if (!adaptive_) eta *= std::pow(initial_t_ + t_, -static_cast<double>(power_t_));
   const float update_scale = static_cast<float>(eta) * importance;
   float update;

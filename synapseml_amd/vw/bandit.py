@@ -12,7 +12,7 @@ import numpy as np
 
 from ..core.dataframe import DataFrame
 from ..core.linalg import DenseVector, SparseVector
-from ..core.params import Param, TypeConverters as T
+from ..core.params import Param, Params, TypeConverters as T
 from ..core.utils import ParamsStringBuilder
 from .featurizer import murmur_hash
 from .learners import (VowpalWabbitBase, VowpalWabbitModelBase, _host_allreduce_f32, _vw, build_args)
@@ -64,7 +64,7 @@ def _blocks_actions(df: DataFrame, cols: List[str], seed: int):
     return blocks, action_indptr
 
 
-class _CBParams:
+class _CBParams(Params):
     sharedCol = Param("Column name of shared features", "shared", T.toString)
     additionalSharedFeatures = Param("Additional namespaces for the shared example", [], T.toListString)
 

@@ -1,0 +1,368 @@
+"""Vowpal Wabbit-compatible learner tests (model: reference
+vw/src/test/scala/.../VerifyVowpalWabbit*.scala and SURVEY §8.2)."""
+import json
+
+import numpy as np
+import pytest
+
+from synapseml_amd.core.dataframe import DataFrame
+from synapseml_amd.core.linalg import SparseVector
+from synapseml_amd.vw import (ContextualBanditMetrics, CressieRead, CressieReadInterval, Ips, KahanSum, Snips,
+                              VectorZipper, VowpalWabbitClassifier, VowpalWabbitContextualBandit,
+                              VowpalWabbitCSETransformer, VowpalWabbitDSJsonTransformer, VowpalWabbitFeaturizer,
+                              VowpalWabbitGeneric, VowpalWabbitGenericProgressive, VowpalWabbitInteractions,
+                              VowpalWabbitMurmurWithPrefix, VowpalWabbitRegressor, murmur_hash)
+from synapseml_amd.ops import native
+
+
+def _u(x):
+    return x & 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------ hashing
+def test_murmur_golden_values():
+    ns = _u(murmur_hash("features", 0))
+    assert ns == 2493003127
+    assert _u(murmur_hash("marie", ns)) == 0xECACEC8A
+    assert _u(murmur_hash("markus", ns)) == 0x07388F83
+    assert _u(murmur_hash("fun", ns)) == 0xA23CC374
+    assert _u(murmur_hash("in", ns)) == 0x30AC2EF4
+    assert _u(murmur_hash("inmarkus", ns)) == 0x02233B72
+    # standard MurmurHash3_x86_32 vectors
+    assert _u(murmur_hash("", 0)) == 0
+    assert _u(murmur_hash("", 1)) == 0x514E28B7
+    assert _u(murmur_hash("test", 0)) == 0xBA6BD213
+    assert _u(murmur_hash("Hello, world!", 0)) == 0xC0363E43
+    assert _u(murmur_hash("The quick brown fox jumps over the lazy dog", 0)) == 0x2E4FF723
+
+
+def test_murmur_with_prefix_matches_concat():
+    m = VowpalWabbitMurmurWithPrefix("prefix")
+    for s in ["", "a", "héllo", "x" * 100]:
+        assert m.hash(s, 17) == murmur_hash("prefix" + s, 17)
+    vw = native.load("_vw")
+    batch = vw.murmur_batch(["a", "bb", "ccc"], 5, "pre")
+    assert [int(b) for b in batch] == [_u(murmur_hash("pre" + s, 5)) for s in ["a", "bb", "ccc"]]
+
+
+# ------------------------------------------------------------------ featurizer
+def test_featurizer_strings_numeric_and_collisions():
+    df = DataFrame({"in": ["markus", "marie"], "num": [2.0, 0.0], "flag": [True, False]})
+    out = VowpalWabbitFeaturizer(inputCols=["in", "num", "flag"], numBits=18).transform(df)
+    ns = _u(murmur_hash("features", 0))
+    mask = (1 << 18) - 1
+    v0 = out["features"][0]
+    assert isinstance(v0, SparseVector) and v0.size == 1 << 18
+    exp = {(_u(murmur_hash("inmarkus", ns)) & mask): 1.0, (_u(murmur_hash("num", ns)) & mask): 2.0,
+           (_u(murmur_hash("flag", ns)) & mask): 1.0}
+    assert dict(zip(v0.indices.tolist(), v0.values.tolist())) == exp
+    v1 = out["features"][1]  # zero numeric + false bool dropped
+    assert len(v1.indices) == 1 and v1.indices[0] == (_u(murmur_hash("inmarie", ns)) & mask)
+    assert 211826 in v0.indices.tolist()
+
+
+def test_featurizer_string_split_and_no_prefix():
+    df = DataFrame({"text": ["marie markus marie"]})
+    out = VowpalWabbitFeaturizer(stringSplitInputCols=["text"], prefixStringsWithColumnName=False,
+                                 numBits=18).transform(df)
+    v = out["features"][0]
+    m = dict(zip(v.indices.tolist(), v.values.tolist()))
+    assert m[60554] == 2.0 and m[36739] == 1.0
+    # collisions removed instead of summed
+    out2 = VowpalWabbitFeaturizer(stringSplitInputCols=["text"], prefixStringsWithColumnName=False, numBits=18,
+                                  sumCollisions=False).transform(df)
+    m2 = dict(zip(out2["features"][0].indices.tolist(), out2["features"][0].values.tolist()))
+    assert m2[60554] == 1.0
+
+
+def test_featurizer_preserve_order_bits():
+    df = DataFrame({"a": ["x"], "b": ["y"]})
+    out = VowpalWabbitFeaturizer(inputCols=["a", "b"], numBits=10, preserveOrderNumBits=2).transform(df)
+    v = out["features"][0]
+    assert v.size == 1 << 30
+    assert sorted((v.indices >> 28).tolist()) == [0, 1]
+    with pytest.raises(ValueError):
+        VowpalWabbitFeaturizer(inputCols=["a"], numBits=29, preserveOrderNumBits=2).transform(df)
+
+
+def test_interactions():
+    df = DataFrame({"a": np.empty(1, object), "b": np.empty(1, object)})
+    df = df.withColumn("a", np.array([SparseVector(8, [1, 2], [1.0, 2.0])], dtype=object))
+    df = df.withColumn("b", np.array([SparseVector(8, [3], [5.0])], dtype=object))
+    out = VowpalWabbitInteractions(inputCols=["a", "b"], outputCol="ab", numBits=10).transform(df)
+    v = out["ab"][0]
+    fnv = 16777619
+    exp = {((1 * fnv) ^ 3) & 1023: 5.0, ((2 * fnv) ^ 3) & 1023: 10.0}
+    assert dict(zip(v.indices.tolist(), v.values.tolist())) == exp
+
+
+# ------------------------------------------------------------------ learners
+def _binary_df(n=4000, d=10, seed=0, parts=1):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, d))
+    w = rng.normal(size=d)
+    y = (X @ w + 0.3 * rng.normal(size=n) > 0).astype(np.float64)
+    return DataFrame({"features": X, "label": y}, num_partitions=parts), X, y
+
+
+def _auc(y, s):
+    from sklearn.metrics import roc_auc_score
+
+    return roc_auc_score(y, s)
+
+
+def test_classifier_binary_learns():
+    df, X, y = _binary_df()
+    m = VowpalWabbitClassifier(labelConversion=True, passThroughArgs="--loss_function logistic").fit(df)
+    out = m.transform(df)
+    assert _auc(y, out["probability"][:, 1]) > 0.95
+    acc = (out["prediction"] == y).mean()
+    assert acc > 0.85
+    stats = m.getPerformanceStatistics()
+    assert stats["numberOfExamplesPerPass"][0] == len(y)
+
+
+def test_classifier_logistic_link_equivalent():
+    df, X, y = _binary_df(n=1000)
+    a = VowpalWabbitClassifier(labelConversion=True, passThroughArgs="--loss_function logistic").fit(df)
+    b = VowpalWabbitClassifier(labelConversion=True,
+                               passThroughArgs="--loss_function logistic --link logistic").fit(df)
+    pa = a.transform(df)["probability"][:, 1]
+    pb = b.transform(df)["probability"][:, 1]
+    np.testing.assert_allclose(pa, pb, rtol=1e-4, atol=1e-5)
+
+
+def test_regressor_and_adaptive_rmse():
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(5000, 6))
+    y = X @ np.array([1.0, -2.0, 0.5, 0.0, 3.0, 1.5]) + 0.1 * rng.normal(size=5000)
+    df = DataFrame({"features": X, "label": y})
+    for args in ["", "--adaptive"]:
+        m = VowpalWabbitRegressor(passThroughArgs=args, numPasses=3).fit(df)
+        p = m.transform(df)["prediction"]
+        rmse = np.sqrt(np.mean((p - y) ** 2))
+        assert rmse < 0.15, (args, rmse)
+
+
+def test_multiclass_oaa_probabilities():
+    rng = np.random.default_rng(2)
+    n, k = 3000, 4
+    centers = rng.normal(scale=3, size=(k, 5))
+    lab = rng.integers(1, k + 1, size=n)
+    X = centers[lab - 1] + rng.normal(size=(n, 5))
+    df = DataFrame({"features": X, "label": lab.astype(np.float64)})
+    m = VowpalWabbitClassifier(numClasses=k, passThroughArgs=f"--oaa {k} --probabilities --loss_function logistic",
+                               numPasses=2).fit(df)
+    out = m.transform(df)
+    probs = out["probability"]
+    assert probs.shape == (n, k)
+    np.testing.assert_allclose(probs.sum(1), 1.0, atol=1e-4)
+    assert (np.argmax(probs, 1) + 1 == lab).mean() > 0.8
+
+
+def test_additional_features_and_interactions_param():
+    rng = np.random.default_rng(3)
+    a = rng.normal(size=(2000, 3))
+    b = rng.normal(size=(2000, 3))
+    y = (a[:, 0] * b[:, 1] > 0).astype(np.float64)  # needs the cross term
+    df = DataFrame({"a": a, "b": b, "label": y})
+    lin = VowpalWabbitClassifier(featuresCol="a", additionalFeatures=["b"], labelConversion=True,
+                                 passThroughArgs="--loss_function logistic", numPasses=3).fit(df)
+    quad = VowpalWabbitClassifier(featuresCol="a", additionalFeatures=["b"], labelConversion=True,
+                                  passThroughArgs="--loss_function logistic", interactions=["ab"],
+                                  numPasses=3).fit(df)
+    auc_lin = _auc(y, lin.transform(df)["probability"][:, 1])
+    auc_quad = _auc(y, quad.transform(df)["probability"][:, 1])
+    assert auc_quad > 0.9 > auc_lin
+
+
+def test_save_load_and_readable_model(tmp_path):
+    from synapseml_amd.core.pipeline import PipelineStage
+
+    df, X, y = _binary_df(n=500)
+    m = VowpalWabbitClassifier(labelConversion=True, passThroughArgs="--loss_function logistic").fit(df)
+    p = tmp_path / "vwm"
+    m.save(str(p))
+    m2 = PipelineStage.load(str(p))
+    np.testing.assert_allclose(m.transform(df)["probability"], m2.transform(df)["probability"])
+    txt = m.getReadableModel()
+    assert "bits" in txt.lower() or ":" in txt
+    m.saveNativeModel(str(tmp_path / "native.model"))
+    assert (tmp_path / "native.model").stat().st_size > 0
+
+
+def test_initial_model_continues():
+    df, X, y = _binary_df(n=2000)
+    a = VowpalWabbitClassifier(labelConversion=True, passThroughArgs="--loss_function logistic").fit(df)
+    b = VowpalWabbitClassifier(labelConversion=True, passThroughArgs="--loss_function logistic",
+                               initialModel=a.getModel()).fit(df)
+    assert b.getPerformanceStatistics()["numberOfExamplesPerPass"][0] == 2000
+    assert not np.allclose(a.transform(df)["rawPrediction"], b.transform(df)["rawPrediction"])
+
+
+def test_split_col_training():
+    df, X, y = _binary_df(n=2000, parts=2)
+    df = df.withColumn("split", np.arange(2000) % 3)
+    m = VowpalWabbitClassifier(labelConversion=True, passThroughArgs="--loss_function logistic",
+                               splitCol="split").fit(df)
+    assert _auc(y, m.transform(df)["probability"][:, 1]) > 0.9
+
+
+def test_empty_partition_ok():
+    df, X, y = _binary_df(n=300)
+    empty = df.filter(np.zeros(300, bool))
+    m = VowpalWabbitClassifier(labelConversion=True).fit(df)
+    assert m.transform(empty).count() == 0
+
+
+# ------------------------------------------------------------------ generic text format
+def test_generic_text_format():
+    rng = np.random.default_rng(4)
+    lines = []
+    ys = []
+    for _ in range(2000):
+        a, b = rng.normal(size=2)
+        yv = 1 if a - b > 0 else -1
+        ys.append(yv)
+        lines.append(f"{yv} |f a:{a:.4f} b:{b:.4f}")
+    df = DataFrame({"value": np.array(lines, dtype=object)})
+    m = VowpalWabbitGeneric(passThroughArgs="--loss_function logistic --link logistic", numPasses=2).fit(df)
+    p = m.transform(df)["prediction"]
+    assert _auc(np.array(ys) > 0, p) > 0.97
+    prog = VowpalWabbitGenericProgressive(passThroughArgs="--loss_function logistic").transform(df)
+    assert prog["prediction"].shape == (2000,)
+
+
+def test_generic_csoaa_text():
+    lines = ["1:0.0 2:1.0 3:1.0 | a", "1:1.0 2:0.0 3:1.0 | b", "1:1.0 2:1.0 3:0.0 | c"] * 200
+    df = DataFrame({"value": np.array(lines, dtype=object)})
+    m = VowpalWabbitGeneric(passThroughArgs="--csoaa 3").fit(df)
+    p = m.transform(DataFrame({"value": np.array(["| a", "| b", "| c"], dtype=object)}))["prediction"]
+    assert p.tolist() == [1.0, 2.0, 3.0]
+
+
+def test_unsupported_reduction_raises():
+    with pytest.raises(Exception):
+        native.load("_vw").VW("--cats 4")
+
+
+# ------------------------------------------------------------------ contextual bandit
+def _cb_df(n=3000, seed=5):
+    rng = np.random.default_rng(seed)
+    shared, actions, chosen, cost, prob = [], [], [], [], []
+    for _ in range(n):
+        s = rng.normal(size=3)
+        acts = [np.eye(3)[j] for j in range(3)]
+        best = int(np.argmax(s))
+        c = int(rng.integers(0, 3))
+        shared.append(s)
+        actions.append(acts)
+        chosen.append(c + 1)
+        cost.append(-1.0 if c == best else 0.0)
+        prob.append(1 / 3)
+    sh = np.stack(shared)
+    acol = np.empty(n, dtype=object)
+    for i, a in enumerate(actions):
+        acol[i] = a
+    return DataFrame({"shared": sh, "features": acol, "chosenAction": np.array(chosen), "label": np.array(cost),
+                      "probability": np.array(prob)}), sh
+
+
+def test_contextual_bandit_learns_policy():
+    df, sh = _cb_df()
+    cb = VowpalWabbitContextualBandit(epsilon=0.1, passThroughArgs="--cb_explore_adf -q sf", numPasses=2)
+    m = cb.fit(df)
+    out = m.transform(df)
+    pred = np.array([np.argmax(p) for p in out["prediction"]])
+    assert (pred == np.argmax(sh, 1)).mean() > 0.7
+    np.testing.assert_allclose([sum(p) for p in out["prediction"][:20]], 1.0, atol=1e-5)
+    with pytest.raises(NotImplementedError):
+        VowpalWabbitContextualBandit(passThroughArgs="--cb 3").fit(df)
+
+
+def test_cb_parallel_fit():
+    df, _ = _cb_df(n=500)
+    cb = VowpalWabbitContextualBandit(passThroughArgs="--cb_explore_adf")
+    models = cb.fit(df, [{cb.epsilon: 0.1}, {cb.epsilon: 0.3}])
+    assert len(models) == 2
+
+
+def test_cb_metrics():
+    m = ContextualBanditMetrics()
+    m.addExample(0.5, 1.0, 1.0)
+    m.addExample(0.5, 0.0, 0.0)
+    assert m.getIpsEstimate() == pytest.approx(1.0)
+    assert m.getSnipsEstimate() == pytest.approx(1.0)
+
+
+# ------------------------------------------------------------------ policy eval
+def test_kahan_sum():
+    k = KahanSum()
+    for _ in range(10):
+        k = k + 0.1
+    assert k.toDouble() == pytest.approx(1.0, abs=1e-15)
+    assert (KahanSum(1.0) + KahanSum(2.0)).toDouble() == 3.0
+
+
+def test_policy_estimators():
+    df = DataFrame({"probLog": [0.5, 0.25, 0.5], "reward": [1.0, 0.0, 1.0], "probPred": [1.0, 0.5, 0.0]})
+    assert Ips().evaluate(df) == pytest.approx((2 * 1 + 2 * 0 + 0) / 3)
+    assert Snips().evaluate(df) == pytest.approx(2.0 / 4.0)
+    cr = CressieRead().evaluate(df, wMin=0, wMax=100)
+    assert np.isfinite(cr)
+    iv = CressieReadInterval(True).evaluate(df, wMin=0, wMax=100)
+    assert iv.lower <= iv.upper
+
+
+def test_dsjson_and_cse():
+    rng = np.random.default_rng(6)
+    lines = []
+    for i in range(200):
+        idx = int(rng.integers(0, 2))
+        lines.append(json.dumps({"EventId": f"e{i}", "_label_cost": float(-(idx == 0)), "_label_probability": 0.5,
+                                 "_labelIndex": idx, "a": [1, 2], "c": {"x": 1}, "other": float(i % 2)}))
+    df = DataFrame({"value": np.array(lines, dtype=object)})
+    t = VowpalWabbitDSJsonTransformer(rewards={"reward": "_label_cost", "r2": "other"}).transform(df)
+    assert t["EventId"][0] == "e0" and t["probLog"][0] == pytest.approx(0.5)
+    assert set(t["rewards"][0].keys()) == {"reward", "r2"}
+    preds = np.empty(200, dtype=object)
+    for i in range(200):
+        preds[i] = [(0, 0.9), (1, 0.1)]
+    t = t.withColumn("predictions", preds)
+    cse = VowpalWabbitCSETransformer().transform(t)
+    assert cse["exampleCount"][0] == 200
+    r = cse["reward"][0]
+    assert r["minReward"] == -1.0 and r["maxReward"] == 0.0
+    # policy always picks action 0 (cost -1): ips ~ -1
+    assert r["ips"] == pytest.approx(-1.0, abs=0.25)
+    assert r["snips"] == pytest.approx(-1.0)
+    strat = VowpalWabbitCSETransformer(metricsStratificationCols=["chosenActionIndex"]).transform(t)
+    assert strat.count() == 2
+
+
+def test_vector_zipper():
+    df = DataFrame({"a": [1, 2], "b": [3, 4]})
+    out = VectorZipper(inputCols=["a", "b"], outputCol="z").transform(df)
+    assert [list(x) for x in out["z"]] == [[1, 3], [2, 4]]
+
+
+# ------------------------------------------------------------------ distributed (gloo, 2 ranks)
+def _vw_rank_fn(part, rank, world):
+    from synapseml_amd.vw import VowpalWabbitClassifier as C
+
+    m = C(labelConversion=True, passThroughArgs="--loss_function logistic", numPasses=2,
+          numSyncsPerPass=1).fit(part)
+    return m.getModel()
+
+
+def test_distributed_allreduce_gloo():
+    from synapseml_amd.parallel.runtime import run_partitions
+
+    df, X, y = _binary_df(n=2000, parts=2)
+    models = run_partitions(_vw_rank_fn, df, num_workers=2)
+    assert len(models) == 2
+    # after the final end-of-pass allreduce the weight tables are identical
+    vw = native.load("_vw")
+    w0 = np.asarray(vw.VW("--testonly", models[0]).weights())
+    w1 = np.asarray(vw.VW("--testonly", models[1]).weights())
+    np.testing.assert_allclose(w0, w1, rtol=1e-6, atol=1e-7)
