@@ -212,6 +212,22 @@ PYBIND11_MODULE(_vw, m) {
         for (uint64_t i = 0; i < n; ++i) o[i] = vw.weights()[i * vw.stride()];
         return out;
       });
+  // import a linear table trained elsewhere (the GPU learner) into w[0] of each slot
+  m.def("import_linear", [](VW& vw, F32 w, double examples, double weighted_labels, double sum_loss, double min_label,
+                            double max_label) {
+    const uint64_t n = vw.NumWeights() / vw.stride();
+    if (static_cast<uint64_t>(w.size()) != n) throw std::runtime_error("import_linear: size mismatch");
+    float* dst = vw.weights();
+    const float* src = w.data();
+    for (uint64_t i = 0; i < n; ++i) dst[i * vw.stride()] = src[i];
+    auto& st = vw.mutable_stats();
+    st.examples += static_cast<int64_t>(examples);
+    st.weighted_examples += examples;
+    st.weighted_labels += weighted_labels;
+    st.sum_loss += sum_loss;
+    st.min_label = std::min(st.min_label, min_label);
+    st.max_label = std::max(st.max_label, max_label);
+  });
   m.def("merge_models", [](std::vector<std::shared_ptr<VW>> ms) {
     std::vector<const VW*> v;
     for (auto& p : ms) v.push_back(p.get());

@@ -96,6 +96,7 @@ class VW {
   std::string SaveModel() const;
   std::string ReadableModel() const;
   const Stats& stats() const { return stats_; }
+  Stats& mutable_stats() { return stats_; }
   const std::string& args() const { return args_str_; }
   std::string OutputPredictionType() const;
   uint64_t NumWeights() const { return weights_.size(); }

@@ -14,6 +14,7 @@ training broadcasts the model per split and averages (mergeModels).
 """
 from __future__ import annotations
 
+import re
 import time
 from typing import List, Optional
 
@@ -142,6 +143,105 @@ def _host_allreduce_f32(arr: np.ndarray) -> None:
         D._dist().all_reduce(t)
 
 
+_GPU_UNSUPPORTED = re.compile(r"(^|\s)(-q|--quadratic|--cubic|--interactions|--oaa|--csoaa|--cb\w*|--ngram|--l1|"
+                              r"--ignore|--passes\s+0)(\s|$)")
+_nccl_cache: dict = {}
+
+
+def _merged_csr(blocks, n: int, constant: bool):
+    """Concatenate namespace blocks row-wise into one CSR (+ VW constant feature)."""
+    counts = np.zeros(n, np.int64)
+    for _, ip, _, _ in blocks:
+        counts += np.diff(ip)
+    if constant:
+        counts += 1
+    indptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    idx = np.empty(indptr[-1], np.uint32)
+    val = np.empty(indptr[-1], np.float32)
+    pos = indptr[:-1].copy()
+    for _, ip, ii, vv in blocks:
+        lens = np.diff(ip)
+        rows = np.repeat(np.arange(n), lens)
+        within = np.arange(len(ii)) - np.repeat(ip[:-1], lens)
+        dst = pos[rows] + within
+        idx[dst] = ii
+        val[dst] = vv
+        pos += lens
+    if constant:
+        idx[pos] = 11650396  # VW constant-feature hash
+        val[pos] = 1.0
+    return indptr, idx, val
+
+
+def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
+    """Device-resident hogwild mini-batch SGD (csrc/vw/vw_gpu.hip, K12).
+
+    Scope: linear squared/logistic learners (regressor / binary classifier)
+    with AdaGrad (default) or plain SGD steps; the trained table is imported
+    into a native VW model so save/load/readable-model/prediction are shared
+    with the CPU learner. Reductions, interactions and l1 stay on the exact
+    sequential CPU learner and are rejected here rather than silently run
+    elsewhere. Weight averaging across ranks at pass boundaries uses RCCL
+    (``nccl`` backend) on the learner's stream."""
+    vwmod = _vw()
+    if not vwmod.gpu_available():
+        raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
+    if _GPU_UNSUPPORTED.search(" " + args + " "):
+        raise ValueError(f"deviceType='gpu' supports linear squared/logistic learners only; got args: {args}")
+    if model_bytes is not None:
+        raise ValueError("deviceType='gpu' does not support initialModel")
+    ref = vwmod.VW(args)  # parses & validates args, owns the final model
+    cfg = vwmod.GpuSgdConfig()
+    cfg.bits = int(ref.num_bits)
+    m = re.search(r"(?:^|\s)(?:-l|--learning_rate)\s+(\S+)", args)
+    cfg.lr = float(m.group(1)) if m else 0.5
+    m = re.search(r"--power_t\s+(\S+)", args)
+    cfg.power_t = float(m.group(1)) if m else 0.5
+    m = re.search(r"--l2\s+(\S+)", args)
+    cfg.l2 = float(m.group(1)) if m else 0.0
+    cfg.loss = 1 if re.search(r"--loss_function\s+logistic", args) else 0
+    cfg.adaptive = "--sgd" not in args
+    import os
+
+    dev = int(os.environ.get("LOCAL_RANK", "0"))
+    g = vwmod.GpuSgd(cfg, dev)
+    t0 = time.perf_counter_ns()
+    cols = [est.getFeaturesCol()] + list(est.getAdditionalFeatures() or [])
+    blocks = namespace_blocks(df, cols, est.getHashSeed())
+    labels, _, _ = est._labels(df)
+    n = df.count()
+    indptr, idx, val = _merged_csr(blocks, n, "--noconstant" not in args)
+    wcol = est.getWeightCol()
+    weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
+    t1 = time.perf_counter_ns()
+    world = D.world_size()
+    comm = None
+    if world > 1 and D.backend() == "nccl":
+        key = world
+        if key not in _nccl_cache:
+            uid = vwmod.nccl_unique_id() if D.rank() == 0 else None
+            _nccl_cache[key] = vwmod.nccl_comm(D.broadcast_object(uid, 0), D.rank(), world)
+        comm = _nccl_cache[key]
+    for _ in range(max(1, est.getNumPasses())):
+        if n:
+            g.learn(indptr, idx, val, labels, weights, int(est.getGpuBatchSize()))
+        if world > 1:
+            if comm is not None:
+                g.allreduce_average(comm)
+            else:
+                w = np.ascontiguousarray(g.weights(), np.float32)
+                _host_allreduce_f32(w)
+                g.set_weights(w / world)
+    t2 = time.perf_counter_ns()
+    lab = labels.astype(np.float64)
+    wts = np.ones(n) if weights is None else weights.astype(np.float64)
+    vwmod.import_linear(ref, np.asarray(g.weights(), np.float32), float(g.examples), float((lab * wts).sum()),
+                        float(g.sum_loss), float(lab.min()) if n else 0.0, float(lab.max()) if n else 0.0)
+    stats = ref.stats()
+    stats.update(timeTotalNs=t2 - t0, timeNativeIngestNs=t1 - t0, timeLearnNs=t2 - t1, timeMultipassNs=0)
+    return ref, stats
+
+
 class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
     model = Param("The VW model bytes", None, complex=True)
     performanceStatistics = Param("Training statistics", None, complex=True)
@@ -189,6 +289,8 @@ class VowpalWabbitBase(Estimator, VowpalWabbitBaseParams, HasLabelCol, HasWeight
         return np.asarray(df[self.getLabelCol()], dtype=np.float32), None, None
 
     def _train_partition(self, df: DataFrame, args: str, model_bytes=None):
+        if (self.getDeviceType() or "cpu").lower() == "gpu":
+            return _train_partition_gpu(self, df, args, model_bytes)
         vw = _vw().VW(args, model_bytes)
         world = D.world_size()
         if world > 1:

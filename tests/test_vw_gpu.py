@@ -1,0 +1,59 @@
+"""GPU hogwild VW learner (csrc/vw/vw_gpu.hip) vs the exact CPU learner."""
+import numpy as np
+import pytest
+
+from synapseml_amd.core.dataframe import DataFrame
+from synapseml_amd.ops import native
+from synapseml_amd.vw import VowpalWabbitClassifier, VowpalWabbitRegressor
+from synapseml_amd.vw.learners import _merged_csr, namespace_blocks
+
+
+def _binary(n=20000, d=20, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, d))
+    w = rng.normal(size=d)
+    y = (X @ w + 0.3 * rng.normal(size=n) > 0).astype(np.float64)
+    return DataFrame({"features": X, "label": y}), y
+
+
+def test_merged_csr_matches_blocks():
+    df = DataFrame({"a": np.array([[1.0, 0.0], [0.0, 2.0]]), "b": np.array([[3.0], [0.0]])})
+    blocks = namespace_blocks(df, ["a", "b"], 0)
+    ip, idx, val = _merged_csr(blocks, 2, True)
+    assert ip.tolist() == [0, 3, 5]
+    assert val.tolist() == [1.0, 3.0, 1.0, 2.0, 1.0]
+    assert idx[2] == 11650396 and idx[4] == 11650396
+
+
+def test_gpu_request_without_gpu_fails_loudly():
+    if native.load("_vw").gpu_available():
+        pytest.skip("GPU present")
+    df, _ = _binary(n=100)
+    with pytest.raises(RuntimeError):
+        VowpalWabbitClassifier(deviceType="gpu", labelConversion=True).fit(df)
+
+
+@pytest.mark.gpu
+def test_gpu_classifier_matches_cpu_quality():
+    from sklearn.metrics import roc_auc_score
+
+    df, y = _binary()
+    args = "--loss_function logistic"
+    gpu = VowpalWabbitClassifier(deviceType="gpu", labelConversion=True, passThroughArgs=args, numPasses=3,
+                                 gpuBatchSize=256).fit(df)
+    cpu = VowpalWabbitClassifier(labelConversion=True, passThroughArgs=args, numPasses=3).fit(df)
+    ag = roc_auc_score(y, gpu.transform(df)["probability"][:, 1])
+    ac = roc_auc_score(y, cpu.transform(df)["probability"][:, 1])
+    assert ag > 0.97 and ag > ac - 0.01, (ag, ac)
+    assert gpu.getPerformanceStatistics()["numberOfExamplesPerPass"][0] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_regressor_rmse():
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(20000, 6))
+    y = X @ np.array([1.0, -2.0, 0.5, 0.0, 3.0, 1.5]) + 0.1 * rng.normal(size=20000)
+    df = DataFrame({"features": X, "label": y})
+    m = VowpalWabbitRegressor(deviceType="gpu", numPasses=5, gpuBatchSize=256).fit(df)
+    p = m.transform(df)["prediction"]
+    assert np.sqrt(np.mean((p - y) ** 2)) < 0.3
