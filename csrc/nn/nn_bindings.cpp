@@ -1,0 +1,34 @@
+// pybind11 module _nn: raw-pointer entry points (torch data_ptr + stream).
+#include <pybind11/pybind11.h>
+
+#include "nn_ops.h"
+
+namespace py = pybind11;
+using namespace smlnn;
+
+template <class T>
+static T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+PYBIND11_MODULE(_nn, m) {
+  m.doc() = "MI355X fused epilogue kernels for the ONNX executor";
+  m.def("gpu_available", &NnGpuAvailable);
+  m.def("affine_act", [](uintptr_t x, int64_t n, int C, int HW, int nhwc, uintptr_t scale, uintptr_t shift,
+                         uintptr_t res, int act, float alpha, int dtype, uintptr_t y, uintptr_t stream) {
+    AffineAct(P<const void>(x), n, C, HW, nhwc, P<const float>(scale), P<const float>(shift), P<const void>(res), act,
+              alpha, dtype, P<void>(y), P<void>(stream));
+  });
+  m.def("add_affine_act", [](uintptr_t a, uintptr_t b, int64_t n, int C, int HW, int nhwc, uintptr_t scale,
+                             uintptr_t shift, int act, int dtype, uintptr_t sum_out, uintptr_t act_out,
+                             uintptr_t stream) {
+    AddAffineAct(P<const void>(a), P<const void>(b), n, C, HW, nhwc, P<const float>(scale), P<const float>(shift), act,
+                 dtype, P<void>(sum_out), P<void>(act_out), P<void>(stream));
+  });
+  m.def("gap_nhwc", [](uintptr_t x, int N, int HW, int C, int dtype, uintptr_t out, uintptr_t stream) {
+    GapNhwc(P<const void>(x), N, HW, C, dtype, P<float>(out), P<void>(stream));
+  });
+  m.def("softmax_rows", [](uintptr_t x, int rows, int cols, uintptr_t y, uintptr_t amax, uintptr_t stream) {
+    SoftmaxRows(P<const float>(x), rows, cols, P<float>(y), P<int64_t>(amax), P<void>(stream));
+  });
+}

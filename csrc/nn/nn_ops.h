@@ -1,0 +1,21 @@
+// Fused epilogue / post-processing kernels of the ONNX executor (module _nn).
+// dtype: 0 fp32, 1 fp16, 2 bf16. act: 0 none, 1 relu, 2 leaky(alpha),
+// 3 sigmoid, 4 clip(0, alpha). All pointers are device pointers.
+#pragma once
+#include <cstdint>
+
+namespace smlnn {
+
+bool NnGpuAvailable();
+// y = act(x * scale[c] + shift[c] + res); scale/shift/res may be null; y may alias x.
+void AffineAct(const void* x, int64_t n, int C, int HW, int nhwc, const float* scale, const float* shift,
+               const void* res, int act, float alpha, int dtype, void* y, void* stream);
+// sum = a + b; act_out = act(sum * scale[c] + shift[c]) (one pass, two outputs)
+void AddAffineAct(const void* a, const void* b, int64_t n, int C, int HW, int nhwc, const float* scale,
+                  const float* shift, int act, int dtype, void* sum_out, void* act_out, void* stream);
+// NHWC global average pool -> fp32 [N, C]
+void GapNhwc(const void* x, int N, int HW, int C, int dtype, float* out, void* stream);
+// fp32 row softmax (y may be null) and argmax (amax may be null)
+void SoftmaxRows(const float* x, int rows, int cols, float* y, int64_t* amax, void* stream);
+
+}  // namespace smlnn

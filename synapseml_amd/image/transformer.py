@@ -1,0 +1,440 @@
+"""ImageTransformer, ImageSetAugmenter, UnrollImage / UnrollBinaryImage,
+ResizeImageTransformer.
+
+Reference: opencv/.../ImageTransformer.scala:31-725 (stages 68-283, tensor
+conversion 335-415, transform 643-686), ImageSetAugmenter.scala:18-77,
+core/.../image/UnrollImage.scala:27-250.
+
+Execution: stage semantics are the OpenCV ones (csrc/image/image_ops.h). On
+the MI355X the common inference pipeline — decode → resize → (center)crop →
+channel reorder → normalize → CHW tensor — runs as ONE batched HIP kernel
+(K19, csrc/image/image_gpu.hip) over a packed host→device upload; other stage
+lists run stage by stage through the native host kernels.
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..core.contracts import HasInputCol, HasOutputCol
+from ..core.dataframe import DataFrame
+from ..core.linalg import DenseVector
+from ..core.params import Param, TypeConverters as T
+from ..core.pipeline import Transformer
+from ..ops import native
+from .schema import make_image_row, row_to_array, to_array
+
+STAGE_NAME = "stageName"
+
+
+def _img():
+    return native.load("_image")
+
+
+def _gpu_ok(device_type: str) -> bool:
+    dt = (device_type or "auto").lower()
+    if dt == "cpu":
+        return False
+    try:
+        import torch
+
+        ok = torch.cuda.is_available()
+    except Exception:
+        ok = False
+    if dt in ("gpu", "cuda", "rocm") and not ok:
+        raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
+    return ok
+
+
+# ---------------------------------------------------------------------- stage application (host)
+def resize_target(stage: dict, h: int, w: int) -> Tuple[int, int]:
+    if "size" in stage:
+        size = int(stage["size"])
+        if stage.get("keepAspectRatio", False):
+            ratio = size / min(w, h)
+            return _jround(ratio * h), _jround(ratio * w)
+        return size, size
+    return int(stage["height"]), int(stage["width"])
+
+
+def _jround(x: float) -> int:
+    """java.lang.Math.round (half up)."""
+    return int(np.floor(x + 0.5))
+
+
+def center_crop_rect(stage: dict, h: int, w: int) -> Tuple[int, int, int, int]:
+    ch, cw = min(int(stage["height"]), h), min(int(stage["width"]), w)
+    y = h // 2 - ch // 2
+    x = w // 2 - cw // 2
+    return y, x, ch, cw
+
+
+def apply_stage(stage: dict, a: np.ndarray) -> np.ndarray:
+    lib = _img()
+    name = stage[STAGE_NAME]
+    if name == "resize":
+        th, tw = resize_target(stage, a.shape[0], a.shape[1])
+        out = lib.resize(a, th, tw)
+        return out if out.ndim == 3 else out[:, :, None]
+    if name == "crop":
+        x, y, h, w = int(stage["x"]), int(stage["y"]), int(stage["height"]), int(stage["width"])
+        if x + w > a.shape[1] or y + h > a.shape[0]:
+            raise ValueError("crop rectangle outside the image")
+        return np.ascontiguousarray(a[y:y + h, x:x + w])
+    if name == "centercrop":
+        y, x, ch, cw = center_crop_rect(stage, a.shape[0], a.shape[1])
+        return np.ascontiguousarray(a[y:y + ch, x:x + cw])
+    if name == "colorformat":
+        out = lib.cvt_color(a, int(stage["format"]))
+        return out if out.ndim == 3 else out[:, :, None]
+    if name == "flip":
+        code = int(stage.get("flipCode", 1))
+        if code == 0:
+            return np.ascontiguousarray(a[::-1])
+        if code > 0:
+            return np.ascontiguousarray(a[:, ::-1])
+        return np.ascontiguousarray(a[::-1, ::-1])
+    if name == "blur":
+        # Imgproc.blur(image, dst, new Size(height, width)): Size(width=height, height=width)
+        kw, kh = int(stage["height"]), int(stage["width"])
+        out = lib.box_blur(a, kw, kh)
+        return out if out.ndim == 3 else out[:, :, None]
+    if name == "threshold":
+        out = lib.threshold(a, float(stage["threshold"]), float(stage["maxVal"]), int(stage["type"]))
+        return out if out.ndim == 3 else out[:, :, None]
+    if name == "gaussiankernel":
+        k = lib.gaussian_kernel(int(stage["apertureSize"]), float(stage["sigma"]))
+        out = lib.column_filter(a, k)
+        return out if out.ndim == 3 else out[:, :, None]
+    raise ValueError(f"unknown image stage {name}")
+
+
+def channel_map(c: int, order: str, auto_color: bool) -> List[int]:
+    """Output channel k <- source channel (extractChannels, ImageTransformer.scala:344-374)."""
+    rgb = order.lower() == "rgb"
+    if c >= 3:
+        return [2, 1, 0] if rgb else [0, 1, 2]
+    if c == 1 and auto_color:
+        return [0, 0, 0]
+    return list(range(c))
+
+
+# ---------------------------------------------------------------------- transformer
+class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
+    stages = Param("Image transformation stages", [], T.identity)
+    toTensor = Param("Convert output image to tensor in the shape of (C * H * W)", False, T.toBoolean)
+    tensorElementType = Param("The element data type for the output tensor (float | double)", "float", T.toString)
+    tensorChannelOrder = Param("The color channel order of the output channels. Valid values are RGB and BGR.",
+                               "RGB", T.toString)
+    normalizeMean = Param("The mean value to use for normalization for each channel", None, T.identity)
+    normalizeStd = Param("The standard deviation to use for normalization for each channel", None, T.identity)
+    colorScaleFactor = Param("The scale factor for color values.", None, T.toFloat)
+    autoConvertToColor = Param("Whether to automatically convert black and white images to color", False,
+                               T.toBoolean)
+    ignoreDecodingErrors = Param("Whether to throw on decoding errors or just return null", False, T.toBoolean)
+    deviceType = Param("auto | cpu | gpu — where batches of images are processed", "auto", T.toString)
+    batchSize = Param("Images per device batch", 256, T.toInt)
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self._setDefault(inputCol="image", outputCol=self.uid + "_output")
+
+    # ---- builder API
+    def _add(self, stage: dict) -> "ImageTransformer":
+        self.set("stages", list(self.getStages() or []) + [stage])
+        return self
+
+    def resize(self, size=None, keep_aspect_ratio=True, height: Optional[int] = None, width: Optional[int] = None,
+               keepAspectRatio: Optional[bool] = None):  # noqa: N803
+        if keepAspectRatio is not None:
+            keep_aspect_ratio = keepAspectRatio
+        if height is not None and width is not None:
+            return self._add({STAGE_NAME: "resize", "height": int(height), "width": int(width)})
+        if isinstance(size, tuple):
+            return self._add({STAGE_NAME: "resize", "height": int(size[1]), "width": int(size[0])})
+        if isinstance(keep_aspect_ratio, (int, np.integer)) and not isinstance(keep_aspect_ratio, bool):
+            # Scala form resize(height, width)
+            return self._add({STAGE_NAME: "resize", "height": int(size), "width": int(keep_aspect_ratio)})
+        if size is None or int(size) < 0:
+            raise ValueError("size should be non-negative")
+        return self._add({STAGE_NAME: "resize", "size": int(size), "keepAspectRatio": bool(keep_aspect_ratio)})
+
+    def crop(self, x: int, y: int, height: int, width: int):
+        if min(x, y, height, width) < 0:
+            raise ValueError("crop values should be non-negative")
+        return self._add({STAGE_NAME: "crop", "x": x, "y": y, "height": height, "width": width})
+
+    def centerCrop(self, height: int, width: int):  # noqa: N802
+        if min(height, width) < 0:
+            raise ValueError("crop values should be non-negative")
+        return self._add({STAGE_NAME: "centercrop", "height": height, "width": width})
+
+    def colorFormat(self, format: int):  # noqa: N802,A002
+        return self._add({STAGE_NAME: "colorformat", "format": int(format)})
+
+    def flip(self, flip_code: int = 1):
+        return self._add({STAGE_NAME: "flip", "flipCode": int(flip_code)})
+
+    def blur(self, height: float, width: float):
+        return self._add({STAGE_NAME: "blur", "height": float(height), "width": float(width)})
+
+    def threshold(self, threshold: float, max_val: float, threshold_type: int):
+        return self._add({STAGE_NAME: "threshold", "threshold": float(threshold), "maxVal": float(max_val),
+                          "type": int(threshold_type)})
+
+    def gaussianKernel(self, aperture_size: int, sigma: float):  # noqa: N802
+        return self._add({STAGE_NAME: "gaussiankernel", "apertureSize": int(aperture_size), "sigma": float(sigma)})
+
+    def normalize(self, mean: Sequence[float], std: Sequence[float], color_scale_factor: float):
+        self.set("toTensor", True)
+        self.set("normalizeMean", [float(v) for v in mean])
+        self.set("normalizeStd", [float(v) for v in std])
+        self.set("colorScaleFactor", float(color_scale_factor))
+        return self
+
+    # ---- execution
+    def _fused_plan(self, arrays: List[np.ndarray]):
+        """(resize_h, resize_w, crop) when the stage list maps onto K19 for this batch."""
+        st = list(self.getStages() or [])
+        if not self.getToTensor() or self.getTensorElementType().lower() != "float":
+            return None
+        rs = None
+        crop = None
+        i = 0
+        if i < len(st) and st[i][STAGE_NAME] == "resize":
+            if "size" in st[i] and st[i].get("keepAspectRatio", False):
+                return None
+            rs = resize_target(st[i], 1, 1)
+            i += 1
+        if i < len(st) and st[i][STAGE_NAME] in ("centercrop", "crop"):
+            crop = st[i]
+            i += 1
+        if i != len(st):
+            return None
+        shapes = {a.shape[:2] for a in arrays}
+        if rs is None and len(shapes) != 1:
+            return None
+        base_h, base_w = rs if rs is not None else next(iter(shapes))
+        if crop is None:
+            cy, cx, ch, cw = 0, 0, base_h, base_w
+        elif crop[STAGE_NAME] == "centercrop":
+            cy, cx, ch, cw = center_crop_rect(crop, base_h, base_w)
+        else:
+            cy, cx, ch, cw = int(crop["y"]), int(crop["x"]), int(crop["height"]), int(crop["width"])
+            if cy + ch > base_h or cx + cw > base_w:
+                return None
+        if len({a.shape[2] for a in arrays}) != 1:
+            return None
+        return (rs or (0, 0)), (cy, cx, ch, cw)
+
+    def _norm_params(self, cout: int):
+        mean = self.getNormalizeMean() or [0.0] * cout
+        std = self.getNormalizeStd() or [1.0] * cout
+        if len(mean) != cout or len(std) != cout:
+            raise ValueError(f"channelLength: {cout}, means length: {len(mean)}, std length: {len(std)}")
+        scale = self.getColorScaleFactor()
+        return [float(m) for m in mean], [float(s) for s in std], float(scale if scale is not None else 1.0)
+
+    def device_tensors(self, arrays: List[np.ndarray], dtype: str = "float32", nhwc: bool = False):
+        """Run the fused K19 path on a batch; returns a device tensor [B,C,H,W] or None if not applicable."""
+        import torch
+
+        plan = self._fused_plan(arrays)
+        if plan is None or not arrays:
+            return None
+        (rh, rw), (cy, cx, ch, cw) = plan
+        c = arrays[0].shape[2]
+        cmap = channel_map(c, self.getTensorChannelOrder(), self.getAutoConvertToColor())
+        mean, std, scale = self._norm_params(len(cmap))
+        sizes = [a.size for a in arrays]
+        offsets = np.zeros(len(arrays), np.int64)
+        offsets[1:] = np.cumsum(sizes)[:-1]
+        host = torch.empty(int(sum(sizes)), dtype=torch.uint8, pin_memory=True)
+        hv = host.numpy()
+        for a, o in zip(arrays, offsets):
+            hv[o:o + a.size] = a.reshape(-1)
+        dims = np.array([[a.shape[0], a.shape[1], a.shape[2]] for a in arrays], np.int32).reshape(-1)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        src = host.to(dev, non_blocking=True)
+        off_d = torch.from_numpy(offsets).to(dev, non_blocking=True)
+        dims_d = torch.from_numpy(dims).to(dev, non_blocking=True)
+        tdt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[dtype]
+        B = len(arrays)
+        out = torch.empty((B, ch, cw, len(cmap)) if nhwc else (B, len(cmap), ch, cw), dtype=tdt, device=dev)
+        if min(rh, rw) == 0:
+            for a in arrays:
+                if cy + ch > a.shape[0] or cx + cw > a.shape[1]:
+                    raise ValueError("crop rectangle outside the image")
+        _img().preprocess_batch_device(src.data_ptr(), off_d.data_ptr(), dims_d.data_ptr(), B, ch, cw, rh, rw, cy, cx,
+                                       cmap, scale, mean, std, {torch.float32: 0, torch.float16: 1,
+                                                                torch.bfloat16: 2}[tdt], int(nhwc), out.data_ptr(),
+                                       torch.cuda.current_stream(dev).cuda_stream)
+        if nhwc:
+            out = out.permute(0, 3, 1, 2)  # logical NCHW view, channels-last memory
+        # keep the upload buffers alive until the kernel has consumed them
+        out._sml_keepalive = (host, src, off_d, dims_d)
+        return out
+
+    def process_host(self, a: np.ndarray):
+        for st in self.getStages() or []:
+            a = apply_stage(st, a)
+        if not self.getToTensor():
+            return a
+        cmap = channel_map(a.shape[2], self.getTensorChannelOrder(), self.getAutoConvertToColor())
+        mean, std, scale = self._norm_params(len(cmap))
+        t = _img().to_tensor(np.ascontiguousarray(a), cmap, scale, mean, std)
+        if self.getTensorElementType().lower() == "double":
+            # the reference normalises in float64: recompute exactly
+            src = a[:, :, cmap].astype(np.float64).transpose(2, 0, 1)
+            return (src * scale - np.asarray(mean)[:, None, None]) / np.asarray(std)[:, None, None]
+        return t
+
+    def decode_column(self, df: DataFrame) -> List[Optional[np.ndarray]]:
+        col = df[self.getInputCol()].tolist()
+        ign = self.getIgnoreDecodingErrors()
+        if len(col) > 8 and any(isinstance(v, (bytes, bytearray)) for v in col[:8]):
+            with ThreadPoolExecutor(max_workers=8) as ex:
+                return list(ex.map(lambda v: to_array(v, ign), col))
+        return [to_array(v, ign) for v in col]
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        arrays = self.decode_column(df)
+        n = len(arrays)
+        out = np.empty(n, dtype=object)
+        valid = [i for i, a in enumerate(arrays) if a is not None]
+        done = set()
+        if self.getToTensor() and valid and _gpu_ok(self.getDeviceType()):
+            bs = max(1, self.getBatchSize())
+            for s in range(0, len(valid), bs):
+                idx = valid[s:s + bs]
+                t = self.device_tensors([arrays[i] for i in idx])
+                if t is None:
+                    break
+                host = t.float().cpu().numpy()
+                for j, i in enumerate(idx):
+                    out[i] = host[j]
+                    done.add(i)
+        for i in valid:
+            if i in done:
+                continue
+            r = self.process_host(arrays[i])
+            if self.getToTensor():
+                out[i] = r
+            else:
+                origin = ""
+                v = df[self.getInputCol()][i]
+                if isinstance(v, dict):
+                    origin = v.get("origin", "")
+                out[i] = make_image_row(r, origin)
+        return df.withColumn(self.getOutputCol(), out)
+
+
+class ImageSetAugmenter(Transformer, HasInputCol, HasOutputCol):
+    flipLeftRight = Param("Symmetric Left-Right", True, T.toBoolean)
+    flipUpDown = Param("Symmetric Up-Down", False, T.toBoolean)
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self._setDefault(inputCol="image", outputCol=self.uid + "_output")
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        base = df.withColumn(self.getOutputCol(), df[self.getInputCol()])
+        parts = [base]
+        for enabled, code in ((self.getFlipLeftRight(), 1), (self.getFlipUpDown(), 0)):
+            if enabled:
+                t = ImageTransformer(inputCol=self.getInputCol(), outputCol=self.getOutputCol()).flip(code)
+                parts.append(t.transform(df))
+        out = parts[0]
+        for p in parts[1:]:
+            out = out.union(p)
+        return out
+
+
+def unroll(row) -> np.ndarray:
+    """Image row -> CHW float vector. Like the reference (UnrollImage.scala:31-51)
+    a 0 byte unrolls to 256.0 (its signed-byte conversion maps b <= 0 to b + 256)."""
+    a = row_to_array(row).astype(np.float64)
+    v = a.transpose(2, 0, 1).reshape(-1)
+    return np.where(v > 0, v, v + 256.0)
+
+
+def roll(values, origin: str, height: int, width: int, n_channels: int, mode: int) -> dict:
+    v = np.clip(np.rint(np.asarray(values, dtype=np.float64)), 0, 255).astype(np.uint8)
+    a = v.reshape(3, height, width).transpose(1, 2, 0)
+    row = make_image_row(a, origin)
+    row["nChannels"], row["mode"] = n_channels, mode
+    return row
+
+
+class UnrollImage(Transformer, HasInputCol, HasOutputCol):
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self._setDefault(inputCol="image", outputCol=self.uid + "_output")
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        col = df[self.getInputCol()]
+        out = np.empty(len(col), dtype=object)
+        for i, r in enumerate(col.tolist()):
+            out[i] = None if r is None else DenseVector(unroll(r))
+        return df.withColumn(self.getOutputCol(), out)
+
+
+class UnrollBinaryImage(Transformer, HasInputCol, HasOutputCol):
+    """Encoded bytes -> unrolled vector, optionally resized (UnrollImage.scala:195-250)."""
+
+    width = Param("the width of the image", None, T.toInt)
+    height = Param("the height of the image", None, T.toInt)
+    nChannels = Param("the number of channels of the target image", None, T.toInt)
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self._setDefault(inputCol="image", outputCol=self.uid + "_output")
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        col = df[self.getInputCol()]
+        out = np.empty(len(col), dtype=object)
+        for i, b in enumerate(col.tolist()):
+            if b is None:
+                out[i] = None
+                continue
+            a = to_array(b, ignore_errors=True)
+            if a is None:
+                out[i] = None
+                continue
+            if self.getHeight() and self.getWidth():
+                a = apply_stage({STAGE_NAME: "resize", "height": self.getHeight(), "width": self.getWidth()}, a)
+            nc = self.getNChannels()
+            if nc == 1 and a.shape[2] >= 3:
+                a = _img().cvt_color(np.ascontiguousarray(a[:, :, :3]), 6)[:, :, None]
+            elif nc == 3 and a.shape[2] == 1:
+                a = np.repeat(a, 3, axis=2)
+            elif nc == 3 and a.shape[2] == 4:
+                a = np.ascontiguousarray(a[:, :, :3])
+            out[i] = DenseVector(unroll({"height": a.shape[0], "width": a.shape[1], "nChannels": a.shape[2],
+                                         "data": a.tobytes()}))
+        return df.withColumn(self.getOutputCol(), out)
+
+
+class ResizeImageTransformer(Transformer, HasInputCol, HasOutputCol):
+    """Resize (and optionally change channels) of image rows (core/.../image/ResizeImageTransformer.scala)."""
+
+    width = Param("the width of the image", None, T.toInt)
+    height = Param("the height of the image", None, T.toInt)
+    nChannels = Param("the number of channels of the target image", None, T.toInt)
+
+    def _transform(self, df: DataFrame) -> DataFrame:
+        col = df[self.getInputCol()]
+        out = np.empty(len(col), dtype=object)
+        for i, r in enumerate(col.tolist()):
+            if r is None:
+                out[i] = None
+                continue
+            a = to_array(r)
+            a = apply_stage({STAGE_NAME: "resize", "height": self.getHeight(), "width": self.getWidth()}, a)
+            nc = self.getNChannels()
+            if nc == 1 and a.shape[2] >= 3:
+                a = _img().cvt_color(np.ascontiguousarray(a[:, :, :3]), 6)[:, :, None]
+            out[i] = make_image_row(a, r.get("origin", "") if isinstance(r, dict) else "")
+        return df.withColumn(self.getOutputCol(), out)

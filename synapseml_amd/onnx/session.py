@@ -1,0 +1,608 @@
+"""ONNX inference session for the MI355X (replaces ONNX Runtime; reference:
+deep-learning/.../onnx/ONNXRuntime.scala:25-107).
+
+Compile pipeline (``optimization_level`` BASIC/EXTENDED/ALL_OPT, NO_OPT skips
+2-4):
+
+1. decode + topologically order the graph (graph.py);
+2. constant folding — every node whose inputs are all constants is evaluated
+   once on the host (shape arithmetic, weight transposes, ...);
+3. Conv→BatchNormalization folding into the conv weights/bias;
+4. epilogue fusion: Conv[+bias][+residual Add][+Relu/LeakyRelu/Sigmoid/Clip]
+   → one conv + one fused epilogue pass; standalone BatchNormalization[+act]
+   → one affine pass; the pre-activation pattern ``s = a + b; y = act(bn(s))``
+   (ResNet v2) → one pass writing both ``s`` and ``y``. On the GPU the
+   epilogues run as the HIP kernels of csrc/nn (module ``_nn``); on the host
+   they run as torch ops with identical math.
+
+Execution: activations live on the session's device in the compute dtype
+(fp32 by default for ORT parity; fp16/bf16 selectable), 4-D activations in
+channels-last layout on the GPU; dead intermediates are freed at their last
+use. For fixed input shapes the whole plan is captured once into a HIP graph
+(``torch.cuda.CUDAGraph`` drives hipGraph on ROCm) and replayed, so a batch
+costs one graph launch instead of one launch per node.
+"""
+from __future__ import annotations
+
+import math
+import threading
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import proto as P
+from .graph import Graph, Node, ValueInfo
+from .ops import OPS, TORCH_OF, conv_args, _sym_pad
+
+OPT_LEVELS = ("NO_OPT", "BASIC_OPT", "EXTENDED_OPT", "ALL_OPT")
+_ACTS = {"Relu": 1, "LeakyRelu": 2, "Sigmoid": 3, "Clip": 4}
+_NONDETERMINISTIC = {"RandomNormal", "RandomUniform", "RandomNormalLike", "RandomUniformLike", "Multinomial",
+                     "Bernoulli"}
+_MAX_FOLD_ELEMS = 1 << 24
+
+
+def _is_const_tensor(v) -> bool:
+    return isinstance(v, (torch.Tensor, np.ndarray))
+
+
+class _RT:
+    """Per-node runtime context handed to op implementations."""
+
+    __slots__ = ("device", "opset", "op_type", "node_outputs", "node_num_outputs", "session")
+
+    def __init__(self, session, node: Node):
+        self.device = session.device
+        self.opset = session.opset
+        self.op_type = node.op_type
+        self.node_outputs = node.outputs
+        self.node_num_outputs = len(node.outputs)
+        self.session = session
+
+    def run_subgraph(self, g: Graph, feeds: Dict[str, Any]):
+        sub = InferenceSession.from_graph(g, device=self.device, optimization_level="NO_OPT",
+                                          outer=self.session._live_values)
+        return sub.run_values(feeds)
+
+
+class InferenceSession:
+    def __init__(self, model: bytes, device: Optional[str] = None, precision: str = "fp32",
+                 optimization_level: str = "ALL_OPT", use_graph: bool = True, channels_last: Optional[bool] = None):
+        g = Graph.from_bytes(model)
+        self._init(g, device, precision, optimization_level, use_graph, channels_last)
+
+    @classmethod
+    def from_graph(cls, g: Graph, device=None, precision="fp32", optimization_level="ALL_OPT", use_graph=False,
+                   outer: Optional[Dict[str, Any]] = None):
+        s = cls.__new__(cls)
+        s._outer = outer or {}
+        s._init(g, device, precision, optimization_level, use_graph, None)
+        return s
+
+    # ------------------------------------------------------------------ setup
+    def _init(self, g: Graph, device, precision, optimization_level, use_graph, channels_last):
+        if not hasattr(self, "_outer"):
+            self._outer = {}
+        self.graph = g
+        if device is None or str(device).upper() in ("GPU", "CUDA", "ROCM", "AUTO"):
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        elif str(device).upper() == "CPU":
+            device = "cpu"
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.gpu = self.device.type == "cuda"
+        self.opset = int(g.opset.get("", g.opset.get("ai.onnx", 13)))
+        self.compute_dtype = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[precision]
+        self.channels_last = self.gpu if channels_last is None else channels_last
+        lvl = optimization_level.upper()
+        if lvl not in OPT_LEVELS:
+            raise ValueError(f"optimizationLevel must be one of {OPT_LEVELS}")
+        self.optimization_level = lvl
+        self.use_graph = use_graph and self.gpu
+        self.inputs: List[ValueInfo] = list(g.inputs)
+        self.outputs: List[ValueInfo] = list(g.outputs)
+        self._nn = None
+        if self.gpu:
+            from ..ops import native
+
+            self._nn = native.load("_nn")  # loud failure if the HIP kernels are missing on a GPU box
+        self._consts: Dict[str, Any] = {}
+        for k, v in g.initializers.items():
+            self._consts[k] = v if v.dtype == object else torch.from_numpy(np.array(v, copy=True))
+        nodes = g.toposort()
+        if lvl != "NO_OPT":
+            nodes = self._fold_constants(nodes)
+            nodes = self._fold_conv_bn(nodes)
+            nodes = self._fuse_epilogues(nodes)
+        self.nodes = nodes
+        self._place_constants()
+        self._plan_liveness()
+        self._graphs: Dict[tuple, Any] = {}
+        self._graph_lock = threading.Lock()
+        self._live_values: Dict[str, Any] = {}
+
+    def _fold_constants(self, nodes: List[Node]) -> List[Node]:
+        out = []
+        for n in nodes:
+            if (n.op_type not in _NONDETERMINISTIC and n.op_type in OPS and n.inputs
+                    and all((not x) or x in self._consts for x in n.inputs)
+                    and not any(isinstance(v, Graph) for v in n.attrs.values())
+                    and all(_numel(self._consts[x]) <= _MAX_FOLD_ELEMS for x in n.inputs if x)):
+                try:
+                    rt = _RT(self, n)
+                    rt.device = torch.device("cpu")
+                    vals = OPS[n.op_type](rt, n.attrs, [self._consts[x] if x else None for x in n.inputs])
+                    if all(_is_const_tensor(v) for v in vals):
+                        for name, v in zip(n.outputs, vals):
+                            if name:
+                                self._consts[name] = v.cpu() if isinstance(v, torch.Tensor) else v
+                        continue
+                except Exception:
+                    pass
+            elif n.op_type == "Constant":
+                vals = OPS["Constant"](_RT(self, n), n.attrs, [])
+                self._consts[n.outputs[0]] = vals[0]
+                continue
+            out.append(n)
+        return out
+
+    def _consumers(self, nodes: List[Node]) -> Dict[str, int]:
+        cnt: Dict[str, int] = {}
+        for n in nodes:
+            for x in n.inputs:
+                if x:
+                    cnt[x] = cnt.get(x, 0) + 1
+        for o in self.outputs:
+            cnt[o.name] = cnt.get(o.name, 0) + 1
+        return cnt
+
+    def _fold_conv_bn(self, nodes: List[Node]) -> List[Node]:
+        cnt = self._consumers(nodes)
+        prod = {o: n for n in nodes for o in n.outputs}
+        drop = set()
+        for n in nodes:
+            if n.op_type != "BatchNormalization" or len(n.outputs) > 1 and any(n.outputs[1:]):
+                continue
+            src = prod.get(n.inputs[0])
+            if src is None or src.op_type != "Conv" or cnt.get(src.outputs[0], 0) != 1:
+                continue
+            if src.inputs[1] not in self._consts or not all(x in self._consts for x in n.inputs[1:5]):
+                continue
+            if len(src.inputs) > 2 and src.inputs[2] and src.inputs[2] not in self._consts:
+                continue
+            w = self._consts[src.inputs[1]].double()
+            gamma, beta, mean, var = (self._consts[x].double() for x in n.inputs[1:5])
+            s = gamma / torch.sqrt(var + n.attrs.get("epsilon", 1e-5))
+            b = self._consts[src.inputs[2]].double() if len(src.inputs) > 2 and src.inputs[2] else torch.zeros_like(mean)
+            wn = (w * s.reshape(-1, *([1] * (w.dim() - 1)))).float()
+            bn = ((b - mean) * s + beta).float()
+            wname, bname = src.inputs[1] + "__bnfold", src.outputs[0] + "__bnfold_bias"
+            self._consts[wname] = wn
+            self._consts[bname] = bn
+            src.inputs = [src.inputs[0], wname, bname]
+            src.outputs = [n.outputs[0]]
+            drop.add(id(n))
+        return [n for n in nodes if id(n) not in drop]
+
+    def _fuse_epilogues(self, nodes: List[Node]) -> List[Node]:
+        cnt = self._consumers(nodes)
+        by_input: Dict[str, List[Node]] = {}
+        for n in nodes:
+            for x in n.inputs:
+                by_input.setdefault(x, []).append(n)
+        drop = set()
+        out_nodes = []
+
+        def sole_consumer(name) -> Optional[Node]:
+            cs = by_input.get(name, [])
+            if len(cs) == 1 and cnt.get(name, 0) == 1 and id(cs[0]) not in drop:
+                return cs[0]
+            return None
+
+        def act_of(n: Node) -> Tuple[int, float]:
+            if n.op_type == "Clip":
+                lo = n.attrs.get("min") if len(n.inputs) < 2 or not n.inputs[1] else _scalar(self._consts.get(n.inputs[1]))
+                hi = n.attrs.get("max") if len(n.inputs) < 3 or not n.inputs[2] else _scalar(self._consts.get(n.inputs[2]))
+                if lo == 0.0 and hi is not None:
+                    return 4, float(hi)
+                return 0, 0.0
+            if n.op_type == "LeakyRelu":
+                return 2, float(n.attrs.get("alpha", 0.01))
+            return _ACTS.get(n.op_type, 0), 0.0
+
+        for n in nodes:
+            if id(n) in drop:
+                continue
+            if n.op_type == "Conv" and n.inputs[1] in self._consts and len(self._consts[n.inputs[1]].shape) == 4:
+                fused = Node("_FusedConv", list(n.inputs[:3]) + [""] * (3 - len(n.inputs[:3])), list(n.outputs),
+                             dict(n.attrs), n.name)
+                cur = n.outputs[0]
+                nxt = sole_consumer(cur)
+                # optional broadcast bias add (mnist style: Conv -> Add(const [C,1,1]))
+                if nxt is not None and nxt.op_type == "Add" and not fused.inputs[2]:
+                    other = nxt.inputs[1] if nxt.inputs[0] == cur else nxt.inputs[0]
+                    c = self._consts.get(other)
+                    cout = self._consts[n.inputs[1]].shape[0]
+                    if isinstance(c, torch.Tensor) and c.numel() == cout and c.dim() >= 1 and \
+                            (c.dim() < 3 or c.shape[-1] == 1):
+                        bname = other + "__as_bias"
+                        self._consts[bname] = c.reshape(-1).float()
+                        fused.inputs[2] = bname
+                        drop.add(id(nxt))
+                        cur = nxt.outputs[0]
+                        nxt = sole_consumer(cur)
+                # residual add of another tensor
+                # (an Add feeding a BatchNormalization is left to the one-pass _AddAffineAct instead)
+                if nxt is not None and nxt.op_type == "Add" and not any(
+                        c.op_type == "BatchNormalization" for c in by_input.get(nxt.outputs[0], [])):
+                    other = nxt.inputs[1] if nxt.inputs[0] == cur else nxt.inputs[0]
+                    if other not in self._consts and other != cur:
+                        fused.inputs.append(other)
+                        drop.add(id(nxt))
+                        cur = nxt.outputs[0]
+                        nxt = sole_consumer(cur)
+                if nxt is not None:
+                    a, alpha = act_of(nxt)
+                    if a:
+                        fused.attrs["__act"] = a
+                        fused.attrs["__alpha"] = alpha
+                        drop.add(id(nxt))
+                        cur = nxt.outputs[0]
+                fused.outputs = [cur]
+                out_nodes.append(fused)
+                continue
+            if n.op_type == "Add" and len(n.inputs) == 2 and all(x not in self._consts for x in n.inputs):
+                bn = None
+                for c in by_input.get(n.outputs[0], []):
+                    if c.op_type == "BatchNormalization" and all(x in self._consts for x in c.inputs[1:5]) and \
+                            (len(c.outputs) == 1 or not any(c.outputs[1:])):
+                        bn = c
+                        break
+                if bn is not None:
+                    nxt = sole_consumer(bn.outputs[0])
+                    a, alpha = act_of(nxt) if nxt is not None else (0, 0.0)
+                    scale, shift = self._bn_affine(bn)
+                    out_name = nxt.outputs[0] if a == 1 else bn.outputs[0]
+                    fn = Node("_AddAffineAct", list(n.inputs) + [scale, shift], [n.outputs[0], out_name],
+                              {"__act": 1 if a == 1 else 0}, n.name)
+                    drop.add(id(bn))
+                    if a == 1:
+                        drop.add(id(nxt))
+                    out_nodes.append(fn)
+                    continue
+            if n.op_type == "BatchNormalization" and all(x in self._consts for x in n.inputs[1:5]) and \
+                    (len(n.outputs) == 1 or not any(n.outputs[1:])):
+                scale, shift = self._bn_affine(n)
+                nxt = sole_consumer(n.outputs[0])
+                a, alpha = act_of(nxt) if nxt is not None else (0, 0.0)
+                outs = [nxt.outputs[0]] if a else [n.outputs[0]]
+                if a:
+                    drop.add(id(nxt))
+                out_nodes.append(Node("_AffineAct", [n.inputs[0], scale, shift], outs, {"__act": a, "__alpha": alpha},
+                                      n.name))
+                continue
+            out_nodes.append(n)
+        return self._reorder([n for n in out_nodes if id(n) not in drop])
+
+    def _reorder(self, nodes: List[Node]) -> List[Node]:
+        """Stable topological re-order (a fused node may read a value produced
+        after the node it replaced, e.g. a ResNet v1 shortcut conv)."""
+        avail = set(self._consts) | {i.name for i in self.inputs} | set(self._outer) | {""}
+        pending, order = list(nodes), []
+        while pending:
+            rest = []
+            for n in pending:
+                if all(x in avail for x in n.inputs):
+                    order.append(n)
+                    avail.update(n.outputs)
+                else:
+                    rest.append(n)
+            if len(rest) == len(pending):
+                order.extend(rest)  # subgraph outer references: keep original order
+                break
+            pending = rest
+        return order
+
+    def _bn_affine(self, bn: Node) -> Tuple[str, str]:
+        gamma, beta, mean, var = (self._consts[x].double() for x in bn.inputs[1:5])
+        s = gamma / torch.sqrt(var + bn.attrs.get("epsilon", 1e-5))
+        sname, tname = bn.outputs[0] + "__scale", bn.outputs[0] + "__shift"
+        self._consts[sname] = s.float()
+        self._consts[tname] = (beta - mean * s).float()
+        return sname, tname
+
+    def _place_constants(self):
+        """Move constants used by device ops to the device (weights in the compute dtype)."""
+        weight_inputs = set()
+        for n in self.nodes:
+            if n.op_type in ("_FusedConv", "Conv", "ConvTranspose", "Gemm", "MatMul"):
+                for x in n.inputs[1:2]:
+                    if x:
+                        weight_inputs.add(x)
+        host_only = set()
+        for n in self.nodes:
+            # shape-like operands stay on the host
+            if n.op_type in ("Reshape", "Expand", "Tile", "Slice", "Squeeze", "Unsqueeze", "ConstantOfShape", "Range",
+                             "TopK", "Pad", "Resize", "Upsample", "Split", "OneHot", "Trilu", "CumSum"):
+                for x in n.inputs[1:]:
+                    host_only.add(x)
+        for k, v in list(self._consts.items()):
+            if not isinstance(v, torch.Tensor) or k in host_only:
+                continue
+            if not self.gpu:
+                if k in weight_inputs and v.is_floating_point():
+                    self._consts[k] = v.to(self.compute_dtype)
+                continue
+            if v.numel() <= 8 and not v.is_floating_point() and k not in weight_inputs:
+                continue  # tiny integer constants (axes, shapes) stay on the host
+            t = v.to(self.device)
+            if k in weight_inputs and t.is_floating_point():
+                t = t.to(self.compute_dtype)
+                if self.channels_last and t.dim() == 4:
+                    t = t.contiguous(memory_format=torch.channels_last)
+            self._consts[k] = t
+
+    def _plan_liveness(self):
+        last: Dict[str, int] = {}
+        for i, n in enumerate(self.nodes):
+            for x in n.inputs:
+                if x:
+                    last[x] = i
+        outs = {o.name for o in self.outputs}
+        self._free_after: List[List[str]] = [[] for _ in self.nodes]
+        for name, i in last.items():
+            if name not in outs and name not in self._consts:
+                self._free_after[i].append(name)
+
+    # ------------------------------------------------------------------ execution
+    def _to_value(self, vi: Optional[ValueInfo], v):
+        if isinstance(v, torch.Tensor):
+            t = v
+        elif isinstance(v, np.ndarray) and (v.dtype == object or v.dtype.kind in "US"):
+            return v.astype(object)
+        else:
+            a = np.asarray(v)
+            if a.dtype == object or a.dtype.kind in "US":
+                return a.astype(object)
+            if vi is not None and vi.kind == "tensor" and vi.elem_type in P.NP_OF and P.NP_OF[vi.elem_type] is not object:
+                a = a.astype(P.NP_OF[vi.elem_type], copy=False)
+            t = torch.from_numpy(a if a.flags.c_contiguous and a.flags.writeable else np.array(a, copy=True))
+        if self.gpu:
+            t = t.to(self.device, non_blocking=True)
+        if t.is_floating_point() and t.dtype != self.compute_dtype:
+            t = t.to(self.compute_dtype)
+        if self.gpu and self.channels_last and t.dim() == 4:
+            t = t.contiguous(memory_format=torch.channels_last)
+        return t
+
+    def run_values(self, feeds: Dict[str, Any], fetch: Optional[Sequence[str]] = None) -> List[Any]:
+        vals: Dict[str, Any] = dict(self._outer)
+        vals.update(self._consts)
+        for vi in self.inputs:
+            if vi.name in feeds:
+                vals[vi.name] = self._to_value(vi, feeds[vi.name])
+        for k, v in feeds.items():
+            if k not in vals:
+                vals[k] = self._to_value(None, v)
+        self._live_values = vals
+        keep = set(fetch) if fetch else ()
+        for i, n in enumerate(self.nodes):
+            fn = OPS.get(n.op_type) or _FUSED.get(n.op_type)
+            if fn is None:
+                raise NotImplementedError(f"ONNX operator {n.domain + '.' if n.domain else ''}{n.op_type} is not "
+                                          f"supported")
+            ins = []
+            for x in n.inputs:
+                if not x:
+                    ins.append(None)
+                    continue
+                if x not in vals:
+                    raise ValueError(f"missing value {x} for node {n.name} ({n.op_type})")
+                ins.append(vals[x])
+            res = fn(_RT(self, n), n.attrs, ins)
+            for name, v in zip(n.outputs, res):
+                if name:
+                    vals[name] = v
+            for name in self._free_after[i]:
+                if name not in keep:
+                    vals.pop(name, None)
+        names = list(fetch) if fetch else [o.name for o in self.outputs]
+        return [vals[nm] for nm in names]
+
+    def run(self, output_names: Optional[Sequence[str]], feeds: Dict[str, Any]) -> List[Any]:
+        """ORT-style ``run``: returns numpy arrays (float outputs as fp32), lists for sequences."""
+        fetch = list(output_names) if output_names else [o.name for o in self.outputs]
+        if self.use_graph and self._graphable(feeds):
+            res = self._run_graph(feeds, fetch)
+        else:
+            res = self.run_values(feeds, fetch)
+        return [_to_host(v) for v in res]
+
+    # ------------------------------------------------------------------ HIP graphs
+    def _graphable(self, feeds) -> bool:
+        if any(vi.kind != "tensor" or vi.elem_type == P.STRING_T for vi in self.inputs + self.outputs):
+            return False
+        return all(not (isinstance(v, np.ndarray) and v.dtype == object) for v in feeds.values())
+
+    def _run_graph(self, feeds, fetch):
+        key = tuple((k, tuple(np.shape(v)), str(getattr(v, "dtype", ""))) for k, v in sorted(feeds.items())) + \
+            tuple(fetch)
+        with self._graph_lock:
+            entry = self._graphs.get(key)
+            if entry is None:
+                entry = self._capture(feeds, fetch)
+                self._graphs[key] = entry
+        if entry == "eager":
+            return self.run_values(feeds, fetch)
+        g, static_in, static_out = entry
+        for k, t in static_in.items():
+            t.copy_(self._to_value(next((vi for vi in self.inputs if vi.name == k), None), feeds[k]),
+                    non_blocking=True)
+        g.replay()
+        return [o.clone() for o in static_out]
+
+    def _capture(self, feeds, fetch):
+        try:
+            static_in = {k: self._to_value(next((vi for vi in self.inputs if vi.name == k), None), v).clone()
+                         for k, v in feeds.items()}
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self.run_values(static_in, fetch)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                static_out = self.run_values(static_in, fetch)
+            if not all(isinstance(o, torch.Tensor) for o in static_out):
+                return "eager"
+            return g, static_in, static_out
+        except Exception:
+            torch.cuda.synchronize(self.device)
+            return "eager"
+
+
+# ---------------------------------------------------------------------- fused ops
+def _dtype_code(t: torch.Tensor) -> int:
+    return {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[t.dtype]
+
+
+def _layout(t: torch.Tensor) -> Optional[int]:
+    """1 = NHWC (channels-last dense), 0 = NCHW dense, None = other."""
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous():
+        return 1
+    if t.is_contiguous():
+        return 0
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return 1
+    return None
+
+
+def _kernel_ok(*ts) -> bool:
+    return all(t is None or (t.is_cuda and t.data_ptr() % 16 == 0 and t.dtype in (torch.float32, torch.float16,
+                                                                               torch.bfloat16)) for t in ts)
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _affine_act_torch(x, scale, shift, res, act, alpha):
+    shp = [1, -1] + [1] * (x.dim() - 2)
+    y = x.float()
+    if scale is not None:
+        y = y * scale.reshape(shp).float()
+    if shift is not None:
+        y = y + shift.reshape(shp).float()
+    if res is not None:
+        y = y + res.float()
+    if act == 1:
+        y = torch.relu(y)
+    elif act == 2:
+        y = torch.nn.functional.leaky_relu(y, alpha)
+    elif act == 3:
+        y = torch.sigmoid(y)
+    elif act == 4:
+        y = torch.clamp(y, 0.0, alpha)
+    return y.to(x.dtype)
+
+
+def _affine_act(rt, x, scale, shift, res, act, alpha, out=None):
+    nn = rt.session._nn
+    if nn is not None and _kernel_ok(x, res) and x.dim() >= 2:
+        lay = _layout(x)
+        if res is not None and (res.shape != x.shape or _layout(res) != lay):
+            res = res.contiguous(memory_format=torch.channels_last) if lay == 1 else res.contiguous()
+        if lay is not None:
+            y = out if out is not None else torch.empty_like(x)
+            C = x.shape[1]
+            HW = int(np.prod(x.shape[2:])) if x.dim() > 2 else 1
+            sc = scale.to(x.device, torch.float32) if scale is not None else None
+            sh = shift.to(x.device, torch.float32) if shift is not None else None
+            nn.affine_act(x.data_ptr(), x.numel(), C, HW, lay, sc.data_ptr() if sc is not None else 0,
+                          sh.data_ptr() if sh is not None else 0, res.data_ptr() if res is not None else 0, act,
+                          float(alpha), _dtype_code(x), y.data_ptr(), _stream(x))
+            return y
+    return _affine_act_torch(x, scale, shift, res, act, alpha)
+
+
+def _fused_conv(rt, at, x):
+    inp, w, b = x[0], x[1], x[2]
+    res = x[3] if len(x) > 3 else None
+    if inp.dtype != w.dtype:
+        inp = inp.to(w.dtype)
+    nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+    inp, pad = _sym_pad(inp, pb, pe)
+    f = {1: torch.nn.functional.conv1d, 2: torch.nn.functional.conv2d, 3: torch.nn.functional.conv3d}[nd]
+    act = at.get("__act", 0)
+    if rt.session._nn is None:
+        # host path: bias inside the conv, epilogue as torch ops
+        y = f(inp, w, b.to(w.dtype) if b is not None else None, stride=strides, padding=pad, dilation=dil,
+              groups=at.get("group", 1))
+        if res is not None or act:
+            y = _affine_act_torch(y, None, None, res.to(y.dtype) if res is not None else None, act,
+                                  at.get("__alpha", 0.0))
+        return [y]
+    y = f(inp, w, None, stride=strides, padding=pad, dilation=dil, groups=at.get("group", 1))
+    if b is None and res is None and not act:
+        return [y]
+    if res is not None and res.dtype != y.dtype:
+        res = res.to(y.dtype)
+    return [_affine_act(rt, y, None, b, res, act, at.get("__alpha", 0.0), out=y)]
+
+
+def _fused_affine_act(rt, at, x):
+    t = x[0]
+    if not t.is_floating_point():
+        t = t.float()
+    return [_affine_act(rt, t, x[1], x[2], None, at.get("__act", 0), at.get("__alpha", 0.0))]
+
+
+def _fused_add_affine_act(rt, at, x):
+    a, b, scale, shift = x
+    a, b = (a, b.to(a.dtype)) if a.dtype == b.dtype or not b.is_floating_point() else (a, b.to(a.dtype))
+    act = at.get("__act", 0)
+    nn = rt.session._nn
+    if nn is not None and a.shape == b.shape and _kernel_ok(a, b):
+        lay = _layout(a)
+        if _layout(b) != lay:
+            b = b.contiguous(memory_format=torch.channels_last) if lay == 1 else b.contiguous()
+        if lay is not None:
+            s = torch.empty_like(a)
+            y = torch.empty_like(a)
+            C = a.shape[1]
+            HW = int(np.prod(a.shape[2:])) if a.dim() > 2 else 1
+            sc = scale.to(a.device, torch.float32)
+            sh = shift.to(a.device, torch.float32)
+            nn.add_affine_act(a.data_ptr(), b.data_ptr(), a.numel(), C, HW, lay, sc.data_ptr(), sh.data_ptr(), act,
+                              _dtype_code(a), s.data_ptr(), y.data_ptr(), _stream(a))
+            return [s, y]
+    s = a + b
+    return [s, _affine_act_torch(s, scale, shift, None, act, 0.0)]
+
+
+_FUSED = {"_FusedConv": _fused_conv, "_AffineAct": _fused_affine_act, "_AddAffineAct": _fused_add_affine_act}
+
+
+def _numel(v) -> int:
+    if isinstance(v, torch.Tensor):
+        return v.numel()
+    return int(np.asarray(v).size)
+
+
+def _scalar(v):
+    if v is None:
+        return None
+    return float(v.reshape(-1)[0]) if isinstance(v, torch.Tensor) else float(np.asarray(v).reshape(-1)[0])
+
+
+def _to_host(v):
+    if isinstance(v, torch.Tensor):
+        t = v.detach()
+        if t.is_floating_point() and t.dtype != torch.float64:
+            t = t.float()
+        if t.dim() == 4 and not t.is_contiguous():
+            t = t.contiguous()
+        return t.cpu().numpy()
+    return v

@@ -1,0 +1,185 @@
+"""Image stage tests (model: reference opencv/src/test/scala/.../ImageTransformerSuite.scala,
+ImageSetAugmenterSuite.scala, core image UnrollImageSuite). OpenCV itself is not available here:
+fixed-point resize / luma values are checked against hand-computed OpenCV arithmetic; GPU
+kernels are checked bit-for-bit against the host path."""
+import numpy as np
+import pytest
+
+from synapseml_amd.core.dataframe import DataFrame
+from synapseml_amd.image import (ImageSetAugmenter, ImageTransformer, UnrollBinaryImage, UnrollImage,
+                                 decode_bytes, encode_png, make_image_row, row_to_array, unroll)
+from synapseml_amd.ops import native
+
+
+def _df(*arrays):
+    col = np.empty(len(arrays), dtype=object)
+    for i, a in enumerate(arrays):
+        col[i] = make_image_row(a, f"img{i}")
+    return DataFrame({"image": col})
+
+
+def test_png_roundtrip_bgr_order():
+    a = np.random.default_rng(0).integers(0, 256, (5, 7, 3), dtype=np.uint8)
+    np.testing.assert_array_equal(decode_bytes(encode_png(a)), a)
+    g = np.random.default_rng(1).integers(0, 256, (5, 7, 1), dtype=np.uint8)
+    np.testing.assert_array_equal(decode_bytes(encode_png(g)), g)
+
+
+def test_resize_dims_and_fixed_point():
+    a = np.random.default_rng(0).integers(0, 256, (40, 60, 3), dtype=np.uint8)
+    out = ImageTransformer(outputCol="o").resize(15, 10).transform(_df(a))["o"][0]
+    assert (out["height"], out["width"]) == (15, 10)
+    img = native.load("_image")
+    src = np.array([[0, 100], [200, 50]], dtype=np.uint8)[:, :, None]
+    assert img.resize(src, 1, 1).reshape(-1)[0] == 88  # (0+100+200+50)/4 = 87.5 rounds up in 22-bit fixed point
+    const = np.full((9, 13, 3), 77, np.uint8)
+    assert (img.resize(const, 20, 7) == 77).all()
+    # keep aspect ratio: shorter side -> size
+    out = ImageTransformer(outputCol="o").resize(20, True).transform(_df(a))["o"][0]
+    assert (out["height"], out["width"]) == (20, 30)
+
+
+def test_tensor_normalization_red_image():
+    red = np.zeros((8, 8, 3), np.uint8)
+    red[:, :, 2] = 255
+    t = ImageTransformer(outputCol="t").normalize([0.5, 0.5, 0.5], [1.0, 1.0, 1.0], 1 / 255).setDeviceType("cpu")
+    v = t.transform(_df(red))["t"][0]
+    assert v.shape == (3, 8, 8)
+    assert np.allclose(v[0], 0.5) and np.allclose(v[1], -0.5) and np.allclose(v[2], -0.5)
+    bgr = t.copy().setTensorChannelOrder("BGR").transform(_df(red))["t"][0]
+    assert np.allclose(bgr[2], 0.5)
+    dbl = t.copy().setTensorElementType("double").transform(_df(red))["t"][0]
+    assert dbl.dtype == np.float64
+
+
+def test_color_threshold_flip_blur_gaussian():
+    img = native.load("_image")
+    px = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255]]], np.uint8)  # BGR blue, green, red
+    gray = img.cvt_color(px, 6).reshape(-1)
+    assert gray.tolist() == [29, 150, 76]
+    x = np.array([[10, 100, 200]], np.uint8)[:, :, None]
+    assert img.threshold(x, 100, 255, 0).reshape(-1).tolist() == [0, 0, 255]
+    assert img.threshold(x, 100, 255, 1).reshape(-1).tolist() == [255, 255, 0]
+    assert img.threshold(x, 100, 255, 2).reshape(-1).tolist() == [10, 100, 100]
+    assert img.threshold(x, 100, 255, 3).reshape(-1).tolist() == [0, 0, 200]
+    assert img.threshold(x, 100, 255, 4).reshape(-1).tolist() == [10, 100, 0]
+    a = np.random.default_rng(2).integers(0, 256, (11, 9, 3), dtype=np.uint8)
+    df = _df(a)
+    f = ImageTransformer(outputCol="o").flip(1).transform(df)["o"][0]
+    np.testing.assert_array_equal(row_to_array(f), a[:, ::-1])
+    const = np.full((6, 6, 1), 40, np.uint8)
+    assert (img.box_blur(const, 3, 5) == 40).all()
+    # box blur interior = mean of the window
+    b = img.box_blur(a, 3, 3)
+    assert b[5, 4, 1] == int(np.floor(a[4:7, 3:6, 1].mean() + 0.5)) or \
+        abs(int(b[5, 4, 1]) - a[4:7, 3:6, 1].mean()) <= 0.5
+    k = np.asarray(img.gaussian_kernel(5, 0.0))
+    np.testing.assert_allclose(k, [0.0625, 0.25, 0.375, 0.25, 0.0625])
+    k2 = np.asarray(img.gaussian_kernel(7, 1.5))
+    assert abs(k2.sum() - 1) < 1e-12 and k2[3] == k2.max()
+    gauss = ImageTransformer(outputCol="o").gaussianKernel(5, 0).transform(df)["o"][0]
+    g = row_to_array(gauss).astype(int)
+    ref = sum(kk * a[min(max(3 + j - 2, 0), 10), 4, 0].astype(float) for j, kk in enumerate(k))
+    assert abs(g[3, 4, 0] - ref) <= 0.5 + 1e-9
+
+
+def test_center_crop_and_stage_chain():
+    a = np.random.default_rng(3).integers(0, 256, (30, 40, 3), dtype=np.uint8)
+    out = ImageTransformer(outputCol="o").centerCrop(10, 20).transform(_df(a))["o"][0]
+    np.testing.assert_array_equal(row_to_array(out), a[10:20, 10:30])
+    out = (ImageTransformer(outputCol="o").resize(30, 40).crop(1, 2, 5, 6).colorFormat(6)
+           .transform(_df(a))["o"][0])
+    assert (out["height"], out["width"], out["nChannels"]) == (5, 6, 1)
+
+
+def test_decoding_errors_and_binary_input():
+    good = encode_png(np.zeros((4, 4, 3), np.uint8))
+    col = np.empty(2, dtype=object)
+    col[0] = good
+    col[1] = b"not an image"
+    df = DataFrame({"image": col})
+    with pytest.raises(Exception):
+        ImageTransformer(outputCol="o").resize(2, 2).transform(df)
+    out = ImageTransformer(outputCol="o").resize(2, 2).setIgnoreDecodingErrors(True).transform(df)
+    assert out["o"][0]["height"] == 2 and out["o"][1] is None
+
+
+def test_augmenter_and_unroll():
+    a = np.random.default_rng(4).integers(1, 256, (3, 4, 3), dtype=np.uint8)
+    df = _df(a)
+    aug = ImageSetAugmenter(outputCol="o", flipUpDown=True).transform(df)
+    assert aug.count() == 3
+    np.testing.assert_array_equal(row_to_array(aug["o"][1]), a[:, ::-1])
+    np.testing.assert_array_equal(row_to_array(aug["o"][2]), a[::-1])
+    u = UnrollImage(outputCol="u").transform(df)["u"][0].toArray()
+    np.testing.assert_array_equal(u, a.transpose(2, 0, 1).reshape(-1).astype(float))
+    z = np.zeros((1, 1, 3), np.uint8)
+    assert unroll(make_image_row(z)).tolist() == [256.0, 256.0, 256.0]  # reference quirk
+    b = DataFrame({"image": np.array([encode_png(a)], dtype=object)})
+    v = UnrollBinaryImage(outputCol="v", width=2, height=2).transform(b)["v"][0]
+    assert len(v.toArray()) == 12
+
+
+@pytest.mark.gpu
+def test_gpu_fused_preprocess_bit_exact():
+    import torch
+
+    rng = np.random.default_rng(5)
+    arrays = [rng.integers(0, 256, (h, w, c), dtype=np.uint8)
+              for h, w, c in [(37, 53, 3), (224, 224, 3), (300, 120, 3), (64, 64, 3)]]
+    t = (ImageTransformer(outputCol="o").resize(height=96, width=80).centerCrop(64, 64)
+         .normalize([0.485, 0.456, 0.406], [0.229, 0.224, 0.225], 1 / 255))
+    dev = t.device_tensors(arrays)
+    assert dev is not None and dev.is_cuda and dev.shape == (4, 3, 64, 64)
+    host = np.stack([t.process_host(a) for a in arrays])
+    np.testing.assert_array_equal(dev.cpu().numpy(), host)
+    nhwc = t.device_tensors(arrays, nhwc=True)
+    np.testing.assert_array_equal(nhwc.contiguous().cpu().numpy(), host)
+    half = t.device_tensors(arrays, dtype="float16")
+    np.testing.assert_allclose(half.float().cpu().numpy(), host, atol=2e-3, rtol=1e-3)
+    gray = [rng.integers(0, 256, (50, 40, 1), dtype=np.uint8) for _ in range(3)]
+    tg = (ImageTransformer(outputCol="o").setAutoConvertToColor(True).resize(height=32, width=32)
+          .normalize([0.5] * 3, [0.25] * 3, 1 / 255))
+    np.testing.assert_array_equal(tg.device_tensors(gray).cpu().numpy(), np.stack([tg.process_host(a) for a in gray]))
+    # end-to-end transform on the GPU path equals the CPU path
+    col = np.empty(len(arrays), dtype=object)
+    for i, a in enumerate(arrays):
+        col[i] = make_image_row(a)
+    df = DataFrame({"image": col})
+    g = t.copy().setDeviceType("gpu").transform(df)["o"]
+    c = t.copy().setDeviceType("cpu").transform(df)["o"]
+    for x, y in zip(g, c):
+        np.testing.assert_array_equal(x, y)
+    del torch
+
+
+@pytest.mark.gpu
+def test_gpu_stage_kernels_match_host():
+    import torch
+
+    img = native.load("_image")
+    rng = np.random.default_rng(6)
+    B, h, w, c = 3, 31, 45, 3
+    a = rng.integers(0, 256, (B, h, w, c), dtype=np.uint8)
+    src = torch.from_numpy(a).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    out = torch.empty((B, 20, 17, c), dtype=torch.uint8, device="cuda")
+    img.resize_batch_device(src.data_ptr(), B, h, w, c, out.data_ptr(), 20, 17, stream)
+    ref = np.stack([img.resize(x, 20, 17) for x in a])
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    bl = torch.empty_like(src)
+    img.box_blur_batch_device(src.data_ptr(), B, h, w, c, bl.data_ptr(), 3, 5, stream)
+    np.testing.assert_array_equal(bl.cpu().numpy(), np.stack([img.box_blur(x, 3, 5) for x in a]))
+    k = img.gaussian_kernel(7, 1.3)
+    gs = torch.empty_like(src)
+    img.column_filter_batch_device(src.data_ptr(), B, h, w, c, gs.data_ptr(), k, stream)
+    np.testing.assert_array_equal(gs.cpu().numpy(), np.stack([img.column_filter(x, k) for x in a]))
+    th = torch.empty_like(src)
+    img.threshold_device(src.data_ptr(), src.numel(), th.data_ptr(), 120.5, 200, 2, stream)
+    np.testing.assert_array_equal(th.cpu().numpy(), img.threshold(a.reshape(-1, w, c), 120.5, 200, 2).reshape(a.shape))
+    fl = torch.empty_like(src)
+    img.flip_batch_device(src.data_ptr(), B, h, w, c, fl.data_ptr(), -1, stream)
+    np.testing.assert_array_equal(fl.cpu().numpy(), a[:, ::-1, ::-1])
+    gr = torch.empty((B, h, w, 1), dtype=torch.uint8, device="cuda")
+    img.cvt_color_device(src.data_ptr(), B * h * w, 3, 6, gr.data_ptr(), stream)
+    np.testing.assert_array_equal(gr.cpu().numpy().reshape(-1), img.cvt_color(a.reshape(-1, w, c), 6).reshape(-1))

@@ -1,0 +1,365 @@
+"""ONNX executor + ONNXModel tests (model: reference deep-learning/src/test/
+scala/.../onnx/ONNXModelSuite.scala). The reference downloads its models;
+here every model is produced by our own writer with the same topology/names
+(random weights), so numerical parity is pinned against an unoptimised
+reference execution of the same graph and against plain numpy/torch math."""
+import numpy as np
+import pytest
+import torch
+
+from synapseml_amd.core.dataframe import DataFrame
+from synapseml_amd.core.linalg import DenseVector
+from synapseml_amd.onnx import Graph, InferenceSession, ONNXModel, proto as P, writer
+from synapseml_amd.onnx.writer import GraphBuilder
+
+
+# ------------------------------------------------------------------ codec
+def test_proto_roundtrip():
+    b = GraphBuilder("g")
+    b.input("x", P.FLOAT32, ["N", 3])
+    w = b.init("w", np.arange(6, dtype=np.float32).reshape(3, 2))
+    b.add("MatMul", ["x", w], out="y")
+    b.add("Softmax", ["y"], {"axis": -1}, out="z")
+    b.output("z", P.FLOAT32, ["N", 2])
+    data = b.to_bytes()
+    m = P.load_model(data)
+    assert m.graph.node[0].op_type == "MatMul"
+    assert m.graph.node[1].attribute[0].i == -1
+    g = Graph.from_bytes(data)
+    assert g.inputs[0].shape == ["N", 3]
+    np.testing.assert_array_equal(g.initializers["w"], np.arange(6, dtype=np.float32).reshape(3, 2))
+    # re-encode the decoded graph
+    g2 = Graph.from_bytes(g.to_bytes())
+    assert [n.op_type for n in g2.nodes] == ["MatMul", "Softmax"]
+    assert P.encode(P.decode("TensorProto", P.encode(P.numpy_to_tensor(np.array([1, -2], np.int64))))) == \
+        P.encode(P.numpy_to_tensor(np.array([1, -2], np.int64)))
+
+
+def test_tensor_formats():
+    t = P.Message("TensorProto", dims=[2], data_type=P.FLOAT32, float_data=[1.5, -2.0])
+    np.testing.assert_array_equal(P.tensor_to_numpy(P.decode("TensorProto", P.encode(t))), [1.5, -2.0])
+    t = P.Message("TensorProto", dims=[3], data_type=P.INT64, int64_data=[1, -5, 7])
+    np.testing.assert_array_equal(P.tensor_to_numpy(P.decode("TensorProto", P.encode(t))), [1, -5, 7])
+    s = P.numpy_to_tensor(np.array(["a", "bc"], dtype=object))
+    assert P.tensor_to_numpy(P.decode("TensorProto", P.encode(s))).tolist() == ["a", "bc"]
+
+
+# ------------------------------------------------------------------ executor numerics
+def _conv_ref(x, w, b, stride, pad):
+    return torch.nn.functional.conv2d(torch.from_numpy(x), torch.from_numpy(w),
+                                      None if b is None else torch.from_numpy(b), stride=stride, padding=pad).numpy()
+
+
+def test_conv_bn_relu_fusion_matches_unfused():
+    rng = np.random.default_rng(0)
+    b = GraphBuilder("cbr")
+    b.input("x", P.FLOAT32, ["N", 4, 9, 9])
+    w = b.init("w", rng.standard_normal((8, 4, 3, 3)).astype(np.float32))
+    y = b.add("Conv", ["x", w], {"kernel_shape": [3, 3], "pads": [1, 1, 1, 1], "strides": [2, 2]})
+    g = b.init("g", rng.random(8).astype(np.float32) + 0.5)
+    be = b.init("be", rng.standard_normal(8).astype(np.float32))
+    m = b.init("m", rng.standard_normal(8).astype(np.float32))
+    v = b.init("v", rng.random(8).astype(np.float32) + 0.5)
+    y = b.add("BatchNormalization", [y, g, be, m, v], {"epsilon": 1e-5})
+    y = b.add("Relu", [y], out="out")
+    b.output("out", P.FLOAT32, None)
+    data = b.to_bytes()
+    x = rng.standard_normal((2, 4, 9, 9)).astype(np.float32)
+    s_opt = InferenceSession(data, device="cpu")
+    assert [n.op_type for n in s_opt.nodes] == ["_FusedConv"]
+    o1 = s_opt.run(None, {"x": x})[0]
+    o0 = InferenceSession(data, device="cpu", optimization_level="NO_OPT").run(None, {"x": x})[0]
+    np.testing.assert_allclose(o1, o0, rtol=1e-4, atol=1e-4)
+    # independent numpy/torch reference
+    ref = _conv_ref(x, b.inits["w"], None, 2, 1)
+    sc = b.inits["g"] / np.sqrt(b.inits["v"] + 1e-5)
+    ref = np.maximum(0, (ref - b.inits["m"][None, :, None, None]) * sc[None, :, None, None] +
+                     b.inits["be"][None, :, None, None])
+    np.testing.assert_allclose(o0, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_preact_add_bn_relu_pattern():
+    rng = np.random.default_rng(1)
+    b = GraphBuilder("preact")
+    b.input("a", P.FLOAT32, ["N", 8, 4, 4])
+    b.input("c", P.FLOAT32, ["N", 8, 4, 4])
+    s = b.add("Add", ["a", "c"], out="sum")
+    params = [b.init(n, (rng.random(8) + 0.5).astype(np.float32)) for n in ("g", "be", "m", "v")]
+    y = b.add("BatchNormalization", [s] + params)
+    b.add("Relu", [y], out="act")
+    b.output("sum", P.FLOAT32, None)
+    b.output("act", P.FLOAT32, None)
+    data = b.to_bytes()
+    sess = InferenceSession(data, device="cpu")
+    assert [n.op_type for n in sess.nodes] == ["_AddAffineAct"]
+    a = rng.standard_normal((2, 8, 4, 4)).astype(np.float32)
+    c = rng.standard_normal((2, 8, 4, 4)).astype(np.float32)
+    o_sum, o_act = sess.run(None, {"a": a, "c": c})
+    r_sum, r_act = InferenceSession(data, device="cpu", optimization_level="NO_OPT").run(None, {"a": a, "c": c})
+    np.testing.assert_allclose(o_sum, a + c, rtol=1e-6)
+    np.testing.assert_allclose(o_act, r_act, rtol=1e-5, atol=1e-5)
+
+
+def test_mnist_and_resnet_slices():
+    m = writer.mnist_cnn()
+    s = InferenceSession(m, device="cpu")
+    x = np.random.default_rng(0).random((1, 1, 28, 28), dtype=np.float32)
+    np.testing.assert_allclose(s.run(None, {"Input3": x})[0],
+                               InferenceSession(m, device="cpu", optimization_level="NO_OPT").run(None, {"Input3": x})[0],
+                               rtol=1e-4, atol=1e-4)
+    r = writer.resnet50_v2(seed=1)
+    g = Graph.from_bytes(r).slice_at(["resnetv24_pool1_fwd"])
+    sess = InferenceSession.from_graph(g, device="cpu")
+    xb = np.random.default_rng(2).random((1, 3, 224, 224), dtype=np.float32)
+    feat = sess.run(None, {"data": xb})[0]
+    assert feat.shape == (1, 2048, 1, 1)
+    full = InferenceSession(r, device="cpu", optimization_level="NO_OPT")
+    ref = full.run_values({"data": xb}, ["resnetv24_pool1_fwd"])[0].numpy()
+    np.testing.assert_allclose(feat, ref, rtol=2e-3, atol=2e-3 * np.abs(ref).max())
+
+
+def test_op_coverage_misc():
+    b = GraphBuilder("misc")
+    b.input("x", P.FLOAT32, ["N", 6])
+    shp = b.add("Shape", ["x"])
+    n = b.add("Gather", [shp, b.init("i0", np.array(0, np.int64))], {"axis": 0})
+    n1 = b.add("Unsqueeze", [n, b.init("ax", np.array([0], np.int64))])
+    tgt = b.add("Concat", [n1, b.init("c", np.array([2, 3], np.int64))], {"axis": 0})
+    r = b.add("Reshape", ["x", tgt])
+    t = b.add("Transpose", [r], {"perm": [0, 2, 1]})
+    red = b.add("ReduceMean", [t], {"axes": [1], "keepdims": 0})
+    sm = b.add("Softmax", [red], {"axis": -1})
+    cl = b.add("Clip", [sm, b.init("lo", np.array(0.1, np.float32)), b.init("hi", np.array(0.9, np.float32))])
+    w = b.add("Where", [b.add("Greater", [cl, b.init("h", np.array(0.5, np.float32))]), cl,
+                        b.init("z", np.array(0.0, np.float32))], out="y")
+    am = b.add("ArgMax", [red], {"axis": 1, "keepdims": 0}, out="am")
+    sl = b.add("Slice", ["x", b.init("s0", np.array([1], np.int64)), b.init("e0", np.array([5], np.int64)),
+                          b.init("a0", np.array([1], np.int64)), b.init("st", np.array([2], np.int64))], out="sl")
+    b.output("y", P.FLOAT32, None)
+    b.output("am", P.INT64, None)
+    b.output("sl", P.FLOAT32, None)
+    x = np.arange(12, dtype=np.float32).reshape(2, 6) / 10
+    y, am, sl = InferenceSession(b.to_bytes(), device="cpu").run(None, {"x": x})
+    ref_red = x.reshape(2, 2, 3).transpose(0, 2, 1).mean(1)
+    e = np.exp(ref_red - ref_red.max(1, keepdims=True))
+    ref_sm = np.clip(e / e.sum(1, keepdims=True), 0.1, 0.9)
+    np.testing.assert_allclose(y, np.where(ref_sm > 0.5, ref_sm, 0), rtol=1e-5)
+    np.testing.assert_array_equal(am, ref_red.argmax(1))
+    np.testing.assert_array_equal(sl, x[:, 1:5:2])
+
+
+# ------------------------------------------------------------------ ONNXModel stage
+def _iris_model():
+    coef = np.array([[-0.4, 0.8, -2.2, -0.9], [0.5, -0.3, -0.2, -0.9], [-0.1, -0.5, 2.4, 1.8]], np.float32)
+    inter = np.array([9.0, 2.0, -11.0], np.float32)
+    return writer.linear_classifier_zipmap(coef, inter, [0, 1, 2]), coef, inter
+
+
+def test_onnx_model_iris_zipmap_and_argmax():
+    data, coef, inter = _iris_model()
+    feats = np.array([[6.7, 3.1, 4.7, 1.5], [4.9, 3.0, 1.4, 0.2], [5.8, 2.7, 5.1, 1.9]], np.float32)
+    col = np.empty(3, dtype=object)
+    for i in range(3):
+        col[i] = feats[i].tolist()
+    df = DataFrame({"features": col})
+    m = (ONNXModel().setModelPayload(data).setFeedDict({"float_input": "features"})
+         .setFetchDict({"prediction": "output_label", "rawProbability": "output_probability"})
+         .setArgMaxDict({"rawProbability": "argmax"}).setSoftMaxDict({"rawProbability": "sm"}).setDeviceType("CPU"))
+    out = m.transform(df)
+    s = feats @ coef.T + inter
+    p = np.exp(s - s.max(1, keepdims=True))
+    p /= p.sum(1, keepdims=True)
+    assert out["prediction"].tolist() == s.argmax(1).tolist()
+    for i in range(3):
+        d = out["rawProbability"][i]
+        assert set(d) == {0, 1, 2}
+        np.testing.assert_allclose([d[k] for k in range(3)], p[i], rtol=1e-5)
+    assert out["argmax"].tolist() == s.argmax(1).astype(float).tolist()
+    assert isinstance(out["sm"][0], DenseVector)
+    # vector and double inputs coerce to the model's float input
+    dv = DataFrame({"features": np.array([DenseVector(r.astype(np.float64)) for r in feats], dtype=object)})
+    assert m.transform(dv)["prediction"].tolist() == s.argmax(1).tolist()
+    assert m.transform(DataFrame({"features": feats.astype(np.float64)}))["prediction"].tolist() == \
+        s.argmax(1).tolist()
+
+
+def test_onnx_model_shape_errors():
+    data, _, _ = _iris_model()
+    m = (ONNXModel().setModelPayload(data).setFeedDict({"float_input": "features"})
+         .setFetchDict({"prediction": "output_label"}).setDeviceType("CPU"))
+    bad = np.empty(1, dtype=object)
+    bad[0] = [6.7, 3.1, 4.7]
+    with pytest.raises(ValueError, match="IllegalArgumentException"):
+        m.transform(DataFrame({"features": bad}))
+    bad2 = np.empty(2, dtype=object)
+    bad2[0] = [6.7, 3.1, 4.7, 1.5]
+    bad2[1] = [6.7, 3.1, 4.7]
+    with pytest.raises(ValueError, match="IllegalArgumentException"):
+        m.transform(DataFrame({"features": bad2}))
+    empty = np.empty(1, dtype=object)
+    empty[0] = []
+    with pytest.raises(ValueError, match="IllegalArgumentException"):
+        m.transform(DataFrame({"features": empty}))
+    with pytest.raises(ValueError):
+        m.setFetchDict({"features": "output_label"}).transform(DataFrame({"features": np.ones((1, 4))}))
+
+
+def test_onnx_model_boolean_and_variable_length_text():
+    m = (ONNXModel().setModelPayload(writer.boolean_and()).setFeedDict({"A": "i1", "B": "i2"})
+         .setFetchDict({"Output": "Y"}).setMiniBatchSize(5).setDeviceType("CPU"))
+    out = m.transform(DataFrame({"i1": [True, True, False], "i2": [True, False, False]}))
+    assert out["Output"].tolist() == [True, False, False]
+    t = ONNXModel().setModelPayload(writer.tfidf_counts()).setFeedDict({"text": "features"}) \
+        .setFetchDict({"encoded": "result"}).setDeviceType("CPU")
+    one = np.empty(1, dtype=object)
+    one[0] = ["A", "B", "C"]
+    r = t.setMiniBatchSize(10).transform(DataFrame({"features": one}))
+    assert np.asarray(r["encoded"][0]).tolist() == [1.0, 1.0, 1.0]
+    two = np.empty(2, dtype=object)
+    two[0] = ["A", "B", "B", "C", "A"]
+    two[1] = ["A", "B", "C"]
+    r = t.setMiniBatchSize(1).transform(DataFrame({"features": two}))
+    assert np.asarray(r["encoded"][0]).tolist() == [2.0, 2.0, 1.0]
+    assert np.asarray(r["encoded"][1]).tolist() == [1.0, 1.0, 1.0]
+    with pytest.raises(ValueError):
+        t.setMiniBatchSize(10).transform(DataFrame({"features": two}))
+
+
+def test_onnx_model_slicing_auto_and_manual():
+    data = writer.resnet50_v2(seed=3)
+    rng = np.random.default_rng(0)
+    imgs = np.empty(2, dtype=object)
+    for i in range(2):
+        imgs[i] = rng.random((3, 224, 224), dtype=np.float32)
+    df = DataFrame({"image": imgs})
+    m = ONNXModel().setModelPayload(data).setFeedDict({"data": "image"}).setDeviceType("CPU")
+    auto = m.copy().setFetchDict({"rawFeatures": "resnetv24_pool1_fwd"})
+    assert "resnetv24_pool1_fwd" not in auto.modelOutput
+    f = auto.transform(df)["rawFeatures"][0]
+    assert np.asarray(f).shape == (2048, 1, 1)
+    sliced = m.sliceAtOutput("resnetv24_pool1_fwd").setFetchDict({"rawFeatures": "resnetv24_pool1_fwd"})
+    assert "resnetv24_pool1_fwd" in sliced.modelOutput
+    np.testing.assert_allclose(np.asarray(sliced.transform(df)["rawFeatures"][1]),
+                               np.asarray(auto.transform(df)["rawFeatures"][1]), rtol=1e-5)
+
+
+def test_tree_ensemble_classifier():
+    # two stumps: x0 <= 0.5 -> class weight
+    b = GraphBuilder("trees")
+    b.input("X", P.FLOAT32, [None, 2])
+    b.add("TreeEnsembleClassifier", ["X"], {
+        "nodes_treeids": [0, 0, 0, 1, 1, 1], "nodes_nodeids": [0, 1, 2, 0, 1, 2],
+        "nodes_featureids": [0, 0, 0, 1, 0, 0], "nodes_values": [0.5, 0, 0, 1.0, 0, 0],
+        "nodes_modes": ["BRANCH_LEQ", "LEAF", "LEAF", "BRANCH_LEQ", "LEAF", "LEAF"],
+        "nodes_truenodeids": [1, 0, 0, 1, 0, 0], "nodes_falsenodeids": [2, 0, 0, 2, 0, 0],
+        "class_treeids": [0, 0, 1, 1], "class_nodeids": [1, 2, 1, 2], "class_ids": [0, 0, 0, 0],
+        "class_weights": [-1.0, 1.0, -0.5, 0.5], "classlabels_int64s": [0, 1], "post_transform": "LOGISTIC"},
+        n_out=2, domain="ai.onnx.ml", out="te")
+    b.nodes[-1].outputs = ["label", "probs"]
+    b.output("label", P.INT64, [None])
+    b.output("probs", P.FLOAT32, [None, 2])
+    X = np.array([[0.0, 0.0], [1.0, 2.0], [0.0, 2.0]], np.float32)
+    lab, pr = InferenceSession(b.to_bytes({"": 13, "ai.onnx.ml": 1}), device="cpu").run(None, {"X": X})
+    s = np.array([-1.5, 1.5, -0.5])
+    np.testing.assert_allclose(pr[:, 1], 1 / (1 + np.exp(-s)), rtol=1e-6)
+    assert lab.tolist() == [0, 1, 0]
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_gpu_resnet_matches_cpu_and_graph_replay():
+    data = writer.resnet50_v2(seed=4)
+    x = np.random.default_rng(5).random((4, 3, 224, 224), dtype=np.float32)
+    cpu = InferenceSession(data, device="cpu").run(None, {"data": x})[0]
+    gpu = InferenceSession(data, device="cuda", use_graph=True)
+    o1 = gpu.run(None, {"data": x})[0]
+    o2 = gpu.run(None, {"data": x})[0]  # HIP graph replay path
+    scale = np.abs(cpu).max()
+    np.testing.assert_allclose(o1, cpu, rtol=0, atol=2e-3 * scale)
+    np.testing.assert_array_equal(o1, o2)
+    assert any(v != "eager" for v in gpu._graphs.values()), "HIP graph capture fell back to eager"
+    half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
+    assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
+
+
+@pytest.mark.gpu
+def test_gpu_epilogue_kernels_match_torch():
+    from synapseml_amd.ops import native
+
+    nn = native.load("_nn")
+    dev = torch.device("cuda")
+    for dtype in (torch.float32, torch.float16, torch.bfloat16):
+        x = torch.randn(2, 64, 7, 7, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+        r = torch.randn_like(x)
+        sc = torch.rand(64, device=dev) + 0.5
+        sh = torch.randn(64, device=dev)
+        y = torch.empty_like(x)
+        nn.affine_act(x.data_ptr(), x.numel(), 64, 49, 1, sc.data_ptr(), sh.data_ptr(), r.data_ptr(), 1, 0.0,
+                      {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[dtype], y.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+        ref = torch.relu(x.float() * sc[None, :, None, None] + sh[None, :, None, None] + r.float())
+        tol = 1e-5 if dtype == torch.float32 else 2e-2
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+        s = torch.empty_like(x)
+        a = torch.empty_like(x)
+        nn.add_affine_act(x.data_ptr(), r.data_ptr(), x.numel(), 64, 49, 1, sc.data_ptr(), sh.data_ptr(), 1,
+                          {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[dtype], s.data_ptr(), a.data_ptr(),
+                          torch.cuda.current_stream().cuda_stream)
+        torch.testing.assert_close(s.float(), (x + r).float(), rtol=tol, atol=tol)
+        ref2 = torch.relu((x + r).float() * sc[None, :, None, None] + sh[None, :, None, None])
+        torch.testing.assert_close(a.float(), ref2, rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.gpu
+def test_gpu_onnx_model_stage():
+    data, coef, inter = _iris_model()
+    feats = np.random.default_rng(0).random((37, 4)).astype(np.float32) * 5
+    m = (ONNXModel().setModelPayload(data).setFeedDict({"float_input": "features"})
+         .setFetchDict({"prediction": "output_label"}).setDeviceType("GPU"))
+    out = m.transform(DataFrame({"features": feats}))
+    assert out["prediction"].tolist() == (feats @ coef.T + inter).argmax(1).tolist()
+
+
+# ------------------------------------------------------------------ ImageFeaturizer
+def _image_df(n=3, seed=0):
+    from synapseml_amd.image import encode_png, make_image_row
+
+    rng = np.random.default_rng(seed)
+    col = np.empty(n, dtype=object)
+    for i in range(n):
+        a = rng.integers(0, 256, (60 + 7 * i, 80, 3), dtype=np.uint8)
+        col[i] = make_image_row(a) if i % 2 == 0 else encode_png(a)
+    return DataFrame({"image": col})
+
+
+def test_image_featurizer_headless_cpu():
+    from synapseml_amd.onnx import ImageFeaturizer
+
+    data = writer.resnet50_v2(seed=7)
+    f = (ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
+                         outputTensorName="resnetv24_dense0_fwd", imageTensorName="data")
+         .setModel(data))
+    f.getOnnxModel().setDeviceType("CPU")
+    df = _image_df()
+    out = f.transform(df)
+    v = out["features"][0]
+    assert isinstance(v, DenseVector) and len(v.toArray()) == 2048
+    head = f.copy().setHeadless(False).transform(df)["features"][1]
+    assert len(head.toArray()) == 1000
+
+
+@pytest.mark.gpu
+def test_image_featurizer_gpu_matches_cpu():
+    from synapseml_amd.onnx import ImageFeaturizer
+
+    data = writer.resnet50_v2(seed=8)
+    df = _image_df(n=5, seed=1)
+
+    def run(dev):
+        f = ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
+                            imageTensorName="data").setModel(data)
+        f.getOnnxModel().setDeviceType(dev)
+        return np.stack([v.toArray() for v in f.transform(df)["features"]])
+
+    g, c = run("GPU"), run("CPU")
+    np.testing.assert_allclose(g, c, rtol=0, atol=2e-3 * np.abs(c).max())

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""ResNet-50 (ONNX model-zoo v2 topology, random-init weights) inference
+throughput on one GPU: (1) session only, device-resident input, per precision
+and batch; (2) ImageFeaturizer end to end (host decode of uint8 images, fused
+resize/crop/normalize kernel, featurization) — BASELINE.json config
+"ONNXModel ResNet-50, synthetic 224x224 images"."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", default="32,128")
+    ap.add_argument("--precisions", default="fp32,fp16,bf16")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--images", type=int, default=512)
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from synapseml_amd.core.dataframe import DataFrame
+    from synapseml_amd.image import make_image_row
+    from synapseml_amd.onnx import ImageFeaturizer, InferenceSession, writer
+
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    model = writer.resnet50_v2(seed=0)
+    for prec in a.precisions.split(","):
+        sess = InferenceSession(model, device=dev, precision=prec, use_graph=not a.no_graph)
+        for bs in [int(b) for b in a.batches.split(",")]:
+            x = torch.rand(bs, 3, 224, 224, device=dev)
+            for _ in range(3):
+                sess.run(None, {"data": x})
+            if dev == "cuda":
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                if a.no_graph or dev == "cpu":
+                    out = sess.run_values({"data": x})
+                else:
+                    out = sess._run_graph({"data": x}, [o.name for o in sess.outputs])
+            if dev == "cuda":
+                torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / a.iters
+            print(json.dumps({"bench": "resnet50_session", "precision": prec, "batch": bs, "ms_per_batch": dt * 1e3,
+                              "images_per_s": bs / dt, "hip_graph": not a.no_graph and dev == "cuda"}), flush=True)
+    # end to end featurizer (decode from image rows, fused preprocess, headless features)
+    rng = np.random.default_rng(0)
+    col = np.empty(a.images, dtype=object)
+    for i in range(a.images):
+        col[i] = make_image_row(rng.integers(0, 256, (256, 256, 3), dtype=np.uint8))
+    df = DataFrame({"image": col})
+    for prec in ("fp32", "fp16"):
+        f = ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
+                            imageTensorName="data").setModel(model)
+        f.getOnnxModel().setPrecision(prec).setMiniBatchSize(128)
+        f.transform(df.limit(128))  # warm-up / graph capture
+        if dev == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = f.transform(df)
+        dt = time.perf_counter() - t0
+        assert out.count() == a.images
+        print(json.dumps({"bench": "image_featurizer_e2e", "precision": prec, "images": a.images,
+                          "images_per_s": a.images / dt, "s": dt}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

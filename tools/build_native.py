@@ -61,6 +61,11 @@ MODULES = {
         ["image_bindings.cpp", "image_ops.cpp", "image_gpu.hip"],
         [],
     ),
+    "_nn": (
+        "csrc/nn",
+        ["nn_bindings.cpp", "nn_ops.hip"],
+        [],
+    ),
 }
 
 CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-Wno-sign-compare"]
