@@ -276,7 +276,8 @@ def test_gpu_resnet_matches_cpu_and_graph_replay():
     o2 = gpu.run(None, {"data": x})[0]  # HIP graph replay path
     scale = np.abs(cpu).max()
     np.testing.assert_allclose(o1, cpu, rtol=0, atol=2e-3 * scale)
-    np.testing.assert_array_equal(o1, o2)
+    # library convolutions may pick split-K (atomic) kernels: replays agree to fp32 rounding
+    np.testing.assert_allclose(o1, o2, rtol=1e-4, atol=1e-5 * scale)
     assert any(v != "eager" for v in gpu._graphs.values()), "HIP graph capture fell back to eager"
     half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
     assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
