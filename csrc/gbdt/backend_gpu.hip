@@ -7,7 +7,7 @@
 //   K4 subtraction    find_split_kernel     larger child = parent - smaller
 //   K5 split search   find_split_kernel     one block per (feature, child), bins
 //                                           on lanes, fp64 prefix scan
-//   K6 partition      part_count/scatter    stable 2-pass partition, wave ballots
+//   K6 partition      part_kernel           single pass, wave ballots + tile cursors
 //   K7 score update   score_kernel          tree traversal on bins
 // The host enqueues a fixed kernel sequence per split; which leaf is split,
 // its row range and the split itself live in device memory, so a tree is built
@@ -37,10 +37,10 @@ constexpr int kFeatPerGroup = 32;          // 8 dwords of bins per block
 constexpr int kHistStride = 257;           // padded LDS row (bank spread)
 constexpr int kMaxHistBlocks = 512;        // = resident capacity at 2 blocks/CU
 constexpr int kMinRowsPerHistBlock = 2048;
-constexpr int kReduceSplit = 8;
 constexpr int kPartThreads = 512;
-constexpr int kMaxPartBlocks = 1024;
-constexpr int kMinRowsPerPartBlock = 4096;
+constexpr int kMaxPartBlocks = 2048;
+constexpr int kPartRows = 16;
+constexpr int kPartTile = kPartThreads * kPartRows;
 
 struct DLeaf {
   int32_t begin, count, buf, depth;  // local row segment; buf: -1 physical, 0/1 ping-pong
@@ -54,9 +54,14 @@ struct DState {
   int32_t small_leaf, large_leaf, parent_slot, max_leaves;
   int32_t phase;  // 0 = root, 1 = children
   // segment of the leaf being partitioned and the partition result
-  int32_t pbegin, pcount, pbuf, ptotal;
-  int32_t pad;
+  int32_t pbegin, pcount, pbuf, pad;
+  // tile cursor of the single-pass partition: left rows claimed so far in the
+  // low 32 bits (filled from pbegin upwards), right rows in the high 32 bits
+  // (filled from pbegin + pcount downwards). One 64-bit atomic per tile.
+  unsigned long long cursor;
 };
+
+__device__ __forceinline__ int PTotal(const DState* st) { return static_cast<int>(st->cursor & 0xFFFFFFFFull); }
 
 // Row segment of the leaf whose histogram is built next (root or smaller child).
 __device__ __forceinline__ DLeaf HistSeg(const DState* st, const DLeaf* leaves) {
@@ -64,8 +69,9 @@ __device__ __forceinline__ DLeaf HistSeg(const DState* st, const DLeaf* leaves) 
   DLeaf L;
   const int ob = st->pbuf == 0 ? 1 : 0;
   L.buf = ob;
-  if (st->small_leaf == st->split_leaf) { L.begin = st->pbegin; L.count = st->ptotal; }
-  else { L.begin = st->pbegin + st->ptotal; L.count = st->pcount - st->ptotal; }
+  const int lt = PTotal(st);
+  if (st->small_leaf == st->split_leaf) { L.begin = st->pbegin; L.count = lt; }
+  else { L.begin = st->pbegin + lt; L.count = st->pcount - lt; }
   return L;
 }
 
@@ -105,10 +111,51 @@ __device__ __forceinline__ bool DeviceGoesLeft(uint32_t b, int nb, int mt, int d
   return b <= thr;
 }
 
+// Block max of (|g|, h) -> per-block partial (no atomics, no fences: a
+// same-address device atomic or an agent-scope fence per block costs tens of
+// ns each on this part, serialised); ghmax_final_kernel folds the partials.
+__device__ void BlockMaxPartial(float mg, float mh, float* __restrict__ partial) {
+  __shared__ float wg[16], wh[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { mg = fmaxf(mg, __shfl_xor(mg, off, 64)); mh = fmaxf(mh, __shfl_xor(mh, off, 64)); }
+  if (lane == 0) { wg[wid] = mg; wh[wid] = mh; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < nw; ++w) { mg = fmaxf(mg, wg[w]); mh = fmaxf(mh, wh[w]); }
+    partial[2 * blockIdx.x] = mg;
+    partial[2 * blockIdx.x + 1] = mh;
+  }
+}
+
+__global__ __launch_bounds__(1024) void ghmax_final_kernel(const float* __restrict__ partial, int nblocks,
+                                                           unsigned int* __restrict__ out_bits) {
+  float mg = 0.f, mh = 0.f;
+  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
+    mg = fmaxf(mg, partial[2 * b]);
+    mh = fmaxf(mh, partial[2 * b + 1]);
+  }
+  __shared__ float wg[16], wh[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { mg = fmaxf(mg, __shfl_xor(mg, off, 64)); mh = fmaxf(mh, __shfl_xor(mh, off, 64)); }
+  if (lane == 0) { wg[wid] = mg; wh[wid] = mh; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < static_cast<int>(blockDim.x >> 6); ++w) { mg = fmaxf(mg, wg[w]); mh = fmaxf(mh, wh[w]); }
+    out_bits[0] = __float_as_uint(mg);
+    out_bits[1] = __float_as_uint(mh);
+  }
+}
+
 // ---------------------------------------------------------------- K2
-__global__ void grad_kernel(ObjParams p, const double* __restrict__ score, const float* __restrict__ label,
-                            const float* __restrict__ weight, float* __restrict__ g, float* __restrict__ h,
-                            int64_t n) {
+// Single-output objectives also produce max |g| / max h (the histogram's
+// fixed-point scales) so no separate pass over g and h is needed.
+__global__ __launch_bounds__(256) void grad_kernel(ObjParams p, const double* __restrict__ score,
+                                                   const float* __restrict__ label, const float* __restrict__ weight,
+                                                   float* __restrict__ g, float* __restrict__ h, int64_t n,
+                                                   float* __restrict__ partial) {
+  float mg = 0.f, mh = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double w = weight ? weight[i] : 1.0;
     if (p.kind == kObjMulticlass) {
@@ -131,8 +178,11 @@ __global__ void grad_kernel(ObjParams p, const double* __restrict__ score, const
       }
     } else {
       PointGradient(p, score[i], label[i], w, &g[i], &h[i]);
+      mg = fmaxf(mg, fabsf(g[i]));
+      mh = fmaxf(mh, fabsf(h[i]));
     }
   }
+  if (partial) BlockMaxPartial(mg, mh, partial);
 }
 
 // ---------------------------------------------------------------- root init
@@ -140,7 +190,7 @@ __global__ void root_init_kernel(DState* st, DLeaf* leaves, int32_t count, int b
   if (threadIdx.x == 0) {
     st->num_leaves = 1; st->done = 0; st->split_leaf = 0; st->new_leaf = -1;
     st->small_leaf = 0; st->large_leaf = -1; st->parent_slot = -1; st->max_leaves = max_leaves;
-    st->phase = 0;
+    st->phase = 0; st->cursor = 0ull;
     DLeaf l{};
     l.begin = 0; l.count = count; l.buf = buf; l.depth = 0; l.gcount = count; l.slot = 0;
     leaves[0] = l;
@@ -163,86 +213,69 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // dwordx4 loads (rows are padded to 16 B), the gradient pair one float2 load
 // from the ordered copy (or the physical arrays for an unpartitioned root).
 // kHistUnroll rows are fetched before any is accumulated so every wave keeps
-// several gathers in flight (the loop is latency-bound otherwise); the adds go
-// to LDS-privatised histograms with ds_add_f32, one row per lane, so the lanes
-// of a wave hit the same feature at random bins (bank = (feature + bin) % 32
-// thanks to the 257-float row pitch).
+// several gathers in flight (the loop is latency-bound otherwise).
+//
+// Accumulation is fixed point with g and h packed in one 64-bit LDS word ->
+// one ds_add_u64 per (row, feature): h >= 0 lives in the low 32 bits (never
+// carries), g in the high 32 (two's complement wraps exactly). The scales
+// depend only on the launch (chunk rows, the tree's max |g| / max h), so every
+// block uses the same scale, the per-block integer sums go to the slab as
+// int2 and the cross-block reduction is an exact int64 sum: the histogram is
+// bitwise independent of row order and of the block decomposition. (A/B on
+// MI355X: float ds_add_f32 13.4 ms/iter, 2x ds_add_u32 4.26, packed u64 4.16.)
 constexpr int kHistUnroll = 4;
 
-// Accumulation modes (selected per backend, SML_HIST_MODE overrides):
-//  0: two ds_add_f32 per (row, feature)
-//  1: fixed point, g and h packed in one 64-bit word -> one ds_add_u64; h >= 0
-//     lives in the low 32 bits (never carries), g in the high 32 (two's
-//     complement wraps exactly). Integer adds are order independent, so the
-//     histogram is bitwise deterministic.
-//  2: fixed point, two ds_add_u32
-// Fixed-point scales are chosen per launch from the block's row count and the
-// tree's max |g|, max h so no block sum can overflow (>= 16 bits per value at
-// the root, ~20 bits for typical leaves).
+__device__ __forceinline__ int HistBlocks(int count) {
+  return max(1, min(kMaxHistBlocks, ceil_div_i(count, kMinRowsPerHistBlock)));
+}
+
+struct HScale {
+  float g, h;
+};
+
+__device__ __forceinline__ HScale ChunkScale(int chunk, const float* ghmax) {
+  const float gmax = fmaxf(ghmax[0], 1e-30f), hmax = fmaxf(ghmax[1], 1e-30f);
+  const float rows = static_cast<float>(max(1, chunk));
+  return HScale{2.0e9f / (rows * gmax), 4.0e9f / (rows * hmax)};
+}
+
+__device__ __forceinline__ HScale HistScale(int count, const float* ghmax) {
+  return ChunkScale(ceil_div_i(count, HistBlocks(count)), ghmax);
+}
+
 __device__ __forceinline__ uint32_t word_of(const uint4& b, int j) {
   return j < 4 ? b.x : (j < 8 ? b.y : (j < 12 ? b.z : b.w));
 }
 
-template <int MODE>
-__device__ __forceinline__ void hist_add(void* lds, int j, uint32_t bin, float2 v, int32_t gq, uint32_t hq,
-                                         unsigned long long packed) {
-  if (MODE == 0) {
-    float* shg = static_cast<float*>(lds);
-    float* shh = shg + kFeatPerGroup * kHistStride;
-    atomicAdd(&shg[j * kHistStride + bin], v.x);
-    atomicAdd(&shh[j * kHistStride + bin], v.y);
-  } else if (MODE == 1) {
-    unsigned long long* sh = static_cast<unsigned long long*>(lds);
-    atomicAdd(&sh[j * kHistStride + bin], packed);
-  } else {
-    uint32_t* shg = static_cast<uint32_t*>(lds);
-    uint32_t* shh = shg + kFeatPerGroup * kHistStride;
-    atomicAdd(&shg[j * kHistStride + bin], static_cast<uint32_t>(gq));
-    atomicAdd(&shh[j * kHistStride + bin], hq);
-  }
+__device__ __forceinline__ unsigned long long PackGH(float2 v, HScale s) {
+  const int32_t gq = __float2int_rn(v.x * s.g);
+  const uint32_t hq = static_cast<uint32_t>(__float2uint_rn(fmaxf(v.y, 0.f) * s.h));
+  return (static_cast<unsigned long long>(static_cast<uint32_t>(gq)) << 32) | hq;
 }
 
-template <int MODE>
-__device__ __forceinline__ void hist_accumulate(void* lds, const uint4& b0, const uint4& b1, float2 v, int Fg,
-                                                float sg, float sh) {
-  int32_t gq = 0;
-  uint32_t hq = 0;
-  unsigned long long packed = 0;
-  if (MODE != 0) {
-    gq = __float2int_rn(v.x * sg);
-    hq = static_cast<uint32_t>(__float2uint_rn(fmaxf(v.y, 0.f) * sh));
-    packed = (static_cast<unsigned long long>(static_cast<uint32_t>(gq)) << 32) | hq;
-  }
+__device__ __forceinline__ void hist_accumulate(unsigned long long* sh, const uint4& b0, const uint4& b1,
+                                                unsigned long long packed, int Fg) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    if (j < Fg) hist_add<MODE>(lds, j, (word_of(b0, j) >> (8 * (j & 3))) & 255u, v, gq, hq, packed);
-  }
+  for (int j = 0; j < 16; ++j)
+    if (j < Fg) atomicAdd(&sh[j * kHistStride + ((word_of(b0, j) >> (8 * (j & 3))) & 255u)], packed);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    if (j + 16 < Fg) hist_add<MODE>(lds, j + 16, (word_of(b1, j) >> (8 * (j & 3))) & 255u, v, gq, hq, packed);
-  }
+  for (int j = 0; j < 16; ++j)
+    if (j + 16 < Fg) atomicAdd(&sh[(j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u)], packed);
 }
 
-template <int MODE>
 __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
     const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
-    const float* __restrict__ h, const float* __restrict__ ghmax, float2* __restrict__ slab) {
+    const float* __restrict__ h, const float* __restrict__ ghmax, int2* __restrict__ slab) {
   if (st->done) return;
   const DLeaf L = HistSeg(st, leaves);
   const int count = L.count;
-  const int nb_active = max(1, min(kMaxHistBlocks, ceil_div_i(count, kMinRowsPerHistBlock)));
+  const int nb_active = HistBlocks(count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  constexpr int kWordBytes = MODE == 1 ? 8 : 4;
-  constexpr int kArrays = MODE == 1 ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kArrays * kFeatPerGroup * kHistStride * kWordBytes];
-  void* lds = lds_raw;
+  __shared__ unsigned long long sh[kFeatPerGroup * kHistStride];
   const int tid = threadIdx.x;
-  {
-    uint32_t* z = reinterpret_cast<uint32_t*>(lds_raw);
-    for (int i = tid; i < kArrays * kFeatPerGroup * kHistStride * kWordBytes / 4; i += kHistThreads) z[i] = 0u;
-  }
+  for (int i = tid; i < kFeatPerGroup * kHistStride; i += kHistThreads) sh[i] = 0ull;
   __syncthreads();
   const int grp = blockIdx.y;
   const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
@@ -251,14 +284,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
   const int chunk = ceil_div_i(count, nb_active);
   const int p0 = L.begin + blockIdx.x * chunk;
   const int p1 = min(L.begin + count, p0 + chunk);
-  // fixed-point scales (unused in MODE 0)
-  float sg = 0.f, shs = 0.f;
-  if (MODE != 0) {
-    const float gmax = fmaxf(ghmax[0], 1e-30f), hmax = fmaxf(ghmax[1], 1e-30f);
-    const float rows = static_cast<float>(max(1, chunk));
-    sg = 2.0e9f / (rows * gmax);
-    shs = (MODE == 1 ? 4.0e9f : 2.0e9f) / (rows * hmax);
-  }
+  const HScale sc = HistScale(count, ghmax);
   const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
   const bool phys = L.buf < 0;
@@ -283,91 +309,70 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     }
 #pragma unroll
     for (int u = 0; u < kHistUnroll; ++u)
-      if (ok[u]) hist_accumulate<MODE>(lds, b0[u], b1[u], v[u], Fg, sg, shs);
+      if (ok[u]) hist_accumulate(sh, b0[u], b1[u], PackGH(v[u], sc), Fg);
   }
   __syncthreads();
-  float2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
+  int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
   for (int i = tid; i < Fg * kBinsPerFeature; i += kHistThreads) {
     const int f = i >> 8, b = i & 255;
-    float2 o;
-    if (MODE == 0) {
-      const float* shg = reinterpret_cast<const float*>(lds_raw);
-      o = make_float2(shg[f * kHistStride + b], shg[kFeatPerGroup * kHistStride + f * kHistStride + b]);
-    } else if (MODE == 1) {
-      const unsigned long long w = reinterpret_cast<const unsigned long long*>(lds_raw)[f * kHistStride + b];
-      o = make_float2(static_cast<float>(static_cast<double>(static_cast<int32_t>(w >> 32)) / sg),
-                      static_cast<float>(static_cast<double>(static_cast<uint32_t>(w)) / shs));
-    } else {
-      const uint32_t* shg = reinterpret_cast<const uint32_t*>(lds_raw);
-      o = make_float2(static_cast<float>(static_cast<double>(static_cast<int32_t>(shg[f * kHistStride + b])) / sg),
-                      static_cast<float>(static_cast<double>(shg[kFeatPerGroup * kHistStride + f * kHistStride + b]) / shs));
-    }
-    out[(grp * kFeatPerGroup + f) * kBinsPerFeature + b] = o;
+    const unsigned long long w = sh[f * kHistStride + b];
+    out[(grp * kFeatPerGroup + f) * kBinsPerFeature + b] =
+        make_int2(static_cast<int32_t>(w >> 32), static_cast<int32_t>(static_cast<uint32_t>(w)));
   }
 }
 
-// max |g|, max h of one class (fixed-point scales of the histogram kernel)
-__global__ void ghmax_kernel(const float* __restrict__ g, const float* __restrict__ h, int64_t n,
-                             unsigned int* __restrict__ out_bits) {
+// max |g|, max h of one class when the gradients did not come from grad_kernel
+// (multiclass, host-provided, GOSS-rescaled).
+constexpr int kGhmaxBlocks = 1024;
+
+__global__ __launch_bounds__(256) void ghmax_kernel(const float* __restrict__ g, const float* __restrict__ h, int64_t n,
+                                                    float* __restrict__ partial) {
   float mg = 0.f, mh = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     mg = fmaxf(mg, fabsf(g[i]));
     mh = fmaxf(mh, fabsf(h[i]));
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) { mg = fmaxf(mg, __shfl_xor(mg, off, 64)); mh = fmaxf(mh, __shfl_xor(mh, off, 64)); }
-  if ((threadIdx.x & 63) == 0) {
-    // non-negative floats order like their bit patterns
-    atomicMax(&out_bits[0], __float_as_uint(mg));
-    atomicMax(&out_bits[1], __float_as_uint(mh));
-  }
+  BlockMaxPartial(mg, mh, partial);
 }
 
-// Fixed-order reduction of the per-block slabs: part[y][e] = sum over blocks
-// y, y+S, ... (deterministic). The last element of part[0] carries the leaf's
-// local row count so one allreduce also yields the global count.
-__global__ void hist_reduce_kernel(const DState* __restrict__ st, const DLeaf* __restrict__ leaves,
-                                   const float2* __restrict__ slab, int E, double2* __restrict__ part,
-                                   double* __restrict__ count_slot) {
+// Exact reduction of the per-block integer slabs: block = 8 groups x 32 bins;
+// group y sums blocks y, y+8, ... in int64, the 8 partials are added in LDS
+// and converted once with the launch's scale. hist[E] (the slot after the
+// histogram) carries the leaf's local row count so one data-parallel
+// allreduce of 2E+2 doubles also yields the global count.
+constexpr int kRedE = 32;
+constexpr int kRedG = 16;
+
+__global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
+    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const int2* __restrict__ slab, int E,
+    const float* __restrict__ ghmax, double2* __restrict__ hist) {
   if (st->done) return;
   const int count = HistSeg(st, leaves).count;
-  const int nb_active = max(1, min(kMaxHistBlocks, ceil_div_i(count, kMinRowsPerHistBlock)));
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int y = blockIdx.y;
+  const int nb_active = HistBlocks(count);
+  const int tid = threadIdx.x, le = tid % kRedE, grp = tid / kRedE;
+  const int e = blockIdx.x * kRedE + le;
+  long long sg = 0, sh = 0;
   if (e < E) {
-    double sg = 0, sh = 0;
-    for (int b = y; b < nb_active; b += kReduceSplit) {
-      const float2 v = slab[static_cast<size_t>(b) * E + e];
-      sg += v.x; sh += v.y;
+#pragma unroll 8
+    for (int b = grp; b < nb_active; b += kRedG) {
+      const int2 v = slab[static_cast<size_t>(b) * E + e];
+      sg += v.x;
+      sh += static_cast<uint32_t>(v.y);
     }
-    part[static_cast<size_t>(y) * E + e] = make_double2(sg, sh);
   }
-  if (e == 0 && y == 0) *count_slot = static_cast<double>(count);
-}
-
-// Data-parallel only: part[0] += part[1..S-1], parts zeroed, count stored in
-// the double right after part[0] so one collective moves everything.
-__global__ void fold_parts_kernel(double2* __restrict__ part, int E, const double* __restrict__ count_slot) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < E) {
-    double2 acc = part[e];
-    for (int y = 1; y < kReduceSplit; ++y) {
-      const double2 v = part[static_cast<size_t>(y) * E + e];
-      acc.x += v.x; acc.y += v.y;
-      part[static_cast<size_t>(y) * E + e] = make_double2(0.0, 0.0);
-    }
-    part[e] = acc;
+  __shared__ long long rg[kRedG][kRedE], rh[kRedG][kRedE];
+  rg[grp][le] = sg;
+  rh[grp][le] = sh;
+  __syncthreads();
+  if (grp == 0 && e < E) {
+    long long tg = 0, th = 0;
+#pragma unroll
+    for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
+    const HScale s = HistScale(count, ghmax);
+    hist[e] = make_double2(static_cast<double>(tg) / static_cast<double>(s.g),
+                           static_cast<double>(th) / static_cast<double>(s.h));
   }
-  if (e == 0) reinterpret_cast<double*>(part + E)[0] = *count_slot;
-}
-
-__global__ void unfold_count_kernel(double2* __restrict__ part, int E, double* __restrict__ count_slot) {
-  if (threadIdx.x == 0) {
-    double* p = reinterpret_cast<double*>(part + E);
-    *count_slot = p[0];
-    p[0] = 0.0;
-    p[1] = 0.0;
-  }
+  if (blockIdx.x == 0 && tid == 0) hist[E] = make_double2(static_cast<double>(count), 0.0);
 }
 
 // ---------------------------------------------------------------- K4 + K5
@@ -439,12 +444,11 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
   }
 }
 
-// grid: (F, nchild). Block = 256 threads, thread = bin.
-__global__ __launch_bounds__(256) void find_split_kernel(
+// Block (f, child): 256 threads, thread = bin.
+__device__ void FindSplitBlock(
     DState* __restrict__ st, DLeaf* __restrict__ leaves, const double2* __restrict__ part, int E,
-    const double* __restrict__ count_slot, double2* __restrict__ hist_pool, FeatMeta fm, SplitParams sp,
+    const double* __restrict__ count_slot, double2* __restrict__ hist_pool, const FeatMeta& fm, const SplitParams& sp,
     SplitResult* __restrict__ fbest, int F) {
-  if (st->done) return;
   const int f = blockIdx.x;
   const int child = blockIdx.y;  // 0 = small (or root), 1 = large
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -452,13 +456,7 @@ __global__ __launch_bounds__(256) void find_split_kernel(
   if (root && child == 1) return;
   const int leaf_id = root ? 0 : (child == 0 ? st->small_leaf : st->large_leaf);
   const int e = f * kBinsPerFeature + tid;
-  // reduce the partial sums (fixed order) -> small histogram
-  double2 sm = make_double2(0, 0);
-#pragma unroll
-  for (int y = 0; y < kReduceSplit; ++y) {
-    const double2 v = part[static_cast<size_t>(y) * E + e];
-    sm.x += v.x; sm.y += v.y;
-  }
+  const double2 sm = part[e];  // smaller child's (or the root's) histogram
   double2 mine;
   if (root || child == 0) {
     mine = sm;
@@ -615,11 +613,9 @@ __device__ __forceinline__ KeyG WaveArgmax(KeyG k) {
   return k;
 }
 
-__global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DLeaf* __restrict__ leaves,
-                                                     SplitResult* __restrict__ lbest, double* __restrict__ lgain,
-                                                     const SplitResult* __restrict__ fbest, int F, DTree t,
-                                                     const double* __restrict__ count_slot) {
-  if (st->done) return;
+__device__ void ChooseBlock(DState* __restrict__ st, DLeaf* __restrict__ leaves, SplitResult* __restrict__ lbest,
+                            double* __restrict__ lgain, const SplitResult* __restrict__ fbest, int F, const DTree& t,
+                            const double* __restrict__ count_slot) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ int sh_best_f[2];
   __shared__ KeyG wk[4];
@@ -654,8 +650,9 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
       const int ob = st->pbuf == 0 ? 1 : 0;
       DLeaf& Lc = leaves[st->split_leaf];
       DLeaf& Rc = leaves[st->new_leaf];
-      Lc.begin = st->pbegin; Lc.count = st->ptotal; Lc.buf = ob;
-      Rc.begin = st->pbegin + st->ptotal; Rc.count = st->pcount - st->ptotal; Rc.buf = ob;
+      const int lt = PTotal(st);
+      Lc.begin = st->pbegin; Lc.count = lt; Lc.buf = ob;
+      Rc.begin = st->pbegin + lt; Rc.count = st->pcount - lt; Rc.buf = ob;
       leaves[small_leaf].gcount = small_cnt;
       leaves[large_leaf].gcount = parent_cnt - small_cnt;
       t.lcount[small_leaf] = small_cnt;
@@ -727,13 +724,30 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
   leaves[nl] = Rc;
   lgain[bl] = -INFINITY;
   lgain[nl] = -INFINITY;
-  st->pbegin = P.begin; st->pcount = P.count; st->pbuf = P.buf; st->ptotal = 0;
+  st->pbegin = P.begin; st->pcount = P.count; st->pbuf = P.buf;
+  st->cursor = 0ull;
   st->split_leaf = bl;
   st->new_leaf = nl;
   st->small_leaf = left_small ? bl : nl;
   st->large_leaf = left_small ? nl : bl;
   st->num_leaves = nl + 1;
   st->phase = 1;
+}
+
+__global__ __launch_bounds__(256) void find_split_kernel(
+    DState* __restrict__ st, DLeaf* __restrict__ leaves, const double2* __restrict__ part, int E,
+    const double* __restrict__ count_slot, double2* __restrict__ hist_pool, FeatMeta fm, SplitParams sp,
+    SplitResult* __restrict__ fbest, int F) {
+  if (st->done) return;
+  FindSplitBlock(st, leaves, part, E, count_slot, hist_pool, fm, sp, fbest, F);
+}
+
+__global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DLeaf* __restrict__ leaves,
+                                                     SplitResult* __restrict__ lbest, double* __restrict__ lgain,
+                                                     const SplitResult* __restrict__ fbest, int F, DTree t,
+                                                     const double* __restrict__ count_slot) {
+  if (st->done) return;
+  ChooseBlock(st, leaves, lbest, lgain, fbest, F, t, count_slot);
 }
 
 // ---------------------------------------------------------------- K6
@@ -747,122 +761,109 @@ __device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int
                         sr.default_left, sr.cat_bits);
 }
 
-__global__ __launch_bounds__(kPartThreads) void part_count_kernel(
-    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const SplitResult* __restrict__ lbest,
-    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
-    const int32_t* __restrict__ perm1, FeatMeta fm, int32_t* __restrict__ counts) {
-  if (st->done) return;
-  DLeaf P;
-  P.begin = st->pbegin; P.count = st->pcount; P.buf = st->pbuf;
-  const SplitResult sr = lbest[st->split_leaf];
-  const int nbp = max(1, min(kMaxPartBlocks, ceil_div_i(P.count, kMinRowsPerPartBlock)));
-  if (static_cast<int>(blockIdx.x) >= nbp) return;
-  const int chunk = ceil_div_i(P.count, nbp);
-  const int p0 = P.begin + blockIdx.x * chunk;
-  const int p1 = min(P.begin + P.count, p0 + chunk);
-  const int32_t* perm = P.buf == 0 ? perm0 : perm1;
-  int c = 0;
-  for (int p = p0 + threadIdx.x; p < p1; p += kPartThreads) {
-    const int r = P.buf < 0 ? p : perm[p];
-    c += RowGoesLeft(cbins, n, r, sr, fm) ? 1 : 0;
-  }
-  __shared__ int sc[kPartThreads / 64];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < kPartThreads / 64; ++w) t += sc[w];
-    counts[blockIdx.x] = t;
-  }
-}
+// Single pass: a block takes tiles of kPartTile rows (kPartRows per thread,
+// strided so every load is coalesced), keeps them in registers, counts the
+// tile's left rows with wave ballots and claims its output ranges with one
+// atomicAdd on the left cursor and one atomicSub on the right cursor, then
+// writes the rows straight to their final slots. Row order inside a child
+// depends on the order tiles claim their ranges; nothing downstream depends
+// on it (histograms are exact integer sums, see K3).
 
-__global__ __launch_bounds__(kPartThreads) void part_scatter_kernel(
-    DState* __restrict__ st, const DLeaf* __restrict__ leaves, const SplitResult* __restrict__ lbest,
-    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
-    const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0,
-    int32_t* __restrict__ wperm1, float2* __restrict__ wogh0, float2* __restrict__ wogh1,
-    const float* __restrict__ g, const float* __restrict__ h, FeatMeta fm, const int32_t* __restrict__ counts) {
+__global__ __launch_bounds__(kPartThreads) void part_kernel(
+    DState* __restrict__ st, const SplitResult* __restrict__ lbest, const uint8_t* __restrict__ cbins, int64_t n,
+    const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
+    const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1,
+    float2* __restrict__ wogh0, float2* __restrict__ wogh1, const float* __restrict__ g,
+    const float* __restrict__ h, FeatMeta fm) {
   if (st->done) return;
-  const int sl = st->split_leaf;
-  DLeaf P;
-  P.begin = st->pbegin; P.count = st->pcount; P.buf = st->pbuf;
-  const SplitResult sr = lbest[sl];
-  const int nbp = max(1, min(kMaxPartBlocks, ceil_div_i(P.count, kMinRowsPerPartBlock)));
-  if (static_cast<int>(blockIdx.x) >= nbp) return;
+  const int pbegin = st->pbegin, pcount = st->pcount, pbuf = st->pbuf;
+  const int ntiles = ceil_div_i(pcount, kPartTile);
+  if (static_cast<int>(blockIdx.x) >= ntiles) return;
+  const SplitResult sr = lbest[st->split_leaf];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  __shared__ int red[2][kPartThreads / 64];
-  __shared__ int wl[kPartThreads / 64];
-  // prefix of left counts before this block + total
-  int before = 0, total = 0;
-  for (int j = tid; j < nbp; j += kPartThreads) {
-    const int c = counts[j];
-    total += c;
-    if (j < static_cast<int>(blockIdx.x)) before += c;
-  }
+  constexpr int kWaves = kPartThreads / 64;
+  __shared__ int wl[kPartRows][kWaves];
+  __shared__ int bases[2];
+  const int32_t* perm = pbuf == 0 ? perm0 : perm1;
+  const float2* ogh = pbuf == 0 ? ogh0 : ogh1;
+  int32_t* operm = pbuf == 0 ? wperm1 : wperm0;
+  float2* oogh = pbuf == 0 ? wogh1 : wogh0;
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int t0 = pbegin + tile * kPartTile;
+    const int tv = min(kPartTile, pbegin + pcount - t0);
+    int r[kPartRows];
+    float2 v[kPartRows];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    before += __shfl_xor(before, off, 64);
-    total += __shfl_xor(total, off, 64);
-  }
-  if (lane == 0) { red[0][wid] = before; red[1][wid] = total; }
-  __syncthreads();
-  before = 0; total = 0;
-  for (int w = 0; w < kPartThreads / 64; ++w) { before += red[0][w]; total += red[1][w]; }
-  const int chunk = ceil_div_i(P.count, nbp);
-  const int p0 = P.begin + blockIdx.x * chunk;
-  const int p1 = min(P.begin + P.count, p0 + chunk);
-  const int ob = P.buf == 0 ? 1 : 0;
-  const int32_t* perm = P.buf == 0 ? perm0 : perm1;
-  const float2* ogh = P.buf == 0 ? ogh0 : ogh1;
-  int32_t* operm = ob == 0 ? wperm0 : wperm1;
-  float2* oogh = ob == 0 ? wogh0 : wogh1;
-  int left_base = P.begin + before;
-  int right_base = P.begin + total + ((p0 - P.begin) - before);
-  for (int tile = p0; tile < p1; tile += kPartThreads) {
-    const int p = tile + tid;
-    const bool valid = p < p1;
-    int r = 0;
-    float2 v = make_float2(0.f, 0.f);
-    bool left = false;
-    if (valid) {
-      if (P.buf < 0) { r = p; v = make_float2(g[r], h[r]); }
-      else { r = perm[p]; v = ogh[p]; }
-      left = RowGoesLeft(cbins, n, r, sr, fm);
+    for (int u = 0; u < kPartRows; ++u) {
+      const int k = u * kPartThreads + tid;
+      r[u] = 0;
+      v[u] = make_float2(0.f, 0.f);
+      if (k < tv) {
+        const int p = t0 + k;
+        if (pbuf < 0) { r[u] = p; v[u] = make_float2(g[p], h[p]); }
+        else { r[u] = perm[p]; v[u] = ogh[p]; }
+      }
     }
-    const unsigned long long bl = __ballot(valid && left);
-    const unsigned long long bv = __ballot(valid);
-    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int rl = __popcll(bl & below);
-    const int rv = __popcll(bv & below);
-    if (lane == 0) wl[wid] = __popcll(bl);
+    int rl[kPartRows];
+    unsigned lmask = 0;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const int k = u * kPartThreads + tid;
+      const bool left = k < tv && RowGoesLeft(cbins, n, r[u], sr, fm);
+      lmask |= left ? (1u << u) : 0u;
+      const unsigned long long bl = __ballot(left);
+      rl[u] = __popcll(bl & below);
+      if (lane == 0) wl[u][wid] = __popcll(bl);
+    }
     __syncthreads();
-    int wbefore_l = 0, tile_l = 0;
-    for (int w = 0; w < kPartThreads / 64; ++w) {
-      if (w < wid) wbefore_l += wl[w];
-      tile_l += wl[w];
+    if (tid == 0) {
+      int tl = 0;
+      for (int u = 0; u < kPartRows; ++u)
+        for (int w = 0; w < kWaves; ++w) tl += wl[u][w];
+      const int tr = tv - tl;
+      const unsigned long long old =
+          atomicAdd(&st->cursor, static_cast<unsigned long long>(tl) | (static_cast<unsigned long long>(tr) << 32));
+      bases[0] = pbegin + static_cast<int>(old & 0xFFFFFFFFull);
+      bases[1] = pbegin + pcount - static_cast<int>(old >> 32) - tr;
     }
-    const int wbase_total = wid * 64;  // valid elements are contiguous from tile start
-    if (valid) {
-      int dst;
-      if (left) dst = left_base + wbefore_l + rl;
-      else dst = right_base + (wbase_total - wbefore_l) + (rv - rl);
-      operm[dst] = r;
-      oogh[dst] = v;
+    __syncthreads();
+    const int lb = bases[0], rb = bases[1];
+    int run = 0;  // left rows in earlier row-groups of this tile
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      int wb = 0, ut = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const int c = wl[u][w];
+        wb += w < wid ? c : 0;
+        ut += c;
+      }
+      const int k = u * kPartThreads + tid;
+      if (k < tv) {
+        const int lbefore = run + wb + rl[u];
+        const int dst = (lmask >> u) & 1u ? lb + lbefore : rb + (k - lbefore);
+        operm[dst] = r[u];
+        oogh[dst] = v[u];
+      }
+      run += ut;
     }
-    const int tile_valid = min(kPartThreads, p1 - tile);
-    left_base += tile_l;
-    right_base += tile_valid - tile_l;
     __syncthreads();
   }
-  if (blockIdx.x == 0 && tid == 0) st->ptotal = total;  // children segments: finalised by choose
 }
 
 // ---------------------------------------------------------------- K7
-// Node = one int4 {feature | missing<<16 | default_left<<18 | is_cat<<19,
-// threshold bin, left, right}: a single 16-B load per level; bins come from the
-// column-major copy so a wave's loads of one level are coalesced.
+// Node = one int4 {feature | missing<<16 | default_left<<18 | is_cat<<19 |
+// missing_bin<<20, threshold bin, left, right}, staged in LDS. A thread loads
+// its row's packed bins once (the row-major copy: two dwordx4 for up to 32
+// features, coalesced across the wave) and walks the tree in registers, so a
+// level costs a few ALU ops instead of a dependent, lane-divergent global
+// load. kScoreRows rows per thread keep several row loads in flight. Rows
+// with more than 32 features fall back to the column-major copy.
+constexpr int kScoreRows = 2;
+constexpr int kScoreThreads = 256;
+constexpr int kScoreLdsNodes = 2048;
+
 struct DevTreeView {
   const int4* nodes;
   const uint32_t* cat_bits;  // 8 words per node
@@ -870,24 +871,83 @@ struct DevTreeView {
   int num_leaves;
 };
 
-__global__ void score_kernel(DevTreeView tv, const uint8_t* __restrict__ cbins, int64_t n, FeatMeta fm,
-                             double scale, double* __restrict__ score, int32_t* __restrict__ leaf_out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int node = 0;
-    if (tv.num_leaves > 1) {
-      for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
-        const int4 nd = tv.nodes[node];
-        const int f = nd.x & 0xFFFF;
-        const int mt = (nd.x >> 16) & 3, dl = (nd.x >> 18) & 1, ic = (nd.x >> 19) & 1;
-        const uint32_t b = cbins[static_cast<size_t>(f) * n + i];
-        const bool left = DeviceGoesLeft(b, fm.num_bin[f], mt, fm.default_bin[f], ic, static_cast<uint32_t>(nd.y), dl,
-                                         tv.cat_bits + node * 8);
-        node = left ? nd.z : nd.w;
+__device__ __forceinline__ uint32_t ByteOfRow(const uint4& a, const uint4& b, int f) {
+  const int w = f >> 2;
+  uint32_t x = w == 0 ? a.x : w == 1 ? a.y : w == 2 ? a.z : w == 3 ? a.w : w == 4 ? b.x : w == 5 ? b.y : w == 6 ? b.z : b.w;
+  return (x >> (8 * (f & 3))) & 255u;
+}
+
+__device__ __forceinline__ int NodeStep(const int4& nd, uint32_t b, const uint32_t* cat_bits, int node) {
+  const int x = nd.x;
+  const int mt = (x >> 16) & 3, dl = (x >> 18) & 1, ic = (x >> 19) & 1;
+  const uint32_t mbin = static_cast<uint32_t>(x >> 20) & 511u;
+  bool left;
+  if (ic) {
+    const uint32_t* cb = cat_bits + node * 8;
+    left = (cb[b >> 5] >> (b & 31)) & 1u;
+  } else if (mt != kMissingNone && b == mbin) {
+    left = dl != 0;
+  } else {
+    left = b <= static_cast<uint32_t>(nd.y);
+  }
+  return left ? nd.z : nd.w;
+}
+
+__global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, const uint4* __restrict__ bins4, int W4,
+                                                              int F, const uint8_t* __restrict__ cbins, int64_t n,
+                                                              double scale, double* __restrict__ score,
+                                                              int32_t* __restrict__ leaf_out) {
+  __shared__ int4 snodes[kScoreLdsNodes];
+  const int ni = tv.num_leaves - 1;
+  const bool lds = ni <= kScoreLdsNodes;
+  if (lds)
+    for (int i = threadIdx.x; i < ni; i += kScoreThreads) snodes[i] = tv.nodes[i];
+  __syncthreads();
+  const int4* nodes = lds ? snodes : tv.nodes;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kScoreThreads;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kScoreThreads + threadIdx.x;
+  const bool packed = F <= 32;
+  int leaf[kScoreRows];
+  if (packed) {
+    uint4 ra[kScoreRows], rb[kScoreRows];
+#pragma unroll
+    for (int u = 0; u < kScoreRows; ++u) {
+      const int64_t i = i0 + u * stride;
+      ra[u] = make_uint4(0, 0, 0, 0);
+      rb[u] = ra[u];
+      if (i < n && ni > 0) {
+        ra[u] = bins4[i * W4];
+        if (F > 16) rb[u] = bins4[i * W4 + 1];
       }
-      node = node < 0 ? ~node : 0;  // a malformed tree cannot loop forever
     }
-    if (score) score[i] += scale * tv.lval[node];
-    if (leaf_out) leaf_out[i] = node;
+#pragma unroll
+    for (int u = 0; u < kScoreRows; ++u) {
+      int node = ni > 0 ? 0 : ~0;
+      for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
+        const int4 nd = nodes[node];
+        node = NodeStep(nd, ByteOfRow(ra[u], rb[u], nd.x & 0xFFFF), tv.cat_bits, node);
+      }
+      leaf[u] = ni > 0 ? ~node : 0;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kScoreRows; ++u) {
+      const int64_t i = i0 + u * stride;
+      int node = (ni > 0 && i < n) ? 0 : ~0;
+      for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
+        const int4 nd = nodes[node];
+        node = NodeStep(nd, cbins[static_cast<size_t>(nd.x & 0xFFFF) * n + i], tv.cat_bits, node);
+      }
+      leaf[u] = ni > 0 ? ~node : 0;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kScoreRows; ++u) {
+    const int64_t i = i0 + u * stride;
+    if (i < n) {
+      if (score) score[i] += scale * tv.lval[leaf[u]];
+      if (leaf_out) leaf_out[i] = leaf[u];
+    }
   }
 }
 
@@ -923,9 +983,8 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipGetDevice(&dev_));
     SML_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     sp_ = MakeSplitParams(cfg);
-    hist_mode_ = 1;  // packed fixed point (deterministic); SML_HIST_MODE=0 selects float atomics
-    if (const char* e = std::getenv("SML_HIST_MODE")) hist_mode_ = std::atoi(e);
-    ghmax_.alloc(2);
+    ghmax_.alloc(2);  // max |g|, max h (float bits)
+    ghmax_partial_.alloc(2 * kGhmaxBlocks);
     F_ = d->ref.num_inner();
     S_ = d->row_stride;
     W_ = S_ / 4;
@@ -949,15 +1008,13 @@ class GpuBackend : public TrainBackend {
     h_.alloc(static_cast<size_t>(n_) * K);
     for (int b = 0; b < 2; ++b) { perm_[b].alloc(n_); ogh_[b].alloc(n_); }
     slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * E_);
-    part_.alloc(static_cast<size_t>(kReduceSplit) * E_);
+    part_.alloc(static_cast<size_t>(E_) + 1);  // histogram + (row count, 0)
     hist_pool_.alloc(static_cast<size_t>(2 * L_ + 2) * E_);
-    count_slot_.alloc(1);
+    part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + kPartTile - 1) / kPartTile)));
     fbest_.alloc(2 * F_);
     lbest_.alloc(L_);
     lgain_.alloc(L_);
     leaves_.alloc(L_);
-    state_.alloc(1);
-    counts_.alloc(kMaxPartBlocks);
     // feature meta
     std::vector<int32_t> nb(F_), mt(F_), db(F_), ic(F_);
     for (int f = 0; f < F_; ++f) {
@@ -974,18 +1031,30 @@ class GpuBackend : public TrainBackend {
     fm_.is_cat = meta_i_.get() + 3 * F_; fm_.mask = mask_.get();
     // device tree
     const int NI = L_ - 1;
-    tree_i_.alloc(static_cast<size_t>(NI) * 6 + L_ * 2);
-    tree_u_.alloc(static_cast<size_t>(NI) * 9);
-    tree_d_.alloc(static_cast<size_t>(NI) * 3 + L_ * 2);
-    tree_l_.alloc(static_cast<size_t>(NI) + L_);
-    int32_t* ti = tree_i_.get();
+    // DState + the device tree live in one allocation so a finished tree comes
+    // back with a single D2H copy
+    n_ti_ = static_cast<size_t>(NI) * 6 + L_ * 2;
+    n_tu_ = static_cast<size_t>(NI) * 9;
+    n_td_ = static_cast<size_t>(NI) * 3 + L_ * 2;
+    n_tl_ = static_cast<size_t>(NI) + L_;
+    off_td_ = (sizeof(DState) + 63) / 64 * 64;
+    off_tl_ = off_td_ + n_td_ * sizeof(double);
+    off_ti_ = off_tl_ + n_tl_ * sizeof(int64_t);
+    off_tu_ = off_ti_ + n_ti_ * sizeof(int32_t);
+    blob_bytes_ = off_tu_ + n_tu_ * sizeof(uint32_t);
+    if (blob_bytes_ > kPinnedBytes) throw std::runtime_error("GPU backend: tree too large for staging buffer");
+    blob_.alloc(blob_bytes_);
+    state_ = reinterpret_cast<DState*>(blob_.get());
+    int32_t* ti = reinterpret_cast<int32_t*>(blob_.get() + off_ti_);
     dt_.feat = ti; dt_.dleft = ti + NI; dt_.is_cat = ti + 2 * NI; dt_.left = ti + 3 * NI; dt_.right = ti + 4 * NI;
     dt_.lparent = ti + 6 * NI; dt_.ldepth = ti + 6 * NI + L_;
     flags_ = ti + 5 * NI;
-    dt_.thr = tree_u_.get(); dt_.cat_bits = tree_u_.get() + NI;
-    double* td = tree_d_.get();
+    uint32_t* tu = reinterpret_cast<uint32_t*>(blob_.get() + off_tu_);
+    dt_.thr = tu; dt_.cat_bits = tu + NI;
+    double* td = reinterpret_cast<double*>(blob_.get() + off_td_);
     dt_.gain = td; dt_.ival = td + NI; dt_.iweight = td + 2 * NI; dt_.lval = td + 3 * NI; dt_.lweight = td + 3 * NI + L_;
-    dt_.icount = tree_l_.get(); dt_.lcount = tree_l_.get() + NI;
+    int64_t* tl = reinterpret_cast<int64_t*>(blob_.get() + off_tl_);
+    dt_.icount = tl; dt_.lcount = tl + NI;
     // score-update tree (uploaded from host trees)
     up_nodes_.alloc(static_cast<size_t>(NI) + 1);
     up_u_.alloc(static_cast<size_t>(NI) * 8 + 8);
@@ -1024,12 +1093,20 @@ class GpuBackend : public TrainBackend {
       return;
     }
     auto t0 = std::chrono::steady_clock::now();
-    hipLaunchKernelGGL(grad_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, p, score_.get(), label_.get(),
-                       weight_.get(), g_.get(), h_.get(), n_);
+    const bool single = p.kind != kObjMulticlass && p.kind != kObjMulticlassOVA;
+    const int grid = std::min(GridFor(n_), kGhmaxBlocks);
+    hipLaunchKernelGGL(grad_kernel, dim3(grid), dim3(256), 0, stream_, p, score_.get(), label_.get(),
+                       weight_.get(), g_.get(), h_.get(), n_, single ? ghmax_partial_.get() : static_cast<float*>(nullptr));
     SML_HIP_CHECK(hipGetLastError());
+    if (single) {
+      hipLaunchKernelGGL(ghmax_final_kernel, dim3(1), dim3(1024), 0, stream_, ghmax_partial_.get(), grid, ghmax_.get());
+      SML_HIP_CHECK(hipGetLastError());
+    }
+    ghmax_valid_ = single && K_ == 1;
     stats.grad_ms += Ms(t0);
   }
   void SetGradients(const float* g, const float* h) override {
+    ghmax_valid_ = false;
     SML_HIP_CHECK(hipMemcpyAsync(g_.get(), g, sizeof(float) * n_ * K_, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipMemcpyAsync(h_.get(), h, sizeof(float) * n_ * K_, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1065,26 +1142,23 @@ class GpuBackend : public TrainBackend {
                          g, h, perm_[0].get(), ogh_[0].get());
       SML_HIP_CHECK(hipGetLastError());
     }
-    if (hist_mode_ != 0) {
-      SML_HIP_CHECK(hipMemsetAsync(ghmax_.get(), 0, 2 * sizeof(unsigned int), stream_));
-      hipLaunchKernelGGL(ghmax_kernel, dim3(GridFor(n_) < 2048 ? GridFor(n_) : 2048), dim3(256), 0, stream_, g, h, n_,
-                         ghmax_.get());
+    if (!ghmax_valid_ || k != 0) {
+      const int grid = std::min(GridFor(n_), kGhmaxBlocks);
+      hipLaunchKernelGGL(ghmax_kernel, dim3(grid), dim3(256), 0, stream_, g, h, n_, ghmax_partial_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(ghmax_final_kernel, dim3(1), dim3(1024), 0, stream_, ghmax_partial_.get(), grid, ghmax_.get());
       SML_HIP_CHECK(hipGetLastError());
     }
-    hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_.get(), leaves_.get(), root_count, root_buf, L_);
+    hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_, leaves_.get(), root_count, root_buf, L_);
     SML_HIP_CHECK(hipGetLastError());
     // root histogram + split search
     EnqueueHistogram(g, h);
     EnqueueFindChoose();
     for (int s = 1; s < L_; ++s) {
       // partition the chosen leaf, histogram its smaller child, search both
-      hipLaunchKernelGGL(part_count_kernel, dim3(kMaxPartBlocks), dim3(kPartThreads), 0, stream_, state_.get(),
-                         leaves_.get(), lbest_.get(), cbins_.get(), n_, perm_[0].get(), perm_[1].get(), fm_, counts_.get());
-      SML_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(part_scatter_kernel, dim3(kMaxPartBlocks), dim3(kPartThreads), 0, stream_, state_.get(),
-                         leaves_.get(), lbest_.get(), cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(),
-                         ogh_[1].get(), perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_,
-                         counts_.get());
+      hipLaunchKernelGGL(part_kernel, dim3(part_grid_), dim3(kPartThreads), 0, stream_, state_, lbest_.get(),
+                         cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
+                         perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
       SML_HIP_CHECK(hipGetLastError());
       EnqueueHistogram(g, h);
       EnqueueFindChoose();
@@ -1096,14 +1170,16 @@ class GpuBackend : public TrainBackend {
 
   void UpdateScore(const Tree& t, int k, double scale) override {
     DevTreeView tv = UploadTree(t);
-    hipLaunchKernelGGL(score_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, tv, cbins_.get(), n_, fm_, scale,
+    hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
+                       reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
                        score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
     SML_HIP_CHECK(hipGetLastError());
   }
 
   void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) override {
     DevTreeView tv = UploadTree(t);
-    hipLaunchKernelGGL(score_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, tv, cbins_.get(), n_, fm_, 0.0,
+    hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
+                       reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, 0.0,
                        static_cast<double*>(nullptr), leaf_idx_.get());
     SML_HIP_CHECK(hipGetLastError());
     leaf->resize(n_);
@@ -1115,60 +1191,54 @@ class GpuBackend : public TrainBackend {
   static double Ms(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  int ScoreGrid() const {
+    const int64_t per_block = static_cast<int64_t>(kScoreThreads) * kScoreRows;
+    return static_cast<int>(std::max<int64_t>(1, (n_ + per_block - 1) / per_block));
+  }
   static int GridFor(int64_t n) {
     int64_t b = (n + 255) / 256;
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(b, 8192)));
   }
 
+  const double* CountSlot() const { return reinterpret_cast<const double*>(part_.get() + E_); }
+
   void EnqueueHistogram(const float* g, const float* h) {
-    auto launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_.get(), leaves_.get(),
-                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(), perm_[1].get(),
-                         ogh_[0].get(), ogh_[1].get(), g, h, reinterpret_cast<const float*>(ghmax_.get()), slab_.get());
-    };
-    if (hist_mode_ == 1) launch(hist_kernel<1>);
-    else if (hist_mode_ == 2) launch(hist_kernel<2>);
-    else launch(hist_kernel<0>);
+    const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
+    hipLaunchKernelGGL(hist_kernel, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_,
+                       leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
+                       perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     SML_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + 255) / 256, kReduceSplit), dim3(256), 0, stream_, state_.get(),
-                       leaves_.get(), slab_.get(), E_, part_.get(), count_slot_.get());
+    hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_,
+                       state_, leaves_.get(), slab_.get(), E_, ghmax, part_.get());
     SML_HIP_CHECK(hipGetLastError());
     if (comm_ && comm_->world() > 1) {
-      // fold the partial sums into part[0] (and the row count next to it), then
-      // one allreduce of E*2+1 doubles over RCCL
-      hipLaunchKernelGGL(fold_parts_kernel, dim3((E_ + 255) / 256), dim3(256), 0, stream_, part_.get(), E_,
-                         count_slot_.get());
-      SML_HIP_CHECK(hipGetLastError());
+      // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL
       auto t0 = std::chrono::steady_clock::now();
-      comm_->AllReduceDeviceF64(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 1, stream_);
+      comm_->AllReduceDeviceF64(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 2, stream_);
       stats.comm_ms += Ms(t0);
-      hipLaunchKernelGGL(unfold_count_kernel, dim3(1), dim3(64), 0, stream_, part_.get(), E_, count_slot_.get());
-      SML_HIP_CHECK(hipGetLastError());
     }
   }
 
   void EnqueueFindChoose() {
-    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, state_.get(), leaves_.get(), part_.get(),
-                       E_, count_slot_.get(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
+    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, state_, leaves_.get(), part_.get(),
+                       E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
     SML_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, state_.get(), leaves_.get(), lbest_.get(),
-                       lgain_.get(), fbest_.get(), F_, dt_, count_slot_.get());
+    hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, state_, leaves_.get(), lbest_.get(),
+                       lgain_.get(), fbest_.get(), F_, dt_, CountSlot());
     SML_HIP_CHECK(hipGetLastError());
   }
 
   Tree ReadTree() {
     const int NI = L_ - 1;
-    DState st;
-    SML_HIP_CHECK(hipMemcpyAsync(&st, state_.get(), sizeof(DState), hipMemcpyDeviceToHost, stream_));
-    std::vector<int32_t> ti(tree_i_.n);
-    std::vector<uint32_t> tu(tree_u_.n);
-    std::vector<double> td(tree_d_.n);
-    std::vector<int64_t> tl(tree_l_.n);
-    SML_HIP_CHECK(hipMemcpyAsync(ti.data(), tree_i_.get(), sizeof(int32_t) * ti.size(), hipMemcpyDeviceToHost, stream_));
-    SML_HIP_CHECK(hipMemcpyAsync(tu.data(), tree_u_.get(), sizeof(uint32_t) * tu.size(), hipMemcpyDeviceToHost, stream_));
-    SML_HIP_CHECK(hipMemcpyAsync(td.data(), tree_d_.get(), sizeof(double) * td.size(), hipMemcpyDeviceToHost, stream_));
-    SML_HIP_CHECK(hipMemcpyAsync(tl.data(), tree_l_.get(), sizeof(int64_t) * tl.size(), hipMemcpyDeviceToHost, stream_));
+    SML_HIP_CHECK(hipMemcpyAsync(pinned_, blob_.get(), blob_bytes_, hipMemcpyDeviceToHost, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
+    const uint8_t* hb = static_cast<const uint8_t*>(pinned_);
+    DState st;
+    std::memcpy(&st, hb, sizeof(DState));
+    const int32_t* ti = reinterpret_cast<const int32_t*>(hb + off_ti_);
+    const uint32_t* tu = reinterpret_cast<const uint32_t*>(hb + off_tu_);
+    const double* td = reinterpret_cast<const double*>(hb + off_td_);
+    const int64_t* tl = reinterpret_cast<const int64_t*>(hb + off_tl_);
     const int nl = st.num_leaves;
     Tree t(L_);
     t.num_leaves = nl;
@@ -1236,7 +1306,9 @@ class GpuBackend : public TrainBackend {
     for (int node = 0; node < t.num_leaves - 1; ++node) {
       const int8_t dt = t.decision_type[node];
       const int mt = (dt >> 2) & 3, dl = (dt >> 1) & 1, ic = dt & 1;
-      pn[node] = make_int4(t.split_feature_inner[node] | (mt << 16) | (dl << 18) | (ic << 19),
+      const BinMapper& m = data_->ref.mappers[data_->ref.used_features[t.split_feature_inner[node]]];
+      const int mbin = mt == kMissingNaN ? m.num_bin - 1 : (mt == kMissingZero ? m.default_bin : 0);
+      pn[node] = make_int4(t.split_feature_inner[node] | (mt << 16) | (dl << 18) | (ic << 19) | (mbin << 20),
                            static_cast<int>(t.threshold_in_bin[node]), t.left_child[node], t.right_child[node]);
       for (int w = 0; w < 8; ++w) pu[node * 8 + w] = 0;
       if (ic) {
@@ -1268,20 +1340,21 @@ class GpuBackend : public TrainBackend {
   DevBuf<double> score_;
   DevBuf<int32_t> perm_[2];
   DevBuf<float2> ogh_[2];
-  DevBuf<float2> slab_;
+  DevBuf<int2> slab_;
   DevBuf<double2> part_, hist_pool_;
-  DevBuf<double> count_slot_, lgain_;
+  DevBuf<double> lgain_;
   DevBuf<SplitResult> fbest_, lbest_;
   DevBuf<DLeaf> leaves_;
-  DevBuf<DState> state_;
-  DevBuf<int32_t> counts_, meta_i_, bag_;
+  DevBuf<int32_t> meta_i_, bag_;
   DevBuf<int8_t> mask_;
   DevBuf<unsigned int> ghmax_;
-  int hist_mode_ = 1;
-  DevBuf<int32_t> tree_i_;
-  DevBuf<uint32_t> tree_u_;
-  DevBuf<double> tree_d_;
-  DevBuf<int64_t> tree_l_;
+  DevBuf<float> ghmax_partial_;
+  bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
+  int part_grid_ = 1;
+  DevBuf<uint8_t> blob_;
+  DState* state_ = nullptr;
+  size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
+  size_t off_td_ = 0, off_tl_ = 0, off_ti_ = 0, off_tu_ = 0, blob_bytes_ = 0;
   DevBuf<int4> up_nodes_;
   DevBuf<uint32_t> up_u_;
   DevBuf<double> up_d_;

@@ -121,3 +121,13 @@ def test_classifier_api_on_gpu():
     assert m.getLightGBMBooster().native.backend == "hip"
     out = m.transform(df)
     assert out["probability"].shape == (30000, 2)
+
+
+def test_gpu_training_is_deterministic():
+    """Single-pass partition writes rows in tile-claim order; the integer
+    histograms make the trees bitwise independent of that order."""
+    X, y = _data(n=200000, f=10, seed=3)
+    p = "objective=binary num_leaves=63 learning_rate=0.1 device_type=gpu"
+    m1 = _train(X, y, p, 8).save_model_string()
+    m2 = _train(X, y, p, 8).save_model_string()
+    assert m1 == m2
