@@ -108,6 +108,9 @@ class ParamsMeta(type):
                 setattr(cls, getter, _make_getter(pname))
             if not hasattr(cls, setter):
                 setattr(cls, setter, _make_setter(pname))
+        hook = getattr(cls, "_params_hook", None)
+        if hook is not None:
+            hook()
         return cls
 
 
