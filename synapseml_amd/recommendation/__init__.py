@@ -250,27 +250,27 @@ class ALS(Estimator, RecommendationParams, HasPredictionCol, HasSeed):
         implicit = self.getImplicitPrefs()
         if implicit:
             P = (R > 0).double()
-            Cw = 1.0 + self.getAlpha() * R
+            Cw = self.getAlpha() * R * M  # confidence - 1 on observed entries
+        nonneg = self.getNonnegative()
+        # Every half-sweep is batched: all normal-equation matrices come from one GEMM against the Y (x) Y
+        # outer products ([n, k*k]) and all k x k systems are solved in one batched call.
         for _ in range(self.getMaxIter()):
-            for X, Y, Rm, Mm in ((U, V, R, M), (V, U, R.T, M.T)):
+            for side in (0, 1):
+                X, Y = (U, V) if side == 0 else (V, U)
+                Mm, Rm = (M, R) if side == 0 else (M.T, R.T)
+                YY = (Y[:, :, None] * Y[:, None, :]).reshape(Y.shape[0], k * k)
                 if implicit:
-                    Pm = P if X is U else P.T
-                    Cm = Cw if X is U else Cw.T
-                    YtY = Y.T @ Y
-                    for a in range(X.shape[0]):
-                        c = Cm[a]
-                        A_ = YtY + (Y.T * (c - 1)) @ Y + lam * eye
-                        X[a] = torch.linalg.solve(A_, (Y.T * c) @ Pm[a])
+                    Cm, Pm = (Cw, P) if side == 0 else (Cw.T, P.T)
+                    A = (Y.T @ Y)[None] + (Cm @ YY).reshape(-1, k, k) + lam * eye
+                    bvec = ((1.0 + Cm) * Pm) @ Y
                 else:
                     n_a = Mm.sum(1)
-                    for a in range(X.shape[0]):
-                        m = Mm[a] > 0
-                        if not bool(m.any()):
-                            continue
-                        Ya = Y[m]
-                        X[a] = torch.linalg.solve(Ya.T @ Ya + lam * n_a[a] * eye, Ya.T @ Rm[a][m])
-                if self.getNonnegative():
-                    X.clamp_(min=0)
+                    A = (Mm @ YY).reshape(-1, k, k) + (lam * n_a.clamp(min=1.0))[:, None, None] * eye
+                    bvec = (Mm * Rm) @ Y
+                sol = torch.linalg.solve(A, bvec.unsqueeze(-1)).squeeze(-1)
+                if not implicit:
+                    sol = torch.where((Mm.sum(1) > 0)[:, None], sol, X)
+                X.copy_(sol.clamp(min=0) if nonneg else sol)
         model = ALSModel(userCol=self.getUserCol(), itemCol=self.getItemCol(), ratingCol=self.getRatingCol(),
                          predictionCol=self.getPredictionCol(), coldStartStrategy=self.getColdStartStrategy())
         model.set("userFactors", U.cpu().numpy())
