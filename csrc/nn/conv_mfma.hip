@@ -1,0 +1,290 @@
+// Implicit-GEMM convolution on the CDNA4 matrix cores with fused prologue and
+// epilogue (module _nn, used by the ONNX executor for NHWC fp16/bf16 graphs).
+//
+//   y[m, n]  = epi( sum_k pro(x_col[m, k]) * w[n, k] )
+//   m = (b, oh, ow) output pixel, n = output channel, k = (r, s, c) tap x input
+//   channel; x NHWC [B,H,W,C], w [Cout][R][S][C] (K contiguous), y NHWC.
+//   pro(v) = relu(v * in_scale[c] + in_shift[c])   (pre-activation BN+ReLU;
+//            padding taps stay 0, as in the unfused graph)
+//   epi(v) = v + bias[n]; relu (optional); + res[m, n] (optional) -> y;
+//            optional second output y2 = relu(y * out_scale[n] + out_shift[n])
+//            (the next pre-activation block's input, written from registers).
+//
+// Tiling: 256 threads = 4 waves in 2x2, block tile BM x BN x BK=64, wave tile
+// (BM/2) x (BN/2) of 16x16x32 MFMAs (f16 or bf16 in, fp32 accumulate). A and B
+// tiles are staged through registers (the prologue is applied there) into a
+// double-buffered LDS image with a 144-byte row pitch (conflict-free 16-lane
+// ds_read_b128 fragment reads); the next tile's global loads are issued before
+// the current tile's MFMAs so HBM latency hides behind matrix work. Blocks are
+// remapped so that each XCD owns a contiguous run of (m, n) tiles: the blocks
+// that share an activation tile (all n for one m) sit on one XCD's L2.
+// Requires C % 64 == 0 (every ResNet conv but the 3-channel stem).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "nn_ops.h"
+
+namespace smlnn {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBK = 64;
+constexpr int kPad = 8;  // elements of row padding (16 B)
+constexpr int kLd = kBK + kPad;
+constexpr int kThreads = 256;
+
+template <class T>
+struct Vec;
+template <>
+struct Vec<_Float16> {
+  typedef h8 type;
+  static __device__ __forceinline__ f4 mfma(const h8& a, const h8& b, const f4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct Vec<__bf16> {
+  typedef b8 type;
+  static __device__ __forceinline__ f4 mfma(const b8& a, const b8& b, const f4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <class T>
+__device__ __forceinline__ float ToF(T v) {
+  return static_cast<float>(v);
+}
+template <class T>
+__device__ __forceinline__ T FromF(float v) {
+  return static_cast<T>(v);
+}
+
+template <class T, int BM, int BN>
+__global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
+  typedef typename Vec<T>::type V8;
+  constexpr int WM = BM / 2, WN = BN / 2;       // wave tile
+  constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
+  constexpr int AR = BM * kBK / 8 / kThreads;   // 16-B A chunks per thread per tile
+  constexpr int BR = BN * kBK / 8 / kThreads;   // 16-B B chunks per thread per tile
+  __shared__ __attribute__((aligned(16))) T lds[2 * (BM + BN) * kLd];
+  T* As = lds;
+  T* Bs = lds + 2 * BM * kLd;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = a.B * a.OH * a.OW;
+  const int K = a.R * a.S * a.C;
+  const int tiles_n = (a.Cout + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int total = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // per-thread A rows (fixed across the K loop) and their input-window origin
+  const int kc = tid & 7;  // 16-B chunk within the 64-wide k tile
+  int rb[AR], rih[AR], riw[AR];
+  bool rok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    rok[i] = m < M;
+    const int mm = rok[i] ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW;
+    const int oh = t2 % a.OH;
+    rb[i] = t2 / a.OH;
+    rih[i] = oh * a.stride_h - a.pad_h;
+    riw[i] = ow * a.stride_w - a.pad_w;
+  }
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const T* __restrict__ w = static_cast<const T*>(a.w);
+
+  uint4 ra[AR], rbv[BR];
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * kBK;
+    const int tap = k0 / a.C;
+    const int c0 = k0 - tap * a.C + kc * 8;
+    const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int ih = rih[i] + r * a.dil_h, iw = riw[i] + s * a.dil_w;
+      const bool ok = rok[i] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(x + ((static_cast<int64_t>(rb[i]) * a.H + ih) * a.W + iw) * a.C + c0)
+                 : make_uint4(0, 0, 0, 0);
+      if (a.in_scale && ok) {
+        T* e = reinterpret_cast<T*>(&ra[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = ToF(e[j]) * a.in_scale[c0 + j] + a.in_shift[c0 + j];
+          e[j] = FromF<T>(a.prologue_relu ? fmaxf(v, 0.f) : v);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rbv[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * K + k0 + kc * 8)
+                          : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + 32 * i) * kLd + kc * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + 32 * i) * kLd + kc * 8) = rbv[i];
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int nk = K / kBK;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+#pragma unroll
+    for (int ks = 0; ks < kBK / 32; ++ks) {
+      V8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + wm0 + i * 16 + fr) * kLd + ks * 32 + fk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + wn0 + j * 16 + fr) * kLd + ks * 32 + fk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue part 1 (registers): lane holds column n = .. + (lane & 15), rows 4*(lane >> 4) + reg;
+  // bias + ReLU in fp32, rounded to T (the unfused graph's conv output), staged per wave through LDS.
+  T* __restrict__ y = static_cast<T*>(a.y);
+  const T* __restrict__ res = static_cast<const T*>(a.res);
+  T* __restrict__ y2 = static_cast<T*>(a.y2);
+  if ((a.Cout & 7) == 0) {
+    constexpr int CL = WN + 8;  // staged row pitch (elements)
+    T* Ct = lds + wid * WM * CL;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn0 + j * 16 + fr;
+      const float bn = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bn;
+          if (a.relu) v = fmaxf(v, 0.f);
+          Ct[(i * 16 + 4 * (lane >> 4) + r) * CL + j * 16 + fr] = FromF<T>(v);
+        }
+    }
+    __syncthreads();
+    // part 2: 16-B row chunks -> residual add, dual output, coalesced 16-B stores
+    constexpr int CPR = WN / 8;
+#pragma unroll
+    for (int it = 0; it < WM * CPR / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx / CPR, ch = idx % CPR;
+      const int m = m0 + wm0 + row, n = n0 + wn0 + ch * 8;
+      if (m >= M || n >= a.Cout) continue;
+      uint4 pv = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * 8);
+      const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
+      if (res) {
+        const uint4 rv = *reinterpret_cast<const uint4*>(res + o);
+        T* pe = reinterpret_cast<T*>(&pv);
+        const T* re = reinterpret_cast<const T*>(&rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pe[e] = FromF<T>(ToF(pe[e]) + ToF(re[e]));
+      }
+      *reinterpret_cast<uint4*>(y + o) = pv;
+      if (y2) {
+        uint4 qv;
+        const T* pe = reinterpret_cast<const T*>(&pv);
+        T* qe = reinterpret_cast<T*>(&qv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * a.out_scale[n + e] + a.out_shift[n + e], 0.f));
+        *reinterpret_cast<uint4*>(y2 + o) = qv;
+      }
+    }
+    return;
+  }
+  // generic epilogue (Cout not a multiple of 8): element stores straight from the accumulators
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + j * 16 + fr;
+    if (n >= a.Cout) continue;
+    const float bn = a.bias ? a.bias[n] : 0.f;
+    const float os = a.out_scale ? a.out_scale[n] : 0.f, ob = a.out_scale ? a.out_shift[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm0 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bn;
+        if (a.relu) v = fmaxf(v, 0.f);
+        const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
+        const T c = FromF<T>(v);
+        const T vt = res ? FromF<T>(ToF(c) + ToF(res[o])) : c;
+        y[o] = vt;
+        if (y2) y2[o] = FromF<T>(fmaxf(ToF(vt) * os + ob, 0.f));
+      }
+    }
+  }
+}
+
+template <class T, int BM, int BN>
+void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
+  const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_mfma_kernel<T, BM, BN>), dim3(blocks), dim3(kThreads), 0, st, a);
+}
+
+// Tile choice: 128-row tiles unless that leaves fewer than two blocks per CU (256 CUs), then 64-row
+// tiles (small spatial extents late in the network).
+template <class T>
+void Launch(const ConvArgs& a, hipStream_t st) {
+  const int M = a.B * a.OH * a.OW;
+  const int bn = a.Cout <= 64 ? 64 : 128;
+  const int blocks128 = ((M + 127) / 128) * ((a.Cout + bn - 1) / bn);
+  const bool small = blocks128 < 512;
+  if (bn == 64) {
+    if (small) LaunchTile<T, 64, 64>(a, M, st);
+    else LaunchTile<T, 128, 64>(a, M, st);
+  } else {
+    if (small) LaunchTile<T, 64, 128>(a, M, st);
+    else LaunchTile<T, 128, 128>(a, M, st);
+  }
+}
+
+}  // namespace
+
+bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
+  return groups == 1 && C % kBK == 0 && C > 0 && Cout > 0 && (dtype == 1 || dtype == 2);
+}
+
+int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
+  if (!ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return -1;
+  if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == 1) Launch<_Float16>(a, st);
+  else Launch<__bf16>(a, st);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace smlnn

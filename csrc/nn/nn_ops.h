@@ -15,6 +15,24 @@ void AddAffineAct(const void* a, const void* b, int64_t n, int C, int HW, int nh
                   const float* shift, int act, int dtype, void* sum_out, void* act_out, void* stream);
 // NHWC global average pool -> fp32 [N, C]
 void GapNhwc(const void* x, int N, int HW, int C, int dtype, float* out, void* stream);
+// Implicit-GEMM MFMA convolution with fused prologue/epilogue (conv_mfma.hip).
+struct ConvArgs {
+  const void* x;           // NHWC [B, H, W, C]
+  const void* w;           // [Cout][R][S][C]
+  void* y;                 // NHWC [B, OH, OW, Cout]
+  const float* in_scale;   // prologue affine per input channel (null: none)
+  const float* in_shift;
+  const float* bias;       // per output channel (null: none)
+  const void* res;         // residual, same layout as y (null: none)
+  const float* out_scale;  // second output y2 = relu(y * out_scale + out_shift) (null: none)
+  const float* out_shift;
+  void* y2;
+  int B, H, W, C, Cout, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, OH, OW;
+  int relu;            // relu after bias (before the residual add)
+  int prologue_relu;   // relu after the prologue affine
+};
+bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);
+int ConvMfma(const ConvArgs& a, int dtype, void* stream);
 // fp32 row softmax (y may be null) and argmax (amax may be null)
 void SoftmaxRows(const float* x, int rows, int cols, float* y, int64_t* amax, void* stream);
 

@@ -1,0 +1,67 @@
+"""Python entry to the MFMA implicit-GEMM convolution (csrc/nn/conv_mfma.hip).
+
+Tensors are torch CUDA tensors in channels_last memory (NHWC); weights are
+packed once to [Cout, R, S, Cin]. Epilogue / prologue tensors are fp32."""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import native
+
+_DT = {torch.float16: 1, torch.bfloat16: 2}
+
+
+def supported(cin: int, cout: int, groups: int, dtype: torch.dtype) -> bool:
+    return dtype in _DT and bool(native.load("_nn").conv_supported(cin, cout, groups, _DT[dtype]))
+
+
+def pack_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """[Cout, Cin, R, S] -> contiguous [Cout, R, S, Cin] in ``dtype``."""
+    return w.permute(0, 2, 3, 1).contiguous().to(dtype)
+
+
+def out_hw(h: int, w: int, r: int, s: int, stride: Sequence[int], pad: Sequence[int], dil: Sequence[int]):
+    oh = (h + 2 * pad[0] - dil[0] * (r - 1) - 1) // stride[0] + 1
+    ow = (w + 2 * pad[1] - dil[1] * (s - 1) - 1) // stride[1] + 1
+    return oh, ow
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
+                bias: Optional[torch.Tensor] = None, relu: bool = False,
+                in_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, in_relu: bool = True,
+                res: Optional[torch.Tensor] = None,
+                out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """y = [relu](conv(pro(x), w) + bias) [+ res]; optionally also y2 = relu(y * out_scale + out_shift).
+
+    ``x``: [B, C, H, W] channels_last, fp16/bf16. ``wp``: packed [Cout, R, S, C]. Returns y (and y2)."""
+    B, C, H, W = x.shape
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv2d_nhwc expects a channels_last input")
+    cout = wp.shape[0]
+    if wp.shape != (cout, r, s, C) or wp.dtype != x.dtype or not wp.is_contiguous():
+        raise ValueError(f"packed weight must be [Cout, {r}, {s}, {C}] {x.dtype}, got {tuple(wp.shape)} {wp.dtype}")
+    oh, ow = out_hw(H, W, r, s, stride, pad, dil)
+    y = torch.empty((B, cout, oh, ow), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    y2 = torch.empty_like(y) if out_affine is not None else None
+    if res is not None and (res.shape != y.shape or not res.is_contiguous(memory_format=torch.channels_last)
+                            or res.dtype != y.dtype):
+        raise ValueError("residual must match the output shape / dtype in channels_last")
+    for t in (bias,) + (in_affine or ()) + (out_affine or ()):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError("bias / affine vectors must be contiguous fp32")
+    geom = [B, H, W, C, cout, r, s, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], oh, ow]
+    native.load("_nn").conv_mfma(
+        x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(in_affine[0] if in_affine else None),
+        _ptr(in_affine[1] if in_affine else None), _ptr(bias), _ptr(res), _ptr(out_affine[0] if out_affine else None),
+        _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu), _DT[x.dtype],
+        torch.cuda.current_stream(x.device).cuda_stream)
+    return (y, y2) if out_affine is not None else y
+
+
+__all__ = ["supported", "pack_weight", "conv2d_nhwc", "out_hw"]

@@ -1,0 +1,80 @@
+"""MFMA implicit-GEMM convolution vs a plain fp32 PyTorch reference of the same
+fused op (prologue affine+ReLU, bias, ReLU, residual, second affine output)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, stride, pad, bias=None, relu=False, pro=None, res=None, post=None):
+    xf = x.float()
+    if pro is not None:
+        xf = torch.relu(xf * pro[0].view(1, -1, 1, 1) + pro[1].view(1, -1, 1, 1))
+    y = F.conv2d(xf, w.float(), None, stride, pad)
+    if bias is not None:
+        y = y + bias.view(1, -1, 1, 1)
+    if relu:
+        y = torch.relu(y)
+    if res is not None:
+        y = y + res.float()
+    y2 = None if post is None else torch.relu(y * post[0].view(1, -1, 1, 1) + post[1].view(1, -1, 1, 1))
+    return y, y2
+
+
+def test_exact_integer_layout():
+    """Small integers are exact in fp16 and fp32: any lane/row/col mapping error shows as a mismatch."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(-2, 3, (2, 64, 9, 7), generator=g).half().cuda().contiguous(memory_format=torch.channels_last)
+    w = torch.randint(-2, 3, (80, 64, 3, 3), generator=g).half().cuda()
+    y = conv2d_nhwc(x, pack_weight(w, torch.float16), 3, 3, (1, 1), (1, 1))
+    ref = F.conv2d(x.float(), w.float(), None, 1, 1)
+    torch.testing.assert_close(y.float(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [
+    # B, C, H, W, Cout, k, stride, pad
+    (4, 64, 56, 56, 64, 1, 1, 0),
+    (4, 64, 56, 56, 256, 1, 1, 0),
+    (2, 256, 28, 28, 128, 3, 1, 1),
+    (2, 128, 29, 29, 128, 3, 2, 1),
+    (3, 512, 14, 14, 1024, 1, 2, 0),
+    (1, 2048, 7, 7, 512, 1, 1, 0),
+])
+def test_conv_matches_fp32_reference(dtype, shape):
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    B, C, H, W, Co, k, st, pd = shape
+    torch.manual_seed(1)
+    x = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)
+    bias = torch.randn(Co, device="cuda")
+    y = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (st, st), (pd, pd), bias=bias, relu=True)
+    ref, _ = _ref(x, w, st, pd, bias=bias, relu=True)
+    tol = 2e-2 if dtype == torch.float16 else 8e-2
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+
+
+def test_prologue_residual_dual_output():
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    torch.manual_seed(2)
+    dt = torch.float16
+    B, C, H, W, Co = 2, 128, 14, 14, 256
+    x = torch.randn(B, C, H, W, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 1, 1, device="cuda") / C ** 0.5).to(dt)
+    pro = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1)
+    res = torch.randn(B, Co, H, W, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    post = (torch.rand(Co, device="cuda") + 0.5, torch.randn(Co, device="cuda") * 0.1)
+    y, y2 = conv2d_nhwc(x, pack_weight(w, dt), 1, 1, in_affine=pro, res=res, out_affine=post)
+    ry, ry2 = _ref(x, w, 1, 0, pro=pro, res=res, post=post)
+    torch.testing.assert_close(y.float(), ry, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(y2.float(), ry2, rtol=2e-2, atol=3e-2)
+    # padding taps stay zero with a prologue (3x3)
+    w3 = (torch.randn(64, C, 3, 3, device="cuda") / (9 * C) ** 0.5).to(dt)
+    y3 = conv2d_nhwc(x, pack_weight(w3, dt), 3, 3, (1, 1), (1, 1), in_affine=pro)
+    r3, _ = _ref(x, w3, 1, 1, pro=pro)
+    torch.testing.assert_close(y3.float(), r3, rtol=2e-2, atol=2e-2)

@@ -1,0 +1,58 @@
+"""Per-layer timing: MFMA implicit-GEMM conv (fused epilogue) vs MIOpen conv + separate bias/ReLU,
+ResNet-50 bottleneck shapes at batch 128, fp16 channels_last."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight  # noqa: E402
+
+SHAPES = [  # C, H, Cout, k, stride
+    (64, 56, 64, 1, 1), (64, 56, 64, 3, 1), (64, 56, 256, 1, 1), (256, 56, 64, 1, 1),
+    (128, 28, 128, 3, 1), (128, 28, 512, 1, 1), (512, 28, 128, 1, 1), (256, 56, 512, 1, 2),
+    (256, 14, 256, 3, 1), (256, 14, 1024, 1, 1), (1024, 14, 256, 1, 1),
+    (512, 7, 512, 3, 1), (512, 7, 2048, 1, 1), (2048, 7, 512, 1, 1),
+]
+
+
+def bench(fn, iters=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    B = 128
+    dt = torch.float16
+    tot_m, tot_t = 0.0, 0.0
+    for C, H, Co, k, st in SHAPES:
+        x = torch.randn(B, C, H, H, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dt)
+        wp = pack_weight(w, dt)
+        bias = torch.randn(Co, device="cuda")
+        pad = k // 2
+        t_m = bench(lambda: conv2d_nhwc(x, wp, k, k, (st, st), (pad, pad), bias=bias, relu=True))
+        wc = w.contiguous(memory_format=torch.channels_last)
+        bh = bias.to(dt)
+        t_t = bench(lambda: torch.relu_(F.conv2d(x, wc, bh, st, pad)))
+        oh = (H + 2 * pad - k) // st + 1
+        flops = 2.0 * B * oh * oh * Co * C * k * k
+        tot_m += t_m
+        tot_t += t_t
+        print(f"C={C:5d} H={H:3d} Cout={Co:5d} k={k} s={st}: mfma {t_m:8.1f} us ({flops / t_m / 1e6:7.1f} TF/s)  "
+              f"miopen+bias+relu {t_t:8.1f} us ({flops / t_t / 1e6:7.1f} TF/s)  speedup {t_t / t_m:5.2f}x")
+    print(f"TOTAL mfma {tot_m:.1f} us  miopen {tot_t:.1f} us  speedup {tot_t / tot_m:.2f}x")
+
+
+if __name__ == "__main__":
+    main()

@@ -63,7 +63,7 @@ MODULES = {
     ),
     "_nn": (
         "csrc/nn",
-        ["nn_bindings.cpp", "nn_ops.hip"],
+        ["nn_bindings.cpp", "nn_ops.hip", "conv_mfma.hip"],
         [],
     ),
 }
