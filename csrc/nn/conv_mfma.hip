@@ -6,7 +6,7 @@
 //   channel; x NHWC [B,H,W,C], w [Cout][R][S][C] (K contiguous), y NHWC.
 //   pro(v) = relu(v * in_scale[c] + in_shift[c])   (pre-activation BN+ReLU;
 //            padding taps stay 0, as in the unfused graph)
-//   epi(v) = v + bias[n]; relu (optional); + res[m, n] (optional) -> y;
+//   epi(v) = v + bias[n]; relu (relu=1); + res[m, n] (optional); relu (relu=2) -> y;
 //            optional second output y2 = relu(y * out_scale[n] + out_shift[n])
 //            (the next pre-activation block's input, written from registers).
 //
@@ -178,6 +178,9 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
   T* __restrict__ y = static_cast<T*>(a.y);
   const T* __restrict__ res = static_cast<const T*>(a.res);
   T* __restrict__ y2 = static_cast<T*>(a.y2);
+  // relu=1: before the residual add; relu=2: after it (identical without a residual)
+  const bool relu_pre = a.relu == 1 || (a.relu == 2 && res == nullptr);
+  const bool relu_post = a.relu == 2 && res != nullptr;
   if ((a.Cout & 7) == 0) {
     constexpr int CL = WN + 8;  // staged row pitch (elements)
     T* Ct = lds + wid * WM * CL;
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] + bn;
-          if (a.relu) v = fmaxf(v, 0.f);
+          if (relu_pre) v = fmaxf(v, 0.f);
           Ct[(i * 16 + 4 * (lane >> 4) + r) * CL + j * 16 + fr] = FromF<T>(v);
         }
     }
@@ -210,7 +213,10 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
         T* pe = reinterpret_cast<T*>(&pv);
         const T* re = reinterpret_cast<const T*>(&rv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pe[e] = FromF<T>(ToF(pe[e]) + ToF(re[e]));
+        for (int e = 0; e < 8; ++e) {
+          const float v = ToF(pe[e]) + ToF(re[e]);
+          pe[e] = FromF<T>(relu_post ? fmaxf(v, 0.f) : v);
+        }
       }
       *reinterpret_cast<uint4*>(y + o) = pv;
       if (y2) {
@@ -238,10 +244,10 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
         const int m = m0 + wm0 + i * 16 + 4 * (lane >> 4) + r;
         if (m >= M) continue;
         float v = acc[i][j][r] + bn;
-        if (a.relu) v = fmaxf(v, 0.f);
+        if (relu_pre) v = fmaxf(v, 0.f);
         const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
         const T c = FromF<T>(v);
-        const T vt = res ? FromF<T>(ToF(c) + ToF(res[o])) : c;
+        const T vt = res ? FromF<T>(relu_post ? fmaxf(ToF(c) + ToF(res[o]), 0.f) : ToF(c) + ToF(res[o])) : c;
         y[o] = vt;
         if (y2) y2[o] = FromF<T>(fmaxf(ToF(vt) * os + ob, 0.f));
       }

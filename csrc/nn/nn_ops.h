@@ -28,7 +28,7 @@ struct ConvArgs {
   const float* out_shift;
   void* y2;
   int B, H, W, C, Cout, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, OH, OW;
-  int relu;            // relu after bias (before the residual add)
+  int relu;            // 0 none, 1 after bias (before the residual add), 2 after the residual add
   int prologue_relu;   // relu after the prologue affine
 };
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);

@@ -115,6 +115,8 @@ class InferenceSession:
             nodes = self._fold_constants(nodes)
             nodes = self._fold_conv_bn(nodes)
             nodes = self._fuse_epilogues(nodes)
+            if self._nn is not None and self.channels_last and self.compute_dtype != torch.float32:
+                nodes = self._fuse_prologues(nodes)
         self.nodes = nodes
         self._place_constants()
         self._plan_liveness()
@@ -284,6 +286,74 @@ class InferenceSession:
                 continue
             out_nodes.append(n)
         return self._reorder([n for n in out_nodes if id(n) not in drop])
+
+    def _mfma_conv(self, n: Node) -> bool:
+        """A _FusedConv the MFMA implicit-GEMM kernel runs (2-D, one group, C % 64 == 0, relu-or-none act)."""
+        if n.op_type != "_FusedConv" or n.inputs[1] not in self._consts:
+            return False
+        w = self._consts[n.inputs[1]]
+        return (isinstance(w, torch.Tensor) and w.dim() == 4 and n.attrs.get("group", 1) == 1
+                and w.shape[1] % 64 == 0 and n.attrs.get("__act", 0) in (0, 1))
+
+    def _fuse_prologues(self, nodes: List[Node]) -> List[Node]:
+        """MFMA-conv fusions (GPU, fp16/bf16, channels_last):
+
+        * a per-channel BN(+ReLU) whose every consumer is an MFMA conv is applied in those convs' A-tile
+          loaders (prologue) instead of being materialised — the pre-activation of ResNet-v2 blocks;
+        * an ``_AddAffineAct`` whose activated output is consumed that way becomes a plain Add, which then
+          folds into the producing conv's epilogue as the residual add.
+        Input layout of a fused conv: [x, w, b, res, pro_scale, pro_shift]."""
+        outs = {o.name for o in self.outputs}
+        by_input: Dict[str, List[Node]] = {}
+        for n in nodes:
+            for x in n.inputs:
+                by_input.setdefault(x, []).append(n)
+        prod = {o: n for n in nodes for o in n.outputs}
+        drop = set()
+
+        def absorb(value: str, src: str, scale: str, shift: str, relu: bool) -> bool:
+            cs = by_input.get(value, [])
+            if value in outs or not cs or not all(self._mfma_conv(c) and c.inputs[0] == value and
+                                                  c.inputs[1:].count(value) == 0 and len(c.inputs) <= 4
+                                                  for c in cs):
+                return False
+            for c in cs:
+                while len(c.inputs) < 4:
+                    c.inputs.append("")
+                c.inputs[0] = src
+                c.inputs += [scale, shift]
+                c.attrs["__pro_relu"] = 1 if relu else 0
+                by_input.setdefault(src, []).append(c)
+            return True
+
+        new_nodes = []
+        for n in nodes:
+            if n.op_type == "_AffineAct" and n.attrs.get("__act", 0) in (0, 1):
+                if absorb(n.outputs[0], n.inputs[0], n.inputs[1], n.inputs[2], n.attrs.get("__act", 0) == 1):
+                    drop.add(id(n))
+                    continue
+            if n.op_type == "_AddAffineAct" and len(n.outputs) > 1 and n.outputs[1]:
+                if absorb(n.outputs[1], n.outputs[0], n.inputs[2], n.inputs[3], n.attrs.get("__act", 0) == 1):
+                    add = Node("Add", n.inputs[:2], [n.outputs[0]], {}, n.name)
+                    # residual epilogue: the conv producing one addend (sole consumer, no act, no residual yet)
+                    for k in (0, 1):
+                        c = prod.get(add.inputs[k])
+                        other = add.inputs[1 - k]
+                        if (c is not None and self._mfma_conv(c) and c.attrs.get("__act", 0) == 0
+                                and (len(c.inputs) < 4 or not c.inputs[3]) and c.outputs[0] not in outs
+                                and len(by_input.get(c.outputs[0], [])) == 1 and other != c.outputs[0]):
+                            while len(c.inputs) < 4:
+                                c.inputs.append("")
+                            c.inputs[3] = other
+                            c.outputs = [add.outputs[0]]
+                            add = None
+                            break
+                    if add is not None:
+                        new_nodes.append(add)
+                    drop.add(id(n))
+                    continue
+            new_nodes.append(n)
+        return self._reorder([n for n in new_nodes if id(n) not in drop])
 
     def _reorder(self, nodes: List[Node]) -> List[Node]:
         """Stable topological re-order (a fused node may read a value produced
@@ -527,15 +597,38 @@ def _affine_act(rt, x, scale, shift, res, act, alpha, out=None):
     return _affine_act_torch(x, scale, shift, res, act, alpha)
 
 
+def _mfma_ok(rt, at, inp, w) -> bool:
+    return (rt.session._nn is not None and inp.is_cuda and inp.dim() == 4 and inp.dtype in (torch.float16, torch.bfloat16)
+            and inp.dtype == w.dtype and w.dim() == 4 and at.get("group", 1) == 1 and inp.shape[1] % 64 == 0
+            and inp.is_contiguous(memory_format=torch.channels_last) and w.permute(0, 2, 3, 1).is_contiguous()
+            and at.get("__act", 0) in (0, 1) and inp.data_ptr() % 16 == 0)
+
+
 def _fused_conv(rt, at, x):
     inp, w, b = x[0], x[1], x[2]
     res = x[3] if len(x) > 3 else None
+    pro = (x[4], x[5]) if len(x) > 5 and x[4] is not None else None
     if inp.dtype != w.dtype:
         inp = inp.to(w.dtype)
+    act = at.get("__act", 0)
+    if _mfma_ok(rt, at, inp, w):
+        from ..ops.conv import conv2d_nhwc
+
+        nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+        if res is not None:
+            res = res.to(inp.dtype).contiguous(memory_format=torch.channels_last)
+        dev = inp.device
+        f32 = lambda t: None if t is None else t.to(dev, torch.float32).contiguous()  # noqa: E731
+        y = conv2d_nhwc(inp, w.permute(0, 2, 3, 1), w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]),
+                        dil, bias=f32(b), relu=2 if act == 1 else 0,
+                        in_affine=(f32(pro[0]), f32(pro[1])) if pro is not None else None,
+                        in_relu=bool(at.get("__pro_relu", 1)), res=res)
+        return [y]
+    if pro is not None:  # prologue outside the kernel (fallback path)
+        inp = _affine_act(rt, inp, pro[0], pro[1], None, 1 if at.get("__pro_relu", 1) else 0, 0.0)
     nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
     inp, pad = _sym_pad(inp, pb, pe)
     f = {1: torch.nn.functional.conv1d, 2: torch.nn.functional.conv2d, 3: torch.nn.functional.conv3d}[nd]
-    act = at.get("__act", 0)
     if rt.session._nn is None:
         # host path: bias inside the conv, epilogue as torch ops
         y = f(inp, w, b.to(w.dtype) if b is not None else None, stride=strides, padding=pad, dilation=dil,

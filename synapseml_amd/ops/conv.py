@@ -23,8 +23,11 @@ def pack_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 
 def out_hw(h: int, w: int, r: int, s: int, stride: Sequence[int], pad: Sequence[int], dil: Sequence[int]):
-    oh = (h + 2 * pad[0] - dil[0] * (r - 1) - 1) // stride[0] + 1
-    ow = (w + 2 * pad[1] - dil[1] * (s - 1) - 1) // stride[1] + 1
+    """``pad`` = (top, left) symmetric or (top, left, bottom, right)."""
+    pt, pl = pad[0], pad[1]
+    pb, pr = (pad[2], pad[3]) if len(pad) == 4 else (pt, pl)
+    oh = (h + pt + pb - dil[0] * (r - 1) - 1) // stride[0] + 1
+    ow = (w + pl + pr - dil[1] * (s - 1) - 1) // stride[1] + 1
     return oh, ow
 
 
@@ -33,13 +36,15 @@ def _ptr(t: Optional[torch.Tensor]) -> int:
 
 
 def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
-                bias: Optional[torch.Tensor] = None, relu: bool = False,
+                bias: Optional[torch.Tensor] = None, relu=False,
                 in_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, in_relu: bool = True,
                 res: Optional[torch.Tensor] = None,
                 out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
-    """y = [relu](conv(pro(x), w) + bias) [+ res]; optionally also y2 = relu(y * out_scale + out_shift).
+    """y = conv(pro(x), w) + bias, ReLU, + res; optionally also y2 = relu(y * out_scale + out_shift).
 
-    ``x``: [B, C, H, W] channels_last, fp16/bf16. ``wp``: packed [Cout, R, S, C]. Returns y (and y2)."""
+    ``relu``: False/0 none, True/1 before the residual add, 2 after it. ``pad``: (top, left) or
+    (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp16/bf16. ``wp``: packed [Cout, R, S, C]
+    (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2)."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv2d_nhwc expects a channels_last input")

@@ -364,3 +364,35 @@ def test_image_featurizer_gpu_matches_cpu():
 
     g, c = run("GPU"), run("CPU")
     np.testing.assert_allclose(g, c, rtol=0, atol=2e-3 * np.abs(c).max())
+
+
+def test_prologue_fusion_pass_cpu_fallback():
+    """The MFMA prologue/residual rewrite (normally GPU-only) applied on CPU: the fallback runtime path must give
+    the same numbers, and the v2 pre-activations disappear from the graph."""
+    data = writer.resnet50_v2(seed=11)
+    x = np.random.default_rng(12).random((1, 3, 64, 64), dtype=np.float32)
+    sess = InferenceSession(data, device="cpu")
+    ref = sess.run(None, {"data": x})[0]
+    before = [n.op_type for n in sess.nodes]
+    sess.nodes = sess._fuse_prologues(sess.nodes)
+    sess._plan_liveness()
+    after = [n.op_type for n in sess.nodes]
+    assert after.count("_AffineAct") < before.count("_AffineAct")
+    assert after.count("_AddAffineAct") < before.count("_AddAffineAct")
+    assert sum(1 for n in sess.nodes if n.op_type == "_FusedConv" and len(n.inputs) > 5) >= 16
+    out = sess.run(None, {"data": x})[0]
+    np.testing.assert_allclose(out, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+def test_gpu_mfma_fused_resnet_matches_cpu(prec):
+    data = writer.resnet50_v2(seed=13)
+    x = np.random.default_rng(14).random((8, 3, 224, 224), dtype=np.float32)
+    cpu = InferenceSession(data, device="cpu").run(None, {"data": x})[0]
+    sess = InferenceSession(data, device="cuda", precision=prec)
+    fused = [n for n in sess.nodes if n.op_type == "_FusedConv" and len(n.inputs) > 5]
+    assert len(fused) >= 16  # pre-activations folded into MFMA conv prologues
+    out = sess.run(None, {"data": x})[0]
+    assert np.corrcoef(out.ravel(), cpu.ravel())[0, 1] > (0.999 if prec == "fp16" else 0.995)
+    assert (out.argmax(1) == cpu.argmax(1)).mean() >= 0.75
