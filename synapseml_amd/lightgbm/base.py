@@ -16,6 +16,8 @@ C8 in SURVEY §2.5) and histograms are allreduced over RCCL inside the engine.
 from __future__ import annotations
 
 import logging
+import json
+import os
 import time
 from typing import List, Optional
 
@@ -214,6 +216,36 @@ class LightGBMBase(Estimator, LightGBMParams):
         return sb.result
 
     # ------------------------------------------------------------- fit
+    # ------------------------------------------------------------- checkpoints
+    def _ckpt_latest(self) -> Optional[dict]:
+        d = self.getCheckpointDir()
+        if not d or not self.getResumeFromCheckpoint():
+            return None
+        p = os.path.join(d, "latest.json")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            meta = json.load(f)
+        with open(os.path.join(d, meta["model"])) as f:
+            meta["model_str"] = f.read()
+        return meta
+
+    def _ckpt_write(self, model_str: str, batch: int, iteration: int, complete: bool) -> None:
+        d = self.getCheckpointDir()
+        if not d or D.rank() != 0:
+            return
+        os.makedirs(d, exist_ok=True)
+        name = f"model_b{batch}_i{iteration}.txt"
+        tmp = os.path.join(d, name + ".tmp")
+        with open(tmp, "w") as f:
+            f.write(model_str)
+        os.replace(tmp, os.path.join(d, name))
+        meta = {"model": name, "batch": batch, "iteration": iteration, "complete": complete}
+        tmp = os.path.join(d, "latest.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f)
+        os.replace(tmp, os.path.join(d, "latest.json"))
+
     def _fit(self, df: DataFrame):
         self._measures = []
         nb = self.getNumBatches()
@@ -222,11 +254,25 @@ class LightGBMBase(Estimator, LightGBMParams):
         booster = None
         num_class = self._num_class(df)
         delegate = self.getDelegate()
+        ck = self._ckpt_latest()
+        start_batch, self._resume_done = 0, 0
+        if ck is not None:
+            model_str = ck["model_str"]
+            start_batch = ck["batch"] + (1 if ck["complete"] else 0)
+            self._resume_done = 0 if ck["complete"] else ck["iteration"]
+            log.info("resuming from checkpoint %s (batch %d, iteration %d)", ck["model"], ck["batch"], ck["iteration"])
+            if start_batch >= len(batches):
+                return self._make_model(LightGBMBooster(model_str), num_class)
         for bi, batch in enumerate(batches):
+            if bi < start_batch:
+                continue
             if delegate is not None:
                 delegate.beforeTrainBatch(bi, log, batch, booster)
             booster = self._train_batch(batch, model_str, bi, num_class)
             model_str = booster.modelStr
+            self._resume_done = 0
+            if self.getCheckpointDir():
+                self._ckpt_write(model_str, bi, self.getNumIterations(), True)
             if delegate is not None:
                 delegate.afterTrainBatch(bi, log, batch, booster)
         return self._make_model(booster, num_class)
@@ -394,8 +440,9 @@ class LightGBMBase(Estimator, LightGBMParams):
         best_result = None
         provide_train = self.getIsProvideTrainingMetric()
         t0 = time.perf_counter()
+        it = getattr(self, "_resume_done", 0)  # iterations already in a resumed checkpoint of this batch
         num_iter = self.getNumIterations()
-        it = 0
+        ck_every = self.getCheckpointInterval() if self.getCheckpointDir() else 0
         finished = False
         while not finished and it < num_iter:
             if delegate is not None:
@@ -439,6 +486,8 @@ class LightGBMBase(Estimator, LightGBMParams):
                 delegate.afterTrainIteration(batch_index, D.rank(), it, log, None, nb, has_valid, finished,
                                              train_res, valid_res)
             it += 1
+            if ck_every > 0 and it % ck_every == 0 and not finished and it < num_iter:
+                self._ckpt_write(nb.save_model_string(), batch_index, it, False)
         nb.synchronize()
         m.mark("training_iterations_ms", (time.perf_counter() - t0) * 1e3)
         return best_result

@@ -81,6 +81,11 @@ class LightGBMLearnerParams(LightGBMDatasetParams):
     maxDepth = Param("Max depth", -1, T.toInt)
     minSumHessianInLeaf = Param("Minimal sum hessian in one leaf", 1e-3, T.toFloat)
     modelString = Param("LightGBM model to retrain", "", T.toString)
+    checkpointDir = Param("Directory for periodic training checkpoints (model text); fit resumes from the latest "
+                          "one when resumeFromCheckpoint is set", None, T.toString)
+    checkpointInterval = Param("Write a checkpoint every this many iterations (0 = off)", 0, T.toInt)
+    resumeFromCheckpoint = Param("Resume from the latest checkpoint in checkpointDir if one exists", True,
+                                 T.toBoolean)
     verbosity = Param("Verbosity where lt 0 is Fatal, eq 0 is Error, eq 1 is Info, gt 1 is Debug", -1, T.toInt)
     boostFromAverage = Param("Adjusts initial score to the mean of labels for faster convergence", True, T.toBoolean)
     boostingType = Param("Default gbdt = traditional Gradient Boosting Decision Tree. Options: gbdt, rf, dart, goss", "gbdt", T.toString)

@@ -29,11 +29,25 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _injected_fault(rank: int) -> Optional[str]:
+    """Test-only fault injection: ``SML_FAULT_INJECT="<rank>:<kind>"`` with kind in
+    raise | crash_before | crash_after_init | empty (the rank sees an empty partition)."""
+    spec = os.environ.get("SML_FAULT_INJECT", "")
+    for item in filter(None, spec.split(",")):
+        r, _, kind = item.partition(":")
+        if r.strip() == str(rank):
+            return kind.strip()
+    return None
+
+
 def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, parts_bytes: bytes, out_dir: str,
             use_gpu: bool) -> None:
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     result: Any
+    fault = _injected_fault(rank)
+    if fault == "crash_before":
+        os._exit(17)  # hard crash before the rendezvous (test-only, SML_FAULT_INJECT)
     try:
         import torch
         import torch.distributed as dist
@@ -44,6 +58,12 @@ def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, par
                                 world_size=world)
         fn = pickle.loads(fn_bytes)
         part = pickle.loads(parts_bytes)
+        if fault == "raise":
+            raise RuntimeError(f"injected fault on rank {rank}")
+        if fault == "crash_after_init":
+            os._exit(18)  # dies while the other ranks wait in collectives
+        if fault == "empty":
+            part = part.slice(0, 0)
         result = ("ok", fn(part, rank, world))
         dist.barrier()
         dist.destroy_process_group()
@@ -79,12 +99,45 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
             p = ctx.Process(target=_worker, args=(r, world, port, backend, fn_bytes, pickle.dumps(parts[r]), d, use_gpu))
             p.start()
             procs.append(p)
-        for p in procs:
-            p.join(timeout_s)
+        # fail fast: a rank that exits with an error (or dies) aborts the job instead of leaving the others
+        # blocked in collectives until the timeout (the reference waits for the Spark task timeout)
+        import time as _time
+
+        deadline = _time.monotonic() + timeout_s
+        failed = None
+        while any(p.is_alive() for p in procs):
+            for r, p in enumerate(procs):
+                if p.is_alive():
+                    continue
+                path = os.path.join(d, f"result_{r}.pkl")
+                if p.exitcode != 0 or not os.path.exists(path):
+                    failed = failed or (r, f"exit code {p.exitcode}")
+                else:
+                    with open(path, "rb") as f:
+                        st = pickle.load(f)[0]  # written by our own worker process
+                    if st != "ok":
+                        failed = failed or (r, "task error")
+            if failed or _time.monotonic() > deadline:
+                break
+            _time.sleep(0.05)
         for p in procs:
             if p.is_alive():
                 p.terminate()
-                p.join()
+                p.join(10)
+                if p.is_alive():
+                    p.kill()
+                    p.join()
+        if failed is not None:
+            r, why = failed
+            path = os.path.join(d, f"result_{r}.pkl")
+            if os.path.exists(path):
+                with open(path, "rb") as f:
+                    st, val = pickle.load(f)  # written by our own worker process
+                if st != "ok":
+                    why = val
+            raise RuntimeError(f"worker {r} failed ({why}); the job was aborted on the remaining ranks")
+        if _time.monotonic() > deadline:
+            raise TimeoutError(f"partition tasks did not finish within {timeout_s}s")
         results = []
         for r in range(world):
             path = os.path.join(d, f"result_{r}.pkl")

@@ -46,3 +46,32 @@ def test_data_parallel_matches_single_process(est_cls):
         return [l for l in m.getNativeModel().splitlines() if l.startswith(("split_feature=", "threshold="))]
 
     assert splits(single) == splits(dist_model)
+
+
+def _sleepy_allreduce(part, rank, world):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.ones(1)
+    dist.all_reduce(t)  # a dead peer would leave this blocked until the timeout
+    return float(t.item())
+
+
+@pytest.mark.parametrize("kind", ["raise", "crash_after_init", "crash_before"])
+def test_rank_failure_aborts_fast(monkeypatch, kind):
+    """A failing / dying rank aborts the whole job promptly with a driver-visible error (fault injection,
+    SURVEY §5.3) instead of blocking the other ranks in collectives until the timeout."""
+    import time
+
+    monkeypatch.setenv("SML_FAULT_INJECT", f"1:{kind}")
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="worker 1"):
+        run_partitions(_sleepy_allreduce, DataFrame({"x": np.arange(4)}, num_partitions=2), num_workers=2,
+                       timeout_s=300)
+    assert time.monotonic() - t0 < 120
+
+
+def test_empty_partition_rank_still_joins(monkeypatch):
+    monkeypatch.setenv("SML_FAULT_INJECT", "1:empty")
+    out = run_partitions(_allreduce_task, DataFrame({"x": np.arange(8.0)}, num_partitions=2), num_workers=2)
+    assert len(out) == 2

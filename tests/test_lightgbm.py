@@ -272,3 +272,38 @@ def test_ranker_lambdarank_ndcg():
         ideal = [(2 ** r - 1) / np.log2(i + 2) for i, r in enumerate(sorted([r for _, r in items], reverse=True)[:5])]
         nd.append(sum(gains) / sum(ideal) if sum(ideal) > 0 else 1.0)
     assert np.mean(nd) > 0.85
+
+
+def test_checkpoint_resume_matches_uninterrupted(tmp_path):
+    """Kill training mid-way (a delegate raises at iteration 12), fit again with the same checkpointDir:
+    training resumes from the last checkpoint (iteration 10) and ends with the same model as an
+    uninterrupted run."""
+    from synapseml_amd.lightgbm import LightGBMClassifier
+    from synapseml_amd.lightgbm.delegate import LightGBMDelegate
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((3000, 6))
+    y = (X[:, 0] + 0.5 * X[:, 1] > 0).astype(float)
+    df = DataFrame({"features": X, "label": y})
+
+    class Crash(LightGBMDelegate):
+        def afterTrainIteration(self, batchIndex, partitionId, curIters, log, trainParams, booster, hasValid,
+                                finished, trainRes, validRes):
+            if curIters == 12:
+                raise RuntimeError("simulated executor loss")
+
+    ck = str(tmp_path / "ck")
+    base = dict(numIterations=20, numLeaves=7, deviceType="cpu", checkpointDir=ck, checkpointInterval=5)
+    with pytest.raises(RuntimeError, match="simulated"):
+        LightGBMClassifier(**base, delegate=Crash()).fit(df)
+    import json
+    import os
+
+    meta = json.load(open(os.path.join(ck, "latest.json")))
+    assert meta["iteration"] == 10 and not meta["complete"]
+    resumed = LightGBMClassifier(**base).fit(df)
+    full = LightGBMClassifier(numIterations=20, numLeaves=7, deviceType="cpu").fit(df)
+    assert resumed.getModel().native.num_total_model == 20
+    np.testing.assert_allclose(resumed.transform(df)["probability"], full.transform(df)["probability"],
+                               rtol=1e-9, atol=1e-12)
+    assert json.load(open(os.path.join(ck, "latest.json")))["complete"]
