@@ -18,6 +18,8 @@ namespace sml {
 
 struct TrainStats {
   double hist_ms = 0, split_ms = 0, partition_ms = 0, grad_ms = 0, score_ms = 0, comm_ms = 0;
+  // device-side (hipEvent) time of whole tree growths and score updates; device memory in use after Init
+  double device_tree_ms = 0, device_score_ms = 0, device_mem_mb = 0;
   int64_t trees = 0;
 };
 

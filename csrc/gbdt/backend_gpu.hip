@@ -25,6 +25,8 @@
 #include <numeric>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "backend.h"
 #include "hip_common.h"
 
@@ -971,6 +973,7 @@ class GpuBackend : public TrainBackend {
   explicit GpuBackend(int dev) : dev_(dev) {}
   ~GpuBackend() override {
     if (stream_) { (void)hipStreamSynchronize(stream_); (void)hipStreamDestroy(stream_); }
+    for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
     if (pinned_) (void)hipHostFree(pinned_);
   }
   std::string Name() const override { return "hip"; }
@@ -1061,7 +1064,10 @@ class GpuBackend : public TrainBackend {
     up_d_.alloc(L_ + 4);
     leaf_idx_.alloc(n_);
     SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
+    for (hipEvent_t& e : ev_) SML_HIP_CHECK(hipEventCreate(&e));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) stats.device_mem_mb = (total_b - free_b) / 1048576.0;
   }
 
   void SetScores(const std::vector<double>& s) override {
@@ -1128,6 +1134,13 @@ class GpuBackend : public TrainBackend {
   void Synchronize() override { SML_HIP_CHECK(hipStreamSynchronize(stream_)); }
 
   Tree TrainTree(int k, const std::vector<char>& fmask_in) override {
+    roctxRangePushA("sml::TrainTree");
+    if (score_pending_ && hipEventQuery(ev_[3]) == hipSuccess) {
+      float sms = 0.f;
+      if (hipEventElapsedTime(&sms, ev_[2], ev_[3]) == hipSuccess) stats.device_score_ms += sms;
+      score_pending_ = false;
+    }
+    SML_HIP_CHECK(hipEventRecord(ev_[0], stream_));
     std::vector<int8_t> fmask(F_, 1);
     for (int f = 0; f < F_ && f < static_cast<int>(fmask_in.size()); ++f) fmask[f] = fmask_in[f] ? 1 : 0;
     SML_HIP_CHECK(hipMemcpyAsync(mask_.get(), fmask.data(), F_, hipMemcpyHostToDevice, stream_));
@@ -1163,17 +1176,26 @@ class GpuBackend : public TrainBackend {
       EnqueueHistogram(g, h);
       EnqueueFindChoose();
     }
+    SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
     // read the tree back (one transfer, one sync)
     Tree t = ReadTree();
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev_[0], ev_[1]) == hipSuccess) stats.device_tree_ms += ms;
+    roctxRangePop();
     return t;
   }
 
   void UpdateScore(const Tree& t, int k, double scale) override {
+    roctxRangePushA("sml::UpdateScore");
     DevTreeView tv = UploadTree(t);
+    SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
     hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
                        reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
                        score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
     SML_HIP_CHECK(hipGetLastError());
+    SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
+    score_pending_ = true;
+    roctxRangePop();
   }
 
   void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) override {
@@ -1327,6 +1349,8 @@ class GpuBackend : public TrainBackend {
   }
 
   static constexpr size_t kPinnedBytes = 4 << 20;
+  hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};  // tree start/end, score start/end
+  bool score_pending_ = false;
   int dev_ = -1;
   hipStream_t stream_ = nullptr;
   const Dataset* data_ = nullptr;

@@ -217,6 +217,8 @@ PYBIND11_MODULE(_gbdt, m) {
           d["grad_ms"] = s->grad_ms; d["hist_ms"] = s->hist_ms; d["split_ms"] = s->split_ms;
           d["partition_ms"] = s->partition_ms; d["score_ms"] = s->score_ms; d["comm_ms"] = s->comm_ms;
           d["trees"] = s->trees;
+          d["device_tree_ms"] = s->device_tree_ms; d["device_score_ms"] = s->device_score_ms;
+          d["device_mem_mb"] = s->device_mem_mb;
         }
         return d;
       });

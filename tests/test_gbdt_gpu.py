@@ -131,3 +131,15 @@ def test_gpu_training_is_deterministic():
     m1 = _train(X, y, p, 8).save_model_string()
     m2 = _train(X, y, p, 8).save_model_string()
     assert m1 == m2
+
+
+def test_gpu_device_stats_populated():
+    """Device-side timings (hipEvent pairs) and memory in use are reported
+    through Booster.stats()."""
+    X, y = _data(n=100000, f=10, seed=5)
+    b = _train(X, y, "objective=binary num_leaves=31 device_type=gpu", 6)
+    s = b.stats()
+    assert s["trees"] == 6
+    assert s["device_tree_ms"] > 0.0
+    assert s["device_score_ms"] > 0.0
+    assert s["device_mem_mb"] > 1.0

@@ -49,7 +49,7 @@ MODULES = {
             "backend_gpu.hip",
             "predict_gpu.hip",
         ],
-        ["-lrccl"],
+        ["-lrccl", "-lrocprofiler-sdk-roctx"],
     ),
     "_vw": (
         "csrc/vw",
