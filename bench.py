@@ -159,6 +159,9 @@ def main() -> None:
                 "backend": booster.backend,
                 "train_auc_sample": auc,
                 "setup_s": round(setup_s, 2),
+                "histogram_allreduce": (None if world == 1 else "host (gloo)" if not use_gpu else
+                                        "p2p-ipc one-shot" if D.p2p_status.get("active") else
+                                        "rccl (%s)" % D.p2p_status.get("reason", "")),
             },
         }
         print(json.dumps(out), flush=True)

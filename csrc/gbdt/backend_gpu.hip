@@ -1254,6 +1254,7 @@ class GpuBackend : public TrainBackend {
     const int NI = L_ - 1;
     SML_HIP_CHECK(hipMemcpyAsync(pinned_, blob_.get(), blob_bytes_, hipMemcpyDeviceToHost, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (comm_) comm_->Check();
     const uint8_t* hb = static_cast<const uint8_t*>(pinned_);
     DState st;
     std::memcpy(&st, hb, sizeof(DState));

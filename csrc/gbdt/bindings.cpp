@@ -139,6 +139,23 @@ PYBIND11_MODULE(_gbdt, m) {
     });
     return c;
   });
+  m.def("p2p_comm", [](PyComm& base, int device, int64_t cap_bytes, double timeout_ms) {
+    PyComm c;
+    std::string why;
+    {
+      py::gil_scoped_release rel;  // the base host allreduce may call back into Python
+      c.c = NewP2pComm(base.c, device, cap_bytes, timeout_ms, &why);
+    }
+    return py::make_tuple(c, why.empty(), why);
+  }, py::arg("base"), py::arg("device"), py::arg("cap_bytes") = 1 << 20, py::arg("timeout_ms") = 60000.0);
+  m.def("comm_device_allreduce", [](PyComm& c, std::vector<double> x, int reps) {
+    py::gil_scoped_release rel;
+    return CommDeviceAllReduce(c.c.get(), x, reps);
+  }, py::arg("comm"), py::arg("x"), py::arg("reps") = 1);
+  m.def("comm_device_allreduce_us", [](PyComm& c, int64_t n, int iters) {
+    py::gil_scoped_release rel;
+    return CommDeviceAllReduceUs(c.c.get(), n, iters);
+  });
   m.def("rccl_unique_id", []() { return py::bytes(RcclGetUniqueId()); });
   m.def("rccl_comm", [](py::bytes uid, int rank, int world, int device) {
     PyComm c;

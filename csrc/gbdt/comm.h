@@ -8,7 +8,9 @@
 #pragma once
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <string>
+#include <vector>
 
 namespace sml {
 
@@ -23,6 +25,8 @@ class Comm {
   virtual void AllReduceDeviceF32(float* buf, int64_t n, void* stream) = 0;
   virtual void AllReduceDeviceF64(double* buf, int64_t n, void* stream) = 0;
   virtual bool is_device() const { return false; }
+  // raise if an asynchronous collective failed (checked once per tree)
+  virtual void Check() {}
 };
 
 class HostComm : public Comm {
@@ -43,5 +47,16 @@ class HostComm : public Comm {
 // RCCL communicator (defined in comm_rccl.cpp)
 std::string RcclGetUniqueId();
 Comm* NewRcclComm(const std::string& unique_id, int rank, int world, int device);
+
+// One-shot P2P (IPC) allreduce for device messages up to cap_bytes, layered on
+// `base` (used for the handle exchange, validation, host reductions and large
+// messages). Falls back to `base` on every rank if set-up or the start-up
+// self-test fails anywhere; *reason then says why. (comm_p2p.hip)
+std::shared_ptr<Comm> NewP2pComm(std::shared_ptr<Comm> base, int device, int64_t cap_bytes, double timeout_ms,
+                                 std::string* reason);
+// test / benchmark helpers: allreduce a host vector through the device path;
+// average microseconds per device allreduce of n doubles
+std::vector<double> CommDeviceAllReduce(Comm* c, const std::vector<double>& x, int reps);
+double CommDeviceAllReduceUs(Comm* c, int64_t n, int iters);
 
 }  // namespace sml

@@ -114,6 +114,35 @@ def allreduce_numpy(a: np.ndarray) -> None:
 
 
 _comm_cache: dict = {}
+p2p_status: dict = {}
+
+
+def _single_node() -> bool:
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    if lw is not None:
+        return int(lw) == world_size()
+    import socket
+
+    hosts = all_gather_object(socket.gethostname())
+    return len(set(hosts)) == 1
+
+
+def maybe_p2p(comm, device: int):
+    """Wrap a device communicator in the intra-node one-shot P2P allreduce
+    (see :func:`gbdt_comm`). The decision is collective: every rank calls
+    this and all end up on the same path."""
+    from ..ops import native
+
+    want = os.environ.get("SML_GBDT_P2P", "1") != "0" and world_size() <= 8 and _single_node()
+    # agree before touching IPC so no rank waits in the self-test alone
+    flags = all_gather_object(bool(want))
+    if not all(flags):
+        p2p_status.update(active=False, reason="disabled or multi-node")
+        return comm
+    cap = int(os.environ.get("SML_GBDT_P2P_CAP", str(1 << 20)))
+    c, ok, why = native.gbdt().p2p_comm(comm, device, cap, float(os.environ.get("SML_GBDT_P2P_TIMEOUT_MS", "60000")))
+    p2p_status.update(active=bool(ok), reason=why)
+    return c
 
 
 def gbdt_comm(use_gpu: bool):
@@ -123,6 +152,13 @@ def gbdt_comm(use_gpu: bool):
     over the control plane, so histogram allreduces are enqueued on the
     engine's own HIP stream with no Python round trip; CPU runs get a host
     communicator that reduces through the default (gloo) group.
+
+    When every rank is on one node the RCCL communicator is wrapped in the
+    one-shot P2P allreduce (``csrc/gbdt/comm_p2p.hip``, K21): per-split
+    histograms (~114 KB) go over xGMI in a single kernel instead of a
+    latency-bound ring; larger messages still use RCCL.  ``SML_GBDT_P2P=0``
+    disables it; if IPC set-up or its start-up self-test fails on any rank,
+    all ranks stay on RCCL together.
     """
     if world_size() <= 1:
         return None
@@ -139,6 +175,7 @@ def gbdt_comm(use_gpu: bool):
 
         dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
         c = g.rccl_comm(uid, rank(), world_size(), dev)
+        c = maybe_p2p(c, dev)
     else:
         c = g.host_comm(rank(), world_size(), lambda arr: allreduce_numpy(arr))
     _comm_cache[key] = c

@@ -143,3 +143,23 @@ def test_gpu_device_stats_populated():
     assert s["device_tree_ms"] > 0.0
     assert s["device_score_ms"] > 0.0
     assert s["device_mem_mb"] > 1.0
+
+
+def test_p2p_allreduce_two_ranks_one_gpu():
+    """K21 one-shot P2P allreduce: two processes share the box's GPU through
+    IPC; exact sums, and data-parallel GBDT over it equals the host comm."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29533", os.path.join(root, "tools", "p2p_check.py")]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 2, p.stdout[-2000:] + p.stderr[-3000:]
+    for o in lines:
+        assert o["p2p_active"], o
+        assert o["allreduce_exact"] and o["train_models_equal"] and o["ranks_agree"], o

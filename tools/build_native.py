@@ -48,6 +48,7 @@ MODULES = {
             "bindings.cpp",
             "backend_gpu.hip",
             "predict_gpu.hip",
+            "comm_p2p.hip",
         ],
         ["-lrccl", "-lrocprofiler-sdk-roctx"],
     ),
