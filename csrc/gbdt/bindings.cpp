@@ -260,6 +260,20 @@ PYBIND11_MODULE(_gbdt, m) {
              return out;
            },
            py::arg("X"), py::arg("normal") = false)
+      .def("predict_contrib", [](GpuPredictor& p, const Booster& b, F64 X) -> py::object {
+        const int64_t n = X.shape(0);
+        py::array_t<double> out({n, static_cast<int64_t>((b.NumFeatures() + 1) * p.NumOutputs())});
+        double* o = out.mutable_data();
+        const double* x = X.data();
+        const int nc = static_cast<int>(X.shape(1));
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = p.PredictContrib(x, n, nc, o);
+        }
+        if (!ok) return py::none();
+        return out;
+      })
       .def("predict_leaf", [](GpuPredictor& p, F64 X) {
         const int64_t n = X.shape(0);
         py::array_t<int32_t> out({n, static_cast<int64_t>(p.NumTrees())});

@@ -19,9 +19,13 @@ class GpuPredictor {
   int NumTrees() const { return num_trees_; }
   void Predict(const double* X, int64_t n, int ncols, bool normal, double* out);
   void PredictLeaf(const double* X, int64_t n, int ncols, int32_t* out);
+  // TreeSHAP contributions, layout of Booster::Predict(kPredictContrib);
+  // false if a path has more unique features than a wave64 holds
+  bool PredictContrib(const double* X, int64_t n, int ncols, double* out);
 
  private:
   struct Impl;
+  bool BuildShap();
   std::unique_ptr<Impl> impl_;
   const Booster* booster_;
   int num_out_ = 1, num_trees_ = 0;

@@ -147,8 +147,16 @@ class LightGBMBooster:
             return gp.predict_leaf(X).astype(np.float64)
         return self.native.predict(X, 2, self.startIteration, self.numIterations)
 
-    def featuresShap(self, X, disable_shape_check=False) -> np.ndarray:  # noqa: N802
+    def featuresShap(self, X, disable_shape_check=False, device="gpu") -> np.ndarray:  # noqa: N802
+        """TreeSHAP contributions, (numFeatures + 1) * numClasses per row (last
+        column of each class block is the expected value). Batches go to the
+        HIP TreeSHAP kernel (K10, ``csrc/gbdt/predict_gpu.hip``)."""
         X = self._shape(X, disable_shape_check)
+        gp = self._gpu(device) if X.shape[0] >= _GPU_BATCH_MIN_ROWS else None
+        if gp is not None:
+            out = gp.predict_contrib(self.native, X)
+            if out is not None:
+                return out
         return self.native.predict(X, 3, self.startIteration, self.numIterations)
 
     def getFeatureImportances(self, importance_type: str = "split") -> np.ndarray:  # noqa: N802

@@ -163,3 +163,33 @@ def test_p2p_allreduce_two_ranks_one_gpu():
     for o in lines:
         assert o["p2p_active"], o
         assert o["allreduce_exact"] and o["train_models_equal"] and o["ranks_agree"], o
+
+
+@pytest.mark.parametrize("kind", ["binary_nan_cat", "multiclass", "rf"])
+def test_gpu_treeshap_matches_cpu(kind):
+    """K10: wave64 path-packed TreeSHAP vs the host recursion."""
+    from synapseml_amd.ops import native
+
+    g = native.gbdt()
+    if kind == "binary_nan_cat":
+        X, y = _data(n=30000, f=10, seed=11, nan_frac=0.05, cat=True)
+        p = "objective=binary num_leaves=31 categorical_feature=0 device_type=gpu"
+    elif kind == "multiclass":
+        X, _ = _data(n=30000, f=10, seed=12)
+        y = (np.digitize(X[:, 0] + X[:, 1], [-0.7, 0.7])).astype(np.float32)
+        p = "objective=multiclass num_class=3 num_leaves=31 device_type=gpu"
+    else:
+        X, y = _data(n=30000, f=10, seed=13)
+        p = "objective=binary boosting=rf bagging_fraction=0.7 bagging_freq=1 num_leaves=63 device_type=gpu"
+    b = _train(X, y, p, 12)
+    Xt = np.ascontiguousarray(X[:3000])
+    cpu = b.predict(Xt, 3, 0, -1)
+    gp = g.GpuPredictor(b, 0, -1, -1)
+    gpu = gp.predict_contrib(b, Xt)
+    assert gpu is not None and gpu.shape == cpu.shape
+    np.testing.assert_allclose(gpu, cpu, rtol=1e-9, atol=1e-9)
+    # local accuracy: contributions sum to the raw score
+    raw = b.predict(Xt, 0, 0, -1)
+    K = raw.shape[1]
+    sums = gpu.reshape(len(Xt), K, -1).sum(-1)
+    np.testing.assert_allclose(sums, raw, rtol=1e-8, atol=1e-8)
