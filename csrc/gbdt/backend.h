@@ -11,6 +11,7 @@
 #include "config.h"
 #include "dataset.h"
 #include "objective.h"
+#include "sampling.h"
 #include "split_math.h"
 #include "tree.h"
 
@@ -37,6 +38,9 @@ class TrainBackend {
   virtual void GetGradients(std::vector<float>* g, std::vector<float>* h) = 0;
   // Restrict training rows (bagging/GOSS). nullptr = all rows.
   virtual void SetBag(const std::vector<int32_t>* rows) = 0;
+  // Draw the bag (and apply GOSS gradient scaling) where the gradients live.
+  // Returns false when the backend leaves sampling to the host.
+  virtual bool SampleRows(const RowSampleSpec& spec) { (void)spec; return false; }
   virtual Tree TrainTree(int k, const std::vector<char>& feature_mask) = 0;
   // score[k] += scale * tree(row) for every training row
   virtual void UpdateScore(const Tree& t, int k, double scale) = 0;

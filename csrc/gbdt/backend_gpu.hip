@@ -2,8 +2,11 @@
 // MI355X with the binned matrix, gradients, scores and row partitions resident
 // in HBM. Kernels:
 //   K2 gradients      grad_kernel           one thread per row, fused objective
+//                     lambdarank_kernel     one wave per query, pairwise lambdas
+//   K8 sampling       goss_key/radix_*/     bagging + GOSS (exact radix top-k)
+//                     sample_kernel         with ballot compaction
 //   K3 histogram      hist_kernel           LDS-privatised per-block histograms
-//                                           (ds_add_f32), fixed-order slab reduce
+//                                           (packed u64 fixed point), exact slab reduce
 //   K4 subtraction    find_split_kernel     larger child = parent - smaller
 //   K5 split search   find_split_kernel     one block per (feature, child), bins
 //                                           on lanes, fp64 prefix scan
@@ -185,6 +188,256 @@ __global__ __launch_bounds__(256) void grad_kernel(ObjParams p, const double* __
     }
   }
   if (partial) BlockMaxPartial(mg, mh, partial);
+}
+
+// ---------------------------------------------------------------- K2 (ranking)
+// LambdaRank gradients, one wave64 workgroup per query (grid-stride over
+// queries). A document's rank is the number of documents that score higher
+// (ties broken by index = the host's stable sort); each lane then owns
+// documents and accumulates the lambdas of every pair its document is part of,
+// so there are no atomics and the result does not depend on scheduling. Pairs
+// are kept exactly as in Objective::LambdarankGradients: different labels and
+// min(rank) < max_position. Queries of up to kRankLds documents keep scores,
+// labels and ranks in LDS and the lambdas in registers; longer ones stream
+// them from global memory (ranks and unnormalised lambdas in scratch).
+constexpr int kRankLds = 256;
+constexpr int kRankPerLane = kRankLds / 64;
+
+struct RankTables {
+  const int32_t* qb;
+  const double* inv_max_dcg;
+  const double* gain;
+  int32_t* rank_scratch;
+  double* lam_scratch;
+  double* hes_scratch;
+  int nq, ngain, max_position, norm;
+  double sigma;
+};
+
+__device__ __forceinline__ double WaveSumD(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// lambda / hessian contribution of the pair (doc i, doc j) to doc i
+__device__ __forceinline__ void PairLambda(const RankTables& t, double si, int li, int ri, double sj, int lj, int rj,
+                                           double imd, bool use_norm, double* lam, double* hes, double* suml) {
+  const bool i_high = li > lj;
+  const int hr = i_high ? ri : rj, lr = i_high ? rj : ri;
+  const unsigned lh = static_cast<unsigned>(i_high ? li : lj), ll = static_cast<unsigned>(i_high ? lj : li);
+  const unsigned top = static_cast<unsigned>(t.ngain - 1);
+  const double gap = t.gain[min(lh, top)] - t.gain[min(ll, top)];
+  const double pd = fabs(1.0 / log2(2.0 + hr) - 1.0 / log2(2.0 + lr));
+  const double ds = i_high ? si - sj : sj - si;
+  double dn = gap * pd * imd;
+  if (use_norm) dn /= (0.01 + fabs(ds));
+  double pl = 1.0 / (1.0 + exp(t.sigma * ds));
+  double ph = pl * (1.0 - pl);
+  pl *= -t.sigma * dn;
+  ph *= t.sigma * t.sigma * dn;
+  *lam += i_high ? pl : -pl;
+  *hes += ph;
+  *suml -= pl;  // each pair is visited from both ends: sum = -2 pl per pair
+}
+
+template <bool kSmall>
+__device__ void LambdarankQuery(const RankTables& t, int q, const double* __restrict__ score,
+                                const float* __restrict__ label, const float* __restrict__ weight,
+                                float* __restrict__ g, float* __restrict__ h, double* s_sc, int* s_lab, int* s_rk) {
+  const int lane = threadIdx.x;
+  const int b = t.qb[q], cnt = t.qb[q + 1] - b;
+  const double* sc = kSmall ? s_sc : score + b;
+  double mx = -INFINITY, mn = INFINITY;
+  for (int i = lane; i < cnt; i += 64) {
+    const double s = score[b + i];
+    if (kSmall) { s_sc[i] = s; s_lab[i] = static_cast<int>(label[b + i]); }
+    mx = fmax(mx, s);
+    mn = fmin(mn, s);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mx = fmax(mx, __shfl_xor(mx, off, 64));
+    mn = fmin(mn, __shfl_xor(mn, off, 64));
+  }
+  __syncthreads();
+  int* rk = kSmall ? s_rk : t.rank_scratch + b;
+  for (int i = lane; i < cnt; i += 64) {
+    const double si = sc[i];
+    int r = 0;
+    for (int j = 0; j < cnt; ++j) {
+      const double sj = sc[j];
+      r += (sj > si) || (sj == si && j < i);
+    }
+    rk[i] = r;
+  }
+  __syncthreads();
+  const double imd = t.inv_max_dcg[q];
+  const bool use_norm = t.norm && mx != mn;
+  double lam[kRankPerLane], hes[kRankPerLane];
+  double suml = 0.0;
+  for (int i0 = 0; i0 < cnt; i0 += 64 * kRankPerLane) {
+#pragma unroll
+    for (int u = 0; u < kRankPerLane; ++u) {
+      const int i = i0 + u * 64 + lane;
+      double la = 0.0, he = 0.0;
+      if (i < cnt) {
+        const double si = sc[i];
+        const int li = kSmall ? s_lab[i] : static_cast<int>(label[b + i]);
+        const int ri = rk[i];
+        for (int j = 0; j < cnt; ++j) {
+          const int lj = kSmall ? s_lab[j] : static_cast<int>(label[b + j]);
+          if (lj == li) continue;
+          const int rj = rk[j];
+          if (min(ri, rj) >= t.max_position) continue;
+          PairLambda(t, si, li, ri, sc[j], lj, rj, imd, use_norm, &la, &he, &suml);
+        }
+      }
+      if (kSmall) {
+        lam[u] = la;
+        hes[u] = he;
+      } else if (i < cnt) {
+        t.lam_scratch[b + i] = la;
+        t.hes_scratch[b + i] = he;
+      }
+    }
+  }
+  suml = WaveSumD(suml);
+  const double nf = (t.norm && suml > 0) ? log2(1.0 + suml) / suml : 1.0;
+  if (kSmall) {
+#pragma unroll
+    for (int u = 0; u < kRankPerLane; ++u) {
+      const int i = u * 64 + lane;
+      if (i < cnt) {
+        const double w = weight ? weight[b + i] : 1.0;
+        g[b + i] = static_cast<float>(lam[u] * nf * w);
+        h[b + i] = static_cast<float>(hes[u] * nf * w);
+      }
+    }
+  } else {
+    for (int i = lane; i < cnt; i += 64) {  // the same lane wrote lam/hes of i above
+      const double w = weight ? weight[b + i] : 1.0;
+      g[b + i] = static_cast<float>(t.lam_scratch[b + i] * nf * w);
+      h[b + i] = static_cast<float>(t.hes_scratch[b + i] * nf * w);
+    }
+  }
+  __syncthreads();  // LDS reuse by the next query
+}
+
+__global__ __launch_bounds__(64) void lambdarank_kernel(RankTables t, const double* __restrict__ score,
+                                                        const float* __restrict__ label,
+                                                        const float* __restrict__ weight, float* __restrict__ g,
+                                                        float* __restrict__ h) {
+  __shared__ double s_sc[kRankLds];
+  __shared__ int s_lab[kRankLds];
+  __shared__ int s_rk[kRankLds];
+  for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
+    const int cnt = t.qb[q + 1] - t.qb[q];
+    if (cnt <= 0) continue;
+    if (cnt <= kRankLds) LambdarankQuery<true>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk);
+    else LambdarankQuery<false>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk);
+  }
+}
+
+// ---------------------------------------------------------------- K8
+// Bagging / GOSS on the device. GOSS needs the top_k-th largest |g*h|: an
+// exact 4-pass MSB radix select over the float bit patterns (non-negative
+// floats order like their bits), one 256-bin LDS histogram per pass, the pick
+// done by one thread, so the threshold never leaves the device. The sampling
+// pass draws RowUniform (sampling.h, same value as the host), rescales the
+// sampled small-gradient rows and compacts the kept rows with wave ballots and
+// one atomic per block; the bag's row order is irrelevant (histogram sums are
+// exact integers, K3).
+struct SelectState {
+  uint32_t prefix, mask;
+  long long k;  // 1-based rank of the wanted key among keys matching prefix
+  int count;    // rows kept by the sampling pass
+  int pad;
+};
+
+__global__ __launch_bounds__(256) void goss_key_kernel(const float* __restrict__ g, const float* __restrict__ h,
+                                                       int64_t n, int K, uint32_t* __restrict__ key) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += fabsf(g[k * n + i] * h[k * n + i]);
+    key[i] = __float_as_uint(s);
+  }
+}
+
+__global__ void select_init_kernel(SelectState* st, long long k) {
+  if (threadIdx.x == 0) { st->prefix = 0u; st->mask = 0u; st->k = k; st->count = 0; }
+}
+
+__global__ __launch_bounds__(256) void radix_hist_kernel(const uint32_t* __restrict__ key, int64_t n,
+                                                         const SelectState* __restrict__ st, int shift,
+                                                         unsigned int* __restrict__ hist) {
+  __shared__ unsigned int lh[256];
+  lh[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t prefix = st->prefix, mask = st->mask;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = key[i];
+    if ((v & mask) == prefix) atomicAdd(&lh[(v >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
+}
+
+__global__ void radix_pick_kernel(SelectState* st, unsigned int* __restrict__ hist, int shift) {
+  if (threadIdx.x != 0) return;
+  long long cum = 0;
+  const long long k = st->k;
+  for (int d = 255; d >= 0; --d) {
+    const long long c = hist[d];
+    if (cum + c >= k) {
+      st->prefix |= static_cast<uint32_t>(d) << shift;
+      st->mask |= 255u << shift;
+      st->k = k - cum;
+      break;
+    }
+    cum += c;
+  }
+  for (int d = 0; d < 256; ++d) hist[d] = 0u;  // ready for the next pass
+}
+
+__global__ __launch_bounds__(256) void sample_kernel(RowSampleSpec sp, int64_t n, int K,
+                                                     const uint32_t* __restrict__ key,
+                                                     SelectState* __restrict__ st, const float* __restrict__ label,
+                                                     float* __restrict__ g, float* __restrict__ h,
+                                                     int32_t* __restrict__ bag) {
+  __shared__ int wcnt[4];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t thr = sp.kind == kSampleGoss ? st->prefix : 0u;
+  const float mult = static_cast<float>(sp.other_mult);
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x; i0 < n; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    bool keep = false;
+    if (i < n) {
+      if (sp.kind == kSampleBagging) {
+        const double frac = sp.balanced ? (label[i] > 0 ? sp.pos_fraction : sp.neg_fraction) : sp.fraction;
+        keep = RowUniform(sp.seed, sp.iter, i) < frac;
+      } else if (key[i] >= thr) {
+        keep = true;
+      } else if (RowUniform(sp.seed, sp.iter, i) < sp.other_prob) {
+        keep = true;
+        for (int k = 0; k < K; ++k) { g[k * n + i] *= mult; h[k * n + i] *= mult; }
+      }
+    }
+    const unsigned long long bl = __ballot(keep);
+    if (lane == 0) wcnt[wid] = __popcll(bl);
+    __syncthreads();
+    if (threadIdx.x == 0) base = atomicAdd(&st->count, wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3]);
+    __syncthreads();
+    if (keep) {
+      int off = base + __popcll(bl & below);
+      for (int w = 0; w < wid; ++w) off += wcnt[w];
+      bag[off] = static_cast<int32_t>(i);
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- root init
@@ -1089,8 +1342,20 @@ class GpuBackend : public TrainBackend {
   }
   void ComputeGradients(const Objective& obj) override {
     const ObjParams& p = obj.params();
+    if (p.kind == kObjLambdarank && K_ == 1) {
+      auto t0 = std::chrono::steady_clock::now();
+      EnsureRankTables(obj);
+      if (rank_.nq > 0) {
+        const int grid = std::min(rank_.nq, 65536);
+        hipLaunchKernelGGL(lambdarank_kernel, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(), label_.get(),
+                           weight_.get(), g_.get(), h_.get());
+        SML_HIP_CHECK(hipGetLastError());
+      }
+      ghmax_valid_ = false;
+      stats.grad_ms += Ms(t0);
+      return;
+    }
     if (p.kind == kObjLambdarank || p.kind == kObjCustom) {
-      // ranking gradients are computed per query on the host (v1)
       std::vector<double> sc;
       GetScores(&sc);
       std::vector<float> g(static_cast<size_t>(n_) * K_), h(g.size());
@@ -1131,15 +1396,50 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
-  void Synchronize() override { SML_HIP_CHECK(hipStreamSynchronize(stream_)); }
+  bool SampleRows(const RowSampleSpec& spec) override {
+    if (spec.kind != kSampleBagging && spec.kind != kSampleGoss) return false;
+    roctxRangePushA("sml::SampleRows");
+    bag_.alloc(static_cast<size_t>(std::max<int64_t>(1, n_)));
+    sel_.alloc(1);
+    const int grid = std::min(GridFor(n_), 2048);
+    hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(64), 0, stream_, sel_.get(),
+                       static_cast<long long>(spec.top_k));
+    SML_HIP_CHECK(hipGetLastError());
+    if (spec.kind == kSampleGoss) {
+      sel_key_.alloc(static_cast<size_t>(std::max<int64_t>(1, n_)));
+      sel_hist_.alloc(256);
+      SML_HIP_CHECK(hipMemsetAsync(sel_hist_.get(), 0, 256 * sizeof(unsigned int), stream_));
+      hipLaunchKernelGGL(goss_key_kernel, dim3(grid), dim3(256), 0, stream_, g_.get(), h_.get(), n_, K_,
+                         sel_key_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        hipLaunchKernelGGL(radix_hist_kernel, dim3(grid), dim3(256), 0, stream_, sel_key_.get(), n_, sel_.get(), shift,
+                           sel_hist_.get());
+        SML_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(radix_pick_kernel, dim3(1), dim3(64), 0, stream_, sel_.get(), sel_hist_.get(), shift);
+        SML_HIP_CHECK(hipGetLastError());
+      }
+    }
+    hipLaunchKernelGGL(sample_kernel, dim3(grid), dim3(256), 0, stream_, spec, n_, K_,
+                       spec.kind == kSampleGoss ? sel_key_.get() : static_cast<const uint32_t*>(nullptr), sel_.get(),
+                       label_.get(), g_.get(), h_.get(), bag_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    SelectState st{};
+    SML_HIP_CHECK(hipMemcpyAsync(&st, sel_.get(), sizeof(SelectState), hipMemcpyDeviceToHost, stream_));
+    SML_HIP_CHECK(hipStreamSynchronize(stream_));
+    bag_n_ = st.count;
+    if (spec.kind == kSampleGoss) ghmax_valid_ = false;  // gradients were rescaled
+    roctxRangePop();
+    return true;
+  }
+
+  void Synchronize() override {
+    SML_HIP_CHECK(hipStreamSynchronize(stream_));
+    AccountScoreTime();
+  }
 
   Tree TrainTree(int k, const std::vector<char>& fmask_in) override {
     roctxRangePushA("sml::TrainTree");
-    if (score_pending_ && hipEventQuery(ev_[3]) == hipSuccess) {
-      float sms = 0.f;
-      if (hipEventElapsedTime(&sms, ev_[2], ev_[3]) == hipSuccess) stats.device_score_ms += sms;
-      score_pending_ = false;
-    }
     SML_HIP_CHECK(hipEventRecord(ev_[0], stream_));
     std::vector<int8_t> fmask(F_, 1);
     for (int f = 0; f < F_ && f < static_cast<int>(fmask_in.size()); ++f) fmask[f] = fmask_in[f] ? 1 : 0;
@@ -1178,9 +1478,10 @@ class GpuBackend : public TrainBackend {
     }
     SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
     // read the tree back (one transfer, one sync)
-    Tree t = ReadTree();
+    Tree t = ReadTree();  // synchronises the stream: every event recorded so far is complete
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ev_[0], ev_[1]) == hipSuccess) stats.device_tree_ms += ms;
+    AccountScoreTime();
     roctxRangePop();
     return t;
   }
@@ -1223,6 +1524,55 @@ class GpuBackend : public TrainBackend {
   }
 
   const double* CountSlot() const { return reinterpret_cast<const double*>(part_.get() + E_); }
+
+  // device time of the last score update; call only after a stream sync
+  void AccountScoreTime() {
+    if (!score_pending_) return;
+    float sms = 0.f;
+    if (hipEventElapsedTime(&sms, ev_[2], ev_[3]) == hipSuccess) stats.device_score_ms += sms;
+    score_pending_ = false;
+  }
+
+  // query boundaries, 1/maxDCG per query and the label gains for the
+  // lambdarank kernel (uploaded once: they depend only on the dataset)
+  void EnsureRankTables(const Objective& obj) {
+    if (rank_ready_) return;
+    const auto& qb = obj.query_boundaries();
+    const auto& imd = obj.inv_max_dcg();
+    const auto& gain = obj.label_gain();
+    if (qb.size() < 2 || gain.empty()) throw std::runtime_error("lambdarank: missing query boundaries or label_gain");
+    if (qb.back() > n_) throw std::runtime_error("lambdarank: query boundaries exceed the number of rows");
+    rank_qb_.alloc(qb.size());
+    rank_imd_.alloc(imd.size());
+    rank_gain_.alloc(gain.size());
+    SML_HIP_CHECK(hipMemcpy(rank_qb_.get(), qb.data(), sizeof(int32_t) * qb.size(), hipMemcpyHostToDevice));
+    SML_HIP_CHECK(hipMemcpy(rank_imd_.get(), imd.data(), sizeof(double) * imd.size(), hipMemcpyHostToDevice));
+    SML_HIP_CHECK(hipMemcpy(rank_gain_.get(), gain.data(), sizeof(double) * gain.size(), hipMemcpyHostToDevice));
+    int max_q = 0;
+    for (size_t q = 0; q + 1 < qb.size(); ++q) max_q = std::max(max_q, qb[q + 1] - qb[q]);
+    rank_ = RankTables{};
+    if (max_q > kRankLds) {  // long queries stream ranks / lambdas through global scratch
+      rank_scratch_.alloc(n_);
+      rank_lam_.alloc(n_);
+      rank_hes_.alloc(n_);
+      rank_.rank_scratch = rank_scratch_.get();
+      rank_.lam_scratch = rank_lam_.get();
+      rank_.hes_scratch = rank_hes_.get();
+    }
+    if (qb.back() < n_ || qb.front() > 0) {  // rows outside every query get zero gradients
+      SML_HIP_CHECK(hipMemsetAsync(g_.get(), 0, sizeof(float) * n_, stream_));
+      SML_HIP_CHECK(hipMemsetAsync(h_.get(), 0, sizeof(float) * n_, stream_));
+    }
+    rank_.qb = rank_qb_.get();
+    rank_.inv_max_dcg = rank_imd_.get();
+    rank_.gain = rank_gain_.get();
+    rank_.nq = static_cast<int>(qb.size()) - 1;
+    rank_.ngain = static_cast<int>(gain.size());
+    rank_.max_position = obj.max_position();
+    rank_.norm = obj.lambdarank_norm() ? 1 : 0;
+    rank_.sigma = obj.params().sigmoid;
+    rank_ready_ = true;
+  }
 
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
@@ -1384,6 +1734,15 @@ class GpuBackend : public TrainBackend {
   DevBuf<uint32_t> up_u_;
   DevBuf<double> up_d_;
   DevBuf<int32_t> leaf_idx_;
+  // device row sampling (K8)
+  DevBuf<SelectState> sel_;
+  DevBuf<uint32_t> sel_key_;
+  DevBuf<unsigned int> sel_hist_;
+  // lambdarank (K2 ranking)
+  bool rank_ready_ = false;
+  RankTables rank_{};
+  DevBuf<int32_t> rank_qb_, rank_scratch_;
+  DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_;
   int32_t* flags_ = nullptr;
   DTree dt_{};
   FeatMeta fm_{};

@@ -227,8 +227,20 @@ PYBIND11_MODULE(_gbdt, m) {
       .def_property_readonly("current_iteration", &Booster::CurrentIteration)
       .def_property_readonly("feature_names", &Booster::FeatureNames)
       .def_property_readonly("backend", &Booster::BackendName)
+      .def("gradients", [](Booster& b) {
+        std::vector<float> g, h;
+        {
+          py::gil_scoped_release rel;
+          b.GetGradients(&g, &h);
+        }
+        return py::make_tuple(py::array_t<float>(g.size(), g.data()), py::array_t<float>(h.size(), h.data()));
+      })
       .def("stats", [](Booster& b) {
         py::dict d;
+        {
+          py::gil_scoped_release rel;
+          b.Synchronize();  // device timings of work still in flight
+        }
         TrainStats* s = b.stats();
         if (s) {
           d["grad_ms"] = s->grad_ms; d["hist_ms"] = s->hist_ms; d["split_ms"] = s->split_ms;

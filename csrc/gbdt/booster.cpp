@@ -186,14 +186,70 @@ void Booster::Bagging(int iter) {
   const bool need = cfg_.bagging_freq > 0 && (cfg_.bagging_fraction < 1.0 || balanced);
   if (!need) { if (bagged_) { backend_->SetBag(nullptr); bagged_ = false; } return; }
   if (iter % cfg_.bagging_freq != 0) return;
-  std::uniform_real_distribution<double> U(0.0, 1.0);
+  RowSampleSpec spec;
+  spec.kind = kSampleBagging;
+  spec.seed = static_cast<uint64_t>(cfg_.bagging_seed);
+  spec.iter = iter;
+  spec.fraction = cfg_.bagging_fraction;
+  spec.pos_fraction = cfg_.pos_bagging_fraction;
+  spec.neg_fraction = cfg_.neg_bagging_fraction;
+  spec.balanced = balanced;
+  // leaf renewal (l1 / quantile / mape) needs the bag on the host
+  if (!objective_->NeedRenewTreeOutput() && backend_->SampleRows(spec)) {
+    bag_rows_.clear();
+    bagged_ = true;
+    return;
+  }
   bag_rows_.clear();
   bag_rows_.reserve(static_cast<size_t>(n * cfg_.bagging_fraction) + 16);
   for (int64_t i = 0; i < n; ++i) {
     double frac = cfg_.bagging_fraction;
     if (balanced) frac = train_->label[i] > 0 ? cfg_.pos_bagging_fraction : cfg_.neg_bagging_fraction;
-    if (U(bag_rng_) < frac) bag_rows_.push_back(static_cast<int32_t>(i));
+    if (RowUniform(spec.seed, iter, i) < frac) bag_rows_.push_back(static_cast<int32_t>(i));
   }
+  backend_->SetBag(&bag_rows_);
+  bagged_ = true;
+}
+
+void Booster::Goss() {
+  const int K = num_tree_per_iter_;
+  const int64_t n = train_->num_data;
+  RowSampleSpec spec;
+  spec.kind = kSampleGoss;
+  spec.seed = static_cast<uint64_t>(cfg_.bagging_seed);
+  spec.iter = iter_;
+  spec.top_k = std::max<int64_t>(1, static_cast<int64_t>(n * cfg_.top_rate));
+  const int64_t other_k = std::max<int64_t>(1, static_cast<int64_t>(n * cfg_.other_rate));
+  spec.other_mult = static_cast<double>(n - spec.top_k) / other_k;
+  spec.other_prob = static_cast<double>(other_k) / std::max<int64_t>(1, n - spec.top_k);
+  if (!objective_->NeedRenewTreeOutput() && backend_->SampleRows(spec)) {
+    bag_rows_.clear();
+    bagged_ = true;
+    return;
+  }
+  std::vector<float> g, h;
+  backend_->GetGradients(&g, &h);
+  // |g*h| summed over classes in float: the device computes the same value
+  std::vector<float> a(n, 0.f);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += std::fabs(g[k * n + i] * h[k * n + i]);
+    a[i] = s;
+  }
+  std::vector<float> tmp = a;
+  std::nth_element(tmp.begin(), tmp.begin() + (spec.top_k - 1), tmp.end(), std::greater<float>());
+  const float thr = tmp[spec.top_k - 1];
+  const float mult = static_cast<float>(spec.other_mult);
+  bag_rows_.clear();
+  for (int64_t i = 0; i < n; ++i) {
+    if (a[i] >= thr) { bag_rows_.push_back(static_cast<int32_t>(i)); continue; }
+    if (RowUniform(spec.seed, iter_, i) < spec.other_prob) {
+      bag_rows_.push_back(static_cast<int32_t>(i));
+      for (int k = 0; k < K; ++k) { g[k * n + i] *= mult; h[k * n + i] *= mult; }
+    }
+  }
+  backend_->SetGradients(g.data(), h.data());
   backend_->SetBag(&bag_rows_);
   bagged_ = true;
 }
@@ -240,29 +296,7 @@ bool Booster::TrainOneIter(const float* grad, const float* hess) {
   }
   // ---- row sampling
   if (is_goss && iter_ >= static_cast<int>(1.0 / cfg_.learning_rate)) {
-    std::vector<float> g, h;
-    backend_->GetGradients(&g, &h);
-    std::vector<double> a(n, 0.0);
-    for (int k = 0; k < K; ++k) for (int64_t i = 0; i < n; ++i) a[i] += std::fabs(static_cast<double>(g[k * n + i]) * h[k * n + i]);
-    const int64_t top_k = std::max<int64_t>(1, static_cast<int64_t>(n * cfg_.top_rate));
-    const int64_t other_k = std::max<int64_t>(1, static_cast<int64_t>(n * cfg_.other_rate));
-    std::vector<double> tmp = a;
-    std::nth_element(tmp.begin(), tmp.begin() + (top_k - 1), tmp.end(), std::greater<double>());
-    const double thr = tmp[top_k - 1];
-    const double mult = static_cast<double>(n - top_k) / other_k;
-    const double prob = static_cast<double>(other_k) / std::max<int64_t>(1, n - top_k);
-    std::uniform_real_distribution<double> U(0.0, 1.0);
-    bag_rows_.clear();
-    for (int64_t i = 0; i < n; ++i) {
-      if (a[i] >= thr) { bag_rows_.push_back(static_cast<int32_t>(i)); continue; }
-      if (U(bag_rng_) < prob) {
-        bag_rows_.push_back(static_cast<int32_t>(i));
-        for (int k = 0; k < K; ++k) { g[k * n + i] *= static_cast<float>(mult); h[k * n + i] *= static_cast<float>(mult); }
-      }
-    }
-    backend_->SetGradients(g.data(), h.data());
-    backend_->SetBag(&bag_rows_);
-    bagged_ = true;
+    Goss();
   } else if (!is_goss) {
     Bagging(iter_);
   }

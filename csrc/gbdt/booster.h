@@ -66,6 +66,8 @@ class Booster {
   std::string BackendName() const { return backend_ ? backend_->Name() : "none"; }
   TrainStats* stats() { return backend_ ? &backend_->stats : nullptr; }
   void Synchronize() { if (backend_) backend_->Synchronize(); }
+  // gradients / hessians of the last iteration (class-major n*K; after GOSS rescaling)
+  void GetGradients(std::vector<float>* g, std::vector<float>* h) { backend_->GetGradients(g, h); }
   // Keep only the first `num_iteration` iterations (early stopping).
   void Truncate(int num_iteration);
   const Objective* objective() const { return objective_.get(); }
@@ -73,6 +75,7 @@ class Booster {
  private:
   void InitTraining();
   void Bagging(int iter);
+  void Goss();
   std::vector<char> SampleFeatures();
   void PredictRaw(const double* x, int start_tree, int end_tree, double* out) const;
   std::pair<int, int> TreeRange(int start_iteration, int num_iteration) const;

@@ -114,6 +114,12 @@ class Objective {
   std::string name() const { return name_; }
   std::string DefaultMetric() const;
   static std::string Canonical(const std::string& name);
+  // lambdarank tables (the HIP gradient kernel uploads them once)
+  const std::vector<int32_t>& query_boundaries() const { return qb_; }
+  const std::vector<double>& inv_max_dcg() const { return inv_max_dcg_; }
+  const std::vector<double>& label_gain() const { return label_gain_; }
+  int max_position() const { return max_position_; }
+  bool lambdarank_norm() const { return lambdarank_norm_; }
 
  private:
   void LambdarankGradients(const double* score, float* g, float* h) const;

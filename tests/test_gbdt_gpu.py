@@ -193,3 +193,85 @@ def test_gpu_treeshap_matches_cpu(kind):
     K = raw.shape[1]
     sums = gpu.reshape(len(Xt), K, -1).sum(-1)
     np.testing.assert_allclose(sums, raw, rtol=1e-8, atol=1e-8)
+
+
+def _rank_data(seed=21, nq=300, long_queries=True):
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(2, 60, size=nq)
+    if long_queries:
+        sizes[:3] = [300, 700, 257]  # > 256 docs: the global-scratch path of the kernel
+    n = int(sizes.sum())
+    X = rng.standard_normal((n, 8))
+    rel = np.clip(np.round(X[:, 0] + 0.5 * X[:, 1] + 1.5 + 0.4 * rng.standard_normal(n)), 0, 4).astype(np.float32)
+    return X, rel, sizes.astype(np.int32)
+
+
+def _train_rank(X, y, sizes, params, iters):
+    from synapseml_amd.ops import native
+
+    g = native.gbdt()
+    ref = g.DatasetReference.from_sample(X, len(X), params, [f"f{i}" for i in range(X.shape[1])])
+    ds = g.Dataset(ref, len(X))
+    ds.push_dense(X, 0)
+    ds.set_label(y)
+    ds.set_group(sizes)
+    b = g.Booster(ds, params, None)
+    for _ in range(iters):
+        b.update()
+    return b
+
+
+def test_gpu_lambdarank_gradients_match_host():
+    """K2 ranking: the wave-per-query lambdarank kernel vs the host pairwise loop (LDS and global paths)."""
+    X, y, sizes = _rank_data()
+    p = "objective=lambdarank num_leaves=15 min_data_in_leaf=5 eval_at=5"
+    bc = _train_rank(X, y, sizes, p + " device_type=cpu", 1)
+    bg = _train_rank(X, y, sizes, p + " device_type=gpu", 1)
+    assert bg.backend == "hip"
+    gc, hc = bc.gradients()
+    gg, hg = bg.gradients()
+    np.testing.assert_allclose(gg, gc, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(hg, hc, rtol=1e-5, atol=1e-7)
+    # later iterations (non-zero scores, ties broken by index) stay in step
+    bc = _train_rank(X, y, sizes, p + " device_type=cpu", 6)
+    bg = _train_rank(X, y, sizes, p + " device_type=gpu", 6)
+    pc = bc.predict(X, 0, 0, -1)[:, 0]
+    pg = bg.predict(X, 0, 0, -1)[:, 0]
+    assert np.corrcoef(pc, pg)[0, 1] > 0.999
+    np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
+
+
+def test_gpu_bagging_draws_the_host_bag():
+    """K8: device bagging draws the same rows as the host (counter-based RNG), so trees match the CPU oracle."""
+    X, y = _data(n=50000)
+    for extra in ["bagging_fraction=0.6 bagging_freq=1", "pos_bagging_fraction=0.5 neg_bagging_fraction=0.8 bagging_freq=2"]:
+        base = f"objective=binary num_leaves=31 {extra}"
+        bc = _train(X, y, base + " device_type=cpu", 3)
+        bg = _train(X, y, base + " device_type=gpu", 3)
+        mc, mg = bc.save_model_string(), bg.save_model_string()
+        for t in ("Tree=0", "Tree=2"):
+            tc = mc.split(t)[1].split("Tree=")[0]
+            tg = mg.split(t)[1].split("Tree=")[0]
+            line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")][0]
+            assert line(tc, "split_feature") == line(tg, "split_feature"), (extra, t)
+            assert line(tc, "leaf_count") == line(tg, "leaf_count"), (extra, t)
+
+
+def test_gpu_goss_matches_host():
+    """K8: device GOSS (radix top-k threshold + sampled rescaling) vs the host path."""
+    from sklearn.metrics import roc_auc_score
+
+    X, y = _data(n=60000)
+    p = "objective=binary boosting=goss learning_rate=0.5 num_leaves=31 top_rate=0.2 other_rate=0.1"
+    bc = _train(X, y, p + " device_type=cpu", 5)
+    bg = _train(X, y, p + " device_type=gpu", 5)
+    gc, _ = bc.gradients()
+    gg, _ = bg.gradients()
+    # same rows rescaled by the same factor (gradients may differ in the last ulp between host and device exp)
+    mult = (len(X) - int(len(X) * 0.2)) / int(len(X) * 0.1)
+    big_c = np.abs(gc) > 0
+    assert abs(np.mean(np.isclose(np.abs(gg), np.abs(gc), rtol=1e-3)) - 1.0) < 0.01
+    pc, pg = bc.predict(X, 0, 0, -1)[:, 0], bg.predict(X, 0, 0, -1)[:, 0]
+    assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 3e-3
+    np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
+    assert big_c.any() and mult > 1
