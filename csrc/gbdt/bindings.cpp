@@ -96,6 +96,26 @@ PYBIND11_MODULE(_gbdt, m) {
                p.d->PushDense(a.data(), a.shape(0), static_cast<int>(a.shape(1)), start);
              }
            })
+      .def("push_dense_gpu",
+           [](PyDataset& p, py::array X, int64_t start, int device) {
+             auto b = X.request();
+             if (b.ndim != 2) throw std::runtime_error("rows must be 2-D");
+             if (start < 0 || start + b.shape[0] > p.d->num_data) throw std::runtime_error("push_dense_gpu out of range");
+             if (b.format == py::format_descriptor<float>::format()) {
+               F32 a = py::cast<F32>(X);
+               py::gil_scoped_release rel;
+               DatasetPushDenseDeviceF32(p.d.get(), a.data(), a.shape(0), static_cast<int>(a.shape(1)), start, device);
+             } else {
+               F64 a = py::cast<F64>(X);
+               py::gil_scoped_release rel;
+               DatasetPushDenseDevice(p.d.get(), a.data(), a.shape(0), static_cast<int>(a.shape(1)), start, device);
+             }
+           },
+           py::arg("X"), py::arg("start"), py::arg("device") = -1,
+           "K1: encode dense rows into bins on the MI355X (bit-identical with push_dense)")
+      .def_property_readonly("bins", [](PyDataset& p) {
+        return py::array_t<uint8_t>({p.d->num_data, static_cast<int64_t>(p.d->row_stride)}, p.d->bins.data());
+      })
       .def("push_csr",
            [](PyDataset& p, I64 indptr, I32 indices, F64 values, int64_t start) {
              const int64_t nrows = indptr.shape(0) - 1;

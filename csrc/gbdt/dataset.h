@@ -111,4 +111,8 @@ struct Dataset {
   inline uint8_t Bin(int64_t row, int inner) const { return bins[row * row_stride + inner]; }
 };
 
+// K1 on the device (bin_encode.hip): same bins as PushDense / PushDenseF32.
+void DatasetPushDenseDevice(Dataset* d, const double* rows, int64_t nrows, int num_cols, int64_t start, int device);
+void DatasetPushDenseDeviceF32(Dataset* d, const float* rows, int64_t nrows, int num_cols, int64_t start, int device);
+
 }  // namespace sml

@@ -391,9 +391,14 @@ class LightGBMBase(Estimator, LightGBMParams):
     def _build_dataset(self, g, ref, df: DataFrame, kind, data, n, num_class):
         ds = g.Dataset(ref, n)
         if kind == "dense":
-            chunk = 1 << 20
-            for s in range(0, n, chunk):
-                ds.push_dense(data[s: s + chunk], s)
+            # K1: large dense partitions are bin-encoded on the MI355X (bit-identical with the host encoder)
+            on_gpu = n >= (1 << 16) and self.getDeviceType() == "gpu" and native.gpu_available()
+            if on_gpu:
+                ds.push_dense_gpu(data, 0)
+            else:
+                chunk = 1 << 20
+                for s in range(0, n, chunk):
+                    ds.push_dense(data[s: s + chunk], s)
         else:
             indptr, indices, values, _ = data
             ds.push_csr(indptr, indices, values, 0)
@@ -413,15 +418,12 @@ class LightGBMBase(Estimator, LightGBMParams):
             ds.set_init_score(arr)
         gcol = self._group_col()
         if gcol and gcol in df:
-            vals = df[gcol].tolist()
-            sizes = []
-            prev = object()
-            for v in vals:
-                if sizes and v == prev:
-                    sizes[-1] += 1
-                else:
-                    sizes.append(1)
-                    prev = v
+            vals = np.asarray(df[gcol])
+            # runs of equal consecutive group ids (rows are already grouped)
+            starts = np.ones(len(vals), dtype=bool)
+            if len(vals) > 1:
+                starts[1:] = np.asarray(vals[1:] != vals[:-1], dtype=bool)
+            sizes = np.diff(np.append(np.flatnonzero(starts), len(vals)))
             ds.set_group(np.asarray(sizes, dtype=np.int32))
         return ds
 

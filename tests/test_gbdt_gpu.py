@@ -275,3 +275,30 @@ def test_gpu_goss_matches_host():
     assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 3e-3
     np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
     assert big_c.any() and mult > 1
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_gpu_bin_encode_bit_identical(dtype):
+    """K1: device bin encoding == host ValueToBin (NaN / zero-as-missing / categorical / unknown categories)."""
+    from synapseml_amd.ops import native
+
+    g = native.gbdt()
+    rng = np.random.default_rng(7)
+    n = 70000
+    X = rng.standard_normal((n, 9))
+    X[:, 0] = rng.integers(0, 40, size=n)          # categorical
+    X[:, 1] = np.where(rng.random(n) < 0.3, 0.0, X[:, 1])
+    X[rng.random((n, 9)) < 0.05] = np.nan
+    X[:, 2] = np.round(X[:, 2] * 3)                  # few distinct values
+    X[:, 8] = 1.0                                    # trivial feature
+    for params in ["categorical_feature=0", "categorical_feature=0 zero_as_missing=true", "use_missing=false"]:
+        ref = g.DatasetReference.from_sample(X[:20000], n, params, [f"f{i}" for i in range(9)])
+        Xt = X.copy()
+        Xt[:100, 0] = 1000  # categories never seen in the sample
+        Xt = Xt.astype(dtype)
+        a = g.Dataset(ref, n)
+        a.push_dense(Xt, 0)
+        b = g.Dataset(ref, n)
+        b.push_dense_gpu(Xt[:40000], 0)
+        b.push_dense_gpu(Xt[40000:], 40000)
+        np.testing.assert_array_equal(a.bins, b.bins, err_msg=params)

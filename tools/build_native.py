@@ -49,6 +49,7 @@ MODULES = {
             "backend_gpu.hip",
             "predict_gpu.hip",
             "comm_p2p.hip",
+            "bin_encode.hip",
         ],
         ["-lrccl", "-lrocprofiler-sdk-roctx"],
     ),
