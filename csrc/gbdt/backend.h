@@ -64,7 +64,7 @@ bool GpuAvailable();
 // histogram. Used by the CPU backend and by tests that compare the device.
 void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinMapper& m,
                           int feature_inner, double sum_g, double sum_h, int64_t cnt,
-                          const SplitParams& sp, SplitResult* best);
+                          const SplitParams& sp, SplitResult* best, const MonoCtx* mc = nullptr);
 SplitParams MakeSplitParams(const Config& cfg);
 
 }  // namespace sml

@@ -23,16 +23,19 @@ SplitParams MakeSplitParams(const Config& c) {
   p.min_data_in_leaf = c.min_data_in_leaf; p.num_leaves = c.num_leaves; p.max_depth = c.max_depth;
   p.cat_l2 = c.cat_l2; p.cat_smooth = c.cat_smooth; p.max_cat_threshold = c.max_cat_threshold;
   p.max_cat_to_onehot = c.max_cat_to_onehot; p.min_data_per_group = c.min_data_per_group;
+  p.has_mono = 0;
+  for (int m : c.monotone_constraints) if (m != 0) p.has_mono = 1;
+  p.monotone_penalty = c.monotone_penalty;
   return p;
 }
 
 static void ConsiderSplit(double gl, double hl, double gr, double hr, int64_t cl, int64_t cr,
                           double parent_gain, const SplitParams& sp, double l2, int feature,
-                          uint32_t thr, int default_left, SplitResult* best) {
+                          uint32_t thr, int default_left, SplitResult* best, const MonoCtx* mc) {
   if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
   if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
-  const double gain = LeafGain(gl, hl, sp.lambda_l1, l2, sp.max_delta_step) +
-                      LeafGain(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+  double gain, lout, rout;
+  if (!EvalSplit(gl, hl, gr, hr, sp.lambda_l1, l2, sp.max_delta_step, mc, &gain, &lout, &rout)) return;
   const double shift = parent_gain + sp.min_gain_to_split;
   if (!(gain > shift)) return;
   const double sg = gain - shift;
@@ -44,13 +47,13 @@ static void ConsiderSplit(double gl, double hl, double gr, double hr, int64_t cl
   best->is_cat = 0;
   best->left_g = gl; best->left_h = hl; best->right_g = gr; best->right_h = hr;
   best->left_cnt = cl; best->right_cnt = cr;
-  best->left_out = LeafOutput(gl, hl, sp.lambda_l1, l2, sp.max_delta_step);
-  best->right_out = LeafOutput(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+  best->left_out = lout;
+  best->right_out = rout;
 }
 
 void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinMapper& m,
                           int fi, double G, double H, int64_t cnt, const SplitParams& sp,
-                          SplitResult* best) {
+                          SplitResult* best, const MonoCtx* mc) {
   const double cnt_factor = cnt / std::max(H, kEpsilon);
   const double parent_gain = LeafGain(G, H, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
   if (m.is_categorical) {
@@ -60,14 +63,18 @@ void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinM
     const double cat_parent = LeafGain(G, H, sp.lambda_l1, l2, sp.max_delta_step);
     SplitResult local = *best;
     bool found = false;
+    // categorical splits are clamped into the leaf's bounds but carry no direction
+    MonoCtx cat_mc{0.0, 0.0, 0};
+    if (mc) cat_mc = MonoCtx{mc->lo, mc->hi, 0};
+    const MonoCtx* cmc = mc ? &cat_mc : nullptr;
     auto try_set = [&](const std::vector<int>& left_bins, double gl, double hl) {
       const double gr = G - gl, hr = H - hl;
       const int64_t cl = EstimateCount(hl, cnt_factor), cr = cnt - cl;
       if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
       if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
       if (static_cast<int>(left_bins.size()) > 1 && (cl < sp.min_data_per_group || cr < sp.min_data_per_group)) return;
-      const double gain = LeafGain(gl, hl, sp.lambda_l1, l2, sp.max_delta_step) +
-                          LeafGain(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+      double gain, lout, rout;
+      if (!EvalSplit(gl, hl, gr, hr, sp.lambda_l1, l2, sp.max_delta_step, cmc, &gain, &lout, &rout)) return;
       const double shift = cat_parent + sp.min_gain_to_split;
       if (!(gain > shift)) return;
       const double sg = gain - shift;
@@ -78,8 +85,8 @@ void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinM
       for (int b : left_bins) local.cat_bits[b / 32] |= 1u << (b % 32);
       local.left_g = gl; local.left_h = hl; local.right_g = gr; local.right_h = hr;
       local.left_cnt = cl; local.right_cnt = cr;
-      local.left_out = LeafOutput(gl, hl, sp.lambda_l1, l2, sp.max_delta_step);
-      local.right_out = LeafOutput(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+      local.left_out = lout;
+      local.right_out = rout;
       found = true;
     };
     if (nb <= sp.max_cat_to_onehot + 1) {
@@ -118,18 +125,18 @@ void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinM
     if (t != zero_bin) { gl += hg[t]; hl += hh[t]; }
     if (mt == kMissingNone) {
       const int64_t cl = EstimateCount(hl, cnt_factor);
-      ConsiderSplit(gl, hl, G - gl, H - hl, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 1, best);
+      ConsiderSplit(gl, hl, G - gl, H - hl, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 1, best, mc);
     } else {
       // missing -> right
       {
         const int64_t cl = EstimateCount(hl, cnt_factor);
-        ConsiderSplit(gl, hl, G - gl, H - hl, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 0, best);
+        ConsiderSplit(gl, hl, G - gl, H - hl, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 0, best, mc);
       }
       // missing -> left
       {
         const double g2 = gl + mg, h2 = hl + mh;
         const int64_t cl = EstimateCount(h2, cnt_factor);
-        ConsiderSplit(g2, h2, G - g2, H - h2, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 1, best);
+        ConsiderSplit(g2, h2, G - g2, H - h2, cl, cnt - cl, parent_gain, sp, sp.lambda_l2, fi, t, 1, best, mc);
       }
     }
   }
@@ -142,6 +149,8 @@ struct LeafInfo {
   int64_t gcount = 0;            // global row count (all ranks)
   double sum_g = 0, sum_h = 0;
   int depth = 0;
+  double lo = -std::numeric_limits<double>::infinity();  // monotone output bounds
+  double hi = std::numeric_limits<double>::infinity();
   SplitResult best;
   bool has_best = false;
 };
@@ -156,6 +165,11 @@ class CpuBackend : public TrainBackend {
     g_.assign(static_cast<size_t>(n_) * K, 0.f);
     h_.assign(static_cast<size_t>(n_) * K, 0.f);
     F_ = d->ref.num_inner();
+    mono_.assign(F_, 0);
+    for (int f = 0; f < F_; ++f) {
+      const int col = d->ref.used_features[f];
+      if (col < static_cast<int>(cfg.monotone_constraints.size())) mono_[f] = cfg.monotone_constraints[col];
+    }
     nthreads_ = 1;
 #ifdef _OPENMP
     nthreads_ = cfg.num_threads > 0 ? cfg.num_threads : omp_get_max_threads();
@@ -228,7 +242,11 @@ class CpuBackend : public TrainBackend {
         if (!fmask[f]) continue;
         const BinMapper& m = data_->ref.mappers[data_->ref.used_features[f]];
         for (int b = 0; b < m.num_bin; ++b) { tg[b] = hist[f * 512 + b * 2]; th[b] = hist[f * 512 + b * 2 + 1]; }
-        FindBestSplitFeature(tg.data(), th.data(), m.num_bin, m, f, leaf->sum_g, leaf->sum_h, leaf->gcount, sp_, &per[f]);
+        const MonoCtx mc{leaf->lo, leaf->hi, mono_[f]};
+        FindBestSplitFeature(tg.data(), th.data(), m.num_bin, m, f, leaf->sum_g, leaf->sum_h, leaf->gcount, sp_, &per[f],
+                             sp_.has_mono ? &mc : nullptr);
+        if (sp_.has_mono && mono_[f] != 0 && sp_.monotone_penalty > 0 && per[f].feature >= 0)
+          per[f].gain *= MonotonePenaltyFactor(leaf->depth, sp_.monotone_penalty);
       }
       for (int f = 0; f < F_; ++f) {
         if (per[f].feature < 0) continue;
@@ -317,6 +335,15 @@ class CpuBackend : public TrainBackend {
       const int depth = P.depth + 1;
       R.begin = P.begin + nl; R.count = P.count - nl; R.sum_g = sr.right_g; R.sum_h = sr.right_h; R.depth = depth;
       Lf.count = nl; Lf.sum_g = sr.left_g; Lf.sum_h = sr.left_h; Lf.depth = depth;
+      // children inherit the parent's output bounds; a monotone split also
+      // separates them at the midpoint of the two outputs (basic method)
+      R.lo = Lf.lo; R.hi = Lf.hi;
+      const int mdir = sr.is_cat ? 0 : mono_[sr.feature];
+      if (mdir != 0) {
+        const double mid = (sr.left_out + sr.right_out) / 2.0;
+        if (mdir < 0) { Lf.lo = std::max(Lf.lo, mid); R.hi = std::min(R.hi, mid); }
+        else { Lf.hi = std::min(Lf.hi, mid); R.lo = std::max(R.lo, mid); }
+      }
       // smaller child (by the globally consistent estimate) gets a fresh
       // histogram, the larger = parent - smaller
       const int64_t pg = P.gcount;
@@ -368,6 +395,7 @@ class CpuBackend : public TrainBackend {
   std::vector<int32_t> bag_;
   bool use_bag_ = false;
   int64_t last_gcount_ = 0;
+  std::vector<int> mono_;  // monotone direction per inner feature
 };
 
 }  // namespace

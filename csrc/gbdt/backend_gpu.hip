@@ -51,6 +51,7 @@ struct DLeaf {
   int32_t begin, count, buf, depth;  // local row segment; buf: -1 physical, 0/1 ping-pong
   int64_t gcount;                    // global rows
   double sum_g, sum_h;
+  double lo, hi;  // monotone output bounds (basic method)
   int32_t slot, pad;
 };
 
@@ -105,6 +106,7 @@ struct FeatMeta {
   const int32_t* default_bin;
   const int32_t* is_cat;
   const int8_t* mask;
+  const int8_t* mono;  // monotone direction per feature
 };
 
 __device__ __forceinline__ bool DeviceGoesLeft(uint32_t b, int nb, int mt, int dbin, int is_cat,
@@ -448,6 +450,7 @@ __global__ void root_init_kernel(DState* st, DLeaf* leaves, int32_t count, int b
     st->phase = 0; st->cursor = 0ull;
     DLeaf l{};
     l.begin = 0; l.count = count; l.buf = buf; l.depth = 0; l.gcount = count; l.slot = 0;
+    l.lo = -INFINITY; l.hi = INFINITY;
     leaves[0] = l;
   }
 }
@@ -644,7 +647,7 @@ __device__ __forceinline__ bool CandBetter(const Cand& a, const Cand& b) {
 }
 
 __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, int fi, double G, double H,
-                                  int64_t cnt, const SplitParams& sp, SplitResult* best, int* idx) {
+                                  int64_t cnt, const SplitParams& sp, const MonoCtx* mc, SplitResult* best, int* idx) {
   // serial port of the host search (one thread): bins are <= 256
   const double cnt_factor = cnt / fmax(H, kEpsilon);
   const int other = nb - 1;
@@ -656,8 +659,8 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
     if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
     if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
     if (nleft > 1 && (cl < sp.min_data_per_group || cr < sp.min_data_per_group)) return;
-    const double gain = LeafGain(gl, hl, sp.lambda_l1, l2, sp.max_delta_step) +
-                        LeafGain(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+    double gain, lout, rout;
+    if (!EvalSplit(gl, hl, gr, hr, sp.lambda_l1, l2, sp.max_delta_step, mc, &gain, &lout, &rout)) return;
     const double shift = cat_parent + sp.min_gain_to_split;
     if (!(gain > shift)) return;
     const double sg = gain - shift;
@@ -668,8 +671,8 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
     for (int k = 0; k < nleft; ++k) best->cat_bits[left_bins[k] >> 5] |= 1u << (left_bins[k] & 31);
     best->left_g = gl; best->left_h = hl; best->right_g = gr; best->right_h = hr;
     best->left_cnt = cl; best->right_cnt = cr;
-    best->left_out = LeafOutput(gl, hl, sp.lambda_l1, l2, sp.max_delta_step);
-    best->right_out = LeafOutput(gr, hr, sp.lambda_l1, l2, sp.max_delta_step);
+    best->left_out = lout;
+    best->right_out = rout;
   };
   if (nb <= sp.max_cat_to_onehot + 1) {
     for (int b = 0; b < other; ++b) { int lb = b; try_set(1, &lb, hg[b], hh[b]); }
@@ -760,11 +763,14 @@ __device__ void FindSplitBlock(
     if (tid == 0) { out->feature = -1; out->gain = -INFINITY; }
     return;
   }
+  // monotone context of this (leaf, feature); categorical splits are clamped but carry no direction
+  const MonoCtx mc{Lf.lo, Lf.hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
+  const MonoCtx* mcp = sp.has_mono ? &mc : nullptr;
   if (fm.is_cat[f]) {
     if (tid == 0) {
       SplitResult best;
       best.feature = -1; best.gain = -INFINITY;
-      CategoricalSearch(sg_, shh_, nb, f, G, H, cnt, sp, &best, idxbuf);
+      CategoricalSearch(sg_, shh_, nb, f, G, H, cnt, sp, mcp, &best, idxbuf);
       *out = best;
     }
     return;
@@ -796,8 +802,8 @@ __device__ void FindSplitBlock(
       const int64_t cl = EstimateCount(hl, cnt_factor), cr = cnt - cl;
       if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
       if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
-      const double gain = LeafGain(gl, hl, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step) +
-                          LeafGain(gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
+      double gain, lout, rout;
+      if (!EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &gain, &lout, &rout)) return;
       if (!(gain > shift)) return;
       Cand c{gain - shift, tid, dl};
       if (CandBetter(c, best)) best = c;
@@ -831,8 +837,9 @@ __device__ void FindSplitBlock(
       r.is_cat = 0;
       r.left_g = gl; r.left_h = hl; r.right_g = gr; r.right_h = hr;
       r.left_cnt = EstimateCount(hl, cnt_factor); r.right_cnt = cnt - r.left_cnt;
-      r.left_out = LeafOutput(gl, hl, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
-      r.right_out = LeafOutput(gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
+      double g2;
+      (void)EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &g2, &r.left_out, &r.right_out);
+      if (mcp && mc.mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(Lf.depth, sp.monotone_penalty);
       for (int w = 0; w < 8; ++w) r.cat_bits[w] = 0;
     }
     *out = r;
@@ -870,7 +877,7 @@ __device__ __forceinline__ KeyG WaveArgmax(KeyG k) {
 
 __device__ void ChooseBlock(DState* __restrict__ st, DLeaf* __restrict__ leaves, SplitResult* __restrict__ lbest,
                             double* __restrict__ lgain, const SplitResult* __restrict__ fbest, int F, const DTree& t,
-                            const double* __restrict__ count_slot) {
+                            const double* __restrict__ count_slot, const int8_t* __restrict__ mono, int has_mono) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ int sh_best_f[2];
   __shared__ KeyG wk[4];
@@ -969,6 +976,14 @@ __device__ void ChooseBlock(DState* __restrict__ st, DLeaf* __restrict__ leaves,
   Lc.depth = depth; Rc.depth = depth;
   Lc.sum_g = sr.left_g; Lc.sum_h = sr.left_h;
   Rc.sum_g = sr.right_g; Rc.sum_h = sr.right_h;
+  // children inherit the parent's output bounds; a monotone split separates
+  // them at the midpoint of the two outputs (basic method)
+  const int mdir = (has_mono && !sr.is_cat) ? static_cast<int>(mono[sr.feature]) : 0;
+  if (mdir != 0) {
+    const double mid = (sr.left_out + sr.right_out) / 2.0;
+    if (mdir < 0) { Lc.lo = fmax(Lc.lo, mid); Rc.hi = fmin(Rc.hi, mid); }
+    else { Lc.hi = fmin(Lc.hi, mid); Rc.lo = fmax(Rc.lo, mid); }
+  }
   const bool left_small = sr.left_cnt <= sr.right_cnt;
   st->parent_slot = P.slot;
   Lc.slot = 2 * node + 1;
@@ -1000,9 +1015,10 @@ __global__ __launch_bounds__(256) void find_split_kernel(
 __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DLeaf* __restrict__ leaves,
                                                      SplitResult* __restrict__ lbest, double* __restrict__ lgain,
                                                      const SplitResult* __restrict__ fbest, int F, DTree t,
-                                                     const double* __restrict__ count_slot) {
+                                                     const double* __restrict__ count_slot,
+                                                     const int8_t* __restrict__ mono, int has_mono) {
   if (st->done) return;
-  ChooseBlock(st, leaves, lbest, lgain, fbest, F, t, count_slot);
+  ChooseBlock(st, leaves, lbest, lgain, fbest, F, t, count_slot, mono, has_mono);
 }
 
 // ---------------------------------------------------------------- K6
@@ -1283,8 +1299,18 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipMemcpy(meta_i_.get() + 2 * F_, db.data(), sizeof(int32_t) * F_, hipMemcpyHostToDevice));
     SML_HIP_CHECK(hipMemcpy(meta_i_.get() + 3 * F_, ic.data(), sizeof(int32_t) * F_, hipMemcpyHostToDevice));
     mask_.alloc(F_);
+    {
+      std::vector<int8_t> mono(F_, 0);
+      for (int f = 0; f < F_; ++f) {
+        const int col = d->ref.used_features[f];
+        if (col < static_cast<int>(cfg.monotone_constraints.size()))
+          mono[f] = static_cast<int8_t>(cfg.monotone_constraints[col] > 0 ? 1 : (cfg.monotone_constraints[col] < 0 ? -1 : 0));
+      }
+      mono_.alloc(F_);
+      SML_HIP_CHECK(hipMemcpy(mono_.get(), mono.data(), F_, hipMemcpyHostToDevice));
+    }
     fm_.num_bin = meta_i_.get(); fm_.missing = meta_i_.get() + F_; fm_.default_bin = meta_i_.get() + 2 * F_;
-    fm_.is_cat = meta_i_.get() + 3 * F_; fm_.mask = mask_.get();
+    fm_.is_cat = meta_i_.get() + 3 * F_; fm_.mask = mask_.get(); fm_.mono = mono_.get();
     // device tree
     const int NI = L_ - 1;
     // DState + the device tree live in one allocation so a finished tree comes
@@ -1596,7 +1622,7 @@ class GpuBackend : public TrainBackend {
                        E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
     SML_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, state_, leaves_.get(), lbest_.get(),
-                       lgain_.get(), fbest_.get(), F_, dt_, CountSlot());
+                       lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono);
     SML_HIP_CHECK(hipGetLastError());
   }
 
@@ -1721,7 +1747,7 @@ class GpuBackend : public TrainBackend {
   DevBuf<SplitResult> fbest_, lbest_;
   DevBuf<DLeaf> leaves_;
   DevBuf<int32_t> meta_i_, bag_;
-  DevBuf<int8_t> mask_;
+  DevBuf<int8_t> mask_, mono_;
   DevBuf<unsigned int> ghmax_;
   DevBuf<float> ghmax_partial_;
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)

@@ -74,6 +74,9 @@ const std::map<std::string, std::string>& Aliases() {
       {"tree", "tree_learner"}, {"tree_type", "tree_learner"}, {"tree_learner_type", "tree_learner"},
       {"device", "device_type"}, {"verbose", "verbosity"}, {"mc", "monotone_constraints"},
       {"monotone_constraint", "monotone_constraints"}, {"top_k", "top_k"}, {"topk", "top_k"},
+      {"monotone_constraining_method", "monotone_constraints_method"}, {"mc_method", "monotone_constraints_method"},
+      {"monotone_splits_penalty", "monotone_penalty"}, {"ms_penalty", "monotone_penalty"},
+      {"mc_penalty", "monotone_penalty"},
   };
   return m;
 }
@@ -146,6 +149,8 @@ void Config::Set(const std::string& key_in, const std::string& value_in) {
   else if (key == "max_cat_to_onehot") max_cat_to_onehot = I();
   else if (key == "min_data_per_group") min_data_per_group = I();
   else if (key == "monotone_constraints") monotone_constraints = ParseList<int>(v);
+  else if (key == "monotone_constraints_method") monotone_constraints_method = v;
+  else if (key == "monotone_penalty") monotone_penalty = D();
   else if (key == "label_gain") label_gain = ParseList<double>(v);
   else if (key == "eval_at") eval_at = ParseList<int>(v);
   else if (key == "max_position" || key == "lambdarank_truncation_level") max_position = I();
@@ -286,6 +291,8 @@ std::string Config::ToParametersSection() const {
   o << "[max_cat_to_onehot: " << max_cat_to_onehot << "]\n";
   o << "[top_k: " << top_k << "]\n";
   o << "[monotone_constraints: " << lst(monotone_constraints) << "]\n";
+  o << "[monotone_constraints_method: " << monotone_constraints_method << "]\n";
+  o << "[monotone_penalty: " << monotone_penalty << "]\n";
   o << "[max_bin: " << max_bin << "]\n";
   o << "[max_bin_by_feature: " << lst(max_bin_by_feature) << "]\n";
   o << "[min_data_in_bin: " << min_data_in_bin << "]\n";
@@ -321,7 +328,7 @@ std::string Config::ToParametersSection() const {
       "lambda_l1", "lambda_l2", "min_gain_to_split", "drop_rate", "max_drop", "skip_drop",
       "xgboost_dart_mode", "uniform_drop", "drop_seed", "top_rate", "other_rate",
       "min_data_per_group", "max_cat_threshold", "cat_l2", "cat_smooth", "max_cat_to_onehot",
-      "top_k", "monotone_constraints", "max_bin", "max_bin_by_feature", "min_data_in_bin",
+      "top_k", "monotone_constraints", "monotone_constraints_method", "monotone_penalty", "max_bin", "max_bin_by_feature", "min_data_in_bin",
       "bin_construct_sample_cnt", "data_random_seed", "is_enable_sparse", "use_missing",
       "zero_as_missing", "categorical_feature", "num_class", "is_unbalance", "scale_pos_weight",
       "sigmoid", "boost_from_average", "alpha", "fair_c", "poisson_max_delta_step",

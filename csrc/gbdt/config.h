@@ -75,6 +75,8 @@ struct Config {
   int min_data_per_group = 100;
   // constraints
   std::vector<int> monotone_constraints;
+  std::string monotone_constraints_method = "basic";  // basic (intermediate/advanced run as basic)
+  double monotone_penalty = 0.0;
   // ranking
   std::vector<double> label_gain;
   std::vector<int> eval_at;

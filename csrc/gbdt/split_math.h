@@ -23,6 +23,19 @@ struct SplitParams {
   // categorical
   double cat_l2, cat_smooth;
   int max_cat_threshold, max_cat_to_onehot, min_data_per_group;
+  // monotone constraints (LightGBM "basic" method): any feature constrained
+  int has_mono;
+  double monotone_penalty;
+};
+
+// Output bounds of the leaf being split and the monotone direction of the
+// candidate feature (+1 increasing, -1 decreasing, 0 none). LightGBM's basic
+// method (BasicLeafConstraints): child outputs are clamped into the leaf's
+// [lo, hi], a split whose clamped outputs violate the direction is rejected,
+// and the gain is evaluated at the clamped outputs.
+struct MonoCtx {
+  double lo, hi;
+  int mono;
 };
 
 SML_HD double ThresholdL1(double s, double l1) {
@@ -48,6 +61,34 @@ SML_HD double LeafGain(double g, double h, double l1, double l2, double max_delt
     return sg * sg / (h + l2);
   }
   return LeafGainGivenOutput(g, h, l1, l2, LeafOutput(g, h, l1, l2, max_delta_step));
+}
+
+// Gain of a candidate split (before subtracting the parent's gain) and the two
+// leaf outputs; false if a monotone constraint rejects it. mc == nullptr is the
+// unconstrained path (bitwise the historical formulas).
+SML_HD bool EvalSplit(double gl, double hl, double gr, double hr, double l1, double l2, double max_delta_step,
+                      const MonoCtx* mc, double* gain, double* lout, double* rout) {
+  double lo = LeafOutput(gl, hl, l1, l2, max_delta_step);
+  double ro = LeafOutput(gr, hr, l1, l2, max_delta_step);
+  if (mc == nullptr) {
+    *gain = LeafGain(gl, hl, l1, l2, max_delta_step) + LeafGain(gr, hr, l1, l2, max_delta_step);
+  } else {
+    lo = lo < mc->lo ? mc->lo : (lo > mc->hi ? mc->hi : lo);
+    ro = ro < mc->lo ? mc->lo : (ro > mc->hi ? mc->hi : ro);
+    if ((mc->mono > 0 && lo > ro) || (mc->mono < 0 && lo < ro)) return false;
+    *gain = LeafGainGivenOutput(gl, hl, l1, l2, lo) + LeafGainGivenOutput(gr, hr, l1, l2, ro);
+  }
+  *lout = lo;
+  *rout = ro;
+  return true;
+}
+
+// LightGBM's monotone_penalty: monotone splits in the first levels are damped
+// (LeafConstraintsBase::ComputeMonotoneSplitGainPenalty).
+SML_HD double MonotonePenaltyFactor(int depth, double penalty) {
+  if (penalty >= depth + 1.0) return kEpsilon;
+  if (penalty <= 1.0) return 1.0 - penalty / pow(2.0, depth) + kEpsilon;
+  return 1.0 - pow(2.0, penalty - 1.0 - depth) + kEpsilon;
 }
 
 SML_HD int64_t EstimateCount(double h, double cnt_factor) {

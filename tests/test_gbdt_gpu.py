@@ -302,3 +302,27 @@ def test_gpu_bin_encode_bit_identical(dtype):
         b.push_dense_gpu(Xt[:40000], 0)
         b.push_dense_gpu(Xt[40000:], 40000)
         np.testing.assert_array_equal(a.bins, b.bins, err_msg=params)
+
+
+@pytest.mark.parametrize("extra", ["monotone_constraints=1,-1,0,0,0,0,0,0,0,0,0,0",
+                                   "monotone_constraints=1,-1,0,0,0,0,0,0,0,0,0,0 monotone_penalty=1.5"])
+def test_gpu_monotone_constraints_match_cpu(extra):
+    """Monotone constraints (basic method) in the device split search / choose bookkeeping."""
+    X, _ = _data(n=60000)
+    y = (1.5 * X[:, 0] - np.sin(3 * X[:, 0]) - X[:, 1] + 0.8 * np.cos(3 * X[:, 1]) + X[:, 2] ** 2).astype(np.float32)
+    base = f"objective=regression num_leaves=31 {extra}"
+    bc = _train(X, y, base + " device_type=cpu", 4)
+    bg = _train(X, y, base + " device_type=gpu", 4)
+    mc, mg = bc.save_model_string(), bg.save_model_string()
+    line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")][0]
+    for t in ("Tree=0", "Tree=3"):
+        tc = mc.split(t)[1].split("Tree=")[0]
+        tg = mg.split(t)[1].split("Tree=")[0]
+        assert line(tc, "split_feature") == line(tg, "split_feature")
+        np.testing.assert_allclose(np.array(line(tc, "leaf_value").split("=")[1].split(), float),
+                                   np.array(line(tg, "leaf_value").split("=")[1].split(), float), rtol=1e-4, atol=1e-6)
+    grid = np.linspace(-2.5, 2.5, 51)
+    rows = np.repeat(X[:20], len(grid), axis=0)
+    rows[:, 0] = np.tile(grid, 20)
+    p = bg.predict(rows, 0, 0, -1)[:, 0].reshape(20, len(grid))
+    assert (np.diff(p, axis=1) >= -1e-12).all()

@@ -307,3 +307,32 @@ def test_checkpoint_resume_matches_uninterrupted(tmp_path):
     np.testing.assert_allclose(resumed.transform(df)["probability"], full.transform(df)["probability"],
                                rtol=1e-9, atol=1e-12)
     assert json.load(open(os.path.join(ck, "latest.json")))["complete"]
+
+
+@pytest.mark.parametrize("penalty", [0.0, 1.5])
+def test_monotone_constraints_basic(penalty):
+    """monotoneConstraints (LightGBMParams.scala:199-216, basic method): predictions are monotone
+    in the constrained features for every setting of the others."""
+    rng = np.random.default_rng(11)
+    n = 4000
+    X = rng.uniform(-2, 2, size=(n, 4))
+    y = 1.5 * X[:, 0] - np.sin(3 * X[:, 0]) - X[:, 1] + 0.8 * np.cos(3 * X[:, 1]) + X[:, 2] ** 2 \
+        + 0.3 * rng.standard_normal(n)
+    df = DataFrame({"features": X, "label": y})
+    m = LightGBMRegressor(deviceType="cpu", numIterations=40, numLeaves=15, monotoneConstraints=[1, -1, 0, 0],
+                          monotonePenalty=penalty).fit(df)
+    assert "[monotone_constraints: 1,-1,0,0]" in m.getNativeModel()
+    grid = np.linspace(-2, 2, 41)
+    base = rng.uniform(-2, 2, size=(30, 4))
+    for f, sign in [(0, 1), (1, -1)]:
+        rows = np.repeat(base, len(grid), axis=0)
+        rows[:, f] = np.tile(grid, len(base))
+        p = m.transform(DataFrame({"features": rows}))["prediction"].reshape(len(base), len(grid))
+        d = np.diff(p, axis=1) * sign
+        assert (d >= -1e-12).all(), (f, d.min())
+    # an unconstrained model is not monotone on this data (the constraint is doing the work)
+    free = LightGBMRegressor(deviceType="cpu", numIterations=40, numLeaves=15).fit(df)
+    rows = np.repeat(base, len(grid), axis=0)
+    rows[:, 0] = np.tile(grid, len(base))
+    p = free.transform(DataFrame({"features": rows}))["prediction"].reshape(len(base), len(grid))
+    assert (np.diff(p, axis=1) < -1e-9).any()
