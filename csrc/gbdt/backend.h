@@ -66,5 +66,7 @@ void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinM
                           int feature_inner, double sum_g, double sum_h, int64_t cnt,
                           const SplitParams& sp, SplitResult* best, const MonoCtx* mc = nullptr);
 SplitParams MakeSplitParams(const Config& cfg);
+// features each node samples under feature_fraction_bynode (0 = every allowed feature)
+int BynodeK(const Config& cfg, const std::vector<char>& allowed);
 
 }  // namespace sml

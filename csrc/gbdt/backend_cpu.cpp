@@ -16,6 +16,13 @@
 
 namespace sml {
 
+int BynodeK(const Config& c, const std::vector<char>& allowed) {
+  if (c.feature_fraction_bynode >= 1.0) return 0;
+  int n = 0;
+  for (char a : allowed) n += a ? 1 : 0;
+  return std::max(1, static_cast<int>(std::ceil(n * c.feature_fraction_bynode - 1e-9)));
+}
+
 SplitParams MakeSplitParams(const Config& c) {
   SplitParams p;
   p.lambda_l1 = c.lambda_l1; p.lambda_l2 = c.lambda_l2; p.max_delta_step = c.max_delta_step;
@@ -26,6 +33,9 @@ SplitParams MakeSplitParams(const Config& c) {
   p.has_mono = 0;
   for (int m : c.monotone_constraints) if (m != 0) p.has_mono = 1;
   p.monotone_penalty = c.monotone_penalty;
+  p.bynode_k = 0;  // set per tree by the backends
+  p.tree_seq = 0;
+  p.bynode_seed = static_cast<unsigned long long>(c.feature_fraction_seed) * 0x2545F4914F6CDD1Dull + 17ull;
   return p;
 }
 
@@ -149,6 +159,7 @@ struct LeafInfo {
   int64_t gcount = 0;            // global row count (all ranks)
   double sum_g = 0, sum_h = 0;
   int depth = 0;
+  int slot = 0;  // node id for feature_fraction_bynode: root 0, children of internal node i: 2i+1, 2i+2
   double lo = -std::numeric_limits<double>::infinity();  // monotone output bounds
   double hi = std::numeric_limits<double>::infinity();
   SplitResult best;
@@ -240,6 +251,10 @@ class CpuBackend : public TrainBackend {
         per[f].feature = -1;
         per[f].gain = -std::numeric_limits<double>::infinity();
         if (!fmask[f]) continue;
+        if (sp_.bynode_k > 0 &&
+            !NodeFeatureSelected(sp_.bynode_seed, sp_.tree_seq, leaf->slot, f,
+                                 reinterpret_cast<const int8_t*>(fmask.data()), F_, sp_.bynode_k))
+          continue;
         const BinMapper& m = data_->ref.mappers[data_->ref.used_features[f]];
         for (int b = 0; b < m.num_bin; ++b) { tg[b] = hist[f * 512 + b * 2]; th[b] = hist[f * 512 + b * 2 + 1]; }
         const MonoCtx mc{leaf->lo, leaf->hi, mono_[f]};
@@ -271,6 +286,8 @@ class CpuBackend : public TrainBackend {
   Tree TrainTree(int k, const std::vector<char>& fmask_in) override {
     std::vector<char> fmask = fmask_in;
     if (static_cast<int>(fmask.size()) != F_) fmask.assign(F_, 1);
+    sp_.tree_seq = tree_seq_++;
+    sp_.bynode_k = BynodeK(cfg_, fmask);
     const int L = std::max(2, cfg_.num_leaves);
     Tree tree(L);
     // root
@@ -338,6 +355,9 @@ class CpuBackend : public TrainBackend {
       // children inherit the parent's output bounds; a monotone split also
       // separates them at the midpoint of the two outputs (basic method)
       R.lo = Lf.lo; R.hi = Lf.hi;
+      const int inode = tree.num_leaves - 2;
+      Lf.slot = 2 * inode + 1;
+      R.slot = 2 * inode + 2;
       const int mdir = sr.is_cat ? 0 : mono_[sr.feature];
       if (mdir != 0) {
         const double mid = (sr.left_out + sr.right_out) / 2.0;
@@ -396,6 +416,7 @@ class CpuBackend : public TrainBackend {
   bool use_bag_ = false;
   int64_t last_gcount_ = 0;
   std::vector<int> mono_;  // monotone direction per inner feature
+  int tree_seq_ = 0;
 };
 
 }  // namespace

@@ -758,7 +758,9 @@ __device__ void FindSplitBlock(
   }
   SplitResult* out = fbest + child * F + f;
   const bool eligible = fm.mask[f] && nb > 1 && cnt >= 2 * static_cast<int64_t>(sp.min_data_in_leaf) &&
-                        (sp.max_depth <= 0 || Lf.depth < sp.max_depth);
+                        (sp.max_depth <= 0 || Lf.depth < sp.max_depth) &&
+                        (sp.bynode_k <= 0 ||
+                         NodeFeatureSelected(sp.bynode_seed, sp.tree_seq, Lf.slot, f, fm.mask, F, sp.bynode_k));
   if (!eligible) {
     if (tid == 0) { out->feature = -1; out->gain = -INFINITY; }
     return;
@@ -1469,6 +1471,8 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipEventRecord(ev_[0], stream_));
     std::vector<int8_t> fmask(F_, 1);
     for (int f = 0; f < F_ && f < static_cast<int>(fmask_in.size()); ++f) fmask[f] = fmask_in[f] ? 1 : 0;
+    sp_.tree_seq = tree_seq_++;
+    sp_.bynode_k = BynodeK(cfg_, std::vector<char>(fmask.begin(), fmask.end()));
     SML_HIP_CHECK(hipMemcpyAsync(mask_.get(), fmask.data(), F_, hipMemcpyHostToDevice, stream_));
     const float* g = g_.get() + static_cast<size_t>(k) * n_;
     const float* h = h_.get() + static_cast<size_t>(k) * n_;
@@ -1750,6 +1754,7 @@ class GpuBackend : public TrainBackend {
   DevBuf<int8_t> mask_, mono_;
   DevBuf<unsigned int> ghmax_;
   DevBuf<float> ghmax_partial_;
+  int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
   int part_grid_ = 1;
   DevBuf<uint8_t> blob_;

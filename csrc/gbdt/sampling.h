@@ -27,6 +27,26 @@ SML_HD double RowUniform(uint64_t seed, int iter, int64_t row) {
   return static_cast<double>(SplitMix64(s + static_cast<uint64_t>(row)) >> 11) * (1.0 / 9007199254740992.0);
 }
 
+// feature_fraction_bynode: is feature f among the k sampled for node `node`
+// of tree `tree`? Every allowed feature gets a hash key; the k smallest win.
+// Pure function of (seed, tree, node, f), so host and device agree and each
+// split-search block decides for its own feature without a shared shuffle.
+SML_HD uint64_t NodeFeatureKey(uint64_t seed, int tree, int node, int f) {
+  return SplitMix64(SplitMix64(seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(tree + 1))) ^
+                    (0xC2B2AE3D27D4EB4Full * static_cast<uint64_t>(node + 1)) ^ static_cast<uint64_t>(f));
+}
+
+SML_HD bool NodeFeatureSelected(uint64_t seed, int tree, int node, int f, const int8_t* allowed, int F, int k) {
+  const uint64_t key = NodeFeatureKey(seed, tree, node, f);
+  int rank = 0;
+  for (int g = 0; g < F; ++g) {
+    if (g == f || !allowed[g]) continue;
+    const uint64_t kg = NodeFeatureKey(seed, tree, node, g);
+    rank += (kg < key) || (kg == key && g < f);
+  }
+  return rank < k;
+}
+
 enum RowSampleKind : int { kSampleBagging = 1, kSampleGoss = 2 };
 
 struct RowSampleSpec {

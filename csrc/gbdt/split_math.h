@@ -26,6 +26,10 @@ struct SplitParams {
   // monotone constraints (LightGBM "basic" method): any feature constrained
   int has_mono;
   double monotone_penalty;
+  // feature_fraction_bynode: each node samples bynode_k of the tree's allowed
+  // features (bynode_k == 0: off); tree_seq numbers the trees of the run
+  int bynode_k, tree_seq;
+  unsigned long long bynode_seed;
 };
 
 // Output bounds of the leaf being split and the monotone direction of the

@@ -326,3 +326,17 @@ def test_gpu_monotone_constraints_match_cpu(extra):
     rows[:, 0] = np.tile(grid, 20)
     p = bg.predict(rows, 0, 0, -1)[:, 0].reshape(20, len(grid))
     assert (np.diff(p, axis=1) >= -1e-12).all()
+
+
+def test_gpu_feature_fraction_bynode_matches_cpu():
+    """feature_fraction_bynode: per-node feature subsets drawn from a (seed, tree, node, feature) hash on both backends."""
+    X, y = _data(n=50000)
+    base = "objective=binary num_leaves=31 feature_fraction_bynode=0.5 feature_fraction=0.8"
+    bc = _train(X, y, base + " device_type=cpu", 4)
+    bg = _train(X, y, base + " device_type=gpu", 4)
+    line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")][0]
+    mc, mg = bc.save_model_string(), bg.save_model_string()
+    for t in ("Tree=0", "Tree=3"):
+        tc = mc.split(t)[1].split("Tree=")[0]
+        tg = mg.split(t)[1].split("Tree=")[0]
+        assert line(tc, "split_feature") == line(tg, "split_feature")

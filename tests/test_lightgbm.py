@@ -336,3 +336,16 @@ def test_monotone_constraints_basic(penalty):
     rows[:, 0] = np.tile(grid, len(base))
     p = free.transform(DataFrame({"features": rows}))["prediction"].reshape(len(base), len(grid))
     assert (np.diff(p, axis=1) < -1e-9).any()
+
+
+def test_feature_fraction_bynode_changes_trees_deterministically():
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((3000, 10))
+    y = (X[:, 0] + X[:, 1] - X[:, 2] > 0).astype(float)
+    df = DataFrame({"features": X, "label": y})
+    a = LightGBMClassifier(deviceType="cpu", numIterations=5, featureFractionByNode=0.3).fit(df)
+    b = LightGBMClassifier(deviceType="cpu", numIterations=5, featureFractionByNode=0.3).fit(df)
+    c = LightGBMClassifier(deviceType="cpu", numIterations=5).fit(df)
+    assert a.getNativeModel() == b.getNativeModel()
+    strip = lambda s: s.split("parameters:")[0]
+    assert strip(a.getNativeModel()) != strip(c.getNativeModel())
