@@ -204,7 +204,8 @@ class CpuBackend : public TrainBackend {
     if (rows) { bag_ = *rows; use_bag_ = true; } else { bag_.clear(); use_bag_ = false; }
   }
 
-  void BuildHist(int k, const LeafInfo& leaf, const std::vector<char>& fmask, std::vector<double>* hist) {
+  void BuildHist(int k, const LeafInfo& leaf, const std::vector<char>& fmask, std::vector<double>* hist,
+                 bool reduce = true) {
     const int stride = 256 * 2;
     hist->assign(static_cast<size_t>(F_) * stride, 0.0);
     const float* g = g_.data() + static_cast<size_t>(k) * n_;
@@ -229,7 +230,7 @@ class CpuBackend : public TrainBackend {
     }
     for (int t = 0; t < nt; ++t)
       for (size_t i = 0; i < hist->size(); ++i) (*hist)[i] += local[t][i];
-    if (comm_ && comm_->world() > 1) {
+    if (reduce && comm_ && comm_->world() > 1) {
       hist->push_back(static_cast<double>(leaf.count));
       comm_->AllReduceHost(hist->data(), static_cast<int64_t>(hist->size()));
       last_gcount_ = static_cast<int64_t>(hist->back());
@@ -240,11 +241,101 @@ class CpuBackend : public TrainBackend {
   }
 
   void FindBest(const std::vector<double>& hist, LeafInfo* leaf, const std::vector<char>& fmask) {
+    std::vector<SplitResult> per;
+    PerFeatureBest(hist, *leaf, fmask, &per);
     SplitResult best{};
     best.feature = -1;
     best.gain = -std::numeric_limits<double>::infinity();
+    for (int f = 0; f < F_; ++f) {
+      if (per[f].feature < 0) continue;
+      if (best.feature < 0 || SplitBetter(per[f].gain, per[f].feature, per[f].threshold, best.gain, best.feature, best.threshold))
+        best = per[f];
+    }
+    leaf->best = best;
+    leaf->has_best = best.feature >= 0;
+  }
+
+  // Voting-parallel split search (PV-Tree; reference parallelism=voting_parallel, topK,
+  // LightGBMParams.scala:25-35, C3 in SURVEY §2.5). Histograms stay local; every rank
+  // votes for its top_k features per leaf by LOCAL gain, one allreduce sums the votes
+  // (and the smaller child's row count), and only the 2*top_k most-voted features'
+  // histograms of each leaf are summed across ranks before the global split search.
+  void VotingFind(const std::vector<LeafInfo*>& ls, const std::vector<const std::vector<double>*>& lh,
+                  const std::vector<char>& fmask, int64_t parent_gcount) {
+    const int C = static_cast<int>(ls.size());
+    const int topk = std::max(1, cfg_.top_k);
+    std::vector<double> msg(static_cast<size_t>(2 * C * F_) + 1, 0.0);
+    std::vector<SplitResult> per;
+    for (int c = 0; c < C; ++c) {
+      LeafInfo loc = *ls[c];
+      double G = 0, H = 0;
+      int f0 = 0;
+      while (f0 < F_ && !fmask[f0]) ++f0;
+      if (f0 < F_)
+        for (int b = 0; b < 256; ++b) { G += (*lh[c])[f0 * 512 + b * 2]; H += (*lh[c])[f0 * 512 + b * 2 + 1]; }
+      loc.sum_g = G; loc.sum_h = H; loc.gcount = loc.count;
+      // local search with per-machine data limits (LightGBM scales min_data / min_hessian by 1/#machines)
+      const SplitParams keep = sp_;
+      sp_.min_data_in_leaf = std::max(1, sp_.min_data_in_leaf / comm_->world());
+      sp_.min_sum_hessian /= comm_->world();
+      PerFeatureBest(*lh[c], loc, fmask, &per);
+      sp_ = keep;
+      std::vector<int> order;
+      for (int f = 0; f < F_; ++f) if (per[f].feature >= 0) order.push_back(f);
+      std::sort(order.begin(), order.end(), [&](int a, int b) {
+        return SplitBetter(per[a].gain, a, 0, per[b].gain, b, 0);
+      });
+      for (int i = 0; i < static_cast<int>(order.size()) && i < topk; ++i) {
+        msg[c * F_ + order[i]] = 1.0;
+        msg[(C + c) * F_ + order[i]] = per[order[i]].gain;
+      }
+    }
+    if (C == 2) msg.back() = static_cast<double>(ls[0]->count);  // ls[0] = smaller child
+    comm_->AllReduceHost(msg.data(), static_cast<int64_t>(msg.size()));
+    if (C == 2) {
+      ls[0]->gcount = static_cast<int64_t>(msg.back());
+      ls[1]->gcount = parent_gcount - ls[0]->gcount;
+    }
+    std::vector<std::vector<int>> sel(C);
+    std::vector<double> compact;
+    for (int c = 0; c < C; ++c) {
+      std::vector<int> cand;
+      for (int f = 0; f < F_; ++f) if (msg[c * F_ + f] > 0) cand.push_back(f);
+      std::sort(cand.begin(), cand.end(), [&](int a, int b) {
+        const double va = msg[c * F_ + a], vb = msg[c * F_ + b];
+        if (va != vb) return va > vb;
+        const double ga = msg[(C + c) * F_ + a], gb = msg[(C + c) * F_ + b];
+        if (ga != gb) return ga > gb;
+        return a < b;
+      });
+      // fewer voted features than slots: fill with unvoted allowed ones (so top_k >= #features == data-parallel)
+      for (int f = 0; f < F_ && static_cast<int>(cand.size()) < 2 * topk; ++f)
+        if (fmask[f] && msg[c * F_ + f] <= 0) cand.push_back(f);
+      if (static_cast<int>(cand.size()) > 2 * topk) cand.resize(2 * topk);
+      sel[c] = cand;
+      for (int f : cand) compact.insert(compact.end(), lh[c]->begin() + f * 512, lh[c]->begin() + (f + 1) * 512);
+    }
+    if (!compact.empty()) comm_->AllReduceHost(compact.data(), static_cast<int64_t>(compact.size()));
+    size_t off = 0;
+    for (int c = 0; c < C; ++c) {
+      std::vector<double> global(static_cast<size_t>(F_) * 512, 0.0);
+      std::vector<char> mask(F_, 0);
+      for (int f : sel[c]) {
+        std::copy(compact.begin() + off, compact.begin() + off + 512, global.begin() + f * 512);
+        off += 512;
+        mask[f] = fmask[f];
+      }
+      FindBest(global, ls[c], mask);
+    }
+  }
+
+  void PerFeatureBest(const std::vector<double>& hist, const LeafInfo& leaf_in, const std::vector<char>& fmask,
+                      std::vector<SplitResult>* per_out) {
+    std::vector<SplitResult>& per = *per_out;
+    per.assign(F_, SplitResult{});
+    for (auto& r : per) { r.feature = -1; r.gain = -std::numeric_limits<double>::infinity(); }
+    const LeafInfo* leaf = &leaf_in;
     if (leaf->gcount >= 2 * sp_.min_data_in_leaf && (sp_.max_depth <= 0 || leaf->depth < sp_.max_depth)) {
-      std::vector<SplitResult> per(F_);
       std::vector<double> tg(256), th(256);
 #pragma omp parallel for schedule(dynamic) firstprivate(tg, th)
       for (int f = 0; f < F_; ++f) {
@@ -263,14 +354,7 @@ class CpuBackend : public TrainBackend {
         if (sp_.has_mono && mono_[f] != 0 && sp_.monotone_penalty > 0 && per[f].feature >= 0)
           per[f].gain *= MonotonePenaltyFactor(leaf->depth, sp_.monotone_penalty);
       }
-      for (int f = 0; f < F_; ++f) {
-        if (per[f].feature < 0) continue;
-        if (best.feature < 0 || SplitBetter(per[f].gain, per[f].feature, per[f].threshold, best.gain, best.feature, best.threshold))
-          best = per[f];
-      }
     }
-    leaf->best = best;
-    leaf->has_best = best.feature >= 0;
   }
 
   bool GoesLeft(const SplitResult& s, const uint8_t* row) const {
@@ -310,8 +394,10 @@ class CpuBackend : public TrainBackend {
     tree.leaf_value[0] = LeafOutput(G, H, sp_.lambda_l1, sp_.lambda_l2, sp_.max_delta_step);
     tree.leaf_count[0] = leaves[0].gcount;
     tree.leaf_weight[0] = H;
-    BuildHist(k, leaves[0], fmask, &hists[0]);
-    FindBest(hists[0], &leaves[0], fmask);
+    const bool voting = cfg_.tree_learner == "voting" && comm_ && comm_->world() > 1;
+    BuildHist(k, leaves[0], fmask, &hists[0], !voting);
+    if (voting) VotingFind({&leaves[0]}, {&hists[0]}, fmask, leaves[0].gcount);
+    else FindBest(hists[0], &leaves[0], fmask);
     std::vector<int64_t> tmp;
     for (int s = 1; s < L; ++s) {
       int bl = -1;
@@ -370,13 +456,17 @@ class CpuBackend : public TrainBackend {
       const bool left_small = sr.left_cnt <= sr.right_cnt;
       int small = left_small ? bl : right, large = left_small ? right : bl;
       std::vector<double> parent = std::move(hists[bl]);
-      BuildHist(k, leaves[small], fmask, &hists[small]);
-      leaves[small].gcount = last_gcount_;
-      leaves[large].gcount = pg - last_gcount_;
+      BuildHist(k, leaves[small], fmask, &hists[small], !voting);
       hists[large].resize(parent.size());
       for (size_t i = 0; i < parent.size(); ++i) hists[large][i] = parent[i] - hists[small][i];
-      FindBest(hists[bl], &leaves[bl], fmask);
-      FindBest(hists[right], &leaves[right], fmask);
+      if (voting) {
+        VotingFind({&leaves[small], &leaves[large]}, {&hists[small], &hists[large]}, fmask, pg);
+      } else {
+        leaves[small].gcount = last_gcount_;
+        leaves[large].gcount = pg - last_gcount_;
+        FindBest(hists[bl], &leaves[bl], fmask);
+        FindBest(hists[right], &leaves[right], fmask);
+      }
     }
     // exact (global) leaf counts
     for (int l = 0; l < tree.num_leaves; ++l) tree.leaf_count[l] = leaves[l].gcount;

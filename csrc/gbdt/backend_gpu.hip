@@ -17,6 +17,10 @@
 // without any host round trip (the tree is read back once at the end).
 // Data-parallel training inserts an RCCL allreduce of the smaller child's
 // histogram between the slab reduce and the split search (C2 over xGMI).
+// tree_learner=voting (C3) runs as data-parallel here: a full-histogram
+// one-shot allreduce over xGMI (~114 KB, comm_p2p.hip) costs less than the
+// vote round trip plus the selected-feature reduction it would replace
+// (SURVEY §5.8); the host backend implements the PV-Tree vote for CPU clusters.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -164,7 +164,12 @@ void Config::Set(const std::string& key_in, const std::string& value_in) {
   else if (key == "extra_seed") extra_seed = I();
   else if (key == "objective_seed") objective_seed = I();
   else if (key == "num_machines") num_machines = I();
-  else if (key == "tree_learner") tree_learner = v;
+  else if (key == "tree_learner") {
+    tree_learner = v;
+    if (v == "voting_parallel") tree_learner = "voting";
+    else if (v == "data_parallel") tree_learner = "data";
+    else if (v == "feature_parallel") tree_learner = "feature";
+  }
   else if (key == "top_k") top_k = I();
   else if (key == "gpu_device_id") gpu_device_id = I();
   else if (key == "use_quantized_grad") use_quantized_grad = B();

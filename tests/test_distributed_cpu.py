@@ -75,3 +75,28 @@ def test_empty_partition_rank_still_joins(monkeypatch):
     monkeypatch.setenv("SML_FAULT_INJECT", "1:empty")
     out = run_partitions(_allreduce_task, DataFrame({"x": np.arange(8.0)}, num_partitions=2), num_workers=2)
     assert len(out) == 2
+
+
+def test_voting_parallel_two_ranks():
+    """voting_parallel (PV-Tree): with topK >= #features every feature is reduced, so the
+    model equals data-parallel; with topK=1 only voted features are reduced and the model still learns."""
+    from sklearn.metrics import roc_auc_score
+
+    rng = np.random.default_rng(1)
+    n = 6000
+    X = rng.standard_normal((n, 8))
+    y = (X[:, 0] + 0.8 * X[:, 1] * X[:, 2] - 0.5 * X[:, 3] > 0).astype(float)
+    df = DataFrame({"features": X, "label": y}, num_partitions=2)
+    ref = LightGBMClassifier(deviceType="cpu", numIterations=1).fit(df) and None
+    base = LightGBMClassifier(deviceType="cpu", numIterations=1)
+    base.fit(df)
+    ref = base._last_reference
+    kw = dict(deviceType="cpu", numIterations=10, numThreads=1, referenceDataset=ref)
+    data_m = distributed_fit(LightGBMClassifier(**kw), df, num_workers=2)
+    vote_all = distributed_fit(LightGBMClassifier(parallelism="voting_parallel", topK=8, **kw), df, num_workers=2)
+    vote_1 = distributed_fit(LightGBMClassifier(parallelism="voting_parallel", topK=1, **kw), df, num_workers=2)
+    splits = lambda m: [l for l in m.getNativeModel().splitlines() if l.startswith(("split_feature=", "threshold="))]
+    assert splits(vote_all) == splits(data_m)
+    assert "[tree_learner: voting]" in vote_1.getNativeModel()
+    p = vote_1.transform(df)["probability"][:, 1]
+    assert roc_auc_score(y, p) > 0.85
