@@ -226,31 +226,65 @@ __device__ __forceinline__ double WaveSumD(double v) {
   return v;
 }
 
-// lambda / hessian contribution of the pair (doc i, doc j) to doc i
-__device__ __forceinline__ void PairLambda(const RankTables& t, double si, int li, int ri, double sj, int lj, int rj,
-                                           double imd, bool use_norm, double* lam, double* hes, double* suml) {
+// lambda / hessian contribution of the pair (doc i, doc j) to doc i; disc(r)
+// = 1/log2(2+r) comes from an LDS table for ranks below kRankLds
+__device__ __forceinline__ double Discount(const double* s_disc, int r) {
+  return r < kRankLds ? s_disc[r] : 1.0 / log2(2.0 + r);
+}
+
+__device__ __forceinline__ void PairLambda(const RankTables& t, const double* s_disc, double si, int li, int ri,
+                                           double sj, int lj, int rj, double imd, bool use_norm, double* lam,
+                                           double* hes, double* suml) {
   const bool i_high = li > lj;
   const int hr = i_high ? ri : rj, lr = i_high ? rj : ri;
   const unsigned lh = static_cast<unsigned>(i_high ? li : lj), ll = static_cast<unsigned>(i_high ? lj : li);
   const unsigned top = static_cast<unsigned>(t.ngain - 1);
-  const double gap = t.gain[min(lh, top)] - t.gain[min(ll, top)];
-  const double pd = fabs(1.0 / log2(2.0 + hr) - 1.0 / log2(2.0 + lr));
-  const double ds = i_high ? si - sj : sj - si;
-  double dn = gap * pd * imd;
-  if (use_norm) dn /= (0.01 + fabs(ds));
-  double pl = 1.0 / (1.0 + exp(t.sigma * ds));
-  double ph = pl * (1.0 - pl);
-  pl *= -t.sigma * dn;
-  ph *= t.sigma * t.sigma * dn;
+  // The per-pair math runs in fp32 (FP64 divides / exp are ~20x the
+  // instruction count and made the kernel FP64-issue bound); the lambdas are
+  // accumulated in fp64 and end up as fp32 gradients, like the host path.
+  const float gap = static_cast<float>(t.gain[min(lh, top)] - t.gain[min(ll, top)]);
+  const float pd = fabsf(static_cast<float>(Discount(s_disc, hr) - Discount(s_disc, lr)));
+  const float ds = static_cast<float>(i_high ? si - sj : sj - si);
+  const float sig = static_cast<float>(t.sigma);
+  float dn = gap * pd * static_cast<float>(imd);
+  if (use_norm) dn = __fdividef(dn, 0.01f + fabsf(ds));
+  float pl = __frcp_rn(1.0f + __expf(sig * ds));
+  float ph = pl * (1.0f - pl);
+  pl *= -sig * dn;
+  ph *= sig * sig * dn;
   *lam += i_high ? pl : -pl;
   *hes += ph;
   *suml -= pl;  // each pair is visited from both ends: sum = -2 pl per pair
 }
 
+// All pairs of doc i: a doc ranked below max_position only pairs with the
+// top max_position documents (s_top, by rank), a top document with every
+// other document.
+template <bool kSmall>
+__device__ __forceinline__ void DocLambdas(const RankTables& t, const double* s_disc, const int* s_top, int ntop,
+                                           const double* sc, const int* labs, const float* __restrict__ label,
+                                           const int* rk, int b, int cnt, int i, double imd, bool use_norm,
+                                           double* la, double* he, double* suml) {
+  const double si = sc[i];
+  const int li = kSmall ? labs[i] : static_cast<int>(label[b + i]);
+  const int ri = rk[i];
+  const bool scan_top = ri >= t.max_position && ntop >= 0;
+  const int m = scan_top ? ntop : cnt;
+  for (int q = 0; q < m; ++q) {
+    const int j = scan_top ? s_top[q] : q;
+    const int lj = kSmall ? labs[j] : static_cast<int>(label[b + j]);
+    if (lj == li) continue;
+    const int rj = rk[j];
+    if (min(ri, rj) >= t.max_position) continue;
+    PairLambda(t, s_disc, si, li, ri, sc[j], lj, rj, imd, use_norm, la, he, suml);
+  }
+}
+
 template <bool kSmall>
 __device__ void LambdarankQuery(const RankTables& t, int q, const double* __restrict__ score,
                                 const float* __restrict__ label, const float* __restrict__ weight,
-                                float* __restrict__ g, float* __restrict__ h, double* s_sc, int* s_lab, int* s_rk) {
+                                float* __restrict__ g, float* __restrict__ h, double* s_sc, int* s_lab, int* s_rk,
+                                const double* s_disc, int* s_top, double* s_tlam, double* s_thes) {
   const int lane = threadIdx.x;
   const int b = t.qb[q], cnt = t.qb[q + 1] - b;
   const double* sc = kSmall ? s_sc : score + b;
@@ -268,6 +302,9 @@ __device__ void LambdarankQuery(const RankTables& t, int q, const double* __rest
   }
   __syncthreads();
   int* rk = kSmall ? s_rk : t.rank_scratch + b;
+  // ranks are a permutation of 0..cnt-1; the documents ranked above
+  // max_position are listed by rank (s_top) when the list fits in LDS
+  const int ntop = t.max_position <= kRankLds ? min(cnt, t.max_position) : -1;
   for (int i = lane; i < cnt; i += 64) {
     const double si = sc[i];
     int r = 0;
@@ -276,35 +313,74 @@ __device__ void LambdarankQuery(const RankTables& t, int q, const double* __rest
       r += (sj > si) || (sj == si && j < i);
     }
     rk[i] = r;
+    if (ntop >= 0 && r < ntop) s_top[r] = i;
   }
   __syncthreads();
   const double imd = t.inv_max_dcg[q];
   const bool use_norm = t.norm && mx != mn;
   double lam[kRankPerLane], hes[kRankPerLane];
   double suml = 0.0;
-  for (int i0 = 0; i0 < cnt; i0 += 64 * kRankPerLane) {
-#pragma unroll
-    for (int u = 0; u < kRankPerLane; ++u) {
-      const int i = i0 + u * 64 + lane;
+  if (ntop >= 0) {
+    // (a) each top document's pairs with every other document: the wave
+    //     spreads the partners over its lanes and reduces (no divergence)
+    for (int r = 0; r < ntop; ++r) {
+      const int i = s_top[r];
+      const double si = sc[i];
+      const int li = kSmall ? s_lab[i] : static_cast<int>(label[b + i]);
       double la = 0.0, he = 0.0;
-      if (i < cnt) {
-        const double si = sc[i];
-        const int li = kSmall ? s_lab[i] : static_cast<int>(label[b + i]);
-        const int ri = rk[i];
-        for (int j = 0; j < cnt; ++j) {
-          const int lj = kSmall ? s_lab[j] : static_cast<int>(label[b + j]);
-          if (lj == li) continue;
-          const int rj = rk[j];
-          if (min(ri, rj) >= t.max_position) continue;
-          PairLambda(t, si, li, ri, sc[j], lj, rj, imd, use_norm, &la, &he, &suml);
+      for (int j = lane; j < cnt; j += 64) {
+        if (j == i) continue;
+        const int lj = kSmall ? s_lab[j] : static_cast<int>(label[b + j]);
+        if (lj == li) continue;
+        PairLambda(t, s_disc, si, li, r, sc[j], lj, rk[j], imd, use_norm, &la, &he, &suml);
+      }
+      la = WaveSumD(la);
+      he = WaveSumD(he);
+      if (lane == 0) { s_tlam[r] = la; s_thes[r] = he; }
+    }
+    // (b) every other document pairs only with the ntop top documents
+    for (int i0 = 0; i0 < cnt; i0 += 64 * kRankPerLane) {
+#pragma unroll
+      for (int u = 0; u < kRankPerLane; ++u) {
+        const int i = i0 + u * 64 + lane;
+        double la = 0.0, he = 0.0;
+        if (i < cnt && rk[i] >= ntop) {
+          const double si = sc[i];
+          const int li = kSmall ? s_lab[i] : static_cast<int>(label[b + i]);
+          const int ri = rk[i];
+          for (int r = 0; r < ntop; ++r) {
+            const int j = s_top[r];
+            const int lj = kSmall ? s_lab[j] : static_cast<int>(label[b + j]);
+            if (lj == li) continue;
+            PairLambda(t, s_disc, si, li, ri, sc[j], lj, r, imd, use_norm, &la, &he, &suml);
+          }
+        }
+        if (kSmall) {
+          lam[u] = la;
+          hes[u] = he;
+        } else if (i < cnt) {
+          t.lam_scratch[b + i] = la;
+          t.hes_scratch[b + i] = he;
         }
       }
-      if (kSmall) {
-        lam[u] = la;
-        hes[u] = he;
-      } else if (i < cnt) {
-        t.lam_scratch[b + i] = la;
-        t.hes_scratch[b + i] = he;
+    }
+    __syncthreads();  // s_tlam / s_thes visible to every lane
+  } else {
+    // max_position beyond the LDS top list: every document scans all partners
+    for (int i0 = 0; i0 < cnt; i0 += 64 * kRankPerLane) {
+#pragma unroll
+      for (int u = 0; u < kRankPerLane; ++u) {
+        const int i = i0 + u * 64 + lane;
+        double la = 0.0, he = 0.0;
+        if (i < cnt)
+          DocLambdas<kSmall>(t, s_disc, s_top, -1, sc, s_lab, label, rk, b, cnt, i, imd, use_norm, &la, &he, &suml);
+        if (kSmall) {
+          lam[u] = la;
+          hes[u] = he;
+        } else if (i < cnt) {
+          t.lam_scratch[b + i] = la;
+          t.hes_scratch[b + i] = he;
+        }
       }
     }
   }
@@ -316,18 +392,142 @@ __device__ void LambdarankQuery(const RankTables& t, int q, const double* __rest
       const int i = u * 64 + lane;
       if (i < cnt) {
         const double w = weight ? weight[b + i] : 1.0;
-        g[b + i] = static_cast<float>(lam[u] * nf * w);
-        h[b + i] = static_cast<float>(hes[u] * nf * w);
+        const int ri = rk[i];
+        const bool top = ri < ntop;
+        g[b + i] = static_cast<float>((top ? s_tlam[ri] : lam[u]) * nf * w);
+        h[b + i] = static_cast<float>((top ? s_thes[ri] : hes[u]) * nf * w);
       }
     }
   } else {
     for (int i = lane; i < cnt; i += 64) {  // the same lane wrote lam/hes of i above
       const double w = weight ? weight[b + i] : 1.0;
-      g[b + i] = static_cast<float>(t.lam_scratch[b + i] * nf * w);
-      h[b + i] = static_cast<float>(t.hes_scratch[b + i] * nf * w);
+      const int ri = rk[i];
+      const bool top = ri < ntop;
+      g[b + i] = static_cast<float>((top ? s_tlam[ri] : t.lam_scratch[b + i]) * nf * w);
+      h[b + i] = static_cast<float>((top ? s_thes[ri] : t.hes_scratch[b + i]) * nf * w);
     }
   }
   __syncthreads();  // LDS reuse by the next query
+}
+
+__device__ __forceinline__ double ReadLaneD(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), l);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+// Register-resident form for the common case (<= kRankLds documents and a
+// top list of <= 64): lane l owns documents l, l+64, ... (score, label, rank
+// in registers); ranks come from comparing against every document broadcast
+// with v_readlane (no memory in the O(cnt^2) loop); the top list lives in the
+// lanes 0..ntop-1 and is broadcast the same way. Pairs: (a) every top
+// document with every document, spread over the lanes and wave-reduced;
+// (b) every other document with the top list, one lane per document.
+template <int NU>  // documents per lane: cnt <= 64 * NU
+__device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __restrict__ score,
+                                    const float* __restrict__ label, const float* __restrict__ weight,
+                                    float* __restrict__ g, float* __restrict__ h, const double* s_disc) {
+  const int lane = threadIdx.x;
+  const int b = t.qb[q], cnt = t.qb[q + 1] - b;
+  const int ntop = min(cnt, t.max_position);
+  double sc[NU];
+  int lab[NU], rk[NU];
+  double mx = -INFINITY, mn = INFINITY;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = u * 64 + lane;
+    sc[u] = i < cnt ? score[b + i] : -INFINITY;
+    lab[u] = i < cnt ? static_cast<int>(label[b + i]) : 0;
+    rk[u] = 0;
+    if (i < cnt) { mx = fmax(mx, sc[u]); mn = fmin(mn, sc[u]); }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mx = fmax(mx, __shfl_xor(mx, off, 64));
+    mn = fmin(mn, __shfl_xor(mn, off, 64));
+  }
+  // ranks: number of documents scoring higher, ties by index (stable sort)
+#pragma unroll
+  for (int v = 0; v < NU; ++v) {
+    if (v * 64 >= cnt) break;
+    const int jn = min(64, cnt - v * 64);
+    for (int jj = 0; jj < jn; ++jj) {
+      const double sj = ReadLaneD(sc[v], jj);
+      const int j = v * 64 + jj;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int i = u * 64 + lane;
+        rk[u] += (sj > sc[u]) || (sj == sc[u] && j < i);
+      }
+    }
+  }
+  // top list: lane r holds the document of rank r (ranks are a permutation)
+  double tsc = 0.0;
+  int tlab = 0, tdoc = 0;
+  {
+    __shared__ int s_doc_of_rank[64];
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      if (u * 64 + lane < cnt && rk[u] < ntop) s_doc_of_rank[rk[u]] = u * 64 + lane;
+    __syncthreads();
+    if (lane < ntop) {
+      tdoc = s_doc_of_rank[lane];
+      tsc = score[b + tdoc];
+      tlab = static_cast<int>(label[b + tdoc]);
+    }
+    __syncthreads();
+  }
+  const double imd = t.inv_max_dcg[q];
+  const bool use_norm = t.norm && mx != mn;
+  double lam[NU], hes[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) { lam[u] = 0.0; hes[u] = 0.0; }
+  double suml = 0.0;
+  // (a) top document r against every document (partners on the lanes)
+  double top_la = 0.0, top_he = 0.0;  // lane r keeps the reduced lambdas of top document r
+  for (int r = 0; r < ntop; ++r) {
+    const double si = ReadLaneD(tsc, r);
+    const int li = __builtin_amdgcn_readlane(tlab, r);
+    const int di = __builtin_amdgcn_readlane(tdoc, r);
+    double la = 0.0, he = 0.0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int j = u * 64 + lane;
+      if (j < cnt && j != di && lab[u] != li)
+        PairLambda(t, s_disc, si, li, r, sc[u], lab[u], rk[u], imd, use_norm, &la, &he, &suml);
+    }
+    la = WaveSumD(la);
+    he = WaveSumD(he);
+    if (lane == r) { top_la = la; top_he = he; }
+  }
+  // (b) every non-top document against the top list
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = u * 64 + lane;
+    if (i >= cnt || rk[u] < ntop) continue;
+    for (int r = 0; r < ntop; ++r) {
+      const int lj = __builtin_amdgcn_readlane(tlab, r);
+      if (lj == lab[u]) continue;
+      PairLambda(t, s_disc, sc[u], lab[u], rk[u], ReadLaneD(tsc, r), lj, r, imd, use_norm, &lam[u], &hes[u], &suml);
+    }
+  }
+  suml = WaveSumD(suml);
+  const double nf = (t.norm && suml > 0) ? log2(1.0 + suml) / suml : 1.0;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = u * 64 + lane;
+    if (i < cnt && rk[u] >= ntop) {
+      const double w = weight ? weight[b + i] : 1.0;
+      g[b + i] = static_cast<float>(lam[u] * nf * w);
+      h[b + i] = static_cast<float>(hes[u] * nf * w);
+    }
+  }
+  if (lane < ntop) {
+    const double w = weight ? weight[b + tdoc] : 1.0;
+    g[b + tdoc] = static_cast<float>(top_la * nf * w);
+    h[b + tdoc] = static_cast<float>(top_he * nf * w);
+  }
 }
 
 __global__ __launch_bounds__(64) void lambdarank_kernel(RankTables t, const double* __restrict__ score,
@@ -335,13 +535,19 @@ __global__ __launch_bounds__(64) void lambdarank_kernel(RankTables t, const doub
                                                         const float* __restrict__ weight, float* __restrict__ g,
                                                         float* __restrict__ h) {
   __shared__ double s_sc[kRankLds];
+  __shared__ double s_disc[kRankLds];
   __shared__ int s_lab[kRankLds];
   __shared__ int s_rk[kRankLds];
+  __shared__ int s_top[kRankLds];
+  __shared__ double s_tlam[kRankLds], s_thes[kRankLds];
+  for (int r = threadIdx.x; r < kRankLds; r += 64) s_disc[r] = 1.0 / log2(2.0 + r);
+  __syncthreads();
   for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
     const int cnt = t.qb[q + 1] - t.qb[q];
     if (cnt <= 0) continue;
-    if (cnt <= kRankLds) LambdarankQuery<true>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk);
-    else LambdarankQuery<false>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk);
+    if (cnt <= kRankLds && t.max_position <= 64) LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc);
+    else if (cnt <= kRankLds) LambdarankQuery<true>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk, s_disc, s_top, s_tlam, s_thes);
+    else LambdarankQuery<false>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk, s_disc, s_top, s_tlam, s_thes);
   }
 }
 

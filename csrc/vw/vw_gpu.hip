@@ -24,15 +24,11 @@ namespace {
 
 constexpr int kWavesPerBlock = 4;
 
-__global__ __launch_bounds__(256) void sgd_kernel(const int64_t* __restrict__ indptr, const uint32_t* __restrict__ idx,
-                                                  const float* __restrict__ val, const float* __restrict__ labels,
-                                                  const float* __restrict__ weights, int64_t n0, int64_t n1,
-                                                  float2* __restrict__ W, uint64_t mask, float lr, float l2, int loss,
-                                                  int adaptive, float eta_scale, float* __restrict__ preds,
-                                                  float* __restrict__ loss_acc, int learn) {
-  const int lane = threadIdx.x & 63;
-  const int64_t e = n0 + static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
-  if (e >= n1) return;
+__device__ __forceinline__ void ExampleStep(const int64_t* __restrict__ indptr, const uint32_t* __restrict__ idx,
+                                            const float* __restrict__ val, const float* __restrict__ labels,
+                                            const float* __restrict__ weights, int64_t e, float2* __restrict__ W,
+                                            uint64_t mask, float lr, float l2, int loss, int adaptive, float eta_scale,
+                                            float* __restrict__ preds, int learn, int lane, float* wloss) {
   const int64_t b = indptr[e], en = indptr[e + 1];
   float s = 0.f;
   for (int64_t p = b + lane; p < en; p += 64) s += W[idx[p] & mask].x * val[p];
@@ -51,7 +47,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(const int64_t* __restrict__ in
     g = 2.f * (s - y);
     l = (s - y) * (s - y);
   }
-  if (lane == 0) atomicAdd(loss_acc, l * imp);
+  if (lane == 0) *wloss = l * imp;
   g *= imp;
   for (int64_t p = b + lane; p < en; p += 64) {
     const uint64_t h = idx[p] & mask;
@@ -66,6 +62,25 @@ __global__ __launch_bounds__(256) void sgd_kernel(const int64_t* __restrict__ in
     }
     if (l2 > 0.f) step += lr * l2 * W[h].x;
     atomicAdd(&W[h].x, -step);
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(const int64_t* __restrict__ indptr, const uint32_t* __restrict__ idx,
+                                                  const float* __restrict__ val, const float* __restrict__ labels,
+                                                  const float* __restrict__ weights, int64_t n0, int64_t n1,
+                                                  float2* __restrict__ W, uint64_t mask, float lr, float l2, int loss,
+                                                  int adaptive, float eta_scale, float* __restrict__ preds,
+                                                  float* __restrict__ loss_acc, int learn) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t e = n0 + static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wid;
+  __shared__ float wloss[kWavesPerBlock];
+  if (lane == 0) wloss[wid] = 0.f;
+  if (e < n1) ExampleStep(indptr, idx, val, labels, weights, e, W, mask, lr, l2, loss, adaptive, eta_scale, preds,
+                          learn, lane, &wloss[wid]);
+  // one loss atomic per block (a same-address atomic per example serialises the launch)
+  if (learn) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss_acc, wloss[0] + wloss[1] + wloss[2] + wloss[3]);
   }
 }
 

@@ -221,10 +221,11 @@ def _train_rank(X, y, sizes, params, iters):
     return b
 
 
-def test_gpu_lambdarank_gradients_match_host():
-    """K2 ranking: the wave-per-query lambdarank kernel vs the host pairwise loop (LDS and global paths)."""
+@pytest.mark.parametrize("maxpos", [20, 80])
+def test_gpu_lambdarank_gradients_match_host(maxpos):
+    """K2 ranking: the wave-per-query lambdarank kernel vs the host pairwise loop (register, LDS and global paths)."""
     X, y, sizes = _rank_data()
-    p = "objective=lambdarank num_leaves=15 min_data_in_leaf=5 eval_at=5"
+    p = f"objective=lambdarank num_leaves=15 min_data_in_leaf=5 eval_at=5 max_position={maxpos}"
     bc = _train_rank(X, y, sizes, p + " device_type=cpu", 1)
     bg = _train_rank(X, y, sizes, p + " device_type=gpu", 1)
     assert bg.backend == "hip"

@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""VowpalWabbitClassifier hashed-sparse training throughput on the MI355X —
+BASELINE.json config "VowpalWabbitClassifier 1B-feature hashed sparse
+synthetic, 8xMI355X model allreduce".
+
+Per GPU: a 2^bits weight table (default 2^30 = 1B features, weight + AdaGrad
+state = 8 GiB resident in HBM), --rows examples per pass with ~--nnz hashed
+features each (32-bit hashed ids from a 2^24 vocabulary, Zipf-like). One step = one pass:
+host -> device transfer of the pass's CSR, hogwild AdaGrad SGD on the device
+(K12, logistic loss), then (N > 1) the endPass weight average over RCCL
+(the whole 2^bits table, bandwidth-bound over xGMI). Prints one
+JSON line with examples/s over all GPUs, the per-pass allreduce time and the
+held-out logistic loss. Synthetic data; labels from a planted sparse model."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+_VOCAB = {}
+
+
+def vocabulary(size_log2=24):
+    """Hashed feature ids: 2^24 distinct 32-bit murmur-like hashes and a planted weight per id."""
+    if size_log2 not in _VOCAB:
+        r = np.random.default_rng(12345)
+        ids = r.integers(0, 2 ** 32, size=2 ** size_log2, dtype=np.uint64).astype(np.uint32)
+        wt = (r.standard_normal(2 ** size_log2) * 0.4).astype(np.float32)
+        _VOCAB[size_log2] = (ids, wt)
+    return _VOCAB[size_log2]
+
+
+def make_pass(n, nnz, seed):
+    rng = np.random.default_rng(seed)
+    ids, wt = vocabulary()
+    counts = rng.integers(max(1, nnz // 2), nnz * 3 // 2 + 1, size=n)
+    indptr = np.zeros(n + 1, np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    tot = int(indptr[-1])
+    # Zipf-like popularity: frequent ids repeat across examples, the tail is rare
+    v = np.minimum((rng.pareto(1.1, size=tot) * 2000).astype(np.int64), len(ids) - 1)
+    idx = ids[v]
+    val = np.ones(tot, np.float32)
+    margin = np.add.reduceat(wt[v], indptr[:-1])
+    y = np.where(margin + 0.3 * rng.standard_normal(n) > 0, 1.0, -1.0).astype(np.float32)
+    return indptr, idx, val, y
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bits", type=int, default=30)
+    ap.add_argument("--rows", type=int, default=2_000_000, help="examples per pass per GPU")
+    ap.add_argument("--nnz", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=16384, help="hogwild mini-batch (examples in flight)")
+    args = ap.parse_args()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench_vw needs an MI355X")
+    torch.cuda.set_device(local_rank)
+    from synapseml_amd.ops import native
+    from synapseml_amd.parallel import distributed as D
+
+    if world > 1:
+        D.init_from_env("nccl")
+    vw = native.load("_vw")
+    cfg = vw.GpuSgdConfig()
+    cfg.bits = args.bits
+    cfg.lr = 0.5
+    cfg.power_t = 0.5
+    cfg.loss = 1
+    cfg.adaptive = True
+    g = vw.GpuSgd(cfg, local_rank)
+    comm = None
+    if world > 1:
+        uid = vw.nccl_unique_id() if rank == 0 else None
+        comm = vw.nccl_comm(D.broadcast_object(uid, 0), rank, world)
+    passes = [make_pass(args.rows, args.nnz, seed=1000 * rank + s) for s in range(2)]
+    hold = make_pass(100_000, args.nnz, seed=999_999)
+    ar_ms = []
+
+    def one_pass(i):
+        ip, ix, vl, y = passes[i % 2]
+        g.learn(ip, ix, vl, y, None, args.batch)
+        if comm is not None:
+            t = time.perf_counter()
+            g.allreduce_average(comm)
+            ar_ms.append((time.perf_counter() - t) * 1e3)
+
+    for i in range(args.warmup):
+        one_pass(i)
+    torch.cuda.synchronize()
+    D.barrier()
+    ar_ms.clear()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_pass(i)
+    torch.cuda.synchronize()
+    D.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        p = g.predict(hold[0], hold[1], hold[2])
+        m = hold[3] * p
+        logloss = float(np.mean(np.log1p(np.exp(-np.clip(m, -50, 50)))))
+        print(json.dumps({
+            "bench": "vw_hashed_sgd", "metric": "examples/sec VowpalWabbitClassifier (whole job)",
+            "value": round(args.rows * world * args.steps / elapsed, 1), "n_gpus": world, "bits": args.bits,
+            "table_gib": round((2 ** args.bits) * 8 / 2 ** 30, 2), "rows_per_gpu_per_pass": args.rows,
+            "nnz_per_row": args.nnz, "batch": args.batch, "ms_per_pass": round(elapsed / args.steps * 1e3, 2),
+            "allreduce_ms_per_pass": round(float(np.mean(ar_ms)), 2) if ar_ms else None,
+            "holdout_logloss": round(logloss, 4),
+            "data": "synthetic hashed sparse (2^24-id vocabulary of 32-bit hashes, Zipf-like popularity, planted model)"}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
