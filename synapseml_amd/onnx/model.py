@@ -224,14 +224,26 @@ class ONNXModel(Transformer):
         n = df.count()
         cols_out = {c: np.empty(n, dtype=object) for c in fetch}
         names = list(fetch.values())
+        # tensor columns (one numeric ndarray per column) stream to the GPU in
+        # large chunks on a side stream, overlapped with the graph replays
+        dense = {inp: col for inp, col in feeds.items() if _dense_tensor_column(df[col], in_info[inp])}
+        prefetch = _DevicePrefetcher(df, dense, in_info, bs, n, sess) if dense and sess.gpu else None
         for start in range(0, n, bs):
             end = min(n, start + bs)
-            batch_feeds = {}
+            batch_feeds = prefetch.batch(start, end) if prefetch is not None else {}
             for inp, col in feeds.items():
+                if inp in batch_feeds:
+                    continue
+                if inp in dense:
+                    batch_feeds[inp] = np.asarray(df[col][start:end]).astype(in_info[inp].np_dtype, copy=False)
+                    continue
                 vals = df[col][start:end]
                 batch_feeds[inp] = _coerce_batch(list(vals), in_info[inp])
             outs = sess.run(names, batch_feeds)
             for (col, _), o in zip(fetch.items(), outs):
+                if isinstance(o, np.ndarray) and o.ndim >= 2 and o.shape[0] == end - start and o.dtype != object:
+                    cols_out[col][start:end] = list(o)  # row views, no per-row conversion
+                    continue
                 parts = _split_output(o, end - start)
                 for j, v in enumerate(parts):
                     cols_out[col][start + j] = _to_py(v)
@@ -244,8 +256,83 @@ class ONNXModel(Transformer):
                 col[i] = _softmax_vec(v)
             out = out.withColumn(dst, col)
         for src, dst in (self.getArgMaxDict() or {}).items():
-            out = out.withColumn(dst, np.asarray([_argmax(v) for v in out[src].tolist()], dtype=np.float64))
+            vals = out[src]
+            stacked = _stack_rows(vals)
+            if stacked is not None:  # equal-shape numeric rows: one vectorised argmax
+                out = out.withColumn(dst, np.argmax(stacked.reshape(len(stacked), -1), axis=1).astype(np.float64))
+            else:
+                out = out.withColumn(dst, np.asarray([_argmax(v) for v in vals.tolist()], dtype=np.float64))
         return out
+
+
+def _stack_rows(col) -> Optional[np.ndarray]:
+    """Rows of an object column as one array when they are equal-shape numeric ndarrays."""
+    if isinstance(col, np.ndarray) and col.dtype != object:
+        return col if col.ndim >= 2 else None
+    if len(col) == 0 or not all(isinstance(v, np.ndarray) and v.dtype != object for v in col):
+        return None
+    if len({v.shape for v in col}) != 1 or col[0].size == 0:
+        return None
+    return np.stack(list(col))
+
+
+def _dense_tensor_column(col, vi: ValueInfo) -> bool:
+    """A numeric ndarray column whose rows already have the model input's shape (no per-row coercion)."""
+    if not isinstance(col, np.ndarray) or col.dtype == object or col.dtype.kind not in "fiub":
+        return False
+    exp = vi.shape
+    if vi.np_dtype is object or exp is None or len(exp) != col.ndim:
+        return False
+    return all(not isinstance(e, int) or e == s for e, s in zip(exp[1:], col.shape[1:]))
+
+
+class _DevicePrefetcher:
+    """Uploads tensor columns to the session's GPU in chunks of several mini-batches from a
+    background thread on its own HIP stream (the pageable copy releases the GIL), so the
+    host->device traffic of chunk k+1 overlaps the graph replays of chunk k."""
+
+    def __init__(self, df, dense, in_info, bs, n, sess, batches_per_chunk: int = 2):
+        import queue
+        import threading
+
+        import torch
+
+        self._torch = torch
+        self.device = sess.device
+        self.chunk = bs * batches_per_chunk
+        self.cur = None  # (lo, hi, {inp: tensor}, event)
+        self.q = queue.Queue(maxsize=2)
+        stream = torch.cuda.Stream(self.device)
+
+        def work():
+            try:
+                for lo in range(0, n, self.chunk):
+                    hi = min(n, lo + self.chunk)
+                    with torch.cuda.stream(stream):
+                        ts = {inp: torch.from_numpy(np.ascontiguousarray(
+                            np.asarray(df[col][lo:hi]).astype(in_info[inp].np_dtype, copy=False)))
+                            .to(self.device, non_blocking=True) for inp, col in dense.items()}
+                        ev = torch.cuda.Event()
+                        ev.record(stream)
+                    self.q.put((lo, hi, ts, ev))
+            except BaseException as e:  # noqa: BLE001 - surfaced in batch()
+                self.q.put(e)
+
+        self.thread = threading.Thread(target=work, daemon=True)
+        self.thread.start()
+
+    def batch(self, start, end):
+        while self.cur is None or start >= self.cur[1]:
+            item = self.q.get()
+            if isinstance(item, BaseException):
+                raise item
+            cs = self._torch.cuda.current_stream(self.device)
+            item[3].wait(cs)
+            for t in item[2].values():
+                t.record_stream(cs)  # freed only after the compute stream is done with it
+            self.cur = item
+        lo, _, ts, _ = self.cur
+        return {inp: t[start - lo:end - lo] for inp, t in ts.items()}
 
 
 def _to_py(v):
