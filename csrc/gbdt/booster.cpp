@@ -495,7 +495,9 @@ void Booster::Predict(const double* X, int64_t nrows, int ncols, int type, int s
   const int osz = PredictOutputSize(type, start_iteration, num_iteration);
   std::unique_ptr<Objective> conv;
   if (type == kPredictNormal) conv = MakeConverter(objective_str_);
-#pragma omp parallel
+  // small batches (serving) stay on the calling thread: waking an OpenMP team
+  // costs more than scoring a handful of rows
+#pragma omp parallel if (nrows * (r.second - r.first) >= 4096)
   {
     std::vector<double> row(std::max(nf, ncols) + 1, 0.0), raw(K);
 #pragma omp for schedule(static)
@@ -524,7 +526,7 @@ void Booster::Predict(const double* X, int64_t nrows, int ncols, int type, int s
 void Booster::ConvertOutputs(const double* raw, int64_t n, double* out) const {
   auto conv = MakeConverter(objective_str_);
   const int K = num_tree_per_iter_;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (n >= 16384)
   for (int64_t i = 0; i < n; ++i) conv->ConvertOutput(raw + i * K, out + i * K);
 }
 

@@ -4,7 +4,9 @@ ServingUDFs}.scala and CORE/io/IOImplicits.scala:100-187).
 
 MI355X-first shape: one server per GPU process. HTTP handler threads enqueue
 requests; a single batching loop drains up to ``max_batch_size`` requests (or
-waits at most ``max_wait_ms`` for the first one to have company), turns them
+waits at most ``max_wait_ms`` for the first one to have company; 0 = take what
+is queued and go, so an idle server answers at once and batches form under
+load while the previous batch runs), turns them
 into one DataFrame(id, request) micro-batch, runs the user's transform —
 typically a pipeline whose heavy stage is a device model, so a whole batch is
 one device launch sequence — and routes the reply column back by id.
@@ -13,12 +15,12 @@ one device launch sequence — and routes the reply column back by id.
 extensions (parsingCheck none/partial/full; 400 "JSON Parsing Failure")."""
 from __future__ import annotations
 
+import asyncio
 import itertools
 import json
-import queue
+import socket
 import threading
 import time
-from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Callable, Dict, List, Optional, Union
 
 import numpy as np
@@ -122,24 +124,23 @@ def make_reply(df: DataFrame, reply_col: str, name: str = "reply") -> DataFrame:
                                      for v in df[reply_col].tolist()]))
 
 
-class _Pending:
-    __slots__ = ("event", "response", "t0")
-
-    def __init__(self):
-        self.event = threading.Event()
-        self.response: Optional[dict] = None
-        self.t0 = time.perf_counter()
-
-
 class ServingServer:
     """Batched HTTP serving of a DataFrame transform.
 
     ``transform(df)`` receives DataFrame(id, request) and must return a
     DataFrame with ``id`` and a ``reply`` column (see ``make_reply``); rows it
-    drops are answered by ``parse_request`` or get a 500."""
+    drops are answered by ``parse_request`` or get a 500.
+
+    One asyncio event loop (its own thread) owns every connection: it parses
+    HTTP/1.1 requests itself (persistent connections, TCP_NODELAY, one write
+    per reply) and scores in the loop thread, so an idle server answers a
+    request with no thread hand-off at all. Requests that arrive while a batch
+    is scoring queue up and form the next micro-batch (``max_batch_size``);
+    ``max_wait_ms`` > 0 additionally holds the first request of a batch that
+    long for company."""
 
     def __init__(self, transform: Callable[[DataFrame], DataFrame], host: str = "127.0.0.1", port: int = 0,
-                 api: str = "", max_batch_size: int = 64, max_wait_ms: float = 1.0, reply_col: str = "reply",
+                 api: str = "", max_batch_size: int = 64, max_wait_ms: float = 0.0, reply_col: str = "reply",
                  request_timeout: float = 60.0):
         self.transform_fn = transform
         self.api = api.strip("/")
@@ -147,63 +148,50 @@ class ServingServer:
         self.max_wait_ms = max_wait_ms
         self.reply_col = reply_col
         self.request_timeout = request_timeout
-        self._q: "queue.Queue" = queue.Queue()
-        self._pending: Dict[int, _Pending] = {}
-        self._lock = threading.Lock()
         self._ids = itertools.count()
-        self._stop = threading.Event()
+        self._queue: list = []
+        self._pending: Dict[int, tuple] = {}
+        self._scheduled = False
+        self._conns: set = set()
         self.batch_sizes: List[int] = []
         self.latencies_ms: List[float] = []
-        outer = self
-
-        class Handler(BaseHTTPRequestHandler):
-            protocol_version = "HTTP/1.1"
-
-            def log_message(self, *a):  # silence default stderr logging
-                pass
-
-            def _handle(self):
-                path = self.path.split("?")[0].strip("/")
-                if outer.api and path != outer.api:
-                    self.send_response(404)
-                    self.send_header("Content-Length", "0")
-                    self.end_headers()
-                    return
-                n = int(self.headers.get("Content-Length") or 0)
-                body = self.rfile.read(n) if n else None
-                req = make_request(self.path, self.command, dict(self.headers.items()), body,
-                                   self.headers.get("Content-Type"))
-                resp = outer._submit(req)
-                ent = resp.get("entity") or {}
-                content = ent.get("content") or b""
-                self.send_response(resp["statusLine"]["statusCode"], resp["statusLine"].get("reasonPhrase"))
-                for h in resp.get("headers") or []:
-                    self.send_header(h["name"], h["value"])
-                self.send_header("Content-Length", str(len(content)))
-                self.end_headers()
-                self.wfile.write(content)
-
-            do_GET = do_POST = do_PUT = _handle
-
-        self._httpd = ThreadingHTTPServer((host, port), Handler)
-        self._httpd.daemon_threads = True
-        self.host, self.port = self._httpd.server_address[:2]
-        self._threads = [threading.Thread(target=self._httpd.serve_forever, daemon=True),
-                         threading.Thread(target=self._batch_loop, daemon=True)]
+        self._loop = asyncio.new_event_loop()
+        self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self._sock.bind((host, port))
+        self._sock.listen(1024)
+        self._sock.setblocking(False)
+        self.host, self.port = self._sock.getsockname()[:2]
+        self._server = None
+        self._thread = threading.Thread(target=self._run_loop, daemon=True)
+        self._ready = threading.Event()
 
     @property
     def address(self) -> str:
         return f"http://{self.host}:{self.port}/{self.api}"
 
     def start(self) -> "ServingServer":
-        for t in self._threads:
-            t.start()
+        self._thread.start()
+        self._ready.wait(30)
         return self
 
     def stop(self) -> None:
-        self._stop.set()
-        self._httpd.shutdown()
-        self._httpd.server_close()
+        if self._loop.is_running():
+            try:
+                asyncio.run_coroutine_threadsafe(self._shutdown(), self._loop).result(10)
+            except Exception:  # noqa: BLE001 - best effort
+                pass
+            self._loop.call_soon_threadsafe(self._loop.stop)
+            self._thread.join(10)
+        self._sock.close()
+
+    async def _shutdown(self) -> None:
+        if self._server is not None:
+            self._server.close()
+        tasks = [t for t in self._conns if not t.done()]
+        for t in tasks:
+            t.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
 
     def __enter__(self):
         return self.start()
@@ -211,59 +199,128 @@ class ServingServer:
     def __exit__(self, *exc):
         self.stop()
 
-    def _submit(self, req: dict) -> dict:
+    # ------------------------------------------------------------------ event loop
+    def _run_loop(self) -> None:
+        asyncio.set_event_loop(self._loop)
+
+        async def boot():
+            self._server = await asyncio.start_server(self._conn, sock=self._sock)
+
+        self._loop.run_until_complete(boot())
+        self._ready.set()
+        try:
+            self._loop.run_forever()
+        finally:
+            if self._server is not None:
+                self._server.close()
+
+    async def _conn(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        task = asyncio.current_task()
+        self._conns.add(task)
+        sock = writer.get_extra_info("socket")
+        if sock is not None:
+            # replies are small: without TCP_NODELAY, Nagle + the client's delayed ACK add ~40 ms
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        try:
+            while True:
+                line = await reader.readline()
+                if not line or not line.strip():
+                    break
+                parts = line.decode("latin-1").split()
+                if len(parts) < 2:
+                    break
+                method, target = parts[0], parts[1]
+                headers: Dict[str, str] = {}
+                while True:
+                    h = await reader.readline()
+                    if not h or h in (b"\r\n", b"\n"):
+                        break
+                    k, _, v = h.decode("latin-1").partition(":")
+                    headers[k.strip()] = v.strip()
+                low = {k.lower(): v for k, v in headers.items()}
+                n = int(low.get("content-length") or 0)
+                body = await reader.readexactly(n) if n else None
+                close = low.get("connection", "").lower() == "close"
+                path = target.split("?")[0].strip("/")
+                if self.api and path != self.api:
+                    writer.write(b"HTTP/1.1 404 Not Found\r\nContent-Length: 0\r\n\r\n")
+                else:
+                    resp = await self._submit(make_request(target, method, headers, body, low.get("content-type")))
+                    writer.write(_serialize(resp))
+                await writer.drain()
+                if close:
+                    break
+        except (asyncio.IncompleteReadError, ConnectionError, asyncio.CancelledError):
+            pass
+        finally:
+            self._conns.discard(task)
+            try:
+                writer.close()
+            except RuntimeError:  # loop shutting down
+                pass
+
+    async def _submit(self, req: dict) -> dict:
         rid = next(self._ids)
-        p = _Pending()
-        with self._lock:
-            self._pending[rid] = p
-        self._q.put((rid, req))
-        if not p.event.wait(self.request_timeout):
-            with self._lock:
-                self._pending.pop(rid, None)
+        fut = self._loop.create_future()
+        self._pending[rid] = (fut, time.perf_counter())
+        self._queue.append((rid, req))
+        if not self._scheduled:
+            self._scheduled = True
+            if self.max_wait_ms > 0:
+                self._loop.call_later(self.max_wait_ms / 1e3, self._drain)
+            else:
+                self._loop.call_soon(self._drain)
+        try:
+            return await asyncio.wait_for(fut, self.request_timeout)
+        except asyncio.TimeoutError:
+            self._pending.pop(rid, None)
             return make_response("request timed out", 504, "Gateway Timeout")
-        return p.response
+
+    def _drain(self) -> None:
+        self._scheduled = False
+        while self._queue:
+            batch = self._queue[: self.max_batch_size]
+            del self._queue[: self.max_batch_size]
+            self._run_batch(batch)
 
     def reply(self, rid: int, response: dict) -> None:
-        with self._lock:
-            p = self._pending.pop(rid, None)
-        if p is not None:
-            p.response = response
-            self.latencies_ms.append((time.perf_counter() - p.t0) * 1e3)
-            p.event.set()
+        """Answer request ``rid`` (callable from the transform or from another thread)."""
+        if threading.current_thread() is not self._thread:
+            self._loop.call_soon_threadsafe(self.reply, rid, response)
+            return
+        entry = self._pending.pop(rid, None)
+        if entry is not None and not entry[0].done():
+            self.latencies_ms.append((time.perf_counter() - entry[1]) * 1e3)
+            entry[0].set_result(response)
 
-    def _batch_loop(self) -> None:
-        while not self._stop.is_set():
-            try:
-                first = self._q.get(timeout=0.05)
-            except queue.Empty:
-                continue
-            batch = [first]
-            deadline = time.perf_counter() + self.max_wait_ms / 1e3
-            while len(batch) < self.max_batch_size:
-                try:
-                    batch.append(self._q.get_nowait())
-                    continue
-                except queue.Empty:
-                    pass
-                left = deadline - time.perf_counter()
-                if left <= 0:
-                    break
-                try:
-                    batch.append(self._q.get(timeout=left))
-                except queue.Empty:
-                    break
-            self.batch_sizes.append(len(batch))
-            ids = [b[0] for b in batch]
-            df = DataFrame({"id": _obj(ids), "request": _obj([b[1] for b in batch])})
-            try:
-                out = self.transform_fn(df)
-                for rid, rep in zip(out["id"].tolist(), out[self.reply_col].tolist()):
-                    self.reply(rid, rep if isinstance(rep, dict) and "statusLine" in rep else make_response(rep))
-            except Exception as e:  # noqa: BLE001 - reported to the client
-                for rid in ids:
-                    self.reply(rid, make_response(f"{type(e).__name__}: {e}", 500, "Internal Server Error"))
-            for rid in ids:  # rows the transform dropped without replying
-                self.reply(rid, make_response("no reply produced", 500, "Internal Server Error"))
+    def _run_batch(self, batch: list) -> None:
+        self.batch_sizes.append(len(batch))
+        ids = [b[0] for b in batch]
+        df = DataFrame({"id": _obj(ids), "request": _obj([b[1] for b in batch])})
+        try:
+            out = self.transform_fn(df)
+            for rid, rep in zip(out["id"].tolist(), out[self.reply_col].tolist()):
+                self.reply(rid, rep if isinstance(rep, dict) and "statusLine" in rep else make_response(rep))
+        except Exception as e:  # noqa: BLE001 - reported to the client
+            for rid in ids:
+                self.reply(rid, make_response(f"{type(e).__name__}: {e}", 500, "Internal Server Error"))
+        for rid in ids:  # rows the transform dropped without replying
+            self.reply(rid, make_response("no reply produced", 500, "Internal Server Error"))
+
+
+def _serialize(resp: dict) -> bytes:
+    st = resp.get("statusLine") or {}
+    code = int(st.get("statusCode", 200))
+    reason = st.get("reasonPhrase") or ""
+    content = (resp.get("entity") or {}).get("content") or b""
+    if isinstance(content, str):
+        content = content.encode("utf-8")
+    head = [f"HTTP/1.1 {code} {reason}"]
+    for h in resp.get("headers") or []:
+        if h["name"].lower() != "content-length":
+            head.append(f"{h['name']}: {h['value']}")
+    head.append(f"Content-Length: {len(content)}")
+    return ("\r\n".join(head) + "\r\n\r\n").encode("latin-1") + content
 
 
 def serve(transform: Callable[[DataFrame], DataFrame], host: str = "127.0.0.1", port: int = 0, api: str = "",
