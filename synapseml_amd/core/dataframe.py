@@ -419,6 +419,46 @@ class DataFrame:
             cols[str(k)] = _as_column(s.tolist()) if s.dtype == object else s.to_numpy()
         return DataFrame(cols, num_partitions=num_partitions)
 
+    def toArrow(self):  # noqa: N802
+        """Arrow table (the columnar interchange Spark's ``mapInArrow`` / ``toArrow`` speak).
+        2-D numeric columns (vectors, tensors) become fixed-size-list columns without a copy
+        of the row data into Python objects."""
+        import pyarrow as pa
+
+        arrays, names = [], []
+        for k, v in self._cols.items():
+            if v.ndim == 2 and v.dtype != object:
+                flat = pa.array(np.ascontiguousarray(v).reshape(-1))
+                arrays.append(pa.FixedSizeListArray.from_arrays(flat, v.shape[1]))
+            elif v.dtype == object:
+                arrays.append(pa.array([_arrow_value(x) for x in v]))
+            else:
+                arrays.append(pa.array(v))
+            names.append(k)
+        return pa.Table.from_arrays(arrays, names=names)
+
+    @staticmethod
+    def fromArrow(table, num_partitions: int = 1) -> "DataFrame":  # noqa: N802
+        """DataFrame from an Arrow table or record batches; fixed-size-list numeric columns
+        become 2-D arrays (the layout the native engines ingest directly)."""
+        import pyarrow as pa
+
+        if isinstance(table, pa.RecordBatch):
+            table = pa.Table.from_batches([table])
+        elif isinstance(table, (list, tuple)):
+            table = pa.Table.from_batches(list(table))
+        cols = {}
+        for name, col in zip(table.column_names, table.columns):
+            t = col.type
+            if pa.types.is_fixed_size_list(t) and (pa.types.is_floating(t.value_type) or pa.types.is_integer(t.value_type)):
+                flat = col.combine_chunks().flatten().to_numpy(zero_copy_only=False)
+                cols[name] = flat.reshape(len(col), t.list_size)
+            elif pa.types.is_floating(t) or pa.types.is_integer(t) or pa.types.is_boolean(t):
+                cols[name] = col.to_numpy()
+            else:
+                cols[name] = _as_column(col.to_pylist())
+        return DataFrame(cols, num_partitions=num_partitions)
+
     @staticmethod
     def fromRows(rows: Iterable[dict], num_partitions: int = 1) -> "DataFrame":  # noqa: N802
         rows = list(rows)
@@ -429,6 +469,16 @@ class DataFrame:
 
     def __repr__(self) -> str:
         return f"DataFrame[{', '.join(f'{k}: {t}' for k, t in self.dtypes)}] ({self._n} rows, {self.getNumPartitions()} partitions)"
+
+
+def _arrow_value(x):
+    if isinstance(x, DenseVector):
+        return x.toArray().tolist()
+    if isinstance(x, np.ndarray):
+        return x.tolist()
+    if isinstance(x, np.generic):
+        return x.item()
+    return x
 
 
 class GroupedData:

@@ -124,3 +124,22 @@ def test_misc_utils():
         return 7
 
     assert retry_with_timeout(flaky, backoffs_ms=(0, 1, 1, 1)) == 7
+
+
+def test_dataframe_arrow_roundtrip():
+    import pyarrow as pa
+
+    from synapseml_amd.core import DataFrame
+
+    X = np.arange(12, dtype=np.float64).reshape(4, 3)
+    df = DataFrame({"features": X, "label": np.array([0.0, 1.0, 1.0, 0.0]), "name": np.array(["a", "b", "c", "d"],
+                                                                                              dtype=object)})
+    t = df.toArrow()
+    assert isinstance(t, pa.Table) and pa.types.is_fixed_size_list(t.schema.field("features").type)
+    back = DataFrame.fromArrow(t, num_partitions=2)
+    np.testing.assert_array_equal(back["features"], X)
+    assert back["name"].tolist() == ["a", "b", "c", "d"]
+    assert back.getNumPartitions() == 2
+    # record batches (Spark mapInArrow delivers an iterator of them)
+    b2 = DataFrame.fromArrow(t.to_batches(max_chunksize=2))
+    np.testing.assert_array_equal(b2["label"], df["label"])
