@@ -143,7 +143,7 @@ def _host_allreduce_f32(arr: np.ndarray) -> None:
         D._dist().all_reduce(t)
 
 
-_GPU_UNSUPPORTED = re.compile(r"(^|\s)(-q|--quadratic|--cubic|--interactions|--oaa|--csoaa|--cb\w*|--ngram|--l1|"
+_GPU_UNSUPPORTED = re.compile(r"(^|\s)(--cubic|--oaa|--csoaa|--cb\w*|--ngram|--l1|"
                               r"--ignore|--passes\s+0)(\s|$)")
 _nccl_cache: dict = {}
 
@@ -173,6 +173,52 @@ def _merged_csr(blocks, n: int, constant: bool):
     return indptr, idx, val
 
 
+_FNV_PRIME = np.uint32(16777619)
+
+
+def _quadratic_pairs(args: str) -> List[str]:
+    """Two-namespace interactions from -q / --quadratic / --interactions (VW command line)."""
+    out = []
+    for m in re.finditer(r"(?:^|\s)(?:-q|--quadratic|--interactions)(?:\s+|=)(\S+)", args):
+        v = m.group(1)
+        if len(v) != 2 or ":" in v:
+            raise ValueError(f"deviceType='gpu' supports two-namespace interactions only; got {v!r}")
+        out.append(v)
+    return out
+
+
+def _interaction_block(blocks, pair: str, n: int):
+    """Host expansion of one quadratic interaction into a CSR block, with the
+    native learner's hashing (vw_core.cpp ForEachFeature: (a * FNV) ^ b, value
+    a.x * b.x; a namespace crossed with itself keeps pairs j >= i). The GPU
+    kernel masks indices to num_bits <= 32, so 32-bit products are exact."""
+    def last(g):
+        found = [b for b in blocks if b[0] == g]
+        return found[-1] if found else None
+
+    A, B = last(pair[0]), last(pair[1])
+    if A is None or B is None:
+        return (pair, np.zeros(n + 1, np.int64), np.zeros(0, np.uint32), np.zeros(0, np.float32))
+    same = A is B
+    ia, a_idx, a_val = A[1], A[2], A[3]
+    ib, b_idx, b_val = B[1], B[2], B[3]
+    la, lb = np.diff(ia), np.diff(ib)
+    npair = la * lb
+    rows = np.repeat(np.arange(n), npair)
+    k = np.arange(int(npair.sum())) - np.repeat(np.concatenate([[0], np.cumsum(npair)[:-1]]), npair)
+    lbr = lb[rows]
+    i = k // np.maximum(lbr, 1)
+    j = k - i * lbr
+    if same:
+        keep = j >= i
+        rows, i, j = rows[keep], i[keep], j[keep]
+    ga, gb = ia[rows] + i, ib[rows] + j
+    idx = (a_idx[ga].astype(np.uint32) * _FNV_PRIME) ^ b_idx[gb].astype(np.uint32)
+    val = (a_val[ga] * b_val[gb]).astype(np.float32)
+    indptr = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=n))]).astype(np.int64)
+    return (pair, indptr, idx.astype(np.uint32), val)
+
+
 def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     """Device-resident hogwild mini-batch SGD (csrc/vw/vw_gpu.hip, K12).
 
@@ -188,8 +234,6 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
         raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
     if _GPU_UNSUPPORTED.search(" " + args + " "):
         raise ValueError(f"deviceType='gpu' supports linear squared/logistic learners only; got args: {args}")
-    if model_bytes is not None:
-        raise ValueError("deviceType='gpu' does not support initialModel")
     ref = vwmod.VW(args)  # parses & validates args, owns the final model
     cfg = vwmod.GpuSgdConfig()
     cfg.bits = int(ref.num_bits)
@@ -205,11 +249,14 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
 
     dev = int(os.environ.get("LOCAL_RANK", "0"))
     g = vwmod.GpuSgd(cfg, dev)
+    if model_bytes is not None:  # initialModel: warm-start the device table (AdaGrad state starts fresh)
+        g.set_weights(np.ascontiguousarray(vwmod.VW(args, bytes(model_bytes)).weights(), np.float32))
     t0 = time.perf_counter_ns()
     cols = [est.getFeaturesCol()] + list(est.getAdditionalFeatures() or [])
     blocks = namespace_blocks(df, cols, est.getHashSeed())
     labels, _, _ = est._labels(df)
     n = df.count()
+    blocks = blocks + [_interaction_block(blocks, pq, n) for pq in _quadratic_pairs(args)]
     indptr, idx, val = _merged_csr(blocks, n, "--noconstant" not in args)
     wcol = est.getWeightCol()
     weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
@@ -222,16 +269,23 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
             uid = vwmod.nccl_unique_id() if D.rank() == 0 else None
             _nccl_cache[key] = vwmod.nccl_comm(D.broadcast_object(uid, 0), D.rank(), world)
         comm = _nccl_cache[key]
+    # numSyncsPerPass: the same number of weight averages on every rank (row-count independent,
+    # VowpalWabbitSyncSchedule.scala:36-72); the last one is the end-of-pass sync
+    syncs = max(1, int(est.getNumSyncsPerPass() or 0))
+    bounds = np.linspace(0, n, syncs + 1).astype(np.int64)
     for _ in range(max(1, est.getNumPasses())):
-        if n:
-            g.learn(indptr, idx, val, labels, weights, int(est.getGpuBatchSize()))
-        if world > 1:
-            if comm is not None:
-                g.allreduce_average(comm)
-            else:
-                w = np.ascontiguousarray(g.weights(), np.float32)
-                _host_allreduce_f32(w)
-                g.set_weights(w / world)
+        for s0, s1 in zip(bounds[:-1], bounds[1:]):
+            if s1 > s0:
+                ip = indptr[s0:s1 + 1]
+                g.learn(ip - ip[0], idx[ip[0]:ip[-1]], val[ip[0]:ip[-1]], labels[s0:s1],
+                        None if weights is None else weights[s0:s1], int(est.getGpuBatchSize()))
+            if world > 1:
+                if comm is not None:
+                    g.allreduce_average(comm)
+                else:
+                    w = np.ascontiguousarray(g.weights(), np.float32)
+                    _host_allreduce_f32(w)
+                    g.set_weights(w / world)
     t2 = time.perf_counter_ns()
     lab = labels.astype(np.float64)
     wts = np.ones(n) if weights is None else weights.astype(np.float64)

@@ -366,3 +366,35 @@ def test_distributed_allreduce_gloo():
     w0 = np.asarray(vw.VW("--testonly", models[0]).weights())
     w1 = np.asarray(vw.VW("--testonly", models[1]).weights())
     np.testing.assert_allclose(w0, w1, rtol=1e-6, atol=1e-7)
+
+
+def test_gpu_path_quadratic_expansion_matches_native_hashing():
+    """The host expansion the GPU learner uses for -q (learners._interaction_block) produces the
+    native core's interaction features: index (a * FNV) ^ b (32-bit), value a.x * b.x, j >= i within
+    one namespace."""
+    from synapseml_amd.vw.learners import _interaction_block
+
+    rng = np.random.default_rng(0)
+    n = 50
+
+    def block(g):
+        lens = rng.integers(0, 5, size=n)
+        ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        return (g, ip, rng.integers(0, 2 ** 32, size=ip[-1], dtype=np.uint64).astype(np.uint32),
+                rng.standard_normal(ip[-1]).astype(np.float32))
+
+    A, B = block("a"), block("b")
+    for pair, same in (("ab", False), ("aa", True)):
+        _, ip, idx, val = _interaction_block([A, B], pair, n)
+        for r in range(n):
+            fa = list(zip(A[2][A[1][r]:A[1][r + 1]], A[3][A[1][r]:A[1][r + 1]]))
+            fb = fa if same else list(zip(B[2][B[1][r]:B[1][r + 1]], B[3][B[1][r]:B[1][r + 1]]))
+            exp = []
+            for i, (ha, xa) in enumerate(fa):
+                for j, (hb, xb) in enumerate(fb):
+                    if same and j < i:
+                        continue
+                    exp.append((((int(ha) * 16777619) & 0xFFFFFFFF) ^ int(hb), np.float32(xa * xb)))
+            got = list(zip(idx[ip[r]:ip[r + 1]].tolist(), val[ip[r]:ip[r + 1]].tolist()))
+            assert [e[0] for e in exp] == [g[0] for g in got]
+            np.testing.assert_allclose([e[1] for e in exp], [g[1] for g in got], rtol=1e-6)

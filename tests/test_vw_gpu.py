@@ -57,3 +57,24 @@ def test_gpu_regressor_rmse():
     m = VowpalWabbitRegressor(deviceType="gpu", numPasses=5, gpuBatchSize=256).fit(df)
     p = m.transform(df)["prediction"]
     assert np.sqrt(np.mean((p - y) ** 2)) < 0.3
+
+
+@pytest.mark.gpu
+def test_gpu_quadratic_interactions_syncs_and_initial_model():
+    """-q on the GPU learner (host-expanded with the native hashing), numSyncsPerPass chunking and
+    initialModel warm start; predictions go through the native model, which applies -q itself."""
+    rng = np.random.default_rng(3)
+    n = 20000
+    A = rng.normal(size=(n, 3))
+    B = rng.normal(size=(n, 3))
+    y = A[:, 0] * B[:, 1] - 0.5 * A[:, 2] * B[:, 0] + 0.05 * rng.normal(size=n)  # pure cross terms
+    df = DataFrame({"a": A, "b": B, "label": y})
+    kw = dict(featuresCol="a", additionalFeatures=["b"], numPasses=4, gpuBatchSize=256)
+    lin = VowpalWabbitRegressor(deviceType="gpu", **kw).fit(df)
+    quad = VowpalWabbitRegressor(deviceType="gpu", passThroughArgs="-q ab", numSyncsPerPass=3, **kw).fit(df)
+    rmse = lambda m: float(np.sqrt(np.mean((m.transform(df)["prediction"] - y) ** 2)))
+    assert rmse(quad) < 0.5 * rmse(lin), (rmse(quad), rmse(lin))
+    # warm start from the trained model: a single extra pass keeps the quality
+    warm = VowpalWabbitRegressor(deviceType="gpu", passThroughArgs="-q ab", initialModel=quad.getModel(),
+                                 **dict(kw, numPasses=1)).fit(df)
+    assert rmse(warm) < 1.2 * rmse(quad) + 0.05
