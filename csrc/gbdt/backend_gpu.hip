@@ -45,11 +45,11 @@ constexpr int kHistThreads = 512;
 constexpr int kFeatPerGroup = 32;          // 8 dwords of bins per block
 constexpr int kHistStride = 257;           // padded LDS row (bank spread)
 constexpr int kMaxHistBlocks = 512;        // = resident capacity at 2 blocks/CU
-constexpr int kMinRowsPerHistBlock = 2048;
+constexpr int kMinRowsPerHistBlockDefault = 1024;  // A/B: 1024 ~ 512 < 2048 < 4096
+__constant__ int c_min_rows_per_hist_block = kMinRowsPerHistBlockDefault;
 constexpr int kPartThreads = 512;
 constexpr int kMaxPartBlocks = 2048;
-constexpr int kPartRows = 16;
-constexpr int kPartTile = kPartThreads * kPartRows;
+constexpr int kPartRowsDefault = 8;  // A/B on MI355X: 8 rows/thread beat 16 and 4 (profiles/README)
 
 struct DLeaf {
   int32_t begin, count, buf, depth;  // local row segment; buf: -1 physical, 0/1 ping-pong
@@ -691,10 +691,10 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // int2 and the cross-block reduction is an exact int64 sum: the histogram is
 // bitwise independent of row order and of the block decomposition. (A/B on
 // MI355X: float ds_add_f32 13.4 ms/iter, 2x ds_add_u32 4.26, packed u64 4.16.)
-constexpr int kHistUnroll = 4;
+constexpr int kHistUnrollDefault = 2;  // A/B: 2 rows in flight per thread beat 4 and 8
 
 __device__ __forceinline__ int HistBlocks(int count) {
-  return max(1, min(kMaxHistBlocks, ceil_div_i(count, kMinRowsPerHistBlock)));
+  return max(1, min(kMaxHistBlocks, ceil_div_i(count, c_min_rows_per_hist_block)));
 }
 
 struct HScale {
@@ -731,6 +731,7 @@ __device__ __forceinline__ void hist_accumulate(unsigned long long* sh, const ui
     if (j + 16 < Fg) atomicAdd(&sh[(j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u)], packed);
 }
 
+template <int kHistUnroll>
 __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
@@ -1252,6 +1253,7 @@ __device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int
 // depends on the order tiles claim their ranges; nothing downstream depends
 // on it (histograms are exact integer sums, see K3).
 
+template <int kPartRows>
 __global__ __launch_bounds__(kPartThreads) void part_kernel(
     DState* __restrict__ st, const SplitResult* __restrict__ lbest, const uint8_t* __restrict__ cbins, int64_t n,
     const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
@@ -1260,6 +1262,7 @@ __global__ __launch_bounds__(kPartThreads) void part_kernel(
     const float* __restrict__ h, FeatMeta fm) {
   if (st->done) return;
   const int pbegin = st->pbegin, pcount = st->pcount, pbuf = st->pbuf;
+  constexpr int kPartTile = kPartThreads * kPartRows;
   const int ntiles = ceil_div_i(pcount, kPartTile);
   if (static_cast<int>(blockIdx.x) >= ntiles) return;
   const SplitResult sr = lbest[st->split_leaf];
@@ -1494,7 +1497,19 @@ class GpuBackend : public TrainBackend {
     slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * E_);
     part_.alloc(static_cast<size_t>(E_) + 1);  // histogram + (row count, 0)
     hist_pool_.alloc(static_cast<size_t>(2 * L_ + 2) * E_);
-    part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + kPartTile - 1) / kPartTile)));
+    // launch-shape knobs for A/B runs (defaults are the measured best)
+    if (const char* e = std::getenv("SML_PART_ROWS")) part_rows_ = std::atoi(e);
+    if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll_ = std::atoi(e);
+    if (part_rows_ != 4 && part_rows_ != 8 && part_rows_ != 16) part_rows_ = kPartRowsDefault;
+    if (const char* e = std::getenv("SML_HIST_MIN_ROWS")) {
+      const int v = std::max(256, std::atoi(e));
+      SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_min_rows_per_hist_block), &v, sizeof(int)));
+    }
+    if (hist_unroll_ != 2 && hist_unroll_ != 4 && hist_unroll_ != 8) hist_unroll_ = kHistUnrollDefault;
+    {
+      const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
+      part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
+    }
     fbest_.alloc(2 * F_);
     lbest_.alloc(L_);
     lgain_.alloc(L_);
@@ -1709,7 +1724,8 @@ class GpuBackend : public TrainBackend {
     EnqueueFindChoose();
     for (int s = 1; s < L_; ++s) {
       // partition the chosen leaf, histogram its smaller child, search both
-      hipLaunchKernelGGL(part_kernel, dim3(part_grid_), dim3(kPartThreads), 0, stream_, state_, lbest_.get(),
+      auto pk = part_rows_ == 16 ? part_kernel<16> : (part_rows_ == 4 ? part_kernel<4> : part_kernel<8>);
+      hipLaunchKernelGGL(pk, dim3(part_grid_), dim3(kPartThreads), 0, stream_, state_, lbest_.get(),
                          cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
                          perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
       SML_HIP_CHECK(hipGetLastError());
@@ -1816,7 +1832,8 @@ class GpuBackend : public TrainBackend {
 
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-    hipLaunchKernelGGL(hist_kernel, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_,
+    auto hk = hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>);
+    hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_,
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
                        perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     SML_HIP_CHECK(hipGetLastError());
@@ -1967,6 +1984,7 @@ class GpuBackend : public TrainBackend {
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
   int part_grid_ = 1;
+  int part_rows_ = kPartRowsDefault, hist_unroll_ = kHistUnrollDefault;
   DevBuf<uint8_t> blob_;
   DState* state_ = nullptr;
   size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
