@@ -129,6 +129,10 @@ def main() -> None:
         t = torch.tensor(el, device="cuda" if use_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # K11: the training metric (AUC over all rows) evaluated where the scores live (outside the timed region)
+    t_ev = time.perf_counter()
+    train_auc = dict(booster.eval(0)).get("auc")
+    eval_ms = (time.perf_counter() - t_ev) * 1e3
     # sanity: holdout AUC of the trained model (outside the timed region)
     auc = None
     if rank == 0:
@@ -165,6 +169,8 @@ def main() -> None:
                 "train_auc_sample": auc,
                 "setup_s": round(setup_s, 2),
                 "bin_encode_s": round(encode_s, 3),
+                "train_auc_all_rows": None if train_auc is None else round(train_auc, 5),
+                "train_metric_eval_ms": round(eval_ms, 2),
                 "histogram_allreduce": (None if world == 1 else "host (gloo)" if not use_gpu else
                                         "p2p-ipc one-shot" if D.p2p_status.get("active") else
                                         "rccl (%s)" % D.p2p_status.get("reason", "")),

@@ -41,6 +41,11 @@ class TrainBackend {
   // Draw the bag (and apply GOSS gradient scaling) where the gradients live.
   // Returns false when the backend leaves sampling to the host.
   virtual bool SampleRows(const RowSampleSpec& spec) { (void)spec; return false; }
+  // Training-metric value computed where the scores live (K11); false = host path.
+  virtual bool EvalOnDevice(const std::string& name, const Objective& obj, double* out) {
+    (void)name; (void)obj; (void)out;
+    return false;
+  }
   virtual Tree TrainTree(int k, const std::vector<char>& feature_mask) = 0;
   // score[k] += scale * tree(row) for every training row
   virtual void UpdateScore(const Tree& t, int k, double scale) = 0;
@@ -59,6 +64,9 @@ std::unique_ptr<TrainBackend> MakeCpuBackend();
 // Defined in the HIP translation unit; returns nullptr if no device.
 std::unique_ptr<TrainBackend> MakeGpuBackend(int device_id);
 bool GpuAvailable();
+// metric_gpu.hip: auc / binary_logloss / binary_error / l2 / rmse / l1 on device scores
+bool DeviceEvalMetric(const std::string& name, const ObjParams& p, const double* score, const float* label,
+                      const float* weight, int64_t n, void* stream, double* out);
 
 // Host reference of the split search (K5): best split of one feature given its
 // histogram. Used by the CPU backend and by tests that compare the device.

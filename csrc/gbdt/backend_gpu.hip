@@ -1686,6 +1686,11 @@ class GpuBackend : public TrainBackend {
     return true;
   }
 
+  bool EvalOnDevice(const std::string& name, const Objective& obj, double* out) override {
+    if (K_ != 1) return false;
+    return DeviceEvalMetric(name, obj.params(), score_.get(), label_.get(), weight_.get(), n_, stream_, out);
+  }
+
   void Synchronize() override {
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
     AccountScoreTime();

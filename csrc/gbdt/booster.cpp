@@ -445,13 +445,21 @@ std::vector<std::pair<std::string, double>> Booster::Eval(int idx) {
   const double* scores;
   if (idx == 0) {
     d = train_.get(); obj = objective_.get();
-    backend_->GetScores(&train_scores);
-    scores = train_scores.data();
+    scores = nullptr;  // fetched from the backend only if a metric has no device implementation
   } else {
     d = valid_[idx - 1].get(); obj = valid_objectives_[idx - 1].get();
     scores = valid_scores_[idx - 1].data();
   }
   for (const auto& name : EvalNames()) {
+    double dv = 0.0;
+    if (idx == 0 && backend_->EvalOnDevice(name, *obj, &dv)) {
+      out.emplace_back(name, dv);
+      continue;
+    }
+    if (!scores) {
+      backend_->GetScores(&train_scores);
+      scores = train_scores.data();
+    }
     double v = EvalMetric(name, *obj, scores, d->label.data(), d->weight.empty() ? nullptr : d->weight.data(),
                           d->num_data, num_class_, d->query_boundaries, cfg_.label_gain);
     out.emplace_back(name, v);

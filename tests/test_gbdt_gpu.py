@@ -344,3 +344,26 @@ def test_gpu_feature_fraction_bynode_matches_cpu():
         tc = mc.split(t)[1].split("Tree=")[0]
         tg = mg.split(t)[1].split("Tree=")[0]
         assert line(tc, "split_feature") == line(tg, "split_feature")
+
+
+def test_gpu_training_metrics_on_device():
+    """K11: auc / binary_logloss / binary_error / rmse of the device-resident training scores vs the host
+    formulas (sorted trapezoid AUC with ties, clipped logloss)."""
+    from sklearn.metrics import roc_auc_score
+
+    X, y = _data(n=80000)
+    X[:, 0] = np.round(X[:, 0], 1)  # coarse feature -> many tied scores
+    b = _train(X, y, "objective=binary metric=auc,binary_logloss,binary_error device_type=gpu", 6)
+    ev = dict(b.eval(0))
+    s = b.train_scores()
+    p = 1 / (1 + np.exp(-s))
+    assert abs(ev["auc"] - roc_auc_score(y, s)) < 1e-9
+    pc = np.clip(p, 1e-15, 1 - 1e-15)
+    np.testing.assert_allclose(ev["binary_logloss"], -np.mean(y * np.log(pc) + (1 - y) * np.log(1 - pc)), rtol=1e-9)
+    np.testing.assert_allclose(ev["binary_error"], np.mean((p > 0.5) != (y > 0)), rtol=1e-12)
+    yr = (X[:, 0] * 2 + X[:, 1] ** 2).astype(np.float32)
+    r = _train(X, yr, "objective=regression metric=rmse,l1 device_type=gpu", 4)
+    er = dict(r.eval(0))
+    sr = r.train_scores()
+    np.testing.assert_allclose(er["rmse"], np.sqrt(np.mean((sr - yr) ** 2)), rtol=1e-9)
+    np.testing.assert_allclose(er["l1"], np.mean(np.abs(sr - yr)), rtol=1e-9)

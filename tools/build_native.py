@@ -50,6 +50,7 @@ MODULES = {
             "predict_gpu.hip",
             "comm_p2p.hip",
             "bin_encode.hip",
+            "metric_gpu.hip",
         ],
         ["-lrccl", "-lrocprofiler-sdk-roctx"],
     ),
