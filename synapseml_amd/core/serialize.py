@@ -173,9 +173,14 @@ def save_stage(stage, path: str, overwrite: bool = False) -> None:
                 locs[k] = _write_complex(v, os.path.join(path, "complexParams", k))
         else:
             param_map[k] = _to_json_value(v)
+    default_locs = {}
     for k, v in stage._defaultParamMap.items():
         if k in decl and not decl[k].complex and _jsonable(_to_json_value(v)):
             default_map[k] = _to_json_value(v)
+        elif k in decl and v is not None and k not in stage._paramMap:
+            # complex defaults built by the constructor (e.g. ImageFeaturizer's inner ONNXModel): a load
+            # does not run the constructor, so they are written like complex params
+            default_locs[k] = _write_complex(v, os.path.join(path, "complexDefaultParams", k))
     meta = {
         "class": class_path(stage),
         "timestamp": int(time.time() * 1000),
@@ -186,6 +191,8 @@ def save_stage(stage, path: str, overwrite: bool = False) -> None:
     }
     if locs:
         meta["complexParamLocs"] = {k: f"complexParams/{k}#{kind}" for k, kind in locs.items()}
+    if default_locs:
+        meta["complexDefaultParamLocs"] = {k: f"complexDefaultParams/{k}#{kind}" for k, kind in default_locs.items()}
     with open(os.path.join(path, "metadata", "part-00000"), "w") as f:
         f.write(json.dumps(meta) + "\n")
     open(os.path.join(path, "metadata", "_SUCCESS"), "w").close()
@@ -210,5 +217,9 @@ def load_stage(path: str):
     for k, loc in meta.get("complexParamLocs", {}).items():
         rel, _, kind = loc.partition("#")
         obj._paramMap[k] = _read_complex(os.path.join(path, rel), kind)
+    for k, loc in meta.get("complexDefaultParamLocs", {}).items():
+        rel, _, kind = loc.partition("#")
+        if k in obj._params_decl:
+            obj._defaultParamMap[k] = _read_complex(os.path.join(path, rel), kind)
     obj._load_extra(path)
     return obj
