@@ -171,7 +171,8 @@ class ServingServer:
         return f"http://{self.host}:{self.port}/{self.api}"
 
     def start(self) -> "ServingServer":
-        self._thread.start()
+        if not self._thread.is_alive():  # idempotent: `with serve(...)` after start() is fine
+            self._thread.start()
         self._ready.wait(30)
         return self
 

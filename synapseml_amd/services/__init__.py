@@ -9,6 +9,7 @@ from .base import CognitiveServicesBase, HasAsyncReply, ServiceParam, ServiceVal
 from .form import (AnalyzeBusinessCards, AnalyzeCustomModel, AnalyzeDocument, AnalyzeIDDocuments, AnalyzeInvoices,
                    AnalyzeLayout, AnalyzeReceipts, FormOntologyLearner, FormOntologyTransformer, GetCustomModel,
                    ListCustomModels)
+from .langchain import LangchainTransformer
 from .misc import (AddDocuments, AddressGeocoder, AzureSearchWriter, BingImageSearch, CheckPointInPolygon,
                    ReverseAddressGeocoder, SpeakerEmotionInference, SpeechToText, SpeechToTextSDK, TextToSpeech)
 from .openai import OpenAIChatCompletion, OpenAICompletion, OpenAIDefaults, OpenAIEmbedding, OpenAIPrompt

@@ -187,3 +187,30 @@ def test_read_binary_files_zip_and_sampling(tmp_path):
     s1 = read_binary_files(str(tmp_path), recursive=True, sampleRatio=0.5, seed=3)
     s2 = read_binary_files(str(tmp_path), recursive=True, sampleRatio=0.5, seed=3)
     assert s1["path"].tolist() == s2["path"].tolist()
+
+
+def test_serve_saved_model_end_to_end(tmp_path):
+    """Save a trained classifier, serve it with serve_model's handler, score over HTTP."""
+    import json
+    import urllib.request
+
+    import numpy as np
+
+    from synapseml_amd.core import DataFrame
+    from synapseml_amd.core.serialize import load_stage
+    from synapseml_amd.io.serve_model import model_handler
+    from synapseml_amd.io.serving import ServingServer
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((600, 4))
+    y = (X[:, 0] > 0).astype(float)
+    m = LightGBMClassifier(numIterations=10, numLeaves=7, deviceType="cpu").fit(DataFrame({"features": X, "label": y}))
+    m.save(str(tmp_path / "m"))
+    model = load_stage(str(tmp_path / "m"))
+    with ServingServer(model_handler(model, ["features"], ["prediction", "probability"])).start() as srv:
+        for row, lab in ((X[0], y[0]), (X[1], y[1])):
+            body = json.dumps({"features": row.tolist()}).encode()
+            r = json.loads(urllib.request.urlopen(urllib.request.Request(srv.address, data=body, method="POST"),
+                                                  timeout=10).read())
+            assert r["prediction"] == lab and len(r["probability"]) == 2

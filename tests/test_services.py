@@ -302,3 +302,46 @@ def test_service_param_persistence_roundtrip(tmp_path):
 
     t2 = load_stage(str(tmp_path / "ts"))
     assert t2.getTextCol() == "text" and t2.getLanguage() == "en" and t2.getSubscriptionKey() == "k"
+
+
+class _FakeChain:
+    """Stands in for a langchain LLMChain (langchain is not installed): uppercases the prompt,
+    fails on 'boom', and records the OpenAI environment it saw."""
+
+    def __init__(self):
+        self.seen_env = None
+
+    def run(self, x):
+        import os
+
+        self.seen_env = os.environ.get("OPENAI_API_KEY")
+        if x == "boom":
+            raise RuntimeError("rate limited")
+        return {"text": x.upper()}
+
+
+class _Runnable:
+    def invoke(self, x):
+        class Msg:
+            content = f"<{x}>"
+
+        return Msg()
+
+
+def test_langchain_transformer_rows_errors_env_and_persistence(tmp_path):
+    import os
+
+    chain = _FakeChain()
+    t = S.LangchainTransformer(inputCol="q", outputCol="a", chain=chain, subscriptionKey="k123", concurrency=4)
+    df = DataFrame({"q": _obj(["hi", "boom", "there"])})
+    out = t.transform(df)
+    assert out["a"].tolist() == ["HI", None, "THERE"]
+    assert out["errorCol"][0] is None and "rate limited" in out["errorCol"][1]
+    assert chain.seen_env == "k123" and os.environ.get("OPENAI_API_KEY") != "k123"  # restored afterwards
+    r = S.LangchainTransformer(inputCol="q", outputCol="a", chain=_Runnable()).transform(df)
+    assert r["a"].tolist() == ["<hi>", "<boom>", "<there>"]
+    t.save(str(tmp_path / "lc"))
+    back = S.LangchainTransformer.load(str(tmp_path / "lc"))
+    assert back.transform(df)["a"].tolist() == ["HI", None, "THERE"]
+    with pytest.raises(ValueError):
+        S.LangchainTransformer(inputCol="q", outputCol="a").transform(df)
