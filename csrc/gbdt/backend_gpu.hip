@@ -257,6 +257,26 @@ __device__ __forceinline__ void PairLambda(const RankTables& t, const double* s_
   *suml -= pl;  // each pair is visited from both ends: sum = -2 pl per pair
 }
 
+// Register-path form: each document's label gain and rank discount are
+// looked up once (fp32) instead of per pair, so the O(pairs) loop is ALU only.
+__device__ __forceinline__ void PairLambdaPre(float sig, float imd, bool use_norm, double si, int li, float gi,
+                                              float di, double sj, int lj, float gj, float dj, double* lam,
+                                              double* hes, double* suml) {
+  const bool i_high = li > lj;
+  const float gap = i_high ? gi - gj : gj - gi;
+  const float pd = fabsf(di - dj);
+  const float ds = static_cast<float>(i_high ? si - sj : sj - si);
+  float dn = gap * pd * imd;
+  if (use_norm) dn = __fdividef(dn, 0.01f + fabsf(ds));
+  float pl = __frcp_rn(1.0f + __expf(sig * ds));
+  float ph = pl * (1.0f - pl);
+  pl *= -sig * dn;
+  ph *= sig * sig * dn;
+  *lam += i_high ? pl : -pl;
+  *hes += ph;
+  *suml -= pl;
+}
+
 // All pairs of doc i: a doc ranked below max_position only pairs with the
 // top max_position documents (s_top, by rank), a top document with every
 // other document.
@@ -462,9 +482,19 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
       }
     }
   }
+  // per-document label gain and rank discount (ranks < cnt <= kRankLds: table hit)
+  const unsigned gtop = static_cast<unsigned>(t.ngain - 1);
+  float gn[NU], dc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const bool ok = u * 64 + lane < cnt;
+    gn[u] = ok ? static_cast<float>(t.gain[min(static_cast<unsigned>(lab[u]), gtop)]) : 0.f;
+    dc[u] = ok ? static_cast<float>(s_disc[rk[u]]) : 0.f;
+  }
   // top list: lane r holds the document of rank r (ranks are a permutation)
   double tsc = 0.0;
   int tlab = 0, tdoc = 0;
+  float tgn = 0.f;
   {
     __shared__ int s_doc_of_rank[64];
 #pragma unroll
@@ -475,10 +505,13 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
       tdoc = s_doc_of_rank[lane];
       tsc = score[b + tdoc];
       tlab = static_cast<int>(label[b + tdoc]);
+      tgn = static_cast<float>(t.gain[min(static_cast<unsigned>(tlab), gtop)]);
     }
     __syncthreads();
   }
-  const double imd = t.inv_max_dcg[q];
+  const float tdc = static_cast<float>(s_disc[lane]);  // discount of rank `lane` (valid for lane < ntop)
+  const float sig = static_cast<float>(t.sigma);
+  const float fimd = static_cast<float>(t.inv_max_dcg[q]);
   const bool use_norm = t.norm && mx != mn;
   double lam[NU], hes[NU];
 #pragma unroll
@@ -490,12 +523,14 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
     const double si = ReadLaneD(tsc, r);
     const int li = __builtin_amdgcn_readlane(tlab, r);
     const int di = __builtin_amdgcn_readlane(tdoc, r);
+    const float gi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tgn), r));
+    const float dci = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tdc), r));
     double la = 0.0, he = 0.0;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int j = u * 64 + lane;
       if (j < cnt && j != di && lab[u] != li)
-        PairLambda(t, s_disc, si, li, r, sc[u], lab[u], rk[u], imd, use_norm, &la, &he, &suml);
+        PairLambdaPre(sig, fimd, use_norm, si, li, gi, dci, sc[u], lab[u], gn[u], dc[u], &la, &he, &suml);
     }
     la = WaveSumD(la);
     he = WaveSumD(he);
@@ -509,7 +544,10 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
     for (int r = 0; r < ntop; ++r) {
       const int lj = __builtin_amdgcn_readlane(tlab, r);
       if (lj == lab[u]) continue;
-      PairLambda(t, s_disc, sc[u], lab[u], rk[u], ReadLaneD(tsc, r), lj, r, imd, use_norm, &lam[u], &hes[u], &suml);
+      const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tgn), r));
+      const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tdc), r));
+      PairLambdaPre(sig, fimd, use_norm, sc[u], lab[u], gn[u], dc[u], ReadLaneD(tsc, r), lj, gj, dj, &lam[u], &hes[u],
+                    &suml);
     }
   }
   suml = WaveSumD(suml);
@@ -530,6 +568,27 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   }
 }
 
+__device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
+  return cnt <= kRankLds && t.max_position <= 64;
+}
+
+// The common case on its own kernel: its LDS is the discount table and the
+// 64-entry rank->doc map (2.3 KB instead of the LDS path's 11.5 KB), so the
+// one-wave blocks are VGPR-limited (4 waves/SIMD) rather than LDS-limited.
+__global__ __launch_bounds__(64) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
+                                                             const float* __restrict__ label,
+                                                             const float* __restrict__ weight, float* __restrict__ g,
+                                                             float* __restrict__ h) {
+  __shared__ double s_disc[kRankLds];
+  for (int r = threadIdx.x; r < kRankLds; r += 64) s_disc[r] = 1.0 / log2(2.0 + r);
+  __syncthreads();
+  for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
+    const int cnt = t.qb[q + 1] - t.qb[q];
+    if (cnt <= 0 || !RegsEligible(t, cnt)) continue;
+    LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc);
+  }
+}
+
 __global__ __launch_bounds__(64) void lambdarank_kernel(RankTables t, const double* __restrict__ score,
                                                         const float* __restrict__ label,
                                                         const float* __restrict__ weight, float* __restrict__ g,
@@ -544,9 +603,8 @@ __global__ __launch_bounds__(64) void lambdarank_kernel(RankTables t, const doub
   __syncthreads();
   for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
     const int cnt = t.qb[q + 1] - t.qb[q];
-    if (cnt <= 0) continue;
-    if (cnt <= kRankLds && t.max_position <= 64) LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc);
-    else if (cnt <= kRankLds) LambdarankQuery<true>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk, s_disc, s_top, s_tlam, s_thes);
+    if (cnt <= 0 || RegsEligible(t, cnt)) continue;  // handled by lambdarank_regs_kernel
+    if (cnt <= kRankLds) LambdarankQuery<true>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk, s_disc, s_top, s_tlam, s_thes);
     else LambdarankQuery<false>(t, q, score, label, weight, g, h, s_sc, s_lab, s_rk, s_disc, s_top, s_tlam, s_thes);
   }
 }
@@ -1600,9 +1658,16 @@ class GpuBackend : public TrainBackend {
       EnsureRankTables(obj);
       if (rank_.nq > 0) {
         const int grid = std::min(rank_.nq, 65536);
-        hipLaunchKernelGGL(lambdarank_kernel, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(), label_.get(),
-                           weight_.get(), g_.get(), h_.get());
-        SML_HIP_CHECK(hipGetLastError());
+        if (rank_regs_) {
+          hipLaunchKernelGGL(lambdarank_regs_kernel, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(),
+                             label_.get(), weight_.get(), g_.get(), h_.get());
+          SML_HIP_CHECK(hipGetLastError());
+        }
+        if (rank_lds_) {
+          hipLaunchKernelGGL(lambdarank_kernel, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(), label_.get(),
+                             weight_.get(), g_.get(), h_.get());
+          SML_HIP_CHECK(hipGetLastError());
+        }
       }
       ghmax_valid_ = false;
       stats.grad_ms += Ms(t0);
@@ -1810,7 +1875,14 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipMemcpy(rank_imd_.get(), imd.data(), sizeof(double) * imd.size(), hipMemcpyHostToDevice));
     SML_HIP_CHECK(hipMemcpy(rank_gain_.get(), gain.data(), sizeof(double) * gain.size(), hipMemcpyHostToDevice));
     int max_q = 0;
-    for (size_t q = 0; q + 1 < qb.size(); ++q) max_q = std::max(max_q, qb[q + 1] - qb[q]);
+    rank_regs_ = rank_lds_ = false;
+    const bool regs_pos = obj.max_position() <= 64;  // RegsEligible, host side: which kernels have work
+    for (size_t q = 0; q + 1 < qb.size(); ++q) {
+      const int c = qb[q + 1] - qb[q];
+      max_q = std::max(max_q, c);
+      if (c <= 0) continue;
+      if (regs_pos && c <= kRankLds) rank_regs_ = true; else rank_lds_ = true;
+    }
     rank_ = RankTables{};
     if (max_q > kRankLds) {  // long queries stream ranks / lambdas through global scratch
       rank_scratch_.alloc(n_);
@@ -2003,7 +2075,7 @@ class GpuBackend : public TrainBackend {
   DevBuf<uint32_t> sel_key_;
   DevBuf<unsigned int> sel_hist_;
   // lambdarank (K2 ranking)
-  bool rank_ready_ = false;
+  bool rank_ready_ = false, rank_regs_ = false, rank_lds_ = false;
   RankTables rank_{};
   DevBuf<int32_t> rank_qb_, rank_scratch_;
   DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_;
