@@ -226,6 +226,34 @@ __device__ __forceinline__ double WaveSumD(double v) {
   return v;
 }
 
+// Full-wave sum on the DPP network (no LDS crossbar): xor-1 / xor-2 quad
+// permutes, half-row and row mirrors give every row its sum, row_bcast:15 and
+// row_bcast:31 fold the rows into lane 63, v_readlane broadcasts it. All 64
+// lanes must be active. Measured on the lambdarank register path it was
+// slower than WaveSumD (1.62 vs 1.46 ms per gradient call: the 64-bit value
+// needs two DPP moves per step plus the readlanes), so it is not used there;
+// see profiles/ranker_dpp_wavesum_experiment_r1.patch.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ double DppD(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(x), kCtrl, kRowMask, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(x >> 32), kCtrl, kRowMask, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+__device__ __forceinline__ double WaveSumDpp(double v) {
+  v += DppD<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v += DppD<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v += DppD<0x141, 0xF>(v);  // row_half_mirror
+  v += DppD<0x140, 0xF>(v);  // row_mirror
+  v += DppD<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v += DppD<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), 63);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), 63);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
 // lambda / hessian contribution of the pair (doc i, doc j) to doc i; disc(r)
 // = 1/log2(2+r) comes from an LDS table for ranks below kRankLds
 __device__ __forceinline__ double Discount(const double* s_disc, int r) {
