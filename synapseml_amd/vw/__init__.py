@@ -3,8 +3,8 @@
 featurizers, regressor/classifier/contextual-bandit/generic estimators,
 progressive validation, DSJson/CSE bandit-log transformers and off-policy
 estimators."""
-from .featurizer import (VowpalWabbitFeaturizer, VowpalWabbitInteractions, VowpalWabbitMurmurWithPrefix,
-                         murmur_hash, sort_and_distinct)
+from .featurizer import (VowpalWabbitFeaturizer, VowpalWabbitInteractions, VowpalWabbitMurmur,
+                         VowpalWabbitMurmurWithPrefix, murmur_hash, sort_and_distinct)
 from .learners import (VowpalWabbitClassificationModel, VowpalWabbitClassifier, VowpalWabbitGeneric,
                        VowpalWabbitGenericModel, VowpalWabbitGenericProgressive, VowpalWabbitProgressive,
                        VowpalWabbitRegressionModel, VowpalWabbitRegressor)

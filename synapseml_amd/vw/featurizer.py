@@ -27,6 +27,19 @@ def murmur_hash(s: str, seed: int) -> int:
     return h - (1 << 32) if h >= (1 << 31) else h
 
 
+class VowpalWabbitMurmur:
+    """Static murmur3_32 entry point of the VW native library
+    (``VowpalWabbitMurmur.hash(str|bytes, seed)``, used at
+    VowpalWabbitMurmurWithPrefix.scala:32,77 and VowpalWabbitUtil.scala:23).
+    Strings hash their UTF-8 bytes; the result is a signed 32-bit int."""
+
+    @staticmethod
+    def hash(value, seed: int) -> int:  # noqa: A003
+        data = value.encode("utf-8") if isinstance(value, str) else bytes(value)
+        h = int(_vw().murmur3(data, seed & 0xFFFFFFFF))
+        return h - (1 << 32) if h >= (1 << 31) else h
+
+
 class VowpalWabbitMurmurWithPrefix:
     """Murmur hashing with a fixed string prefix (VowpalWabbitMurmurWithPrefix.scala:15-79)."""
 

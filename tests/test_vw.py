@@ -45,6 +45,16 @@ def test_murmur_with_prefix_matches_concat():
     assert [int(b) for b in batch] == [_u(murmur_hash("pre" + s, 5)) for s in ["a", "bb", "ccc"]]
 
 
+def test_murmur_static_hash_str_and_bytes():
+    from synapseml_amd.vw import VowpalWabbitMurmur
+
+    for s in ["", "features", "héllo"]:
+        assert VowpalWabbitMurmur.hash(s, 0) == murmur_hash(s, 0)
+        assert VowpalWabbitMurmur.hash(s.encode("utf-8"), 0) == murmur_hash(s, 0)
+    assert _u(VowpalWabbitMurmur.hash(b"test", 0)) == 0xBA6BD213
+    assert VowpalWabbitMurmur.hash("Hello, world!", 0) < 0  # signed like the JVM int (0xC0363E43)
+
+
 # ------------------------------------------------------------------ featurizer
 def test_featurizer_strings_numeric_and_collisions():
     df = DataFrame({"in": ["markus", "marie"], "num": [2.0, 0.0], "flag": [True, False]})
