@@ -29,6 +29,51 @@ from .schema import make_image_row, row_to_array, to_array
 STAGE_NAME = "stageName"
 
 
+class _Stage:
+    """Named stage-map builders (the reference's ImageTransformer stage objects,
+    ImageTransformer.scala:31-283): ``ResizeImage.stageName == "resize"`` and
+    ``ResizeImage.make(height=.., width=..)`` gives the map an ImageTransformer
+    ``stages`` list holds."""
+
+    stageName = ""
+
+    @classmethod
+    def make(cls, **params) -> dict:
+        return {STAGE_NAME: cls.stageName, **params}
+
+
+class ResizeImage(_Stage):
+    stageName = "resize"
+
+
+class CropImage(_Stage):
+    stageName = "crop"
+
+
+class CenterCropImage(_Stage):
+    stageName = "centercrop"
+
+
+class ColorFormat(_Stage):
+    stageName = "colorformat"
+
+
+class Flip(_Stage):
+    stageName = "flip"
+
+
+class Blur(_Stage):
+    stageName = "blur"
+
+
+class Threshold(_Stage):
+    stageName = "threshold"
+
+
+class GaussianKernel(_Stage):
+    stageName = "gaussiankernel"
+
+
 def _img():
     return native.load("_image")
 

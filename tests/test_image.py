@@ -183,3 +183,11 @@ def test_gpu_stage_kernels_match_host():
     gr = torch.empty((B, h, w, 1), dtype=torch.uint8, device="cuda")
     img.cvt_color_device(src.data_ptr(), B * h * w, 3, 6, gr.data_ptr(), stream)
     np.testing.assert_array_equal(gr.cpu().numpy().reshape(-1), img.cvt_color(a.reshape(-1, w, c), 6).reshape(-1))
+
+
+def test_named_stage_maps_match_builder():
+    from synapseml_amd.image import CenterCropImage, Flip, ImageTransformer, ResizeImage
+
+    t = ImageTransformer().resize(height=8, width=6).centerCrop(4, 4).flip(1)
+    assert t.getStages() == [ResizeImage.make(height=8, width=6), CenterCropImage.make(height=4, width=4),
+                             Flip.make(flipCode=1)]
