@@ -777,6 +777,15 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // int2 and the cross-block reduction is an exact int64 sum: the histogram is
 // bitwise independent of row order and of the block decomposition. (A/B on
 // MI355X: float ds_add_f32 13.4 ms/iter, 2x ds_add_u32 4.26, packed u64 4.16.)
+// Precision: the quantum of one row is chunk_rows * max|g| / 2^31 (g) and
+// chunk_rows * max h / 2^32 (h) with chunk_rows <= count / blocks (>= 1024),
+// e.g. ~1e-5 * max|g| for the 11M-row root. A bin holding k rows then carries
+// ~sqrt(k) * quantum / 3.5 of rounding error: about the relative precision of
+// an fp32 histogram (LightGBM's GPU learner default, gpu_use_dp=false) on
+// populated bins, coarser on nearly empty bins; hessians far below
+// quantum / 2 (very confident rows of a near-separable problem) round to zero.
+// test_gpu_histogram_quantisation_skewed_hessians pins tree structure, node
+// hessian sums and loss against the fp64 host oracle in that regime.
 constexpr int kHistUnrollDefault = 2;  // A/B: 2 rows in flight per thread beat 4 and 8
 
 __device__ __forceinline__ int HistBlocks(int count) {

@@ -629,6 +629,9 @@ std::unique_ptr<Booster> Booster::FromModelString(const std::string& model) {
   b->num_tree_per_iter_ = header.count("num_tree_per_iteration") ? std::stoi(header["num_tree_per_iteration"]) : b->num_class_;
   b->label_index_ = header.count("label_index") ? std::stoi(header["label_index"]) : 0;
   b->max_feature_idx_ = header.count("max_feature_idx") ? std::stoi(header["max_feature_idx"]) : 0;
+  if (b->max_feature_idx_ < 0 || b->max_feature_idx_ > (1 << 28)) throw std::runtime_error("model string: bad max_feature_idx");
+  if (b->num_class_ < 1 || b->num_tree_per_iter_ < 1 || b->num_class_ > (1 << 16) || b->num_tree_per_iter_ > (1 << 16))
+    throw std::runtime_error("model string: bad num_class / num_tree_per_iteration");
   b->objective_str_ = header.count("objective") ? header["objective"] : "regression";
   {
     std::istringstream fs(header["feature_names"]);
@@ -639,11 +642,21 @@ std::unique_ptr<Booster> Booster::FromModelString(const std::string& model) {
   }
   // trees
   std::string block;
-  bool in_tree = false;
+  bool in_tree = false, saw_tree = false, saw_end = false;
   for (; i < lines.size(); ++i) {
     std::string l = Trim(lines[i]);
+    if (l.rfind("Tree=", 0) == 0) saw_tree = true;
+    if (l == "end of trees") saw_end = true;
     if (l.rfind("Tree=", 0) == 0 || l == "end of trees") {
-      if (in_tree) b->trees_.push_back(Tree::FromString(block));
+      if (in_tree) {
+        Tree t = Tree::FromString(block);
+        for (int n = 0; n + 1 < t.num_leaves; ++n)
+          if (t.split_feature[n] > b->max_feature_idx_)
+            throw std::runtime_error("malformed tree in model string: split_feature " +
+                                     std::to_string(t.split_feature[n]) + " > max_feature_idx " +
+                                     std::to_string(b->max_feature_idx_));
+        b->trees_.push_back(std::move(t));
+      }
       block.clear();
       in_tree = l.rfind("Tree=", 0) == 0;
       if (l == "end of trees") { ++i; break; }
@@ -651,6 +664,7 @@ std::unique_ptr<Booster> Booster::FromModelString(const std::string& model) {
     }
     if (in_tree) { block += l; block += "\n"; }
   }
+  if (saw_tree && !saw_end) throw std::runtime_error("model string is truncated: no 'end of trees' after the trees");
   // parameters section
   std::ostringstream params;
   bool in_params = false;

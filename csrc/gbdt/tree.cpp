@@ -1,6 +1,7 @@
 #include "tree.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -8,6 +9,7 @@
 #include <map>
 #include <sstream>
 #include <stdexcept>
+#include <type_traits>
 
 namespace sml {
 
@@ -347,11 +349,35 @@ std::vector<T> ParseVec(const std::string& s) {
   std::vector<T> out;
   std::istringstream is(s);
   std::string tok;
-  while (is >> tok) out.push_back(static_cast<T>(std::stod(tok)));
+  while (is >> tok) {
+    const double v = std::stod(tok);  // std::invalid_argument / out_of_range on junk
+    if (std::is_integral<T>::value &&
+        !(v >= static_cast<double>(std::numeric_limits<T>::lowest()) &&
+          v <= static_cast<double>(std::numeric_limits<T>::max())))
+      throw std::runtime_error("model string: integer field out of range: " + tok);
+    out.push_back(static_cast<T>(v));
+  }
   return out;
+}
+
+[[noreturn]] void BadTree(const std::string& what) { throw std::runtime_error("malformed tree in model string: " + what); }
+
+// A required per-node / per-leaf array: present and at least `need` entries long.
+template <class T>
+std::vector<T> Field(std::map<std::string, std::string>& kv, const char* key, size_t need) {
+  auto it = kv.find(key);
+  if (it == kv.end()) BadTree(std::string("missing ") + key);
+  std::vector<T> v = ParseVec<T>(it->second);
+  if (v.size() < need)
+    BadTree(std::string(key) + " has " + std::to_string(v.size()) + " entries, expected " + std::to_string(need));
+  return v;
 }
 }  // namespace
 
+// Model strings can come from users (loadNativeModelFromString, LightGBMBooster(model_str)), so every
+// array length, child index and categorical boundary is checked and the node graph must be a tree
+// rooted at node 0 that reaches every node and leaf exactly once; anything else throws instead of
+// indexing out of bounds or recursing without end.
 Tree Tree::FromString(const std::string& block) {
   std::map<std::string, std::string> kv;
   std::istringstream is(block);
@@ -361,22 +387,31 @@ Tree Tree::FromString(const std::string& block) {
     if (eq == std::string::npos) continue;
     kv[line.substr(0, eq)] = line.substr(eq + 1);
   }
-  int nl = std::stoi(kv.at("num_leaves"));
+  if (!kv.count("num_leaves")) BadTree("missing num_leaves");
+  const int nl = std::stoi(kv.at("num_leaves"));
+  if (nl < 1 || nl > (1 << 24)) BadTree("num_leaves out of range: " + std::to_string(nl));
   Tree t(nl);
   t.num_leaves = nl;
   t.num_cat = kv.count("num_cat") ? std::stoi(kv["num_cat"]) : 0;
-  auto lv = ParseVec<double>(kv["leaf_value"]);
-  for (int i = 0; i < nl && i < static_cast<int>(lv.size()); ++i) t.leaf_value[i] = lv[i];
+  if (t.num_cat < 0 || t.num_cat > nl) BadTree("num_cat out of range");
+  const auto lv = Field<double>(kv, "leaf_value", static_cast<size_t>(nl));
+  for (int i = 0; i < nl; ++i) t.leaf_value[i] = lv[i];
   if (kv.count("leaf_weight")) { auto v = ParseVec<double>(kv["leaf_weight"]); for (int i = 0; i < nl && i < (int)v.size(); ++i) t.leaf_weight[i] = v[i]; }
   if (kv.count("leaf_count")) { auto v = ParseVec<double>(kv["leaf_count"]); for (int i = 0; i < nl && i < (int)v.size(); ++i) t.leaf_count[i] = static_cast<int64_t>(v[i]); }
   if (nl > 1) {
-    auto sf = ParseVec<int>(kv["split_feature"]);
-    auto sg = ParseVec<double>(kv["split_gain"]);
-    auto th = ParseVec<double>(kv["threshold"]);
-    auto dt = ParseVec<int>(kv["decision_type"]);
-    auto lc = ParseVec<int>(kv["left_child"]);
-    auto rc = ParseVec<int>(kv["right_child"]);
+    const size_t ni = static_cast<size_t>(nl - 1);
+    const auto sf = Field<int>(kv, "split_feature", ni);
+    const auto th = Field<double>(kv, "threshold", ni);
+    const auto dt = Field<int>(kv, "decision_type", ni);
+    const auto lc = Field<int>(kv, "left_child", ni);
+    const auto rc = Field<int>(kv, "right_child", ni);
+    const auto sg = kv.count("split_gain") ? ParseVec<double>(kv["split_gain"]) : std::vector<double>();
     for (int i = 0; i < nl - 1; ++i) {
+      if (sf[i] < 0) BadTree("negative split_feature");
+      if (dt[i] < 0 || dt[i] > 127) BadTree("decision_type out of range");
+      for (int c : {lc[i], rc[i]}) {
+        if (c >= 0 ? c >= nl - 1 : ~c >= nl) BadTree("child index out of range: " + std::to_string(c));
+      }
       t.split_feature[i] = sf[i];
       t.split_feature_inner[i] = sf[i];
       t.split_gain[i] = i < (int)sg.size() ? sg[i] : 0;
@@ -388,20 +423,47 @@ Tree Tree::FromString(const std::string& block) {
     if (kv.count("internal_value")) { auto v = ParseVec<double>(kv["internal_value"]); for (int i = 0; i < nl - 1 && i < (int)v.size(); ++i) t.internal_value[i] = v[i]; }
     if (kv.count("internal_weight")) { auto v = ParseVec<double>(kv["internal_weight"]); for (int i = 0; i < nl - 1 && i < (int)v.size(); ++i) t.internal_weight[i] = v[i]; }
     if (kv.count("internal_count")) { auto v = ParseVec<double>(kv["internal_count"]); for (int i = 0; i < nl - 1 && i < (int)v.size(); ++i) t.internal_count[i] = static_cast<int64_t>(v[i]); }
-    // parents & depths
-    std::function<void(int, int)> walk = [&](int node, int depth) {
+    // parents & depths: iterative walk; each node and leaf must be reached exactly once
+    std::vector<char> seen_node(nl - 1, 0), seen_leaf(nl, 0);
+    std::vector<std::pair<int, int>> stack{{0, 0}};
+    seen_node[0] = 1;
+    int reached_nodes = 1, reached_leaves = 0;
+    while (!stack.empty()) {
+      const auto [node, depth] = stack.back();
+      stack.pop_back();
       for (int c : {t.left_child[node], t.right_child[node]}) {
-        if (c < 0) { t.leaf_parent[~c] = node; t.leaf_depth[~c] = depth + 1; }
-        else walk(c, depth + 1);
+        if (c < 0) {
+          if (seen_leaf[~c]++) BadTree("leaf reached twice");
+          ++reached_leaves;
+          t.leaf_parent[~c] = node;
+          t.leaf_depth[~c] = depth + 1;
+        } else {
+          if (seen_node[c]++) BadTree("node reached twice (cycle or shared subtree)");
+          ++reached_nodes;
+          stack.push_back({c, depth + 1});
+        }
       }
-    };
-    walk(0, 0);
+    }
+    if (reached_nodes != nl - 1 || reached_leaves != nl) BadTree("nodes or leaves unreachable from the root");
   }
   if (t.num_cat > 0) {
-    t.cat_boundaries = ParseVec<int>(kv["cat_boundaries"]);
-    auto ct = ParseVec<double>(kv["cat_threshold"]);
+    t.cat_boundaries = Field<int>(kv, "cat_boundaries", static_cast<size_t>(t.num_cat) + 1);
+    auto ct = kv.count("cat_threshold") ? ParseVec<double>(kv["cat_threshold"]) : std::vector<double>();
     t.cat_threshold.clear();
-    for (double d : ct) t.cat_threshold.push_back(static_cast<uint32_t>(d));
+    for (double d : ct) {
+      if (!(d >= 0 && d <= 4294967295.0)) BadTree("cat_threshold word out of range");
+      t.cat_threshold.push_back(static_cast<uint32_t>(d));
+    }
+    if (t.cat_boundaries[0] != 0) BadTree("cat_boundaries must start at 0");
+    for (int c = 0; c < t.num_cat; ++c)
+      if (t.cat_boundaries[c + 1] < t.cat_boundaries[c]) BadTree("cat_boundaries not increasing");
+    if (t.cat_boundaries[t.num_cat] > static_cast<int>(t.cat_threshold.size())) BadTree("cat_boundaries beyond cat_threshold");
+  }
+  for (int i = 0; i < nl - 1; ++i) {
+    if (t.decision_type[i] & 1) {  // categorical: threshold is an index into cat_boundaries
+      const double ci = t.threshold[i];
+      if (!(ci >= 0 && ci < t.num_cat) || ci != std::floor(ci)) BadTree("categorical split without a category set");
+    }
   }
   t.shrinkage = kv.count("shrinkage") ? std::stod(kv["shrinkage"]) : 1.0;
   return t;

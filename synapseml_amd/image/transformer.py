@@ -26,7 +26,20 @@ from ..core.pipeline import Transformer
 from ..ops import native
 from .schema import make_image_row, row_to_array, to_array
 
-STAGE_NAME = "stageName"
+# The reference keys every stage map by "action" (ImageTransformerStage.stageNameKey,
+# ImageTransformer.scala:39); maps written by an older build of this package used
+# "stageName" and are still read.
+STAGE_NAME = "action"
+_LEGACY_STAGE_NAME = "stageName"
+
+
+def stage_action(stage: dict) -> str:
+    """The stage's name ("resize", "crop", ...) from a reference-style map."""
+    if STAGE_NAME in stage:
+        return stage[STAGE_NAME]
+    if _LEGACY_STAGE_NAME in stage:
+        return stage[_LEGACY_STAGE_NAME]
+    raise KeyError(f"image stage map has no {STAGE_NAME!r} key: {stage!r}")
 
 
 class _Stage:
@@ -118,7 +131,7 @@ def center_crop_rect(stage: dict, h: int, w: int) -> Tuple[int, int, int, int]:
 
 def apply_stage(stage: dict, a: np.ndarray) -> np.ndarray:
     lib = _img()
-    name = stage[STAGE_NAME]
+    name = stage_action(stage)
     if name == "resize":
         th, tw = resize_target(stage, a.shape[0], a.shape[1])
         out = lib.resize(a, th, tw)
@@ -248,12 +261,12 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         rs = None
         crop = None
         i = 0
-        if i < len(st) and st[i][STAGE_NAME] == "resize":
+        if i < len(st) and stage_action(st[i]) == "resize":
             if "size" in st[i] and st[i].get("keepAspectRatio", False):
                 return None
             rs = resize_target(st[i], 1, 1)
             i += 1
-        if i < len(st) and st[i][STAGE_NAME] in ("centercrop", "crop"):
+        if i < len(st) and stage_action(st[i]) in ("centercrop", "crop"):
             crop = st[i]
             i += 1
         if i != len(st):
@@ -264,7 +277,7 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         base_h, base_w = rs if rs is not None else next(iter(shapes))
         if crop is None:
             cy, cx, ch, cw = 0, 0, base_h, base_w
-        elif crop[STAGE_NAME] == "centercrop":
+        elif stage_action(crop) == "centercrop":
             cy, cx, ch, cw = center_crop_rect(crop, base_h, base_w)
         else:
             cy, cx, ch, cw = int(crop["y"]), int(crop["x"]), int(crop["height"]), int(crop["width"])

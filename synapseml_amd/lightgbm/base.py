@@ -217,18 +217,67 @@ class LightGBMBase(Estimator, LightGBMParams):
 
     # ------------------------------------------------------------- fit
     # ------------------------------------------------------------- checkpoints
-    def _ckpt_latest(self) -> Optional[dict]:
+    # Params that change where checkpoints go or how often, not what is trained.
+    _CKPT_EXCLUDE = ("checkpointDir", "checkpointInterval", "resumeFromCheckpoint", "delegate", "fobj",
+                     "referenceDataset", "modelString")
+
+    def _ckpt_fingerprint(self, df: DataFrame) -> str:
+        """Identity of one training job: training params (minus checkpoint bookkeeping and
+        non-JSON values), the row count, the feature width and a strided content sample of the
+        features and labels. A checkpoint is only resumed when its fingerprint matches."""
+        import hashlib
+
+        pm = {}
+        for name, v in sorted(self.extractParamMap().items()):
+            if name in self._CKPT_EXCLUDE or callable(v):
+                continue
+            try:
+                json.dumps(v)
+            except TypeError:
+                v = repr(type(v))
+            pm[name] = v
+        h = hashlib.sha256(json.dumps(pm, sort_keys=True, default=str).encode())
+        n = len(df)
+        h.update(str(n).encode())
+        idx = np.unique(np.linspace(0, max(0, n - 1), num=min(n, 64)).astype(np.int64)) if n else np.zeros(0, np.int64)
+        for col in (self.getFeaturesCol(), self.getLabelCol()):
+            if col not in df:
+                continue
+            vals = df[col]
+            try:
+                sample = as_matrix(vals[idx]) if getattr(vals, "dtype", None) == object else np.asarray(vals)[idx]
+                arr = np.ascontiguousarray(np.asarray(sample, dtype=np.float64))
+                h.update(str(arr.shape).encode())
+                h.update(arr.tobytes())
+            except Exception:  # sparse / exotic columns: the row count and params still pin the job
+                h.update(repr(type(vals)).encode())
+        if D.world_size() > 1:
+            # every rank holds a different partition: the job is the set of all partitions
+            parts = D.all_gather_object(h.hexdigest())
+            return hashlib.sha256("|".join(parts).encode()).hexdigest()
+        return h.hexdigest()
+
+    def _ckpt_latest(self, fingerprint: Optional[str] = None) -> Optional[dict]:
+        """The checkpoint to resume from, or None. Rank 0 decides (only it writes checkpoints) and
+        broadcasts the decision, so every rank takes the same path even when the checkpoint
+        directory is not shared between hosts."""
         d = self.getCheckpointDir()
         if not d or not self.getResumeFromCheckpoint():
             return None
-        p = os.path.join(d, "latest.json")
-        if not os.path.exists(p):
-            return None
-        with open(p) as f:
-            meta = json.load(f)
-        with open(os.path.join(d, meta["model"])) as f:
-            meta["model_str"] = f.read()
-        return meta
+        meta = None
+        if D.rank() == 0:
+            p = os.path.join(d, "latest.json")
+            if os.path.exists(p):
+                with open(p) as f:
+                    meta = json.load(f)
+                if fingerprint is not None and meta.get("fingerprint") != fingerprint:
+                    log.warning("checkpoint %s was written by a different job (params or data differ); "
+                                "starting fresh", p)
+                    meta = None
+                else:
+                    with open(os.path.join(d, meta["model"])) as f:
+                        meta["model_str"] = f.read()
+        return D.broadcast_object(meta, 0)
 
     def _ckpt_write(self, model_str: str, batch: int, iteration: int, complete: bool) -> None:
         d = self.getCheckpointDir()
@@ -240,7 +289,8 @@ class LightGBMBase(Estimator, LightGBMParams):
         with open(tmp, "w") as f:
             f.write(model_str)
         os.replace(tmp, os.path.join(d, name))
-        meta = {"model": name, "batch": batch, "iteration": iteration, "complete": complete}
+        meta = {"model": name, "batch": batch, "iteration": iteration, "complete": complete,
+                "fingerprint": getattr(self, "_ckpt_fp", None)}
         tmp = os.path.join(d, "latest.json.tmp")
         with open(tmp, "w") as f:
             json.dump(meta, f)
@@ -254,7 +304,8 @@ class LightGBMBase(Estimator, LightGBMParams):
         booster = None
         num_class = self._num_class(df)
         delegate = self.getDelegate()
-        ck = self._ckpt_latest()
+        self._ckpt_fp = self._ckpt_fingerprint(df) if self.getCheckpointDir() else None
+        ck = self._ckpt_latest(self._ckpt_fp)
         start_batch, self._resume_done = 0, 0
         if ck is not None:
             model_str = ck["model_str"]
@@ -361,11 +412,13 @@ class LightGBMBase(Estimator, LightGBMParams):
         if valid is not None:
             nb.add_valid(valid, "valid")
         m.mark("booster_init_ms", (time.perf_counter() - t0) * 1e3)
-        prior_iters = nb.current_iteration
+        # iterations from earlier batches / modelString; a mid-batch checkpoint's iterations of THIS batch
+        # are counted by _iterate (it starts at _resume_done), so they are not part of the base
+        base_iters = nb.current_iteration - getattr(self, "_resume_done", 0)
         best = self._iterate(nb, valid is not None, batch_index, m, n, num_class)
         if best is not None and best >= 0:
             # keep iterations up to and including the best one (BasePartitionTask.scala:450-457)
-            nb.truncate(prior_iters + best + 1)
+            nb.truncate(base_iters + best + 1)
         m.mark("total_ms", (time.perf_counter() - t_start) * 1e3)
         m["backend"] = nb.backend
         m["native_stats"] = nb.stats()

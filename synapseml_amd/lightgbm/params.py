@@ -84,8 +84,8 @@ class LightGBMLearnerParams(LightGBMDatasetParams):
     checkpointDir = Param("Directory for periodic training checkpoints (model text); fit resumes from the latest "
                           "one when resumeFromCheckpoint is set", None, T.toString)
     checkpointInterval = Param("Write a checkpoint every this many iterations (0 = off)", 0, T.toInt)
-    resumeFromCheckpoint = Param("Resume from the latest checkpoint in checkpointDir if one exists", True,
-                                 T.toBoolean)
+    resumeFromCheckpoint = Param("Resume from the latest checkpoint in checkpointDir if one exists and was written "
+                                 "by the same job (same params and data)", False, T.toBoolean)
     verbosity = Param("Verbosity where lt 0 is Fatal, eq 0 is Error, eq 1 is Info, gt 1 is Debug", -1, T.toInt)
     boostFromAverage = Param("Adjusts initial score to the mean of labels for faster convergence", True, T.toBoolean)
     boostingType = Param("Default gbdt = traditional Gradient Boosting Decision Tree. Options: gbdt, rf, dart, goss", "gbdt", T.toString)

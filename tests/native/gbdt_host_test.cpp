@@ -80,7 +80,75 @@ static void run(const std::string& params, bool csr) {
   std::printf("ok  %-70s csr=%d trees=%zu\n", params.c_str(), csr ? 1 : 0, b.trees().size());
 }
 
+// Truncated / corrupted model strings must be rejected with an exception (never read out of bounds or
+// recurse without end): each mutation below breaks one invariant of a valid two-tree model.
+static void malformed_models() {
+  const int n = 500, F = 3;
+  std::mt19937 rng(3);
+  std::normal_distribution<double> nd;
+  std::vector<double> X(static_cast<size_t>(n) * F);
+  std::vector<float> y(n);
+  for (int i = 0; i < n; ++i) {
+    for (int f = 0; f < F; ++f) X[i * F + f] = nd(rng);
+    y[i] = X[i * F] > 0 ? 1.f : 0.f;
+  }
+  const std::string params = "objective=binary num_leaves=4 min_data_in_leaf=5 device_type=cpu";
+  Config cfg = Config::Parse(params);
+  auto ref = DatasetReference::FromSample(X.data(), n, F, n, cfg, {"a", "b", "c"});
+  auto ds = std::make_shared<Dataset>();
+  ds->Init(ref, n);
+  ds->PushDense(X.data(), n, F, 0);
+  ds->label = y;
+  Booster b(ds, params);
+  b.TrainOneIter();
+  b.TrainOneIter();
+  const std::string good = b.SaveModelToString(0, -1, 0);
+  auto replace_line = [&](const std::string& key, const std::string& val) {
+    std::string m = good;
+    const size_t p = m.find("\n" + key + "=");
+    if (p == std::string::npos) return std::string();
+    const size_t e = m.find('\n', p + 1);
+    return m.substr(0, p + 1) + key + "=" + val + m.substr(e);
+  };
+  const std::vector<std::pair<std::string, std::string>> bad = {
+      {"left_child", "1 -2"},           // truncated array
+      {"left_child", "5 -1 -3"},        // child index out of range
+      {"left_child", "0 -1 -3"},        // cycle back to the root
+      {"right_child", "-2 -2 -4"},      // one leaf reached twice, another never
+      {"split_feature", "0 99 1"},      // feature beyond max_feature_idx
+      {"leaf_value", "0.1"},            // too few leaf values
+      {"num_leaves", "-3"},             // negative size
+      {"decision_type", "1 1 1"},       // categorical split with no category sets
+      {"threshold", "abc def ghi"},     // not numbers
+  };
+  int rejected = 0;
+  for (const auto& kv : bad) {
+    const std::string m = replace_line(kv.first, kv.second);
+    if (m.empty()) { std::fprintf(stderr, "no %s line to mutate\n", kv.first.c_str()); ++failures; continue; }
+    try {
+      auto bb = Booster::FromModelString(m);
+      std::vector<double> out(n);
+      bb->Predict(X.data(), n, F, 0, 0, -1, out.data());
+      std::fprintf(stderr, "malformed model accepted: %s=%s\n", kv.first.c_str(), kv.second.c_str());
+      ++failures;
+    } catch (const std::exception&) {
+      ++rejected;
+    }
+  }
+  // a truncated string (cut mid-tree) is rejected too
+  try {
+    auto bb = Booster::FromModelString(good.substr(0, good.find("leaf_value")));
+    (void)bb;
+    std::fprintf(stderr, "truncated model accepted\n");
+    ++failures;
+  } catch (const std::exception&) {
+    ++rejected;
+  }
+  std::printf("ok  malformed model strings rejected: %d\n", rejected);
+}
+
 int main() {
+  malformed_models();
   run("objective=binary num_leaves=15 device_type=cpu", false);
   run("objective=binary num_leaves=15 device_type=cpu", true);
   run("objective=regression num_leaves=31 lambda_l2=1 device_type=cpu", false);

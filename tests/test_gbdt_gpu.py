@@ -367,3 +367,42 @@ def test_gpu_training_metrics_on_device():
     sr = r.train_scores()
     np.testing.assert_allclose(er["rmse"], np.sqrt(np.mean((sr - yr) ** 2)), rtol=1e-9)
     np.testing.assert_allclose(er["l1"], np.mean(np.abs(sr - yr)), rtol=1e-9)
+
+
+def test_gpu_histogram_quantisation_skewed_hessians():
+    """Near-separable binary data driven to confident predictions: most rows end with hessians many orders
+    of magnitude below the largest one. The HIP histogram quantises (g, h) to 32-bit fixed point per block
+    (scale from the tree's max |g| / max h); the tree structure, the per-node hessian sums and the model's
+    loss must still track the fp64 host oracle."""
+    rng = np.random.default_rng(17)
+    n, f = 120000, 8
+    X = rng.standard_normal((n, f))
+    y = (X[:, 0] + 0.3 * X[:, 1] + 0.02 * rng.standard_normal(n) > 0).astype(np.float32)
+    base = "objective=binary num_leaves=15 learning_rate=0.5 min_sum_hessian_in_leaf=1e-3"
+    iters = 60  # by then ~45% of the rows have h < 1e-6 against max h ~0.25
+    bc = _train(X, y, base + " device_type=cpu", iters)
+    bg = _train(X, y, base + " device_type=gpu", iters)
+    assert bg.backend == "hip"
+    # the gradients of the last iteration really are skewed (h spans many decades)
+    gc, hc = bc.gradients()
+    hc = np.asarray(hc, dtype=np.float64)
+    assert hc.max() / max(np.median(hc), 1e-300) > 1e4
+    mc, mg = bc.save_model_string(), bg.save_model_string()
+    blocks = lambda s: s.split("end of trees")[0].split("Tree=")[1:]
+    tc, tg = blocks(mc), blocks(mg)
+    assert len(tc) == len(tg) == iters
+    field = lambda t, k: np.array([l for l in t.splitlines() if l.startswith(k + "=")][0].split("=")[1].split(), float)
+    same_structure = 0
+    for a, b in zip(tc, tg):
+        if "split_feature" not in a or "split_feature" not in b:
+            continue
+        if np.array_equal(field(a, "split_feature"), field(b, "split_feature")) and \
+                np.array_equal(field(a, "threshold"), field(b, "threshold")):
+            same_structure += 1
+            # per-node hessian sums agree to the quantisation error
+            np.testing.assert_allclose(field(a, "internal_weight"), field(b, "internal_weight"), rtol=2e-3, atol=1e-9)
+    assert same_structure >= iters - 6, same_structure
+    pc = bc.predict(X, 0, 0, -1)[:, 0]
+    pg = bg.predict(X, 0, 0, -1)[:, 0]
+    ll = lambda p: float(-np.mean(y * np.log(np.clip(p, 1e-15, 1)) + (1 - y) * np.log(np.clip(1 - p, 1e-15, 1))))
+    assert abs(ll(pc) - ll(pg)) <= 0.02 * ll(pc) + 1e-6, (ll(pc), ll(pg))

@@ -191,3 +191,27 @@ def test_named_stage_maps_match_builder():
     t = ImageTransformer().resize(height=8, width=6).centerCrop(4, 4).flip(1)
     assert t.getStages() == [ResizeImage.make(height=8, width=6), CenterCropImage.make(height=4, width=4),
                              Flip.make(flipCode=1)]
+
+
+def test_reference_action_keyed_stage_list():
+    """Stage maps keyed by "action" (ImageTransformerStage.stageNameKey, ImageTransformer.scala:39) as the
+    reference's builder methods emit them; legacy "stageName" maps are still accepted."""
+    from synapseml_amd.image.transformer import ResizeImage, stage_action
+
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, size=(40, 30, 3), dtype=np.uint8)
+    df = _df(img)
+    ref_style = [{"action": "resize", "height": 20, "width": 16},
+                 {"action": "centercrop", "height": 10, "width": 8},
+                 {"action": "flip", "flipCode": 1}]
+    out = ImageTransformer(outputCol="out", stages=ref_style).transform(df)
+    built = ImageTransformer(outputCol="out").resize(20, 16).centerCrop(10, 8).flip(1)
+    assert built.getStages() == ref_style
+    np.testing.assert_array_equal(row_to_array(out["out"][0]), row_to_array(built.transform(df)["out"][0]))
+    legacy = [{"stageName": s["action"], **{k: v for k, v in s.items() if k != "action"}} for s in ref_style]
+    out2 = ImageTransformer(outputCol="out", stages=legacy).transform(df)
+    np.testing.assert_array_equal(row_to_array(out["out"][0]), row_to_array(out2["out"][0]))
+    assert ResizeImage.make(height=1, width=2)["action"] == "resize"
+    assert stage_action({"action": "blur"}) == "blur"
+    with pytest.raises(KeyError):
+        stage_action({"height": 3})

@@ -349,3 +349,74 @@ def test_feature_fraction_bynode_changes_trees_deterministically():
     assert a.getNativeModel() == b.getNativeModel()
     strip = lambda s: s.split("parameters:")[0]
     assert strip(a.getNativeModel()) != strip(c.getNativeModel())
+
+
+def test_resume_mid_batch_with_early_stopping_truncates_at_best(tmp_path):
+    """A fit that crashes after a mid-batch checkpoint and resumes with early stopping must cut the model
+    at the same best iteration as an uninterrupted run (the resumed iterations belong to this batch)."""
+    rng = np.random.default_rng(21)
+    n = 4000
+    X = rng.standard_normal((n, 8))
+    y = (X[:, 0] + 0.7 * X[:, 1] * X[:, 2] + 0.8 * rng.standard_normal(n) > 0).astype(float)
+    df = DataFrame({"features": X, "label": y, "isVal": rng.random(n) < 0.3})
+
+    class Crash(LightGBMDelegate):
+        def afterTrainIteration(self, batchIndex, partitionId, curIters, log, trainParams, booster, hasValid,
+                                finished, trainRes, validRes):
+            if curIters == 12:
+                raise RuntimeError("simulated executor loss")
+
+    base = dict(numIterations=300, numLeaves=31, learningRate=0.3, earlyStoppingRound=4,
+                validationIndicatorCol="isVal", metric="binary_logloss", deviceType="cpu")
+    ck = str(tmp_path / "ck")
+    with pytest.raises(RuntimeError, match="simulated"):
+        LightGBMClassifier(**base, checkpointDir=ck, checkpointInterval=10, resumeFromCheckpoint=True,
+                           delegate=Crash()).fit(df)
+    resumed = LightGBMClassifier(**base, checkpointDir=ck, checkpointInterval=10, resumeFromCheckpoint=True).fit(df)
+    full = LightGBMClassifier(**base).fit(df)
+    nf = full.getModel().native.num_total_model
+    assert nf < 300, "early stopping did not trigger; the test needs a stopping point after the checkpoint"
+    assert resumed.getModel().native.num_total_model == nf
+    np.testing.assert_allclose(resumed.transform(df)["probability"], full.transform(df)["probability"],
+                               rtol=1e-9, atol=1e-12)
+
+
+def test_checkpoint_of_another_job_is_not_resumed(tmp_path):
+    """latest.json carries a fingerprint of params + data: a fit with different data (or params) and the same
+    checkpointDir starts fresh instead of returning or continuing the old model."""
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((2000, 5))
+    y = (X[:, 0] > 0).astype(float)
+    ck = str(tmp_path / "ck")
+    kw = dict(numIterations=10, numLeaves=7, deviceType="cpu", checkpointDir=ck, checkpointInterval=5,
+              resumeFromCheckpoint=True)
+    first = LightGBMClassifier(**kw).fit(DataFrame({"features": X, "label": y}))
+    X2 = rng.standard_normal((2000, 5))
+    y2 = (X2[:, 1] > 0).astype(float)
+    df2 = DataFrame({"features": X2, "label": y2})
+    second = LightGBMClassifier(**kw).fit(df2)
+    fresh = LightGBMClassifier(numIterations=10, numLeaves=7, deviceType="cpu").fit(df2)
+    assert second.getNativeModel().split("parameters:")[0] != first.getNativeModel().split("parameters:")[0]
+    np.testing.assert_allclose(second.transform(df2)["probability"], fresh.transform(df2)["probability"],
+                               rtol=1e-9, atol=1e-12)
+    # different params, same data: also a fresh start
+    third = LightGBMClassifier(**dict(kw, numLeaves=5)).fit(df2)
+    assert third.getModel().native.num_total_model == 10
+    # resumeFromCheckpoint defaults to off: an existing complete checkpoint is ignored
+    assert LightGBMClassifier().getResumeFromCheckpoint() is False
+
+
+@pytest.mark.parametrize("mutate", [
+    lambda s: s.replace("left_child=", "left_child=77 ", 1),
+    lambda s: s[: s.index("end of trees")],
+    lambda s: s.replace("num_leaves=", "num_leaves=9", 1),
+    lambda s: s.replace("split_feature=", "split_feature=4000 ", 1),
+])
+def test_malformed_native_model_string_raises(mutate):
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((1000, 4))
+    df = DataFrame({"features": X, "label": (X[:, 0] > 0).astype(float)})
+    good = LightGBMClassifier(numIterations=3, numLeaves=5, deviceType="cpu").fit(df).getNativeModel()
+    LightGBMClassificationModel.loadNativeModelFromString(good)  # the untouched string loads
+    with pytest.raises((RuntimeError, ValueError, IndexError)):
+        LightGBMClassificationModel.loadNativeModelFromString(mutate(good)).transform(df)
