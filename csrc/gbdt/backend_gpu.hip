@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -952,8 +953,11 @@ __device__ __forceinline__ bool CandBetter(const Cand& a, const Cand& b) {
   return a.dl < b.dl;
 }
 
-__device__ void CategoricalSearch(const double* hg, const double* hh, int nb, int fi, double G, double H,
-                                  int64_t cnt, const SplitParams& sp, const MonoCtx* mc, SplitResult* best, int* idx) {
+// left: caller-provided buffer of 256 ints for the left-bin list (LDS in split_kernel, so the search
+// needs no scratch)
+__device__ void CategoricalSearchBuf(const double* hg, const double* hh, int nb, int fi, double G, double H,
+                                     int64_t cnt, const SplitParams& sp, const MonoCtx* mc, SplitResult* best, int* idx,
+                                     int* left) {
   // serial port of the host search (one thread): bins are <= 256
   const double cnt_factor = cnt / fmax(H, kEpsilon);
   const int other = nb - 1;
@@ -996,7 +1000,6 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
     idx[j + 1] = v;
   }
   const int maxk = min(sp.max_cat_threshold, (m + 1) / 2);
-  int left[256];
   for (int dir = 0; dir < 2; ++dir) {
     double gl = 0, hl = 0;
     for (int k = 0; k < m && k < maxk; ++k) {
@@ -1006,6 +1009,12 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
       try_set(k + 1, left, gl, hl);
     }
   }
+}
+
+__device__ void CategoricalSearch(const double* hg, const double* hh, int nb, int fi, double G, double H,
+                                  int64_t cnt, const SplitParams& sp, const MonoCtx* mc, SplitResult* best, int* idx) {
+  int left[256];
+  CategoricalSearchBuf(hg, hh, nb, fi, G, H, cnt, sp, mc, best, idx, left);
 }
 
 // Block (f, child): 256 threads, thread = bin.
@@ -1033,7 +1042,9 @@ __device__ void FindSplitBlock(
   __shared__ double sg_[256], shh_[256];
   __shared__ double wtot_g[4], wtot_h[4];
   __shared__ Cand wbest[4];
-  __shared__ int idxbuf[256];
+  __shared__ int idxbuf[256], leftbuf[256];
+  __shared__ SplitResult s_cat_best;
+  __shared__ MonoCtx s_mc;  // by pointer into EvalSplit / the categorical search: LDS, not scratch
   sg_[tid] = mine.x;
   shh_[tid] = mine.y;
   const int nb = fm.num_bin[f];
@@ -1072,14 +1083,17 @@ __device__ void FindSplitBlock(
     return;
   }
   // monotone context of this (leaf, feature); categorical splits are clamped but carry no direction
-  const MonoCtx mc{Lf.lo, Lf.hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
-  const MonoCtx* mcp = sp.has_mono ? &mc : nullptr;
+  if (tid == 0) s_mc = MonoCtx{Lf.lo, Lf.hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
+  __syncthreads();
+  const MonoCtx* mcp = sp.has_mono ? &s_mc : nullptr;
   if (fm.is_cat[f]) {
     if (tid == 0) {
-      SplitResult best;
+      SplitResult& best = s_cat_best;
       best.feature = -1; best.gain = -INFINITY;
-      CategoricalSearch(sg_, shh_, nb, f, G, H, cnt, sp, mcp, &best, idxbuf);
-      *out = best;
+      CategoricalSearchBuf(sg_, shh_, nb, f, G, H, cnt, sp, mcp, &best, idxbuf, leftbuf);
+      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&best);
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
+      for (int w = 0; w < static_cast<int>(sizeof(SplitResult) / 8); ++w) dst[w] = src[w];
     }
     return;
   }
@@ -1147,7 +1161,7 @@ __device__ void FindSplitBlock(
       r.left_cnt = EstimateCount(hl, cnt_factor); r.right_cnt = cnt - r.left_cnt;
       double g2;
       (void)EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &g2, &r.left_out, &r.right_out);
-      if (mcp && mc.mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(Lf.depth, sp.monotone_penalty);
+      if (mcp && mcp->mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(Lf.depth, sp.monotone_penalty);
       for (int w = 0; w < 8; ++w) r.cat_bits[w] = 0;
     }
     *out = r;
@@ -1329,15 +1343,407 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
   ChooseBlock(st, leaves, lbest, lgain, fbest, F, t, count_slot, mono, has_mono);
 }
 
+// ---------------------------------------------------------------- K4 + K5 + choose, one launch
+// split_kernel replaces hist_reduce -> find_split -> choose (three launches,
+// ~21 us per split at the ~6 us floor each small kernel has on this part) by
+// one launch of F blocks x 1024 threads:
+//   1. (kFromSlab) the block of feature f reduces that feature's 256 bins of
+//      the per-block integer slabs exactly (4 thread groups stride the slabs,
+//      int64 partials added in LDS) - or reads the allreduced histogram when
+//      data-parallel ranks inserted an RCCL / P2P allreduce in between;
+//   2. threads 0-255 search the smaller child (or the root), threads 256-511
+//      the larger child (= parent - smaller), as find_split_kernel does;
+//   3. each block publishes its two SplitResults with agent-scope (sc1, L2
+//      write-through) stores, drains them (s_waitcnt vmcnt(0)), joins a
+//      workgroup barrier, and one lane adds to an arrival counter; the block
+//      whose add returns F-1 is the last one and runs the choose step, reading
+//      the records with sc1 loads (the hand-off recipe of the MI355X guide:
+//      every store and load of the handed-off bytes sc1, one agent-scope add
+//      per storing workgroup after its drain + barrier). It resets the counter
+//      for the next launch (kernel boundaries order that reset).
+// No part of the result depends on which block arrives last.
+static_assert(offsetof(SplitResult, threshold) == offsetof(SplitResult, feature) + 4 &&
+                  offsetof(SplitResult, feature) % 8 == 0,
+              "ChooseFused reads {feature, threshold} as one 8-byte granule");
+constexpr int kSplitThreads = 1024;
+constexpr int kSplitRedGroups = kSplitThreads / kBinsPerFeature;  // 4
+
+__device__ __forceinline__ void StoreAgent8(void* p, unsigned long long v) {
+  __hip_atomic_store(static_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long LoadAgent8(const void* p) {
+  return __hip_atomic_load(static_cast<unsigned long long*>(const_cast<void*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// Word copies of 8-byte-granule records (no local struct whose address is taken:
+// that would put the record in scratch).
+template <class T>
+__device__ __forceinline__ void PublishAgent(T* dst, const T* src) {  // plain (LDS) -> sc1 stores
+  static_assert(sizeof(T) % 8 == 0 && alignof(T) >= 8, "8-byte granules");
+  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(src);
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
+#pragma unroll
+  for (int i = 0; i < static_cast<int>(sizeof(T) / 8); ++i) StoreAgent8(d + i, s[i]);
+}
+template <class T>
+__device__ __forceinline__ void FetchAgent(T* dst, const T* src) {  // sc1 loads -> plain stores
+  static_assert(sizeof(T) % 8 == 0 && alignof(T) >= 8, "8-byte granules");
+  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(src);
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
+#pragma unroll
+  for (int i = 0; i < static_cast<int>(sizeof(T) / 8); ++i) d[i] = LoadAgent8(s + i);
+}
+__device__ __forceinline__ double LoadAgentD(const double* p) {
+  return __longlong_as_double(static_cast<long long>(LoadAgent8(p)));
+}
+__device__ __forceinline__ int64_t LoadAgentI64(const int64_t* p) { return static_cast<int64_t>(LoadAgent8(p)); }
+
+// The choose step of ChooseBlock for a 1024-thread block whose per-feature
+// records (and, at the root, leaves[0]'s totals) were published in this launch:
+// those are read with sc1 loads; everything else was written by earlier launches.
+__device__ void ChooseFused(DState* __restrict__ st, DLeaf* __restrict__ leaves, SplitResult* __restrict__ lbest,
+                            double* __restrict__ lgain, const SplitResult* __restrict__ fbest, int F, const DTree& t,
+                            int64_t small_cnt, const int8_t* __restrict__ mono, int has_mono) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ int sh_best_f[2];
+  __shared__ KeyG wk[4];
+  const bool root = st->phase == 0;
+  const int nchild = root ? 1 : 2;
+  const int small_leaf = st->small_leaf, large_leaf = st->large_leaf;
+  if (wid < nchild) {
+    KeyG k{-INFINITY, 1 << 30, 1 << 30};
+    for (int f = lane; f < F; f += 64) {
+      const SplitResult* r = fbest + wid * F + f;
+      const unsigned long long ft = LoadAgent8(&r->feature);  // {feature, threshold}: one 8-byte granule
+      const int feat = static_cast<int>(static_cast<uint32_t>(ft));
+      if (feat < 0) continue;
+      const uint32_t thr = static_cast<uint32_t>(ft >> 32);
+      const double gain = __longlong_as_double(static_cast<long long>(LoadAgent8(&r->gain)));
+      KeyG c{gain, feat, static_cast<int>(thr)};
+      if (KeyBetter(c, k)) { k = c; k.b = (static_cast<int>(thr) & 0xFFFF) | (f << 16); }
+    }
+    k = WaveArgmax(k);
+    if (lane == 0) sh_best_f[wid] = k.gain == -INFINITY ? -1 : (k.b >> 16);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (root) {
+      const int bi = sh_best_f[0];
+      if (bi >= 0) { FetchAgent(lbest, fbest + bi); lgain[0] = LoadAgentD(&fbest[bi].gain); }
+      else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; lgain[0] = -INFINITY; }
+      t.lval[0] = 0.0;
+      t.lcount[0] = LoadAgentI64(&leaves[0].gcount);  // totals published by feature 0's block
+      t.lweight[0] = LoadAgentD(&leaves[0].sum_h);
+      t.lparent[0] = -1;
+      t.ldepth[0] = 0;
+    } else {
+      const int64_t parent_cnt = leaves[large_leaf].gcount;  // stored by the previous choose
+      const int ob = st->pbuf == 0 ? 1 : 0;
+      DLeaf& Lc = leaves[st->split_leaf];
+      DLeaf& Rc = leaves[st->new_leaf];
+      const int lt = PTotal(st);
+      Lc.begin = st->pbegin; Lc.count = lt; Lc.buf = ob;
+      Rc.begin = st->pbegin + lt; Rc.count = st->pcount - lt; Rc.buf = ob;
+      leaves[small_leaf].gcount = small_cnt;
+      leaves[large_leaf].gcount = parent_cnt - small_cnt;
+      t.lcount[small_leaf] = small_cnt;
+      t.lcount[large_leaf] = parent_cnt - small_cnt;
+      for (int c = 0; c < 2; ++c) {
+        const int leaf = c == 0 ? small_leaf : large_leaf;
+        const int bi = sh_best_f[c];
+        if (bi >= 0) { FetchAgent(lbest + leaf, fbest + c * F + bi); lgain[leaf] = LoadAgentD(&fbest[c * F + bi].gain); }
+        else { lbest[leaf].feature = -1; lbest[leaf].gain = -INFINITY; lgain[leaf] = -INFINITY; }
+      }
+    }
+  }
+  __syncthreads();
+  const int nl = st->num_leaves;
+  if (nl >= st->max_leaves) {
+    if (tid == 0) st->done = 1;
+    return;
+  }
+  KeyG k{-INFINITY, 1 << 30, 0};
+  if (tid < 256)
+    for (int i = tid; i < nl; i += 256) {
+      const double gi = lgain[i];
+      KeyG c{gi, i, 0};
+      if (gi > -INFINITY && KeyBetter(c, k)) k = c;
+    }
+  k = WaveArgmax(k);
+  if (lane == 0 && wid < 4) wk[wid] = k;
+  __syncthreads();
+  if (tid != 0) return;
+  KeyG best = wk[0];
+  for (int w = 1; w < 4; ++w) if (KeyBetter(wk[w], best)) best = wk[w];
+  const int bl = best.gain == -INFINITY ? -1 : best.a;
+  if (bl < 0 || !(best.gain > 0.0)) { st->done = 1; return; }
+  const SplitResult sr = lbest[bl];
+  const int node = nl - 1;
+  const int parent = t.lparent[bl];
+  if (parent >= 0) {
+    if (t.left[parent] == ~bl) t.left[parent] = node; else t.right[parent] = node;
+  }
+  t.feat[node] = sr.feature;
+  t.thr[node] = sr.threshold;
+  t.dleft[node] = sr.default_left;
+  t.is_cat[node] = sr.is_cat;
+  for (int w = 0; w < 8; ++w) t.cat_bits[node * 8 + w] = sr.cat_bits[w];
+  t.left[node] = ~bl;
+  t.right[node] = ~nl;
+  t.gain[node] = sr.gain;
+  t.ival[node] = t.lval[bl];
+  t.iweight[node] = sr.left_h + sr.right_h;
+  DLeaf P = leaves[bl];
+  if (root) {  // bl == 0; its totals were published in this launch
+    P.gcount = LoadAgentI64(&leaves[0].gcount);
+    P.sum_g = LoadAgentD(&leaves[0].sum_g);
+    P.sum_h = LoadAgentD(&leaves[0].sum_h);
+  }
+  t.icount[node] = P.gcount;
+  t.lparent[bl] = node; t.lparent[nl] = node;
+  t.lval[bl] = sr.left_out; t.lval[nl] = sr.right_out;
+  t.lweight[bl] = sr.left_h; t.lweight[nl] = sr.right_h;
+  t.lcount[bl] = sr.left_cnt; t.lcount[nl] = sr.right_cnt;
+  const int depth = t.ldepth[bl] + 1;
+  t.ldepth[bl] = depth; t.ldepth[nl] = depth;
+  DLeaf Lc = P, Rc = P;
+  Lc.depth = depth; Rc.depth = depth;
+  Lc.sum_g = sr.left_g; Lc.sum_h = sr.left_h;
+  Rc.sum_g = sr.right_g; Rc.sum_h = sr.right_h;
+  const int mdir = (has_mono && !sr.is_cat) ? static_cast<int>(mono[sr.feature]) : 0;
+  if (mdir != 0) {
+    const double mid = (sr.left_out + sr.right_out) / 2.0;
+    if (mdir < 0) { Lc.lo = fmax(Lc.lo, mid); Rc.hi = fmin(Rc.hi, mid); }
+    else { Lc.hi = fmin(Lc.hi, mid); Rc.lo = fmax(Rc.lo, mid); }
+  }
+  const bool left_small = sr.left_cnt <= sr.right_cnt;
+  st->parent_slot = P.slot;
+  Lc.slot = 2 * node + 1;
+  Rc.slot = 2 * node + 2;
+  if (left_small) { Rc.gcount = P.gcount; } else { Lc.gcount = P.gcount; }
+  leaves[bl] = Lc;
+  leaves[nl] = Rc;
+  lgain[bl] = -INFINITY;
+  lgain[nl] = -INFINITY;
+  st->pbegin = P.begin; st->pcount = P.count; st->pbuf = P.buf;
+  st->cursor = 0ull;
+  st->split_leaf = bl;
+  st->new_leaf = nl;
+  st->small_leaf = left_small ? bl : nl;
+  st->large_leaf = left_small ? nl : bl;
+  st->num_leaves = nl + 1;
+  st->phase = 1;
+}
+
+template <bool kFromSlab>
+__global__ __launch_bounds__(kSplitThreads) void split_kernel(
+    DState* __restrict__ st, DLeaf* __restrict__ leaves, const int2* __restrict__ slab,
+    const double2* __restrict__ part, int E, const float* __restrict__ ghmax, double2* __restrict__ hist_pool,
+    FeatMeta fm, SplitParams sp, SplitResult* __restrict__ fbest, int F, SplitResult* __restrict__ lbest,
+    double* __restrict__ lgain, DTree t, const int8_t* __restrict__ mono, int has_mono,
+    unsigned int* __restrict__ arrive) {
+  if (st->done) return;
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int c = tid >> 8;          // 0: smaller child / root, 1: larger child, 2-3: reduction helpers
+  const int ltid = tid & 255;      // bin
+  const int cw = (tid >> 6) & 3;   // wave within the child's 256 threads
+  const int cc = c & 1;            // LDS row (helpers alias rows 0/1 but never write them)
+  const bool root = st->phase == 0;
+  const bool act = c == 0 || (c == 1 && !root);
+  const int e = f * kBinsPerFeature + ltid;
+  __shared__ long long red_g[kSplitRedGroups][kBinsPerFeature], red_h[kSplitRedGroups][kBinsPerFeature];
+  __shared__ double2 s_small[kBinsPerFeature];
+  __shared__ double s_g[2][kBinsPerFeature], s_h[2][kBinsPerFeature];
+  __shared__ double s_pg[2][kBinsPerFeature], s_ph[2][kBinsPerFeature];
+  __shared__ double s_tg[2][4], s_th[2][4], s_sg[2][4], s_sh[2][4];
+  __shared__ Cand s_wbest[2][4];
+  __shared__ int s_idx[2][kBinsPerFeature], s_left[2][kBinsPerFeature];
+  __shared__ int s_last;
+  __shared__ SplitResult s_res[2];
+  __shared__ MonoCtx s_mc[2];
+  // ---- 1. the smaller child's (or the root's) histogram of feature f
+  int64_t gcnt;
+  if (kFromSlab) {
+    const int count = HistSeg(st, leaves).count;
+    const int nb_active = HistBlocks(count);
+    long long sg = 0, sh = 0;
+#pragma unroll 8
+    for (int b = c; b < nb_active; b += kSplitRedGroups) {
+      const int2 v = slab[static_cast<size_t>(b) * E + e];
+      sg += v.x;
+      sh += static_cast<uint32_t>(v.y);
+    }
+    red_g[c][ltid] = sg;
+    red_h[c][ltid] = sh;
+    __syncthreads();
+    if (tid < kBinsPerFeature) {
+      long long tg = 0, th = 0;
+#pragma unroll
+      for (int k = 0; k < kSplitRedGroups; ++k) { tg += red_g[k][tid]; th += red_h[k][tid]; }
+      const HScale s = HistScale(count, ghmax);
+      s_small[tid] = make_double2(static_cast<double>(tg) / static_cast<double>(s.g),
+                                  static_cast<double>(th) / static_cast<double>(s.h));
+    }
+    gcnt = count;
+  } else {
+    if (tid < kBinsPerFeature) s_small[tid] = part[e];
+    gcnt = static_cast<int64_t>(part[E].x);
+  }
+  __syncthreads();
+  // ---- 2. split search, threads [0,256) child 0, [256,512) child 1
+  const int leaf_id = root ? 0 : (c == 0 ? st->small_leaf : st->large_leaf);
+  double2 mine = make_double2(0.0, 0.0);
+  DLeaf Lf{};
+  if (act) {
+    const double2 sm = s_small[ltid];
+    if (c == 0) mine = sm;
+    else {
+      const double2 par = hist_pool[static_cast<size_t>(st->parent_slot) * E + e];
+      mine = make_double2(par.x - sm.x, par.y - sm.y);
+    }
+    Lf = leaves[leaf_id];
+    hist_pool[static_cast<size_t>(Lf.slot) * E + e] = mine;
+    s_g[cc][ltid] = mine.x;
+    s_h[cc][ltid] = mine.y;
+    // monotone context of this (leaf, feature) in LDS: the categorical search takes it by pointer
+    if (ltid == 0) s_mc[cc] = MonoCtx{Lf.lo, Lf.hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
+  }
+  const int nb = fm.num_bin[f];
+  const int mt = fm.missing[f];
+  const int dbin = fm.default_bin[f];
+  {
+    double tg = (act && ltid < nb) ? mine.x : 0.0, th = (act && ltid < nb) ? mine.y : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) { tg += __shfl_xor(tg, off, 64); th += __shfl_xor(th, off, 64); }
+    if (act && lane == 0) { s_tg[cc][cw] = tg; s_th[cc][cw] = th; }
+  }
+  __syncthreads();
+  double G = 0.0, H = 0.0;
+  int64_t cnt = 0;
+  if (act) {
+    G = s_tg[cc][0] + s_tg[cc][1] + s_tg[cc][2] + s_tg[cc][3];
+    H = s_th[cc][0] + s_th[cc][1] + s_th[cc][2] + s_th[cc][3];
+    if (root) {
+      cnt = gcnt;
+      if (f == 0 && ltid == 0) {  // published for the chooser (sc1), like every other hand-off here
+        StoreAgent8(&leaves[0].sum_g, static_cast<unsigned long long>(__double_as_longlong(G)));
+        StoreAgent8(&leaves[0].sum_h, static_cast<unsigned long long>(__double_as_longlong(H)));
+        StoreAgent8(&leaves[0].gcount, static_cast<unsigned long long>(cnt));
+      }
+    } else {
+      cnt = c == 0 ? gcnt : (Lf.gcount - gcnt);  // Lf.gcount of the large child holds the parent count
+      G = Lf.sum_g; H = Lf.sum_h;
+    }
+  }
+  const bool eligible = act && fm.mask[f] && nb > 1 && cnt >= 2 * static_cast<int64_t>(sp.min_data_in_leaf) &&
+                        (sp.max_depth <= 0 || Lf.depth < sp.max_depth) &&
+                        (sp.bynode_k <= 0 ||
+                         NodeFeatureSelected(sp.bynode_seed, sp.tree_seq, Lf.slot, f, fm.mask, F, sp.bynode_k));
+  const bool is_cat = fm.is_cat[f] != 0;
+  const bool numer = eligible && !is_cat;
+  const MonoCtx* mcp = sp.has_mono ? &s_mc[cc] : nullptr;
+  const int nan_bin = mt == kMissingNaN ? nb - 1 : -1;
+  const int zero_bin = mt == kMissingZero ? dbin : -1;
+  const int last = nan_bin >= 0 ? nb - 2 : nb - 1;
+  double vg = (numer && ltid < nb && ltid != zero_bin && ltid != nan_bin) ? mine.x : 0.0;
+  double vh = (numer && ltid < nb && ltid != zero_bin && ltid != nan_bin) ? mine.y : 0.0;
+  vg = wave_incl_scan(vg, lane);
+  vh = wave_incl_scan(vh, lane);
+  if (act && lane == 63) { s_sg[cc][cw] = vg; s_sh[cc][cw] = vh; }
+  __syncthreads();
+  Cand best{-INFINITY, 1 << 30, 1 << 30};
+  double mg = 0.0, mh = 0.0, cnt_factor = 0.0;
+  if (act) {
+    for (int w = 0; w < cw; ++w) { vg += s_sg[cc][w]; vh += s_sh[cc][w]; }
+    s_pg[cc][ltid] = vg;
+    s_ph[cc][ltid] = vh;
+    mg = nan_bin >= 0 ? s_g[cc][nan_bin] : (zero_bin >= 0 ? s_g[cc][zero_bin] : 0.0);
+    mh = nan_bin >= 0 ? s_h[cc][nan_bin] : (zero_bin >= 0 ? s_h[cc][zero_bin] : 0.0);
+    cnt_factor = cnt / fmax(H, kEpsilon);
+    if (numer && ltid < last) {
+      const double parent_gain = LeafGain(G, H, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
+      const double shift = parent_gain + sp.min_gain_to_split;
+      auto consider = [&](double gl, double hl, int dl) {
+        const double gr = G - gl, hr = H - hl;
+        const int64_t cl = EstimateCount(hl, cnt_factor), cr = cnt - cl;
+        if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
+        if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
+        double gain, lout, rout;
+        if (!EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &gain, &lout, &rout)) return;
+        if (!(gain > shift)) return;
+        Cand cd{gain - shift, ltid, dl};
+        if (CandBetter(cd, best)) best = cd;
+      };
+      if (mt == kMissingNone) consider(vg, vh, 1);
+      else { consider(vg, vh, 0); consider(vg + mg, vh + mh, 1); }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    Cand o;
+    o.gain = __shfl_xor(best.gain, off, 64);
+    o.thr = __shfl_xor(best.thr, off, 64);
+    o.dl = __shfl_xor(best.dl, off, 64);
+    if (CandBetter(o, best)) best = o;
+  }
+  if (act && lane == 0) s_wbest[cc][cw] = best;
+  __syncthreads();
+  if (act && ltid == 0) {
+    SplitResult& r = s_res[cc];
+    r.feature = -1; r.gain = -INFINITY;
+    if (eligible && is_cat) {
+      CategoricalSearchBuf(s_g[cc], s_h[cc], nb, f, G, H, cnt, sp, mcp, &r, s_idx[cc], s_left[cc]);
+    } else if (eligible) {
+      Cand b = s_wbest[cc][0];
+      for (int w = 1; w < 4; ++w) if (CandBetter(s_wbest[cc][w], b)) b = s_wbest[cc][w];
+      if (b.gain != -INFINITY) {
+        double gl = s_pg[cc][b.thr], hl = s_ph[cc][b.thr];
+        if (mt != kMissingNone && b.dl) { gl += mg; hl += mh; }
+        const double gr = G - gl, hr = H - hl;
+        r.feature = f; r.gain = b.gain; r.threshold = static_cast<uint32_t>(b.thr); r.default_left = b.dl;
+        r.is_cat = 0;
+        r.left_g = gl; r.left_h = hl; r.right_g = gr; r.right_h = hr;
+        r.left_cnt = EstimateCount(hl, cnt_factor); r.right_cnt = cnt - r.left_cnt;
+        double g2;
+        (void)EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &g2, &r.left_out,
+                        &r.right_out);
+        if (mcp && mcp->mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(Lf.depth, sp.monotone_penalty);
+        for (int w = 0; w < 8; ++w) r.cat_bits[w] = 0;
+      }
+    }
+    PublishAgent(fbest + c * F + f, &r);
+  }
+  // ---- 3. publish + arrive; the last block chooses
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned int old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == static_cast<unsigned int>(F - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ChooseFused(st, leaves, lbest, lgain, fbest, F, t, gcnt, mono, has_mono);
+}
+
 // ---------------------------------------------------------------- K6
 // Decisions read the column-major copy: the lanes of a wave touch one byte
 // column (contiguous for the physical root, increasing for partitioned leaves)
 // instead of one 32-B row each.
-__device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int r, const SplitResult& sr, FeatMeta fm) {
-  const int f = sr.feature;
-  const uint32_t b = cbins[static_cast<size_t>(f) * n + r];
-  return DeviceGoesLeft(b, fm.num_bin[f], fm.missing[f], fm.default_bin[f], sr.is_cat, sr.threshold,
-                        sr.default_left, sr.cat_bits);
+// The split the partition applies: scalars (wave-uniform, SGPRs) plus the
+// category bitset staged in LDS. Copying the whole 120-byte SplitResult into
+// a local made the compiler place it in scratch (cat_bits is indexed by a
+// per-row bin): 128 B/lane of scratch on every partition launch.
+struct PartSplit {
+  int feature, nb, mt, dbin, is_cat, dleft;
+  uint32_t thr;
+};
+
+__device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int r, const PartSplit& ps,
+                                            const uint32_t* s_cat) {
+  const uint32_t b = cbins[static_cast<size_t>(ps.feature) * n + r];
+  return DeviceGoesLeft(b, ps.nb, ps.mt, ps.dbin, ps.is_cat, ps.thr, ps.dleft, s_cat);
 }
 
 // Single pass: a block takes tiles of kPartTile rows (kPartRows per thread,
@@ -1360,11 +1766,22 @@ __global__ __launch_bounds__(kPartThreads) void part_kernel(
   constexpr int kPartTile = kPartThreads * kPartRows;
   const int ntiles = ceil_div_i(pcount, kPartTile);
   if (static_cast<int>(blockIdx.x) >= ntiles) return;
-  const SplitResult sr = lbest[st->split_leaf];
+  const SplitResult* srp = lbest + st->split_leaf;
+  PartSplit ps;
+  ps.feature = srp->feature;
+  ps.is_cat = srp->is_cat;
+  ps.dleft = srp->default_left;
+  ps.thr = srp->threshold;
+  ps.nb = fm.num_bin[ps.feature];
+  ps.mt = fm.missing[ps.feature];
+  ps.dbin = fm.default_bin[ps.feature];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int kWaves = kPartThreads / 64;
   __shared__ int wl[kPartRows][kWaves];
   __shared__ int bases[2];
+  __shared__ uint32_t s_cat[8];
+  if (tid < 8) s_cat[tid] = ps.is_cat ? srp->cat_bits[tid] : 0u;
+  __syncthreads();
   const int32_t* perm = pbuf == 0 ? perm0 : perm1;
   const float2* ogh = pbuf == 0 ? ogh0 : ogh1;
   int32_t* operm = pbuf == 0 ? wperm1 : wperm0;
@@ -1391,7 +1808,7 @@ __global__ __launch_bounds__(kPartThreads) void part_kernel(
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       const int k = u * kPartThreads + tid;
-      const bool left = k < tv && RowGoesLeft(cbins, n, r[u], sr, fm);
+      const bool left = k < tv && RowGoesLeft(cbins, n, r[u], ps, s_cat);
       lmask |= left ? (1u << u) : 0u;
       const unsigned long long bl = __ballot(left);
       rl[u] = __popcll(bl & below);
@@ -1605,6 +2022,9 @@ class GpuBackend : public TrainBackend {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
     }
+    if (const char* e = std::getenv("SML_FUSED_SPLIT")) fused_split_ = std::atoi(e);
+    arrive_.alloc(1);
+    SML_HIP_CHECK(hipMemsetAsync(arrive_.get(), 0, sizeof(unsigned int), stream_));
     fbest_.alloc(2 * F_);
     lbest_.alloc(L_);
     lgain_.alloc(L_);
@@ -1951,10 +2371,11 @@ class GpuBackend : public TrainBackend {
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
                        perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     SML_HIP_CHECK(hipGetLastError());
+    if (fused_split_ == 1 && !Distributed()) return;  // split_kernel reduces the slabs itself
     hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_,
                        state_, leaves_.get(), slab_.get(), E_, ghmax, part_.get());
     SML_HIP_CHECK(hipGetLastError());
-    if (comm_ && comm_->world() > 1) {
+    if (Distributed()) {
       // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL
       auto t0 = std::chrono::steady_clock::now();
       comm_->AllReduceDeviceF64(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 2, stream_);
@@ -1962,7 +2383,18 @@ class GpuBackend : public TrainBackend {
     }
   }
 
+  bool Distributed() const { return comm_ && comm_->world() > 1; }
+
   void EnqueueFindChoose() {
+    if (fused_split_) {
+      const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
+      auto k = (Distributed() || fused_split_ == 2) ? split_kernel<false> : split_kernel<true>;
+      hipLaunchKernelGGL(k, dim3(F_), dim3(kSplitThreads), 0, stream_, state_, leaves_.get(), slab_.get(),
+                         part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(), F_, lbest_.get(),
+                         lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      return;
+    }
     hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, state_, leaves_.get(), part_.get(),
                        E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
     SML_HIP_CHECK(hipGetLastError());
@@ -2094,6 +2526,10 @@ class GpuBackend : public TrainBackend {
   DevBuf<int32_t> meta_i_, bag_;
   DevBuf<int8_t> mask_, mono_;
   DevBuf<unsigned int> ghmax_;
+  DevBuf<unsigned int> arrive_;  // split_kernel arrival counter (reset by the last block)
+  // SML_FUSED_SPLIT: 0 = reduce / find / choose launches, 1 = one split_kernel (slab reduce inside),
+  // 2 = reduce launch + split_kernel (find + choose)
+  int fused_split_ = 0;  // A/B on MI355X: 0 = 2.30 ms/iter, 2 = 2.41, 1 = 2.51 (profiles/README)
   DevBuf<float> ghmax_partial_;
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
