@@ -827,8 +827,8 @@ __device__ __forceinline__ void hist_accumulate(unsigned long long* sh, const ui
     if (j + 16 < Fg) atomicAdd(&sh[(j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u)], packed);
 }
 
-template <int kHistUnroll>
-__global__ __launch_bounds__(kHistThreads) void hist_kernel(
+template <int kHistUnroll, int kThreads = kHistThreads>
+__global__ __launch_bounds__(kThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
     const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
   __shared__ unsigned long long sh[kFeatPerGroup * kHistStride];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kFeatPerGroup * kHistStride; i += kHistThreads) sh[i] = 0ull;
+  for (int i = tid; i < kFeatPerGroup * kHistStride; i += kThreads) sh[i] = 0ull;
   __syncthreads();
   const int grp = blockIdx.y;
   const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
@@ -853,12 +853,12 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
   const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
   const bool phys = L.buf < 0;
-  for (int base = p0 + tid; base < p1; base += kHistThreads * kHistUnroll) {
+  for (int base = p0 + tid; base < p1; base += kThreads * kHistUnroll) {
     int r[kHistUnroll];
     bool ok[kHistUnroll];
 #pragma unroll
     for (int u = 0; u < kHistUnroll; ++u) {
-      const int pos = base + u * kHistThreads;
+      const int pos = base + u * kThreads;
       ok[u] = pos < p1;
       r[u] = ok[u] ? (phys ? pos : perm[pos]) : 0;
     }
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     float2 v[kHistUnroll];
 #pragma unroll
     for (int u = 0; u < kHistUnroll; ++u) {
-      const int pos = base + u * kHistThreads;
+      const int pos = base + u * kThreads;
       const size_t rb = static_cast<size_t>(r[u]) * W4 + col;
       b0[u] = bins4[rb];
       b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
@@ -878,10 +878,90 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
   }
   __syncthreads();
   int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
-  for (int i = tid; i < Fg * kBinsPerFeature; i += kHistThreads) {
+  for (int i = tid; i < Fg * kBinsPerFeature; i += kThreads) {
     const int f = i >> 8, b = i & 255;
     const unsigned long long w = sh[f * kHistStride + b];
     out[(grp * kFeatPerGroup + f) * kBinsPerFeature + b] =
+        make_int2(static_cast<int32_t>(w >> 32), static_cast<int32_t>(static_cast<uint32_t>(w)));
+  }
+}
+
+// Feature-lane variant (SML_HIST_MODE=1; measured slower, kept for A/B): lane l of a wave owns
+// feature (l & 15) of the row in its quad (l >> 4), so one wave instruction
+// adds 4 rows x 16 features. The block's LDS histogram is bin-major,
+// sh[bin][32 features] of packed u64: the 16 lanes of a 64-bit atomic's lane
+// group (one row, features 0-15) always hit 16 different bank pairs whatever
+// their bins are, so the atomics never conflict; each lane extracts its byte
+// with a constant shift (no per-lane dynamic select). The per-row gradient
+// pair and the row's bin dwords are read by the 16 lanes of a quad as one
+// coalesced segment. Slabs are written bin-major ([block][bin][32 * groups]),
+// which hist_reduce_kernel<true> reads contiguously.
+template <int kUnroll>
+__global__ __launch_bounds__(kHistThreads) void hist_fl_kernel(
+    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint32_t* __restrict__ bins32,
+    int W, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
+    const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
+    const float* __restrict__ h, const float* __restrict__ ghmax, int2* __restrict__ slab) {
+  if (st->done) return;
+  const DLeaf L = HistSeg(st, leaves);
+  const int count = L.count;
+  const int nb_active = HistBlocks(count);
+  if (static_cast<int>(blockIdx.x) >= nb_active) return;
+  __shared__ unsigned long long sh[kBinsPerFeature * kFeatPerGroup];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int i = tid; i < kBinsPerFeature * kFeatPerGroup; i += kHistThreads) sh[i] = 0ull;
+  __syncthreads();
+  const int grp = blockIdx.y;
+  const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
+  const int fl = lane & 15, quad = lane >> 4;
+  const bool f0 = fl < Fg, f1 = fl + 16 < Fg;
+  const int w0off = grp * 8 + (fl >> 2), w1off = grp * 8 + 4 + (fl >> 2);
+  const int shift = (fl & 3) * 8;
+  const int chunk = ceil_div_i(count, nb_active);
+  const int p0 = L.begin + blockIdx.x * chunk;
+  const int p1 = min(L.begin + count, p0 + chunk);
+  const HScale sc = HistScale(count, ghmax);
+  const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
+  const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
+  const bool phys = L.buf < 0;
+  constexpr int kWaves = kHistThreads / 64;
+  constexpr int kStep = kWaves * 4;  // rows per block per unrolled slot
+  for (int base = p0 + wid * 4 + quad; base < p1; base += kStep * kUnroll) {
+    int r[kUnroll];
+    bool ok[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int pos = base + u * kStep;
+      ok[u] = pos < p1;
+      r[u] = ok[u] ? (phys ? pos : perm[pos]) : 0;
+    }
+    uint32_t a[kUnroll], b[kUnroll];
+    float2 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int pos = base + u * kStep;
+      const uint32_t* row = bins32 + static_cast<size_t>(r[u]) * W;
+      a[u] = f0 && ok[u] ? row[w0off] : 0u;
+      b[u] = f1 && ok[u] ? row[w1off] : 0u;
+      v[u] = !ok[u] ? make_float2(0.f, 0.f) : (phys ? make_float2(g[r[u]], h[r[u]]) : ogh[pos]);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (!ok[u]) continue;
+      const unsigned long long packed = PackGH(v[u], sc);
+      if (f0) atomicAdd(&sh[((a[u] >> shift) & 255u) * kFeatPerGroup + fl], packed);
+      if (f1) atomicAdd(&sh[((b[u] >> shift) & 255u) * kFeatPerGroup + 16 + fl], packed);
+    }
+  }
+  __syncthreads();
+  // bin-major slab: element (bin, f) of group grp at bin * FP + grp * 32 + f (FP = 32 * groups)
+  const int FP = static_cast<int>(gridDim.y) * kFeatPerGroup;
+  int2* out = slab + static_cast<size_t>(blockIdx.x) * FP * kBinsPerFeature;
+  for (int i = tid; i < kBinsPerFeature * kFeatPerGroup; i += kHistThreads) {
+    const int bin = i >> 5, f = i & 31;
+    if (f >= Fg) continue;
+    const unsigned long long w = sh[i];
+    out[bin * FP + grp * kFeatPerGroup + f] =
         make_int2(static_cast<int32_t>(w >> 32), static_cast<int32_t>(static_cast<uint32_t>(w)));
   }
 }
@@ -908,19 +988,31 @@ __global__ __launch_bounds__(256) void ghmax_kernel(const float* __restrict__ g,
 constexpr int kRedE = 32;
 constexpr int kRedG = 16;
 
+// kBinMajor: slabs of hist_fl_kernel, element (bin, f) at bin * FP + f with
+// FP = 32 * feature groups; thread le walks slab elements contiguously and
+// writes the feature-major histogram entry e = f * 256 + bin.
+template <bool kBinMajor>
 __global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
-    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const int2* __restrict__ slab, int E,
-    const float* __restrict__ ghmax, double2* __restrict__ hist) {
+    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const int2* __restrict__ slab, int E, int FP,
+    int F, const float* __restrict__ ghmax, double2* __restrict__ hist) {
   if (st->done) return;
   const int count = HistSeg(st, leaves).count;
   const int nb_active = HistBlocks(count);
   const int tid = threadIdx.x, le = tid % kRedE, grp = tid / kRedE;
-  const int e = blockIdx.x * kRedE + le;
+  const int si = blockIdx.x * kRedE + le;  // slab element
+  const int ES = kBinMajor ? FP * kBinsPerFeature : E;
+  int e = si;
+  bool valid = si < ES;
+  if (kBinMajor) {
+    const int f = si % FP, bin = si / FP;
+    valid = valid && f < F;
+    e = f * kBinsPerFeature + bin;
+  }
   long long sg = 0, sh = 0;
-  if (e < E) {
+  if (valid) {
 #pragma unroll 8
     for (int b = grp; b < nb_active; b += kRedG) {
-      const int2 v = slab[static_cast<size_t>(b) * E + e];
+      const int2 v = slab[static_cast<size_t>(b) * ES + si];
       sg += v.x;
       sh += static_cast<uint32_t>(v.y);
     }
@@ -929,7 +1021,7 @@ __global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
   rg[grp][le] = sg;
   rh[grp][le] = sh;
   __syncthreads();
-  if (grp == 0 && e < E) {
+  if (grp == 0 && valid) {
     long long tg = 0, th = 0;
 #pragma unroll
     for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
@@ -2006,7 +2098,9 @@ class GpuBackend : public TrainBackend {
     g_.alloc(static_cast<size_t>(n_) * K);
     h_.alloc(static_cast<size_t>(n_) * K);
     for (int b = 0; b < 2; ++b) { perm_[b].alloc(n_); ogh_[b].alloc(n_); }
-    slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * E_);
+    if (const char* e = std::getenv("SML_HIST_MODE")) hist_mode_ = std::atoi(e) == 1 ? 1 : 0;
+    // bin-major slabs (hist_fl_kernel) are padded to 32 features per group
+    slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * std::max<size_t>(E_, static_cast<size_t>(FG_) * kFeatPerGroup * kBinsPerFeature));
     part_.alloc(static_cast<size_t>(E_) + 1);  // histogram + (row count, 0)
     hist_pool_.alloc(static_cast<size_t>(2 * L_ + 2) * E_);
     // launch-shape knobs for A/B runs (defaults are the measured best)
@@ -2018,6 +2112,8 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_min_rows_per_hist_block), &v, sizeof(int)));
     }
     if (hist_unroll_ != 2 && hist_unroll_ != 4 && hist_unroll_ != 8) hist_unroll_ = kHistUnrollDefault;
+    if (const char* e = std::getenv("SML_HIST_THREADS")) hist_threads_ = std::atoi(e);
+    if (hist_threads_ != 256 && hist_threads_ != 512 && hist_threads_ != 1024) hist_threads_ = kHistThreads;
     {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
@@ -2366,14 +2462,26 @@ class GpuBackend : public TrainBackend {
 
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-    auto hk = hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>);
-    hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_,
-                       leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
-                       perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
+    if (hist_mode_ == 1) {
+      auto hk = hist_unroll_ == 8 ? hist_fl_kernel<8> : (hist_unroll_ == 4 ? hist_fl_kernel<4> : hist_fl_kernel<2>);
+      hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_, leaves_.get(),
+                         reinterpret_cast<const uint32_t*>(bins_.get()), S_ / 4, F_, perm_[0].get(), perm_[1].get(),
+                         ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
+    } else {
+      auto hk = hist_threads_ == 1024 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024> : hist_kernel<2, 1024>)
+                : hist_threads_ == 256 ? (hist_unroll_ == 4 ? hist_kernel<4, 256> : hist_kernel<2, 256>)
+                : (hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>));
+      hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(hist_threads_), 0, stream_, state_,
+                         leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
+                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
+    }
     SML_HIP_CHECK(hipGetLastError());
-    if (fused_split_ == 1 && !Distributed()) return;  // split_kernel reduces the slabs itself
-    hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_,
-                       state_, leaves_.get(), slab_.get(), E_, ghmax, part_.get());
+    if (fused_split_ == 1 && hist_mode_ == 0 && !Distributed()) return;  // split_kernel reduces the slabs itself
+    const int FP = FG_ * kFeatPerGroup;
+    const int ES = hist_mode_ == 1 ? FP * kBinsPerFeature : E_;
+    hipLaunchKernelGGL(hist_mode_ == 1 ? hist_reduce_kernel<true> : hist_reduce_kernel<false>,
+                       dim3((ES + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, state_, leaves_.get(),
+                       slab_.get(), E_, FP, F_, ghmax, part_.get());
     SML_HIP_CHECK(hipGetLastError());
     if (Distributed()) {
       // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL
@@ -2388,7 +2496,7 @@ class GpuBackend : public TrainBackend {
   void EnqueueFindChoose() {
     if (fused_split_) {
       const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-      auto k = (Distributed() || fused_split_ == 2) ? split_kernel<false> : split_kernel<true>;
+      auto k = (Distributed() || fused_split_ == 2 || hist_mode_ == 1) ? split_kernel<false> : split_kernel<true>;
       hipLaunchKernelGGL(k, dim3(F_), dim3(kSplitThreads), 0, stream_, state_, leaves_.get(), slab_.get(),
                          part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(), F_, lbest_.get(),
                          lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get());
@@ -2534,7 +2642,11 @@ class GpuBackend : public TrainBackend {
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
   int part_grid_ = 1;
-  int part_rows_ = kPartRowsDefault, hist_unroll_ = kHistUnrollDefault;
+  int part_rows_ = kPartRowsDefault, hist_unroll_ = kHistUnrollDefault, hist_threads_ = kHistThreads;
+  // SML_HIST_MODE: 0 = row-per-lane hist_kernel (default), 1 = feature-lane conflict-free hist_fl_kernel
+  // (A/B on MI355X: 2.28 vs 3.01 ms/iter - 16x the memory instructions per row cost more than the bank
+  // conflicts it removes; profiles/README)
+  int hist_mode_ = 0;
   DevBuf<uint8_t> blob_;
   DState* state_ = nullptr;
   size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
