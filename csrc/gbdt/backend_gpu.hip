@@ -740,7 +740,22 @@ __global__ __launch_bounds__(256) void sample_kernel(RowSampleSpec sp, int64_t n
 }
 
 // ---------------------------------------------------------------- root init
-__global__ void root_init_kernel(DState* st, DLeaf* leaves, int32_t count, int buf, int max_leaves) {
+// nparts > 0: also fold the per-block max |g| / max h partials of the pass that
+// produced this tree's gradients into ghmax (what ghmax_final_kernel does, one
+// launch fewer per tree).
+__global__ __launch_bounds__(64) void root_init_kernel(DState* st, DLeaf* leaves, int32_t count, int buf,
+                                                       int max_leaves, const float* __restrict__ partial, int nparts,
+                                                       unsigned int* __restrict__ ghmax) {
+  if (nparts > 0) {
+    float mg = 0.f, mh = 0.f;
+    for (int b = threadIdx.x; b < nparts; b += 64) {
+      mg = fmaxf(mg, partial[2 * b]);
+      mh = fmaxf(mh, partial[2 * b + 1]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) { mg = fmaxf(mg, __shfl_xor(mg, off, 64)); mh = fmaxf(mh, __shfl_xor(mh, off, 64)); }
+    if (threadIdx.x == 0) { ghmax[0] = __float_as_uint(mg); ghmax[1] = __float_as_uint(mh); }
+  }
   if (threadIdx.x == 0) {
     st->num_leaves = 1; st->done = 0; st->split_leaf = 0; st->new_leaf = -1;
     st->small_leaf = 0; st->large_leaf = -1; st->parent_slot = -1; st->max_leaves = max_leaves;
@@ -2041,6 +2056,93 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, co
   }
 }
 
+// ---------------------------------------------------------------- K7 + K2 + root K3, one pass
+// The score update of the tree just grown, the next iteration's gradients and
+// the next tree's root histogram all walk every row in physical order and the
+// first and last read the same 32-B bin row, so one kernel does all three:
+// per row it walks the tree on the row's bins (nodes + leaf values staged in
+// LDS), adds scale * leaf value to the score, evaluates the objective on the
+// new score, stores g and h, and accumulates the packed fixed-point (g, h) into
+// the block's LDS histogram exactly as hist_kernel does for the root. The
+// grid/chunk decomposition is hist_kernel's root decomposition (HistBlocks(n)
+// blocks of ceil(n / blocks) contiguous rows), so hist_reduce_kernel reduces
+// these slabs unchanged. The fixed-point scale cannot wait for this pass's
+// max |g| / max h, so it comes from an a-priori bound of the objective
+// (binary: sigmoid * label weight * max weight, h <= sigmoid^2 / 4 * ...;
+// cross-entropy: |g| <= w, h <= w / 4) stored in `bound`; the pass still emits
+// the block maxima of |g| and h, which the rest of the tree's histograms use.
+// Replaces score_kernel + grad_kernel + the root hist_kernel (150 + 54 + 131
+// us at 11M x 28 on MI355X, three full passes over rows).
+constexpr int kPrepMaxNodes = 255;  // trees up to 256 leaves keep nodes + values in LDS
+
+template <int kUnroll>
+__global__ __launch_bounds__(kHistThreads) void score_grad_hist_kernel(
+    DevTreeView tv, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
+    double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
+    float* __restrict__ g, float* __restrict__ h, const float* __restrict__ bound, float* __restrict__ partial,
+    int2* __restrict__ slab) {
+  const int nb_active = HistBlocks(n);
+  if (static_cast<int>(blockIdx.x) >= nb_active) return;
+  __shared__ unsigned long long sh[kFeatPerGroup * kHistStride];
+  __shared__ int4 snodes[kPrepMaxNodes];
+  __shared__ double slval[kPrepMaxNodes + 1];
+  const int tid = threadIdx.x;
+  const int ni = tv.num_leaves - 1;
+  for (int i = tid; i < kFeatPerGroup * kHistStride; i += kHistThreads) sh[i] = 0ull;
+  for (int i = tid; i < ni; i += kHistThreads) snodes[i] = tv.nodes[i];
+  for (int i = tid; i < tv.num_leaves; i += kHistThreads) slval[i] = tv.lval[i];
+  __syncthreads();
+  const int chunk = ceil_div_i(n, nb_active);
+  const int p0 = blockIdx.x * chunk;
+  const int p1 = min(n, p0 + chunk);
+  const HScale sc = HistScale(n, bound);
+  const bool two = F > 16;
+  float mg = 0.f, mh = 0.f;
+  for (int base = p0 + tid; base < p1; base += kHistThreads * kUnroll) {
+    uint4 b0[kUnroll], b1[kUnroll];
+    double s[kUnroll];
+    float y[kUnroll], w[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int i = base + u * kHistThreads;
+      const bool ok = i < p1;
+      const size_t rb = static_cast<size_t>(ok ? i : p0) * W4;
+      b0[u] = bins4[rb];
+      b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
+      s[u] = ok ? score[i] : 0.0;
+      y[u] = ok ? label[i] : 0.f;
+      w[u] = ok && weight ? weight[i] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int i = base + u * kHistThreads;
+      if (i >= p1) continue;
+      int node = ni > 0 ? 0 : ~0;
+      for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
+        const int4 nd = snodes[node];
+        node = NodeStep(nd, ByteOfRow(b0[u], b1[u], nd.x & 0xFFFF), tv.cat_bits, node);
+      }
+      const double sn = s[u] + scale * slval[ni > 0 ? ~node : 0];
+      score[i] = sn;
+      float gg, hh;
+      PointGradient(p, sn, y[u], w[u], &gg, &hh);
+      g[i] = gg;
+      h[i] = hh;
+      mg = fmaxf(mg, fabsf(gg));
+      mh = fmaxf(mh, fabsf(hh));
+      hist_accumulate(sh, b0[u], b1[u], PackGH(make_float2(gg, hh), sc), F);
+    }
+  }
+  BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
+  __syncthreads();
+  int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
+  for (int i = tid; i < F * kBinsPerFeature; i += kHistThreads) {
+    const int f = i >> 8, b = i & 255;
+    const unsigned long long v = sh[f * kHistStride + b];
+    out[i] = make_int2(static_cast<int32_t>(v >> 32), static_cast<int32_t>(static_cast<uint32_t>(v)));
+  }
+}
+
 // row-major -> column-major bin copy (once per dataset)
 __global__ void transpose_bins_kernel(const uint8_t* __restrict__ bins, int S, int F, int64_t n,
                                       uint8_t* __restrict__ cbins) {
@@ -2119,6 +2221,25 @@ class GpuBackend : public TrainBackend {
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
     }
     if (const char* e = std::getenv("SML_FUSED_SPLIT")) fused_split_ = std::atoi(e);
+    if (const char* e = std::getenv("SML_HIST_MIN_ROWS")) min_rows_hist_ = std::max(256, std::atoi(e));
+    {
+      // score_grad_hist_kernel: one class, every row in every tree (no bagging / GOSS / RF / DART
+      // rescaling between the score update and the next gradients), <= 32 features, row-per-lane slabs
+      const bool sampled = cfg.boosting != "gbdt" ||
+                           (cfg.bagging_freq > 0 && (cfg.bagging_fraction < 1.0 || cfg.pos_bagging_fraction < 1.0 ||
+                                                     cfg.neg_bagging_fraction < 1.0));
+      const char* e = std::getenv("SML_PREP");
+      prep_ok_ = K == 1 && !sampled && hist_mode_ == 0 && fused_split_ == 0 && F_ > 0 && F_ <= kFeatPerGroup &&
+                 L_ <= kPrepMaxNodes + 1 && !(e && std::atoi(e) == 0);
+      wmax_ = 1.0;
+      if (!d->weight.empty()) {
+        wmax_ = 0.0;
+        for (float w : d->weight) wmax_ = std::max(wmax_, static_cast<double>(std::fabs(w)));
+      }
+      ymax_ = 0.0;
+      for (float y : d->label) ymax_ = std::max(ymax_, static_cast<double>(std::fabs(y)));
+      ghbound_.alloc(2);
+    }
     arrive_.alloc(1);
     SML_HIP_CHECK(hipMemsetAsync(arrive_.get(), 0, sizeof(unsigned int), stream_));
     fbest_.alloc(2 * F_);
@@ -2176,9 +2297,7 @@ class GpuBackend : public TrainBackend {
     int64_t* tl = reinterpret_cast<int64_t*>(blob_.get() + off_tl_);
     dt_.icount = tl; dt_.lcount = tl + NI;
     // score-update tree (uploaded from host trees)
-    up_nodes_.alloc(static_cast<size_t>(NI) + 1);
-    up_u_.alloc(static_cast<size_t>(NI) * 8 + 8);
-    up_d_.alloc(L_ + 4);
+    up_blob_.alloc(static_cast<size_t>(NI + 1) * (16 + 32) + static_cast<size_t>(L_ + 4) * 8);
     leaf_idx_.alloc(n_);
     SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
     for (hipEvent_t& e : ev_) SML_HIP_CHECK(hipEventCreate(&e));
@@ -2188,6 +2307,7 @@ class GpuBackend : public TrainBackend {
   }
 
   void SetScores(const std::vector<double>& s) override {
+    prep_valid_ = root_ready_ = false;
     SML_HIP_CHECK(hipMemcpyAsync(score_.get(), s.data(), sizeof(double) * s.size(), hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
   }
@@ -2197,15 +2317,28 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   void AddBias(int k, double b) override {
+    prep_valid_ = root_ready_ = false;
     hipLaunchKernelGGL(axpby_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, score_.get() + k * n_, n_, 1.0, b);
     SML_HIP_CHECK(hipGetLastError());
   }
   void ScaleScore(int k, double sc) override {
+    prep_valid_ = root_ready_ = false;
     hipLaunchKernelGGL(axpby_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, score_.get() + k * n_, n_, sc, 0.0);
     SML_HIP_CHECK(hipGetLastError());
   }
   void ComputeGradients(const Objective& obj) override {
     const ObjParams& p = obj.params();
+    if (prep_valid_ && std::memcmp(&p, &prep_params_, sizeof(ObjParams)) == 0) {
+      // score_grad_hist_kernel already evaluated this objective on the current scores and built the
+      // next root histogram's slabs; its block maxima are folded into ghmax by root_init_kernel
+      prep_valid_ = false;
+      root_ready_ = true;
+      ghmax_valid_ = true;
+      pending_parts_ = prep_blocks_;
+      return;
+    }
+    prep_valid_ = false;
+    root_ready_ = false;
     if (p.kind == kObjLambdarank && K_ == 1) {
       auto t0 = std::chrono::steady_clock::now();
       EnsureRankTables(obj);
@@ -2240,15 +2373,20 @@ class GpuBackend : public TrainBackend {
     hipLaunchKernelGGL(grad_kernel, dim3(grid), dim3(256), 0, stream_, p, score_.get(), label_.get(),
                        weight_.get(), g_.get(), h_.get(), n_, single ? ghmax_partial_.get() : static_cast<float*>(nullptr));
     SML_HIP_CHECK(hipGetLastError());
-    if (single) {
+    if (single && K_ == 1) {
+      pending_parts_ = grid;  // folded into ghmax by the next root_init_kernel
+    } else if (single) {
       hipLaunchKernelGGL(ghmax_final_kernel, dim3(1), dim3(1024), 0, stream_, ghmax_partial_.get(), grid, ghmax_.get());
       SML_HIP_CHECK(hipGetLastError());
     }
     ghmax_valid_ = single && K_ == 1;
+    ArmPrep(p);
     stats.grad_ms += Ms(t0);
   }
   void SetGradients(const float* g, const float* h) override {
     ghmax_valid_ = false;
+    prep_valid_ = root_ready_ = false;
+    pending_parts_ = 0;
     SML_HIP_CHECK(hipMemcpyAsync(g_.get(), g, sizeof(float) * n_ * K_, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipMemcpyAsync(h_.get(), h, sizeof(float) * n_ * K_, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -2321,9 +2459,14 @@ class GpuBackend : public TrainBackend {
     for (int f = 0; f < F_ && f < static_cast<int>(fmask_in.size()); ++f) fmask[f] = fmask_in[f] ? 1 : 0;
     sp_.tree_seq = tree_seq_++;
     sp_.bynode_k = BynodeK(cfg_, std::vector<char>(fmask.begin(), fmask.end()));
-    SML_HIP_CHECK(hipMemcpyAsync(mask_.get(), fmask.data(), F_, hipMemcpyHostToDevice, stream_));
+    if (fmask != mask_host_) {  // one H2D copy fewer per tree when the feature mask is unchanged
+      mask_host_ = fmask;
+      SML_HIP_CHECK(hipMemcpyAsync(mask_.get(), mask_host_.data(), F_, hipMemcpyHostToDevice, stream_));
+    }
     const float* g = g_.get() + static_cast<size_t>(k) * n_;
     const float* h = h_.get() + static_cast<size_t>(k) * n_;
+    const bool root_prepared = root_ready_ && bag_n_ < 0 && k == 0;
+    root_ready_ = false;
     int32_t root_count = static_cast<int32_t>(n_);
     int root_buf = -1;
     if (bag_n_ >= 0) {
@@ -2339,11 +2482,18 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL(ghmax_final_kernel, dim3(1), dim3(1024), 0, stream_, ghmax_partial_.get(), grid, ghmax_.get());
       SML_HIP_CHECK(hipGetLastError());
+      pending_parts_ = 0;
     }
-    hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_, leaves_.get(), root_count, root_buf, L_);
+    hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_, leaves_.get(), root_count, root_buf, L_,
+                       ghmax_partial_.get(), pending_parts_, ghmax_.get());
     SML_HIP_CHECK(hipGetLastError());
-    // root histogram + split search
-    EnqueueHistogram(g, h);
+    pending_parts_ = 0;
+    // root histogram (slabs already built by score_grad_hist_kernel, or built here) + split search
+    if (root_prepared) {
+      EnqueueReduce(reinterpret_cast<const float*>(ghbound_.get()));
+    } else {
+      EnqueueHistogram(g, h);
+    }
     EnqueueFindChoose();
     for (int s = 1; s < L_; ++s) {
       // partition the chosen leaf, histogram its smaller child, search both
@@ -2369,10 +2519,21 @@ class GpuBackend : public TrainBackend {
     roctxRangePushA("sml::UpdateScore");
     DevTreeView tv = UploadTree(t);
     SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
-                       reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
-                       score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
-    SML_HIP_CHECK(hipGetLastError());
+    prep_valid_ = root_ready_ = false;
+    if (prep_armed_ && k == 0 && t.num_leaves <= kPrepMaxNodes + 1) {
+      // score update + next gradients + next root histogram in one pass (see score_grad_hist_kernel)
+      hipLaunchKernelGGL(score_grad_hist_kernel<2>, dim3(kMaxHistBlocks), dim3(kHistThreads), 0, stream_, tv,
+                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, static_cast<int32_t>(n_), scale,
+                         score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
+                         reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      prep_valid_ = true;
+    } else {
+      hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
+                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
+                         score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
+      SML_HIP_CHECK(hipGetLastError());
+    }
     SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
     score_pending_ = true;
     roctxRangePop();
@@ -2460,6 +2621,35 @@ class GpuBackend : public TrainBackend {
     rank_ready_ = true;
   }
 
+  // Enable the fused score/gradient/root-histogram pass for objectives whose |g| and h have an
+  // a-priori bound (the pass needs its fixed-point scale before it sees the gradients).
+  void ArmPrep(const ObjParams& p) {
+    prep_armed_ = false;
+    if (!prep_ok_) return;
+    double gb, hb;
+    if (p.kind == kObjBinary) {
+      const double lw = std::max(std::fabs(p.pos_weight), std::fabs(p.neg_weight));
+      gb = std::fabs(p.sigmoid) * lw * wmax_;
+      hb = p.sigmoid * p.sigmoid * 0.25 * lw * wmax_;
+    } else if (p.kind == kObjCrossEntropy) {
+      gb = (1.0 + ymax_) * wmax_;
+      hb = 0.25 * wmax_;
+    } else {
+      return;
+    }
+    // float rounding of a gradient never exceeds the float rounding of its bound; 1e-4 of headroom
+    const float nb[2] = {static_cast<float>(gb * 1.0001), static_cast<float>(hb * 1.0001)};
+    if (nb[0] != bound_host_[0] || nb[1] != bound_host_[1]) {
+      bound_host_[0] = nb[0];
+      bound_host_[1] = nb[1];
+      SML_HIP_CHECK(hipMemcpyAsync(ghbound_.get(), bound_host_, sizeof(bound_host_), hipMemcpyHostToDevice, stream_));
+      SML_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    prep_params_ = p;
+    prep_blocks_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxHistBlocks, (n_ + min_rows_hist_ - 1) / min_rows_hist_)));
+    prep_armed_ = true;
+  }
+
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
     if (hist_mode_ == 1) {
@@ -2477,6 +2667,11 @@ class GpuBackend : public TrainBackend {
     }
     SML_HIP_CHECK(hipGetLastError());
     if (fused_split_ == 1 && hist_mode_ == 0 && !Distributed()) return;  // split_kernel reduces the slabs itself
+    EnqueueReduce(ghmax);
+  }
+
+  // slab reduce with the scale the slabs were built with (+ the data-parallel allreduce)
+  void EnqueueReduce(const float* ghmax) {
     const int FP = FG_ * kFeatPerGroup;
     const int ES = hist_mode_ == 1 ? FP * kBinsPerFeature : E_;
     hipLaunchKernelGGL(hist_mode_ == 1 ? hist_reduce_kernel<true> : hist_reduce_kernel<false>,
@@ -2578,9 +2773,6 @@ class GpuBackend : public TrainBackend {
   DevTreeView UploadTree(const Tree& t) {
     const int NI = std::max(1, t.num_leaves - 1);
     const size_t need_n = static_cast<size_t>(NI), need_u = static_cast<size_t>(NI) * 8, need_d = t.num_leaves;
-    if (need_n > up_nodes_.n) up_nodes_.alloc(need_n);
-    if (need_u > up_u_.n) up_u_.alloc(need_u);
-    if (need_d > up_d_.n) up_d_.alloc(need_d);
     const size_t bytes = need_n * 16 + need_u * 4 + need_d * 8;
     if (bytes > kPinnedBytes) throw std::runtime_error("tree too large for staging buffer");
     SML_HIP_CHECK(hipStreamSynchronize(stream_));  // pinned buffer reuse
@@ -2602,11 +2794,14 @@ class GpuBackend : public TrainBackend {
       }
     }
     for (int l = 0; l < t.num_leaves; ++l) pd[l] = t.leaf_value[l];
-    SML_HIP_CHECK(hipMemcpyAsync(up_nodes_.get(), pn, need_n * 16, hipMemcpyHostToDevice, stream_));
-    SML_HIP_CHECK(hipMemcpyAsync(up_u_.get(), pu, need_u * 4, hipMemcpyHostToDevice, stream_));
-    SML_HIP_CHECK(hipMemcpyAsync(up_d_.get(), pd, need_d * 8, hipMemcpyHostToDevice, stream_));
+    // nodes | cat words | leaf values are contiguous in the pinned buffer: one H2D copy
+    if (bytes > up_blob_.n) up_blob_.alloc(bytes);
+    SML_HIP_CHECK(hipMemcpyAsync(up_blob_.get(), pinned_, bytes, hipMemcpyHostToDevice, stream_));
     DevTreeView tv;
-    tv.nodes = up_nodes_.get(); tv.cat_bits = up_u_.get(); tv.lval = up_d_.get(); tv.num_leaves = t.num_leaves;
+    tv.nodes = reinterpret_cast<const int4*>(up_blob_.get());
+    tv.cat_bits = reinterpret_cast<const uint32_t*>(up_blob_.get() + need_n * 16);
+    tv.lval = reinterpret_cast<const double*>(up_blob_.get() + need_n * 16 + need_u * 4);
+    tv.num_leaves = t.num_leaves;
     return tv;
   }
 
@@ -2641,6 +2836,19 @@ class GpuBackend : public TrainBackend {
   DevBuf<float> ghmax_partial_;
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
+  int pending_parts_ = 0;     // > 0: ghmax_ is the max over that many block partials, folded by root_init_kernel
+  // fused score update + gradients + root histogram (score_grad_hist_kernel)
+  bool prep_ok_ = false;      // dataset / config eligible
+  bool prep_armed_ = false;   // the last ComputeGradients used an objective with a-priori bounds
+  bool prep_valid_ = false;   // g, h and the root slabs match the current scores (set by UpdateScore)
+  bool root_ready_ = false;   // ComputeGradients consumed them: the next TrainTree skips its root histogram
+  ObjParams prep_params_{};
+  int prep_blocks_ = 0;
+  int min_rows_hist_ = kMinRowsPerHistBlockDefault;
+  double wmax_ = 1.0, ymax_ = 0.0;
+  float bound_host_[2] = {-1.f, -1.f};
+  DevBuf<float> ghbound_;  // a-priori max |g|, max h: the fused pass's fixed-point scale
+  std::vector<int8_t> mask_host_;
   int part_grid_ = 1;
   int part_rows_ = kPartRowsDefault, hist_unroll_ = kHistUnrollDefault, hist_threads_ = kHistThreads;
   // SML_HIST_MODE: 0 = row-per-lane hist_kernel (default), 1 = feature-lane conflict-free hist_fl_kernel
@@ -2651,9 +2859,7 @@ class GpuBackend : public TrainBackend {
   DState* state_ = nullptr;
   size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
   size_t off_td_ = 0, off_tl_ = 0, off_ti_ = 0, off_tu_ = 0, blob_bytes_ = 0;
-  DevBuf<int4> up_nodes_;
-  DevBuf<uint32_t> up_u_;
-  DevBuf<double> up_d_;
+  DevBuf<uint8_t> up_blob_;  // uploaded score-update tree: nodes | cat words | leaf values
   DevBuf<int32_t> leaf_idx_;
   // device row sampling (K8)
   DevBuf<SelectState> sel_;

@@ -406,3 +406,46 @@ def test_gpu_histogram_quantisation_skewed_hessians():
     pg = bg.predict(X, 0, 0, -1)[:, 0]
     ll = lambda p: float(-np.mean(y * np.log(np.clip(p, 1e-15, 1)) + (1 - y) * np.log(np.clip(1 - p, 1e-15, 1))))
     assert abs(ll(pc) - ll(pg)) <= 0.02 * ll(pc) + 1e-6, (ll(pc), ll(pg))
+
+
+@pytest.mark.parametrize("obj", ["binary", "binary scale_pos_weight=3", "cross_entropy"])
+def test_gpu_fused_score_grad_root_pass(obj, monkeypatch):
+    """score_grad_hist_kernel (score update + next gradients + next root
+    histogram in one pass, a-priori fixed-point scale) against the unfused
+    launches (SML_PREP=0): same trees, scores equal the model's predictions and
+    the gradients left on the device match the objective at those scores."""
+    X, y = _data(n=80000, seed=11)
+    w = np.random.default_rng(2).uniform(0.5, 2.0, len(X)).astype(np.float32)
+    p = f"objective={obj} num_leaves=31 learning_rate=0.2 device_type=gpu"
+
+    def fit(prep):
+        monkeypatch.setenv("SML_PREP", prep)
+        from synapseml_amd.ops import native
+
+        g = native.gbdt()
+        ref = g.DatasetReference.from_sample(X[:50000], len(X), p, [f"f{i}" for i in range(X.shape[1])])
+        ds = g.Dataset(ref, len(X))
+        ds.push_dense(X, 0)
+        ds.set_label(y)
+        ds.set_weight(w)
+        b = g.Booster(ds, p, None)
+        for _ in range(6):
+            b.update()
+        return b
+
+    bf, bu = fit("1"), fit("0")
+    line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")]
+    mf, mu = bf.save_model_string(), bu.save_model_string()
+    assert line(mf, "split_feature")[:3] == line(mu, "split_feature")[:3]
+    s = bf.train_scores()
+    np.testing.assert_allclose(s, bf.predict(X, 0, 0, -1)[:, 0], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(s, bu.train_scores(), rtol=1e-3, atol=1e-3)
+    g, h = bf.gradients()
+    z = 1.0 / (1.0 + np.exp(-s))
+    if obj == "cross_entropy":
+        ge, he = (z - y) * w, z * (1 - z) * w
+    else:
+        lw = np.where(y > 0, 3.0 if "scale_pos" in obj else 1.0, 1.0)
+        ge, he = (z - y) * lw * w, z * (1 - z) * lw * w
+    np.testing.assert_allclose(g, ge, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(h, he, rtol=1e-4, atol=1e-6)

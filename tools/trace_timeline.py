@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Per-iteration timeline of a rocprofv3 kernel trace of bench.py.
 
-Splits the dispatch stream at each ``grad_kernel`` (one boosting iteration
-starts there), and for the last complete iterations reports the wall span,
+Splits the dispatch stream at each ``root_init_kernel`` (one per tree), and for the last complete iterations reports the wall span,
 the summed kernel busy time, the idle gaps between dispatches and the busy
 time / call count per kernel family.
 
@@ -35,9 +34,9 @@ def main() -> None:
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                          int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))))
     rows.sort()
-    starts = [i for i, r in enumerate(rows) if r[2].startswith("grad_kernel")]
+    starts = [i for i, r in enumerate(rows) if r[2].startswith("root_init_kernel")]
     if len(starts) < 2:
-        raise SystemExit("need >= 2 grad_kernel dispatches")
+        raise SystemExit("need >= 2 root_init_kernel dispatches")
     spans = list(zip(starts[:-1], starts[1:]))[-args.iters:]
     for a, b in spans:
         it = rows[a:b]
