@@ -48,6 +48,7 @@ constexpr int kHistStride = 257;           // padded LDS row (bank spread)
 constexpr int kMaxHistBlocks = 512;        // = resident capacity at 2 blocks/CU
 constexpr int kMinRowsPerHistBlockDefault = 1024;  // A/B: 1024 ~ 512 < 2048 < 4096
 __constant__ int c_min_rows_per_hist_block = kMinRowsPerHistBlockDefault;
+__constant__ int c_max_hist_blocks = kMaxHistBlocks;  // 256 for the one-block-per-CU shape (SML_HIST_SHAPE)
 constexpr int kPartThreads = 512;
 constexpr int kMaxPartBlocks = 2048;
 constexpr int kPartRowsDefault = 8;  // A/B on MI355X: 8 rows/thread beat 16 and 4 (profiles/README)
@@ -805,7 +806,7 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 constexpr int kHistUnrollDefault = 2;  // A/B: 2 rows in flight per thread beat 4 and 8
 
 __device__ __forceinline__ int HistBlocks(int count) {
-  return max(1, min(kMaxHistBlocks, ceil_div_i(count, c_min_rows_per_hist_block)));
+  return max(1, min(c_max_hist_blocks, ceil_div_i(count, c_min_rows_per_hist_block)));
 }
 
 struct HScale {
@@ -842,7 +843,12 @@ __device__ __forceinline__ void hist_accumulate(unsigned long long* sh, const ui
     if (j + 16 < Fg) atomicAdd(&sh[(j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u)], packed);
 }
 
-template <int kHistUnroll, int kThreads = kHistThreads>
+// kCopies = 2 (1024-thread blocks, one per CU): waves 0-7 and 8-15 accumulate into
+// two LDS copies of the histogram (2 x 65.8 KB), summed when the slab is
+// written; half the slabs (and half the dirty bytes at the kernel boundary) of
+// two 512-thread blocks per CU. Packed words add exactly: a block's h sum
+// stays below 2^32 by construction of the scale.
+template <int kHistUnroll, int kThreads = kHistThreads, int kCopies = 1>
 __global__ __launch_bounds__(kThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
@@ -853,10 +859,11 @@ __global__ __launch_bounds__(kThreads) void hist_kernel(
   const int count = L.count;
   const int nb_active = HistBlocks(count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long sh[kFeatPerGroup * kHistStride];
+  __shared__ unsigned long long shc[kCopies * kFeatPerGroup * kHistStride];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kFeatPerGroup * kHistStride; i += kThreads) sh[i] = 0ull;
+  for (int i = tid; i < kCopies * kFeatPerGroup * kHistStride; i += kThreads) shc[i] = 0ull;
   __syncthreads();
+  unsigned long long* sh = shc + (kCopies > 1 && tid >= kThreads / 2 ? kFeatPerGroup * kHistStride : 0);
   const int grp = blockIdx.y;
   const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
   const int col = grp * 2;            // first uint4 of this group in a row
@@ -895,7 +902,8 @@ __global__ __launch_bounds__(kThreads) void hist_kernel(
   int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
   for (int i = tid; i < Fg * kBinsPerFeature; i += kThreads) {
     const int f = i >> 8, b = i & 255;
-    const unsigned long long w = sh[f * kHistStride + b];
+    unsigned long long w = shc[f * kHistStride + b];
+    if (kCopies > 1) w += shc[kFeatPerGroup * kHistStride + f * kHistStride + b];
     out[(grp * kFeatPerGroup + f) * kBinsPerFeature + b] =
         make_int2(static_cast<int32_t>(w >> 32), static_cast<int32_t>(static_cast<uint32_t>(w)));
   }
@@ -2075,22 +2083,23 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, co
 // us at 11M x 28 on MI355X, three full passes over rows).
 constexpr int kPrepMaxNodes = 255;  // trees up to 256 leaves keep nodes + values in LDS
 
-template <int kUnroll>
-__global__ __launch_bounds__(kHistThreads) void score_grad_hist_kernel(
+template <int kUnroll, int kThreads = kHistThreads, int kCopies = 1>
+__global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
     DevTreeView tv, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
     float* __restrict__ g, float* __restrict__ h, const float* __restrict__ bound, float* __restrict__ partial,
     int2* __restrict__ slab) {
   const int nb_active = HistBlocks(n);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long sh[kFeatPerGroup * kHistStride];
+  __shared__ unsigned long long shc[kCopies * kFeatPerGroup * kHistStride];
   __shared__ int4 snodes[kPrepMaxNodes];
   __shared__ double slval[kPrepMaxNodes + 1];
   const int tid = threadIdx.x;
   const int ni = tv.num_leaves - 1;
-  for (int i = tid; i < kFeatPerGroup * kHistStride; i += kHistThreads) sh[i] = 0ull;
-  for (int i = tid; i < ni; i += kHistThreads) snodes[i] = tv.nodes[i];
-  for (int i = tid; i < tv.num_leaves; i += kHistThreads) slval[i] = tv.lval[i];
+  for (int i = tid; i < kCopies * kFeatPerGroup * kHistStride; i += kThreads) shc[i] = 0ull;
+  unsigned long long* sh = shc + (kCopies > 1 && tid >= kThreads / 2 ? kFeatPerGroup * kHistStride : 0);
+  for (int i = tid; i < ni; i += kThreads) snodes[i] = tv.nodes[i];
+  for (int i = tid; i < tv.num_leaves; i += kThreads) slval[i] = tv.lval[i];
   __syncthreads();
   const int chunk = ceil_div_i(n, nb_active);
   const int p0 = blockIdx.x * chunk;
@@ -2098,13 +2107,13 @@ __global__ __launch_bounds__(kHistThreads) void score_grad_hist_kernel(
   const HScale sc = HistScale(n, bound);
   const bool two = F > 16;
   float mg = 0.f, mh = 0.f;
-  for (int base = p0 + tid; base < p1; base += kHistThreads * kUnroll) {
+  for (int base = p0 + tid; base < p1; base += kThreads * kUnroll) {
     uint4 b0[kUnroll], b1[kUnroll];
     double s[kUnroll];
     float y[kUnroll], w[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const int i = base + u * kHistThreads;
+      const int i = base + u * kThreads;
       const bool ok = i < p1;
       const size_t rb = static_cast<size_t>(ok ? i : p0) * W4;
       b0[u] = bins4[rb];
@@ -2115,7 +2124,7 @@ __global__ __launch_bounds__(kHistThreads) void score_grad_hist_kernel(
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const int i = base + u * kHistThreads;
+      const int i = base + u * kThreads;
       if (i >= p1) continue;
       int node = ni > 0 ? 0 : ~0;
       for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
@@ -2136,9 +2145,10 @@ __global__ __launch_bounds__(kHistThreads) void score_grad_hist_kernel(
   BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
   __syncthreads();
   int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
-  for (int i = tid; i < F * kBinsPerFeature; i += kHistThreads) {
+  for (int i = tid; i < F * kBinsPerFeature; i += kThreads) {
     const int f = i >> 8, b = i & 255;
-    const unsigned long long v = sh[f * kHistStride + b];
+    unsigned long long v = shc[f * kHistStride + b];
+    if (kCopies > 1) v += shc[kFeatPerGroup * kHistStride + f * kHistStride + b];
     out[i] = make_int2(static_cast<int32_t>(v >> 32), static_cast<int32_t>(static_cast<uint32_t>(v)));
   }
 }
@@ -2216,6 +2226,14 @@ class GpuBackend : public TrainBackend {
     if (hist_unroll_ != 2 && hist_unroll_ != 4 && hist_unroll_ != 8) hist_unroll_ = kHistUnrollDefault;
     if (const char* e = std::getenv("SML_HIST_THREADS")) hist_threads_ = std::atoi(e);
     if (hist_threads_ != 256 && hist_threads_ != 512 && hist_threads_ != 1024) hist_threads_ = kHistThreads;
+    // SML_HIST_SHAPE (A/B): 0 = two 512-thread blocks per CU (512 slabs), 1 = one 1024-thread block
+    // per CU with two LDS histogram copies (256 slabs), 2 = one 1024-thread block, one copy.
+    // MI355X, 11M x 28: 2.14 / 2.06 / 2.05 ms/iter (half the slab bytes written, reduced and
+    // written back at the kernel boundary; the second LDS copy buys nothing)
+    if (const char* e = std::getenv("SML_HIST_SHAPE")) hist_shape_ = std::atoi(e);
+    if (hist_shape_ < 0 || hist_shape_ > 2) hist_shape_ = 2;
+    max_hist_blocks_ = hist_shape_ == 0 ? kMaxHistBlocks : kMaxHistBlocks / 2;
+    SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_max_hist_blocks), &max_hist_blocks_, sizeof(int)));
     {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
@@ -2522,7 +2540,9 @@ class GpuBackend : public TrainBackend {
     prep_valid_ = root_ready_ = false;
     if (prep_armed_ && k == 0 && t.num_leaves <= kPrepMaxNodes + 1) {
       // score update + next gradients + next root histogram in one pass (see score_grad_hist_kernel)
-      hipLaunchKernelGGL(score_grad_hist_kernel<2>, dim3(kMaxHistBlocks), dim3(kHistThreads), 0, stream_, tv,
+      auto pk = hist_shape_ == 1 ? score_grad_hist_kernel<2, 1024, 2>
+                : hist_shape_ == 2 ? score_grad_hist_kernel<2, 1024, 1> : score_grad_hist_kernel<2, kHistThreads, 1>;
+      hipLaunchKernelGGL(pk, dim3(max_hist_blocks_), dim3(hist_shape_ == 0 ? kHistThreads : 1024), 0, stream_, tv,
                          reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, static_cast<int32_t>(n_), scale,
                          score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
                          reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
@@ -2646,7 +2666,7 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipStreamSynchronize(stream_));
     }
     prep_params_ = p;
-    prep_blocks_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxHistBlocks, (n_ + min_rows_hist_ - 1) / min_rows_hist_)));
+    prep_blocks_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(max_hist_blocks_, (n_ + min_rows_hist_ - 1) / min_rows_hist_)));
     prep_armed_ = true;
   }
 
@@ -2658,10 +2678,12 @@ class GpuBackend : public TrainBackend {
                          reinterpret_cast<const uint32_t*>(bins_.get()), S_ / 4, F_, perm_[0].get(), perm_[1].get(),
                          ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     } else {
-      auto hk = hist_threads_ == 1024 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024> : hist_kernel<2, 1024>)
+      auto hk = hist_shape_ == 1 ? hist_kernel<2, 1024, 2>
+                : hist_shape_ == 2 ? hist_kernel<2, 1024, 1>
+                : hist_threads_ == 1024 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024> : hist_kernel<2, 1024>)
                 : hist_threads_ == 256 ? (hist_unroll_ == 4 ? hist_kernel<4, 256> : hist_kernel<2, 256>)
                 : (hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>));
-      hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(hist_threads_), 0, stream_, state_,
+      hipLaunchKernelGGL(hk, dim3(max_hist_blocks_, FG_), dim3(hist_shape_ == 0 ? hist_threads_ : 1024), 0, stream_, state_,
                          leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
                          perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     }
@@ -2855,6 +2877,7 @@ class GpuBackend : public TrainBackend {
   // (A/B on MI355X: 2.28 vs 3.01 ms/iter - 16x the memory instructions per row cost more than the bank
   // conflicts it removes; profiles/README)
   int hist_mode_ = 0;
+  int hist_shape_ = 2, max_hist_blocks_ = kMaxHistBlocks / 2;
   DevBuf<uint8_t> blob_;
   DState* state_ = nullptr;
   size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
