@@ -1444,7 +1444,9 @@ __device__ void ChooseBlock(DState* __restrict__ st, DLeaf* __restrict__ leaves,
 __global__ __launch_bounds__(256) void find_split_kernel(
     DState* __restrict__ st, DLeaf* __restrict__ leaves, const double2* __restrict__ part, int E,
     const double* __restrict__ count_slot, double2* __restrict__ hist_pool, FeatMeta fm, SplitParams sp,
-    SplitResult* __restrict__ fbest, int F) {
+    SplitResult* __restrict__ fbest, int F, DState* __restrict__ st_next) {
+  // choose_part_kernel partitions on the next state version's cursor: zero it here (nothing reads it now)
+  if (st_next && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st_next->cursor = 0ull;
   if (st->done) return;
   FindSplitBlock(st, leaves, part, E, count_slot, hist_pool, fm, sp, fbest, F);
 }
@@ -1869,34 +1871,22 @@ __device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int
 // depends on the order tiles claim their ranges; nothing downstream depends
 // on it (histograms are exact integer sums, see K3).
 
+// Tile loop of the single-pass partition of segment [pbegin, pbegin + pcount)
+// of ping-pong buffer pbuf (-1 = physical rows) by split ps; claims output
+// ranges on *cursor (zeroed before the launch).
 template <int kPartRows>
-__global__ __launch_bounds__(kPartThreads) void part_kernel(
-    DState* __restrict__ st, const SplitResult* __restrict__ lbest, const uint8_t* __restrict__ cbins, int64_t n,
-    const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
-    const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1,
-    float2* __restrict__ wogh0, float2* __restrict__ wogh1, const float* __restrict__ g,
-    const float* __restrict__ h, FeatMeta fm) {
-  if (st->done) return;
-  const int pbegin = st->pbegin, pcount = st->pcount, pbuf = st->pbuf;
+__device__ __forceinline__ void PartitionTiles(
+    const PartSplit& ps, const uint32_t* s_cat, int pbegin, int pcount, int pbuf, unsigned long long* cursor,
+    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
+    const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
+    int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1, float2* __restrict__ wogh0,
+    float2* __restrict__ wogh1, const float* __restrict__ g, const float* __restrict__ h) {
   constexpr int kPartTile = kPartThreads * kPartRows;
   const int ntiles = ceil_div_i(pcount, kPartTile);
-  if (static_cast<int>(blockIdx.x) >= ntiles) return;
-  const SplitResult* srp = lbest + st->split_leaf;
-  PartSplit ps;
-  ps.feature = srp->feature;
-  ps.is_cat = srp->is_cat;
-  ps.dleft = srp->default_left;
-  ps.thr = srp->threshold;
-  ps.nb = fm.num_bin[ps.feature];
-  ps.mt = fm.missing[ps.feature];
-  ps.dbin = fm.default_bin[ps.feature];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int kWaves = kPartThreads / 64;
   __shared__ int wl[kPartRows][kWaves];
   __shared__ int bases[2];
-  __shared__ uint32_t s_cat[8];
-  if (tid < 8) s_cat[tid] = ps.is_cat ? srp->cat_bits[tid] : 0u;
-  __syncthreads();
   const int32_t* perm = pbuf == 0 ? perm0 : perm1;
   const float2* ogh = pbuf == 0 ? ogh0 : ogh1;
   int32_t* operm = pbuf == 0 ? wperm1 : wperm0;
@@ -1936,7 +1926,7 @@ __global__ __launch_bounds__(kPartThreads) void part_kernel(
         for (int w = 0; w < kWaves; ++w) tl += wl[u][w];
       const int tr = tv - tl;
       const unsigned long long old =
-          atomicAdd(&st->cursor, static_cast<unsigned long long>(tl) | (static_cast<unsigned long long>(tr) << 32));
+          atomicAdd(cursor, static_cast<unsigned long long>(tl) | (static_cast<unsigned long long>(tr) << 32));
       bases[0] = pbegin + static_cast<int>(old & 0xFFFFFFFFull);
       bases[1] = pbegin + pcount - static_cast<int>(old >> 32) - tr;
     }
@@ -1963,6 +1953,235 @@ __global__ __launch_bounds__(kPartThreads) void part_kernel(
     }
     __syncthreads();
   }
+}
+
+template <int kPartRows>
+__global__ __launch_bounds__(kPartThreads) void part_kernel(
+    DState* __restrict__ st, const SplitResult* __restrict__ lbest, const uint8_t* __restrict__ cbins, int64_t n,
+    const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
+    const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1,
+    float2* __restrict__ wogh0, float2* __restrict__ wogh1, const float* __restrict__ g,
+    const float* __restrict__ h, FeatMeta fm) {
+  if (st->done) return;
+  const int pbegin = st->pbegin, pcount = st->pcount, pbuf = st->pbuf;
+  constexpr int kPartTile = kPartThreads * kPartRows;
+  const int ntiles = ceil_div_i(pcount, kPartTile);
+  if (static_cast<int>(blockIdx.x) >= ntiles) return;
+  const SplitResult* srp = lbest + st->split_leaf;
+  PartSplit ps;
+  ps.feature = srp->feature;
+  ps.is_cat = srp->is_cat;
+  ps.dleft = srp->default_left;
+  ps.thr = srp->threshold;
+  ps.nb = fm.num_bin[ps.feature];
+  ps.mt = fm.missing[ps.feature];
+  ps.dbin = fm.default_bin[ps.feature];
+  __shared__ uint32_t s_cat[8];
+  if (threadIdx.x < 8) s_cat[threadIdx.x] = ps.is_cat ? srp->cat_bits[threadIdx.x] : 0u;
+  __syncthreads();
+  PartitionTiles<kPartRows>(ps, s_cat, pbegin, pcount, pbuf, &st->cursor, cbins, n, perm0, perm1, ogh0, ogh1,
+                            wperm0, wperm1, wogh0, wogh1, g, h);
+}
+
+// ---------------------------------------------------------------- choose + K6, one launch
+// The choose step (ChooseBlock) fused into the partition it decides: every
+// block redundantly reduces the new children's per-feature records and the
+// leaves' best gains (a few KB of L2-resident reads) to find the leaf to split
+// and its split, then partitions its tiles; the LAST block (usually without
+// tiles) alone writes the bookkeeping. That saves the 1-block choose launch
+// per split. Nothing a block reads is written in the same launch except fields
+// whose bytes do not change:
+//  * the tree state is double-buffered: `sin` (read by all) -> `sout` (written
+//    by the bookkeeping block; its cursor was zeroed by the preceding
+//    find_split_kernel and only receives the partition's atomics here);
+//  * lgain / lbest of the two new children are taken from fbest in registers
+//    by every block; the bookkeeping block stores them for later launches and
+//    does NOT mark the split leaf's gain -inf (the next launch replaces both
+//    children's gains from fbest before any argmax reads them);
+//  * leaves[bl] is rewritten with unchanged begin / count / buf (the only
+//    fields the other blocks read).
+template <int kPartRows>
+__global__ __launch_bounds__(kPartThreads) void choose_part_kernel(
+    const DState* __restrict__ sin, DState* __restrict__ sout, DLeaf* __restrict__ leaves,
+    SplitResult* __restrict__ lbest, double* __restrict__ lgain, const SplitResult* __restrict__ fbest, int F,
+    DTree t, const double* __restrict__ count_slot, const int8_t* __restrict__ mono, int has_mono,
+    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
+    const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
+    int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1, float2* __restrict__ wogh0,
+    float2* __restrict__ wogh1, const float* __restrict__ g, const float* __restrict__ h, FeatMeta fm) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int kWaves = kPartThreads / 64;
+  const bool keeper = blockIdx.x == gridDim.x - 1;  // writes the bookkeeping
+  const DState S = *sin;
+  if (S.done) {
+    if (keeper && tid == 0) {
+      DState o = S;
+      o.cursor = 0ull;
+      *sout = o;
+    }
+    return;
+  }
+  __shared__ int s_bf[2];
+  __shared__ KeyG s_wk[kWaves];
+  __shared__ uint32_t s_cat[8];
+  const bool root = S.phase == 0;
+  const int nchild = root ? 1 : 2;
+  const int nl = S.num_leaves;
+  // the leaves' stored gains do not depend on the children's records: load them first
+  const double my_gain = tid < nl ? lgain[tid] : -INFINITY;
+  if (wid < nchild) {
+    KeyG k{-INFINITY, 1 << 30, 1 << 30};
+    for (int f = lane; f < F; f += 64) {
+      const SplitResult& r = fbest[wid * F + f];
+      if (r.feature < 0) continue;
+      KeyG c{r.gain, r.feature, static_cast<int>(r.threshold)};
+      if (KeyBetter(c, k)) { k = c; k.b = (static_cast<int>(r.threshold) & 0xFFFF) | (f << 16); }
+    }
+    k = WaveArgmax(k);
+    if (lane == 0) s_bf[wid] = k.gain == -INFINITY ? -1 : (k.b >> 16);
+  }
+  __syncthreads();
+  const int bf0 = s_bf[0], bf1 = root ? -1 : s_bf[1];
+  const double cg0 = bf0 >= 0 ? fbest[bf0].gain : -INFINITY;
+  const double cg1 = bf1 >= 0 ? fbest[F + bf1].gain : -INFINITY;
+  const int small_leaf = S.small_leaf, large_leaf = S.large_leaf;
+  // argmax over leaves (ties -> smaller leaf id), the children's gains from registers
+  KeyG k{-INFINITY, 1 << 30, 0};
+  if (nl < S.max_leaves) {
+    for (int i = tid; i < nl; i += kPartThreads) {
+      const double gi = root ? cg0 : (i == small_leaf ? cg0 : (i == large_leaf ? cg1 : (i == tid ? my_gain : lgain[i])));
+      KeyG c{gi, i, 0};
+      if (gi > -INFINITY && KeyBetter(c, k)) k = c;
+    }
+  }
+  k = WaveArgmax(k);
+  if (lane == 0) s_wk[wid] = k;
+  __syncthreads();
+  KeyG best = s_wk[0];
+  for (int w = 1; w < kWaves; ++w) if (KeyBetter(s_wk[w], best)) best = s_wk[w];
+  const int bl = best.gain == -INFINITY ? -1 : best.a;
+  const bool go = nl < S.max_leaves && bl >= 0 && best.gain > 0.0;
+  // the chosen split and the segment of leaf bl
+  const SplitResult* srp = nullptr;
+  int pb = 0, pc = 0, pbuf = -1;
+  if (go) {
+    srp = (root || bl == small_leaf) ? fbest + bf0 : (bl == large_leaf ? fbest + F + bf1 : lbest + bl);
+    if (!root && (bl == S.split_leaf || bl == S.new_leaf)) {
+      const int lt = static_cast<int>(S.cursor & 0xFFFFFFFFull);
+      pb = bl == S.split_leaf ? S.pbegin : S.pbegin + lt;
+      pc = bl == S.split_leaf ? lt : S.pcount - lt;
+      pbuf = S.pbuf == 0 ? 1 : 0;
+    } else {
+      pb = leaves[bl].begin; pc = leaves[bl].count; pbuf = leaves[bl].buf;
+    }
+  }
+  if (keeper && tid == 0) {
+    // children of the previous split (ChooseBlock's first half)
+    if (root) {
+      if (bf0 >= 0) { lbest[0] = fbest[bf0]; lgain[0] = cg0; }
+      else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; lgain[0] = -INFINITY; }
+      t.lval[0] = 0.0;
+      t.lcount[0] = leaves[0].gcount;
+      t.lweight[0] = leaves[0].sum_h;
+      t.lparent[0] = -1;
+      t.ldepth[0] = 0;
+    } else {
+      const int64_t small_cnt = static_cast<int64_t>(*count_slot);
+      const int64_t parent_cnt = leaves[large_leaf].gcount;  // stored by the previous choose
+      const int lt = static_cast<int>(S.cursor & 0xFFFFFFFFull);
+      const int ob = S.pbuf == 0 ? 1 : 0;
+      DLeaf& Lc = leaves[S.split_leaf];
+      DLeaf& Rc = leaves[S.new_leaf];
+      Lc.begin = S.pbegin; Lc.count = lt; Lc.buf = ob;
+      Rc.begin = S.pbegin + lt; Rc.count = S.pcount - lt; Rc.buf = ob;
+      leaves[small_leaf].gcount = small_cnt;
+      leaves[large_leaf].gcount = parent_cnt - small_cnt;
+      t.lcount[small_leaf] = small_cnt;
+      t.lcount[large_leaf] = parent_cnt - small_cnt;
+      for (int c = 0; c < 2; ++c) {
+        const int leaf = c == 0 ? small_leaf : large_leaf;
+        const int bi = c == 0 ? bf0 : bf1;
+        if (bi >= 0) { lbest[leaf] = fbest[c * F + bi]; lgain[leaf] = c == 0 ? cg0 : cg1; }
+        else { lbest[leaf].feature = -1; lbest[leaf].gain = -INFINITY; lgain[leaf] = -INFINITY; }
+      }
+    }
+    DState o = S;
+    o.cursor = 0ull;
+    if (!go) {
+      o.done = 1;
+      *sout = o;
+    } else {
+      // the split itself (ChooseBlock's second half, without the -inf gain marks)
+      const SplitResult sr = *srp;
+      const int node = nl - 1;
+      const int parent = t.lparent[bl];
+      if (parent >= 0) {
+        if (t.left[parent] == ~bl) t.left[parent] = node; else t.right[parent] = node;
+      }
+      t.feat[node] = sr.feature;
+      t.thr[node] = sr.threshold;
+      t.dleft[node] = sr.default_left;
+      t.is_cat[node] = sr.is_cat;
+      for (int w = 0; w < 8; ++w) t.cat_bits[node * 8 + w] = sr.cat_bits[w];
+      t.left[node] = ~bl;
+      t.right[node] = ~nl;
+      t.gain[node] = sr.gain;
+      t.ival[node] = t.lval[bl];
+      t.iweight[node] = sr.left_h + sr.right_h;
+      t.icount[node] = leaves[bl].gcount;
+      t.lparent[bl] = node; t.lparent[nl] = node;
+      t.lval[bl] = sr.left_out; t.lval[nl] = sr.right_out;
+      t.lweight[bl] = sr.left_h; t.lweight[nl] = sr.right_h;
+      t.lcount[bl] = sr.left_cnt; t.lcount[nl] = sr.right_cnt;
+      const int depth = t.ldepth[bl] + 1;
+      t.ldepth[bl] = depth; t.ldepth[nl] = depth;
+      const DLeaf P = leaves[bl];
+      DLeaf Lc = P, Rc = P;
+      Lc.depth = depth; Rc.depth = depth;
+      Lc.sum_g = sr.left_g; Lc.sum_h = sr.left_h;
+      Rc.sum_g = sr.right_g; Rc.sum_h = sr.right_h;
+      const int mdir = (has_mono && !sr.is_cat) ? static_cast<int>(mono[sr.feature]) : 0;
+      if (mdir != 0) {
+        const double mid = (sr.left_out + sr.right_out) / 2.0;
+        if (mdir < 0) { Lc.lo = fmax(Lc.lo, mid); Rc.hi = fmin(Rc.hi, mid); }
+        else { Lc.hi = fmin(Lc.hi, mid); Rc.lo = fmax(Rc.lo, mid); }
+      }
+      const bool left_small = sr.left_cnt <= sr.right_cnt;
+      Lc.slot = 2 * node + 1;
+      Rc.slot = 2 * node + 2;
+      if (left_small) { Rc.gcount = P.gcount; } else { Lc.gcount = P.gcount; }
+      leaves[bl] = Lc;
+      leaves[nl] = Rc;
+      o.parent_slot = P.slot;
+      o.pbegin = P.begin; o.pcount = P.count; o.pbuf = P.buf;
+      o.split_leaf = bl;
+      o.new_leaf = nl;
+      o.small_leaf = left_small ? bl : nl;
+      o.large_leaf = left_small ? nl : bl;
+      o.num_leaves = nl + 1;
+      o.phase = 1;
+      // every field but the cursor (the other blocks are adding to it)
+      sout->num_leaves = o.num_leaves; sout->done = 0; sout->split_leaf = o.split_leaf; sout->new_leaf = o.new_leaf;
+      sout->small_leaf = o.small_leaf; sout->large_leaf = o.large_leaf; sout->parent_slot = o.parent_slot;
+      sout->max_leaves = o.max_leaves; sout->phase = o.phase;
+      sout->pbegin = o.pbegin; sout->pcount = o.pcount; sout->pbuf = o.pbuf;
+    }
+  }
+  if (!go) return;
+  constexpr int kPartTile = kPartThreads * kPartRows;
+  if (static_cast<int>(blockIdx.x) >= ceil_div_i(pc, kPartTile)) return;
+  PartSplit ps;
+  ps.feature = srp->feature;
+  ps.is_cat = srp->is_cat;
+  ps.dleft = srp->default_left;
+  ps.thr = srp->threshold;
+  ps.nb = fm.num_bin[ps.feature];
+  ps.mt = fm.missing[ps.feature];
+  ps.dbin = fm.default_bin[ps.feature];
+  if (tid < 8) s_cat[tid] = ps.is_cat ? srp->cat_bits[tid] : 0u;
+  __syncthreads();
+  PartitionTiles<kPartRows>(ps, s_cat, pb, pc, pbuf, &sout->cursor, cbins, n, perm0, perm1, ogh0, ogh1, wperm0,
+                            wperm1, wogh0, wogh1, g, h);
 }
 
 // ---------------------------------------------------------------- K7
@@ -2234,11 +2453,24 @@ class GpuBackend : public TrainBackend {
     if (hist_shape_ < 0 || hist_shape_ > 2) hist_shape_ = 2;
     max_hist_blocks_ = hist_shape_ == 0 ? kMaxHistBlocks : kMaxHistBlocks / 2;
     SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_max_hist_blocks), &max_hist_blocks_, sizeof(int)));
+    if (const char* e = std::getenv("SML_FUSED_SPLIT")) fused_split_ = std::atoi(e);
+    if (const char* e = std::getenv("SML_MERGED_CHOOSE")) merged_choose_ = std::atoi(e) != 0;
     {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
+      // choose_part_kernel: every block pays the choose prologue, so keep the grid within one resident
+      // round (A/B on MI355X, 11M x 28: 2048 blocks 2.09-2.10 ms/iter, 1024 1.99-2.01, 768 1.97-2.01, 512 2.01-2.04)
+      if (merged_choose_ && fused_split_ == 0) {
+        int per_cu = 0, cus = 0;
+        auto ck = part_rows_ == 16 ? choose_part_kernel<16> : (part_rows_ == 4 ? choose_part_kernel<4> : choose_part_kernel<8>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ck, kPartThreads, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_) == hipSuccess && per_cu > 0 && cus > 0)
+          part_grid_ = std::max(1, std::min(part_grid_, per_cu * cus));
+        else
+          (void)hipGetLastError();
+      }
+      if (const char* e = std::getenv("SML_PART_GRID")) part_grid_ = std::max(1, std::min(part_grid_, std::atoi(e)));
     }
-    if (const char* e = std::getenv("SML_FUSED_SPLIT")) fused_split_ = std::atoi(e);
     if (const char* e = std::getenv("SML_HIST_MIN_ROWS")) min_rows_hist_ = std::max(256, std::atoi(e));
     {
       // score_grad_hist_kernel: one class, every row in every tree (no bagging / GOSS / RF / DART
@@ -2296,7 +2528,7 @@ class GpuBackend : public TrainBackend {
     n_tu_ = static_cast<size_t>(NI) * 9;
     n_td_ = static_cast<size_t>(NI) * 3 + L_ * 2;
     n_tl_ = static_cast<size_t>(NI) + L_;
-    off_td_ = (sizeof(DState) + 63) / 64 * 64;
+    off_td_ = (2 * sizeof(DState) + 63) / 64 * 64;  // two DState versions (choose_part_kernel) + tree
     off_tl_ = off_td_ + n_td_ * sizeof(double);
     off_ti_ = off_tl_ + n_tl_ * sizeof(int64_t);
     off_tu_ = off_ti_ + n_ti_ * sizeof(int32_t);
@@ -2304,6 +2536,7 @@ class GpuBackend : public TrainBackend {
     if (blob_bytes_ > kPinnedBytes) throw std::runtime_error("GPU backend: tree too large for staging buffer");
     blob_.alloc(blob_bytes_);
     state_ = reinterpret_cast<DState*>(blob_.get());
+    st_cur_ = state_;
     int32_t* ti = reinterpret_cast<int32_t*>(blob_.get() + off_ti_);
     dt_.feat = ti; dt_.dleft = ti + NI; dt_.is_cat = ti + 2 * NI; dt_.left = ti + 3 * NI; dt_.right = ti + 4 * NI;
     dt_.lparent = ti + 6 * NI; dt_.ldepth = ti + 6 * NI + L_;
@@ -2502,6 +2735,9 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipGetLastError());
       pending_parts_ = 0;
     }
+    const bool merged = merged_choose_ && fused_split_ == 0;
+    st_cur_ = state_;
+    st_next_ = merged ? state_ + 1 : nullptr;
     hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_, leaves_.get(), root_count, root_buf, L_,
                        ghmax_partial_.get(), pending_parts_, ghmax_.get());
     SML_HIP_CHECK(hipGetLastError());
@@ -2512,17 +2748,31 @@ class GpuBackend : public TrainBackend {
     } else {
       EnqueueHistogram(g, h);
     }
-    EnqueueFindChoose();
+    EnqueueFindChoose(!merged);
     for (int s = 1; s < L_; ++s) {
-      // partition the chosen leaf, histogram its smaller child, search both
-      auto pk = part_rows_ == 16 ? part_kernel<16> : (part_rows_ == 4 ? part_kernel<4> : part_kernel<8>);
-      hipLaunchKernelGGL(pk, dim3(part_grid_), dim3(kPartThreads), 0, stream_, state_, lbest_.get(),
-                         cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
-                         perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
-      SML_HIP_CHECK(hipGetLastError());
+      // (choose +) partition the chosen leaf, histogram its smaller child, search both
+      if (merged) {
+        DState* sin = st_cur_;
+        DState* sout = st_cur_ == state_ ? state_ + 1 : state_;
+        auto ck = part_rows_ == 16 ? choose_part_kernel<16> : (part_rows_ == 4 ? choose_part_kernel<4> : choose_part_kernel<8>);
+        hipLaunchKernelGGL(ck, dim3(part_grid_), dim3(kPartThreads), 0, stream_, sin, sout, leaves_.get(),
+                           lbest_.get(), lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono,
+                           cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
+                           perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
+        SML_HIP_CHECK(hipGetLastError());
+        st_cur_ = sout;
+        st_next_ = sin;
+      } else {
+        auto pk = part_rows_ == 16 ? part_kernel<16> : (part_rows_ == 4 ? part_kernel<4> : part_kernel<8>);
+        hipLaunchKernelGGL(pk, dim3(part_grid_), dim3(kPartThreads), 0, stream_, st_cur_, lbest_.get(),
+                           cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
+                           perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
+        SML_HIP_CHECK(hipGetLastError());
+      }
       EnqueueHistogram(g, h);
-      EnqueueFindChoose();
+      EnqueueFindChoose(!merged || s == L_ - 1);
     }
+    final_v_ = st_cur_ == state_ ? 0 : 1;
     SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
     // read the tree back (one transfer, one sync)
     Tree t = ReadTree();  // synchronises the stream: every event recorded so far is complete
@@ -2674,7 +2924,7 @@ class GpuBackend : public TrainBackend {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
     if (hist_mode_ == 1) {
       auto hk = hist_unroll_ == 8 ? hist_fl_kernel<8> : (hist_unroll_ == 4 ? hist_fl_kernel<4> : hist_fl_kernel<2>);
-      hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, state_, leaves_.get(),
+      hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, st_cur_, leaves_.get(),
                          reinterpret_cast<const uint32_t*>(bins_.get()), S_ / 4, F_, perm_[0].get(), perm_[1].get(),
                          ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     } else {
@@ -2683,7 +2933,7 @@ class GpuBackend : public TrainBackend {
                 : hist_threads_ == 1024 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024> : hist_kernel<2, 1024>)
                 : hist_threads_ == 256 ? (hist_unroll_ == 4 ? hist_kernel<4, 256> : hist_kernel<2, 256>)
                 : (hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>));
-      hipLaunchKernelGGL(hk, dim3(max_hist_blocks_, FG_), dim3(hist_shape_ == 0 ? hist_threads_ : 1024), 0, stream_, state_,
+      hipLaunchKernelGGL(hk, dim3(max_hist_blocks_, FG_), dim3(hist_shape_ == 0 ? hist_threads_ : 1024), 0, stream_, st_cur_,
                          leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
                          perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     }
@@ -2697,7 +2947,7 @@ class GpuBackend : public TrainBackend {
     const int FP = FG_ * kFeatPerGroup;
     const int ES = hist_mode_ == 1 ? FP * kBinsPerFeature : E_;
     hipLaunchKernelGGL(hist_mode_ == 1 ? hist_reduce_kernel<true> : hist_reduce_kernel<false>,
-                       dim3((ES + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, state_, leaves_.get(),
+                       dim3((ES + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, st_cur_, leaves_.get(),
                        slab_.get(), E_, FP, F_, ghmax, part_.get());
     SML_HIP_CHECK(hipGetLastError());
     if (Distributed()) {
@@ -2710,20 +2960,21 @@ class GpuBackend : public TrainBackend {
 
   bool Distributed() const { return comm_ && comm_->world() > 1; }
 
-  void EnqueueFindChoose() {
+  void EnqueueFindChoose(bool choose_now = true) {
     if (fused_split_) {
       const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
       auto k = (Distributed() || fused_split_ == 2 || hist_mode_ == 1) ? split_kernel<false> : split_kernel<true>;
-      hipLaunchKernelGGL(k, dim3(F_), dim3(kSplitThreads), 0, stream_, state_, leaves_.get(), slab_.get(),
+      hipLaunchKernelGGL(k, dim3(F_), dim3(kSplitThreads), 0, stream_, st_cur_, leaves_.get(), slab_.get(),
                          part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(), F_, lbest_.get(),
                          lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get());
       SML_HIP_CHECK(hipGetLastError());
       return;
     }
-    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, state_, leaves_.get(), part_.get(),
-                       E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
+    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), part_.get(),
+                       E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_, st_next_);
     SML_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, state_, leaves_.get(), lbest_.get(),
+    if (!choose_now) return;  // choose_part_kernel does the choose step with the next partition
+    hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, st_cur_, leaves_.get(), lbest_.get(),
                        lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono);
     SML_HIP_CHECK(hipGetLastError());
   }
@@ -2735,7 +2986,7 @@ class GpuBackend : public TrainBackend {
     if (comm_) comm_->Check();
     const uint8_t* hb = static_cast<const uint8_t*>(pinned_);
     DState st;
-    std::memcpy(&st, hb, sizeof(DState));
+    std::memcpy(&st, hb + final_v_ * sizeof(DState), sizeof(DState));
     const int32_t* ti = reinterpret_cast<const int32_t*>(hb + off_ti_);
     const uint32_t* tu = reinterpret_cast<const uint32_t*>(hb + off_tu_);
     const double* td = reinterpret_cast<const double*>(hb + off_td_);
@@ -2879,7 +3130,11 @@ class GpuBackend : public TrainBackend {
   int hist_mode_ = 0;
   int hist_shape_ = 2, max_hist_blocks_ = kMaxHistBlocks / 2;
   DevBuf<uint8_t> blob_;
-  DState* state_ = nullptr;
+  DState* state_ = nullptr;   // two versions: choose_part_kernel reads one and writes the other
+  DState* st_cur_ = nullptr;  // version the next hist / reduce / find / choose launches read
+  DState* st_next_ = nullptr; // version whose cursor find_split_kernel zeroes (nullptr: none)
+  int final_v_ = 0;           // version holding the finished tree's state
+  bool merged_choose_ = true; // SML_MERGED_CHOOSE=0: separate choose_kernel + part_kernel launches
   size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
   size_t off_td_ = 0, off_tl_ = 0, off_ti_ = 0, off_tu_ = 0, blob_bytes_ = 0;
   DevBuf<uint8_t> up_blob_;  // uploaded score-update tree: nodes | cat words | leaf values
