@@ -47,6 +47,14 @@ class TrainBackend {
     return false;
   }
   virtual Tree TrainTree(int k, const std::vector<char>& feature_mask) = 0;
+  // Grow a tree and, when the backend can, apply score[k] += shrink * tree(row) right behind the
+  // growth on the device (no host round trip between them); *updated tells the caller whether
+  // it still has to call UpdateScore(t, k, 1.0) with the returned (unshrunk) tree shrunk by `shrink`.
+  virtual Tree TrainTreeAndUpdateScore(int k, const std::vector<char>& feature_mask, double shrink, bool* updated) {
+    (void)shrink;
+    *updated = false;
+    return TrainTree(k, feature_mask);
+  }
   // score[k] += scale * tree(row) for every training row
   virtual void UpdateScore(const Tree& t, int k, double scale) = 0;
   // Leaf index of every training row for `t` (renew / DART helpers).

@@ -2302,9 +2302,20 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, co
 // us at 11M x 28 on MI355X, three full passes over rows).
 constexpr int kPrepMaxNodes = 255;  // trees up to 256 leaves keep nodes + values in LDS
 
+// The tree just grown, read where it was built (TrainTreeAndUpdateScore): nodes are encoded as
+// UploadTree encodes them on the host, leaf values are lval * shrink (the host's Tree::Shrink).
+struct DevTreeSrc {
+  DTree t;
+  const DState* st;  // final state version (num_leaves); nullptr: use the uploaded DevTreeView
+  const int32_t* num_bin;
+  const int32_t* missing;
+  const int32_t* default_bin;
+  double shrink;
+};
+
 template <int kUnroll, int kThreads = kHistThreads, int kCopies = 1>
 __global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
-    DevTreeView tv, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
+    DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
     float* __restrict__ g, float* __restrict__ h, const float* __restrict__ bound, float* __restrict__ partial,
     int2* __restrict__ slab) {
@@ -2314,11 +2325,25 @@ __global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
   __shared__ int4 snodes[kPrepMaxNodes];
   __shared__ double slval[kPrepMaxNodes + 1];
   const int tid = threadIdx.x;
-  const int ni = tv.num_leaves - 1;
+  const int num_leaves = src.st ? src.st->num_leaves : tv.num_leaves;
+  const int ni = num_leaves - 1;
+  const uint32_t* cat_bits = src.st ? src.t.cat_bits : tv.cat_bits;
   for (int i = tid; i < kCopies * kFeatPerGroup * kHistStride; i += kThreads) shc[i] = 0ull;
   unsigned long long* sh = shc + (kCopies > 1 && tid >= kThreads / 2 ? kFeatPerGroup * kHistStride : 0);
-  for (int i = tid; i < ni; i += kThreads) snodes[i] = tv.nodes[i];
-  for (int i = tid; i < tv.num_leaves; i += kThreads) slval[i] = tv.lval[i];
+  if (src.st) {
+    for (int i = tid; i < ni; i += kThreads) {
+      const int f = src.t.feat[i], ic = src.t.is_cat[i] ? 1 : 0;
+      const int mt = ic ? kMissingNaN : src.missing[f];
+      const int dl = ic ? 0 : (src.t.dleft[i] ? 1 : 0);
+      const int mbin = mt == kMissingNaN ? src.num_bin[f] - 1 : (mt == kMissingZero ? src.default_bin[f] : 0);
+      snodes[i] = make_int4(f | (mt << 16) | (dl << 18) | (ic << 19) | (mbin << 20), static_cast<int>(src.t.thr[i]),
+                            src.t.left[i], src.t.right[i]);
+    }
+    for (int i = tid; i < num_leaves; i += kThreads) slval[i] = src.t.lval[i] * src.shrink;
+  } else {
+    for (int i = tid; i < ni; i += kThreads) snodes[i] = tv.nodes[i];
+    for (int i = tid; i < num_leaves; i += kThreads) slval[i] = tv.lval[i];
+  }
   __syncthreads();
   const int chunk = ceil_div_i(n, nb_active);
   const int p0 = blockIdx.x * chunk;
@@ -2346,9 +2371,9 @@ __global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
       const int i = base + u * kThreads;
       if (i >= p1) continue;
       int node = ni > 0 ? 0 : ~0;
-      for (int guard = 0; node >= 0 && guard < tv.num_leaves; ++guard) {
+      for (int guard = 0; node >= 0 && guard < num_leaves; ++guard) {
         const int4 nd = snodes[node];
-        node = NodeStep(nd, ByteOfRow(b0[u], b1[u], nd.x & 0xFFFF), tv.cat_bits, node);
+        node = NodeStep(nd, ByteOfRow(b0[u], b1[u], nd.x & 0xFFFF), cat_bits, node);
       }
       const double sn = s[u] + scale * slval[ni > 0 ? ~node : 0];
       score[i] = sn;
@@ -2393,6 +2418,7 @@ class GpuBackend : public TrainBackend {
   ~GpuBackend() override {
     if (stream_) { (void)hipStreamSynchronize(stream_); (void)hipStreamDestroy(stream_); }
     for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
+    if (ev_copy_) (void)hipEventDestroy(ev_copy_);
     if (pinned_) (void)hipHostFree(pinned_);
   }
   std::string Name() const override { return "hip"; }
@@ -2552,6 +2578,7 @@ class GpuBackend : public TrainBackend {
     leaf_idx_.alloc(n_);
     SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
     for (hipEvent_t& e : ev_) SML_HIP_CHECK(hipEventCreate(&e));
+    SML_HIP_CHECK(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) stats.device_mem_mb = (total_b - free_b) / 1048576.0;
@@ -2705,6 +2732,32 @@ class GpuBackend : public TrainBackend {
 
   Tree TrainTree(int k, const std::vector<char>& fmask_in) override {
     roctxRangePushA("sml::TrainTree");
+    GrowTree(k, fmask_in);
+    EnqueueTreeCopy();
+    Tree t = FinishTree();
+    AccountScoreTime();
+    roctxRangePop();
+    return t;
+  }
+
+  // Grow the tree and run the fused score / next-gradient / next-root-histogram pass on the device
+  // tree right behind it: the host reads the tree back while that pass runs.
+  Tree TrainTreeAndUpdateScore(int k, const std::vector<char>& fmask_in, double shrink, bool* updated) override {
+    *updated = false;
+    if (!(prep_armed_ && k == 0 && K_ == 1 && L_ <= kPrepMaxNodes + 1)) return TrainTree(k, fmask_in);
+    roctxRangePushA("sml::TrainTreeAndUpdateScore");
+    GrowTree(k, fmask_in);
+    EnqueueTreeCopy();
+    AccountScoreTime();  // the previous pass (done before this growth) frees the event pair
+    DevTreeSrc src{dt_, state_ + final_v_, fm_.num_bin, fm_.missing, fm_.default_bin, shrink};
+    LaunchPrep(DevTreeView{}, src, 1.0);
+    Tree t = FinishTree();
+    *updated = true;
+    roctxRangePop();
+    return t;
+  }
+
+  void GrowTree(int k, const std::vector<char>& fmask_in) {
     SML_HIP_CHECK(hipEventRecord(ev_[0], stream_));
     std::vector<int8_t> fmask(F_, 1);
     for (int f = 0; f < F_ && f < static_cast<int>(fmask_in.size()); ++f) fmask[f] = fmask_in[f] ? 1 : 0;
@@ -2774,12 +2827,19 @@ class GpuBackend : public TrainBackend {
     }
     final_v_ = st_cur_ == state_ ? 0 : 1;
     SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
-    // read the tree back (one transfer, one sync)
-    Tree t = ReadTree();  // synchronises the stream: every event recorded so far is complete
+  }
+
+  // the finished tree (state + arrays: one allocation) -> pinned host memory, one transfer
+  void EnqueueTreeCopy() {
+    SML_HIP_CHECK(hipMemcpyAsync(pinned_, blob_.get(), blob_bytes_, hipMemcpyDeviceToHost, stream_));
+    SML_HIP_CHECK(hipEventRecord(ev_copy_, stream_));
+  }
+
+  Tree FinishTree() {
+    SML_HIP_CHECK(hipEventSynchronize(ev_copy_));
+    Tree t = ReadTree();
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ev_[0], ev_[1]) == hipSuccess) stats.device_tree_ms += ms;
-    AccountScoreTime();
-    roctxRangePop();
     return t;
   }
 
@@ -2789,15 +2849,7 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
     prep_valid_ = root_ready_ = false;
     if (prep_armed_ && k == 0 && t.num_leaves <= kPrepMaxNodes + 1) {
-      // score update + next gradients + next root histogram in one pass (see score_grad_hist_kernel)
-      auto pk = hist_shape_ == 1 ? score_grad_hist_kernel<2, 1024, 2>
-                : hist_shape_ == 2 ? score_grad_hist_kernel<2, 1024, 1> : score_grad_hist_kernel<2, kHistThreads, 1>;
-      hipLaunchKernelGGL(pk, dim3(max_hist_blocks_), dim3(hist_shape_ == 0 ? kHistThreads : 1024), 0, stream_, tv,
-                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, static_cast<int32_t>(n_), scale,
-                         score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
-                         reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
-      SML_HIP_CHECK(hipGetLastError());
-      prep_valid_ = true;
+      LaunchPrep(tv, DevTreeSrc{}, scale);  // score update + next gradients + next root histogram, one pass
     } else {
       hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
                          reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
@@ -2836,8 +2888,28 @@ class GpuBackend : public TrainBackend {
   const double* CountSlot() const { return reinterpret_cast<const double*>(part_.get() + E_); }
 
   // device time of the last score update; call only after a stream sync
+  // score update + next gradients + next root histogram in one pass (score_grad_hist_kernel) with
+  // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
+  void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
+    if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
+    auto pk = hist_shape_ == 1 ? score_grad_hist_kernel<2, 1024, 2>
+              : hist_shape_ == 2 ? score_grad_hist_kernel<2, 1024, 1> : score_grad_hist_kernel<2, kHistThreads, 1>;
+    hipLaunchKernelGGL(pk, dim3(max_hist_blocks_), dim3(hist_shape_ == 0 ? kHistThreads : 1024), 0, stream_, tv, src,
+                       reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, static_cast<int32_t>(n_), scale,
+                       score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
+                       reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    if (src.st) {
+      SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
+      score_pending_ = true;
+    }
+    prep_valid_ = true;
+    root_ready_ = false;
+  }
+
   void AccountScoreTime() {
     if (!score_pending_) return;
+    SML_HIP_CHECK(hipEventSynchronize(ev_[3]));
     float sms = 0.f;
     if (hipEventElapsedTime(&sms, ev_[2], ev_[3]) == hipSuccess) stats.device_score_ms += sms;
     score_pending_ = false;
@@ -2979,10 +3051,9 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipGetLastError());
   }
 
+  // parse the tree copied by EnqueueTreeCopy (the caller has waited for the copy)
   Tree ReadTree() {
     const int NI = L_ - 1;
-    SML_HIP_CHECK(hipMemcpyAsync(pinned_, blob_.get(), blob_bytes_, hipMemcpyDeviceToHost, stream_));
-    SML_HIP_CHECK(hipStreamSynchronize(stream_));
     if (comm_) comm_->Check();
     const uint8_t* hb = static_cast<const uint8_t*>(pinned_);
     DState st;
@@ -3080,6 +3151,7 @@ class GpuBackend : public TrainBackend {
 
   static constexpr size_t kPinnedBytes = 4 << 20;
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};  // tree start/end, score start/end
+  hipEvent_t ev_copy_ = nullptr;                               // tree copied to pinned memory
   bool score_pending_ = false;
   int dev_ = -1;
   hipStream_t stream_ = nullptr;

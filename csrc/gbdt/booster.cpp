@@ -303,9 +303,15 @@ bool Booster::TrainOneIter(const float* grad, const float* hess) {
   // ---- grow one tree per class
   bool any_split = false;
   std::vector<Tree> new_trees;
+  // plain boosting: the backend may apply the shrunk tree to the scores right behind its growth
+  const bool device_update = !is_rf && !is_dart && !objective_->NeedRenewTreeOutput();
+  std::vector<char> updated(K, 0);
   for (int k = 0; k < K; ++k) {
     std::vector<char> fmask = SampleFeatures();
-    Tree t = backend_->TrainTree(k, fmask);
+    bool upd = false;
+    Tree t = device_update ? backend_->TrainTreeAndUpdateScore(k, fmask, cfg_.learning_rate, &upd)
+                           : backend_->TrainTree(k, fmask);
+    updated[k] = upd ? 1 : 0;
     if (t.num_leaves > 1) {
       any_split = true;
       if (objective_->NeedRenewTreeOutput()) {
@@ -346,7 +352,7 @@ bool Booster::TrainOneIter(const float* grad, const float* hess) {
       backend_->ScaleScore(k, c / (c + 1.0));
       backend_->UpdateScore(t, k, 1.0 / (c + 1.0));
     } else {
-      backend_->UpdateScore(t, k, 1.0);
+      if (!updated[k]) backend_->UpdateScore(t, k, 1.0);
       if (!boosted_first_ && CurrentIteration() == 0) t.AddBias(init_scores_[k]);
     }
   }
