@@ -255,6 +255,10 @@ class CognitiveServicesBase(Transformer, HasServiceParams, ConcurrencyParams, Ha
             return s
 
     # --------------------------------------------------------------- execution
+    def _modify_polling_url(self, url: str) -> str:
+        """Hook for services whose polling URL needs extra query parameters (reference: modifyPollingURI)."""
+        return url
+
     def _poll(self, session, resp, headers) -> dict:
         loc = None
         for h in resp["headers"]:
@@ -262,6 +266,7 @@ class CognitiveServicesBase(Transformer, HasServiceParams, ConcurrencyParams, Ha
                 loc = h["value"]
         if not loc:
             return resp
+        loc = self._modify_polling_url(loc)
         delay = self.getPollingDelay() / 1000.0
         auth = {k: v for k, v in headers.items() if k != "Content-Type"}
         for _ in range(self.getMaxPollingRetries()):

@@ -13,7 +13,8 @@ import numpy as np
 from ..core.dataframe import DataFrame
 from ..core.params import Param, TypeConverters as T
 from ..core.pipeline import Transformer
-from .base import CognitiveServicesBase, HasAPIVersion, HasAsyncReply, ServiceParam
+from ..io.http import error_of
+from .base import CognitiveServicesBase, HasAPIVersion, HasAsyncReply, ServiceParam, _obj
 
 
 # ---------------------------------------------------------------------- speech
@@ -32,9 +33,121 @@ class SpeechToText(CognitiveServicesBase):
         return bytes(vals["audioData"]), "audio/wav; codecs=audio/pcm; samplerate=16000"
 
 
+def wav_chunks(data: bytes, max_seconds: float) -> List[tuple]:
+    """Split a PCM WAV file into (offset_seconds, wav_bytes) pieces of at most ``max_seconds`` (the reference
+    streams a WavStream into the SDK; the short-audio REST endpoint takes <= 60 s per request)."""
+    import io
+    import wave
+
+    with wave.open(io.BytesIO(bytes(data)), "rb") as w:
+        params = w.getparams()
+        rate = w.getframerate()
+        frames = w.readframes(w.getnframes())
+    step = max(1, int(max_seconds * rate))
+    fbytes = params.sampwidth * params.nchannels
+    out = []
+    for f0 in range(0, max(1, len(frames) // fbytes), step):
+        buf = io.BytesIO()
+        with wave.open(buf, "wb") as o:
+            o.setparams(params)
+            o.writeframes(frames[f0 * fbytes:(f0 + step) * fbytes])
+        out.append((f0 / rate, buf.getvalue()))
+    return out
+
+
+_AUDIO_TYPES = {"wav": "audio/wav; codecs=audio/pcm; samplerate=16000", "ogg": "audio/ogg; codecs=opus"}
+
+
 class SpeechToTextSDK(SpeechToText):
-    """The reference streams audio through the Speech SDK; without the SDK this sends each row's audio to the
-    REST endpoint in one request (same output fields: RecognitionStatus, DisplayText, Offset, Duration)."""
+    """Continuous recognition of arbitrarily long audio (reference: SpeechToTextSDK.scala:44-510). The
+    reference streams the audio through the native Speech SDK; that SDK does not exist for this platform,
+    so WAV audio is cut into pieces the short-audio REST endpoint accepts (``chunkSeconds``) and each
+    piece is recognised in turn: the output is the list of per-piece results (``Offset`` shifted to the
+    position in the whole file, in 100-ns ticks as the SDK reports it), or, with
+    ``streamIntermediateResults``, one output row per result (the reference's flatMap of the stream).
+    OGG/OPUS is sent whole; other compressed formats (the SDK's CompressedStream: mp3, flac, ...) need a
+    decoder and are rejected with a clear error."""
+
+    fileType = ServiceParam("The file type of the sound files, supported types: wav, ogg, mp3", default="wav")
+    streamIntermediateResults = Param("Whether or not to immediately return itermediate results, or group in "
+                                      "a sequence", True, T.toBoolean)
+    wordLevelTimestamps = ServiceParam("Whether to request timestamps foe each indivdual word", default=False)
+    endpointId = ServiceParam("endpoint for custom speech models", url_param=True, payload_name="cid")
+    chunkSeconds = Param("longest audio piece sent in one request (the REST limit is 60 s)", 55.0, T.toFloat)
+
+    def _query(self, vals):
+        q = super()._query(vals)
+        if vals.get("wordLevelTimestamps"):
+            q.append(("wordLevelTimestamps", "true"))
+        return q
+
+    def _pieces(self, vals) -> List[tuple]:
+        ftype = str(vals.get("fileType", "wav")).lower()
+        if ftype not in _AUDIO_TYPES:
+            raise ValueError(f"{type(self).__name__}: fileType {ftype!r} needs an audio decoder that is not "
+                             f"available; supported: {sorted(_AUDIO_TYPES)}")
+        data = bytes(vals["audioData"])
+        return wav_chunks(data, self.getChunkSeconds()) if ftype == "wav" else [(0.0, data)]
+
+    def _transform(self, df):
+        import requests
+
+        reqs, allvals = self._requests_for(df)
+        session = requests.Session()
+        results, errs = [], []
+        for req, vals in zip(reqs, allvals):
+            if req is None:
+                results.append(None)
+                errs.append(None)
+                continue
+            method, url, headers, _ = req
+            pieces = self._pieces(vals)
+            h = dict(headers, **{"Content-Type": _AUDIO_TYPES[str(vals.get("fileType", "wav")).lower()]})
+            row_res, row_err = [], None
+            for off, piece in pieces:
+                resp = self._send(session, (method, url, h, piece))
+                err = error_of(resp)
+                if err is not None:
+                    row_err = err
+                    break
+                r = self._parse(resp)
+                if isinstance(r, dict):
+                    r = self._decorate(dict(r), vals)
+                    if "Offset" in r:
+                        r["Offset"] = int(r["Offset"]) + int(round(off * 1e7))
+                row_res.append(r)
+            results.append(row_res if row_err is None else None)
+            errs.append(row_err)
+        if not self.getStreamIntermediateResults():
+            return df.withColumn(self.getOutputCol(), _obj(results)).withColumn(self.getErrorCol(), _obj(errs))
+        idx, outs, oerr = [], [], []
+        for i, (rs, e) in enumerate(zip(results, errs)):
+            for r in (rs or [None]):
+                idx.append(i)
+                outs.append(r)
+                oerr.append(e)
+        out = df._take_rows(np.asarray(idx, dtype=np.int64))
+        return out.withColumn(self.getOutputCol(), _obj(outs)).withColumn(self.getErrorCol(), _obj(oerr))
+
+    def _decorate(self, r: dict, vals) -> dict:
+        return r
+
+
+class ConversationTranscription(SpeechToTextSDK):
+    """Multi-speaker transcription (reference: SpeechToTextSDK.scala:511-600, ConversationTranscriber). The
+    REST endpoint does not separate speakers, so every result carries ``SpeakerId = "Unidentified"`` (the
+    value the SDK itself reports for voices it cannot match); ``participantsJson`` is validated and kept
+    for API parity."""
+
+    participantsJson = ServiceParam("a json representation of a list of conversation participants (email, "
+                                    "language, user)")
+
+    def _decorate(self, r: dict, vals) -> dict:
+        if vals.get("participantsJson"):
+            json.loads(vals["participantsJson"])  # malformed participant lists fail like the SDK call would
+        r.setdefault("SpeakerId", "Unidentified")
+        r.setdefault("Type", "ConversationTranscription")
+        return r
 
 
 class TextToSpeech(CognitiveServicesBase):
@@ -280,5 +393,5 @@ class CheckPointInPolygon(_MapsBase):
         return parsed
 
 
-__all__ = ["SpeechToText", "SpeechToTextSDK", "TextToSpeech", "SpeakerEmotionInference", "BingImageSearch",
+__all__ = ["SpeechToText", "SpeechToTextSDK", "ConversationTranscription", "wav_chunks", "TextToSpeech", "SpeakerEmotionInference", "BingImageSearch",
            "AzureSearchWriter", "AddDocuments", "AddressGeocoder", "ReverseAddressGeocoder", "CheckPointInPolygon"]

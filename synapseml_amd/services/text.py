@@ -11,6 +11,7 @@ from __future__ import annotations
 import json
 from typing import Any, Dict, List
 
+from ..core.params import Param, TypeConverters as T
 from .base import CognitiveServicesBase, HasAPIVersion, HasAsyncReply, ServiceParam
 
 
@@ -101,6 +102,66 @@ class AnalyzeHealthText(TextAnalyticsBase, HasAsyncReply):
 
     def _postprocess(self, parsed, vals):
         return _unpack(parsed.get("results", parsed) if isinstance(parsed, dict) else parsed, vals)
+
+
+_ANALYZE_TASKS = (  # (include param, params param, request task list, output field)
+    ("includeEntityRecognition", "entityRecognitionParams", "entityRecognitionTasks", "entityRecognition"),
+    ("includeEntityLinking", "entityLinkingParams", "entityLinkingTasks", "entityLinking"),
+    ("includePii", "piiParams", "entityRecognitionPiiTasks", "pii"),
+    ("includeKeyPhraseExtraction", "keyPhraseExtractionParams", "keyPhraseExtractionTasks", "keyPhraseExtraction"),
+    ("includeSentimentAnalysis", "sentimentAnalysisParams", "sentimentAnalysisTasks", "sentimentAnalysis"),
+)
+
+
+class TextAnalyze(TextAnalyticsBase, HasAsyncReply):
+    """Several Text Analytics tasks over the same documents in one asynchronous ``/analyze`` job
+    (reference: TextAnalytics.scala:488-703). The output holds, per document, one record with
+    ``entityRecognition``, ``entityLinking``, ``pii``, ``keyPhraseExtraction`` and
+    ``sentimentAnalysis`` (null for tasks that were not included), each that task's per-document
+    result (the reference's UnpackedTextAnalyzeResponse)."""
+
+    url_path = "/text/analytics/v3.1/analyze"
+    includeEntityRecognition = Param("Whether to perform entity recognition", True, T.toBoolean)
+    entityRecognitionParams = Param("the parameters to pass to the entity recognition model",
+                                    {"model-version": "latest"}, T.toDictStrStr)
+    includePii = Param("Whether to perform PII Detection", True, T.toBoolean)
+    piiParams = Param("the parameters to pass to the PII model", {"model-version": "latest"}, T.toDictStrStr)
+    includeEntityLinking = Param("Whether to perform EntityLinking", True, T.toBoolean)
+    entityLinkingParams = Param("the parameters to pass to the entityLinking model",
+                                {"model-version": "latest"}, T.toDictStrStr)
+    includeKeyPhraseExtraction = Param("Whether to perform KeyPhraseExtraction", True, T.toBoolean)
+    keyPhraseExtractionParams = Param("the parameters to pass to the keyPhraseExtraction model",
+                                      {"model-version": "latest"}, T.toDictStrStr)
+    includeSentimentAnalysis = Param("Whether to perform SentimentAnalysis", True, T.toBoolean)
+    sentimentAnalysisParams = Param("the parameters to pass to the sentimentAnalysis model",
+                                    {"model-version": "latest"}, T.toDictStrStr)
+
+    def _entity(self, vals):
+        tasks = {}
+        for inc, prm, key, _ in _ANALYZE_TASKS:
+            tasks[key] = [{"parameters": dict(self.getOrDefault(prm))}] if self.getOrDefault(inc) else []
+        body = {"displayName": "SynapseML", "analysisInput": {"documents": _docs(vals)}, "tasks": tasks}
+        return json.dumps(body).encode("utf-8"), "application/json"
+
+    def _modify_polling_url(self, url: str) -> str:
+        # the job pages 20 documents by default; the API takes the first $top it sees
+        base, _, query = url.partition("?")
+        return base + "?$top=25" + ("&" + query if query else "")
+
+    def _postprocess(self, parsed, vals):
+        if not isinstance(parsed, dict) or "tasks" not in parsed:
+            return parsed
+        tasks = parsed["tasks"]
+        per_task = {}
+        for _, _, key, field in _ANALYZE_TASKS:
+            lst = tasks.get(key) or []
+            per_task[field] = _unpack(lst[0].get("results", {}), dict(vals, text=vals["text"])) if lst else None
+        single = isinstance(vals["text"], str)
+        n = 1 if single else len(vals["text"])
+        docs = []
+        for i in range(n):
+            docs.append({f: (None if r is None else (r if single else r[i])) for f, r in per_task.items()})
+        return docs[0] if single else docs
 
 
 class AnalyzeText(CognitiveServicesBase, HasAPIVersion):

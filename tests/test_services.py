@@ -345,3 +345,118 @@ def test_langchain_transformer_rows_errors_env_and_persistence(tmp_path):
     assert back.transform(df)["a"].tolist() == ["HI", None, "THERE"]
     with pytest.raises(ValueError):
         S.LangchainTransformer(inputCol="q", outputCol="a").transform(df)
+
+
+def test_text_analyze_tasks_and_unpack(mock):
+    def start(p, q, h, b):
+        body = json.loads(b)
+        assert body["tasks"]["entityRecognitionTasks"] == [{"parameters": {"model-version": "latest"}}]
+        assert body["tasks"]["keyPhraseExtractionTasks"] == []
+        state["docs"] = body["analysisInput"]["documents"]
+        r = make_response("", 202, "Accepted")
+        r["headers"].append({"name": "Operation-Location", "value": m.base + "/analyze/jobs/7?x=1"})
+        return r
+
+    def poll(p, q, h, b):
+        assert q["$top"] == ["25"] and q["x"] == ["1"]
+        res = lambda tag: [{"results": {"documents": [{"id": d["id"], "tag": tag} for d in state["docs"]],
+                                        "errors": []}}]
+        return make_response({"status": "succeeded", "tasks": {
+            "entityRecognitionTasks": res("ner"), "entityLinkingTasks": res("link"),
+            "entityRecognitionPiiTasks": res("pii"), "keyPhraseExtractionTasks": [],
+            "sentimentAnalysisTasks": res("sent")}})
+
+    state = {}
+    m = mock({"/analyze": start, "/analyze/jobs/7": poll})
+    t = S.TextAnalyze(url=m.base + "/text/analytics/v3.1/analyze", outputCol="o", pollingDelay=1) \
+        .setSubscriptionKey("k").setTextCol("t").setIncludeKeyPhraseExtraction(False)
+    out = t.transform(DataFrame({"t": _obj([["a", "b"], "c"])}))["o"].tolist()
+    assert [d["entityRecognition"]["tag"] for d in out[0]] == ["ner", "ner"]
+    assert out[0][1]["pii"]["id"] == "1" and out[0][0]["keyPhraseExtraction"] is None
+    assert out[1]["sentimentAnalysis"]["tag"] == "sent"
+
+
+def test_multivariate_fit_detect_and_last(mock, tmp_path):
+    ts = [f"2021-01-01T00:0{i}:00Z" for i in range(6)]
+    df = DataFrame({"timestamp": _obj(ts[::-1]), "a": np.arange(6.0)[::-1].copy(), "b": np.ones(6)})
+    seen = {}
+
+    def train(p, q, h, b):
+        body = json.loads(b)
+        seen["train"] = body
+        r = make_response("", 201, "Created")
+        r["headers"].append({"name": "Location", "value": m.base + "/multivariate/models/m1"})
+        return r
+
+    def model(p, q, h, b):
+        seen["polls"] = seen.get("polls", 0) + 1
+        st = "RUNNING" if seen["polls"] < 2 else "READY"
+        return make_response({"modelId": "m1", "modelInfo": {"status": st, "diagnosticsInfo": {"x": 1}}})
+
+    def batch(p, q, h, b):
+        seen["batch"] = json.loads(b)
+        r = make_response("", 202, "Accepted")
+        return make_response({"resultId": "r9", "summary": {"status": "CREATED"}}, 202, "Accepted")
+
+    def result(p, q, h, b):
+        return make_response({"summary": {"status": "READY"}, "results": [
+            {"timestamp": t, "value": {"isAnomaly": i == 3, "severity": 0.5 * (i == 3)}} for i, t in enumerate(ts)]})
+
+    def last(p, q, h, b):
+        body = json.loads(b)
+        seen.setdefault("last", []).append(body)
+        tl = body["variables"][0]["timestamps"][-1]
+        return make_response({"results": [{"timestamp": tl, "value": {"isAnomaly": tl.endswith("05:00Z")}}]})
+
+    m = mock({"/models": train, "/models/m1": model, "/m1:detect-batch": batch, "/detect-batch/r9": result,
+              "/m1:detect-last": last})
+    est = S.SimpleFitMultivariateAnomaly(url=m.base + "/multivariate/models", pollingDelay=1, inputCols=["a", "b"],
+                                         intermediateSaveDir=str(tmp_path), startTime="2021-01-01T00:00:00Z",
+                                         endTime="2021-01-01T00:05:00Z").setSubscriptionKey("k")
+    model_ = est.fit(df)
+    assert seen["train"]["dataSchema"] == "OneTable" and seen["train"]["slidingWindow"] == 300
+    assert seen["train"]["alignPolicy"] == {"alignMode": "Outer", "fillNAMethod": "Linear"}
+    csv = open(seen["train"]["dataSource"]).read().splitlines()
+    assert csv[0] == "timestamp,a,b" and csv[1].startswith("2021-01-01T00:00:00Z,0.0")  # sorted by time
+    assert model_.getModelId() == "m1" and model_.getDiagnosticsInfo() == {"x": 1}
+    out = model_.transform(df)
+    assert out["timestamp"].tolist() == ts and out["isAnomaly"].tolist() == [i == 3 for i in range(6)]
+    assert seen["batch"]["topContributorCount"] == 10
+    dl = S.DetectLastMultivariateAnomaly(url=m.base + "/multivariate/models", modelId="m1", batchSize=2,
+                                         inputVariablesCols=["a", "b"], outputCol="o").setSubscriptionKey("k")
+    o2 = dl.transform(df)
+    assert o2["isAnomaly"].tolist() == [False] * 5 + [True]
+    assert [len(x["variables"][0]["values"]) for x in seen["last"]] == [1, 2, 3, 3, 3, 3]
+
+
+def test_speech_sdk_chunks_long_wav_and_conversation(mock):
+    import io
+    import wave
+
+    buf = io.BytesIO()
+    with wave.open(buf, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(1000)
+        w.writeframes(b"\x00\x01" * 2500)  # 2.5 s
+    calls = []
+
+    def rec(p, q, h, b):
+        calls.append((h["content-type"], len(b)))
+        return make_response({"RecognitionStatus": "Success", "DisplayText": f"part{len(calls)}", "Offset": 5,
+                              "Duration": 10})
+
+    m = mock({"/cognitiveservices/v1": rec})
+    df = DataFrame({"audio": _obj([buf.getvalue()])})
+    t = S.SpeechToTextSDK(url=m.base + "/speech/recognition/conversation/cognitiveservices/v1", outputCol="o",
+                          chunkSeconds=1.0).setSubscriptionKey("k").setAudioDataCol("audio").setLanguage("en-US")
+    out = t.transform(df)
+    assert len(calls) == 3 and calls[0][0].startswith("audio/wav")
+    assert out["o"].tolist()[1]["Offset"] == 5 + 10_000_000 and out.count() == 3
+    t2 = S.ConversationTranscription(url=t.getUrl(), outputCol="o", chunkSeconds=2.0, streamIntermediateResults=False) \
+        .setSubscriptionKey("k").setAudioDataCol("audio").setParticipantsJson('[{"name": "a"}]')
+    res = t2.transform(df)["o"].tolist()[0]
+    assert [r["SpeakerId"] for r in res] == ["Unidentified"] * 2
+    with pytest.raises(ValueError):
+        S.SpeechToTextSDK(url=t.getUrl()).setSubscriptionKey("k").setAudioDataCol("audio").setFileType("mp3") \
+            .transform(df)
