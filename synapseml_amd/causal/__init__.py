@@ -54,6 +54,28 @@ class ResidualTransformer(Transformer):
         return df.withColumn(self.getOutputCol(), obs - p)
 
 
+class OrthoForestVariableTransformer(Transformer):
+    """Per-row target and weight of the orthogonal forest: outcome residual / treatment residual and
+    treatment residual squared (reference: causal/OrthoForestVariableTransformer.scala:23-88)."""
+
+    treatmentResidualCol = Param("Treatment Residual Col", "TResid", T.toString)
+    outcomeResidualCol = Param("Outcome Residual Col", "OResid", T.toString)
+    outputCol = Param("The name of the output column", "_tmp_tsOutcome", T.toString)
+    weightsCol = Param("Weights Col", "_tmp_twOutcome", T.toString)
+
+    def _transform(self, df):
+        cols = {}
+        for name in (self.getTreatmentResidualCol(), self.getOutcomeResidualCol()):
+            c = df[name]
+            if not np.issubdtype(c.dtype, np.floating):
+                raise TypeError(f"{name} must be of type double, got {c.dtype}")
+            cols[name] = c.astype(np.float64)
+        t, o = cols[self.getTreatmentResidualCol()], cols[self.getOutcomeResidualCol()]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = o / t
+        return df.withColumn(self.getOutputCol(), ratio).withColumn(self.getWeightsCol(), t * t)
+
+
 class _DMLParams(HasFeaturesCol, HasWeightCol):
     treatmentCol = Param("treatment column", "treatment", T.toString)
     outcomeCol = Param("outcome column", "outcome", T.toString)
@@ -174,7 +196,10 @@ class OrthoForestDMLEstimator(Estimator, _DMLParams):
         tres = np.concatenate([p[1] for p in parts])
         yres = np.concatenate([p[2] for p in parts])
         safe = np.where(np.abs(tres) < 1e-6, np.sign(tres + 1e-12) * 1e-6, tres)
-        target = yres / safe
+        tr_col, or_col = self.getTreatmentResidualCol(), self.getOutcomeResidualCol()
+        vt = OrthoForestVariableTransformer(treatmentResidualCol=tr_col, outcomeResidualCol=or_col).transform(
+            DataFrame({tr_col: safe, or_col: yres}))
+        target = vt["_tmp_tsOutcome"]
         wts = tres * tres
         rng = np.random.default_rng(0)
         forest = []
@@ -383,4 +408,5 @@ class SyntheticDiffInDiffEstimator(Estimator, _SyntheticParams):
 
 __all__ = ["DoubleMLEstimator", "DoubleMLModel", "OrthoForestDMLEstimator", "OrthoForestDMLModel",
            "DiffInDiffEstimator", "DiffInDiffModel", "DiffInDiffSummary", "SyntheticControlEstimator",
-           "SyntheticDiffInDiffEstimator", "ResidualTransformer", "simplex_least_squares"]
+           "SyntheticDiffInDiffEstimator", "ResidualTransformer", "OrthoForestVariableTransformer",
+           "simplex_least_squares"]

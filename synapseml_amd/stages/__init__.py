@@ -1,6 +1,7 @@
 """General-purpose pipeline stages (reference: core/.../stages/*.scala,
 SURVEY §2.2.5 "Mini-batching" and "Other stages")."""
-from .batching import (DynamicMiniBatchTransformer, FixedMiniBatchTransformer, FlattenBatch, HasMiniBatcher,
+from .batching import (DynamicBufferedBatcher, DynamicMiniBatchTransformer, FixedBatcher, FixedBufferedBatcher,
+                       FixedMiniBatchTransformer, FlattenBatch, HasMiniBatcher, TimeIntervalBatcher,
                        TimeIntervalMiniBatchTransformer)
 from .basic import (Cacher, ClassBalancer, ClassBalancerModel, DropColumns, EnsembleByKey, Explode, Lambda,
                     MultiColumnAdapter, PartitionConsolidator, RenameColumn, Repartition, SelectColumns,

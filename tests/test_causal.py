@@ -80,3 +80,19 @@ def test_simplex_ls_and_synthetic_estimators():
     sdid = SyntheticDiffInDiffEstimator(maxIter=3000, tol=1e-12).fit(df)
     assert sdid.getSummary().treatmentEffect == pytest.approx(5.0, abs=0.5)
     assert sdid.getTimeWeights() is not None
+
+
+def test_ortho_forest_variable_transformer():
+    import numpy as np
+
+    from synapseml_amd.causal import OrthoForestVariableTransformer
+    from synapseml_amd.core.dataframe import DataFrame
+
+    df = DataFrame({"TResid": np.array([2.0, -0.5]), "OResid": np.array([1.0, 1.0])})
+    out = OrthoForestVariableTransformer().transform(df)
+    np.testing.assert_allclose(out["_tmp_tsOutcome"], [0.5, -2.0])
+    np.testing.assert_allclose(out["_tmp_twOutcome"], [4.0, 0.25])
+    import pytest
+
+    with pytest.raises(TypeError):
+        OrthoForestVariableTransformer().transform(DataFrame({"TResid": np.array([1, 2]), "OResid": np.ones(2)}))

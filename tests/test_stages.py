@@ -113,3 +113,41 @@ def test_timer_and_multicolumn_adapter():
     mca = MultiColumnAdapter(inputCols=["a", "b"], outputCols=["ai", "bi"]).set("baseStage", ValueIndexer())
     out = mca.fit(df).transform(df)
     assert out["bi"].tolist() == [0, 0, 1]
+
+
+def test_iterator_batchers():
+    """Batchers.scala equivalents over lazy iterators (reference: core/.../stages/Batchers.scala)."""
+    import threading
+    import time as _t
+
+    from synapseml_amd.stages import DynamicBufferedBatcher, FixedBatcher, FixedBufferedBatcher, TimeIntervalBatcher
+
+    assert list(FixedBatcher(range(7), 3)) == [[0, 1, 2], [3, 4, 5], [6]]
+    assert list(FixedBufferedBatcher(iter(range(7)), 3, max_buffer_size=1)) == [[0, 1, 2], [3, 4, 5], [6]]
+    assert list(FixedBatcher([], 3)) == []
+
+    def slow():
+        for i in range(6):
+            _t.sleep(0.01)
+            yield i
+
+    got = list(DynamicBufferedBatcher(slow()))
+    assert sum(got, []) == list(range(6)) and all(len(b) >= 1 for b in got)
+    # a slow consumer sees larger batches: everything buffered meanwhile
+    b = DynamicBufferedBatcher(iter(range(100)))
+    first = next(b)
+    _t.sleep(0.05)
+    rest = sum(list(b), [])
+    assert first + rest == list(range(100)) and max(len(first), len(rest)) > 1
+    tb = list(TimeIntervalBatcher(iter(range(10)), millis=1000, max_buffer_size=4))
+    assert tb == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+
+    def boom():
+        yield 1
+        raise RuntimeError("source failed")
+
+    import pytest
+
+    with pytest.raises(RuntimeError):
+        list(FixedBufferedBatcher(boom(), 5))
+    assert threading.active_count() < 50
