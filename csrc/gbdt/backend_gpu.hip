@@ -1652,13 +1652,17 @@ __device__ void ChooseFused(DState* __restrict__ st, DLeaf* __restrict__ leaves,
   st->phase = 1;
 }
 
-template <bool kFromSlab>
+// kChoose = false (SML_FUSED_SPLIT=3): slab reduce + split search only, for choose_part_kernel
+// to consume after the kernel boundary (plain stores; the row count goes to part[E] as
+// hist_reduce_kernel leaves it; st_next's partition cursor is zeroed as find_split_kernel does).
+template <bool kFromSlab, bool kChoose = true>
 __global__ __launch_bounds__(kSplitThreads) void split_kernel(
     DState* __restrict__ st, DLeaf* __restrict__ leaves, const int2* __restrict__ slab,
-    const double2* __restrict__ part, int E, const float* __restrict__ ghmax, double2* __restrict__ hist_pool,
+    double2* __restrict__ part, int E, const float* __restrict__ ghmax, double2* __restrict__ hist_pool,
     FeatMeta fm, SplitParams sp, SplitResult* __restrict__ fbest, int F, SplitResult* __restrict__ lbest,
     double* __restrict__ lgain, DTree t, const int8_t* __restrict__ mono, int has_mono,
-    unsigned int* __restrict__ arrive) {
+    unsigned int* __restrict__ arrive, DState* __restrict__ st_next) {
+  if (!kChoose && st_next && blockIdx.x == 0 && threadIdx.x == 0) st_next->cursor = 0ull;
   if (st->done) return;
   const int f = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1701,6 +1705,7 @@ __global__ __launch_bounds__(kSplitThreads) void split_kernel(
       const HScale s = HistScale(count, ghmax);
       s_small[tid] = make_double2(static_cast<double>(tg) / static_cast<double>(s.g),
                                   static_cast<double>(th) / static_cast<double>(s.h));
+      if (!kChoose && f == 0 && tid == 0) part[E] = make_double2(static_cast<double>(count), 0.0);
     }
     gcnt = count;
   } else {
@@ -1744,9 +1749,13 @@ __global__ __launch_bounds__(kSplitThreads) void split_kernel(
     if (root) {
       cnt = gcnt;
       if (f == 0 && ltid == 0) {  // published for the chooser (sc1), like every other hand-off here
-        StoreAgent8(&leaves[0].sum_g, static_cast<unsigned long long>(__double_as_longlong(G)));
-        StoreAgent8(&leaves[0].sum_h, static_cast<unsigned long long>(__double_as_longlong(H)));
-        StoreAgent8(&leaves[0].gcount, static_cast<unsigned long long>(cnt));
+        if (kChoose) {
+          StoreAgent8(&leaves[0].sum_g, static_cast<unsigned long long>(__double_as_longlong(G)));
+          StoreAgent8(&leaves[0].sum_h, static_cast<unsigned long long>(__double_as_longlong(H)));
+          StoreAgent8(&leaves[0].gcount, static_cast<unsigned long long>(cnt));
+        } else {
+          leaves[0].sum_g = G; leaves[0].sum_h = H; leaves[0].gcount = cnt;
+        }
       }
     } else {
       cnt = c == 0 ? gcnt : (Lf.gcount - gcnt);  // Lf.gcount of the large child holds the parent count
@@ -1829,8 +1838,10 @@ __global__ __launch_bounds__(kSplitThreads) void split_kernel(
         for (int w = 0; w < 8; ++w) r.cat_bits[w] = 0;
       }
     }
-    PublishAgent(fbest + c * F + f, &r);
+    if (kChoose) PublishAgent(fbest + c * F + f, &r);
+    else fbest[c * F + f] = r;
   }
+  if (!kChoose) return;
   // ---- 3. publish + arrive; the last block chooses
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2486,7 +2497,7 @@ class GpuBackend : public TrainBackend {
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
       // choose_part_kernel: every block pays the choose prologue, so keep the grid within one resident
       // round (A/B on MI355X, 11M x 28: 2048 blocks 2.09-2.10 ms/iter, 1024 1.99-2.01, 768 1.97-2.01, 512 2.01-2.04)
-      if (merged_choose_ && fused_split_ == 0) {
+      if (merged_choose_ && (fused_split_ == 0 || fused_split_ == 3)) {
         int per_cu = 0, cus = 0;
         auto ck = part_rows_ == 16 ? choose_part_kernel<16> : (part_rows_ == 4 ? choose_part_kernel<4> : choose_part_kernel<8>);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ck, kPartThreads, 0) == hipSuccess &&
@@ -2505,7 +2516,8 @@ class GpuBackend : public TrainBackend {
                            (cfg.bagging_freq > 0 && (cfg.bagging_fraction < 1.0 || cfg.pos_bagging_fraction < 1.0 ||
                                                      cfg.neg_bagging_fraction < 1.0));
       const char* e = std::getenv("SML_PREP");
-      prep_ok_ = K == 1 && !sampled && hist_mode_ == 0 && fused_split_ == 0 && F_ > 0 && F_ <= kFeatPerGroup &&
+      prep_ok_ = K == 1 && !sampled && hist_mode_ == 0 && (fused_split_ == 0 || fused_split_ == 3) && F_ > 0 &&
+                 F_ <= kFeatPerGroup &&
                  L_ <= kPrepMaxNodes + 1 && !(e && std::atoi(e) == 0);
       wmax_ = 1.0;
       if (!d->weight.empty()) {
@@ -2788,7 +2800,7 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipGetLastError());
       pending_parts_ = 0;
     }
-    const bool merged = merged_choose_ && fused_split_ == 0;
+    const bool merged = merged_choose_ && (fused_split_ == 0 || fused_split_ == 3);
     st_cur_ = state_;
     st_next_ = merged ? state_ + 1 : nullptr;
     hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_, leaves_.get(), root_count, root_buf, L_,
@@ -2796,12 +2808,14 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipGetLastError());
     pending_parts_ = 0;
     // root histogram (slabs already built by score_grad_hist_kernel, or built here) + split search
+    const float* root_scale = nullptr;
     if (root_prepared) {
-      EnqueueReduce(reinterpret_cast<const float*>(ghbound_.get()));
+      root_scale = reinterpret_cast<const float*>(ghbound_.get());
+      if (!(fused_split_ == 3 && !Distributed())) EnqueueReduce(root_scale);
     } else {
       EnqueueHistogram(g, h);
     }
-    EnqueueFindChoose(!merged);
+    EnqueueFindChoose(!merged, root_scale);
     for (int s = 1; s < L_; ++s) {
       // (choose +) partition the chosen leaf, histogram its smaller child, search both
       if (merged) {
@@ -3010,7 +3024,7 @@ class GpuBackend : public TrainBackend {
                          perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     }
     SML_HIP_CHECK(hipGetLastError());
-    if (fused_split_ == 1 && hist_mode_ == 0 && !Distributed()) return;  // split_kernel reduces the slabs itself
+    if ((fused_split_ == 1 || fused_split_ == 3) && hist_mode_ == 0 && !Distributed()) return;  // split_kernel reduces
     EnqueueReduce(ghmax);
   }
 
@@ -3032,13 +3046,26 @@ class GpuBackend : public TrainBackend {
 
   bool Distributed() const { return comm_ && comm_->world() > 1; }
 
-  void EnqueueFindChoose(bool choose_now = true) {
-    if (fused_split_) {
+  void EnqueueFindChoose(bool choose_now = true, const float* scale = nullptr) {
+    if (fused_split_ == 3 && !Distributed()) {
+      // slab reduce + split search in one launch; the choose step runs in choose_part_kernel (or below)
+      const float* ghmax = scale ? scale : reinterpret_cast<const float*>(ghmax_.get());
+      hipLaunchKernelGGL((split_kernel<true, false>), dim3(F_), dim3(kSplitThreads), 0, stream_, st_cur_,
+                         leaves_.get(), slab_.get(), part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(),
+                         F_, lbest_.get(), lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get(), st_next_);
+      SML_HIP_CHECK(hipGetLastError());
+      if (!choose_now) return;
+      hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, st_cur_, leaves_.get(), lbest_.get(),
+                         lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono);
+      SML_HIP_CHECK(hipGetLastError());
+      return;
+    }
+    if (fused_split_ == 1 || fused_split_ == 2) {
       const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
       auto k = (Distributed() || fused_split_ == 2 || hist_mode_ == 1) ? split_kernel<false> : split_kernel<true>;
       hipLaunchKernelGGL(k, dim3(F_), dim3(kSplitThreads), 0, stream_, st_cur_, leaves_.get(), slab_.get(),
                          part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(), F_, lbest_.get(),
-                         lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get());
+                         lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get(), static_cast<DState*>(nullptr));
       SML_HIP_CHECK(hipGetLastError());
       return;
     }
@@ -3176,7 +3203,8 @@ class GpuBackend : public TrainBackend {
   DevBuf<unsigned int> ghmax_;
   DevBuf<unsigned int> arrive_;  // split_kernel arrival counter (reset by the last block)
   // SML_FUSED_SPLIT: 0 = reduce / find / choose launches, 1 = one split_kernel (slab reduce inside),
-  // 2 = reduce launch + split_kernel (find + choose)
+  // 2 = reduce launch + split_kernel (find + choose), 3 = split_kernel<slab, no choose> + choose_part_kernel
+  // (A/B with the merged choose: 2.05 ms/iter vs 1.97 for 0 - 28 blocks cannot pull the slabs fast enough)
   int fused_split_ = 0;  // A/B on MI355X: 0 = 2.30 ms/iter, 2 = 2.41, 1 = 2.51 (profiles/README)
   DevBuf<float> ghmax_partial_;
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
