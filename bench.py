@@ -65,12 +65,16 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = args.device == "gpu" and torch.cuda.is_available()
+    # more ranks than GPUs (a rehearsal of the multi-GPU path on a small box): ranks share devices, so the
+    # control plane is gloo and histograms go over the one-shot IPC allreduce on a host base communicator
+    # (RCCL cannot put two ranks on one device). The driver's N-GPU runs have one GPU per rank.
+    shared = use_gpu and world > torch.cuda.device_count()
     if use_gpu:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
     from synapseml_amd.parallel import distributed as D
 
     if world > 1:
-        D.init_from_env("nccl" if use_gpu else "gloo")
+        D.init_from_env("nccl" if use_gpu and not shared else "gloo")
     from synapseml_amd.ops import native
 
     g = native.gbdt()
@@ -102,7 +106,7 @@ def main() -> None:
     n_hold = min(200_000, args.rows)
     X_hold, y_hold = X[:n_hold].astype(np.float64), y[:n_hold]
     del X
-    comm = D.gbdt_comm(use_gpu) if world > 1 else None
+    comm = D.gbdt_comm(use_gpu, shared_device=shared) if world > 1 else None
     booster = g.Booster(ds, params, comm)
     setup_s = time.perf_counter() - t_setup
 
@@ -127,7 +131,7 @@ def main() -> None:
     if world > 1:
         import torch.distributed as dist
 
-        t = torch.tensor(el, device="cuda" if use_gpu else "cpu")
+        t = torch.tensor(el, device="cuda" if use_gpu and not shared else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # K11: the training metric (AUC over all rows) evaluated where the scores live (outside the timed region)

@@ -145,7 +145,7 @@ def maybe_p2p(comm, device: int):
     return c
 
 
-def gbdt_comm(use_gpu: bool):
+def gbdt_comm(use_gpu: bool, shared_device: bool = False):
     """Communicator for the native GBDT engine, or None when world == 1.
 
     GPU runs get a native RCCL communicator whose ncclUniqueId is broadcast
@@ -159,16 +159,25 @@ def gbdt_comm(use_gpu: bool):
     latency-bound ring; larger messages still use RCCL.  ``SML_GBDT_P2P=0``
     disables it; if IPC set-up or its start-up self-test fails on any rank,
     all ranks stay on RCCL together.
+
+    ``shared_device``: ranks share GPUs (more ranks than devices, e.g. a
+    rehearsal on a one-GPU box). RCCL cannot place two ranks on one device, so
+    the P2P allreduce wraps the host (gloo) communicator instead.
     """
     if world_size() <= 1:
         return None
     from ..ops import native
 
     g = native.gbdt()
-    key = ("rccl" if use_gpu else "host", world_size())
+    key = ("shared" if use_gpu and shared_device else "rccl" if use_gpu else "host", world_size())
     if key in _comm_cache:
         return _comm_cache[key]
-    if use_gpu:
+    if use_gpu and shared_device:
+        import torch
+
+        host = g.host_comm(rank(), world_size(), lambda arr: allreduce_numpy(arr))
+        c = maybe_p2p(host, torch.cuda.current_device())
+    elif use_gpu:
         uid = g.rccl_unique_id() if rank() == 0 else None
         uid = broadcast_object(uid, 0)
         import torch
