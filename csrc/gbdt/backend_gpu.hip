@@ -547,7 +547,8 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
 #pragma unroll
   for (int u = 0; u < NU; ++u) { lam[u] = 0.0; hes[u] = 0.0; }
   double suml = 0.0;
-  // (a) top document r against every document (partners on the lanes)
+  // (a) top document r against every document (partners on the lanes). Grouping four top documents
+  // so their wave sums interleave measured no faster (1.44 vs 1.35 ms per call): not shuffle-latency bound.
   double top_la = 0.0, top_he = 0.0;  // lane r keeps the reduced lambdas of top document r
   for (int r = 0; r < ntop; ++r) {
     const double si = ReadLaneD(tsc, r);
@@ -612,10 +613,15 @@ __global__ __launch_bounds__(64) void lambdarank_regs_kernel(RankTables t, const
   __shared__ double s_disc[kRankLds];
   for (int r = threadIdx.x; r < kRankLds; r += 64) s_disc[r] = 1.0 / log2(2.0 + r);
   __syncthreads();
+  // documents per lane sized to the query: the pair loops run NU-wide, so a 100-document query
+  // costs half of what the kRankLds-wide form would
   for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
     const int cnt = t.qb[q + 1] - t.qb[q];
     if (cnt <= 0 || !RegsEligible(t, cnt)) continue;
-    LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc);
+    if (cnt <= 64) LambdarankQueryRegs<1>(t, q, score, label, weight, g, h, s_disc);
+    else if (cnt <= 128) LambdarankQueryRegs<2>(t, q, score, label, weight, g, h, s_disc);
+    else if (cnt <= 192) LambdarankQueryRegs<3>(t, q, score, label, weight, g, h, s_disc);
+    else LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc);
   }
 }
 
@@ -2214,6 +2220,32 @@ struct DevTreeView {
   int num_leaves;
 };
 
+constexpr int kPrepMaxNodes = 255;  // device-tree score updates: trees up to 256 leaves (nodes + values in LDS)
+
+// The tree just grown, read where it was built (TrainTreeAndUpdateScore): nodes are encoded as
+// UploadTree encodes them on the host, leaf values are lval * shrink (the host's Tree::Shrink).
+struct DevTreeSrc {
+  DTree t;
+  const DState* st;  // final state version (num_leaves); nullptr: use the uploaded DevTreeView
+  const int32_t* num_bin;
+  const int32_t* missing;
+  const int32_t* default_bin;
+  double shrink;
+};
+
+__device__ __forceinline__ void StageDeviceTree(const DevTreeSrc& src, int num_leaves, int4* snodes, double* slval,
+                                                int tid, int nthreads) {
+  for (int i = tid; i < num_leaves - 1; i += nthreads) {
+    const int f = src.t.feat[i], ic = src.t.is_cat[i] ? 1 : 0;
+    const int mt = ic ? kMissingNaN : src.missing[f];
+    const int dl = ic ? 0 : (src.t.dleft[i] ? 1 : 0);
+    const int mbin = mt == kMissingNaN ? src.num_bin[f] - 1 : (mt == kMissingZero ? src.default_bin[f] : 0);
+    snodes[i] = make_int4(f | (mt << 16) | (dl << 18) | (ic << 19) | (mbin << 20), static_cast<int>(src.t.thr[i]),
+                          src.t.left[i], src.t.right[i]);
+  }
+  for (int i = tid; i < num_leaves; i += nthreads) slval[i] = src.t.lval[i] * src.shrink;
+}
+
 __device__ __forceinline__ uint32_t ByteOfRow(const uint4& a, const uint4& b, int f) {
   const int w = f >> 2;
   uint32_t x = w == 0 ? a.x : w == 1 ? a.y : w == 2 ? a.z : w == 3 ? a.w : w == 4 ? b.x : w == 5 ? b.y : w == 6 ? b.z : b.w;
@@ -2236,14 +2268,22 @@ __device__ __forceinline__ int NodeStep(const int4& nd, uint32_t b, const uint32
   return left ? nd.z : nd.w;
 }
 
-__global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, const uint4* __restrict__ bins4, int W4,
+__global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, DevTreeSrc src,
+                                                              const uint4* __restrict__ bins4, int W4,
                                                               int F, const uint8_t* __restrict__ cbins, int64_t n,
                                                               double scale, double* __restrict__ score,
                                                               int32_t* __restrict__ leaf_out) {
   __shared__ int4 snodes[kScoreLdsNodes];
+  __shared__ double slv[kPrepMaxNodes + 1];
+  if (src.st) {  // the tree just grown, straight from the device arrays (TrainTreeAndUpdateScore)
+    tv.num_leaves = src.st->num_leaves;
+    tv.cat_bits = src.t.cat_bits;
+    tv.lval = slv;
+    StageDeviceTree(src, tv.num_leaves, snodes, slv, threadIdx.x, kScoreThreads);
+  }
   const int ni = tv.num_leaves - 1;
   const bool lds = ni <= kScoreLdsNodes;
-  if (lds)
+  if (lds && !src.st)
     for (int i = threadIdx.x; i < ni; i += kScoreThreads) snodes[i] = tv.nodes[i];
   __syncthreads();
   const int4* nodes = lds ? snodes : tv.nodes;
@@ -2311,18 +2351,6 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, co
 // the block maxima of |g| and h, which the rest of the tree's histograms use.
 // Replaces score_kernel + grad_kernel + the root hist_kernel (150 + 54 + 131
 // us at 11M x 28 on MI355X, three full passes over rows).
-constexpr int kPrepMaxNodes = 255;  // trees up to 256 leaves keep nodes + values in LDS
-
-// The tree just grown, read where it was built (TrainTreeAndUpdateScore): nodes are encoded as
-// UploadTree encodes them on the host, leaf values are lval * shrink (the host's Tree::Shrink).
-struct DevTreeSrc {
-  DTree t;
-  const DState* st;  // final state version (num_leaves); nullptr: use the uploaded DevTreeView
-  const int32_t* num_bin;
-  const int32_t* missing;
-  const int32_t* default_bin;
-  double shrink;
-};
 
 template <int kUnroll, int kThreads = kHistThreads, int kCopies = 1>
 __global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
@@ -2342,15 +2370,7 @@ __global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
   for (int i = tid; i < kCopies * kFeatPerGroup * kHistStride; i += kThreads) shc[i] = 0ull;
   unsigned long long* sh = shc + (kCopies > 1 && tid >= kThreads / 2 ? kFeatPerGroup * kHistStride : 0);
   if (src.st) {
-    for (int i = tid; i < ni; i += kThreads) {
-      const int f = src.t.feat[i], ic = src.t.is_cat[i] ? 1 : 0;
-      const int mt = ic ? kMissingNaN : src.missing[f];
-      const int dl = ic ? 0 : (src.t.dleft[i] ? 1 : 0);
-      const int mbin = mt == kMissingNaN ? src.num_bin[f] - 1 : (mt == kMissingZero ? src.default_bin[f] : 0);
-      snodes[i] = make_int4(f | (mt << 16) | (dl << 18) | (ic << 19) | (mbin << 20), static_cast<int>(src.t.thr[i]),
-                            src.t.left[i], src.t.right[i]);
-    }
-    for (int i = tid; i < num_leaves; i += kThreads) slval[i] = src.t.lval[i] * src.shrink;
+    StageDeviceTree(src, num_leaves, snodes, slval, tid, kThreads);
   } else {
     for (int i = tid; i < ni; i += kThreads) snodes[i] = tv.nodes[i];
     for (int i = tid; i < num_leaves; i += kThreads) slval[i] = tv.lval[i];
@@ -2756,13 +2776,25 @@ class GpuBackend : public TrainBackend {
   // tree right behind it: the host reads the tree back while that pass runs.
   Tree TrainTreeAndUpdateScore(int k, const std::vector<char>& fmask_in, double shrink, bool* updated) override {
     *updated = false;
-    if (!(prep_armed_ && k == 0 && K_ == 1 && L_ <= kPrepMaxNodes + 1)) return TrainTree(k, fmask_in);
+    if (L_ > kPrepMaxNodes + 1) return TrainTree(k, fmask_in);
     roctxRangePushA("sml::TrainTreeAndUpdateScore");
     GrowTree(k, fmask_in);
     EnqueueTreeCopy();
     AccountScoreTime();  // the previous pass (done before this growth) frees the event pair
     DevTreeSrc src{dt_, state_ + final_v_, fm_.num_bin, fm_.missing, fm_.default_bin, shrink};
-    LaunchPrep(DevTreeView{}, src, 1.0);
+    if (prep_armed_ && k == 0 && K_ == 1) {
+      LaunchPrep(DevTreeView{}, src, 1.0);
+    } else {
+      // any other objective: the plain score update, still without the host round trip
+      prep_valid_ = root_ready_ = false;
+      SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
+      hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, DevTreeView{}, src,
+                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, 1.0,
+                         score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
+      SML_HIP_CHECK(hipGetLastError());
+      SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
+      score_pending_ = true;
+    }
     Tree t = FinishTree();
     *updated = true;
     roctxRangePop();
@@ -2865,7 +2897,7 @@ class GpuBackend : public TrainBackend {
     if (prep_armed_ && k == 0 && t.num_leaves <= kPrepMaxNodes + 1) {
       LaunchPrep(tv, DevTreeSrc{}, scale);  // score update + next gradients + next root histogram, one pass
     } else {
-      hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
+      hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv, DevTreeSrc{},
                          reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
                          score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
       SML_HIP_CHECK(hipGetLastError());
@@ -2877,7 +2909,7 @@ class GpuBackend : public TrainBackend {
 
   void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) override {
     DevTreeView tv = UploadTree(t);
-    hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv,
+    hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv, DevTreeSrc{},
                        reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, 0.0,
                        static_cast<double*>(nullptr), leaf_idx_.get());
     SML_HIP_CHECK(hipGetLastError());
