@@ -52,6 +52,8 @@ __constant__ int c_max_hist_blocks = kMaxHistBlocks;  // 256 for the one-block-p
 // slab stores write through L2 (sc1) so the kernel boundary has ~15 MB less to write back before the
 // reduce reads them from the other XCDs (A/B on MI355X: 1.952 -> 1.923 ms/iter); SML_SLAB_WT=0: plain
 __constant__ int c_slab_wt = 1;
+// SML_PART_WT=1: partition outputs (perm, ordered g/h) written through L2 (A/B: 1.96 -> 1.99 ms/iter, slower)
+__constant__ int c_part_wt = 0;
 
 // one slab element (g | h packed as int2); write-through (agent-scope relaxed store = sc1) when c_slab_wt
 __device__ __forceinline__ void SlabStore(int2* p, unsigned long long w) {
@@ -824,7 +826,9 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // quantum / 2 (very confident rows of a near-separable problem) round to zero.
 // test_gpu_histogram_quantisation_skewed_hessians pins tree structure, node
 // hessian sums and loss against the fp64 host oracle in that regime.
-constexpr int kHistUnrollDefault = 2;  // A/B: 2 rows in flight per thread beat 4 and 8
+// A/B: 2 rows in flight per thread beat 4 and 8 (round 2, one 1024-thread block per CU: 1.93 / 1.97 / 2.04
+// ms/iter; more rows in flight only queue more LDS atomics)
+constexpr int kHistUnrollDefault = 2;
 
 __device__ __forceinline__ int HistBlocks(int count) {
   return max(1, min(c_max_hist_blocks, ceil_div_i(count, c_min_rows_per_hist_block)));
@@ -1977,8 +1981,15 @@ __device__ __forceinline__ void PartitionTiles(
       if (k < tv) {
         const int lbefore = run + wb + rl[u];
         const int dst = (lmask >> u) & 1u ? lb + lbefore : rb + (k - lbefore);
-        operm[dst] = r[u];
-        oogh[dst] = v[u];
+        if (c_part_wt) {
+          __hip_atomic_store(operm + dst, r[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(oogh + dst),
+                             (static_cast<unsigned long long>(__float_as_uint(v[u].y)) << 32) | __float_as_uint(v[u].x),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          operm[dst] = r[u];
+          oogh[dst] = v[u];
+        }
       }
       run += ut;
     }
@@ -2524,6 +2535,10 @@ class GpuBackend : public TrainBackend {
     if (hist_shape_ < 0 || hist_shape_ > 2) hist_shape_ = 2;
     max_hist_blocks_ = hist_shape_ == 0 ? kMaxHistBlocks : kMaxHistBlocks / 2;
     SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_max_hist_blocks), &max_hist_blocks_, sizeof(int)));
+    if (const char* e = std::getenv("SML_PART_WT")) {
+      const int v = std::atoi(e) != 0 ? 1 : 0;
+      SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_part_wt), &v, sizeof(int)));
+    }
     if (const char* e = std::getenv("SML_SLAB_WT")) {
       const int v = std::atoi(e) != 0 ? 1 : 0;
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_slab_wt), &v, sizeof(int)));
@@ -3065,7 +3080,8 @@ class GpuBackend : public TrainBackend {
                          ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     } else {
       auto hk = hist_shape_ == 1 ? hist_kernel<2, 1024, 2>
-                : hist_shape_ == 2 ? hist_kernel<2, 1024, 1>
+                : hist_shape_ == 2 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024, 1>
+                                      : hist_unroll_ == 8 ? hist_kernel<8, 1024, 1> : hist_kernel<2, 1024, 1>)
                 : hist_threads_ == 1024 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024> : hist_kernel<2, 1024>)
                 : hist_threads_ == 256 ? (hist_unroll_ == 4 ? hist_kernel<4, 256> : hist_kernel<2, 256>)
                 : (hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>));
