@@ -73,6 +73,29 @@ PYBIND11_MODULE(_vw, m) {
     }
     return out;
   }, py::arg("strings"), py::arg("seed"), py::arg("prefix") = "");
+  // packed UTF-8 strings (Arrow layout: bytes + n+1 offsets) -> murmur3 & mask; K13 on the GPU when asked
+  m.def("murmur_offsets", [](py::array_t<uint8_t, py::array::c_style> bytes, py::array_t<int64_t, py::array::c_style> offs,
+                             uint32_t seed, uint32_t mask, bool device) {
+    const int64_t n = static_cast<int64_t>(offs.size()) - 1;
+    if (n < 0) throw std::runtime_error("murmur_offsets: offsets must hold n + 1 entries");
+    const int64_t* o = offs.data();
+    const int64_t nb = static_cast<int64_t>(bytes.size());
+    for (int64_t i = 0; i < n; ++i)
+      if (o[i] < 0 || o[i] > o[i + 1] || o[i + 1] > nb) throw std::runtime_error("murmur_offsets: bad offsets");
+    py::array_t<uint32_t> out(std::max<int64_t>(n, 0));
+    uint32_t* r = out.mutable_data();
+    const uint8_t* b = bytes.data();
+    {
+      py::gil_scoped_release rel;
+      if (device) {
+        MurmurBatchGpu(b, nb, o, n, seed, mask, r);
+      } else {
+#pragma omp parallel for schedule(static) if (n > 4096)
+        for (int64_t i = 0; i < n; ++i) r[i] = Murmur3(b + o[i], static_cast<size_t>(o[i + 1] - o[i]), seed) & mask;
+      }
+    }
+    return out;
+  }, py::arg("bytes"), py::arg("offsets"), py::arg("seed"), py::arg("mask") = 0xFFFFFFFFu, py::arg("device") = false);
   m.def("gpu_available", &VwGpuAvailable);
 
   py::class_<VW, std::shared_ptr<VW>>(m, "VW")

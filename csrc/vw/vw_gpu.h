@@ -46,5 +46,8 @@ class GpuSgd {
 };
 
 bool VwGpuAvailable();
+// K13: murmur3_32(bytes[offsets[i]:offsets[i+1]], seed) & mask for every i, on the device
+void MurmurBatchGpu(const uint8_t* bytes, int64_t nbytes, const int64_t* offsets, int64_t n, uint32_t seed,
+                    uint32_t mask, uint32_t* out);
 
 }  // namespace smlvw

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -23,6 +24,43 @@ namespace smlvw {
 namespace {
 
 constexpr int kWavesPerBlock = 4;
+
+// ---------------------------------------------------------------- K13
+// VW murmur3_32 of many strings at once: one thread per string over a packed
+// UTF-8 byte buffer with (n + 1) offsets (the Arrow string-column layout), the
+// featurizer's namespace hash as the seed and the feature mask applied on the
+// way out. Bytes are read individually (strings start at arbitrary offsets);
+// lanes of a wave hash neighbouring strings, so the loads stay coalesced.
+__device__ __forceinline__ uint32_t Rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+__global__ __launch_bounds__(256) void murmur_batch_kernel(const uint8_t* __restrict__ bytes,
+                                                           const int64_t* __restrict__ offsets, int64_t n,
+                                                           uint32_t seed, uint32_t mask, uint32_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint8_t* d = bytes + offsets[i];
+    const int64_t len = offsets[i + 1] - offsets[i];
+    const int64_t nb = len / 4;
+    uint32_t h = seed;
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    for (int64_t b = 0; b < nb; ++b) {
+      uint32_t k = static_cast<uint32_t>(d[4 * b]) | (static_cast<uint32_t>(d[4 * b + 1]) << 8) |
+                   (static_cast<uint32_t>(d[4 * b + 2]) << 16) | (static_cast<uint32_t>(d[4 * b + 3]) << 24);
+      k *= c1; k = Rotl(k, 15); k *= c2;
+      h ^= k; h = Rotl(h, 13); h = h * 5 + 0xe6546b64u;
+    }
+    const uint8_t* t = d + 4 * nb;
+    uint32_t k = 0;
+    switch (len & 3) {
+      case 3: k ^= static_cast<uint32_t>(t[2]) << 16; [[fallthrough]];
+      case 2: k ^= static_cast<uint32_t>(t[1]) << 8; [[fallthrough]];
+      case 1: k ^= t[0]; k *= c1; k = Rotl(k, 15); k *= c2; h ^= k;
+    }
+    h ^= static_cast<uint32_t>(len);
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    out[i] = h & mask;
+  }
+}
 
 __device__ __forceinline__ void ExampleStep(const int64_t* __restrict__ indptr, const uint32_t* __restrict__ idx,
                                             const float* __restrict__ val, const float* __restrict__ labels,
@@ -123,6 +161,36 @@ struct GpuSgd::Impl {
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
+
+void MurmurBatchGpu(const uint8_t* bytes, int64_t nbytes, const int64_t* offsets, int64_t n, uint32_t seed,
+                    uint32_t mask, uint32_t* out) {
+  if (n <= 0) return;
+  hipStream_t st = nullptr;
+  VW_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  uint8_t* db = nullptr;
+  int64_t* doff = nullptr;
+  uint32_t* dout = nullptr;
+  try {
+    VW_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&db), static_cast<size_t>(std::max<int64_t>(1, nbytes)), st));
+    VW_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&doff), sizeof(int64_t) * (n + 1), st));
+    VW_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dout), sizeof(uint32_t) * n, st));
+    if (nbytes > 0) VW_HIP_CHECK(hipMemcpyAsync(db, bytes, nbytes, hipMemcpyHostToDevice, st));
+    VW_HIP_CHECK(hipMemcpyAsync(doff, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    const int grid = static_cast<int>(std::min<int64_t>((n + 255) / 256, 65536));
+    hipLaunchKernelGGL(murmur_batch_kernel, dim3(grid), dim3(256), 0, st, db, doff, n, seed, mask, dout);
+    VW_HIP_CHECK(hipGetLastError());
+    VW_HIP_CHECK(hipMemcpyAsync(out, dout, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+    VW_HIP_CHECK(hipStreamSynchronize(st));
+  } catch (...) {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(db); (void)hipFree(doff); (void)hipFree(dout);
+    (void)hipStreamDestroy(st);
+    throw;
+  }
+  (void)hipFreeAsync(db, st); (void)hipFreeAsync(doff, st); (void)hipFreeAsync(dout, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+}
 
 bool VwGpuAvailable() {
   int n = 0;

@@ -21,6 +21,26 @@ def _vw():
     return native.load("_vw")
 
 
+_GPU_HASH_MIN = 200_000  # strings per call above which the device kernel pays for its copies
+
+
+def hash_strings(strings, seed: int, mask: int = 0xFFFFFFFF, device: str = "auto") -> np.ndarray:
+    """murmur3_32(utf8(s), seed) & mask for every string, in one native call over the packed UTF-8
+    bytes (Arrow layout). ``device``: "gpu" runs the batched HIP kernel (K13), "cpu" the host loop,
+    "auto" the kernel for large batches when a device is present."""
+    enc = [x.encode("utf-8") for x in strings]
+    lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=len(enc))
+    offs = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    data = np.frombuffer(b"".join(enc), dtype=np.uint8) if enc else np.zeros(0, np.uint8)
+    vw = _vw()
+    if device == "auto":
+        on_gpu = len(enc) >= _GPU_HASH_MIN and bool(vw.gpu_available())
+    else:
+        on_gpu = device == "gpu"
+    return vw.murmur_offsets(data, offs, seed & 0xFFFFFFFF, mask & 0xFFFFFFFF, on_gpu)
+
+
 def murmur_hash(s: str, seed: int) -> int:
     """VW murmur3_32 of the UTF-8 bytes of ``s`` (signed like the JVM int)."""
     h = int(_vw().murmur3(s.encode("utf-8"), seed & 0xFFFFFFFF))
@@ -124,7 +144,19 @@ class VowpalWabbitFeaturizer(HasNumBits, HasInputCols, HasOutputCol):
                         add(int(i), [h], [vals[i]])
                 continue
             # object columns: strings, string lists, maps, vectors
-            for i, v in enumerate(col.tolist()):
+            vals = col.tolist()
+            strs = [i for i, v in enumerate(vals) if isinstance(v, str)]
+            if strs and len(strs) == sum(v is not None for v in vals):
+                # a string column: every row's tokens hashed in one native call (K13 on the GPU for big columns)
+                toks = [vals[i].split() if c in split_cols else [vals[i]] for i in strs]
+                flat = [pre + t for tk in toks for t in tk]
+                hs = hash_strings(flat, ns_hash, mask).astype(np.int64)
+                pos = 0
+                for i, tk in zip(strs, toks):
+                    add(i, hs[pos:pos + len(tk)], np.ones(len(tk)))
+                    pos += len(tk)
+                continue
+            for i, v in enumerate(vals):
                 if v is None:
                     continue
                 if isinstance(v, str):

@@ -408,3 +408,19 @@ def test_gpu_path_quadratic_expansion_matches_native_hashing():
             got = list(zip(idx[ip[r]:ip[r + 1]].tolist(), val[ip[r]:ip[r + 1]].tolist()))
             assert [e[0] for e in exp] == [g[0] for g in got]
             np.testing.assert_allclose([e[1] for e in exp], [g[1] for g in got], rtol=1e-6)
+
+
+def test_hash_strings_packed_matches_murmur():
+    """Packed-UTF-8 batched murmur (one native call per column) == per-string murmur3 (SURVEY §8.2 goldens)."""
+    import numpy as np
+
+    from synapseml_amd.vw.featurizer import hash_strings, murmur_hash
+
+    rng = np.random.default_rng(0)
+    xs = ["", "a", "fun", "inmarkus", "héllo wörld ✓"] + ["".join(chr(97 + int(c)) for c in rng.integers(0, 26, n))
+                                                        for n in rng.integers(0, 40, 500)]
+    for seed in (0, 2493003127):
+        got = hash_strings(xs, seed, device="cpu")
+        assert got.tolist() == [murmur_hash(x, seed) & 0xFFFFFFFF for x in xs]
+    assert hash_strings(["marie", "markus"], 2493003127, (1 << 18) - 1, device="cpu").tolist() == [60554, 36739]
+    assert hash_strings([], 1, device="cpu").tolist() == []

@@ -78,3 +78,17 @@ def test_gpu_quadratic_interactions_syncs_and_initial_model():
     warm = VowpalWabbitRegressor(deviceType="gpu", passThroughArgs="-q ab", initialModel=quad.getModel(),
                                  **dict(kw, numPasses=1)).fit(df)
     assert rmse(warm) < 1.2 * rmse(quad) + 0.05
+
+
+def test_murmur_batch_kernel_matches_host():
+    """K13: the HIP batched murmur kernel equals the host hash on random UTF-8 strings."""
+    import numpy as np
+
+    from synapseml_amd.vw.featurizer import hash_strings
+
+    rng = np.random.default_rng(1)
+    xs = ["", "ü", "inmarkus"] + ["".join(chr(int(c)) for c in rng.integers(32, 0x2FF, n))
+                                  for n in rng.integers(0, 70, 300_000)]
+    for seed, mask in ((0, 0xFFFFFFFF), (2493003127, (1 << 18) - 1)):
+        np.testing.assert_array_equal(hash_strings(xs, seed, mask, device="gpu"),
+                                      hash_strings(xs, seed, mask, device="cpu"))
