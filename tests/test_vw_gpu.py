@@ -80,6 +80,7 @@ def test_gpu_quadratic_interactions_syncs_and_initial_model():
     assert rmse(warm) < 1.2 * rmse(quad) + 0.05
 
 
+@pytest.mark.gpu
 def test_murmur_batch_kernel_matches_host():
     """K13: the HIP batched murmur kernel equals the host hash on random UTF-8 strings."""
     import numpy as np
