@@ -33,6 +33,11 @@ PYBIND11_MODULE(_nn, m) {
   m.def("gap_nhwc", [](uintptr_t x, int N, int HW, int C, int dtype, uintptr_t out, uintptr_t stream) {
     GapNhwc(P<const void>(x), N, HW, C, dtype, P<float>(out), P<void>(stream));
   });
+  m.def("maxpool_nhwc", [](uintptr_t x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw,
+                           int OH, int OW, int dtype, uintptr_t y, uintptr_t stream) {
+    MaxPoolNhwc(reinterpret_cast<const void*>(x), N, H, W, C, kh, kw, sh, sw, ph, pw, OH, OW, dtype,
+                reinterpret_cast<void*>(y), reinterpret_cast<void*>(stream));
+  });
   m.def("conv_supported", &ConvMfmaSupported);
   m.def("conv_mfma", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale, uintptr_t in_shift,
                         uintptr_t bias, uintptr_t res, uintptr_t out_scale, uintptr_t out_shift, uintptr_t y2,

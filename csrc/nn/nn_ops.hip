@@ -11,6 +11,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -142,6 +143,45 @@ __global__ __launch_bounds__(kThreads) void gap_nhwc_kernel(const T* __restrict_
   out[i] = s / HW;
 }
 
+// K16: max pool over an NHWC tensor (kh x kw window, stride, symmetric pads, no dilation; padded cells
+// never win, as ONNX pads max pools with -inf). One thread per (output pixel, 8 channels): 16-B loads
+// of consecutive channels for fp16 / bf16. C % 8 == 0 (the host checks).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void maxpool_nhwc_kernel(const T* __restrict__ x, int N, int H, int W, int C,
+                                                                int kh, int kw, int sh, int sw, int ph, int pw,
+                                                                int OH, int OW, T* __restrict__ y) {
+  const int cv8 = C / kVec;
+  const int64_t total = static_cast<int64_t>(N) * OH * OW * cv8;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int cg = static_cast<int>(t % cv8);
+    int64_t r = t / cv8;
+    const int ow = static_cast<int>(r % OW); r /= OW;
+    const int oh = static_cast<int>(r % OH);
+    const int n = static_cast<int>(r / OH);
+    float m[kVec];
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) m[j] = -INFINITY;
+    const int h0 = oh * sh - ph, w0 = ow * sw - pw;
+    for (int i = 0; i < kh; ++i) {
+      const int hh = h0 + i;
+      if (hh < 0 || hh >= H) continue;
+      for (int k = 0; k < kw; ++k) {
+        const int ww = w0 + k;
+        if (ww < 0 || ww >= W) continue;
+        const Vec8<T> v = *reinterpret_cast<const Vec8<T>*>(x + ((static_cast<int64_t>(n) * H + hh) * W + ww) * C +
+                                                           cg * kVec);
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) m[j] = fmaxf(m[j], ld<T>(v.v, j));
+      }
+    }
+    Vec8<T> o;
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) o.v[j] = cv<T>(m[j]);
+    *reinterpret_cast<Vec8<T>*>(y + ((static_cast<int64_t>(n) * OH + oh) * OW + ow) * C + cg * kVec) = o;
+  }
+}
+
 // row softmax / argmax, one wave per row (fp32)
 __global__ __launch_bounds__(kThreads) void softmax_rows_kernel(const float* __restrict__ x, int rows, int cols,
                                                                 float* __restrict__ y, int64_t* __restrict__ amax) {
@@ -177,6 +217,26 @@ int Blocks(int64_t n, int per_thread) {
 }
 
 }  // namespace
+
+void MaxPoolNhwc(const void* x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw, int OH,
+                 int OW, int dtype, void* y, void* stream) {
+  if (C % kVec != 0) throw std::runtime_error("maxpool_nhwc: channels must be a multiple of 8");
+  const int64_t total = static_cast<int64_t>(N) * OH * OW * (C / kVec);
+  if (total <= 0) return;
+  auto s = static_cast<hipStream_t>(stream);
+  const int g = static_cast<int>(std::min<int64_t>((total + kThreads - 1) / kThreads, 1 << 20));
+  if (dtype == 1)
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<__half>, dim3(g), dim3(kThreads), 0, s, static_cast<const __half*>(x), N, H,
+                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, static_cast<__half*>(y));
+  else if (dtype == 2)
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<__hip_bfloat16>, dim3(g), dim3(kThreads), 0, s,
+                       static_cast<const __hip_bfloat16*>(x), N, H, W, C, kh, kw, sh, sw, ph, pw, OH, OW,
+                       static_cast<__hip_bfloat16*>(y));
+  else
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<float>, dim3(g), dim3(kThreads), 0, s, static_cast<const float*>(x), N, H,
+                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, static_cast<float*>(y));
+  NN_HIP_CHECK(hipGetLastError());
+}
 
 bool NnGpuAvailable() {
   int n = 0;

@@ -690,6 +690,21 @@ def _maxpool(rt, at, x):
     dil = at.get("dilations", [1] * nd)
     pb, pe = _pads_for(at, list(t.shape[2:]), k, strides, dil)
     ceil = bool(at.get("ceil_mode", 0))
+    nn = getattr(getattr(rt, "session", None), "_nn", None)
+    if (nn is not None and nd == 2 and t.is_cuda and t.dim() == 4 and not ceil and list(dil) == [1, 1]
+            and list(pb) == list(pe) and t.shape[1] % 8 == 0 and t.dtype in (torch.float16, torch.bfloat16, torch.float32)
+            and t.is_contiguous(memory_format=torch.channels_last) and t.data_ptr() % 16 == 0
+            and not (len(rt.node_outputs) > 1 and rt.node_outputs[1])):
+        # K16: NHWC max pool on the HIP kernel (csrc/nn/nn_ops.hip), output stays channels-last
+        from .session import _dtype_code, _stream
+
+        N, C, H, W = t.shape
+        OH = (H + 2 * pb[0] - k[0]) // strides[0] + 1
+        OW = (W + 2 * pb[1] - k[1]) // strides[1] + 1
+        y = torch.empty((N, C, OH, OW), dtype=t.dtype, device=t.device, memory_format=torch.channels_last)
+        nn.maxpool_nhwc(t.data_ptr(), N, H, W, C, k[0], k[1], strides[0], strides[1], pb[0], pb[1], OH, OW,
+                        _dtype_code(t), y.data_ptr(), _stream(t))
+        return [y]
     t, pad = _sym_pad(t, pb, pe, value=-math.inf)
     f = {1: Fn.max_pool1d, 2: Fn.max_pool2d, 3: Fn.max_pool3d}[nd]
     if len(rt.node_outputs) > 1 and rt.node_outputs[1]:

@@ -396,3 +396,25 @@ def test_gpu_mfma_fused_resnet_matches_cpu(prec):
     out = sess.run(None, {"data": x})[0]
     assert np.corrcoef(out.ravel(), cpu.ravel())[0, 1] > (0.999 if prec == "fp16" else 0.995)
     assert (out.argmax(1) == cpu.argmax(1)).mean() >= 0.75
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+def test_gpu_maxpool_nhwc_kernel_matches_torch(dtype):
+    """K16: the NHWC max-pool kernel (ResNet stem 3x3/2 pad 1, and 2x2/2) against torch's max_pool2d."""
+    import torch
+
+    from synapseml_amd.ops import native
+
+    nn = native.load("_nn")
+    dt = getattr(torch, dtype)
+    code = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[dt]
+    for (n, c, h, w, k, s, p) in ((4, 64, 112, 112, 3, 2, 1), (2, 32, 15, 9, 2, 2, 0)):
+        x = torch.randn(n, c, h, w, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+        ref = torch.nn.functional.max_pool2d(x.float(), k, s, p)
+        oh, ow = ref.shape[2:]
+        y = torch.empty((n, c, oh, ow), dtype=dt, device="cuda", memory_format=torch.channels_last)
+        nn.maxpool_nhwc(x.data_ptr(), n, h, w, c, k, k, s, s, p, p, oh, ow, code, y.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(y.float(), ref.to(dt).float())
