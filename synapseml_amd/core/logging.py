@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import json
 import logging
+import re
 import time
 import traceback
 
@@ -15,6 +16,14 @@ LIBRARY_VERSION = "0.1.0"
 PROTOCOL_VERSION = "0.0.1"
 
 logger = logging.getLogger(LIBRARY_NAME)
+
+# Shared Access Signatures must never reach a log (reference: logging/common/Scrubber.scala SASScrubber)
+_SAS = re.compile(r"(?i)sig=[a-z0-9%]{43,63}%3d")
+
+
+def scrub(message: str) -> str:
+    """Replace SAS token signatures (``sig=...%3d``) in a message before it is logged."""
+    return _SAS.sub("sig=####", message)
 
 
 def payload(stage, method: str, num_cols=None, seconds=None, error=None) -> dict:
@@ -32,7 +41,7 @@ def payload(stage, method: str, num_cols=None, seconds=None, error=None) -> dict
         p["executionSeconds"] = seconds
     if error is not None:
         p["errorType"] = type(error).__name__
-        p["errorMessage"] = str(error)
+        p["errorMessage"] = scrub(str(error))
     return p
 
 
@@ -44,7 +53,7 @@ def log_verb(stage, method: str, fn, df=None):
     except Exception as e:
         if logger.isEnabledFor(logging.DEBUG):
             logger.debug(json.dumps(payload(stage, method, ncols, time.perf_counter() - t0, e)))
-            logger.debug(traceback.format_exc())
+            logger.debug(scrub(traceback.format_exc()))
         raise
     if logger.isEnabledFor(logging.DEBUG):
         logger.debug(json.dumps(payload(stage, method, ncols, time.perf_counter() - t0)))

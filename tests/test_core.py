@@ -143,3 +143,14 @@ def test_dataframe_arrow_roundtrip():
     # record batches (Spark mapInArrow delivers an iterator of them)
     b2 = DataFrame.fromArrow(t.to_batches(max_chunksize=2))
     np.testing.assert_array_equal(b2["label"], df["label"])
+
+
+def test_sas_scrubber():
+    from synapseml_amd.core.logging import payload, scrub
+
+    sig = "sig=" + "a1B2c3D4e5%2F" * 4 + "%3D"
+    msg = f"GET https://acct.blob.core.windows.net/c/f?sv=2020&{sig}&se=x failed"
+    out = scrub(msg)
+    assert "sig=####" in out and sig not in out and out.startswith("GET https://acct")
+    assert scrub("no token here") == "no token here"
+    assert "sig=####" in payload(object(), "fit", error=RuntimeError(msg))["errorMessage"]
