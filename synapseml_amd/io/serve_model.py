@@ -53,6 +53,72 @@ def model_handler(model, input_cols: List[str], output_cols: Optional[List[str]]
     return handle
 
 
+class DistributedServing:
+    """One serving worker process per device on ONE port (reference: DistributedHTTPSource - a server
+    per executor behind the cluster's load balancer - and ``readStream.distributedServer()``).
+
+    Every worker loads the saved pipeline, pins its GPU through ``HIP_VISIBLE_DEVICES`` and listens
+    with ``SO_REUSEPORT``: the kernel balances incoming connections across the workers, so each GPU
+    batches and scores its own share of the traffic with no front-end process. Replies carry
+    ``X-Served-By: <worker>``. The parent never touches the GPU; workers are child processes."""
+
+    def __init__(self, model_dir: str, num_workers: int, port: int, host: str = "127.0.0.1", input_cols: str = "features",
+                 output_cols: str = "", api: str = "", max_batch_size: int = 64, gpus: Optional[List[int]] = None,
+                 startup_timeout: float = 120.0):
+        import os
+        import subprocess
+        import sys
+        import time
+        import urllib.request
+
+        if port <= 0:
+            raise ValueError("DistributedServing needs an explicit port (every worker binds it)")
+        self.port, self.host, self.api = port, host, api
+        self.procs = []
+        for w in range(num_workers):
+            env = dict(os.environ)
+            if gpus is not None:
+                env["HIP_VISIBLE_DEVICES"] = str(gpus[w % len(gpus)])
+            cmd = [sys.executable, "-m", "synapseml_amd.io.serve_model", "--model", model_dir, "--host", host,
+                   "--port", str(port), "--input-cols", input_cols, "--output-cols", output_cols, "--api", api,
+                   "--max-batch-size", str(max_batch_size), "--reuse-port", "--worker-id", str(w)]
+            self.procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                               text=True))
+        # each worker prints one "serving ..." line once it listens
+        deadline = time.monotonic() + startup_timeout
+        for p in self.procs:
+            while True:
+                line = p.stdout.readline()
+                if line.startswith("serving"):
+                    break
+                if not line and p.poll() is not None or time.monotonic() > deadline:
+                    self.stop()
+                    raise RuntimeError(f"serving worker failed to start: {line!r}")
+
+    @property
+    def address(self) -> str:
+        return f"http://{self.host}:{self.port}/{self.api}"
+
+    def stop(self) -> None:
+        import signal as _signal
+
+        for p in self.procs:
+            if p.poll() is None:
+                p.send_signal(_signal.SIGTERM)
+        for p in self.procs:
+            try:
+                p.wait(20)
+            except Exception:  # noqa: BLE001 - escalate below
+                p.kill()
+                p.wait(5)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
+
+
 def main(argv=None) -> None:
     from ..core.serialize import load_stage
 
@@ -64,11 +130,29 @@ def main(argv=None) -> None:
     ap.add_argument("--port", type=int, default=8898)
     ap.add_argument("--api", default="")
     ap.add_argument("--max-batch-size", type=int, default=64)
+    ap.add_argument("--workers", type=int, default=1, help="worker processes on the port (one per GPU)")
+    ap.add_argument("--reuse-port", action="store_true", help="bind with SO_REUSEPORT (set for workers)")
+    ap.add_argument("--worker-id", default=None)
     a = ap.parse_args(argv)
+    if a.workers > 1:
+        import os
+
+        n_dev = int(os.environ.get("SML_SERVE_GPUS", "0")) or None
+        srv_d = DistributedServing(a.model, a.workers, a.port, a.host, a.input_cols, a.output_cols, a.api,
+                                   a.max_batch_size, gpus=list(range(n_dev)) if n_dev else None)
+        print(f"serving {a.workers} workers at {srv_d.address}", flush=True)
+        done = threading.Event()
+        signal.signal(signal.SIGTERM, lambda *_: done.set())
+        try:
+            done.wait()
+        except KeyboardInterrupt:
+            pass
+        srv_d.stop()
+        return
     model = load_stage(a.model)
     outs = [c for c in a.output_cols.split(",") if c] or None
     srv = ServingServer(model_handler(model, a.input_cols.split(","), outs), a.host, a.port, a.api,
-                        max_batch_size=a.max_batch_size).start()
+                        max_batch_size=a.max_batch_size, reuse_port=a.reuse_port, worker_id=a.worker_id).start()
     print(f"serving {type(model).__name__} at {srv.address}", flush=True)
     done = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: done.set())

@@ -141,7 +141,7 @@ class ServingServer:
 
     def __init__(self, transform: Callable[[DataFrame], DataFrame], host: str = "127.0.0.1", port: int = 0,
                  api: str = "", max_batch_size: int = 64, max_wait_ms: float = 0.0, reply_col: str = "reply",
-                 request_timeout: float = 60.0):
+                 request_timeout: float = 60.0, reuse_port: bool = False, worker_id: Optional[str] = None):
         self.transform_fn = transform
         self.api = api.strip("/")
         self.max_batch_size = max_batch_size
@@ -158,6 +158,10 @@ class ServingServer:
         self._loop = asyncio.new_event_loop()
         self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        if reuse_port:
+            # several worker processes (one per GPU) listen on one port; the kernel spreads connections
+            self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+        self.worker_id = worker_id  # echoed as X-Served-By on every reply
         self._sock.bind((host, port))
         self._sock.listen(1024)
         self._sock.setblocking(False)
@@ -247,7 +251,7 @@ class ServingServer:
                     writer.write(b"HTTP/1.1 404 Not Found\r\nContent-Length: 0\r\n\r\n")
                 else:
                     resp = await self._submit(make_request(target, method, headers, body, low.get("content-type")))
-                    writer.write(_serialize(resp))
+                    writer.write(_serialize(resp, self.worker_id))
                 await writer.drain()
                 if close:
                     break
@@ -309,7 +313,7 @@ class ServingServer:
             self.reply(rid, make_response("no reply produced", 500, "Internal Server Error"))
 
 
-def _serialize(resp: dict) -> bytes:
+def _serialize(resp: dict, worker_id: Optional[str] = None) -> bytes:
     st = resp.get("statusLine") or {}
     code = int(st.get("statusCode", 200))
     reason = st.get("reasonPhrase") or ""
@@ -320,6 +324,8 @@ def _serialize(resp: dict) -> bytes:
     for h in resp.get("headers") or []:
         if h["name"].lower() != "content-length":
             head.append(f"{h['name']}: {h['value']}")
+    if worker_id is not None:
+        head.append(f"X-Served-By: {worker_id}")
     head.append(f"Content-Length: {len(content)}")
     return ("\r\n".join(head) + "\r\n\r\n").encode("latin-1") + content
 

@@ -214,3 +214,36 @@ def test_serve_saved_model_end_to_end(tmp_path):
             r = json.loads(urllib.request.urlopen(urllib.request.Request(srv.address, data=body, method="POST"),
                                                   timeout=10).read())
             assert r["prediction"] == lab and len(r["probability"]) == 2
+
+
+def test_distributed_serving_reuse_port(tmp_path):
+    """Two worker processes share one port via SO_REUSEPORT (reference DistributedHTTPSource);
+    every reply is correct and carries the id of the worker that scored it."""
+    import json
+    import socket
+    import urllib.request
+
+    import numpy as np
+
+    from synapseml_amd.core import DataFrame
+    from synapseml_amd.io.serve_model import DistributedServing
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((400, 4))
+    y = (X[:, 1] > 0).astype(float)
+    LightGBMClassifier(numIterations=8, numLeaves=7, deviceType="cpu").fit(
+        DataFrame({"features": X, "label": y})).save(str(tmp_path / "m"))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    seen = set()
+    with DistributedServing(str(tmp_path / "m"), 2, port, output_cols="prediction") as d:
+        for i in range(40):
+            body = json.dumps({"features": X[i].tolist()}).encode()
+            resp = urllib.request.urlopen(urllib.request.Request(d.address, data=body, method="POST"), timeout=20)
+            seen.add(resp.headers["X-Served-By"])
+            assert json.loads(resp.read())["prediction"] == y[i]
+    assert seen <= {"0", "1"} and seen
+    assert all(p.poll() is not None for p in d.procs)
