@@ -30,6 +30,7 @@ def payload(stage, method: str, num_cols=None, seconds=None, error=None) -> dict
     p = {
         "modelUid": getattr(stage, "uid", None),
         "className": type(stage).__name__,
+        "module": type(stage).__module__,
         "method": method,
         "libraryVersion": LIBRARY_VERSION,
         "libraryName": LIBRARY_NAME,
@@ -45,16 +46,42 @@ def payload(stage, method: str, num_cols=None, seconds=None, error=None) -> dict
     return p
 
 
+_sinks: list = []
+
+
+def add_event_sink(fn) -> None:
+    """Receive every usage payload (dict) - e.g. utils.fabric.CertifiedEventClient's sink."""
+    if fn not in _sinks:
+        _sinks.append(fn)
+
+
+def remove_event_sink(fn) -> None:
+    if fn in _sinks:
+        _sinks.remove(fn)
+
+
+def _emit(p: dict) -> None:
+    if logger.isEnabledFor(logging.DEBUG):
+        logger.debug(json.dumps(p))
+    for fn in list(_sinks):
+        try:
+            fn(p)
+        except Exception:  # noqa: BLE001 - telemetry never breaks a fit/transform
+            logger.debug("event sink failed", exc_info=True)
+
+
 def log_verb(stage, method: str, fn, df=None):
     t0 = time.perf_counter()
     ncols = len(df.columns) if df is not None and hasattr(df, "columns") else None
+    active = bool(_sinks) or logger.isEnabledFor(logging.DEBUG)
     try:
         out = fn()
     except Exception as e:
-        if logger.isEnabledFor(logging.DEBUG):
-            logger.debug(json.dumps(payload(stage, method, ncols, time.perf_counter() - t0, e)))
-            logger.debug(scrub(traceback.format_exc()))
+        if active:
+            _emit(payload(stage, method, ncols, time.perf_counter() - t0, e))
+            if logger.isEnabledFor(logging.DEBUG):
+                logger.debug(scrub(traceback.format_exc()))
         raise
-    if logger.isEnabledFor(logging.DEBUG):
-        logger.debug(json.dumps(payload(stage, method, ncols, time.perf_counter() - t0)))
+    if active:
+        _emit(payload(stage, method, ncols, time.perf_counter() - t0))
     return out

@@ -4,6 +4,6 @@ from .featurize import (CleanMissingData, CleanMissingDataModel, CountSelector, 
                         Featurize, IndexToValue, MultiNGram, PageSplitter, TextFeaturizer, TextFeaturizerModel,
                         ValueIndexer, ValueIndexerModel, categorical_metadata)
 from .ml import (IDF, HashingTF, IDFModel, NGram, OneHotEncoder, OneHotEncoderModel, RegexTokenizer, StopWordsRemover,
-                 StringIndexer, StringIndexerModel, Tokenizer, VectorAssembler)
+                 StringIndexer, StringIndexerModel, Tokenizer, VectorAssembler, FastVectorAssembler)
 
 __all__ = [n for n in dir() if not n.startswith("_")]

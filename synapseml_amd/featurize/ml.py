@@ -285,3 +285,9 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol):
                         off += len(a)
             out.append(SparseVector(off, idx, val))
         return df.withColumn(self.getOutputCol(), _obj(out))
+
+
+class FastVectorAssembler(VectorAssembler):
+    """Assembler that keeps categorical slot metadata without a pass over the data (reference:
+    SPX/ml/feature/FastVectorAssembler.scala). Columnar assembly above never scans rows for
+    attribute metadata, so this is the same kernel under the reference's name."""

@@ -6,8 +6,10 @@ Hosted token services are not reachable offline; tokens come from the environmen
 ``running_on_fabric()``."""
 from __future__ import annotations
 
+import json
 import os
-from typing import Optional
+import urllib.request
+from typing import Dict, Optional
 
 from .platform import running_on_fabric
 
@@ -39,4 +41,54 @@ class FabricClient:
         return running_on_fabric() and FabricClient.MLWorkloadEndpointML() is not None
 
 
-__all__ = ["TokenLibrary", "OpenAITokenLibrary", "FabricClient"]
+# feature names used for certified events (reference: logging/FeatureNames.scala)
+FEATURE_NAMES = {"lightgbm": "LightGBM", "vw": "VowpalWabbit", "onnx": "ONNX", "services": "AiServices",
+                 "explainers": "Explainers", "causal": "Causal", "recommendation": "Recommendation",
+                 "featurize": "Featurize", "stages": "Core", "automl": "AutoML", "dl": "DeepLearning"}
+
+
+class CertifiedEventClient:
+    """Posts certified usage events to the Fabric telemetry endpoint (reference:
+    logging/fabric/CertifiedEventClient.scala:13-37). Only active when ``FabricClient.available()``;
+    ``install()`` subscribes it to every fit/transform payload of core.logging."""
+
+    @staticmethod
+    def feature_name(payload: Dict) -> str:
+        mod = str(payload.get("module", "")).split(".")
+        return FEATURE_NAMES.get(mod[1] if len(mod) > 1 else "", "SynapseML")
+
+    @staticmethod
+    def log_to_certified_events(feature_name: str, activity_name: str, attributes: Dict,
+                                endpoint: Optional[str] = None, timeout: float = 5.0) -> Optional[int]:
+        endpoint = endpoint or FabricClient.MLWorkloadEndpointML()
+        if endpoint is None:
+            return None
+        body = json.dumps({"timestamp": __import__("time").time(), "feature_name": feature_name,
+                           "activity_name": activity_name, "attributes": attributes}).encode()
+        req = urllib.request.Request(endpoint.rstrip("/") + "/telemetry", data=body, method="POST",
+                                     headers={"Content-Type": "application/json"})
+        auth = TokenLibrary.getAuthHeader()
+        if auth:
+            req.add_header("Authorization", auth)
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return r.status
+
+    @staticmethod
+    def sink(payload: Dict) -> None:
+        if payload.get("method") not in ("fit", "transform"):
+            return
+        attrs = {k: str(v) for k, v in payload.items() if k in ("className", "method", "modelUid", "errorType")}
+        CertifiedEventClient.log_to_certified_events(CertifiedEventClient.feature_name(payload),
+                                                     f"{payload.get('className')}.{payload.get('method')}", attrs)
+
+    @staticmethod
+    def install(force: bool = False) -> bool:
+        from ..core.logging import add_event_sink
+
+        if force or FabricClient.available():
+            add_event_sink(CertifiedEventClient.sink)
+            return True
+        return False
+
+
+__all__ = ["TokenLibrary", "OpenAITokenLibrary", "FabricClient", "CertifiedEventClient", "FEATURE_NAMES"]

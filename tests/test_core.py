@@ -154,3 +154,45 @@ def test_sas_scrubber():
     assert "sig=####" in out and sig not in out and out.startswith("GET https://acct")
     assert scrub("no token here") == "no token here"
     assert "sig=####" in payload(object(), "fit", error=RuntimeError(msg))["errorMessage"]
+
+
+def test_certified_events_sink():
+    """fit/transform payloads reach registered sinks; the Fabric client posts them to <endpoint>/telemetry."""
+    import json
+    import threading
+    from http.server import BaseHTTPRequestHandler, HTTPServer
+
+    import numpy as np
+
+    from synapseml_amd.core import DataFrame
+    from synapseml_amd.core.logging import add_event_sink, remove_event_sink
+    from synapseml_amd.featurize import VectorAssembler
+    from synapseml_amd.utils.fabric import CertifiedEventClient
+
+    got = []
+
+    class H(BaseHTTPRequestHandler):
+        def do_POST(self):  # noqa: N802
+            got.append((self.path, json.loads(self.rfile.read(int(self.headers["Content-Length"])))))
+            self.send_response(200)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    seen = []
+    try:
+        add_event_sink(seen.append)
+        df = DataFrame({"a": np.arange(3.0), "b": np.ones(3)})
+        VectorAssembler(inputCols=["a", "b"], outputCol="v").transform(df)
+        assert any(p["method"] == "transform" and p["className"] == "VectorAssembler" for p in seen)
+        st = CertifiedEventClient.log_to_certified_events(
+            CertifiedEventClient.feature_name(seen[-1]), "VectorAssembler.transform", {"k": "v"},
+            endpoint=f"http://127.0.0.1:{srv.server_port}")
+        assert st == 200 and got[0][0] == "/telemetry"
+        assert got[0][1]["feature_name"] == "Featurize" and got[0][1]["attributes"] == {"k": "v"}
+    finally:
+        remove_event_sink(seen.append)
+        srv.shutdown()
