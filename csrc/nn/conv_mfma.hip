@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "nn_ops.h"
 
@@ -63,7 +65,7 @@ __device__ __forceinline__ T FromF(float v) {
   return static_cast<T>(v);
 }
 
-template <class T, int BM, int BN>
+template <class T, int BM, int BN, bool kPro>
 __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int WM = BM / 2, WN = BN / 2;       // wave tile
@@ -102,43 +104,8 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
   }
   const T* __restrict__ x = static_cast<const T*>(a.x);
   const T* __restrict__ w = static_cast<const T*>(a.w);
-
-  uint4 ra[AR], rbv[BR];
-  auto load_tile = [&](int kt) {
-    const int k0 = kt * kBK;
-    const int tap = k0 / a.C;
-    const int c0 = k0 - tap * a.C + kc * 8;
-    const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int ih = rih[i] + r * a.dil_h, iw = riw[i] + s * a.dil_w;
-      const bool ok = rok[i] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(x + ((static_cast<int64_t>(rb[i]) * a.H + ih) * a.W + iw) * a.C + c0)
-                 : make_uint4(0, 0, 0, 0);
-      if (a.in_scale && ok) {
-        T* e = reinterpret_cast<T*>(&ra[i]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float v = ToF(e[j]) * a.in_scale[c0 + j] + a.in_shift[c0 + j];
-          e[j] = FromF<T>(a.prologue_relu ? fmaxf(v, 0.f) : v);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      rbv[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * K + k0 + kc * 8)
-                          : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < AR; ++i)
-      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + 32 * i) * kLd + kc * 8) = ra[i];
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + 32 * i) * kLd + kc * 8) = rbv[i];
-  };
+  constexpr bool pro = kPro;  // prologue affine present (a.in_scale != nullptr): a template
+                              // parameter, so no runtime branch sits between loads and their use
 
   f4 acc[TM][TN];
 #pragma unroll
@@ -149,12 +116,8 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
   const int fr = lane & 15, fk = 8 * (lane >> 4);
   const int nk = K / kBK;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int ks = 0; ks < kBK / 32; ++ks) {
       V8 af[TM], bf[TN];
@@ -169,6 +132,70 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
     }
+  };
+
+  // The global loads of tile kt+1 are issued before the MFMAs of tile kt and consumed (written to
+  // LDS) after them. The prologue affine is applied at that LDS write, not at the load, so prologue
+  // layers keep the same overlap (its per-channel scale/shift are loaded with the tile).
+  uint4 ra[AR], rbv[BR];
+  float4 q[4];
+  unsigned okm = 0;
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * kBK;
+    const int tap = k0 / a.C;
+    const int c0 = k0 - tap * a.C + kc * 8;
+    const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int ih = rih[i] + r * a.dil_h, iw = riw[i] + s * a.dil_w;
+      const bool ok = rok[i] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      okm |= ok ? (1u << i) : 0u;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(x + ((static_cast<int64_t>(rb[i]) * a.H + ih) * a.W + iw) * a.C + c0)
+                 : make_uint4(0, 0, 0, 0);
+    }
+    if constexpr (pro) {
+      q[0] = *reinterpret_cast<const float4*>(a.in_scale + c0);
+      q[1] = *reinterpret_cast<const float4*>(a.in_scale + c0 + 4);
+      q[2] = *reinterpret_cast<const float4*>(a.in_shift + c0);
+      q[3] = *reinterpret_cast<const float4*>(a.in_shift + c0 + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rbv[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * K + k0 + kc * 8)
+                          : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      uint4 v = ra[i];
+      if constexpr (pro) {
+        const float sc[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
+        const float sh[8] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+        T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = ToF(e[j]) * sc[j] + sh[j];
+          e[j] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
+        }
+        const unsigned mk = 0u - ((okm >> i) & 1u);  // padding taps stay 0, as in the unfused graph
+        v.x &= mk; v.y &= mk; v.z &= mk; v.w &= mk;
+      }
+      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + 32 * i) * kLd + kc * 8) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + 32 * i) * kLd + kc * 8) = rbv[i];
+  };
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    compute(buf);
     if (kt + 1 < nk) store_tile(buf ^ 1);
     __syncthreads();
   }
@@ -258,24 +285,35 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
 template <class T, int BM, int BN>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_mfma_kernel<T, BM, BN>), dim3(blocks), dim3(kThreads), 0, st, a);
+  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true> : conv_mfma_kernel<T, BM, BN, false>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(kThreads), 0, st, a);
 }
 
-// Tile choice: 128-row tiles unless that leaves fewer than two blocks per CU (256 CUs), then 64-row
-// tiles (small spatial extents late in the network).
 template <class T>
 void Launch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.OH * a.OW;
-  const int bn = a.Cout <= 64 ? 64 : 128;
-  const int blocks128 = ((M + 127) / 128) * ((a.Cout + bn - 1) / bn);
-  const bool small = blocks128 < 512;
-  if (bn == 64) {
-    if (small) LaunchTile<T, 64, 64>(a, M, st);
-    else LaunchTile<T, 128, 64>(a, M, st);
-  } else {
-    if (small) LaunchTile<T, 64, 128>(a, M, st);
-    else LaunchTile<T, 128, 128>(a, M, st);
+  // SML_CONV_TILE=BMxBN forces one tile shape (per-shape tuning sweeps)
+  static const int forced = [] {
+    const char* e = std::getenv("SML_CONV_TILE");
+    if (!e) return 0;
+    const int bm = std::atoi(e);
+    const char* x = std::strchr(e, 'x');
+    return x ? bm * 1000 + std::atoi(x + 1) : 0;
+  }();
+  switch (forced) {
+    case 64064: return LaunchTile<T, 64, 64>(a, M, st);
+    case 128064: return LaunchTile<T, 128, 64>(a, M, st);
+    case 64128: return LaunchTile<T, 64, 128>(a, M, st);
+    case 128128: return LaunchTile<T, 128, 128>(a, M, st);
+    default: break;
   }
+  // Tile choice (per-shape sweep over the ResNet-50 bottleneck shapes at batch 128, r2 conv1 logs):
+  // Cout <= 64 -> 64x64 (store-bound 1x1 layers want more blocks in flight); otherwise 128x128 when
+  // that still gives >= 384 blocks, else 64x128 (the 7x7 stage, 196 blocks of 128x128).
+  if (a.Cout <= 64) return LaunchTile<T, 64, 64>(a, M, st);
+  const int blocks128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
+  if (blocks128 >= 384) LaunchTile<T, 128, 128>(a, M, st);
+  else LaunchTile<T, 64, 128>(a, M, st);
 }
 
 }  // namespace

@@ -228,6 +228,19 @@ class ONNXModel(Transformer):
         # large chunks on a side stream, overlapped with the graph replays
         dense = {inp: col for inp, col in feeds.items() if _dense_tensor_column(df[col], in_info[inp])}
         prefetch = _DevicePrefetcher(df, dense, in_info, bs, n, sess) if dense and sess.gpu else None
+
+        def collect(start, end, handle):
+            outs = handle.result() if hasattr(handle, "result") else handle
+            for (col, _), o in zip(fetch.items(), outs):
+                if isinstance(o, np.ndarray) and o.ndim >= 2 and o.shape[0] == end - start and o.dtype != object:
+                    cols_out[col][start:end] = list(o)  # row views, no per-row conversion
+                    continue
+                parts = _split_output(o, end - start)
+                for j, v in enumerate(parts):
+                    cols_out[col][start + j] = _to_py(v)
+
+        # one mini-batch in flight: batch k+1 is queued on the GPU before batch k's outputs are collected
+        pending = None
         for start in range(0, n, bs):
             end = min(n, start + bs)
             batch_feeds = prefetch.batch(start, end) if prefetch is not None else {}
@@ -239,14 +252,13 @@ class ONNXModel(Transformer):
                     continue
                 vals = df[col][start:end]
                 batch_feeds[inp] = _coerce_batch(list(vals), in_info[inp])
-            outs = sess.run(names, batch_feeds)
-            for (col, _), o in zip(fetch.items(), outs):
-                if isinstance(o, np.ndarray) and o.ndim >= 2 and o.shape[0] == end - start and o.dtype != object:
-                    cols_out[col][start:end] = list(o)  # row views, no per-row conversion
-                    continue
-                parts = _split_output(o, end - start)
-                for j, v in enumerate(parts):
-                    cols_out[col][start + j] = _to_py(v)
+            run_async = getattr(sess, "run_async", None)
+            handle = run_async(names, batch_feeds) if run_async is not None else sess.run(names, batch_feeds)
+            if pending is not None:
+                collect(*pending)
+            pending = (start, end, handle)
+        if pending is not None:
+            collect(*pending)
         out = df
         for c, v in cols_out.items():
             out = out.withColumn(c, _maybe_numeric(v))

@@ -489,6 +489,30 @@ class InferenceSession:
             res = self.run_values(feeds, fetch)
         return [_to_host(v) for v in res]
 
+    def run_async(self, output_names: Optional[Sequence[str]], feeds: Dict[str, Any]) -> "_Pending":
+        """``run`` whose device->host copies are queued behind the graph replay: ``.result()`` waits and
+        returns what ``run`` would. The caller submits batch k+1 before collecting batch k, so the GPU
+        never idles while the host turns batch k's outputs into rows."""
+        fetch = list(output_names) if output_names else [o.name for o in self.outputs]
+        if not self.gpu:
+            return _Pending(self.run(fetch, feeds), None)
+        res = self._run_graph(feeds, fetch) if self.use_graph and self._graphable(feeds) else self.run_values(feeds, fetch)
+        if not all(isinstance(v, torch.Tensor) for v in res):
+            return _Pending([_to_host(v) for v in res], None)
+        outs = []
+        for v in res:
+            t = v.detach()
+            if t.is_floating_point() and t.dtype != torch.float64:
+                t = t.float()
+            if t.dim() == 4 and not t.is_contiguous():
+                t = t.contiguous()
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            outs.append(h)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return _Pending(outs, ev)
+
     # ------------------------------------------------------------------ HIP graphs
     def _graphable(self, feeds) -> bool:
         if any(vi.kind != "tensor" or vi.elem_type == P.STRING_T for vi in self.inputs + self.outputs):
@@ -688,6 +712,20 @@ def _scalar(v):
     if v is None:
         return None
     return float(v.reshape(-1)[0]) if isinstance(v, torch.Tensor) else float(np.asarray(v).reshape(-1)[0])
+
+
+class _Pending:
+    """Outputs of ``run_async``: pinned host tensors filled by queued copies (or ready values)."""
+
+    def __init__(self, outs, event):
+        self._outs, self._event = outs, event
+
+    def result(self) -> List[Any]:
+        if self._event is None:
+            return self._outs
+        self._event.synchronize()
+        # copy out of page-locked memory so the staging buffers go back to the pinned pool
+        return [np.array(h.numpy()) for h in self._outs]
 
 
 def _to_host(v):

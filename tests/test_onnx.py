@@ -319,6 +319,11 @@ def test_gpu_onnx_model_stage():
          .setFetchDict({"prediction": "output_label"}).setDeviceType("GPU"))
     out = m.transform(DataFrame({"features": feats}))
     assert out["prediction"].tolist() == (feats @ coef.T + inter).argmax(1).tolist()
+    # many prefetch chunks through the pinned staging ring (wraps 3 slots), float64 column cast to the
+    # model's float32 input while staging
+    feats64 = np.random.default_rng(1).random((1001, 4)) * 5
+    out = m.copy().setMiniBatchSize(7).transform(DataFrame({"features": feats64}))
+    assert out["prediction"].tolist() == (feats64.astype(np.float32) @ coef.T + inter).argmax(1).tolist()
 
 
 # ------------------------------------------------------------------ ImageFeaturizer
