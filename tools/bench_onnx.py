@@ -53,6 +53,8 @@ def main():
             print(json.dumps({"bench": "resnet50_session", "precision": prec, "batch": bs, "ms_per_batch": dt * 1e3,
                               "images_per_s": bs / dt, "hip_graph": not a.no_graph and dev == "cuda"}), flush=True)
     # end to end featurizer (decode from image rows, fused preprocess, headless features)
+    if a.images <= 0:
+        return
     rng = np.random.default_rng(0)
     col = np.empty(a.images, dtype=object)
     for i in range(a.images):
