@@ -65,141 +65,14 @@ __device__ __forceinline__ T FromF(float v) {
   return static_cast<T>(v);
 }
 
-template <class T, int BM, int BN, bool kPro>
-__global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
-  typedef typename Vec<T>::type V8;
-  constexpr int WM = BM / 2, WN = BN / 2;       // wave tile
-  constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
-  constexpr int AR = BM * kBK / 8 / kThreads;   // 16-B A chunks per thread per tile
-  constexpr int BR = BN * kBK / 8 / kThreads;   // 16-B B chunks per thread per tile
-  __shared__ __attribute__((aligned(16))) T lds[2 * (BM + BN) * kLd];
-  T* As = lds;
-  T* Bs = lds + 2 * BM * kLd;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int M = a.B * a.OH * a.OW;
-  const int K = a.R * a.S * a.C;
-  const int tiles_n = (a.Cout + BN - 1) / BN;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int total = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
-  const int tn = bid % tiles_n, tm = bid / tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // per-thread A rows (fixed across the K loop) and their input-window origin
-  const int kc = tid & 7;  // 16-B chunk within the 64-wide k tile
-  int rb[AR], rih[AR], riw[AR];
-  bool rok[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
-    rok[i] = m < M;
-    const int mm = rok[i] ? m : 0;
-    const int ow = mm % a.OW, t2 = mm / a.OW;
-    const int oh = t2 % a.OH;
-    rb[i] = t2 / a.OH;
-    rih[i] = oh * a.stride_h - a.pad_h;
-    riw[i] = ow * a.stride_w - a.pad_w;
-  }
-  const T* __restrict__ x = static_cast<const T*>(a.x);
-  const T* __restrict__ w = static_cast<const T*>(a.w);
-  constexpr bool pro = kPro;  // prologue affine present (a.in_scale != nullptr): a template
-                              // parameter, so no runtime branch sits between loads and their use
-
-  f4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-
+// Epilogue shared by the conv kernels: bias, ReLU, residual add and the optional second output,
+// staged per wave through LDS (lds must hold 4 * (BM/2) * (BN/2 + 8) elements and be free).
+template <class T, int WM, int WN>
+__device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 16][WN / 16], T* lds, int M, int m0,
+                                             int n0, int wid, int lane) {
+  constexpr int TM = WM / 16, TN = WN / 16;
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
-  const int nk = K / kBK;
-
-  auto compute = [&](int buf) {
-#pragma unroll
-    for (int ks = 0; ks < kBK / 32; ++ks) {
-      V8 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + wm0 + i * 16 + fr) * kLd + ks * 32 + fk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + wn0 + j * 16 + fr) * kLd + ks * 32 + fk);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
-    }
-  };
-
-  // The global loads of tile kt+1 are issued before the MFMAs of tile kt and consumed (written to
-  // LDS) after them. The prologue affine is applied at that LDS write, not at the load, so prologue
-  // layers keep the same overlap (its per-channel scale/shift are loaded with the tile).
-  uint4 ra[AR], rbv[BR];
-  float4 q[4];
-  unsigned okm = 0;
-  auto load_tile = [&](int kt) {
-    const int k0 = kt * kBK;
-    const int tap = k0 / a.C;
-    const int c0 = k0 - tap * a.C + kc * 8;
-    const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
-    okm = 0;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int ih = rih[i] + r * a.dil_h, iw = riw[i] + s * a.dil_w;
-      const bool ok = rok[i] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      okm |= ok ? (1u << i) : 0u;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(x + ((static_cast<int64_t>(rb[i]) * a.H + ih) * a.W + iw) * a.C + c0)
-                 : make_uint4(0, 0, 0, 0);
-    }
-    if constexpr (pro) {
-      q[0] = *reinterpret_cast<const float4*>(a.in_scale + c0);
-      q[1] = *reinterpret_cast<const float4*>(a.in_scale + c0 + 4);
-      q[2] = *reinterpret_cast<const float4*>(a.in_shift + c0);
-      q[3] = *reinterpret_cast<const float4*>(a.in_shift + c0 + 4);
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      rbv[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * K + k0 + kc * 8)
-                          : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      uint4 v = ra[i];
-      if constexpr (pro) {
-        const float sc[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
-        const float sh[8] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
-        T* e = reinterpret_cast<T*>(&v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float t = ToF(e[j]) * sc[j] + sh[j];
-          e[j] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
-        }
-        const unsigned mk = 0u - ((okm >> i) & 1u);  // padding taps stay 0, as in the unfused graph
-        v.x &= mk; v.y &= mk; v.z &= mk; v.w &= mk;
-      }
-      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + 32 * i) * kLd + kc * 8) = v;
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + 32 * i) * kLd + kc * 8) = rbv[i];
-  };
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
-    compute(buf);
-    if (kt + 1 < nk) store_tile(buf ^ 1);
-    __syncthreads();
-  }
-
+  const int fr = lane & 15;
   // epilogue part 1 (registers): lane holds column n = .. + (lane & 15), rows 4*(lane >> 4) + reg;
   // bias + ReLU in fp32, rounded to T (the unfused graph's conv output), staged per wave through LDS.
   T* __restrict__ y = static_cast<T*>(a.y);
@@ -282,38 +155,216 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_kernel(ConvArgs a) {
   }
 }
 
-template <class T, int BM, int BN>
+// kThr = 256 (4 waves, 2x2) or 512 (8 waves, 4x2: the 256x128 / 128x256 tiles, one block per CU)
+template <class T, int BM, int BN, bool kPro, int kThr = kThreads>
+__global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
+  typedef typename Vec<T>::type V8;
+  constexpr int kWavesM = kThr / 128;           // waves along M (2 along N)
+  constexpr int WM = BM / kWavesM, WN = BN / 2; // wave tile
+  constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
+  constexpr int AR = BM * kBK / 8 / kThr;       // 16-B A chunks per thread per tile
+  constexpr int BR = BN * kBK / 8 / kThr;       // 16-B B chunks per thread per tile
+  constexpr int RS = kThr / 8;                  // tile rows covered by one pass of the block
+  __shared__ __attribute__((aligned(16))) T lds[2 * (BM + BN) * kLd];
+  T* As = lds;
+  T* Bs = lds + 2 * BM * kLd;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = a.B * a.OH * a.OW;
+  const int K = a.R * a.S * a.C;
+  const int tiles_n = (a.Cout + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int total = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // Operands are read through buffer resources: a lane whose tap falls in the padding (or whose row
+  // is past M / channel past Cout) gets an out-of-range offset and the hardware returns zeros, so the
+  // loads need no select and no branch. Per row the valid taps are a bit mask computed once; per
+  // K tile a row costs one add, one bit test and one select (the tap / channel state is scalar).
+  const int kc = tid & 7;  // 16-B chunk within the 64-wide k tile
+  constexpr uint32_t kOob = 0x80000000u;
+  int abase[AR];       // element offset of the row's window origin (tap 0, channel kc*8)
+  uint64_t amask[AR];  // bit t: tap t = r*S + s is inside the input
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + (tid >> 3) + RS * i;
+    const int mm = m < M ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW;
+    const int oh = t2 % a.OH, b = t2 / a.OH;
+    const int ih0 = oh * a.stride_h - a.pad_h, iw0 = ow * a.stride_w - a.pad_w;
+    abase[i] = ((b * a.H + ih0) * a.W + iw0) * a.C + kc * 8;
+    uint64_t mk = 0;
+    if (m < M)
+      for (int r = 0, t = 0; r < a.R; ++r)
+        for (int s2 = 0; s2 < a.S; ++s2, ++t) {
+          const int ih = ih0 + r * a.dil_h, iw = iw0 + s2 * a.dil_w;
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) mk |= 1ull << t;
+        }
+    amask[i] = mk;
+  }
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, a.B * a.H * a.W * a.C * static_cast<int>(sizeof(T)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.w), 0, a.Cout * K * static_cast<int>(sizeof(T)), 0x00020000);
+  uint32_t boff[BR];  // byte offset of the thread's weight row chunk (out of range past Cout)
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + RS * i;
+    boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kc * 8) * static_cast<int>(sizeof(T))) : kOob;
+  }
+  constexpr bool pro = kPro;  // prologue affine present (a.in_scale != nullptr): a template
+                              // parameter, so no runtime branch sits between loads and their use
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int nk = K / kBK;
+
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < kBK / 32; ++ks) {
+      V8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + wm0 + i * 16 + fr) * kLd + ks * 32 + fk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + wn0 + j * 16 + fr) * kLd + ks * 32 + fk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+    }
+  };
+
+  // The global loads of tile kt+1 are issued before the MFMAs of tile kt and consumed (written to
+  // LDS) after them. The prologue affine is applied at that LDS write, not at the load, so prologue
+  // layers keep the same overlap (its per-channel scale/shift are loaded with the tile).
+  uint4 ra[AR], rbv[BR];
+  float4 q[4];
+  // next tile to load: tap (lr, ls) = index lt, channel offset lc0, element offset of the tap toff
+  int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0;
+  unsigned okm = 0;
+  auto load_tile = [&]() {
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const bool ok = (amask[i] >> lt) & 1ull;
+      okm |= ok ? (1u << i) : 0u;
+      const uint32_t vo = ok ? static_cast<uint32_t>((abase[i] + toff) * static_cast<int>(sizeof(T))) : kOob;
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(xres, vo, lc0 * static_cast<int>(sizeof(T)), 0);
+      ra[i] = *reinterpret_cast<uint4*>(&v);
+    }
+    if constexpr (pro) {
+      const float4* scp = reinterpret_cast<const float4*>(a.in_scale + lc0 + kc * 8);
+      const float4* shp = reinterpret_cast<const float4*>(a.in_shift + lc0 + kc * 8);
+      q[0] = scp[0];
+      q[1] = scp[1];
+      q[2] = shp[0];
+      q[3] = shp[1];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(wres, boff[i], lk0 * static_cast<int>(sizeof(T)), 0);
+      rbv[i] = *reinterpret_cast<uint4*>(&v);
+    }
+    // advance to the next K tile: 64 more channels, or the next tap
+    lk0 += kBK;
+    lc0 += kBK;
+    if (lc0 == a.C) {
+      lc0 = 0;
+      ++lt;
+      if (++ls == a.S) {
+        ls = 0;
+        ++lr;
+      }
+      toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      uint4 v = ra[i];
+      if constexpr (pro) {
+        const float sc[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
+        const float sh[8] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+        T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = ToF(e[j]) * sc[j] + sh[j];
+          e[j] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
+        }
+        const unsigned mk = 0u - ((okm >> i) & 1u);  // padding taps stay 0, as in the unfused graph
+        v.x &= mk; v.y &= mk; v.z &= mk; v.w &= mk;
+      }
+      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + RS * i) * kLd + kc * 8) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + RS * i) * kLd + kc * 8) = rbv[i];
+  };
+  load_tile();
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_tile();
+    compute(buf);
+    if (kt + 1 < nk) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  ConvEpilogue<T, WM, WN>(a, acc, lds, M, m0, n0, wid, lane);
+}
+
+template <class T, int BM, int BN, int kThr = kThreads>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
-  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true> : conv_mfma_kernel<T, BM, BN, false>;
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(kThreads), 0, st, a);
+  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr> : conv_mfma_kernel<T, BM, BN, false, kThr>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
 
 template <class T>
-void Launch(const ConvArgs& a, hipStream_t st) {
+int Launch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.OH * a.OW;
-  // SML_CONV_TILE=BMxBN forces one tile shape (per-shape tuning sweeps)
-  static const int forced = [] {
+  // SML_CONV_TILE=BMxBN forces one register-staged tile shape for the process (tuning sweeps);
+  // ConvArgs::kernel forces a kernel per call (tests)
+  static const int env_tile = [] {
     const char* e = std::getenv("SML_CONV_TILE");
     if (!e) return 0;
     const int bm = std::atoi(e);
     const char* x = std::strchr(e, 'x');
     return x ? bm * 1000 + std::atoi(x + 1) : 0;
   }();
-  switch (forced) {
-    case 64064: return LaunchTile<T, 64, 64>(a, M, st);
-    case 128064: return LaunchTile<T, 128, 64>(a, M, st);
-    case 64128: return LaunchTile<T, 64, 128>(a, M, st);
-    case 128128: return LaunchTile<T, 128, 128>(a, M, st);
-    default: break;
+  switch (a.kernel ? a.kernel : env_tile) {
+    case 64064: LaunchTile<T, 64, 64>(a, M, st); return 0;
+    case 128064: LaunchTile<T, 128, 64>(a, M, st); return 0;
+    case 64128: LaunchTile<T, 64, 128>(a, M, st); return 0;
+    case 128128: LaunchTile<T, 128, 128>(a, M, st); return 0;
+    case 256128: LaunchTile<T, 256, 128, 512>(a, M, st); return 0;
+    case 128256: LaunchTile<T, 128, 256, 512>(a, M, st); return 0;
+    case 0: break;
+    default: return -4;
   }
   // Tile choice (per-shape sweep over the ResNet-50 bottleneck shapes at batch 128, r2 conv1 logs):
   // Cout <= 64 -> 64x64 (store-bound 1x1 layers want more blocks in flight); otherwise 128x128 when
   // that still gives >= 384 blocks, else 64x128 (the 7x7 stage, 196 blocks of 128x128).
-  if (a.Cout <= 64) return LaunchTile<T, 64, 64>(a, M, st);
+  if (a.Cout <= 64) {
+    LaunchTile<T, 64, 64>(a, M, st);
+    return 0;
+  }
   const int blocks128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
   if (blocks128 >= 384) LaunchTile<T, 128, 128>(a, M, st);
   else LaunchTile<T, 64, 128>(a, M, st);
+  return 0;
 }
 
 }  // namespace
@@ -325,9 +376,13 @@ bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
 int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
   if (!ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return -1;
   if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
+  // buffer-resource offsets are 32-bit and the per-row tap mask holds 64 taps
+  if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * 2 >= (1ll << 31) ||
+      static_cast<int64_t>(a.Cout) * a.R * a.S * a.C * 2 >= (1ll << 31) || a.R * a.S > 64)
+    return -5;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (dtype == 1) Launch<_Float16>(a, st);
-  else Launch<__bf16>(a, st);
+  const int rc = dtype == 1 ? Launch<_Float16>(a, st) : Launch<__bf16>(a, st);
+  if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -41,15 +41,18 @@ PYBIND11_MODULE(_nn, m) {
   m.def("conv_supported", &ConvMfmaSupported);
   m.def("conv_mfma", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale, uintptr_t in_shift,
                         uintptr_t bias, uintptr_t res, uintptr_t out_scale, uintptr_t out_shift, uintptr_t y2,
-                        std::vector<int> g, int relu, int prologue_relu, int dtype, uintptr_t stream) {
+                        std::vector<int> g, int relu, int prologue_relu, int dtype, uintptr_t stream, int kernel) {
     if (g.size() != 15) throw std::invalid_argument("geometry: B,H,W,C,Cout,R,S,sh,sw,ph,pw,dh,dw,OH,OW");
     ConvArgs a{P<const void>(x), P<const void>(w), P<void>(y), P<const float>(in_scale), P<const float>(in_shift),
                P<const float>(bias), P<const void>(res), P<const float>(out_scale), P<const float>(out_shift),
                P<void>(y2), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13],
-               g[14], relu, prologue_relu};
+               g[14], relu, prologue_relu, kernel};
     const int rc = ConvMfma(a, dtype, P<void>(stream));
     if (rc != 0) throw std::runtime_error("conv_mfma failed (rc=" + std::to_string(rc) + ")");
-  });
+  }, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("in_scale"), pybind11::arg("in_shift"),
+     pybind11::arg("bias"), pybind11::arg("res"), pybind11::arg("out_scale"), pybind11::arg("out_shift"),
+     pybind11::arg("y2"), pybind11::arg("geom"), pybind11::arg("relu"), pybind11::arg("prologue_relu"),
+     pybind11::arg("dtype"), pybind11::arg("stream"), pybind11::arg("kernel") = 0);
   m.def("softmax_rows", [](uintptr_t x, int rows, int cols, uintptr_t y, uintptr_t amax, uintptr_t stream) {
     SoftmaxRows(P<const float>(x), rows, cols, P<float>(y), P<int64_t>(amax), P<void>(stream));
   });

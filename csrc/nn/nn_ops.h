@@ -33,6 +33,8 @@ struct ConvArgs {
   int B, H, W, C, Cout, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, OH, OW;
   int relu;            // 0 none, 1 after bias (before the residual add), 2 after the residual add
   int prologue_relu;   // relu after the prologue affine
+  int kernel = 0;      // 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128,
+                       // 128128, 256128, 128256)
 };
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);
 int ConvMfma(const ConvArgs& a, int dtype, void* stream);

@@ -625,7 +625,8 @@ def _mfma_ok(rt, at, inp, w) -> bool:
     return (rt.session._nn is not None and inp.is_cuda and inp.dim() == 4 and inp.dtype in (torch.float16, torch.bfloat16)
             and inp.dtype == w.dtype and w.dim() == 4 and at.get("group", 1) == 1 and inp.shape[1] % 64 == 0
             and inp.is_contiguous(memory_format=torch.channels_last) and w.permute(0, 2, 3, 1).is_contiguous()
-            and at.get("__act", 0) in (0, 1) and inp.data_ptr() % 16 == 0)
+            and at.get("__act", 0) in (0, 1) and inp.data_ptr() % 16 == 0
+            and inp.numel() * 2 < 2 ** 31 and w.numel() * 2 < 2 ** 31 and w.shape[2] * w.shape[3] <= 64)
 
 
 def _fused_conv(rt, at, x):

@@ -39,12 +39,13 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
                 bias: Optional[torch.Tensor] = None, relu=False,
                 in_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, in_relu: bool = True,
                 res: Optional[torch.Tensor] = None,
-                out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+                out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, kernel: int = 0):
     """y = conv(pro(x), w) + bias, ReLU, + res; optionally also y2 = relu(y * out_scale + out_shift).
 
     ``relu``: False/0 none, True/1 before the residual add, 2 after it. ``pad``: (top, left) or
     (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp16/bf16. ``wp``: packed [Cout, R, S, C]
-    (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2)."""
+    (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2).
+    ``kernel``: 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128, 128128, 256128, 128256)."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv2d_nhwc expects a channels_last input")
@@ -65,7 +66,7 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
         x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(in_affine[0] if in_affine else None),
         _ptr(in_affine[1] if in_affine else None), _ptr(bias), _ptr(res), _ptr(out_affine[0] if out_affine else None),
         _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu), _DT[x.dtype],
-        torch.cuda.current_stream(x.device).cuda_stream)
+        torch.cuda.current_stream(x.device).cuda_stream, int(kernel))
     return (y, y2) if out_affine is not None else y
 
 

@@ -22,16 +22,23 @@ def _ref(x, w, stride, pad, bias=None, relu=False, pro=None, res=None, post=None
     return y, y2
 
 
-def test_exact_integer_layout():
-    """Small integers are exact in fp16 and fp32: any lane/row/col mapping error shows as a mismatch."""
+# 0 = shape-chosen tile; BM*1000+BN = forced tile
+KERNELS = [0, 64064, 128064, 64128, 128128, 256128, 128256]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_exact_integer_layout(kernel):
+    """Small integers are exact in fp16 and fp32: any lane/row/col mapping (or LDS swizzle) error shows as a
+    mismatch. Shapes leave partial tiles in M and N and padding taps on every border."""
     from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
 
     g = torch.Generator().manual_seed(0)
-    x = torch.randint(-2, 3, (2, 64, 9, 7), generator=g).half().cuda().contiguous(memory_format=torch.channels_last)
-    w = torch.randint(-2, 3, (80, 64, 3, 3), generator=g).half().cuda()
-    y = conv2d_nhwc(x, pack_weight(w, torch.float16), 3, 3, (1, 1), (1, 1))
-    ref = F.conv2d(x.float(), w.float(), None, 1, 1)
-    torch.testing.assert_close(y.float(), ref, rtol=0, atol=0)
+    for (B, C, H, W, Co) in ((2, 64, 9, 7, 80), (3, 128, 17, 11, 200)):
+        x = torch.randint(-2, 3, (B, C, H, W), generator=g).half().cuda().contiguous(memory_format=torch.channels_last)
+        w = torch.randint(-2, 3, (Co, C, 3, 3), generator=g).half().cuda()
+        y = conv2d_nhwc(x, pack_weight(w, torch.float16), 3, 3, (1, 1), (1, 1), kernel=kernel)
+        ref = F.conv2d(x.float(), w.float(), None, 1, 1)
+        torch.testing.assert_close(y.float(), ref, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
@@ -52,10 +59,11 @@ def test_conv_matches_fp32_reference(dtype, shape):
     x = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)
     bias = torch.randn(Co, device="cuda")
-    y = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (st, st), (pd, pd), bias=bias, relu=True)
     ref, _ = _ref(x, w, st, pd, bias=bias, relu=True)
     tol = 2e-2 if dtype == torch.float16 else 8e-2
-    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+    for kernel in (0, 128128, 256128, 128256):
+        y = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: f"kernel {kernel}: {m}")
 
 
 def test_prologue_residual_dual_output():
@@ -73,6 +81,12 @@ def test_prologue_residual_dual_output():
     ry, ry2 = _ref(x, w, 1, 0, pro=pro, res=res, post=post)
     torch.testing.assert_close(y.float(), ry, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(y2.float(), ry2, rtol=2e-2, atol=3e-2)
+    # the same through the 8-wave 256x128 tile
+    yq, yq2 = conv2d_nhwc(x, pack_weight(w, dt), 1, 1, in_affine=pro, res=res, out_affine=post, kernel=256128)
+    torch.testing.assert_close(yq.float(), ry, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(yq2.float(), ry2, rtol=2e-2, atol=3e-2)
+    with pytest.raises(RuntimeError):  # unknown tile code
+        conv2d_nhwc(x, pack_weight(w, dt), 1, 1, kernel=12345)
     # padding taps stay zero with a prologue (3x3)
     w3 = (torch.randn(64, C, 3, 3, device="cuda") / (9 * C) ** 0.5).to(dt)
     y3 = conv2d_nhwc(x, pack_weight(w3, dt), 3, 3, (1, 1), (1, 1), in_affine=pro)
