@@ -247,78 +247,84 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 
   // The global loads of tile kt+1 are issued before the MFMAs of tile kt and consumed (written to
   // LDS) after them. The prologue affine is applied at that LDS write, not at the load, so prologue
-  // layers keep the same overlap (its per-channel scale/shift are loaded with the tile).
-  uint4 ra[AR], rbv[BR];
-  float4 q[4];
+  // layers keep the same overlap (its per-channel scale/shift are loaded with the tile). (A two-stage
+  // register pipeline - tile kt+2 in flight - measured 7 % slower: profiles/r2_onnx/README.)
+  struct Stage {
+    uint4 a[AR], b[BR];
+    float4 q[4];
+    unsigned okm;
+  };
   // next tile to load: tap (lr, ls) = index lt, channel offset lc0, element offset of the tap toff
-  int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0;
-  unsigned okm = 0;
-  auto load_tile = [&]() {
-    okm = 0;
+  int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0, loaded = 0;
+  auto load_tile = [&](Stage& st) {
+    st.okm = 0;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const bool ok = (amask[i] >> lt) & 1ull;
-      okm |= ok ? (1u << i) : 0u;
+      st.okm |= ok ? (1u << i) : 0u;
       const uint32_t vo = ok ? static_cast<uint32_t>((abase[i] + toff) * static_cast<int>(sizeof(T))) : kOob;
       auto v = __builtin_amdgcn_raw_buffer_load_b128(xres, vo, lc0 * static_cast<int>(sizeof(T)), 0);
-      ra[i] = *reinterpret_cast<uint4*>(&v);
+      st.a[i] = *reinterpret_cast<uint4*>(&v);
     }
     if constexpr (pro) {
       const float4* scp = reinterpret_cast<const float4*>(a.in_scale + lc0 + kc * 8);
       const float4* shp = reinterpret_cast<const float4*>(a.in_shift + lc0 + kc * 8);
-      q[0] = scp[0];
-      q[1] = scp[1];
-      q[2] = shp[0];
-      q[3] = shp[1];
+      st.q[0] = scp[0];
+      st.q[1] = scp[1];
+      st.q[2] = shp[0];
+      st.q[3] = shp[1];
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       auto v = __builtin_amdgcn_raw_buffer_load_b128(wres, boff[i], lk0 * static_cast<int>(sizeof(T)), 0);
-      rbv[i] = *reinterpret_cast<uint4*>(&v);
+      st.b[i] = *reinterpret_cast<uint4*>(&v);
     }
-    // advance to the next K tile: 64 more channels, or the next tap
-    lk0 += kBK;
-    lc0 += kBK;
-    if (lc0 == a.C) {
-      lc0 = 0;
-      ++lt;
-      if (++ls == a.S) {
-        ls = 0;
-        ++lr;
+    // advance to the next K tile (64 more channels, or the next tap)
+    if (++loaded < nk) {
+      lk0 += kBK;
+      lc0 += kBK;
+      if (lc0 == a.C) {
+        lc0 = 0;
+        ++lt;
+        if (++ls == a.S) {
+          ls = 0;
+          ++lr;
+        }
+        toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
       }
-      toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const Stage& st) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      uint4 v = ra[i];
+      uint4 v = st.a[i];
       if constexpr (pro) {
-        const float sc[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
-        const float sh[8] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+        const float sc[8] = {st.q[0].x, st.q[0].y, st.q[0].z, st.q[0].w, st.q[1].x, st.q[1].y, st.q[1].z, st.q[1].w};
+        const float sh[8] = {st.q[2].x, st.q[2].y, st.q[2].z, st.q[2].w, st.q[3].x, st.q[3].y, st.q[3].z, st.q[3].w};
         T* e = reinterpret_cast<T*>(&v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float t = ToF(e[j]) * sc[j] + sh[j];
           e[j] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
         }
-        const unsigned mk = 0u - ((okm >> i) & 1u);  // padding taps stay 0, as in the unfused graph
+        const unsigned mk = 0u - ((st.okm >> i) & 1u);  // padding taps stay 0, as in the unfused graph
         v.x &= mk; v.y &= mk; v.z &= mk; v.w &= mk;
       }
       *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + RS * i) * kLd + kc * 8) = v;
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + RS * i) * kLd + kc * 8) = rbv[i];
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + RS * i) * kLd + kc * 8) = st.b[i];
   };
-  load_tile();
-  store_tile(0);
+  Stage s0;
+  load_tile(s0);
+  store_tile(0, s0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile();
+    if (kt + 1 < nk) load_tile(s0);
     compute(buf);
-    if (kt + 1 < nk) store_tile(buf ^ 1);
+    if (kt + 1 < nk) store_tile(buf ^ 1, s0);
     __syncthreads();
   }
 

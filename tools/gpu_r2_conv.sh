@@ -12,8 +12,10 @@ rc=$?; echo "pytest rc=$rc $(tail -1 $OUT/pytest.log)"
 for T in ${TILES:-default 64x64 128x64 64x128 128x128}; do
   if [ "$T" = default ]; then
     timeout -k 10 300 python tools/bench_conv.py > $OUT/conv_$T.log 2>&1 || exit $?
-  elif [ "$T" = glds1 ] || [ "$T" = glds2 ]; then
-    SML_CONV_GLDS=${T#glds} timeout -k 10 300 python tools/bench_conv.py --no-ref > $OUT/conv_$T.log 2>&1 || exit $?
+  elif [ "$T" = depth2 ]; then
+    SML_CONV_DEPTH=2 timeout -k 10 300 python tools/bench_conv.py --no-ref > $OUT/conv_$T.log 2>&1 || exit $?
+  elif [ "$T" = depth1 ]; then
+    timeout -k 10 300 python tools/bench_conv.py --no-ref > $OUT/conv_$T.log 2>&1 || exit $?
   else
     SML_CONV_TILE=$T timeout -k 10 300 python tools/bench_conv.py --no-ref > $OUT/conv_$T.log 2>&1 || exit $?
   fi
