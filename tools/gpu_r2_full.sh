@@ -3,7 +3,7 @@
 set -o pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 cd "$ROOT"
-OUT=gpurun_out/full
+OUT=gpurun_out/${TAG:-full}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
@@ -21,3 +21,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof_rank" -o rank \
   -- python3 "$ROOT/tools/bench_ranker.py" --steps 5 --warmup 1 > "$ROOT/$OUT/prof_rank.log" 2>&1
 echo "rocprof rc=$?"
+cd "$ROOT"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
+echo "smoke rc=$? $(tail -1 $OUT/smoke.log)"
