@@ -131,7 +131,8 @@ __global__ void scale_kernel(float* w, uint64_t n, float s) {
 }  // namespace
 
 struct GpuSgd::Impl {
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, copy_stream = nullptr;
+  std::vector<hipEvent_t> events;
   float2* W = nullptr;
   uint64_t nw = 0;
   int64_t* indptr = nullptr;
@@ -156,6 +157,9 @@ struct GpuSgd::Impl {
   }
   ~Impl() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     (void)hipFree(W); (void)hipFree(indptr); (void)hipFree(idx); (void)hipFree(val);
     (void)hipFree(lab); (void)hipFree(wt); (void)hipFree(pred); (void)hipFree(loss);
     if (stream) (void)hipStreamDestroy(stream);
@@ -201,6 +205,7 @@ bool VwGpuAvailable() {
 GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cfg) {
   if (device >= 0) VW_HIP_CHECK(hipSetDevice(device));
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
+  VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
   impl_->nw = 1ull << cfg.bits;
   VW_HIP_CHECK(hipMalloc(&impl_->W, impl_->nw * sizeof(float2)));
   VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float2), impl_->stream));
@@ -216,25 +221,52 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
   if (n <= 0) return;
   const size_t nnz = static_cast<size_t>(indptr[n] - indptr[0]);
   impl_->Reserve(n, nnz);
-  hipStream_t s = impl_->stream;
+  hipStream_t s = impl_->stream, cs = impl_->copy_stream;
   std::vector<int64_t> ip(indptr, indptr + n + 1);
   for (auto& v : ip) v -= indptr[0];
   VW_HIP_CHECK(hipMemcpyAsync(impl_->indptr, ip.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  VW_HIP_CHECK(hipMemcpyAsync(impl_->idx, indices + indptr[0], nnz * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  VW_HIP_CHECK(hipMemcpyAsync(impl_->val, values + indptr[0], nnz * sizeof(float), hipMemcpyHostToDevice, s));
   VW_HIP_CHECK(hipMemcpyAsync(impl_->lab, labels, n * sizeof(float), hipMemcpyHostToDevice, s));
   if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), s));
   const uint64_t mask = impl_->nw - 1;
   batch = std::max(1, batch);
-  for (int64_t b0 = 0; b0 < n; b0 += batch) {
-    const int64_t b1 = std::min<int64_t>(n, b0 + batch);
-    const float eta = static_cast<float>(std::pow(examples_ + b0 + 1.0, -static_cast<double>(cfg_.power_t)));
-    const int grid = static_cast<int>((b1 - b0 + kWavesPerBlock - 1) / kWavesPerBlock);
-    hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(64 * kWavesPerBlock), 0, s, impl_->indptr, impl_->idx,
-                       impl_->val, impl_->lab, weights ? impl_->wt : nullptr, b0, b1, impl_->W, mask, cfg_.lr,
-                       cfg_.l2, cfg_.loss, cfg_.adaptive ? 1 : 0, eta, impl_->pred, impl_->loss, 1);
-    VW_HIP_CHECK(hipGetLastError());
+  // The pass's feature ids / values stream in chunks of 16 mini-batches on a copy stream: the
+  // (host-blocking, pageable) copy of chunk k+1 runs while the device learns chunk k, so the
+  // host->device traffic (8 B per nonzero) hides behind the SGD instead of preceding it.
+  const int64_t chunk_rows = static_cast<int64_t>(batch) * 16;
+  const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
+  if (impl_->events.size() < static_cast<size_t>(nchunks)) {
+    for (size_t i = impl_->events.size(); i < static_cast<size_t>(nchunks); ++i) {
+      hipEvent_t e;
+      VW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      impl_->events.push_back(e);
+    }
+  }
+  auto copy_chunk = [&](int64_t c) {
+    const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
+    const size_t p0 = static_cast<size_t>(ip[r0]), p1 = static_cast<size_t>(ip[r1]);
+    if (p1 > p0) {
+      VW_HIP_CHECK(hipMemcpyAsync(impl_->idx + p0, indices + indptr[0] + p0, (p1 - p0) * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, cs));
+      VW_HIP_CHECK(hipMemcpyAsync(impl_->val + p0, values + indptr[0] + p0, (p1 - p0) * sizeof(float),
+                                  hipMemcpyHostToDevice, cs));
+    }
+    VW_HIP_CHECK(hipEventRecord(impl_->events[c], cs));
+  };
+  copy_chunk(0);
+  for (int64_t c = 0; c < nchunks; ++c) {
+    VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
+    const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
+    for (int64_t b0 = r0; b0 < r1; b0 += batch) {
+      const int64_t b1 = std::min<int64_t>(r1, b0 + batch);
+      const float eta = static_cast<float>(std::pow(examples_ + b0 + 1.0, -static_cast<double>(cfg_.power_t)));
+      const int grid = static_cast<int>((b1 - b0 + kWavesPerBlock - 1) / kWavesPerBlock);
+      hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(64 * kWavesPerBlock), 0, s, impl_->indptr, impl_->idx,
+                         impl_->val, impl_->lab, weights ? impl_->wt : nullptr, b0, b1, impl_->W, mask, cfg_.lr,
+                         cfg_.l2, cfg_.loss, cfg_.adaptive ? 1 : 0, eta, impl_->pred, impl_->loss, 1);
+      VW_HIP_CHECK(hipGetLastError());
+    }
+    if (c + 1 < nchunks) copy_chunk(c + 1);
   }
   float l = 0;
   VW_HIP_CHECK(hipMemcpyAsync(&l, impl_->loss, sizeof(float), hipMemcpyDeviceToHost, s));
