@@ -59,7 +59,7 @@ class RcclComm : public Comm {
     SML_HIP_CHECK(hipMalloc(&scratch_, 64));
   }
   ~RcclComm() override {
-    if (comm_) ncclCommDestroy(comm_);
+    if (comm_) ncclCommDestroy(comm_);  // (null after an abort)
     if (scratch_) (void)hipFree(scratch_);
   }
   int rank() const override { return rank_; }
@@ -79,6 +79,18 @@ class RcclComm : public Comm {
   void AllReduceDeviceF32(float* buf, int64_t n, void* stream) override {
     if (world_ <= 1) return;
     SML_NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, comm_, static_cast<hipStream_t>(stream)));
+  }
+  // Called once per tree by the backend (RCCL async-error polling): a peer that died or
+  // a broken link surfaces as an exception on every rank instead of a collective that never returns.
+  void Check() override {
+    if (!comm_ || world_ <= 1) return;
+    ncclResult_t async = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &async) != ncclSuccess) return;
+    if (async != ncclSuccess && async != ncclInProgress) {
+      (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+      throw std::runtime_error(std::string("RCCL communicator failed: ") + ncclGetErrorString(async));
+    }
   }
   void AllReduceDeviceF64(double* buf, int64_t n, void* stream) override {
     if (world_ <= 1) return;
