@@ -94,6 +94,11 @@ class DistributedServing:
                 if not line and p.poll() is not None or time.monotonic() > deadline:
                     self.stop()
                     raise RuntimeError(f"serving worker failed to start: {line!r}")
+        # keep draining each worker's output (a full pipe would block a worker that logs)
+        import threading as _threading
+
+        for p in self.procs:
+            _threading.Thread(target=lambda f=p.stdout: [None for _ in f], daemon=True).start()
 
     @property
     def address(self) -> str:
