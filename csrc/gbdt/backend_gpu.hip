@@ -245,6 +245,12 @@ __device__ __forceinline__ double WaveSumD(double v) {
   return v;
 }
 
+__device__ __forceinline__ float WaveSumF(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
 // Full-wave sum on the DPP network (no LDS crossbar): xor-1 / xor-2 quad
 // permutes, half-row and row mirrors give every row its sum, row_bcast:15 and
 // row_bcast:31 fold the rows into lane 63, v_readlane broadcasts it. All 64
@@ -306,9 +312,10 @@ __device__ __forceinline__ void PairLambda(const RankTables& t, const double* s_
 
 // Register-path form: each document's label gain and rank discount are
 // looked up once (fp32) instead of per pair, so the O(pairs) loop is ALU only.
+template <class A>
 __device__ __forceinline__ void PairLambdaPre(float sig, float imd, bool use_norm, double si, int li, float gi,
-                                              float di, double sj, int lj, float gj, float dj, double* lam,
-                                              double* hes, double* suml) {
+                                              float di, double sj, int lj, float gj, float dj, A* lam,
+                                              A* hes, A* suml) {
   const bool i_high = li > lj;
   const float gap = i_high ? gi - gj : gj - gi;
   const float pd = fabsf(di - dj);
@@ -560,28 +567,29 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   const float sig = static_cast<float>(t.sigma);
   const float fimd = static_cast<float>(t.inv_max_dcg[q]);
   const bool use_norm = t.norm && mx != mn;
-  double lam[NU], hes[NU];
+  // fp32 accumulators: a document sums at most max_position + cnt pair terms, each already fp32
+  float lam[NU], hes[NU];
 #pragma unroll
-  for (int u = 0; u < NU; ++u) { lam[u] = 0.0; hes[u] = 0.0; }
-  double suml = 0.0;
+  for (int u = 0; u < NU; ++u) { lam[u] = 0.f; hes[u] = 0.f; }
+  float suml = 0.f;
   // (a) top document r against every document (partners on the lanes). Grouping four top documents
   // so their wave sums interleave measured no faster (1.44 vs 1.35 ms per call): not shuffle-latency bound.
-  double top_la = 0.0, top_he = 0.0;  // lane r keeps the reduced lambdas of top document r
+  float top_la = 0.f, top_he = 0.f;  // lane r keeps the reduced lambdas of top document r
   for (int r = 0; r < ntop; ++r) {
     const double si = ReadLaneD(tsc, r);
     const int li = __builtin_amdgcn_readlane(tlab, r);
     const int di = __builtin_amdgcn_readlane(tdoc, r);
     const float gi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tgn), r));
     const float dci = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tdc), r));
-    double la = 0.0, he = 0.0;
+    float la = 0.f, he = 0.f;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int j = u * 64 + lane;
       if (j < cnt && j != di && lab[u] != li)
         PairLambdaPre(sig, fimd, use_norm, si, li, gi, dci, sc[u], lab[u], gn[u], dc[u], &la, &he, &suml);
     }
-    la = WaveSumD(la);
-    he = WaveSumD(he);
+    la = WaveSumF(la);
+    he = WaveSumF(he);
     if (lane == r) { top_la = la; top_he = he; }
   }
   // (b) every non-top document against the top list
@@ -598,8 +606,8 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
                     &suml);
     }
   }
-  suml = WaveSumD(suml);
-  const double nf = (t.norm && suml > 0) ? log2(1.0 + suml) / suml : 1.0;
+  const double sumd = WaveSumF(suml);
+  const double nf = (t.norm && sumd > 0) ? log2(1.0 + sumd) / sumd : 1.0;
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int i = u * 64 + lane;
