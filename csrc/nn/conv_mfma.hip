@@ -1,5 +1,5 @@
 // Implicit-GEMM convolution on the CDNA4 matrix cores with fused prologue and
-// epilogue (module _nn, used by the ONNX executor for NHWC fp16/bf16 graphs).
+// epilogue (module _nn, used by the ONNX executor for NHWC fp32/fp16/bf16 graphs).
 //
 //   y[m, n]  = epi( sum_k pro(x_col[m, k]) * w[n, k] )
 //   m = (b, oh, ow) output pixel, n = output channel, k = (r, s, c) tap x input
@@ -10,15 +10,20 @@
 //            optional second output y2 = relu(y * out_scale[n] + out_shift[n])
 //            (the next pre-activation block's input, written from registers).
 //
-// Tiling: 256 threads = 4 waves in 2x2, block tile BM x BN x BK=64, wave tile
-// (BM/2) x (BN/2) of 16x16x32 MFMAs (f16 or bf16 in, fp32 accumulate). A and B
+// Tiling: 256 threads = 4 waves in 2x2, block tile BM x BN x 128 bytes of K
+// (BK = 64 f16/bf16 or 32 f32 elements), wave tile (BM/2) x (BN/2) of 16x16x32
+// f16/bf16 MFMAs, or of 16x16x4 f32 MFMAs (exact f32, the fp32 graphs: ORT
+// parity without TF32-style rounding; gfx950 has no xf32). A and B
 // tiles are staged through registers (the prologue is applied there) into a
 // double-buffered LDS image with a 144-byte row pitch (conflict-free 16-lane
 // ds_read_b128 fragment reads); the next tile's global loads are issued before
 // the current tile's MFMAs so HBM latency hides behind matrix work. Blocks are
 // remapped so that each XCD owns a contiguous run of (m, n) tiles: the blocks
 // that share an activation tile (all n for one m) sit on one XCD's L2.
-// Requires C % 64 == 0 (every ResNet conv but the 3-channel stem).
+// The f32 form reads one 16-B fragment per lane and operand (k = 4*(lane>>4)..+3)
+// and issues four MFMAs from its components: A and B use the same k order, so
+// the 16-k sum is the same set of products (k order within an fmaf chain).
+// Requires C % BK == 0 (every ResNet conv but the 3-channel stem).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -34,10 +39,15 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBK = 64;
-constexpr int kPad = 8;  // elements of row padding (16 B)
-constexpr int kLd = kBK + kPad;
+constexpr int kBKBytes = 128;  // K extent of a tile row in bytes (8 16-B chunks)
 constexpr int kThreads = 256;
+// per element type: K elements per tile, elements per 16-B chunk, LDS row pitch (16 B of padding)
+template <class T>
+struct Tile {
+  static constexpr int BK = kBKBytes / static_cast<int>(sizeof(T));
+  static constexpr int EPV = 16 / static_cast<int>(sizeof(T));
+  static constexpr int LD = BK + EPV;
+};
 
 template <class T>
 struct Vec;
@@ -54,6 +64,10 @@ struct Vec<__bf16> {
   static __device__ __forceinline__ f4 mfma(const b8& a, const b8& b, const f4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
+};
+template <>
+struct Vec<float> {
+  typedef f4 type;  // four consecutive k of one row: the operands of four 16x16x4 MFMAs
 };
 
 template <class T>
@@ -81,6 +95,7 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
   // relu=1: before the residual add; relu=2: after it (identical without a residual)
   const bool relu_pre = a.relu == 1 || (a.relu == 2 && res == nullptr);
   const bool relu_post = a.relu == 2 && res != nullptr;
+  constexpr int EPV = Tile<T>::EPV;
   if ((a.Cout & 7) == 0) {
     constexpr int CL = WN + 8;  // staged row pitch (elements)
     T* Ct = lds + wid * WM * CL;
@@ -99,21 +114,21 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
     }
     __syncthreads();
     // part 2: 16-B row chunks -> residual add, dual output, coalesced 16-B stores
-    constexpr int CPR = WN / 8;
+    constexpr int CPR = WN / EPV;
 #pragma unroll
     for (int it = 0; it < WM * CPR / 64; ++it) {
       const int idx = it * 64 + lane;
       const int row = idx / CPR, ch = idx % CPR;
-      const int m = m0 + wm0 + row, n = n0 + wn0 + ch * 8;
+      const int m = m0 + wm0 + row, n = n0 + wn0 + ch * EPV;
       if (m >= M || n >= a.Cout) continue;
-      uint4 pv = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * 8);
+      uint4 pv = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * EPV);
       const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
       if (res) {
         const uint4 rv = *reinterpret_cast<const uint4*>(res + o);
         T* pe = reinterpret_cast<T*>(&pv);
         const T* re = reinterpret_cast<const T*>(&rv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < EPV; ++e) {
           const float v = ToF(pe[e]) + ToF(re[e]);
           pe[e] = FromF<T>(relu_post ? fmaxf(v, 0.f) : v);
         }
@@ -124,7 +139,7 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
         const T* pe = reinterpret_cast<const T*>(&pv);
         T* qe = reinterpret_cast<T*>(&qv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * a.out_scale[n + e] + a.out_shift[n + e], 0.f));
+        for (int e = 0; e < EPV; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * a.out_scale[n + e] + a.out_shift[n + e], 0.f));
         *reinterpret_cast<uint4*>(y2 + o) = qv;
       }
     }
@@ -159,12 +174,15 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 template <class T, int BM, int BN, bool kPro, int kThr = kThreads>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
+  constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
   constexpr int kWavesM = kThr / 128;           // waves along M (2 along N)
   constexpr int WM = BM / kWavesM, WN = BN / 2; // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
-  constexpr int AR = BM * kBK / 8 / kThr;       // 16-B A chunks per thread per tile
-  constexpr int BR = BN * kBK / 8 / kThr;       // 16-B B chunks per thread per tile
+  constexpr int AR = BM * kBKBytes / 16 / kThr;  // 16-B A chunks per thread per tile
+  constexpr int BR = BN * kBKBytes / 16 / kThr;  // 16-B B chunks per thread per tile
   constexpr int RS = kThr / 8;                  // tile rows covered by one pass of the block
+  // the epilogue re-uses the operand buffers to stage each wave's tile
+  static_assert(2 * (BM + BN) * kLd >= (kThr / 64) * WM * (WN + 8), "epilogue staging exceeds the LDS tile");
   __shared__ __attribute__((aligned(16))) T lds[2 * (BM + BN) * kLd];
   T* As = lds;
   T* Bs = lds + 2 * BM * kLd;
@@ -195,7 +213,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     const int ow = mm % a.OW, t2 = mm / a.OW;
     const int oh = t2 % a.OH, b = t2 / a.OH;
     const int ih0 = oh * a.stride_h - a.pad_h, iw0 = ow * a.stride_w - a.pad_w;
-    abase[i] = ((b * a.H + ih0) * a.W + iw0) * a.C + kc * 8;
+    abase[i] = ((b * a.H + ih0) * a.W + iw0) * a.C + kc * EPV;
     uint64_t mk = 0;
     if (m < M)
       for (int r = 0, t = 0; r < a.R; ++r)
@@ -213,7 +231,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int n = n0 + (tid >> 3) + RS * i;
-    boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kc * 8) * static_cast<int>(sizeof(T))) : kOob;
+    boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kc * EPV) * static_cast<int>(sizeof(T))) : kOob;
   }
   constexpr bool pro = kPro;  // prologue affine present (a.in_scale != nullptr): a template
                               // parameter, so no runtime branch sits between loads and their use
@@ -225,23 +243,45 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int fr = lane & 15, fk = EPV * (lane >> 4);
   const int nk = K / kBK;
 
   auto compute = [&](int buf) {
+    if constexpr (sizeof(T) == 4) {
+      // 16 k per step; lane group g = lane >> 4 holds k = 4g..4g+3 of its A row and B column, and MFMA c
+      // takes component c of both: every (k, row, col) product is summed exactly once
 #pragma unroll
-    for (int ks = 0; ks < kBK / 32; ++ks) {
-      V8 af[TM], bf[TN];
+      for (int ks = 0; ks < kBK / 16; ++ks) {
+        f4 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + wm0 + i * 16 + fr) * kLd + ks * 32 + fk);
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const f4*>(As + (buf * BM + wm0 + i * 16 + fr) * kLd + ks * 16 + fk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + wn0 + j * 16 + fr) * kLd + ks * 32 + fk);
+        for (int j = 0; j < TN; ++j)
+          bf[j] = *reinterpret_cast<const f4*>(Bs + (buf * BN + wn0 + j * 16 + fr) * kLd + ks * 16 + fk);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][c], bf[j][c], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < kBK / 32; ++ks) {
+        V8 af[TM], bf[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + wm0 + i * 16 + fr) * kLd + ks * 32 + fk);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + wn0 + j * 16 + fr) * kLd + ks * 32 + fk);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+      }
     }
   };
 
@@ -249,9 +289,10 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   // LDS) after them. The prologue affine is applied at that LDS write, not at the load, so prologue
   // layers keep the same overlap (its per-channel scale/shift are loaded with the tile). (A two-stage
   // register pipeline - tile kt+2 in flight - measured 7 % slower: profiles/r2_onnx/README.)
+  constexpr int NQ = EPV / 4;  // float4s of prologue scale (and of shift) per 16-B chunk
   struct Stage {
     uint4 a[AR], b[BR];
-    float4 q[4];
+    f4 q[2 * NQ];
     unsigned okm;
   };
   // next tile to load: tap (lr, ls) = index lt, channel offset lc0, element offset of the tap toff
@@ -267,12 +308,13 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
       st.a[i] = *reinterpret_cast<uint4*>(&v);
     }
     if constexpr (pro) {
-      const float4* scp = reinterpret_cast<const float4*>(a.in_scale + lc0 + kc * 8);
-      const float4* shp = reinterpret_cast<const float4*>(a.in_shift + lc0 + kc * 8);
-      st.q[0] = scp[0];
-      st.q[1] = scp[1];
-      st.q[2] = shp[0];
-      st.q[3] = shp[1];
+      const f4* scp = reinterpret_cast<const f4*>(a.in_scale + lc0 + kc * EPV);
+      const f4* shp = reinterpret_cast<const f4*>(a.in_shift + lc0 + kc * EPV);
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) {
+        st.q[t] = scp[t];
+        st.q[NQ + t] = shp[t];
+      }
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
@@ -299,22 +341,20 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     for (int i = 0; i < AR; ++i) {
       uint4 v = st.a[i];
       if constexpr (pro) {
-        const float sc[8] = {st.q[0].x, st.q[0].y, st.q[0].z, st.q[0].w, st.q[1].x, st.q[1].y, st.q[1].z, st.q[1].w};
-        const float sh[8] = {st.q[2].x, st.q[2].y, st.q[2].z, st.q[2].w, st.q[3].x, st.q[3].y, st.q[3].z, st.q[3].w};
         T* e = reinterpret_cast<T*>(&v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float t = ToF(e[j]) * sc[j] + sh[j];
+        for (int j = 0; j < EPV; ++j) {
+          const float t = ToF(e[j]) * st.q[j >> 2][j & 3] + st.q[NQ + (j >> 2)][j & 3];
           e[j] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
         }
         const unsigned mk = 0u - ((st.okm >> i) & 1u);  // padding taps stay 0, as in the unfused graph
         v.x &= mk; v.y &= mk; v.z &= mk; v.w &= mk;
       }
-      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + RS * i) * kLd + kc * 8) = v;
+      *reinterpret_cast<uint4*>(As + (buf * BM + (tid >> 3) + RS * i) * kLd + kc * EPV) = v;
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + RS * i) * kLd + kc * 8) = st.b[i];
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + (tid >> 3) + RS * i) * kLd + kc * EPV) = st.b[i];
   };
   Stage s0;
   load_tile(s0);
@@ -355,15 +395,24 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 128064: LaunchTile<T, 128, 64>(a, M, st); return 0;
     case 64128: LaunchTile<T, 64, 128>(a, M, st); return 0;
     case 128128: LaunchTile<T, 128, 128>(a, M, st); return 0;
-    case 256128: LaunchTile<T, 256, 128, 512>(a, M, st); return 0;
-    case 128256: LaunchTile<T, 128, 256, 512>(a, M, st); return 0;
+    case 256128:
+    case 128256:
+      // 8-wave tiles: the f32 epilogue staging would not fit the operand LDS
+      if constexpr (sizeof(T) == 2) {
+        if ((a.kernel ? a.kernel : env_tile) == 256128) LaunchTile<T, 256, 128, 512>(a, M, st);
+        else LaunchTile<T, 128, 256, 512>(a, M, st);
+        return 0;
+      }
+      return -4;
     case 0: break;
     default: return -4;
   }
   // Tile choice (per-shape sweep over the ResNet-50 bottleneck shapes at batch 128, r2 conv1 logs):
   // Cout <= 64 -> 64x64 (store-bound 1x1 layers want more blocks in flight); otherwise 128x128 when
   // that still gives >= 384 blocks, else 64x128 (the 7x7 stage, 196 blocks of 128x128).
-  if (a.Cout <= 64) {
+  // f32: 64x64 on every shape (r2_fp32conv sweep: 2625 us over the 14 shapes vs 2865-3258 for the larger
+  // tiles; 36 KB of LDS, four blocks per CU hide the per-tile barrier behind the 32-cycle MFMAs)
+  if (a.Cout <= 64 || sizeof(T) == 4) {
     LaunchTile<T, 64, 64>(a, M, st);
     return 0;
   }
@@ -375,19 +424,22 @@ int Launch(const ConvArgs& a, hipStream_t st) {
 
 }  // namespace
 
+// dtype: 0 fp32, 1 fp16, 2 bf16 (C must be a multiple of one tile's K: 32 f32 / 64 f16/bf16 channels)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
-  return groups == 1 && C % kBK == 0 && C > 0 && Cout > 0 && (dtype == 1 || dtype == 2);
+  const int bk = dtype == 0 ? Tile<float>::BK : Tile<_Float16>::BK;
+  return groups == 1 && C > 0 && C % bk == 0 && Cout > 0 && (dtype == 0 || dtype == 1 || dtype == 2);
 }
 
 int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
   if (!ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return -1;
   if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
   // buffer-resource offsets are 32-bit and the per-row tap mask holds 64 taps
-  if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * 2 >= (1ll << 31) ||
-      static_cast<int64_t>(a.Cout) * a.R * a.S * a.C * 2 >= (1ll << 31) || a.R * a.S > 64)
+  const int64_t es = dtype == 0 ? 4 : 2;
+  if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * es >= (1ll << 31) ||
+      static_cast<int64_t>(a.Cout) * a.R * a.S * a.C * es >= (1ll << 31) || a.R * a.S > 64)
     return -5;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int rc = dtype == 1 ? Launch<_Float16>(a, st) : Launch<__bf16>(a, st);
+  const int rc = dtype == 0 ? Launch<float>(a, st) : dtype == 1 ? Launch<_Float16>(a, st) : Launch<__bf16>(a, st);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -115,7 +115,7 @@ class InferenceSession:
             nodes = self._fold_constants(nodes)
             nodes = self._fold_conv_bn(nodes)
             nodes = self._fuse_epilogues(nodes)
-            if self._nn is not None and self.channels_last and self.compute_dtype != torch.float32:
+            if self._nn is not None and self.channels_last:
                 nodes = self._fuse_prologues(nodes)
         self.nodes = nodes
         self._place_constants()
@@ -296,7 +296,7 @@ class InferenceSession:
                 and w.shape[1] % 64 == 0 and n.attrs.get("__act", 0) in (0, 1))
 
     def _fuse_prologues(self, nodes: List[Node]) -> List[Node]:
-        """MFMA-conv fusions (GPU, fp16/bf16, channels_last):
+        """MFMA-conv fusions (GPU, channels_last; fp32 runs the exact f32-input MFMA form):
 
         * a per-channel BN(+ReLU) whose every consumer is an MFMA conv is applied in those convs' A-tile
           loaders (prologue) instead of being materialised — the pre-activation of ResNet-v2 blocks;
@@ -622,11 +622,13 @@ def _affine_act(rt, x, scale, shift, res, act, alpha, out=None):
 
 
 def _mfma_ok(rt, at, inp, w) -> bool:
-    return (rt.session._nn is not None and inp.is_cuda and inp.dim() == 4 and inp.dtype in (torch.float16, torch.bfloat16)
+    return (rt.session._nn is not None and inp.is_cuda and inp.dim() == 4
+            and inp.dtype in (torch.float32, torch.float16, torch.bfloat16)
             and inp.dtype == w.dtype and w.dim() == 4 and at.get("group", 1) == 1 and inp.shape[1] % 64 == 0
             and inp.is_contiguous(memory_format=torch.channels_last) and w.permute(0, 2, 3, 1).is_contiguous()
             and at.get("__act", 0) in (0, 1) and inp.data_ptr() % 16 == 0
-            and inp.numel() * 2 < 2 ** 31 and w.numel() * 2 < 2 ** 31 and w.shape[2] * w.shape[3] <= 64)
+            and inp.numel() * inp.element_size() < 2 ** 31 and w.numel() * w.element_size() < 2 ** 31
+            and w.shape[2] * w.shape[3] <= 64)
 
 
 def _fused_conv(rt, at, x):

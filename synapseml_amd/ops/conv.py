@@ -1,7 +1,8 @@
 """Python entry to the MFMA implicit-GEMM convolution (csrc/nn/conv_mfma.hip).
 
 Tensors are torch CUDA tensors in channels_last memory (NHWC); weights are
-packed once to [Cout, R, S, Cin]. Epilogue / prologue tensors are fp32."""
+packed once to [Cout, R, S, Cin]. Epilogue / prologue tensors are fp32. fp32 activations run on the
+exact f32-input MFMA (16x16x4), fp16/bf16 on 16x16x32."""
 from __future__ import annotations
 
 from typing import Optional, Sequence, Tuple
@@ -10,7 +11,7 @@ import torch
 
 from . import native
 
-_DT = {torch.float16: 1, torch.bfloat16: 2}
+_DT = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 
 
 def supported(cin: int, cout: int, groups: int, dtype: torch.dtype) -> bool:
@@ -43,7 +44,7 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
     """y = conv(pro(x), w) + bias, ReLU, + res; optionally also y2 = relu(y * out_scale + out_shift).
 
     ``relu``: False/0 none, True/1 before the residual add, 2 after it. ``pad``: (top, left) or
-    (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp16/bf16. ``wp``: packed [Cout, R, S, C]
+    (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp32/fp16/bf16 (C % 32 == 0 for fp32, % 64 otherwise). ``wp``: packed [Cout, R, S, C]
     (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2).
     ``kernel``: 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128, 128128, 256128, 128256)."""
     B, C, H, W = x.shape

@@ -92,3 +92,66 @@ def test_prologue_residual_dual_output():
     y3 = conv2d_nhwc(x, pack_weight(w3, dt), 3, 3, (1, 1), (1, 1), in_affine=pro)
     r3, _ = _ref(x, w3, 1, 1, pro=pro)
     torch.testing.assert_close(y3.float(), r3, rtol=2e-2, atol=2e-2)
+
+
+# ---------------------------------------------------------------- fp32 (exact f32-input 16x16x4 MFMA)
+F32_KERNELS = [0, 64064, 128064, 64128, 128128]
+
+
+@pytest.mark.parametrize("kernel", F32_KERNELS)
+def test_fp32_exact_integer_layout(kernel):
+    """fp32 form: 16-B fragments feed four MFMAs from their components; small integers make any k / lane /
+    row mapping error an exact mismatch. C = 32 and 96 exercise the 32-channel K tile (not a multiple of 64)."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    g = torch.Generator().manual_seed(3)
+    for (B, C, H, W, Co, k) in ((2, 32, 9, 7, 80, 3), (3, 96, 17, 11, 200, 3), (2, 64, 8, 8, 36, 1)):
+        x = torch.randint(-3, 4, (B, C, H, W), generator=g).float().cuda().contiguous(memory_format=torch.channels_last)
+        w = torch.randint(-3, 4, (Co, C, k, k), generator=g).float().cuda()
+        y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (1, 1), (k // 2, k // 2), kernel=kernel)
+        ref = F.conv2d(x.cpu().double(), w.cpu().double(), None, 1, k // 2)
+        torch.testing.assert_close(y.cpu().double(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("shape", [
+    (4, 64, 56, 56, 256, 1, 1, 0),
+    (2, 256, 28, 28, 128, 3, 1, 1),
+    (2, 128, 29, 29, 128, 3, 2, 1),
+    (1, 2048, 7, 7, 512, 1, 1, 0),
+])
+def test_fp32_conv_matches_fp64_reference(shape):
+    """fp32 MFMA conv (+bias, ReLU) against an fp64 host convolution: fp32-level error, no reduced-precision path."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    B, C, H, W, Co, k, st, pd = shape
+    torch.manual_seed(4)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5
+    bias = torch.randn(Co, device="cuda")
+    ref = torch.relu(F.conv2d(x.cpu().double(), w.cpu().double(), bias.cpu().double(), st, pd))
+    for kernel in (0, 128128, 64128):
+        y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
+        torch.testing.assert_close(y.cpu().double(), ref, rtol=1e-5, atol=2e-5, msg=lambda m: f"kernel {kernel}: {m}")
+    with pytest.raises(RuntimeError):  # the 8-wave tiles are f16/bf16 only
+        conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), kernel=256128)
+
+
+def test_fp32_prologue_residual_dual_output():
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    torch.manual_seed(5)
+    B, C, H, W, Co = 2, 128, 14, 14, 256
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    pro = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1)
+    res = torch.randn(B, Co, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    post = (torch.rand(Co, device="cuda") + 0.5, torch.randn(Co, device="cuda") * 0.1)
+    for k in (1, 3):
+        w = torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5
+        y, y2 = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (1, 1), (k // 2, k // 2), in_affine=pro,
+                            res=res, out_affine=post)
+        xd = torch.relu(x.cpu().double() * pro[0].cpu().double().view(1, -1, 1, 1)
+                        + pro[1].cpu().double().view(1, -1, 1, 1))
+        ry = F.conv2d(xd, w.cpu().double(), None, 1, k // 2) + res.cpu().double()
+        ry2 = torch.relu(ry * post[0].cpu().double().view(1, -1, 1, 1) + post[1].cpu().double().view(1, -1, 1, 1))
+        torch.testing.assert_close(y.cpu().double(), ry, rtol=1e-5, atol=2e-5)
+        torch.testing.assert_close(y2.cpu().double(), ry2, rtol=1e-5, atol=3e-5)

@@ -279,6 +279,8 @@ def test_gpu_resnet_matches_cpu_and_graph_replay():
     # library convolutions may pick split-K (atomic) kernels: replays agree to fp32 rounding
     np.testing.assert_allclose(o1, o2, rtol=1e-4, atol=1e-5 * scale)
     assert any(v != "eager" for v in gpu._graphs.values()), "HIP graph capture fell back to eager"
+    # fp32 graphs run the exact f32-input MFMA conv with the pre-activation BN+ReLU folded into its loader
+    assert any(n.op_type == "_FusedConv" and len(n.inputs) > 5 and n.inputs[4] for n in gpu.nodes)
     half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
     assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
 

@@ -1,5 +1,5 @@
 """Per-layer timing: MFMA implicit-GEMM conv (fused epilogue) vs MIOpen conv + separate bias/ReLU,
-ResNet-50 bottleneck shapes at batch 128, fp16 channels_last."""
+ResNet-50 bottleneck shapes at batch 128, channels_last; ``--dtype fp32|fp16|bf16`` (default fp16)."""
 import os
 import sys
 
@@ -37,6 +37,9 @@ def main():
     quick = "--quick" in sys.argv
     B = 128
     dt = torch.float16
+    if "--dtype" in sys.argv:
+        dt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[sys.argv[sys.argv.index("--dtype") + 1]]
+    print(f"dtype {dt}")
     tot_m, tot_t = 0.0, 0.0
     for C, H, Co, k, st in (SHAPES[:4] if quick else SHAPES):
         x = torch.randn(B, C, H, H, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
