@@ -171,7 +171,8 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 }
 
 // kThr = 256 (4 waves, 2x2) or 512 (8 waves, 4x2: the 256x128 / 128x256 tiles, one block per CU)
-template <class T, int BM, int BN, bool kPro, int kThr = kThreads>
+// kDepth 2: two register stages (tile kt+2's loads in flight during tile kt's MFMAs)
+template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
@@ -359,13 +360,30 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   Stage s0;
   load_tile(s0);
   store_tile(0, s0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(s0);
-    compute(buf);
-    if (kt + 1 < nk) store_tile(buf ^ 1, s0);
+  if constexpr (kDepth == 2) {
+    Stage s1;
+    if (nk > 1) load_tile(s1);
     __syncthreads();
+    // step kt: tile kt+1 sits in `nxt`, tile kt+2 is loaded into `far` (whose tile was stored last step)
+    auto step = [&](int kt, Stage& nxt, Stage& far) {
+      if (kt + 2 < nk) load_tile(far);
+      compute(kt & 1);
+      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, nxt);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, s1, s0);
+      if (kt + 1 < nk) step(kt + 1, s0, s1);
+    }
+  } else {
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) load_tile(s0);
+      compute(buf);
+      if (kt + 1 < nk) store_tile(buf ^ 1, s0);
+      __syncthreads();
+    }
   }
 
   ConvEpilogue<T, WM, WN>(a, acc, lds, M, m0, n0, wid, lane);
@@ -374,6 +392,21 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 template <class T, int BM, int BN, int kThr = kThreads>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  // f32 64x64: two register stages when the K loop is long enough and there is no prologue (the prologue
+  // variant drops to 3 waves/SIMD at depth 2); r2_convdepth A/B: 2615-2623 -> 2536-2541 us over the 14
+  // shapes, the short-K layers (C=64/256 1x1) a little slower. SML_CONV_DEPTH=1/2 forces one.
+  static const int depth = [] {
+    const char* e = std::getenv("SML_CONV_DEPTH");
+    return e ? std::atoi(e) : 0;
+  }();
+  if constexpr (sizeof(T) == 4 && BM == 64 && BN == 64) {
+    const int nk = a.R * a.S * a.C / Tile<T>::BK;
+    if (depth == 2 || (depth == 0 && !a.in_scale && nk > 8)) {
+      auto k2 = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 2> : conv_mfma_kernel<T, BM, BN, false, kThr, 2>;
+      hipLaunchKernelGGL(k2, dim3(blocks), dim3(kThr), 0, st, a);
+      return;
+    }
+  }
   auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr> : conv_mfma_kernel<T, BM, BN, false, kThr>;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
