@@ -428,6 +428,7 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 128064: LaunchTile<T, 128, 64>(a, M, st); return 0;
     case 64128: LaunchTile<T, 64, 128>(a, M, st); return 0;
     case 128128: LaunchTile<T, 128, 128>(a, M, st); return 0;
+    case 128999: LaunchTile<T, 128, 128, 512>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
     case 256128:
     case 128256:
       // 8-wave tiles: the f32 epilogue staging would not fit the operand LDS
@@ -440,18 +441,17 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 0: break;
     default: return -4;
   }
-  // Tile choice (per-shape sweep over the ResNet-50 bottleneck shapes at batch 128, r2 conv1 logs):
-  // Cout <= 64 -> 64x64 (store-bound 1x1 layers want more blocks in flight); otherwise 128x128 when
-  // that still gives >= 384 blocks, else 64x128 (the 7x7 stage, 196 blocks of 128x128).
+  // Tile choice (per-shape sweeps over the ResNet-50 bottleneck shapes at batch 128, r2 conv1 / r2_s3
+  // logs): Cout <= 64 -> 64x64 (store-bound 1x1 layers want more blocks in flight).
   // f32: 64x64 on every shape (r2_fp32conv sweep: 2625 us over the 14 shapes vs 2865-3258 for the larger
   // tiles; 36 KB of LDS, four blocks per CU hide the per-tile barrier behind the 32-cycle MFMAs)
   if (a.Cout <= 64 || sizeof(T) == 4) {
     LaunchTile<T, 64, 64>(a, M, st);
     return 0;
   }
-  const int blocks128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
-  if (blocks128 >= 384) LaunchTile<T, 128, 128>(a, M, st);
-  else LaunchTile<T, 64, 128>(a, M, st);
+  // f16/bf16, Cout > 64: 128x128 with 8 waves (4x2, 32x64 wave tiles, two blocks per CU): r2_s3 sweep
+  // 632 us over the 14 shapes vs 687 us for the 4-wave 128x128 / 64x128 table
+  if constexpr (sizeof(T) == 2) LaunchTile<T, 128, 128, 512>(a, M, st);
   return 0;
 }
 
