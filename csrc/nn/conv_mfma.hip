@@ -97,7 +97,9 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
   const bool relu_post = a.relu == 2 && res != nullptr;
   constexpr int EPV = Tile<T>::EPV;
   if ((a.Cout & 7) == 0) {
-    constexpr int CL = WN + 8;  // staged row pitch (elements)
+    // staged row pitch (elements): 144 B for f16/bf16 (WN=64) and 16 B of padding for f32, so the
+    // accumulator rows 4 apart that one 32-lane write group touches land on different banks
+    constexpr int CL = WN + (sizeof(T) == 4 ? 4 : 8);
     T* Ct = lds + wid * WM * CL;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
