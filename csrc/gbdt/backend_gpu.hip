@@ -310,12 +310,14 @@ __device__ __forceinline__ void PairLambda(const RankTables& t, const double* s_
   *suml -= pl;  // each pair is visited from both ends: sum = -2 pl per pair
 }
 
-// Register-path form: each document's label gain and rank discount are
-// looked up once (fp32) instead of per pair, so the O(pairs) loop is ALU only.
-template <class A>
-__device__ __forceinline__ void PairLambdaPre(float sig, float imd, bool use_norm, double si, int li, float gi,
-                                              float di, double sj, int lj, float gj, float dj, A* lam,
-                                              A* hes, A* suml) {
+// Register-path pair terms (each document's label gain and rank discount looked up once, fp32, so the
+// O(pairs) loop is ALU only) for the single visit of a (top, other) pair: c is the
+// contribution to doc i's lambda (the partner's is exactly -c: the pair terms are symmetric in the
+// two documents and only the sign follows the higher label), ph the hessian term of both, pl the
+// term the normaliser sum takes from each end of the pair.
+__device__ __forceinline__ void PairTermsPre(float sig, float imd, bool use_norm, double si, int li, float gi, float di,
+                                             double sj, int lj, float gj, float dj, float* c, float* ph_out,
+                                             float* pl_out) {
   const bool i_high = li > lj;
   const float gap = i_high ? gi - gj : gj - gi;
   const float pd = fabsf(di - dj);
@@ -326,9 +328,9 @@ __device__ __forceinline__ void PairLambdaPre(float sig, float imd, bool use_nor
   float ph = pl * (1.0f - pl);
   pl *= -sig * dn;
   ph *= sig * sig * dn;
-  *lam += i_high ? pl : -pl;
-  *hes += ph;
-  *suml -= pl;
+  *c = i_high ? pl : -pl;
+  *ph_out = ph;
+  *pl_out = pl;
 }
 
 // All pairs of doc i: a doc ranked below max_position only pairs with the
@@ -572,8 +574,12 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
 #pragma unroll
   for (int u = 0; u < NU; ++u) { lam[u] = 0.f; hes[u] = 0.f; }
   float suml = 0.f;
-  // (a) top document r against every document (partners on the lanes). Grouping four top documents
-  // so their wave sums interleave measured no faster (1.44 vs 1.35 ms per call): not shuffle-latency bound.
+  // Top document r against every document (partners on the lanes), each pair evaluated once: the
+  // top document's terms are wave-reduced, a non-top partner (which pairs with the top list only) takes
+  // the mirrored terms into its own registers in the same order of r as a separate pass over the top
+  // list would (bitwise the same lambdas; that pass was ~18 % of the kernel's VALU work), and the
+  // normaliser sum takes such a pair's term from both ends. Grouping four top documents so their wave
+  // sums interleave measured no faster (1.44 vs 1.35 ms per call): not shuffle-latency bound.
   float top_la = 0.f, top_he = 0.f;  // lane r keeps the reduced lambdas of top document r
   for (int r = 0; r < ntop; ++r) {
     const double si = ReadLaneD(tsc, r);
@@ -585,26 +591,22 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int j = u * 64 + lane;
-      if (j < cnt && j != di && lab[u] != li)
-        PairLambdaPre(sig, fimd, use_norm, si, li, gi, dci, sc[u], lab[u], gn[u], dc[u], &la, &he, &suml);
+      if (j < cnt && j != di && lab[u] != li) {
+        float c, ph, pl;
+        PairTermsPre(sig, fimd, use_norm, si, li, gi, dci, sc[u], lab[u], gn[u], dc[u], &c, &ph, &pl);
+        la += c;
+        he += ph;
+        suml -= pl;
+        if (rk[u] >= ntop) {
+          lam[u] -= c;
+          hes[u] += ph;
+          suml -= pl;
+        }
+      }
     }
     la = WaveSumF(la);
     he = WaveSumF(he);
     if (lane == r) { top_la = la; top_he = he; }
-  }
-  // (b) every non-top document against the top list
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int i = u * 64 + lane;
-    if (i >= cnt || rk[u] < ntop) continue;
-    for (int r = 0; r < ntop; ++r) {
-      const int lj = __builtin_amdgcn_readlane(tlab, r);
-      if (lj == lab[u]) continue;
-      const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tgn), r));
-      const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tdc), r));
-      PairLambdaPre(sig, fimd, use_norm, sc[u], lab[u], gn[u], dc[u], ReadLaneD(tsc, r), lj, gj, dj, &lam[u], &hes[u],
-                    &suml);
-    }
   }
   const double sumd = WaveSumF(suml);
   const double nf = (t.norm && sumd > 0) ? log2(1.0 + sumd) / sumd : 1.0;
