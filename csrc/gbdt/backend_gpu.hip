@@ -523,18 +523,24 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
     mx = fmax(mx, __shfl_xor(mx, off, 64));
     mn = fmin(mn, __shfl_xor(mn, off, 64));
   }
-  // ranks: number of documents scoring higher, ties by index (stable sort)
+  // ranks: number of documents scoring higher, ties by index (stable sort):
+  // rank(i) = #{j: sj > si || (sj == si && j < i)} = #{j < i: sj >= si} + #{j > i: sj >= next_up(si)},
+  // one fp64 compare per pair. Whether j < i is static for documents in different lane slots
+  // (u != v) and jj < lane within one; the document itself (sj < next_up(sj)) counts 0.
+  double sup[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) sup[u] = nextafter(sc[u], INFINITY);
 #pragma unroll
   for (int v = 0; v < NU; ++v) {
     if (v * 64 >= cnt) break;
     const int jn = min(64, cnt - v * 64);
     for (int jj = 0; jj < jn; ++jj) {
       const double sj = ReadLaneD(sc[v], jj);
-      const int j = v * 64 + jj;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
-        const int i = u * 64 + lane;
-        rk[u] += (sj > sc[u]) || (sj == sc[u] && j < i);
+        if (u < v) rk[u] += sj >= sup[u] ? 1 : 0;         // every j of slot v is after i
+        else if (u > v) rk[u] += sj >= sc[u] ? 1 : 0;     // every j of slot v is before i
+        else rk[u] += sj >= (jj < lane ? sc[u] : sup[u]) ? 1 : 0;
       }
     }
   }
