@@ -34,10 +34,13 @@ PYBIND11_MODULE(_nn, m) {
     GapNhwc(P<const void>(x), N, HW, C, dtype, P<float>(out), P<void>(stream));
   });
   m.def("maxpool_nhwc", [](uintptr_t x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw,
-                           int OH, int OW, int dtype, uintptr_t y, uintptr_t stream) {
+                           int OH, int OW, int dtype, uintptr_t y, uintptr_t stream, uintptr_t shift, int relu) {
     MaxPoolNhwc(reinterpret_cast<const void*>(x), N, H, W, C, kh, kw, sh, sw, ph, pw, OH, OW, dtype,
-                reinterpret_cast<void*>(y), reinterpret_cast<void*>(stream));
-  });
+                reinterpret_cast<void*>(y), reinterpret_cast<void*>(stream), reinterpret_cast<const float*>(shift), relu);
+  }, pybind11::arg("x"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"),
+     pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
+     pybind11::arg("pw"), pybind11::arg("OH"), pybind11::arg("OW"), pybind11::arg("dtype"), pybind11::arg("y"),
+     pybind11::arg("stream"), pybind11::arg("shift") = 0, pybind11::arg("relu") = 0);
   m.def("conv_supported", &ConvMfmaSupported);
   m.def("conv_mfma", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale, uintptr_t in_shift,
                         uintptr_t bias, uintptr_t res, uintptr_t out_scale, uintptr_t out_shift, uintptr_t y2,

@@ -14,8 +14,9 @@ void AffineAct(const void* x, int64_t n, int C, int HW, int nhwc, const float* s
 void AddAffineAct(const void* a, const void* b, int64_t n, int C, int HW, int nhwc, const float* scale,
                   const float* shift, int act, int dtype, void* sum_out, void* act_out, void* stream);
 // NHWC max pool (symmetric pads, -inf padding, no dilation), C % 8 == 0
+// shift (per channel, fp32, may be null) and relu: epilogue applied to the pooled maxima
 void MaxPoolNhwc(const void* x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw, int OH,
-                 int OW, int dtype, void* y, void* stream);
+                 int OW, int dtype, void* y, void* stream, const float* shift = nullptr, int relu = 0);
 // NHWC global average pool -> fp32 [N, C]
 void GapNhwc(const void* x, int N, int HW, int C, int dtype, float* out, void* stream);
 // Implicit-GEMM MFMA convolution with fused prologue/epilogue (conv_mfma.hip).

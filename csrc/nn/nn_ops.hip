@@ -146,10 +146,13 @@ __global__ __launch_bounds__(kThreads) void gap_nhwc_kernel(const T* __restrict_
 // K16: max pool over an NHWC tensor (kh x kw window, stride, symmetric pads, no dilation; padded cells
 // never win, as ONNX pads max pools with -inf). One thread per (output pixel, 8 channels): 16-B loads
 // of consecutive channels for fp16 / bf16. C % 8 == 0 (the host checks).
+// Optional epilogue y = relu?(max + shift[c]): the producing conv's bias + ReLU moved past the pool
+// (x -> round(x + b), ReLU are monotone, so max commutes with them exactly) - a quarter of the writes.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void maxpool_nhwc_kernel(const T* __restrict__ x, int N, int H, int W, int C,
                                                                 int kh, int kw, int sh, int sw, int ph, int pw,
-                                                                int OH, int OW, T* __restrict__ y) {
+                                                                int OH, int OW, const float* __restrict__ shift,
+                                                                int relu, T* __restrict__ y) {
   const int cv8 = C / kVec;
   const int64_t total = static_cast<int64_t>(N) * OH * OW * cv8;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
@@ -174,6 +177,14 @@ __global__ __launch_bounds__(kThreads) void maxpool_nhwc_kernel(const T* __restr
 #pragma unroll
         for (int j = 0; j < kVec; ++j) m[j] = fmaxf(m[j], ld<T>(v.v, j));
       }
+    }
+    if (shift) {
+#pragma unroll
+      for (int j = 0; j < kVec; ++j) m[j] += shift[cg * kVec + j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < kVec; ++j) m[j] = fmaxf(m[j], 0.f);
     }
     Vec8<T> o;
 #pragma unroll
@@ -219,7 +230,7 @@ int Blocks(int64_t n, int per_thread) {
 }  // namespace
 
 void MaxPoolNhwc(const void* x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw, int OH,
-                 int OW, int dtype, void* y, void* stream) {
+                 int OW, int dtype, void* y, void* stream, const float* shift, int relu) {
   if (C % kVec != 0) throw std::runtime_error("maxpool_nhwc: channels must be a multiple of 8");
   const int64_t total = static_cast<int64_t>(N) * OH * OW * (C / kVec);
   if (total <= 0) return;
@@ -227,14 +238,14 @@ void MaxPoolNhwc(const void* x, int N, int H, int W, int C, int kh, int kw, int 
   const int g = static_cast<int>(std::min<int64_t>((total + kThreads - 1) / kThreads, 1 << 20));
   if (dtype == 1)
     hipLaunchKernelGGL(maxpool_nhwc_kernel<__half>, dim3(g), dim3(kThreads), 0, s, static_cast<const __half*>(x), N, H,
-                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, static_cast<__half*>(y));
+                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu, static_cast<__half*>(y));
   else if (dtype == 2)
     hipLaunchKernelGGL(maxpool_nhwc_kernel<__hip_bfloat16>, dim3(g), dim3(kThreads), 0, s,
-                       static_cast<const __hip_bfloat16*>(x), N, H, W, C, kh, kw, sh, sw, ph, pw, OH, OW,
+                       static_cast<const __hip_bfloat16*>(x), N, H, W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu,
                        static_cast<__hip_bfloat16*>(y));
   else
     hipLaunchKernelGGL(maxpool_nhwc_kernel<float>, dim3(g), dim3(kThreads), 0, s, static_cast<const float*>(x), N, H,
-                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, static_cast<float*>(y));
+                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu, static_cast<float*>(y));
   NN_HIP_CHECK(hipGetLastError());
 }
 

@@ -684,6 +684,10 @@ def _convT(rt, at, x):
 @op("MaxPool")
 def _maxpool(rt, at, x):
     t = x[0]
+    # executor fusion (session._move_epilogue_past_pool): x[1] = the producing conv's bias and
+    # at["__act"] = 1 its ReLU, applied to the pooled maxima (max commutes with both exactly)
+    shift = x[1] if len(x) > 1 else None
+    act = at.get("__act", 0)
     k = at["kernel_shape"]
     nd = len(k)
     strides = at.get("strides", [1] * nd)
@@ -702,15 +706,22 @@ def _maxpool(rt, at, x):
         OH = (H + 2 * pb[0] - k[0]) // strides[0] + 1
         OW = (W + 2 * pb[1] - k[1]) // strides[1] + 1
         y = torch.empty((N, C, OH, OW), dtype=t.dtype, device=t.device, memory_format=torch.channels_last)
+        sh = shift.to(t.device, torch.float32).contiguous() if shift is not None else None
         nn.maxpool_nhwc(t.data_ptr(), N, H, W, C, k[0], k[1], strides[0], strides[1], pb[0], pb[1], OH, OW,
-                        _dtype_code(t), y.data_ptr(), _stream(t))
+                        _dtype_code(t), y.data_ptr(), _stream(t), sh.data_ptr() if sh is not None else 0, int(act == 1))
         return [y]
     t, pad = _sym_pad(t, pb, pe, value=-math.inf)
     f = {1: Fn.max_pool1d, 2: Fn.max_pool2d, 3: Fn.max_pool3d}[nd]
     if len(rt.node_outputs) > 1 and rt.node_outputs[1]:
         y, i = f(t, k, strides, pad, dil, ceil_mode=ceil, return_indices=True)
         return [y, i]
-    return [f(t, k, strides, pad, dil, ceil_mode=ceil)]
+    y = f(t, k, strides, pad, dil, ceil_mode=ceil)
+    if shift is not None or act == 1:
+        yf = y.float()
+        if shift is not None:
+            yf = yf + shift.to(y.device, torch.float32).reshape([1, -1] + [1] * (y.dim() - 2))
+        y = (torch.relu(yf) if act == 1 else yf).to(y.dtype)
+    return [y]
 
 
 @op("AveragePool")

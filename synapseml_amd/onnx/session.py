@@ -117,6 +117,8 @@ class InferenceSession:
             nodes = self._fuse_epilogues(nodes)
             if self._nn is not None and self.channels_last:
                 nodes = self._fuse_prologues(nodes)
+            if self._nn is not None:
+                nodes = self._move_epilogue_past_pool(nodes)
         self.nodes = nodes
         self._place_constants()
         self._plan_liveness()
@@ -354,6 +356,30 @@ class InferenceSession:
                     continue
             new_nodes.append(n)
         return self._reorder([n for n in new_nodes if id(n) not in drop])
+
+    def _move_epilogue_past_pool(self, nodes: List[Node]) -> List[Node]:
+        """A library conv (not the MFMA kernel, e.g. the 3-channel ResNet stem) whose bias(+ReLU) epilogue
+        feeds only a MaxPool: the epilogue runs on the pooled maxima inside the pool kernel instead of as a
+        full-resolution pass. Exact: x -> round(x + b) and ReLU are monotone, so they commute with max."""
+        outs = {o.name for o in self.outputs}
+        by_input: Dict[str, List[Node]] = {}
+        for n in nodes:
+            for x in n.inputs:
+                by_input.setdefault(x, []).append(n)
+        for n in nodes:
+            if (n.op_type != "_FusedConv" or self._mfma_conv(n) or n.attrs.get("__act", 0) not in (0, 1)
+                    or len(n.inputs) < 3 or not n.inputs[2] or any(n.inputs[3:]) or n.outputs[0] in outs):
+                continue
+            cs = by_input.get(n.outputs[0], [])
+            if len(cs) != 1 or cs[0].op_type != "MaxPool" or len(cs[0].inputs) != 1 or \
+                    (len(cs[0].outputs) > 1 and cs[0].outputs[1]):
+                continue
+            pool = cs[0]
+            pool.inputs = [pool.inputs[0], n.inputs[2]]
+            pool.attrs = dict(pool.attrs, __act=n.attrs.get("__act", 0))
+            n.inputs = [n.inputs[0], n.inputs[1], ""]
+            n.attrs["__act"] = 0
+        return nodes
 
     def _reorder(self, nodes: List[Node]) -> List[Node]:
         """Stable topological re-order (a fused node may read a value produced

@@ -425,3 +425,26 @@ def test_gpu_maxpool_nhwc_kernel_matches_torch(dtype):
                         torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert torch.equal(y.float(), ref.to(dt).float())
+        # fused epilogue (a stem conv's bias + ReLU moved past the pool): bitwise the unfused order, since
+        # rounding x + b and ReLU are monotone and commute with max
+        b = torch.randn(c, device="cuda")
+        unfused = torch.nn.functional.max_pool2d(torch.relu(x.float() + b.view(1, -1, 1, 1)).to(dt).float(), k, s, p)
+        y2 = torch.empty_like(y)
+        nn.maxpool_nhwc(x.data_ptr(), n, h, w, c, k, k, s, s, p, p, oh, ow, code, y2.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream, b.data_ptr(), 1)
+        torch.cuda.synchronize()
+        assert torch.equal(y2.float(), unfused)
+
+
+@pytest.mark.gpu
+def test_gpu_stem_epilogue_moves_past_maxpool():
+    """ResNet-50 v2 on the GPU: the library stem conv's bias + ReLU run inside the max-pool kernel, and the
+    session output still matches the unfused host execution."""
+    data = writer.resnet50_v2(seed=7)
+    x = np.random.default_rng(8).random((2, 3, 224, 224), dtype=np.float32)
+    gpu = InferenceSession(data, device="cuda")
+    pools = [n for n in gpu.nodes if n.op_type == "MaxPool"]
+    assert pools and len(pools[0].inputs) == 2 and pools[0].attrs.get("__act") == 1
+    cpu = InferenceSession(data, device="cpu").run(None, {"data": x})[0]
+    out = gpu.run(None, {"data": x})[0]
+    np.testing.assert_allclose(out, cpu, rtol=0, atol=2e-3 * np.abs(cpu).max())
