@@ -354,6 +354,26 @@ class InferenceSession:
                         new_nodes.append(add)
                     drop.add(id(n))
                     continue
+            if n.op_type == "_AddAffineAct" and n.attrs.get("__act", 0) == 1 and len(n.outputs) > 1 and n.outputs[1]:
+                # activated output not consumed by MFMA convs (e.g. the last block's post-activation before the
+                # pooling): the producing conv adds the residual and writes relu(y * scale + shift) as its
+                # second output from registers, instead of a separate add + BN + ReLU pass
+                for k in (0, 1):
+                    c = prod.get(n.inputs[k])
+                    other = n.inputs[1 - k]
+                    if (c is not None and self._mfma_conv(c) and c.attrs.get("__act", 0) == 0
+                            and len(c.inputs) <= 6 and (len(c.inputs) < 4 or not c.inputs[3])
+                            and c.outputs[0] not in outs and len(by_input.get(c.outputs[0], [])) == 1
+                            and other != c.outputs[0] and id(c) not in drop):
+                        while len(c.inputs) < 6:
+                            c.inputs.append("")
+                        c.inputs[3] = other
+                        c.inputs += [n.inputs[2], n.inputs[3]]
+                        c.outputs = [n.outputs[0], n.outputs[1]]
+                        drop.add(id(n))
+                        break
+                if id(n) in drop:
+                    continue
             new_nodes.append(n)
         return self._reorder([n for n in new_nodes if id(n) not in drop])
 
@@ -661,6 +681,7 @@ def _fused_conv(rt, at, x):
     inp, w, b = x[0], x[1], x[2]
     res = x[3] if len(x) > 3 else None
     pro = (x[4], x[5]) if len(x) > 5 and x[4] is not None else None
+    post = (x[6], x[7]) if len(x) > 7 and x[6] is not None else None  # second output relu(y * s + t)
     if inp.dtype != w.dtype:
         inp = inp.to(w.dtype)
     act = at.get("__act", 0)
@@ -675,8 +696,16 @@ def _fused_conv(rt, at, x):
         y = conv2d_nhwc(inp, w.permute(0, 2, 3, 1), w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]),
                         dil, bias=f32(b), relu=2 if act == 1 else 0,
                         in_affine=(f32(pro[0]), f32(pro[1])) if pro is not None else None,
-                        in_relu=bool(at.get("__pro_relu", 1)), res=res)
-        return [y]
+                        in_relu=bool(at.get("__pro_relu", 1)), res=res,
+                        out_affine=(f32(post[0]), f32(post[1])) if post is not None else None)
+        return list(y) if post is not None else [y]
+    ys = _fused_conv_fallback(rt, at, inp, w, b, res, pro, act)
+    if post is not None:
+        return ys + [_affine_act(rt, ys[0], post[0], post[1], None, 1, 0.0)]
+    return ys
+
+
+def _fused_conv_fallback(rt, at, inp, w, b, res, pro, act):
     if pro is not None:  # prologue outside the kernel (fallback path)
         inp = _affine_act(rt, inp, pro[0], pro[1], None, 1 if at.get("__pro_relu", 1) else 0, 0.0)
     nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)

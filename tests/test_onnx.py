@@ -438,13 +438,18 @@ def test_gpu_maxpool_nhwc_kernel_matches_torch(dtype):
 
 @pytest.mark.gpu
 def test_gpu_stem_epilogue_moves_past_maxpool():
-    """ResNet-50 v2 on the GPU: the library stem conv's bias + ReLU run inside the max-pool kernel, and the
-    session output still matches the unfused host execution."""
+    """ResNet-50 v2 on the GPU: the library stem conv's bias + ReLU run inside the max-pool kernel, the last
+    add + BN + ReLU is the final conv's dual output, and the session output still matches the unfused host
+    execution (fp32 and fp16)."""
     data = writer.resnet50_v2(seed=7)
     x = np.random.default_rng(8).random((2, 3, 224, 224), dtype=np.float32)
     gpu = InferenceSession(data, device="cuda")
     pools = [n for n in gpu.nodes if n.op_type == "MaxPool"]
     assert pools and len(pools[0].inputs) == 2 and pools[0].attrs.get("__act") == 1
+    # the last block's residual add + post-activation BN + ReLU: the final conv's second output
+    assert any(n.op_type == "_FusedConv" and len(n.outputs) == 2 and len(n.inputs) == 8 for n in gpu.nodes)
     cpu = InferenceSession(data, device="cpu").run(None, {"data": x})[0]
     out = gpu.run(None, {"data": x})[0]
     np.testing.assert_allclose(out, cpu, rtol=0, atol=2e-3 * np.abs(cpu).max())
+    half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
+    assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
