@@ -577,8 +577,16 @@ class InferenceSession:
             return self.run_values(feeds, fetch)
         g, static_in, static_out = entry
         for k, t in static_in.items():
-            t.copy_(self._to_value(next((vi for vi in self.inputs if vi.name == k), None), feeds[k]),
-                    non_blocking=True)
+            v = feeds[k]
+            if (t.is_floating_point() and tuple(np.shape(v)) == tuple(t.shape)
+                    and (isinstance(v, torch.Tensor) and v.is_floating_point()
+                         or isinstance(v, np.ndarray) and v.dtype.kind == "f")):
+                # one pass straight into the captured input: host->device, dtype and layout conversion in a
+                # single copy (instead of cast, channels_last copy and this copy as three passes)
+                t.copy_(v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v)),
+                        non_blocking=True)
+            else:
+                t.copy_(self._to_value(next((vi for vi in self.inputs if vi.name == k), None), v), non_blocking=True)
         g.replay()
         return [o.clone() for o in static_out]
 
