@@ -1491,6 +1491,18 @@ __global__ __launch_bounds__(256) void find_split_kernel(
   FindSplitBlock(st, leaves, part, E, count_slot, hist_pool, fm, sp, fbest, F);
 }
 
+// The last split of a tree (single process): its children are never split, so their histograms and split
+// searches are not needed; only their exact row counts are, and the partition just counted them (the
+// split's estimated counts came from hessian sums). One thread replaces hist + reduce + find + choose.
+__global__ void finalize_last_split_kernel(const DState* __restrict__ st, const DLeaf* __restrict__ leaves, DTree t) {
+  if (threadIdx.x != 0 || st->done || st->phase == 0) return;
+  const int lt = PTotal(st);
+  const int64_t small_cnt = st->small_leaf == st->split_leaf ? lt : st->pcount - lt;
+  const int64_t parent_cnt = leaves[st->large_leaf].gcount;  // the keeper left the parent's count there
+  t.lcount[st->small_leaf] = small_cnt;
+  t.lcount[st->large_leaf] = parent_cnt - small_cnt;
+}
+
 __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DLeaf* __restrict__ leaves,
                                                      SplitResult* __restrict__ lbest, double* __restrict__ lgain,
                                                      const SplitResult* __restrict__ fbest, int F, DTree t,
@@ -2560,6 +2572,7 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_slab_wt), &v, sizeof(int)));
     }
     if (const char* e = std::getenv("SML_FUSED_SPLIT")) fused_split_ = std::atoi(e);
+    if (const char* e = std::getenv("SML_SKIP_LAST_SPLIT")) skip_last_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_MERGED_CHOOSE")) merged_choose_ = std::atoi(e) != 0;
     {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
@@ -2910,6 +2923,11 @@ class GpuBackend : public TrainBackend {
         SML_HIP_CHECK(hipGetLastError());
         st_cur_ = sout;
         st_next_ = sin;
+        if (s == L_ - 1 && skip_last_ && fused_split_ == 0 && hist_mode_ == 0 && !Distributed()) {
+          hipLaunchKernelGGL(finalize_last_split_kernel, dim3(1), dim3(64), 0, stream_, st_cur_, leaves_.get(), dt_);
+          SML_HIP_CHECK(hipGetLastError());
+          break;
+        }
       } else {
         auto pk = part_rows_ == 16 ? part_kernel<16> : (part_rows_ == 4 ? part_kernel<4> : part_kernel<8>);
         hipLaunchKernelGGL(pk, dim3(part_grid_), dim3(kPartThreads), 0, stream_, st_cur_, lbest_.get(),
@@ -3287,6 +3305,7 @@ class GpuBackend : public TrainBackend {
   // SML_FUSED_SPLIT: 0 = reduce / find / choose launches, 1 = one split_kernel (slab reduce inside),
   // 2 = reduce launch + split_kernel (find + choose), 3 = split_kernel<slab, no choose> + choose_part_kernel
   // (A/B with the merged choose: 2.05 ms/iter vs 1.97 for 0 - 28 blocks cannot pull the slabs fast enough)
+  bool skip_last_ = true;  // SML_SKIP_LAST_SPLIT=0: histogram + search the last split's children too
   int fused_split_ = 0;  // A/B on MI355X: 0 = 2.30 ms/iter, 2 = 2.41, 1 = 2.51 (profiles/README)
   DevBuf<float> ghmax_partial_;
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
