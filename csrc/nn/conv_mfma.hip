@@ -174,7 +174,10 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 
 // kThr = 256 (4 waves, 2x2) or 512 (8 waves, 4x2: the 256x128 / 128x256 tiles, one block per CU)
 // kDepth 2: two register stages (tile kt+2's loads in flight during tile kt's MFMAs)
-template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1>
+// kStem: a few-channel stem conv (the 3-channel ResNet stem, input padded to C = 4, weights packed to
+// [Cout][8][8][4] with zero taps): a 16-B A chunk is two horizontally adjacent pixels (taps s, s+1 of row r),
+// each read as its own 8-B buffer load (zero outside the image), a 64-wide K tile = two tap rows.
+template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     const int ow = mm % a.OW, t2 = mm / a.OW;
     const int oh = t2 % a.OH, b = t2 / a.OH;
     const int ih0 = oh * a.stride_h - a.pad_h, iw0 = ow * a.stride_w - a.pad_w;
-    abase[i] = ((b * a.H + ih0) * a.W + iw0) * a.C + kc * EPV;
+    abase[i] = ((b * a.H + ih0) * a.W + iw0) * a.C + (kStem ? 0 : kc * EPV);
     uint64_t mk = 0;
     if (m < M)
       for (int r = 0, t = 0; r < a.R; ++r)
@@ -302,6 +305,18 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0, loaded = 0;
   auto load_tile = [&](Stage& st) {
     st.okm = 0;
+    if constexpr (kStem) {
+      const int r = 2 * loaded + (kc >> 2), s0 = 2 * (kc & 3), t0 = r * 8 + s0;
+      const int toff_s = (r * a.W + s0) * 4;  // element offset of tap (r, s0) from the window origin
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const uint32_t o0 = (amask[i] >> t0) & 1ull ? static_cast<uint32_t>((abase[i] + toff_s) * 2) : kOob;
+        const uint32_t o1 = (amask[i] >> (t0 + 1)) & 1ull ? static_cast<uint32_t>((abase[i] + toff_s + 4) * 2) : kOob;
+        auto lo = __builtin_amdgcn_raw_buffer_load_b64(xres, o0, 0, 0);
+        auto hi = __builtin_amdgcn_raw_buffer_load_b64(xres, o1, 0, 0);
+        st.a[i] = make_uint4(lo[0], lo[1], hi[0], hi[1]);
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const bool ok = (amask[i] >> lt) & 1ull;
@@ -309,6 +324,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
       const uint32_t vo = ok ? static_cast<uint32_t>((abase[i] + toff) * static_cast<int>(sizeof(T))) : kOob;
       auto v = __builtin_amdgcn_raw_buffer_load_b128(xres, vo, lc0 * static_cast<int>(sizeof(T)), 0);
       st.a[i] = *reinterpret_cast<uint4*>(&v);
+    }
     }
     if constexpr (pro) {
       const f4* scp = reinterpret_cast<const f4*>(a.in_scale + lc0 + kc * EPV);
@@ -459,6 +475,14 @@ int Launch(const ConvArgs& a, hipStream_t st) {
 
 }  // namespace
 
+template <class T>
+int LaunchStem(const ConvArgs& a, hipStream_t st) {
+  const int M = a.B * a.OH * a.OW;
+  const int blocks = ((M + 63) / 64) * ((a.Cout + 63) / 64);
+  hipLaunchKernelGGL((conv_mfma_kernel<T, 64, 64, false, kThreads, 1, true>), dim3(blocks), dim3(kThreads), 0, st, a);
+  return 0;
+}
+
 // dtype: 0 fp32, 1 fp16, 2 bf16 (C must be a multiple of one tile's K: 32 f32 / 64 f16/bf16 channels)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
   const int bk = dtype == 0 ? Tile<float>::BK : Tile<_Float16>::BK;
@@ -466,6 +490,16 @@ bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
 }
 
 int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
+  if (a.kernel == kConvStem) {  // packed few-channel stem: C = 4, 8 x 8 taps, f16/bf16, no prologue
+    if (a.C != 4 || a.R != 8 || a.S != 8 || (dtype != 1 && dtype != 2) || a.in_scale || a.dil_h != 1 || a.dil_w != 1)
+      return -1;
+    if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
+    if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * 2 >= (1ll << 31)) return -5;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int rc = dtype == 1 ? LaunchStem<_Float16>(a, st) : LaunchStem<__bf16>(a, st);
+    if (rc != 0) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
   if (!ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return -1;
   if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
   // buffer-resource offsets are 32-bit and the per-row tap mask holds 64 taps

@@ -37,6 +37,7 @@ struct ConvArgs {
   int kernel = 0;      // 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128,
                        // 128128, 256128, 128256)
 };
+constexpr int kConvStem = 1;  // ConvArgs::kernel: the packed few-channel stem form (C = 4, R = S = 8)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);
 int ConvMfma(const ConvArgs& a, int dtype, void* stream);
 // fp32 row softmax (y may be null) and argmax (amax may be null)

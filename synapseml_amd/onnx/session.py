@@ -25,6 +25,7 @@ costs one graph launch instead of one launch per node.
 from __future__ import annotations
 
 import math
+import os
 import threading
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -707,10 +708,51 @@ def _fused_conv(rt, at, x):
                         in_relu=bool(at.get("__pro_relu", 1)), res=res,
                         out_affine=(f32(post[0]), f32(post[1])) if post is not None else None)
         return list(y) if post is not None else [y]
+    if _STEM_MFMA and pro is None and post is None and _stem_ok(rt, at, inp, w):
+        return [_stem_conv(rt, at, inp, w, b, res, act)]
     ys = _fused_conv_fallback(rt, at, inp, w, b, res, pro, act)
     if post is not None:
         return ys + [_affine_act(rt, ys[0], post[0], post[1], None, 1, 0.0)]
     return ys
+
+
+# SML_STEM_MFMA=1: run the 3-channel stem on the packed MFMA form. Off by default: ResNet-50 fp16 measured
+# 39.7k -> 38.0k img/s with it (profiles/r2_s3/stem/: the zero-padded 4-channel input copy and the 256-wide
+# padded K cost more than MIOpen's stem kernel saves).
+_STEM_MFMA = os.environ.get("SML_STEM_MFMA", "0") == "1"
+
+
+def _stem_ok(rt, at, inp, w) -> bool:
+    """A few-channel conv (the 3-channel image stem) the MFMA kernel runs in its packed form: C <= 4 and
+    R, S <= 8 zero-padded to [Cout][8][8][4], input padded to 4 channels."""
+    return (rt.session._nn is not None and inp.is_cuda and inp.dim() == 4 and inp.dtype in (torch.float16, torch.bfloat16)
+            and inp.dtype == w.dtype and w.dim() == 4 and at.get("group", 1) == 1 and 1 <= inp.shape[1] <= 4
+            and w.shape[2] <= 8 and w.shape[3] <= 8 and at.get("__act", 0) in (0, 1)
+            and list(at.get("dilations", [1, 1])) == [1, 1] and inp.numel() // inp.shape[1] * 4 * 2 < 2 ** 31)
+
+
+def _stem_conv(rt, at, inp, w, b, res, act):
+    from ..ops.conv import conv2d_nhwc
+
+    B, C, H, W = inp.shape
+    cache = rt.session.__dict__.setdefault("_stem_w", {})
+    key = (w.data_ptr(), tuple(w.shape), w.dtype)
+    wp = cache.get(key)
+    if wp is None:  # packed once per weight: [Cout][8][8][4], zero taps / channels
+        wp = torch.zeros((w.shape[0], 8, 8, 4), dtype=w.dtype, device=w.device)
+        wp[:, :w.shape[2], :w.shape[3], :C] = w.permute(0, 2, 3, 1)
+        cache[key] = wp
+    x4 = torch.empty((B, 4, H, W), dtype=inp.dtype, device=inp.device, memory_format=torch.channels_last).zero_()
+    x4[:, :C] = inp
+    nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+    # the 8-tap window is one row / column longer than the real one: one more (virtual) padding row and
+    # column at the far side gives the real output size; the extra taps have zero weights
+    pad = (pb[0], pb[1], pe[0] + 8 - w.shape[2], pe[1] + 8 - w.shape[3])
+    dev = inp.device
+    if res is not None:
+        res = res.to(inp.dtype).contiguous(memory_format=torch.channels_last)
+    return conv2d_nhwc(x4, wp, 8, 8, strides, pad, (1, 1), bias=None if b is None else b.to(dev, torch.float32).contiguous(),
+                       relu=2 if act == 1 else 0, res=res, kernel=1)
 
 
 def _fused_conv_fallback(rt, at, inp, w, b, res, pro, act):

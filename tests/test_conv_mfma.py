@@ -155,3 +155,24 @@ def test_fp32_prologue_residual_dual_output():
         ry2 = torch.relu(ry * post[0].cpu().double().view(1, -1, 1, 1) + post[1].cpu().double().view(1, -1, 1, 1))
         torch.testing.assert_close(y.cpu().double(), ry, rtol=1e-5, atol=2e-5)
         torch.testing.assert_close(y2.cpu().double(), ry2, rtol=1e-5, atol=3e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_stem_packed_form_exact(dtype):
+    """Few-channel stem form (kernel=1): input padded to 4 channels, weights packed to [Cout][8][8][4] with
+    zero taps, one more virtual padding row / column; small integers make any tap / pixel-pair mapping error an
+    exact mismatch (ResNet stem 7x7/2 pad 3, and a 5x5/1 odd-size case)."""
+    from synapseml_amd.ops.conv import conv2d_nhwc
+
+    g = torch.Generator().manual_seed(9)
+    for (B, C, H, W, Co, k, st, pd) in ((2, 3, 37, 29, 64, 7, 2, 3), (3, 3, 15, 17, 40, 5, 1, 2)):
+        x = torch.randint(-2, 3, (B, C, H, W), generator=g).float()
+        w = torch.randint(-2, 3, (Co, C, k, k), generator=g).float()
+        ref = F.conv2d(x.double(), w.double(), None, st, pd)
+        x4 = torch.empty((B, 4, H, W), dtype=dtype, device="cuda", memory_format=torch.channels_last).zero_()
+        x4[:, :C] = x.to(dtype).cuda()
+        wp = torch.zeros((Co, 8, 8, 4), dtype=dtype, device="cuda")
+        wp[:, :k, :k, :C] = w.permute(0, 2, 3, 1).to(dtype).cuda()
+        y = conv2d_nhwc(x4, wp, 8, 8, (st, st), (pd, pd, pd + 8 - k, pd + 8 - k), kernel=1)
+        assert y.shape == ref.shape
+        torch.testing.assert_close(y.cpu().double(), ref, rtol=0, atol=0)
