@@ -2264,7 +2264,9 @@ __global__ __launch_bounds__(kPartThreads) void choose_part_kernel(
 // with more than 32 features fall back to the column-major copy.
 constexpr int kScoreRows = 2;
 constexpr int kScoreThreads = 256;
-constexpr int kScoreLdsNodes = 2048;
+// Nodes staged in LDS (trees up to 257 leaves; larger ones walk the global copy). 6 KB of LDS per block
+// instead of 34 KB: the LDS no longer caps the streaming kernel at 4 blocks per CU.
+constexpr int kScoreLdsNodes = 256;
 
 struct DevTreeView {
   const int4* nodes;
