@@ -447,6 +447,7 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 64128: LaunchTile<T, 64, 128>(a, M, st); return 0;
     case 128128: LaunchTile<T, 128, 128>(a, M, st); return 0;
     case 128999: LaunchTile<T, 128, 128, 512>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
+    case 64999: LaunchTile<T, 64, 64, 512>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
     case 256128:
     case 128256:
       // 8-wave tiles: the f32 epilogue staging would not fit the operand LDS
@@ -462,8 +463,13 @@ int Launch(const ConvArgs& a, hipStream_t st) {
   // Tile choice (per-shape sweeps over the ResNet-50 bottleneck shapes at batch 128, r2 conv1 / r2_s3
   // logs): Cout <= 64 -> 64x64 (store-bound 1x1 layers want more blocks in flight).
   // f32: 64x64 on every shape (r2_fp32conv sweep: 2625 us over the 14 shapes vs 2865-3258 for the larger
-  // tiles; 36 KB of LDS, four blocks per CU hide the per-tile barrier behind the 32-cycle MFMAs)
-  if (a.Cout <= 64 || sizeof(T) == 4) {
+  // tiles; 36 KB of LDS, four blocks per CU hide the per-tile barrier behind the 32-cycle MFMAs), with
+  // 8 waves of 16x32 (r2_tile64w8: 2537 -> 2467 us)
+  if constexpr (sizeof(T) == 4) {
+    LaunchTile<T, 64, 64, 512>(a, M, st);
+    return 0;
+  }
+  if (a.Cout <= 64) {
     LaunchTile<T, 64, 64>(a, M, st);
     return 0;
   }

@@ -22,8 +22,8 @@ def _ref(x, w, stride, pad, bias=None, relu=False, pro=None, res=None, post=None
     return y, y2
 
 
-# 0 = shape-chosen tile; BM*1000+BN = forced tile (128999: 128x128 with 8 waves)
-KERNELS = [0, 64064, 128064, 64128, 128128, 128999, 256128, 128256]
+# 0 = shape-chosen tile; BM*1000+BN = forced tile (128999 / 64999: 128x128 / 64x64 with 8 waves)
+KERNELS = [0, 64064, 64999, 128064, 64128, 128128, 128999, 256128, 128256]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -95,7 +95,7 @@ def test_prologue_residual_dual_output():
 
 
 # ---------------------------------------------------------------- fp32 (exact f32-input 16x16x4 MFMA)
-F32_KERNELS = [0, 64064, 128064, 64128, 128128]
+F32_KERNELS = [0, 64064, 64999, 128064, 64128, 128128]
 
 
 @pytest.mark.parametrize("kernel", F32_KERNELS)
@@ -129,7 +129,7 @@ def test_fp32_conv_matches_fp64_reference(shape):
     w = torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5
     bias = torch.randn(Co, device="cuda")
     ref = torch.relu(F.conv2d(x.cpu().double(), w.cpu().double(), bias.cpu().double(), st, pd))
-    for kernel in (0, 128128, 64128):
+    for kernel in (0, 64064, 128128, 64128):
         y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
         torch.testing.assert_close(y.cpu().double(), ref, rtol=1e-5, atol=2e-5, msg=lambda m: f"kernel {kernel}: {m}")
     with pytest.raises(RuntimeError):  # the 8-wave tiles are f16/bf16 only
