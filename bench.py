@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
-"""Headline benchmark: LightGBMClassifier boosting throughput on a Higgs-shape
-synthetic dataset (11M rows x 28 float features per GPU), 1..8 MI355X.
+"""Headline benchmark: ``LightGBMClassifier.fit`` throughput on a Higgs-shape
+synthetic DataFrame (11M rows x 28 float features per GPU), 1..8 MI355X.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1
-it is launched under torch.distributed.run with one rank per GPU. One step =
-one boosting iteration (gradients -> 31-leaf tree -> score update) over the
-full training matrix at the reference's defaults (numLeaves 31, maxBin 255,
-learningRate 0.1, minDataInLeaf 20, binary objective). W untimed warmup
-iterations, then exactly K timed iterations bracketed by barrier + device
-synchronize; time is the max over ranks. ``value`` = total rows x K / seconds
-(whole job). Data is synthetic (no datasets are downloadable here); per-GPU
-work is fixed as N grows (weak scaling): N=8 trains on 88M rows.
+Metric (BASELINE.md:35, primary): ``N_rows / fit_wall_s`` — rows of the
+training DataFrame per second of the WHOLE public ``fit`` call at the
+reference's defaults (numIterations 100, numLeaves 31, maxBin 255,
+binSampleCount 200000, learningRate 0.1, minDataInLeaf 20, binary objective).
+The timed region is everything the reference's ``LightGBMBase.train``
+(lightgbm/.../LightGBMBase.scala:36-65,396-447) does after the DataFrame
+exists: column extraction, row sampling + bin boundaries (reference dataset),
+dataset construction (K1 device bin encode), booster creation, 100 boosting
+iterations, and the returned LightGBMClassificationModel (model string).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
+N > 1 it runs under torch.distributed.run with one rank per GPU (RCCL
+histogram allreduce inside the engine). One step = one complete ``fit``.
+W untimed warmup fits, then exactly K timed fits bracketed by barrier +
+device synchronize; time is the max over ranks. ``value`` = total rows x K /
+seconds (whole job). Per-GPU rows are fixed as N grows (weak scaling).
+The secondary metric (N_rows x numIterations / iteration-loop seconds) and a
+per-phase breakdown are reported under ``config``.
 """
 from __future__ import annotations
 
@@ -50,13 +59,14 @@ def higgs_like(n: int, f: int, seed: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=5, help="timed fits")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed fits")
     ap.add_argument("--rows", type=int, default=11_000_000, help="rows per GPU (weak scaling)")
     ap.add_argument("--features", type=int, default=28)
     ap.add_argument("--leaves", type=int, default=31)
+    ap.add_argument("--iterations", type=int, default=100, help="numIterations of each fit (reference default 100)")
     ap.add_argument("--device", default="gpu")
-    ap.add_argument("--save-model", default=None, help="write the trained model text here (after timing)")
+    ap.add_argument("--save-model", default=None, help="write the last model's text here (after timing)")
     args = ap.parse_args()
 
     import torch
@@ -75,89 +85,79 @@ def main() -> None:
 
     if world > 1:
         D.init_from_env("nccl" if use_gpu and not shared else "gloo")
+        if shared:
+            os.environ["SML_GBDT_SHARED_DEVICE"] = "1"
+    from synapseml_amd.core.dataframe import DataFrame
+    from synapseml_amd.lightgbm import LightGBMClassifier
     from synapseml_amd.ops import native
 
-    g = native.gbdt()
-    t_setup = time.perf_counter()
+    native.gbdt()
+    t_gen = time.perf_counter()
     X, y = higgs_like(args.rows, args.features, seed=1234 + rank)
-    params = (f"objective=binary num_iterations={args.warmup + args.steps} learning_rate=0.1 "
-              f"num_leaves={args.leaves} max_bin=255 min_data_in_leaf=20 bin_construct_sample_cnt=200000 "
-              f"device_type={'gpu' if use_gpu else 'cpu'} num_machines={world} tree_learner=data metric=auc")
-    names = [f"f{i}" for i in range(args.features)]
-    # shared bin boundaries: rank 0 samples, broadcasts the serialized reference
-    ser = None
-    if rank == 0:
-        rng = np.random.default_rng(1)
-        idx = np.sort(rng.choice(args.rows, size=min(200_000, args.rows), replace=False))
-        ser = bytes(g.DatasetReference.from_sample(X[idx].astype(np.float64), args.rows * world, params, names)
-                    .serialize())
-    ser = D.broadcast_object(ser, 0)
-    ref = g.DatasetReference.deserialize(ser)
-    ds = g.Dataset(ref, args.rows)
-    t_enc = time.perf_counter()
-    if use_gpu:
-        ds.push_dense_gpu(X, 0)  # K1 bin encode on the device
-    else:
-        chunk = 1 << 20
-        for s in range(0, args.rows, chunk):
-            ds.push_dense(X[s: s + chunk], s)
-    encode_s = time.perf_counter() - t_enc
-    ds.set_label(y)
+    # this rank's partition of the training DataFrame (one process per GPU = one Spark executor)
+    df = DataFrame({"features": X, "label": y})
+    gen_s = time.perf_counter() - t_gen
     n_hold = min(200_000, args.rows)
     X_hold, y_hold = X[:n_hold].astype(np.float64), y[:n_hold]
     del X
-    comm = D.gbdt_comm(use_gpu, shared_device=shared) if world > 1 else None
-    booster = g.Booster(ds, params, comm)
-    setup_s = time.perf_counter() - t_setup
+
+    est = LightGBMClassifier(numIterations=args.iterations, learningRate=0.1, numLeaves=args.leaves, maxBin=255,
+                             binSampleCount=200000, minDataInLeaf=20, objective="binary",
+                             deviceType="gpu" if use_gpu else "cpu", metric="auc")
 
     def sync():
-        booster.synchronize()
         if use_gpu:
             torch.cuda.synchronize()
 
+    model = None
     for _ in range(args.warmup):
-        booster.update()
+        model = est.fit(df)
     sync()
     D.barrier()
     sync()
     t0 = time.perf_counter()
+    measures = []
     for _ in range(args.steps):
-        booster.update()
+        model = est.fit(df)
+        measures.append(est.getPerformanceMeasures()[0])
     sync()
     D.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    el = np.array([elapsed], dtype=np.float64)
     if world > 1:
         import torch.distributed as dist
 
-        t = torch.tensor(el, device="cuda" if use_gpu and not shared else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu and not shared else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # K11: the training metric (AUC over all rows) evaluated where the scores live (outside the timed region)
-    t_ev = time.perf_counter()
-    train_auc = dict(booster.eval(0)).get("auc")
-    eval_ms = (time.perf_counter() - t_ev) * 1e3
-    # sanity: holdout AUC of the trained model (outside the timed region)
+
+    # per-phase breakdown (ms, mean over the timed fits) from the estimator's instrumentation measures
+    phases = {}
+    for k in ("sampling_ms", "dataset_creation_ms", "booster_init_ms", "training_iterations_ms", "total_ms"):
+        vals = [m.get(k, 0.0) for m in measures]
+        phases[k] = round(float(np.mean(vals)), 2) if vals else None
+    native_stats = measures[-1].get("native_stats", {}) if measures else {}
+    iter_s = (phases["training_iterations_ms"] or 0.0) / 1e3
+    # sanity (outside the timed region): holdout AUC of the last model on this rank's first rows
     auc = None
-    if rank == 0:
+    if rank == 0 and model is not None:
         try:
             from sklearn.metrics import roc_auc_score
 
-            p = booster.predict(X_hold, 0, 0, -1)[:, 0]
+            p = model.getModel().score(X_hold, raw=False, classification=True)[:, 1]
             auc = float(roc_auc_score(y_hold, p))
         except Exception:  # pragma: no cover
             auc = None
-    if args.save_model and rank == 0:
+    if args.save_model and rank == 0 and model is not None:
         with open(args.save_model, "w") as fh:
-            fh.write(booster.save_model_string())
+            fh.write(model.getNativeModel())
     total_rows = args.rows * world
     value = total_rows * args.steps / elapsed
     if rank == 0:
         out = {
             "metric": METRIC,
             "value": round(value, 1),
-            "unit": "rows/s (row-iterations per second, whole job)",
+            "unit": "rows/s (training rows / LightGBMClassifier.fit wall seconds, 100 iterations, whole job)",
             "n_gpus": world if use_gpu else 0,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -165,24 +165,28 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            # histograms: per-block 32-bit fixed-point (g, h) sums (scale from the tree's max |g| / max h and
-            # the block's row count), exact int64 cross-block reduction, fp64 split gains and leaf sums
-            # (reference LightGBM CPU: fp32 gradients, fp64 histograms; LightGBM's GPU learner: fp32 histograms)
+            # gradients/hessians fp32 (as the reference's LightGBM), histogram sums 64-bit fixed point per
+            # (feature, bin) with a per-row quantum <= 2^-38 of max|g| (at least fp64-of-fp32 precision),
+            # split gains and leaf values fp64
             "dtype": "fp32",
-            "data": "synthetic Higgs-shape (21 heavy-tailed + 7 derived float features), random labels w/ noise",
+            "data": "synthetic Higgs-shape (21 heavy-tailed + 7 derived float32 features), noisy nonlinear labels",
             "config": {
-                "model": "LightGBMClassifier(binary, numLeaves=%d, maxBin=255, lr=0.1, minDataInLeaf=20)" % args.leaves,
+                "model": "LightGBMClassifier(binary, numIterations=%d, numLeaves=%d, maxBin=255, lr=0.1, "
+                         "minDataInLeaf=20, binSampleCount=200000)" % (args.iterations, args.leaves),
                 "global_batch": total_rows,
                 "seq_len": args.features,
                 "parallelism": f"dp{world}",
                 "rows_per_gpu": args.rows,
-                "backend": booster.backend,
-                "train_auc_sample": auc,
-                "setup_s": round(setup_s, 2),
-                "bin_encode_s": round(encode_s, 3),
-                "train_auc_all_rows": None if train_auc is None else round(train_auc, 5),
-                "train_metric_eval_ms": round(eval_ms, 2),
-                "histogram_accumulation": "int32 fixed-point per block -> exact int64 reduce -> fp64",
+                "timed_region": "LightGBMClassifier.fit(df) end to end (DataFrame built before timing)",
+                "fit_phases_ms": phases,
+                "iteration_loop_row_iters_per_s": round(total_rows * args.iterations / iter_s, 1) if iter_s else None,
+                "iteration_ms": round(phases["training_iterations_ms"] / args.iterations, 3)
+                if phases["training_iterations_ms"] else None,
+                "backend": measures[-1].get("backend") if measures else None,
+                "holdout_auc_first_rows": auc,
+                "datagen_s": round(gen_s, 2),
+                "native_comm_ms": native_stats.get("comm_ms"),
+                "histogram_accumulation": "int64 fixed point per (feature, bin), exact int64 block reduce -> fp64",
                 "histogram_allreduce": (None if world == 1 else "host (gloo)" if not use_gpu else
                                         "p2p-ipc one-shot" if D.p2p_status.get("active") else
                                         "rccl (%s)" % D.p2p_status.get("reason", "")),

@@ -3,6 +3,7 @@
 // D4); the HIP backend keeps the binned matrix, gradients, scores and the
 // whole leaf-wise growth loop resident on the MI355X.
 #pragma once
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <vector>
@@ -19,6 +20,7 @@ namespace sml {
 
 struct TrainStats {
   double hist_ms = 0, split_ms = 0, partition_ms = 0, grad_ms = 0, score_ms = 0, comm_ms = 0;
+  int64_t comm_calls = 0;  // device histogram allreduces issued
   // device-side (hipEvent) time of whole tree growths and score updates; device memory in use after Init
   double device_tree_ms = 0, device_score_ms = 0, device_mem_mb = 0;
   int64_t trees = 0;
@@ -30,6 +32,12 @@ class TrainBackend {
   virtual std::string Name() const = 0;
   virtual void Init(const Dataset* data, const Config& cfg, int num_tree_per_iter) = 0;
   virtual void SetScores(const std::vector<double>& s) = 0;  // class-major n*K
+  // score[k][i] = per_class[k] for every row (boost-from-average start); backends fill in place
+  virtual void FillScores(const std::vector<double>& per_class, int64_t n) {
+    std::vector<double> s(static_cast<size_t>(n) * per_class.size());
+    for (size_t k = 0; k < per_class.size(); ++k) std::fill(s.begin() + k * n, s.begin() + (k + 1) * n, per_class[k]);
+    SetScores(s);
+  }
   virtual void GetScores(std::vector<double>* s) = 0;
   virtual void AddBias(int k, double b) = 0;
   virtual void ScaleScore(int k, double s) = 0;

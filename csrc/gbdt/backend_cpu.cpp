@@ -170,6 +170,7 @@ class CpuBackend : public TrainBackend {
  public:
   std::string Name() const override { return "cpu"; }
   void Init(const Dataset* d, const Config& cfg, int K) override {
+    d->EnsureHostBins();  // the host learner reads the host bin matrix
     data_ = d; cfg_ = cfg; K_ = K; n_ = d->num_data;
     sp_ = MakeSplitParams(cfg);
     score_.assign(static_cast<size_t>(n_) * K, 0.0);

@@ -31,41 +31,31 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "backend.h"
+#include "comm.h"
 #include "hip_common.h"
 
 namespace sml {
 namespace {
 
 constexpr int kBinsPerFeature = 256;
-constexpr int kHistThreads = 512;
 constexpr int kFeatPerGroup = 32;          // 8 dwords of bins per block
 constexpr int kHistStride = 257;           // padded LDS row (bank spread)
-constexpr int kMaxHistBlocks = 512;        // = resident capacity at 2 blocks/CU
+constexpr int kMaxHistBlocks = 256;        // = resident capacity: one 1024-thread, 131.6 KB-LDS block per CU
 constexpr int kMinRowsPerHistBlockDefault = 1024;  // A/B: 1024 ~ 512 < 2048 < 4096
 __constant__ int c_min_rows_per_hist_block = kMinRowsPerHistBlockDefault;
-__constant__ int c_max_hist_blocks = kMaxHistBlocks;  // 256 for the one-block-per-CU shape (SML_HIST_SHAPE)
-// slab stores write through L2 (sc1) so the kernel boundary has ~15 MB less to write back before the
+__constant__ int c_max_hist_blocks = kMaxHistBlocks;
+// slab stores write through L2 (sc1) so the kernel boundary has less to write back before the
 // reduce reads them from the other XCDs (A/B on MI355X: 1.952 -> 1.923 ms/iter); SML_SLAB_WT=0: plain
 __constant__ int c_slab_wt = 1;
 // SML_PART_WT=1: partition outputs (perm, ordered g/h) written through L2 (A/B: 1.96 -> 1.99 ms/iter, slower)
 __constant__ int c_part_wt = 0;
 
-// one slab element (g | h packed as int2); write-through (agent-scope relaxed store = sc1) when c_slab_wt
-__device__ __forceinline__ void SlabStore(int2* p, unsigned long long w) {
-  const int2 v = make_int2(static_cast<int32_t>(w >> 32), static_cast<int32_t>(static_cast<uint32_t>(w)));
-  if (c_slab_wt) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                       (static_cast<unsigned long long>(static_cast<uint32_t>(v.y)) << 32) | static_cast<uint32_t>(v.x),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
 constexpr int kPartThreads = 512;
 constexpr int kMaxPartBlocks = 2048;
 constexpr int kPartRowsDefault = 8;  // A/B on MI355X: 8 rows/thread beat 16 and 4 (profiles/README)
@@ -825,86 +815,105 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // kHistUnroll rows are fetched before any is accumulated so every wave keeps
 // several gathers in flight (the loop is latency-bound otherwise).
 //
-// Accumulation is fixed point with g and h packed in one 64-bit LDS word ->
-// one ds_add_u64 per (row, feature): h >= 0 lives in the low 32 bits (never
-// carries), g in the high 32 (two's complement wraps exactly). The scales
-// depend only on the launch (chunk rows, the tree's max |g| / max h), so every
-// block uses the same scale, the per-block integer sums go to the slab as
-// int2 and the cross-block reduction is an exact int64 sum: the histogram is
-// bitwise independent of row order and of the block decomposition. (A/B on
-// MI355X: float ds_add_f32 13.4 ms/iter, 2x ds_add_u32 4.26, packed u64 4.16.)
-// Precision: the quantum of one row is chunk_rows * max|g| / 2^31 (g) and
-// chunk_rows * max h / 2^32 (h) with chunk_rows <= count / blocks (>= 1024),
-// e.g. ~1e-5 * max|g| for the 11M-row root. A bin holding k rows then carries
-// ~sqrt(k) * quantum / 3.5 of rounding error: about the relative precision of
-// an fp32 histogram (LightGBM's GPU learner default, gpu_use_dp=false) on
-// populated bins, coarser on nearly empty bins; hessians far below
-// quantum / 2 (very confident rows of a near-separable problem) round to zero.
-// test_gpu_histogram_quantisation_skewed_hessians pins tree structure, node
-// hessian sums and loss against the fp64 host oracle in that regime.
-// A/B: 2 rows in flight per thread beat 4 and 8 (round 2, one 1024-thread block per CU: 1.93 / 1.97 / 2.04
+// Accumulation is 64-bit fixed point with g and h in separate LDS words: two
+// ds_add_u64 per (row, feature) into 2 x 32 x 257 words (131.6 KB, one
+// 1024-thread block per CU). Both scales are powers of two chosen per
+// histogram from the leaf's row count and the tree's max |g| / max h so that
+// the sum over ALL of the leaf's rows stays below 2^62 in magnitude: every
+// per-block sum and the exact int64 cross-block reduction fit, the histogram
+// is bitwise independent of row order and of the block decomposition, and the
+// conversion back (x 2^-k) is exact up to one final int64 -> double rounding.
+// Precision: one row's quantum is <= count * max / 2^61, i.e. <= 2^-37.6 of
+// max |g| for the 11M-row root and <= 2^-50 for leaves under 2k rows; a bin of
+// k rows carries ~sqrt(k) * quantum / 3.5 of rounding error - at or below the
+// rounding of LightGBM's fp64 accumulation of fp32 gradients (~k * 2^-53 of
+// the bin's sum) on populated bins. (Round 1-2 packed g | h as two 32-bit
+// halves of one word: ~1e-5 of max |g| at the root; A/B in profiles/README.)
+// A/B: 2 rows in flight per thread beat 4 and 8 (one 1024-thread block per CU: 1.93 / 1.97 / 2.04
 // ms/iter; more rows in flight only queue more LDS atomics)
-constexpr int kHistUnrollDefault = 2;
+constexpr int kHistUnroll = 2;
+constexpr int kHistBlockThreads = 1024;
+constexpr int kHistWords = kFeatPerGroup * kHistStride;  // per plane (g or h)
 
 __device__ __forceinline__ int HistBlocks(int count) {
   return max(1, min(c_max_hist_blocks, ceil_div_i(count, c_min_rows_per_hist_block)));
 }
 
 struct HScale {
-  float g, h;
+  double g, h;    // 2^eg, 2^eh: quantisation scales
+  double ig, ih;  // 2^-eg, 2^-eh: conversion back
 };
 
-__device__ __forceinline__ HScale ChunkScale(int chunk, const float* ghmax) {
-  const float gmax = fmaxf(ghmax[0], 1e-30f), hmax = fmaxf(ghmax[1], 1e-30f);
-  const float rows = static_cast<float>(max(1, chunk));
-  return HScale{2.0e9f / (rows * gmax), 4.0e9f / (rows * hmax)};
+__device__ __forceinline__ int ScaleExp(int count, float vmax) {
+  // largest e with count * vmax * 2^e <= 2^62
+  const double r = 4.611686018427387904e18 / (static_cast<double>(max(1, count)) * fmax(static_cast<double>(vmax), 1e-300));
+  return max(-1000, min(1000, ilogb(r)));
 }
 
 __device__ __forceinline__ HScale HistScale(int count, const float* ghmax) {
-  return ChunkScale(ceil_div_i(count, HistBlocks(count)), ghmax);
+  const int eg = ScaleExp(count, ghmax[0]), eh = ScaleExp(count, ghmax[1]);
+  return HScale{ldexp(1.0, eg), ldexp(1.0, eh), ldexp(1.0, -eg), ldexp(1.0, -eh)};
 }
 
 __device__ __forceinline__ uint32_t word_of(const uint4& b, int j) {
   return j < 4 ? b.x : (j < 8 ? b.y : (j < 12 ? b.z : b.w));
 }
 
-__device__ __forceinline__ unsigned long long PackGH(float2 v, HScale s) {
-  const int32_t gq = __float2int_rn(v.x * s.g);
-  const uint32_t hq = static_cast<uint32_t>(__float2uint_rn(fmaxf(v.y, 0.f) * s.h));
-  return (static_cast<unsigned long long>(static_cast<uint32_t>(gq)) << 32) | hq;
+struct QGH {
+  unsigned long long g, h;  // g two's complement (wraps exactly in unsigned adds)
+};
+
+__device__ __forceinline__ QGH QuantGH(float2 v, const HScale& s) {
+  const long long gq = static_cast<long long>(__builtin_rint(static_cast<double>(v.x) * s.g));
+  const unsigned long long hq =
+      static_cast<unsigned long long>(__builtin_rint(static_cast<double>(fmaxf(v.y, 0.f)) * s.h));
+  return QGH{static_cast<unsigned long long>(gq), hq};
 }
 
-__device__ __forceinline__ void hist_accumulate(unsigned long long* sh, const uint4& b0, const uint4& b1,
-                                                unsigned long long packed, int Fg) {
+__device__ __forceinline__ void hist_accumulate(unsigned long long* shg, unsigned long long* shh, const uint4& b0,
+                                                const uint4& b1, const QGH& q, int Fg) {
 #pragma unroll
   for (int j = 0; j < 16; ++j)
-    if (j < Fg) atomicAdd(&sh[j * kHistStride + ((word_of(b0, j) >> (8 * (j & 3))) & 255u)], packed);
+    if (j < Fg) {
+      const int i = j * kHistStride + ((word_of(b0, j) >> (8 * (j & 3))) & 255u);
+      atomicAdd(&shg[i], q.g);
+      atomicAdd(&shh[i], q.h);
+    }
 #pragma unroll
   for (int j = 0; j < 16; ++j)
-    if (j + 16 < Fg) atomicAdd(&sh[(j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u)], packed);
+    if (j + 16 < Fg) {
+      const int i = (j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u);
+      atomicAdd(&shg[i], q.g);
+      atomicAdd(&shh[i], q.h);
+    }
 }
 
-// kCopies = 2 (1024-thread blocks, one per CU): waves 0-7 and 8-15 accumulate into
-// two LDS copies of the histogram (2 x 65.8 KB), summed when the slab is
-// written; half the slabs (and half the dirty bytes at the kernel boundary) of
-// two 512-thread blocks per CU. Packed words add exactly: a block's h sum
-// stays below 2^32 by construction of the scale.
-template <int kHistUnroll, int kThreads = kHistThreads, int kCopies = 1>
-__global__ __launch_bounds__(kThreads) void hist_kernel(
+// one slab element: (g, h) int64 pair; write-through (agent-scope relaxed stores = sc1) when c_slab_wt
+__device__ __forceinline__ void SlabStore(ulonglong2* p, unsigned long long g, unsigned long long h) {
+  if (c_slab_wt) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *p = make_ulonglong2(g, h);
+  }
+}
+
+template <int kUnroll>
+__global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
     const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
-    const float* __restrict__ h, const float* __restrict__ ghmax, int2* __restrict__ slab) {
+    const float* __restrict__ h, const float* __restrict__ ghmax, ulonglong2* __restrict__ slab) {
   if (st->done) return;
   const DLeaf L = HistSeg(st, leaves);
   const int count = L.count;
   const int nb_active = HistBlocks(count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long shc[kCopies * kFeatPerGroup * kHistStride];
+  __shared__ unsigned long long shg[kHistWords], shh[kHistWords];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kCopies * kFeatPerGroup * kHistStride; i += kThreads) shc[i] = 0ull;
+  for (int i = tid; i < kHistWords; i += kHistBlockThreads) { shg[i] = 0ull; shh[i] = 0ull; }
   __syncthreads();
-  unsigned long long* sh = shc + (kCopies > 1 && tid >= kThreads / 2 ? kFeatPerGroup * kHistStride : 0);
   const int grp = blockIdx.y;
   const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
   const int col = grp * 2;            // first uint4 of this group in a row
@@ -916,116 +925,34 @@ __global__ __launch_bounds__(kThreads) void hist_kernel(
   const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
   const bool phys = L.buf < 0;
-  for (int base = p0 + tid; base < p1; base += kThreads * kHistUnroll) {
-    int r[kHistUnroll];
-    bool ok[kHistUnroll];
+  for (int base = p0 + tid; base < p1; base += kHistBlockThreads * kUnroll) {
+    int r[kUnroll];
+    bool ok[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kHistUnroll; ++u) {
-      const int pos = base + u * kThreads;
+    for (int u = 0; u < kUnroll; ++u) {
+      const int pos = base + u * kHistBlockThreads;
       ok[u] = pos < p1;
       r[u] = ok[u] ? (phys ? pos : perm[pos]) : 0;
     }
-    uint4 b0[kHistUnroll], b1[kHistUnroll];
-    float2 v[kHistUnroll];
+    uint4 b0[kUnroll], b1[kUnroll];
+    float2 v[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kHistUnroll; ++u) {
-      const int pos = base + u * kThreads;
+    for (int u = 0; u < kUnroll; ++u) {
+      const int pos = base + u * kHistBlockThreads;
       const size_t rb = static_cast<size_t>(r[u]) * W4 + col;
       b0[u] = bins4[rb];
       b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
       v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : (ok[u] ? ogh[pos] : make_float2(0.f, 0.f));
     }
 #pragma unroll
-    for (int u = 0; u < kHistUnroll; ++u)
-      if (ok[u]) hist_accumulate(sh, b0[u], b1[u], PackGH(v[u], sc), Fg);
+    for (int u = 0; u < kUnroll; ++u)
+      if (ok[u]) hist_accumulate(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), Fg);
   }
   __syncthreads();
-  int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
-  for (int i = tid; i < Fg * kBinsPerFeature; i += kThreads) {
+  ulonglong2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
+  for (int i = tid; i < Fg * kBinsPerFeature; i += kHistBlockThreads) {
     const int f = i >> 8, b = i & 255;
-    unsigned long long w = shc[f * kHistStride + b];
-    if (kCopies > 1) w += shc[kFeatPerGroup * kHistStride + f * kHistStride + b];
-    SlabStore(out + (grp * kFeatPerGroup + f) * kBinsPerFeature + b, w);
-  }
-}
-
-// Feature-lane variant (SML_HIST_MODE=1; measured slower, kept for A/B): lane l of a wave owns
-// feature (l & 15) of the row in its quad (l >> 4), so one wave instruction
-// adds 4 rows x 16 features. The block's LDS histogram is bin-major,
-// sh[bin][32 features] of packed u64: the 16 lanes of a 64-bit atomic's lane
-// group (one row, features 0-15) always hit 16 different bank pairs whatever
-// their bins are, so the atomics never conflict; each lane extracts its byte
-// with a constant shift (no per-lane dynamic select). The per-row gradient
-// pair and the row's bin dwords are read by the 16 lanes of a quad as one
-// coalesced segment. Slabs are written bin-major ([block][bin][32 * groups]),
-// which hist_reduce_kernel<true> reads contiguously.
-template <int kUnroll>
-__global__ __launch_bounds__(kHistThreads) void hist_fl_kernel(
-    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint32_t* __restrict__ bins32,
-    int W, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
-    const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
-    const float* __restrict__ h, const float* __restrict__ ghmax, int2* __restrict__ slab) {
-  if (st->done) return;
-  const DLeaf L = HistSeg(st, leaves);
-  const int count = L.count;
-  const int nb_active = HistBlocks(count);
-  if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long sh[kBinsPerFeature * kFeatPerGroup];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int i = tid; i < kBinsPerFeature * kFeatPerGroup; i += kHistThreads) sh[i] = 0ull;
-  __syncthreads();
-  const int grp = blockIdx.y;
-  const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
-  const int fl = lane & 15, quad = lane >> 4;
-  const bool f0 = fl < Fg, f1 = fl + 16 < Fg;
-  const int w0off = grp * 8 + (fl >> 2), w1off = grp * 8 + 4 + (fl >> 2);
-  const int shift = (fl & 3) * 8;
-  const int chunk = ceil_div_i(count, nb_active);
-  const int p0 = L.begin + blockIdx.x * chunk;
-  const int p1 = min(L.begin + count, p0 + chunk);
-  const HScale sc = HistScale(count, ghmax);
-  const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
-  const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
-  const bool phys = L.buf < 0;
-  constexpr int kWaves = kHistThreads / 64;
-  constexpr int kStep = kWaves * 4;  // rows per block per unrolled slot
-  for (int base = p0 + wid * 4 + quad; base < p1; base += kStep * kUnroll) {
-    int r[kUnroll];
-    bool ok[kUnroll];
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int pos = base + u * kStep;
-      ok[u] = pos < p1;
-      r[u] = ok[u] ? (phys ? pos : perm[pos]) : 0;
-    }
-    uint32_t a[kUnroll], b[kUnroll];
-    float2 v[kUnroll];
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int pos = base + u * kStep;
-      const uint32_t* row = bins32 + static_cast<size_t>(r[u]) * W;
-      a[u] = f0 && ok[u] ? row[w0off] : 0u;
-      b[u] = f1 && ok[u] ? row[w1off] : 0u;
-      v[u] = !ok[u] ? make_float2(0.f, 0.f) : (phys ? make_float2(g[r[u]], h[r[u]]) : ogh[pos]);
-    }
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      if (!ok[u]) continue;
-      const unsigned long long packed = PackGH(v[u], sc);
-      if (f0) atomicAdd(&sh[((a[u] >> shift) & 255u) * kFeatPerGroup + fl], packed);
-      if (f1) atomicAdd(&sh[((b[u] >> shift) & 255u) * kFeatPerGroup + 16 + fl], packed);
-    }
-  }
-  __syncthreads();
-  // bin-major slab: element (bin, f) of group grp at bin * FP + grp * 32 + f (FP = 32 * groups)
-  const int FP = static_cast<int>(gridDim.y) * kFeatPerGroup;
-  int2* out = slab + static_cast<size_t>(blockIdx.x) * FP * kBinsPerFeature;
-  for (int i = tid; i < kBinsPerFeature * kFeatPerGroup; i += kHistThreads) {
-    const int bin = i >> 5, f = i & 31;
-    if (f >= Fg) continue;
-    const unsigned long long w = sh[i];
-    out[bin * FP + grp * kFeatPerGroup + f] =
-        make_int2(static_cast<int32_t>(w >> 32), static_cast<int32_t>(static_cast<uint32_t>(w)));
+    SlabStore(out + (grp * kFeatPerGroup + f) * kBinsPerFeature + b, shg[f * kHistStride + b], shh[f * kHistStride + b]);
   }
 }
 
@@ -1043,54 +970,43 @@ __global__ __launch_bounds__(256) void ghmax_kernel(const float* __restrict__ g,
   BlockMaxPartial(mg, mh, partial);
 }
 
-// Exact reduction of the per-block integer slabs: block = 8 groups x 32 bins;
-// group y sums blocks y, y+8, ... in int64, the 8 partials are added in LDS
-// and converted once with the launch's scale. hist[E] (the slot after the
-// histogram) carries the leaf's local row count so one data-parallel
-// allreduce of 2E+2 doubles also yields the global count.
+// Exact reduction of the per-block integer slabs: block = 16 groups x 32
+// elements; group y sums blocks y, y+16, ... in int64, the 16 partials are
+// added in LDS and converted once with the histogram's scale. hist[E] (the
+// slot after the histogram) carries the leaf's local row count so one
+// data-parallel allreduce of 2E+2 doubles also yields the global count.
 constexpr int kRedE = 32;
 constexpr int kRedG = 16;
 
-// kBinMajor: slabs of hist_fl_kernel, element (bin, f) at bin * FP + f with
-// FP = 32 * feature groups; thread le walks slab elements contiguously and
-// writes the feature-major histogram entry e = f * 256 + bin.
-template <bool kBinMajor>
 __global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
-    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const int2* __restrict__ slab, int E, int FP,
-    int F, const float* __restrict__ ghmax, double2* __restrict__ hist) {
+    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const ulonglong2* __restrict__ slab, int E,
+    const float* __restrict__ ghmax, double2* __restrict__ hist) {
   if (st->done) return;
   const int count = HistSeg(st, leaves).count;
   const int nb_active = HistBlocks(count);
   const int tid = threadIdx.x, le = tid % kRedE, grp = tid / kRedE;
-  const int si = blockIdx.x * kRedE + le;  // slab element
-  const int ES = kBinMajor ? FP * kBinsPerFeature : E;
-  int e = si;
-  bool valid = si < ES;
-  if (kBinMajor) {
-    const int f = si % FP, bin = si / FP;
-    valid = valid && f < F;
-    e = f * kBinsPerFeature + bin;
-  }
-  long long sg = 0, sh = 0;
+  const int e = blockIdx.x * kRedE + le;
+  const bool valid = e < E;
+  unsigned long long sg = 0, sh = 0;
   if (valid) {
 #pragma unroll 8
     for (int b = grp; b < nb_active; b += kRedG) {
-      const int2 v = slab[static_cast<size_t>(b) * ES + si];
+      const ulonglong2 v = slab[static_cast<size_t>(b) * E + e];
       sg += v.x;
-      sh += static_cast<uint32_t>(v.y);
+      sh += v.y;
     }
   }
-  __shared__ long long rg[kRedG][kRedE], rh[kRedG][kRedE];
+  __shared__ unsigned long long rg[kRedG][kRedE], rh[kRedG][kRedE];
   rg[grp][le] = sg;
   rh[grp][le] = sh;
   __syncthreads();
   if (grp == 0 && valid) {
-    long long tg = 0, th = 0;
+    unsigned long long tg = 0, th = 0;
 #pragma unroll
     for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
     const HScale s = HistScale(count, ghmax);
-    hist[e] = make_double2(static_cast<double>(tg) / static_cast<double>(s.g),
-                           static_cast<double>(th) / static_cast<double>(s.h));
+    hist[e] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
+                           static_cast<double>(static_cast<long long>(th)) * s.ih);
   }
   if (blockIdx.x == 0 && tid == 0) hist[E] = make_double2(static_cast<double>(count), 0.0);
 }
@@ -1512,401 +1428,6 @@ __global__ __launch_bounds__(256) void choose_kernel(DState* __restrict__ st, DL
   ChooseBlock(st, leaves, lbest, lgain, fbest, F, t, count_slot, mono, has_mono);
 }
 
-// ---------------------------------------------------------------- K4 + K5 + choose, one launch
-// split_kernel replaces hist_reduce -> find_split -> choose (three launches,
-// ~21 us per split at the ~6 us floor each small kernel has on this part) by
-// one launch of F blocks x 1024 threads:
-//   1. (kFromSlab) the block of feature f reduces that feature's 256 bins of
-//      the per-block integer slabs exactly (4 thread groups stride the slabs,
-//      int64 partials added in LDS) - or reads the allreduced histogram when
-//      data-parallel ranks inserted an RCCL / P2P allreduce in between;
-//   2. threads 0-255 search the smaller child (or the root), threads 256-511
-//      the larger child (= parent - smaller), as find_split_kernel does;
-//   3. each block publishes its two SplitResults with agent-scope (sc1, L2
-//      write-through) stores, drains them (s_waitcnt vmcnt(0)), joins a
-//      workgroup barrier, and one lane adds to an arrival counter; the block
-//      whose add returns F-1 is the last one and runs the choose step, reading
-//      the records with sc1 loads (the hand-off recipe of the MI355X guide:
-//      every store and load of the handed-off bytes sc1, one agent-scope add
-//      per storing workgroup after its drain + barrier). It resets the counter
-//      for the next launch (kernel boundaries order that reset).
-// No part of the result depends on which block arrives last.
-static_assert(offsetof(SplitResult, threshold) == offsetof(SplitResult, feature) + 4 &&
-                  offsetof(SplitResult, feature) % 8 == 0,
-              "ChooseFused reads {feature, threshold} as one 8-byte granule");
-constexpr int kSplitThreads = 1024;
-constexpr int kSplitRedGroups = kSplitThreads / kBinsPerFeature;  // 4
-
-__device__ __forceinline__ void StoreAgent8(void* p, unsigned long long v) {
-  __hip_atomic_store(static_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long LoadAgent8(const void* p) {
-  return __hip_atomic_load(static_cast<unsigned long long*>(const_cast<void*>(p)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-// Word copies of 8-byte-granule records (no local struct whose address is taken:
-// that would put the record in scratch).
-template <class T>
-__device__ __forceinline__ void PublishAgent(T* dst, const T* src) {  // plain (LDS) -> sc1 stores
-  static_assert(sizeof(T) % 8 == 0 && alignof(T) >= 8, "8-byte granules");
-  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(src);
-  unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
-#pragma unroll
-  for (int i = 0; i < static_cast<int>(sizeof(T) / 8); ++i) StoreAgent8(d + i, s[i]);
-}
-template <class T>
-__device__ __forceinline__ void FetchAgent(T* dst, const T* src) {  // sc1 loads -> plain stores
-  static_assert(sizeof(T) % 8 == 0 && alignof(T) >= 8, "8-byte granules");
-  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(src);
-  unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
-#pragma unroll
-  for (int i = 0; i < static_cast<int>(sizeof(T) / 8); ++i) d[i] = LoadAgent8(s + i);
-}
-__device__ __forceinline__ double LoadAgentD(const double* p) {
-  return __longlong_as_double(static_cast<long long>(LoadAgent8(p)));
-}
-__device__ __forceinline__ int64_t LoadAgentI64(const int64_t* p) { return static_cast<int64_t>(LoadAgent8(p)); }
-
-// The choose step of ChooseBlock for a 1024-thread block whose per-feature
-// records (and, at the root, leaves[0]'s totals) were published in this launch:
-// those are read with sc1 loads; everything else was written by earlier launches.
-__device__ void ChooseFused(DState* __restrict__ st, DLeaf* __restrict__ leaves, SplitResult* __restrict__ lbest,
-                            double* __restrict__ lgain, const SplitResult* __restrict__ fbest, int F, const DTree& t,
-                            int64_t small_cnt, const int8_t* __restrict__ mono, int has_mono) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  __shared__ int sh_best_f[2];
-  __shared__ KeyG wk[4];
-  const bool root = st->phase == 0;
-  const int nchild = root ? 1 : 2;
-  const int small_leaf = st->small_leaf, large_leaf = st->large_leaf;
-  if (wid < nchild) {
-    KeyG k{-INFINITY, 1 << 30, 1 << 30};
-    for (int f = lane; f < F; f += 64) {
-      const SplitResult* r = fbest + wid * F + f;
-      const unsigned long long ft = LoadAgent8(&r->feature);  // {feature, threshold}: one 8-byte granule
-      const int feat = static_cast<int>(static_cast<uint32_t>(ft));
-      if (feat < 0) continue;
-      const uint32_t thr = static_cast<uint32_t>(ft >> 32);
-      const double gain = __longlong_as_double(static_cast<long long>(LoadAgent8(&r->gain)));
-      KeyG c{gain, feat, static_cast<int>(thr)};
-      if (KeyBetter(c, k)) { k = c; k.b = (static_cast<int>(thr) & 0xFFFF) | (f << 16); }
-    }
-    k = WaveArgmax(k);
-    if (lane == 0) sh_best_f[wid] = k.gain == -INFINITY ? -1 : (k.b >> 16);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    if (root) {
-      const int bi = sh_best_f[0];
-      if (bi >= 0) { FetchAgent(lbest, fbest + bi); lgain[0] = LoadAgentD(&fbest[bi].gain); }
-      else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; lgain[0] = -INFINITY; }
-      t.lval[0] = 0.0;
-      t.lcount[0] = LoadAgentI64(&leaves[0].gcount);  // totals published by feature 0's block
-      t.lweight[0] = LoadAgentD(&leaves[0].sum_h);
-      t.lparent[0] = -1;
-      t.ldepth[0] = 0;
-    } else {
-      const int64_t parent_cnt = leaves[large_leaf].gcount;  // stored by the previous choose
-      const int ob = st->pbuf == 0 ? 1 : 0;
-      DLeaf& Lc = leaves[st->split_leaf];
-      DLeaf& Rc = leaves[st->new_leaf];
-      const int lt = PTotal(st);
-      Lc.begin = st->pbegin; Lc.count = lt; Lc.buf = ob;
-      Rc.begin = st->pbegin + lt; Rc.count = st->pcount - lt; Rc.buf = ob;
-      leaves[small_leaf].gcount = small_cnt;
-      leaves[large_leaf].gcount = parent_cnt - small_cnt;
-      t.lcount[small_leaf] = small_cnt;
-      t.lcount[large_leaf] = parent_cnt - small_cnt;
-      for (int c = 0; c < 2; ++c) {
-        const int leaf = c == 0 ? small_leaf : large_leaf;
-        const int bi = sh_best_f[c];
-        if (bi >= 0) { FetchAgent(lbest + leaf, fbest + c * F + bi); lgain[leaf] = LoadAgentD(&fbest[c * F + bi].gain); }
-        else { lbest[leaf].feature = -1; lbest[leaf].gain = -INFINITY; lgain[leaf] = -INFINITY; }
-      }
-    }
-  }
-  __syncthreads();
-  const int nl = st->num_leaves;
-  if (nl >= st->max_leaves) {
-    if (tid == 0) st->done = 1;
-    return;
-  }
-  KeyG k{-INFINITY, 1 << 30, 0};
-  if (tid < 256)
-    for (int i = tid; i < nl; i += 256) {
-      const double gi = lgain[i];
-      KeyG c{gi, i, 0};
-      if (gi > -INFINITY && KeyBetter(c, k)) k = c;
-    }
-  k = WaveArgmax(k);
-  if (lane == 0 && wid < 4) wk[wid] = k;
-  __syncthreads();
-  if (tid != 0) return;
-  KeyG best = wk[0];
-  for (int w = 1; w < 4; ++w) if (KeyBetter(wk[w], best)) best = wk[w];
-  const int bl = best.gain == -INFINITY ? -1 : best.a;
-  if (bl < 0 || !(best.gain > 0.0)) { st->done = 1; return; }
-  const SplitResult sr = lbest[bl];
-  const int node = nl - 1;
-  const int parent = t.lparent[bl];
-  if (parent >= 0) {
-    if (t.left[parent] == ~bl) t.left[parent] = node; else t.right[parent] = node;
-  }
-  t.feat[node] = sr.feature;
-  t.thr[node] = sr.threshold;
-  t.dleft[node] = sr.default_left;
-  t.is_cat[node] = sr.is_cat;
-  for (int w = 0; w < 8; ++w) t.cat_bits[node * 8 + w] = sr.cat_bits[w];
-  t.left[node] = ~bl;
-  t.right[node] = ~nl;
-  t.gain[node] = sr.gain;
-  t.ival[node] = t.lval[bl];
-  t.iweight[node] = sr.left_h + sr.right_h;
-  DLeaf P = leaves[bl];
-  if (root) {  // bl == 0; its totals were published in this launch
-    P.gcount = LoadAgentI64(&leaves[0].gcount);
-    P.sum_g = LoadAgentD(&leaves[0].sum_g);
-    P.sum_h = LoadAgentD(&leaves[0].sum_h);
-  }
-  t.icount[node] = P.gcount;
-  t.lparent[bl] = node; t.lparent[nl] = node;
-  t.lval[bl] = sr.left_out; t.lval[nl] = sr.right_out;
-  t.lweight[bl] = sr.left_h; t.lweight[nl] = sr.right_h;
-  t.lcount[bl] = sr.left_cnt; t.lcount[nl] = sr.right_cnt;
-  const int depth = t.ldepth[bl] + 1;
-  t.ldepth[bl] = depth; t.ldepth[nl] = depth;
-  DLeaf Lc = P, Rc = P;
-  Lc.depth = depth; Rc.depth = depth;
-  Lc.sum_g = sr.left_g; Lc.sum_h = sr.left_h;
-  Rc.sum_g = sr.right_g; Rc.sum_h = sr.right_h;
-  const int mdir = (has_mono && !sr.is_cat) ? static_cast<int>(mono[sr.feature]) : 0;
-  if (mdir != 0) {
-    const double mid = (sr.left_out + sr.right_out) / 2.0;
-    if (mdir < 0) { Lc.lo = fmax(Lc.lo, mid); Rc.hi = fmin(Rc.hi, mid); }
-    else { Lc.hi = fmin(Lc.hi, mid); Rc.lo = fmax(Rc.lo, mid); }
-  }
-  const bool left_small = sr.left_cnt <= sr.right_cnt;
-  st->parent_slot = P.slot;
-  Lc.slot = 2 * node + 1;
-  Rc.slot = 2 * node + 2;
-  if (left_small) { Rc.gcount = P.gcount; } else { Lc.gcount = P.gcount; }
-  leaves[bl] = Lc;
-  leaves[nl] = Rc;
-  lgain[bl] = -INFINITY;
-  lgain[nl] = -INFINITY;
-  st->pbegin = P.begin; st->pcount = P.count; st->pbuf = P.buf;
-  st->cursor = 0ull;
-  st->split_leaf = bl;
-  st->new_leaf = nl;
-  st->small_leaf = left_small ? bl : nl;
-  st->large_leaf = left_small ? nl : bl;
-  st->num_leaves = nl + 1;
-  st->phase = 1;
-}
-
-// kChoose = false (SML_FUSED_SPLIT=3): slab reduce + split search only, for choose_part_kernel
-// to consume after the kernel boundary (plain stores; the row count goes to part[E] as
-// hist_reduce_kernel leaves it; st_next's partition cursor is zeroed as find_split_kernel does).
-template <bool kFromSlab, bool kChoose = true>
-__global__ __launch_bounds__(kSplitThreads) void split_kernel(
-    DState* __restrict__ st, DLeaf* __restrict__ leaves, const int2* __restrict__ slab,
-    double2* __restrict__ part, int E, const float* __restrict__ ghmax, double2* __restrict__ hist_pool,
-    FeatMeta fm, SplitParams sp, SplitResult* __restrict__ fbest, int F, SplitResult* __restrict__ lbest,
-    double* __restrict__ lgain, DTree t, const int8_t* __restrict__ mono, int has_mono,
-    unsigned int* __restrict__ arrive, DState* __restrict__ st_next) {
-  if (!kChoose && st_next && blockIdx.x == 0 && threadIdx.x == 0) st_next->cursor = 0ull;
-  if (st->done) return;
-  const int f = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int c = tid >> 8;          // 0: smaller child / root, 1: larger child, 2-3: reduction helpers
-  const int ltid = tid & 255;      // bin
-  const int cw = (tid >> 6) & 3;   // wave within the child's 256 threads
-  const int cc = c & 1;            // LDS row (helpers alias rows 0/1 but never write them)
-  const bool root = st->phase == 0;
-  const bool act = c == 0 || (c == 1 && !root);
-  const int e = f * kBinsPerFeature + ltid;
-  __shared__ long long red_g[kSplitRedGroups][kBinsPerFeature], red_h[kSplitRedGroups][kBinsPerFeature];
-  __shared__ double2 s_small[kBinsPerFeature];
-  __shared__ double s_g[2][kBinsPerFeature], s_h[2][kBinsPerFeature];
-  __shared__ double s_pg[2][kBinsPerFeature], s_ph[2][kBinsPerFeature];
-  __shared__ double s_tg[2][4], s_th[2][4], s_sg[2][4], s_sh[2][4];
-  __shared__ Cand s_wbest[2][4];
-  __shared__ int s_idx[2][kBinsPerFeature], s_left[2][kBinsPerFeature];
-  __shared__ int s_last;
-  __shared__ SplitResult s_res[2];
-  __shared__ MonoCtx s_mc[2];
-  // ---- 1. the smaller child's (or the root's) histogram of feature f
-  int64_t gcnt;
-  if (kFromSlab) {
-    const int count = HistSeg(st, leaves).count;
-    const int nb_active = HistBlocks(count);
-    long long sg = 0, sh = 0;
-#pragma unroll 8
-    for (int b = c; b < nb_active; b += kSplitRedGroups) {
-      const int2 v = slab[static_cast<size_t>(b) * E + e];
-      sg += v.x;
-      sh += static_cast<uint32_t>(v.y);
-    }
-    red_g[c][ltid] = sg;
-    red_h[c][ltid] = sh;
-    __syncthreads();
-    if (tid < kBinsPerFeature) {
-      long long tg = 0, th = 0;
-#pragma unroll
-      for (int k = 0; k < kSplitRedGroups; ++k) { tg += red_g[k][tid]; th += red_h[k][tid]; }
-      const HScale s = HistScale(count, ghmax);
-      s_small[tid] = make_double2(static_cast<double>(tg) / static_cast<double>(s.g),
-                                  static_cast<double>(th) / static_cast<double>(s.h));
-      if (!kChoose && f == 0 && tid == 0) part[E] = make_double2(static_cast<double>(count), 0.0);
-    }
-    gcnt = count;
-  } else {
-    if (tid < kBinsPerFeature) s_small[tid] = part[e];
-    gcnt = static_cast<int64_t>(part[E].x);
-  }
-  __syncthreads();
-  // ---- 2. split search, threads [0,256) child 0, [256,512) child 1
-  const int leaf_id = root ? 0 : (c == 0 ? st->small_leaf : st->large_leaf);
-  double2 mine = make_double2(0.0, 0.0);
-  DLeaf Lf{};
-  if (act) {
-    const double2 sm = s_small[ltid];
-    if (c == 0) mine = sm;
-    else {
-      const double2 par = hist_pool[static_cast<size_t>(st->parent_slot) * E + e];
-      mine = make_double2(par.x - sm.x, par.y - sm.y);
-    }
-    Lf = leaves[leaf_id];
-    hist_pool[static_cast<size_t>(Lf.slot) * E + e] = mine;
-    s_g[cc][ltid] = mine.x;
-    s_h[cc][ltid] = mine.y;
-    // monotone context of this (leaf, feature) in LDS: the categorical search takes it by pointer
-    if (ltid == 0) s_mc[cc] = MonoCtx{Lf.lo, Lf.hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
-  }
-  const int nb = fm.num_bin[f];
-  const int mt = fm.missing[f];
-  const int dbin = fm.default_bin[f];
-  {
-    double tg = (act && ltid < nb) ? mine.x : 0.0, th = (act && ltid < nb) ? mine.y : 0.0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) { tg += __shfl_xor(tg, off, 64); th += __shfl_xor(th, off, 64); }
-    if (act && lane == 0) { s_tg[cc][cw] = tg; s_th[cc][cw] = th; }
-  }
-  __syncthreads();
-  double G = 0.0, H = 0.0;
-  int64_t cnt = 0;
-  if (act) {
-    G = s_tg[cc][0] + s_tg[cc][1] + s_tg[cc][2] + s_tg[cc][3];
-    H = s_th[cc][0] + s_th[cc][1] + s_th[cc][2] + s_th[cc][3];
-    if (root) {
-      cnt = gcnt;
-      if (f == 0 && ltid == 0) {  // published for the chooser (sc1), like every other hand-off here
-        if (kChoose) {
-          StoreAgent8(&leaves[0].sum_g, static_cast<unsigned long long>(__double_as_longlong(G)));
-          StoreAgent8(&leaves[0].sum_h, static_cast<unsigned long long>(__double_as_longlong(H)));
-          StoreAgent8(&leaves[0].gcount, static_cast<unsigned long long>(cnt));
-        } else {
-          leaves[0].sum_g = G; leaves[0].sum_h = H; leaves[0].gcount = cnt;
-        }
-      }
-    } else {
-      cnt = c == 0 ? gcnt : (Lf.gcount - gcnt);  // Lf.gcount of the large child holds the parent count
-      G = Lf.sum_g; H = Lf.sum_h;
-    }
-  }
-  const bool eligible = act && fm.mask[f] && nb > 1 && cnt >= 2 * static_cast<int64_t>(sp.min_data_in_leaf) &&
-                        (sp.max_depth <= 0 || Lf.depth < sp.max_depth) &&
-                        (sp.bynode_k <= 0 ||
-                         NodeFeatureSelected(sp.bynode_seed, sp.tree_seq, Lf.slot, f, fm.mask, F, sp.bynode_k));
-  const bool is_cat = fm.is_cat[f] != 0;
-  const bool numer = eligible && !is_cat;
-  const MonoCtx* mcp = sp.has_mono ? &s_mc[cc] : nullptr;
-  const int nan_bin = mt == kMissingNaN ? nb - 1 : -1;
-  const int zero_bin = mt == kMissingZero ? dbin : -1;
-  const int last = nan_bin >= 0 ? nb - 2 : nb - 1;
-  double vg = (numer && ltid < nb && ltid != zero_bin && ltid != nan_bin) ? mine.x : 0.0;
-  double vh = (numer && ltid < nb && ltid != zero_bin && ltid != nan_bin) ? mine.y : 0.0;
-  vg = wave_incl_scan(vg, lane);
-  vh = wave_incl_scan(vh, lane);
-  if (act && lane == 63) { s_sg[cc][cw] = vg; s_sh[cc][cw] = vh; }
-  __syncthreads();
-  Cand best{-INFINITY, 1 << 30, 1 << 30};
-  double mg = 0.0, mh = 0.0, cnt_factor = 0.0;
-  if (act) {
-    for (int w = 0; w < cw; ++w) { vg += s_sg[cc][w]; vh += s_sh[cc][w]; }
-    s_pg[cc][ltid] = vg;
-    s_ph[cc][ltid] = vh;
-    mg = nan_bin >= 0 ? s_g[cc][nan_bin] : (zero_bin >= 0 ? s_g[cc][zero_bin] : 0.0);
-    mh = nan_bin >= 0 ? s_h[cc][nan_bin] : (zero_bin >= 0 ? s_h[cc][zero_bin] : 0.0);
-    cnt_factor = cnt / fmax(H, kEpsilon);
-    if (numer && ltid < last) {
-      const double parent_gain = LeafGain(G, H, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step);
-      const double shift = parent_gain + sp.min_gain_to_split;
-      auto consider = [&](double gl, double hl, int dl) {
-        const double gr = G - gl, hr = H - hl;
-        const int64_t cl = EstimateCount(hl, cnt_factor), cr = cnt - cl;
-        if (cl < sp.min_data_in_leaf || cr < sp.min_data_in_leaf) return;
-        if (hl < sp.min_sum_hessian || hr < sp.min_sum_hessian) return;
-        double gain, lout, rout;
-        if (!EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &gain, &lout, &rout)) return;
-        if (!(gain > shift)) return;
-        Cand cd{gain - shift, ltid, dl};
-        if (CandBetter(cd, best)) best = cd;
-      };
-      if (mt == kMissingNone) consider(vg, vh, 1);
-      else { consider(vg, vh, 0); consider(vg + mg, vh + mh, 1); }
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    Cand o;
-    o.gain = __shfl_xor(best.gain, off, 64);
-    o.thr = __shfl_xor(best.thr, off, 64);
-    o.dl = __shfl_xor(best.dl, off, 64);
-    if (CandBetter(o, best)) best = o;
-  }
-  if (act && lane == 0) s_wbest[cc][cw] = best;
-  __syncthreads();
-  if (act && ltid == 0) {
-    SplitResult& r = s_res[cc];
-    r.feature = -1; r.gain = -INFINITY;
-    if (eligible && is_cat) {
-      CategoricalSearchBuf(s_g[cc], s_h[cc], nb, f, G, H, cnt, sp, mcp, &r, s_idx[cc], s_left[cc]);
-    } else if (eligible) {
-      Cand b = s_wbest[cc][0];
-      for (int w = 1; w < 4; ++w) if (CandBetter(s_wbest[cc][w], b)) b = s_wbest[cc][w];
-      if (b.gain != -INFINITY) {
-        double gl = s_pg[cc][b.thr], hl = s_ph[cc][b.thr];
-        if (mt != kMissingNone && b.dl) { gl += mg; hl += mh; }
-        const double gr = G - gl, hr = H - hl;
-        r.feature = f; r.gain = b.gain; r.threshold = static_cast<uint32_t>(b.thr); r.default_left = b.dl;
-        r.is_cat = 0;
-        r.left_g = gl; r.left_h = hl; r.right_g = gr; r.right_h = hr;
-        r.left_cnt = EstimateCount(hl, cnt_factor); r.right_cnt = cnt - r.left_cnt;
-        double g2;
-        (void)EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &g2, &r.left_out,
-                        &r.right_out);
-        if (mcp && mcp->mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(Lf.depth, sp.monotone_penalty);
-        for (int w = 0; w < 8; ++w) r.cat_bits[w] = 0;
-      }
-    }
-    if (kChoose) PublishAgent(fbest + c * F + f, &r);
-    else fbest[c * F + f] = r;
-  }
-  if (!kChoose) return;
-  // ---- 3. publish + arrive; the last block chooses
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned int old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == static_cast<unsigned int>(F - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (tid == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ChooseFused(st, leaves, lbest, lgain, fbest, F, t, gcnt, mono, has_mono);
-}
-
 // ---------------------------------------------------------------- K6
 // Decisions read the column-major copy: the lanes of a wave touch one byte
 // column (contiguous for the physical root, increasing for partitioned leaves)
@@ -2023,34 +1544,6 @@ __device__ __forceinline__ void PartitionTiles(
     }
     __syncthreads();
   }
-}
-
-template <int kPartRows>
-__global__ __launch_bounds__(kPartThreads) void part_kernel(
-    DState* __restrict__ st, const SplitResult* __restrict__ lbest, const uint8_t* __restrict__ cbins, int64_t n,
-    const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
-    const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1,
-    float2* __restrict__ wogh0, float2* __restrict__ wogh1, const float* __restrict__ g,
-    const float* __restrict__ h, FeatMeta fm) {
-  if (st->done) return;
-  const int pbegin = st->pbegin, pcount = st->pcount, pbuf = st->pbuf;
-  constexpr int kPartTile = kPartThreads * kPartRows;
-  const int ntiles = ceil_div_i(pcount, kPartTile);
-  if (static_cast<int>(blockIdx.x) >= ntiles) return;
-  const SplitResult* srp = lbest + st->split_leaf;
-  PartSplit ps;
-  ps.feature = srp->feature;
-  ps.is_cat = srp->is_cat;
-  ps.dleft = srp->default_left;
-  ps.thr = srp->threshold;
-  ps.nb = fm.num_bin[ps.feature];
-  ps.mt = fm.missing[ps.feature];
-  ps.dbin = fm.default_bin[ps.feature];
-  __shared__ uint32_t s_cat[8];
-  if (threadIdx.x < 8) s_cat[threadIdx.x] = ps.is_cat ? srp->cat_bits[threadIdx.x] : 0u;
-  __syncthreads();
-  PartitionTiles<kPartRows>(ps, s_cat, pbegin, pcount, pbuf, &st->cursor, cbins, n, perm0, perm1, ogh0, ogh1,
-                            wperm0, wperm1, wogh0, wogh1, g, h);
 }
 
 // ---------------------------------------------------------------- choose + K6, one launch
@@ -2395,7 +1888,7 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
 // first and last read the same 32-B bin row, so one kernel does all three:
 // per row it walks the tree on the row's bins (nodes + leaf values staged in
 // LDS), adds scale * leaf value to the score, evaluates the objective on the
-// new score, stores g and h, and accumulates the packed fixed-point (g, h) into
+// new score, stores g and h, and accumulates the 64-bit fixed-point (g, h) into
 // the block's LDS histogram exactly as hist_kernel does for the root. The
 // grid/chunk decomposition is hist_kernel's root decomposition (HistBlocks(n)
 // blocks of ceil(n / blocks) contiguous rows), so hist_reduce_kernel reduces
@@ -2407,23 +1900,23 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
 // Replaces score_kernel + grad_kernel + the root hist_kernel (150 + 54 + 131
 // us at 11M x 28 on MI355X, three full passes over rows).
 
-template <int kUnroll, int kThreads = kHistThreads, int kCopies = 1>
-__global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
+template <int kUnroll>
+__global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
     float* __restrict__ g, float* __restrict__ h, const float* __restrict__ bound, float* __restrict__ partial,
-    int2* __restrict__ slab) {
+    ulonglong2* __restrict__ slab) {
+  constexpr int kThreads = kHistBlockThreads;
   const int nb_active = HistBlocks(n);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long shc[kCopies * kFeatPerGroup * kHistStride];
+  __shared__ unsigned long long shg[kHistWords], shh[kHistWords];
   __shared__ int4 snodes[kPrepMaxNodes];
   __shared__ double slval[kPrepMaxNodes + 1];
   const int tid = threadIdx.x;
   const int num_leaves = src.st ? src.st->num_leaves : tv.num_leaves;
   const int ni = num_leaves - 1;
   const uint32_t* cat_bits = src.st ? src.t.cat_bits : tv.cat_bits;
-  for (int i = tid; i < kCopies * kFeatPerGroup * kHistStride; i += kThreads) shc[i] = 0ull;
-  unsigned long long* sh = shc + (kCopies > 1 && tid >= kThreads / 2 ? kFeatPerGroup * kHistStride : 0);
+  for (int i = tid; i < kHistWords; i += kThreads) { shg[i] = 0ull; shh[i] = 0ull; }
   if (src.st) {
     StageDeviceTree(src, num_leaves, snodes, slval, tid, kThreads);
   } else {
@@ -2469,17 +1962,15 @@ __global__ __launch_bounds__(kThreads) void score_grad_hist_kernel(
       h[i] = hh;
       mg = fmaxf(mg, fabsf(gg));
       mh = fmaxf(mh, fabsf(hh));
-      hist_accumulate(sh, b0[u], b1[u], PackGH(make_float2(gg, hh), sc), F);
+      hist_accumulate(shg, shh, b0[u], b1[u], QuantGH(make_float2(gg, hh), sc), F);
     }
   }
   BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
   __syncthreads();
-  int2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
+  ulonglong2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
   for (int i = tid; i < F * kBinsPerFeature; i += kThreads) {
     const int f = i >> 8, b = i & 255;
-    unsigned long long v = shc[f * kHistStride + b];
-    if (kCopies > 1) v += shc[kFeatPerGroup * kHistStride + f * kHistStride + b];
-    SlabStore(out + i, v);
+    SlabStore(out + i, shg[f * kHistStride + b], shh[f * kHistStride + b]);
   }
 }
 
@@ -2490,6 +1981,10 @@ __global__ void transpose_bins_kernel(const uint8_t* __restrict__ bins, int S, i
     const uint8_t* row = bins + i * S;
     for (int f = 0; f < F; ++f) cbins[static_cast<size_t>(f) * n + i] = row[f];
   }
+}
+
+__global__ void fill_f64_kernel(double* __restrict__ s, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) s[i] = v;
 }
 
 __global__ void axpby_kernel(double* __restrict__ s, int64_t n, double a, double b) {
@@ -2505,6 +2000,8 @@ class GpuBackend : public TrainBackend {
     if (stream_) { (void)hipStreamSynchronize(stream_); (void)hipStreamDestroy(stream_); }
     for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
     if (ev_copy_) (void)hipEventDestroy(ev_copy_);
+    if (ev_sync_) (void)hipEventDestroy(ev_sync_);
+    for (hipEvent_t e : comm_ev_) if (e) (void)hipEventDestroy(e);
     if (pinned_) (void)hipHostFree(pinned_);
   }
   std::string Name() const override { return "hip"; }
@@ -2525,10 +2022,18 @@ class GpuBackend : public TrainBackend {
     E_ = F_ * kBinsPerFeature;
     L_ = std::max(2, cfg.num_leaves);
     FG_ = (F_ + kFeatPerGroup - 1) / kFeatPerGroup;
-    bins_.alloc(static_cast<size_t>(n_) * S_);
-    SML_HIP_CHECK(hipMemcpyAsync(bins_.get(), d->bins.data(), static_cast<size_t>(n_) * S_, hipMemcpyHostToDevice, stream_));
+    if (d->dev && d->dev_valid && d->dev->device == dev_) {
+      // K1 left the bin matrix in HBM on this device: adopt it (no host round trip)
+      dev_bins_ = d->dev;
+      bins_ptr_ = dev_bins_->rows;
+    } else {
+      d->EnsureHostBins();
+      bins_.alloc(static_cast<size_t>(n_) * S_);
+      SML_HIP_CHECK(hipMemcpyAsync(bins_.get(), d->bins.data(), static_cast<size_t>(n_) * S_, hipMemcpyHostToDevice, stream_));
+      bins_ptr_ = bins_.get();
+    }
     cbins_.alloc(static_cast<size_t>(n_) * std::max(1, F_));
-    hipLaunchKernelGGL(transpose_bins_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, bins_.get(), S_, F_, n_,
+    hipLaunchKernelGGL(transpose_bins_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, bins_ptr_, S_, F_, n_,
                        cbins_.get());
     SML_HIP_CHECK(hipGetLastError());
     label_.alloc(n_);
@@ -2541,30 +2046,16 @@ class GpuBackend : public TrainBackend {
     g_.alloc(static_cast<size_t>(n_) * K);
     h_.alloc(static_cast<size_t>(n_) * K);
     for (int b = 0; b < 2; ++b) { perm_[b].alloc(n_); ogh_[b].alloc(n_); }
-    if (const char* e = std::getenv("SML_HIST_MODE")) hist_mode_ = std::atoi(e) == 1 ? 1 : 0;
-    // bin-major slabs (hist_fl_kernel) are padded to 32 features per group
-    slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * std::max<size_t>(E_, static_cast<size_t>(FG_) * kFeatPerGroup * kBinsPerFeature));
+    slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * E_);
     part_.alloc(static_cast<size_t>(E_) + 1);  // histogram + (row count, 0)
     hist_pool_.alloc(static_cast<size_t>(2 * L_ + 2) * E_);
     // launch-shape knobs for A/B runs (defaults are the measured best)
     if (const char* e = std::getenv("SML_PART_ROWS")) part_rows_ = std::atoi(e);
-    if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll_ = std::atoi(e);
     if (part_rows_ != 4 && part_rows_ != 8 && part_rows_ != 16) part_rows_ = kPartRowsDefault;
     if (const char* e = std::getenv("SML_HIST_MIN_ROWS")) {
       const int v = std::max(256, std::atoi(e));
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_min_rows_per_hist_block), &v, sizeof(int)));
     }
-    if (hist_unroll_ != 2 && hist_unroll_ != 4 && hist_unroll_ != 8) hist_unroll_ = kHistUnrollDefault;
-    if (const char* e = std::getenv("SML_HIST_THREADS")) hist_threads_ = std::atoi(e);
-    if (hist_threads_ != 256 && hist_threads_ != 512 && hist_threads_ != 1024) hist_threads_ = kHistThreads;
-    // SML_HIST_SHAPE (A/B): 0 = two 512-thread blocks per CU (512 slabs), 1 = one 1024-thread block
-    // per CU with two LDS histogram copies (256 slabs), 2 = one 1024-thread block, one copy.
-    // MI355X, 11M x 28: 2.14 / 2.06 / 2.05 ms/iter (half the slab bytes written, reduced and
-    // written back at the kernel boundary; the second LDS copy buys nothing)
-    if (const char* e = std::getenv("SML_HIST_SHAPE")) hist_shape_ = std::atoi(e);
-    if (hist_shape_ < 0 || hist_shape_ > 2) hist_shape_ = 2;
-    max_hist_blocks_ = hist_shape_ == 0 ? kMaxHistBlocks : kMaxHistBlocks / 2;
-    SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_max_hist_blocks), &max_hist_blocks_, sizeof(int)));
     if (const char* e = std::getenv("SML_PART_WT")) {
       const int v = std::atoi(e) != 0 ? 1 : 0;
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_part_wt), &v, sizeof(int)));
@@ -2573,15 +2064,14 @@ class GpuBackend : public TrainBackend {
       const int v = std::atoi(e) != 0 ? 1 : 0;
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_slab_wt), &v, sizeof(int)));
     }
-    if (const char* e = std::getenv("SML_FUSED_SPLIT")) fused_split_ = std::atoi(e);
     if (const char* e = std::getenv("SML_SKIP_LAST_SPLIT")) skip_last_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SML_MERGED_CHOOSE")) merged_choose_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SML_GBDT_COMM_WORLD1")) comm_world1_ = std::atoi(e) != 0;
     {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
       // choose_part_kernel: every block pays the choose prologue, so keep the grid within one resident
       // round (A/B on MI355X, 11M x 28: 2048 blocks 2.09-2.10 ms/iter, 1024 1.99-2.01, 768 1.97-2.01, 512 2.01-2.04)
-      if (merged_choose_ && (fused_split_ == 0 || fused_split_ == 3)) {
+      {
         int per_cu = 0, cus = 0;
         auto ck = part_rows_ == 16 ? choose_part_kernel<16> : (part_rows_ == 4 ? choose_part_kernel<4> : choose_part_kernel<8>);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ck, kPartThreads, 0) == hipSuccess &&
@@ -2600,7 +2090,7 @@ class GpuBackend : public TrainBackend {
                            (cfg.bagging_freq > 0 && (cfg.bagging_fraction < 1.0 || cfg.pos_bagging_fraction < 1.0 ||
                                                      cfg.neg_bagging_fraction < 1.0));
       const char* e = std::getenv("SML_PREP");
-      prep_ok_ = K == 1 && !sampled && hist_mode_ == 0 && (fused_split_ == 0 || fused_split_ == 3) && F_ > 0 &&
+      prep_ok_ = K == 1 && !sampled && F_ > 0 &&
                  F_ <= kFeatPerGroup &&
                  L_ <= kPrepMaxNodes + 1 && !(e && std::atoi(e) == 0);
       wmax_ = 1.0;
@@ -2608,12 +2098,9 @@ class GpuBackend : public TrainBackend {
         wmax_ = 0.0;
         for (float w : d->weight) wmax_ = std::max(wmax_, static_cast<double>(std::fabs(w)));
       }
-      ymax_ = 0.0;
-      for (float y : d->label) ymax_ = std::max(ymax_, static_cast<double>(std::fabs(y)));
+      ymax_ = -1.0;  // max |label|: computed when a cross-entropy prep pass first needs it
       ghbound_.alloc(2);
     }
-    arrive_.alloc(1);
-    SML_HIP_CHECK(hipMemsetAsync(arrive_.get(), 0, sizeof(unsigned int), stream_));
     fbest_.alloc(2 * F_);
     lbest_.alloc(L_);
     lgain_.alloc(L_);
@@ -2675,6 +2162,7 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
     for (hipEvent_t& e : ev_) SML_HIP_CHECK(hipEventCreate(&e));
     SML_HIP_CHECK(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming));
+    SML_HIP_CHECK(hipEventCreateWithFlags(&ev_sync_, hipEventDisableTiming));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) stats.device_mem_mb = (total_b - free_b) / 1048576.0;
@@ -2684,6 +2172,14 @@ class GpuBackend : public TrainBackend {
     prep_valid_ = root_ready_ = false;
     SML_HIP_CHECK(hipMemcpyAsync(score_.get(), s.data(), sizeof(double) * s.size(), hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  void FillScores(const std::vector<double>& per_class, int64_t n) override {
+    prep_valid_ = root_ready_ = false;
+    for (size_t k = 0; k < per_class.size(); ++k) {
+      hipLaunchKernelGGL(fill_f64_kernel, dim3(GridFor(n)), dim3(256), 0, stream_, score_.get() + k * n, n,
+                         per_class[k]);
+      SML_HIP_CHECK(hipGetLastError());
+    }
   }
   void GetScores(std::vector<double>* s) override {
     s->resize(static_cast<size_t>(n_) * K_);
@@ -2822,6 +2318,10 @@ class GpuBackend : public TrainBackend {
   }
 
   void Synchronize() override {
+    if (Distributed()) {
+      SML_HIP_CHECK(hipEventRecord(ev_sync_, stream_));
+      WaitEvent(ev_sync_);
+    }
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
     AccountScoreTime();
   }
@@ -2853,7 +2353,7 @@ class GpuBackend : public TrainBackend {
       prep_valid_ = root_ready_ = false;
       SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
       hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, DevTreeView{}, src,
-                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, 1.0,
+                         reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, cbins_.get(), n_, 1.0,
                          score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
@@ -2896,9 +2396,8 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipGetLastError());
       pending_parts_ = 0;
     }
-    const bool merged = merged_choose_ && (fused_split_ == 0 || fused_split_ == 3);
     st_cur_ = state_;
-    st_next_ = merged ? state_ + 1 : nullptr;
+    st_next_ = state_ + 1;
     hipLaunchKernelGGL(root_init_kernel, dim3(1), dim3(64), 0, stream_, state_, leaves_.get(), root_count, root_buf, L_,
                        ghmax_partial_.get(), pending_parts_, ghmax_.get());
     SML_HIP_CHECK(hipGetLastError());
@@ -2907,38 +2406,30 @@ class GpuBackend : public TrainBackend {
     const float* root_scale = nullptr;
     if (root_prepared) {
       root_scale = reinterpret_cast<const float*>(ghbound_.get());
-      if (!(fused_split_ == 3 && !Distributed())) EnqueueReduce(root_scale);
+      EnqueueReduce(root_scale);
     } else {
       EnqueueHistogram(g, h);
     }
-    EnqueueFindChoose(!merged, root_scale);
+    EnqueueFindChoose(false);
     for (int s = 1; s < L_; ++s) {
-      // (choose +) partition the chosen leaf, histogram its smaller child, search both
-      if (merged) {
-        DState* sin = st_cur_;
-        DState* sout = st_cur_ == state_ ? state_ + 1 : state_;
-        auto ck = part_rows_ == 16 ? choose_part_kernel<16> : (part_rows_ == 4 ? choose_part_kernel<4> : choose_part_kernel<8>);
-        hipLaunchKernelGGL(ck, dim3(part_grid_), dim3(kPartThreads), 0, stream_, sin, sout, leaves_.get(),
-                           lbest_.get(), lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono,
-                           cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
-                           perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
+      // choose + partition the chosen leaf, histogram its smaller child, search both
+      DState* sin = st_cur_;
+      DState* sout = st_cur_ == state_ ? state_ + 1 : state_;
+      auto ck = part_rows_ == 16 ? choose_part_kernel<16> : (part_rows_ == 4 ? choose_part_kernel<4> : choose_part_kernel<8>);
+      hipLaunchKernelGGL(ck, dim3(part_grid_), dim3(kPartThreads), 0, stream_, sin, sout, leaves_.get(),
+                         lbest_.get(), lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono,
+                         cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
+                         perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
+      SML_HIP_CHECK(hipGetLastError());
+      st_cur_ = sout;
+      st_next_ = sin;
+      if (s == L_ - 1 && skip_last_ && !Distributed()) {
+        hipLaunchKernelGGL(finalize_last_split_kernel, dim3(1), dim3(64), 0, stream_, st_cur_, leaves_.get(), dt_);
         SML_HIP_CHECK(hipGetLastError());
-        st_cur_ = sout;
-        st_next_ = sin;
-        if (s == L_ - 1 && skip_last_ && fused_split_ == 0 && hist_mode_ == 0 && !Distributed()) {
-          hipLaunchKernelGGL(finalize_last_split_kernel, dim3(1), dim3(64), 0, stream_, st_cur_, leaves_.get(), dt_);
-          SML_HIP_CHECK(hipGetLastError());
-          break;
-        }
-      } else {
-        auto pk = part_rows_ == 16 ? part_kernel<16> : (part_rows_ == 4 ? part_kernel<4> : part_kernel<8>);
-        hipLaunchKernelGGL(pk, dim3(part_grid_), dim3(kPartThreads), 0, stream_, st_cur_, lbest_.get(),
-                           cbins_.get(), n_, perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(),
-                           perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, fm_);
-        SML_HIP_CHECK(hipGetLastError());
+        break;
       }
       EnqueueHistogram(g, h);
-      EnqueueFindChoose(!merged || s == L_ - 1);
+      EnqueueFindChoose(s == L_ - 1);
     }
     final_v_ = st_cur_ == state_ ? 0 : 1;
     SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
@@ -2951,11 +2442,41 @@ class GpuBackend : public TrainBackend {
   }
 
   Tree FinishTree() {
-    SML_HIP_CHECK(hipEventSynchronize(ev_copy_));
+    WaitEvent(ev_copy_);
     Tree t = ReadTree();
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ev_[0], ev_[1]) == hipSuccess) stats.device_tree_ms += ms;
+    for (int i = 0; i < comm_used_; ++i)
+      if (hipEventElapsedTime(&ms, comm_ev_[2 * i], comm_ev_[2 * i + 1]) == hipSuccess) stats.comm_ms += ms;
+    comm_used_ = 0;
     return t;
+  }
+
+  // Wait for `ev`. Data-parallel runs poll instead of blocking: a collective stuck on a dead peer never
+  // completes, so while waiting the communicator's async error state is checked (CommError on failure)
+  // and after cfg time_out minutes the communicator is aborted (its pending kernels return) and the wait
+  // raises CommError - every rank fails instead of hanging (NetworkManager.scala:195-218).
+  void WaitEvent(hipEvent_t ev) {
+    if (!Distributed()) {
+      SML_HIP_CHECK(hipEventSynchronize(ev));
+      return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const double limit_s = 60.0 * std::max(1, cfg_.time_out);
+    int spins = 0;
+    for (;;) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) SML_HIP_CHECK(q);
+      comm_->Check();
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+        comm_->Abort();
+        throw CommError("collective did not complete within time_out=" + std::to_string(cfg_.time_out) +
+                        " min (a peer rank died or diverged); communicator aborted");
+      }
+      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    comm_->Check();
   }
 
   void UpdateScore(const Tree& t, int k, double scale) override {
@@ -2967,7 +2488,7 @@ class GpuBackend : public TrainBackend {
       LaunchPrep(tv, DevTreeSrc{}, scale);  // score update + next gradients + next root histogram, one pass
     } else {
       hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv, DevTreeSrc{},
-                         reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, scale,
+                         reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, cbins_.get(), n_, scale,
                          score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
       SML_HIP_CHECK(hipGetLastError());
     }
@@ -2979,7 +2500,7 @@ class GpuBackend : public TrainBackend {
   void PredictLeafIndex(const Tree& t, std::vector<int32_t>* leaf) override {
     DevTreeView tv = UploadTree(t);
     hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, tv, DevTreeSrc{},
-                       reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, cbins_.get(), n_, 0.0,
+                       reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, cbins_.get(), n_, 0.0,
                        static_cast<double*>(nullptr), leaf_idx_.get());
     SML_HIP_CHECK(hipGetLastError());
     leaf->resize(n_);
@@ -3007,10 +2528,8 @@ class GpuBackend : public TrainBackend {
   // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
   void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
     if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    auto pk = hist_shape_ == 1 ? score_grad_hist_kernel<2, 1024, 2>
-              : hist_shape_ == 2 ? score_grad_hist_kernel<2, 1024, 1> : score_grad_hist_kernel<2, kHistThreads, 1>;
-    hipLaunchKernelGGL(pk, dim3(max_hist_blocks_), dim3(hist_shape_ == 0 ? kHistThreads : 1024), 0, stream_, tv, src,
-                       reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, static_cast<int32_t>(n_), scale,
+    hipLaunchKernelGGL(score_grad_hist_kernel<kHistUnroll>, dim3(kMaxHistBlocks), dim3(kHistBlockThreads), 0, stream_, tv, src,
+                       reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, static_cast<int32_t>(n_), scale,
                        score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
                        reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
     SML_HIP_CHECK(hipGetLastError());
@@ -3089,6 +2608,10 @@ class GpuBackend : public TrainBackend {
       gb = std::fabs(p.sigmoid) * lw * wmax_;
       hb = p.sigmoid * p.sigmoid * 0.25 * lw * wmax_;
     } else if (p.kind == kObjCrossEntropy) {
+      if (ymax_ < 0.0) {
+        ymax_ = 0.0;
+        for (float y : data_->label) ymax_ = std::max(ymax_, static_cast<double>(std::fabs(y)));
+      }
       gb = (1.0 + ymax_) * wmax_;
       hb = 0.25 * wmax_;
     } else {
@@ -3103,78 +2626,47 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipStreamSynchronize(stream_));
     }
     prep_params_ = p;
-    prep_blocks_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(max_hist_blocks_, (n_ + min_rows_hist_ - 1) / min_rows_hist_)));
+    prep_blocks_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxHistBlocks, (n_ + min_rows_hist_ - 1) / min_rows_hist_)));
     prep_armed_ = true;
   }
 
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-    if (hist_mode_ == 1) {
-      auto hk = hist_unroll_ == 8 ? hist_fl_kernel<8> : (hist_unroll_ == 4 ? hist_fl_kernel<4> : hist_fl_kernel<2>);
-      hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, FG_), dim3(kHistThreads), 0, stream_, st_cur_, leaves_.get(),
-                         reinterpret_cast<const uint32_t*>(bins_.get()), S_ / 4, F_, perm_[0].get(), perm_[1].get(),
-                         ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
-    } else {
-      auto hk = hist_shape_ == 1 ? hist_kernel<2, 1024, 2>
-                : hist_shape_ == 2 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024, 1>
-                                      : hist_unroll_ == 8 ? hist_kernel<8, 1024, 1> : hist_kernel<2, 1024, 1>)
-                : hist_threads_ == 1024 ? (hist_unroll_ == 4 ? hist_kernel<4, 1024> : hist_kernel<2, 1024>)
-                : hist_threads_ == 256 ? (hist_unroll_ == 4 ? hist_kernel<4, 256> : hist_kernel<2, 256>)
-                : (hist_unroll_ == 8 ? hist_kernel<8> : (hist_unroll_ == 4 ? hist_kernel<4> : hist_kernel<2>));
-      hipLaunchKernelGGL(hk, dim3(max_hist_blocks_, FG_), dim3(hist_shape_ == 0 ? hist_threads_ : 1024), 0, stream_, st_cur_,
-                         leaves_.get(), reinterpret_cast<const uint4*>(bins_.get()), S_ / 16, F_, perm_[0].get(),
-                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
-    }
+    hipLaunchKernelGGL(hist_kernel<kHistUnroll>, dim3(kMaxHistBlocks, FG_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
+                       leaves_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
+                       perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     SML_HIP_CHECK(hipGetLastError());
-    if ((fused_split_ == 1 || fused_split_ == 3) && hist_mode_ == 0 && !Distributed()) return;  // split_kernel reduces
     EnqueueReduce(ghmax);
   }
 
   // slab reduce with the scale the slabs were built with (+ the data-parallel allreduce)
   void EnqueueReduce(const float* ghmax) {
-    const int FP = FG_ * kFeatPerGroup;
-    const int ES = hist_mode_ == 1 ? FP * kBinsPerFeature : E_;
-    hipLaunchKernelGGL(hist_mode_ == 1 ? hist_reduce_kernel<true> : hist_reduce_kernel<false>,
-                       dim3((ES + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, st_cur_, leaves_.get(),
-                       slab_.get(), E_, FP, F_, ghmax, part_.get());
+    hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, st_cur_,
+                       leaves_.get(), slab_.get(), E_, ghmax, part_.get());
     SML_HIP_CHECK(hipGetLastError());
     if (Distributed()) {
-      // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL
-      auto t0 = std::chrono::steady_clock::now();
+      // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL / P2P,
+      // timed on the device (hipEvents around the collective on the engine stream)
+      EnsureCommEvents();
+      const bool timed = comm_used_ < static_cast<int>(comm_ev_.size()) / 2;
+      if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_], stream_));
       comm_->AllReduceDeviceF64(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 2, stream_);
-      stats.comm_ms += Ms(t0);
+      if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_ + 1], stream_));
+      comm_used_ += timed ? 1 : 0;
+      ++stats.comm_calls;
     }
   }
 
-  bool Distributed() const { return comm_ && comm_->world() > 1; }
+  // SML_GBDT_COMM_WORLD1=1 (tests): a world-1 communicator runs the full data-parallel path (allreduce per
+  // split, device comm timing, polling waits) so a one-GPU box executes it end to end
+  bool Distributed() const { return comm_ && (comm_->world() > 1 || comm_world1_); }
 
-  void EnqueueFindChoose(bool choose_now = true, const float* scale = nullptr) {
-    if (fused_split_ == 3 && !Distributed()) {
-      // slab reduce + split search in one launch; the choose step runs in choose_part_kernel (or below)
-      const float* ghmax = scale ? scale : reinterpret_cast<const float*>(ghmax_.get());
-      hipLaunchKernelGGL((split_kernel<true, false>), dim3(F_), dim3(kSplitThreads), 0, stream_, st_cur_,
-                         leaves_.get(), slab_.get(), part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(),
-                         F_, lbest_.get(), lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get(), st_next_);
-      SML_HIP_CHECK(hipGetLastError());
-      if (!choose_now) return;
-      hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, st_cur_, leaves_.get(), lbest_.get(),
-                         lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono);
-      SML_HIP_CHECK(hipGetLastError());
-      return;
-    }
-    if (fused_split_ == 1 || fused_split_ == 2) {
-      const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-      auto k = (Distributed() || fused_split_ == 2 || hist_mode_ == 1) ? split_kernel<false> : split_kernel<true>;
-      hipLaunchKernelGGL(k, dim3(F_), dim3(kSplitThreads), 0, stream_, st_cur_, leaves_.get(), slab_.get(),
-                         part_.get(), E_, ghmax, hist_pool_.get(), fm_, sp_, fbest_.get(), F_, lbest_.get(),
-                         lgain_.get(), dt_, mono_.get(), sp_.has_mono, arrive_.get(), static_cast<DState*>(nullptr));
-      SML_HIP_CHECK(hipGetLastError());
-      return;
-    }
+  // root (choose_now = false): choose_part_kernel does the choose step with the next partition
+  void EnqueueFindChoose(bool choose_now) {
     hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), part_.get(),
                        E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_, st_next_);
     SML_HIP_CHECK(hipGetLastError());
-    if (!choose_now) return;  // choose_part_kernel does the choose step with the next partition
+    if (!choose_now) return;
     hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, st_cur_, leaves_.get(), lbest_.get(),
                        lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono);
     SML_HIP_CHECK(hipGetLastError());
@@ -3290,12 +2782,14 @@ class GpuBackend : public TrainBackend {
   int K_ = 1, F_ = 0, S_ = 4, W_ = 1, E_ = 0, L_ = 2, FG_ = 1;
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
-  DevBuf<uint8_t> bins_, cbins_;
+  DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident
+  std::shared_ptr<DeviceBins> dev_bins_;   // adopted K1 output (keeps it alive)
+  const uint8_t* bins_ptr_ = nullptr;      // row-major bin matrix the kernels read
   DevBuf<float> label_, weight_, g_, h_;
   DevBuf<double> score_;
   DevBuf<int32_t> perm_[2];
   DevBuf<float2> ogh_[2];
-  DevBuf<int2> slab_;
+  DevBuf<ulonglong2> slab_;
   DevBuf<double2> part_, hist_pool_;
   DevBuf<double> lgain_;
   DevBuf<SplitResult> fbest_, lbest_;
@@ -3303,13 +2797,20 @@ class GpuBackend : public TrainBackend {
   DevBuf<int32_t> meta_i_, bag_;
   DevBuf<int8_t> mask_, mono_;
   DevBuf<unsigned int> ghmax_;
-  DevBuf<unsigned int> arrive_;  // split_kernel arrival counter (reset by the last block)
-  // SML_FUSED_SPLIT: 0 = reduce / find / choose launches, 1 = one split_kernel (slab reduce inside),
-  // 2 = reduce launch + split_kernel (find + choose), 3 = split_kernel<slab, no choose> + choose_part_kernel
-  // (A/B with the merged choose: 2.05 ms/iter vs 1.97 for 0 - 28 blocks cannot pull the slabs fast enough)
+  // Fusing reduce / find / choose into one launch (F blocks, slab reduce inside) measured slower on MI355X
+  // (2.05 vs 1.97 ms/iter: 28 blocks cannot pull the slabs fast enough; profiles/README, round 2)
   bool skip_last_ = true;  // SML_SKIP_LAST_SPLIT=0: histogram + search the last split's children too
-  int fused_split_ = 0;  // A/B on MI355X: 0 = 2.30 ms/iter, 2 = 2.41, 1 = 2.51 (profiles/README)
+  bool comm_world1_ = false;
   DevBuf<float> ghmax_partial_;
+  // event pairs around this tree's histogram allreduces (device comm time, summed when the tree is read)
+  std::vector<hipEvent_t> comm_ev_;
+  int comm_used_ = 0;
+  hipEvent_t ev_sync_ = nullptr;
+  void EnsureCommEvents() {
+    if (!comm_ev_.empty()) return;
+    comm_ev_.assign(2 * static_cast<size_t>(L_ + 1), nullptr);
+    for (hipEvent_t& e : comm_ev_) SML_HIP_CHECK(hipEventCreate(&e));
+  }
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)
   bool ghmax_valid_ = false;  // ghmax_ already holds this iteration's class-0 maxima (from grad_kernel)
   int pending_parts_ = 0;     // > 0: ghmax_ is the max over that many block partials, folded by root_init_kernel
@@ -3326,18 +2827,14 @@ class GpuBackend : public TrainBackend {
   DevBuf<float> ghbound_;  // a-priori max |g|, max h: the fused pass's fixed-point scale
   std::vector<int8_t> mask_host_;
   int part_grid_ = 1;
-  int part_rows_ = kPartRowsDefault, hist_unroll_ = kHistUnrollDefault, hist_threads_ = kHistThreads;
-  // SML_HIST_MODE: 0 = row-per-lane hist_kernel (default), 1 = feature-lane conflict-free hist_fl_kernel
-  // (A/B on MI355X: 2.28 vs 3.01 ms/iter - 16x the memory instructions per row cost more than the bank
-  // conflicts it removes; profiles/README)
-  int hist_mode_ = 0;
-  int hist_shape_ = 2, max_hist_blocks_ = kMaxHistBlocks / 2;
+  int part_rows_ = kPartRowsDefault;
+  // A feature-lane, bank-conflict-free histogram (lane = feature) measured slower on MI355X (2.28 vs 3.01
+  // ms/iter: 16x the memory instructions per row cost more than the conflicts it removes; profiles/README)
   DevBuf<uint8_t> blob_;
   DState* state_ = nullptr;   // two versions: choose_part_kernel reads one and writes the other
   DState* st_cur_ = nullptr;  // version the next hist / reduce / find / choose launches read
   DState* st_next_ = nullptr; // version whose cursor find_split_kernel zeroes (nullptr: none)
   int final_v_ = 0;           // version holding the finished tree's state
-  bool merged_choose_ = true; // SML_MERGED_CHOOSE=0: separate choose_kernel + part_kernel launches
   size_t n_ti_ = 0, n_tu_ = 0, n_td_ = 0, n_tl_ = 0;
   size_t off_td_ = 0, off_tl_ = 0, off_ti_ = 0, off_tu_ = 0, blob_bytes_ = 0;
   DevBuf<uint8_t> up_blob_;  // uploaded score-update tree: nodes | cat words | leaf values

@@ -7,13 +7,16 @@
 // binary search over that feature's upper bounds held in LDS, using the same
 // double comparisons as BinMapper::ValueToBin, so the result is bit-identical
 // with the host path. Categorical features use a dense category->bin table.
-// The bins are copied back into the Dataset (the training backends and the
-// validation scorer read them there); the encode itself replaces an
-// O(rows x features x log bins) host loop with one pass at HBM speed.
+// The bins stay in HBM (Dataset::dev): the HIP training backend adopts them
+// without a host round trip, and a host copy is only materialised when a host
+// consumer asks for it (Dataset::EnsureHostBins). The raw rows stream up in
+// chunks whose copies overlap the previous chunk's encode.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <vector>
 
@@ -141,29 +144,46 @@ class Encoder {
     m_.F = F; m_.stride = stride; m_.total_bounds = static_cast<int>(bounds.size());
   }
 
+  // Encode `nrows` raw rows into the device bin matrix at `dev_out` (row-major). The raw input streams
+  // up in ~64 MB chunks through two staging buffers: chunk c+1's host->device copy (copy stream) overlaps
+  // chunk c's encode (kernel stream); event pairs order slot reuse.
   template <class T>
-  void Encode(const T* rows, int64_t nrows, int ncols, uint8_t* host_out, hipStream_t s) {
+  void Encode(const T* rows, int64_t nrows, int ncols, uint8_t* dev_out, hipStream_t ks, hipStream_t cs) {
     if (nrows <= 0) return;
-    // chunks of ~64 MB of raw input through one device staging buffer
     const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / (static_cast<int64_t>(std::max(1, ncols)) * sizeof(T)));
     const int64_t cap = std::min(chunk, nrows);
-    in_.alloc(static_cast<size_t>(cap) * ncols * sizeof(T));
-    out_.alloc(static_cast<size_t>(cap) * m_.stride);
+    for (int b = 0; b < 2; ++b) in_[b].alloc(static_cast<size_t>(cap) * ncols * sizeof(T));
     const size_t lds = sizeof(double) * std::max(1, m_.total_bounds);
-    for (int64_t r0 = 0; r0 < nrows; r0 += chunk) {
+    int c = 0;
+    for (int64_t r0 = 0; r0 < nrows; r0 += chunk, ++c) {
+      const int slot = c & 1;
       const int64_t nr = std::min(chunk, nrows - r0);
-      SML_HIP_CHECK(hipMemcpyAsync(in_.get(), rows + r0 * ncols, static_cast<size_t>(nr) * ncols * sizeof(T),
-                                   hipMemcpyHostToDevice, s));
+      if (c >= 2) SML_HIP_CHECK(hipStreamWaitEvent(cs, done_[slot], 0));
+      SML_HIP_CHECK(hipMemcpyAsync(in_[slot].get(), rows + r0 * ncols, static_cast<size_t>(nr) * ncols * sizeof(T),
+                                   hipMemcpyHostToDevice, cs));
+      SML_HIP_CHECK(hipEventRecord(copied_[slot], cs));
+      SML_HIP_CHECK(hipStreamWaitEvent(ks, copied_[slot], 0));
       const int64_t words = nr * (m_.stride / 4);
       const int grid =
           static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(4096, (words + kEncThreads - 1) / kEncThreads)));
-      hipLaunchKernelGGL(encode_kernel<T>, dim3(grid), dim3(kEncThreads), lds, s, m_,
-                         reinterpret_cast<const T*>(in_.get()), nr, ncols, reinterpret_cast<uint32_t*>(out_.get()));
+      hipLaunchKernelGGL(encode_kernel<T>, dim3(grid), dim3(kEncThreads), lds, ks, m_,
+                         reinterpret_cast<const T*>(in_[slot].get()), nr, ncols,
+                         reinterpret_cast<uint32_t*>(dev_out + r0 * m_.stride));
       SML_HIP_CHECK(hipGetLastError());
-      SML_HIP_CHECK(hipMemcpyAsync(host_out + r0 * m_.stride, out_.get(), static_cast<size_t>(nr) * m_.stride,
-                                   hipMemcpyDeviceToHost, s));
-      SML_HIP_CHECK(hipStreamSynchronize(s));  // the staging buffers are reused by the next chunk
+      SML_HIP_CHECK(hipEventRecord(done_[slot], ks));
     }
+    SML_HIP_CHECK(hipStreamSynchronize(ks));
+  }
+
+  Encoder(const Encoder&) = delete;
+  Encoder& operator=(const Encoder&) = delete;
+  ~Encoder() {
+    for (hipEvent_t e : copied_) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : done_) if (e) (void)hipEventDestroy(e);
+  }
+  void MakeEvents() {
+    for (hipEvent_t& e : copied_) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : done_) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
 
  private:
@@ -171,24 +191,92 @@ class Encoder {
   DevBuf<int32_t> ints_;
   DevBuf<double> bounds_;
   DevBuf<uint16_t> cats_;
-  DevBuf<uint8_t> in_, out_;
+  DevBuf<uint8_t> in_[2];
+  hipEvent_t copied_[2] = {nullptr, nullptr}, done_[2] = {nullptr, nullptr};
 };
+
+// every row = the dataset's default row (each feature's zero bin)
+__global__ void fill_rows_kernel(uint4* __restrict__ out, int64_t nrows, int w4, uint4 a, uint4 b) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nrows * w4; t += (int64_t)gridDim.x * blockDim.x)
+    out[t] = (t % w4) == 0 ? a : b;
+}
+
+std::mutex& DevBinsMutex() {
+  static std::mutex m;
+  return m;
+}
+
+// The HBM bin matrix of `d` on `device`, current for every row pushed so far (uploads the host copy or
+// fills default rows the first time).
+void EnsureDeviceBins(Dataset* d, int device, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(DevBinsMutex());
+  if (d->dev && d->dev->device != device) { d->dev.reset(); d->dev_valid = false; }
+  if (!d->dev) {
+    auto db = std::make_shared<DeviceBins>();
+    db->device = device;
+    db->rows = static_cast<uint8_t*>(DevPoolAlloc(std::max<size_t>(16, static_cast<size_t>(d->num_data) * d->row_stride),
+                                                  &db->granted));
+    d->dev = db;
+    d->dev_valid = false;
+  }
+  if (d->dev_valid) return;
+  if (d->host_valid) {
+    SML_HIP_CHECK(hipMemcpyAsync(d->dev->rows, d->bins.data(), static_cast<size_t>(d->num_data) * d->row_stride,
+                                 hipMemcpyHostToDevice, s));
+  } else if (d->num_data > 0) {
+    if (d->row_stride % 16 != 0 || d->row_stride > 32 * 16) throw std::runtime_error("device bins: row stride");
+    const std::vector<uint8_t> z = d->DefaultRow();
+    // rows are 16 or 32 bytes for <= 32 features; wider rows repeat the fill per 16-byte word
+    const int w4 = d->row_stride / 16;
+    if (w4 > 2) {
+      std::vector<uint8_t> all(static_cast<size_t>(d->num_data) * d->row_stride);
+      for (int64_t i = 0; i < d->num_data; ++i) std::memcpy(&all[i * d->row_stride], z.data(), d->row_stride);
+      SML_HIP_CHECK(hipMemcpyAsync(d->dev->rows, all.data(), all.size(), hipMemcpyHostToDevice, s));
+      SML_HIP_CHECK(hipStreamSynchronize(s));
+    } else {
+      uint4 a, b = make_uint4(0, 0, 0, 0);
+      std::memcpy(&a, z.data(), 16);
+      if (w4 == 2) std::memcpy(&b, z.data() + 16, 16);
+      else b = a;
+      const int64_t words = d->num_data * w4;
+      const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(8192, (words + 255) / 256)));
+      hipLaunchKernelGGL(fill_rows_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint4*>(d->dev->rows),
+                         d->num_data, w4, a, b);
+      SML_HIP_CHECK(hipGetLastError());
+    }
+  }
+  SML_HIP_CHECK(hipStreamSynchronize(s));
+  d->dev_valid = true;
+}
 
 template <class T>
 void PushDenseDeviceImpl(Dataset* d, const T* rows, int64_t nrows, int num_cols, int64_t start, int device) {
   if (start < 0 || start + nrows > d->num_data) throw std::runtime_error("push_dense_gpu out of range");
   if (d->row_stride % 4 != 0) throw std::runtime_error("device bin encode needs a 4-byte aligned row stride");
   if (device >= 0) SML_HIP_CHECK(hipSetDevice(device));
-  hipStream_t s = nullptr;
-  SML_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  SML_HIP_CHECK(hipGetDevice(&device));
+  hipStream_t ks = nullptr, cs = nullptr;
+  SML_HIP_CHECK(hipStreamCreateWithFlags(&ks, hipStreamNonBlocking));
   try {
-    Encoder enc(d->ref, d->row_stride);
-    enc.Encode(rows, nrows, num_cols, d->bins.data() + start * d->row_stride, s);
+    SML_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    EnsureDeviceBins(d, device, ks);
+    uint8_t* dst = d->dev->rows + static_cast<size_t>(start) * d->row_stride;
+    {
+      Encoder enc(d->ref, d->row_stride);
+      enc.MakeEvents();
+      enc.Encode(rows, nrows, num_cols, dst, ks, cs);
+    }
+    // a host copy that already exists stays complete: mirror the pushed rows
+    if (d->host_valid)
+      SML_HIP_CHECK(hipMemcpy(d->bins.data() + static_cast<size_t>(start) * d->row_stride, dst,
+                              static_cast<size_t>(nrows) * d->row_stride, hipMemcpyDeviceToHost));
   } catch (...) {
-    (void)hipStreamDestroy(s);
+    (void)hipStreamDestroy(ks);
+    if (cs) (void)hipStreamDestroy(cs);
     throw;
   }
-  SML_HIP_CHECK(hipStreamDestroy(s));
+  SML_HIP_CHECK(hipStreamDestroy(ks));
+  SML_HIP_CHECK(hipStreamDestroy(cs));
 }
 
 }  // namespace
@@ -200,6 +288,19 @@ void DatasetPushDenseDevice(Dataset* d, const double* rows, int64_t nrows, int n
 void DatasetPushDenseDeviceF32(Dataset* d, const float* rows, int64_t nrows, int num_cols, int64_t start,
                                int device) {
   PushDenseDeviceImpl(d, rows, nrows, num_cols, start, device);
+}
+
+void DatasetDownloadBins(const Dataset& d, uint8_t* host) {
+  if (!d.dev || !d.dev_valid) throw std::runtime_error("dataset has no device bins");
+  int cur = -1;
+  SML_HIP_CHECK(hipGetDevice(&cur));
+  if (cur != d.dev->device) SML_HIP_CHECK(hipSetDevice(d.dev->device));
+  SML_HIP_CHECK(hipMemcpy(host, d.dev->rows, static_cast<size_t>(d.num_data) * d.row_stride, hipMemcpyDeviceToHost));
+  if (cur != d.dev->device) SML_HIP_CHECK(hipSetDevice(cur));
+}
+
+DeviceBins::~DeviceBins() {
+  if (rows) DevPoolFree(rows, granted);
 }
 
 }  // namespace sml

@@ -39,6 +39,8 @@ struct PyComm {
 PYBIND11_MODULE(_gbdt, m) {
   m.doc() = "MI355X-native gradient boosting engine (HIP kernels + RCCL)";
   m.def("gpu_available", &GpuAvailable);
+  // a failed / timed-out collective: fit() re-raises it on every rank (never "early termination")
+  py::register_exception<CommError>(m, "CommError", PyExc_RuntimeError);
 
   py::class_<DatasetReference, std::shared_ptr<DatasetReference>>(m, "DatasetReference")
       .def_static("from_sample",
@@ -114,8 +116,10 @@ PYBIND11_MODULE(_gbdt, m) {
            py::arg("X"), py::arg("start"), py::arg("device") = -1,
            "K1: encode dense rows into bins on the MI355X (bit-identical with push_dense)")
       .def_property_readonly("bins", [](PyDataset& p) {
+        p.d->EnsureHostBins();
         return py::array_t<uint8_t>({p.d->num_data, static_cast<int64_t>(p.d->row_stride)}, p.d->bins.data());
       })
+      .def_property_readonly("device_resident", [](const PyDataset& p) { return p.d->dev && p.d->dev_valid; })
       .def("push_csr",
            [](PyDataset& p, I64 indptr, I32 indices, F64 values, int64_t start) {
              const int64_t nrows = indptr.shape(0) - 1;
@@ -140,6 +144,7 @@ PYBIND11_MODULE(_gbdt, m) {
       .def_property_readonly("num_features", [](const PyDataset& p) { return p.d->ref.num_total_features; })
       .def("get_label", [](const PyDataset& p) { return py::array_t<float>(p.d->label.size(), p.d->label.data()); })
       .def("get_bins", [](const PyDataset& p) {
+        p.d->EnsureHostBins();
         return py::array_t<uint8_t>({p.d->num_data, static_cast<int64_t>(p.d->row_stride)}, p.d->bins.data());
       });
 
@@ -155,7 +160,11 @@ PYBIND11_MODULE(_gbdt, m) {
     c.c = std::make_shared<HostComm>(rank, world, [fn](double* buf, int64_t n) {
       py::gil_scoped_acquire acq;
       py::array_t<double> a({n}, {sizeof(double)}, buf, py::none());
-      fn(a);
+      try {
+        fn(a);
+      } catch (py::error_already_set& e) {  // gloo / TCP failure of the host collective (peer died, timeout)
+        throw CommError(std::string("host allreduce failed: ") + e.what());
+      }
     });
     return c;
   });
@@ -264,7 +273,7 @@ PYBIND11_MODULE(_gbdt, m) {
         TrainStats* s = b.stats();
         if (s) {
           d["grad_ms"] = s->grad_ms; d["hist_ms"] = s->hist_ms; d["split_ms"] = s->split_ms;
-          d["partition_ms"] = s->partition_ms; d["score_ms"] = s->score_ms; d["comm_ms"] = s->comm_ms;
+          d["partition_ms"] = s->partition_ms; d["score_ms"] = s->score_ms; d["comm_ms"] = s->comm_ms; d["comm_calls"] = s->comm_calls;
           d["trees"] = s->trees;
           d["device_tree_ms"] = s->device_tree_ms; d["device_score_ms"] = s->device_score_ms;
           d["device_mem_mb"] = s->device_mem_mb;

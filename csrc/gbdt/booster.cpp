@@ -96,27 +96,26 @@ void Booster::InitTraining() {
   backend_->Init(train_.get(), cfg_, num_tree_per_iter_);
   const int64_t n = train_->num_data;
   const int K = num_tree_per_iter_;
-  std::vector<double> scores(static_cast<size_t>(n) * K, 0.0);
+  init_scores_.assign(K, 0.0);
   if (!train_->init_score.empty()) {
     if (static_cast<int64_t>(train_->init_score.size()) != n * K)
       throw std::runtime_error("init_score has wrong size");
-    scores = train_->init_score;
-  }
-  init_scores_.assign(K, 0.0);
-  if (train_->init_score.empty() && cfg_.boost_from_average && objective_->params().kind != kObjLambdarank &&
-      objective_->params().kind != kObjCustom) {
-    for (int k = 0; k < K; ++k) {
-      double v = objective_->BoostFromScore(k);
-      if (comm_ && comm_->world() > 1) {
-        double buf[2] = {v * n, static_cast<double>(n)};
-        comm_->AllReduceHost(buf, 2);
-        v = buf[1] > 0 ? buf[0] / buf[1] : 0.0;
+    backend_->SetScores(train_->init_score);
+  } else {
+    if (cfg_.boost_from_average && objective_->params().kind != kObjLambdarank &&
+        objective_->params().kind != kObjCustom) {
+      for (int k = 0; k < K; ++k) {
+        double v = objective_->BoostFromScore(k);
+        if (comm_ && comm_->world() > 1) {
+          double buf[2] = {v * n, static_cast<double>(n)};
+          comm_->AllReduceHost(buf, 2);
+          v = buf[1] > 0 ? buf[0] / buf[1] : 0.0;
+        }
+        init_scores_[k] = v;
       }
-      init_scores_[k] = v;
-      for (int64_t i = 0; i < n; ++i) scores[k * n + i] += v;
     }
+    backend_->FillScores(init_scores_, n);  // constant start scores, written where the scores live
   }
-  backend_->SetScores(scores);
   bag_rng_.seed(cfg_.bagging_seed);
   feat_rng_.seed(cfg_.feature_fraction_seed);
   drop_rng_.seed(cfg_.drop_seed);
@@ -124,6 +123,7 @@ void Booster::InitTraining() {
 }
 
 void Booster::AddValidData(std::shared_ptr<Dataset> valid, const std::string& name) {
+  valid->EnsureHostBins();  // validation scores are kept on the host
   const int K = num_tree_per_iter_;
   std::vector<double> s(static_cast<size_t>(valid->num_data) * K, 0.0);
   if (!valid->init_score.empty()) s = valid->init_score;

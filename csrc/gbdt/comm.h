@@ -9,10 +9,17 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 namespace sml {
+
+// A collective failed or timed out (a peer died, a link broke, ranks diverged). Training must fail on
+// every rank instead of ending early with a truncated model (Python: synapseml_amd._gbdt.CommError).
+struct CommError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 class Comm {
  public:
@@ -25,8 +32,10 @@ class Comm {
   virtual void AllReduceDeviceF32(float* buf, int64_t n, void* stream) = 0;
   virtual void AllReduceDeviceF64(double* buf, int64_t n, void* stream) = 0;
   virtual bool is_device() const { return false; }
-  // raise if an asynchronous collective failed (checked once per tree)
+  // raise CommError if an asynchronous collective failed; polled while the backend waits on the device
   virtual void Check() {}
+  // unblock collectives stuck on a dead peer (RCCL: ncclCommAbort); the communicator is unusable after
+  virtual void Abort() {}
 };
 
 class HostComm : public Comm {

@@ -178,9 +178,10 @@ class P2pComm : public Comm {
   }
   void Check() override {
     if (err_ && __atomic_load_n(err_, __ATOMIC_ACQUIRE))
-      throw std::runtime_error("p2p allreduce timed out waiting for a peer (a rank died or diverged)");
+      throw CommError("p2p allreduce timed out waiting for a peer (a rank died or diverged)");
     base_->Check();
   }
+  void Abort() override { base_->Abort(); }
 
  private:
   bool Use(int64_t bytes) const { return active_ && world_ > 1 && bytes <= cap_; }

@@ -65,9 +65,10 @@ class RcclComm : public Comm {
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   bool is_device() const override { return true; }
+  // (a world-1 communicator still runs every collective: that is how the one-GPU tests execute this path)
   void AllReduceHost(double* buf, int64_t n) override {
     // small host reductions (root sums, init scores): stage through the device
-    if (world_ <= 1) return;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
     double* d = nullptr;
     SML_HIP_CHECK(hipMalloc(&d, sizeof(double) * n));
     SML_HIP_CHECK(hipMemcpy(d, buf, sizeof(double) * n, hipMemcpyHostToDevice));
@@ -77,23 +78,26 @@ class RcclComm : public Comm {
     SML_HIP_CHECK(hipFree(d));
   }
   void AllReduceDeviceF32(float* buf, int64_t n, void* stream) override {
-    if (world_ <= 1) return;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
     SML_NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, comm_, static_cast<hipStream_t>(stream)));
   }
-  // Called once per tree by the backend (RCCL async-error polling): a peer that died or
-  // a broken link surfaces as an exception on every rank instead of a collective that never returns.
+  // Polled by the backend while it waits for a tree (RCCL async-error polling): a peer that
+  // died or a broken link surfaces as a CommError on every rank instead of a collective that never returns.
   void Check() override {
-    if (!comm_ || world_ <= 1) return;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
     ncclResult_t async = ncclSuccess;
     if (ncclCommGetAsyncError(comm_, &async) != ncclSuccess) return;
     if (async != ncclSuccess && async != ncclInProgress) {
-      (void)ncclCommAbort(comm_);
-      comm_ = nullptr;
-      throw std::runtime_error(std::string("RCCL communicator failed: ") + ncclGetErrorString(async));
+      Abort();
+      throw CommError(std::string("RCCL communicator failed: ") + ncclGetErrorString(async));
     }
   }
+  void Abort() override {
+    if (comm_) (void)ncclCommAbort(comm_);  // makes kernels of pending collectives return
+    comm_ = nullptr;
+  }
   void AllReduceDeviceF64(double* buf, int64_t n, void* stream) override {
-    if (world_ <= 1) return;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
     SML_NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm_, static_cast<hipStream_t>(stream)));
   }
 

@@ -171,6 +171,7 @@ void Config::Set(const std::string& key_in, const std::string& value_in) {
     else if (v == "feature_parallel") tree_learner = "feature";
   }
   else if (key == "top_k") top_k = I();
+  else if (key == "time_out") time_out = I();
   else if (key == "gpu_device_id") gpu_device_id = I();
   else if (key == "use_quantized_grad") use_quantized_grad = B();
   // unknown keys are kept in `raw` (echoed in the model) and otherwise ignored,
@@ -338,7 +339,7 @@ std::string Config::ToParametersSection() const {
       "zero_as_missing", "categorical_feature", "num_class", "is_unbalance", "scale_pos_weight",
       "sigmoid", "boost_from_average", "alpha", "fair_c", "poisson_max_delta_step",
       "tweedie_variance_power", "max_position", "lambdarank_norm", "label_gain", "eval_at",
-      "num_machines", "gpu_device_id", "use_quantized_grad"};
+      "num_machines", "gpu_device_id", "use_quantized_grad", "time_out"};
   for (const auto& kv : raw) {
     bool k = false;
     for (const char* n : known) if (kv.first == n) { k = true; break; }

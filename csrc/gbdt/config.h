@@ -96,6 +96,7 @@ struct Config {
   int num_machines = 1;
   std::string tree_learner = "serial";
   int top_k = 20;
+  int time_out = 120;  // minutes a collective may block before the job fails (LightGBM `time_out`)
   // gpu
   int gpu_device_id = -1;
   bool use_quantized_grad = false;

@@ -13,6 +13,8 @@
 #include <cmath>
 #include <cstdint>
 #include <limits>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -90,17 +92,35 @@ struct DatasetReference {
   int row_stride() const { return std::max(16, ((num_inner() + 15) / 16) * 16); }
 };
 
+// Row-major bin matrix resident in HBM (num_data x row_stride bytes), written by the K1 device encoder
+// and adopted by the HIP training backend without a host round trip (bin_encode.hip).
+struct DeviceBins {
+  int device = -1;
+  uint8_t* rows = nullptr;
+  size_t granted = 0;
+  ~DeviceBins();
+};
+
 struct Dataset {
   DatasetReference ref;
   int64_t num_data = 0;
   int row_stride = 4;                 // bytes per row in `bins`
-  std::vector<uint8_t> bins;          // num_data * row_stride
+  // Host copy of the bin matrix (num_data * row_stride). Datasets built by the device encoder keep their
+  // bins only in HBM (`dev`); the host copy is materialised on first use by a host consumer (CPU backend,
+  // validation scoring, get_bins) - call EnsureHostBins() before touching `bins`.
+  mutable std::vector<uint8_t> bins;
+  mutable bool host_valid = false;    // `bins` holds every pushed row
+  std::shared_ptr<DeviceBins> dev;    // device copy, current when dev_valid
+  bool dev_valid = false;
   std::vector<float> label;
   std::vector<float> weight;          // empty = unweighted
   std::vector<double> init_score;     // empty or num_data * num_tree_per_iteration
   std::vector<int32_t> query_boundaries;  // ranking: size num_queries+1
 
   void Init(const DatasetReference& r, int64_t n);
+  // host bins: download the device copy, or allocate rows filled with every feature's zero bin
+  void EnsureHostBins() const;
+  std::vector<uint8_t> DefaultRow() const;
   // Push a block of dense rows (row-major, num_cols doubles each) at `start`.
   void PushDense(const double* rows, int64_t nrows, int num_cols, int64_t start);
   void PushDenseF32(const float* rows, int64_t nrows, int num_cols, int64_t start);
@@ -111,8 +131,10 @@ struct Dataset {
   inline uint8_t Bin(int64_t row, int inner) const { return bins[row * row_stride + inner]; }
 };
 
-// K1 on the device (bin_encode.hip): same bins as PushDense / PushDenseF32.
+// K1 on the device (bin_encode.hip): same bins as PushDense / PushDenseF32; the rows stay in HBM.
 void DatasetPushDenseDevice(Dataset* d, const double* rows, int64_t nrows, int num_cols, int64_t start, int device);
 void DatasetPushDenseDeviceF32(Dataset* d, const float* rows, int64_t nrows, int num_cols, int64_t start, int device);
+// device -> host copy of a device-resident bin matrix (bin_encode.hip)
+void DatasetDownloadBins(const Dataset& d, uint8_t* host);
 
 }  // namespace sml

@@ -17,22 +17,37 @@ namespace sml {
 
 constexpr int kWave = 64;
 
+// Caching device allocator shared by every engine buffer of the process (dev_pool.cpp).
+void* DevPoolAlloc(size_t bytes, size_t* granted);
+void DevPoolFree(void* p, size_t granted);
+void DevPoolTrim();
+struct DevPoolStats {
+  size_t cached_bytes, live_bytes;
+  int64_t hits, misses;
+};
+DevPoolStats DevPoolGetStats();
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  size_t granted = 0;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() { if (p) (void)hipFree(p); }
+  ~DevBuf() { release(); }
   void alloc(size_t count) {
     if (count <= n && p) return;
-    if (p) (void)hipFree(p);
-    p = nullptr;
+    release();
+    if (count) p = static_cast<T*>(DevPoolAlloc(sizeof(T) * count, &granted));
     n = count;
-    if (count) SML_HIP_CHECK(hipMalloc(&p, sizeof(T) * count));
   }
-  void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+  void release() {
+    if (p) DevPoolFree(p, granted);
+    p = nullptr;
+    n = 0;
+    granted = 0;
+  }
   T* get() const { return p; }
 };
 

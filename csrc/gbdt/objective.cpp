@@ -188,6 +188,7 @@ double Objective::BoostFromScore(int class_id) const {
     case kObjMulticlassOVA:
     case kObjCrossEntropy: {
       double sl = 0, sw = 0;
+#pragma omp parallel for schedule(static) reduction(+ : sl, sw)
       for (int64_t i = 0; i < n; ++i) {
         double y = p_.kind == kObjMulticlassOVA ? (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0)
                                                : (p_.kind == kObjBinary ? (label_[i] > 0 ? 1.0 : 0.0) : label_[i]);
@@ -201,6 +202,7 @@ double Objective::BoostFromScore(int class_id) const {
     }
     case kObjMulticlass: {
       double sl = 0, sw = 0;
+#pragma omp parallel for schedule(static) reduction(+ : sl, sw)
       for (int64_t i = 0; i < n; ++i) { sl += (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0) * W(i); sw += W(i); }
       double p = sw > 0 ? sl / sw : 1.0 / p_.num_class;
       return std::log(std::max(kEpsilon, p));

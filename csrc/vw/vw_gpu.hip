@@ -296,7 +296,7 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
 }
 
 void GpuSgd::AllReduceAverage(void* comm, int world) {
-  if (world <= 1 || !comm) return;
+  if (world < 1 || !comm) return;  // a world-1 communicator still runs the collective (one-GPU tests)
   hipStream_t s = impl_->stream;
   ncclComm_t c = static_cast<ncclComm_t>(comm);
   const uint64_t nf = impl_->nw * 2;

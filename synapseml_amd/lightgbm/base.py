@@ -47,7 +47,11 @@ def _features(df: DataFrame, col: str, matrix_type: str):
     if isinstance(c, np.ndarray) and c.ndim == 2:
         if matrix_type == "sparse":
             return "sparse", as_csr(c)
-        return "dense", np.ascontiguousarray(c, dtype=np.float64)
+        # float32 feature matrices stay float32 end to end (the native push and the K1 device encoder take
+        # them as is, and ValueToBin compares in double either way): an 11M x 28 float64 copy would be a
+        # 2.5 GB host pass inside fit
+        dt = np.float32 if c.dtype == np.float32 else np.float64
+        return "dense", np.ascontiguousarray(c, dtype=dt)
     sparse = matrix_type == "sparse" or (matrix_type == "auto" and any(isinstance(v, SparseVector) for v in c[:10]))
     if sparse:
         return "sparse", as_csr(c)
@@ -87,6 +91,16 @@ def _sample_dense(kind, data, idx) -> np.ndarray:
         a, b = indptr[r], indptr[r + 1]
         out[i, indices[a:b]] = values[a:b]
     return out
+
+
+def _injected_iteration_crash() -> Optional[int]:
+    """Test-only fault injection: ``SML_FAULT_INJECT="<rank>:crash_iter=<k>"`` makes that rank's
+    process exit at boosting iteration k, while its peers wait in the histogram allreduce."""
+    for item in filter(None, os.environ.get("SML_FAULT_INJECT", "").split(",")):
+        r, _, kind = item.partition(":")
+        if r.strip() == str(D.rank()) and kind.strip().startswith("crash_iter="):
+            return int(kind.strip().split("=", 1)[1])
+    return None
 
 
 class LightGBMBase(Estimator, LightGBMParams):
@@ -173,6 +187,9 @@ class LightGBMBase(Estimator, LightGBMParams):
         sb.appendParamValueIfNotThere("num_iterations", self.getNumIterations())
         sb.appendParamValueIfNotThere("learning_rate", self.getLearningRate())
         sb.appendParamValueIfNotThere("num_machines", num_machines)
+        # `timeout` (seconds, the reference's network timeout) bounds how long a collective may block before
+        # the engine aborts the communicator and fails the fit on every rank (native `time_out` is minutes)
+        sb.appendParamValueIfNotThere("time_out", max(1, int(-(-float(self.getTimeout()) // 60))))
         sb.appendParamValueIfNotThere("verbosity", self.getVerbosity())
         sb.appendParamValueIfNotThere("early_stopping_round", self.getEarlyStoppingRound())
         sb.appendParamListIfNotThere("categorical_feature", cat_idx)
@@ -499,7 +516,10 @@ class LightGBMBase(Estimator, LightGBMParams):
         num_iter = self.getNumIterations()
         ck_every = self.getCheckpointInterval() if self.getCheckpointDir() else 0
         finished = False
+        crash_at = _injected_iteration_crash()
         while not finished and it < num_iter:
+            if crash_at is not None and it == crash_at:
+                os._exit(19)  # test-only (SML_FAULT_INJECT="<rank>:crash_iter=<k>"): this rank dies mid-fit
             if delegate is not None:
                 delegate.beforeTrainIteration(batch_index, D.rank(), it, log, None, nb, has_valid)
                 new_lr = delegate.getLearningRate(batch_index, D.rank(), it, log, None, lr)
@@ -519,7 +539,11 @@ class LightGBMBase(Estimator, LightGBMParams):
                     finished = nb.update(grad, hess)
                 else:
                     finished = nb.update()
-            except RuntimeError as e:  # early termination (TrainUtils.scala:89-95)
+            except RuntimeError as e:
+                # a failed or timed-out collective (peer died, link broke, ranks diverged) fails the job on
+                # every rank; anything else ends this task's training early (TrainUtils.scala:89-95)
+                if isinstance(e, native.gbdt().CommError):
+                    raise
                 log.warning("training stopped early on this task: %s", e)
                 finished = True
             train_res = dict(nb.eval(0)) if provide_train and not finished else None

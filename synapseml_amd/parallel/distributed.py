@@ -168,6 +168,7 @@ def gbdt_comm(use_gpu: bool, shared_device: bool = False):
         return None
     from ..ops import native
 
+    shared_device = shared_device or os.environ.get("SML_GBDT_SHARED_DEVICE") == "1"
     g = native.gbdt()
     key = ("shared" if use_gpu and shared_device else "rccl" if use_gpu else "host", world_size())
     if key in _comm_cache:

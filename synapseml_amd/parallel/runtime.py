@@ -74,7 +74,8 @@ def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, par
 
 
 def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_workers: Optional[int] = None,
-                   backend: Optional[str] = None, use_gpu: bool = False, timeout_s: float = 1200.0) -> List[Any]:
+                   backend: Optional[str] = None, use_gpu: bool = False, timeout_s: float = 1200.0,
+                   fail_fast: bool = True) -> List[Any]:
     """Run ``fn(partition_df, rank, world)`` in ``num_workers`` processes.
 
     Partitions are grouped contiguously onto workers (coalesce). Returns the
@@ -117,7 +118,7 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
                         st = pickle.load(f)[0]  # written by our own worker process
                     if st != "ok":
                         failed = failed or (r, "task error")
-            if failed or _time.monotonic() > deadline:
+            if (failed and fail_fast) or _time.monotonic() > deadline:
                 break
             _time.sleep(0.05)
         for p in procs:
@@ -127,6 +128,19 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
                 if p.is_alive():
                     p.kill()
                     p.join()
+        if failed is not None and not fail_fast:
+            # every rank ran to its own end: report what each one saw
+            errs = []
+            for r in range(world):
+                path = os.path.join(d, f"result_{r}.pkl")
+                if not os.path.exists(path):
+                    errs.append(f"worker {r}: exit code {procs[r].exitcode}, no result")
+                    continue
+                with open(path, "rb") as f:
+                    st, val = pickle.load(f)  # written by our own worker process
+                if st != "ok":
+                    errs.append(f"worker {r}: {val}")
+            raise RuntimeError("partition tasks failed: " + " | ".join(errs))
         if failed is not None:
             r, why = failed
             path = os.path.join(d, f"result_{r}.pkl")
@@ -161,7 +175,9 @@ class _FitTask:
         return model if rank == 0 else None
 
 
-def distributed_fit(estimator, df: DataFrame, num_workers: Optional[int] = None, use_gpu: bool = False):
+def distributed_fit(estimator, df: DataFrame, num_workers: Optional[int] = None, use_gpu: bool = False,
+                    **kw):
     """Data-parallel ``fit`` across worker processes; returns rank 0's model
-    (only the main worker returns the model, BasePartitionTask.scala:450-461)."""
-    return run_partitions(_FitTask(estimator), df, num_workers=num_workers, use_gpu=use_gpu)[0]
+    (only the main worker returns the model, BasePartitionTask.scala:450-461).
+    Extra keyword arguments go to :func:`run_partitions` (timeout_s, fail_fast)."""
+    return run_partitions(_FitTask(estimator), df, num_workers=num_workers, use_gpu=use_gpu, **kw)[0]

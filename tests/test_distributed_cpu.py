@@ -71,6 +71,27 @@ def test_rank_failure_aborts_fast(monkeypatch, kind):
     assert time.monotonic() - t0 < 120
 
 
+def test_rank_death_mid_fit_fails_every_rank(monkeypatch):
+    """A rank that dies inside the boosting loop must fail the fit on the surviving ranks with a CommError
+    (the histogram allreduce cannot complete) - never a warning plus a truncated model."""
+    import time
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((4000, 6))
+    y = (X[:, 0] > 0).astype(float)
+    df = DataFrame({"features": X, "label": y}, num_partitions=2)
+    monkeypatch.setenv("SML_FAULT_INJECT", "1:crash_iter=3")
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError) as ei:
+        # fail_fast=False: the driver lets the survivor run to its own end, so what it raised is reported
+        distributed_fit(LightGBMClassifier(deviceType="cpu", numIterations=20, numThreads=1, timeout=60.0), df,
+                        num_workers=2, timeout_s=300, fail_fast=False)
+    msg = str(ei.value)
+    assert "worker 1: exit code 19" in msg, msg[-2000:]
+    assert "worker 0: CommError" in msg, msg[-2000:]
+    assert time.monotonic() - t0 < 200
+
+
 def test_empty_partition_rank_still_joins(monkeypatch):
     monkeypatch.setenv("SML_FAULT_INJECT", "1:empty")
     out = run_partitions(_allreduce_task, DataFrame({"x": np.arange(8.0)}, num_partitions=2), num_workers=2)

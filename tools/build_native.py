@@ -45,6 +45,7 @@ MODULES = {
             "backend_cpu.cpp",
             "booster.cpp",
             "comm_rccl.cpp",
+            "dev_pool.cpp",
             "bindings.cpp",
             "backend_gpu.hip",
             "predict_gpu.hip",
