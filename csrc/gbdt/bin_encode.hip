@@ -18,6 +18,7 @@
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "dataset.h"
@@ -175,6 +176,19 @@ class Encoder {
     SML_HIP_CHECK(hipStreamSynchronize(ks));
   }
 
+  // Encode rows already resident in HBM (DeviceRows): one launch over all rows.
+  template <class T>
+  void EncodeResident(const T* dev_rows, int64_t nrows, int ncols, uint8_t* dev_out, hipStream_t ks) {
+    if (nrows <= 0) return;
+    const size_t lds = sizeof(double) * std::max(1, m_.total_bounds);
+    const int64_t words = nrows * (m_.stride / 4);
+    const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(8192, (words + kEncThreads - 1) / kEncThreads)));
+    hipLaunchKernelGGL(encode_kernel<T>, dim3(grid), dim3(kEncThreads), lds, ks, m_, dev_rows, nrows, ncols,
+                       reinterpret_cast<uint32_t*>(dev_out));
+    SML_HIP_CHECK(hipGetLastError());
+    SML_HIP_CHECK(hipStreamSynchronize(ks));
+  }
+
   Encoder(const Encoder&) = delete;
   Encoder& operator=(const Encoder&) = delete;
   ~Encoder() {
@@ -279,7 +293,75 @@ void PushDenseDeviceImpl(Dataset* d, const T* rows, int64_t nrows, int num_cols,
   SML_HIP_CHECK(hipStreamDestroy(cs));
 }
 
+template <class T>
+void PushResidentImpl(Dataset* d, DeviceRows* src, int64_t start) {
+  src->Wait();
+  const int64_t nrows = src->nrows;
+  if (start < 0 || start + nrows > d->num_data) throw std::runtime_error("push_device_rows out of range");
+  if (d->row_stride % 4 != 0) throw std::runtime_error("device bin encode needs a 4-byte aligned row stride");
+  SML_HIP_CHECK(hipSetDevice(src->device));
+  hipStream_t ks = nullptr;
+  SML_HIP_CHECK(hipStreamCreateWithFlags(&ks, hipStreamNonBlocking));
+  try {
+    EnsureDeviceBins(d, src->device, ks);
+    uint8_t* dst = d->dev->rows + static_cast<size_t>(start) * d->row_stride;
+    {
+      Encoder enc(d->ref, d->row_stride);
+      enc.EncodeResident(static_cast<const T*>(src->ptr), nrows, src->ncols, dst, ks);
+    }
+    if (d->host_valid)
+      SML_HIP_CHECK(hipMemcpy(d->bins.data() + static_cast<size_t>(start) * d->row_stride, dst,
+                              static_cast<size_t>(nrows) * d->row_stride, hipMemcpyDeviceToHost));
+  } catch (...) {
+    (void)hipStreamDestroy(ks);
+    throw;
+  }
+  SML_HIP_CHECK(hipStreamDestroy(ks));
+}
+
 }  // namespace
+
+// ---------------------------------------------------------------- DeviceRows
+DeviceRows::DeviceRows(const void* host, int64_t nrows_, int ncols_, int elem_bytes_, int device_)
+    : nrows(nrows_), ncols(ncols_), elem_bytes(elem_bytes_), device(device_) {
+  if (elem_bytes != 4 && elem_bytes != 8) throw std::runtime_error("DeviceRows: float32 or float64 rows");
+  if (device < 0) SML_HIP_CHECK(hipGetDevice(&device));
+  SML_HIP_CHECK(hipSetDevice(device));
+  const size_t bytes = static_cast<size_t>(nrows) * ncols * elem_bytes;
+  ptr = DevPoolAlloc(std::max<size_t>(bytes, 16), &granted);
+  // the copy runs on its own thread and stream so the caller (row sampling, bin boundaries) overlaps it
+  worker = std::thread([this, host, bytes]() {
+    try {
+      SML_HIP_CHECK(hipSetDevice(device));
+      hipStream_t s = nullptr;
+      SML_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      const size_t chunk = 64ull << 20;
+      const char* h = static_cast<const char*>(host);
+      for (size_t off = 0; off < bytes; off += chunk)
+        SML_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(ptr) + off, h + off, std::min(chunk, bytes - off),
+                                     hipMemcpyHostToDevice, s));
+      SML_HIP_CHECK(hipStreamSynchronize(s));
+      SML_HIP_CHECK(hipStreamDestroy(s));
+    } catch (const std::exception& e) {
+      error = e.what();
+    }
+  });
+}
+
+void DeviceRows::Wait() {
+  if (worker.joinable()) worker.join();
+  if (!error.empty()) throw std::runtime_error("DeviceRows upload failed: " + error);
+}
+
+DeviceRows::~DeviceRows() {
+  if (worker.joinable()) worker.join();
+  if (ptr) DevPoolFree(ptr, granted);
+}
+
+void DatasetPushDeviceRows(Dataset* d, DeviceRows* src, int64_t start) {
+  if (src->elem_bytes == 4) PushResidentImpl<float>(d, src, start);
+  else PushResidentImpl<double>(d, src, start);
+}
 
 void DatasetPushDenseDevice(Dataset* d, const double* rows, int64_t nrows, int num_cols, int64_t start, int device) {
   PushDenseDeviceImpl(d, rows, nrows, num_cols, start, device);

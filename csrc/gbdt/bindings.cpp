@@ -34,6 +34,11 @@ struct PyComm {
   std::shared_ptr<Comm> c;
 };
 
+struct PyDeviceRows {
+  py::object keep;                // the host rows; released only after the copy thread has joined
+  std::shared_ptr<DeviceRows> r;  // destroyed first (members go in reverse order): joins the copy
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_gbdt, m) {
@@ -76,6 +81,21 @@ PYBIND11_MODULE(_gbdt, m) {
       .def("upper_bounds", [](const DatasetReference& r, int f) { return r.mappers.at(f).upper_bounds; })
       .def("value_to_bin", [](const DatasetReference& r, int f, double v) { return r.mappers.at(f).ValueToBin(v); });
 
+  // K1 input staging: the raw rows go up on a native thread while Python samples / builds bin boundaries
+  py::class_<PyDeviceRows>(m, "DeviceRows")
+      .def(py::init([](py::array X, int device) {
+             auto b = X.request();
+             if (b.ndim != 2) throw std::runtime_error("rows must be 2-D");
+             const bool f32 = b.format == py::format_descriptor<float>::format();
+             PyDeviceRows p;
+             p.keep = f32 ? py::array(py::cast<F32>(X)) : py::array(py::cast<F64>(X));  // C-contiguous, kept alive
+             auto ab = p.keep.cast<py::array>().request();
+             p.r = std::make_shared<DeviceRows>(ab.ptr, ab.shape[0], static_cast<int>(ab.shape[1]), f32 ? 4 : 8, device);
+             return p;
+           }),
+           py::arg("X"), py::arg("device") = -1)
+      .def("wait", [](PyDeviceRows& p) { py::gil_scoped_release rel; p.r->Wait(); })
+      .def_property_readonly("num_rows", [](const PyDeviceRows& p) { return p.r->nrows; });
   py::class_<PyDataset>(m, "Dataset")
       .def(py::init([](std::shared_ptr<DatasetReference> ref, int64_t n) {
         PyDataset p;
@@ -115,6 +135,13 @@ PYBIND11_MODULE(_gbdt, m) {
            },
            py::arg("X"), py::arg("start"), py::arg("device") = -1,
            "K1: encode dense rows into bins on the MI355X (bit-identical with push_dense)")
+      .def("push_device_rows",
+           [](PyDataset& p, PyDeviceRows& rows, int64_t start) {
+             py::gil_scoped_release rel;
+             DatasetPushDeviceRows(p.d.get(), rows.r.get(), start);
+           },
+           py::arg("rows"), py::arg("start") = 0,
+           "K1 on rows already uploaded by DeviceRows (waits for the upload, encodes in HBM)")
       .def_property_readonly("bins", [](PyDataset& p) {
         p.d->EnsureHostBins();
         return py::array_t<uint8_t>({p.d->num_data, static_cast<int64_t>(p.d->row_stride)}, p.d->bins.data());

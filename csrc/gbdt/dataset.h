@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -134,6 +135,24 @@ struct Dataset {
 // K1 on the device (bin_encode.hip): same bins as PushDense / PushDenseF32; the rows stay in HBM.
 void DatasetPushDenseDevice(Dataset* d, const double* rows, int64_t nrows, int num_cols, int64_t start, int device);
 void DatasetPushDenseDeviceF32(Dataset* d, const float* rows, int64_t nrows, int num_cols, int64_t start, int device);
+// Raw dense rows (float32 / float64, row-major) uploaded to HBM on a background thread, so the caller can
+// sample rows and build bin boundaries while the copy runs; DatasetPushDeviceRows then bin-encodes them
+// in place (no second transfer). Keeps `owner` (e.g. the numpy array) alive until the copy is done.
+struct DeviceRows {
+  DeviceRows(const void* host, int64_t nrows, int ncols, int elem_bytes, int device);
+  ~DeviceRows();
+  DeviceRows(const DeviceRows&) = delete;
+  DeviceRows& operator=(const DeviceRows&) = delete;
+  void Wait();  // copy finished (raises if it failed)
+  int64_t nrows;
+  int ncols, elem_bytes, device;
+  void* ptr = nullptr;
+  size_t granted = 0;
+  std::thread worker;
+  std::string error;
+};
+void DatasetPushDeviceRows(Dataset* d, DeviceRows* src, int64_t start);
+
 // device -> host copy of a device-resident bin matrix (bin_encode.hip)
 void DatasetDownloadBins(const Dataset& d, uint8_t* host);
 

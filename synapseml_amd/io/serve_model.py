@@ -84,21 +84,37 @@ class DistributedServing:
                    "--max-batch-size", str(max_batch_size), "--reuse-port", "--worker-id", str(w)]
             self.procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                                text=True))
-        # each worker prints one "serving ..." line once it listens
-        deadline = time.monotonic() + startup_timeout
-        for p in self.procs:
-            while True:
-                line = p.stdout.readline()
-                if line.startswith("serving"):
-                    break
-                if not line and p.poll() is not None or time.monotonic() > deadline:
-                    self.stop()
-                    raise RuntimeError(f"serving worker failed to start: {line!r}")
-        # keep draining each worker's output (a full pipe would block a worker that logs)
+        # each worker prints one "serving ..." line once it listens. Its output is read on a thread that
+        # feeds a queue, so a worker that hangs silently (model load, GPU init) cannot block the parent past
+        # the deadline; the same thread keeps draining the pipe afterwards (a full pipe blocks a worker)
+        import queue as _queue
         import threading as _threading
 
-        for p in self.procs:
-            _threading.Thread(target=lambda f=p.stdout: [None for _ in f], daemon=True).start()
+        ready: "_queue.Queue" = _queue.Queue()
+
+        def _pump(w, f):
+            announced = False
+            for line in f:
+                if not announced and line.startswith("serving"):
+                    announced = True
+                    ready.put((w, line))
+            if not announced:
+                ready.put((w, None))  # exited without listening
+
+        for w, p in enumerate(self.procs):
+            _threading.Thread(target=_pump, args=(w, p.stdout), daemon=True).start()
+        deadline = time.monotonic() + startup_timeout
+        pending = set(range(num_workers))
+        while pending:
+            try:
+                w, line = ready.get(timeout=max(0.0, deadline - time.monotonic()))
+            except _queue.Empty:
+                self.stop()
+                raise RuntimeError(f"serving workers {sorted(pending)} did not start within {startup_timeout}s")
+            if line is None:
+                self.stop()
+                raise RuntimeError(f"serving worker {w} exited before listening (code {self.procs[w].poll()})")
+            pending.discard(w)
 
     @property
     def address(self) -> str:
@@ -124,6 +140,31 @@ class DistributedServing:
         self.stop()
 
 
+def _worker_gpus(spec: Optional[str]) -> Optional[List[int]]:
+    """Device ids the serving workers are spread over (one per worker, round robin): ``--gpus``, else
+    SML_SERVE_GPUS (a count), else the visible devices - counted without initialising a GPU in the
+    parent (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES, else torch's device count, which on this image
+    does not initialise the runtime). None when there is no GPU."""
+    import os
+
+    if spec:
+        return [int(x) for x in spec.split(",") if x.strip()]
+    n = int(os.environ.get("SML_SERVE_GPUS", "0"))
+    if n:
+        return list(range(n))
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            return list(range(len([x for x in v.split(",") if x.strip()])))
+    try:
+        import torch
+
+        n = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001 - no torch / no ROCm: CPU workers
+        n = 0
+    return list(range(n)) if n else None
+
+
 def main(argv=None) -> None:
     from ..core.serialize import load_stage
 
@@ -138,13 +179,11 @@ def main(argv=None) -> None:
     ap.add_argument("--workers", type=int, default=1, help="worker processes on the port (one per GPU)")
     ap.add_argument("--reuse-port", action="store_true", help="bind with SO_REUSEPORT (set for workers)")
     ap.add_argument("--worker-id", default=None)
+    ap.add_argument("--gpus", default=None, help="comma-separated device ids for the workers (default: all visible)")
     a = ap.parse_args(argv)
     if a.workers > 1:
-        import os
-
-        n_dev = int(os.environ.get("SML_SERVE_GPUS", "0")) or None
         srv_d = DistributedServing(a.model, a.workers, a.port, a.host, a.input_cols, a.output_cols, a.api,
-                                   a.max_batch_size, gpus=list(range(n_dev)) if n_dev else None)
+                                   a.max_batch_size, gpus=_worker_gpus(a.gpus))
         print(f"serving {a.workers} workers at {srv_d.address}", flush=True)
         done = threading.Event()
         signal.signal(signal.SIGTERM, lambda *_: done.set())

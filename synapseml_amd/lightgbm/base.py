@@ -283,18 +283,26 @@ class LightGBMBase(Estimator, LightGBMParams):
             return None
         meta = None
         if D.rank() == 0:
-            p = os.path.join(d, "latest.json")
-            if os.path.exists(p):
-                with open(p) as f:
-                    meta = json.load(f)
-                if fingerprint is not None and meta.get("fingerprint") != fingerprint:
-                    log.warning("checkpoint %s was written by a different job (params or data differ); "
-                                "starting fresh", p)
-                    meta = None
-                else:
-                    with open(os.path.join(d, meta["model"])) as f:
-                        meta["model_str"] = f.read()
-        return D.broadcast_object(meta, 0)
+            # rank 0 always reaches the broadcast: a failed read travels to every rank as an error marker,
+            # so all ranks raise together instead of the others waiting in the broadcast forever
+            try:
+                p = os.path.join(d, "latest.json")
+                if os.path.exists(p):
+                    with open(p) as f:
+                        meta = json.load(f)
+                    if fingerprint is not None and meta.get("fingerprint") != fingerprint:
+                        log.warning("checkpoint %s was written by a different job (params or data differ); "
+                                    "starting fresh", p)
+                        meta = None
+                    else:
+                        with open(os.path.join(d, meta["model"])) as f:
+                            meta["model_str"] = f.read()
+            except Exception as e:  # noqa: BLE001 - reported on every rank below
+                meta = {"__error__": f"{type(e).__name__}: {e}"}
+        meta = D.broadcast_object(meta, 0)
+        if meta is not None and "__error__" in meta:
+            raise RuntimeError(f"cannot resume from checkpoint directory {d!r}: {meta['__error__']}")
+        return meta
 
     def _ckpt_write(self, model_str: str, batch: int, iteration: int, complete: bool) -> None:
         d = self.getCheckpointDir()
@@ -337,7 +345,8 @@ class LightGBMBase(Estimator, LightGBMParams):
             if delegate is not None:
                 delegate.beforeTrainBatch(bi, log, batch, booster)
             booster = self._train_batch(batch, model_str, bi, num_class)
-            model_str = booster.modelStr
+            # the model text is only needed to continue into the next batch or for a checkpoint
+            model_str = booster.modelStr if (bi + 1 < len(batches) or self.getCheckpointDir()) else None
             self._resume_done = 0
             if self.getCheckpointDir():
                 self._ckpt_write(model_str, bi, self.getNumIterations(), True)
@@ -377,6 +386,9 @@ class LightGBMBase(Estimator, LightGBMParams):
         names = self._slot_names(df, ncols)
         params = self._train_params(num_class, cat_idx, world)
         use_gpu = self.getDeviceType() == "gpu" and native.gpu_available()
+        # K1 input staging: a large dense partition starts its host->HBM copy now, on a native thread, so it
+        # overlaps the row sampling and bin-boundary construction below (the encode then runs in HBM)
+        upload = g.DeviceRows(data) if (kind == "dense" and use_gpu and n >= (1 << 16)) else None
         # --- bin boundaries (reference dataset)
         t0 = time.perf_counter()
         ref_bytes = self.getReferenceDataset()
@@ -406,7 +418,8 @@ class LightGBMBase(Estimator, LightGBMParams):
         if delegate is not None:
             delegate.beforeGenerateTrainDataset(batch_index, D.rank(), None, df.schema, log, params)
         t0 = time.perf_counter()
-        train = self._build_dataset(g, ref, df, kind, data, n, num_class)
+        train = self._build_dataset(g, ref, df, kind, data, n, num_class, upload=upload)
+        upload = None  # the raw rows' HBM copy is released (back to the device pool)
         m.mark("dataset_creation_ms", (time.perf_counter() - t0) * 1e3)
         if delegate is not None:
             delegate.afterGenerateTrainDataset(batch_index, D.rank(), None, df.schema, log, params)
@@ -458,12 +471,14 @@ class LightGBMBase(Estimator, LightGBMParams):
             idx = np.sort(rng.choice(n, size=cnt, replace=False))
         return _sample_dense(kind, data, idx)
 
-    def _build_dataset(self, g, ref, df: DataFrame, kind, data, n, num_class):
+    def _build_dataset(self, g, ref, df: DataFrame, kind, data, n, num_class, upload=None):
         ds = g.Dataset(ref, n)
         if kind == "dense":
             # K1: large dense partitions are bin-encoded on the MI355X (bit-identical with the host encoder)
             on_gpu = n >= (1 << 16) and self.getDeviceType() == "gpu" and native.gpu_available()
-            if on_gpu:
+            if upload is not None:
+                ds.push_device_rows(upload, 0)
+            elif on_gpu:
                 ds.push_dense_gpu(data, 0)
             else:
                 chunk = 1 << 20

@@ -73,13 +73,56 @@ class CertifiedEventClient:
         with urllib.request.urlopen(req, timeout=timeout) as r:
             return r.status
 
+    # events are posted by one daemon thread from a bounded queue: telemetry never adds latency to a
+    # fit/transform (serving mini-batches included); when the endpoint is slow and the queue is full,
+    # new events are dropped rather than blocking the caller
+    _queue = None
+    _lock = __import__("threading").Lock()
+    dropped = 0
+
+    @staticmethod
+    def _worker(q) -> None:
+        while True:
+            item = q.get()
+            try:
+                CertifiedEventClient.log_to_certified_events(*item)
+            except Exception:  # noqa: BLE001 - telemetry failures are never surfaced to the workload
+                pass
+            finally:
+                q.task_done()
+
+    @classmethod
+    def _enqueue(cls, item) -> None:
+        import queue
+        import threading
+
+        with cls._lock:
+            if cls._queue is None:
+                cls._queue = queue.Queue(maxsize=1024)
+                threading.Thread(target=cls._worker, args=(cls._queue,), daemon=True,
+                                 name="sml-certified-events").start()
+        try:
+            cls._queue.put_nowait(item)
+        except queue.Full:
+            cls.dropped += 1
+
+    @staticmethod
+    def flush(timeout: float = 5.0) -> None:
+        """Wait (up to `timeout`) until queued events were posted (tests, process exit)."""
+        import time
+
+        q = CertifiedEventClient._queue
+        end = time.monotonic() + timeout
+        while q is not None and q.unfinished_tasks and time.monotonic() < end:
+            time.sleep(0.01)
+
     @staticmethod
     def sink(payload: Dict) -> None:
         if payload.get("method") not in ("fit", "transform"):
             return
         attrs = {k: str(v) for k, v in payload.items() if k in ("className", "method", "modelUid", "errorType")}
-        CertifiedEventClient.log_to_certified_events(CertifiedEventClient.feature_name(payload),
-                                                     f"{payload.get('className')}.{payload.get('method')}", attrs)
+        CertifiedEventClient._enqueue((CertifiedEventClient.feature_name(payload),
+                                       f"{payload.get('className')}.{payload.get('method')}", attrs))
 
     @staticmethod
     def install(force: bool = False) -> bool:

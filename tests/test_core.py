@@ -196,3 +196,26 @@ def test_certified_events_sink():
     finally:
         remove_event_sink(seen.append)
         srv.shutdown()
+
+
+def test_certified_event_sink_never_blocks(monkeypatch):
+    """telemetry posts run on a background thread from a bounded queue, so a slow endpoint adds
+    no latency to transform()."""
+    import time
+
+    from synapseml_amd.utils.fabric import CertifiedEventClient
+
+    posted = []
+
+    def slow_post(feature, activity, attrs, endpoint=None, timeout=5.0):
+        time.sleep(0.5)
+        posted.append(activity)
+        return 200
+
+    monkeypatch.setattr(CertifiedEventClient, "log_to_certified_events", staticmethod(slow_post))
+    t0 = time.perf_counter()
+    for _ in range(3):
+        CertifiedEventClient.sink({"method": "transform", "className": "X", "module": "synapseml_amd.stages.x"})
+    assert time.perf_counter() - t0 < 0.2
+    CertifiedEventClient.flush(5.0)
+    assert posted == ["X.transform"] * 3

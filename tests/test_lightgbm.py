@@ -420,3 +420,27 @@ def test_malformed_native_model_string_raises(mutate):
     LightGBMClassificationModel.loadNativeModelFromString(good)  # the untouched string loads
     with pytest.raises((RuntimeError, ValueError, IndexError)):
         LightGBMClassificationModel.loadNativeModelFromString(mutate(good)).transform(df)
+
+
+def test_checkpoint_unreadable_raises_clearly(tmp_path):
+    """a broken checkpoint (latest.json names a missing model file) raises on every rank
+    instead of leaving the non-zero ranks waiting in the broadcast."""
+    import json as _json
+
+    import numpy as np
+    import pytest
+
+    from synapseml_amd.core import DataFrame
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    ck = tmp_path / "ck"
+    ck.mkdir()
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((500, 4))
+    df = DataFrame({"features": X, "label": (X[:, 0] > 0).astype(float)})
+    est = LightGBMClassifier(numIterations=3, deviceType="cpu", checkpointDir=str(ck), resumeFromCheckpoint=True)
+    fp = est._ckpt_fingerprint(df)
+    (ck / "latest.json").write_text(_json.dumps({"model": "gone.txt", "batch": 0, "iteration": 2,
+                                                 "complete": False, "fingerprint": fp}))
+    with pytest.raises(RuntimeError, match="cannot resume"):
+        est.fit(df)
