@@ -56,6 +56,42 @@ PYBIND11_MODULE(_nn, m) {
      pybind11::arg("bias"), pybind11::arg("res"), pybind11::arg("out_scale"), pybind11::arg("out_shift"),
      pybind11::arg("y2"), pybind11::arg("geom"), pybind11::arg("relu"), pybind11::arg("prologue_relu"),
      pybind11::arg("dtype"), pybind11::arg("stream"), pybind11::arg("kernel") = 0);
+  // conv: [] or [H, W, C, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, OH, OW] (implicit im2col A)
+  m.def("gemm", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int batch, int64_t lda, int64_t ldb,
+                   int64_t ldc, int64_t sa, int64_t sb, int64_t sc, int trans_a, int trans_b, float alpha, float beta,
+                   uintptr_t bias, uintptr_t cmat, int64_t ldcm, int64_t scm, int act, int dtype, uintptr_t stream,
+                   std::vector<int> conv, int64_t stride_bias) {
+    GemmArgs g;
+    if (!conv.empty()) {
+      if (conv.size() != 13) throw std::invalid_argument("conv geometry: H,W,C,R,S,sh,sw,ph,pw,dh,dw,OH,OW");
+      g.conv = 1;
+      g.H = conv[0]; g.W = conv[1]; g.C = conv[2]; g.R = conv[3]; g.S = conv[4]; g.stride_h = conv[5];
+      g.stride_w = conv[6]; g.pad_h = conv[7]; g.pad_w = conv[8]; g.dil_h = conv[9]; g.dil_w = conv[10];
+      g.OH = conv[11]; g.OW = conv[12];
+    }
+    g.stride_bias = stride_bias;
+    g.a = P<const void>(a); g.b = P<const void>(b); g.c = P<void>(c);
+    g.M = M; g.N = N; g.K = K; g.batch = batch;
+    g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.stride_a = sa; g.stride_b = sb; g.stride_c = sc;
+    g.trans_a = trans_a; g.trans_b = trans_b; g.alpha = alpha; g.beta = beta;
+    g.bias = P<const float>(bias); g.cmat = P<const void>(cmat); g.ldcm = ldcm; g.stride_cm = scm; g.act = act;
+    const int rc = GemmMfma(g, dtype, P<void>(stream));
+    if (rc != 0) throw std::runtime_error("gemm_mfma failed (rc=" + std::to_string(rc) + ")");
+  }, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"), pybind11::arg("M"), pybind11::arg("N"),
+     pybind11::arg("K"), pybind11::arg("batch"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"),
+     pybind11::arg("sa"), pybind11::arg("sb"), pybind11::arg("sc"), pybind11::arg("trans_a"), pybind11::arg("trans_b"),
+     pybind11::arg("alpha"), pybind11::arg("beta"), pybind11::arg("bias"), pybind11::arg("cmat"), pybind11::arg("ldcm"),
+     pybind11::arg("scm"), pybind11::arg("act"), pybind11::arg("dtype"), pybind11::arg("stream"),
+     pybind11::arg("conv") = std::vector<int>(), pybind11::arg("stride_bias") = 0);
+  m.def("group_conv", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t bias, uintptr_t res, std::vector<int> g,
+                         int groups, int relu, int dtype, uintptr_t stream) {
+    if (g.size() != 15) throw std::invalid_argument("geometry: B,H,W,C,Cout,R,S,sh,sw,ph,pw,dh,dw,OH,OW");
+    GroupConvArgs a{P<const void>(x), P<const void>(w), P<void>(y), P<const float>(bias), P<const void>(res),
+                    g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14],
+                    groups, relu};
+    const int rc = GroupConv(a, dtype, P<void>(stream));
+    if (rc != 0) throw std::runtime_error("group_conv failed (rc=" + std::to_string(rc) + ")");
+  });
   m.def("softmax_rows", [](uintptr_t x, int rows, int cols, uintptr_t y, uintptr_t amax, uintptr_t stream) {
     SoftmaxRows(P<const float>(x), rows, cols, P<float>(y), P<int64_t>(amax), P<void>(stream));
   });

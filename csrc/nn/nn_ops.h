@@ -40,6 +40,45 @@ struct ConvArgs {
 constexpr int kConvStem = 1;  // ConvArgs::kernel: the packed few-channel stem form (C = 4, R = S = 8)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);
 int ConvMfma(const ConvArgs& a, int dtype, void* stream);
+// K17: batched GEMM with fused epilogue (gemm_mfma.hip), dtype 0 fp32 / 1 fp16 / 2 bf16:
+//   C[b] = act(alpha * op(A[b]) * op(B[b]) + beta * (bias[n] | Cin[b]))
+// op(A) is [M][K] (trans_a = 0, lda >= K) or A stored [K][M] (trans_a = 1, lda >= M);
+// op(B) is [K][N] stored [K][N] (trans_b = 0, ldb >= N) or stored [N][K] (trans_b = 1, ldb >= K).
+// Batch strides are in elements (0 = broadcast). Returns 0, or < 0 when the shape is not supported.
+struct GemmArgs {
+  const void* a = nullptr;
+  const void* b = nullptr;
+  void* c = nullptr;
+  int M = 0, N = 0, K = 0, batch = 1;
+  int64_t lda = 0, ldb = 0, ldc = 0;
+  int64_t stride_a = 0, stride_b = 0, stride_c = 0;
+  int trans_a = 0, trans_b = 0;
+  float alpha = 1.f, beta = 1.f;
+  const float* bias = nullptr;   // [N] (scaled by beta); batch z reads bias + z * stride_bias
+  int64_t stride_bias = 0;
+  const void* cmat = nullptr;    // [M][N] additive input, ldcm, batch stride stride_cm (scaled by beta)
+  int64_t ldcm = 0, stride_cm = 0;
+  int act = 0;                   // 0 none, 1 relu
+  // conv = 1: A is the implicit im2col of an NHWC input (any channel count, the 3-channel stem included):
+  // row m = (b, oh, ow) of [B, OH, OW], column k = (r, s, c) of [R, S, Cg]; the element is
+  // a[((b * H + ih) * W + iw) * C + c] (+ batch stride: a group's channel offset), zero in the padding.
+  // K must equal R * S * Cg; M = B * OH * OW; C is the input's pixel stride (all channels).
+  int conv = 0;
+  int H = 0, W = 0, C = 0, R = 1, S = 1, stride_h = 1, stride_w = 1, pad_h = 0, pad_w = 0, dil_h = 1, dil_w = 1;
+  int OH = 0, OW = 0;
+};
+int GemmMfma(const GemmArgs& g, int dtype, void* stream);
+// Direct grouped / depthwise NHWC convolution (conv_direct.hip): x [B,H,W,C], w [Cout][R][S][C/groups],
+// y [B,OH,OW,Cout]; fp32 accumulation; y = conv + bias, relu (1: before the residual add, 2: after), + res.
+struct GroupConvArgs {
+  const void* x;
+  const void* w;
+  void* y;
+  const float* bias;
+  const void* res;
+  int B, H, W, C, Cout, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, OH, OW, groups, relu;
+};
+int GroupConv(const GroupConvArgs& a, int dtype, void* stream);
 // fp32 row softmax (y may be null) and argmax (amax may be null)
 void SoftmaxRows(const float* x, int rows, int cols, float* y, int64_t* amax, void* stream);
 

@@ -588,26 +588,48 @@ OPS["Hardmax"] = _softmax_like("hard")
 
 
 # ------------------------------------------------------------------ linear algebra
+def _mfma_gemm_ok(rt, *ts) -> bool:
+    """K17 on the device: float operands of one dtype on the GPU with the _nn module loaded."""
+    from ..ops import gemm as G
+
+    return getattr(getattr(rt, "session", None), "_nn", None) is not None and G.supported(*ts)
+
+
 @op("MatMul")
 def _matmul(rt, at, x):
     a, b = _promote(x[0], x[1])
-    return [torch.matmul(a, b)]
+    if _mfma_gemm_ok(rt, a, b) and a.dim() >= 1 and b.dim() >= 1:
+        from ..ops import gemm as G
+
+        return [G.matmul(a, b)]  # one batched MFMA launch (broadcast operands read with batch stride 0)
+    return [torch.matmul(a, b)]  # host / integer graphs
 
 
 @op("Gemm")
 def _gemm(rt, at, x):
     a, b = _promote(x[0], x[1])
     if at.get("transA", 0):
-        a = a.t()
+        a = a.t()  # a view: the GEMM reads the transposed layout in place
     if at.get("transB", 0):
         b = b.t()
     alpha, beta = at.get("alpha", 1.0), at.get("beta", 1.0)
+    c = x[2] if len(x) > 2 and x[2] is not None else None
+    if _mfma_gemm_ok(rt, a, b) and a.dim() == 2 and b.dim() == 2:
+        from ..ops import gemm as G
+
+        N = b.shape[1]
+        act = at.get("__act", 0)
+        if c is not None and c.numel() == N and (c.dim() == 1 or c.shape[0] == 1):
+            return [G.gemm(a, b, bias=c, alpha=alpha, beta=beta, relu=act == 1)]  # FC bias in the epilogue
+        return [G.gemm(a, b, c=c, alpha=alpha, beta=beta if c is not None else 0.0, relu=act == 1)]
     y = torch.matmul(a, b)
     if alpha != 1.0:
         y = y * alpha
-    if len(x) > 2 and x[2] is not None:
-        c = x[2].to(y.device, y.dtype)
+    if c is not None:
+        c = c.to(y.device, y.dtype)
         y = y + (c * beta if beta != 1.0 else c)
+    if at.get("__act", 0) == 1:
+        y = torch.relu(y)
     return [y]
 
 

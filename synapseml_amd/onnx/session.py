@@ -219,6 +219,14 @@ class InferenceSession:
         for n in nodes:
             if id(n) in drop:
                 continue
+            if n.op_type == "Gemm":
+                # Gemm -> Relu: the ReLU runs in the MFMA GEMM's epilogue (K17)
+                nxt = sole_consumer(n.outputs[0])
+                if nxt is not None and nxt.op_type == "Relu" and not n.attrs.get("__act", 0):
+                    g = Node("Gemm", list(n.inputs), [nxt.outputs[0]], dict(n.attrs, __act=1), n.name)
+                    drop.add(id(nxt))
+                    out_nodes.append(g)
+                    continue
             if n.op_type == "Conv" and n.inputs[1] in self._consts and len(self._consts[n.inputs[1]].shape) == 4:
                 fused = Node("_FusedConv", list(n.inputs[:3]) + [""] * (3 - len(n.inputs[:3])), list(n.outputs),
                              dict(n.attrs), n.name)
@@ -755,9 +763,35 @@ def _stem_conv(rt, at, inp, w, b, res, act):
                        relu=2 if act == 1 else 0, res=res, kernel=1)
 
 
+def _general_conv_ok(rt, at, inp, w) -> bool:
+    """2-D convs outside the tiled MFMA kernel's domain (any channel count, grouped / depthwise) that the
+    GEMM-with-im2col or direct NHWC kernels run (ops.conv.conv2d_nhwc_general)."""
+    return (rt.session._nn is not None and inp.is_cuda and inp.dim() == 4 and w.dim() == 4
+            and inp.dtype in (torch.float32, torch.float16, torch.bfloat16) and inp.dtype == w.dtype
+            and at.get("__act", 0) in (0, 1) and inp.numel() * inp.element_size() < 2 ** 31
+            and inp.shape[1] % at.get("group", 1) == 0)
+
+
+def _packed_weight(rt, w):
+    """[Cout, Cg, R, S] -> contiguous [Cout, R, S, Cg], packed once per weight tensor."""
+    cache = rt.session.__dict__.setdefault("_wpack", {})
+    key = (w.data_ptr(), tuple(w.shape), w.dtype)
+    wp = cache.get(key)
+    if wp is None:
+        wp = cache[key] = w.permute(0, 2, 3, 1).contiguous()
+    return wp
+
+
 def _fused_conv_fallback(rt, at, inp, w, b, res, pro, act):
     if pro is not None:  # prologue outside the kernel (fallback path)
         inp = _affine_act(rt, inp, pro[0], pro[1], None, 1 if at.get("__pro_relu", 1) else 0, 0.0)
+    if _general_conv_ok(rt, at, inp, w):
+        from ..ops.conv import conv2d_nhwc_general
+
+        nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+        return [conv2d_nhwc_general(inp, _packed_weight(rt, w), w.shape[2], w.shape[3], strides,
+                                    (pb[0], pb[1], pe[0], pe[1]), dil, groups=at.get("group", 1), bias=b,
+                                    relu=2 if act == 1 else 0, res=res)]
     nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
     inp, pad = _sym_pad(inp, pb, pe)
     f = {1: torch.nn.functional.conv1d, 2: torch.nn.functional.conv2d, 3: torch.nn.functional.conv3d}[nd]

@@ -72,3 +72,43 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
 
 
 __all__ = ["supported", "pack_weight", "conv2d_nhwc", "out_hw"]
+
+
+def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),
+                        dil=(1, 1), groups: int = 1, bias: Optional[torch.Tensor] = None, relu: int = 0,
+                        res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Convolutions the tiled implicit-GEMM kernel does not take: any channel count (the 3-channel stem,
+    C % 64 != 0) and grouped / depthwise layers. ``x`` [B, C, H, W] channels_last, ``wp`` packed
+    [Cout, R, S, C / groups]. groups == 1, or groups whose per-group GEMM is at least 16 wide: the MFMA
+    GEMM with an implicit-im2col A operand (one batch entry per group); otherwise (depthwise, narrow
+    groups) the direct NHWC kernel. ``relu``: 0 none, 1 before the residual add, 2 after it."""
+    B, C, H, W = x.shape
+    cout = wp.shape[0]
+    cg, ng = C // groups, cout // groups
+    if wp.shape != (cout, r, s, cg) or not wp.is_contiguous() or wp.dtype != x.dtype:
+        raise ValueError(f"packed weight must be [Cout, {r}, {s}, {cg}] {x.dtype}")
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    oh, ow = out_hw(H, W, r, s, stride, pad, dil)
+    y = torch.empty((B, cout, oh, ow), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    if res is not None:
+        res = res.to(x.dtype).contiguous(memory_format=torch.channels_last)
+    b32 = None if bias is None else bias.reshape(-1).to(x.device, torch.float32).contiguous()
+    nn = native.load("_nn")
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    K = r * s * cg
+    if groups == 1 or (ng >= 16 and K >= 16):
+        M = B * oh * ow
+        # the GEMM epilogue adds the residual before its ReLU: relu=1 with a residual adds it afterwards
+        act = 1 if relu else 0
+        cm = None if (relu == 1 and res is not None) else res
+        nn.gemm(x.data_ptr(), wp.data_ptr(), y.data_ptr(), M, ng, K, groups, 0, K, cout, cg, ng * K, ng, 0, 1, 1.0, 1.0,
+                _ptr(b32), _ptr(cm), cout, ng, act, _DT[x.dtype], stream,
+                [H, W, C, r, s, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], oh, ow], ng)
+        if res is not None and cm is None:  # relu before the residual add (rare): add it after
+            y.add_(res)
+        return y
+    nn.group_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(b32), _ptr(res),
+                  [B, H, W, C, cout, r, s, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], oh, ow],
+                  groups, int(relu), _DT[x.dtype], stream)
+    return y

@@ -67,7 +67,7 @@ MODULES = {
     ),
     "_nn": (
         "csrc/nn",
-        ["nn_bindings.cpp", "nn_ops.hip", "conv_mfma.hip"],
+        ["nn_bindings.cpp", "nn_ops.hip", "conv_mfma.hip", "gemm_mfma.hip", "conv_direct.hip"],
         [],
     ),
 }

@@ -1,8 +1,8 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gbdt_gpu.py tests/test_comm_gpu.py > gpurun_out/t1.log 2>&1
+timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_onnx.py tests/test_conv_mfma.py -m gpu > gpurun_out/t3.log 2>&1
 rc=$?
-tail -3 gpurun_out/t1.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 5 --warmup 1 > gpurun_out/b1.log 2>&1
-rc=$?; tail -1 gpurun_out/b1.log; exit $rc
+tail -15 gpurun_out/t3.log
+timeout -k 10 600 python tools/bench_onnx.py --batches 128 --precisions fp32,fp16 > gpurun_out/onnx1.log 2>&1
+tail -8 gpurun_out/onnx1.log
+exit $rc
