@@ -197,6 +197,37 @@ PYBIND11_MODULE(_vw, m) {
              return probs;
            },
            py::arg("lines"), py::arg("learn") = true)
+      // one record per line in the shape of the learner's prediction type (VowpalWabbitPrediction.scala:18-101):
+      // scalar (prediction, confidence) | scalars [..] | multiclass int | action_scores / action_probs
+      // [(action, value)] | pdf [(left, right, pdf_value)] | action_pdf_value (action, pdf_value)
+      .def("predict_text_structured",
+           [](VW& vw, const std::vector<std::string>& lines, bool learn) {
+             const std::string type = vw.OutputPredictionType();
+             py::list out;
+             for (const auto& line : lines) {
+               Example ex = vw.ParseLine(line);
+               if (learn) vw.Learn(ex); else vw.Predict(ex);
+               if (type == "prediction_type_t::pdf") {
+                 py::list segs;
+                 for (auto& sg : ex.pdf_segments) segs.append(py::make_tuple(sg[0], sg[1], sg[2]));
+                 out.append(segs);
+               } else if (type == "prediction_type_t::action_pdf_value") {
+                 out.append(py::make_tuple(ex.cats_action, ex.cats_pdf_value));
+               } else if (type == "prediction_type_t::multiclass") {
+                 out.append(static_cast<int>(ex.pred));
+               } else if (type == "prediction_type_t::scalars") {
+                 out.append(ex.scores);
+               } else if (type == "prediction_type_t::action_probs" || type == "prediction_type_t::action_scores") {
+                 py::list l;
+                 for (auto& ap : ex.action_probs) l.append(py::make_tuple(ap.first, ap.second));
+                 out.append(l);
+               } else {
+                 out.append(py::make_tuple(ex.pred, 0.f));
+               }
+             }
+             return py::make_tuple(type, out);
+           },
+           py::arg("lines"), py::arg("learn") = false)
       .def("end_pass", &VW::EndPass)
       .def("perform_remaining_passes", &VW::PerformRemainingPasses)
       .def("save_model", [](const VW& vw) { return py::bytes(vw.SaveModel()); })

@@ -108,7 +108,7 @@ void VW::ParseArgs(const std::string& args) {
     else if (k == "--cb_adf") cb_adf_ = true;
     else if (k == "--cb_explore_adf") { cb_adf_ = true; cb_explore_ = true; }
     else if (k == "--cb_type") cb_type_ = val();
-    else if (k == "--epsilon") epsilon_ = std::stof(val());
+    else if (k == "--epsilon") { epsilon_ = std::stof(val()); epsilon_set_ = true; }
     else if (k == "--passes") passes_ = std::stoi(val());
     else if (k == "-t" || k == "--testonly") testonly_ = true;
     else if (k == "--holdout_off") holdout_off_ = true;
@@ -117,15 +117,37 @@ void VW::ParseArgs(const std::string& args) {
     else if (k == "--normalized") { normalized = true; any_update_flag = true; }
     else if (k == "--invariant") { invariant = true; any_update_flag = true; }
     else if (k == "--ngram") ngram_ = std::stoi(val());
-    else if (k == "--cats" || k == "--bfgs" || k == "--lda" || k == "--ksvm")
-      throw std::runtime_error("VW option " + k + " is not supported by this engine");
+    else if (k == "--cats_pdf") { cats_k_ = std::stoi(val()); cats_sample_ = false; }
+    else if (k == "--cats") { cats_k_ = std::stoi(val()); cats_sample_ = true; }
+    else if (k == "--bandwidth") bandwidth_ = std::stof(val());
+    else if (k == "--min_value") min_value_ = std::stof(val());
+    else if (k == "--max_value") max_value_ = std::stof(val());
     else if (k == "--cache_file" || k == "--span_server" || k == "--span_server_port" || k == "--unique_id" ||
              k == "--total" || k == "--node" || k == "--random_seed" || k == "--readable_model" || k == "-f" ||
-             k == "-i" || k == "--initial_regressor" || k == "--min_value" || k == "--max_value" ||
-             k == "--bandwidth" || k == "--quantile_loss" || k == "--data" || k == "-d") {
-      if (!has_inline) next();
+             k == "-i" || k == "--initial_regressor" || k == "--quantile_loss" || k == "--data" || k == "-d" ||
+             k == "--final_regressor" || k == "--cb_force_legacy" || k == "--save_resume") {
+      if (!has_inline && k != "--cb_force_legacy" && k != "--save_resume") next();
+    } else if (k == "--quiet" || k == "--no_stdin" || k == "-k" || k == "--kill_cache" || k == "--audit" ||
+               k == "--predict_only_model" || k == "--save_per_pass") {
+      // front-end / IO flags without an effect on learning
+    } else if (k == "--bfgs" || k == "--lda" || k == "--ksvm" || k == "--nn" || k == "--boosting" ||
+               k == "--cb_explore" || k == "--cb" || k == "--ccb_explore_adf" || k == "--slates" || k == "--bootstrap" ||
+               k == "--search" || k == "--lrq" || k == "--stage_poly" || k == "--active" || k == "--multilabel_oaa" ||
+               k == "--ect" || k == "--log_multi" || k == "--recall_tree" || k == "--plt" || k == "--dsjson" ||
+               k == "--json" || k == "--ftrl" || k == "--coin" || k == "--pistol" || k == "--OjaNewton" ||
+               k == "--marginal" || k == "--explore_eval" || k == "--cbify" || k == "--warm_cb") {
+      throw std::runtime_error("VW option " + k + " is not supported by this engine");
+    } else {
+      // a typo or an unknown reduction must not silently train a different model
+      throw std::runtime_error("unrecognised VW option '" + tok[i] + "'");
     }
-    // flags without values (quiet, no_stdin, -k, audit, holdout_off, ...) are accepted
+  }
+  if (cats_k_ > 0) {
+    if (cats_k_ < 2) throw std::runtime_error("--cats / --cats_pdf needs at least 2 discrete actions");
+    if (!(max_value_ > min_value_)) throw std::runtime_error("CATS needs --min_value < --max_value");
+    if (!(bandwidth_ > 0.f)) throw std::runtime_error("CATS needs --bandwidth > 0");
+    cats_depth_ = 0;
+    while ((1 << cats_depth_) < cats_k_) ++cats_depth_;
   }
   if (any_update_flag) {
     adaptive_ = adaptive; normalized_ = normalized; invariant_ = invariant;
@@ -278,7 +300,98 @@ void VW::Update(const Example& ex, uint64_t offset, float pred, float label, flo
 }
 
 // ----------------------------------------------------------------- learners
+// ----------------------------------------------------------------- CATS
+int VW::CatsPredictLeaf(const Example& ex) const {
+  int node = 0;
+  const int leaves = 1 << cats_depth_;
+  for (int d = 0; d < cats_depth_; ++d) {
+    // right only when its subtree holds a real action (K need not be a power of two)
+    const int right = 2 * node + 2;
+    int first_leaf = right;
+    while (first_leaf < leaves - 1) first_leaf = 2 * first_leaf + 1;
+    const bool right_ok = first_leaf - (leaves - 1) < cats_k_;
+    const float sc = Dot(ex, CatsNodeOffset(node));
+    node = (sc > 0.f && right_ok) ? right : 2 * node + 1;
+  }
+  return node - (leaves - 1);
+}
+
+void VW::CatsSegments(int leaf, Example* ex) const {
+  const float range = max_value_ - min_value_;
+  const float unit = range / cats_k_;
+  const float c = min_value_ + (leaf + 0.5f) * unit;
+  const float lo = std::max(min_value_, c - bandwidth_), hi = std::min(max_value_, c + bandwidth_);
+  const float eps = epsilon_set_ ? epsilon_ : 0.05f;
+  const float base = eps / range;
+  ex->pdf_segments.clear();
+  if (lo > min_value_) ex->pdf_segments.push_back({min_value_, lo, base});
+  ex->pdf_segments.push_back({lo, hi, (1.f - eps) / (hi - lo) + base});
+  if (hi < max_value_) ex->pdf_segments.push_back({hi, max_value_, base});
+  if (cats_sample_) {
+    // deterministic draw (per-model counter): the window w.p. 1 - eps, else uniform over the range
+    uint64_t z = (cats_draws_ + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const double u1 = static_cast<double>(z >> 11) * (1.0 / 9007199254740992.0);
+    const double u2 = static_cast<double>((z * 0x2545F4914F6CDD1Dull) >> 11) * (1.0 / 9007199254740992.0);
+    const float a = u1 < 1.0 - eps ? static_cast<float>(lo + u2 * (hi - lo)) : static_cast<float>(min_value_ + u2 * range);
+    ex->cats_action = a;
+    ex->cats_pdf_value = (a >= lo && a <= hi) ? (1.f - eps) / (hi - lo) + base : base;
+  }
+}
+
+void VW::CatsLearn(Example& ex) {
+  stats_.examples += 1;
+  stats_.weighted_examples += 1;
+  const int leaf = CatsPredictLeaf(ex);
+  CatsSegments(leaf, &ex);
+  if (cats_sample_) ++cats_draws_;
+  ex.pred = cats_sample_ ? ex.cats_action : min_value_ + (leaf + 0.5f) * (max_value_ - min_value_) / cats_k_;
+  if (!ex.l.cats_has || testonly_) return;
+  stats_.sum_loss += ex.l.cats_cost;
+  // IPS estimate of each discrete action's smoothed cost with a control variate: a running mean cost b
+  // (this example included) stands in for an unobserved action, a covered one gets
+  // b + (c - b) / (|window_k| * p). Unbiased for every action, and a single cost carries signal (cheaper
+  // than usual pulls the policy towards the windows that covered it, dearer pushes it away).
+  cats_cost_sum_ += ex.l.cats_cost;
+  cats_cost_n_ += 1.0;
+  const float b = static_cast<float>(cats_cost_sum_ / cats_cost_n_);
+  const int leaves = 1 << cats_depth_;
+  const float unit = (max_value_ - min_value_) / cats_k_;
+  const float p = std::max(ex.l.cats_pdf, 1e-12f);
+  std::vector<float> win(2 * leaves - 1, b);
+  std::vector<char> valid(2 * leaves - 1, 0);
+  for (int k = 0; k < cats_k_; ++k) {
+    const float c = min_value_ + (k + 0.5f) * unit;
+    const float lo = std::max(min_value_, c - bandwidth_), hi = std::min(max_value_, c + bandwidth_);
+    valid[leaves - 1 + k] = 1;
+    if (ex.l.cats_action >= lo && ex.l.cats_action <= hi) win[leaves - 1 + k] = b + (ex.l.cats_cost - b) / ((hi - lo) * p);
+  }
+  // filter-tree update, bottom up: each node learns which child's tournament winner (the leaf its current
+  // routing reaches) has the lower estimate, weighted by the difference
+  for (int node = leaves - 2; node >= 0; --node) {
+    const int l = 2 * node + 1, r = 2 * node + 2;
+    valid[node] = valid[l] || valid[r];
+    if (!valid[l] || !valid[r]) {
+      win[node] = valid[l] ? win[l] : win[r];
+      continue;
+    }
+    const float sc = Dot(ex, CatsNodeOffset(node));
+    const float imp = std::fabs(win[l] - win[r]);
+    if (imp > 0.f) Update(ex, CatsNodeOffset(node), sc, win[r] < win[l] ? 1.f : -1.f, imp);
+    win[node] = sc > 0.f ? win[r] : win[l];
+  }
+}
+
 void VW::Predict(Example& ex) {
+  if (cats_k_ > 0) {
+    const int leaf = CatsPredictLeaf(ex);
+    CatsSegments(leaf, &ex);
+    if (cats_sample_) ++cats_draws_;
+    ex.pred = cats_sample_ ? ex.cats_action : min_value_ + (leaf + 0.5f) * (max_value_ - min_value_) / cats_k_;
+    return;
+  }
   if (oaa_ > 0 || csoaa_ > 0) {
     const int K = oaa_ > 0 ? oaa_ : csoaa_;
     ex.scores.assign(K, 0.f);
@@ -305,6 +418,7 @@ void VW::Predict(Example& ex) {
 
 void VW::Learn(Example& ex) {
   if (caching_ && stats_.passes == 0) cache_.push_back(ex);
+  if (cats_k_ > 0) { CatsLearn(ex); return; }
   const float w = ex.l.weight;
   stats_.examples += 1;
   stats_.weighted_examples += w;
@@ -436,6 +550,7 @@ void VW::PredictMulti(std::vector<Example>& exs) {
 }
 
 std::string VW::OutputPredictionType() const {
+  if (cats_k_ > 0) return cats_sample_ ? "prediction_type_t::action_pdf_value" : "prediction_type_t::pdf";
   if (cb_explore_) return "prediction_type_t::action_probs";
   if (cb_adf_) return "prediction_type_t::action_scores";
   if (oaa_ > 0 && probabilities_) return "prediction_type_t::scalars";
@@ -455,6 +570,18 @@ Example VW::ParseLine(const std::string& line) const {
   if (!ht.empty()) {
     if (ht[0] == "shared") {
       ex.l.cb_shared = true;
+    } else if (ht[0] == "ca") {
+      // CATS: "ca action:cost:pdf_value"
+      if (ht.size() > 1) {
+        const std::string& v = ht[1];
+        auto c1 = v.find(':'), c2 = c1 == std::string::npos ? std::string::npos : v.find(':', c1 + 1);
+        if (c1 == std::string::npos || c2 == std::string::npos)
+          throw std::runtime_error("CATS label must be 'ca action:cost:pdf_value', got '" + v + "'");
+        ex.l.cats_has = true;
+        ex.l.cats_action = std::stof(v.substr(0, c1));
+        ex.l.cats_cost = std::stof(v.substr(c1 + 1, c2 - c1 - 1));
+        ex.l.cats_pdf = std::stof(v.substr(c2 + 1));
+      }
     } else if (cb_adf_ && ht[0].find(':') != std::string::npos) {
       // action:cost:probability
       std::string s = ht[0];

@@ -14,6 +14,7 @@
 // multi-pass replay, model averaging (endPass allreduce / mergeModels), a
 // binary model format and --readable_model.
 #pragma once
+#include <array>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -44,6 +45,9 @@ struct Namespace {
 };
 
 struct Label {
+  // CATS label "ca action:cost:pdf_value"
+  bool cats_has = false;
+  float cats_action = 0.f, cats_cost = 0.f, cats_pdf = 1.f;
   float label = 0.f;          // simple label (FLT_MAX = none)
   float weight = 1.f;         // importance
   float initial = 0.f;
@@ -65,6 +69,10 @@ struct Example {
   float pred = 0.f;
   std::vector<float> scores;                // oaa/csoaa/cb scores
   std::vector<std::pair<int, float>> action_probs;  // cb_explore: (action 0-based, prob)
+  // CATS (continuous actions): the smoothed policy's density as (left, right, value) segments (--cats_pdf),
+  // or a sampled action with its density (--cats)
+  std::vector<std::array<float, 3>> pdf_segments;
+  float cats_action = 0.f, cats_pdf_value = 0.f;
   float loss = 0.f;
   Namespace& Get(unsigned char c);
 };
@@ -121,6 +129,13 @@ class VW {
   float FirstDeriv(float pred, float label) const;
   float FinalizePred(float raw) const;
   void CbLearn(std::vector<Example>& exs, bool learn);
+  // CATS: continuous actions over [min_value, max_value] discretised into cats_k_ centroids, a binary tree of
+  // linear node scorers picks one, the policy is that centroid's bandwidth window (prob 1 - epsilon) plus a
+  // uniform epsilon over the range
+  int CatsPredictLeaf(const Example& ex) const;
+  void CatsSegments(int leaf, Example* ex) const;
+  void CatsLearn(Example& ex);
+  uint64_t CatsNodeOffset(int node) const { return static_cast<uint64_t>(node + 1) * 2654435761ull; }
 
   std::string args_str_;
   int bits_ = 18;
@@ -144,6 +159,13 @@ class VW {
   bool testonly_ = false;
   bool holdout_off_ = true;
   int ngram_ = 0;
+  int cats_k_ = 0;             // --cats_pdf K / --cats K: discrete centroids
+  bool cats_sample_ = false;   // --cats: emit a sampled action (action_pdf_value) instead of the pdf
+  float bandwidth_ = -1.f, min_value_ = 0.f, max_value_ = -1.f;
+  bool epsilon_set_ = false;
+  int cats_depth_ = 0;
+  uint64_t cats_draws_ = 0;
+  double cats_cost_sum_ = 0, cats_cost_n_ = 0;  // control-variate baseline of the CATS cost estimates
   std::vector<float> weights_;
   double t_ = 0;                    // weighted examples seen (power_t schedule)
   double total_weight_ = 0, sum_norm_x_ = 0;

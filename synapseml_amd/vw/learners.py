@@ -494,6 +494,13 @@ class VowpalWabbitClassifier(VowpalWabbitBase, HasRawPredictionCol, HasProbabili
 
 
 # ============================================================ generic (VW text format)
+def _object_column(values) -> np.ndarray:
+    col = np.empty(len(values), dtype=object)
+    for i, v in enumerate(values):
+        col[i] = v
+    return col
+
+
 class VowpalWabbitGenericModel(Model, HasPredictionCol):
     model = Param("The VW model bytes", None, complex=True)
     vwArgs = Param("Arguments the model was trained with", "", T.toString)
@@ -501,9 +508,31 @@ class VowpalWabbitGenericModel(Model, HasPredictionCol):
     testArgs = Param("Additional test-time arguments", "", T.toString)
 
     def _transform(self, df: DataFrame) -> DataFrame:
+        """Adds the columns of the learner's prediction type, as the reference's schema map does
+        (VowpalWabbitPrediction.scala:18-101, VowpalWabbitSchema.scala): scalar -> prediction, confidence;
+        scalars -> predictions; multiclass / prob -> prediction; action_scores -> predictions [(action, score)];
+        action_probs -> predictions [(action, probability)]; pdf -> segments [(left, right, pdfValue)];
+        action_pdf_value -> action, pdf."""
         vw = _vw().VW(self.getVwArgs() + " --testonly " + self.getTestArgs(), self.getModel())
-        preds = vw.learn_text([str(s) for s in df[self.getInputCol()].tolist()], False)
-        return df.withColumn(self.getPredictionCol(), np.asarray(preds, np.float64))
+        lines = [str(s) for s in df[self.getInputCol()].tolist()]
+        ptype, recs = vw.predict_text_structured(lines, False)
+        kind = ptype.split("::")[-1]
+        obj = lambda xs: _object_column(xs)  # noqa: E731
+        if kind == "pdf":
+            segs = [[{"left": float(a), "right": float(b), "pdfValue": float(v)} for a, b, v in r] for r in recs]
+            return df.withColumn("segments", obj(segs))
+        if kind == "action_pdf_value":
+            return (df.withColumn("action", np.asarray([r[0] for r in recs], np.float64))
+                    .withColumn("pdf", np.asarray([r[1] for r in recs], np.float64)))
+        if kind in ("action_probs", "action_scores"):
+            field = "probability" if kind == "action_probs" else "score"
+            return df.withColumn("predictions", obj([[{"action": int(a), field: float(v)} for a, v in r] for r in recs]))
+        if kind == "scalars":
+            return df.withColumn("predictions", obj([list(map(float, r)) for r in recs]))
+        if kind == "multiclass":
+            return df.withColumn(self.getPredictionCol(), np.asarray(recs, np.int64))
+        out = df.withColumn(self.getPredictionCol(), np.asarray([r[0] for r in recs], np.float64))
+        return out.withColumn("confidence", np.asarray([r[1] for r in recs], np.float64))
 
     def getReadableModel(self) -> str:  # noqa: N802
         return _vw().VW(self.getVwArgs(), self.getModel()).readable_model()

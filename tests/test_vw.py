@@ -424,3 +424,77 @@ def test_hash_strings_packed_matches_murmur():
         assert got.tolist() == [murmur_hash(x, seed) & 0xFFFFFFFF for x in xs]
     assert hash_strings(["marie", "markus"], 2493003127, (1 << 18) - 1, device="cpu").tolist() == [60554, 36739]
     assert hash_strings([], 1, device="cpu").tolist() == []
+
+
+def _cats_df():
+    return DataFrame({"value": np.array(["ca 185.121:0.657567:6.20426e-05 | a b",
+                                         "ca 772.592:0.458316:6.20426e-05 | b c",
+                                         "ca 15140.6:0.31791:6.20426e-05 | d"], dtype=object)})
+
+
+def test_generic_cats_pdf_matches_reference():
+    """Mirror of VerifyVowpalWabbitGeneric.scala:107-132 ('Verify VowpalWabbitGeneric using CATS'): the pdf
+    segments of the first example after training on three CATS-labelled examples."""
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    m = VowpalWabbitGeneric(passThroughArgs="--cats_pdf 3 --bandwidth 5000 --min_value 0 --max_value 20000").fit(
+        _cats_df())
+    seg = m.transform(_cats_df().slice(0, 1))["segments"][0]
+    got = [(s["left"], s["right"], s["pdfValue"]) for s in seg]
+    want = [(0.0, 8333.333, 1.165e-4), (8333.333, 20000.0, 2.5e-6)]
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-3)
+    # the density integrates to one
+    assert abs(sum((r - l) * v for l, r, v in got) - 1.0) < 1e-4
+
+
+def test_generic_cats_action_pdf_value():
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    m = VowpalWabbitGeneric(passThroughArgs="--cats 3 --bandwidth 5000 --min_value 0 --max_value 20000").fit(
+        _cats_df())
+    out = m.transform(_cats_df())
+    a, p = out["action"], out["pdf"]
+    assert ((a >= 0) & (a <= 20000)).all()
+    assert np.all(p > 0)
+
+
+def test_cats_learns_the_cheap_region():
+    """Costs low near 15000 and high elsewhere: the learned policy's window moves there."""
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    rng = np.random.default_rng(0)
+    lines = []
+    for _ in range(3000):
+        a = rng.uniform(0, 20000)
+        cost = 0.0 if 12000 < a < 18000 else 1.0
+        lines.append(f"ca {a:.2f}:{cost}:{1 / 20000:.8f} | x")
+    df = DataFrame({"value": np.array(lines, dtype=object)})
+    m = VowpalWabbitGeneric(passThroughArgs="--cats_pdf 4 --bandwidth 2500 --min_value 0 --max_value 20000").fit(df)
+    seg = m.transform(df.slice(0, 1))["segments"][0]
+    best = max(seg, key=lambda s: s["pdfValue"])
+    assert 12000 <= (best["left"] + best["right"]) / 2 <= 18000, seg
+
+
+@pytest.mark.parametrize("args", ["--nn 10", "--boosting 3", "--cb_explore 4", "--bogus_flag", "--cats 1 --bandwidth 1 "
+                                  "--min_value 0 --max_value 1", "--cats_pdf 3 --min_value 0 --max_value 10"])
+def test_unknown_or_unsupported_options_are_rejected(args):
+    """options the engine does not implement must raise, never train a different model."""
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    df = DataFrame({"value": np.array(["1 | a b"], dtype=object)})
+    with pytest.raises(RuntimeError):
+        VowpalWabbitGeneric(passThroughArgs=args).fit(df)
+
+
+def test_generic_prediction_schemas():
+    """Prediction columns follow the learner's prediction type (VowpalWabbitSchema.scala)."""
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    reg = DataFrame({"value": np.array(["1 | a:1 b:2", "0 | a:2 c:1"], dtype=object)})
+    out = VowpalWabbitGeneric().fit(reg).transform(reg)
+    assert "prediction" in out and "confidence" in out
+    mc = DataFrame({"value": np.array(["1 | a", "2 | b", "3 | c"], dtype=object)})
+    out = VowpalWabbitGeneric(passThroughArgs="--oaa 3").fit(mc).transform(mc)
+    assert out["prediction"].dtype == np.int64
