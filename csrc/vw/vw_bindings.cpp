@@ -97,6 +97,7 @@ PYBIND11_MODULE(_vw, m) {
     return out;
   }, py::arg("bytes"), py::arg("offsets"), py::arg("seed"), py::arg("mask") = 0xFFFFFFFFu, py::arg("device") = false);
   m.def("gpu_available", &VwGpuAvailable);
+  m.def("describe_args", &VW::DescribeArgs, "parse + validate a VW command line (no weight table)");
 
   py::class_<VW, std::shared_ptr<VW>>(m, "VW")
       .def(py::init([](const std::string& args, py::object model) {
@@ -309,9 +310,13 @@ PYBIND11_MODULE(_vw, m) {
       .def_readwrite("bits", &GpuSgdConfig::bits)
       .def_readwrite("lr", &GpuSgdConfig::lr)
       .def_readwrite("power_t", &GpuSgdConfig::power_t)
+      .def_readwrite("initial_t", &GpuSgdConfig::initial_t)
       .def_readwrite("l2", &GpuSgdConfig::l2)
       .def_readwrite("loss", &GpuSgdConfig::loss)
-      .def_readwrite("adaptive", &GpuSgdConfig::adaptive);
+      .def_readwrite("adaptive", &GpuSgdConfig::adaptive)
+      .def_readwrite("normalized", &GpuSgdConfig::normalized)
+      .def_readwrite("invariant", &GpuSgdConfig::invariant)
+      .def_readwrite("oaa", &GpuSgdConfig::oaa);
   py::class_<GpuSgd, std::shared_ptr<GpuSgd>>(m, "GpuSgd")
       .def(py::init([](const GpuSgdConfig& c, int dev) { return std::make_shared<GpuSgd>(c, dev); }),
            py::arg("config"), py::arg("device") = -1)
@@ -344,15 +349,56 @@ PYBIND11_MODULE(_vw, m) {
         py::gil_scoped_release rel;
         g.AllReduceAverage(h->c, h->world);
       })
-      .def("weights", [](const GpuSgd& g) {
-        py::array_t<float> out(g.NumWeights());
-        g.CopyWeights(out.mutable_data());
-        return out;
+      // model bytes in the host learner's format (vw_core.cpp VW::SaveModel), built from the device nonzeros
+      .def("export_model", [](const GpuSgd& g, const std::string& args) {
+        std::vector<uint64_t> idx;
+        std::vector<float> val;
+        double t, tw, snx;
+        {
+          py::gil_scoped_release rel;
+          g.ExportNonzeros(&idx, &val);
+          g.GlobalState(&t, &tw, &snx);
+        }
+        std::string s = "SMLVW001";
+        auto put = [&s](const auto& v) { s.append(reinterpret_cast<const char*>(&v), sizeof(v)); };
+        put(static_cast<uint32_t>(args.size()));
+        s += args;
+        int32_t bits = 0;
+        while ((1ull << bits) < g.NumWeights()) ++bits;
+        put(bits);
+        put(static_cast<uint32_t>(4));
+        put(t); put(tw); put(snx);
+        put(g.min_label()); put(g.max_label());
+        put(static_cast<uint64_t>(idx.size()));
+        for (size_t i = 0; i < idx.size(); ++i) { put(idx[i]); put(val[i]); }
+        return py::bytes(s);
       })
-      .def("set_weights", [](GpuSgd& g, F32 w) {
-        if (static_cast<uint64_t>(w.size()) != g.NumWeights()) throw std::runtime_error("size mismatch");
-        g.SetWeights(w.data());
+      // warm start from model bytes of either learner (same format)
+      .def("import_model", [](GpuSgd& g, const std::string& bytes) {
+        if (bytes.size() < 12 || bytes.compare(0, 8, "SMLVW001") != 0) throw std::runtime_error("not a VW model");
+        const char* p = bytes.data() + 8;
+        const char* end = bytes.data() + bytes.size();
+        auto need = [&p, end](size_t k) {
+          if (static_cast<size_t>(end - p) < k) throw std::runtime_error("truncated VW model");
+        };
+        auto get = [&p, &need](auto* v) { need(sizeof(*v)); std::memcpy(v, p, sizeof(*v)); p += sizeof(*v); };
+        uint32_t alen; get(&alen); need(alen); p += alen;
+        int32_t bits; uint32_t stride; get(&bits); get(&stride);
+        if (stride != 4 || (1ull << bits) != g.NumWeights()) throw std::runtime_error("model table geometry differs");
+        double t, tw, snx, lo, hi; get(&t); get(&tw); get(&snx); get(&lo); get(&hi);
+        uint64_t nz; get(&nz);
+        if (nz > static_cast<uint64_t>(end - p) / 12) throw std::runtime_error("truncated VW model");
+        std::vector<uint64_t> idx(nz);
+        std::vector<float> val(nz);
+        for (uint64_t i = 0; i < nz; ++i) { get(&idx[i]); get(&val[i]); }
+        py::gil_scoped_release rel;
+        g.ImportNonzeros(idx, val);
+        g.SetGlobalState(t, tw, snx);
+        g.SetLabelRange(lo, hi);
       })
+      .def_property_readonly("num_weights", &GpuSgd::NumWeights)
+      .def_property_readonly("last_sync_bytes", &GpuSgd::last_sync_bytes)
+      .def_property_readonly("last_sync_blocks", &GpuSgd::last_sync_blocks)
       .def_property_readonly("examples", &GpuSgd::examples)
       .def_property_readonly("sum_loss", &GpuSgd::sum_loss);
 }

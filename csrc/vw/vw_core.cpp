@@ -158,6 +158,38 @@ void VW::ParseArgs(const std::string& args) {
   if (loss_ == "logistic") { stats_.min_label = -50; stats_.max_label = 50; }
 }
 
+std::map<std::string, std::string> VW::DescribeArgs(const std::string& args) {
+  VW v;
+  v.ParseArgs(args);
+  std::map<std::string, std::string> d;
+  auto f = [](double x) { std::ostringstream o; o.precision(9); o << x; return o.str(); };
+  d["bits"] = std::to_string(v.bits_);
+  d["learning_rate"] = f(v.lr_);
+  d["power_t"] = f(v.power_t_);
+  d["initial_t"] = f(v.initial_t_);
+  d["l1"] = f(v.l1_);
+  d["l2"] = f(v.l2_);
+  d["loss_function"] = v.loss_;
+  d["adaptive"] = v.adaptive_ ? "1" : "0";
+  d["normalized"] = v.normalized_ ? "1" : "0";
+  d["invariant"] = v.invariant_ ? "1" : "0";
+  d["oaa"] = std::to_string(v.oaa_);
+  d["csoaa"] = std::to_string(v.csoaa_);
+  d["cb_adf"] = v.cb_adf_ ? "1" : "0";
+  d["cats"] = std::to_string(v.cats_k_);
+  d["ngram"] = std::to_string(v.ngram_);
+  d["ignore"] = std::string(v.ignore_.begin(), v.ignore_.end());
+  d["link_logistic"] = v.link_logistic_ ? "1" : "0";
+  d["probabilities"] = v.probabilities_ ? "1" : "0";
+  d["constant"] = v.constant_ ? "1" : "0";
+  d["hash_seed"] = std::to_string(v.hash_seed_);
+  d["passes"] = std::to_string(v.passes_);
+  std::string inter;
+  for (const auto& q : v.interactions_) inter += (inter.empty() ? "" : ",") + q;
+  d["interactions"] = inter;
+  return d;
+}
+
 VW::VW(const std::string& args, const std::string* model_bytes) : args_str_(args) {
   ParseArgs(args);
   weights_.assign(static_cast<size_t>(mask_ + 1) * stride_, 0.f);

@@ -114,10 +114,13 @@ class VW {
   uint32_t HashSeed() const { return hash_seed_; }
   // model averaging: w = sum over models / n (mergeModels / endPass allreduce)
   static std::unique_ptr<VW> Merge(const std::vector<const VW*>& models);
+  // parse and validate a command line without allocating the weight table (GPU learner set-up)
+  static std::map<std::string, std::string> DescribeArgs(const std::string& args);
   void SetAllReduce(std::function<void(float*, size_t)> fn) { allreduce_ = std::move(fn); }
   int world_size = 1;
 
  private:
+  VW() = default;  // DescribeArgs: parse only
   void ParseArgs(const std::string& args);
   void LoadModel(const std::string& bytes);
   // linear core over (interaction-expanded) features of one example with a

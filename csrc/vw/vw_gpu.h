@@ -1,12 +1,14 @@
 // Device-resident hashed linear learner (K12/K13 of SURVEY §2.4): the weight
-// table (2^b x {w, G}) lives in HBM, mini-batches of CSR examples are learned
-// by one wave per example with AdaGrad-style hogwild updates (atomics on the
-// touched weights), and the table is averaged across GPUs with RCCL at pass
-// boundaries (C4: the reference's spanning-tree AllReduce at endPass).
+// table (2^b x {w, G, N}) lives in HBM, mini-batches of CSR examples are learned
+// by one wave per example with VW's adaptive / normalized / invariant update as
+// hogwild atomics on the touched weights (batch 1 = the sequential learner),
+// --oaa runs one wave per class, and touched blocks are averaged across GPUs with
+// RCCL at sync points (C4: the reference's spanning-tree AllReduce at endPass).
 #pragma once
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace smlvw {
 
@@ -14,35 +16,50 @@ struct GpuSgdConfig {
   int bits = 18;
   float lr = 0.5f;
   float power_t = 0.5f;
+  float initial_t = 0.f;
   float l2 = 0.f;
-  int loss = 0;        // 0 squared, 1 logistic
-  bool adaptive = true;
+  int loss = 0;          // 0 squared, 1 logistic
+  bool adaptive = true;  // VW's default update: adaptive + normalized + invariant
+  bool normalized = true;
+  bool invariant = true;
+  int oaa = 0;           // one-against-all classes (0: scalar learner)
 };
 
 class GpuSgd {
  public:
   GpuSgd(const GpuSgdConfig& cfg, int device);
   ~GpuSgd();
-  // indices are pre-hashed feature ids (masked on device); labels in the
-  // loss's convention (logistic: -1/+1). Returns the progressive predictions.
+  // indices are pre-hashed feature ids (masked on device); labels in the loss's convention (logistic:
+  // -1/+1; oaa: 1-based class). Returns the progressive predictions (oaa: predicted class).
   void Learn(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
              const float* weights, int64_t n, int batch, float* preds_out);
   void Predict(const int64_t* indptr, const uint32_t* indices, const float* values, int64_t n, float* out);
-  // in-place sum over ranks of the weight table via the supplied device allreduce, then / world
+  // weighted average over ranks of the blocks touched since the last sync (RCCL on the learner's stream)
   void AllReduceAverage(void* nccl_comm_handle, int world);
   uint64_t NumWeights() const;
-  void CopyWeights(float* host_out) const;
-  void SetWeights(const float* host_in);
+  // the table's nonzero components as (stride-4 index, value) - the host model format's records
+  void ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val) const;
+  void ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val);
+  void GlobalState(double* t, double* total_weight, double* sum_norm_x) const;
+  void SetGlobalState(double t, double total_weight, double sum_norm_x);
   double examples() const { return examples_; }
   double sum_loss() const { return sum_loss_; }
+  double min_label() const { return min_label_; }
+  double max_label() const { return max_label_; }
+  void SetLabelRange(double lo, double hi) { min_label_ = lo; max_label_ = hi; }
+  int64_t last_sync_bytes() const { return last_sync_bytes_; }
+  int64_t last_sync_blocks() const { return last_sync_blocks_; }
   void* weights_device();
   void* stream();
 
  private:
+  void Launch(int64_t b0, int64_t b1, bool learn, bool have_weights);
   struct Impl;
   std::unique_ptr<Impl> impl_;
   GpuSgdConfig cfg_;
   double examples_ = 0, sum_loss_ = 0;
+  double min_label_ = 0, max_label_ = 0;
+  int64_t last_sync_bytes_ = 0, last_sync_blocks_ = 0;
 };
 
 bool VwGpuAvailable();

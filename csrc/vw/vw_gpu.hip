@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -62,70 +63,272 @@ __global__ __launch_bounds__(256) void murmur_batch_kernel(const uint8_t* __rest
   }
 }
 
-__device__ __forceinline__ void ExampleStep(const int64_t* __restrict__ indptr, const uint32_t* __restrict__ idx,
-                                            const float* __restrict__ val, const float* __restrict__ labels,
-                                            const float* __restrict__ weights, int64_t e, float2* __restrict__ W,
-                                            uint64_t mask, float lr, float l2, int loss, int adaptive, float eta_scale,
-                                            float* __restrict__ preds, int learn, int lane, float* wloss) {
-  const int64_t b = indptr[e], en = indptr[e + 1];
-  float s = 0.f;
-  for (int64_t p = b + lane; p < en; p += 64) s += W[idx[p] & mask].x * val[p];
+// ---------------------------------------------------------------- K12
+// Weight slot = float4 {w, G (adaptive sum of squared gradients), N (normalizer: max |x| seen), -}: the
+// CPU learner's stride-4 layout, so the exported table loads into the host model unchanged. One wave per
+// (example, learner offset): lanes stride over the features, the dot product is a wave reduction, and the
+// update follows the sequential learner's Update() (vw_core.cpp) step for step - VW's default
+// adaptive + normalized + invariant ("safe") update or any subset of it:
+//   pass 1: G += g^2 x^2 (adaptive); N = max(N, |x|), w rescaled when N grows (normalized);
+//           rate = G^-1/2 * N^-1 (or N^-2 without adaptive); sum_x2rate, sum_norm_x (wave sums)
+//   global: t, total weight, sum of feature norms (fp64 atomics): eta = lr * sqrt(tw / snx) (normalized,
+//           adaptive) * (initial_t + t)^-power_t (non-adaptive)
+//   update: importance-invariant closed form (squared) / bounded implicit step (logistic), else -g eta
+//   pass 2: w += update * x * rate (+ l2), and the slot's 16 K-slot block is marked dirty for the sync.
+// Hogwild: examples of a mini-batch run concurrently on atomics (conflicts are rare in a 2^b table);
+// batch = 1 is the exact sequential learner.
+constexpr int kDirtyShift = 12;  // dirty-tracking granularity: 4096 slots (64 KB) per block
+
+struct SgdArgs {
+  const int64_t* indptr;
+  const uint32_t* idx;
+  const float* val;
+  const float* lab;    // scalar label, or the 1-based class for oaa
+  const float* wt;     // importance (null = 1)
+  const float* lo;     // running label range (prediction clamp), per example
+  const float* hi;
+  int64_t n0, n1;
+  float4* W;
+  uint64_t mask;
+  uint8_t* dirty;
+  double* gs;          // [t, total weight, sum of feature norms]
+  float lr, power_t, initial_t, l2;
+  int loss;            // 0 squared, 1 logistic
+  int adaptive, normalized, invariant;
+  int K;               // oaa classes (0: scalar learner)
+  float* preds;
+  float* loss_acc;
+  int learn;
+};
+
+__device__ __forceinline__ float WaveSum(float v) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (preds && lane == 0) preds[e] = s;
-  if (!learn) return;
-  const float y = labels[e];
-  const float imp = weights ? weights[e] : 1.f;
-  float g, l;
-  if (loss == 1) {
-    const float m = y * s;
-    g = -y / (1.f + expf(m));
-    l = log1pf(expf(-m));
-  } else {
-    g = 2.f * (s - y);
-    l = (s - y) * (s - y);
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float Dot(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, int lane) {
+  float s = 0.f;
+  for (int64_t p = b + lane; p < en; p += 64) s += a.W[(a.idx[p] + off) & a.mask].x * a.val[p];
+  return WaveSum(s);
+}
+
+__device__ __forceinline__ float Rate(const SgdArgs& a, float G, float N) {
+  float r = 1.f;
+  if (a.adaptive) r = G > 0.f ? rsqrtf(G) : 0.f;
+  if (a.normalized) {
+    const float inv = 1.f / N;
+    r *= a.adaptive ? inv : inv * inv;
   }
-  if (lane == 0) *wloss = l * imp;
-  g *= imp;
+  return r;
+}
+
+// one Update() of the sequential learner for (example rows [b, en), offset) at raw prediction `raw`
+__device__ void UpdateWave(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y, float imp,
+                           int lane) {
+  float g;
+  if (a.loss == 1) g = -y / (1.f + expf(y * raw));
+  else g = 2.f * (raw - y);
+  const float grad_sq = g * g * imp;
+  float ppu = 0.f, norm_x = 0.f;
   for (int64_t p = b + lane; p < en; p += 64) {
-    const uint64_t h = idx[p] & mask;
-    const float x = val[p];
-    const float gx = g * x;
-    float step;
-    if (adaptive) {
-      const float G = atomicAdd(&W[h].y, gx * gx) + gx * gx;
-      step = lr * gx * rsqrtf(G + 1e-12f);
-    } else {
-      step = lr * eta_scale * gx;
+    const uint64_t h = (a.idx[p] + off) & a.mask;
+    float4* w = &a.W[h];
+    const float x = a.val[p];
+    float x2 = x * x;
+    if (x2 < FLT_MIN) x2 = FLT_MIN;
+    float G = 0.f, N = 1.f;
+    if (a.adaptive) G = atomicAdd(&w->y, grad_sq * x2) + grad_sq * x2;
+    if (a.normalized) {
+      const float ax = fabsf(x);
+      // N only grows: the float bits of non-negative values order like unsigned integers
+      const float old = __uint_as_float(atomicMax(reinterpret_cast<unsigned int*>(&w->z), __float_as_uint(ax)));
+      if (ax > old && old > 0.f) {
+        const float r = old / ax;
+        w->x *= a.adaptive ? r : r * r;  // hogwild rescale of this slot's weight
+      }
+      N = fmaxf(old, ax);
+      norm_x += x2 / (N * N);
     }
-    if (l2 > 0.f) step += lr * l2 * W[h].x;
-    atomicAdd(&W[h].x, -step);
+    ppu += x2 * Rate(a, G, N);
+  }
+  ppu = WaveSum(ppu);
+  norm_x = WaveSum(norm_x);
+  double eta = a.lr;
+  if (lane == 0) {
+    const double t = atomicAdd(&a.gs[0], static_cast<double>(imp)) + imp;
+    const double tw = atomicAdd(&a.gs[1], static_cast<double>(imp)) + imp;
+    const double snx = atomicAdd(&a.gs[2], static_cast<double>(imp) * norm_x) + static_cast<double>(imp) * norm_x;
+    if (a.normalized && snx > 0.0) {
+      const double avg = tw / snx;
+      eta *= a.adaptive ? sqrt(avg) : avg;
+    }
+    if (!a.adaptive) eta *= pow(static_cast<double>(a.initial_t) + t, -static_cast<double>(a.power_t));
+  }
+  eta = __shfl(eta, 0, 64);
+  const float us = static_cast<float>(eta) * imp;
+  float update;
+  if (a.invariant) {
+    const float pp = fmaxf(ppu, FLT_MIN);
+    if (a.loss == 0) {
+      update = us * pp < 1e-6f ? 2.f * (y - raw) * us : (y - raw) * (1.f - expf(-2.f * us * pp)) / pp;
+    } else {
+      const float step = y * us / (1.f + expf(y * raw));
+      update = fabsf(step * pp) > 50.f ? copysignf(50.f / pp, step) : step;
+    }
+  } else {
+    update = -g * us;
+  }
+  const float decay = static_cast<float>(eta) * a.l2;
+  for (int64_t p = b + lane; p < en; p += 64) {
+    const uint64_t h = (a.idx[p] + off) & a.mask;
+    float4* w = &a.W[h];
+    const float x = a.val[p];
+    const float rate = Rate(a, a.adaptive ? w->y : 0.f, a.normalized ? w->z : 1.f);
+    const float nw = atomicAdd(&w->x, update * x * rate) + update * x * rate;
+    if (decay > 0.f) atomicAdd(&w->x, -decay * nw);
+    a.dirty[h >> kDirtyShift] = 1;
   }
 }
 
-__global__ __launch_bounds__(256) void sgd_kernel(const int64_t* __restrict__ indptr, const uint32_t* __restrict__ idx,
-                                                  const float* __restrict__ val, const float* __restrict__ labels,
-                                                  const float* __restrict__ weights, int64_t n0, int64_t n1,
-                                                  float2* __restrict__ W, uint64_t mask, float lr, float l2, int loss,
-                                                  int adaptive, float eta_scale, float* __restrict__ preds,
-                                                  float* __restrict__ loss_acc, int learn) {
+__device__ __forceinline__ float LossOf(int loss, float p, float y) {
+  if (loss == 1) return log1pf(expf(-y * p));
+  return (p - y) * (p - y);
+}
+
+// scalar learners: one wave per example
+__global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t e = n0 + static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wid;
-  __shared__ float wloss[kWavesPerBlock];
+  const int64_t e = a.n0 + static_cast<int64_t>(blockIdx.x) * 4 + wid;
+  __shared__ float wloss[4];
   if (lane == 0) wloss[wid] = 0.f;
-  if (e < n1) ExampleStep(indptr, idx, val, labels, weights, e, W, mask, lr, l2, loss, adaptive, eta_scale, preds,
-                          learn, lane, &wloss[wid]);
-  // one loss atomic per block (a same-address atomic per example serialises the launch)
-  if (learn) {
+  if (e < a.n1) {
+    const int64_t b = a.indptr[e], en = a.indptr[e + 1];
+    const float raw = Dot(a, b, en, 0, lane);
+    float p = isnan(raw) ? 0.f : raw;
+    if (a.lo) p = fminf(fmaxf(p, a.lo[e]), a.hi[e]);  // the learner's running label range
+    if (a.preds && lane == 0) a.preds[e] = p;
+    if (a.learn) {
+      const float y = a.lab[e], imp = a.wt ? a.wt[e] : 1.f;
+      if (lane == 0) wloss[wid] = LossOf(a.loss, p, y) * imp;
+      if (imp > 0.f) UpdateWave(a, b, en, 0, raw, y, imp, lane);
+    }
+  }
+  if (a.learn) {
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(loss_acc, wloss[0] + wloss[1] + wloss[2] + wloss[3]);
+    if (threadIdx.x == 0) atomicAdd(a.loss_acc, wloss[0] + wloss[1] + wloss[2] + wloss[3]);
   }
 }
 
-__global__ void scale_kernel(float* w, uint64_t n, float s) {
-  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
-       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
-    w[i] *= s;
+// --oaa K: one block per example, wave c handles classes c, c + waves, ...: scores (predict), then the
+// per-class binary updates (label +1 for the true class, -1 otherwise) at the class offsets
+constexpr uint64_t kOaaOffset = 1315423911ull;
+constexpr int kOaaMaxWaves = 8;
+
+__global__ __launch_bounds__(64 * kOaaMaxWaves) void oaa_kernel(SgdArgs a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int64_t e = a.n0 + blockIdx.x;
+  if (e >= a.n1) return;
+  extern __shared__ float scores[];
+  const int64_t b = a.indptr[e], en = a.indptr[e + 1];
+  for (int k = wid; k < a.K; k += nw) {
+    const float s = Dot(a, b, en, static_cast<uint64_t>(k) * kOaaOffset, lane);
+    if (lane == 0) scores[k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int k = 1; k < a.K; ++k) if (scores[k] > scores[best]) best = k;
+    if (a.preds) a.preds[e] = static_cast<float>(best + 1);
+    if (a.learn) atomicAdd(a.loss_acc, (best + 1 == static_cast<int>(a.lab[e]) ? 0.f : 1.f) * (a.wt ? a.wt[e] : 1.f));
+  }
+  if (!a.learn) return;
+  const float imp = a.wt ? a.wt[e] : 1.f;
+  if (imp <= 0.f) return;
+  const int y = static_cast<int>(a.lab[e]);
+  for (int k = wid; k < a.K; k += nw) UpdateWave(a, b, en, static_cast<uint64_t>(k) * kOaaOffset, scores[k],
+                                                 k + 1 == y ? 1.f : -1.f, imp, lane);
+}
+
+__global__ void pack_kernel(const float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk,
+                            uint64_t nw, int adaptive, float* __restrict__ sums, float* __restrict__ nmax) {
+  constexpr int64_t B = int64_t(1) << kDirtyShift;
+  const int64_t m = nblk * B;
+  for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < m;
+       j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
+    const float4 v = slot < nw ? W[slot] : make_float4(0.f, 0.f, 0.f, 0.f);
+    sums[3 * j] = v.x;
+    sums[3 * j + 1] = adaptive ? v.x * v.y : 0.f;
+    sums[3 * j + 2] = v.y;
+    nmax[j] = v.z;
+  }
+}
+
+// VW's weighted averaging: with adaptive state w = sum(w G) / sum(G) (plain mean where no rank has
+// gradient mass), G = sum(G) / world; N = max(N); without adaptive w = sum(w) / world
+__global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk, uint64_t nw,
+                              int adaptive, float inv_world, const float* __restrict__ sums,
+                              const float* __restrict__ nmax) {
+  constexpr int64_t B = int64_t(1) << kDirtyShift;
+  const int64_t m = nblk * B;
+  for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < m;
+       j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
+    if (slot >= nw) continue;
+    float4 v = W[slot];
+    const float sw = sums[3 * j], swg = sums[3 * j + 1], sg = sums[3 * j + 2];
+    v.x = (adaptive && sg > 0.f) ? swg / sg : sw * inv_world;
+    v.y = sg * inv_world;
+    v.z = nmax[j];
+    W[slot] = v;
+  }
+}
+
+__global__ void dirty_list_kernel(const uint8_t* __restrict__ dirty, int64_t nblk, const int32_t* __restrict__ pos,
+                                  int32_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < nblk;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    if (dirty[i]) out[pos[i]] = static_cast<int32_t>(i);
+}
+
+// nonzero components of the table -> (stride-4 index, value) records (model export, no host table)
+__global__ void count_nz_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per, int32_t* __restrict__ cnt) {
+  const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * per, s1 = min(nw, s0 + per);
+  int c = 0;
+  for (uint64_t s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
+    const float4 v = W[s];
+    c += (v.x != 0.f) + (v.y != 0.f) + (v.z != 0.f);
+  }
+  c = static_cast<int>(WaveSum(static_cast<float>(c)));
+  __shared__ int ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void write_nz_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per, const int64_t* __restrict__ base,
+                                uint64_t* __restrict__ oidx, float* __restrict__ oval) {
+  // one thread per block keeps the records in slot order (the host model's order) - blocks are small
+  if (threadIdx.x != 0) return;
+  const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * per, s1 = min(nw, s0 + per);
+  int64_t o = base[blockIdx.x];
+  for (uint64_t s = s0; s < s1; ++s) {
+    const float4 v = W[s];
+    if (v.x != 0.f) { oidx[o] = 4 * s; oval[o++] = v.x; }
+    if (v.y != 0.f) { oidx[o] = 4 * s + 1; oval[o++] = v.y; }
+    if (v.z != 0.f) { oidx[o] = 4 * s + 2; oval[o++] = v.z; }
+  }
+}
+
+__global__ void scatter_kernel(float4* __restrict__ W, uint64_t nw, const uint64_t* __restrict__ idx,
+                               const float* __restrict__ val, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t s = idx[i] >> 2;
+    const int c = static_cast<int>(idx[i] & 3);
+    if (s < nw && c < 3) reinterpret_cast<float*>(&W[s])[c] = val[i];
+  }
 }
 
 }  // namespace
@@ -133,25 +336,36 @@ __global__ void scale_kernel(float* w, uint64_t n, float s) {
 struct GpuSgd::Impl {
   hipStream_t stream = nullptr, copy_stream = nullptr;
   std::vector<hipEvent_t> events;
-  float2* W = nullptr;
+  float4* W = nullptr;
   uint64_t nw = 0;
+  uint8_t* dirty = nullptr;
+  int64_t nblk = 0;
+  double* gs = nullptr;
   int64_t* indptr = nullptr;
   uint32_t* idx = nullptr;
-  float *val = nullptr, *lab = nullptr, *wt = nullptr, *pred = nullptr, *loss = nullptr;
+  float *val = nullptr, *lab = nullptr, *wt = nullptr, *lo = nullptr, *hi = nullptr, *pred = nullptr, *loss = nullptr;
   size_t cap_rows = 0, cap_nnz = 0;
+  // sync scratch
+  int32_t *pos = nullptr, *blocks = nullptr;
+  float *sums = nullptr, *nmax = nullptr;
+  size_t cap_sync = 0;
   void Reserve(size_t rows, size_t nnz) {
     if (rows > cap_rows) {
-      (void)hipFree(indptr); (void)hipFree(lab); (void)hipFree(wt); (void)hipFree(pred);
+      for (void* q : {static_cast<void*>(indptr), static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo),
+                      static_cast<void*>(hi), static_cast<void*>(pred)})
+        (void)hipFree(q);
       VW_HIP_CHECK(hipMalloc(&indptr, (rows + 1) * sizeof(int64_t)));
       VW_HIP_CHECK(hipMalloc(&lab, rows * sizeof(float)));
       VW_HIP_CHECK(hipMalloc(&wt, rows * sizeof(float)));
+      VW_HIP_CHECK(hipMalloc(&lo, rows * sizeof(float)));
+      VW_HIP_CHECK(hipMalloc(&hi, rows * sizeof(float)));
       VW_HIP_CHECK(hipMalloc(&pred, rows * sizeof(float)));
       cap_rows = rows;
     }
     if (nnz > cap_nnz) {
       (void)hipFree(idx); (void)hipFree(val);
-      VW_HIP_CHECK(hipMalloc(&idx, nnz * sizeof(uint32_t)));
-      VW_HIP_CHECK(hipMalloc(&val, nnz * sizeof(float)));
+      VW_HIP_CHECK(hipMalloc(&idx, std::max<size_t>(1, nnz) * sizeof(uint32_t)));
+      VW_HIP_CHECK(hipMalloc(&val, std::max<size_t>(1, nnz) * sizeof(float)));
       cap_nnz = nnz;
     }
   }
@@ -160,8 +374,12 @@ struct GpuSgd::Impl {
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    (void)hipFree(W); (void)hipFree(indptr); (void)hipFree(idx); (void)hipFree(val);
-    (void)hipFree(lab); (void)hipFree(wt); (void)hipFree(pred); (void)hipFree(loss);
+    for (void* q : {static_cast<void*>(W), static_cast<void*>(dirty), static_cast<void*>(gs),
+                    static_cast<void*>(indptr), static_cast<void*>(idx), static_cast<void*>(val),
+                    static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo), static_cast<void*>(hi),
+                    static_cast<void*>(pred), static_cast<void*>(loss), static_cast<void*>(pos),
+                    static_cast<void*>(blocks), static_cast<void*>(sums), static_cast<void*>(nmax)})
+      (void)hipFree(q);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -204,17 +422,53 @@ bool VwGpuAvailable() {
 
 GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cfg) {
   if (device >= 0) VW_HIP_CHECK(hipSetDevice(device));
+  if (cfg.oaa > 256) throw std::runtime_error("GPU oaa supports at most 256 classes");
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
   impl_->nw = 1ull << cfg.bits;
-  VW_HIP_CHECK(hipMalloc(&impl_->W, impl_->nw * sizeof(float2)));
-  VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float2), impl_->stream));
+  VW_HIP_CHECK(hipMalloc(&impl_->W, impl_->nw * sizeof(float4)));
+  VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), impl_->stream));
+  impl_->nblk = static_cast<int64_t>((impl_->nw + (1ull << kDirtyShift) - 1) >> kDirtyShift);
+  VW_HIP_CHECK(hipMalloc(&impl_->dirty, impl_->nblk));
+  VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, impl_->nblk, impl_->stream));
+  VW_HIP_CHECK(hipMalloc(&impl_->gs, 3 * sizeof(double)));
+  VW_HIP_CHECK(hipMemsetAsync(impl_->gs, 0, 3 * sizeof(double), impl_->stream));
   VW_HIP_CHECK(hipMalloc(&impl_->loss, sizeof(float)));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), impl_->stream));
   VW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
+  if (cfg.loss == 1) { min_label_ = -50.0; max_label_ = 50.0; }
 }
 
 GpuSgd::~GpuSgd() = default;
+
+namespace {
+SgdArgs BaseArgs(const GpuSgdConfig& c) {
+  SgdArgs a{};
+  a.lr = c.lr; a.power_t = c.power_t; a.initial_t = c.initial_t; a.l2 = c.l2; a.loss = c.loss;
+  a.adaptive = c.adaptive ? 1 : 0; a.normalized = c.normalized ? 1 : 0; a.invariant = c.invariant ? 1 : 0;
+  a.K = c.oaa;
+  return a;
+}
+}  // namespace
+
+void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
+  SgdArgs a = BaseArgs(cfg_);
+  a.indptr = impl_->indptr; a.idx = impl_->idx; a.val = impl_->val; a.lab = impl_->lab;
+  a.wt = have_weights ? impl_->wt : nullptr;
+  a.lo = (learn && cfg_.oaa == 0) ? impl_->lo : nullptr;
+  a.hi = impl_->hi;
+  a.n0 = b0; a.n1 = b1; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
+  a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = learn ? 1 : 0;
+  if (cfg_.oaa > 0) {
+    const int waves = std::min(cfg_.oaa, kOaaMaxWaves);
+    hipLaunchKernelGGL(oaa_kernel, dim3(static_cast<unsigned>(b1 - b0)), dim3(64 * waves), sizeof(float) * cfg_.oaa,
+                       impl_->stream, a);
+  } else {
+    const int grid = static_cast<int>((b1 - b0 + 3) / 4);
+    hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, impl_->stream, a);
+  }
+  VW_HIP_CHECK(hipGetLastError());
+}
 
 void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
                    const float* weights, int64_t n, int batch, float* preds_out) {
@@ -224,23 +478,33 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
   hipStream_t s = impl_->stream, cs = impl_->copy_stream;
   std::vector<int64_t> ip(indptr, indptr + n + 1);
   for (auto& v : ip) v -= indptr[0];
+  // the sequential learner's running label range (squared loss: starts at [0, 0], grows with every label
+  // before the example is predicted; logistic: fixed [-50, 50]) -> per-example clamp bounds
+  std::vector<float> lo(n), hi(n);
+  for (int64_t i = 0; i < n; ++i) {
+    if (cfg_.loss != 1 && cfg_.oaa == 0) {
+      min_label_ = std::min<double>(min_label_, labels[i]);
+      max_label_ = std::max<double>(max_label_, labels[i]);
+    }
+    lo[i] = static_cast<float>(min_label_);
+    hi[i] = static_cast<float>(max_label_);
+  }
   VW_HIP_CHECK(hipMemcpyAsync(impl_->indptr, ip.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   VW_HIP_CHECK(hipMemcpyAsync(impl_->lab, labels, n * sizeof(float), hipMemcpyHostToDevice, s));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->lo, lo.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->hi, hi.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
   if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), s));
-  const uint64_t mask = impl_->nw - 1;
   batch = std::max(1, batch);
   // The pass's feature ids / values stream in chunks of 16 mini-batches on a copy stream: the
   // (host-blocking, pageable) copy of chunk k+1 runs while the device learns chunk k, so the
   // host->device traffic (8 B per nonzero) hides behind the SGD instead of preceding it.
   const int64_t chunk_rows = static_cast<int64_t>(batch) * 16;
   const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
-  if (impl_->events.size() < static_cast<size_t>(nchunks)) {
-    for (size_t i = impl_->events.size(); i < static_cast<size_t>(nchunks); ++i) {
-      hipEvent_t e;
-      VW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      impl_->events.push_back(e);
-    }
+  for (size_t i = impl_->events.size(); i < static_cast<size_t>(nchunks); ++i) {
+    hipEvent_t e;
+    VW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    impl_->events.push_back(e);
   }
   auto copy_chunk = [&](int64_t c) {
     const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
@@ -257,15 +521,7 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
   for (int64_t c = 0; c < nchunks; ++c) {
     VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
     const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
-    for (int64_t b0 = r0; b0 < r1; b0 += batch) {
-      const int64_t b1 = std::min<int64_t>(r1, b0 + batch);
-      const float eta = static_cast<float>(std::pow(examples_ + b0 + 1.0, -static_cast<double>(cfg_.power_t)));
-      const int grid = static_cast<int>((b1 - b0 + kWavesPerBlock - 1) / kWavesPerBlock);
-      hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(64 * kWavesPerBlock), 0, s, impl_->indptr, impl_->idx,
-                         impl_->val, impl_->lab, weights ? impl_->wt : nullptr, b0, b1, impl_->W, mask, cfg_.lr,
-                         cfg_.l2, cfg_.loss, cfg_.adaptive ? 1 : 0, eta, impl_->pred, impl_->loss, 1);
-      VW_HIP_CHECK(hipGetLastError());
-    }
+    for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, weights != nullptr);
     if (c + 1 < nchunks) copy_chunk(c + 1);
   }
   float l = 0;
@@ -283,42 +539,145 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
   hipStream_t s = impl_->stream;
   std::vector<int64_t> ip(indptr, indptr + n + 1);
   for (auto& v : ip) v -= indptr[0];
+  std::vector<float> lo(n, static_cast<float>(min_label_)), hi(n, static_cast<float>(max_label_));
   VW_HIP_CHECK(hipMemcpyAsync(impl_->indptr, ip.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  VW_HIP_CHECK(hipMemcpyAsync(impl_->idx, indices + indptr[0], nnz * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  VW_HIP_CHECK(hipMemcpyAsync(impl_->val, values + indptr[0], nnz * sizeof(float), hipMemcpyHostToDevice, s));
-  const int grid = static_cast<int>((n + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(64 * kWavesPerBlock), 0, s, impl_->indptr, impl_->idx, impl_->val,
-                     nullptr, nullptr, int64_t(0), n, impl_->W, impl_->nw - 1, 0.f, 0.f, 0, 0, 0.f, impl_->pred,
-                     impl_->loss, 0);
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->lo, lo.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->hi, hi.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+  if (nnz) {
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->idx, indices + indptr[0], nnz * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->val, values + indptr[0], nnz * sizeof(float), hipMemcpyHostToDevice, s));
+  }
+  SgdArgs a = BaseArgs(cfg_);
+  a.indptr = impl_->indptr; a.idx = impl_->idx; a.val = impl_->val;
+  a.lo = cfg_.oaa == 0 ? impl_->lo : nullptr; a.hi = impl_->hi;
+  a.n0 = 0; a.n1 = n; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
+  a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = 0;
+  if (cfg_.oaa > 0) {
+    const int waves = std::min(cfg_.oaa, kOaaMaxWaves);
+    hipLaunchKernelGGL(oaa_kernel, dim3(static_cast<unsigned>(n)), dim3(64 * waves), sizeof(float) * cfg_.oaa, s, a);
+  } else {
+    hipLaunchKernelGGL(sgd_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0, s, a);
+  }
   VW_HIP_CHECK(hipGetLastError());
   VW_HIP_CHECK(hipMemcpyAsync(out, impl_->pred, n * sizeof(float), hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+// Average the table over ranks: only the 64 KB blocks some rank touched since the last sync (the union
+// of the dirty maps, one small max-allreduce) are packed, reduced (sum of {w, wG, G}, max of N) and
+// unpacked with VW's weighted averaging - no host staging, and a sparse pass moves a fraction of the table.
 void GpuSgd::AllReduceAverage(void* comm, int world) {
-  if (world < 1 || !comm) return;  // a world-1 communicator still runs the collective (one-GPU tests)
+  if (world < 1 || !comm) return;  // a world-1 communicator still runs the collectives (one-GPU tests)
   hipStream_t s = impl_->stream;
   ncclComm_t c = static_cast<ncclComm_t>(comm);
-  const uint64_t nf = impl_->nw * 2;
-  ncclResult_t r = ncclAllReduce(impl_->W, impl_->W, nf, ncclFloat, ncclSum, c, s);
-  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL allreduce failed: ") + ncclGetErrorString(r));
-  hipLaunchKernelGGL(scale_kernel, dim3(4096), dim3(256), 0, s, reinterpret_cast<float*>(impl_->W), nf, 1.f / world);
-  VW_HIP_CHECK(hipGetLastError());
+  auto nccl = [](ncclResult_t r) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL allreduce failed: ") + ncclGetErrorString(r));
+  };
+  const int64_t nblk = impl_->nblk;
+  nccl(ncclAllReduce(impl_->dirty, impl_->dirty, nblk, ncclUint8, ncclMax, c, s));
+  // deterministic compaction (every rank packs the same blocks in the same order): host prefix over the map
+  std::vector<uint8_t> hd(nblk);
+  VW_HIP_CHECK(hipMemcpyAsync(hd.data(), impl_->dirty, nblk, hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<int32_t> list;
+  for (int64_t i = 0; i < nblk; ++i) if (hd[i]) list.push_back(static_cast<int32_t>(i));
+  const int64_t m = static_cast<int64_t>(list.size());
+  last_sync_bytes_ = 0;
+  if (m > 0) {
+    const size_t slots = static_cast<size_t>(m) << kDirtyShift;
+    if (slots > impl_->cap_sync) {
+      (void)hipFree(impl_->blocks); (void)hipFree(impl_->sums); (void)hipFree(impl_->nmax);
+      VW_HIP_CHECK(hipMalloc(&impl_->blocks, nblk * sizeof(int32_t)));
+      VW_HIP_CHECK(hipMalloc(&impl_->sums, slots * 3 * sizeof(float)));
+      VW_HIP_CHECK(hipMalloc(&impl_->nmax, slots * sizeof(float)));
+      impl_->cap_sync = slots;
+    }
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->blocks, list.data(), m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const int grid = static_cast<int>(std::min<size_t>(65536, (slots + 255) / 256));
+    const int adaptive = cfg_.adaptive ? 1 : 0;
+    hipLaunchKernelGGL(pack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
+                       impl_->sums, impl_->nmax);
+    VW_HIP_CHECK(hipGetLastError());
+    nccl(ncclAllReduce(impl_->sums, impl_->sums, slots * 3, ncclFloat, ncclSum, c, s));
+    nccl(ncclAllReduce(impl_->nmax, impl_->nmax, slots, ncclFloat, ncclMax, c, s));
+    hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
+                       1.f / world, impl_->sums, impl_->nmax);
+    VW_HIP_CHECK(hipGetLastError());
+    last_sync_bytes_ = static_cast<int64_t>(slots) * 4 * sizeof(float) + nblk;
+  }
+  VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, nblk, s));
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  last_sync_blocks_ = m;
 }
 
 uint64_t GpuSgd::NumWeights() const { return impl_->nw; }
 
-void GpuSgd::CopyWeights(float* host_out) const {
-  std::vector<float2> tmp(impl_->nw);
-  VW_HIP_CHECK(hipMemcpy(tmp.data(), impl_->W, impl_->nw * sizeof(float2), hipMemcpyDeviceToHost));
-  for (uint64_t i = 0; i < impl_->nw; ++i) host_out[i] = tmp[i].x;
+// Nonzero table components as (stride-4 index, value), compacted on the device: the host only ever holds
+// the nonzeros (a 2^30-slot table never crosses PCIe whole)
+void GpuSgd::ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val) const {
+  hipStream_t s = impl_->stream;
+  const uint64_t per = 4096;
+  const int64_t nb = static_cast<int64_t>((impl_->nw + per - 1) / per);
+  int32_t* cnt = nullptr;
+  int64_t* base = nullptr;
+  VW_HIP_CHECK(hipMalloc(&cnt, nb * sizeof(int32_t)));
+  VW_HIP_CHECK(hipMalloc(&base, nb * sizeof(int64_t)));
+  hipLaunchKernelGGL(count_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, s, impl_->W, impl_->nw, per, cnt);
+  std::vector<int32_t> hc(nb);
+  VW_HIP_CHECK(hipMemcpyAsync(hc.data(), cnt, nb * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<int64_t> hb(nb);
+  int64_t tot = 0;
+  for (int64_t i = 0; i < nb; ++i) { hb[i] = tot; tot += hc[i]; }
+  idx->resize(tot);
+  val->resize(tot);
+  if (tot > 0) {
+    uint64_t* di = nullptr;
+    float* dv = nullptr;
+    VW_HIP_CHECK(hipMalloc(&di, tot * sizeof(uint64_t)));
+    VW_HIP_CHECK(hipMalloc(&dv, tot * sizeof(float)));
+    VW_HIP_CHECK(hipMemcpyAsync(base, hb.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(write_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw, per, base,
+                       di, dv);
+    VW_HIP_CHECK(hipMemcpyAsync(idx->data(), di, tot * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    VW_HIP_CHECK(hipMemcpyAsync(val->data(), dv, tot * sizeof(float), hipMemcpyDeviceToHost, s));
+    VW_HIP_CHECK(hipStreamSynchronize(s));
+    (void)hipFree(di);
+    (void)hipFree(dv);
+  }
+  (void)hipFree(cnt);
+  (void)hipFree(base);
 }
 
-void GpuSgd::SetWeights(const float* host_in) {
-  std::vector<float2> tmp(impl_->nw);
-  for (uint64_t i = 0; i < impl_->nw; ++i) tmp[i] = make_float2(host_in[i], 0.f);
-  VW_HIP_CHECK(hipMemcpy(impl_->W, tmp.data(), impl_->nw * sizeof(float2), hipMemcpyHostToDevice));
+void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val) {
+  hipStream_t s = impl_->stream;
+  VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), s));
+  const int64_t n = static_cast<int64_t>(idx.size());
+  if (n > 0) {
+    uint64_t* di = nullptr;
+    float* dv = nullptr;
+    VW_HIP_CHECK(hipMalloc(&di, n * sizeof(uint64_t)));
+    VW_HIP_CHECK(hipMalloc(&dv, n * sizeof(float)));
+    VW_HIP_CHECK(hipMemcpyAsync(di, idx.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(dv, val.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(scatter_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(65536, (n + 255) / 256))), dim3(256),
+                       0, s, impl_->W, impl_->nw, di, dv, n);
+    VW_HIP_CHECK(hipStreamSynchronize(s));
+    (void)hipFree(di);
+    (void)hipFree(dv);
+  }
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void GpuSgd::GlobalState(double* t, double* total_weight, double* sum_norm_x) const {
+  double h[3] = {0, 0, 0};
+  VW_HIP_CHECK(hipMemcpy(h, impl_->gs, sizeof(h), hipMemcpyDeviceToHost));
+  *t = h[0]; *total_weight = h[1]; *sum_norm_x = h[2];
+}
+
+void GpuSgd::SetGlobalState(double t, double total_weight, double sum_norm_x) {
+  const double h[3] = {t, total_weight, sum_norm_x};
+  VW_HIP_CHECK(hipMemcpy(impl_->gs, h, sizeof(h), hipMemcpyHostToDevice));
 }
 
 void* GpuSgd::weights_device() { return impl_->W; }

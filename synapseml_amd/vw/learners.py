@@ -143,8 +143,6 @@ def _host_allreduce_f32(arr: np.ndarray) -> None:
         D._dist().all_reduce(t)
 
 
-_GPU_UNSUPPORTED = re.compile(r"(^|\s)(--cubic|--oaa|--csoaa|--cb\w*|--ngram|--l1|"
-                              r"--ignore|--passes\s+0)(\s|$)")
 _nccl_cache: dict = {}
 
 
@@ -219,81 +217,103 @@ def _interaction_block(blocks, pair: str, n: int):
     return (pair, indptr, idx.astype(np.uint32), val)
 
 
-def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
-    """Device-resident hogwild mini-batch SGD (csrc/vw/vw_gpu.hip, K12).
+class _GpuTrainedModel:
+    """What the training loop hands back from the GPU learner: the model bytes (host learner format, built
+    from the device table's nonzeros - the table itself never crosses to the host) and the identifying
+    args, with the same surface the CPU learner's native object offers _fit (save_model / args / ...)."""
 
-    Scope: linear squared/logistic learners (regressor / binary classifier)
-    with AdaGrad (default) or plain SGD steps; the trained table is imported
-    into a native VW model so save/load/readable-model/prediction are shared
-    with the CPU learner. Reductions, interactions and l1 stay on the exact
-    sequential CPU learner and are rejected here rather than silently run
-    elsewhere. Weight averaging across ranks at pass boundaries uses RCCL
-    (``nccl`` backend) on the learner's stream."""
+    def __init__(self, model: bytes, args: str, info: dict):
+        self._model, self.args = model, args
+        self.hash_seed, self.num_bits = int(info["hash_seed"]), int(info["bits"])
+
+    def save_model(self) -> bytes:
+        return self._model
+
+
+def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
+    """Device-resident hogwild mini-batch learner (csrc/vw/vw_gpu.hip, K12).
+
+    Runs VW's update rule - adaptive + normalized + invariant by default, or the subset the command line
+    selects (--sgd / --adaptive / --normalized / --invariant) - for squared / logistic loss, scalar
+    learners and --oaa K, with -q interactions expanded on the host. gpuBatchSize=1 is the exact
+    sequential learner; larger batches update concurrently with atomics (hogwild). csoaa, contextual
+    bandits, CATS, l1, ngrams, ignore and cubic interactions run on the CPU learner and are rejected here
+    rather than silently run elsewhere. Ranks average the blocks they touched at every sync with RCCL
+    (VW's weighted averaging), and the model is exported from the device nonzeros."""
     vwmod = _vw()
+    info = vwmod.describe_args(args)  # parses + validates the command line without a host table
+    bad = [k for k in ("csoaa", "cats", "ngram") if int(info[k])] + (["cb_adf"] if info["cb_adf"] == "1" else []) + \
+        (["l1"] if float(info["l1"]) else []) + (["ignore"] if info["ignore"] else []) + \
+        (["loss_function " + info["loss_function"]] if info["loss_function"] not in ("squared", "logistic") else []) + \
+        (["cubic interactions"] if any(len(q) > 2 for q in info["interactions"].split(",") if q) else [])
+    if bad:
+        raise ValueError(f"deviceType='gpu' does not run {', '.join(bad)}; use deviceType='cpu' (args: {args})")
     if not vwmod.gpu_available():
         raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
-    if _GPU_UNSUPPORTED.search(" " + args + " "):
-        raise ValueError(f"deviceType='gpu' supports linear squared/logistic learners only; got args: {args}")
-    ref = vwmod.VW(args)  # parses & validates args, owns the final model
     cfg = vwmod.GpuSgdConfig()
-    cfg.bits = int(ref.num_bits)
-    m = re.search(r"(?:^|\s)(?:-l|--learning_rate)\s+(\S+)", args)
-    cfg.lr = float(m.group(1)) if m else 0.5
-    m = re.search(r"--power_t\s+(\S+)", args)
-    cfg.power_t = float(m.group(1)) if m else 0.5
-    m = re.search(r"--l2\s+(\S+)", args)
-    cfg.l2 = float(m.group(1)) if m else 0.0
-    cfg.loss = 1 if re.search(r"--loss_function\s+logistic", args) else 0
-    cfg.adaptive = "--sgd" not in args
+    cfg.bits = int(info["bits"])
+    cfg.lr = float(info["learning_rate"])
+    cfg.power_t = float(info["power_t"])
+    cfg.initial_t = float(info["initial_t"])
+    cfg.l2 = float(info["l2"])
+    cfg.loss = 1 if info["loss_function"] == "logistic" else 0
+    cfg.adaptive, cfg.normalized, cfg.invariant = (info[k] == "1" for k in ("adaptive", "normalized", "invariant"))
+    cfg.oaa = int(info["oaa"])
     import os
 
     dev = int(os.environ.get("LOCAL_RANK", "0"))
     g = vwmod.GpuSgd(cfg, dev)
-    if model_bytes is not None:  # initialModel: warm-start the device table (AdaGrad state starts fresh)
-        g.set_weights(np.ascontiguousarray(vwmod.VW(args, bytes(model_bytes)).weights(), np.float32))
+    if model_bytes is not None:  # initialModel: warm start (weights, adaptive / normalizer state, schedule)
+        g.import_model(bytes(model_bytes))
     t0 = time.perf_counter_ns()
     cols = [est.getFeaturesCol()] + list(est.getAdditionalFeatures() or [])
     blocks = namespace_blocks(df, cols, est.getHashSeed())
-    labels, _, _ = est._labels(df)
+    labels, multiclass, _ = est._labels(df)
+    if cfg.oaa > 0:
+        if multiclass is None:
+            raise ValueError("--oaa needs integer class labels")
+        labels = np.asarray(multiclass, np.float32)
     n = df.count()
     blocks = blocks + [_interaction_block(blocks, pq, n) for pq in _quadratic_pairs(args)]
-    indptr, idx, val = _merged_csr(blocks, n, "--noconstant" not in args)
+    indptr, idx, val = _merged_csr(blocks, n, info["constant"] == "1")
     wcol = est.getWeightCol()
     weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
     t1 = time.perf_counter_ns()
     world = D.world_size()
     comm = None
-    if world > 1 and D.backend() == "nccl":
+    if world > 1:
+        if D.backend() != "nccl":
+            raise RuntimeError("the GPU VW learner averages over RCCL: start the ranks with the nccl backend")
         key = world
         if key not in _nccl_cache:
             uid = vwmod.nccl_unique_id() if D.rank() == 0 else None
             _nccl_cache[key] = vwmod.nccl_comm(D.broadcast_object(uid, 0), D.rank(), world)
         comm = _nccl_cache[key]
-    # numSyncsPerPass: the same number of weight averages on every rank (row-count independent,
-    # VowpalWabbitSyncSchedule.scala:36-72); the last one is the end-of-pass sync
-    syncs = max(1, int(est.getNumSyncsPerPass() or 0))
-    bounds = np.linspace(0, n, syncs + 1).astype(np.int64)
+    # numSyncsPerPass intermediate weight averages + the end-of-pass one, the same count on every rank
+    # whatever its row count (VowpalWabbitSyncSchedule.scala:36-72)
+    segs = max(0, int(est.getNumSyncsPerPass() or 0)) + 1
+    bounds = np.linspace(0, n, segs + 1).astype(np.int64)
+    sync_bytes = []
     for _ in range(max(1, est.getNumPasses())):
         for s0, s1 in zip(bounds[:-1], bounds[1:]):
             if s1 > s0:
                 ip = indptr[s0:s1 + 1]
                 g.learn(ip - ip[0], idx[ip[0]:ip[-1]], val[ip[0]:ip[-1]], labels[s0:s1],
                         None if weights is None else weights[s0:s1], int(est.getGpuBatchSize()))
-            if world > 1:
-                if comm is not None:
-                    g.allreduce_average(comm)
-                else:
-                    w = np.ascontiguousarray(g.weights(), np.float32)
-                    _host_allreduce_f32(w)
-                    g.set_weights(w / world)
+            if comm is not None:
+                g.allreduce_average(comm)
+                sync_bytes.append(int(g.last_sync_bytes))
     t2 = time.perf_counter_ns()
-    lab = labels.astype(np.float64)
+    lab = np.asarray(labels, np.float64)
     wts = np.ones(n) if weights is None else weights.astype(np.float64)
-    vwmod.import_linear(ref, np.asarray(g.weights(), np.float32), float(g.examples), float((lab * wts).sum()),
-                        float(g.sum_loss), float(lab.min()) if n else 0.0, float(lab.max()) if n else 0.0)
-    stats = ref.stats()
-    stats.update(timeTotalNs=t2 - t0, timeNativeIngestNs=t1 - t0, timeLearnNs=t2 - t1, timeMultipassNs=0)
-    return ref, stats
+    wsum = float(wts.sum())
+    stats = {"numberOfExamplesPerPass": int(n), "weightedExampleSum": wsum,
+             "weightedLabelSum": float((lab * wts).sum()), "averageLoss": float(g.sum_loss) / max(wsum, 1e-300),
+             "bestConstant": float((lab * wts).sum()) / max(wsum, 1e-300), "totalNumberOfFeatures": float(len(idx)),
+             "passes": int(max(1, est.getNumPasses())), "ipsEstimate": 0.0, "snipsEstimate": 0.0,
+             "syncBytes": int(sum(sync_bytes)), "timeTotalNs": t2 - t0, "timeNativeIngestNs": t1 - t0,
+             "timeLearnNs": t2 - t1, "timeMultipassNs": 0}
+    return _GpuTrainedModel(g.export_model(args), args, info), stats
 
 
 class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
@@ -432,6 +452,7 @@ class VowpalWabbitBase(Estimator, VowpalWabbitBaseParams, HasLabelCol, HasWeight
                 vw, stats = self._train_partition(p, args, model)
                 models.append(vw)
             if models:
+                models = [_vw().VW(args, m.save_model()) if isinstance(m, _GpuTrainedModel) else m for m in models]
                 vw = _vw().merge_models(models) if len(models) > 1 else models[0]
                 model = bytes(vw.save_model())
         return vw, stats

@@ -75,24 +75,27 @@ def test_gbdt_data_parallel_path_on_world1_rccl(monkeypatch):
 
 
 def test_vw_gpu_allreduce_average_world1():
-    """GpuSgd::AllReduceAverage on a world-1 RCCL communicator (ncclAllReduce + 1/world scale): the
-    averaged weights equal the local weights."""
+    """GpuSgd::AllReduceAverage on a world-1 RCCL communicator (weighted ncclAllReduce of the touched
+    blocks, divided by the summed weight): the exported model is unchanged and the sync moved bytes."""
     from synapseml_amd.ops import native
 
     vw = native.load("_vw")
     cfg = vw.GpuSgdConfig()
     cfg.bits = 16
-    cfg.lr = 0.5
-    sgd = vw.GpuSgd(cfg)
+    cfg.loss = 1
+    sgd = vw.GpuSgd(cfg, 0)
     rng = np.random.default_rng(0)
     n, k = 4000, 8
     idx = rng.integers(0, 1 << 16, size=n * k).astype(np.uint32)
     val = rng.standard_normal(n * k).astype(np.float32)
     ip = np.arange(0, n * k + 1, k, dtype=np.int64)
     lab = (rng.random(n) > 0.5).astype(np.float32) * 2 - 1
-    sgd.learn(ip, idx, val, lab)
-    w0 = sgd.weights().copy()
-    assert np.abs(w0).sum() > 0
+    sgd.learn(ip, idx, val, lab, None, 64)
+    m0 = sgd.export_model("--loss_function logistic -b 16")
+    p0 = sgd.predict(ip, idx, val)
+    assert np.abs(p0).sum() > 0
     comm = vw.nccl_comm(vw.nccl_unique_id(), 0, 1)
     sgd.allreduce_average(comm)
-    np.testing.assert_array_equal(sgd.weights(), w0)
+    assert sgd.last_sync_bytes > 0 and sgd.last_sync_blocks > 0
+    np.testing.assert_allclose(sgd.predict(ip, idx, val), p0, rtol=1e-6, atol=1e-6)
+    assert len(sgd.export_model("--loss_function logistic -b 16")) == len(m0)

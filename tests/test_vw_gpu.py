@@ -25,6 +25,17 @@ def test_merged_csr_matches_blocks():
     assert idx[2] == 11650396 and idx[4] == 11650396
 
 
+@pytest.mark.parametrize("args", ["--csoaa 3", "--cb_explore_adf", "--cats 4 --bandwidth 1 --min_value 0 --max_value 1",
+                                  "--l1 0.001", "--ngram 2", "--ignore a", "--loss_function hinge",
+                                  "--interactions abc"])
+def test_gpu_rejects_reductions_it_does_not_run(args):
+    """Reductions the device learner does not implement are refused by name before any GPU work,
+    never silently run on the host."""
+    df, _ = _binary(n=50)
+    with pytest.raises(ValueError, match="deviceType='gpu' does not run"):
+        VowpalWabbitRegressor(deviceType="gpu", passThroughArgs=args).fit(df)
+
+
 def test_gpu_request_without_gpu_fails_loudly():
     if native.load("_vw").gpu_available():
         pytest.skip("GPU present")
@@ -93,3 +104,39 @@ def test_murmur_batch_kernel_matches_host():
     for seed, mask in ((0, 0xFFFFFFFF), (2493003127, (1 << 18) - 1)):
         np.testing.assert_array_equal(hash_strings(xs, seed, mask, device="gpu"),
                                       hash_strings(xs, seed, mask, device="cpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", ["", "--sgd", "--adaptive", "--normalized --invariant", "--loss_function logistic -l 0.3"])
+def test_gpu_batch1_is_the_sequential_learner(args):
+    """gpuBatchSize=1 runs VW's update rule example by example: on mixed-scale features (where the
+    normalized update matters) the exported GPU model predicts like the exact host learner's."""
+    rng = np.random.default_rng(5)
+    n = 3000
+    X = rng.normal(size=(n, 6)) * np.array([1e-2, 1.0, 30.0, 1.0, 5.0, 0.3])
+    y = X @ np.array([20.0, -1.0, 0.05, 0.7, 0.2, 2.0]) + 0.05 * rng.normal(size=n)
+    if "logistic" in args:
+        y = np.where(y > 0, 1.0, -1.0)
+    df = DataFrame({"features": X, "label": y})
+    kw = dict(passThroughArgs=args, numPasses=1)
+    g = VowpalWabbitRegressor(deviceType="gpu", gpuBatchSize=1, **kw).fit(df)
+    c = VowpalWabbitRegressor(**kw).fit(df)
+    pg, pc = g.transform(df)["prediction"], c.transform(df)["prediction"]
+    np.testing.assert_allclose(pg, pc, rtol=2e-3, atol=2e-3 * np.abs(pc).max())
+
+
+@pytest.mark.gpu
+def test_gpu_oaa_multiclass():
+    """--oaa K on the device (one wave per class per example): accuracy close to the host learner's."""
+    rng = np.random.default_rng(7)
+    n, d, K = 20000, 10, 4
+    X = rng.normal(size=(n, d))
+    W = rng.normal(size=(d, K))
+    y = (np.argmax(X @ W, 1) + 1).astype(np.float64)
+    df = DataFrame({"features": X, "label": y})
+    kw = dict(passThroughArgs=f"--oaa {K}", numClasses=K, numPasses=3)
+    g = VowpalWabbitClassifier(deviceType="gpu", gpuBatchSize=64, **kw).fit(df)
+    c = VowpalWabbitClassifier(**kw).fit(df)
+    acc = lambda m: float(np.mean(m.transform(df)["prediction"] == y))
+    ag, ac = acc(g), acc(c)
+    assert ag > 0.8 and ag > ac - 0.03, (ag, ac)

@@ -3,12 +3,13 @@
 BASELINE.json config "VowpalWabbitClassifier 1B-feature hashed sparse
 synthetic, 8xMI355X model allreduce".
 
-Per GPU: a 2^bits weight table (default 2^30 = 1B features, weight + AdaGrad
-state = 8 GiB resident in HBM), --rows examples per pass with ~--nnz hashed
+Per GPU: a 2^bits weight table (default 2^30 = 1B features; 16 B per slot:
+weight, adaptive sum of squared gradients, normalizer = 16 GiB resident in HBM), --rows examples per pass with ~--nnz hashed
 features each (32-bit hashed ids from a 2^24 vocabulary, Zipf-like). One step = one pass:
-host -> device transfer of the pass's CSR, hogwild AdaGrad SGD on the device
-(K12, logistic loss), then (N > 1) the endPass weight average over RCCL
-(the whole 2^bits table, bandwidth-bound over xGMI). Prints one
+host -> device transfer of the pass's CSR (overlapped with learning), hogwild
+mini-batches of VW's default adaptive + normalized + invariant update on the
+device (K12, logistic loss), then (N > 1) the endPass weighted average over
+RCCL of the 64 KiB table blocks some rank touched. Prints one
 JSON line with examples/s over all GPUs, the per-pass allreduce time and the
 held-out logistic loss. Synthetic data; labels from a planted sparse model."""
 from __future__ import annotations
@@ -81,8 +82,7 @@ def main() -> None:
     cfg.bits = args.bits
     cfg.lr = 0.5
     cfg.power_t = 0.5
-    cfg.loss = 1
-    cfg.adaptive = True
+    cfg.loss = 1  # adaptive / normalized / invariant default on, as in VW
     g = vw.GpuSgd(cfg, local_rank)
     comm = None
     if world > 1:
@@ -90,7 +90,7 @@ def main() -> None:
         comm = vw.nccl_comm(D.broadcast_object(uid, 0), rank, world)
     passes = [make_pass(args.rows, args.nnz, seed=1000 * rank + s) for s in range(2)]
     hold = make_pass(100_000, args.nnz, seed=999_999)
-    ar_ms = []
+    ar_ms, sync_mb = [], []
 
     def one_pass(i):
         ip, ix, vl, y = passes[i % 2]
@@ -99,12 +99,14 @@ def main() -> None:
             t = time.perf_counter()
             g.allreduce_average(comm)
             ar_ms.append((time.perf_counter() - t) * 1e3)
+            sync_mb.append(g.last_sync_bytes / 2 ** 20)
 
     for i in range(args.warmup):
         one_pass(i)
     torch.cuda.synchronize()
     D.barrier()
     ar_ms.clear()
+    sync_mb.clear()
     t0 = time.perf_counter()
     for i in range(args.steps):
         one_pass(i)
@@ -124,9 +126,10 @@ def main() -> None:
         print(json.dumps({
             "bench": "vw_hashed_sgd", "metric": "examples/sec VowpalWabbitClassifier (whole job)",
             "value": round(args.rows * world * args.steps / elapsed, 1), "n_gpus": world, "bits": args.bits,
-            "table_gib": round((2 ** args.bits) * 8 / 2 ** 30, 2), "rows_per_gpu_per_pass": args.rows,
+            "table_gib": round((2 ** args.bits) * 16 / 2 ** 30, 2), "rows_per_gpu_per_pass": args.rows,
             "nnz_per_row": args.nnz, "batch": args.batch, "ms_per_pass": round(elapsed / args.steps * 1e3, 2),
             "allreduce_ms_per_pass": round(float(np.mean(ar_ms)), 2) if ar_ms else None,
+            "allreduce_mib_per_pass": round(float(np.mean(sync_mb)), 1) if sync_mb else None,
             "holdout_logloss": round(logloss, 4),
             "data": "synthetic hashed sparse (2^24-id vocabulary of 32-bit hashes, Zipf-like popularity, planted model)"}), flush=True)
     if world > 1:

@@ -1,8 +1,11 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_onnx.py tests/test_conv_mfma.py -m gpu > gpurun_out/t3.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_vw_gpu.py tests/test_comm_gpu.py -m gpu > gpurun_out/vwt.log 2>&1
 rc=$?
-tail -15 gpurun_out/t3.log
-timeout -k 10 600 python tools/bench_onnx.py --batches 128 --precisions fp32,fp16 > gpurun_out/onnx1.log 2>&1
-tail -8 gpurun_out/onnx1.log
+tail -30 gpurun_out/vwt.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python tools/bench_vw.py --bits 26 --rows 1000000 --steps 3 > gpurun_out/vwb.log 2>&1
+rc=$?
+tail -3 gpurun_out/vwb.log
 exit $rc
