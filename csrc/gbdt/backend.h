@@ -5,6 +5,7 @@
 #pragma once
 #include <algorithm>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,25 @@ class TrainBackend {
   // Training-metric value computed where the scores live (K11); false = host path.
   virtual bool EvalOnDevice(const std::string& name, const Objective& obj, double* out) {
     (void)name; (void)obj; (void)out;
+    return false;
+  }
+  // K11 validation sets: the backend may keep a validation set's bins and scores where its own scores
+  // live (true: it now owns the scores, `scores` = the class-major start values); false = host-resident.
+  virtual bool AddValidSet(int vi, const Dataset& vd, const std::vector<double>& scores, const Config& cfg) {
+    (void)vi; (void)vd; (void)scores; (void)cfg;
+    return false;
+  }
+  // fold tree `t` (class k) into a backend-owned validation set's scores (ValidOp in valid_gpu.h)
+  virtual void ValidApplyTree(int vi, const Tree& t, int k, int op, double p) {
+    (void)vi; (void)t; (void)k; (void)op; (void)p;
+    throw std::logic_error("backend holds no validation sets");
+  }
+  virtual void GetValidScores(int vi, std::vector<double>* s) {
+    (void)vi; (void)s;
+    throw std::logic_error("backend holds no validation sets");
+  }
+  virtual bool EvalValidOnDevice(int vi, const std::string& name, const Objective& obj, double* out) {
+    (void)vi; (void)name; (void)obj; (void)out;
     return false;
   }
   virtual Tree TrainTree(int k, const std::vector<char>& feature_mask) = 0;

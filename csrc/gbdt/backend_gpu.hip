@@ -39,6 +39,7 @@
 #include "backend.h"
 #include "comm.h"
 #include "hip_common.h"
+#include "valid_gpu.h"
 
 namespace sml {
 namespace {
@@ -1997,6 +1998,7 @@ class GpuBackend : public TrainBackend {
  public:
   explicit GpuBackend(int dev) : dev_(dev) {}
   ~GpuBackend() override {
+    vsets_.clear();  // they sync on stream_ before it goes
     if (stream_) { (void)hipStreamSynchronize(stream_); (void)hipStreamDestroy(stream_); }
     for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
     if (ev_copy_) (void)hipEventDestroy(ev_copy_);
@@ -2313,8 +2315,33 @@ class GpuBackend : public TrainBackend {
   }
 
   bool EvalOnDevice(const std::string& name, const Objective& obj, double* out) override {
-    if (K_ != 1) return false;
-    return DeviceEvalMetric(name, obj.params(), score_.get(), label_.get(), weight_.get(), n_, stream_, out);
+    DeviceMetricInputs in;
+    in.score = score_.get(); in.label = label_.get(); in.weight = weight_.get(); in.n = n_; in.num_class = K_;
+    const bool rank = name.rfind("ndcg", 0) == 0 || name.rfind("map", 0) == 0;
+    if (rank) {
+      if (obj.params().kind != kObjLambdarank) return false;  // the query tables come with the objective
+      EnsureRankTables(obj);
+      in.qb = rank_qb_.get(); in.nq = rank_.nq; in.gain = rank_gain_.get(); in.ngain = rank_.ngain;
+    }
+    return DeviceEvalMetricFull(name, obj.params(), in, stream_, out);
+  }
+
+  // K11: validation sets live in HBM; every tree is folded into their scores by a device traversal and
+  // their metrics reduce on the device (valid_gpu.hip)
+  bool AddValidSet(int vi, const Dataset& vd, const std::vector<double>& scores, const Config& cfg) override {
+    if (vd.num_data >= (int64_t(1) << 31) || vd.row_stride < vd.ref.num_inner()) return false;
+    if (static_cast<int>(vsets_.size()) <= vi) vsets_.resize(vi + 1);
+    vsets_[vi].reset(new DeviceValidSet(vd, scores, K_, cfg.label_gain, dev_, stream_));
+    return true;
+  }
+  DeviceValidSet& VSet(int vi) {
+    if (vi < 0 || vi >= static_cast<int>(vsets_.size()) || !vsets_[vi]) throw std::logic_error("no device validation set");
+    return *vsets_[vi];
+  }
+  void ValidApplyTree(int vi, const Tree& t, int k, int op, double p) override { VSet(vi).ApplyTree(t, k, op, p); }
+  void GetValidScores(int vi, std::vector<double>* s) override { VSet(vi).GetScores(s); }
+  bool EvalValidOnDevice(int vi, const std::string& name, const Objective& obj, double* out) override {
+    return VSet(vi).Eval(name, obj.params(), K_, out);
   }
 
   void Synchronize() override {
@@ -2847,6 +2874,7 @@ class GpuBackend : public TrainBackend {
   bool rank_ready_ = false, rank_regs_ = false, rank_lds_ = false;
   RankTables rank_{};
   DevBuf<int32_t> rank_qb_, rank_scratch_;
+  std::vector<std::unique_ptr<DeviceValidSet>> vsets_;
   DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_;
   int32_t* flags_ = nullptr;
   DTree dt_{};

@@ -242,7 +242,8 @@ PYBIND11_MODULE(_gbdt, m) {
            },
            py::arg("grad") = py::none(), py::arg("hess") = py::none())
       .def("rollback_one_iter", &Booster::RollbackOneIter)
-      .def("eval", &Booster::Eval)
+      .def("eval", &Booster::Eval, py::arg("idx"), py::arg("device") = true,
+           "metrics of data set idx (0 = train); device=False forces the host reference path")
       .def("eval_names", &Booster::EvalNames)
       .def("truncate", &Booster::Truncate)
       .def("synchronize", [](Booster& b) { py::gil_scoped_release rel; b.Synchronize(); })
@@ -251,6 +252,7 @@ PYBIND11_MODULE(_gbdt, m) {
         b.GetTrainScores(&s);
         return py::array_t<double>(s.size(), s.data());
       })
+      .def("valid_on_device", [](const Booster& b, int i) { return b.ValidOnDevice(i); })
       .def("valid_scores", [](const Booster& b, int i) {
         std::vector<double> s;
         b.GetPredictForValid(i, &s);

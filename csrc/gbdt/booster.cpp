@@ -1,4 +1,5 @@
 #include "booster.h"
+#include "valid_gpu.h"
 
 #include <algorithm>
 #include <cmath>
@@ -123,24 +124,41 @@ void Booster::InitTraining() {
 }
 
 void Booster::AddValidData(std::shared_ptr<Dataset> valid, const std::string& name) {
-  valid->EnsureHostBins();  // validation scores are kept on the host
   const int K = num_tree_per_iter_;
   std::vector<double> s(static_cast<size_t>(valid->num_data) * K, 0.0);
   if (!valid->init_score.empty()) s = valid->init_score;
   else for (int k = 0; k < K; ++k) for (int64_t i = 0; i < valid->num_data; ++i) s[k * valid->num_data + i] += (trees_.empty() ? init_scores_[k] : 0.0);
-  // existing trees
-  for (size_t t = 0; t < trees_.size(); ++t) {
-    int k = static_cast<int>(t % K);
-    Tree tr = trees_[t];
-    for (int64_t i = 0; i < valid->num_data; ++i)
-      s[k * valid->num_data + i] += tr.leaf_value[tr.GetLeafByBins(&valid->bins[i * valid->row_stride], valid->ref.mappers, valid->ref.used_features)];
-  }
+  const size_t vi = valid_.size();
+  // K11: with a device backend the set's bins and scores stay in HBM (no host bins needed)
+  const bool on_dev = backend_ && backend_->AddValidSet(static_cast<int>(vi), *valid, s, cfg_);
+  if (!on_dev) valid->EnsureHostBins();
   std::unique_ptr<Objective> vo(new Objective(cfg_));
   vo->Init(*valid);
   valid_objectives_.push_back(std::move(vo));
   valid_.push_back(std::move(valid));
   valid_names_.push_back(name);
-  valid_scores_.push_back(std::move(s));
+  valid_dev_.push_back(on_dev ? 1 : 0);
+  valid_scores_.push_back(on_dev ? std::vector<double>() : std::move(s));
+  // existing trees
+  for (size_t t = 0; t < trees_.size(); ++t) ValidApply(vi, trees_[t], static_cast<int>(t % K), kValidAdd, 1.0);
+}
+
+void Booster::ValidApply(size_t vi, const Tree& t, int k, int op, double p) {
+  if (valid_dev_[vi]) {
+    backend_->ValidApplyTree(static_cast<int>(vi), t, k, op, p);
+    return;
+  }
+  auto& vd = valid_[vi];
+  double* vs = valid_scores_[vi].data() + static_cast<size_t>(k) * vd->num_data;
+  if (op == kValidConst) {
+    for (int64_t i = 0; i < vd->num_data; ++i) vs[i] = ValidFold(vs[i], 0.0, op, p);
+    return;
+  }
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < vd->num_data; ++i) {
+    const double o = t.leaf_value[t.GetLeafByBins(&vd->bins[i * vd->row_stride], vd->ref.mappers, vd->ref.used_features)];
+    vs[i] = ValidFold(vs[i], o, op, p);
+  }
 }
 
 void Booster::MergeFrom(const Booster& other) {
@@ -149,10 +167,8 @@ void Booster::MergeFrom(const Booster& other) {
   if (other.num_tree_per_iter_ != K) throw std::runtime_error("cannot merge models with different class counts");
   // Continued training: remove the boost-from-average offset, add the old trees.
   for (int k = 0; k < K; ++k) if (init_scores_[k] != 0.0) backend_->AddBias(k, -init_scores_[k]);
-  for (auto& v : valid_scores_) {
-    int64_t n = static_cast<int64_t>(v.size()) / K;
-    for (int k = 0; k < K; ++k) for (int64_t i = 0; i < n; ++i) v[k * n + i] -= init_scores_[k];
-  }
+  for (size_t vi = 0; vi < valid_.size(); ++vi)
+    for (int k = 0; k < K; ++k) ValidApply(vi, Tree(), k, kValidConst, -init_scores_[k]);
   init_scores_.assign(K, 0.0);
   std::vector<Tree> old = other.trees_;
   for (size_t t = 0; t < old.size(); ++t) {
@@ -160,11 +176,7 @@ void Booster::MergeFrom(const Booster& other) {
     const int k = static_cast<int>(t % K);
     const double scale = other.average_output_ ? 1.0 / std::max(1, other.CurrentIteration()) : 1.0;
     backend_->UpdateScore(old[t], k, scale);
-    for (size_t vi = 0; vi < valid_.size(); ++vi) {
-      auto& vd = valid_[vi];
-      for (int64_t i = 0; i < vd->num_data; ++i)
-        valid_scores_[vi][k * vd->num_data + i] += scale * old[t].leaf_value[old[t].GetLeafByBins(&vd->bins[i * vd->row_stride], vd->ref.mappers, vd->ref.used_features)];
-    }
+    for (size_t vi = 0; vi < valid_.size(); ++vi) ValidApply(vi, old[t], k, kValidAdd, scale);
   }
   trees_.insert(trees_.begin(), old.begin(), old.end());
   boosted_first_ = true;
@@ -366,36 +378,20 @@ bool Booster::TrainOneIter(const float* grad, const float* hess) {
         old.Shrink(factor);
         backend_->UpdateScore(old, k, 1.0);
         // valid scores: old contribution was unscaled; remove (1-factor) of it
-        for (size_t vi = 0; vi < valid_.size(); ++vi) {
-          auto& vd = valid_[vi];
-          for (int64_t i = 0; i < vd->num_data; ++i) {
-            double v = old.leaf_value[old.GetLeafByBins(&vd->bins[i * vd->row_stride], vd->ref.mappers, vd->ref.used_features)];
-            valid_scores_[vi][k * vd->num_data + i] += v - v / factor;
-          }
-        }
+        for (size_t vi = 0; vi < valid_.size(); ++vi) ValidApply(vi, old, k, kValidDart, factor);
       }
     }
   }
   // validation scores
   const int citer = CurrentIteration();
   for (size_t vi = 0; vi < valid_.size(); ++vi) {
-    auto& vd = valid_[vi];
     for (int k = 0; k < K; ++k) {
       const Tree& t = new_trees[k];
-      double* vs = valid_scores_[vi].data() + k * vd->num_data;
       if (is_rf) {
-        const double c = static_cast<double>(citer);
-        for (int64_t i = 0; i < vd->num_data; ++i) {
-          double out = t.leaf_value[t.GetLeafByBins(&vd->bins[i * vd->row_stride], vd->ref.mappers, vd->ref.used_features)];
-          if (c == 0) vs[i] = out; else vs[i] = (vs[i] * c + out) / (c + 1.0);
-        }
+        ValidApply(vi, t, k, kValidRfAvg, static_cast<double>(citer));
       } else {
-        bool first_bias = !boosted_first_ && citer == 0;
-        for (int64_t i = 0; i < vd->num_data; ++i) {
-          double out = t.leaf_value[t.GetLeafByBins(&vd->bins[i * vd->row_stride], vd->ref.mappers, vd->ref.used_features)];
-          if (first_bias) out -= init_scores_[k];  // valid scores already carry the init bias
-          vs[i] += out;
-        }
+        const bool first_bias = !boosted_first_ && citer == 0;  // valid scores already carry the init bias
+        ValidApply(vi, t, k, kValidAddSub, first_bias ? init_scores_[k] : 0.0);
       }
     }
   }
@@ -443,7 +439,7 @@ std::vector<std::string> Booster::EvalNames() const {
   return names;
 }
 
-std::vector<std::pair<std::string, double>> Booster::Eval(int idx) {
+std::vector<std::pair<std::string, double>> Booster::Eval(int idx, bool device) {
   std::vector<std::pair<std::string, double>> out;
   const Dataset* d;
   const Objective* obj;
@@ -454,16 +450,19 @@ std::vector<std::pair<std::string, double>> Booster::Eval(int idx) {
     scores = nullptr;  // fetched from the backend only if a metric has no device implementation
   } else {
     d = valid_[idx - 1].get(); obj = valid_objectives_[idx - 1].get();
-    scores = valid_scores_[idx - 1].data();
+    scores = valid_dev_[idx - 1] ? nullptr : valid_scores_[idx - 1].data();
   }
   for (const auto& name : EvalNames()) {
     double dv = 0.0;
-    if (idx == 0 && backend_->EvalOnDevice(name, *obj, &dv)) {
+    const bool on_dev = device && (idx == 0 ? backend_->EvalOnDevice(name, *obj, &dv)
+                                            : valid_dev_[idx - 1] && backend_->EvalValidOnDevice(idx - 1, name, *obj, &dv));
+    if (on_dev) {
       out.emplace_back(name, dv);
       continue;
     }
-    if (!scores) {
-      backend_->GetScores(&train_scores);
+    if (!scores) {  // a metric without a device implementation: one score copy for the remaining metrics
+      if (idx == 0) backend_->GetScores(&train_scores);
+      else backend_->GetValidScores(idx - 1, &train_scores);
       scores = train_scores.data();
     }
     double v = EvalMetric(name, *obj, scores, d->label.data(), d->weight.empty() ? nullptr : d->weight.data(),
@@ -474,7 +473,10 @@ std::vector<std::pair<std::string, double>> Booster::Eval(int idx) {
 }
 
 void Booster::GetTrainScores(std::vector<double>* s) { backend_->GetScores(s); }
-void Booster::GetPredictForValid(int idx, std::vector<double>* s) const { *s = valid_scores_.at(idx); }
+void Booster::GetPredictForValid(int idx, std::vector<double>* s) const {
+  if (valid_dev_.at(idx)) backend_->GetValidScores(idx, s);
+  else *s = valid_scores_.at(idx);
+}
 
 std::pair<int, int> Booster::TreeRange(int start_iteration, int num_iteration) const {
   const int K = num_tree_per_iter_;

@@ -31,6 +31,7 @@ class Booster {
   static std::unique_ptr<Booster> FromModelString(const std::string& model);
 
   void AddValidData(std::shared_ptr<Dataset> valid, const std::string& name);
+  bool ValidOnDevice(int i) const { return valid_dev_.at(i) != 0; }
   void MergeFrom(const Booster& other);       // continue training from `other`
   void ResetParameter(const std::string& params);
   // One boosting iteration. Custom gradients (class-major n*K) if non-null.
@@ -38,7 +39,7 @@ class Booster {
   bool TrainOneIter(const float* grad = nullptr, const float* hess = nullptr);
   void RollbackOneIter();
   // metric values of data set `idx` (0 = train, 1.. = valid)
-  std::vector<std::pair<std::string, double>> Eval(int idx);
+  std::vector<std::pair<std::string, double>> Eval(int idx, bool device = true);
   std::vector<std::string> EvalNames() const;
   void GetTrainScores(std::vector<double>* s);
   void GetPredictForValid(int idx, std::vector<double>* s) const;
@@ -85,7 +86,10 @@ class Booster {
   std::shared_ptr<Dataset> train_;
   std::vector<std::shared_ptr<Dataset>> valid_;
   std::vector<std::string> valid_names_;
-  std::vector<std::vector<double>> valid_scores_;
+  std::vector<std::vector<double>> valid_scores_;  // host-resident sets only (empty when on the device)
+  std::vector<char> valid_dev_;                    // the backend holds set vi's bins and scores
+  // fold tree t into validation set vi's class-k scores (ValidOp), on the device or the host
+  void ValidApply(size_t vi, const Tree& t, int k, int op, double p);
   std::unique_ptr<Objective> objective_;
   std::vector<std::unique_ptr<Objective>> valid_objectives_;
   std::unique_ptr<TrainBackend> backend_;

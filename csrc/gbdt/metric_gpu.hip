@@ -10,6 +10,11 @@
 //              = the host's trapezoid over tied groups (objective.cpp AUC)
 //   binary_logloss / binary_error (binary objective) and l2 / rmse / l1 / mae
 //   (identity-output objectives): one fused transform-reduce
+//   multi_logloss / multi_error@k (softmax multiclass): the same reduce, one row's K class-major scores
+//   per thread
+//   ndcg@k / map@k: one wave64 per query; the top-k documents are selected k times by a wave arg-max
+//   over (score desc, index asc) strictly after the previous pick - the order of the host's stable
+//   sort, with no per-query scratch - and DCG / IDCG / AP accumulate in the host's order
 // hipCUB is used only for the generic sort / scan / reduce-by-key.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -21,6 +26,7 @@
 
 #include "hip_common.h"
 #include "objective.h"
+#include "valid_gpu.h"
 
 namespace sml {
 namespace {
@@ -80,7 +86,35 @@ struct PointLoss {
   }
 };
 
-__global__ void point_loss_kernel(PointLoss f, int64_t n, double2* __restrict__ partial) {
+struct MultiLoss {
+  int kind;  // 0 multi_logloss, 1 multi_error (top_k)
+  int K, top_k;
+  int64_t n;
+  const double* score;
+  const float* label;
+  const float* weight;
+  __device__ double2 operator()(int64_t i) const {
+    const double w = weight ? weight[i] : 1.0;
+    const int y = static_cast<int>(label[i]);
+    double mx = score[i];
+    for (int k = 1; k < K; ++k) mx = fmax(mx, score[k * n + i]);
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) s += exp(score[k * n + i] - mx);
+    const double py = exp(score[y * n + i] - mx) / s;
+    double v;
+    if (kind == 0) {
+      v = -log(fmax(py, kEpsilon));
+    } else {
+      int rank = 0;
+      for (int k = 0; k < K; ++k) rank += (exp(score[k * n + i] - mx) / s) > py;
+      v = rank >= top_k ? 1.0 : 0.0;
+    }
+    return make_double2(v * w, w);
+  }
+};
+
+template <class F>
+__global__ void reduce_kernel(F f, int64_t n, double2* __restrict__ partial) {
   double a = 0.0, b = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double2 v = f(i);
@@ -92,6 +126,81 @@ __global__ void point_loss_kernel(PointLoss f, int64_t n, double2* __restrict__ 
   a = BR(ta).Sum(a);
   b = BR(tb).Sum(b);
   if (threadIdx.x == 0) partial[blockIdx.x] = make_double2(a, b);
+}
+
+// wave arg-max of (key desc, index asc); every lane returns the winner's index (-1: none)
+__device__ __forceinline__ int WaveArgMax(double key, int idx) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ok = __shfl_xor(key, off, 64);
+    const int oi = __shfl_xor(idx, off, 64);
+    if (oi >= 0 && (idx < 0 || ok > key || (ok == key && oi < idx))) { key = ok; idx = oi; }
+  }
+  return idx;
+}
+
+// one wave per query (grid-stride): ndcg@k (is_map 0) or map@k (1) of the query into per_query[q]
+__global__ __launch_bounds__(64) void rank_metric_kernel(const double* __restrict__ score, const float* __restrict__ label,
+                                                         const int32_t* __restrict__ qb, int nq, int k, int is_map,
+                                                         const double* __restrict__ gain, int ngain,
+                                                         double* __restrict__ per_query) {
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int b = qb[q], cnt = qb[q + 1] - qb[q];
+    const int kk = min(k, cnt);
+    auto gain_of = [&](float l) {
+      const size_t li = static_cast<size_t>(static_cast<int>(l));  // the host's size_t clamp of an int label
+      return gain[li < static_cast<size_t>(ngain - 1) ? li : static_cast<size_t>(ngain - 1)];
+    };
+    // picks strictly after (ps, pi) in (score desc, index asc) order
+    double ps = INFINITY, ls = INFINITY;
+    int pi = -1, li_prev = -1;
+    double dcg = 0.0, idcg = 0.0, hits = 0.0, ap = 0.0;
+    int npos = 0;
+    if (is_map) {
+      int c = 0;
+      for (int j = lane; j < cnt; j += 64) c += label[b + j] > 0.5f;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+      npos = c;
+    }
+    for (int i = 0; i < kk; ++i) {
+      double bk = -INFINITY;
+      int bi = -1;
+      for (int j = lane; j < cnt; j += 64) {
+        const double s = score[b + j];
+        const bool after = s < ps || (s == ps && j > pi);
+        if (after && (bi < 0 || s > bk)) { bk = s; bi = j; }  // j ascends per lane: ties keep the lowest
+      }
+      const int w = WaveArgMax(bk, bi);
+      if (w < 0) break;  // NaN scores are never picked (the host's order is undefined for them too)
+      ps = score[b + w];
+      pi = w;
+      const float lw = label[b + w];
+      if (is_map) {
+        if (lw > 0.5f) { hits += 1.0; ap += hits / (i + 1.0); }
+      } else {
+        dcg += gain_of(lw) / log2(2.0 + i);
+        // ideal order: labels desc (ties by index: the gains are equal either way)
+        double lk = -INFINITY;
+        int lj = -1;
+        for (int j = lane; j < cnt; j += 64) {
+          const double l = static_cast<double>(static_cast<int>(label[b + j]));
+          const bool after = l < ls || (l == ls && j > li_prev);
+          if (after && (lj < 0 || l > lk)) { lk = l; lj = j; }
+        }
+        const int wl = WaveArgMax(lk, lj);
+        if (wl < 0) break;
+        ls = static_cast<double>(static_cast<int>(label[b + wl]));
+        li_prev = wl;
+        idcg += gain_of(label[b + wl]) / log2(2.0 + i);
+      }
+    }
+    if (lane == 0) {
+      if (is_map) per_query[q] = npos > 0 ? ap / min(k, npos) : 1.0;
+      else per_query[q] = idcg > 0 ? dcg / idcg : 1.0;
+    }
+  }
 }
 
 int Grid(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(2048, (n + kThreads - 1) / kThreads))); }
@@ -149,14 +258,69 @@ double DeviceAUC(const double* score, const float* label, const float* weight, i
   return h[0] / (h[1] * h[2]);
 }
 
+template <class F>
+double ReduceRatio(F f, int64_t n, hipStream_t s) {
+  const int grid = Grid(n);
+  DevBuf<double2> partial;
+  partial.alloc(grid);
+  hipLaunchKernelGGL(reduce_kernel<F>, dim3(grid), dim3(kThreads), 0, s, f, n, partial.get());
+  SML_HIP_CHECK(hipGetLastError());
+  std::vector<double2> h(grid);
+  SML_HIP_CHECK(hipMemcpyAsync(h.data(), partial.get(), sizeof(double2) * grid, hipMemcpyDeviceToHost, s));
+  SML_HIP_CHECK(hipStreamSynchronize(s));
+  double a = 0, b = 0;
+  for (const auto& v : h) { a += v.x; b += v.y; }
+  return b > 0 ? a / b : 0.0;
+}
+
+double DeviceRankMetric(const DeviceMetricInputs& in, int k, bool is_map, hipStream_t s) {
+  if (in.nq <= 0) return 0.0;
+  DevBuf<double> per_q, total;
+  per_q.alloc(in.nq);
+  total.alloc(1);
+  const int grid = std::min(in.nq, 65536);
+  hipLaunchKernelGGL(rank_metric_kernel, dim3(grid), dim3(64), 0, s, in.score, in.label, in.qb, in.nq, k,
+                     is_map ? 1 : 0, in.gain, in.ngain, per_q.get());
+  SML_HIP_CHECK(hipGetLastError());
+  size_t t = 0;
+  SML_HIP_CHECK(hipcub::DeviceReduce::Sum(nullptr, t, per_q.get(), total.get(), in.nq, s));
+  DevBuf<uint8_t> tmp;
+  tmp.alloc(std::max<size_t>(1, t));
+  SML_HIP_CHECK(hipcub::DeviceReduce::Sum(tmp.get(), t, per_q.get(), total.get(), in.nq, s));
+  double h = 0;
+  SML_HIP_CHECK(hipMemcpyAsync(&h, total.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+  SML_HIP_CHECK(hipStreamSynchronize(s));
+  return h / in.nq;
+}
+
 }  // namespace
 
-bool DeviceEvalMetric(const std::string& name, const ObjParams& p, const double* score, const float* label,
-                      const float* weight, int64_t n, void* stream, double* out) {
+bool DeviceEvalMetricFull(const std::string& name_in, const ObjParams& p, const DeviceMetricInputs& in, void* stream,
+                          double* out) {
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = in.n;
   if (n <= 0 || n >= (int64_t(1) << 31)) return false;
+  std::string name = name_in;
+  int at = -1;
+  const auto pos = name.find('@');
+  if (pos != std::string::npos) {
+    try { at = std::stoi(name.substr(pos + 1)); } catch (...) { return false; }
+    name = name.substr(0, pos);
+  }
+  if (name == "ndcg" || name == "map") {
+    if (!in.qb || in.nq <= 0 || (name == "ndcg" && (!in.gain || in.ngain <= 0))) return false;
+    *out = DeviceRankMetric(in, at > 0 ? at : 5, name == "map", s);
+    return true;
+  }
+  if (name == "multi_logloss" || name == "multi_error") {
+    if (p.kind != kObjMulticlass || in.num_class < 2) return false;
+    MultiLoss f{name == "multi_logloss" ? 0 : 1, in.num_class, at > 0 ? at : 1, n, in.score, in.label, in.weight};
+    *out = ReduceRatio(f, n, s);
+    return true;
+  }
+  if (at > 0 || in.num_class != 1) return false;
   if (name == "auc") {
-    *out = DeviceAUC(score, label, weight, n, s);
+    *out = DeviceAUC(in.score, in.label, in.weight, n, s);
     return true;
   }
   int kind = -1;
@@ -167,21 +331,17 @@ bool DeviceEvalMetric(const std::string& name, const ObjParams& p, const double*
     kind = 2;
   if (identity && (name == "l1" || name == "mae")) kind = 3;
   if (kind < 0) return false;
-  PointLoss f{kind, p.sigmoid, score, label, weight};
-  const int grid = Grid(n);
-  DevBuf<double2> partial;
-  partial.alloc(grid);
-  hipLaunchKernelGGL(point_loss_kernel, dim3(grid), dim3(kThreads), 0, s, f, n, partial.get());
-  SML_HIP_CHECK(hipGetLastError());
-  std::vector<double2> h(grid);
-  SML_HIP_CHECK(hipMemcpyAsync(h.data(), partial.get(), sizeof(double2) * grid, hipMemcpyDeviceToHost, s));
-  SML_HIP_CHECK(hipStreamSynchronize(s));
-  double a = 0, b = 0;
-  for (const auto& v : h) { a += v.x; b += v.y; }
-  double r = b > 0 ? a / b : 0.0;
+  double r = ReduceRatio(PointLoss{kind, p.sigmoid, in.score, in.label, in.weight}, n, s);
   if (name == "rmse" || name == "l2_root") r = std::sqrt(r);
   *out = r;
   return true;
+}
+
+bool DeviceEvalMetric(const std::string& name, const ObjParams& p, const double* score, const float* label,
+                      const float* weight, int64_t n, void* stream, double* out) {
+  DeviceMetricInputs in;
+  in.score = score; in.label = label; in.weight = weight; in.n = n;
+  return DeviceEvalMetricFull(name, p, in, stream, out);
 }
 
 }  // namespace sml

@@ -250,25 +250,28 @@ __global__ __launch_bounds__(64 * kOaaMaxWaves) void oaa_kernel(SgdArgs a) {
                                                  k + 1 == y ? 1.f : -1.f, imp, lane);
 }
 
+// Sync payload per slot: double {w G (adaptive) or w, G} + float N. The weighted sum goes in double: a
+// float w * G underflows (and is flushed) for slots with a tiny gradient mass, which would zero their
+// weight on the average even at world 1.
 __global__ void pack_kernel(const float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk,
-                            uint64_t nw, int adaptive, float* __restrict__ sums, float* __restrict__ nmax) {
+                            uint64_t nw, int adaptive, double* __restrict__ sums, float* __restrict__ nmax) {
   constexpr int64_t B = int64_t(1) << kDirtyShift;
   const int64_t m = nblk * B;
   for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < m;
        j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
     const float4 v = slot < nw ? W[slot] : make_float4(0.f, 0.f, 0.f, 0.f);
-    sums[3 * j] = v.x;
-    sums[3 * j + 1] = adaptive ? v.x * v.y : 0.f;
-    sums[3 * j + 2] = v.y;
+    sums[2 * j] = adaptive ? static_cast<double>(v.x) * v.y : static_cast<double>(v.x);
+    sums[2 * j + 1] = v.y;
     nmax[j] = v.z;
   }
 }
 
-// VW's weighted averaging: with adaptive state w = sum(w G) / sum(G) (plain mean where no rank has
-// gradient mass), G = sum(G) / world; N = max(N); without adaptive w = sum(w) / world
+// VW's weighted averaging: with adaptive state w = sum(w G) / sum(G) (a slot no rank has gradient mass
+// on was never updated and keeps its value), G = sum(G) / world; N = max(N); without adaptive
+// w = sum(w) / world
 __global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk, uint64_t nw,
-                              int adaptive, float inv_world, const float* __restrict__ sums,
+                              int adaptive, double inv_world, const double* __restrict__ sums,
                               const float* __restrict__ nmax) {
   constexpr int64_t B = int64_t(1) << kDirtyShift;
   const int64_t m = nblk * B;
@@ -277,9 +280,10 @@ __global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict_
     const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
     if (slot >= nw) continue;
     float4 v = W[slot];
-    const float sw = sums[3 * j], swg = sums[3 * j + 1], sg = sums[3 * j + 2];
-    v.x = (adaptive && sg > 0.f) ? swg / sg : sw * inv_world;
-    v.y = sg * inv_world;
+    const double s0 = sums[2 * j], sg = sums[2 * j + 1];
+    if (!adaptive) v.x = static_cast<float>(s0 * inv_world);
+    else if (sg > 0.0) v.x = static_cast<float>(s0 / sg);
+    v.y = static_cast<float>(sg * inv_world);
     v.z = nmax[j];
     W[slot] = v;
   }
@@ -347,7 +351,8 @@ struct GpuSgd::Impl {
   size_t cap_rows = 0, cap_nnz = 0;
   // sync scratch
   int32_t *pos = nullptr, *blocks = nullptr;
-  float *sums = nullptr, *nmax = nullptr;
+  double* sums = nullptr;
+  float* nmax = nullptr;
   size_t cap_sync = 0;
   void Reserve(size_t rows, size_t nnz) {
     if (rows > cap_rows) {
@@ -564,7 +569,7 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
 }
 
 // Average the table over ranks: only the 64 KB blocks some rank touched since the last sync (the union
-// of the dirty maps, one small max-allreduce) are packed, reduced (sum of {w, wG, G}, max of N) and
+// of the dirty maps, one small max-allreduce) are packed, reduced (fp64 sums of {wG or w, G}, max of N) and
 // unpacked with VW's weighted averaging - no host staging, and a sparse pass moves a fraction of the table.
 void GpuSgd::AllReduceAverage(void* comm, int world) {
   if (world < 1 || !comm) return;  // a world-1 communicator still runs the collectives (one-GPU tests)
@@ -588,7 +593,7 @@ void GpuSgd::AllReduceAverage(void* comm, int world) {
     if (slots > impl_->cap_sync) {
       (void)hipFree(impl_->blocks); (void)hipFree(impl_->sums); (void)hipFree(impl_->nmax);
       VW_HIP_CHECK(hipMalloc(&impl_->blocks, nblk * sizeof(int32_t)));
-      VW_HIP_CHECK(hipMalloc(&impl_->sums, slots * 3 * sizeof(float)));
+      VW_HIP_CHECK(hipMalloc(&impl_->sums, slots * 2 * sizeof(double)));
       VW_HIP_CHECK(hipMalloc(&impl_->nmax, slots * sizeof(float)));
       impl_->cap_sync = slots;
     }
@@ -598,12 +603,12 @@ void GpuSgd::AllReduceAverage(void* comm, int world) {
     hipLaunchKernelGGL(pack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
                        impl_->sums, impl_->nmax);
     VW_HIP_CHECK(hipGetLastError());
-    nccl(ncclAllReduce(impl_->sums, impl_->sums, slots * 3, ncclFloat, ncclSum, c, s));
+    nccl(ncclAllReduce(impl_->sums, impl_->sums, slots * 2, ncclDouble, ncclSum, c, s));
     nccl(ncclAllReduce(impl_->nmax, impl_->nmax, slots, ncclFloat, ncclMax, c, s));
     hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
-                       1.f / world, impl_->sums, impl_->nmax);
+                       1.0 / world, impl_->sums, impl_->nmax);
     VW_HIP_CHECK(hipGetLastError());
-    last_sync_bytes_ = static_cast<int64_t>(slots) * 4 * sizeof(float) + nblk;
+    last_sync_bytes_ = static_cast<int64_t>(slots) * (2 * sizeof(double) + sizeof(float)) + nblk;
   }
   VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, nblk, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));

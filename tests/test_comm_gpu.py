@@ -99,3 +99,37 @@ def test_vw_gpu_allreduce_average_world1():
     assert sgd.last_sync_bytes > 0 and sgd.last_sync_blocks > 0
     np.testing.assert_allclose(sgd.predict(ip, idx, val), p0, rtol=1e-6, atol=1e-6)
     assert len(sgd.export_model("--loss_function logistic -b 16")) == len(m0)
+
+
+def test_vw_gpu_2p30_table_sync_and_export_keep_host_rss_flat():
+    """A 2^30-slot table (16 GiB in HBM): learning, a world-1 RCCL sync and a model export only move
+    the touched blocks / nonzeros through the host - the process RSS does not grow by the table size."""
+    import psutil
+
+    from synapseml_amd.ops import native
+
+    vw = native.load("_vw")
+    cfg = vw.GpuSgdConfig()
+    cfg.bits = 30
+    cfg.loss = 1
+    proc = psutil.Process()
+    sgd = vw.GpuSgd(cfg, 0)
+    rss0 = proc.memory_info().rss
+    rng = np.random.default_rng(1)
+    n, k = 20000, 16
+    vocab = rng.integers(0, 1 << 32, size=5000, dtype=np.uint64).astype(np.uint32)  # 5000 hashed features
+    idx = vocab[rng.integers(0, len(vocab), size=n * k)]
+    val = np.ones(n * k, np.float32)
+    ip = np.arange(0, n * k + 1, k, dtype=np.int64)
+    lab = (rng.random(n) > 0.5).astype(np.float32) * 2 - 1
+    sgd.learn(ip, idx, val, lab, None, 1024)
+    comm = vw.nccl_comm(vw.nccl_unique_id(), 0, 1)
+    sgd.allreduce_average(comm)
+    # touched blocks only: at most one 4096-slot block per distinct feature, a sliver of the 2^18 blocks
+    assert 0 < sgd.last_sync_blocks <= len(vocab)
+    assert sgd.last_sync_bytes <= len(vocab) * 4096 * 20 + (1 << 18)
+    model = sgd.export_model("--loss_function logistic -b 30")
+    assert len(model) < 36 * len(vocab) + 4096  # the nonzeros (<= 3 per touched slot, 12 B each) + header
+    grown = proc.memory_info().rss - rss0
+    assert grown < (2 << 30), f"host RSS grew by {grown / 2**30:.2f} GiB"
+    del sgd

@@ -451,3 +451,77 @@ def test_gpu_fused_score_grad_root_pass(obj, monkeypatch):
         ge, he = (z - y) * lw * w, z * (1 - z) * lw * w
     np.testing.assert_allclose(g, ge, rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(h, he, rtol=1e-4, atol=1e-6)
+
+
+def _with_valid(X, y, Xv, yv, params, iters, sizes=None, vsizes=None, wv=None):
+    from synapseml_amd.ops import native
+
+    g = native.gbdt()
+    ref = g.DatasetReference.from_sample(X[:50000], len(X), params, [f"f{i}" for i in range(X.shape[1])])
+    ds = g.Dataset(ref, len(X))
+    ds.push_dense(X, 0)
+    ds.set_label(y)
+    dv = g.Dataset(ref, len(Xv))
+    dv.push_dense(Xv, 0)
+    dv.set_label(yv)
+    if wv is not None:
+        dv.set_weight(wv)
+    if sizes is not None:
+        ds.set_group(sizes)
+        dv.set_group(vsizes)
+    b = g.Booster(ds, params, None)
+    b.add_valid(dv, "valid_0")
+    for _ in range(iters):
+        b.update()
+    return b
+
+
+def _assert_device_metrics_match_host(b, idx):
+    dev, host = dict(b.eval(idx)), dict(b.eval(idx, device=False))
+    assert dev.keys() == host.keys() and dev
+    for k in dev:
+        np.testing.assert_allclose(dev[k], host[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    return dev
+
+
+@pytest.mark.parametrize("boosting", ["gbdt", "rf bagging_fraction=0.7 bagging_freq=1", "dart drop_rate=0.3"])
+def test_gpu_validation_set_on_device_binary(boosting):
+    """K11: the validation set's scores live in HBM - every tree is folded in by the device traversal
+    (gbdt add, rf running mean, dart renormalisation) - and auc / logloss / error reduce there; both
+    equal the host paths (model predict, host metric formulas) on weighted data with NaNs and ties."""
+    X, y = _data(n=60000, nan_frac=0.05)
+    Xv, yv = _data(n=20000, seed=5, nan_frac=0.05)
+    Xv[:, 0] = np.round(Xv[:, 0], 1)
+    wv = np.random.default_rng(3).uniform(0.5, 2.0, size=len(yv)).astype(np.float32)
+    p = f"objective=binary num_leaves=31 metric=auc,binary_logloss,binary_error boosting={boosting} device_type=gpu"
+    b = _with_valid(X, y, Xv, yv, p, 8, wv=wv)
+    assert b.backend == "hip" and b.valid_on_device(0)
+    np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 1, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)
+    _assert_device_metrics_match_host(b, 1)
+
+
+def test_gpu_validation_set_on_device_multiclass_categorical():
+    X, _ = _data(n=40000, cat=True)
+    y = (np.nan_to_num(X[:, 1]) > 0.3).astype(np.float32) + (X[:, 0] % 4 == 1)
+    Xv, _ = _data(n=15000, seed=9, cat=True)
+    yv = (np.nan_to_num(Xv[:, 1]) > 0.3).astype(np.float32) + (Xv[:, 0] % 4 == 1)
+    p = "objective=multiclass num_class=3 num_leaves=15 categorical_feature=0 metric=multi_logloss,multi_error device_type=gpu"
+    b = _with_valid(X, y.astype(np.float32), Xv, yv.astype(np.float32), p, 6)
+    assert b.valid_on_device(0)
+    raw = b.predict(Xv, 1, 0, -1)  # n x K
+    np.testing.assert_allclose(b.valid_scores(0), raw.T.reshape(-1), rtol=1e-9, atol=1e-10)
+    _assert_device_metrics_match_host(b, 1)
+
+
+def test_gpu_ranking_metrics_on_device():
+    """ndcg@k / map@k (one wave per query, top-k by repeated wave arg-max in the host's stable order)
+    on the training set and a validation set, vs the host loops at 1e-9; queries up to 700 documents."""
+    X, y, sizes = _rank_data()
+    Xv, yv, vsizes = _rank_data(seed=33, nq=200)
+    p = "objective=lambdarank num_leaves=15 min_data_in_leaf=5 metric=ndcg,map eval_at=1,3,5,10 device_type=gpu"
+    b = _with_valid(X, y, Xv, yv, p, 5, sizes=sizes, vsizes=vsizes)
+    assert b.valid_on_device(0)
+    dev = _assert_device_metrics_match_host(b, 1)
+    assert {"ndcg@1", "ndcg@10", "map@3"} <= dev.keys()
+    _assert_device_metrics_match_host(b, 0)
+    np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 1, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)

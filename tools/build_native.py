@@ -48,6 +48,7 @@ MODULES = {
             "dev_pool.cpp",
             "bindings.cpp",
             "backend_gpu.hip",
+            "valid_gpu.hip",
             "predict_gpu.hip",
             "comm_p2p.hip",
             "bin_encode.hip",
