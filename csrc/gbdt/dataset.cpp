@@ -354,9 +354,17 @@ void Dataset::EnsureHostBins() const {
   host_valid = true;
 }
 
-void Dataset::PushDense(const double* rows, int64_t nrows, int num_cols, int64_t start) {
+// Host pushes run concurrently at disjoint offsets (one thread per partition, StreamingPartitionTask.scala:
+// 220-231): the shared state they touch - materialising the host matrix, invalidating the device copy -
+// changes under the bins mutex; the row writes themselves are disjoint.
+void Dataset::BeginHostPush() {
   EnsureHostBins();
+  std::lock_guard<std::mutex> lk(BinsMutex());
   dev_valid = false;  // the device copy (if any) no longer has every row
+}
+
+void Dataset::PushDense(const double* rows, int64_t nrows, int num_cols, int64_t start) {
+  BeginHostPush();
   const int ni = ref.num_inner();
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < nrows; ++i) {
@@ -371,8 +379,7 @@ void Dataset::PushDense(const double* rows, int64_t nrows, int num_cols, int64_t
 }
 
 void Dataset::PushDenseF32(const float* rows, int64_t nrows, int num_cols, int64_t start) {
-  EnsureHostBins();
-  dev_valid = false;
+  BeginHostPush();
   const int ni = ref.num_inner();
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < nrows; ++i) {
@@ -388,8 +395,7 @@ void Dataset::PushDenseF32(const float* rows, int64_t nrows, int num_cols, int64
 
 void Dataset::PushCSR(const int64_t* indptr, const int32_t* indices, const double* values,
                       int64_t nrows, int64_t start) {
-  EnsureHostBins();
-  dev_valid = false;
+  BeginHostPush();
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < nrows; ++i) {
     uint8_t* dst = &bins[(start + i) * row_stride];

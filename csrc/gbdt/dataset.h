@@ -129,6 +129,8 @@ struct Dataset {
   void PushCSR(const int64_t* indptr, const int32_t* indices, const double* values,
                int64_t nrows, int64_t start);
   void SetQueryFromGroupSizes(const std::vector<int32_t>& sizes);
+  // host bins materialised and the device copy invalidated (thread-safe; called by every host push)
+  void BeginHostPush();
   inline uint8_t Bin(int64_t row, int inner) const { return bins[row * row_stride + inner]; }
 };
 

@@ -82,6 +82,12 @@ std::vector<double> GaussianKernel(int n, double sigma) {
 
 // cvtColor codes used by the reference's ColorFormat stage (OpenCV enum values)
 int CvtChannelsOut(int code, int cin) {
+  // the source channels each conversion reads (a 3-channel image given to BGRA2RGBA would read past
+  // every pixel into the next one, and past the buffer at the last)
+  const int need = (code == 1 || code == 3 || code == 5) ? 4 : ((code == 8 || code == 9) ? 1 : 3);
+  if (code >= 0 && code <= 11 && (cin < need || cin > 4))
+    throw std::invalid_argument("color conversion code " + std::to_string(code) + " needs a " + std::to_string(need) +
+                                "-channel source, got " + std::to_string(cin));
   switch (code) {
     case 0: case 2: return 4;                 // BGR2BGRA / BGR2RGBA
     case 1: case 3: return 3;                 // BGRA2BGR / BGRA2RGB
@@ -92,7 +98,6 @@ int CvtChannelsOut(int code, int cin) {
     case 9: return 4;                         // GRAY2BGRA
     default: throw std::invalid_argument("unsupported color conversion code " + std::to_string(code));
   }
-  (void)cin;
 }
 
 void CvtColorHost(const uint8_t* src, int64_t npx, int cin, int code, uint8_t* dst) {

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cctype>
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
@@ -87,12 +88,33 @@ void VW::ParseArgs(const std::string& args) {
     bool has_inline = false;
     if (eq != std::string::npos && k.rfind("--", 0) == 0) { inline_val = k.substr(eq + 1); k = k.substr(0, eq); has_inline = true; }
     auto val = [&]() { return has_inline ? inline_val : next(); };
-    if (k == "-b" || k == "--bit_precision") bits_ = std::stoi(val());
-    else if (k == "-l" || k == "--learning_rate") lr_ = std::stof(val());
-    else if (k == "--power_t") power_t_ = std::stof(val());
-    else if (k == "--initial_t") initial_t_ = std::stof(val());
-    else if (k == "--l1") l1_ = std::stof(val());
-    else if (k == "--l2") l2_ = std::stof(val());
+    // numeric values: the whole token must parse, and a bad one names its option
+    auto ival = [&]() {
+      const std::string v = val();
+      try {
+        size_t used = 0;
+        const int x = std::stoi(v, &used);
+        if (used == v.size()) return x;
+      } catch (const std::exception&) {
+      }
+      throw std::runtime_error("VW option " + k + " expects an integer, got '" + v + "'");
+    };
+    auto fval = [&]() {
+      const std::string v = val();
+      try {
+        size_t used = 0;
+        const float x = std::stof(v, &used);
+        if (used == v.size()) return x;
+      } catch (const std::exception&) {
+      }
+      throw std::runtime_error("VW option " + k + " expects a number, got '" + v + "'");
+    };
+    if (k == "-b" || k == "--bit_precision") bits_ = ival();
+    else if (k == "-l" || k == "--learning_rate") lr_ = fval();
+    else if (k == "--power_t") power_t_ = fval();
+    else if (k == "--initial_t") initial_t_ = fval();
+    else if (k == "--l1") l1_ = fval();
+    else if (k == "--l2") l2_ = fval();
     else if (k == "--hash_seed") hash_seed_ = static_cast<uint32_t>(std::stoul(val()));
     else if (k == "-q" || k == "--quadratic") interactions_.push_back(val());
     else if (k == "--cubic") interactions_.push_back(val());
@@ -100,28 +122,40 @@ void VW::ParseArgs(const std::string& args) {
     else if (k == "--ignore") { for (char c : val()) ignore_.push_back(static_cast<unsigned char>(c)); }
     else if (k == "--noconstant") constant_ = false;
     else if (k == "--loss_function") loss_ = val();
-    else if (k == "--quantile_tau") quantile_tau_ = std::stof(val());
+    else if (k == "--quantile_tau") quantile_tau_ = fval();
     else if (k == "--link") link_logistic_ = (val() == "logistic");
-    else if (k == "--oaa") oaa_ = std::stoi(val());
+    else if (k == "--oaa") oaa_ = ival();
     else if (k == "--probabilities") probabilities_ = true;
-    else if (k == "--csoaa") csoaa_ = std::stoi(val());
+    else if (k == "--csoaa") csoaa_ = ival();
     else if (k == "--cb_adf") cb_adf_ = true;
     else if (k == "--cb_explore_adf") { cb_adf_ = true; cb_explore_ = true; }
     else if (k == "--cb_type") cb_type_ = val();
-    else if (k == "--epsilon") { epsilon_ = std::stof(val()); epsilon_set_ = true; }
-    else if (k == "--passes") passes_ = std::stoi(val());
+    else if (k == "--epsilon") { epsilon_ = fval(); epsilon_set_ = true; }
+    else if (k == "--passes") passes_ = ival();
     else if (k == "-t" || k == "--testonly") testonly_ = true;
     else if (k == "--holdout_off") holdout_off_ = true;
     else if (k == "--sgd") { sgd = true; any_update_flag = true; }
     else if (k == "--adaptive") { adaptive = true; any_update_flag = true; }
     else if (k == "--normalized") { normalized = true; any_update_flag = true; }
     else if (k == "--invariant") { invariant = true; any_update_flag = true; }
-    else if (k == "--ngram") ngram_ = std::stoi(val());
-    else if (k == "--cats_pdf") { cats_k_ = std::stoi(val()); cats_sample_ = false; }
-    else if (k == "--cats") { cats_k_ = std::stoi(val()); cats_sample_ = true; }
-    else if (k == "--bandwidth") bandwidth_ = std::stof(val());
-    else if (k == "--min_value") min_value_ = std::stof(val());
-    else if (k == "--max_value") max_value_ = std::stof(val());
+    else if (k == "--ngram") {
+      // "--ngram N" (every namespace) or "--ngram aN" (namespace a only)
+      const std::string v = has_inline ? inline_val : (i + 1 < tok.size() ? tok[i + 1] : std::string());
+      if (!v.empty() && !std::isdigit(static_cast<unsigned char>(v[0]))) {
+        val();
+        int g = 0;
+        try { size_t used = 0; g = std::stoi(v.substr(1), &used); if (used != v.size() - 1) g = 0; } catch (...) { g = 0; }
+        if (g < 1) throw std::runtime_error("VW option --ngram expects N or <namespace>N, got '" + v + "'");
+        ngram_ns_[static_cast<unsigned char>(v[0])] = g;
+      } else {
+        ngram_ = ival();
+      }
+    }
+    else if (k == "--cats_pdf") { cats_k_ = ival(); cats_sample_ = false; }
+    else if (k == "--cats") { cats_k_ = ival(); cats_sample_ = true; }
+    else if (k == "--bandwidth") bandwidth_ = fval();
+    else if (k == "--min_value") min_value_ = fval();
+    else if (k == "--max_value") max_value_ = fval();
     else if (k == "--cache_file" || k == "--span_server" || k == "--span_server_port" || k == "--unique_id" ||
              k == "--total" || k == "--node" || k == "--random_seed" || k == "--readable_model" || k == "-f" ||
              k == "-i" || k == "--initial_regressor" || k == "--quantile_loss" || k == "--data" || k == "-d" ||
@@ -153,6 +187,8 @@ void VW::ParseArgs(const std::string& args) {
     adaptive_ = adaptive; normalized_ = normalized; invariant_ = invariant;
     if (sgd) { adaptive_ = normalized_ = invariant_ = false; }
   }
+  if (loss_ != "squared" && loss_ != "classic" && loss_ != "logistic" && loss_ != "hinge" && loss_ != "quantile")
+    throw std::runtime_error("VW --loss_function " + loss_ + " is not supported (squared, classic, logistic, hinge, quantile)");
   if (bits_ < 1 || bits_ > 32) throw std::runtime_error("bit_precision must be in [1, 32]");
   mask_ = (bits_ >= 64) ? ~0ull : ((1ull << bits_) - 1);
   if (loss_ == "logistic") { stats_.min_label = -50; stats_.max_label = 50; }
@@ -177,7 +213,9 @@ std::map<std::string, std::string> VW::DescribeArgs(const std::string& args) {
   d["csoaa"] = std::to_string(v.csoaa_);
   d["cb_adf"] = v.cb_adf_ ? "1" : "0";
   d["cats"] = std::to_string(v.cats_k_);
-  d["ngram"] = std::to_string(v.ngram_);
+  int ng = v.ngram_;
+  for (int g : v.ngram_ns_) ng = std::max(ng, g);
+  d["ngram"] = std::to_string(ng);
   d["ignore"] = std::string(v.ignore_.begin(), v.ignore_.end());
   d["link_logistic"] = v.link_logistic_ ? "1" : "0";
   d["probabilities"] = v.probabilities_ ? "1" : "0";
@@ -673,7 +711,8 @@ Example VW::ParseLine(const std::string& line) const {
       words.emplace_back(name, v * ns_scale);
       n.f.push_back(Feature{v * ns_scale, HashString(name, ns_hash)});
     }
-    for (int g = 2; g <= ngram_; ++g) {
+    const int ngram = ngram_ns_[ns_char] ? ngram_ns_[ns_char] : ngram_;
+    for (int g = 2; g <= ngram; ++g) {
       for (size_t i = 0; i + g <= words.size(); ++i) {
         std::string nm = words[i].first;
         for (int j = 1; j < g; ++j) nm += "^" + words[i + j].first;
@@ -707,7 +746,21 @@ void VW::PerformRemainingPasses() {
 // ----------------------------------------------------------------- model io
 namespace {
 template <class T> void Put(std::string* s, const T& v) { s->append(reinterpret_cast<const char*>(&v), sizeof(T)); }
-template <class T> T Get(const char*& p) { T v; std::memcpy(&v, p, sizeof(T)); p += sizeof(T); return v; }
+// bounds-checked reader over model bytes: a truncated or corrupted model throws instead of reading past the end
+struct Reader {
+  const char* p;
+  const char* end;
+  void Need(size_t k) const {
+    if (static_cast<size_t>(end - p) < k) throw std::runtime_error("truncated VW model");
+  }
+  template <class T> T Get() {
+    Need(sizeof(T));
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+  }
+};
 }  // namespace
 
 std::string VW::SaveModel() const {
@@ -728,25 +781,31 @@ std::string VW::SaveModel() const {
 
 void VW::LoadModel(const std::string& bytes) {
   if (bytes.size() < 8 || bytes.compare(0, 8, "SMLVW001") != 0) throw std::runtime_error("not a VW model of this engine");
-  const char* p = bytes.data() + 8;
-  uint32_t alen = Get<uint32_t>(p);
-  std::string margs(p, p + alen);
-  p += alen;
-  int32_t bits = Get<int32_t>(p);
-  uint32_t stride = Get<uint32_t>(p);
+  Reader r{bytes.data() + 8, bytes.data() + bytes.size()};
+  const uint32_t alen = r.Get<uint32_t>();
+  r.Need(alen);
+  r.p += alen;
+  const int32_t bits = r.Get<int32_t>();
+  const uint32_t stride = r.Get<uint32_t>();
+  if (bits < 1 || bits > 32 || stride < 1 || stride > 64) throw std::runtime_error("corrupt VW model header");
+  const double t = r.Get<double>(), tw = r.Get<double>(), snx = r.Get<double>();
+  const double lo = r.Get<double>(), hi = r.Get<double>();
+  const uint64_t nz = r.Get<uint64_t>();
+  if (nz > static_cast<uint64_t>(r.end - r.p) / (sizeof(uint64_t) + sizeof(float))) throw std::runtime_error("truncated VW model");
   if (bits != bits_ || stride != stride_) {
     // the model defines the table geometry
     bits_ = bits;
     mask_ = (1ull << bits_) - 1;
     stride_ = stride;
     weights_.assign(static_cast<size_t>(mask_ + 1) * stride_, 0.f);
+  } else {
+    std::fill(weights_.begin(), weights_.end(), 0.f);
   }
-  t_ = Get<double>(p); total_weight_ = Get<double>(p); sum_norm_x_ = Get<double>(p);
-  stats_.min_label = Get<double>(p); stats_.max_label = Get<double>(p);
-  uint64_t nz = Get<uint64_t>(p);
+  t_ = t; total_weight_ = tw; sum_norm_x_ = snx;
+  stats_.min_label = lo; stats_.max_label = hi;
   for (uint64_t k = 0; k < nz; ++k) {
-    uint64_t i = Get<uint64_t>(p);
-    float v = Get<float>(p);
+    const uint64_t i = r.Get<uint64_t>();
+    const float v = r.Get<float>();
     if (i < weights_.size()) weights_[i] = v;
   }
 }

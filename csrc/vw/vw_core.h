@@ -162,6 +162,7 @@ class VW {
   bool testonly_ = false;
   bool holdout_off_ = true;
   int ngram_ = 0;
+  std::array<int, 256> ngram_ns_{};  // per-namespace "--ngram aN"
   int cats_k_ = 0;             // --cats_pdf K / --cats K: discrete centroids
   bool cats_sample_ = false;   // --cats: emit a sampled action (action_pdf_value) instead of the pdf
   float bandwidth_ = -1.f, min_value_ = 0.f, max_value_ = -1.f;

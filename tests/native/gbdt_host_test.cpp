@@ -1,11 +1,15 @@
 // Native host test of the GBDT engine for sanitizer builds (ASan + UBSan, TSan):
 // dataset construction (dense + CSR), training for several objectives/boosting modes with the OpenMP CPU
-// backend, model text round trip, prediction consistency. Exit code != 0 on any mismatch.
+// backend, model text round trip, prediction consistency, and the concurrent paths the Python layer drives
+// from worker threads (disjoint-offset pushes into one Dataset - StreamingPartitionTask.scala:220-231 - and
+// predictions from several threads on one Booster), which the TSan build checks with >= 4 threads.
+// Exit code != 0 on any mismatch.
 #include <cmath>
 #include <cstdio>
 #include <memory>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "booster.h"
@@ -56,8 +60,25 @@ static void run(const std::string& params, bool csr) {
   }
   ds->label = y;
   Booster b(ds, params);
+  // a validation set (the first 1000 rows): its incrementally folded scores equal the model's raw predictions
+  const int nv = 1000;
+  auto vd = std::make_shared<Dataset>();
+  vd->Init(ref, nv);
+  vd->PushDense(X.data(), nv, F, 0);
+  vd->label.assign(y.begin(), y.begin() + nv);
+  b.AddValidData(vd, "valid_0");
   for (int it = 0; it < 15; ++it)
     if (b.TrainOneIter()) break;
+  {
+    std::vector<double> vs, raw(static_cast<size_t>(nv) * b.NumClasses());
+    b.GetPredictForValid(0, &vs);
+    b.Predict(X.data(), nv, F, kPredictRaw, 0, -1, raw.data());  // raw scores, row-major n x K
+    const int K = b.NumClasses();
+    CHECK(vs.size() == raw.size());
+    for (int i = 0; i < nv && vs.size() == raw.size(); ++i)
+      for (int k = 0; k < K; ++k) CHECK(std::fabs(vs[k * nv + i] - raw[i * K + k]) <= 1e-9 * (1 + std::fabs(raw[i * K + k])));
+    for (const auto& kv : b.Eval(1)) CHECK(std::isfinite(kv.second));
+  }
   std::vector<double> p1(static_cast<size_t>(n) * b.NumClasses());
   b.Predict(X.data(), n, F, 0, 0, -1, p1.data());
   const std::string model = b.SaveModelToString(0, -1, 0);
@@ -147,7 +168,77 @@ static void malformed_models() {
   std::printf("ok  malformed model strings rejected: %d\n", rejected);
 }
 
+// Four threads push disjoint row blocks of one Dataset at once (dense f64, dense f32 and CSR pushes),
+// then four threads predict disjoint row ranges of one trained Booster while OpenMP runs inside each call.
+static void concurrent_push_and_predict() {
+  const int n = 24000, F = 9, T = 4;
+  std::mt19937 rng(11);
+  std::normal_distribution<double> nd;
+  std::vector<double> X(static_cast<size_t>(n) * F);
+  std::vector<float> Xf(X.size());
+  std::vector<float> y(n);
+  for (int i = 0; i < n; ++i) {
+    for (int f = 0; f < F; ++f) X[i * F + f] = (f == 4 && i % 3 == 0) ? 0.0 : nd(rng);
+    y[i] = X[i * F] + X[i * F + 1] > 0 ? 1.f : 0.f;
+  }
+  for (size_t i = 0; i < X.size(); ++i) Xf[i] = static_cast<float>(X[i]);
+  const std::string params = "objective=binary num_leaves=15 device_type=cpu num_threads=4";
+  Config cfg = Config::Parse(params);
+  std::vector<std::string> names;
+  for (int f = 0; f < F; ++f) names.push_back("f" + std::to_string(f));
+  auto ref = DatasetReference::FromSample(X.data(), n, F, n, cfg, names);
+  auto serial = std::make_shared<Dataset>();
+  serial->Init(ref, n);
+  serial->PushDense(X.data(), n, F, 0);
+  for (int mode = 0; mode < 3; ++mode) {
+    auto ds = std::make_shared<Dataset>();
+    ds->Init(ref, n);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) {
+      th.emplace_back([&, t]() {
+        const int64_t r0 = static_cast<int64_t>(n) * t / T, r1 = static_cast<int64_t>(n) * (t + 1) / T;
+        const int64_t m = r1 - r0;
+        if (mode == 0) {
+          ds->PushDense(X.data() + r0 * F, m, F, r0);
+        } else if (mode == 1) {
+          ds->PushDenseF32(Xf.data() + r0 * F, m, F, r0);
+        } else {
+          std::vector<int64_t> ip(m + 1, 0);
+          std::vector<int32_t> idx;
+          std::vector<double> val;
+          for (int64_t i = 0; i < m; ++i) {
+            for (int f = 0; f < F; ++f)
+              if (X[(r0 + i) * F + f] != 0.0) { idx.push_back(f); val.push_back(X[(r0 + i) * F + f]); }
+            ip[i + 1] = static_cast<int64_t>(idx.size());
+          }
+          ds->PushCSR(ip.data(), idx.data(), val.data(), m, r0);
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    if (mode != 1) CHECK(ds->bins == serial->bins);  // f32 rounding may move a bin edge: compare f64 pushes
+    if (mode == 0) {
+      ds->label = y;
+      Booster b(ds, params);
+      for (int it = 0; it < 8; ++it) b.TrainOneIter();
+      std::vector<double> ref_pred(n), par(n);
+      b.Predict(X.data(), n, F, 0, 0, -1, ref_pred.data());
+      std::vector<std::thread> pt;
+      for (int t = 0; t < T; ++t) {
+        pt.emplace_back([&, t]() {
+          const int64_t r0 = static_cast<int64_t>(n) * t / T, r1 = static_cast<int64_t>(n) * (t + 1) / T;
+          b.Predict(X.data() + r0 * F, r1 - r0, F, 0, 0, -1, par.data() + r0);
+        });
+      }
+      for (auto& t : pt) t.join();
+      for (int i = 0; i < n; ++i) CHECK(par[i] == ref_pred[i]);
+    }
+  }
+  std::printf("ok  concurrent pushes (dense f64 / f32 / CSR) and predictions from %d threads\n", T);
+}
+
 int main() {
+  concurrent_push_and_predict();
   malformed_models();
   run("objective=binary num_leaves=15 device_type=cpu", false);
   run("objective=binary num_leaves=15 device_type=cpu", true);

@@ -496,7 +496,7 @@ def test_gpu_validation_set_on_device_binary(boosting):
     p = f"objective=binary num_leaves=31 metric=auc,binary_logloss,binary_error boosting={boosting} device_type=gpu"
     b = _with_valid(X, y, Xv, yv, p, 8, wv=wv)
     assert b.backend == "hip" and b.valid_on_device(0)
-    np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 1, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)
+    np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 0, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)
     _assert_device_metrics_match_host(b, 1)
 
 
@@ -508,7 +508,7 @@ def test_gpu_validation_set_on_device_multiclass_categorical():
     p = "objective=multiclass num_class=3 num_leaves=15 categorical_feature=0 metric=multi_logloss,multi_error device_type=gpu"
     b = _with_valid(X, y.astype(np.float32), Xv, yv.astype(np.float32), p, 6)
     assert b.valid_on_device(0)
-    raw = b.predict(Xv, 1, 0, -1)  # n x K
+    raw = b.predict(Xv, 0, 0, -1)  # n x K
     np.testing.assert_allclose(b.valid_scores(0), raw.T.reshape(-1), rtol=1e-9, atol=1e-10)
     _assert_device_metrics_match_host(b, 1)
 
@@ -524,4 +524,4 @@ def test_gpu_ranking_metrics_on_device():
     dev = _assert_device_metrics_match_host(b, 1)
     assert {"ndcg@1", "ndcg@10", "map@3"} <= dev.keys()
     _assert_device_metrics_match_host(b, 0)
-    np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 1, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)
+    np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 0, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)
