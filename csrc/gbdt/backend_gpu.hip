@@ -17,10 +17,12 @@
 // without any host round trip (the tree is read back once at the end).
 // Data-parallel training inserts an RCCL allreduce of the smaller child's
 // histogram between the slab reduce and the split search (C2 over xGMI).
-// tree_learner=voting (C3) runs as data-parallel here: a full-histogram
-// one-shot allreduce over xGMI (~114 KB, comm_p2p.hip) costs less than the
-// vote round trip plus the selected-feature reduction it would replace
-// (SURVEY §5.8); the host backend implements the PV-Tree vote for CPU clusters.
+// tree_learner=voting (C3) is refused on multi-rank device training rather than
+// silently run as data-parallel (it grows different trees): a full-histogram
+// one-shot allreduce over xGMI (~114 KB, comm_p2p.hip) costs less than the vote
+// round trip plus the selected-feature reduction PV-Tree would replace (SURVEY
+// §5.8), so data_parallel is the device mode; the host backend implements the
+// PV-Tree vote for CPU clusters.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2010,6 +2012,11 @@ class GpuBackend : public TrainBackend {
 
   void Init(const Dataset* d, const Config& cfg, int K) override {
     data_ = d; cfg_ = cfg; K_ = K; n_ = d->num_data;
+    if (cfg.tree_learner == "voting" && comm_ && comm_->world() > 1)
+      throw std::runtime_error(
+          "tree_learner=voting (parallelism=voting_parallel) is not run by the GPU backend: use "
+          "parallelism=data_parallel on the device (a full-histogram allreduce over xGMI costs less than the "
+          "PV-Tree vote), or deviceType=cpu for voting-parallel trees");
     if (n_ >= (int64_t(1) << 31)) throw std::runtime_error("GPU backend: more than 2^31 rows per device");
     if (cfg.num_leaves > 4096) throw std::runtime_error("GPU backend: num_leaves > 4096");
     if (dev_ >= 0) SML_HIP_CHECK(hipSetDevice(dev_));

@@ -157,6 +157,13 @@ class LightGBMBase(Estimator, LightGBMParams):
                 raise ValueError(f"Invalid slot name {n!r}: slot names cannot contain \" , : [ ] {{ }}")
         return names
 
+    def _check_parallelism(self, use_gpu: bool, world: int) -> None:
+        """voting_parallel grows PV-Tree trees on the host backend only; on several GPUs it is refused up front
+        (before any data moves) instead of silently running data-parallel (backend_gpu.hip header)."""
+        if use_gpu and world > 1 and self.getParallelism() == "voting_parallel":
+            raise ValueError("parallelism='voting_parallel' is not run on the GPU backend with several ranks: use "
+                             "parallelism='data_parallel' (full-histogram allreduce over xGMI) or deviceType='cpu'")
+
     def _train_params(self, num_class: int, cat_idx: List[int], num_machines: int) -> str:
         sb = ParamsStringBuilder()
         sb.append(self.getPassThroughArgs())
@@ -386,6 +393,7 @@ class LightGBMBase(Estimator, LightGBMParams):
         names = self._slot_names(df, ncols)
         params = self._train_params(num_class, cat_idx, world)
         use_gpu = self.getDeviceType() == "gpu" and native.gpu_available()
+        self._check_parallelism(use_gpu, world)
         # K1 input staging: a large dense partition starts its host->HBM copy now, on a native thread, so it
         # overlaps the row sampling and bin-boundary construction below (the encode then runs in HBM)
         upload = g.DeviceRows(data) if (kind == "dense" and use_gpu and n >= (1 << 16)) else None

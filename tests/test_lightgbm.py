@@ -444,3 +444,16 @@ def test_checkpoint_unreadable_raises_clearly(tmp_path):
                                                  "complete": False, "fingerprint": fp}))
     with pytest.raises(RuntimeError, match="cannot resume"):
         est.fit(df)
+
+
+def test_voting_parallel_refused_on_multi_rank_gpu():
+    """voting_parallel is never silently run as data-parallel on the device: multi-rank GPU training is
+    refused with a message naming the alternatives; one rank, or the CPU backend, is fine."""
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    est = LightGBMClassifier(parallelism="voting_parallel", deviceType="gpu")
+    with pytest.raises(ValueError, match="data_parallel"):
+        est._check_parallelism(True, 2)
+    est._check_parallelism(True, 1)
+    est._check_parallelism(False, 4)
+    LightGBMClassifier(parallelism="data_parallel")._check_parallelism(True, 8)
