@@ -145,6 +145,30 @@ def maybe_p2p(comm, device: int):
     return c
 
 
+def init_with_retries(make, what: str, retries: int = 3, delay_s: float = 1.0):
+    """Collective network initialisation with the reference's retry policy (NetworkManager.scala:195-218,
+    3 retries, 1 s doubled): every rank tries, the outcomes are all-gathered over the control plane, and if
+    any rank failed all ranks retry together (a fresh unique id each time), so no rank is left holding a
+    half-initialised communicator."""
+    import time
+
+    for attempt in range(retries + 1):
+        c, err = None, None
+        try:
+            c = make()
+        except Exception as e:  # noqa: BLE001 - shared with the other ranks below
+            err = f"rank {rank()}: {type(e).__name__}: {e}"
+        errs = [e for e in all_gather_object(err) if e]
+        if not errs:
+            return c
+        del c
+        if attempt == retries:
+            raise RuntimeError(f"{what} initialisation failed after {retries} retries: " + "; ".join(errs))
+        time.sleep(delay_s)
+        delay_s *= 2
+    raise AssertionError("unreachable")
+
+
 def gbdt_comm(use_gpu: bool, shared_device: bool = False):
     """Communicator for the native GBDT engine, or None when world == 1.
 
@@ -179,12 +203,15 @@ def gbdt_comm(use_gpu: bool, shared_device: bool = False):
         host = g.host_comm(rank(), world_size(), lambda arr: allreduce_numpy(arr))
         c = maybe_p2p(host, torch.cuda.current_device())
     elif use_gpu:
-        uid = g.rccl_unique_id() if rank() == 0 else None
-        uid = broadcast_object(uid, 0)
         import torch
 
         dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
-        c = g.rccl_comm(uid, rank(), world_size(), dev)
+
+        def make():
+            uid = g.rccl_unique_id() if rank() == 0 else None
+            return g.rccl_comm(broadcast_object(uid, 0), rank(), world_size(), dev)
+
+        c = init_with_retries(make, "RCCL communicator")
         c = maybe_p2p(c, dev)
     else:
         c = g.host_comm(rank(), world_size(), lambda arr: allreduce_numpy(arr))

@@ -29,9 +29,53 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+MAX_PORT = 65535
+NETWORK_RETRIES = 3          # LightGBMConstants.NetworkRetries
+INITIAL_DELAY_S = 1.0        # LightGBMConstants.InitialDelay (ms 1000), doubled per retry
+
+
+def _bindable(port: int) -> bool:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        try:
+            s.bind(("127.0.0.1", port))
+            return True
+        except OSError:
+            return False
+
+
+def find_open_port(base: int, max_tries: int = 1000) -> int:
+    """First bindable port at or above ``base`` (NetworkManager.findOpenPort, NetworkManager.scala:240-271):
+    at most ``max_tries`` ports are probed and none above 65535."""
+    if base <= 0:
+        return _free_port()
+    if base > MAX_PORT:
+        raise ValueError(f"port {base} out of range")
+    for port in range(base, min(MAX_PORT, base + max_tries - 1) + 1):
+        if _bindable(port):
+            return port
+    raise RuntimeError(f"could not find an open port in [{base}, {min(MAX_PORT, base + max_tries - 1)}]")
+
+
+def rendezvous_port(driver_listen_port: int = 0, default_listen_port: int = 0) -> int:
+    """The rank-0 rendezvous (TCPStore) port for a job this runtime launches - the role of the reference
+    driver's listen socket and the workers' LightGBM listen ports (LightGBMParams.scala:39-49):
+    ``driverListenPort > 0`` is used as given (an error if it is taken, as the driver's bind would fail);
+    otherwise the first open port at or above ``defaultListenPort`` (12400 by default); otherwise any
+    free port."""
+    if driver_listen_port and driver_listen_port > 0:
+        if driver_listen_port > MAX_PORT:
+            raise ValueError(f"driverListenPort {driver_listen_port} out of range")
+        if not _bindable(driver_listen_port):
+            raise RuntimeError(f"driverListenPort {driver_listen_port} is already in use")
+        return driver_listen_port
+    return find_open_port(default_listen_port) if default_listen_port and default_listen_port > 0 else _free_port()
+
+
 def _injected_fault(rank: int) -> Optional[str]:
     """Test-only fault injection: ``SML_FAULT_INJECT="<rank>:<kind>"`` with kind in
-    raise | crash_before | crash_after_init | empty (the rank sees an empty partition)."""
+    raise | crash_before | crash_after_init | empty (the rank sees an empty partition) | netinit_fail (the
+    rank's first rendezvous attempt fails)."""
     spec = os.environ.get("SML_FAULT_INJECT", "")
     for item in filter(None, spec.split(",")):
         r, _, kind = item.partition(":")
@@ -41,7 +85,7 @@ def _injected_fault(rank: int) -> Optional[str]:
 
 
 def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, parts_bytes: bytes, out_dir: str,
-            use_gpu: bool) -> None:
+            use_gpu: bool, attempt: int = 0) -> None:
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     result: Any
@@ -54,8 +98,16 @@ def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, par
 
         if use_gpu:
             torch.cuda.set_device(rank % max(1, torch.cuda.device_count()))
-        dist.init_process_group(backend=backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                                world_size=world)
+        try:
+            if fault == "netinit_fail" and attempt == 0:
+                raise OSError("injected network-init failure")
+            dist.init_process_group(backend=backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                    world_size=world, timeout=_init_timeout())
+        except Exception as e:  # noqa: BLE001 - the driver retries the rendezvous (NetworkManager retry)
+            result = ("netinit", f"{type(e).__name__}: {e}")
+            with open(os.path.join(out_dir, f"result_{rank}.pkl"), "wb") as f:
+                pickle.dump(result, f)
+            return
         fn = pickle.loads(fn_bytes)
         part = pickle.loads(parts_bytes)
         if fault == "raise":
@@ -73,14 +125,50 @@ def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, par
         pickle.dump(result, f)
 
 
+def _init_timeout():
+    import datetime
+
+    return datetime.timedelta(seconds=float(os.environ.get("SML_RENDEZVOUS_TIMEOUT_S", "120")))
+
+
 def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_workers: Optional[int] = None,
                    backend: Optional[str] = None, use_gpu: bool = False, timeout_s: float = 1200.0,
-                   fail_fast: bool = True) -> List[Any]:
+                   fail_fast: bool = True, port: Optional[int] = None, default_listen_port: int = 0,
+                   network_retries: int = NETWORK_RETRIES, initial_delay_s: float = INITIAL_DELAY_S) -> List[Any]:
     """Run ``fn(partition_df, rank, world)`` in ``num_workers`` processes.
 
     Partitions are grouped contiguously onto workers (coalesce). Returns the
     per-rank results in rank order.
+
+    Network initialisation follows the reference's NetworkInit retry (NetworkManager.scala:195-218): when
+    any rank fails to join the rendezvous, every rank of that attempt is stopped and the job is relaunched
+    on the next open port, up to ``network_retries`` times, sleeping ``initial_delay_s`` doubled per retry.
+    ``port`` pins the rendezvous port (driverListenPort); otherwise the first open port at or above
+    ``default_listen_port`` (defaultListenPort), or any free port.
     """
+    import time as _time
+
+    delay = initial_delay_s
+    pinned = port
+    for attempt in range(network_retries + 1):
+        p = pinned if pinned else (find_open_port(default_listen_port) if default_listen_port > 0 else _free_port())
+        try:
+            return _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, p, attempt)
+        except _NetworkInitError as e:
+            if attempt == network_retries:
+                raise RuntimeError(f"network init failed after {network_retries} retries: {e}") from None
+            _time.sleep(delay)
+            delay *= 2
+            if default_listen_port > 0 and not pinned:
+                default_listen_port = p + 1  # the next open port, as findOpenPort walks upward
+    raise AssertionError("unreachable")
+
+
+class _NetworkInitError(RuntimeError):
+    pass
+
+
+def _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, port, attempt) -> List[Any]:
     import tempfile
 
     import torch.multiprocessing as mp
@@ -91,13 +179,13 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
         parts.append(df.slice(0, 0))
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
-    port = _free_port()
     fn_bytes = pickle.dumps(fn)
     ctx = mp.get_context("spawn")
     with tempfile.TemporaryDirectory() as d:
         procs = []
         for r in range(world):
-            p = ctx.Process(target=_worker, args=(r, world, port, backend, fn_bytes, pickle.dumps(parts[r]), d, use_gpu))
+            p = ctx.Process(target=_worker,
+                            args=(r, world, port, backend, fn_bytes, pickle.dumps(parts[r]), d, use_gpu, attempt))
             p.start()
             procs.append(p)
         # fail fast: a rank that exits with an error (or dies) aborts the job instead of leaving the others
@@ -116,9 +204,11 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
                 else:
                     with open(path, "rb") as f:
                         st = pickle.load(f)[0]  # written by our own worker process
-                    if st != "ok":
+                    if st == "netinit":
+                        failed = failed or (r, "netinit")
+                    elif st != "ok":
                         failed = failed or (r, "task error")
-            if (failed and fail_fast) or _time.monotonic() > deadline:
+            if (failed and (fail_fast or failed[1] == "netinit")) or _time.monotonic() > deadline:
                 break
             _time.sleep(0.05)
         for p in procs:
@@ -128,6 +218,10 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
                 if p.is_alive():
                     p.kill()
                     p.join()
+        if failed is not None and failed[1] == "netinit":
+            with open(os.path.join(d, f"result_{failed[0]}.pkl"), "rb") as f:
+                msg = pickle.load(f)[1]  # written by our own worker process
+            raise _NetworkInitError(f"rank {failed[0]} on port {port}: {msg}")
         if failed is not None and not fail_fast:
             # every rank ran to its own end: report what each one saw
             errs = []
@@ -179,5 +273,12 @@ def distributed_fit(estimator, df: DataFrame, num_workers: Optional[int] = None,
                     **kw):
     """Data-parallel ``fit`` across worker processes; returns rank 0's model
     (only the main worker returns the model, BasePartitionTask.scala:450-461).
-    Extra keyword arguments go to :func:`run_partitions` (timeout_s, fail_fast)."""
+    Extra keyword arguments go to :func:`run_partitions` (timeout_s, fail_fast, ...). An estimator with
+    driverListenPort / defaultListenPort params (LightGBM) sets the rendezvous port from them."""
+    if "port" not in kw and hasattr(estimator, "getDriverListenPort"):
+        dp = int(estimator.getDriverListenPort() or 0)
+        if dp > 0:
+            kw["port"] = rendezvous_port(dp)
+        elif hasattr(estimator, "getDefaultListenPort"):
+            kw.setdefault("default_listen_port", int(estimator.getDefaultListenPort() or 0))
     return run_partitions(_FitTask(estimator), df, num_workers=num_workers, use_gpu=use_gpu, **kw)[0]

@@ -121,3 +121,93 @@ def test_voting_parallel_two_ranks():
     assert "[tree_learner: voting]" in vote_1.getNativeModel()
     p = vote_1.transform(df)["probability"][:, 1]
     assert roc_auc_score(y, p) > 0.85
+
+
+def _port_task(part, rank, world):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    return int(os.environ["MASTER_PORT"]), float(t.item())
+
+
+def test_network_init_retries_with_backoff(monkeypatch):
+    """NetworkInit retry semantics (NetworkManager.scala:195-218): a rank whose first rendezvous fails makes
+    the driver relaunch every rank after a delay; with no retries left the job fails naming the cause."""
+    import time
+
+    monkeypatch.setenv("SML_FAULT_INJECT", "1:netinit_fail")
+    df = DataFrame({"x": np.arange(4)}, num_partitions=2)
+    t0 = time.monotonic()
+    res = run_partitions(_port_task, df, num_workers=2, initial_delay_s=0.2)
+    assert [r[1] for r in res] == [2.0, 2.0]
+    assert time.monotonic() - t0 < 120
+    with pytest.raises(RuntimeError, match="network init failed after 0 retries"):
+        run_partitions(_port_task, df, num_workers=2, network_retries=0)
+
+
+def test_listen_port_semantics():
+    """defaultListenPort: first open port at or above it (findOpenPort); driverListenPort: used as given,
+    an error when taken (LightGBMParams.scala:39-49)."""
+    import socket
+
+    from synapseml_amd.parallel.runtime import find_open_port, rendezvous_port
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        s.listen(1)
+        busy = s.getsockname()[1]
+        assert find_open_port(busy) > busy
+        with pytest.raises(RuntimeError, match="already in use"):
+            rendezvous_port(driver_listen_port=busy)
+    free = find_open_port(busy)
+    assert rendezvous_port(driver_listen_port=free) == free
+    with pytest.raises(ValueError):
+        find_open_port(70000)
+    df = DataFrame({"x": np.arange(4)}, num_partitions=2)
+    res = run_partitions(_port_task, df, num_workers=2, port=free)
+    assert [r[0] for r in res] == [free, free]
+
+
+def test_distributed_fit_uses_estimator_ports():
+    from synapseml_amd.parallel.runtime import find_open_port
+
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((400, 4))
+    y = (X[:, 0] > 0).astype(float)
+    df = DataFrame({"features": X, "label": y}, num_partitions=2)
+    port = find_open_port(23000)
+    m = distributed_fit(LightGBMClassifier(numIterations=3, driverListenPort=port), df, num_workers=2)
+    assert m.getNativeModel()
+
+
+def _retry_task(part, rank, world):
+    from synapseml_amd.parallel.distributed import init_with_retries
+
+    calls = {"n": 0}
+
+    def make():
+        calls["n"] += 1
+        if rank == 1 and calls["n"] == 1:
+            raise OSError("transient bootstrap failure")
+        return f"comm{calls['n']}"
+
+    c = init_with_retries(make, "test comm", delay_s=0.05)
+    try:
+        init_with_retries(lambda: (_ for _ in ()).throw(OSError("down")) if rank == 0 else "ok", "dead comm",
+                          retries=1, delay_s=0.01)
+        failed = None
+    except RuntimeError as e:
+        failed = str(e)
+    return c, calls["n"], failed
+
+
+def test_collective_init_retries_together():
+    """A communicator that fails to initialise on one rank is retried on every rank together; when it keeps
+    failing, every rank raises with the failing rank named."""
+    res = run_partitions(_retry_task, DataFrame({"x": np.arange(4)}, num_partitions=2), num_workers=2)
+    assert [r[0] for r in res] == ["comm2", "comm2"] and [r[1] for r in res] == [2, 2]
+    assert all(r[2] and "rank 0: OSError: down" in r[2] and "after 1 retries" in r[2] for r in res)
