@@ -2697,6 +2697,9 @@ class GpuBackend : public TrainBackend {
 
   // root (choose_now = false): choose_part_kernel does the choose step with the next partition
   void EnqueueFindChoose(bool choose_now) {
+    // (A/B, round 3: folding this search into the slab reduce - the last of a feature's 8 reduce blocks
+    // searching it after a device-scope release/acquire hand-off - ran 3.11 vs 2.14 ms/iter: the per-block
+    // fences cost more than the launch they save)
     hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), part_.get(),
                        E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_, st_next_);
     SML_HIP_CHECK(hipGetLastError());

@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 
@@ -49,10 +50,21 @@ PYBIND11_MODULE(_gbdt, m) {
 
   py::class_<DatasetReference, std::shared_ptr<DatasetReference>>(m, "DatasetReference")
       .def_static("from_sample",
-                  [](F64 sample, int64_t total_rows, const std::string& params, std::vector<std::string> names) {
-                    auto b = sample.request();
-                    if (b.ndim != 2) throw std::runtime_error("sample must be 2-D");
+                  [](py::array sample, int64_t total_rows, const std::string& params, std::vector<std::string> names) {
                     Config cfg = Config::Parse(params);
+                    // float32 samples are binned as they are (no float64 copy of the sample)
+                    if (py::isinstance<py::array_t<float>>(sample) && (sample.flags() & py::array::c_style)) {
+                      auto f = py::cast<py::array_t<float, py::array::c_style>>(sample);
+                      if (f.ndim() != 2) throw std::runtime_error("sample must be 2-D");
+                      const float* p = f.data();
+                      const int64_t n = f.shape(0);
+                      const int c = static_cast<int>(f.shape(1));
+                      py::gil_scoped_release rel;
+                      return std::make_shared<DatasetReference>(DatasetReference::FromSampleF32(p, n, c, total_rows, cfg, names));
+                    }
+                    auto d = py::cast<F64>(sample);
+                    auto b = d.request();
+                    if (b.ndim != 2) throw std::runtime_error("sample must be 2-D");
                     py::gil_scoped_release rel;
                     return std::make_shared<DatasetReference>(DatasetReference::FromSample(
                         static_cast<const double*>(b.ptr), b.shape[0], static_cast<int>(b.shape[1]), total_rows, cfg, names));
@@ -82,6 +94,35 @@ PYBIND11_MODULE(_gbdt, m) {
       .def("value_to_bin", [](const DatasetReference& r, int f, double v) { return r.mappers.at(f).ValueToBin(v); });
 
   // K1 input staging: the raw rows go up on a native thread while Python samples / builds bin boundaries
+  m.def("sample_dense_rows",
+        [](py::array X, int64_t count, uint64_t seed) -> py::array {
+          // `count` distinct rows of a dense C-contiguous float32 / float64 matrix, in row order, gathered
+          // in parallel (bin-boundary sampling; LightGBM's bin_construct_sample_cnt)
+          auto run = [&](auto tag) -> py::array {
+            using T = decltype(tag);
+            auto a = py::cast<py::array_t<T, py::array::c_style>>(X);
+            if (a.ndim() != 2) throw std::runtime_error("X must be 2-D");
+            const int64_t n = a.shape(0), c = a.shape(1);
+            std::vector<int64_t> idx;
+            {
+              py::gil_scoped_release rel;
+              idx = SampleRowIndices(n, count, seed);
+            }
+            py::array_t<T> out({static_cast<int64_t>(idx.size()), c});
+            T* o = out.mutable_data();
+            const T* src = a.data();
+            {
+              py::gil_scoped_release rel;
+              const int64_t k = static_cast<int64_t>(idx.size());
+#pragma omp parallel for schedule(static)
+              for (int64_t i = 0; i < k; ++i) std::memcpy(o + i * c, src + idx[i] * c, sizeof(T) * c);
+            }
+            return out;
+          };
+          if (py::isinstance<py::array_t<float>>(X)) return run(float{});
+          return run(double{});
+        },
+        py::arg("X"), py::arg("count"), py::arg("seed"));
   py::class_<PyDeviceRows>(m, "DeviceRows")
       .def(py::init([](py::array X, int device) {
              auto b = X.request();

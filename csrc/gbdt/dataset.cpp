@@ -10,6 +10,10 @@
 
 #ifdef _OPENMP
 #include <omp.h>
+#else
+static inline int omp_get_max_threads() { return 1; }
+static inline int omp_get_thread_num() { return 0; }
+static inline int omp_get_num_threads() { return 1; }
 #endif
 
 namespace sml {
@@ -71,24 +75,30 @@ std::vector<double> GreedyBins(const std::vector<double>& vals, const std::vecto
 // 11-bit digits, skipping digits every key shares (float32-origin samples have 29 zero low mantissa
 // bits, so 3 of the 6 passes vanish). ~10x std::sort on the 200k-row bin sample; same order except
 // that -0.0 sorts before +0.0 (both are counted as the zero bin by the caller).
+// LSD radix sort of doubles (order-preserving key map), 8-bit digits: 256 buckets stay in L1, and a
+// digit every key shares is skipped - float32-origin samples have 29 zero mantissa bits, so 3 of the 8
+// passes drop out.
 void SortDoubles(std::vector<double>* v) {
   const size_t n = v->size();
   if (n < 2048) { std::sort(v->begin(), v->end()); return; }
   std::vector<uint64_t> a(n), b(n);
+  uint64_t all_or = 0, all_and = ~uint64_t(0);
   for (size_t i = 0; i < n; ++i) {
     uint64_t u;
     std::memcpy(&u, &(*v)[i], 8);
     a[i] = (u >> 63) ? ~u : (u | (uint64_t(1) << 63));
+    all_or |= a[i];
+    all_and &= a[i];
   }
-  constexpr int kBits = 11, kB = 1 << kBits;
-  std::vector<uint32_t> cnt(kB);
-  for (int shift = 0; shift < 64; shift += kBits) {
-    std::fill(cnt.begin(), cnt.end(), 0u);
-    for (size_t i = 0; i < n; ++i) ++cnt[(a[i] >> shift) & (kB - 1)];
-    if (cnt[(a[0] >> shift) & (kB - 1)] == n) continue;  // every key has this digit
+  const uint64_t varying = all_or ^ all_and;  // bits that differ between some keys
+  uint32_t cnt[256];
+  for (int shift = 0; shift < 64; shift += 8) {
+    if (((varying >> shift) & 0xFFu) == 0) continue;  // every key has this digit
+    std::memset(cnt, 0, sizeof(cnt));
+    for (size_t i = 0; i < n; ++i) ++cnt[(a[i] >> shift) & 0xFFu];
     uint32_t run = 0;
-    for (int d = 0; d < kB; ++d) { const uint32_t c = cnt[d]; cnt[d] = run; run += c; }
-    for (size_t i = 0; i < n; ++i) b[cnt[(a[i] >> shift) & (kB - 1)]++] = a[i];
+    for (int d = 0; d < 256; ++d) { const uint32_t c = cnt[d]; cnt[d] = run; run += c; }
+    for (size_t i = 0; i < n; ++i) b[cnt[(a[i] >> shift) & 0xFFu]++] = a[i];
     a.swap(b);
   }
   for (size_t i = 0; i < n; ++i) {
@@ -298,20 +308,78 @@ DatasetReference DatasetReference::FromSampledColumns(const std::vector<std::vec
   return r;
 }
 
+namespace {
+// sampled rows (row-major) -> per-feature columns of the values that are not (near) zero, one pass over
+// the rows per thread block of features: the sample is read in row order (no 28-way strided re-reads)
+template <class T>
+std::vector<std::vector<double>> SampleColumns(const T* sample, int64_t n_sample, int num_cols) {
+  std::vector<std::vector<double>> cols(num_cols);
+  const int nt = std::max(1, std::min(omp_get_max_threads(), num_cols));
+#pragma omp parallel num_threads(nt)
+  {
+    const int t = omp_get_thread_num(), T_ = omp_get_num_threads();
+    const int f0 = static_cast<int>(static_cast<int64_t>(num_cols) * t / T_);
+    const int f1 = static_cast<int>(static_cast<int64_t>(num_cols) * (t + 1) / T_);
+    for (int f = f0; f < f1; ++f) cols[f].reserve(static_cast<size_t>(n_sample));
+    for (int64_t i = 0; i < n_sample; ++i) {
+      const T* row = sample + i * num_cols;
+      for (int f = f0; f < f1; ++f) {
+        const double v = static_cast<double>(row[f]);
+        if (std::isnan(v) || std::fabs(v) > kZeroThreshold) cols[f].push_back(v);
+      }
+    }
+  }
+  return cols;
+}
+}  // namespace
+
 DatasetReference DatasetReference::FromSample(const double* sample, int64_t n_sample, int num_cols,
                                               int64_t total_rows, const Config& cfg,
                                               const std::vector<std::string>& names) {
   (void)total_rows;
-  std::vector<std::vector<double>> cols(num_cols);
-#pragma omp parallel for schedule(static)
-  for (int f = 0; f < num_cols; ++f) {
-    cols[f].reserve(n_sample);
-    for (int64_t i = 0; i < n_sample; ++i) {
-      double v = sample[i * num_cols + f];
-      if (std::isnan(v) || std::fabs(v) > kZeroThreshold) cols[f].push_back(v);
+  return FromSampledColumns(SampleColumns(sample, n_sample, num_cols), n_sample, cfg, names);
+}
+
+DatasetReference DatasetReference::FromSampleF32(const float* sample, int64_t n_sample, int num_cols,
+                                                 int64_t total_rows, const Config& cfg,
+                                                 const std::vector<std::string>& names) {
+  (void)total_rows;
+  return FromSampledColumns(SampleColumns(sample, n_sample, num_cols), n_sample, cfg, names);
+}
+
+std::vector<int64_t> SampleRowIndices(int64_t n, int64_t k, uint64_t seed) {
+  // Floyd's algorithm over a bitmap: k distinct rows of [0, n) uniformly at random in O(k) draws, then the
+  // bitmap scan returns them sorted (sequential reads of the sampled rows). splitmix64 stream of `seed`.
+  std::vector<int64_t> out;
+  if (n <= 0 || k <= 0) return out;
+  if (k >= n) {
+    out.resize(n);
+    for (int64_t i = 0; i < n; ++i) out[i] = i;
+    return out;
+  }
+  std::vector<uint64_t> bits(static_cast<size_t>((n + 63) / 64), 0);
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+  auto next = [&x]() {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  for (int64_t j = n - k; j < n; ++j) {
+    // uniform in [0, j] (128-bit multiply: no modulo bias worth measuring at these sizes)
+    const int64_t t = static_cast<int64_t>((static_cast<unsigned __int128>(next()) * static_cast<uint64_t>(j + 1)) >> 64);
+    const int64_t pick = (bits[t >> 6] >> (t & 63)) & 1ull ? j : t;
+    bits[pick >> 6] |= 1ull << (pick & 63);
+  }
+  out.reserve(static_cast<size_t>(k));
+  for (size_t w = 0; w < bits.size(); ++w) {
+    uint64_t m = bits[w];
+    while (m) {
+      out.push_back(static_cast<int64_t>(w * 64 + __builtin_ctzll(m)));
+      m &= m - 1;
     }
   }
-  return FromSampledColumns(cols, n_sample, cfg, names);
+  return out;
 }
 
 void Dataset::Init(const DatasetReference& r, int64_t n) {

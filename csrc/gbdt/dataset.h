@@ -82,6 +82,8 @@ struct DatasetReference {
   static DatasetReference FromSample(const double* sample, int64_t n_sample, int num_cols,
                                      int64_t total_rows, const Config& cfg,
                                      const std::vector<std::string>& names);
+  static DatasetReference FromSampleF32(const float* sample, int64_t n_sample, int num_cols, int64_t total_rows,
+                                        const Config& cfg, const std::vector<std::string>& names);
   // Build from a column-wise sample with explicit non-zero values per column
   // (LGBM_DatasetCreateFromSampledColumn semantics).
   static DatasetReference FromSampledColumns(const std::vector<std::vector<double>>& cols,
@@ -154,8 +156,13 @@ struct DeviceRows {
   std::string error;
 };
 void DatasetPushDeviceRows(Dataset* d, DeviceRows* src, int64_t start);
+// host (pageable) -> device copy through pinned staging buffers filled by parallel CPU threads (bin_encode.hip)
+void UploadPinned(const char* host, char* dev, size_t bytes);
 
 // device -> host copy of a device-resident bin matrix (bin_encode.hip)
 void DatasetDownloadBins(const Dataset& d, uint8_t* host);
+
+// k distinct row indices of [0, n), sorted, drawn from the seed (bin-boundary sampling, K1's host side)
+std::vector<int64_t> SampleRowIndices(int64_t n, int64_t k, uint64_t seed);
 
 }  // namespace sml

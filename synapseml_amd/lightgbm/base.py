@@ -470,6 +470,12 @@ class LightGBMBase(Estimator, LightGBMParams):
         mode = self.getSamplingMode()
         if n == 0:
             return np.zeros((0, _num_cols(kind, data)))
+        if kind == "dense" and mode != "fixed" and isinstance(data, np.ndarray) and data.dtype in (np.float32,
+                                                                                                   np.float64):
+            # native: Floyd sampling of distinct rows + a parallel gather, in the input dtype (no float64 copy)
+            pop = data[:min(n, self.getSamplingSubsetSize())] if mode == "subset" else data
+            return native.gbdt().sample_dense_rows(np.ascontiguousarray(pop), min(cnt, len(pop)),
+                                                   int(self.getDataRandomSeed()) & 0xFFFFFFFFFFFFFFFF)
         if mode == "fixed":
             idx = np.arange(cnt)
         elif mode == "subset":
