@@ -6,8 +6,9 @@ from .http import (CustomInputParser, CustomOutputParser, HTTPTransformer, JSONI
                    response_string, send_with_retries)
 from .powerbi import PowerBIWriter
 from .serving import ServingServer, make_reply, make_response, parse_request, request_to_string, serve
+from .streaming import ContinuousServingServer, ServingQuery, read_stream
 
-__all__ = ["BinaryFileFields", "read_binary_files", "write_binary_files", "zip_bytes", "HTTPTransformer",
+__all__ = ["ContinuousServingServer", "ServingQuery", "read_stream", "BinaryFileFields", "read_binary_files", "write_binary_files", "zip_bytes", "HTTPTransformer",
            "SimpleHTTPTransformer", "JSONInputParser", "JSONOutputParser", "StringOutputParser",
            "CustomInputParser", "CustomOutputParser", "advanced_handler", "basic_handler", "make_request",
            "response_string", "send_with_retries", "PowerBIWriter", "ServingServer", "serve", "parse_request",
