@@ -551,31 +551,49 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
         return res.withColumn(self.getOutputCol(), vec).drop(tmp)
 
     def _transform_device(self, df: DataFrame, model: ONNXModel, img_name: str, out_name: str) -> DataFrame:
-        """GPU path: decode on the host, one fused preprocess kernel per batch writes the input tensor
-        straight into device memory, the session consumes it without a host round trip."""
+        """GPU path: decode on a host thread pool running ahead of the device, one fused preprocess kernel per
+        batch writes the input tensor straight into device memory, the session consumes it without a host
+        round trip. Batch k+1.. decode (PIL releases the GIL) while batch k preprocesses + runs on the GPU."""
+        import os as _os
+        from concurrent.futures import ThreadPoolExecutor
+
         import torch
 
+        from ..image.schema import to_array
+
         tr = self._image_transformer("__unused__")
-        arrays = tr.decode_column(df)
-        keep = np.asarray([a is not None for a in arrays])
-        if not self.getDropNa() and not keep.all():
-            raise ValueError("undecodable images present and dropNa is false")
-        df = df.filter(keep) if not keep.all() else df
-        arrays = [a for a in arrays if a is not None]
+        values = df[self.getInputCol()].tolist()
+        ign = tr.getIgnoreDecodingErrors()
         requested = [out_name]
         sess = model._session(None if sorted(model.modelOutput) == requested else requested)
         bs = max(1, int(model.getMiniBatchSize()))
         # larger device batches amortise launches; results are identical per row
         bs = max(bs, 64)
         prec = {torch.float32: "float32", torch.float16: "float16", torch.bfloat16: "bfloat16"}[sess.compute_dtype]
+        workers = max(1, min(16, (_os.cpu_count() or 8)))
+        keep = np.ones(len(values), dtype=bool)
         outs = []
-        for s in range(0, len(arrays), bs):
-            chunk = arrays[s:s + bs]
-            t = tr.device_tensors(chunk, dtype=prec, nhwc=sess.channels_last)
-            if t is None:
-                t = torch.from_numpy(np.stack([tr.process_host(a) for a in chunk]))
-            res = sess.run([out_name], {img_name: t})[0]
-            outs.append(np.asarray(res, dtype=np.float64).reshape(len(chunk), -1))
+        with ThreadPoolExecutor(max_workers=workers) as ex:
+            # every batch's decode is queued up front: the pool stays ahead of the device loop below
+            futs = [[ex.submit(to_array, v, ign) for v in values[s:s + bs]] for s in range(0, len(values), bs)]
+            for k, fs in enumerate(futs):
+                arrays = [f.result() for f in fs]
+                for j, a in enumerate(arrays):
+                    if a is None:
+                        keep[k * bs + j] = False
+                chunk = [a for a in arrays if a is not None]
+                if not chunk:
+                    continue
+                t = tr.device_tensors(chunk, dtype=prec, nhwc=sess.channels_last)
+                if t is None:
+                    t = torch.from_numpy(np.stack([tr.process_host(a) for a in chunk]))
+                res = sess.run([out_name], {img_name: t})[0]
+                outs.append(np.asarray(res, dtype=np.float64).reshape(len(chunk), -1))
+        if not keep.all():
+            if not self.getDropNa():
+                raise ValueError("undecodable images present and dropNa is false")
+            df = df.filter(keep)
+        arrays = [None] * int(keep.sum())
         feats = np.concatenate(outs) if outs else np.zeros((0, 0))
         col = np.empty(len(arrays), dtype=object)
         for i in range(len(arrays)):

@@ -118,13 +118,13 @@ p2p_status: dict = {}
 
 
 def _single_node() -> bool:
-    lw = os.environ.get("LOCAL_WORLD_SIZE")
-    if lw is not None:
-        return int(lw) == world_size()
+    """Every rank on one host. Collective on every rank (the hostname gather runs even when
+    LOCAL_WORLD_SIZE is set, so ranks with different environments cannot split into different paths)."""
     import socket
 
     hosts = all_gather_object(socket.gethostname())
-    return len(set(hosts)) == 1
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    return len(set(hosts)) == 1 and (lw is None or int(lw) == world_size())
 
 
 def maybe_p2p(comm, device: int):
@@ -133,7 +133,8 @@ def maybe_p2p(comm, device: int):
     this and all end up on the same path."""
     from ..ops import native
 
-    want = os.environ.get("SML_GBDT_P2P", "1") != "0" and world_size() <= 8 and _single_node()
+    single = _single_node()  # collective: every rank runs it, whatever its own P2P setting
+    want = os.environ.get("SML_GBDT_P2P", "1") != "0" and world_size() <= 8 and single
     # agree before touching IPC so no rank waits in the self-test alone
     flags = all_gather_object(bool(want))
     if not all(flags):

@@ -211,3 +211,37 @@ def test_collective_init_retries_together():
     res = run_partitions(_retry_task, DataFrame({"x": np.arange(4)}, num_partitions=2), num_workers=2)
     assert [r[0] for r in res] == ["comm2", "comm2"] and [r[1] for r in res] == [2, 2]
     assert all(r[2] and "rank 0: OSError: down" in r[2] and "after 1 retries" in r[2] for r in res)
+
+
+def _p2p_decision_task(part, rank, world):
+    import os
+
+    from synapseml_amd.parallel import distributed as D
+
+    sentinel = object()
+    if rank == 1:
+        os.environ["LOCAL_WORLD_SIZE"] = "1"  # this rank believes it is alone on its node
+    c = D.maybe_p2p(sentinel, -1)
+    return c is sentinel, dict(D.p2p_status)
+
+
+def _p2p_disabled_on_one_rank(part, rank, world):
+    import os
+
+    from synapseml_amd.parallel import distributed as D
+
+    sentinel = object()
+    if rank == 0:
+        os.environ["SML_GBDT_P2P"] = "0"
+    c = D.maybe_p2p(sentinel, -1)
+    return c is sentinel, dict(D.p2p_status)
+
+
+@pytest.mark.parametrize("task", [_p2p_decision_task, _p2p_disabled_on_one_rank])
+def test_p2p_fallback_is_collective(task):
+    """maybe_p2p's fallback (distributed.py): when any rank sees a multi-node layout (LOCAL_WORLD_SIZE !=
+    world) or has P2P disabled, EVERY rank keeps the plain RCCL/host communicator - no rank enters the IPC
+    self-test alone."""
+    res = run_partitions(task, DataFrame({"x": np.arange(4)}, num_partitions=2), num_workers=2)
+    assert all(kept for kept, _ in res)
+    assert all(st.get("active") is False and "multi-node" in st.get("reason", "") for _, st in res)

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """ResNet-50 (ONNX model-zoo v2 topology, random-init weights) inference
 throughput on one GPU: (1) session only, device-resident input, per precision
-and batch; (2) ImageFeaturizer end to end (host decode of uint8 images, fused
-resize/crop/normalize kernel, featurization) — BASELINE.json config
-"ONNXModel ResNet-50, synthetic 224x224 images"."""
+and batch; (2) ImageFeaturizer end to end from ENCODED JPEG bytes (host decode
+on a thread pool running ahead of the device, fused resize/crop/normalize
+kernel, featurization) and, for reference, from pre-decoded image rows —
+BASELINE.json config "ONNXModel ResNet-50, synthetic 224x224 images".
+Precision is reported per line; fp32 is the reference's precision."""
 from __future__ import annotations
 
 import argparse
@@ -52,27 +54,43 @@ def main():
             dt = (time.perf_counter() - t0) / a.iters
             print(json.dumps({"bench": "resnet50_session", "precision": prec, "batch": bs, "ms_per_batch": dt * 1e3,
                               "images_per_s": bs / dt, "hip_graph": not a.no_graph and dev == "cuda"}), flush=True)
-    # end to end featurizer (decode from image rows, fused preprocess, headless features)
+    # end to end featurizer: JPEG bytes (decode included) and pre-decoded rows, fused preprocess, headless features
     if a.images <= 0:
         return
+    import io as _io
+
+    from PIL import Image
+
     rng = np.random.default_rng(0)
-    col = np.empty(a.images, dtype=object)
+    yy, xx = np.mgrid[0:256, 0:256]
+    jpegs = np.empty(a.images, dtype=object)
+    rows = np.empty(a.images, dtype=object)
     for i in range(a.images):
-        col[i] = make_image_row(rng.integers(0, 256, (256, 256, 3), dtype=np.uint8))
-    df = DataFrame({"image": col})
-    for prec in ("fp32", "fp16"):
-        f = ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
-                            imageTensorName="data").setModel(model)
-        f.getOnnxModel().setPrecision(prec).setMiniBatchSize(128)
-        f.transform(df.limit(128))  # warm-up / graph capture
-        if dev == "cuda":
-            torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        out = f.transform(df)
-        dt = time.perf_counter() - t0
-        assert out.count() == a.images
-        print(json.dumps({"bench": "image_featurizer_e2e", "precision": prec, "images": a.images,
-                          "images_per_s": a.images / dt, "s": dt}), flush=True)
+        # smooth colour fields + noise: JPEG sizes like photos (~20-40 KB at 256x256, quality 90)
+        base = np.stack([(xx * (1 + i % 3) + yy) % 256, (yy * 2 + i) % 256, (xx + 2 * yy + 3 * i) % 256], -1)
+        img = np.clip(base + rng.normal(0, 12, base.shape), 0, 255).astype(np.uint8)
+        buf = _io.BytesIO()
+        Image.fromarray(img).save(buf, format="JPEG", quality=90)
+        jpegs[i] = buf.getvalue()
+        rows[i] = make_image_row(img[:, :, ::-1].copy())
+    avg_kb = float(np.mean([len(b) for b in jpegs])) / 1024
+    for src, col in (("jpeg_bytes", jpegs), ("decoded_rows", rows)):
+        df = DataFrame({"image": col})
+        for prec in ("fp32", "fp16"):
+            f = ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
+                                imageTensorName="data").setModel(model)
+            f.getOnnxModel().setPrecision(prec).setMiniBatchSize(128)
+            f.transform(df.limit(128))  # warm-up / graph capture
+            if dev == "cuda":
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = f.transform(df)
+            dt = time.perf_counter() - t0
+            assert out.count() == a.images
+            print(json.dumps({"bench": "image_featurizer_e2e", "input": src, "decode_included": src == "jpeg_bytes",
+                              "jpeg_kb_avg": round(avg_kb, 1) if src == "jpeg_bytes" else None,
+                              "precision": prec, "images": a.images, "images_per_s": a.images / dt, "s": dt}),
+                  flush=True)
 
 
 if __name__ == "__main__":
