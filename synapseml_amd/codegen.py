@@ -7,7 +7,9 @@ imports the stage through reticulate, sets the non-NULL params, and returns the 
 plus ``sml_fit`` / ``sml_transform`` / ``sml_save`` / ``sml_load`` and R <-> DataFrame conversion.
 A testthat file per module constructs every stage (the reference's generated R tests do the same).
 
-usage: ``python -m synapseml_amd.codegen --r-out build/R/synapsemlamd``"""
+The .NET binding (``generate_dotnet``) is a P/Invoke layer over the engine's C ABI (libsml_gbdt.so).
+
+usage: ``python -m synapseml_amd.codegen --r-out build/R/synapsemlamd --dotnet-out build/dotnet``"""
 from __future__ import annotations
 
 import argparse
@@ -191,12 +193,155 @@ def generate_r(out_dir: str, version: str = "0.2.0") -> List[str]:
     return exported
 
 
+# ====================================================================== native C ABI + .NET
+# The GBDT engine's C ABI (csrc/gbdt/c_api.cpp, libsml_gbdt.so) as data: (name, [(arg, C type)]). Every
+# function returns int (0 ok, -1 error; SML_GetLastError for the message). The ctypes binding below and the
+# generated C# P/Invoke layer are both derived from this one table, and the ctypes side is executed by the
+# tests against the built library, so the .NET signatures are checked by construction.
+C_API: List[Tuple[str, List[Tuple[str, str]]]] = [
+    ("SML_DatasetCreateFromMat", [("data", "void*"), ("data_type", "int"), ("nrow", "int32"), ("ncol", "int32"),
+                                  ("parameters", "char*"), ("label", "float*"), ("out", "void**")]),
+    ("SML_DatasetSetWeight", [("dataset", "void*"), ("weight", "float*"), ("n", "int32")]),
+    ("SML_DatasetGetNumData", [("dataset", "void*"), ("out", "int32*")]),
+    ("SML_DatasetFree", [("dataset", "void*")]),
+    ("SML_BoosterCreate", [("train", "void*"), ("parameters", "char*"), ("out", "void**")]),
+    ("SML_BoosterAddValidData", [("booster", "void*"), ("valid", "void*")]),
+    ("SML_BoosterLoadModelFromString", [("model", "char*"), ("out", "void**")]),
+    ("SML_BoosterFree", [("booster", "void*")]),
+    ("SML_BoosterUpdateOneIter", [("booster", "void*"), ("is_finished", "int*")]),
+    ("SML_BoosterGetCurrentIteration", [("booster", "void*"), ("out", "int*")]),
+    ("SML_BoosterGetNumClasses", [("booster", "void*"), ("out", "int*")]),
+    ("SML_BoosterGetEval", [("booster", "void*"), ("data_idx", "int"), ("out_len", "int*"),
+                            ("out_results", "double*")]),
+    ("SML_BoosterPredictForMat", [("booster", "void*"), ("data", "void*"), ("data_type", "int"), ("nrow", "int32"),
+                                  ("ncol", "int32"), ("predict_type", "int"), ("start_iteration", "int"),
+                                  ("num_iteration", "int"), ("out_len", "int64*"), ("out_result", "double*")]),
+    ("SML_BoosterSaveModelToString", [("booster", "void*"), ("start_iteration", "int"), ("num_iteration", "int"),
+                                      ("buffer_len", "int64"), ("out_len", "int64*"), ("out_str", "char*")]),
+]
+
+_CS_TYPES = {"void*": "IntPtr", "void**": "out IntPtr", "int": "int", "int32": "int", "int*": "out int",
+             "int32*": "out int", "int64": "long", "int64*": "out long", "float*": "float[]",
+             "double*": "double[]", "char*": "string"}
+_CS_OVERRIDE = {("SML_BoosterSaveModelToString", "out_str"): "byte[]",
+                ("SML_DatasetCreateFromMat", "data"): "float[]", ("SML_BoosterPredictForMat", "data"): "float[]"}
+
+
+def native_library_path() -> str:
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsml_gbdt.so")
+
+
+def load_c_api(path: Optional[str] = None):
+    """ctypes binding of libsml_gbdt.so with argtypes / restype from C_API."""
+    import ctypes as C
+
+    ct = {"void*": C.c_void_p, "void**": C.POINTER(C.c_void_p), "int": C.c_int, "int32": C.c_int32,
+          "int*": C.POINTER(C.c_int), "int32*": C.POINTER(C.c_int32), "int64": C.c_int64,
+          "int64*": C.POINTER(C.c_int64), "float*": C.POINTER(C.c_float), "double*": C.POINTER(C.c_double),
+          "char*": C.c_char_p}
+    lib = C.CDLL(path or native_library_path())
+    for name, args in C_API:
+        f = getattr(lib, name)
+        f.argtypes = [ct[t] for _, t in args]
+        f.restype = C.c_int
+    lib.SML_GetLastError.restype = C.c_char_p
+    lib.SML_GetLastError.argtypes = []
+    return lib
+
+
+def generate_dotnet(out_dir: str, namespace: str = "SynapseML.Amd") -> str:
+    """C# binding of the native engine: a P/Invoke layer over libsml_gbdt.so (every C_API entry) and
+    managed Dataset / Booster classes (IDisposable handles, errors raised as SynapseMLException) - the .NET
+    surface the reference generates for its stages (CORE/codegen/DotnetCodegen.scala), over this engine's C
+    ABI instead of a JVM bridge. Returns the path of the generated .cs file."""
+    os.makedirs(out_dir, exist_ok=True)
+    lines = ["// <auto-generated> by synapseml_amd.codegen.generate_dotnet - do not edit </auto-generated>",
+             "using System;", "using System.Runtime.InteropServices;", "using System.Text;", "",
+             f"namespace {namespace}", "{",
+             "    public sealed class SynapseMLException : Exception",
+             "    {", "        public SynapseMLException(string message) : base(message) { }", "    }", "",
+             "    internal static class NativeMethods", "    {",
+             '        private const string Lib = "sml_gbdt";', "",
+             "        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]",
+             "        internal static extern IntPtr SML_GetLastError();"]
+    for name, args in C_API:
+        ps = []
+        for a, t in args:
+            cst = _CS_OVERRIDE.get((name, a), _CS_TYPES[t])
+            ps.append(f"{cst} {a}")
+        lines += ["", "        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)]",
+                  f"        internal static extern int {name}({', '.join(ps)});"]
+    lines += ["", "        internal static void Check(int rc)", "        {",
+              "            if (rc != 0) throw new SynapseMLException(Marshal.PtrToStringAnsi(SML_GetLastError()));",
+              "        }", "    }", "",
+              "    /// <summary>Binned training data (LightGBM Dataset semantics) owned by the native engine.</summary>",
+              "    public sealed class GbdtDataset : IDisposable", "    {",
+              "        internal IntPtr Handle;", "",
+              "        public GbdtDataset(float[] rowMajor, int nrow, int ncol, float[] label, string parameters = \"\")",
+              "        {",
+              "            NativeMethods.Check(NativeMethods.SML_DatasetCreateFromMat(rowMajor, 0, nrow, ncol, parameters, label, out Handle));",
+              "        }", "",
+              "        public int NumData", "        {",
+              "            get { NativeMethods.Check(NativeMethods.SML_DatasetGetNumData(Handle, out int n)); return n; }",
+              "        }", "",
+              "        public void SetWeight(float[] weight) =>",
+              "            NativeMethods.Check(NativeMethods.SML_DatasetSetWeight(Handle, weight, weight.Length));", "",
+              "        public void Dispose()", "        {",
+              "            if (Handle != IntPtr.Zero) { NativeMethods.SML_DatasetFree(Handle); Handle = IntPtr.Zero; }",
+              "        }", "    }", "",
+              "    /// <summary>Gradient-boosted trees (device_type=gpu trains on the MI355X).</summary>",
+              "    public sealed class GbdtBooster : IDisposable", "    {",
+              "        private IntPtr handle;", "",
+              "        public GbdtBooster(GbdtDataset train, string parameters)", "        {",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterCreate(train.Handle, parameters, out handle));",
+              "        }", "",
+              "        private GbdtBooster(IntPtr h) { handle = h; }", "",
+              "        public static GbdtBooster FromModelString(string model)", "        {",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterLoadModelFromString(model, out IntPtr h));",
+              "            return new GbdtBooster(h);", "        }", "",
+              "        public void AddValidData(GbdtDataset valid) =>",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterAddValidData(handle, valid.Handle));", "",
+              "        /// <returns>true when no further tree could be grown</returns>",
+              "        public bool UpdateOneIter()", "        {",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterUpdateOneIter(handle, out int finished));",
+              "            return finished != 0;", "        }", "",
+              "        public int CurrentIteration", "        {",
+              "            get { NativeMethods.Check(NativeMethods.SML_BoosterGetCurrentIteration(handle, out int i)); return i; }",
+              "        }", "",
+              "        public double[] GetEval(int dataIdx)", "        {",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterGetEval(handle, dataIdx, out int n, null));",
+              "            var r = new double[n];",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterGetEval(handle, dataIdx, out n, r));",
+              "            return r;", "        }", "",
+              "        /// <param name=\"predictType\">0 raw, 1 normal, 2 leaf index, 3 contributions</param>",
+              "        public double[] Predict(float[] rowMajor, int nrow, int ncol, int predictType = 1, int numIteration = -1)",
+              "        {",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterPredictForMat(handle, rowMajor, 0, nrow, ncol, predictType, 0, numIteration, out long len, null));",
+              "            var r = new double[len];",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterPredictForMat(handle, rowMajor, 0, nrow, ncol, predictType, 0, numIteration, out len, r));",
+              "            return r;", "        }", "",
+              "        public string SaveModelToString(int numIteration = -1)", "        {",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterSaveModelToString(handle, 0, numIteration, 0, out long need, null));",
+              "            var buf = new byte[need];",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterSaveModelToString(handle, 0, numIteration, need, out need, buf));",
+              "            return Encoding.UTF8.GetString(buf, 0, (int)need - 1);", "        }", "",
+              "        public void Dispose()", "        {",
+              "            if (handle != IntPtr.Zero) { NativeMethods.SML_BoosterFree(handle); handle = IntPtr.Zero; }",
+              "        }", "    }", "}", ""]
+    path = os.path.join(out_dir, f"{namespace}.Gbdt.cs")
+    with open(path, "w") as f:
+        f.write("\n".join(lines))
+    return path
+
+
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--r-out", default=os.path.join("build", "R", R_PACKAGE))
+    ap.add_argument("--dotnet-out", default=os.path.join("build", "dotnet"))
     a = ap.parse_args(argv)
     names = generate_r(a.r_out)
     print(f"{len(names)} R functions -> {a.r_out}")
+    print(f".NET binding -> {generate_dotnet(a.dotnet_out)}")
 
 
 if __name__ == "__main__":

@@ -56,6 +56,18 @@ def decode_bytes(data: bytes) -> np.ndarray:
         return np.ascontiguousarray(a[:, :, ::-1])
 
 
+def decode_bytes_rgb(data: bytes):
+    """Encoded bytes -> (HWC uint8, is_rgb). RGB images (every JPEG) come back in RGB order straight from the
+    decoder - no convert() copy and no BGR flip; the fused device preprocess maps channels itself. Other
+    modes fall back to decode_bytes (OpenCV order, is_rgb False)."""
+    from PIL import Image
+
+    with Image.open(io.BytesIO(bytes(data))) as im:
+        if im.mode == "RGB":
+            return np.asarray(im), True
+    return decode_bytes(data), False
+
+
 def encode_png(arr: np.ndarray) -> bytes:
     """HWC OpenCV-order array -> PNG bytes."""
     from PIL import Image

@@ -295,8 +295,11 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         scale = self.getColorScaleFactor()
         return [float(m) for m in mean], [float(s) for s in std], float(scale if scale is not None else 1.0)
 
-    def device_tensors(self, arrays: List[np.ndarray], dtype: str = "float32", nhwc: bool = False):
-        """Run the fused K19 path on a batch; returns a device tensor [B,C,H,W] or None if not applicable."""
+    def device_tensors(self, arrays: List[np.ndarray], dtype: str = "float32", nhwc: bool = False,
+                       src_rgb: bool = False):
+        """Run the fused K19 path on a batch; returns a device tensor [B,C,H,W] or None if not applicable.
+        ``src_rgb``: the 3-channel arrays are in RGB order (decode_bytes_rgb) instead of OpenCV's BGR; the
+        kernel's channel map absorbs the difference."""
         import torch
 
         plan = self._fused_plan(arrays)
@@ -305,6 +308,8 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         (rh, rw), (cy, cx, ch, cw) = plan
         c = arrays[0].shape[2]
         cmap = channel_map(c, self.getTensorChannelOrder(), self.getAutoConvertToColor())
+        if src_rgb and c == 3:
+            cmap = [2 - k for k in cmap]
         mean, std, scale = self._norm_params(len(cmap))
         sizes = [a.size for a in arrays]
         offsets = np.zeros(len(arrays), np.int64)

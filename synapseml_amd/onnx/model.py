@@ -559,7 +559,17 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
 
         import torch
 
-        from ..image.schema import to_array
+        from ..image.schema import decode_bytes_rgb, to_array
+
+        def decode(v):
+            if isinstance(v, (bytes, bytearray, memoryview)):
+                try:
+                    return decode_bytes_rgb(v)
+                except Exception:
+                    if ign:
+                        return None, False
+                    raise
+            return to_array(v, ign), False
 
         tr = self._image_transformer("__unused__")
         values = df[self.getInputCol()].tolist()
@@ -575,17 +585,22 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
         outs = []
         with ThreadPoolExecutor(max_workers=workers) as ex:
             # every batch's decode is queued up front: the pool stays ahead of the device loop below
-            futs = [[ex.submit(to_array, v, ign) for v in values[s:s + bs]] for s in range(0, len(values), bs)]
+            futs = [[ex.submit(decode, v) for v in values[s:s + bs]] for s in range(0, len(values), bs)]
             for k, fs in enumerate(futs):
-                arrays = [f.result() for f in fs]
-                for j, a in enumerate(arrays):
+                pairs = [f.result() for f in fs]
+                for j, (a, _) in enumerate(pairs):
                     if a is None:
                         keep[k * bs + j] = False
-                chunk = [a for a in arrays if a is not None]
-                if not chunk:
+                pairs = [(a, rgb) for a, rgb in pairs if a is not None]
+                if not pairs:
                     continue
-                t = tr.device_tensors(chunk, dtype=prec, nhwc=sess.channels_last)
+                all_rgb = all(rgb for _, rgb in pairs)
+                # a batch mixing RGB-decoded bytes with OpenCV-order rows goes through in OpenCV order
+                chunk = [a if (all_rgb or not rgb) else np.ascontiguousarray(a[:, :, ::-1]) for a, rgb in pairs]
+                t = tr.device_tensors(chunk, dtype=prec, nhwc=sess.channels_last, src_rgb=all_rgb)
                 if t is None:
+                    if all_rgb:
+                        chunk = [np.ascontiguousarray(a[:, :, ::-1]) if a.shape[2] == 3 else a for a in chunk]
                     t = torch.from_numpy(np.stack([tr.process_host(a) for a in chunk]))
                 res = sess.run([out_name], {img_name: t})[0]
                 outs.append(np.asarray(res, dtype=np.float64).reshape(len(chunk), -1))

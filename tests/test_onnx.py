@@ -462,3 +462,29 @@ def test_gpu_stem_epilogue_moves_past_maxpool():
     np.testing.assert_allclose(out, cpu, rtol=0, atol=2e-3 * np.abs(cpu).max())
     half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
     assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
+
+
+@pytest.mark.gpu
+def test_gpu_featurizer_encoded_bytes_match_decoded_rows():
+    """ImageFeaturizer on encoded PNG bytes (decoded in RGB order, the channel flip folded into the fused
+    preprocess kernel's channel map) equals the features of the same images given as decoded OpenCV rows."""
+    from synapseml_amd.core.dataframe import DataFrame
+    from synapseml_amd.image import encode_png, make_image_row
+    from synapseml_amd.onnx import ImageFeaturizer, writer
+
+    rng = np.random.default_rng(4)
+    imgs = [rng.integers(0, 256, (96 + 8 * i, 112, 3), dtype=np.uint8) for i in range(6)]
+    rows = np.empty(6, dtype=object)
+    pngs = np.empty(6, dtype=object)
+    for i, a in enumerate(imgs):
+        rows[i] = make_image_row(a)
+        pngs[i] = encode_png(a)
+    model = writer.resnet50_v2(seed=0)
+
+    def feats(col):
+        f = ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
+                            imageTensorName="data").setModel(model)
+        f.getOnnxModel().setPrecision("fp32").setDeviceType("gpu")
+        return np.stack([v.toArray() for v in f.transform(DataFrame({"image": col}))["features"]])
+
+    np.testing.assert_allclose(feats(pngs), feats(rows), rtol=1e-5, atol=1e-5)

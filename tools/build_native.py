@@ -56,6 +56,14 @@ MODULES = {
         ],
         ["-lrccl", "-lrocprofiler-sdk-roctx"],
     ),
+    # plain C ABI (no Python): csrc/gbdt/c_api.cpp over the same engine objects -> synapseml_amd/lib/
+    "libsml_gbdt": (
+        "csrc/gbdt",
+        ["config.cpp", "dataset.cpp", "tree.cpp", "objective.cpp", "backend_cpu.cpp", "booster.cpp", "comm_rccl.cpp",
+         "dev_pool.cpp", "backend_gpu.hip", "valid_gpu.hip", "predict_gpu.hip", "metric_gpu.hip", "bin_encode.hip",
+         "comm_p2p.hip", "c_api.cpp"],
+        ["-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-z,defs"],
+    ),
     "_vw": (
         "csrc/vw",
         ["vw_core.cpp", "vw_bindings.cpp", "vw_gpu.hip"],
@@ -123,7 +131,11 @@ def build(jobs: int = 8, force: bool = False, only: str | None = None) -> list[P
         inc = [f"-I{src_dir}", f"-I{ROOT / 'csrc'}", *_py_includes()]
         with ThreadPoolExecutor(max_workers=jobs) as ex:
             objs = list(ex.map(lambda s: compile_one(s, inc), sources))
-        out = ROOT / "synapseml_amd" / f"{name}{ext}"
+        if name.startswith("lib"):
+            (ROOT / "synapseml_amd" / "lib").mkdir(exist_ok=True)
+            out = ROOT / "synapseml_amd" / "lib" / f"{name}.so"
+        else:
+            out = ROOT / "synapseml_amd" / f"{name}{ext}"
         link = ["g++", "-shared", "-fopenmp", "-o", str(out), *map(str, objs), f"-L{ROCM}/lib",
                 "-lamdhip64", *libs, f"-Wl,-rpath,{ROCM}/lib"]
         _run(link)
