@@ -180,6 +180,11 @@ def main(argv=None) -> None:
     ap.add_argument("--reuse-port", action="store_true", help="bind with SO_REUSEPORT (set for workers)")
     ap.add_argument("--worker-id", default=None)
     ap.add_argument("--gpus", default=None, help="comma-separated device ids for the workers (default: all visible)")
+    ap.add_argument("--mode", choices=("microbatch", "continuous"), default="microbatch",
+                    help="continuous: per-request partition tasks with epochs (io/streaming.py)")
+    ap.add_argument("--num-partitions", type=int, default=2, help="continuous mode: partition tasks")
+    ap.add_argument("--epoch-ms", type=float, default=30000.0, help="continuous mode: epoch (checkpoint) interval")
+    ap.add_argument("--checkpoint-location", default=None, help="continuous mode: offsets/commits directory")
     a = ap.parse_args(argv)
     if a.workers > 1:
         srv_d = DistributedServing(a.model, a.workers, a.port, a.host, a.input_cols, a.output_cols, a.api,
@@ -195,8 +200,15 @@ def main(argv=None) -> None:
         return
     model = load_stage(a.model)
     outs = [c for c in a.output_cols.split(",") if c] or None
-    srv = ServingServer(model_handler(model, a.input_cols.split(","), outs), a.host, a.port, a.api,
-                        max_batch_size=a.max_batch_size, reuse_port=a.reuse_port, worker_id=a.worker_id).start()
+    handler = model_handler(model, a.input_cols.split(","), outs)
+    if a.mode == "continuous":
+        from .streaming import ContinuousServingServer
+
+        srv = ContinuousServingServer(handler, a.host, a.port, a.api, num_partitions=a.num_partitions,
+                                      epoch_length_ms=a.epoch_ms, checkpoint_location=a.checkpoint_location).start()
+    else:
+        srv = ServingServer(handler, a.host, a.port, a.api, max_batch_size=a.max_batch_size,
+                            reuse_port=a.reuse_port, worker_id=a.worker_id).start()
     print(f"serving {type(model).__name__} at {srv.address}", flush=True)
     done = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: done.set())

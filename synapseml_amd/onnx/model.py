@@ -583,6 +583,7 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
         workers = max(1, min(16, (_os.cpu_count() or 8)))
         keep = np.ones(len(values), dtype=bool)
         outs = []
+        pending = None
         with ThreadPoolExecutor(max_workers=workers) as ex:
             # every batch's decode is queued up front: the pool stays ahead of the device loop below
             futs = [[ex.submit(decode, v) for v in values[s:s + bs]] for s in range(0, len(values), bs)]
@@ -602,8 +603,14 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
                     if all_rgb:
                         chunk = [np.ascontiguousarray(a[:, :, ::-1]) if a.shape[2] == 3 else a for a in chunk]
                     t = torch.from_numpy(np.stack([tr.process_host(a) for a in chunk]))
-                res = sess.run([out_name], {img_name: t})[0]
-                outs.append(np.asarray(res, dtype=np.float64).reshape(len(chunk), -1))
+                # batch k is queued (preprocess + graph replay + D2H into pinned memory) before batch k-1 is
+                # collected: the host packs / converts while the GPU runs
+                nxt = (sess.run_async([out_name], {img_name: t}), len(chunk))
+                if pending is not None:
+                    outs.append(np.asarray(pending[0].result()[0], dtype=np.float64).reshape(pending[1], -1))
+                pending = nxt
+            if pending is not None:
+                outs.append(np.asarray(pending[0].result()[0], dtype=np.float64).reshape(pending[1], -1))
         if not keep.all():
             if not self.getDropNa():
                 raise ValueError("undecodable images present and dropNa is false")
