@@ -334,6 +334,30 @@ PYBIND11_MODULE(_vw, m) {
            },
            py::arg("indptr"), py::arg("indices"), py::arg("values"), py::arg("labels"), py::arg("weights") = py::none(),
            py::arg("batch") = 1024)
+      .def("stage",
+           [](GpuSgd& g, I64 indptr, U32 idx, F32 val, F32 labels, py::object weights) {
+             const int64_t n = indptr.size() - 1;
+             if (labels.size() != n) throw std::runtime_error("labels must have one entry per row");
+             F32 w;
+             if (!weights.is_none()) {
+               w = py::cast<F32>(weights);
+               if (w.size() != n) throw std::runtime_error("weights must have one entry per row");
+             }
+             py::gil_scoped_release rel;
+             g.Stage(indptr.data(), idx.data(), val.data(), labels.data(), weights.is_none() ? nullptr : w.data(), n);
+           },
+           py::arg("indptr"), py::arg("indices"), py::arg("values"), py::arg("labels"), py::arg("weights") = py::none())
+      .def("learn_staged",
+           [](GpuSgd& g, int64_t r0, int64_t r1, int batch) {
+             py::array_t<float> preds(std::max<int64_t>(0, r1 - r0));
+             float* pr = preds.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               g.LearnStaged(r0, r1, batch, pr);
+             }
+             return preds;
+           },
+           py::arg("r0"), py::arg("r1"), py::arg("batch") = 1024)
       .def("predict",
            [](GpuSgd& g, I64 indptr, U32 idx, F32 val) {
              const int64_t n = indptr.size() - 1;

@@ -34,6 +34,11 @@ class GpuSgd {
   void Learn(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
              const float* weights, int64_t n, int batch, float* preds_out);
   void Predict(const int64_t* indptr, const uint32_t* indices, const float* values, int64_t n, float* out);
+  // device-resident pass data (multi-pass / multi-segment training reads it from HBM): Stage uploads once,
+  // LearnStaged learns rows [r0, r1) of it in order
+  void Stage(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
+             const float* weights, int64_t n);
+  void LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out);
   // weighted average over ranks of the blocks touched since the last sync (RCCL on the learner's stream)
   void AllReduceAverage(void* nccl_comm_handle, int world);
   uint64_t NumWeights() const;
@@ -60,6 +65,9 @@ class GpuSgd {
   double examples_ = 0, sum_loss_ = 0;
   double min_label_ = 0, max_label_ = 0;
   int64_t last_sync_bytes_ = 0, last_sync_blocks_ = 0;
+  std::vector<float> staged_labels_;
+  int64_t staged_n_ = 0;
+  bool staged_weights_ = false;
 };
 
 bool VwGpuAvailable();

@@ -9,8 +9,12 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vw_gpu.h"
@@ -123,21 +127,39 @@ __device__ __forceinline__ float Rate(const SgdArgs& a, float G, float N) {
   return r;
 }
 
-// one Update() of the sequential learner for (example rows [b, en), offset) at raw prediction `raw`
-__device__ void UpdateWave(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y, float imp,
-                           int lane) {
+// One Update() of the sequential learner for (example rows [b, en), offset) at raw prediction `raw`, in two
+// halves around the learner's global state (t, total weight, sum of normalised |x|^2): the first pass
+// updates the touched slots' G and N and returns the wave sums the learning rate needs; the caller then
+// advances the global state (one device atomic per block in sgd_kernel) and the second pass applies the
+// update to the weights.
+// Lanes keep the rates of their first kRateCache features from the first pass for the second (the
+// sequential learner's second pass sees exactly those G / N); longer rows re-read the slots beyond.
+constexpr int kRateCache = 4;
+
+struct UpdPrep {
+  float g, ppu, norm_x;
+  float rate[kRateCache];
+};
+
+__device__ UpdPrep UpdateFirstPass(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y,
+                                   float imp, int lane) {
+  UpdPrep pr;
   float g;
   if (a.loss == 1) g = -y / (1.f + expf(y * raw));
   else g = 2.f * (raw - y);
   const float grad_sq = g * g * imp;
   float ppu = 0.f, norm_x = 0.f;
-  for (int64_t p = b + lane; p < en; p += 64) {
+  int k = 0;
+  for (int64_t p = b + lane; p < en; p += 64, ++k) {
     const uint64_t h = (a.idx[p] + off) & a.mask;
     float4* w = &a.W[h];
     const float x = a.val[p];
     float x2 = x * x;
     if (x2 < FLT_MIN) x2 = FLT_MIN;
     float G = 0.f, N = 1.f;
+    // G and N come back from returning atomics: in a hogwild batch of examples sharing dense features, each
+    // update must see the accumulators of the updates serialized before it (a plain load would hand every
+    // concurrent example the same tiny G and a huge first-step rate - measured: AUC 0.65 instead of 0.998)
     if (a.adaptive) G = atomicAdd(&w->y, grad_sq * x2) + grad_sq * x2;
     if (a.normalized) {
       const float ax = fabsf(x);
@@ -150,26 +172,29 @@ __device__ void UpdateWave(const SgdArgs& a, int64_t b, int64_t en, uint64_t off
       N = fmaxf(old, ax);
       norm_x += x2 / (N * N);
     }
-    ppu += x2 * Rate(a, G, N);
+    const float rt = Rate(a, G, N);
+    if (k < kRateCache) pr.rate[k] = rt;
+    ppu += x2 * rt;
   }
-  ppu = WaveSum(ppu);
-  norm_x = WaveSum(norm_x);
+  pr.g = g;
+  pr.ppu = WaveSum(ppu);
+  pr.norm_x = WaveSum(norm_x);
+  return pr;
+}
+
+// t, tw, snx: the global state including this update (what the sequential learner sees)
+__device__ void UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y,
+                                 float imp, int lane, const UpdPrep& pr, double t, double tw, double snx) {
   double eta = a.lr;
-  if (lane == 0) {
-    const double t = atomicAdd(&a.gs[0], static_cast<double>(imp)) + imp;
-    const double tw = atomicAdd(&a.gs[1], static_cast<double>(imp)) + imp;
-    const double snx = atomicAdd(&a.gs[2], static_cast<double>(imp) * norm_x) + static_cast<double>(imp) * norm_x;
-    if (a.normalized && snx > 0.0) {
-      const double avg = tw / snx;
-      eta *= a.adaptive ? sqrt(avg) : avg;
-    }
-    if (!a.adaptive) eta *= pow(static_cast<double>(a.initial_t) + t, -static_cast<double>(a.power_t));
+  if (a.normalized && snx > 0.0) {
+    const double avg = tw / snx;
+    eta *= a.adaptive ? sqrt(avg) : avg;
   }
-  eta = __shfl(eta, 0, 64);
+  if (!a.adaptive) eta *= pow(static_cast<double>(a.initial_t) + t, -static_cast<double>(a.power_t));
   const float us = static_cast<float>(eta) * imp;
   float update;
   if (a.invariant) {
-    const float pp = fmaxf(ppu, FLT_MIN);
+    const float pp = fmaxf(pr.ppu, FLT_MIN);
     if (a.loss == 0) {
       update = us * pp < 1e-6f ? 2.f * (y - raw) * us : (y - raw) * (1.f - expf(-2.f * us * pp)) / pp;
     } else {
@@ -177,18 +202,38 @@ __device__ void UpdateWave(const SgdArgs& a, int64_t b, int64_t en, uint64_t off
       update = fabsf(step * pp) > 50.f ? copysignf(50.f / pp, step) : step;
     }
   } else {
-    update = -g * us;
+    update = -pr.g * us;
   }
   const float decay = static_cast<float>(eta) * a.l2;
-  for (int64_t p = b + lane; p < en; p += 64) {
+  int k = 0;
+  for (int64_t p = b + lane; p < en; p += 64, ++k) {
     const uint64_t h = (a.idx[p] + off) & a.mask;
     float4* w = &a.W[h];
     const float x = a.val[p];
-    const float rate = Rate(a, a.adaptive ? w->y : 0.f, a.normalized ? w->z : 1.f);
-    const float nw = atomicAdd(&w->x, update * x * rate) + update * x * rate;
-    if (decay > 0.f) atomicAdd(&w->x, -decay * nw);
+    const float rate = k < kRateCache ? pr.rate[k] : Rate(a, a.adaptive ? w->y : 0.f, a.normalized ? w->z : 1.f);
+    if (decay > 0.f) {
+      const float nw = atomicAdd(&w->x, update * x * rate) + update * x * rate;
+      atomicAdd(&w->x, -decay * nw);
+    } else {
+      atomicAdd(&w->x, update * x * rate);  // result unused: a non-returning atomic
+    }
     a.dirty[h >> kDirtyShift] = 1;
   }
+}
+
+// whole update with its own global-state step (oaa: one per class update)
+__device__ void UpdateWave(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y, float imp,
+                           int lane) {
+  const UpdPrep pr = UpdateFirstPass(a, b, en, off, raw, y, imp, lane);
+  double t = 0.0, tw = 0.0, snx = 0.0;
+  if (lane == 0) {
+    t = atomicAdd(&a.gs[0], static_cast<double>(imp)) + imp;
+    tw = atomicAdd(&a.gs[1], static_cast<double>(imp)) + imp;
+    const double dn = static_cast<double>(imp) * pr.norm_x;
+    snx = atomicAdd(&a.gs[2], dn) + dn;
+  }
+  t = __shfl(t, 0, 64); tw = __shfl(tw, 0, 64); snx = __shfl(snx, 0, 64);
+  UpdateSecondPass(a, b, en, off, raw, y, imp, lane, pr, t, tw, snx);
 }
 
 __device__ __forceinline__ float LossOf(int loss, float p, float y) {
@@ -196,28 +241,56 @@ __device__ __forceinline__ float LossOf(int loss, float p, float y) {
   return (p - y) * (p - y);
 }
 
-// scalar learners: one wave per example
-__global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
+// scalar learners: one wave per example, kSgdWaves examples per block. The global learner state advances
+// with ONE device atomic per component per block (block sum; each wave takes its prefix), not one per
+// example: every update's t / tw / snx still includes exactly the updates ordered before it, and a
+// one-example launch (gpuBatchSize=1) is the sequential learner.
+constexpr int kSgdWaves = 16;
+
+__global__ __launch_bounds__(64 * kSgdWaves) void sgd_kernel(SgdArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t e = a.n0 + static_cast<int64_t>(blockIdx.x) * 4 + wid;
-  __shared__ float wloss[4];
+  const int64_t e = a.n0 + static_cast<int64_t>(blockIdx.x) * kSgdWaves + wid;
+  __shared__ float wloss[kSgdWaves];
+  __shared__ double s_imp[kSgdWaves], s_nx[kSgdWaves], s_base[3];
+  const bool act = e < a.n1;
+  int64_t b = 0, en = 0;
+  float raw = 0.f, y = 0.f, imp = 0.f;
   if (lane == 0) wloss[wid] = 0.f;
-  if (e < a.n1) {
-    const int64_t b = a.indptr[e], en = a.indptr[e + 1];
-    const float raw = Dot(a, b, en, 0, lane);
+  if (act) {
+    b = a.indptr[e]; en = a.indptr[e + 1];
+    raw = Dot(a, b, en, 0, lane);
     float p = isnan(raw) ? 0.f : raw;
     if (a.lo) p = fminf(fmaxf(p, a.lo[e]), a.hi[e]);  // the learner's running label range
     if (a.preds && lane == 0) a.preds[e] = p;
     if (a.learn) {
-      const float y = a.lab[e], imp = a.wt ? a.wt[e] : 1.f;
+      y = a.lab[e];
+      imp = a.wt ? a.wt[e] : 1.f;
       if (lane == 0) wloss[wid] = LossOf(a.loss, p, y) * imp;
-      if (imp > 0.f) UpdateWave(a, b, en, 0, raw, y, imp, lane);
     }
   }
-  if (a.learn) {
-    __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(a.loss_acc, wloss[0] + wloss[1] + wloss[2] + wloss[3]);
+  if (!a.learn) return;  // uniform over the launch
+  const bool upd = act && imp > 0.f;
+  UpdPrep pr{0.f, 0.f, 0.f};
+  if (upd) pr = UpdateFirstPass(a, b, en, 0, raw, y, imp, lane);
+  if (lane == 0) {
+    s_imp[wid] = upd ? static_cast<double>(imp) : 0.0;
+    s_nx[wid] = upd ? static_cast<double>(imp) * pr.norm_x : 0.0;
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double si = 0.0, sn = 0.0;
+    float sl = 0.f;
+    for (int w = 0; w < kSgdWaves; ++w) { si += s_imp[w]; sn += s_nx[w]; sl += wloss[w]; }
+    s_base[0] = si > 0.0 ? atomicAdd(&a.gs[0], si) : 0.0;
+    s_base[1] = si > 0.0 ? atomicAdd(&a.gs[1], si) : 0.0;
+    s_base[2] = sn > 0.0 ? atomicAdd(&a.gs[2], sn) : 0.0;
+    atomicAdd(a.loss_acc, sl);
+  }
+  __syncthreads();
+  if (!upd) return;
+  double pi = 0.0, pn = 0.0;
+  for (int w = 0; w <= wid; ++w) { pi += s_imp[w]; pn += s_nx[w]; }
+  UpdateSecondPass(a, b, en, 0, raw, y, imp, lane, pr, s_base[0] + pi, s_base[1] + pi, s_base[2] + pn);
 }
 
 // --oaa K: one block per example, wave c handles classes c, c + waves, ...: scores (predict), then the
@@ -337,8 +410,61 @@ __global__ void scatter_kernel(float4* __restrict__ W, uint64_t nw, const uint64
 
 }  // namespace
 
+// Host -> HBM copies of a pass's CSR through pinned staging buffers: the pageable path stages through one
+// runtime memcpy thread (~25 GB/s, and a 2M x 64-nonzero pass is 1 GB); here kStage buffers are filled by
+// kStageThreads CPU threads in parallel and drained by the copy engine, the CPU copy of piece k+1
+// overlapping the DMA of piece k.
+namespace {
+constexpr int kStage = 4;
+constexpr size_t kStageBytes = 32ull << 20;
+constexpr int kStageThreads = 8;
+
+// One per learner (its events are recorded on that learner's copy stream only), buffers allocated on first use.
+struct Stager {
+  std::mutex mu;
+  char* buf[kStage] = {};
+  hipEvent_t ev[kStage] = {};
+  bool used[kStage] = {};
+  int next = 0;
+  ~Stager() {
+    for (int k = 0; k < kStage; ++k) {
+      if (ev[k]) { (void)hipEventSynchronize(ev[k]); (void)hipEventDestroy(ev[k]); }
+      if (buf[k]) (void)hipHostFree(buf[k]);
+    }
+  }
+  // queue `bytes` from pageable `src` to device `dst` on stream s (caller holds mu)
+  void Copy(char* dst, const char* src, size_t bytes, hipStream_t s) {
+    for (size_t off = 0; off < bytes; off += kStageBytes) {
+      const int k = next;
+      next = (next + 1) % kStage;
+      if (!buf[k]) {
+        VW_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&buf[k]), kStageBytes, hipHostMallocDefault));
+        VW_HIP_CHECK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+      }
+      if (used[k]) VW_HIP_CHECK(hipEventSynchronize(ev[k]));
+      const size_t n = std::min(kStageBytes, bytes - off);
+      if (n < (1u << 20)) {
+        std::memcpy(buf[k], src + off, n);  // small pieces: a thread team costs more than the copy
+      } else {
+        const size_t per = (n + kStageThreads - 1) / kStageThreads;
+        std::vector<std::thread> th;
+        for (int t = 0; t < kStageThreads && t * per < n; ++t) {
+          const size_t a0 = t * per, a1 = std::min(n, a0 + per);
+          th.emplace_back([=]() { std::memcpy(buf[k] + a0, src + off + a0, a1 - a0); });
+        }
+        for (auto& x : th) x.join();
+      }
+      VW_HIP_CHECK(hipMemcpyAsync(dst + off, buf[k], n, hipMemcpyHostToDevice, s));
+      VW_HIP_CHECK(hipEventRecord(ev[k], s));
+      used[k] = true;
+    }
+  }
+};
+}  // namespace
+
 struct GpuSgd::Impl {
   hipStream_t stream = nullptr, copy_stream = nullptr;
+  Stager stager;  // pinned host->device staging of pass data (copy_stream)
   std::vector<hipEvent_t> events;
   float4* W = nullptr;
   uint64_t nw = 0;
@@ -469,8 +595,8 @@ void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
     hipLaunchKernelGGL(oaa_kernel, dim3(static_cast<unsigned>(b1 - b0)), dim3(64 * waves), sizeof(float) * cfg_.oaa,
                        impl_->stream, a);
   } else {
-    const int grid = static_cast<int>((b1 - b0 + 3) / 4);
-    hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, impl_->stream, a);
+    const int grid = static_cast<int>((b1 - b0 + kSgdWaves - 1) / kSgdWaves);
+    hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(64 * kSgdWaves), 0, impl_->stream, a);
   }
   VW_HIP_CHECK(hipGetLastError());
 }
@@ -501,9 +627,9 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
   if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), s));
   batch = std::max(1, batch);
-  // The pass's feature ids / values stream in chunks of 16 mini-batches on a copy stream: the
-  // (host-blocking, pageable) copy of chunk k+1 runs while the device learns chunk k, so the
-  // host->device traffic (8 B per nonzero) hides behind the SGD instead of preceding it.
+  // The pass's feature ids / values stream in chunks of 16 mini-batches: a native thread copies chunk
+  // k+1 through the pinned stager on the copy stream while the device learns chunk k (the launch loop waits
+  // on the host until a chunk's event is recorded, then on the device for the copy itself).
   const int64_t chunk_rows = static_cast<int64_t>(batch) * 16;
   const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
   for (size_t i = impl_->events.size(); i < static_cast<size_t>(nchunks); ++i) {
@@ -511,29 +637,117 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
     VW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     impl_->events.push_back(e);
   }
-  auto copy_chunk = [&](int64_t c) {
-    const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
-    const size_t p0 = static_cast<size_t>(ip[r0]), p1 = static_cast<size_t>(ip[r1]);
-    if (p1 > p0) {
-      VW_HIP_CHECK(hipMemcpyAsync(impl_->idx + p0, indices + indptr[0] + p0, (p1 - p0) * sizeof(uint32_t),
-                                  hipMemcpyHostToDevice, cs));
-      VW_HIP_CHECK(hipMemcpyAsync(impl_->val + p0, values + indptr[0] + p0, (p1 - p0) * sizeof(float),
-                                  hipMemcpyHostToDevice, cs));
+  std::mutex rmu;
+  std::condition_variable rcv;
+  int64_t recorded = 0;
+  std::string upload_error;
+  const int dev = [] { int d = 0; (void)hipGetDevice(&d); return d; }();
+  std::thread uploader([&]() {
+    try {
+      VW_HIP_CHECK(hipSetDevice(dev));
+      Stager& st = impl_->stager;
+      std::lock_guard<std::mutex> lk(st.mu);
+      for (int64_t c = 0; c < nchunks; ++c) {
+        const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
+        const size_t p0 = static_cast<size_t>(ip[r0]), p1 = static_cast<size_t>(ip[r1]);
+        if (p1 > p0) {
+          st.Copy(reinterpret_cast<char*>(impl_->idx + p0), reinterpret_cast<const char*>(indices + indptr[0] + p0),
+                  (p1 - p0) * sizeof(uint32_t), cs);
+          st.Copy(reinterpret_cast<char*>(impl_->val + p0), reinterpret_cast<const char*>(values + indptr[0] + p0),
+                  (p1 - p0) * sizeof(float), cs);
+        }
+        VW_HIP_CHECK(hipEventRecord(impl_->events[c], cs));
+        std::lock_guard<std::mutex> g(rmu);
+        recorded = c + 1;
+        rcv.notify_all();
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(rmu);
+      upload_error = e.what();
+      recorded = nchunks;  // release the launch loop; it rethrows
+      rcv.notify_all();
     }
-    VW_HIP_CHECK(hipEventRecord(impl_->events[c], cs));
-  };
-  copy_chunk(0);
-  for (int64_t c = 0; c < nchunks; ++c) {
-    VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
-    const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
-    for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, weights != nullptr);
-    if (c + 1 < nchunks) copy_chunk(c + 1);
+  });
+  try {
+    for (int64_t c = 0; c < nchunks; ++c) {
+      {
+        std::unique_lock<std::mutex> g(rmu);
+        rcv.wait(g, [&] { return recorded > c; });
+        if (!upload_error.empty()) break;
+      }
+      VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
+      const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
+      for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, weights != nullptr);
+    }
+  } catch (...) {
+    uploader.join();
+    throw;
   }
+  uploader.join();
+  if (!upload_error.empty()) throw std::runtime_error("VW pass upload failed: " + upload_error);
   float l = 0;
   VW_HIP_CHECK(hipMemcpyAsync(&l, impl_->loss, sizeof(float), hipMemcpyDeviceToHost, s));
   if (preds_out) VW_HIP_CHECK(hipMemcpyAsync(preds_out, impl_->pred, n * sizeof(float), hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
   examples_ += n;
+  sum_loss_ += l;
+}
+
+// Device-resident pass data (VW's cache for multi-pass training): the CSR, labels and weights are uploaded
+// once; LearnStaged(r0, r1) then learns rows [r0, r1) from HBM - passes and sync segments re-read nothing
+// over PCIe. Only the per-row label-range clamp bounds of the rows being learned move (8 B / row).
+void GpuSgd::Stage(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
+                   const float* weights, int64_t n) {
+  if (n < 0) throw std::runtime_error("negative row count");
+  const size_t nnz = static_cast<size_t>(n ? indptr[n] - indptr[0] : 0);
+  impl_->Reserve(std::max<int64_t>(1, n), nnz);
+  hipStream_t s = impl_->stream, cs = impl_->copy_stream;
+  std::vector<int64_t> ip(indptr, indptr + n + 1);
+  for (auto& v : ip) v -= indptr[0];
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->indptr, ip.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  if (n) {
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->lab, labels, n * sizeof(float), hipMemcpyHostToDevice, s));
+    if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
+  }
+  if (nnz) {
+    Stager& st = impl_->stager;
+    std::lock_guard<std::mutex> lk(st.mu);
+    st.Copy(reinterpret_cast<char*>(impl_->idx), reinterpret_cast<const char*>(indices + indptr[0]),
+            nnz * sizeof(uint32_t), cs);
+    st.Copy(reinterpret_cast<char*>(impl_->val), reinterpret_cast<const char*>(values + indptr[0]), nnz * sizeof(float),
+            cs);
+    VW_HIP_CHECK(hipStreamSynchronize(cs));
+  }
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  staged_labels_.assign(labels, labels + n);
+  staged_n_ = n;
+  staged_weights_ = weights != nullptr;
+}
+
+void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
+  if (r0 < 0 || r1 > staged_n_ || r0 > r1) throw std::runtime_error("LearnStaged: rows outside the staged set");
+  if (r1 == r0) return;
+  hipStream_t s = impl_->stream;
+  const int64_t m = r1 - r0;
+  std::vector<float> lo(m), hi(m);
+  for (int64_t i = 0; i < m; ++i) {
+    if (cfg_.loss != 1 && cfg_.oaa == 0) {
+      min_label_ = std::min<double>(min_label_, staged_labels_[r0 + i]);
+      max_label_ = std::max<double>(max_label_, staged_labels_[r0 + i]);
+    }
+    lo[i] = static_cast<float>(min_label_);
+    hi[i] = static_cast<float>(max_label_);
+  }
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->lo + r0, lo.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->hi + r0, hi.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
+  VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), s));
+  batch = std::max(1, batch);
+  for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, staged_weights_);
+  float l = 0;
+  VW_HIP_CHECK(hipMemcpyAsync(&l, impl_->loss, sizeof(float), hipMemcpyDeviceToHost, s));
+  if (preds_out) VW_HIP_CHECK(hipMemcpyAsync(preds_out, impl_->pred + r0, m * sizeof(float), hipMemcpyDeviceToHost, s));
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  examples_ += m;
   sum_loss_ += l;
 }
 
@@ -561,7 +775,8 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
     const int waves = std::min(cfg_.oaa, kOaaMaxWaves);
     hipLaunchKernelGGL(oaa_kernel, dim3(static_cast<unsigned>(n)), dim3(64 * waves), sizeof(float) * cfg_.oaa, s, a);
   } else {
-    hipLaunchKernelGGL(sgd_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(sgd_kernel, dim3(static_cast<unsigned>((n + kSgdWaves - 1) / kSgdWaves)), dim3(64 * kSgdWaves), 0,
+                       s, a);
   }
   VW_HIP_CHECK(hipGetLastError());
   VW_HIP_CHECK(hipMemcpyAsync(out, impl_->pred, n * sizeof(float), hipMemcpyDeviceToHost, s));

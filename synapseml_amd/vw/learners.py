@@ -294,12 +294,13 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     segs = max(0, int(est.getNumSyncsPerPass() or 0)) + 1
     bounds = np.linspace(0, n, segs + 1).astype(np.int64)
     sync_bytes = []
+    # the partition's CSR goes to HBM once; every pass and sync segment learns from there (VW's cache file)
+    g.stage(indptr, idx, val, np.ascontiguousarray(labels, dtype=np.float32),
+            None if weights is None else np.ascontiguousarray(weights, dtype=np.float32))
     for _ in range(max(1, est.getNumPasses())):
         for s0, s1 in zip(bounds[:-1], bounds[1:]):
             if s1 > s0:
-                ip = indptr[s0:s1 + 1]
-                g.learn(ip - ip[0], idx[ip[0]:ip[-1]], val[ip[0]:ip[-1]], labels[s0:s1],
-                        None if weights is None else weights[s0:s1], int(est.getGpuBatchSize()))
+                g.learn_staged(int(s0), int(s1), int(est.getGpuBatchSize()))
             if comm is not None:
                 g.allreduce_average(comm)
                 sync_bytes.append(int(g.last_sync_bytes))

@@ -63,6 +63,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=16384, help="hogwild mini-batch (examples in flight)")
+    ap.add_argument("--resident", action="store_true",
+                    help="multi-pass mode: the pass is staged in HBM once and every step re-learns it from there")
     args = ap.parse_args()
     import torch
 
@@ -92,9 +94,16 @@ def main() -> None:
     hold = make_pass(100_000, args.nnz, seed=999_999)
     ar_ms, sync_mb = [], []
 
+    if args.resident:
+        ip0, ix0, vl0, y0 = passes[0]
+        g.stage(ip0, ix0, vl0, y0)
+
     def one_pass(i):
-        ip, ix, vl, y = passes[i % 2]
-        g.learn(ip, ix, vl, y, None, args.batch)
+        if args.resident:
+            g.learn_staged(0, args.rows, args.batch)
+        else:
+            ip, ix, vl, y = passes[i % 2]
+            g.learn(ip, ix, vl, y, None, args.batch)
         if comm is not None:
             t = time.perf_counter()
             g.allreduce_average(comm)
@@ -130,7 +139,7 @@ def main() -> None:
             "nnz_per_row": args.nnz, "batch": args.batch, "ms_per_pass": round(elapsed / args.steps * 1e3, 2),
             "allreduce_ms_per_pass": round(float(np.mean(ar_ms)), 2) if ar_ms else None,
             "allreduce_mib_per_pass": round(float(np.mean(sync_mb)), 1) if sync_mb else None,
-            "holdout_logloss": round(logloss, 4),
+            "holdout_logloss": round(logloss, 4), "pass_data": "resident in HBM" if args.resident else "uploaded per pass",
             "data": "synthetic hashed sparse (2^24-id vocabulary of 32-bit hashes, Zipf-like popularity, planted model)"}), flush=True)
     if world > 1:
         import torch.distributed as dist
