@@ -236,6 +236,12 @@ class _DiDParams(Params):
 class DiffInDiffModel(Model, _DiDParams):
     timeCol = Param("time column", "time", T.toString)
     unitCol = Param("unit column", "unit", T.toString)
+    # the synthetic estimators' index DataFrames: position in timeWeights / unitWeights <-> time / unit value
+    # (BaseDiffInDiffEstimator.scala:105-119)
+    timeIndex = Param("time index", None, complex=True)
+    timeIndexCol = Param("time index column", "time_index", T.toString)
+    unitIndex = Param("unit index", None, complex=True)
+    unitIndexCol = Param("unit index column", "unit_index", T.toString)
 
     def getSummary(self) -> DiffInDiffSummary:  # noqa: N802
         if getattr(self, "_summary", None) is None:
@@ -256,6 +262,14 @@ class DiffInDiffModel(Model, _DiDParams):
 
     def _transform(self, df):
         return df
+
+    def _set_indexes(self, units, times) -> None:
+        """timeIndex / unitIndex DataFrames (value, index) as the reference's synthetic estimators set them."""
+        self._unit_index, self._time_index = _obj(units), _obj(times)
+        self.set("timeIndex", DataFrame({self.getTimeCol(): _obj(times),
+                                         self.getTimeIndexCol(): np.arange(len(times), dtype=np.int64)}))
+        self.set("unitIndex", DataFrame({self.getUnitCol(): _obj(units),
+                                         self.getUnitIndexCol(): np.arange(len(units), dtype=np.int64)}))
 
 
 def _weighted_did(y, treat, post, w) -> DiffInDiffSummary:
@@ -373,7 +387,8 @@ class SyntheticControlEstimator(Estimator, _SyntheticParams):
         s.lossHistoryUnitWeights = hist
         m = DiffInDiffModel(treatmentCol=self.getTreatmentCol(), postTreatmentCol=self.getPostTreatmentCol(),
                             outcomeCol=self.getOutcomeCol(), timeCol=self.getTimeCol(), unitCol=self.getUnitCol())
-        m._summary, m._unit_index, m._time_index = s, _obj(units), _obj(times)
+        m._summary = s
+        m._set_indexes(units, times)
         return m
 
 
@@ -402,7 +417,8 @@ class SyntheticDiffInDiffEstimator(Estimator, _SyntheticParams):
         s.lossHistoryUnitWeights, s.lossHistoryTimeWeights = uh, th
         m = DiffInDiffModel(treatmentCol=self.getTreatmentCol(), postTreatmentCol=self.getPostTreatmentCol(),
                             outcomeCol=self.getOutcomeCol(), timeCol=self.getTimeCol(), unitCol=self.getUnitCol())
-        m._summary, m._unit_index, m._time_index = s, _obj(units), _obj(times)
+        m._summary = s
+        m._set_indexes(units, times)
         return m
 
 

@@ -80,6 +80,11 @@ def test_simplex_ls_and_synthetic_estimators():
     sdid = SyntheticDiffInDiffEstimator(maxIter=3000, tol=1e-12).fit(df)
     assert sdid.getSummary().treatmentEffect == pytest.approx(5.0, abs=0.5)
     assert sdid.getTimeWeights() is not None
+    # index DataFrames map weight positions to time / unit values (BaseDiffInDiffEstimator.scala:105-119)
+    ti, ui = sdid.getTimeIndex(), sdid.getUnitIndex()
+    assert ti.count() == T_ and ui.count() == U
+    assert list(ti[sdid.getTimeIndexCol()]) == list(range(T_)) and list(ti["time"]) == list(range(T_))
+    assert list(ui["unit"]) == list(range(U))
 
 
 def test_ortho_forest_variable_transformer():
