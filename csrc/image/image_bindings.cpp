@@ -7,6 +7,7 @@
 #include <stdexcept>
 
 #include "image_cpu.h"
+#include "jpeg_decode.h"
 
 namespace py = pybind11;
 using namespace smlimg;
@@ -90,6 +91,64 @@ PYBIND11_MODULE(_image, m) {
     py::array_t<float> out({co, d.h, d.w});
     ToTensorHost(img.data(), d.h, d.w, d.c, chan_map.data(), co, scale, mean.data(), stdv.data(), out.mutable_data());
     return out;
+  });
+
+  // ---------------------------------------------------------------- JPEG decode
+  m.def("jpeg_probe", [](const std::vector<py::bytes>& files) {
+    const py::ssize_t n = static_cast<py::ssize_t>(files.size());
+    py::array_t<int32_t> out({n, py::ssize_t(4)});  // height, width, channels, supported
+    auto o = out.mutable_unchecked<2>();
+    for (py::ssize_t i = 0; i < n; ++i) {
+      char* p = nullptr;
+      py::ssize_t len = 0;
+      PyBytes_AsStringAndSize(files[i].ptr(), &p, &len);
+      JpegInfo info = JpegProbe(reinterpret_cast<const uint8_t*>(p), static_cast<size_t>(len));
+      o(i, 0) = info.height; o(i, 1) = info.width; o(i, 2) = info.channels; o(i, 3) = info.supported ? 1 : 0;
+    }
+    return out;
+  });
+  m.def("jpeg_decode", [](py::bytes data) -> py::object {
+    char* p = nullptr;
+    py::ssize_t len = 0;
+    PyBytes_AsStringAndSize(data.ptr(), &p, &len);
+    JpegInfo info = JpegProbe(reinterpret_cast<const uint8_t*>(p), static_cast<size_t>(len));
+    if (!info.supported) return py::none();
+    U8 out = NewImage(info.height, info.width, info.channels);
+    std::string why;
+    uint8_t* dst = out.mutable_data();
+    const size_t cap = static_cast<size_t>(out.nbytes());
+    bool ok;
+    {
+      py::gil_scoped_release rel;
+      ok = JpegDecode(reinterpret_cast<const uint8_t*>(p), static_cast<size_t>(len), dst, cap, &why);
+    }
+    if (!ok) return py::none();
+    return std::move(out);
+  });
+  // batch decode straight into a caller-owned buffer (e.g. pinned host memory): image i -> out + offsets[i],
+  // sizes[i] bytes reserved (from jpeg_probe); returns per-image success flags (0 -> caller falls back)
+  m.def("jpeg_decode_into", [](const std::vector<py::bytes>& files, uintptr_t out, uint64_t out_len,
+                               std::vector<int64_t> offsets, std::vector<int64_t> sizes, int threads) {
+    const size_t n = files.size();
+    if (offsets.size() != n || sizes.size() != n) throw std::invalid_argument("offsets / sizes length mismatch");
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<size_t> lens(n);
+    for (size_t i = 0; i < n; ++i) {
+      char* p = nullptr;
+      py::ssize_t len = 0;
+      PyBytes_AsStringAndSize(files[i].ptr(), &p, &len);
+      ptrs[i] = reinterpret_cast<const uint8_t*>(p);
+      lens[i] = static_cast<size_t>(len);
+      if (offsets[i] >= 0 && (sizes[i] < 0 || static_cast<uint64_t>(offsets[i]) + static_cast<uint64_t>(sizes[i]) > out_len))
+        throw std::invalid_argument("jpeg_decode_into: image slot outside the output buffer");
+    }
+    py::array_t<uint8_t> ok(static_cast<py::ssize_t>(n));
+    uint8_t* okp = ok.mutable_data();
+    {
+      py::gil_scoped_release rel;
+      JpegDecodeBatch(ptrs, lens, Ptr<uint8_t>(out), offsets, sizes, okp, threads);
+    }
+    return ok;
   });
 
   // ---------------------------------------------------------------- device

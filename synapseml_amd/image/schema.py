@@ -3,7 +3,8 @@ mode, data — data is row-major BGR(A)/gray uint8) and decoding.
 
 Reference: opencv/.../ImageTransformer.scala:285-330 (row2mat / decodeImage),
 core/.../schema/ImageSchemaUtils.scala; mode codes CV_8UC1=0, CV_8UC3=16,
-CV_8UC4=24. Decoding uses PIL (JPEG/PNG/BMP/...)."""
+CV_8UC4=24. Baseline JPEGs decode natively (csrc/image/jpeg_decode.cpp, pixel-identical to
+PIL's libjpeg), everything else (progressive JPEG, PNG, BMP, ...) through PIL."""
 from __future__ import annotations
 
 import io
@@ -42,8 +43,14 @@ def row_to_array(row) -> np.ndarray:
 
 
 def decode_bytes(data: bytes) -> np.ndarray:
-    """Encoded image bytes -> HWC uint8 in OpenCV order (BGR / BGRA / gray)."""
+    """Encoded image bytes -> HWC uint8 in OpenCV order (BGR / BGRA / gray). Baseline JPEGs go through
+    the native decoder (same pixels as PIL, no GIL held), everything else through PIL."""
     from PIL import Image
+
+    if bytes(data[:2]) == b"\xff\xd8":
+        a = decode_jpeg_native(data)
+        if a is not None:
+            return np.ascontiguousarray(a[:, :, ::-1]) if a.shape[2] == 3 else a
 
     with Image.open(io.BytesIO(bytes(data))) as im:
         if im.mode in ("L", "1", "I;16", "I", "F"):
@@ -62,10 +69,124 @@ def decode_bytes_rgb(data: bytes):
     modes fall back to decode_bytes (OpenCV order, is_rgb False)."""
     from PIL import Image
 
+    if bytes(data[:2]) == b"\xff\xd8":
+        a = decode_jpeg_native(data)
+        if a is not None:
+            return (a, True) if a.shape[2] == 3 else (a, False)
     with Image.open(io.BytesIO(bytes(data))) as im:
         if im.mode == "RGB":
             return np.asarray(im), True
     return decode_bytes(data), False
+
+
+def decode_jpeg_native(data: bytes) -> Optional[np.ndarray]:
+    """Baseline JPEG -> HWC uint8 (RGB, or gray as HxWx1) with the native decoder (csrc/image/jpeg_decode.cpp,
+    pixel-identical to PIL's libjpeg decode), or None when the file is outside its scope (progressive,
+    CMYK, ...), the extension is not built, or ``SML_NATIVE_JPEG=0`` (A/B against PIL)."""
+    if os.environ.get("SML_NATIVE_JPEG", "1") == "0":
+        return None
+    try:
+        from ..ops import native
+
+        a = native.load("_image").jpeg_decode(bytes(data))
+    except (ImportError, OSError):
+        return None
+    if a is None:
+        return None
+    return a if a.ndim == 3 else a[:, :, None]
+
+
+def pack_decoded(values, ignore_errors: bool = False, threads: int = 8, pinned: bool = False):
+    """Decode a batch of image values (encoded bytes, image rows or arrays) into ONE contiguous uint8 buffer.
+
+    JPEGs in the native decoder's scope are decoded by a pool of native threads straight into the buffer
+    (no per-image Python, no GIL, no intermediate array); everything else goes through PIL / the row
+    readers and is copied in. With ``pinned`` the buffer is page-locked host memory, ready for an
+    asynchronous H2D copy. Returns ``(buf, offsets, shapes, rgb, ok)``: image i is ``shapes[i]`` (h, w, c)
+    at ``offsets[i]``; ``rgb[i]`` marks 3-channel images in RGB order (JPEG decodes) rather than OpenCV's
+    BGR; ``ok[i]`` is False for an undecodable value (only with ``ignore_errors``; otherwise it raises).
+    """
+    n = len(values)
+    shapes: List[Optional[tuple]] = [None] * n
+    rgb = [False] * n
+    arrays: List[Optional[np.ndarray]] = [None] * n
+    jidx, jbytes = [], []
+    for i, v in enumerate(values):
+        if isinstance(v, (bytes, bytearray, memoryview)):
+            jidx.append(i)
+            jbytes.append(v if isinstance(v, bytes) else bytes(v))
+    lib = None
+    native_idx: List[int] = []
+    if jbytes and os.environ.get("SML_NATIVE_JPEG", "1") != "0":
+        try:
+            from ..ops import native
+
+            lib = native.load("_image")
+        except (ImportError, OSError):
+            lib = None
+    if lib is not None:
+        info = lib.jpeg_probe(jbytes)
+        for k, i in enumerate(jidx):
+            h, w, c, sup = (int(x) for x in info[k])
+            if sup:
+                shapes[i] = (h, w, c)
+                rgb[i] = c == 3
+                native_idx.append(i)
+    native_set = set(native_idx)
+
+    def fallback(i):
+        v = values[i]
+        try:
+            if isinstance(v, (bytes, bytearray, memoryview)):
+                a, r = decode_bytes_rgb(v)
+            else:
+                a, r = to_array(v, ignore_errors), False
+        except Exception:
+            if ignore_errors:
+                return None, False
+            raise
+        if a is not None and a.ndim == 2:
+            a = a[:, :, None]
+        return a, r
+
+    for i in range(n):
+        if i not in native_set:
+            arrays[i], rgb[i] = fallback(i)
+            if arrays[i] is not None:
+                shapes[i] = arrays[i].shape
+    sizes = np.array([int(np.prod(sh)) if sh is not None else 0 for sh in shapes], np.int64)
+    offsets = np.zeros(n, np.int64)
+    if n:
+        offsets[1:] = np.cumsum(sizes)[:-1]
+    total = int(sizes.sum())
+    if pinned:
+        import torch
+
+        buf = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+        view, ptr = buf.numpy(), buf.data_ptr()
+    else:
+        buf = view = np.empty(max(total, 1), np.uint8)
+        ptr = view.ctypes.data
+    if native_idx:
+        nb = [values[i] if isinstance(values[i], bytes) else bytes(values[i]) for i in native_idx]
+        okn = lib.jpeg_decode_into(nb, ptr, max(total, 1), [int(offsets[i]) for i in native_idx],
+                                   [int(sizes[i]) for i in native_idx], max(1, int(threads)))
+        for k, i in enumerate(native_idx):
+            if not okn[k]:  # corrupt / truncated: let PIL decide (it may recover or raise)
+                a, r = fallback(i)
+                if a is not None and a.shape != shapes[i]:
+                    a = None
+                arrays[i], rgb[i] = a, r
+                if a is None:
+                    shapes[i] = None
+    for i in range(n):
+        a = arrays[i]
+        if a is not None:
+            view[offsets[i]:offsets[i] + a.size] = np.ascontiguousarray(a).reshape(-1)
+    ok = [sh is not None for sh in shapes]
+    if not ignore_errors and not all(ok) and any(v is not None for v, o in zip(values, ok) if not o):
+        raise ValueError("undecodable image in batch")
+    return buf, offsets, shapes, rgb, ok
 
 
 def encode_png(arr: np.ndarray) -> bytes:

@@ -253,8 +253,8 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         return self
 
     # ---- execution
-    def _fused_plan(self, arrays: List[np.ndarray]):
-        """(resize_h, resize_w, crop) when the stage list maps onto K19 for this batch."""
+    def _fused_plan(self, shapes: List[tuple]):
+        """(resize_h, resize_w, crop) when the stage list maps onto K19 for a batch of (h, w, c) shapes."""
         st = list(self.getStages() or [])
         if not self.getToTensor() or self.getTensorElementType().lower() != "float":
             return None
@@ -271,10 +271,10 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
             i += 1
         if i != len(st):
             return None
-        shapes = {a.shape[:2] for a in arrays}
-        if rs is None and len(shapes) != 1:
+        hw = {tuple(sh[:2]) for sh in shapes}
+        if rs is None and len(hw) != 1:
             return None
-        base_h, base_w = rs if rs is not None else next(iter(shapes))
+        base_h, base_w = rs if rs is not None else next(iter(hw))
         if crop is None:
             cy, cx, ch, cw = 0, 0, base_h, base_w
         elif stage_action(crop) == "centercrop":
@@ -283,7 +283,7 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
             cy, cx, ch, cw = int(crop["y"]), int(crop["x"]), int(crop["height"]), int(crop["width"])
             if cy + ch > base_h or cx + cw > base_w:
                 return None
-        if len({a.shape[2] for a in arrays}) != 1:
+        if len({sh[2] for sh in shapes}) != 1:
             return None
         return (rs or (0, 0)), (cy, cx, ch, cw)
 
@@ -302,15 +302,9 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         kernel's channel map absorbs the difference."""
         import torch
 
-        plan = self._fused_plan(arrays)
-        if plan is None or not arrays:
+        shapes = [a.shape for a in arrays]
+        if not arrays or self._fused_plan(shapes) is None:
             return None
-        (rh, rw), (cy, cx, ch, cw) = plan
-        c = arrays[0].shape[2]
-        cmap = channel_map(c, self.getTensorChannelOrder(), self.getAutoConvertToColor())
-        if src_rgb and c == 3:
-            cmap = [2 - k for k in cmap]
-        mean, std, scale = self._norm_params(len(cmap))
         sizes = [a.size for a in arrays]
         offsets = np.zeros(len(arrays), np.int64)
         offsets[1:] = np.cumsum(sizes)[:-1]
@@ -318,17 +312,34 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         hv = host.numpy()
         for a, o in zip(arrays, offsets):
             hv[o:o + a.size] = a.reshape(-1)
-        dims = np.array([[a.shape[0], a.shape[1], a.shape[2]] for a in arrays], np.int32).reshape(-1)
+        return self.device_tensors_packed(host, offsets, shapes, dtype, nhwc, src_rgb)
+
+    def device_tensors_packed(self, host, offsets: np.ndarray, shapes: List[tuple], dtype: str = "float32",
+                              nhwc: bool = False, src_rgb: bool = False):
+        """:meth:`device_tensors` on images already packed into one pinned uint8 buffer (image i at
+        ``offsets[i]``, HWC ``shapes[i]``) - e.g. written there directly by the native JPEG decoder."""
+        import torch
+
+        plan = self._fused_plan(shapes)
+        if plan is None or not shapes:
+            return None
+        (rh, rw), (cy, cx, ch, cw) = plan
+        c = shapes[0][2]
+        cmap = channel_map(c, self.getTensorChannelOrder(), self.getAutoConvertToColor())
+        if src_rgb and c == 3:
+            cmap = [2 - k for k in cmap]
+        mean, std, scale = self._norm_params(len(cmap))
+        dims = np.array([[sh[0], sh[1], sh[2]] for sh in shapes], np.int32).reshape(-1)
         dev = torch.device("cuda", torch.cuda.current_device())
         src = host.to(dev, non_blocking=True)
-        off_d = torch.from_numpy(offsets).to(dev, non_blocking=True)
+        off_d = torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).to(dev, non_blocking=True)
         dims_d = torch.from_numpy(dims).to(dev, non_blocking=True)
         tdt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[dtype]
-        B = len(arrays)
+        B = len(shapes)
         out = torch.empty((B, ch, cw, len(cmap)) if nhwc else (B, len(cmap), ch, cw), dtype=tdt, device=dev)
         if min(rh, rw) == 0:
-            for a in arrays:
-                if cy + ch > a.shape[0] or cx + cw > a.shape[1]:
+            for sh in shapes:
+                if cy + ch > sh[0] or cx + cw > sh[1]:
                     raise ValueError("crop rectangle outside the image")
         _img().preprocess_batch_device(src.data_ptr(), off_d.data_ptr(), dims_d.data_ptr(), B, ch, cw, rh, rw, cy, cx,
                                        cmap, scale, mean, std, {torch.float32: 0, torch.float16: 1,

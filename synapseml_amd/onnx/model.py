@@ -551,25 +551,17 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
         return res.withColumn(self.getOutputCol(), vec).drop(tmp)
 
     def _transform_device(self, df: DataFrame, model: ONNXModel, img_name: str, out_name: str) -> DataFrame:
-        """GPU path: decode on a host thread pool running ahead of the device, one fused preprocess kernel per
-        batch writes the input tensor straight into device memory, the session consumes it without a host
-        round trip. Batch k+1.. decode (PIL releases the GIL) while batch k preprocesses + runs on the GPU."""
+        """GPU path: each batch is decoded into one pinned host buffer (baseline JPEGs by the native
+        multi-threaded decoder, straight into the buffer; anything else through PIL), one fused preprocess
+        kernel per batch writes the input tensor straight into device memory, and the session consumes it
+        without a host round trip. Decoding runs two batches ahead of the device on a helper thread (the
+        native decoder releases the GIL), so batch k+1.. decode while batch k preprocesses + runs."""
         import os as _os
         from concurrent.futures import ThreadPoolExecutor
 
         import torch
 
-        from ..image.schema import decode_bytes_rgb, to_array
-
-        def decode(v):
-            if isinstance(v, (bytes, bytearray, memoryview)):
-                try:
-                    return decode_bytes_rgb(v)
-                except Exception:
-                    if ign:
-                        return None, False
-                    raise
-            return to_array(v, ign), False
+        from ..image.schema import pack_decoded
 
         tr = self._image_transformer("__unused__")
         values = df[self.getInputCol()].tolist()
@@ -580,32 +572,52 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
         # larger device batches amortise launches; results are identical per row
         bs = max(bs, 64)
         prec = {torch.float32: "float32", torch.float16: "float16", torch.bfloat16: "bfloat16"}[sess.compute_dtype]
-        workers = max(1, min(16, (_os.cpu_count() or 8)))
+        threads = max(1, min(16, (_os.cpu_count() or 8)))
         keep = np.ones(len(values), dtype=bool)
         outs = []
         pending = None
-        with ThreadPoolExecutor(max_workers=workers) as ex:
-            # every batch's decode is queued up front: the pool stays ahead of the device loop below
-            futs = [[ex.submit(decode, v) for v in values[s:s + bs]] for s in range(0, len(values), bs)]
-            for k, fs in enumerate(futs):
-                pairs = [f.result() for f in fs]
-                for j, (a, _) in enumerate(pairs):
-                    if a is None:
-                        keep[k * bs + j] = False
-                pairs = [(a, rgb) for a, rgb in pairs if a is not None]
-                if not pairs:
+        starts = list(range(0, len(values), bs))
+        lookahead = 2
+        with ThreadPoolExecutor(max_workers=lookahead) as ex:
+            futs = {}
+
+            def submit(k):
+                if k < len(starts) and k not in futs:
+                    s0 = starts[k]
+                    futs[k] = ex.submit(pack_decoded, values[s0:s0 + bs], ign, threads, True)
+
+            for k in range(lookahead):
+                submit(k)
+            for k, s0 in enumerate(starts):
+                buf, offs, shapes, rgb, ok = futs.pop(k).result()
+                submit(k + lookahead)
+                sel = [j for j, o in enumerate(ok) if o]
+                for j, o in enumerate(ok):
+                    if not o:
+                        keep[s0 + j] = False
+                if not sel:
                     continue
-                all_rgb = all(rgb for _, rgb in pairs)
-                # a batch mixing RGB-decoded bytes with OpenCV-order rows goes through in OpenCV order
-                chunk = [a if (all_rgb or not rgb) else np.ascontiguousarray(a[:, :, ::-1]) for a, rgb in pairs]
-                t = tr.device_tensors(chunk, dtype=prec, nhwc=sess.channels_last, src_rgb=all_rgb)
+                shp = [shapes[j] for j in sel]
+                color = [j for j in sel if shapes[j][2] == 3]
+                all_rgb = bool(color) and all(rgb[j] for j in color)
+                hv = buf.numpy()
+                if not all_rgb:
+                    # a batch mixing RGB-decoded JPEGs with OpenCV-order rows goes through in OpenCV order
+                    for j in color:
+                        if rgb[j]:
+                            v = hv[offs[j]:offs[j] + int(np.prod(shapes[j]))].reshape(shapes[j])
+                            v[...] = v[:, :, ::-1].copy()
+                t = tr.device_tensors_packed(buf, offs[sel], shp, dtype=prec, nhwc=sess.channels_last,
+                                             src_rgb=all_rgb)
                 if t is None:
-                    if all_rgb:
-                        chunk = [np.ascontiguousarray(a[:, :, ::-1]) if a.shape[2] == 3 else a for a in chunk]
+                    chunk = []
+                    for j in sel:
+                        a = hv[offs[j]:offs[j] + int(np.prod(shapes[j]))].reshape(shapes[j])
+                        chunk.append(np.ascontiguousarray(a[:, :, ::-1]) if all_rgb and a.shape[2] == 3 else a.copy())
                     t = torch.from_numpy(np.stack([tr.process_host(a) for a in chunk]))
                 # batch k is queued (preprocess + graph replay + D2H into pinned memory) before batch k-1 is
                 # collected: the host packs / converts while the GPU runs
-                nxt = (sess.run_async([out_name], {img_name: t}), len(chunk))
+                nxt = (sess.run_async([out_name], {img_name: t}), len(sel))
                 if pending is not None:
                     outs.append(np.asarray(pending[0].result()[0], dtype=np.float64).reshape(pending[1], -1))
                 pending = nxt

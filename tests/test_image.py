@@ -215,3 +215,76 @@ def test_reference_action_keyed_stage_list():
     assert stage_action({"action": "blur"}) == "blur"
     with pytest.raises(KeyError):
         stage_action({"height": 3})
+
+
+def _jpeg(a, **kw):
+    import io
+
+    from PIL import Image
+
+    b = io.BytesIO()
+    Image.fromarray(a).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _noise_image(h, w, seed=0):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = np.stack([x * 255 // max(w - 1, 1), y * 255 // max(h - 1, 1), ((x + y) * 3) % 256], -1)
+    return np.clip(base + rng.normal(0, 20, (h, w, 3)), 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (7, 9), (17, 33), (224, 224), (101, 67)])
+def test_native_jpeg_decoder_matches_pil(shape):
+    """csrc/image/jpeg_decode.cpp reproduces libjpeg's ISLOW IDCT, fancy upsampling and YCbCr tables: the
+    pixels equal PIL's decode exactly for 4:4:4 / 4:2:2 / 4:2:0, gray, restart intervals and optimised
+    Huffman tables; progressive files are declined (-> PIL)."""
+    import io
+
+    from PIL import Image
+
+    from synapseml_amd.image.schema import decode_jpeg_native
+
+    a = _noise_image(*shape)
+    files = [_jpeg(a, quality=q, subsampling=s) for q in (50, 95) for s in (0, 1, 2)]
+    files += [_jpeg(a[:, :, 0]), _jpeg(a, restart_marker_blocks=3), _jpeg(a, optimize=True)]
+    for d in files:
+        with Image.open(io.BytesIO(d)) as im:
+            ref = np.asarray(im)
+        got = decode_jpeg_native(d)
+        assert got is not None
+        np.testing.assert_array_equal(got, ref if ref.ndim == 3 else ref[:, :, None])
+    assert decode_jpeg_native(_jpeg(a, progressive=True)) is None
+    d = files[0]
+    assert decode_jpeg_native(d[: len(d) // 2]) is None  # truncated entropy data
+    assert decode_jpeg_native(b"not a jpeg") is None
+
+
+def test_pack_decoded_mixed_batch():
+    """pack_decoded: native JPEGs, a progressive JPEG and a PNG (PIL; all RGB order), an image row (OpenCV
+    order) and undecodable values share one buffer; every slot holds the right pixels."""
+    import io
+
+    from PIL import Image
+
+    from synapseml_amd.image.schema import pack_decoded
+
+    a = _noise_image(20, 30, 1)
+    b = _noise_image(12, 8, 2)
+    vals = [_jpeg(a), _jpeg(a, progressive=True), encode_png(b), make_image_row(b), b"garbage", None, _jpeg(b[:, :, 1])]
+    buf, offs, shapes, rgb, ok = pack_decoded(vals, ignore_errors=True, threads=3)
+    assert ok == [True, True, True, True, False, False, True]
+
+    def slot(i):
+        return buf[offs[i]:offs[i] + int(np.prod(shapes[i]))].reshape(shapes[i])
+
+    with Image.open(io.BytesIO(vals[0])) as im:
+        np.testing.assert_array_equal(slot(0), np.asarray(im))
+    assert rgb[0] and rgb[1] and rgb[2] and not rgb[3]  # PIL decodes RGB-mode files in RGB order too
+    with Image.open(io.BytesIO(vals[1])) as im:
+        np.testing.assert_array_equal(slot(1), np.asarray(im))
+    np.testing.assert_array_equal(slot(2), b[:, :, ::-1])  # encode_png took OpenCV order
+    np.testing.assert_array_equal(slot(3), b)
+    assert shapes[6] == (12, 8, 1)
+    with pytest.raises(Exception):
+        pack_decoded([b"garbage"], ignore_errors=False)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """ResNet-50 (ONNX model-zoo v2 topology, random-init weights) inference
 throughput on one GPU: (1) session only, device-resident input, per precision
-and batch; (2) ImageFeaturizer end to end from ENCODED JPEG bytes (host decode
-on a thread pool running ahead of the device, fused resize/crop/normalize
+and batch; (2) ImageFeaturizer end to end from ENCODED JPEG bytes (native
+multi-threaded JPEG decode into pinned memory running ahead of the device -
+or PIL with SML_NATIVE_JPEG=0 / --decoders pil - fused resize/crop/normalize
 kernel, featurization) and, for reference, from pre-decoded image rows —
 BASELINE.json config "ONNXModel ResNet-50, synthetic 224x224 images".
 Precision is reported per line; fp32 is the reference's precision."""
@@ -26,6 +27,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--images", type=int, default=512)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--decoders", default="native", help="comma list of native,pil for the JPEG e2e runs")
     a = ap.parse_args()
     import torch
 
@@ -74,8 +76,11 @@ def main():
         jpegs[i] = buf.getvalue()
         rows[i] = make_image_row(img[:, :, ::-1].copy())
     avg_kb = float(np.mean([len(b) for b in jpegs])) / 1024
-    for src, col in (("jpeg_bytes", jpegs), ("decoded_rows", rows)):
+    runs = [("jpeg_bytes", jpegs, d) for d in a.decoders.split(",")] + [("decoded_rows", rows, None)]
+    for src, col, decoder in runs:
         df = DataFrame({"image": col})
+        if decoder is not None:
+            os.environ["SML_NATIVE_JPEG"] = "1" if decoder == "native" else "0"
         for prec in ("fp32", "fp16"):
             f = ImageFeaturizer(inputCol="image", outputCol="features", featureTensorName="resnetv24_pool1_fwd",
                                 imageTensorName="data").setModel(model)
@@ -88,6 +93,7 @@ def main():
             dt = time.perf_counter() - t0
             assert out.count() == a.images
             print(json.dumps({"bench": "image_featurizer_e2e", "input": src, "decode_included": src == "jpeg_bytes",
+                              "decoder": decoder,
                               "jpeg_kb_avg": round(avg_kb, 1) if src == "jpeg_bytes" else None,
                               "precision": prec, "images": a.images, "images_per_s": a.images / dt, "s": dt}),
                   flush=True)

@@ -71,7 +71,7 @@ MODULES = {
     ),
     "_image": (
         "csrc/image",
-        ["image_bindings.cpp", "image_ops.cpp", "image_gpu.hip"],
+        ["image_bindings.cpp", "image_ops.cpp", "jpeg_decode.cpp", "image_gpu.hip"],
         [],
     ),
     "_nn": (

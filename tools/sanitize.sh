@@ -27,7 +27,7 @@ if [ "$ONLY" = all ] || [ "$ONLY" = vw ]; then
 fi
 if [ "$ONLY" = all ] || [ "$ONLY" = image ]; then
   g++ $COMMON $ASAN -fopenmp -I"$ROOT/csrc/image" "$ROOT/csrc/image/image_ops.cpp" \
-    "$ROOT/tests/native/image_host_test.cpp" -o "$OUT/image_asan"
+    "$ROOT/csrc/image/jpeg_decode.cpp" "$ROOT/tests/native/image_host_test.cpp" -o "$OUT/image_asan"
   OMP_NUM_THREADS=4 "$OUT/image_asan"
 fi
 if [ "${SKIP_TSAN:-0}" != "1" ] && { [ "$ONLY" = all ] || [ "$ONLY" = tsan ]; }; then
