@@ -284,14 +284,14 @@ def test_gpu_resnet_matches_cpu_and_graph_replay(monkeypatch):
     assert not lib, "a library conv / matmul ran on the GPU path"
     scale = np.abs(cpu).max()
     # exact-f32 MFMA convs and GEMM: fp32-level agreement with the CPU graph (was 2e-3 with library kernels)
-    np.testing.assert_allclose(o1, cpu, rtol=0, atol=2e-4 * scale)
+    np.testing.assert_allclose(o1, cpu, rtol=0, atol=2e-5 * scale)
     # our kernels have no split-K atomics: replays are bitwise identical
     np.testing.assert_array_equal(o1, o2)
     assert any(v != "eager" for v in gpu._graphs.values()), "HIP graph capture fell back to eager"
     # fp32 graphs run the exact f32-input MFMA conv with the pre-activation BN+ReLU folded into its loader
     assert any(n.op_type == "_FusedConv" and len(n.inputs) > 5 and n.inputs[4] for n in gpu.nodes)
-    half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
-    assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
+    half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0].astype(np.float64)
+    assert np.linalg.norm(half - cpu) / np.linalg.norm(cpu) < 3e-3
 
 
 @pytest.mark.gpu
@@ -379,7 +379,9 @@ def test_image_featurizer_gpu_matches_cpu():
         return np.stack([v.toArray() for v in f.transform(df)["features"]])
 
     g, c = run("GPU"), run("CPU")
-    np.testing.assert_allclose(g, c, rtol=0, atol=2e-3 * np.abs(c).max())
+    # fused preprocess is bit-exact with the host stages and the MFMA convs / GEMM are exact-f32 (measured
+    # 1.6e-6 max relative error of the whole network on MI355X)
+    np.testing.assert_allclose(g, c, rtol=0, atol=2e-5 * np.abs(c).max())
 
 
 def test_prologue_fusion_pass_cpu_fallback():
@@ -409,9 +411,12 @@ def test_gpu_mfma_fused_resnet_matches_cpu(prec):
     sess = InferenceSession(data, device="cuda", precision=prec)
     fused = [n for n in sess.nodes if n.op_type == "_FusedConv" and len(n.inputs) > 5]
     assert len(fused) >= 16  # pre-activations folded into MFMA conv prologues
-    out = sess.run(None, {"data": x})[0]
-    assert np.corrcoef(out.ravel(), cpu.ravel())[0, 1] > (0.999 if prec == "fp16" else 0.995)
-    assert (out.argmax(1) == cpu.argmax(1)).mean() >= 0.75
+    out = sess.run(None, {"data": x})[0].astype(np.float64)
+    # relative L2 error of the logits vs the fp32 host graph: measured 7.3e-4 (fp16) / 5.4e-3 (bf16) on
+    # MI355X, i.e. the rounding of the storage format; a wrong fusion (dropped bias, BN or residual) is O(1)
+    rel = np.linalg.norm(out - cpu) / np.linalg.norm(cpu)
+    assert rel < (3e-3 if prec == "fp16" else 2e-2), rel
+    assert (out.argmax(1) == cpu.argmax(1)).mean() >= 7 / 8
 
 
 @pytest.mark.gpu
@@ -459,9 +464,9 @@ def test_gpu_stem_epilogue_moves_past_maxpool():
     assert any(n.op_type == "_FusedConv" and len(n.outputs) == 2 and len(n.inputs) == 8 for n in gpu.nodes)
     cpu = InferenceSession(data, device="cpu").run(None, {"data": x})[0]
     out = gpu.run(None, {"data": x})[0]
-    np.testing.assert_allclose(out, cpu, rtol=0, atol=2e-3 * np.abs(cpu).max())
-    half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0]
-    assert np.corrcoef(half.ravel(), cpu.ravel())[0, 1] > 0.999
+    np.testing.assert_allclose(out, cpu, rtol=0, atol=2e-5 * np.abs(cpu).max())
+    half = InferenceSession(data, device="cuda", precision="fp16").run(None, {"data": x})[0].astype(np.float64)
+    assert np.linalg.norm(half - cpu) / np.linalg.norm(cpu) < 3e-3
 
 
 @pytest.mark.gpu
