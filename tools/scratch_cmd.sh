@@ -1,9 +1,6 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests/test_gbdt_gpu.py -m gpu > gpurun_out/t10.log 2>&1
-rc=$?; tail -3 gpurun_out/t10.log; [ $rc -ne 0 ] && exit $rc
-for cfg in "SML_FUSE_HIST_FROM=0" "SML_FUSE_HIST_FROM=1" "SML_FUSE_HIST_FROM=1 SML_FUSED_ROWS=2" "SML_FUSE_HIST_FROM=1 SML_FUSED_ROWS=8" "SML_FUSE_HIST_FROM=4"; do
-  env $cfg timeout -k 10 200 python bench.py --steps 4 --warmup 1 > gpurun_out/ab.log 2>&1 || exit $?
-  tail -1 gpurun_out/ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('$cfg', round(d['value']/1e6,2), c['iteration_ms'], c['fit_phases_ms']['training_iterations_ms'], c.get('holdout_auc_first_rows'))"
-done
+mkdir -p gpurun_out/jpeg
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_image.py tests/test_onnx.py > gpurun_out/jpeg/tests.log 2>&1 &&
+timeout -k 10 500 python -u tools/bench_onnx.py --precisions fp32 --batches 128 --iters 5 --images 2048 --decoders native,pil > gpurun_out/jpeg/bench.log 2>&1
+rc=$?; tail -3 gpurun_out/jpeg/tests.log | cut -c1-300; cut -c1-260 gpurun_out/jpeg/bench.log | tail -8; exit $rc
