@@ -37,6 +37,7 @@
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include "trace.h"
 
 #include "backend.h"
 #include "comm.h"
@@ -2011,6 +2012,7 @@ class GpuBackend : public TrainBackend {
   std::string Name() const override { return "hip"; }
 
   void Init(const Dataset* d, const Config& cfg, int K) override {
+    TraceRange tr("sml::BackendInit");
     data_ = d; cfg_ = cfg; K_ = K; n_ = d->num_data;
     if (cfg.tree_learner == "voting" && comm_ && comm_->world() > 1)
       throw std::runtime_error(
@@ -2322,6 +2324,7 @@ class GpuBackend : public TrainBackend {
   }
 
   bool EvalOnDevice(const std::string& name, const Objective& obj, double* out) override {
+    TraceRange tr("sml::EvalTrain");
     DeviceMetricInputs in;
     in.score = score_.get(); in.label = label_.get(); in.weight = weight_.get(); in.n = n_; in.num_class = K_;
     const bool rank = name.rfind("ndcg", 0) == 0 || name.rfind("map", 0) == 0;
@@ -2336,6 +2339,7 @@ class GpuBackend : public TrainBackend {
   // K11: validation sets live in HBM; every tree is folded into their scores by a device traversal and
   // their metrics reduce on the device (valid_gpu.hip)
   bool AddValidSet(int vi, const Dataset& vd, const std::vector<double>& scores, const Config& cfg) override {
+    TraceRange tr("sml::AddValidSet");
     if (vd.num_data >= (int64_t(1) << 31) || vd.row_stride < vd.ref.num_inner()) return false;
     if (static_cast<int>(vsets_.size()) <= vi) vsets_.resize(vi + 1);
     vsets_[vi].reset(new DeviceValidSet(vd, scores, K_, cfg.label_gain, dev_, stream_));
@@ -2345,9 +2349,13 @@ class GpuBackend : public TrainBackend {
     if (vi < 0 || vi >= static_cast<int>(vsets_.size()) || !vsets_[vi]) throw std::logic_error("no device validation set");
     return *vsets_[vi];
   }
-  void ValidApplyTree(int vi, const Tree& t, int k, int op, double p) override { VSet(vi).ApplyTree(t, k, op, p); }
+  void ValidApplyTree(int vi, const Tree& t, int k, int op, double p) override {
+    TraceRange tr("sml::ValidApplyTree");
+    VSet(vi).ApplyTree(t, k, op, p);
+  }
   void GetValidScores(int vi, std::vector<double>* s) override { VSet(vi).GetScores(s); }
   bool EvalValidOnDevice(int vi, const std::string& name, const Objective& obj, double* out) override {
+    TraceRange tr("sml::EvalValid");
     return VSet(vi).Eval(name, obj.params(), K_, out);
   }
 

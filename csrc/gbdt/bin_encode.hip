@@ -24,6 +24,7 @@
 
 #include "dataset.h"
 #include "hip_common.h"
+#include "trace.h"
 
 namespace sml {
 namespace {
@@ -257,6 +258,7 @@ std::mutex& DevBinsMutex() {
 // The HBM bin matrix of `d` on `device`, current for every row pushed so far (uploads the host copy or
 // fills default rows the first time).
 void EnsureDeviceBins(Dataset* d, int device, hipStream_t s) {
+  TraceRange tr("sml::EnsureDeviceBins");
   std::lock_guard<std::mutex> lk(DevBinsMutex());
   if (d->dev && d->dev->device != device) { d->dev.reset(); d->dev_valid = false; }
   if (!d->dev) {
@@ -299,6 +301,7 @@ void EnsureDeviceBins(Dataset* d, int device, hipStream_t s) {
 
 template <class T>
 void PushDenseDeviceImpl(Dataset* d, const T* rows, int64_t nrows, int num_cols, int64_t start, int device) {
+  TraceRange tr("sml::PushRowsEncode");
   if (start < 0 || start + nrows > d->num_data) throw std::runtime_error("push_dense_gpu out of range");
   if (d->row_stride % 4 != 0) throw std::runtime_error("device bin encode needs a 4-byte aligned row stride");
   if (device >= 0) SML_HIP_CHECK(hipSetDevice(device));
@@ -329,6 +332,7 @@ void PushDenseDeviceImpl(Dataset* d, const T* rows, int64_t nrows, int num_cols,
 
 template <class T>
 void PushResidentImpl(Dataset* d, DeviceRows* src, int64_t start) {
+  TraceRange tr("sml::EncodeResidentRows");
   src->Wait();
   const int64_t nrows = src->nrows;
   if (start < 0 || start + nrows > d->num_data) throw std::runtime_error("push_device_rows out of range");
@@ -400,6 +404,7 @@ void ParallelCopy(char* dst, const char* src, size_t bytes, int threads) {
 }  // namespace
 
 void UploadPinned(const char* host, char* dev, size_t bytes) {
+  TraceRange tr("sml::UploadPinned");
   StagePool& sp = Stage();
   std::lock_guard<std::mutex> lk(sp.mu);  // one pinned pipeline at a time per process
   for (auto& b : sp.buf)

@@ -12,6 +12,7 @@
 
 #include "comm.h"
 #include "hip_common.h"
+#include "trace.h"
 
 namespace sml {
 
@@ -67,6 +68,7 @@ class RcclComm : public Comm {
   bool is_device() const override { return true; }
   // (a world-1 communicator still runs every collective: that is how the one-GPU tests execute this path)
   void AllReduceHost(double* buf, int64_t n) override {
+    TraceRange tr("sml::AllReduceHost");
     // small host reductions (root sums, init scores): stage through the device
     if (!comm_) throw CommError("RCCL communicator was aborted");
     double* d = nullptr;

@@ -9,6 +9,7 @@
 
 #include "booster.h"
 #include "hip_common.h"
+#include "trace.h"
 #include "predictor.h"
 
 namespace sml {
@@ -318,6 +319,7 @@ GpuPredictor::GpuPredictor(const Booster& b, int start_iteration, int num_iterat
 GpuPredictor::~GpuPredictor() = default;
 
 void GpuPredictor::Predict(const double* X, int64_t n, int ncols, bool normal, double* out) {
+  TraceRange tr("sml::Predict");
   if (n <= 0) return;
   impl_->x.alloc(static_cast<size_t>(n) * ncols);
   impl_->o.alloc(static_cast<size_t>(n) * num_out_);
@@ -336,6 +338,7 @@ void GpuPredictor::Predict(const double* X, int64_t n, int ncols, bool normal, d
 }
 
 void GpuPredictor::PredictLeaf(const double* X, int64_t n, int ncols, int32_t* out) {
+  TraceRange tr("sml::PredictLeaf");
   if (n <= 0 || num_trees_ == 0) return;
   impl_->x.alloc(static_cast<size_t>(n) * ncols);
   impl_->lo.alloc(static_cast<size_t>(n) * num_trees_);
@@ -493,6 +496,7 @@ bool GpuPredictor::BuildShap() {
 }
 
 bool GpuPredictor::PredictContrib(const double* X, int64_t n, int ncols, double* out) {
+  TraceRange tr("sml::PredictContrib");
   if (!impl_->shap_ready) BuildShap();
   if (!impl_->shap_ok) return false;
   Impl& I = *impl_;
