@@ -17,12 +17,12 @@
 // without any host round trip (the tree is read back once at the end).
 // Data-parallel training inserts an RCCL allreduce of the smaller child's
 // histogram between the slab reduce and the split search (C2 over xGMI).
-// tree_learner=voting (C3) is refused on multi-rank device training rather than
-// silently run as data-parallel (it grows different trees): a full-histogram
-// one-shot allreduce over xGMI (~114 KB, comm_p2p.hip) costs less than the vote
-// round trip plus the selected-feature reduction PV-Tree would replace (SURVEY
-// §5.8), so data_parallel is the device mode; the host backend implements the
-// PV-Tree vote for CPU clusters.
+// tree_learner=voting (C3, PV-Tree) keeps the histograms local and reduces
+// only the 2*top_k most-voted features of each new leaf (vote_kernel ..
+// unpack_kernel): two small collectives per split instead of one full
+// histogram. Over xGMI the full-histogram one-shot allreduce (~114 KB for 28
+// features) is usually cheaper, so data_parallel stays the default; voting pays
+// off for wide feature sets (thousands of features) or slower links.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1092,11 +1092,22 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
   CategoricalSearchBuf(hg, hh, nb, fi, G, H, cnt, sp, mc, best, idx, left);
 }
 
+// Search modes (tree_learner=voting runs 1 then 2 per split; everything else runs 0):
+//   kFindFull   : `part` = the (globally reduced) smaller child / root histogram; the larger child is
+//                 parent - smaller from the pool; both are stored in the pool
+//   kFindLocal  : PV-Tree local pass - same histograms but LOCAL (not reduced), leaf totals and row counts
+//                 local, min_data / min_hessian already divided by the world size in `sp`
+//   kFindVoted  : PV-Tree global pass - `part` / `part1` = the globally reduced histograms of the voted
+//                 features of the smaller / larger child (no pool access); only features with sel[child*F+f]
+//                 are searched, leaf totals come from the split record (root: its own voted histogram)
+enum FindMode { kFindFull = 0, kFindLocal = 1, kFindVoted = 2 };
+
 // Block (f, child): 256 threads, thread = bin.
 __device__ void FindSplitBlock(
     DState* __restrict__ st, DLeaf* __restrict__ leaves, const double2* __restrict__ part, int E,
     const double* __restrict__ count_slot, double2* __restrict__ hist_pool, const FeatMeta& fm, const SplitParams& sp,
-    SplitResult* __restrict__ fbest, int F) {
+    SplitResult* __restrict__ fbest, int F, int mode, const double2* __restrict__ part1,
+    const int8_t* __restrict__ sel, const int32_t* __restrict__ sel_first) {
   const int f = blockIdx.x;
   const int child = blockIdx.y;  // 0 = small (or root), 1 = large
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1104,16 +1115,20 @@ __device__ void FindSplitBlock(
   if (root && child == 1) return;
   const int leaf_id = root ? 0 : (child == 0 ? st->small_leaf : st->large_leaf);
   const int e = f * kBinsPerFeature + tid;
-  const double2 sm = part[e];  // smaller child's (or the root's) histogram
   double2 mine;
-  if (root || child == 0) {
-    mine = sm;
+  if (mode == kFindVoted) {
+    mine = (root || child == 0) ? part[e] : part1[e];
   } else {
-    const double2 par = hist_pool[static_cast<size_t>(st->parent_slot) * E + e];
-    mine = make_double2(par.x - sm.x, par.y - sm.y);
+    const double2 sm = part[e];  // smaller child's (or the root's) histogram
+    if (root || child == 0) {
+      mine = sm;
+    } else {
+      const double2 par = hist_pool[static_cast<size_t>(st->parent_slot) * E + e];
+      mine = make_double2(par.x - sm.x, par.y - sm.y);
+    }
   }
   const DLeaf Lf = leaves[leaf_id];
-  hist_pool[static_cast<size_t>(Lf.slot) * E + e] = mine;
+  if (mode != kFindVoted) hist_pool[static_cast<size_t>(Lf.slot) * E + e] = mine;
   __shared__ double sg_[256], shh_[256];
   __shared__ double wtot_g[4], wtot_h[4];
   __shared__ Cand wbest[4];
@@ -1140,16 +1155,23 @@ __device__ void FindSplitBlock(
   }
   if (root) {
     cnt = static_cast<int64_t>(*count_slot);
-    if (f == 0 && tid == 0) {
+    const int writer = mode == kFindFull ? 0 : (mode == kFindVoted ? *sel_first : -1);
+    if (f == writer && tid == 0) {
       leaves[0].sum_g = G; leaves[0].sum_h = H; leaves[0].gcount = cnt;
     }
+  } else if (mode == kFindLocal) {
+    // local totals (this feature's own histogram) and local row counts: the smaller child's from the slab
+    // reduce's count slot, the larger's = the parent's local segment minus it
+    const int64_t small_cnt = static_cast<int64_t>(*count_slot);
+    cnt = child == 0 ? small_cnt : (static_cast<int64_t>(st->pcount) - small_cnt);
   } else {
     const int64_t small_cnt = static_cast<int64_t>(*count_slot);
     cnt = child == 0 ? small_cnt : (Lf.gcount - small_cnt);  // Lf.gcount of large holds the parent count (set by choose)
     G = Lf.sum_g; H = Lf.sum_h;
   }
   SplitResult* out = fbest + child * F + f;
-  const bool eligible = fm.mask[f] && nb > 1 && cnt >= 2 * static_cast<int64_t>(sp.min_data_in_leaf) &&
+  const bool eligible = fm.mask[f] && nb > 1 && (mode != kFindVoted || sel[child * F + f]) &&
+                        cnt >= 2 * static_cast<int64_t>(sp.min_data_in_leaf) &&
                         (sp.max_depth <= 0 || Lf.depth < sp.max_depth) &&
                         (sp.bynode_k <= 0 ||
                          NodeFeatureSelected(sp.bynode_seed, sp.tree_seq, Lf.slot, f, fm.mask, F, sp.bynode_k));
@@ -1404,11 +1426,160 @@ __device__ void ChooseBlock(DState* __restrict__ st, DLeaf* __restrict__ leaves,
 __global__ __launch_bounds__(256) void find_split_kernel(
     DState* __restrict__ st, DLeaf* __restrict__ leaves, const double2* __restrict__ part, int E,
     const double* __restrict__ count_slot, double2* __restrict__ hist_pool, FeatMeta fm, SplitParams sp,
-    SplitResult* __restrict__ fbest, int F, DState* __restrict__ st_next) {
+    SplitResult* __restrict__ fbest, int F, DState* __restrict__ st_next, int mode,
+    const double2* __restrict__ part1, const int8_t* __restrict__ sel, const int32_t* __restrict__ sel_first) {
   // choose_part_kernel partitions on the next state version's cursor: zero it here (nothing reads it now)
   if (st_next && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st_next->cursor = 0ull;
   if (st->done) return;
-  FindSplitBlock(st, leaves, part, E, count_slot, hist_pool, fm, sp, fbest, F);
+  FindSplitBlock(st, leaves, part, E, count_slot, hist_pool, fm, sp, fbest, F, mode, part1, sel, sel_first);
+}
+
+// ---------------------------------------------------------------- C3: PV-Tree voting on the device
+// (reference parallelism=voting_parallel / topK, LightGBMParams.scala:25-35; the host backend's VotingFind
+// in backend_cpu.cpp is the same algorithm on host buffers). Per split, after the LOCAL histograms and a local
+// split search (kFindLocal):
+//   vote_kernel     each rank votes for its top_k features of each new leaf by local gain
+//   [allreduce]     votes + summed local gains + the smaller child's row count (4F+1 doubles)
+//   select_kernel   per leaf the 2*top_k most-voted features (ties: summed gain, then feature id), filled with
+//                   unvoted allowed features when fewer were voted
+//   pack_kernel     the selected features' local histograms -> one compact buffer
+//   [allreduce]     2 x 2*top_k x 256 bins x (g, h)
+//   unpack_kernel   -> per-leaf global histograms of the selected features, then kFindVoted searches them
+constexpr int kVoteMaxF = 8192;  // LDS flags of the vote / select kernels
+constexpr int kVoteThreads = 1024;
+
+struct VKey {
+  double v, g;  // votes, summed gain (larger first)
+  int f;        // feature (smaller first)
+};
+
+__device__ __forceinline__ bool VKeyBetter(const VKey& a, const VKey& b) {
+  if (a.v != b.v) return a.v > b.v;
+  if (a.g != b.g) return a.g > b.g;
+  return a.f < b.f;
+}
+
+// block argmax of `k` (every thread of a kVoteThreads block calls it); returns the winner on every thread
+__device__ VKey BlockArgmaxV(VKey k, VKey* s_w) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    VKey o;
+    o.v = __shfl_xor(k.v, off, 64);
+    o.g = __shfl_xor(k.g, off, 64);
+    o.f = __shfl_xor(k.f, off, 64);
+    if (VKeyBetter(o, k)) k = o;
+  }
+  if (lane == 0) s_w[wid] = k;
+  __syncthreads();
+  VKey b = s_w[0];
+  for (int w = 1; w < kVoteThreads / 64; ++w) if (VKeyBetter(s_w[w], b)) b = s_w[w];
+  __syncthreads();  // s_w is reused by the next call
+  return b;
+}
+
+// top_k rounds of a block argmax over the local per-feature results (key: gain, then feature id = the host's
+// SplitBetter order); vote layout [votes child 0 | votes child 1 | gains child 0 | gains child 1 | count]
+__global__ __launch_bounds__(kVoteThreads) void vote_kernel(const DState* __restrict__ st,
+                                                            const SplitResult* __restrict__ floc, int F, int topk,
+                                                            const double* __restrict__ local_count,
+                                                            double* __restrict__ vote) {
+  __shared__ unsigned char chosen[2][kVoteMaxF];
+  __shared__ VKey s_w[kVoteThreads / 64];
+  const int tid = threadIdx.x;
+  const bool done = st->done;
+  const int C = st->phase == 0 ? 1 : 2;
+  for (int c = 0; c < 2; ++c)
+    for (int f = tid; f < F; f += kVoteThreads) chosen[c][f] = 0;
+  __syncthreads();
+  for (int c = 0; c < C && !done; ++c) {
+    for (int r = 0; r < topk; ++r) {
+      VKey k{-INFINITY, 0.0, 1 << 30};
+      for (int f = tid; f < F; f += kVoteThreads) {
+        const SplitResult& s = floc[c * F + f];
+        if (s.feature < 0 || chosen[c][f]) continue;
+        VKey o{s.gain, 0.0, f};
+        if (VKeyBetter(o, k)) k = o;
+      }
+      const VKey b = BlockArgmaxV(k, s_w);
+      if (b.v == -INFINITY) break;
+      if (tid == 0) chosen[c][b.f] = 1;
+      __syncthreads();
+    }
+  }
+  // one writer per element
+  for (int c = 0; c < 2; ++c)
+    for (int f = tid; f < F; f += kVoteThreads) {
+      const bool on = chosen[c][f] != 0;
+      vote[c * F + f] = on ? 1.0 : 0.0;
+      vote[(2 + c) * F + f] = on ? floc[c * F + f].gain : 0.0;
+    }
+  if (tid == 0) vote[4 * F] = *local_count;
+}
+
+// the summed votes -> per-leaf selection of up to K2 = min(2 top_k, F) features
+__global__ __launch_bounds__(kVoteThreads) void select_kernel(const DState* __restrict__ st,
+                                                              const double* __restrict__ vote, int F, int K2,
+                                                              const int8_t* __restrict__ mask,
+                                                              int32_t* __restrict__ sel_idx,
+                                                              int32_t* __restrict__ sel_pos,
+                                                              int8_t* __restrict__ sel_mask) {
+  __shared__ int16_t rank[2][kVoteMaxF];
+  __shared__ VKey s_w[kVoteThreads / 64];
+  const int tid = threadIdx.x;
+  const bool done = st->done;
+  const int C = st->phase == 0 ? 1 : 2;
+  for (int c = 0; c < 2; ++c)
+    for (int f = tid; f < F; f += kVoteThreads) rank[c][f] = -1;
+  __syncthreads();
+  for (int c = 0; c < 2; ++c) {
+    int r = 0;
+    for (; c < C && !done && r < K2; ++r) {
+      VKey k{-INFINITY, 0.0, 1 << 30};
+      for (int f = tid; f < F; f += kVoteThreads) {
+        const double v = vote[c * F + f];
+        if (rank[c][f] >= 0 || !(v > 0.0 || mask[f])) continue;
+        VKey o{v, v > 0.0 ? vote[(2 + c) * F + f] : 0.0, f};
+        if (VKeyBetter(o, k)) k = o;
+      }
+      const VKey b = BlockArgmaxV(k, s_w);
+      if (b.v == -INFINITY) break;
+      if (tid == 0) { rank[c][b.f] = static_cast<int16_t>(r); sel_idx[c * K2 + r] = b.f; }
+      __syncthreads();
+    }
+    for (int i = r + tid; i < K2; i += kVoteThreads) sel_idx[c * K2 + i] = -1;
+  }
+  __syncthreads();
+  for (int c = 0; c < 2; ++c)
+    for (int f = tid; f < F; f += kVoteThreads) {
+      sel_pos[c * F + f] = rank[c][f];
+      sel_mask[c * F + f] = rank[c][f] >= 0 ? 1 : 0;
+    }
+}
+
+// block (i, c): the i-th selected feature of leaf c, its LOCAL histogram (stored in the pool by kFindLocal)
+__global__ __launch_bounds__(256) void pack_kernel(const DState* __restrict__ st, const DLeaf* __restrict__ leaves,
+                                                   const int32_t* __restrict__ sel_idx, int K2,
+                                                   const double2* __restrict__ hist_pool, int E,
+                                                   double2* __restrict__ compact) {
+  const int i = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  double2* dst = compact + (static_cast<size_t>(c) * K2 + i) * kBinsPerFeature + tid;
+  const bool root = st->phase == 0;
+  const int f = st->done ? -1 : sel_idx[c * K2 + i];
+  if (f < 0 || (root && c == 1)) { *dst = make_double2(0.0, 0.0); return; }
+  const int leaf_id = root ? 0 : (c == 0 ? st->small_leaf : st->large_leaf);
+  *dst = hist_pool[static_cast<size_t>(leaves[leaf_id].slot) * E + f * kBinsPerFeature + tid];
+}
+
+// block (f, c): the reduced histogram of feature f of leaf c (zeros when f was not selected)
+__global__ __launch_bounds__(256) void unpack_kernel(const DState* __restrict__ st, const int32_t* __restrict__ sel_pos,
+                                                     int F, int K2, const double2* __restrict__ compact, int E,
+                                                     double2* __restrict__ gh) {
+  if (st->done) return;
+  const int f = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int p = sel_pos[c * F + f];
+  gh[static_cast<size_t>(c) * E + f * kBinsPerFeature + tid] =
+      p >= 0 ? compact[(static_cast<size_t>(c) * K2 + p) * kBinsPerFeature + tid] : make_double2(0.0, 0.0);
 }
 
 // The last split of a tree (single process): its children are never split, so their histograms and split
@@ -2014,11 +2185,6 @@ class GpuBackend : public TrainBackend {
   void Init(const Dataset* d, const Config& cfg, int K) override {
     TraceRange tr("sml::BackendInit");
     data_ = d; cfg_ = cfg; K_ = K; n_ = d->num_data;
-    if (cfg.tree_learner == "voting" && comm_ && comm_->world() > 1)
-      throw std::runtime_error(
-          "tree_learner=voting (parallelism=voting_parallel) is not run by the GPU backend: use "
-          "parallelism=data_parallel on the device (a full-histogram allreduce over xGMI costs less than the "
-          "PV-Tree vote), or deviceType=cpu for voting-parallel trees");
     if (n_ >= (int64_t(1) << 31)) throw std::runtime_error("GPU backend: more than 2^31 rows per device");
     if (cfg.num_leaves > 4096) throw std::runtime_error("GPU backend: num_leaves > 4096");
     if (dev_ >= 0) SML_HIP_CHECK(hipSetDevice(dev_));
@@ -2077,6 +2243,21 @@ class GpuBackend : public TrainBackend {
     }
     if (const char* e = std::getenv("SML_SKIP_LAST_SPLIT")) skip_last_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_GBDT_COMM_WORLD1")) comm_world1_ = std::atoi(e) != 0;
+    voting_ = cfg.tree_learner == "voting" && Distributed();
+    if (voting_) {
+      if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
+      vote_k2_ = std::max(1, std::min(2 * std::max(1, cfg.top_k), F_));
+      sp_local_ = sp_;
+      sp_local_.min_data_in_leaf = std::max(1, sp_.min_data_in_leaf / comm_->world());
+      sp_local_.min_sum_hessian = sp_.min_sum_hessian / comm_->world();
+      floc_.alloc(2 * F_);
+      vote_.alloc(4 * static_cast<size_t>(F_) + 1);
+      sel_idx_.alloc(2 * static_cast<size_t>(vote_k2_));
+      sel_pos_.alloc(2 * static_cast<size_t>(F_));
+      sel_mask_.alloc(2 * static_cast<size_t>(F_));
+      compact_.alloc(2 * static_cast<size_t>(vote_k2_) * kBinsPerFeature);
+      gh_.alloc(2 * static_cast<size_t>(E_));
+    }
     {
       const int64_t tile = static_cast<int64_t>(kPartThreads) * part_rows_;
       part_grid_ = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, (n_ + tile - 1) / tile)));
@@ -2563,7 +2744,11 @@ class GpuBackend : public TrainBackend {
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(b, 8192)));
   }
 
-  const double* CountSlot() const { return reinterpret_cast<const double*>(part_.get() + E_); }
+  // the smaller child's (root's) GLOBAL row count: the allreduced histogram's extra slot, or under voting
+  // the allreduced vote buffer's last slot
+  const double* CountSlot() const {
+    return voting_ ? vote_.get() + 4 * static_cast<size_t>(F_) : reinterpret_cast<const double*>(part_.get() + E_);
+  }
 
   // device time of the last score update; call only after a stream sync
   // score update + next gradients + next root histogram in one pass (score_grad_hist_kernel) with
@@ -2686,31 +2871,71 @@ class GpuBackend : public TrainBackend {
     hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, st_cur_,
                        leaves_.get(), slab_.get(), E_, ghmax, part_.get());
     SML_HIP_CHECK(hipGetLastError());
-    if (Distributed()) {
-      // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL / P2P,
-      // timed on the device (hipEvents around the collective on the engine stream)
-      EnsureCommEvents();
-      const bool timed = comm_used_ < static_cast<int>(comm_ev_.size()) / 2;
-      if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_], stream_));
-      comm_->AllReduceDeviceF64(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 2, stream_);
-      if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_ + 1], stream_));
-      comm_used_ += timed ? 1 : 0;
-      ++stats.comm_calls;
-    }
+    // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL / P2P, timed on
+    // the device (hipEvents around the collective on the engine stream). Voting keeps them local.
+    if (Distributed() && !voting_) TimedAllReduce(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 2);
   }
 
   // SML_GBDT_COMM_WORLD1=1 (tests): a world-1 communicator runs the full data-parallel path (allreduce per
   // split, device comm timing, polling waits) so a one-GPU box executes it end to end
   bool Distributed() const { return comm_ && (comm_->world() > 1 || comm_world1_); }
 
+  // one device allreduce on the engine stream, timed with a hipEvent pair while pairs are left
+  void TimedAllReduce(double* buf, int64_t n) {
+    EnsureCommEvents();
+    const bool timed = comm_used_ < static_cast<int>(comm_ev_.size()) / 2;
+    if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_], stream_));
+    comm_->AllReduceDeviceF64(buf, n, stream_);
+    if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_ + 1], stream_));
+    comm_used_ += timed ? 1 : 0;
+    ++stats.comm_calls;
+  }
+
+  // PV-Tree split search of the new leaves (see vote_kernel): local search, vote, allreduce of the votes,
+  // selection, allreduce of only the selected features' histograms, global search of those
+  void EnqueueVote() {
+    const double* local_count = reinterpret_cast<const double*>(part_.get() + E_);
+    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), part_.get(),
+                       E_, local_count, hist_pool_.get(), fm_, sp_local_, floc_.get(), F_,
+                       static_cast<DState*>(nullptr), static_cast<int>(kFindLocal),
+                       static_cast<const double2*>(nullptr), static_cast<const int8_t*>(nullptr),
+                       static_cast<const int32_t*>(nullptr));
+    SML_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(vote_kernel, dim3(1), dim3(kVoteThreads), 0, stream_, st_cur_, floc_.get(), F_,
+                       std::max(1, cfg_.top_k), local_count, vote_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    TimedAllReduce(vote_.get(), 4 * static_cast<int64_t>(F_) + 1);
+    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(kVoteThreads), 0, stream_, st_cur_, vote_.get(), F_, vote_k2_,
+                       mask_.get(), sel_idx_.get(), sel_pos_.get(), sel_mask_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(pack_kernel, dim3(vote_k2_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), sel_idx_.get(),
+                       vote_k2_, hist_pool_.get(), E_, compact_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    TimedAllReduce(reinterpret_cast<double*>(compact_.get()), 2 * 2 * static_cast<int64_t>(vote_k2_) * kBinsPerFeature);
+    hipLaunchKernelGGL(unpack_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, sel_pos_.get(), F_, vote_k2_,
+                       compact_.get(), E_, gh_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), gh_.get(), E_,
+                       CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_, st_next_,
+                       static_cast<int>(kFindVoted), static_cast<const double2*>(gh_.get() + E_),
+                       static_cast<const int8_t*>(sel_mask_.get()), static_cast<const int32_t*>(sel_idx_.get()));
+    SML_HIP_CHECK(hipGetLastError());
+  }
+
   // root (choose_now = false): choose_part_kernel does the choose step with the next partition
   void EnqueueFindChoose(bool choose_now) {
     // (A/B, round 3: folding this search into the slab reduce - the last of a feature's 8 reduce blocks
     // searching it after a device-scope release/acquire hand-off - ran 3.11 vs 2.14 ms/iter: the per-block
     // fences cost more than the launch they save)
-    hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), part_.get(),
-                       E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_, st_next_);
-    SML_HIP_CHECK(hipGetLastError());
+    if (voting_) {
+      EnqueueVote();
+    } else {
+      hipLaunchKernelGGL(find_split_kernel, dim3(F_, 2), dim3(256), 0, stream_, st_cur_, leaves_.get(), part_.get(),
+                         E_, CountSlot(), hist_pool_.get(), fm_, sp_, fbest_.get(), F_, st_next_,
+                         static_cast<int>(kFindFull), static_cast<const double2*>(nullptr),
+                         static_cast<const int8_t*>(nullptr), static_cast<const int32_t*>(nullptr));
+      SML_HIP_CHECK(hipGetLastError());
+    }
     if (!choose_now) return;
     hipLaunchKernelGGL(choose_kernel, dim3(1), dim3(256), 0, stream_, st_cur_, leaves_.get(), lbest_.get(),
                        lgain_.get(), fbest_.get(), F_, dt_, CountSlot(), mono_.get(), sp_.has_mono);
@@ -2846,6 +3071,15 @@ class GpuBackend : public TrainBackend {
   // (2.05 vs 1.97 ms/iter: 28 blocks cannot pull the slabs fast enough; profiles/README, round 2)
   bool skip_last_ = true;  // SML_SKIP_LAST_SPLIT=0: histogram + search the last split's children too
   bool comm_world1_ = false;
+  // tree_learner=voting (PV-Tree, C3): local search results, votes, selection and the reduced histograms
+  bool voting_ = false;
+  int vote_k2_ = 0;          // features reduced per leaf: min(2 top_k, F)
+  SplitParams sp_local_{};   // min_data_in_leaf / min_sum_hessian divided by the world size
+  DevBuf<SplitResult> floc_;
+  DevBuf<double> vote_;
+  DevBuf<int32_t> sel_idx_, sel_pos_;
+  DevBuf<int8_t> sel_mask_;
+  DevBuf<double2> compact_, gh_;
   DevBuf<float> ghmax_partial_;
   // event pairs around this tree's histogram allreduces (device comm time, summed when the tree is read)
   std::vector<hipEvent_t> comm_ev_;
@@ -2853,7 +3087,7 @@ class GpuBackend : public TrainBackend {
   hipEvent_t ev_sync_ = nullptr;
   void EnsureCommEvents() {
     if (!comm_ev_.empty()) return;
-    comm_ev_.assign(2 * static_cast<size_t>(L_ + 1), nullptr);
+    comm_ev_.assign(4 * static_cast<size_t>(L_ + 1), nullptr);  // voting: two collectives per split
     for (hipEvent_t& e : comm_ev_) SML_HIP_CHECK(hipEventCreate(&e));
   }
   int tree_seq_ = 0;  // trees grown so far (feature_fraction_bynode node keys)

@@ -76,6 +76,78 @@ class OrthoForestVariableTransformer(Transformer):
         return df.withColumn(self.getOutputCol(), ratio).withColumn(self.getWeightsCol(), t * t)
 
 
+def commons_percentile(values, p: float) -> float:
+    """Apache commons-math ``Percentile.evaluate(p)`` (default estimation: position p(n+1)/100 with linear
+    interpolation, clamped to the sample range) - the estimator the reference's confidence intervals and
+    BLB bounds use (DoubleMLEstimator.scala percentile, OrthoForestDMLEstimator.scala getBLBBounds)."""
+    v = np.sort(np.asarray(values, np.float64))
+    n = len(v)
+    if n == 0:
+        return float("nan")
+    if n == 1:
+        return float(v[0])
+    pos = p * (n + 1) / 100.0
+    if pos < 1:
+        return float(v[0])
+    if pos >= n:
+        return float(v[-1])
+    lo = int(np.floor(pos))
+    return float(v[lo - 1] + (pos - lo) * (v[lo] - v[lo - 1]))
+
+
+def _commons_percentile_rows(sorted_rows: np.ndarray, p: float) -> np.ndarray:
+    """commons_percentile over each row of an already sorted (k, n) matrix"""
+    n = sorted_rows.shape[1]
+    if n == 1:
+        return sorted_rows[:, 0].copy()
+    pos = p * (n + 1) / 100.0
+    if pos < 1:
+        return sorted_rows[:, 0].copy()
+    if pos >= n:
+        return sorted_rows[:, -1].copy()
+    lo = int(np.floor(pos))
+    return sorted_rows[:, lo - 1] + (pos - lo) * (sorted_rows[:, lo] - sorted_rows[:, lo - 1])
+
+
+def _model_kind(model) -> str:
+    """'binary' for probabilistic classifiers, 'continuous' for regressors (reference DoubleMLParams
+    ensureSupportedEstimator: anything else is refused)"""
+    if model.hasParam("probabilityCol"):
+        return "binary"
+    if model.hasParam("predictionCol"):
+        return "continuous"
+    raise TypeError(f"DoubleMLEstimator only supports regressors and probabilistic classifiers as treatment or "
+                    f"outcome model types, but got {type(model).__name__}")
+
+
+def _check_col_for_model(col: np.ndarray, name: str, model) -> None:
+    """Column type vs model type (reference DoubleMLEstimator.validateColTypeWithModel)"""
+    kind = _model_kind(model)
+    if col.dtype == bool:
+        if kind == "continuous":
+            raise TypeError(f"column '{name}' in dataset is boolean data type, but you set to use a regression "
+                            "model for it.")
+    elif np.issubdtype(col.dtype, np.integer):
+        if kind == "binary" and not np.isin(col, (0, 1)).all():
+            raise ValueError(f"column '{name}' in dataset is integer data type and you set to use a classification "
+                             "model for it, its all values must be either 0 or 1, but it has other values.")
+    elif np.issubdtype(col.dtype, np.floating):
+        if kind == "binary":
+            raise TypeError(f"column '{name}' in dataset is double or long data type, but you set to use a "
+                            "classification model for it.")
+    else:
+        raise TypeError(f"column '{name}' must be of type DoubleType, LongType, IntegerType or BooleanType "
+                        f"but got {col.dtype}")
+
+
+def _ols_slope(x: np.ndarray, y: np.ndarray) -> float:
+    """slope of a gaussian / identity GLM y ~ 1 + x (the reference's GeneralizedLinearRegression with
+    fitIntercept=true on the residuals)"""
+    xc = x - x.mean()
+    den = float(xc @ xc)
+    return float(xc @ (y - y.mean())) / den if den > 0 else 0.0
+
+
 class _DMLParams(HasFeaturesCol, HasWeightCol):
     treatmentCol = Param("treatment column", "treatment", T.toString)
     outcomeCol = Param("outcome column", "outcome", T.toString)
@@ -86,29 +158,46 @@ class _DMLParams(HasFeaturesCol, HasWeightCol):
     confidenceLevel = Param("confidence level, default value is 0.975", 0.975, T.toFloat)
     parallelism = Param("the number of threads to use when running parallel algorithms", 10, T.toInt)
 
-    def _predict(self, model, df, label: str) -> np.ndarray:
+    def _models(self):
+        """(treatment, outcome) estimators; the reference defaults both to LogisticRegression"""
+        from ..models import LogisticRegression
+
+        tm = self.getTreatmentModel() or LogisticRegression()
+        om = self.getOutcomeModel() or LogisticRegression()
+        return tm, om
+
+    def _fit_nuisance(self, model, df, label: str, features: str):
         est = model.copy()
-        for p, v in (("labelCol", label), ("featuresCol", self.getFeaturesCol())):
+        for p, v in (("labelCol", label), ("featuresCol", features)):
             if est.hasParam(p):
                 est.set(p, v)
-        fitted = est.fit(df)
-        return fitted
+        if self.isSet("weightCol") and self.getWeightCol():
+            if not est.hasParam("weightCol"):
+                raise ValueError(f"The selected {label} model does not support sample weight, but the weightCol "
+                                 f"parameter was set. Please select a model that supports sample weight.")
+            est.set("weightCol", self.getWeightCol())
+        return est.fit(df)
 
-    def _residuals(self, train: DataFrame, test: DataFrame, rng=None):
+    @staticmethod
+    def _prediction(model, out) -> np.ndarray:
+        """P(class 1) of a probabilistic classifier, else the prediction (ResidualTransformer classIndex 1)"""
+        if model.hasParam("probabilityCol"):
+            col = out[model.getProbabilityCol() if hasattr(model, "getProbabilityCol") else "probability"]
+            return np.asarray(col[:, 1] if getattr(col, "ndim", 1) == 2 else
+                              [np.asarray(v.toArray() if hasattr(v, "toArray") else v)[1] for v in col], np.float64)
+        return np.asarray(out[model.getPredictionCol() if hasattr(model, "getPredictionCol") else "prediction"],
+                          np.float64)
+
+    def _residuals(self, train: DataFrame, test: DataFrame, features: Optional[str] = None):
+        """treatment and outcome nuisance models fit on `train`, residuals observed - predicted on `test`"""
         tcol, ycol = self.getTreatmentCol(), self.getOutcomeCol()
-        tm = self._predict(self.getTreatmentModel(), train, tcol)
-        om = self._predict(self.getOutcomeModel(), train, ycol)
-        to = tm.transform(test)
-        oo = om.transform(test)
-        t_obs = np.asarray(test[tcol], np.float64)
-        y_obs = np.asarray(test[ycol], np.float64)
-        if "probability" in to.columns and to["probability"].ndim == 2:
-            t_hat = to["probability"][:, 1]
-        else:
-            t_hat = np.asarray(to["prediction"], np.float64)
-        y_hat = np.asarray(oo["prediction"], np.float64) if "prediction" in oo.columns else \
-            np.asarray(oo["probability"][:, 1])
-        return t_obs - t_hat, y_obs - y_hat
+        feats = features or self.getFeaturesCol()
+        tmodel, omodel = self._models()
+        tm = self._fit_nuisance(tmodel, train, tcol, feats)
+        om = self._fit_nuisance(omodel, train, ycol, feats)
+        t_hat = self._prediction(tmodel, tm.transform(test))
+        y_hat = self._prediction(omodel, om.transform(test))
+        return np.asarray(test[tcol], np.float64) - t_hat, np.asarray(test[ycol], np.float64) - y_hat
 
 
 class DoubleMLModel(Model, _DMLParams):
@@ -116,40 +205,72 @@ class DoubleMLModel(Model, _DMLParams):
 
     def getAvgTreatmentEffect(self) -> float:  # noqa: N802
         v = self.getRawTreatmentEffects()
-        return float(np.mean(v))
+        return float(np.sum(v) / len(v))
 
     def getPValue(self) -> float:  # noqa: N802
+        """two-sided one-sample t-test of the raw effects against 0 (commons-math TTest.tTest(0, values);
+        it needs at least two iterations)"""
         from scipy import stats
 
-        v = np.asarray(self.getRawTreatmentEffects())
-        if len(v) < 2 or np.std(v) == 0:
+        v = np.asarray(self.getRawTreatmentEffects(), np.float64)
+        if len(v) < 2:
+            raise ValueError("the p-value needs maxIter >= 2 (a t-test of the per-iteration effects)")
+        if np.std(v) == 0:
             return 0.0 if abs(np.mean(v)) > 0 else 1.0
         return float(stats.ttest_1samp(v, 0.0).pvalue)
 
     def getConfidenceInterval(self) -> List[float]:  # noqa: N802
-        v = np.asarray(self.getRawTreatmentEffects())
+        v = self.getRawTreatmentEffects()
         cl = self.getConfidenceLevel()
-        return [float(np.percentile(v, 100 * (1 - cl))), float(np.percentile(v, 100 * cl))]
+        return [commons_percentile(v, 100 * (1 - cl)), commons_percentile(v, 100 * cl)]
 
     def _transform(self, df):
         return df
 
 
 class DoubleMLEstimator(Estimator, _DMLParams):
-    def _fit(self, df):
+    """Double machine learning ATE (reference core/.../causal/DoubleMLEstimator.scala:63-268): each of
+    ``maxIter`` iterations (run on ``parallelism`` threads) redraws the data with replacement (not when
+    maxIter == 1), splits it by ``sampleSplitRatio``, fits the treatment / outcome nuisance models on one
+    half and takes residuals on the other, both ways, and averages the two slopes of outcome residual on
+    treatment residual (GLM with intercept). Failed iterations are dropped; all failing is an error."""
+
+    def _one_ate(self, df: DataFrame, it: int) -> float:
+        work = df if self.getMaxIter() == 1 else df.sample(1.0, seed=it, withReplacement=True)
         ratio = np.asarray(self.getSampleSplitRatio(), float)
-        ratio = ratio / ratio.sum()
-        effects = []
-        for it in range(self.getMaxIter()):
-            a, b = df.randomSplit(list(ratio), seed=it)
-            num = den = 0.0
-            for tr, te in ((a, b), (b, a)):
-                tres, yres = self._residuals(tr, te)
-                num += float(np.sum(tres * yres))
-                den += float(np.sum(tres * tres))
-            effects.append(num / den if den else 0.0)
-        m = DoubleMLModel(treatmentCol=self.getTreatmentCol(), outcomeCol=self.getOutcomeCol(),
-                          confidenceLevel=self.getConfidenceLevel(), rawTreatmentEffects=effects)
+        a, b = work.randomSplit(list(ratio / ratio.sum()), seed=it)
+        slopes = []
+        for tr, te in ((a, b), (b, a)):
+            tres, yres = self._residuals(tr, te)
+            ok = np.isfinite(tres) & np.isfinite(yres)  # VectorAssembler handleInvalid=skip
+            slopes.append(_ols_slope(tres[ok], yres[ok]))
+        return float(sum(slopes) / len(slopes))
+
+    def _fit(self, df):
+        if self.getMaxIter() <= 0:
+            raise ValueError("maxIter should be larger than 0!")
+        tmodel, omodel = self._models()
+        _check_col_for_model(np.asarray(df[self.getTreatmentCol()]), self.getTreatmentCol(), tmodel)
+        _check_col_for_model(np.asarray(df[self.getOutcomeCol()]), self.getOutcomeCol(), omodel)
+        from concurrent.futures import ThreadPoolExecutor
+
+        def run(it):
+            try:
+                return self._one_ate(df, it)
+            except Exception as e:  # reference: logged and skipped
+                import logging
+
+                logging.getLogger(__name__).warning("ATE calculation failed on iteration %d: %s", it, e)
+                return None
+
+        with ThreadPoolExecutor(max_workers=max(1, min(self.getParallelism(), self.getMaxIter()))) as ex:
+            ates = [a for a in ex.map(run, range(1, self.getMaxIter() + 1)) if a is not None]
+        if not ates:
+            raise RuntimeError("ATE calculation failed on all iterations. Please check the log for details.")
+        m = DoubleMLModel(rawTreatmentEffects=ates)
+        for name in ("treatmentCol", "outcomeCol", "confidenceLevel", "maxIter", "sampleSplitRatio", "parallelism",
+                     "featuresCol"):
+            m.set(name, self.getOrDefault(name))
         return m
 
 
@@ -160,54 +281,86 @@ class OrthoForestDMLModel(Model, _DMLParams):
     outputHighCol = Param("output column", "EffectUpperBound", T.toString)
     forest = Param("fitted per-tree effect models", None, complex=True)
 
+    def _blb_bounds(self, preds: np.ndarray, rng) -> np.ndarray:
+        """Bag of little bootstraps over each row's per-tree effects (reference getBLBBounds): groups of
+        ceil(sqrt(n)) trees, 100 draws with replacement per group, per-group lower / median / upper
+        percentile, averaged over the groups -> (rows, 3)"""
+        rows, n = preds.shape
+        b = int(np.ceil(np.sqrt(n)))
+        cl = self.getConfidenceLevel()
+        acc = np.zeros((rows, 3))
+        groups = [(s, min(n, s + b)) for s in range(0, n, b)]
+        for s, e in groups:
+            draws = preds[:, s:e][np.arange(rows)[:, None], rng.integers(0, e - s, size=(rows, 100))]
+            draws.sort(axis=1)
+            acc[:, 0] += _commons_percentile_rows(draws, 100 * (1 - cl))
+            acc[:, 1] += _commons_percentile_rows(draws, 50)
+            acc[:, 2] += _commons_percentile_rows(draws, 100 * cl)
+        return acc / len(groups)
+
     def _transform(self, df):
         X = as_matrix(df[self.getHeterogeneityVecCol()])
         tmp = DataFrame({"features": X})
         preds = np.stack([np.asarray(t.transform(tmp)["prediction"], np.float64) for t in self.getForest()], 1)
-        cl = self.getConfidenceLevel()
-        return (df.withColumn(self.getOutputCol(), preds.mean(1))
-                .withColumn(self.getOutputLowCol(), np.percentile(preds, 100 * (1 - cl), axis=1))
-                .withColumn(self.getOutputHighCol(), np.percentile(preds, 100 * cl, axis=1)))
+        lo_med_hi = self._blb_bounds(preds, np.random.default_rng(0))
+        return (df.withColumn(self.getOutputLowCol(), lo_med_hi[:, 0])
+                .withColumn(self.getOutputCol(), lo_med_hi[:, 1])
+                .withColumn(self.getOutputHighCol(), lo_med_hi[:, 2]))
 
 
 class OrthoForestDMLEstimator(Estimator, _DMLParams):
+    """Orthogonal random forest DML (reference OrthoForestDMLEstimator.scala:30-160): cross-fitted treatment /
+    outcome residuals on the confounders, target = outcome residual / treatment residual with weight =
+    treatment residual^2 (OrthoForestVariableTransformer), a random forest of ``numTrees`` depth-``maxDepth``
+    trees on the heterogeneity features per residual half; the model's per-row effect and bounds come from a
+    bag of little bootstraps over all trees."""
+
     heterogeneityVecCol = Param("Vector to divide the treatment by", "X", T.toString)
     confounderVecCol = Param("Confounders to control for", "XW", T.toString)
     numTrees = Param("Number of trees", 20, T.toInt)
     maxDepth = Param("Max Depth of Tree", 5, T.toInt)
     minSamplesLeaf = Param("Max Depth of Tree", 10, T.toInt)
-    treatmentResidualCol = Param("Treatment Residual Column", "TResid", T.toString)
-    outcomeResidualCol = Param("Outcome Residual Column", "OResid", T.toString)
+    treatmentResidualCol = Param("Treatment Residual Column", "TreatmentResidual", T.toString)
+    outcomeResidualCol = Param("Outcome Residual Column", "OutcomeResidual", T.toString)
     outputCol = Param("output column", "EffectAverage", T.toString)
     outputLowCol = Param("output column", "EffectLowerBound", T.toString)
     outputHighCol = Param("output column", "EffectUpperBound", T.toString)
 
+    def _models(self):
+        from ..models import GBTRegressor
+
+        tm = self.getTreatmentModel() or GBTRegressor(seed=0)
+        om = self.getOutcomeModel() or GBTRegressor(seed=0)
+        return tm, om
+
     def _fit(self, df):
         from ..models import DecisionTreeRegressor
 
-        feat = self.getFeaturesCol()
-        work = df.withColumn(feat, as_matrix(df[self.getConfounderVecCol()]))
-        a, b = work.randomSplit([0.5, 0.5], seed=0)
-        parts = []
-        for tr, te in ((a, b), (b, a)):
-            tres, yres = self._residuals(tr, te)
-            parts.append((te, tres, yres))
-        X = np.concatenate([as_matrix(p[0][self.getHeterogeneityVecCol()]) for p in parts])
-        tres = np.concatenate([p[1] for p in parts])
-        yres = np.concatenate([p[2] for p in parts])
-        safe = np.where(np.abs(tres) < 1e-6, np.sign(tres + 1e-12) * 1e-6, tres)
+        if self.getNumTrees() <= 0:
+            raise ValueError("You need at least one tree in a forest")
+        tcol = df[self.getTreatmentCol()]
+        if not np.issubdtype(np.asarray(tcol).dtype, np.floating):
+            raise TypeError(f"TreatmentCol must be of type DoubleType but got {np.asarray(tcol).dtype}")
+        ratio = np.asarray(self.getSampleSplitRatio(), float)
+        a, b = df.randomSplit(list(ratio / ratio.sum()), seed=0)
         tr_col, or_col = self.getTreatmentResidualCol(), self.getOutcomeResidualCol()
-        vt = OrthoForestVariableTransformer(treatmentResidualCol=tr_col, outcomeResidualCol=or_col).transform(
-            DataFrame({tr_col: safe, or_col: yres}))
-        target = vt["_tmp_tsOutcome"]
-        wts = tres * tres
-        rng = np.random.default_rng(0)
         forest = []
-        for t in range(self.getNumTrees()):
-            idx = rng.choice(len(target), size=len(target) // 2, replace=False)
-            d = DataFrame({"features": X[idx], "label": target[idx], "w": wts[idx]})
-            forest.append(DecisionTreeRegressor(maxDepth=self.getMaxDepth(), minInstancesPerNode=self.getMinSamplesLeaf(),
-                                                weightCol="w", seed=t, deviceType="cpu").fit(d))
+        for half, (tr, te) in enumerate(((a, b), (b, a))):
+            tres, yres = self._residuals(tr, te, features=self.getConfounderVecCol())
+            vt = OrthoForestVariableTransformer(treatmentResidualCol=tr_col, outcomeResidualCol=or_col).transform(
+                DataFrame({tr_col: tres, or_col: yres}))
+            target, wts = np.asarray(vt["_tmp_tsOutcome"]), np.asarray(vt["_tmp_twOutcome"])
+            ok = np.isfinite(target) & (wts > 0)
+            X = as_matrix(te[self.getHeterogeneityVecCol()])[ok]
+            target, wts = target[ok], wts[ok]
+            rng = np.random.default_rng(half)
+            for t in range(self.getNumTrees()):
+                # random forest member: bootstrap rows, one tree
+                idx = rng.integers(0, len(target), len(target))
+                d = DataFrame({"features": X[idx], "label": target[idx], "w": wts[idx]})
+                forest.append(DecisionTreeRegressor(maxDepth=self.getMaxDepth(),
+                                                    minInstancesPerNode=self.getMinSamplesLeaf(), weightCol="w",
+                                                    seed=1000 * half + t, deviceType="cpu").fit(d))
         m = OrthoForestDMLModel(heterogeneityVecCol=self.getHeterogeneityVecCol(), outputCol=self.getOutputCol(),
                                 outputLowCol=self.getOutputLowCol(), outputHighCol=self.getOutputHighCol(),
                                 confidenceLevel=self.getConfidenceLevel())

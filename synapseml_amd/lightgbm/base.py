@@ -158,11 +158,11 @@ class LightGBMBase(Estimator, LightGBMParams):
         return names
 
     def _check_parallelism(self, use_gpu: bool, world: int) -> None:
-        """voting_parallel grows PV-Tree trees on the host backend only; on several GPUs it is refused up front
-        (before any data moves) instead of silently running data-parallel (backend_gpu.hip header)."""
-        if use_gpu and world > 1 and self.getParallelism() == "voting_parallel":
-            raise ValueError("parallelism='voting_parallel' is not run on the GPU backend with several ranks: use "
-                             "parallelism='data_parallel' (full-histogram allreduce over xGMI) or deviceType='cpu'")
+        """data_parallel (full-histogram allreduce per split) and voting_parallel (PV-Tree: local top-k votes,
+        only the 2*topK most-voted features' histograms reduced) run on both backends and any number of ranks
+        (reference LightGBMParams.scala:25-35); anything else is refused before any data moves."""
+        if self.getParallelism() not in ("data_parallel", "voting_parallel"):
+            raise ValueError(f"parallelism={self.getParallelism()!r}: expected 'data_parallel' or 'voting_parallel'")
 
     def _train_params(self, num_class: int, cat_idx: List[int], num_machines: int) -> str:
         sb = ParamsStringBuilder()

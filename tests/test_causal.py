@@ -14,7 +14,7 @@ def test_double_ml_recovers_ate():
     rng = np.random.default_rng(0)
     n = 3000
     X = rng.normal(size=(n, 3))
-    t = (X[:, 0] + rng.normal(size=n) > 0).astype(float)
+    t = (X[:, 0] + rng.normal(size=n) > 0).astype(np.int32)  # 0/1 integer column for a classifier
     y = 2.0 * t + X @ np.array([1.0, -1.0, 0.5]) + rng.normal(size=n) * 0.5
     df = DataFrame({"features": X, "treatment": t, "outcome": y})
     est = DoubleMLEstimator(treatmentModel=LogisticRegression(), outcomeModel=LinearRegression(), maxIter=5)
@@ -23,6 +23,36 @@ def test_double_ml_recovers_ate():
     lo, hi = m.getConfidenceInterval()
     assert lo <= m.getAvgTreatmentEffect() <= hi
     assert m.getPValue() < 0.01
+    assert len(m.getRawTreatmentEffects()) == 5
+
+
+def test_double_ml_reference_semantics():
+    """Column/model type checks, weight support, commons-math percentiles, single-iteration p-value
+    (reference DoubleMLEstimator.scala validateColTypeWithModel / DoubleMLModel)."""
+    from synapseml_amd.causal import commons_percentile
+
+    rng = np.random.default_rng(3)
+    n = 1500
+    X = rng.normal(size=(n, 2))
+    t = (X[:, 0] + rng.normal(size=n) > 0).astype(np.int64)
+    y = 1.5 * t + X[:, 1] + 0.3 * rng.normal(size=n)
+    df = DataFrame({"features": X, "treatment": t, "outcome": y, "w": np.ones(n)})
+    with pytest.raises(TypeError, match="classification"):  # double outcome with a classifier
+        DoubleMLEstimator(treatmentModel=LogisticRegression(), outcomeModel=LogisticRegression()).fit(df)
+    with pytest.raises(ValueError, match="0 or 1"):
+        DoubleMLEstimator(treatmentModel=LogisticRegression(), outcomeModel=LinearRegression()).fit(
+            df.withColumn("treatment", t * 2))
+    with pytest.raises(ValueError, match="maxIter"):
+        DoubleMLEstimator(treatmentModel=LogisticRegression(), outcomeModel=LinearRegression(), maxIter=0).fit(df)
+    m = DoubleMLEstimator(treatmentModel=LogisticRegression(), outcomeModel=LinearRegression(), weightCol="w").fit(df)
+    assert m.getAvgTreatmentEffect() == pytest.approx(1.5, abs=0.2)
+    with pytest.raises(ValueError, match="maxIter >= 2"):
+        m.getPValue()
+    # commons-math Percentile (legacy estimation): position p(n+1)/100
+    v = [1.0, 2.0, 3.0, 4.0]
+    assert commons_percentile(v, 50) == pytest.approx(2.5)
+    assert commons_percentile(v, 97.5) == 4.0 and commons_percentile(v, 2.5) == 1.0
+    assert commons_percentile(v, 25) == pytest.approx(1.25)
 
 
 def test_ortho_forest_heterogeneous_effect():
@@ -38,6 +68,7 @@ def test_ortho_forest_heterogeneous_effect():
                                 maxDepth=3, minSamplesLeaf=20).fit(df)
     out = m.transform(DataFrame({"X": np.array([[0.2], [0.8]])}))
     lo_eff, hi_eff = out["EffectAverage"]
+    assert len(m.getForest()) == 2 * 10  # one forest per cross-fitting half
     assert lo_eff == pytest.approx(1.0, abs=0.4) and hi_eff == pytest.approx(3.0, abs=0.5)
     assert (out["EffectLowerBound"] <= out["EffectUpperBound"]).all()
 

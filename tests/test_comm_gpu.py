@@ -133,3 +133,37 @@ def test_vw_gpu_2p30_table_sync_and_export_keep_host_rss_flat():
     grown = proc.memory_info().rss - rss0
     assert grown < (2 << 30), f"host RSS grew by {grown / 2**30:.2f} GiB"
     del sgd
+
+
+def _train_p(X, y, comm, p, iters=8):
+    g = _gbdt()
+    ref = g.DatasetReference.from_sample(X[:50000].astype(np.float64), len(X), p, [f"f{i}" for i in range(X.shape[1])])
+    ds = g.Dataset(ref, len(X))
+    ds.push_dense_gpu(X, 0)
+    ds.set_label(y)
+    b = g.Booster(ds, p, comm)
+    for _ in range(iters):
+        b.update()
+    b.synchronize()
+    return b
+
+
+@pytest.mark.parametrize("top_k", [1, 2, 20])
+def test_gbdt_voting_parallel_on_world1_rccl(monkeypatch, top_k):
+    """Device PV-Tree (tree_learner=voting): local search, vote, vote allreduce, selection, selected-feature
+    histogram allreduce, global search - every kernel and both ncclAllReduce calls per split executed.
+    At world 1 the local gains are the global ones, so the best feature is always among the voted ones and
+    the trees equal the single-process trees for any top_k (top_k=1 reduces 2 of the 10 features)."""
+    X, y = _data()
+    p = "objective=binary num_leaves=31 learning_rate=0.1 device_type=gpu"
+    base = _train_p(X, y, None, p)
+    monkeypatch.setenv("SML_GBDT_COMM_WORLD1", "1")
+    c = _rccl_world1()
+    vote = _train_p(X, y, c, p + f" tree_learner=voting top_k={top_k}")
+    s = vote.stats()
+    # two collectives per split search: the root + one per further split
+    assert s["comm_calls"] >= 8 * 2 * 2 and s["comm_calls"] <= 8 * 2 * 31, s
+    split = lambda m: [l for l in m.splitlines() if l.startswith(("split_feature=", "threshold=", "leaf_count="))]
+    assert split(vote.save_model_string()) == split(base.save_model_string())
+    np.testing.assert_allclose(vote.predict(X[:5000].astype(np.float64), 0, 0, -1),
+                               base.predict(X[:5000].astype(np.float64), 0, 0, -1), rtol=1e-12, atol=1e-12)

@@ -166,6 +166,7 @@ def test_p2p_allreduce_two_ranks_one_gpu():
     for o in lines:
         assert o["p2p_active"], o
         assert o["allreduce_exact"] and o["train_models_equal"] and o["ranks_agree"], o
+        assert o["voting_gpu_eq_cpu"] and o["voting_ranks_agree"], o
 
 
 @pytest.mark.parametrize("kind", ["binary_nan_cat", "multiclass", "rf"])

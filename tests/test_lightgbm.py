@@ -446,14 +446,14 @@ def test_checkpoint_unreadable_raises_clearly(tmp_path):
         est.fit(df)
 
 
-def test_voting_parallel_refused_on_multi_rank_gpu():
-    """voting_parallel is never silently run as data-parallel on the device: multi-rank GPU training is
-    refused with a message naming the alternatives; one rank, or the CPU backend, is fine."""
+def test_parallelism_values_checked():
+    """Both reference tree learners run on the GPU backend with any number of ranks (voting_parallel as the
+    device PV-Tree vote); an unknown value is refused before training."""
     from synapseml_amd.lightgbm import LightGBMClassifier
 
-    est = LightGBMClassifier(parallelism="voting_parallel", deviceType="gpu")
-    with pytest.raises(ValueError, match="data_parallel"):
-        est._check_parallelism(True, 2)
-    est._check_parallelism(True, 1)
-    est._check_parallelism(False, 4)
-    LightGBMClassifier(parallelism="data_parallel")._check_parallelism(True, 8)
+    for par in ("data_parallel", "voting_parallel"):
+        for gpu in (True, False):
+            for world in (1, 2, 8):
+                LightGBMClassifier(parallelism=par)._check_parallelism(gpu, world)
+    with pytest.raises(ValueError, match="voting_parallel"):
+        LightGBMClassifier(parallelism="feature_parallel")._check_parallelism(True, 2)

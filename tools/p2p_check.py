@@ -57,6 +57,28 @@ def main():
         out["train_models_equal"] = models[0] == models[1]
         allm = D.all_gather_object(models[0])
         out["ranks_agree"] = all(m == allm[0] for m in allm)
+        # PV-Tree voting (topK=1: 2 of the 8 features reduced per leaf) on the device over P2P vs the host
+        # backend's voting over the host comm: same split structure; and it differs from data-parallel
+        # somewhere (the vote really restricted the search)
+        vp = params + " tree_learner=voting top_k=1"
+        vm = []
+        for dev_type, comm in (("gpu", c), ("cpu", host)):
+            ds = g.Dataset(ref, len(X))
+            ds.push_dense(X, 0)
+            ds.set_label(y)
+            b = g.Booster(ds, vp.replace("device_type=gpu", "device_type=" + dev_type), comm)
+            for _ in range(5):
+                b.update()
+            vm.append(b.save_model_string())
+        keys = ("split_feature=", "threshold=", "leaf_count=")
+        struct = lambda m: [l for l in m.splitlines() if l.startswith(keys)]
+        # first tree (as test_gpu_trees_match_cpu: later trees inherit fp64-summation differences of the scores)
+        tree0 = lambda m: [l for l in m.split("Tree=0")[1].split("Tree=1")[0].splitlines()
+                           if l.startswith(("split_feature=", "threshold="))]
+        out["voting_gpu_eq_cpu"] = tree0(vm[0]) == tree0(vm[1])
+        out["voting_differs_from_data_parallel"] = struct(vm[0]) != struct(models[0])
+        allv = D.all_gather_object(vm[0])
+        out["voting_ranks_agree"] = all(m == allv[0] for m in allv)
     print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()
