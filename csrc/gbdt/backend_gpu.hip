@@ -903,7 +903,9 @@ __device__ __forceinline__ void SlabStore(ulonglong2* p, unsigned long long g, u
   }
 }
 
-template <int kUnroll>
+// kFPG features per block (blockIdx.y = feature group): 32 = one 131.6 KB LDS histogram per CU; 16 halves
+// the LDS (two blocks per CU) at the price of reading every row's perm / g / h once per group
+template <int kUnroll, int kFPG>
 __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
@@ -914,14 +916,15 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
   const int count = L.count;
   const int nb_active = HistBlocks(count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long shg[kHistWords], shh[kHistWords];
+  constexpr int kWords = kFPG * kHistStride;
+  __shared__ unsigned long long shg[kWords], shh[kWords];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kHistWords; i += kHistBlockThreads) { shg[i] = 0ull; shh[i] = 0ull; }
+  for (int i = tid; i < kWords; i += kHistBlockThreads) { shg[i] = 0ull; shh[i] = 0ull; }
   __syncthreads();
   const int grp = blockIdx.y;
-  const int Fg = min(kFeatPerGroup, F - grp * kFeatPerGroup);
-  const int col = grp * 2;            // first uint4 of this group in a row
-  const bool two = Fg > 16;
+  const int Fg = min(kFPG, F - grp * kFPG);
+  const int col = grp * (kFPG / 16);  // first uint4 of this group in a row
+  const bool two = kFPG > 16 && Fg > 16;
   const int chunk = ceil_div_i(count, nb_active);
   const int p0 = L.begin + blockIdx.x * chunk;
   const int p1 = min(L.begin + count, p0 + chunk);
@@ -956,7 +959,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
   ulonglong2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
   for (int i = tid; i < Fg * kBinsPerFeature; i += kHistBlockThreads) {
     const int f = i >> 8, b = i & 255;
-    SlabStore(out + (grp * kFeatPerGroup + f) * kBinsPerFeature + b, shg[f * kHistStride + b], shh[f * kHistStride + b]);
+    SlabStore(out + (grp * kFPG + f) * kBinsPerFeature + b, shg[f * kHistStride + b], shh[f * kHistStride + b]);
   }
 }
 
@@ -2243,6 +2246,7 @@ class GpuBackend : public TrainBackend {
     }
     if (const char* e = std::getenv("SML_SKIP_LAST_SPLIT")) skip_last_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_GBDT_COMM_WORLD1")) comm_world1_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -2859,7 +2863,8 @@ class GpuBackend : public TrainBackend {
 
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-    hipLaunchKernelGGL(hist_kernel<kHistUnroll>, dim3(kMaxHistBlocks, FG_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
+    auto hk = hist_fpg_ == 16 ? hist_kernel<kHistUnroll, 16> : hist_kernel<kHistUnroll, kFeatPerGroup>;
+    hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
                        perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
     SML_HIP_CHECK(hipGetLastError());
@@ -3050,6 +3055,7 @@ class GpuBackend : public TrainBackend {
   Config cfg_;
   SplitParams sp_{};
   int K_ = 1, F_ = 0, S_ = 4, W_ = 1, E_ = 0, L_ = 2, FG_ = 1;
+  int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
   DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident
