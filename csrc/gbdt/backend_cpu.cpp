@@ -2,6 +2,7 @@
 // It is the numerical oracle for the HIP kernels and the runtime for hosts
 // without an MI355X (BASELINE config 1, "local[2] CPU plumbing").
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -154,6 +155,18 @@ void FindBestSplitFeature(const double* hg, const double* hh, int nb, const BinM
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+inline double Ms(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+struct ScoreTimer {
+  explicit ScoreTimer(double* acc) : acc_(acc), t0_(Clock::now()) {}
+  ~ScoreTimer() { *acc_ += Ms(t0_); }
+  double* acc_;
+  Clock::time_point t0_;
+};
+
 struct LeafInfo {
   int64_t begin = 0, count = 0;  // local row range
   int64_t gcount = 0;            // global row count (all ranks)
@@ -195,7 +208,11 @@ class CpuBackend : public TrainBackend {
   void ScaleScore(int k, double sc) override {
     for (int64_t i = 0; i < n_; ++i) score_[k * n_ + i] *= sc;
   }
-  void ComputeGradients(const Objective& obj) override { obj.GetGradients(score_.data(), g_.data(), h_.data()); }
+  void ComputeGradients(const Objective& obj) override {
+    const auto t0 = Clock::now();
+    obj.GetGradients(score_.data(), g_.data(), h_.data());
+    stats.grad_ms += Ms(t0);
+  }
   void SetGradients(const float* g, const float* h) override {
     std::memcpy(g_.data(), g, sizeof(float) * g_.size());
     std::memcpy(h_.data(), h, sizeof(float) * h_.size());
@@ -205,45 +222,136 @@ class CpuBackend : public TrainBackend {
     if (rows) { bag_ = *rows; use_bag_ = true; } else { bag_.clear(); use_bag_ = false; }
   }
 
+  // Histogram of one leaf, feature-parallel: the leaf's (g, h) are gathered once into a contiguous
+  // ordered buffer, then every thread walks all of the leaf's rows for its own slice of the features and
+  // accumulates them in fp64 straight into the output (each (feature, bin) has one writer: no per-thread
+  // tables, no reduction, an L1-sized working set per thread, and a summation order that does not depend
+  // on the thread count). Few features and many threads: rows are also split, with per-row-group tables.
   void BuildHist(int k, const LeafInfo& leaf, const std::vector<char>& fmask, std::vector<double>* hist,
                  bool reduce = true) {
+    const auto t0 = Clock::now();
     const int stride = 256 * 2;
-    hist->assign(static_cast<size_t>(F_) * stride, 0.0);
+    const size_t hsz = static_cast<size_t>(F_) * stride;
+    hist->assign(hsz, 0.0);
     const float* g = g_.data() + static_cast<size_t>(k) * n_;
     const float* h = h_.data() + static_cast<size_t>(k) * n_;
     const int64_t cnt = leaf.count;
-    const int nt = std::max<int>(1, std::min<int64_t>(nthreads_, cnt / 4096 + 1));
-    std::vector<std::vector<double>> local(nt, std::vector<double>(hist->size(), 0.0));
+    std::vector<int> feats;
+    for (int f = 0; f < F_; ++f) if (fmask[f]) feats.push_back(f);
+    const int nf = static_cast<int>(feats.size());
+    const int* fl = feats.data();
+    const int64_t rs = data_->row_stride;
+    const uint8_t* bins = data_->bins.data();
+    const int64_t* idx = idx_.data() + leaf.begin;
+    const int nt = std::max<int>(1, std::min<int64_t>(nthreads_, cnt / 2048 + 1));
+    if (static_cast<int64_t>(ogh_.size()) < 2 * cnt) ogh_.resize(2 * cnt);
+    float* og = ogh_.data();
 #pragma omp parallel for num_threads(nt) schedule(static)
-    for (int t = 0; t < nt; ++t) {
-      double* hl = local[t].data();
-      int64_t b = leaf.begin + cnt * t / nt, e = leaf.begin + cnt * (t + 1) / nt;
-      for (int64_t p = b; p < e; ++p) {
-        const int64_t r = idx_[p];
-        const uint8_t* row = &data_->bins[r * data_->row_stride];
-        const double gv = g[r], hv = h[r];
-        for (int f = 0; f < F_; ++f) {
-          if (!fmask[f]) continue;
-          double* c = hl + f * stride + row[f] * 2;
-          c[0] += gv; c[1] += hv;
+    for (int64_t p = 0; p < cnt; ++p) {
+      const int64_t r = idx[p];
+      og[2 * p] = g[r];
+      og[2 * p + 1] = h[r];
+    }
+    // row groups x feature slices; one row group unless there are fewer features than threads
+    const int fs = std::max(1, std::min(nt, nf));
+    const int rg = std::max(1, nt / fs);
+    if (rg > 1) {
+      if (static_cast<int>(hloc_.size()) < rg) hloc_.resize(rg);
+      for (int gi = 1; gi < rg; ++gi) if (hloc_[gi].size() < hsz) hloc_[gi].resize(hsz);
+    }
+    double* out = hist->data();
+#pragma omp parallel for num_threads(fs * rg) schedule(static, 1) collapse(2)
+    for (int gi = 0; gi < rg; ++gi) {
+      for (int si = 0; si < fs; ++si) {
+        double* dst = out;
+        if (rg > 1 && gi > 0) dst = hloc_[gi].data();  // row group 0 writes the output directly
+        const int fa = nf * si / fs, fb = nf * (si + 1) / fs;
+        if (rg > 1 && gi > 0)
+          for (int j = fa; j < fb; ++j) std::fill(dst + fl[j] * stride, dst + (fl[j] + 1) * stride, 0.0);
+        const int64_t pa = cnt * gi / rg, pb = cnt * (gi + 1) / rg;
+        for (int64_t p = pa; p < pb; ++p) {
+          if (p + 24 < pb) __builtin_prefetch(bins + idx[p + 24] * rs);  // random rows of a child leaf
+          const uint8_t* row = bins + idx[p] * rs;
+          const double gv = og[2 * p], hv = og[2 * p + 1];
+          for (int j = fa; j < fb; ++j) {
+            const int f = fl[j];
+            double* c = dst + f * stride + row[f] * 2;
+            c[0] += gv;
+            c[1] += hv;
+          }
         }
       }
     }
-    for (int t = 0; t < nt; ++t)
-      for (size_t i = 0; i < hist->size(); ++i) (*hist)[i] += local[t][i];
+    if (rg > 1) {
+      for (int j = 0; j < nf; ++j) {
+        double* o = out + fl[j] * stride;
+        for (int gi = 1; gi < rg; ++gi) {
+          const double* src = hloc_[gi].data() + fl[j] * stride;
+          for (int b = 0; b < stride; ++b) o[b] += src[b];
+        }
+      }
+    }
+    stats.hist_ms += Ms(t0);
     if (reduce && comm_ && comm_->world() > 1) {
+      const auto tc = Clock::now();
       hist->push_back(static_cast<double>(leaf.count));
       comm_->AllReduceHost(hist->data(), static_cast<int64_t>(hist->size()));
       last_gcount_ = static_cast<int64_t>(hist->back());
       hist->pop_back();
+      stats.comm_ms += Ms(tc);
+      ++stats.comm_calls;
     } else {
       last_gcount_ = leaf.count;
     }
   }
 
+  // Stable partition of idx_[begin, begin + count) by `left(r)`: every thread flags and counts its chunk,
+  // an exclusive scan of the per-thread counts gives each chunk its output offsets on both sides, then the
+  // chunks scatter into the scratch buffer in parallel, which is copied back. Returns the left count.
+  template <typename Pred>
+  int64_t ParallelPartition(int64_t begin, int64_t count, Pred left, const uint8_t* pf, int64_t pf_stride) {
+    const int nt = std::max<int>(1, std::min<int64_t>(nthreads_, count / 4096 + 1));
+    if (static_cast<int64_t>(part_tmp_.size()) < count) part_tmp_.resize(count);
+    if (static_cast<int64_t>(part_flag_.size()) < count) part_flag_.resize(count);
+    std::vector<int64_t> nleft(nt + 1, 0);
+    int64_t* idx = idx_.data() + begin;
+    uint8_t* flag = part_flag_.data();
+#pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+      const int t = omp_get_thread_num();
+#else
+      const int t = 0;
+#endif
+      const int64_t b = count * t / nt, e = count * (t + 1) / nt;
+      int64_t c = 0;
+      for (int64_t p = b; p < e; ++p) {
+        if (p + 24 < e) __builtin_prefetch(pf + idx[p + 24] * pf_stride);
+        const uint8_t l = left(idx[p]) ? 1 : 0;
+        flag[p] = l;
+        c += l;
+      }
+      nleft[t + 1] = c;
+#pragma omp barrier
+#pragma omp single
+      for (int i = 0; i < nt; ++i) nleft[i + 1] += nleft[i];
+      const int64_t total_left = nleft[nt];
+      int64_t lo = nleft[t], ro = total_left + (b - nleft[t]);
+      int64_t* tmp = part_tmp_.data();
+      for (int64_t p = b; p < e; ++p) {
+        if (flag[p]) tmp[lo++] = idx[p]; else tmp[ro++] = idx[p];
+      }
+#pragma omp barrier
+      std::memcpy(idx + b, tmp + b, sizeof(int64_t) * (e - b));
+    }
+    return nleft[nt];
+  }
+
   void FindBest(const std::vector<double>& hist, LeafInfo* leaf, const std::vector<char>& fmask) {
+    const auto t0 = Clock::now();
     std::vector<SplitResult> per;
     PerFeatureBest(hist, *leaf, fmask, &per);
+    stats.split_ms += Ms(t0);
     SplitResult best{};
     best.feature = -1;
     best.gain = -std::numeric_limits<double>::infinity();
@@ -332,30 +440,70 @@ class CpuBackend : public TrainBackend {
 
   void PerFeatureBest(const std::vector<double>& hist, const LeafInfo& leaf_in, const std::vector<char>& fmask,
                       std::vector<SplitResult>* per_out) {
-    std::vector<SplitResult>& per = *per_out;
-    per.assign(F_, SplitResult{});
-    for (auto& r : per) { r.feature = -1; r.gain = -std::numeric_limits<double>::infinity(); }
-    const LeafInfo* leaf = &leaf_in;
-    if (leaf->gcount >= 2 * sp_.min_data_in_leaf && (sp_.max_depth <= 0 || leaf->depth < sp_.max_depth)) {
-      std::vector<double> tg(256), th(256);
-#pragma omp parallel for schedule(dynamic) firstprivate(tg, th)
-      for (int f = 0; f < F_; ++f) {
-        per[f].feature = -1;
-        per[f].gain = -std::numeric_limits<double>::infinity();
-        if (!fmask[f]) continue;
-        if (sp_.bynode_k > 0 &&
-            !NodeFeatureSelected(sp_.bynode_seed, sp_.tree_seq, leaf->slot, f,
-                                 reinterpret_cast<const int8_t*>(fmask.data()), F_, sp_.bynode_k))
-          continue;
-        const BinMapper& m = data_->ref.mappers[data_->ref.used_features[f]];
-        for (int b = 0; b < m.num_bin; ++b) { tg[b] = hist[f * 512 + b * 2]; th[b] = hist[f * 512 + b * 2 + 1]; }
-        const MonoCtx mc{leaf->lo, leaf->hi, mono_[f]};
-        FindBestSplitFeature(tg.data(), th.data(), m.num_bin, m, f, leaf->sum_g, leaf->sum_h, leaf->gcount, sp_, &per[f],
-                             sp_.has_mono ? &mc : nullptr);
-        if (sp_.has_mono && mono_[f] != 0 && sp_.monotone_penalty > 0 && per[f].feature >= 0)
-          per[f].gain *= MonotonePenaltyFactor(leaf->depth, sp_.monotone_penalty);
-      }
+    std::vector<std::vector<SplitResult>*> outs{per_out};
+    PerFeatureBestMulti({&hist}, {&leaf_in}, fmask, outs);
+  }
+
+  // per-feature best splits of several leaves in ONE parallel region over (leaf, feature) pairs
+  void PerFeatureBestMulti(const std::vector<const std::vector<double>*>& hists,
+                           const std::vector<const LeafInfo*>& lv, const std::vector<char>& fmask,
+                           const std::vector<std::vector<SplitResult>*>& outs) {
+    const int C = static_cast<int>(lv.size());
+    std::vector<char> ok(C);
+    for (int c = 0; c < C; ++c) {
+      std::vector<SplitResult>& per = *outs[c];
+      per.assign(F_, SplitResult{});
+      for (auto& r : per) { r.feature = -1; r.gain = -std::numeric_limits<double>::infinity(); }
+      ok[c] = lv[c]->gcount >= 2 * sp_.min_data_in_leaf && (sp_.max_depth <= 0 || lv[c]->depth < sp_.max_depth);
     }
+    const int tasks = C * F_;
+    const int nt = std::max(1, std::min(nthreads_, tasks / 4));
+#pragma omp parallel for schedule(dynamic, 2) num_threads(nt)
+    for (int task = 0; task < tasks; ++task) {
+      const int c = task / F_, f = task % F_;
+      if (!ok[c] || !fmask[f]) continue;
+      const LeafInfo* leaf = lv[c];
+      if (sp_.bynode_k > 0 &&
+          !NodeFeatureSelected(sp_.bynode_seed, sp_.tree_seq, leaf->slot, f,
+                               reinterpret_cast<const int8_t*>(fmask.data()), F_, sp_.bynode_k))
+        continue;
+      double tg[256], th[256];
+      const std::vector<double>& hist = *hists[c];
+      SplitResult& out = (*outs[c])[f];
+      const BinMapper& m = data_->ref.mappers[data_->ref.used_features[f]];
+      for (int b = 0; b < m.num_bin; ++b) { tg[b] = hist[f * 512 + b * 2]; th[b] = hist[f * 512 + b * 2 + 1]; }
+      const MonoCtx mc{leaf->lo, leaf->hi, mono_[f]};
+      FindBestSplitFeature(tg, th, m.num_bin, m, f, leaf->sum_g, leaf->sum_h, leaf->gcount, sp_, &out,
+                           sp_.has_mono ? &mc : nullptr);
+      if (sp_.has_mono && mono_[f] != 0 && sp_.monotone_penalty > 0 && out.feature >= 0)
+        out.gain *= MonotonePenaltyFactor(leaf->depth, sp_.monotone_penalty);
+    }
+  }
+
+  // best split of several leaves (FindBest per leaf, one parallel region)
+  void FindBestMulti(const std::vector<const std::vector<double>*>& hists, const std::vector<LeafInfo*>& ls,
+                     const std::vector<char>& fmask) {
+    const auto t0 = Clock::now();
+    const int C = static_cast<int>(ls.size());
+    std::vector<std::vector<SplitResult>> per(C);
+    std::vector<std::vector<SplitResult>*> outs;
+    std::vector<const LeafInfo*> lv;
+    for (int c = 0; c < C; ++c) { outs.push_back(&per[c]); lv.push_back(ls[c]); }
+    PerFeatureBestMulti(hists, lv, fmask, outs);
+    for (int c = 0; c < C; ++c) {
+      SplitResult best{};
+      best.feature = -1;
+      best.gain = -std::numeric_limits<double>::infinity();
+      for (int f = 0; f < F_; ++f) {
+        if (per[c][f].feature < 0) continue;
+        if (best.feature < 0 ||
+            SplitBetter(per[c][f].gain, per[c][f].feature, per[c][f].threshold, best.gain, best.feature, best.threshold))
+          best = per[c][f];
+      }
+      ls[c]->best = best;
+      ls[c]->has_best = best.feature >= 0;
+    }
+    stats.split_ms += Ms(t0);
   }
 
   bool GoesLeft(const SplitResult& s, const uint8_t* row) const {
@@ -399,7 +547,6 @@ class CpuBackend : public TrainBackend {
     BuildHist(k, leaves[0], fmask, &hists[0], !voting);
     if (voting) VotingFind({&leaves[0]}, {&hists[0]}, fmask, leaves[0].gcount);
     else FindBest(hists[0], &leaves[0], fmask);
-    std::vector<int64_t> tmp;
     for (int s = 1; s < L; ++s) {
       int bl = -1;
       for (int l = 0; l < tree.num_leaves; ++l) {
@@ -410,13 +557,27 @@ class CpuBackend : public TrainBackend {
       const SplitResult sr = leaves[bl].best;
       LeafInfo& P = leaves[bl];
       // stable partition of the leaf's rows
-      tmp.resize(P.count);
-      int64_t nl = 0;
-      for (int64_t p = 0; p < P.count; ++p) {
-        const int64_t r = idx_[P.begin + p];
-        if (GoesLeft(sr, &data_->bins[r * data_->row_stride])) idx_[P.begin + nl++] = r; else tmp[p - nl] = r;
+      const auto tp = Clock::now();
+      const uint8_t* col = data_->bins.data() + sr.feature;  // the split feature's byte in every row
+      const int64_t rs = data_->row_stride;
+      const BinMapper& pm = data_->ref.mappers[data_->ref.used_features[sr.feature]];
+      const uint32_t miss_bin = pm.missing_type == kMissingZero ? static_cast<uint32_t>(pm.default_bin)
+                                : (pm.missing_type == kMissingNaN ? static_cast<uint32_t>(pm.num_bin - 1) : 256u);
+      const bool dleft = sr.default_left != 0;
+      const uint32_t thr = sr.threshold;
+      int64_t nl;
+      if (sr.is_cat) {
+        nl = ParallelPartition(P.begin, P.count, [&](int64_t r) {
+          const uint32_t b = col[r * rs];
+          return ((sr.cat_bits[b / 32] >> (b % 32)) & 1u) != 0;
+        }, col, rs);
+      } else {
+        nl = ParallelPartition(P.begin, P.count, [&](int64_t r) {
+          const uint32_t b = col[r * rs];
+          return b == miss_bin ? dleft : b <= thr;
+        }, col, rs);
       }
-      std::memcpy(&idx_[P.begin + nl], tmp.data(), sizeof(int64_t) * (P.count - nl));
+      stats.partition_ms += Ms(tp);
       const int fr = data_->ref.used_features[sr.feature];
       const BinMapper& m = data_->ref.mappers[fr];
       int right;
@@ -465,16 +626,41 @@ class CpuBackend : public TrainBackend {
       } else {
         leaves[small].gcount = last_gcount_;
         leaves[large].gcount = pg - last_gcount_;
-        FindBest(hists[bl], &leaves[bl], fmask);
-        FindBest(hists[right], &leaves[right], fmask);
+        FindBestMulti({&hists[bl], &hists[right]}, {&leaves[bl], &leaves[right]}, fmask);
       }
     }
-    // exact (global) leaf counts
-    for (int l = 0; l < tree.num_leaves; ++l) tree.leaf_count[l] = leaves[l].gcount;
+    // exact (global) leaf counts; each leaf's row segment is kept for the score update
+    seg_.resize(tree.num_leaves);
+    for (int l = 0; l < tree.num_leaves; ++l) {
+      tree.leaf_count[l] = leaves[l].gcount;
+      seg_[l] = {leaves[l].begin, leaves[l].count};
+    }
     return tree;
   }
 
+  // Without bagging every row sits in exactly one leaf's segment of idx_ after the growth, so the new
+  // tree's shrunk output is added per segment instead of walking the tree for every row (LightGBM's
+  // score updater does the same with its data partition).
+  Tree TrainTreeAndUpdateScore(int k, const std::vector<char>& feature_mask, double shrink, bool* updated) override {
+    Tree t = TrainTree(k, feature_mask);
+    *updated = false;
+    if (use_bag_ || t.num_leaves <= 1) return t;
+    const auto t0 = Clock::now();
+    double* s = score_.data() + static_cast<size_t>(k) * n_;
+    const int64_t* idx = idx_.data();
+    for (int l = 0; l < t.num_leaves; ++l) {
+      const double v = t.leaf_value[l] * shrink;
+      const int64_t b = seg_[l].first, e = b + seg_[l].second;
+#pragma omp parallel for schedule(static) num_threads(std::max<int>(1, std::min<int64_t>(nthreads_, (e - b) / 16384 + 1)))
+      for (int64_t p = b; p < e; ++p) s[idx[p]] += v;
+    }
+    stats.score_ms += Ms(t0);
+    *updated = true;
+    return t;
+  }
+
   void UpdateScore(const Tree& t, int k, double scale) override {
+    const ScoreTimer timer(&stats.score_ms);
     double* s = score_.data() + static_cast<size_t>(k) * n_;
     if (t.num_leaves <= 1) {
       for (int64_t i = 0; i < n_; ++i) s[i] += scale * t.leaf_value[0];
@@ -503,6 +689,11 @@ class CpuBackend : public TrainBackend {
   std::vector<double> score_;
   std::vector<float> g_, h_;
   std::vector<int64_t> idx_;
+  std::vector<std::pair<int64_t, int64_t>> seg_;  // (begin, count) in idx_ of each leaf of the last tree
+  std::vector<std::vector<double>> hloc_;         // per-thread histogram tables (BuildHist)
+  std::vector<float> ogh_;                        // the leaf's (g, h) in row order (BuildHist)
+  std::vector<int64_t> part_tmp_;                 // partition scratch
+  std::vector<uint8_t> part_flag_;
   std::vector<int32_t> bag_;
   bool use_bag_ = false;
   int64_t last_gcount_ = 0;
