@@ -8,7 +8,7 @@ initializers; ONNXUtils.scala:267-370)."""
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Iterable, Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -188,8 +188,9 @@ class Graph:
             defined.update(n.outputs)
         return refs
 
-    def toposort(self) -> List[Node]:
-        avail = set(self.initializers) | {i.name for i in self.inputs} | {""}
+    def toposort(self, outer: Iterable[str] = ()) -> List[Node]:
+        """nodes in dependency order; `outer`: names a subgraph may read from its enclosing scope"""
+        avail = set(self.initializers) | {i.name for i in self.inputs} | {""} | set(outer)
         pending = list(self.nodes)
         order: List[Node] = []
         while pending:

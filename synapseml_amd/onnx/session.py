@@ -35,6 +35,7 @@ import torch
 from . import proto as P
 from .graph import Graph, Node, ValueInfo
 from .ops import OPS, TORCH_OF, conv_args, _sym_pad
+from . import ops_ext  # noqa: F401  (registers the extended operator set)
 
 OPT_LEVELS = ("NO_OPT", "BASIC_OPT", "EXTENDED_OPT", "ALL_OPT")
 _ACTS = {"Relu": 1, "LeakyRelu": 2, "Sigmoid": 3, "Clip": 4}
@@ -45,6 +46,21 @@ _MAX_FOLD_ELEMS = 1 << 24
 
 def _is_const_tensor(v) -> bool:
     return isinstance(v, (torch.Tensor, np.ndarray))
+
+
+def _outer_refs(g: Graph) -> set:
+    """names a graph (and its nested subgraphs) reads without producing them: its outer-scope references"""
+    produced = set(g.initializers) | {v.name for v in g.inputs}
+    refs = set()
+    for n in g.nodes:
+        for x in n.inputs:
+            if x and x not in produced:
+                refs.add(x)
+        for v in n.attrs.values():
+            if isinstance(v, Graph):
+                refs |= {x for x in _outer_refs(v) if x not in produced}
+        produced.update(o for o in n.outputs if o)
+    return refs
 
 
 class _RT:
@@ -61,8 +77,15 @@ class _RT:
         self.session = session
 
     def run_subgraph(self, g: Graph, feeds: Dict[str, Any]):
-        sub = InferenceSession.from_graph(g, device=self.device, optimization_level="NO_OPT",
-                                          outer=self.session._live_values)
+        """Run a graph attribute (If branch, Loop / Scan body) with this graph's live values as its outer
+        scope. The sub-session is built once per graph and reused across iterations and runs."""
+        cache = self.session.__dict__.setdefault("_sub_sessions", {})
+        sub = cache.get(id(g))
+        if sub is None or sub.graph is not g:
+            sub = InferenceSession.from_graph(g, device=self.device, optimization_level="NO_OPT",
+                                              outer=self.session._live_values)
+            cache[id(g)] = sub
+        sub._outer = self.session._live_values
         return sub.run_values(feeds)
 
 
@@ -111,7 +134,7 @@ class InferenceSession:
         self._consts: Dict[str, Any] = {}
         for k, v in g.initializers.items():
             self._consts[k] = v if v.dtype == object else torch.from_numpy(np.array(v, copy=True))
-        nodes = g.toposort()
+        nodes = g.toposort(outer=g.outer_refs() if self._outer else ())
         if lvl != "NO_OPT":
             nodes = self._fold_constants(nodes)
             nodes = self._fold_conv_bn(nodes)
@@ -474,6 +497,11 @@ class InferenceSession:
             for x in n.inputs:
                 if x:
                     last[x] = i
+            # values a subgraph (If / Loop / Scan body) reads from this scope stay alive until that node
+            for v in n.attrs.values():
+                if isinstance(v, Graph):
+                    for x in _outer_refs(v):
+                        last[x] = i
         outs = {o.name for o in self.outputs}
         self._free_after: List[List[str]] = [[] for _ in self.nodes]
         for name, i in last.items():
