@@ -66,7 +66,9 @@ class LogisticRegressionModel(Model, HasFeaturesCol, HasPredictionCol, HasRawPre
         s = self._scores(X)
         if s.shape[1] == 1:
             raw = np.concatenate([-s, s], axis=1)
-            p1 = 1.0 / (1.0 + np.exp(-s[:, 0]))
+            from scipy.special import expit
+
+            p1 = expit(s[:, 0])  # overflow-free logistic
             prob = np.stack([1 - p1, p1], axis=1)
         else:
             raw = s

@@ -136,8 +136,10 @@ class _ForestParams(Params):
         if frac is None:
             frac = float(s)
         sub = self.getSubsamplingRate()
+        # SparkML samples the candidate features at every node (featureSubsetStrategy), LightGBM's
+        # feature_fraction is per tree: the per-node form is feature_fraction_bynode
         return dict(boostingType="rf", numIterations=self.getNumTrees(), baggingFraction=min(sub, 0.999),
-                    baggingFreq=1, featureFraction=min(1.0, max(frac, 1e-6)))
+                    baggingFreq=1, featureFraction=1.0, featureFractionByNode=min(1.0, max(frac, 1e-6)))
 
 
 class RandomForestClassifier(_TreeClassifier, _ForestParams):
