@@ -12,8 +12,9 @@
 //
 // Tiling: 256 threads = 4 waves in 2x2, block tile BM x BN x 128 bytes of K
 // (BK = 64 f16/bf16 or 32 f32 elements), wave tile (BM/2) x (BN/2) of 16x16x32
-// f16/bf16 MFMAs, or of 16x16x4 f32 MFMAs (exact f32, the fp32 graphs: ORT
-// parity without TF32-style rounding; gfx950 has no xf32). A and B
+// f16/bf16 MFMAs, or of 16x16x4 f32 MFMAs (exact f32; gfx950 has no xf32), or - for f32 - of
+// 16x16x32 bf16 MFMAs over operands split into 2 or 3 bf16 planes (kSplit: 3 or 6 products per
+// pair; the 6-product form matches the exact f32 MFMA's error and is the fp32 graphs' default). A and B
 // tiles are staged through registers (the prologue is applied there) into a
 // double-buffered LDS image with a 144-byte row pitch (conflict-free 16-lane
 // ds_read_b128 fragment reads); the next tile's global loads are issued before
@@ -177,7 +178,12 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 // kStem: a few-channel stem conv (the 3-channel ResNet stem, input padded to C = 4, weights packed to
 // [Cout][8][8][4] with zero taps): a 16-B A chunk is two horizontally adjacent pixels (taps s, s+1 of row r),
 // each read as its own 8-B buffer load (zero outside the image), a 64-wide K tile = two tap rows.
-template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false>
+// kSplit (f32 only): 0 = exact f32 MFMAs; 2 / 3 = every f32 operand split into that many bf16 planes
+// (x = x1 + x2 (+ x3), each the bf16 rounding of what the earlier planes left) and the product rebuilt from
+// the 16x16x32 bf16 MFMAs of the plane pairs whose weight reaches the f32 rounding level: 3 products for 2
+// planes (~16 significant bits per product), 6 for 3 planes (~24 bits, f32-class). One K tile (32 f32) is
+// one 16x16x32 step per plane pair instead of eight 16x16x4 f32 MFMAs (1/16 of the bf16 rate on gfx950).
+template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false, int kSplit = 0>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
@@ -187,11 +193,18 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   constexpr int AR = BM * kBKBytes / 16 / kThr;  // 16-B A chunks per thread per tile
   constexpr int BR = BN * kBKBytes / 16 / kThr;  // 16-B B chunks per thread per tile
   constexpr int RS = kThr / 8;                  // tile rows covered by one pass of the block
+  static_assert(kSplit == 0 || sizeof(T) == 4, "bf16 operand splitting is an f32 mode");
+  constexpr int kLdB = kBK + 8;                 // split planes: bf16 row pitch (80 B: conflict-free b128 reads)
+  constexpr int kOpBytes = kSplit ? 2 * kSplit * (BM + BN) * kLdB * 2 : 2 * (BM + BN) * kLd * static_cast<int>(sizeof(T));
   // the epilogue re-uses the operand buffers to stage each wave's tile
-  static_assert(2 * (BM + BN) * kLd >= (kThr / 64) * WM * (WN + 8), "epilogue staging exceeds the LDS tile");
-  __shared__ __attribute__((aligned(16))) T lds[2 * (BM + BN) * kLd];
+  constexpr int kEpiBytes = (kThr / 64) * WM * (WN + 8) * static_cast<int>(sizeof(T));
+  static_assert(kSplit || kOpBytes >= kEpiBytes, "epilogue staging exceeds the LDS tile");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kOpBytes > kEpiBytes ? kOpBytes : kEpiBytes];
+  T* lds = reinterpret_cast<T*>(smem);
   T* As = lds;
   T* Bs = lds + 2 * BM * kLd;
+  __bf16* Asb = reinterpret_cast<__bf16*>(smem);            // [plane][buf][BM][kLdB]
+  __bf16* Bsb = Asb + 2 * (kSplit ? kSplit : 1) * BM * kLdB;  // [plane][buf][BN][kLdB]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int M = a.B * a.OH * a.OW;
@@ -253,7 +266,34 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   const int nk = K / kBK;
 
   auto compute = [&](int buf) {
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (kSplit > 0) {
+      // one 32-deep k step: lane group g = lane >> 4 holds k = 8g..8g+7 of its A row / B column per plane
+      const int kb = 8 * (lane >> 4);
+      b8 af[kSplit][TM], bf[kSplit][TN];
+#pragma unroll
+      for (int p = 0; p < kSplit; ++p) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[p][i] = *reinterpret_cast<const b8*>(Asb + ((p * 2 + buf) * BM + wm0 + i * 16 + fr) * kLdB + kb);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bf[p][j] = *reinterpret_cast<const b8*>(Bsb + ((p * 2 + buf) * BN + wn0 + j * 16 + fr) * kLdB + kb);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          // small terms first
+          if constexpr (kSplit == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2][i], bf[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bf[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bf[2][j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bf[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
+        }
+    } else if constexpr (sizeof(T) == 4) {
       // 16 k per step; lane group g = lane >> 4 holds k = 4g..4g+3 of its A row and B column, and MFMA c
       // takes component c of both: every (k, row, col) product is summed exactly once
 #pragma unroll
@@ -355,7 +395,42 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
       }
     }
   };
+  // split planes: 4 f32 -> kSplit x 4 bf16 (8 B per plane), x_p = bf16(x - x_1 - ... - x_{p-1})
+  auto store_split = [&](__bf16* base, int rows, int buf, int row, const uint4& v) {
+    const float* e = reinterpret_cast<const float*>(&v);
+    float r[4] = {e[0], e[1], e[2], e[3]};
+#pragma unroll
+    for (int p = 0; p < (kSplit ? kSplit : 1); ++p) {
+      __bf16 q[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        q[t] = static_cast<__bf16>(r[t]);
+        r[t] -= static_cast<float>(q[t]);
+      }
+      *reinterpret_cast<uint2*>(base + ((p * 2 + buf) * rows + row) * kLdB + kc * 4) = *reinterpret_cast<const uint2*>(q);
+    }
+  };
   auto store_tile = [&](int buf, const Stage& st) {
+    if constexpr (kSplit > 0) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        uint4 v = st.a[i];
+        if constexpr (pro) {
+          float* e = reinterpret_cast<float*>(&v);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float t = e[j] * st.q[0][j] + st.q[NQ][j];
+            e[j] = a.prologue_relu ? fmaxf(t, 0.f) : t;
+          }
+          const unsigned mk = 0u - ((st.okm >> i) & 1u);
+          v.x &= mk; v.y &= mk; v.z &= mk; v.w &= mk;
+        }
+        store_split(Asb, BM, buf, (tid >> 3) + RS * i, v);
+      }
+#pragma unroll
+      for (int i = 0; i < BR; ++i) store_split(Bsb, BN, buf, (tid >> 3) + RS * i, st.b[i]);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       uint4 v = st.a[i];
@@ -407,7 +482,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   ConvEpilogue<T, WM, WN>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
-template <class T, int BM, int BN, int kThr = kThreads>
+template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   // f32 64x64: two register stages when the K loop is long enough and there is no prologue (the prologue
@@ -420,16 +495,18 @@ void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   if constexpr (sizeof(T) == 4 && BM == 64 && BN == 64) {
     const int nk = a.R * a.S * a.C / Tile<T>::BK;
     if (depth == 2 || (depth == 0 && !a.in_scale && nk > 8)) {
-      auto k2 = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 2> : conv_mfma_kernel<T, BM, BN, false, kThr, 2>;
+      auto k2 = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 2, false, kSplit>
+                           : conv_mfma_kernel<T, BM, BN, false, kThr, 2, false, kSplit>;
       hipLaunchKernelGGL(k2, dim3(blocks), dim3(kThr), 0, st, a);
       return;
     }
   }
-  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr> : conv_mfma_kernel<T, BM, BN, false, kThr>;
+  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit>
+                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit>;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
 
-template <class T>
+template <class T, int kSplit = 0>
 int Launch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.OH * a.OW;
   // SML_CONV_TILE=BMxBN forces one register-staged tile shape for the process (tuning sweeps);
@@ -442,12 +519,12 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     return x ? bm * 1000 + std::atoi(x + 1) : 0;
   }();
   switch (a.kernel ? a.kernel : env_tile) {
-    case 64064: LaunchTile<T, 64, 64>(a, M, st); return 0;
-    case 128064: LaunchTile<T, 128, 64>(a, M, st); return 0;
-    case 64128: LaunchTile<T, 64, 128>(a, M, st); return 0;
-    case 128128: LaunchTile<T, 128, 128>(a, M, st); return 0;
-    case 128999: LaunchTile<T, 128, 128, 512>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
-    case 64999: LaunchTile<T, 64, 64, 512>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
+    case 64064: LaunchTile<T, 64, 64, kThreads, kSplit>(a, M, st); return 0;
+    case 128064: LaunchTile<T, 128, 64, kThreads, kSplit>(a, M, st); return 0;
+    case 64128: LaunchTile<T, 64, 128, kThreads, kSplit>(a, M, st); return 0;
+    case 128128: LaunchTile<T, 128, 128, kThreads, kSplit>(a, M, st); return 0;
+    case 128999: LaunchTile<T, 128, 128, 512, kSplit>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
+    case 64999: LaunchTile<T, 64, 64, 512, kSplit>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
     case 256128:
     case 128256:
       // 8-wave tiles: the f32 epilogue staging would not fit the operand LDS
@@ -465,8 +542,16 @@ int Launch(const ConvArgs& a, hipStream_t st) {
   // f32: 64x64 on every shape (r2_fp32conv sweep: 2625 us over the 14 shapes vs 2865-3258 for the larger
   // tiles; 36 KB of LDS, four blocks per CU hide the per-tile barrier behind the 32-cycle MFMAs), with
   // 8 waves of 16x32 (r2_tile64w8: 2537 -> 2467 us)
-  if constexpr (sizeof(T) == 4) {
+  if constexpr (sizeof(T) == 4 && kSplit == 0) {
     LaunchTile<T, 64, 64, 512>(a, M, st);
+    return 0;
+  }
+  // f32 on bf16 planes: the K loop is MFMA-light, so the larger tile's operand reuse wins except on the
+  // Cout = 64 layers (r3 sweep, bf16x3, 14 shapes: 64x64 (4 waves) 1591 us, 128x128 8 waves 1391 us, this
+  // rule ~1323 us; exact f32 2502 us)
+  if constexpr (kSplit > 0) {
+    if (a.Cout <= 64) LaunchTile<T, 64, 64, kThreads, kSplit>(a, M, st);
+    else LaunchTile<T, 128, 128, 512, kSplit>(a, M, st);
     return 0;
   }
   if (a.Cout <= 64) {
@@ -489,10 +574,12 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
   return 0;
 }
 
-// dtype: 0 fp32, 1 fp16, 2 bf16 (C must be a multiple of one tile's K: 32 f32 / 64 f16/bf16 channels)
+// dtype: 0 fp32 (exact f32 MFMAs), 1 fp16, 2 bf16, 3 fp32 on 2 bf16 planes (3 products), 4 fp32 on 3 bf16
+// planes (6 products) (C must be a multiple of one tile's K: 32 f32 / 64 f16/bf16 channels)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
-  const int bk = dtype == 0 ? Tile<float>::BK : Tile<_Float16>::BK;
-  return groups == 1 && C > 0 && C % bk == 0 && Cout > 0 && (dtype == 0 || dtype == 1 || dtype == 2);
+  const bool f32 = dtype == 0 || dtype == 3 || dtype == 4;
+  const int bk = f32 ? Tile<float>::BK : Tile<_Float16>::BK;
+  return groups == 1 && C > 0 && C % bk == 0 && Cout > 0 && dtype >= 0 && dtype <= 4;
 }
 
 int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
@@ -509,12 +596,16 @@ int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
   if (!ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return -1;
   if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
   // buffer-resource offsets are 32-bit and the per-row tap mask holds 64 taps
-  const int64_t es = dtype == 0 ? 4 : 2;
+  const int64_t es = (dtype == 0 || dtype == 3 || dtype == 4) ? 4 : 2;
   if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * es >= (1ll << 31) ||
       static_cast<int64_t>(a.Cout) * a.R * a.S * a.C * es >= (1ll << 31) || a.R * a.S > 64)
     return -5;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int rc = dtype == 0 ? Launch<float>(a, st) : dtype == 1 ? Launch<_Float16>(a, st) : Launch<__bf16>(a, st);
+  const int rc = dtype == 0 ? Launch<float>(a, st)
+                 : dtype == 1 ? Launch<_Float16>(a, st)
+                 : dtype == 2 ? Launch<__bf16>(a, st)
+                 : dtype == 3 ? Launch<float, 2>(a, st)
+                              : Launch<float, 3>(a, st);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -174,8 +174,9 @@ class ONNXModel(Transformer):
                        "If not specified, auto detection will be used.", None, T.toString)
     optimizationLevel = Param("Specify the optimization level for the ONNX graph optimizations: NO_OPT, BASIC_OPT, "
                               "EXTENDED_OPT, ALL_OPT", "ALL_OPT", T.toString)
-    precision = Param("Compute precision of floating-point operators: fp32 (ORT parity), fp16 or bf16", "fp32",
-                      T.toString)
+    precision = Param("Compute precision of floating-point operators: fp32 (ORT parity), fp16 or bf16; "
+                      "fp32-exact / fp32-bf16x6 / fp32-bf16x3 pick how fp32 convolutions use the matrix cores "
+                      "(exact f32 MFMAs, or f32 operands split over 3 / 2 bf16 planes)", "fp32", T.toString)
 
     # ---- model bytes
     def setModelLocation(self, path: str) -> "ONNXModel":  # noqa: N802

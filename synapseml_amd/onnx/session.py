@@ -117,7 +117,15 @@ class InferenceSession:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.gpu = self.device.type == "cuda"
         self.opset = int(g.opset.get("", g.opset.get("ai.onnx", 13)))
-        self.compute_dtype = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[precision]
+        # "fp32" | "fp16" | "bf16", or "fp32-<mode>" choosing how fp32 convolutions use the matrix cores
+        # (ops.conv.F32_MODES: exact f32 MFMAs, or f32 operands split over bf16 planes; default SML_CONV_F32)
+        base, _, mode = str(precision).partition("-")
+        self.compute_dtype = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[base]
+        from ..ops.conv import F32_MODES
+
+        if mode and (base != "fp32" or mode not in F32_MODES):
+            raise ValueError(f"precision {precision!r}: fp32 modes are {['fp32-' + m for m in F32_MODES]}")
+        self.f32_conv_mode = mode or None
         self.channels_last = self.gpu if channels_last is None else channels_last
         lvl = optimization_level.upper()
         if lvl not in OPT_LEVELS:
@@ -742,7 +750,8 @@ def _fused_conv(rt, at, x):
                         dil, bias=f32(b), relu=2 if act == 1 else 0,
                         in_affine=(f32(pro[0]), f32(pro[1])) if pro is not None else None,
                         in_relu=bool(at.get("__pro_relu", 1)), res=res,
-                        out_affine=(f32(post[0]), f32(post[1])) if post is not None else None)
+                        out_affine=(f32(post[0]), f32(post[1])) if post is not None else None,
+                        f32_mode=rt.session.f32_conv_mode)
         return list(y) if post is not None else [y]
     if _STEM_MFMA and pro is None and post is None and _stem_ok(rt, at, inp, w):
         return [_stem_conv(rt, at, inp, w, b, res, act)]

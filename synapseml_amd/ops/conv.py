@@ -1,8 +1,9 @@
 """Python entry to the MFMA implicit-GEMM convolution (csrc/nn/conv_mfma.hip).
 
 Tensors are torch CUDA tensors in channels_last memory (NHWC); weights are
-packed once to [Cout, R, S, Cin]. Epilogue / prologue tensors are fp32. fp32 activations run on the
-exact f32-input MFMA (16x16x4), fp16/bf16 on 16x16x32."""
+packed once to [Cout, R, S, Cin]. Epilogue / prologue tensors are fp32. fp16/bf16 run on the 16x16x32
+MFMA; fp32 either on the exact f32-input MFMA (16x16x4, 1/16 of the bf16 rate) or with every f32 operand
+split over bf16 planes and the products rebuilt from 16x16x32 MFMAs (F32_MODES)."""
 from __future__ import annotations
 
 from typing import Optional, Sequence, Tuple
@@ -12,6 +13,22 @@ import torch
 from . import native
 
 _DT = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+# fp32 convolution modes: exact f32 MFMAs (16x16x4, 1/16 of the bf16 rate on gfx950), or every f32 operand
+# split into 2 / 3 bf16 planes with the products rebuilt from 3 / 6 bf16 MFMAs (16x16x32): ~16 / ~24
+# significant bits per product (TF32 keeps 11), fp32 accumulation, fp32 in and out.
+F32_MODES = {"exact": 0, "bf16x3": 3, "bf16x6": 4}
+
+
+def f32_mode_default() -> str:
+    import os
+
+    # bf16x6 by default: its error against an fp64 convolution measured at or below the exact f32 MFMA's
+    # (0.2-1.0e-6 vs 0.3-1.4e-6 of max |y| on four ResNet shapes) and ResNet-50 fp32 runs 4 % faster;
+    # bf16x3 (~3e-6) is the fast opt-in (+60 %: 11.9k -> 18.3k img/s at batch 128; profiles/r3/conv_f32_modes)
+    m = os.environ.get("SML_CONV_F32", "bf16x6")
+    if m not in F32_MODES:
+        raise ValueError(f"SML_CONV_F32={m!r}: expected one of {sorted(F32_MODES)}")
+    return m
 
 
 def supported(cin: int, cout: int, groups: int, dtype: torch.dtype) -> bool:
@@ -40,13 +57,15 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
                 bias: Optional[torch.Tensor] = None, relu=False,
                 in_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, in_relu: bool = True,
                 res: Optional[torch.Tensor] = None,
-                out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, kernel: int = 0):
+                out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, kernel: int = 0,
+                f32_mode: Optional[str] = None):
     """y = conv(pro(x), w) + bias, ReLU, + res; optionally also y2 = relu(y * out_scale + out_shift).
 
     ``relu``: False/0 none, True/1 before the residual add, 2 after it. ``pad``: (top, left) or
     (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp32/fp16/bf16 (C % 32 == 0 for fp32, % 64 otherwise). ``wp``: packed [Cout, R, S, C]
     (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2).
-    ``kernel``: 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128, 128128, 256128, 128256)."""
+    ``kernel``: 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128, 128128, 256128, 128256).
+    ``f32_mode`` (fp32 inputs): "exact" | "bf16x3" | "bf16x6" (see F32_MODES; default SML_CONV_F32 or exact)."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv2d_nhwc expects a channels_last input")
@@ -66,12 +85,13 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
     native.load("_nn").conv_mfma(
         x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(in_affine[0] if in_affine else None),
         _ptr(in_affine[1] if in_affine else None), _ptr(bias), _ptr(res), _ptr(out_affine[0] if out_affine else None),
-        _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu), _DT[x.dtype],
+        _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu),
+        F32_MODES[f32_mode or f32_mode_default()] if x.dtype == torch.float32 else _DT[x.dtype],
         torch.cuda.current_stream(x.device).cuda_stream, int(kernel))
     return (y, y2) if out_affine is not None else y
 
 
-__all__ = ["supported", "pack_weight", "conv2d_nhwc", "out_hw"]
+__all__ = ["supported", "pack_weight", "conv2d_nhwc", "out_hw", "F32_MODES"]
 
 
 def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),

@@ -176,3 +176,70 @@ def test_stem_packed_form_exact(dtype):
         y = conv2d_nhwc(x4, wp, 8, 8, (st, st), (pd, pd, pd + 8 - k, pd + 8 - k), kernel=1)
         assert y.shape == ref.shape
         torch.testing.assert_close(y.cpu().double(), ref, rtol=0, atol=0)
+
+
+# ---------------------------------------------------------------- fp32 on split bf16 planes
+@pytest.mark.parametrize("mode", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("kernel", [0, 64064, 64999, 128064, 64128, 128128])
+def test_fp32_split_integer_layout(mode, kernel):
+    """Small integers are exact in the first bf16 plane (the others are zero): any plane / k / lane / row
+    mapping error of the split form is an exact mismatch."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    g = torch.Generator().manual_seed(3)
+    for (B, C, H, W, Co, k) in ((2, 32, 9, 7, 80, 3), (3, 96, 17, 11, 200, 3), (2, 64, 8, 8, 36, 1)):
+        x = torch.randint(-3, 4, (B, C, H, W), generator=g).float().cuda().contiguous(memory_format=torch.channels_last)
+        w = torch.randint(-3, 4, (Co, C, k, k), generator=g).float().cuda()
+        y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (1, 1), (k // 2, k // 2), kernel=kernel, f32_mode=mode)
+        ref = F.conv2d(x.cpu().double(), w.cpu().double(), None, 1, k // 2)
+        torch.testing.assert_close(y.cpu().double(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("shape", [
+    (4, 64, 56, 56, 256, 1, 1, 0),
+    (2, 256, 28, 28, 128, 3, 1, 1),
+    (2, 128, 29, 29, 128, 3, 2, 1),
+    (1, 2048, 7, 7, 512, 1, 1, 0),
+])
+def test_fp32_split_modes_error_vs_fp64(shape):
+    """Error of the three fp32 modes against an fp64 convolution, relative to max |y|: bf16x6 keeps every
+    product term down to the f32 rounding level (same bound as the exact f32 MFMA), bf16x3 ~16 bits per
+    product (TF32, the reference's default fp32 conv math on NVIDIA tensor cores, keeps 11)."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    B, C, H, W, Co, k, st, pd = shape
+    torch.manual_seed(4)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5
+    bias = torch.randn(Co, device="cuda")
+    ref = torch.relu(F.conv2d(x.cpu().double(), w.cpu().double(), bias.cpu().double(), st, pd))
+    scale = float(ref.abs().max())
+    errs = {}
+    for mode in ("exact", "bf16x6", "bf16x3"):
+        y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), bias=bias, relu=True, f32_mode=mode)
+        errs[mode] = float((y.cpu().double() - ref).abs().max()) / scale
+    print("max |err| / max |y|:", {m: f"{e:.2e}" for m, e in errs.items()})
+    assert errs["exact"] < 2e-6
+    assert errs["bf16x6"] < 2e-6
+    assert errs["bf16x3"] < 5e-5
+
+
+def test_fp32_split_prologue_residual_dual_output():
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    torch.manual_seed(5)
+    B, C, H, W, Co = 2, 128, 14, 14, 256
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    pro = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1)
+    res = torch.randn(B, Co, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    post = (torch.rand(Co, device="cuda") + 0.5, torch.randn(Co, device="cuda") * 0.1)
+    for k in (1, 3):
+        w = torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5
+        y, y2 = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (1, 1), (k // 2, k // 2), in_affine=pro,
+                            res=res, out_affine=post, f32_mode="bf16x6")
+        xd = torch.relu(x.cpu().double() * pro[0].cpu().double().view(1, -1, 1, 1)
+                        + pro[1].cpu().double().view(1, -1, 1, 1))
+        ry = F.conv2d(xd, w.cpu().double(), None, 1, k // 2) + res.cpu().double()
+        ry2 = torch.relu(ry * post[0].cpu().double().view(1, -1, 1, 1) + post[1].cpu().double().view(1, -1, 1, 1))
+        torch.testing.assert_close(y.cpu().double(), ry, rtol=1e-5, atol=2e-5)
+        torch.testing.assert_close(y2.cpu().double(), ry2, rtol=1e-5, atol=3e-5)
