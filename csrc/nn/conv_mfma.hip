@@ -183,7 +183,10 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 // the 16x16x32 bf16 MFMAs of the plane pairs whose weight reaches the f32 rounding level: 3 products for 2
 // planes (~16 significant bits per product), 6 for 3 planes (~24 bits, f32-class). One K tile (32 f32) is
 // one 16x16x32 step per plane pair instead of eight 16x16x4 f32 MFMAs (1/16 of the bf16 rate on gfx950).
-template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false, int kSplit = 0>
+// kWPre (with kSplit): the weights arrive already split, a.w = [kSplit][Cout][R][S][C] bf16 planes (packed
+// once per model by the executor): no split work for B at staging, 2 B per plane and element from HBM / L2.
+template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false, int kSplit = 0,
+          bool kWPre = false>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
@@ -244,13 +247,15 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   }
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.x), 0, a.B * a.H * a.W * a.C * static_cast<int>(sizeof(T)), 0x00020000);
+  constexpr int kWElem = kWPre ? 2 : static_cast<int>(sizeof(T));  // bytes per weight element (per plane)
+  const int wplane = a.Cout * K * kWElem;                             // bytes of one weight plane
   const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(a.w), 0, a.Cout * K * static_cast<int>(sizeof(T)), 0x00020000);
+      const_cast<void*>(a.w), 0, wplane * (kWPre ? kSplit : 1), 0x00020000);
   uint32_t boff[BR];  // byte offset of the thread's weight row chunk (out of range past Cout)
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int n = n0 + (tid >> 3) + RS * i;
-    boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kc * EPV) * static_cast<int>(sizeof(T))) : kOob;
+    boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kc * EPV) * kWElem) : kOob;
   }
   constexpr bool pro = kPro;  // prologue affine present (a.in_scale != nullptr): a template
                               // parameter, so no runtime branch sits between loads and their use
@@ -338,6 +343,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   constexpr int NQ = EPV / 4;  // float4s of prologue scale (and of shift) per 16-B chunk
   struct Stage {
     uint4 a[AR], b[BR];
+    uint2 bp[kWPre ? kSplit : 1][kWPre ? BR : 1];  // pre-split weight planes: 4 bf16 per plane and chunk
     f4 q[2 * NQ];
     unsigned okm;
   };
@@ -375,10 +381,20 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
         st.q[NQ + t] = shp[t];
       }
     }
+    if constexpr (kWPre) {
 #pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(wres, boff[i], lk0 * static_cast<int>(sizeof(T)), 0);
-      st.b[i] = *reinterpret_cast<uint4*>(&v);
+      for (int p = 0; p < kSplit; ++p)
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+          auto v = __builtin_amdgcn_raw_buffer_load_b64(wres, boff[i] + static_cast<uint32_t>(p * wplane), lk0 * 2, 0);
+          st.bp[p][i] = make_uint2(v[0], v[1]);
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(wres, boff[i], lk0 * static_cast<int>(sizeof(T)), 0);
+        st.b[i] = *reinterpret_cast<uint4*>(&v);
+      }
     }
     // advance to the next K tile (64 more channels, or the next tap)
     if (++loaded < nk) {
@@ -427,8 +443,16 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
         }
         store_split(Asb, BM, buf, (tid >> 3) + RS * i, v);
       }
+      if constexpr (kWPre) {
 #pragma unroll
-      for (int i = 0; i < BR; ++i) store_split(Bsb, BN, buf, (tid >> 3) + RS * i, st.b[i]);
+        for (int p = 0; p < kSplit; ++p)
+#pragma unroll
+          for (int i = 0; i < BR; ++i)
+            *reinterpret_cast<uint2*>(Bsb + ((p * 2 + buf) * BN + (tid >> 3) + RS * i) * kLdB + kc * 4) = st.bp[p][i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < BR; ++i) store_split(Bsb, BN, buf, (tid >> 3) + RS * i, st.b[i]);
+      }
       return;
     }
 #pragma unroll
@@ -482,7 +506,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   ConvEpilogue<T, WM, WN>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
-template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0>
+template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   // f32 64x64: two register stages when the K loop is long enough and there is no prologue (the prologue
@@ -495,18 +519,18 @@ void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   if constexpr (sizeof(T) == 4 && BM == 64 && BN == 64) {
     const int nk = a.R * a.S * a.C / Tile<T>::BK;
     if (depth == 2 || (depth == 0 && !a.in_scale && nk > 8)) {
-      auto k2 = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 2, false, kSplit>
-                           : conv_mfma_kernel<T, BM, BN, false, kThr, 2, false, kSplit>;
+      auto k2 = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 2, false, kSplit, kWPre>
+                           : conv_mfma_kernel<T, BM, BN, false, kThr, 2, false, kSplit, kWPre>;
       hipLaunchKernelGGL(k2, dim3(blocks), dim3(kThr), 0, st, a);
       return;
     }
   }
-  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit>
-                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit>;
+  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit, kWPre>
+                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit, kWPre>;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
 
-template <class T, int kSplit = 0>
+template <class T, int kSplit = 0, bool kWPre = false>
 int Launch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.OH * a.OW;
   // SML_CONV_TILE=BMxBN forces one register-staged tile shape for the process (tuning sweeps);
@@ -519,12 +543,12 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     return x ? bm * 1000 + std::atoi(x + 1) : 0;
   }();
   switch (a.kernel ? a.kernel : env_tile) {
-    case 64064: LaunchTile<T, 64, 64, kThreads, kSplit>(a, M, st); return 0;
-    case 128064: LaunchTile<T, 128, 64, kThreads, kSplit>(a, M, st); return 0;
-    case 64128: LaunchTile<T, 64, 128, kThreads, kSplit>(a, M, st); return 0;
-    case 128128: LaunchTile<T, 128, 128, kThreads, kSplit>(a, M, st); return 0;
-    case 128999: LaunchTile<T, 128, 128, 512, kSplit>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
-    case 64999: LaunchTile<T, 64, 64, 512, kSplit>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
+    case 64064: LaunchTile<T, 64, 64, kThreads, kSplit, kWPre>(a, M, st); return 0;
+    case 128064: LaunchTile<T, 128, 64, kThreads, kSplit, kWPre>(a, M, st); return 0;
+    case 64128: LaunchTile<T, 64, 128, kThreads, kSplit, kWPre>(a, M, st); return 0;
+    case 128128: LaunchTile<T, 128, 128, kThreads, kSplit, kWPre>(a, M, st); return 0;
+    case 128999: LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
+    case 64999: LaunchTile<T, 64, 64, 512, kSplit, kWPre>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
     case 256128:
     case 128256:
       // 8-wave tiles: the f32 epilogue staging would not fit the operand LDS
@@ -550,8 +574,8 @@ int Launch(const ConvArgs& a, hipStream_t st) {
   // Cout = 64 layers (r3 sweep, bf16x3, 14 shapes: 64x64 (4 waves) 1591 us, 128x128 8 waves 1391 us, this
   // rule ~1323 us; exact f32 2502 us)
   if constexpr (kSplit > 0) {
-    if (a.Cout <= 64) LaunchTile<T, 64, 64, kThreads, kSplit>(a, M, st);
-    else LaunchTile<T, 128, 128, 512, kSplit>(a, M, st);
+    if (a.Cout <= 64) LaunchTile<T, 64, 64, kThreads, kSplit, kWPre>(a, M, st);
+    else LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st);
     return 0;
   }
   if (a.Cout <= 64) {
@@ -575,11 +599,12 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
 }
 
 // dtype: 0 fp32 (exact f32 MFMAs), 1 fp16, 2 bf16, 3 fp32 on 2 bf16 planes (3 products), 4 fp32 on 3 bf16
-// planes (6 products) (C must be a multiple of one tile's K: 32 f32 / 64 f16/bf16 channels)
+// planes (6 products), 5 / 6 = 3 / 4 with the weights pre-split (w = [planes][Cout][R][S][C] bf16)
+// (C must be a multiple of one tile's K: 32 f32 / 64 f16/bf16 channels)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
-  const bool f32 = dtype == 0 || dtype == 3 || dtype == 4;
+  const bool f32 = dtype == 0 || dtype >= 3;
   const int bk = f32 ? Tile<float>::BK : Tile<_Float16>::BK;
-  return groups == 1 && C > 0 && C % bk == 0 && Cout > 0 && dtype >= 0 && dtype <= 4;
+  return groups == 1 && C > 0 && C % bk == 0 && Cout > 0 && dtype >= 0 && dtype <= 6;
 }
 
 int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
@@ -596,7 +621,7 @@ int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
   if (!ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return -1;
   if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;
   // buffer-resource offsets are 32-bit and the per-row tap mask holds 64 taps
-  const int64_t es = (dtype == 0 || dtype == 3 || dtype == 4) ? 4 : 2;
+  const int64_t es = (dtype == 0 || dtype >= 3) ? 4 : 2;
   if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * es >= (1ll << 31) ||
       static_cast<int64_t>(a.Cout) * a.R * a.S * a.C * es >= (1ll << 31) || a.R * a.S > 64)
     return -5;
@@ -605,7 +630,9 @@ int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
                  : dtype == 1 ? Launch<_Float16>(a, st)
                  : dtype == 2 ? Launch<__bf16>(a, st)
                  : dtype == 3 ? Launch<float, 2>(a, st)
-                              : Launch<float, 3>(a, st);
+                 : dtype == 4 ? Launch<float, 3>(a, st)
+                 : dtype == 5 ? Launch<float, 2, true>(a, st)
+                              : Launch<float, 3, true>(a, st);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

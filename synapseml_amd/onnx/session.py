@@ -746,8 +746,20 @@ def _fused_conv(rt, at, x):
             res = res.to(inp.dtype).contiguous(memory_format=torch.channels_last)
         dev = inp.device
         f32 = lambda t: None if t is None else t.to(dev, torch.float32).contiguous()  # noqa: E731
-        y = conv2d_nhwc(inp, w.permute(0, 2, 3, 1), w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]),
-                        dil, bias=f32(b), relu=2 if act == 1 else 0,
+        wp = w.permute(0, 2, 3, 1)
+        planes = None
+        if inp.dtype == torch.float32:
+            from ..ops.conv import f32_mode_default, split_weight
+
+            mode = rt.session.f32_conv_mode or f32_mode_default()
+            if mode != "exact":  # fp32 weights split into bf16 planes once per model (the kernel reads them)
+                cache = rt.session.__dict__.setdefault("_w_planes", {})
+                key = (w.data_ptr(), tuple(w.shape), mode)
+                planes = cache.get(key)
+                if planes is None:
+                    planes = cache[key] = split_weight(wp, mode)
+        y = conv2d_nhwc(inp, wp, w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]),
+                        dil, bias=f32(b), relu=2 if act == 1 else 0, w_planes=planes,
                         in_affine=(f32(pro[0]), f32(pro[1])) if pro is not None else None,
                         in_relu=bool(at.get("__pro_relu", 1)), res=res,
                         out_affine=(f32(post[0]), f32(post[1])) if post is not None else None,

@@ -35,6 +35,21 @@ def supported(cin: int, cout: int, groups: int, dtype: torch.dtype) -> bool:
     return dtype in _DT and bool(native.load("_nn").conv_supported(cin, cout, groups, _DT[dtype]))
 
 
+_PLANES = {"bf16x3": 2, "bf16x6": 3}
+
+
+def split_weight(wp: torch.Tensor, mode: str) -> torch.Tensor:
+    """packed fp32 weights [Cout, R, S, C] -> [planes, Cout, R, S, C] bf16 with w = sum of the planes up to the
+    last plane's rounding (each plane the RNE bf16 of what the earlier ones left: the kernel's own split)"""
+    r = wp.float()
+    planes = []
+    for _ in range(_PLANES[mode]):
+        h = r.to(torch.bfloat16)
+        planes.append(h)
+        r = r - h.float()
+    return torch.stack(planes).contiguous()
+
+
 def pack_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """[Cout, Cin, R, S] -> contiguous [Cout, R, S, Cin] in ``dtype``."""
     return w.permute(0, 2, 3, 1).contiguous().to(dtype)
@@ -58,14 +73,16 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
                 in_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, in_relu: bool = True,
                 res: Optional[torch.Tensor] = None,
                 out_affine: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, kernel: int = 0,
-                f32_mode: Optional[str] = None):
+                f32_mode: Optional[str] = None, w_planes: Optional[torch.Tensor] = None):
     """y = conv(pro(x), w) + bias, ReLU, + res; optionally also y2 = relu(y * out_scale + out_shift).
 
     ``relu``: False/0 none, True/1 before the residual add, 2 after it. ``pad``: (top, left) or
     (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp32/fp16/bf16 (C % 32 == 0 for fp32, % 64 otherwise). ``wp``: packed [Cout, R, S, C]
     (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2).
     ``kernel``: 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128, 128128, 256128, 128256).
-    ``f32_mode`` (fp32 inputs): "exact" | "bf16x3" | "bf16x6" (see F32_MODES; default SML_CONV_F32 or exact)."""
+    ``f32_mode`` (fp32 inputs): "exact" | "bf16x3" | "bf16x6" (see F32_MODES; default SML_CONV_F32 or bf16x6).
+    ``w_planes``: split_weight(wp, mode) computed once per weight; the split modes then read the planes instead
+    of splitting the weights in every block."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv2d_nhwc expects a channels_last input")
@@ -82,16 +99,23 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
         if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
             raise ValueError("bias / affine vectors must be contiguous fp32")
     geom = [B, H, W, C, cout, r, s, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], oh, ow]
+    mode = (f32_mode or f32_mode_default()) if x.dtype == torch.float32 else None
+    dt = F32_MODES[mode] if mode else _DT[x.dtype]
+    wptr = wp.data_ptr()
+    if w_planes is not None and mode in _PLANES:
+        if (w_planes.shape != (_PLANES[mode], cout, r, s, C) or w_planes.dtype != torch.bfloat16
+                or not w_planes.is_contiguous()):
+            raise ValueError(f"w_planes must be [{_PLANES[mode]}, {cout}, {r}, {s}, {C}] bf16 contiguous")
+        dt, wptr = dt + 2, w_planes.data_ptr()
     native.load("_nn").conv_mfma(
-        x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(in_affine[0] if in_affine else None),
+        x.data_ptr(), wptr, y.data_ptr(), _ptr(in_affine[0] if in_affine else None),
         _ptr(in_affine[1] if in_affine else None), _ptr(bias), _ptr(res), _ptr(out_affine[0] if out_affine else None),
-        _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu),
-        F32_MODES[f32_mode or f32_mode_default()] if x.dtype == torch.float32 else _DT[x.dtype],
+        _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu), dt,
         torch.cuda.current_stream(x.device).cuda_stream, int(kernel))
     return (y, y2) if out_affine is not None else y
 
 
-__all__ = ["supported", "pack_weight", "conv2d_nhwc", "out_hw", "F32_MODES"]
+__all__ = ["supported", "pack_weight", "split_weight", "conv2d_nhwc", "out_hw", "F32_MODES"]
 
 
 def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),

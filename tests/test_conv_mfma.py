@@ -243,3 +243,22 @@ def test_fp32_split_prologue_residual_dual_output():
         ry2 = torch.relu(ry * post[0].cpu().double().view(1, -1, 1, 1) + post[1].cpu().double().view(1, -1, 1, 1))
         torch.testing.assert_close(y.cpu().double(), ry, rtol=1e-5, atol=2e-5)
         torch.testing.assert_close(y2.cpu().double(), ry2, rtol=1e-5, atol=3e-5)
+
+
+@pytest.mark.parametrize("mode", ["bf16x3", "bf16x6"])
+def test_fp32_presplit_weight_planes_bitwise(mode):
+    """Weights split once on the host side (split_weight) give bitwise the in-kernel split's result (same
+    RNE bf16 planes, same products in the same order), with and without the prologue."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight, split_weight
+
+    torch.manual_seed(7)
+    B, C, H, W, Co = 2, 96, 13, 11, 160
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    pro = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1)
+    for k, kernel in ((3, 0), (1, 0), (3, 64064), (1, 128999)):
+        wp = pack_weight(torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5, torch.float32)
+        for ia in (None, pro):
+            a = conv2d_nhwc(x, wp, k, k, (1, 1), (k // 2, k // 2), in_affine=ia, f32_mode=mode, kernel=kernel)
+            b = conv2d_nhwc(x, wp, k, k, (1, 1), (k // 2, k // 2), in_affine=ia, f32_mode=mode, kernel=kernel,
+                            w_planes=split_weight(wp, mode))
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
