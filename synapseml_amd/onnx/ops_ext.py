@@ -35,6 +35,15 @@ import torch.nn.functional as Fn
 from . import proto as P
 from .ops import OPS, TORCH_OF, _ints, _to_np, op
 
+# ops whose outputs' shapes / control flow depend on tensor values (or that read values on the host): a graph
+# containing one is run eagerly, never captured into a hipGraph (a host sync inside a capture invalidates it)
+HOST_SYNC_OPS = {"Loop", "Scan", "If", "NonZero", "Compress", "Unique", "NonMaxSuppression", "SequenceAt",
+                 "SequenceInsert", "SequenceErase", "SplitToSequence", "ReverseSequence", "CenterCropPad",
+                 "DynamicQuantizeLinear", "MatMulInteger", "ConvInteger", "QLinearMatMul", "QLinearConv",
+                 "LSTM", "GRU", "RNN", "Bernoulli", "Multinomial", "RandomNormal", "RandomUniform",
+                 "RandomNormalLike", "RandomUniformLike", "StringNormalizer", "StringConcat", "StringSplit",
+                 "RegexFullMatch", "CategoryMapper", "DictVectorizer", "FeatureVectorizer"}
+
 
 def _t(v, device=None, dtype=None) -> torch.Tensor:
     if isinstance(v, torch.Tensor):
@@ -276,6 +285,7 @@ def _rnn_common(at, x, gates: int):
     B = _t(x[3], dev, dt) if len(x) > 3 and x[3] is not None else torch.zeros(nd, 2 * gates * H, device=dev, dtype=dt)
     T, N = X.shape[0], X.shape[1]
     lens = (_to_np(x[4]).astype(np.int64) if len(x) > 4 and x[4] is not None else np.full(N, T, np.int64))
+    # (sequence_lens is read on the host once per call: the op sits in HOST_SYNC_OPS when it is an input)
     direction = at.get("direction", "forward")
     direction = direction.decode() if isinstance(direction, bytes) else direction
     if nd == 2 and direction != "bidirectional":
@@ -343,9 +353,7 @@ def _run_lstm(step, XW, nd, direction, T, N, H, lens, init, dev, dt):
         st = [s[d].clone() for s in init]
         for stp in range(T):
             tt = (lens_t - 1 - stp) if rev else torch.full((N,), stp, device=dev, dtype=torch.long)
-            valid = (tt >= 0) & (tt < lens_t)
-            if not bool(valid.any()):
-                continue
+            valid = (tt >= 0) & (tt < lens_t)  # all-false steps are masked no-ops: no host sync in the loop
             ti = tt.clamp(0, T - 1)
             new = step(d, proj[d][ti, ar], st)
             m = valid.unsqueeze(1)

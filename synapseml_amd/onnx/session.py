@@ -608,6 +608,8 @@ class InferenceSession:
     def _graphable(self, feeds) -> bool:
         if any(vi.kind != "tensor" or vi.elem_type == P.STRING_T for vi in self.inputs + self.outputs):
             return False
+        if any(n.op_type in ops_ext.HOST_SYNC_OPS for n in self.nodes):
+            return False  # value-dependent shapes / control flow: eager (a sync inside a capture breaks it)
         return all(not (isinstance(v, np.ndarray) and v.dtype == object) for v in feeds.values())
 
     def _run_graph(self, feeds, fetch):
