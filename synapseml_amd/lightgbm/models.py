@@ -28,6 +28,11 @@ def _features_matrix(df: DataFrame, col: str) -> np.ndarray:
 class _LightGBMModelBase(Model, LightGBMModelParams):
     """Shared model methods (LightGBMModelMethods.scala:13-133)."""
 
+    def setPredictDisableShapeCheck(self, value=None):  # noqa: N802
+        """reference mixin.py:83-95: a missing / falsy value means False"""
+        self.set("predictDisableShapeCheck", bool(value))
+        return self
+
     def getModel(self) -> LightGBMBooster:  # noqa: N802
         return self.getLightGBMBooster()
 

@@ -36,6 +36,17 @@ def _vw():
     return native.load("_vw")
 
 
+def _initial_model_bytes(model):
+    """VowpalWabbitPythonBase.setInitialModel (reference vw/.../VowpalWabbitPythonBase.py:22-26) takes a fitted
+    model; raw model bytes are accepted too"""
+    if model is None or isinstance(model, (bytes, bytearray)):
+        return None if model is None else bytes(model)
+    get = getattr(model, "getModel", None)
+    if get is None:
+        raise TypeError(f"setInitialModel expects a fitted VowpalWabbit model or model bytes, got {type(model).__name__}")
+    return bytes(get())
+
+
 class VowpalWabbitBaseParams(HasFeaturesCol):
     passThroughArgs = Param("VW command line arguments passed", "", T.toString)
     additionalFeatures = Param("Additional feature columns", [], T.toListString)
@@ -50,6 +61,10 @@ class VowpalWabbitBaseParams(HasFeaturesCol):
     initialModel = Param("Initial model to start from", None, complex=True)
     numPasses = Param("Number of passes over the data", 1, T.toInt)
     numSyncsPerPass = Param("Number of times weights should be synchronized within each pass", 0, T.toInt)
+
+    def setInitialModel(self, model):  # noqa: N802
+        self.set("initialModel", _initial_model_bytes(model))
+        return self
     useBarrierExecutionMode = Param("Use barrier execution mode, on by default.", True, T.toBoolean)
     splitCol = Param("The column to split on for inter-pass sync", None, T.toString)
     splitColValues = Param("Sorted values to use to select each split to train on", None)
@@ -567,6 +582,10 @@ class VowpalWabbitGeneric(Estimator, HasPredictionCol):
     inputCol = Param("Column with examples in VW text format", "value", T.toString)
     numPasses = Param("Number of passes over the data", 1, T.toInt)
     initialModel = Param("Initial model to start from", None, complex=True)
+
+    def setInitialModel(self, model):  # noqa: N802
+        self.set("initialModel", _initial_model_bytes(model))
+        return self
 
     def _fit(self, df: DataFrame):
         args = self.getPassThroughArgs() + (f" --passes {self.getNumPasses()}" if self.getNumPasses() > 1 else "")
