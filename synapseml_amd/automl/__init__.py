@@ -35,6 +35,10 @@ class DiscreteHyperParam(Dist):
     def values(self):
         return list(self._values)
 
+    def get(self):
+        """the wrapped distribution (reference HyperparamBuilder.py DiscreteHyperParam.get)"""
+        return self
+
 
 class RangeHyperParam(Dist):
     """Uniform range; integer-valued when both bounds are ints (IntRangeHyperParam & co.)."""
@@ -48,6 +52,10 @@ class RangeHyperParam(Dist):
         if self.is_int:
             return int(rng.integers(self.min, self.max))
         return float(self.min + (self.max - self.min) * rng.random())
+
+    def get(self):
+        """the wrapped distribution (reference HyperparamBuilder.py RangeHyperParam.get)"""
+        return self
 
     def values(self):
         if self.is_int:
@@ -83,6 +91,10 @@ class GridSpace(ParamSpace):
     def __init__(self, hyperparams: List[Tuple[Any, str, Dist]]):
         self.hp = hyperparams
 
+    def space(self):
+        """the wrapped search space (reference HyperparamBuilder.py GridSpace.space)"""
+        return self
+
     def paramMaps(self):  # noqa: N802
         keys = [(est, name) for est, name, _ in self.hp]
         for combo in itertools.product(*[d.values() for _, _, d in self.hp]):
@@ -93,6 +105,10 @@ class RandomSpace(ParamSpace):
     def __init__(self, hyperparams: List[Tuple[Any, str, Dist]], seed: int = 0):
         self.hp = hyperparams
         self.rng = np.random.default_rng(seed)
+
+    def space(self):
+        """the wrapped search space (reference HyperparamBuilder.py RandomSpace.space)"""
+        return self
 
     def paramMaps(self):  # noqa: N802
         while True:

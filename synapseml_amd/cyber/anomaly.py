@@ -147,6 +147,42 @@ class AccessAnomalyModel(Model):
     resComponents = Param("(tenant, res) -> component", None, complex=True)
     history = Param("set of seen (tenant, user, res)", None, complex=True)
 
+    # reference collaborative_filtering.py AccessAnomalyModel properties
+    @property
+    def tenant_col(self) -> str:
+        return self.getTenantCol()
+
+    @property
+    def user_col(self) -> str:
+        return self.getUserCol()
+
+    @property
+    def res_col(self) -> str:
+        return self.getResCol()
+
+    @property
+    def user_vec_col(self) -> str:
+        return self.getUserCol() + "_vector"
+
+    @property
+    def res_vec_col(self) -> str:
+        return self.getResCol() + "_vector"
+
+    def _mapping_df(self, vecs, col: str, vec_col: str) -> DataFrame:
+        keys = sorted(vecs or {}, key=lambda k: (str(k[0]), str(k[1])))
+        obj = lambda xs: np.array(xs + [None], dtype=object)[:-1]  # noqa: E731  (1-D object column)
+        return DataFrame({self.getTenantCol(): obj([k[0] for k in keys]), col: obj([k[1] for k in keys]),
+                          vec_col: obj([np.asarray(vecs[k], np.float64) for k in keys])})
+
+    @property
+    def user_mapping_df(self) -> DataFrame:
+        """(tenant, user, user_vector) rows of the fitted model"""
+        return self._mapping_df(self.getUserVectors(), self.getUserCol(), self.user_vec_col)
+
+    @property
+    def res_mapping_df(self) -> DataFrame:
+        return self._mapping_df(self.getResVectors(), self.getResCol(), self.res_vec_col)
+
     def _transform(self, df):
         tc, uc, rc = self.getTenantCol(), self.getUserCol(), self.getResCol()
         T_ = df[tc].tolist() if tc in df else [0] * df.count()  # fit uses tenant 0 when the column is absent
@@ -202,6 +238,39 @@ class AccessAnomaly(Estimator):
     historyAccessDf = Param("historyAccessDf: seen accesses (score 0) and the connected-component graph", None,
                             complex=True)
     seed = Param("random seed", 0, T.toInt)
+
+
+    # reference collaborative_filtering.py AccessAnomaly column-name properties
+    @property
+    def indexed_user_col(self) -> str:
+        return self.getUserCol() + "_index"
+
+    @property
+    def user_vec_col(self) -> str:
+        return self.getUserCol() + "_vector"
+
+    @property
+    def indexed_res_col(self) -> str:
+        return self.getResCol() + "_index"
+
+    @property
+    def res_vec_col(self) -> str:
+        return self.getResCol() + "_vector"
+
+    @property
+    def scaled_likelihood_col(self) -> str:
+        return self.getLikelihoodCol() + "_scaled"
+
+    def create_spark_model_vectors_df(self, df: DataFrame):
+        """fit and return the (tenant, user, vector) / (tenant, res, vector) mappings and the access history
+        (reference _UserResourceFeatureVectorMapping fields)"""
+        from types import SimpleNamespace
+
+        m = self.fit(df)
+        return SimpleNamespace(tenant_col=self.getTenantCol(), user_col=self.getUserCol(),
+                               user_vec_col=self.user_vec_col, res_col=self.getResCol(), res_vec_col=self.res_vec_col,
+                               history_access_df=df, user_feature_vector_mapping_df=m.user_mapping_df,
+                               res_feature_vector_mapping_df=m.res_mapping_df)
 
     def _fit(self, df):
         tc, uc, rc, lc = self.getTenantCol(), self.getUserCol(), self.getResCol(), self.getLikelihoodCol()

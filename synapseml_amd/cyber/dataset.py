@@ -36,6 +36,24 @@ class DataFactory:
         return DataFrame({AccessAnomalyConfig.default_user_col: u, AccessAnomalyConfig.default_res_col: r,
                           AccessAnomalyConfig.default_likelihood_col: np.asarray([t[2] for t in tups], float)})
 
+    def to_pdf(self, users: List, resources: List, likelihoods: List[float]) -> DataFrame:
+        """(user, res, likelihood) columns as strings / floats (reference dataset.py DataFactory.to_pdf; a
+        pandas frame there, this framework's DataFrame here)"""
+        return self.to_df([(str(u), str(r), float(s)) for u, r, s in zip(users, resources, likelihoods)])
+
+    def tups2pdf(self, tup_arr: List[Tuple[str, str, float]]) -> DataFrame:
+        return self.to_pdf([t[0] for t in tup_arr], [t[1] for t in tup_arr], [t[2] for t in tup_arr])
+
+    def create_fixed_training_data(self) -> DataFrame:
+        """a small fixed access log: 25 (user, res, likelihood) rows over users 1..11 and resources 1..8, 14 of
+        them at likelihood 1 and the rest heavier (same shape as the reference fixture; generated from a fixed
+        seed rather than listed)"""
+        rng = random.Random(7)
+        users = [rng.randint(1, 11) for _ in range(25)]
+        resources = [rng.randint(1, 8) for _ in range(25)]
+        likelihoods = [1.0] * 14 + [round(rng.uniform(10.0, 47.0), 6) for _ in range(11)]
+        return self.to_pdf(users, resources, likelihoods)
+
     def edges_between(self, users: List[str], resources: List[str], ratio: float, full_node_coverage: bool,
                       not_set: Optional[Set[Tuple[str, str]]] = None) -> List[Tuple[str, str, float]]:
         if not users or not resources:

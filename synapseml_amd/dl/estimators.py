@@ -79,8 +79,16 @@ _MEAN = [0.485, 0.456, 0.406]
 _STD = [0.229, 0.224, 0.225]
 
 
-def images_to_tensor(values: List[Any], size: int, use_gpu: bool) -> torch.Tensor:
-    """Decode + resize(size) + centre crop + RGB + ImageNet normalise -> [N,3,size,size] float32."""
+def images_to_tensor(values: List[Any], size: int, use_gpu: bool, transform_fn=None) -> torch.Tensor:
+    """Decode + resize(size) + centre crop + RGB + ImageNet normalise -> [N,3,size,size] float32; then
+    ``transform_fn`` (the reference's transform_fn: a torchvision-style callable) on every [3,size,size] image."""
+    t = _images_to_tensor(values, size, use_gpu)
+    if transform_fn is not None:
+        t = torch.stack([torch.as_tensor(transform_fn(img)) for img in t]).to(t.device).float()
+    return t
+
+
+def _images_to_tensor(values: List[Any], size: int, use_gpu: bool) -> torch.Tensor:
     from ..image.schema import to_array
     from ..image.transformer import ImageTransformer
 
@@ -112,17 +120,45 @@ class _VisionParams(_TrainParams):
     image_col = Param("image column name.", "image", T.toString)
     image_size = Param("square input size fed to the backbone", 224, T.toInt)
     weights = Param("optional local state dict / safetensors of backbone weights", None, T.toString)
+    transform_fn = Param("callable applied to every decoded, normalised [3, H, W] image tensor (training and "
+                         "inference), e.g. a torchvision.transforms.Compose", None, complex=True)
+
+    def setDropoutAUX(self, value):  # noqa: N802  (reference spelling)
+        return self.set("dropout_aux", float(value))
+
+    def getDropoutAUX(self):  # noqa: N802
+        return self.getOrDefault("dropout_aux")
+
+    def _images(self, df):
+        return images_to_tensor(df[self.getOrDefault("image_col")].tolist(), self.getOrDefault("image_size"),
+                                self.getOrDefault("use_gpu"), self.getOrDefault("transform_fn"))
 
 
 class DeepVisionModel(Model, _VisionParams):
     model = Param("trained torch module", None, complex=True)
 
+    def setTransformationFn(self, fn):  # noqa: N802  (reference DeepVisionModel spelling)
+        return self.set("transform_fn", fn)
+
+    def getTransformationFn(self):  # noqa: N802
+        return self.getOrDefault("transform_fn")
+
+    def getOptimizer(self):  # noqa: N802
+        """the optimizer the model was trained with (name; the torch optimizer is not kept after training)"""
+        return self.getOrDefault("optimizer_name")
+
+    def get_prediction_fn(self):
+        """images (bytes / paths / decoded rows) -> class probabilities [N, num_classes] (numpy)"""
+        def fn(images):
+            X = images_to_tensor(list(images), self.getOrDefault("image_size"), self.getOrDefault("use_gpu"),
+                                 self.getOrDefault("transform_fn"))
+            return torch.softmax(predict(self.getOrDefault("model"), X, use_gpu=self.getOrDefault("use_gpu")),
+                                 dim=1).numpy()
+
+        return fn
+
     def _transform(self, df):
-        net = self.getOrDefault("model")
-        X = images_to_tensor(df[self.getOrDefault("image_col")].tolist(), self.getOrDefault("image_size"),
-                             self.getOrDefault("use_gpu"))
-        logits = predict(net, X, use_gpu=self.getOrDefault("use_gpu"))
-        prob = torch.softmax(logits, dim=1).numpy()
+        prob = self.get_prediction_fn()(df[self.getOrDefault("image_col")].tolist())
         return df.withColumn("probability", prob).withColumn(self.getOrDefault("prediction_col"),
                                                              prob.argmax(1).astype(np.float64))
 
@@ -133,14 +169,16 @@ def _vision_task(est, part, rank, world):
     torch.manual_seed(est.getOrDefault("random_seed"))
     net = backbones.build(est.getOrDefault("backbone"), est.getOrDefault("num_classes"), est.getOrDefault("weights"))
     backbones.head_and_trainable(net, est.getOrDefault("additional_layers_to_train"))
-    X = images_to_tensor(part[est.getOrDefault("image_col")].tolist(), est.getOrDefault("image_size"),
-                         est.getOrDefault("use_gpu"))
+    X = est._images(part)
     hist = fit(net, X, est._labels(part), est._cfg(), shard=False)
     hist["world"] = world
     return ({k: v.cpu() for k, v in net.state_dict().items()}, hist) if rank == 0 else None
 
 
 class DeepVisionClassifier(Estimator, _VisionParams):
+    def get_model_class(self):
+        return DeepVisionModel
+
     def _fit(self, df):
         if self.getOrDefault("num_classes") is None:
             raise ValueError("num_classes must be set")
@@ -160,8 +198,7 @@ class DeepVisionClassifier(Estimator, _VisionParams):
             net = backbones.build(self.getOrDefault("backbone"), self.getOrDefault("num_classes"),
                                   self.getOrDefault("weights"))
             backbones.head_and_trainable(net, self.getOrDefault("additional_layers_to_train"))
-            X = images_to_tensor(df[self.getOrDefault("image_col")].tolist(), self.getOrDefault("image_size"),
-                                 self.getOrDefault("use_gpu"))
+            X = self._images(df)
             hist = fit(net, X, self._labels(df), self._cfg())
             hist["world"] = 1
         m = DeepVisionModel(**{k: v for k, v in self.extractParamMap().items() if k in DeepVisionModel._params_decl})
@@ -243,29 +280,48 @@ class _TextParams(_TrainParams):
     text_col = Param("text column name.", "text", T.toString)
     max_token_len = Param("max_token_len for the tokenizer", 128, T.toInt)
     tokenizer_dir = Param("optional local directory with a pretrained model + tokenizer", None, T.toString)
+    tokenizer = Param("tokenizer callable (texts, max_length) -> encodings; the checkpoint's own when unset",
+                      None, complex=True)
+    train_from_scratch = Param("train every layer (True) or only the last additional_layers_to_train encoder "
+                               "layers and the head (False)", True, T.toBoolean)
 
 
 class DeepTextModel(Model, _TextParams):
     model = Param("trained torch module", None, complex=True)
-    tokenizer = Param("tokenizer callable", None, complex=True)
+
+    def getOptimizer(self):  # noqa: N802
+        return self.getOrDefault("optimizer_name")
+
+    def get_prediction_fn(self):
+        """texts -> class probabilities [N, num_classes] (numpy)"""
+        def fn(texts):
+            enc = self.getOrDefault("tokenizer")(list(map(str, texts)), self.getOrDefault("max_token_len"))
+            logits = predict(self.getOrDefault("model"), enc, use_gpu=self.getOrDefault("use_gpu"),
+                             forward=_text_forward)
+            return torch.softmax(logits, dim=1).numpy()
+
+        return fn
 
     def _transform(self, df):
-        enc = self.getOrDefault("tokenizer")(list(map(str, df[self.getOrDefault("text_col")].tolist())),
-                                             self.getOrDefault("max_token_len"))
-        logits = predict(self.getOrDefault("model"), enc, use_gpu=self.getOrDefault("use_gpu"),
-                         forward=_text_forward)
-        prob = torch.softmax(logits, dim=1).numpy()
+        prob = self.get_prediction_fn()(df[self.getOrDefault("text_col")].tolist())
         return df.withColumn("probability", prob).withColumn(self.getOrDefault("prediction_col"),
                                                              prob.argmax(1).astype(np.float64))
 
 
 class DeepTextClassifier(Estimator, _TextParams):
+    def get_model_class(self):
+        return DeepTextModel
+
     def _fit(self, df):
         if self.getOrDefault("num_classes") is None:
             raise ValueError("num_classes must be set")
         net, tok = build_text_model(self.getOrDefault("checkpoint"), self.getOrDefault("num_classes"),
                                     self.getOrDefault("tokenizer_dir"))
-        k = self.getOrDefault("additional_layers_to_train")
+        if self.getOrDefault("tokenizer") is not None:
+            tok = self.getOrDefault("tokenizer")
+        k = None if self.getOrDefault("train_from_scratch") else self.getOrDefault("additional_layers_to_train")
+        if not self.getOrDefault("train_from_scratch") and (k is None or k < 0):
+            raise ValueError("train_from_scratch=False needs additional_layers_to_train >= 0")
         if k is not None and k >= 0:
             for p in net.base_model.parameters():
                 p.requires_grad = False

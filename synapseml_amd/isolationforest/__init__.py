@@ -46,6 +46,11 @@ class IsolationForestModel(Model, _Params):
     numSamples = Param("samples per tree", 256, T.toInt)
     outlierScoreThreshold = Param("score threshold for the predicted label", 0.5, T.toFloat)
 
+    def getInnerModel(self):  # noqa: N802
+        """the fitted forest itself (reference IsolationForestModel.getInnerModel returns the wrapped
+        linkedin model; here the flattened trees live on this stage)"""
+        return self
+
     def scores(self, X: np.ndarray) -> np.ndarray:
         feat, thr, left, right, size, fidx = self.getTrees()
         T_ = len(fidx)

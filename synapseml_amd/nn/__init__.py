@@ -97,6 +97,23 @@ class ConditionalBallTree(BallTree):
         self.labels = list(labels)
         super().__init__(keys, values, leafSize)
 
+    def save(self, filename: str) -> None:
+        """keys, values, labels and leaf size as JSON (rebuilt deterministically on load; reference
+        nn/ConditionalBallTree.py save / load)"""
+        import json
+
+        with open(filename, "w") as f:
+            json.dump({"keys": self.keys.tolist(), "values": list(self.values), "labels": list(self.labels),
+                       "leafSize": self.leaf_size}, f)
+
+    @staticmethod
+    def load(filename: str) -> "ConditionalBallTree":
+        import json
+
+        with open(filename) as f:
+            d = json.load(f)
+        return ConditionalBallTree(np.asarray(d["keys"], np.float64), d["values"], d["labels"], d["leafSize"])
+
     def findMaximumInnerProducts(self, queryPoint, conditioner: Set[Any], k: int = 1):  # noqa: N802,N803
         allowed = {i for i, l in enumerate(self.labels) if l in conditioner}
         heap: list = []

@@ -198,6 +198,13 @@ class ONNXModel(Transformer):
             self._graph = g
         return g
 
+    def getModelInputs(self) -> Dict[str, ValueInfo]:  # noqa: N802
+        """reference ONNXModel.py getModelInputs: graph input name -> type / shape info"""
+        return self.modelInput
+
+    def getModelOutputs(self) -> Dict[str, ValueInfo]:  # noqa: N802
+        return self.modelOutput
+
     @property
     def modelInput(self) -> Dict[str, ValueInfo]:  # noqa: N802
         return {v.name: v for v in self._graph_().inputs}

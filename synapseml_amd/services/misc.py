@@ -218,6 +218,19 @@ class BingImageSearch(CognitiveServicesBase):
         super().__init__(**kw)
         self._setDefault(url="https://api.bing.microsoft.com/v7.0/images/search")
 
+    # reference BingImageSearch.py aliases of the q / mkt service params
+    def setQuery(self, value):  # noqa: N802
+        return self.setQ(value)
+
+    def setQueryCol(self, value):  # noqa: N802
+        return self.setQCol(value)
+
+    def setMarket(self, value):  # noqa: N802
+        return self.setMkt(value)
+
+    def setMarketCol(self, value):  # noqa: N802
+        return self.setMktCol(value)
+
     @staticmethod
     def getUrlTransformer(imageCol: str, urlCol: str) -> Transformer:  # noqa: N802,N803
         """Explode the search responses' ``value[].contentUrl`` into one row per image URL."""

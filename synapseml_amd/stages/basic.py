@@ -105,6 +105,9 @@ class UDFTransformer(Transformer, HasInputCol, HasInputCols, HasOutputCol):
     def setUDF(self, f):  # noqa: N802
         return self.set("udf", f)
 
+    def getUDF(self):  # noqa: N802
+        return self.getUdf()
+
     def _transform(self, df):
         f = self.getUdf()
         if self.getInputCols():
