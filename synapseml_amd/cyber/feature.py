@@ -123,6 +123,14 @@ class _ScalerModel(Model, _Cols):
     def per_group_stats(self):
         return self.getStats()
 
+    @property
+    def use_pandas(self) -> bool:
+        return False  # columnar numpy transform (the reference's pandas-UDF switch)
+
+    def is_partitioned(self) -> bool:
+        """statistics are kept per partition-key group (reference scalers.py is_partitioned)"""
+        return self.getPartitionKey() is not None
+
     def _transform(self, df):
         x = np.asarray(df[self.getInputCol()], dtype=np.float64)
         ks = _keys(df, self.getPartitionKey())
@@ -138,6 +146,10 @@ class _ScalerModel(Model, _Cols):
 
 
 class _ScalerEstimator(Estimator, _Cols):
+    @property
+    def use_pandas(self) -> bool:
+        return False
+
     def _stats(self, x: np.ndarray) -> Dict[str, float]:
         raise NotImplementedError
 
@@ -222,3 +234,8 @@ class LinearScalarScaler(_ScalerEstimator):
 
 __all__ = ["IdIndexer", "IdIndexerModel", "MultiIndexer", "MultiIndexerModel", "StandardScalarScaler",
            "StandardScalarScalerModel", "LinearScalarScaler", "LinearScalarScalerModel"]
+
+
+# reference cyber/feature/scalers.py names of the per-partition scaler bases
+PerPartitionScalarScalerEstimator = _ScalerEstimator
+PerPartitionScalarScalerModel = _ScalerModel

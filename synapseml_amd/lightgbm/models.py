@@ -267,3 +267,7 @@ class LightGBMRanker(LightGBMBase, HasGroupCol):
         m.set("startIteration", 0)
         m.parent = self
         return m
+
+
+# reference lightgbm/mixin.py: the model-method mixin of the three LightGBM model classes
+LightGBMModelMixin = _LightGBMModelBase

@@ -333,6 +333,10 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
 
 
 class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
+    def getNativeModel(self) -> bytes:  # noqa: N802
+        """the binary VW model (reference VowpalWabbitPythonBase.py getNativeModel)"""
+        return bytes(self.getModel())
+
     model = Param("The VW model bytes", None, complex=True)
     performanceStatistics = Param("Training statistics", None, complex=True)
     testArgs = Param("Additional arguments passed to VW at test time", "", T.toString)
@@ -643,3 +647,8 @@ class VowpalWabbitProgressive(Transformer, VowpalWabbitBaseParams, HasLabelCol, 
             preds, _ = vw.learn_batch(blocks, np.asarray(part[self.getLabelCol()], np.float32), None, None, None, True)
             out.append(np.asarray(preds, np.float64))
         return df.withColumn(self.getPredictionCol(), np.concatenate(out) if out else np.zeros(0))
+
+
+# reference vw/VowpalWabbitPythonBase.py: the Python-side base mixins
+VowpalWabbitPythonBase = VowpalWabbitBase
+VowpalWabbitPythonBaseModel = VowpalWabbitModelBase

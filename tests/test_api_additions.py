@@ -77,3 +77,31 @@ def test_text_train_from_scratch_requires_layers():
         DeepTextClassifier(checkpoint="tiny-bert", num_classes=2, train_from_scratch=False,
                            additional_layers_to_train=-1, use_gpu=False).fit(df)
     assert DeepTextClassifier().get_model_class().__name__ == "DeepTextModel"
+
+
+def test_synapseml_logger_decorators():
+    from synapseml_amd.core.logging import SynapseMLLogger, add_event_sink, remove_event_sink
+
+    seen = []
+    add_event_sink(seen.append)
+    try:
+        class Thing(SynapseMLLogger):
+            @SynapseMLLogger.log_transform()
+            def transform(self, df):
+                return df
+
+            @SynapseMLLogger.log_fit()
+            def fit(self, df):
+                raise ValueError("bad sig=" + "a" * 50 + "%3d")
+
+        t = Thing(uid="thing_1")
+        t.log_class("tests")
+        t.transform(DataFrame({"a": np.arange(3), "b": np.arange(3)}))
+        with pytest.raises(ValueError):
+            t.fit(None)
+    finally:
+        remove_event_sink(seen.append)
+    methods = [p.get("method") for p in seen]
+    assert methods == ["constructor", "transform", "fit"]
+    assert seen[1]["dfInfo"]["input"]["numCols"] == 2 and "executionSeconds" in seen[1]
+    assert seen[2]["errorType"] == "ValueError" and "sig=####" in seen[2]["errorMessage"]
