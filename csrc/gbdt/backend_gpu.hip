@@ -49,8 +49,7 @@ namespace {
 
 constexpr int kBinsPerFeature = 256;
 constexpr int kFeatPerGroup = 32;          // 8 dwords of bins per block
-constexpr int kHistStride = 257;           // padded LDS row (bank spread)
-constexpr int kMaxHistBlocks = 256;        // = resident capacity: one 1024-thread, 131.6 KB-LDS block per CU
+constexpr int kMaxHistBlocks = 256;        // = resident capacity: one 1024-thread, 128 KB-LDS block per CU
 constexpr int kMinRowsPerHistBlockDefault = 1024;  // A/B: 1024 ~ 512 < 2048 < 4096
 __constant__ int c_min_rows_per_hist_block = kMinRowsPerHistBlockDefault;
 __constant__ int c_max_hist_blocks = kMaxHistBlocks;
@@ -820,7 +819,7 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // several gathers in flight (the loop is latency-bound otherwise).
 //
 // Accumulation is 64-bit fixed point with g and h in separate LDS words: two
-// ds_add_u64 per (row, feature) into 2 x 32 x 257 words (131.6 KB, one
+// ds_add_u64 per (row, feature) into 2 x 256 x 32 words (128 KB, one
 // 1024-thread block per CU). Both scales are powers of two chosen per
 // histogram from the leaf's row count and the tree's max |g| / max h so that
 // the sum over ALL of the leaf's rows stays below 2^62 in magnitude: every
@@ -837,7 +836,7 @@ __global__ void gather_bag_kernel(const int32_t* __restrict__ rows, int32_t n, c
 // ms/iter; more rows in flight only queue more LDS atomics)
 constexpr int kHistUnroll = 2;
 constexpr int kHistBlockThreads = 1024;
-constexpr int kHistWords = kFeatPerGroup * kHistStride;  // per plane (g or h)
+constexpr int kHistWords = kFeatPerGroup * kBinsPerFeature;  // per plane (g or h), bin-major
 
 __device__ __forceinline__ int HistBlocks(int count) {
   return max(1, min(c_max_hist_blocks, ceil_div_i(count, c_min_rows_per_hist_block)));
@@ -859,10 +858,6 @@ __device__ __forceinline__ HScale HistScale(int count, const float* ghmax) {
   return HScale{ldexp(1.0, eg), ldexp(1.0, eh), ldexp(1.0, -eg), ldexp(1.0, -eh)};
 }
 
-__device__ __forceinline__ uint32_t word_of(const uint4& b, int j) {
-  return j < 4 ? b.x : (j < 8 ? b.y : (j < 12 ? b.z : b.w));
-}
-
 struct QGH {
   unsigned long long g, h;  // g two's complement (wraps exactly in unsigned adds)
 };
@@ -874,22 +869,38 @@ __device__ __forceinline__ QGH QuantGH(float2 v, const HScale& s) {
   return QGH{static_cast<unsigned long long>(gq), hq};
 }
 
-__device__ __forceinline__ void hist_accumulate(unsigned long long* shg, unsigned long long* shh, const uint4& b0,
-                                                const uint4& b1, const QGH& q, int Fg) {
+// LDS histogram layout: bin-major, sh[b * kFPG + f] (kFPG = 16 or 32 feature slots per bin). A 64-bit LDS
+// atomic is serviced in 4 groups of 16 contiguous lanes over 32 banks (an 8-B slot's bank pair = slot mod 16),
+// so slot mod 16 = f mod 16 whatever the bin. Lane l walks its row's S features rotated by l & 15 (step j:
+// feature (j + (l & 15)) mod S; 16 consecutive integers have distinct residues mod 16), so the 16 lanes of
+// a group always add into 16 different bank pairs: conflict-free. (The round-1/2 [f][257] layout put the
+// random bins of one feature on random bank pairs: ~3.5-way conflicts, 65 % of the LDS cycles in the PMC
+// pass of profiles/r2_pmc.) The row is rotated once in registers (two dword-rotation selects + alignbyte),
+// so every step extracts a fixed byte. Slots f >= Fg of a partial group collect the row's padding bytes
+// (always < 256) and are never read.
+template <int S, int kFPG>
+__device__ __forceinline__ void hist_accumulate_rot(unsigned long long* shg, unsigned long long* shh,
+                                                    const uint4& b0, const uint4& b1, const QGH& q, int rot) {
+  static_assert(S == 16 || S == 32, "16 or 32 features per rotated row");
+  static_assert(kFPG % 16 == 0 && S <= kFPG, "slots per bin");
+  constexpr int NW = S / 4;
+  uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  const int qd = rot >> 2, rb = rot & 3;
+  uint32_t v[NW], u[NW], r[NW];
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (j < Fg) {
-      const int i = j * kHistStride + ((word_of(b0, j) >> (8 * (j & 3))) & 255u);
-      atomicAdd(&shg[i], q.g);
-      atomicAdd(&shh[i], q.h);
-    }
+  for (int k = 0; k < NW; ++k) v[k] = (qd & 1) ? w[(k + 1) % NW] : w[k];
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (j + 16 < Fg) {
-      const int i = (j + 16) * kHistStride + ((word_of(b1, j) >> (8 * (j & 3))) & 255u);
-      atomicAdd(&shg[i], q.g);
-      atomicAdd(&shh[i], q.h);
-    }
+  for (int k = 0; k < NW; ++k) u[k] = (qd & 2) ? v[(k + 2) % NW] : v[k];
+  // r byte j = row byte (j + rot) mod S
+#pragma unroll
+  for (int k = 0; k < NW; ++k) r[k] = __builtin_amdgcn_alignbyte(u[(k + 1) % NW], u[k], static_cast<uint32_t>(rb));
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int f = (j + rot) & (S - 1);
+    const int i = static_cast<int>((r[j >> 2] >> (8 * (j & 3))) & 255u) * kFPG + f;
+    atomicAdd(&shg[i], q.g);
+    atomicAdd(&shh[i], q.h);
+  }
 }
 
 // one slab element: (g, h) int64 pair; write-through (agent-scope relaxed stores = sc1) when c_slab_wt
@@ -903,7 +914,19 @@ __device__ __forceinline__ void SlabStore(ulonglong2* p, unsigned long long g, u
   }
 }
 
-// kFPG features per block (blockIdx.y = feature group): 32 = one 131.6 KB LDS histogram per CU; 16 halves
+// Block slab, bin-major over ALL features: element b * F + f (the LDS order of each group, so the copy
+// reads LDS conflict-free and writes runs of Fg contiguous elements); hist_reduce_kernel transposes to the
+// [f][b] histogram while summing.
+template <int kFPG, int kThr>
+__device__ __forceinline__ void SlabWrite(ulonglong2* out, const unsigned long long* shg, const unsigned long long* shh,
+                                          int F, int f0, int Fg, int tid) {
+  for (int i = tid; i < kFPG * kBinsPerFeature; i += kThr) {
+    const int b = i / kFPG, fl = i % kFPG;
+    if (fl < Fg) SlabStore(out + b * F + f0 + fl, shg[i], shh[i]);
+  }
+}
+
+// kFPG features per block (blockIdx.y = feature group): 32 = one 128 KB LDS histogram per CU; 16 halves
 // the LDS (two blocks per CU) at the price of reading every row's perm / g / h once per group
 template <int kUnroll, int kFPG>
 __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
@@ -916,7 +939,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
   const int count = L.count;
   const int nb_active = HistBlocks(count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  constexpr int kWords = kFPG * kHistStride;
+  constexpr int kWords = kFPG * kBinsPerFeature;
   __shared__ unsigned long long shg[kWords], shh[kWords];
   const int tid = threadIdx.x;
   for (int i = tid; i < kWords; i += kHistBlockThreads) { shg[i] = 0ull; shh[i] = 0ull; }
@@ -951,16 +974,17 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
       b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
       v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : (ok[u] ? ogh[pos] : make_float2(0.f, 0.f));
     }
+    const int rot = tid & 15;
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
-      if (ok[u]) hist_accumulate(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), Fg);
+      if (ok[u]) {
+        if (kFPG > 16 && two) hist_accumulate_rot<(kFPG > 16 ? 32 : 16), kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
+        else hist_accumulate_rot<16, kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
+      }
   }
   __syncthreads();
-  ulonglong2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
-  for (int i = tid; i < Fg * kBinsPerFeature; i += kHistBlockThreads) {
-    const int f = i >> 8, b = i & 255;
-    SlabStore(out + (grp * kFPG + f) * kBinsPerFeature + b, shg[f * kHistStride + b], shh[f * kHistStride + b]);
-  }
+  SlabWrite<kFPG, kHistBlockThreads>(slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature, shg, shh, F,
+                                     grp * kFPG, Fg, tid);
 }
 
 // max |g|, max h of one class when the gradients did not come from grad_kernel
@@ -1012,7 +1036,9 @@ __global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
 #pragma unroll
     for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
     const HScale s = HistScale(count, ghmax);
-    hist[e] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
+    const int F = E / kBinsPerFeature;  // slab element e = b * F + f -> histogram [f][b]
+    const int bin = e / F, f = e - bin * F;
+    hist[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
                            static_cast<double>(static_cast<long long>(th)) * s.ih);
   }
   if (blockIdx.x == 0 && tid == 0) hist[E] = make_double2(static_cast<double>(count), 0.0);
@@ -2107,6 +2133,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   const int p1 = min(n, p0 + chunk);
   const HScale sc = HistScale(n, bound);
   const bool two = F > 16;
+  const int rot = tid & 15;
   float mg = 0.f, mh = 0.f;
   for (int base = p0 + tid; base < p1; base += kThreads * kUnroll) {
     uint4 b0[kUnroll], b1[kUnroll];
@@ -2140,16 +2167,14 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
       h[i] = hh;
       mg = fmaxf(mg, fabsf(gg));
       mh = fmaxf(mh, fabsf(hh));
-      hist_accumulate(shg, shh, b0[u], b1[u], QuantGH(make_float2(gg, hh), sc), F);
+      // all 32 slots (b1 = 0 when F <= 16: bin 0 of unused slots): one code path keeps this kernel unspilled
+      hist_accumulate_rot<32, kFeatPerGroup>(shg, shh, b0[u], b1[u], QuantGH(make_float2(gg, hh), sc), rot);
     }
   }
   BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
   __syncthreads();
-  ulonglong2* out = slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature;
-  for (int i = tid; i < F * kBinsPerFeature; i += kThreads) {
-    const int f = i >> 8, b = i & 255;
-    SlabStore(out + i, shg[f * kHistStride + b], shh[f * kHistStride + b]);
-  }
+  SlabWrite<kFeatPerGroup, kThreads>(slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature, shg, shh, F, 0, F,
+                                     tid);
 }
 
 // row-major -> column-major bin copy (once per dataset)

@@ -8,6 +8,7 @@ out="gpurun_out/${1:-ab_so}"
 mkdir -p "$out"
 export PYTHONUNBUFFERED=1
 so=$(ls synapseml_amd/_gbdt.cpython-*.so)
+cp "$so" /tmp/new_gbdt.so
 timeout -k 10 400 python -u -m pytest tests/test_gbdt_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
   > "$out/pytest_gbdt_gpu.log" 2>&1 || { tail -30 "$out/pytest_gbdt_gpu.log"; exit 1; }
 tail -2 "$out/pytest_gbdt_gpu.log"
