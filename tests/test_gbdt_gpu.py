@@ -61,6 +61,32 @@ def test_gpu_trees_match_cpu(extra):
     np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("f,fpg", [(5, "32"), (17, "32"), (28, "32"), (40, "32"), (70, "32"), (28, "16"), (40, "16")])
+def test_gpu_histogram_feature_groups_match_cpu(f, fpg, monkeypatch):
+    """The rotated bin-major LDS histogram over every feature-group shape: one partial 16-wide group (5),
+    32-wide groups with padding slots (17, 28), a 32-wide group plus a 16-step tail (40), three groups (70),
+    and the 16-feature-group kernel (SML_HIST_FPG=16, read at booster construction). The first two trees
+    must equal the CPU oracle's split for split."""
+    monkeypatch.setenv("SML_HIST_FPG", fpg)
+    rng = np.random.default_rng(f)
+    X = rng.standard_normal((40000, f))
+    w = rng.standard_normal(f) * (rng.random(f) < 0.5)
+    y = (X @ w + 0.7 * X[:, f - 1] * X[:, 0] + 0.5 * rng.standard_normal(len(X)) > 0).astype(np.float32)
+    base = "objective=binary num_leaves=31 learning_rate=0.1"
+    bc = _train(X, y, base + " device_type=cpu", 2)
+    bg = _train(X, y, base + " device_type=gpu", 2)
+    assert bg.backend == "hip"
+    mc, mg = bc.save_model_string(), bg.save_model_string()
+    line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")][0]
+    for t in range(2):
+        tc = mc.split(f"Tree={t}")[1].split(f"Tree={t + 1}")[0]
+        tg = mg.split(f"Tree={t}")[1].split(f"Tree={t + 1}")[0]
+        assert line(tc, "split_feature") == line(tg, "split_feature")
+        assert line(tc, "threshold") == line(tg, "threshold")
+        np.testing.assert_allclose(np.array(line(tc, "leaf_value").split("=")[1].split(), float),
+                                   np.array(line(tg, "leaf_value").split("=")[1].split(), float), rtol=1e-6, atol=1e-9)
+
+
 def test_gpu_missing_and_categorical():
     from sklearn.metrics import roc_auc_score
 
