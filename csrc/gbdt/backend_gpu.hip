@@ -2272,6 +2272,7 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_SKIP_LAST_SPLIT")) skip_last_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_GBDT_COMM_WORLD1")) comm_world1_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
+    if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -2888,7 +2889,8 @@ class GpuBackend : public TrainBackend {
 
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
-    auto hk = hist_fpg_ == 16 ? hist_kernel<kHistUnroll, 16> : hist_kernel<kHistUnroll, kFeatPerGroup>;
+    auto hk = hist_fpg_ == 16 ? hist_kernel<kHistUnroll, 16>
+              : (hist_unroll4_ ? hist_kernel<4, kFeatPerGroup> : hist_kernel<kHistUnroll, kFeatPerGroup>);
     hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
                        perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
@@ -3081,6 +3083,7 @@ class GpuBackend : public TrainBackend {
   SplitParams sp_{};
   int K_ = 1, F_ = 0, S_ = 4, W_ = 1, E_ = 0, L_ = 2, FG_ = 1;
   int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
+  bool hist_unroll4_ = false;     // SML_HIST_UNROLL=4: 4 gathered rows in flight per thread (A/B knob)
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
   DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident
