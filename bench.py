@@ -14,7 +14,14 @@ iterations, and the returned LightGBMClassificationModel (model string).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
 N > 1 it runs under torch.distributed.run with one rank per GPU (RCCL
-histogram allreduce inside the engine). One step = one complete ``fit``.
+histogram allreduce inside the engine). Started WITHOUT a torchrun
+environment and ``--gpus N > 1``, this script launches
+``python -m torch.distributed.run --nproc-per-node N bench.py ...`` as a child
+process before anything touches the GPU (the parent never imports torch),
+streams the ranks' output and exits with the child's code. Every rank checks
+that the world it joined has exactly N ranks and, on the GPU, N distinct
+devices (``--allow-shared-device`` opts into a rehearsal with ranks sharing a
+device); otherwise it fails. One step = one complete ``fit``.
 W untimed warmup fits, then exactly K timed fits bracketed by barrier +
 device synchronize; time is the max over ranks. ``value`` = total rows x K /
 seconds (whole job). Per-GPU rows are fixed as N grows (weak scaling).
@@ -56,6 +63,36 @@ def higgs_like(n: int, f: int, seed: int):
     return X, y
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, script: str, argv: list) -> int:
+    """Run ``script argv`` as n torchrun ranks in a CHILD process (no exec, no torch import here: this
+    process must not initialise the GPU). Returns the child's exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", script] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 8) // max(n, 1))))
+    return subprocess.call(cmd, env=env)
+
+
+def _parse_gpus(argv: list) -> int:
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,18 +104,30 @@ def main() -> None:
     ap.add_argument("--iterations", type=int, default=100, help="numIterations of each fit (reference default 100)")
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--save-model", default=None, help="write the last model's text here (after timing)")
+    ap.add_argument("--allow-shared-device", action="store_true",
+                    help="rehearsal only: allow more ranks than visible GPUs (ranks share devices)")
     args = ap.parse_args()
-
-    import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but this process is one of WORLD_SIZE={world} ranks; "
+              "refusing to report a run whose world differs from the requested GPU count", file=sys.stderr)
+        sys.exit(2)
+
+    import torch
+
     use_gpu = args.device == "gpu" and torch.cuda.is_available()
+    ndev = torch.cuda.device_count() if use_gpu else 0
     # more ranks than GPUs (a rehearsal of the multi-GPU path on a small box): ranks share devices, so the
     # control plane is gloo and histograms go over the one-shot IPC allreduce on a host base communicator
     # (RCCL cannot put two ranks on one device). The driver's N-GPU runs have one GPU per rank.
-    shared = use_gpu and world > torch.cuda.device_count()
+    shared = use_gpu and world > ndev
+    if shared and not args.allow_shared_device:
+        print(f"bench.py: {world} ranks but only {ndev} visible GPU(s); a {world}-GPU measurement needs {world} "
+              "devices (pass --allow-shared-device for a shared-device rehearsal)", file=sys.stderr)
+        sys.exit(3)
     if use_gpu:
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
     from synapseml_amd.parallel import distributed as D
@@ -153,12 +202,18 @@ def main() -> None:
             fh.write(model.getNativeModel())
     total_rows = args.rows * world
     value = total_rows * args.steps / elapsed
+    comm = next(iter(D._comm_cache.values()), None) if world > 1 else None
+    comm_world = int(comm.world) if comm is not None else world
+    if comm_world != world:
+        print(f"bench.py: communicator world {comm_world} != {world} ranks", file=sys.stderr)
+        sys.exit(4)
+    n_devices = (min(world, ndev) if shared else world) if use_gpu else 0
     if rank == 0:
         out = {
             "metric": METRIC,
             "value": round(value, 1),
-            "unit": "rows/s (training rows / LightGBMClassifier.fit wall seconds, 100 iterations, whole job)",
-            "n_gpus": world if use_gpu else 0,
+            "unit": "rows/s (training rows / LightGBMClassifier.fit wall seconds, %d iterations, whole job)" % args.iterations,
+            "n_gpus": n_devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -177,6 +232,13 @@ def main() -> None:
                 "seq_len": args.features,
                 "parallelism": f"dp{world}",
                 "rows_per_gpu": args.rows,
+                "world": world,
+                "distinct_devices": n_devices,
+                "shared_device_rehearsal": bool(shared),
+                "data_plane_world": comm_world,
+                "data_plane": (None if world == 1 else type(comm).__name__ if comm is None else
+                               ("rccl" if use_gpu and not shared else "host") +
+                               ("+p2p-ipc" if D.p2p_status.get("active") else "")),
                 "timed_region": "LightGBMClassifier.fit(df) end to end (DataFrame built before timing)",
                 "fit_phases_ms": phases,
                 "iteration_loop_row_iters_per_s": round(total_rows * args.iterations / iter_s, 1) if iter_s else None,
@@ -200,4 +262,6 @@ def main() -> None:
 
 
 if __name__ == "__main__":
+    if "WORLD_SIZE" not in os.environ and _parse_gpus(sys.argv[1:]) > 1:
+        sys.exit(launch_ranks(_parse_gpus(sys.argv[1:]), os.path.abspath(__file__), sys.argv[1:]))
     main()

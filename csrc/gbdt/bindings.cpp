@@ -219,6 +219,9 @@ PYBIND11_MODULE(_gbdt, m) {
   py::class_<PyComm>(m, "Comm")
       .def_property_readonly("rank", [](const PyComm& c) { return c.c->rank(); })
       .def_property_readonly("world", [](const PyComm& c) { return c.c->world(); })
+      .def_property_readonly("is_device", [](const PyComm& c) { return c.c->is_device(); })
+      .def_property_readonly("aborted", [](const PyComm& c) { return c.c->aborted(); })
+      .def("abort", [](PyComm& c) { c.c->Abort(); })
       .def("allreduce_host", [](PyComm& c, py::array_t<double> a) {
         auto b = a.request();
         c.c->AllReduceHost(static_cast<double*>(b.ptr), b.size);
@@ -254,11 +257,13 @@ PYBIND11_MODULE(_gbdt, m) {
     return CommDeviceAllReduceUs(c.c.get(), n, iters);
   });
   m.def("rccl_unique_id", []() { return py::bytes(RcclGetUniqueId()); });
-  m.def("rccl_comm", [](py::bytes uid, int rank, int world, int device) {
+  m.def("rccl_comm", [](py::bytes uid, int rank, int world, int device, double timeout_ms) {
     PyComm c;
-    c.c.reset(NewRcclComm(std::string(uid), rank, world, device));
+    std::string id(uid);
+    py::gil_scoped_release rel;
+    c.c.reset(NewRcclComm(id, rank, world, device, timeout_ms));
     return c;
-  });
+  }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("timeout_ms") = 120000.0);
 
   py::class_<Booster, std::shared_ptr<Booster>>(m, "Booster")
       .def(py::init([](PyDataset& d, const std::string& params, py::object comm) {

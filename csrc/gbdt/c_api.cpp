@@ -140,11 +140,13 @@ int SML_BoosterGetNumClasses(void* booster, int* out) {
 }
 
 // Metrics of data set data_idx (0 = train, 1.. = validation sets), in EvalNames order; *out_len = count.
-int SML_BoosterGetEval(void* booster, int data_idx, int* out_len, double* out_results) {
+// out_results holds buffer_len doubles; a call with a smaller buffer (or none) only reports the count, so a
+// caller sized for a stale metric list (e.g. before ResetParameter changed the metrics) cannot overflow it.
+int SML_BoosterGetEval(void* booster, int data_idx, int buffer_len, int* out_len, double* out_results) {
   return Guard([&] {
     auto ev = static_cast<Booster*>(booster)->Eval(data_idx);
     *out_len = static_cast<int>(ev.size());
-    if (out_results)
+    if (out_results && buffer_len >= *out_len)
       for (size_t i = 0; i < ev.size(); ++i) out_results[i] = ev[i].second;
   });
 }

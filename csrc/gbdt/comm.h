@@ -36,6 +36,8 @@ class Comm {
   virtual void Check() {}
   // unblock collectives stuck on a dead peer (RCCL: ncclCommAbort); the communicator is unusable after
   virtual void Abort() {}
+  // true once Abort() ran (a cached communicator in this state must be rebuilt, not reused)
+  virtual bool aborted() const { return false; }
 };
 
 class HostComm : public Comm {
@@ -55,7 +57,9 @@ class HostComm : public Comm {
 
 // RCCL communicator (defined in comm_rccl.cpp)
 std::string RcclGetUniqueId();
-Comm* NewRcclComm(const std::string& unique_id, int rank, int world, int device);
+// Non-blocking init bounded by timeout_ms (<= 0: wait forever); a failed or timed-out init aborts the
+// half-built communicator and throws CommError.
+Comm* NewRcclComm(const std::string& unique_id, int rank, int world, int device, double timeout_ms);
 
 // One-shot P2P (IPC) allreduce for device messages up to cap_bytes, layered on
 // `base` (used for the handle exchange, validation, host reductions and large

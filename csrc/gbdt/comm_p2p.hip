@@ -182,6 +182,7 @@ class P2pComm : public Comm {
     base_->Check();
   }
   void Abort() override { base_->Abort(); }
+  bool aborted() const override { return base_->aborted(); }
 
  private:
   bool Use(int64_t bytes) const { return active_ && world_ > 1 && bytes <= cap_; }

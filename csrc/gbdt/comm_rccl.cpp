@@ -5,9 +5,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "comm.h"
@@ -49,14 +51,30 @@ void HostComm::AllReduceDeviceF64(double* buf, int64_t n, void* stream) {
 
 namespace {
 
+double NowMs() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The communicator is created non-blocking so that a peer that never reaches (or dies inside) the collective
+// init cannot hang the healthy ranks: init polls ncclCommGetAsyncError against a deadline and aborts the
+// half-built communicator when it passes (the Python side then retries on every rank together).
 class RcclComm : public Comm {
  public:
-  RcclComm(const std::string& uid, int rank, int world, int device) : rank_(rank), world_(world) {
+  RcclComm(const std::string& uid, int rank, int world, int device, double timeout_ms)
+      : rank_(rank), world_(world), timeout_ms_(timeout_ms) {
     if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     if (device >= 0) SML_HIP_CHECK(hipSetDevice(device));
-    SML_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_) (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r) + " (ncclCommInitRankConfig)");
+    }
+    Settle(r, "ncclCommInitRankConfig");
     SML_HIP_CHECK(hipMalloc(&scratch_, 64));
   }
   ~RcclComm() override {
@@ -74,14 +92,14 @@ class RcclComm : public Comm {
     double* d = nullptr;
     SML_HIP_CHECK(hipMalloc(&d, sizeof(double) * n));
     SML_HIP_CHECK(hipMemcpy(d, buf, sizeof(double) * n, hipMemcpyHostToDevice));
-    SML_NCCL_CHECK(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm_, nullptr));
+    Settle(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm_, nullptr), "ncclAllReduce");
     SML_HIP_CHECK(hipStreamSynchronize(nullptr));
     SML_HIP_CHECK(hipMemcpy(buf, d, sizeof(double) * n, hipMemcpyDeviceToHost));
     SML_HIP_CHECK(hipFree(d));
   }
   void AllReduceDeviceF32(float* buf, int64_t n, void* stream) override {
     if (!comm_) throw CommError("RCCL communicator was aborted");
-    SML_NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, comm_, static_cast<hipStream_t>(stream)));
+    Settle(ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, comm_, static_cast<hipStream_t>(stream)), "ncclAllReduce");
   }
   // Polled by the backend while it waits for a tree (RCCL async-error polling): a peer that
   // died or a broken link surfaces as a CommError on every rank instead of a collective that never returns.
@@ -98,13 +116,39 @@ class RcclComm : public Comm {
     if (comm_) (void)ncclCommAbort(comm_);  // makes kernels of pending collectives return
     comm_ = nullptr;
   }
+  bool aborted() const override { return comm_ == nullptr; }
   void AllReduceDeviceF64(double* buf, int64_t n, void* stream) override {
     if (!comm_) throw CommError("RCCL communicator was aborted");
-    SML_NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm_, static_cast<hipStream_t>(stream)));
+    Settle(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm_, static_cast<hipStream_t>(stream)), "ncclAllReduce");
   }
 
  private:
+  // Non-blocking communicators may answer ncclInProgress (init, and the lazy peer connection of a first
+  // collective); the next call on the communicator must wait until the state settles. Bounded by the
+  // timeout: past it the communicator is aborted and the call fails with CommError.
+  void Settle(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return;
+    if (r != ncclInProgress) throw CommError(std::string("RCCL error: ") + ncclGetErrorString(r) + " (" + what + ")");
+    const double t0 = NowMs();
+    ncclResult_t st = ncclInProgress;
+    while (true) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+      if (st != ncclInProgress) break;
+      if (timeout_ms_ > 0 && NowMs() - t0 > timeout_ms_) {
+        Abort();
+        throw CommError(std::string(what) + " did not complete within " + std::to_string(timeout_ms_) +
+                        " ms (a peer rank failed or never joined); communicator aborted");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    if (st != ncclSuccess) {
+      Abort();
+      throw CommError(std::string("RCCL error: ") + ncclGetErrorString(st) + " (" + what + ")");
+    }
+  }
+
   int rank_, world_;
+  double timeout_ms_;
   ncclComm_t comm_ = nullptr;
   void* scratch_ = nullptr;
 };
@@ -117,8 +161,8 @@ std::string RcclGetUniqueId() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-Comm* NewRcclComm(const std::string& uid, int rank, int world, int device) {
-  return new RcclComm(uid, rank, world, device);
+Comm* NewRcclComm(const std::string& uid, int rank, int world, int device, double timeout_ms) {
+  return new RcclComm(uid, rank, world, device, timeout_ms);
 }
 
 }  // namespace sml

@@ -321,8 +321,10 @@ bool ParseHeaders(const uint8_t* d, size_t len, Jpeg* j) {
         break;
       case 0xDA: {  // SOS
         if (!j->baseline) { j->why = "SOS before SOF"; return false; }
+        if (se - s < 1) { j->why = "bad SOS"; return false; }
         const int ns = s[0];
         if (ns != j->ncomp) { j->why = "multi-scan JPEG"; return false; }
+        if (se - s < 1 + 2 * ns) { j->why = "bad SOS"; return false; }
         for (int i = 0; i < ns; ++i) {
           const int cid = s[1 + 2 * i];
           int c = 0;

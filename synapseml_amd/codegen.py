@@ -211,7 +211,7 @@ C_API: List[Tuple[str, List[Tuple[str, str]]]] = [
     ("SML_BoosterUpdateOneIter", [("booster", "void*"), ("is_finished", "int*")]),
     ("SML_BoosterGetCurrentIteration", [("booster", "void*"), ("out", "int*")]),
     ("SML_BoosterGetNumClasses", [("booster", "void*"), ("out", "int*")]),
-    ("SML_BoosterGetEval", [("booster", "void*"), ("data_idx", "int"), ("out_len", "int*"),
+    ("SML_BoosterGetEval", [("booster", "void*"), ("data_idx", "int"), ("buffer_len", "int"), ("out_len", "int*"),
                             ("out_results", "double*")]),
     ("SML_BoosterPredictForMat", [("booster", "void*"), ("data", "void*"), ("data_type", "int"), ("nrow", "int32"),
                                   ("ncol", "int32"), ("predict_type", "int"), ("start_iteration", "int"),
@@ -309,9 +309,9 @@ def generate_dotnet(out_dir: str, namespace: str = "SynapseML.Amd") -> str:
               "            get { NativeMethods.Check(NativeMethods.SML_BoosterGetCurrentIteration(handle, out int i)); return i; }",
               "        }", "",
               "        public double[] GetEval(int dataIdx)", "        {",
-              "            NativeMethods.Check(NativeMethods.SML_BoosterGetEval(handle, dataIdx, out int n, null));",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterGetEval(handle, dataIdx, 0, out int n, null));",
               "            var r = new double[n];",
-              "            NativeMethods.Check(NativeMethods.SML_BoosterGetEval(handle, dataIdx, out n, r));",
+              "            NativeMethods.Check(NativeMethods.SML_BoosterGetEval(handle, dataIdx, r.Length, out n, r));",
               "            return r;", "        }", "",
               "        /// <param name=\"predictType\">0 raw, 1 normal, 2 leaf index, 3 contributions</param>",
               "        public double[] Predict(float[] rowMajor, int nrow, int ncol, int predictType = 1, int numIteration = -1)",

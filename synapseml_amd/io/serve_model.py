@@ -186,6 +186,11 @@ def main(argv=None) -> None:
     ap.add_argument("--epoch-ms", type=float, default=30000.0, help="continuous mode: epoch (checkpoint) interval")
     ap.add_argument("--checkpoint-location", default=None, help="continuous mode: offsets/commits directory")
     a = ap.parse_args(argv)
+    if a.workers > 1 and a.mode == "continuous":
+        # the multi-worker front end runs micro-batch workers only; continuous mode's epochs/offsets are per
+        # process (one checkpoint location each), so scale it with one replica per GPU instead
+        ap.error("--mode continuous serves from one process: use --workers 1 per replica (one checkpoint "
+                 "location per replica), not --workers > 1")
     if a.workers > 1:
         srv_d = DistributedServing(a.model, a.workers, a.port, a.host, a.input_cols, a.output_cols, a.api,
                                    a.max_batch_size, gpus=_worker_gpus(a.gpus))

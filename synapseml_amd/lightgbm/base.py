@@ -35,6 +35,35 @@ from .params import LightGBMParams
 log = logging.getLogger("synapseml_amd.lightgbm")
 
 
+
+def _group_order(g) -> Optional[np.ndarray]:
+    """Row order that makes each query group contiguous (groups in first-appearance order, rows stable
+    inside a group), or None when the rows already are grouped (the common case: no copy at all).
+
+    Vectorised (LightGBMRanker.scala:88-120 needs contiguous groups). The column is cut into runs of equal
+    ids; when no id starts two runs the rows are grouped. Otherwise the run ids are factorised (a hash pass
+    over runs, first-appearance codes) and the runs are stably ordered by code and expanded back to rows."""
+    a = np.asarray(g)
+    n = len(a)
+    if n < 2:
+        return None
+    brk = np.flatnonzero(a[1:] != a[:-1]) + 1
+    starts = np.concatenate(([0], brk))
+    run_ids = a[starts]
+    if len(np.unique(run_ids)) == len(starts):
+        return None
+    import pandas as pd
+
+    codes, _ = pd.factorize(run_ids, sort=False)
+    lens = np.diff(np.append(starts, n))
+    run_order = np.argsort(codes, kind="stable")
+    rs, rl = starts[run_order], lens[run_order]
+    # expand runs to row indices: row i of the output = rs[run] + (i - first output row of that run)
+    out_first = np.concatenate(([0], np.cumsum(rl)[:-1]))
+    idx = np.arange(n, dtype=np.int64)
+    idx -= np.repeat(out_first - rs, rl)
+    return idx
+
 class InstrumentationMeasures(dict):
     """Per-phase wall-clock timings (reference: LightGBMPerformance.scala:11-183)."""
 
@@ -365,11 +394,9 @@ class LightGBMBase(Estimator, LightGBMParams):
         """Column extraction; ranker rows are grouped contiguously."""
         gcol = self._group_col()
         if gcol:
-            g = df[gcol]
-            codes = {}
-            ids = np.asarray([codes.setdefault(v, len(codes)) for v in g.tolist()], dtype=np.int64)
-            order = np.argsort(ids, kind="stable")
-            df = df._take_rows(order)
+            order = _group_order(df[gcol])
+            if order is not None:
+                df = df._take_rows(order)
         return df
 
     def _train_batch(self, df: DataFrame, model_str: Optional[str], batch_index: int, num_class: int):
@@ -570,8 +597,10 @@ class LightGBMBase(Estimator, LightGBMParams):
                     finished = nb.update()
             except RuntimeError as e:
                 # a failed or timed-out collective (peer died, link broke, ranks diverged) fails the job on
-                # every rank; anything else ends this task's training early (TrainUtils.scala:89-95)
+                # every rank; anything else ends this task's training early (TrainUtils.scala:89-95). The
+                # aborted communicator is evicted so a later fit in this process builds a fresh one.
                 if isinstance(e, native.gbdt().CommError):
+                    D.evict_comm(str(e))
                     raise
                 log.warning("training stopped early on this task: %s", e)
                 finished = True
@@ -596,6 +625,11 @@ class LightGBMBase(Estimator, LightGBMParams):
             it += 1
             if ck_every > 0 and it % ck_every == 0 and not finished and it < num_iter:
                 self._ckpt_write(nb.save_model_string(), batch_index, it, False)
-        nb.synchronize()
+        try:
+            nb.synchronize()
+        except RuntimeError as e:
+            if isinstance(e, native.gbdt().CommError):
+                D.evict_comm(str(e))
+            raise
         m.mark("training_iterations_ms", (time.perf_counter() - t0) * 1e3)
         return best_result

@@ -146,28 +146,68 @@ def maybe_p2p(comm, device: int):
     return c
 
 
-def init_with_retries(make, what: str, retries: int = 3, delay_s: float = 1.0):
+def _abort_quietly(c) -> None:
+    abort = getattr(c, "abort", None)
+    if abort is not None:
+        try:
+            abort()
+        except Exception:  # noqa: BLE001 - best effort on a communicator that is being thrown away
+            pass
+
+
+def init_with_retries(make, what: str, retries: int = 3, delay_s: float = 1.0, prepare=None):
     """Collective network initialisation with the reference's retry policy (NetworkManager.scala:195-218,
-    3 retries, 1 s doubled): every rank tries, the outcomes are all-gathered over the control plane, and if
-    any rank failed all ranks retry together (a fresh unique id each time), so no rank is left holding a
-    half-initialised communicator."""
+    3 retries, 1 s doubled).
+
+    Two agreement points per attempt, both over the control plane, so no rank can be left blocked inside a
+    collective init its peers never entered:
+
+    1. ``prepare()`` (non-collective: device selection, unique-id creation) runs on every rank and the
+       outcomes are all-gathered; the collective ``make(payload)`` is only entered when every rank is ready.
+       ``payload`` is rank 0's ``prepare()`` result (e.g. the ncclUniqueId), broadcast with the outcomes.
+    2. ``make`` itself must be bounded (the native RCCL init is non-blocking with a deadline and aborts
+       itself on timeout); its outcomes are all-gathered, and if any rank failed every rank aborts the
+       communicator it built and all retry together with a fresh ``prepare()``.
+    """
     import time
 
     for attempt in range(retries + 1):
-        c, err = None, None
-        try:
-            c = make()
-        except Exception as e:  # noqa: BLE001 - shared with the other ranks below
-            err = f"rank {rank()}: {type(e).__name__}: {e}"
-        errs = [e for e in all_gather_object(err) if e]
+        c, err, payload = None, None, None
+        if prepare is not None:
+            try:
+                payload = prepare()
+            except Exception as e:  # noqa: BLE001 - shared with the other ranks below
+                err = f"rank {rank()} (prepare): {type(e).__name__}: {e}"
+            outcomes = all_gather_object((err, payload if rank() == 0 else None))
+            errs = [e for e, _ in outcomes if e]
+            payload = outcomes[0][1]
+        else:
+            errs = []
         if not errs:
-            return c
+            try:
+                c = make(payload) if prepare is not None else make()
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {rank()}: {type(e).__name__}: {e}"
+            errs = [e for e in all_gather_object(err) if e]
+            if not errs:
+                return c
+        if c is not None:
+            _abort_quietly(c)  # a peer failed: this rank's communicator is half of a broken group
         del c
         if attempt == retries:
             raise RuntimeError(f"{what} initialisation failed after {retries} retries: " + "; ".join(errs))
         time.sleep(delay_s)
         delay_s *= 2
     raise AssertionError("unreachable")
+
+
+def evict_comm(reason: str = "") -> None:
+    """Drop cached communicators (called when a fit re-raises a CommError: an aborted communicator must not
+    be handed to the next fit of this process)."""
+    for c in list(_comm_cache.values()):
+        _abort_quietly(c)
+    _comm_cache.clear()
+    p2p_status.clear()
 
 
 def gbdt_comm(use_gpu: bool, shared_device: bool = False):
@@ -197,7 +237,9 @@ def gbdt_comm(use_gpu: bool, shared_device: bool = False):
     g = native.gbdt()
     key = ("shared" if use_gpu and shared_device else "rccl" if use_gpu else "host", world_size())
     if key in _comm_cache:
-        return _comm_cache[key]
+        if not getattr(_comm_cache[key], "aborted", False):
+            return _comm_cache[key]
+        del _comm_cache[key]  # aborted by a CommError in an earlier fit: rebuild
     if use_gpu and shared_device:
         import torch
 
@@ -208,11 +250,17 @@ def gbdt_comm(use_gpu: bool, shared_device: bool = False):
 
         dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
 
-        def make():
-            uid = g.rccl_unique_id() if rank() == 0 else None
-            return g.rccl_comm(broadcast_object(uid, 0), rank(), world_size(), dev)
+        timeout_ms = float(os.environ.get("SML_RCCL_INIT_TIMEOUT_MS", "120000"))
 
-        c = init_with_retries(make, "RCCL communicator")
+        def prepare():
+            if dev >= 0:
+                torch.cuda.set_device(dev)
+            return g.rccl_unique_id() if rank() == 0 else None
+
+        def make(uid):
+            return g.rccl_comm(uid, rank(), world_size(), dev, timeout_ms)
+
+        c = init_with_retries(make, "RCCL communicator", prepare=prepare)
         c = maybe_p2p(c, dev)
     else:
         c = g.host_comm(rank(), world_size(), lambda arr: allreduce_numpy(arr))

@@ -126,6 +126,25 @@ int main() {
         JpegDecode(buf.data(), buf.size(), o.data(), o.size(), &why);
       }
     }
+    // truncated SOS segments at the very end of the input (segment length 2 = no component count, and a
+    // count whose component list runs past the segment): refused without reading past the buffer (ASan)
+    {
+      size_t sos = 0;
+      for (size_t i = 0; i + 1 < sizeof(kColor420); ++i)
+        if (kColor420[i] == 0xFF && kColor420[i + 1] == 0xDA) { sos = i; break; }
+      CHECK(sos > 0);
+      for (int seglen : {2, 3, 4}) {
+        std::vector<uint8_t> t(kColor420, kColor420 + sos + 2);
+        t.push_back(0);
+        t.push_back(static_cast<uint8_t>(seglen));
+        if (seglen >= 3) t.push_back(3);  // 3 components named, none or one listed
+        if (seglen >= 4) t.push_back(1);
+        t.shrink_to_fit();
+        std::string why;
+        std::vector<uint8_t> o(23 * 19 * 3);
+        CHECK(!JpegDecode(t.data(), t.size(), o.data(), o.size(), &why));
+      }
+    }
     // threaded batch: both files twice, plus an invalid entry
     std::vector<const uint8_t*> ptrs = {kColor420, kGray, kColor420, kGray, kGray};
     std::vector<size_t> lens = {sizeof(kColor420), sizeof(kGray), sizeof(kColor420), sizeof(kGray), 10};

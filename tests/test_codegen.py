@@ -83,9 +83,12 @@ def test_native_c_api_trains_and_predicts_like_the_python_engine():
     it = C.c_int()
     assert lib.SML_BoosterGetCurrentIteration(bst, C.byref(it)) == 0 and it.value == 10
     ne = C.c_int()
-    assert lib.SML_BoosterGetEval(bst, 0, C.byref(ne), None) == 0 and ne.value == 1
+    assert lib.SML_BoosterGetEval(bst, 0, 0, C.byref(ne), None) == 0 and ne.value == 1
     ev = (C.c_double * ne.value)()
-    assert lib.SML_BoosterGetEval(bst, 0, C.byref(ne), ev) == 0 and 0.9 < ev[0] <= 1.0
+    ev[0] = -7.0
+    # a buffer too small for the metric list is left untouched (only the count is reported)
+    assert lib.SML_BoosterGetEval(bst, 0, 0, C.byref(ne), ev) == 0 and ne.value == 1 and ev[0] == -7.0
+    assert lib.SML_BoosterGetEval(bst, 0, ne.value, C.byref(ne), ev) == 0 and 0.9 < ev[0] <= 1.0
     ln = C.c_int64()
     assert lib.SML_BoosterPredictForMat(bst, X.ctypes.data_as(C.c_void_p), 0, 3000, 6, 1, 0, -1, C.byref(ln), None) == 0
     out = np.zeros(ln.value)

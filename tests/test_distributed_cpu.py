@@ -245,3 +245,106 @@ def test_p2p_fallback_is_collective(task):
     res = run_partitions(task, DataFrame({"x": np.arange(4)}, num_partitions=2), num_workers=2)
     assert all(kept for kept, _ in res)
     assert all(st.get("active") is False and "multi-node" in st.get("reason", "") for _, st in res)
+
+
+class _FakeComm:
+    def __init__(self, tag):
+        self.tag, self.aborted = tag, False
+
+    def abort(self):
+        self.aborted = True
+
+
+def _prepare_failure_task(part, rank, world):
+    """prepare() fails on rank 1 in the first attempt; make() is collective (a gloo barrier stands in for
+    ncclCommInitRank). Without the readiness agreement rank 0 would sit in the barrier forever."""
+    import torch.distributed as dist
+
+    from synapseml_amd.parallel.distributed import init_with_retries
+
+    st = {"prep": 0, "make": 0, "built": []}
+
+    def prepare():
+        st["prep"] += 1
+        if rank == 1 and st["prep"] == 1:
+            raise OSError("device not ready")
+        return f"uid{st['prep']}" if rank == 0 else None
+
+    def make(uid):
+        st["make"] += 1
+        dist.barrier()  # collective: both ranks must be inside
+        c = _FakeComm(uid)
+        st["built"].append(c)
+        if rank == 0 and st["make"] == 1 and uid == "uid-never":
+            raise OSError("unreachable")
+        return c
+
+    c = init_with_retries(make, "collective comm", delay_s=0.01, prepare=prepare)
+    return c.tag, st["prep"], st["make"]
+
+
+def _make_failure_aborts_task(part, rank, world):
+    """make() fails on rank 1 after rank 0 built its half: rank 0 must abort its communicator before the
+    retry (a half-built RCCL communicator is never left alive)."""
+    from synapseml_amd.parallel.distributed import init_with_retries
+
+    built = []
+
+    def make(uid):
+        c = _FakeComm(uid)
+        built.append(c)
+        if rank == 1 and len(built) == 1:
+            raise OSError("init failed inside the collective")
+        return c
+
+    c = init_with_retries(make, "collective comm", delay_s=0.01, prepare=lambda: "uid")
+    return [b.aborted for b in built], c.aborted
+
+
+def test_collective_init_agrees_on_readiness_before_entering():
+    res = run_partitions(_prepare_failure_task, DataFrame({"x": np.arange(4)}, num_partitions=2), num_workers=2,
+                         timeout_s=120)
+    # the uid is rank 0's second prepare() result on every rank; make() was entered once, together
+    assert res == [("uid2", 2, 1), ("uid2", 2, 1)]
+
+
+def test_failed_collective_init_aborts_peers_communicators():
+    res = run_partitions(_make_failure_aborts_task, DataFrame({"x": np.arange(4)}, num_partitions=2),
+                         num_workers=2, timeout_s=120)
+    assert res[0] == ([True, False], False)
+    assert res[1] == ([False, False], False)  # rank 1's first make raised before returning a communicator
+
+
+def test_comm_cache_evicts_aborted(monkeypatch):
+    from synapseml_amd.parallel import distributed as D
+
+    c = _FakeComm("x")
+    D._comm_cache[("host", 2)] = c
+    D.evict_comm("test")
+    assert c.aborted and not D._comm_cache
+
+
+def test_bench_launches_n_ranks_on_cpu():
+    """bench.py --gpus 2 started without a torchrun environment launches 2 ranks itself (child process)
+    and the JSON line reports a 2-rank data-parallel world; a rank whose world != --gpus refuses."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu",
+                          "--rows", "20000", "--iterations", "3", "--steps", "1", "--warmup", "0"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["config"]["parallelism"] == "dp2" and rec["config"]["world"] == 2
+    assert rec["config"]["data_plane_world"] == 2 and rec["config"]["global_batch"] == 40000
+    env1 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu",
+                          "--rows", "2000", "--iterations", "1", "--steps", "1", "--warmup", "0"],
+                         env=env1, capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE=1" in bad.stderr

@@ -457,3 +457,18 @@ def test_parallelism_values_checked():
                 LightGBMClassifier(parallelism=par)._check_parallelism(gpu, world)
     with pytest.raises(ValueError, match="voting_parallel"):
         LightGBMClassifier(parallelism="feature_parallel")._check_parallelism(True, 2)
+
+
+def test_ranker_group_order_vectorised():
+    """Group prep (base.py::_group_order): grouped input is left alone (no copy); scattered groups are made
+    contiguous in first-appearance order with rows stable inside each group (the per-row dict it replaced)."""
+    from synapseml_amd.lightgbm.base import _group_order
+
+    assert _group_order(np.repeat(np.arange(50), 7)) is None
+    assert _group_order(np.repeat(np.array([9, 3, 5]), 4)) is None  # contiguous, not sorted
+    assert _group_order(np.array(["b", "b", "a"], dtype=object)) is None
+    rng = np.random.default_rng(3)
+    for ids in (rng.integers(0, 40, 500), np.array(["q%d" % i for i in rng.integers(0, 9, 200)], dtype=object)):
+        codes = {}
+        ref = np.argsort(np.asarray([codes.setdefault(v, len(codes)) for v in ids.tolist()]), kind="stable")
+        assert np.array_equal(_group_order(ids), ref)

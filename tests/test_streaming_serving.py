@@ -195,3 +195,13 @@ def test_helm_chart_renders_both_modes():
                 cur = cur[k]
         assert src.count("{{- if") + src.count("{{ if") == src.count("{{- end") + src.count("{{ end") - \
             src.count("{{- range")
+
+
+def test_serve_model_rejects_continuous_with_workers():
+    """Continuous mode keeps epochs/offsets per process: --workers > 1 (micro-batch workers only) with
+    --mode continuous is refused instead of silently dropping the continuous options."""
+    from synapseml_amd.io import serve_model
+
+    with pytest.raises(SystemExit) as e:
+        serve_model.main(["--model", "/nonexistent", "--workers", "2", "--mode", "continuous"])
+    assert e.value.code == 2
