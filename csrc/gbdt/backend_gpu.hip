@@ -926,19 +926,16 @@ __device__ __forceinline__ void SlabWrite(ulonglong2* out, const unsigned long l
   }
 }
 
-// kFPG features per block (blockIdx.y = feature group): 32 = one 128 KB LDS histogram per CU; 16 halves
-// the LDS (two blocks per CU) at the price of reading every row's perm / g / h once per group
+// One block's share of a leaf histogram: rows [begin, begin + count) of ping-pong buffer `buf` (-1 =
+// physical rows) are cut into nb_active chunks; this block (chunk lb, feature group blockIdx.y) accumulates
+// its chunk into LDS and writes its slab.
 template <int kUnroll, int kFPG>
-__global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
-    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
-    int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
-    const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
-    const float* __restrict__ h, const float* __restrict__ ghmax, ulonglong2* __restrict__ slab) {
-  if (st->done) return;
-  const DLeaf L = HistSeg(st, leaves);
-  const int count = L.count;
-  const int nb_active = HistBlocks(count);
-  if (static_cast<int>(blockIdx.x) >= nb_active) return;
+__device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_active, int lb, const uint4* __restrict__ bins4,
+                                         int W4, int F, const int32_t* __restrict__ perm0,
+                                         const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
+                                         const float2* __restrict__ ogh1, const float* __restrict__ g,
+                                         const float* __restrict__ h, const float* __restrict__ ghmax,
+                                         ulonglong2* __restrict__ slab_out) {
   constexpr int kWords = kFPG * kBinsPerFeature;
   __shared__ unsigned long long shg[kWords], shh[kWords];
   const int tid = threadIdx.x;
@@ -949,12 +946,12 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
   const int col = grp * (kFPG / 16);  // first uint4 of this group in a row
   const bool two = kFPG > 16 && Fg > 16;
   const int chunk = ceil_div_i(count, nb_active);
-  const int p0 = L.begin + blockIdx.x * chunk;
-  const int p1 = min(L.begin + count, p0 + chunk);
+  const int p0 = begin + lb * chunk;
+  const int p1 = min(begin + count, p0 + chunk);
   const HScale sc = HistScale(count, ghmax);
-  const int32_t* __restrict__ perm = L.buf == 0 ? perm0 : perm1;
-  const float2* __restrict__ ogh = L.buf == 0 ? ogh0 : ogh1;
-  const bool phys = L.buf < 0;
+  const int32_t* __restrict__ perm = buf == 0 ? perm0 : perm1;
+  const float2* __restrict__ ogh = buf == 0 ? ogh0 : ogh1;
+  const bool phys = buf < 0;
   for (int base = p0 + tid; base < p1; base += kHistBlockThreads * kUnroll) {
     int r[kUnroll];
     bool ok[kUnroll];
@@ -983,8 +980,23 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
       }
   }
   __syncthreads();
-  SlabWrite<kFPG, kHistBlockThreads>(slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature, shg, shh, F,
-                                     grp * kFPG, Fg, tid);
+  SlabWrite<kFPG, kHistBlockThreads>(slab_out, shg, shh, F, grp * kFPG, Fg, tid);
+}
+
+// kFPG features per block (blockIdx.y = feature group): 32 = one 128 KB LDS histogram per CU; 16 halves
+// the LDS (two blocks per CU) at the price of reading every row's perm / g / h once per group
+template <int kUnroll, int kFPG>
+__global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
+    const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
+    int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
+    const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
+    const float* __restrict__ h, const float* __restrict__ ghmax, ulonglong2* __restrict__ slab) {
+  if (st->done) return;
+  const DLeaf L = HistSeg(st, leaves);
+  const int nb_active = HistBlocks(L.count);
+  if (static_cast<int>(blockIdx.x) >= nb_active) return;
+  HistBody<kUnroll, kFPG>(L.begin, L.count, L.buf, nb_active, blockIdx.x, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
+                          ghmax, slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature);
 }
 
 // max |g|, max h of one class when the gradients did not come from grad_kernel
@@ -1131,6 +1143,11 @@ __device__ void CategoricalSearch(const double* hg, const double* hh, int nb, in
 //                 are searched, leaf totals come from the split record (root: its own voted histogram)
 enum FindMode { kFindFull = 0, kFindLocal = 1, kFindVoted = 2 };
 
+__device__ void HistTotals(double2 mine, int nb, double* G, double* H);
+__device__ void SearchFeatureBlock(double2 mine, double G, double H, int64_t cnt, int depth, int slot, double lo,
+                                   double hi, int f, int F, const FeatMeta& fm, const SplitParams& sp, SplitResult* out,
+                                   bool selected);
+
 // Block (f, child): 256 threads, thread = bin.
 __device__ void FindSplitBlock(
     DState* __restrict__ st, DLeaf* __restrict__ leaves, const double2* __restrict__ part, int E,
@@ -1139,7 +1156,7 @@ __device__ void FindSplitBlock(
     const int8_t* __restrict__ sel, const int32_t* __restrict__ sel_first) {
   const int f = blockIdx.x;
   const int child = blockIdx.y;  // 0 = small (or root), 1 = large
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x;
   const bool root = st->phase == 0;
   if (root && child == 1) return;
   const int leaf_id = root ? 0 : (child == 0 ? st->small_leaf : st->large_leaf);
@@ -1158,30 +1175,10 @@ __device__ void FindSplitBlock(
   }
   const DLeaf Lf = leaves[leaf_id];
   if (mode != kFindVoted) hist_pool[static_cast<size_t>(Lf.slot) * E + e] = mine;
-  __shared__ double sg_[256], shh_[256];
-  __shared__ double wtot_g[4], wtot_h[4];
-  __shared__ Cand wbest[4];
-  __shared__ int idxbuf[256], leftbuf[256];
-  __shared__ SplitResult s_cat_best;
-  __shared__ MonoCtx s_mc;  // by pointer into EvalSplit / the categorical search: LDS, not scratch
-  sg_[tid] = mine.x;
-  shh_[tid] = mine.y;
-  const int nb = fm.num_bin[f];
-  const int mt = fm.missing[f];
-  const int dbin = fm.default_bin[f];
   // leaf totals: from this feature's histogram (root) or the split record
   double G, H;
   int64_t cnt;
-  {
-    // total over bins (for the root and as a consistent parent sum)
-    double tg = tid < nb ? mine.x : 0.0, th = tid < nb ? mine.y : 0.0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) { tg += __shfl_xor(tg, off, 64); th += __shfl_xor(th, off, 64); }
-    if (lane == 0) { wtot_g[wid] = tg; wtot_h[wid] = th; }
-    __syncthreads();
-    G = wtot_g[0] + wtot_g[1] + wtot_g[2] + wtot_g[3];
-    H = wtot_h[0] + wtot_h[1] + wtot_h[2] + wtot_h[3];
-  }
+  HistTotals(mine, fm.num_bin[f], &G, &H);
   if (root) {
     cnt = static_cast<int64_t>(*count_slot);
     const int writer = mode == kFindFull ? 0 : (mode == kFindVoted ? *sel_first : -1);
@@ -1198,18 +1195,51 @@ __device__ void FindSplitBlock(
     cnt = child == 0 ? small_cnt : (Lf.gcount - small_cnt);  // Lf.gcount of large holds the parent count (set by choose)
     G = Lf.sum_g; H = Lf.sum_h;
   }
-  SplitResult* out = fbest + child * F + f;
-  const bool eligible = fm.mask[f] && nb > 1 && (mode != kFindVoted || sel[child * F + f]) &&
+  SearchFeatureBlock(mine, G, H, cnt, Lf.depth, Lf.slot, Lf.lo, Lf.hi, f, F, fm, sp, fbest + child * F + f,
+                     mode != kFindVoted || sel[child * F + f]);
+}
+
+// Sum over the feature's bins of the block's histogram (thread = bin): the leaf totals at the root.
+__device__ void HistTotals(double2 mine, int nb, double* G, double* H) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ double wtot_g[4], wtot_h[4];
+  double tg = tid < nb ? mine.x : 0.0, th = tid < nb ? mine.y : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { tg += __shfl_xor(tg, off, 64); th += __shfl_xor(th, off, 64); }
+  if (lane == 0) { wtot_g[wid] = tg; wtot_h[wid] = th; }
+  __syncthreads();
+  *G = wtot_g[0] + wtot_g[1] + wtot_g[2] + wtot_g[3];
+  *H = wtot_h[0] + wtot_h[1] + wtot_h[2] + wtot_h[3];
+}
+
+// Best split of one (leaf, feature): 256 threads, thread = bin; `mine` = this thread's bin (g, h), G / H / cnt
+// the leaf's totals, depth / slot / [lo, hi] its tree position and monotone bounds. Writes *out (feature -1,
+// gain -inf when the feature cannot split the leaf).
+__device__ void SearchFeatureBlock(double2 mine, double G, double H, int64_t cnt, int depth, int slot, double lo,
+                                   double hi, int f, int F, const FeatMeta& fm, const SplitParams& sp, SplitResult* out,
+                                   bool selected) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ double sg_[256], shh_[256];
+  __shared__ Cand wbest[4];
+  __shared__ int idxbuf[256], leftbuf[256];
+  __shared__ SplitResult s_cat_best;
+  __shared__ MonoCtx s_mc;  // by pointer into EvalSplit / the categorical search: LDS, not scratch
+  sg_[tid] = mine.x;
+  shh_[tid] = mine.y;
+  const int nb = fm.num_bin[f];
+  const int mt = fm.missing[f];
+  const int dbin = fm.default_bin[f];
+  const bool eligible = fm.mask[f] && nb > 1 && selected &&
                         cnt >= 2 * static_cast<int64_t>(sp.min_data_in_leaf) &&
-                        (sp.max_depth <= 0 || Lf.depth < sp.max_depth) &&
+                        (sp.max_depth <= 0 || depth < sp.max_depth) &&
                         (sp.bynode_k <= 0 ||
-                         NodeFeatureSelected(sp.bynode_seed, sp.tree_seq, Lf.slot, f, fm.mask, F, sp.bynode_k));
+                         NodeFeatureSelected(sp.bynode_seed, sp.tree_seq, slot, f, fm.mask, F, sp.bynode_k));
   if (!eligible) {
     if (tid == 0) { out->feature = -1; out->gain = -INFINITY; }
     return;
   }
   // monotone context of this (leaf, feature); categorical splits are clamped but carry no direction
-  if (tid == 0) s_mc = MonoCtx{Lf.lo, Lf.hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
+  if (tid == 0) s_mc = MonoCtx{lo, hi, fm.is_cat[f] ? 0 : static_cast<int>(fm.mono[f])};
   __syncthreads();
   const MonoCtx* mcp = sp.has_mono ? &s_mc : nullptr;
   if (fm.is_cat[f]) {
@@ -1287,7 +1317,7 @@ __device__ void FindSplitBlock(
       r.left_cnt = EstimateCount(hl, cnt_factor); r.right_cnt = cnt - r.left_cnt;
       double g2;
       (void)EvalSplit(gl, hl, gr, hr, sp.lambda_l1, sp.lambda_l2, sp.max_delta_step, mcp, &g2, &r.left_out, &r.right_out);
-      if (mcp && mcp->mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(Lf.depth, sp.monotone_penalty);
+      if (mcp && mcp->mono != 0 && sp.monotone_penalty > 0) r.gain *= MonotonePenaltyFactor(depth, sp.monotone_penalty);
       for (int w = 0; w < 8; ++w) r.cat_bits[w] = 0;
     }
     *out = r;
@@ -1659,18 +1689,16 @@ __device__ __forceinline__ bool RowGoesLeft(const uint8_t* cbins, int64_t n, int
 // depends on the order tiles claim their ranges; nothing downstream depends
 // on it (histograms are exact integer sums, see K3).
 
-// Tile loop of the single-pass partition of segment [pbegin, pbegin + pcount)
-// of ping-pong buffer pbuf (-1 = physical rows) by split ps; claims output
-// ranges on *cursor (zeroed before the launch).
+// One tile of the single-pass partition of segment [pbegin, pbegin + pcount) of ping-pong buffer pbuf (-1 =
+// physical rows) by split ps; claims its output ranges on *cursor (zeroed before the launch).
 template <int kPartRows>
-__device__ __forceinline__ void PartitionTiles(
-    const PartSplit& ps, const uint32_t* s_cat, int pbegin, int pcount, int pbuf, unsigned long long* cursor,
+__device__ __forceinline__ void PartitionTile(
+    const PartSplit& ps, const uint32_t* s_cat, int tile, int pbegin, int pcount, int pbuf, unsigned long long* cursor,
     const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
     int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1, float2* __restrict__ wogh0,
     float2* __restrict__ wogh1, const float* __restrict__ g, const float* __restrict__ h) {
   constexpr int kPartTile = kPartThreads * kPartRows;
-  const int ntiles = ceil_div_i(pcount, kPartTile);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int kWaves = kPartThreads / 64;
   __shared__ int wl[kPartRows][kWaves];
@@ -1680,7 +1708,7 @@ __device__ __forceinline__ void PartitionTiles(
   int32_t* operm = pbuf == 0 ? wperm1 : wperm0;
   float2* oogh = pbuf == 0 ? wogh1 : wogh0;
   const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  {
     const int t0 = pbegin + tile * kPartTile;
     const int tv = min(kPartTile, pbegin + pcount - t0);
     int r[kPartRows];
@@ -1748,6 +1776,21 @@ __device__ __forceinline__ void PartitionTiles(
     }
     __syncthreads();
   }
+}
+
+// Tile loop of the single-pass partition of one segment (blocks stride over its tiles).
+template <int kPartRows>
+__device__ __forceinline__ void PartitionTiles(
+    const PartSplit& ps, const uint32_t* s_cat, int pbegin, int pcount, int pbuf, unsigned long long* cursor,
+    const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
+    const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
+    int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1, float2* __restrict__ wogh0,
+    float2* __restrict__ wogh1, const float* __restrict__ g, const float* __restrict__ h) {
+  constexpr int kPartTile = kPartThreads * kPartRows;
+  const int ntiles = ceil_div_i(pcount, kPartTile);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+    PartitionTile<kPartRows>(ps, s_cat, tile, pbegin, pcount, pbuf, cursor, cbins, n, perm0, perm1, ogh0, ogh1, wperm0,
+                             wperm1, wogh0, wogh1, g, h);
 }
 
 // ---------------------------------------------------------------- choose + K6, one launch
@@ -1949,6 +1992,460 @@ __global__ __launch_bounds__(kPartThreads) void choose_part_kernel(
   __syncthreads();
   PartitionTiles<kPartRows>(ps, s_cat, pb, pc, pbuf, &sout->cursor, cbins, n, perm0, perm1, ogh0, ogh1, wperm0,
                             wperm1, wogh0, wogh1, g, h);
+}
+
+// ---------------------------------------------------------------- batched speculative growth
+// Leaf-wise growth splits the leaf of largest gain, one split at a time: ~4 dependent kernels per split, and
+// at 31 leaves the per-split launch/latency chain was half of the iteration (profiles/README, round 3). The
+// sequence of splits it makes is a pure function of the gains: in best-first order a node is split iff it is
+// among the first B = num_leaves - 1 pops, and a node's gain never changes once its histogram exists. So
+// splits can be computed AHEAD of their turn and the sequential order recovered afterwards:
+//   bplan_kernel   replays the sequential best-first pops over the explored tree (nodes whose children's best
+//                  splits are known). The first pop of an unexplored node u is exactly the next split the
+//                  sequential learner would make; u and the next (spec_k - 1) unexplored nodes the replay
+//                  would pop if u's children did not overtake them are expanded together this round.
+//                  When the replay completes B pops (or runs out of positive gains) on explored nodes only,
+//                  the tree is final: it is written in sequential node / leaf numbering, identical to the
+//                  one-split-at-a-time result (expanded nodes that were never popped are simply leaves).
+//   bpart_kernel   partitions all expansions of the round in one launch (tiles of every segment)
+//   bhist_kernel   histograms of every expansion's smaller child (blocks shared out by row count)
+//   breduce_kernel exact int64 slab reduce per expansion (+ one allreduce of all of them, data-parallel)
+//   bfind_kernel   split search of both children of every expansion (larger = parent - smaller)
+// Trees are bit-identical to the sequential growth (same histograms, same subtraction side, same tie
+// breaks); the kernel count per tree drops from ~4 per split to ~5 per round, with ~B / spec_k rounds.
+// The host keeps one round ahead of the device and stops when the plan of a round reports the tree final.
+constexpr int kMaxSpec = 16;
+constexpr int kBatchMaxLeaves = 256;
+constexpr int kBatchMaxNodes = 1 + 2 * (2 * (kBatchMaxLeaves - 1) + kMaxSpec);
+
+struct BNode {
+  int32_t begin, count, buf, depth;  // local row segment
+  int64_t gcount;                    // global rows
+  double sum_g, sum_h, lo, hi;       // totals, monotone output bounds
+  double out;                        // output as a leaf (the parent's left_out / right_out; root 0)
+  int32_t c0, c1;                    // children (expanded) or -1
+};
+
+struct BExp {
+  int32_t node, c0, c1, left_small;
+  int32_t pbegin, pcount, pbuf, tile0;  // parent segment; first global partition tile of this expansion
+  PartSplit ps;
+  uint32_t cat[8];
+};
+
+struct BState {
+  int32_t nexp, done, nnodes, expanded;
+  int32_t spec_used, ntiles, cap_nodes, cap_exp;
+  unsigned long long cursor[kMaxSpec];
+  BExp exp[kMaxSpec];
+};
+
+// Histogram block budget per expansion (the slab holds kMaxHistBlocks blocks): HistBlocks(count) each, scaled
+// down proportionally (at least 1) when they do not fit. Deterministic in the counts, so bhist and breduce
+// agree on it.
+__device__ __forceinline__ void BatchHistAlloc(const int* cnt, int nexp, int* nb, int* off) {
+  int tot = 0;
+  for (int j = 0; j < nexp; ++j) { nb[j] = HistBlocks(cnt[j]); tot += nb[j]; }
+  if (tot > c_max_hist_blocks) {
+    const int spare = c_max_hist_blocks - nexp;
+    int t2 = 0;
+    for (int j = 0; j < nexp; ++j) { nb[j] = 1 + (nb[j] - 1) * spare / max(1, tot - nexp); t2 += nb[j]; }
+  }
+  int o = 0;
+  for (int j = 0; j < nexp; ++j) { off[j] = o; o += nb[j]; }
+}
+
+__device__ __forceinline__ int BatchSmallCount(const BState* bs, int j) {
+  const BExp& x = bs->exp[j];
+  const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+  return x.left_small ? lt : x.pcount - lt;
+}
+
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct SimKey {  // frontier entry order: larger gain, then smaller leaf index (the sequential argmax)
+  double gain;
+  int li, idx;
+};
+
+__device__ __forceinline__ bool SimBetter(const SimKey& x, const SimKey& y) {
+  if (x.gain != y.gain) return x.gain > y.gain;
+  return x.li < y.li;
+}
+
+constexpr int kPlanThreads = 1024;
+
+// round outcome for the host (coherent pinned memory, read after the plan's event): system-scope vector store
+__device__ __forceinline__ void SetHostFlag(int* f, int v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
+    BState* __restrict__ bs, BNode* __restrict__ nodes, SplitResult* __restrict__ nbest,
+    const SplitResult* __restrict__ fbest, int F, const double2* __restrict__ part, int E,
+    const DLeaf* __restrict__ leaves, DState* __restrict__ st, DTree t, FeatMeta fm, const int8_t* __restrict__ mono,
+    int has_mono, int first, int spec_k, int budget, int part_tile, int* __restrict__ host_flag) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int kWaves = kPlanThreads / 64;
+  __shared__ double s_gain[kBatchMaxNodes];
+  __shared__ int s_c0[kBatchMaxNodes], s_c1[kBatchMaxNodes], s_pop[kBatchMaxNodes];
+  __shared__ int f_node[kBatchMaxLeaves + 1], f_li[kBatchMaxLeaves + 1];
+  __shared__ double f_gain[kBatchMaxLeaves + 1];
+  __shared__ int p_node[kBatchMaxLeaves], p_li[kBatchMaxLeaves];
+  __shared__ int ch_node[kMaxSpec];
+  __shared__ int s_nnodes, s_nexp_prev;
+  if (first) {
+    if (tid == 0) {
+      const DLeaf R = leaves[0];
+      BNode r;
+      r.begin = R.begin; r.count = R.count; r.buf = R.buf; r.depth = 0;
+      r.gcount = R.gcount; r.sum_g = R.sum_g; r.sum_h = R.sum_h; r.lo = -INFINITY; r.hi = INFINITY;
+      r.out = 0.0; r.c0 = -1; r.c1 = -1;
+      nodes[0] = r;
+      bs->nexp = 0; bs->done = 0; bs->nnodes = 1; bs->expanded = 0; bs->spec_used = 0; bs->ntiles = 0;
+      bs->cap_exp = 2 * budget + kMaxSpec;
+      bs->cap_nodes = min(kBatchMaxNodes, 1 + 2 * bs->cap_exp);
+      s_nnodes = 1;
+      s_nexp_prev = 0;
+    }
+  } else {
+    if (bs->done) {
+      if (tid == 0) { bs->nexp = 0; SetHostFlag(host_flag, 1); }
+      return;
+    }
+    if (tid == 0) { s_nnodes = bs->nnodes; s_nexp_prev = bs->nexp; }
+  }
+  __syncthreads();
+  const int nnodes = s_nnodes, nexp = s_nexp_prev;
+  // ---- absorb: the children of last round's expansions (first: the root) get their best splits, global
+  // counts and row segments. One wave per child; lanes stride over features (ties: smaller feature).
+  const int nchild = first ? 1 : 2 * nexp;
+  for (int c = wid; c < nchild; c += kWaves) {
+    KeyG k{-INFINITY, 1 << 30, 0};
+    for (int f = lane; f < F; f += 64) {
+      const SplitResult& r = fbest[c * F + f];
+      if (r.feature < 0) continue;
+      KeyG cand{r.gain, f, 0};
+      if (KeyBetter(cand, k)) k = cand;
+    }
+    k = WaveArgmax(k);
+    if (lane == 0) {
+      int id;
+      if (first) {
+        id = 0;
+      } else {
+        const int j = c >> 1;
+        const BExp& x = bs->exp[j];
+        const int small = x.left_small ? x.c0 : x.c1;
+        id = (c & 1) ? (small == x.c0 ? x.c1 : x.c0) : small;
+        const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+        const int64_t small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
+        BNode& nd = nodes[id];
+        const bool is_left = id == x.c0;
+        nd.begin = is_left ? x.pbegin : x.pbegin + lt;
+        nd.count = is_left ? lt : x.pcount - lt;
+        nd.buf = x.pbuf == 0 ? 1 : 0;
+        nd.gcount = (c & 1) ? nodes[x.node].gcount - small_cnt : small_cnt;
+      }
+      if (k.gain == -INFINITY) {
+        nbest[id].feature = -1;
+        nbest[id].gain = -INFINITY;
+      } else {
+        nbest[id] = fbest[c * F + k.a];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- node gains and expansion links into LDS (the replay's dependent reads stay on chip)
+  for (int i = tid; i < nnodes; i += kPlanThreads) {
+    const SplitResult& r = nbest[i];
+    s_gain[i] = r.feature >= 0 ? r.gain : -INFINITY;
+    s_c0[i] = nodes[i].c0;
+    s_c1[i] = nodes[i].c1;
+    s_pop[i] = -1;
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  // ---- replay of the sequential best-first growth (one wave)
+  int nf = 1, pops = 0, nch = 0;
+  if (lane == 0) { f_node[0] = 0; f_li[0] = 0; f_gain[0] = s_gain[0]; }
+  WaveSync();
+  const int spec_room = max(1, min(spec_k, bs->cap_exp - bs->expanded));
+  const bool may_spec = bs->spec_used < budget && nnodes + 2 * spec_k <= bs->cap_nodes;
+  while (pops < budget) {
+    SimKey k{-INFINITY, 1 << 30, -1};
+    for (int i = lane; i < nf; i += 64) {
+      SimKey c{f_gain[i], f_li[i], i};
+      if (c.gain > -INFINITY && SimBetter(c, k)) k = c;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      SimKey o;
+      o.gain = __shfl_xor(k.gain, off, 64);
+      o.li = __shfl_xor(k.li, off, 64);
+      o.idx = __shfl_xor(k.idx, off, 64);
+      if (SimBetter(o, k)) k = o;
+    }
+    if (k.idx < 0 || !(k.gain > 0.0)) break;
+    const int v = f_node[k.idx];
+    if (v < 0 || v >= nnodes || nf > kBatchMaxLeaves - 1) {  // invariant broken: stop (host raises), never fault
+      if (lane == 0) { bs->done = 1; bs->nexp = 0; SetHostFlag(host_flag, 2); }
+      return;
+    }
+    const bool explored = s_c0[v] >= 0;
+    if (lane == 0) {
+      const int last = nf - 1;  // the popped entry is replaced by the last one
+      f_node[k.idx] = f_node[last]; f_li[k.idx] = f_li[last]; f_gain[k.idx] = f_gain[last];
+      if (explored) {
+        const int a = s_c0[v], b = s_c1[v];
+        f_node[last] = a; f_li[last] = k.li; f_gain[last] = s_gain[a];
+        f_node[last + 1] = b; f_li[last + 1] = pops + 1; f_gain[last + 1] = s_gain[b];
+        p_node[pops] = v; p_li[pops] = k.li;
+        s_pop[v] = pops;
+      } else {
+        ch_node[nch] = v;
+      }
+    }
+    nf = explored ? nf + 1 : nf - 1;
+    if (!explored) {
+      ++nch;
+      if (nch >= spec_room || !may_spec) { ++pops; break; }
+    }
+    ++pops;
+    WaveSync();
+  }
+  WaveSync();
+  if (nch == 0) {
+    // ---- the tree is final: write it in sequential numbering. Pop i = internal node i; its left child
+    // keeps the popped leaf's index, its right child gets leaf index i + 1.
+    const int nl = pops + 1;
+    for (int i = lane; i < pops; i += 64) {
+      const int v = p_node[i];
+      const SplitResult sr = nbest[v];
+      const BNode P = nodes[v];
+      const int a = s_c0[v], b = s_c1[v];
+      t.feat[i] = sr.feature;
+      t.thr[i] = sr.threshold;
+      t.dleft[i] = sr.default_left;
+      t.is_cat[i] = sr.is_cat;
+      for (int w = 0; w < 8; ++w) t.cat_bits[i * 8 + w] = sr.cat_bits[w];
+      t.left[i] = s_pop[a] >= 0 ? s_pop[a] : ~p_li[i];
+      t.right[i] = s_pop[b] >= 0 ? s_pop[b] : ~(i + 1);
+      t.gain[i] = sr.gain;
+      t.ival[i] = P.out;
+      t.iweight[i] = sr.left_h + sr.right_h;
+      t.icount[i] = P.gcount;
+    }
+    // leaves: the final frontier (every entry is a node never popped) plus, for a stump, the root
+    for (int i = lane; i < nf; i += 64) {
+      const int v = f_node[i], li = f_li[i];
+      const BNode L = nodes[v];
+      t.lval[li] = L.out;
+      t.lweight[li] = L.sum_h;
+      t.lcount[li] = L.gcount;
+      t.ldepth[li] = L.depth;
+    }
+    // parent of each leaf: the pop that created it (leaf index li of a child of pop i: left = p_li[i], right = i+1)
+    for (int i = lane; i < pops; i += 64) {
+      const int v = p_node[i];
+      if (s_pop[s_c0[v]] < 0) t.lparent[p_li[i]] = i;
+      if (s_pop[s_c1[v]] < 0) t.lparent[i + 1] = i;
+    }
+    if (lane == 0) {
+      if (pops == 0) t.lparent[0] = -1;
+      st->num_leaves = nl;
+      st->done = 1;
+      bs->done = 1;
+      bs->nexp = 0;
+      SetHostFlag(host_flag, 1);
+    }
+    return;
+  }
+  // ---- plan this round's expansions: ch_node[0] is the sequential learner's next split, the rest are
+  // speculative (counted against the waste budget spec_used < budget)
+  const int base = nnodes;
+  if (lane < nch) {
+    const int j = lane, v = ch_node[j];
+    const SplitResult sr = nbest[v];
+    const BNode P = nodes[v];
+    const int a = base + 2 * j, b = a + 1;
+    BNode L = P, R = P;
+    L.depth = R.depth = P.depth + 1;
+    L.sum_g = sr.left_g; L.sum_h = sr.left_h; L.out = sr.left_out;
+    R.sum_g = sr.right_g; R.sum_h = sr.right_h; R.out = sr.right_out;
+    L.c0 = L.c1 = R.c0 = R.c1 = -1;
+    const int mdir = (has_mono && !sr.is_cat) ? static_cast<int>(mono[sr.feature]) : 0;
+    if (mdir != 0) {
+      const double mid = (sr.left_out + sr.right_out) / 2.0;
+      if (mdir < 0) { L.lo = fmax(L.lo, mid); R.hi = fmin(R.hi, mid); }
+      else { L.hi = fmin(L.hi, mid); R.lo = fmax(R.lo, mid); }
+    }
+    nodes[a] = L;
+    nodes[b] = R;
+    nodes[v].c0 = a;
+    nodes[v].c1 = b;
+    BExp x;
+    x.node = v; x.c0 = a; x.c1 = b;
+    x.left_small = sr.left_cnt <= sr.right_cnt ? 1 : 0;
+    x.pbegin = P.begin; x.pcount = P.count; x.pbuf = P.buf;
+    x.ps.feature = sr.feature;
+    x.ps.is_cat = sr.is_cat;
+    x.ps.dleft = sr.default_left;
+    x.ps.thr = sr.threshold;
+    x.ps.nb = fm.num_bin[sr.feature];
+    x.ps.mt = fm.missing[sr.feature];
+    x.ps.dbin = fm.default_bin[sr.feature];
+    for (int w = 0; w < 8; ++w) x.cat[w] = sr.is_cat ? sr.cat_bits[w] : 0u;
+    // first global tile: prefix over the expansions' tile counts
+    const int nt = (P.count + part_tile - 1) / part_tile;
+    int pre = nt;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const int o = __shfl_up(pre, off, 64);
+      if (lane >= off) pre += o;
+    }
+    x.tile0 = pre - nt;
+    bs->exp[j] = x;
+    bs->cursor[j] = 0ull;
+    if (j == nch - 1) bs->ntiles = pre;
+  }
+  if (lane == 0) {
+    bs->nexp = nch;
+    bs->nnodes = base + 2 * nch;
+    bs->expanded += nch;
+    bs->spec_used += nch - 1;
+    SetHostFlag(host_flag, 0);
+  }
+}
+
+template <int kPartRows>
+__global__ __launch_bounds__(kPartThreads) void bpart_kernel(
+    BState* __restrict__ bs, const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
+    const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
+    int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1, float2* __restrict__ wogh0,
+    float2* __restrict__ wogh1, const float* __restrict__ g, const float* __restrict__ h) {
+  const int nexp = bs->nexp;
+  if (nexp == 0) return;
+  const int ntiles = bs->ntiles;
+  if (static_cast<int>(blockIdx.x) >= ntiles) return;
+  __shared__ int s_tile0[kMaxSpec];
+  __shared__ uint32_t s_cat[kMaxSpec][8];
+  const int tid = threadIdx.x;
+  if (tid < nexp) s_tile0[tid] = bs->exp[tid].tile0;
+  if (tid < nexp * 8) s_cat[tid >> 3][tid & 7] = bs->exp[tid >> 3].cat[tid & 7];
+  __syncthreads();
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int j = 0;
+    while (j + 1 < nexp && s_tile0[j + 1] <= tile) ++j;
+    const BExp& x = bs->exp[j];
+    const PartSplit ps = x.ps;
+    PartitionTile<kPartRows>(ps, s_cat[j], tile - s_tile0[j], x.pbegin, x.pcount, x.pbuf, &bs->cursor[j], cbins, n,
+                             perm0, perm1, ogh0, ogh1, wperm0, wperm1, wogh0, wogh1, g, h);
+  }
+}
+
+template <int kUnroll, int kFPG>
+__global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
+    const BState* __restrict__ bs, const uint4* __restrict__ bins4, int W4, int F, const int32_t* __restrict__ perm0,
+    const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
+    const float* __restrict__ g, const float* __restrict__ h, const float* __restrict__ ghmax,
+    ulonglong2* __restrict__ slab) {
+  const int nexp = bs->nexp;
+  if (nexp == 0) return;
+  __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < nexp; ++q) s_cnt[q] = BatchSmallCount(bs, q);
+    BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
+  }
+  __syncthreads();
+  const int bx = blockIdx.x;
+  int j = -1;
+  for (int q = 0; q < nexp; ++q) if (bx >= s_off[q] && bx < s_off[q] + s_nb[q]) j = q;
+  if (j < 0) return;
+  const BExp& x = bs->exp[j];
+  const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+  const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
+  HistBody<kUnroll, kFPG>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
+                          ogh1, g, h, ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature);
+}
+
+// grid (ceil(E / kRedE), spec_k): block (x, j) reduces the slabs of expansion j into part[j * (E + 1) ..]
+__global__ __launch_bounds__(kRedE * kRedG) void breduce_kernel(const BState* __restrict__ bs,
+                                                                 const ulonglong2* __restrict__ slab, int E,
+                                                                 const float* __restrict__ ghmax,
+                                                                 double2* __restrict__ part) {
+  const int nexp = bs->nexp;
+  const int j = blockIdx.y;
+  if (j >= nexp) return;
+  const int tid = threadIdx.x, le = tid % kRedE, grp = tid / kRedE;
+  __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
+  if (tid == 0) {
+    for (int q = 0; q < nexp; ++q) s_cnt[q] = BatchSmallCount(bs, q);
+    BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
+  }
+  __syncthreads();
+  const int count = s_cnt[j];
+  const int nbj = s_nb[j], offj = s_off[j];
+  const int e = blockIdx.x * kRedE + le;
+  const bool valid = e < E;
+  unsigned long long sg = 0, sh = 0;
+  if (valid) {
+    const ulonglong2* sl = slab + static_cast<size_t>(offj) * E;
+#pragma unroll 8
+    for (int b = grp; b < nbj; b += kRedG) {
+      const ulonglong2 v = sl[static_cast<size_t>(b) * E + e];
+      sg += v.x;
+      sh += v.y;
+    }
+  }
+  __shared__ unsigned long long rg[kRedG][kRedE], rh[kRedG][kRedE];
+  rg[grp][le] = sg;
+  rh[grp][le] = sh;
+  __syncthreads();
+  double2* out = part + static_cast<size_t>(j) * (E + 1);
+  if (grp == 0 && valid) {
+    unsigned long long tg = 0, th = 0;
+#pragma unroll
+    for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
+    const HScale s = HistScale(count, ghmax);
+    const int F = E / kBinsPerFeature;
+    const int bin = e / F, f = e - bin * F;
+    out[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
+                                                  static_cast<double>(static_cast<long long>(th)) * s.ih);
+  }
+  if (blockIdx.x == 0 && tid == 0) out[E] = make_double2(static_cast<double>(count), 0.0);
+}
+
+// grid (F, 2 * spec_k): block (f, 2j + c) searches feature f of expansion j's smaller (c = 0) or larger (c = 1)
+// child; the larger child's histogram is the parent's minus the smaller's. Both go to the pool (slot = node id).
+__global__ __launch_bounds__(256) void bfind_kernel(const BState* __restrict__ bs, const BNode* __restrict__ nodes,
+                                                    const double2* __restrict__ part, int E,
+                                                    double2* __restrict__ hist_pool, FeatMeta fm, SplitParams sp,
+                                                    SplitResult* __restrict__ fbest, int F) {
+  const int j = blockIdx.y >> 1, c = blockIdx.y & 1;
+  if (j >= bs->nexp) return;
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const BExp& x = bs->exp[j];
+  const int small = x.left_small ? x.c0 : x.c1;
+  const int child = c == 0 ? small : (small == x.c0 ? x.c1 : x.c0);
+  const double2* pj = part + static_cast<size_t>(j) * (E + 1);
+  const int e = f * kBinsPerFeature + tid;
+  const double2 sm = pj[e];
+  double2 mine = sm;
+  if (c == 1) {
+    const double2 par = hist_pool[static_cast<size_t>(x.node) * E + e];
+    mine = make_double2(par.x - sm.x, par.y - sm.y);
+  }
+  hist_pool[static_cast<size_t>(child) * E + e] = mine;
+  const BNode nd = nodes[child];
+  const int64_t small_cnt = static_cast<int64_t>(pj[E].x);
+  const int64_t cnt = c == 0 ? small_cnt : nodes[x.node].gcount - small_cnt;
+  SearchFeatureBlock(mine, nd.sum_g, nd.sum_h, cnt, nd.depth, 0, nd.lo, nd.hi, f, F, fm, sp,
+                     fbest + static_cast<size_t>(blockIdx.y) * F + f, true);
 }
 
 // ---------------------------------------------------------------- K7
@@ -2207,6 +2704,8 @@ class GpuBackend : public TrainBackend {
     if (ev_sync_) (void)hipEventDestroy(ev_sync_);
     for (hipEvent_t e : comm_ev_) if (e) (void)hipEventDestroy(e);
     if (pinned_) (void)hipHostFree(pinned_);
+    for (hipEvent_t e : bev_) if (e) (void)hipEventDestroy(e);
+    if (bflag_host_) (void)hipHostFree(bflag_host_);
   }
   std::string Name() const override { return "hip"; }
 
@@ -2252,8 +2751,25 @@ class GpuBackend : public TrainBackend {
     h_.alloc(static_cast<size_t>(n_) * K);
     for (int b = 0; b < 2; ++b) { perm_[b].alloc(n_); ogh_[b].alloc(n_); }
     slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * E_);
-    part_.alloc(static_cast<size_t>(E_) + 1);  // histogram + (row count, 0)
-    hist_pool_.alloc(static_cast<size_t>(2 * L_ + 2) * E_);
+    // batched speculative growth (bplan_kernel ..): one-split-at-a-time stays for voting, bynode sampling,
+    // num_leaves > 256 and SML_GBDT_SPEC=0; SML_GBDT_SPEC=k sets the expansions per round (default 8)
+    spec_k_ = 8;
+    if (const char* e = std::getenv("SML_GBDT_SPEC")) spec_k_ = std::atoi(e);
+    batch_ok_ = spec_k_ > 0 && L_ <= kBatchMaxLeaves && !(cfg.tree_learner == "voting" && comm_ && comm_->world() > 1);
+    spec_k_ = std::max(1, std::min(kMaxSpec, spec_k_));
+    if (const char* e = std::getenv("SML_GBDT_LOOKAHEAD")) blook_ = std::max(1, std::min(4, std::atoi(e)));
+    const int cap_nodes = std::min(kBatchMaxNodes, 1 + 2 * (2 * (L_ - 1) + kMaxSpec));
+    // histogram + (row count, 0) per expansion of a round
+    part_.alloc(static_cast<size_t>(E_ + 1) * (batch_ok_ ? kMaxSpec : 1));
+    hist_pool_.alloc(static_cast<size_t>(std::max(2 * L_ + 2, batch_ok_ ? cap_nodes : 0)) * E_);
+    if (batch_ok_) {
+      bstate_.alloc(1);
+      bnodes_.alloc(cap_nodes);
+      nbest_.alloc(cap_nodes);
+      SML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&bflag_host_), sizeof(int) * kBRing, hipHostMallocMapped | hipHostMallocCoherent));
+      SML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&bflag_dev_), bflag_host_, 0));
+      for (hipEvent_t& e : bev_) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     // launch-shape knobs for A/B runs (defaults are the measured best)
     if (const char* e = std::getenv("SML_PART_ROWS")) part_rows_ = std::atoi(e);
     if (part_rows_ != 4 && part_rows_ != 8 && part_rows_ != 16) part_rows_ = kPartRowsDefault;
@@ -2323,7 +2839,7 @@ class GpuBackend : public TrainBackend {
       ymax_ = -1.0;  // max |label|: computed when a cross-entropy prep pass first needs it
       ghbound_.alloc(2);
     }
-    fbest_.alloc(2 * F_);
+    fbest_.alloc(static_cast<size_t>(2) * F_ * (batch_ok_ ? kMaxSpec : 1));
     lbest_.alloc(L_);
     lgain_.alloc(L_);
     leaves_.alloc(L_);
@@ -2664,6 +3180,12 @@ class GpuBackend : public TrainBackend {
       EnqueueHistogram(g, h);
     }
     EnqueueFindChoose(false);
+    if (batch_ok_ && sp_.bynode_k <= 0 && !voting_) {
+      GrowBatched(g, h);
+      final_v_ = 0;
+      SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
+      return;
+    }
     for (int s = 1; s < L_; ++s) {
       // choose + partition the chosen leaf, histogram its smaller child, search both
       DState* sin = st_cur_;
@@ -2686,6 +3208,63 @@ class GpuBackend : public TrainBackend {
     }
     final_v_ = st_cur_ == state_ ? 0 : 1;
     SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  }
+
+  // Rounds of the batched speculative growth (see bplan_kernel). The host stays blook_ rounds ahead: before
+  // enqueueing round r it waits for the plan of round r - blook_ and stops once a plan reported the tree
+  // final (the rounds already queued behind it are no-ops).
+  void GrowBatched(const float* g, const float* h) {
+    TraceRange tr("sml::GrowBatched");
+    const int budget = L_ - 1;
+    const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
+    const int part_tile = kPartThreads * part_rows_;
+    const int max_rounds = budget + 2;
+    auto bp = part_rows_ == 16 ? bpart_kernel<16> : (part_rows_ == 4 ? bpart_kernel<4> : bpart_kernel<8>);
+    auto bh = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16>
+              : (hist_unroll4_ ? bhist_kernel<4, kFeatPerGroup> : bhist_kernel<kHistUnroll, kFeatPerGroup>);
+    int r = 0;
+    for (; r <= max_rounds; ++r) {
+      if (r >= blook_) {
+        const int q = r - blook_;
+        SpinEvent(bev_[q % kBRing]);
+        const int fl = bflag_host_[q % kBRing];
+        if (fl == 2) throw std::runtime_error("batched tree growth: device replay invariant violated");
+        if (fl) break;
+      }
+      hipLaunchKernelGGL(bplan_kernel, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
+                         nbest_.get(), fbest_.get(), F_, part_.get(), E_, leaves_.get(), state_, dt_, fm_, mono_.get(),
+                         sp_.has_mono, r == 0 ? 1 : 0, spec_k_, budget, part_tile, bflag_dev_ + r % kBRing);
+      SML_HIP_CHECK(hipGetLastError());
+      SML_HIP_CHECK(hipEventRecord(bev_[r % kBRing], stream_));
+      hipLaunchKernelGGL(bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
+                         perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), perm_[0].get(), perm_[1].get(),
+                         ogh_[0].get(), ogh_[1].get(), g, h);
+      SML_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(bh, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_,
+                         bstate_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
+                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(breduce_kernel, dim3((E_ + kRedE - 1) / kRedE, spec_k_), dim3(kRedE * kRedG), 0, stream_,
+                         bstate_.get(), slab_.get(), E_, ghmax, part_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      // every expansion's smaller-child histogram + row count in ONE collective per round
+      if (Distributed()) TimedAllReduce(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_ + 1) * 2 * spec_k_);
+      hipLaunchKernelGGL(bfind_kernel, dim3(F_, 2 * spec_k_), dim3(256), 0, stream_, bstate_.get(), bnodes_.get(),
+                         part_.get(), E_, hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
+      SML_HIP_CHECK(hipGetLastError());
+    }
+    if (r > max_rounds) throw std::runtime_error("batched tree growth did not finish within num_leaves rounds");
+  }
+
+  // spin on an event (a blocking sync can sleep through the few microseconds the batched growth waits);
+  // data-parallel runs poll the communicator and honour time_out like WaitEvent
+  void SpinEvent(hipEvent_t ev) {
+    if (Distributed()) { WaitEvent(ev); return; }
+    for (;;) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) SML_HIP_CHECK(q);
+    }
   }
 
   // the finished tree (state + arrays: one allocation) -> pinned host memory, one transfer
@@ -3163,6 +3742,17 @@ class GpuBackend : public TrainBackend {
   std::vector<std::unique_ptr<DeviceValidSet>> vsets_;
   DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_;
   int32_t* flags_ = nullptr;
+  // batched speculative growth
+  static constexpr int kBRing = 8;
+  bool batch_ok_ = false;
+  int spec_k_ = 8;
+  int blook_ = 1;
+  DevBuf<BState> bstate_;
+  DevBuf<BNode> bnodes_;
+  DevBuf<SplitResult> nbest_;
+  int* bflag_host_ = nullptr;
+  int* bflag_dev_ = nullptr;
+  hipEvent_t bev_[kBRing] = {};
   DTree dt_{};
   FeatMeta fm_{};
   void* pinned_ = nullptr;

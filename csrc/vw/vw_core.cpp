@@ -245,31 +245,80 @@ void VW::ForEachFeature(const Example& ex, F&& fn) const {
     if (ignored(n.ns)) continue;
     for (const auto& f : n.f) fn(f.idx, f.x);
   }
-  // interactions
+  // interactions (VW semantics): a ':' position is a wildcard over the namespaces present in the example
+  // (constant namespace excluded), expanded to combinations with repetition - `-q ::` over {a,b,c} is aa ab
+  // ac bb bc cc, each unordered namespace multiset once; adjacent positions naming the same namespace keep
+  // only non-decreasing feature positions (no duplicate permutations of a self-interaction), as VW does
+  // without --leave_duplicate_interactions. Hash: ((f1 * FNV) ^ f2) [* FNV ^ f3].
+  if (interactions_.empty()) { if (constant_) fn(static_cast<uint64_t>(kConstantHash), 1.f); return; }
+  const std::vector<Feature>* by_char[256] = {};
+  unsigned char present[256];
+  int npresent = 0;
+  for (const auto& n : ex.ns) {
+    if (n.ns == kConstantNamespace || ignored(n.ns) || n.f.empty()) continue;
+    if (!by_char[n.ns]) present[npresent++] = n.ns;
+    by_char[n.ns] = &n.f;
+  }
+  std::sort(present, present + npresent);
+  auto pair = [&](unsigned char ca, unsigned char cb) {
+    const auto* A = by_char[ca];
+    const auto* B = by_char[cb];
+    if (!A || !B) return;
+    const bool same = ca == cb;
+    for (size_t i = 0; i < A->size(); ++i) {
+      const uint64_t h1 = (*A)[i].idx * kFnvPrime;
+      const float x1 = (*A)[i].x;
+      for (size_t j = same ? i : 0; j < B->size(); ++j) fn(h1 ^ (*B)[j].idx, x1 * (*B)[j].x);
+    }
+  };
+  auto triple = [&](unsigned char c1, unsigned char c2, unsigned char c3) {
+    const auto* A = by_char[c1];
+    const auto* B = by_char[c2];
+    const auto* C = by_char[c3];
+    if (!A || !B || !C) return;
+    const bool s12 = c1 == c2, s23 = c2 == c3;
+    for (size_t i = 0; i < A->size(); ++i)
+      for (size_t j = s12 ? i : 0; j < B->size(); ++j) {
+        const uint64_t h12 = (((*A)[i].idx * kFnvPrime) ^ (*B)[j].idx) * kFnvPrime;
+        const float x12 = (*A)[i].x * (*B)[j].x;
+        for (size_t k = s23 ? j : 0; k < C->size(); ++k) fn(h12 ^ (*C)[k].idx, x12 * (*C)[k].x);
+      }
+  };
   for (const auto& inter : interactions_) {
-    if (inter.size() == 2) {
-      const Namespace* a = nullptr;
-      const Namespace* b = nullptr;
-      for (const auto& n : ex.ns) {
-        if (n.ns == static_cast<unsigned char>(inter[0]) || inter[0] == ':') a = &n;
-        if (n.ns == static_cast<unsigned char>(inter[1]) || inter[1] == ':') b = &n;
-      }
-      if (!a || !b) continue;
-      const bool same = a == b;
-      for (size_t i = 0; i < a->f.size(); ++i) {
-        const uint64_t h1 = a->f[i].idx * kFnvPrime;
-        for (size_t j = same ? i : 0; j < b->f.size(); ++j) fn(h1 ^ b->f[j].idx, a->f[i].x * b->f[j].x);
-      }
-    } else if (inter.size() == 3) {
-      const Namespace* n3[3] = {nullptr, nullptr, nullptr};
-      for (int q = 0; q < 3; ++q)
-        for (const auto& n : ex.ns) if (n.ns == static_cast<unsigned char>(inter[q])) n3[q] = &n;
-      if (!n3[0] || !n3[1] || !n3[2]) continue;
-      for (const auto& f1 : n3[0]->f)
-        for (const auto& f2 : n3[1]->f) {
-          const uint64_t h12 = ((f1.idx * kFnvPrime) ^ f2.idx) * kFnvPrime;
-          for (const auto& f3 : n3[2]->f) fn(h12 ^ f3.idx, f1.x * f2.x * f3.x);
+    const size_t m = inter.size();
+    if (m != 2 && m != 3) continue;
+    bool wild = false;
+    for (char c : inter) wild |= c == ':';
+    if (!wild) {
+      if (m == 2) pair(static_cast<unsigned char>(inter[0]), static_cast<unsigned char>(inter[1]));
+      else triple(static_cast<unsigned char>(inter[0]), static_cast<unsigned char>(inter[1]),
+                  static_cast<unsigned char>(inter[2]));
+      continue;
+    }
+    // expand the wildcard positions over the present namespaces; keep each namespace multiset once (the
+    // first expansion in sorted order, so `::` yields ab, never ba)
+    std::vector<std::array<unsigned char, 3>> seen;
+    std::array<int, 3> it{0, 0, 0};
+    while (true) {
+      std::array<unsigned char, 3> c{0, 0, 0};
+      for (size_t q = 0; q < m; ++q)
+        c[q] = inter[q] == ':' ? (npresent ? present[it[q]] : 0) : static_cast<unsigned char>(inter[q]);
+      if (npresent) {
+        std::array<unsigned char, 3> key = c;
+        std::sort(key.begin(), key.begin() + m);
+        if (std::find(seen.begin(), seen.end(), key) == seen.end()) {
+          seen.push_back(key);
+          if (m == 2) pair(c[0], c[1]); else triple(c[0], c[1], c[2]);
         }
+      }
+      // odometer over the wildcard positions (last position fastest)
+      int q = static_cast<int>(m) - 1;
+      for (; q >= 0; --q) {
+        if (inter[q] != ':') continue;
+        if (++it[q] < npresent) break;
+        it[q] = 0;
+      }
+      if (q < 0 || !npresent) break;
     }
   }
   if (constant_) fn(static_cast<uint64_t>(kConstantHash), 1.f);

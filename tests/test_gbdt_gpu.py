@@ -21,6 +21,35 @@ def _data(n=60000, f=12, seed=0, nan_frac=0.0, cat=False):
     return X, y
 
 
+def _tree_blocks(model: str):
+    return model.split("end of trees")[0].split("Tree=")[1:]
+
+
+def _field(block: str, key: str):
+    lines = [l for l in block.splitlines() if l.startswith(key + "=")]
+    return lines[0].split("=", 1)[1] if lines else None
+
+
+def _assert_same_trees(mc: str, mg: str, rtol=1e-6, atol=1e-8):
+    """Every tree of the device model equals the fp64 host oracle's: identical structure (split features,
+    bin thresholds, decision types, children, leaf and node row counts) and node / leaf values to the
+    precision the int64 fixed-point histograms allow (plus ulp-level differences of device exp/log in the
+    gradients of non-quadratic objectives)."""
+    tc, tg = _tree_blocks(mc), _tree_blocks(mg)
+    assert len(tc) == len(tg)
+    for i, (a, b) in enumerate(zip(tc, tg)):
+        for k in ("num_leaves", "split_feature", "threshold", "decision_type", "left_child", "right_child",
+                  "leaf_count", "internal_count", "num_cat", "cat_boundaries", "cat_threshold"):
+            assert _field(a, k) == _field(b, k), (i, k)
+        for k in ("leaf_value", "internal_value", "internal_weight", "leaf_weight", "split_gain"):
+            va, vb = _field(a, k), _field(b, k)
+            if va is None:
+                assert vb is None
+                continue
+            np.testing.assert_allclose(np.array(vb.split(), float), np.array(va.split(), float), rtol=rtol,
+                                       atol=atol, err_msg=f"tree {i} {k}")
+
+
 def _train(X, y, params, iters):
     from synapseml_amd.ops import native
 
@@ -45,15 +74,8 @@ def test_gpu_trees_match_cpu(extra):
     bg = _train(X, y, base + " device_type=gpu", 5)
     assert bg.backend == "hip"
     mc, mg = bc.save_model_string(), bg.save_model_string()
-    # the first tree must be identical in structure (same splits)
-    t0c = mc.split("Tree=0")[1].split("Tree=1")[0]
-    t0g = mg.split("Tree=0")[1].split("Tree=1")[0]
-    line = lambda s, k: [l for l in s.splitlines() if l.startswith(k + "=")][0]
-    assert line(t0c, "split_feature") == line(t0g, "split_feature")
-    assert line(t0c, "threshold") == line(t0g, "threshold")
-    lc = np.array(line(t0c, "leaf_value").split("=")[1].split(), float)
-    lg = np.array(line(t0g, "leaf_value").split("=")[1].split(), float)
-    np.testing.assert_allclose(lc, lg, rtol=1e-4, atol=1e-6)
+    # every tree identical to the host oracle (structure, counts; values to the histogram precision)
+    _assert_same_trees(mc, mg)
     pc = bc.predict(X, 0, 0, -1)[:, 0]
     pg = bg.predict(X, 0, 0, -1)[:, 0]
     assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 2e-3
@@ -95,9 +117,11 @@ def test_gpu_missing_and_categorical():
     bc = _train(X, y, p + " device_type=cpu", 8)
     bg = _train(X, y, p + " device_type=gpu", 8)
     assert bg.backend == "hip"
+    # NaN (missing-bin default directions) and categorical bitset splits: tree for tree the host's
+    _assert_same_trees(bc.save_model_string(), bg.save_model_string())
     pc = bc.predict(X, 1, 0, -1)[:, 0]
     pg = bg.predict(X, 1, 0, -1)[:, 0]
-    assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 5e-3
+    assert abs(roc_auc_score(y, pc) - roc_auc_score(y, pg)) < 1e-6
     np.testing.assert_allclose(bg.train_scores(), bg.predict(X, 0, 0, -1)[:, 0], rtol=1e-5, atol=1e-5)
 
 
@@ -112,9 +136,10 @@ def test_gpu_objectives(obj):
         y = (X[:, 0] * 2 + X[:, 1] ** 2).astype(np.float32)
     bc = _train(X, y, f"objective={obj} device_type=cpu", 5)
     bg = _train(X, y, f"objective={obj} device_type=gpu", 5)
+    _assert_same_trees(bc.save_model_string(), bg.save_model_string())
     pc = bc.predict(X, 1, 0, -1)
     pg = bg.predict(X, 1, 0, -1)
-    assert np.corrcoef(pc.ravel(), pg.ravel())[0, 1] > 0.999
+    np.testing.assert_allclose(pg, pc, rtol=1e-6, atol=1e-9)
 
 
 def test_gpu_bagging_goss_rf():
@@ -552,3 +577,25 @@ def test_gpu_ranking_metrics_on_device():
     assert {"ndcg@1", "ndcg@10", "map@3"} <= dev.keys()
     _assert_device_metrics_match_host(b, 0)
     np.testing.assert_allclose(b.valid_scores(0), b.predict(Xv, 0, 0, -1)[:, 0], rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5", "num_leaves=63 max_depth=5",
+                                   "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
+                                   "num_leaves=2", "num_leaves=31 min_gain_to_split=5.0",
+                                   "num_leaves=31 objective=multiclass num_class=3"])
+@pytest.mark.parametrize("spec", ["1", "3", "16"])
+def test_gpu_batched_growth_equals_sequential(extra, spec, monkeypatch):
+    """Batched speculative growth (bplan_kernel ..; SML_GBDT_SPEC=k expansions per round) builds exactly the
+    trees of the one-split-at-a-time growth (SML_GBDT_SPEC=0): byte-identical model text, for small / deep /
+    depth-capped / categorical + monotone / stump-like / gain-limited / multiclass trees."""
+    X, y = _data(n=80000, nan_frac=0.02, cat="categorical" in extra)
+    if "multiclass" in extra:
+        y = (np.digitize(np.nan_to_num(X[:, 0] + X[:, 1]), [-0.5, 0.5])).astype(np.float32)
+    p = ("objective=binary " if "objective" not in extra else "") + f"learning_rate=0.2 {extra} device_type=gpu"
+
+    def fit(k):
+        monkeypatch.setenv("SML_GBDT_SPEC", k)
+        return _train(X, y, p, 6).save_model_string()
+
+    seq, bat = fit("0"), fit(spec)
+    assert bat == seq

@@ -518,3 +518,57 @@ def test_set_initial_model_from_fitted_model():
     err = lambda m: float(np.mean((m.transform(df)["prediction"] - y) ** 2))  # noqa: E731
     assert err(warm) < err(cold)
     assert VowpalWabbitRegressor().setInitialModel(first.getModel()).getInitialModel() == bytes(first.getModel())
+
+
+def _touched(args, blocks):
+    """weight-table slots an example's features touch in the native learner (one squared-loss update)"""
+    from synapseml_amd.ops import native
+
+    vw = native.load("_vw").VW(args + " --noconstant -b 24")
+    vw.learn_batch(blocks, np.ones(1, np.float32), None, None, None, True)
+    lines = vw.readable_model().split("Checksum: 0\n:0\n", 1)[1].strip().splitlines()
+    return {int(l.split(":")[0]) for l in lines if l}
+
+
+def _one_row(feats):
+    return [(g, np.array([0, len(ix)], np.int64), np.array(ix, np.uint32), np.array(xs, np.float32))
+            for g, ix, xs in feats]
+
+
+def test_wildcard_and_cubic_interactions_vw_semantics():
+    """`-q ::` expands to the combinations with repetition of the namespaces present (aa ab ac bb bc cc, each
+    unordered pair once, first namespace = the smaller), `-q a:` to a crossed with every namespace, and
+    `--cubic :::` / `--cubic aab` keep non-decreasing feature positions inside repeated namespaces (VW without
+    --leave_duplicate_interactions). Hash (a * FNV) ^ b [* FNV ^ c], masked to the table."""
+    P, M = 16777619, (1 << 24) - 1
+    A, B, C = [1, 2], [10], [100, 101]
+    blocks = _one_row([("c", C, [2.0, 1.0]), ("a", A, [1.0, 0.5]), ("b", B, [1.0])])  # unsorted on purpose
+    base = set(A + B + C)
+
+    def q(x, y, same):
+        return {((i * P) ^ j) & M for k, i in enumerate(x) for l, j in enumerate(y) if not same or l >= k}
+
+    def cub(x, y, z, s12, s23):
+        out = set()
+        for i1, a in enumerate(x):
+            for i2, b in enumerate(y):
+                if s12 and i2 < i1:
+                    continue
+                for i3, c in enumerate(z):
+                    if s23 and i3 < i2:
+                        continue
+                    out.add(((((a * P) ^ b) * P) ^ c) & M)
+        return out
+
+    exp_qq = base | q(A, A, 1) | q(A, B, 0) | q(A, C, 0) | q(B, B, 1) | q(B, C, 0) | q(C, C, 1)
+    assert _touched("-q ::", blocks) == {x & M for x in exp_qq}
+    exp_qa = base | q(A, A, 1) | q(A, B, 0) | q(A, C, 0)
+    assert _touched("-q a:", blocks) == {x & M for x in exp_qa}
+    ns = {"a": A, "b": B, "c": C}
+    exp_c = set(base)
+    for t in ("aaa", "aab", "aac", "abb", "abc", "acc", "bbb", "bbc", "bcc", "ccc"):
+        exp_c |= cub(ns[t[0]], ns[t[1]], ns[t[2]], t[0] == t[1], t[1] == t[2])
+    assert _touched("--cubic :::", blocks) == {x & M for x in exp_c}
+    assert _touched("--cubic aab", blocks) == {x & M for x in base | cub(A, A, B, True, False)}
+    # an explicit pair is NOT canonicalised: -q ba hashes b first
+    assert _touched("-q ba", blocks) == {x & M for x in base | q(B, A, 0)}
