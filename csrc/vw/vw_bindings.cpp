@@ -1,6 +1,7 @@
 // pybind11 module `synapseml_amd._vw`: VW-style learner + hashing + GPU SGD.
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
+#include <array>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <rccl/rccl.h>
@@ -96,6 +97,102 @@ PYBIND11_MODULE(_vw, m) {
     }
     return out;
   }, py::arg("bytes"), py::arg("offsets"), py::arg("seed"), py::arg("mask") = 0xFFFFFFFFu, py::arg("device") = false);
+  // Text examples -> the GPU learner's columnar form (VowpalWabbitGeneric, deviceType="gpu"). Single-line:
+  // {"blocks": [(ns, indptr, idx, val)] over rows, "labels", "weights", "multiclass", "cptr", "ccls", "ccost"}.
+  // Multi-line (blank-line separated ADF groups, optional "shared" first line): {"shared": blocks over
+  // examples, "actions": blocks over action rows, "aip", "chosen" (0-based, -1 none), "cost", "prob"}.
+  m.def("parse_blocks", [](const std::string& args, const std::vector<std::string>& lines, bool multiline) {
+    std::vector<Example> exs;
+    {
+      py::gil_scoped_release rel;
+      exs = VW::ParseLines(args, lines);
+    }
+    auto to_blocks = [](const std::vector<const Example*>& rows) {
+      // namespace char -> CSR over the rows (chars in first-appearance order)
+      std::vector<unsigned char> order;
+      std::array<int, 256> slot;
+      slot.fill(-1);
+      for (const Example* e : rows)
+        for (const auto& ns : e->ns)
+          if (slot[ns.ns] < 0) { slot[ns.ns] = static_cast<int>(order.size()); order.push_back(ns.ns); }
+      const size_t n = rows.size();
+      py::list out;
+      for (unsigned char c : order) {
+        std::vector<int64_t> ip(n + 1, 0);
+        std::vector<uint32_t> idx;
+        std::vector<float> val;
+        for (size_t r = 0; r < n; ++r) {
+          for (const auto& ns : rows[r]->ns)
+            if (ns.ns == c)
+              for (const auto& f : ns.f) { idx.push_back(static_cast<uint32_t>(f.idx)); val.push_back(f.x); }
+          ip[r + 1] = static_cast<int64_t>(idx.size());
+        }
+        out.append(py::make_tuple(std::string(1, static_cast<char>(c)), py::array_t<int64_t>(ip.size(), ip.data()),
+                                  py::array_t<uint32_t>(idx.size(), idx.data()), py::array_t<float>(val.size(), val.data())));
+      }
+      return out;
+    };
+    py::dict d;
+    if (!multiline) {
+      std::vector<const Example*> rows;
+      std::vector<float> lab, w;
+      std::vector<uint8_t> has;
+      std::vector<int32_t> mc, ccls;
+      std::vector<int64_t> cptr{0};
+      std::vector<float> ccost;
+      for (const auto& e : exs) {
+        rows.push_back(&e);
+        lab.push_back(e.l.label);
+        w.push_back(e.l.weight);
+        has.push_back(e.l.has_label || e.l.multiclass > 0 || !e.l.costs.empty() ? 1 : 0);
+        mc.push_back(e.l.multiclass);
+        for (const auto& c : e.l.costs) { ccls.push_back(c.first); ccost.push_back(c.second); }
+        cptr.push_back(static_cast<int64_t>(ccls.size()));
+      }
+      d["blocks"] = to_blocks(rows);
+      d["labels"] = py::array_t<float>(lab.size(), lab.data());
+      d["weights"] = py::array_t<float>(w.size(), w.data());
+      d["has_label"] = py::array_t<uint8_t>(has.size(), has.data());
+      d["multiclass"] = py::array_t<int32_t>(mc.size(), mc.data());
+      d["cptr"] = py::array_t<int64_t>(cptr.size(), cptr.data());
+      d["ccls"] = py::array_t<int32_t>(ccls.size(), ccls.data());
+      d["ccost"] = py::array_t<float>(ccost.size(), ccost.data());
+      return d;
+    }
+    std::vector<const Example*> shared, actions;
+    std::vector<int64_t> aip{0};
+    std::vector<int32_t> chosen;
+    std::vector<float> cost, prob;
+    Example empty;
+    size_t i = 0;
+    while (i < lines.size()) {
+      // skip separators, then take one group
+      while (i < lines.size() && lines[i].find_first_not_of(" \t\r\n") == std::string::npos) ++i;
+      if (i >= lines.size()) break;
+      const Example* sh = &empty;
+      if (exs[i].l.cb_shared) { sh = &exs[i]; ++i; }
+      int ch = -1, a = 0;
+      float c = 0.f, p = 1.f;
+      while (i < lines.size() && lines[i].find_first_not_of(" \t\r\n") != std::string::npos) {
+        if (exs[i].l.cb_has) { ch = a; c = exs[i].l.cb_cost; p = exs[i].l.cb_prob; }
+        actions.push_back(&exs[i]);
+        ++a;
+        ++i;
+      }
+      shared.push_back(sh);
+      aip.push_back(static_cast<int64_t>(actions.size()));
+      chosen.push_back(ch);
+      cost.push_back(c);
+      prob.push_back(p);
+    }
+    d["shared"] = to_blocks(shared);
+    d["actions"] = to_blocks(actions);
+    d["aip"] = py::array_t<int64_t>(aip.size(), aip.data());
+    d["chosen"] = py::array_t<int32_t>(chosen.size(), chosen.data());
+    d["cost"] = py::array_t<float>(cost.size(), cost.data());
+    d["prob"] = py::array_t<float>(prob.size(), prob.data());
+    return d;
+  }, py::arg("args"), py::arg("lines"), py::arg("multiline") = false);
   m.def("gpu_available", &VwGpuAvailable);
   m.def("describe_args", &VW::DescribeArgs, "parse + validate a VW command line (no weight table)");
 
@@ -316,7 +413,11 @@ PYBIND11_MODULE(_vw, m) {
       .def_readwrite("adaptive", &GpuSgdConfig::adaptive)
       .def_readwrite("normalized", &GpuSgdConfig::normalized)
       .def_readwrite("invariant", &GpuSgdConfig::invariant)
-      .def_readwrite("oaa", &GpuSgdConfig::oaa);
+      .def_readwrite("oaa", &GpuSgdConfig::oaa)
+      .def_readwrite("csoaa", &GpuSgdConfig::csoaa)
+      .def_readwrite("cb", &GpuSgdConfig::cb)
+      .def_readwrite("cb_explore", &GpuSgdConfig::cb_explore)
+      .def_readwrite("epsilon", &GpuSgdConfig::epsilon);
   py::class_<GpuSgd, std::shared_ptr<GpuSgd>>(m, "GpuSgd")
       .def(py::init([](const GpuSgdConfig& c, int dev) { return std::make_shared<GpuSgd>(c, dev); }),
            py::arg("config"), py::arg("device") = -1)
@@ -347,6 +448,92 @@ PYBIND11_MODULE(_vw, m) {
              g.Stage(indptr.data(), idx.data(), val.data(), labels.data(), weights.is_none() ? nullptr : w.data(), n);
            },
            py::arg("indptr"), py::arg("indices"), py::arg("values"), py::arg("labels"), py::arg("weights") = py::none())
+      // device featurization: blocks = [(group, level, indptr, indices, values)], interactions = [(a, b, c)]
+      // (namespace group ids, c = -1 for pairs), row_map (n int64) for level-1 blocks
+      .def("stage_plan",
+           [](GpuSgd& g, py::list blocks, int ngroups, py::list inter, bool constant, py::object row_map, int64_t n,
+              py::object labels, py::object weights) {
+             FeatPlan plan;
+             std::vector<I64> keep_i;
+             std::vector<U32> keep_u;
+             std::vector<F32> keep_f;
+             for (auto item : blocks) {
+               auto t = item.cast<py::tuple>();
+               HostBlock b;
+               b.group = t[0].cast<int>();
+               b.level = t[1].cast<int>();
+               keep_i.push_back(t[2].cast<I64>());
+               keep_u.push_back(t[3].cast<U32>());
+               keep_f.push_back(t[4].cast<F32>());
+               b.ip = keep_i.back().data();
+               b.rows = keep_i.back().size() - 1;
+               b.idx = keep_u.back().data();
+               b.val = keep_f.back().data();
+               if (keep_u.back().size() < static_cast<size_t>(b.ip[b.rows]) || keep_f.back().size() < static_cast<size_t>(b.ip[b.rows]))
+                 throw std::runtime_error("block indices / values shorter than indptr says");
+               plan.blocks.push_back(b);
+             }
+             plan.ngroups = ngroups;
+             for (auto item : inter) {
+               auto t = item.cast<py::tuple>();
+               plan.inter.push_back({t[0].cast<int>(), t[1].cast<int>(), t.size() > 2 ? t[2].cast<int>() : -1});
+             }
+             plan.constant = constant;
+             I64 rm;
+             if (!row_map.is_none()) {
+               rm = row_map.cast<I64>();
+               if (rm.size() != n) throw std::runtime_error("row_map must have one entry per row");
+               plan.row_map = rm.data();
+             }
+             F32 lab, w;
+             if (!labels.is_none()) {
+               lab = labels.cast<F32>();
+               if (lab.size() != n) throw std::runtime_error("labels must have one entry per row");
+             }
+             if (!weights.is_none()) {
+               w = weights.cast<F32>();
+               if (w.size() != n) throw std::runtime_error("weights must have one entry per row");
+             }
+             std::vector<float> zeros;
+             if (labels.is_none()) zeros.assign(static_cast<size_t>(std::max<int64_t>(0, n)), 0.f);
+             py::gil_scoped_release rel;
+             g.StagePlan(plan, n, labels.is_none() ? zeros.data() : lab.data(), weights.is_none() ? nullptr : w.data());
+           },
+           py::arg("blocks"), py::arg("ngroups"), py::arg("interactions"), py::arg("constant"), py::arg("row_map"),
+           py::arg("n"), py::arg("labels") = py::none(), py::arg("weights") = py::none())
+      .def("stage_costs",
+           [](GpuSgd& g, I64 cptr, py::array_t<int32_t, py::array::c_style | py::array::forcecast> cls, F32 cost) {
+             const int64_t n = cptr.size() - 1;
+             if (cls.size() < cptr.data()[n] || cost.size() < cptr.data()[n]) throw std::runtime_error("cost lists too short");
+             py::gil_scoped_release rel;
+             g.StageCosts(cptr.data(), cls.data(), cost.data(), n);
+           })
+      .def("stage_cb",
+           [](GpuSgd& g, I64 aip, py::array_t<int32_t, py::array::c_style | py::array::forcecast> chosen, F32 cost,
+              F32 prob) {
+             const int64_t ne = aip.size() - 1;
+             if (chosen.size() != ne || cost.size() != ne || prob.size() != ne)
+               throw std::runtime_error("chosen / cost / prob need one entry per example");
+             py::gil_scoped_release rel;
+             g.StageCb(aip.data(), chosen.data(), cost.data(), prob.data(), ne);
+           })
+      .def("predict_staged",
+           [](GpuSgd& g) {
+             py::array_t<float> out(g.staged_rows());
+             py::array_t<float> best(g.staged_examples());
+             float* o = out.mutable_data();
+             float* b = best.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               g.PredictStaged(o, b);
+             }
+             return py::make_tuple(out, best);
+           })
+      .def_property_readonly("cb_stats", [](const GpuSgd& g) {
+        double a, b, c;
+        g.CbStats(&a, &b, &c);
+        return py::make_tuple(a, b, c);
+      })
       .def("learn_staged",
            [](GpuSgd& g, int64_t r0, int64_t r1, int batch) {
              py::array_t<float> preds(std::max<int64_t>(0, r1 - r0));

@@ -222,10 +222,23 @@ std::map<std::string, std::string> VW::DescribeArgs(const std::string& args) {
   d["constant"] = v.constant_ ? "1" : "0";
   d["hash_seed"] = std::to_string(v.hash_seed_);
   d["passes"] = std::to_string(v.passes_);
+  d["cb_type"] = v.cb_type_;
+  d["cb_explore"] = v.cb_explore_ ? "1" : "0";
+  d["epsilon"] = f(v.epsilon_);
+  d["loss_quantile_tau"] = f(v.quantile_tau_);
   std::string inter;
   for (const auto& q : v.interactions_) inter += (inter.empty() ? "" : ",") + q;
   d["interactions"] = inter;
   return d;
+}
+
+std::vector<Example> VW::ParseLines(const std::string& args, const std::vector<std::string>& lines) {
+  VW v;
+  v.ParseArgs(args);
+  std::vector<Example> out;
+  out.reserve(lines.size());
+  for (const auto& l : lines) out.push_back(v.ParseLine(l));
+  return out;
 }
 
 VW::VW(const std::string& args, const std::string* model_bytes) : args_str_(args) {

@@ -116,6 +116,9 @@ class VW {
   static std::unique_ptr<VW> Merge(const std::vector<const VW*>& models);
   // parse and validate a command line without allocating the weight table (GPU learner set-up)
   static std::map<std::string, std::string> DescribeArgs(const std::string& args);
+  // parse text examples with a command line's hashing / ngram settings, without a weight table (the GPU
+  // learner's text ingest)
+  static std::vector<Example> ParseLines(const std::string& args, const std::vector<std::string>& lines);
   void SetAllReduce(std::function<void(float*, size_t)> fn) { allreduce_ = std::move(fn); }
   int world_size = 1;
 

@@ -5,6 +5,7 @@
 // --oaa runs one wave per class, and touched blocks are averaged across GPUs with
 // RCCL at sync points (C4: the reference's spanning-tree AllReduce at endPass).
 #pragma once
+#include <array>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -23,6 +24,30 @@ struct GpuSgdConfig {
   bool normalized = true;
   bool invariant = true;
   int oaa = 0;           // one-against-all classes (0: scalar learner)
+  int csoaa = 0;         // cost-sensitive one-against-all classes (0: off)
+  int cb = -1;           // contextual bandit with action-dependent features: -1 off, 0 mtr, 1 dr, 2 ips
+  bool cb_explore = false;
+  float epsilon = 0.05f;
+};
+
+// Namespace blocks of a partition for the device featurization (GpuSgd::StagePlan): one CSR per feature
+// column, already hashed; `group` = the namespace (blocks sharing it are concatenated per row), `level` 1 =
+// indexed through the plan's row_map (contextual-bandit action rows reading their example's shared block).
+struct HostBlock {
+  const int64_t* ip;
+  const uint32_t* idx;
+  const float* val;
+  int64_t rows;
+  int level;
+  int group;
+};
+
+struct FeatPlan {
+  std::vector<HostBlock> blocks;
+  int ngroups = 0;
+  std::vector<std::array<int, 3>> inter;  // namespace groups; [2] = -1 for a pair
+  bool constant = true;
+  const int64_t* row_map = nullptr;       // n entries (level-1 blocks)
 };
 
 class GpuSgd {
@@ -39,6 +64,18 @@ class GpuSgd {
   void Stage(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
              const float* weights, int64_t n);
   void LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out);
+  // Device featurization: the plan's namespace blocks -> the staged example CSR (interactions and the
+  // constant expanded on the device). Then optionally the per-example label extras of the reductions:
+  // csoaa (class, cost) lists, or the CB multi-line structure (rows of the plan = action rows).
+  void StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights);
+  void StageCosts(const int64_t* cptr, const int32_t* cls, const float* cost, int64_t n);
+  void StageCb(const int64_t* aip, const int32_t* chosen, const float* cost, const float* prob, int64_t n_examples);
+  // predictions of every staged row (scalar: clamped score; oaa / csoaa: 1-based class; cb: action scores,
+  // plus the greedy action per example in *best)
+  void PredictStaged(float* out, float* best);
+  int64_t staged_rows() const { return staged_rows_; }
+  int64_t staged_examples() const { return staged_n_; }
+  void CbStats(double* ips_num, double* snips_den, double* examples) const;
   // weighted average over ranks of the blocks touched since the last sync (RCCL on the learner's stream)
   void AllReduceAverage(void* nccl_comm_handle, int world);
   uint64_t NumWeights() const;
@@ -66,8 +103,12 @@ class GpuSgd {
   double min_label_ = 0, max_label_ = 0;
   int64_t last_sync_bytes_ = 0, last_sync_blocks_ = 0;
   std::vector<float> staged_labels_;
-  int64_t staged_n_ = 0;
+  int64_t staged_n_ = 0;       // examples
+  int64_t staged_rows_ = 0;    // CSR rows (= examples, or action rows under cb)
   bool staged_weights_ = false;
+  bool staged_costs_ = false;
+  int64_t max_actions_ = 0;
+  void ExpandToStage(const FeatPlan& plan, int64_t n);
 };
 
 bool VwGpuAvailable();

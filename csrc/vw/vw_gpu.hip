@@ -4,6 +4,7 @@
 // scatter AdaGrad updates back with float atomics (conflicts are rare in a
 // 2^b table, which is what makes hogwild converge like sequential SGD).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -323,6 +324,291 @@ __global__ __launch_bounds__(64 * kOaaMaxWaves) void oaa_kernel(SgdArgs a) {
                                                  k + 1 == y ? 1.f : -1.f, imp, lane);
 }
 
+// ---------------------------------------------------------------- device featurization
+// The learner's example CSR is built on the device from the namespace blocks (one CSR per feature column,
+// already hashed): base features of every namespace, then each interaction's crosses, then VW's constant.
+// Namespaces are groups of up to kMaxGroupBlocks blocks (columns sharing a first letter, or a CB action's
+// namespace plus the shared example's); a block is indexed by the row itself (level 0) or by row_map[row]
+// (level 1: contextual-bandit action rows read their example's shared features). Interactions follow the
+// host learner (vw_core.cpp ForEachFeature): (a * FNV) ^ b [* FNV ^ c] in 32 bits (the table mask keeps
+// <= 32 bits, so the low words of the host's 64-bit products), a namespace crossed with itself keeps only
+// non-decreasing feature positions. Pass 1 counts every row's features (closed forms), a device scan gives
+// the row offsets, pass 2 writes them with one wave per row.
+constexpr int kMaxGroups = 32;
+constexpr int kMaxGroupBlocks = 4;
+constexpr int kMaxInter = 64;
+constexpr uint32_t kFnv = 16777619u;
+constexpr uint32_t kConstantIdx = 11650396u;
+
+struct DevBlock {
+  const int64_t* ip;
+  const uint32_t* idx;
+  const float* val;
+  int level;
+};
+
+struct ExpandSpec {
+  int ngroups, ninter, constant, pad;
+  int gblocks[kMaxGroups];
+  DevBlock blk[kMaxGroups][kMaxGroupBlocks];
+  int inter[kMaxInter][3];
+  const int64_t* row_map;
+};
+
+__device__ __forceinline__ int64_t GroupLen(const ExpandSpec& s, int g, int64_t r, int64_t rm) {
+  int64_t l = 0;
+  for (int k = 0; k < s.gblocks[g]; ++k) {
+    const DevBlock& b = s.blk[g][k];
+    const int64_t row = b.level ? rm : r;
+    l += b.ip[row + 1] - b.ip[row];
+  }
+  return l;
+}
+
+__device__ __forceinline__ int64_t InterCount(const ExpandSpec& s, int q, const int64_t* len) {
+  const int a = s.inter[q][0], b = s.inter[q][1], c = s.inter[q][2];
+  const int64_t la = len[a], lb = len[b];
+  if (c < 0) return a == b ? la * (la + 1) / 2 : la * lb;
+  const int64_t lc = len[c];
+  const bool s12 = a == b, s23 = b == c;
+  if (s12 && s23) return la * (la + 1) * (la + 2) / 6;
+  if (s12) return la * (la + 1) / 2 * lc;
+  if (s23) return la * (lb * (lb + 1) / 2);
+  return la * lb * lc;
+}
+
+__global__ __launch_bounds__(256) void expand_count_kernel(const ExpandSpec* __restrict__ sp, int64_t n,
+                                                           int64_t* __restrict__ counts) {
+  const ExpandSpec& s = *sp;
+  for (int64_t r = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; r < n;
+       r += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t rm = s.row_map ? s.row_map[r] : r;
+    int64_t len[kMaxGroups];
+    int64_t c = s.constant ? 1 : 0;
+    for (int g = 0; g < s.ngroups; ++g) { len[g] = GroupLen(s, g, r, rm); c += len[g]; }
+    for (int q = 0; q < s.ninter; ++q) c += InterCount(s, q, len);
+    counts[r] = c;
+  }
+}
+
+// one wave per row; the group's block extents of the row are staged per wave in LDS
+constexpr int kExpandWaves = 4;
+
+struct RowExt {
+  int64_t st[kMaxGroupBlocks];
+  int32_t len[kMaxGroupBlocks];
+  int32_t tot;
+};
+
+__device__ __forceinline__ void GroupFeat(const ExpandSpec& s, const RowExt& e, int g, int i, uint32_t* h, float* x) {
+  for (int k = 0; k < s.gblocks[g]; ++k) {
+    if (i < e.len[k]) {
+      const DevBlock& b = s.blk[g][k];
+      *h = b.idx[e.st[k] + i];
+      *x = b.val[e.st[k] + i];
+      return;
+    }
+    i -= e.len[k];
+  }
+  *h = 0;
+  *x = 0.f;
+}
+
+__global__ __launch_bounds__(64 * kExpandWaves) void expand_fill_kernel(const ExpandSpec* __restrict__ sp, int64_t n,
+                                                                         const int64_t* __restrict__ indptr,
+                                                                         uint32_t* __restrict__ oidx,
+                                                                         float* __restrict__ oval) {
+  const ExpandSpec& s = *sp;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __shared__ RowExt ext[kExpandWaves][kMaxGroups];
+  for (int64_t r = blockIdx.x * static_cast<int64_t>(kExpandWaves) + wid; r < n;
+       r += static_cast<int64_t>(gridDim.x) * kExpandWaves) {
+    const int64_t rm = s.row_map ? s.row_map[r] : r;
+    RowExt* E = ext[wid];
+    for (int g = lane; g < s.ngroups; g += 64) {
+      int tot = 0;
+      for (int k = 0; k < s.gblocks[g]; ++k) {
+        const DevBlock& b = s.blk[g][k];
+        const int64_t row = b.level ? rm : r;
+        E[g].st[k] = b.ip[row];
+        E[g].len[k] = static_cast<int32_t>(b.ip[row + 1] - b.ip[row]);
+        tot += E[g].len[k];
+      }
+      E[g].tot = tot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int64_t pos = indptr[r];
+    for (int g = 0; g < s.ngroups; ++g) {
+      const int la = E[g].tot;
+      for (int i = lane; i < la; i += 64) {
+        uint32_t h;
+        float x;
+        GroupFeat(s, E[g], g, i, &h, &x);
+        oidx[pos + i] = h;
+        oval[pos + i] = x;
+      }
+      pos += la;
+    }
+    for (int q = 0; q < s.ninter; ++q) {
+      const int a = s.inter[q][0], b = s.inter[q][1], c = s.inter[q][2];
+      const int la = E[a].tot, lb = E[b].tot;
+      if (c < 0) {
+        const bool same = a == b;
+        for (int i = 0; i < la; ++i) {
+          uint32_t ha;
+          float xa;
+          GroupFeat(s, E[a], a, i, &ha, &xa);
+          const uint32_t h1 = ha * kFnv;
+          const int j0 = same ? i : 0;
+          for (int j = j0 + lane; j < lb; j += 64) {
+            uint32_t hb;
+            float xb;
+            GroupFeat(s, E[b], b, j, &hb, &xb);
+            oidx[pos + (j - j0)] = h1 ^ hb;
+            oval[pos + (j - j0)] = xa * xb;
+          }
+          pos += lb - j0;
+        }
+      } else {
+        const int lc = E[c].tot;
+        const bool s12 = a == b, s23 = b == c;
+        for (int i = 0; i < la; ++i) {
+          uint32_t ha;
+          float xa;
+          GroupFeat(s, E[a], a, i, &ha, &xa);
+          for (int j = s12 ? i : 0; j < lb; ++j) {
+            uint32_t hb;
+            float xb;
+            GroupFeat(s, E[b], b, j, &hb, &xb);
+            const uint32_t h12 = ((ha * kFnv) ^ hb) * kFnv;
+            const float x12 = xa * xb;
+            const int k0 = s23 ? j : 0;
+            for (int k = k0 + lane; k < lc; k += 64) {
+              uint32_t hc;
+              float xc;
+              GroupFeat(s, E[c], c, k, &hc, &xc);
+              oidx[pos + (k - k0)] = h12 ^ hc;
+              oval[pos + (k - k0)] = x12 * xc;
+            }
+            pos += lc - k0;
+          }
+        }
+      }
+    }
+    if (s.constant && lane == 0) {
+      oidx[pos] = kConstantIdx;
+      oval[pos] = 1.f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- --csoaa K
+// One block per example: wave c scores classes c, c + waves, ... (class offsets as --oaa), the prediction is
+// the class of smallest score (first on ties, std::min_element); wave 0 then applies the example's (class,
+// cost) regressions one after another, as the host learner does (batch 1 = the sequential learner).
+__global__ __launch_bounds__(64 * kOaaMaxWaves) void csoaa_kernel(SgdArgs a, const int64_t* __restrict__ cptr,
+                                                                  const int32_t* __restrict__ ccls,
+                                                                  const float* __restrict__ ccost) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int64_t e = a.n0 + blockIdx.x;
+  if (e >= a.n1) return;
+  extern __shared__ float scores[];
+  __shared__ int s_best;
+  const int64_t b = a.indptr[e], en = a.indptr[e + 1];
+  for (int k = wid; k < a.K; k += nw) {
+    const float sc = Dot(a, b, en, static_cast<uint64_t>(k) * kOaaOffset, lane);
+    if (lane == 0) scores[k] = sc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int k = 1; k < a.K; ++k) if (scores[k] < scores[best]) best = k;
+    s_best = best;
+    if (a.preds) a.preds[e] = static_cast<float>(best + 1);
+    if (a.learn && cptr) {
+      float chosen = 0.f;
+      for (int64_t p = cptr[e]; p < cptr[e + 1]; ++p) if (ccls[p] == best + 1) chosen = ccost[p];
+      atomicAdd(a.loss_acc, chosen * (a.wt ? a.wt[e] : 1.f));
+    }
+  }
+  if (!a.learn || !cptr || wid != 0) return;
+  const float imp = a.wt ? a.wt[e] : 1.f;
+  if (imp <= 0.f) return;
+  for (int64_t p = cptr[e]; p < cptr[e + 1]; ++p) {
+    const int k = ccls[p] - 1;
+    if (k < 0 || k >= a.K) continue;
+    UpdateWave(a, b, en, static_cast<uint64_t>(k) * kOaaOffset, scores[k], ccost[p], imp, lane);
+  }
+}
+
+// ---------------------------------------------------------------- --cb_adf / --cb_explore_adf
+// One block per multi-line example: its action rows [aip[e], aip[e+1]) (shared features merged in by the
+// device featurization) are scored by the waves, the greedy action is the smallest score, the exploration
+// distribution is epsilon-greedy; with a logged (action, cost, probability) the IPS / SNIPS sums advance and
+// the update follows --cb_type: mtr (the logged action regressed on its cost with importance 1/p), dr (every
+// action towards its doubly-robust target) or ips (every action towards cost/p on the logged one, 0 else),
+// applied action after action by wave 0 as the host learner does.
+struct CbArgs {
+  const int64_t* aip;
+  const int32_t* chosen;  // 0-based logged action or -1
+  const float* cost;
+  const float* prob;
+  int cb_type;            // 0 mtr, 1 dr, 2 ips
+  int explore;
+  float epsilon;
+  double* stats;          // [ips numerator, snips denominator, examples]
+  float* best_out;        // per example: greedy action (0-based)
+};
+
+constexpr int kCbWaves = 8;
+
+__global__ __launch_bounds__(64 * kCbWaves) void cb_kernel(SgdArgs a, CbArgs cb) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t e = a.n0 + blockIdx.x;
+  if (e >= a.n1) return;
+  extern __shared__ float scores[];
+  __shared__ int s_best;
+  const int64_t r0 = cb.aip[e], r1 = cb.aip[e + 1];
+  const int A = static_cast<int>(r1 - r0);
+  if (A <= 0) return;
+  for (int k = wid; k < A; k += kCbWaves) {
+    const float sc = Dot(a, a.indptr[r0 + k], a.indptr[r0 + k + 1], 0, lane);
+    if (lane == 0) {
+      scores[k] = sc;
+      if (a.preds) a.preds[r0 + k] = sc;
+    }
+  }
+  __syncthreads();
+  const int logged = cb.chosen ? cb.chosen[e] : -1;
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int k = 1; k < A; ++k) if (scores[k] < scores[best]) best = k;
+    s_best = best;
+    if (cb.best_out) cb.best_out[e] = static_cast<float>(best);
+    if (cb.stats && logged >= 0 && logged < A) {
+      const float p = fmaxf(cb.prob[e], 1e-6f);
+      const float ppred = cb.explore ? (logged == best ? 1.f - cb.epsilon + cb.epsilon / A : cb.epsilon / A)
+                                     : (logged == best ? 1.f : 0.f);
+      atomicAdd(&cb.stats[0], static_cast<double>(cb.cost[e] * ppred / p));
+      atomicAdd(&cb.stats[1], static_cast<double>(ppred / p));
+    }
+    if (cb.stats) atomicAdd(&cb.stats[2], 1.0);
+  }
+  if (!a.learn || logged < 0 || logged >= A || wid != 0) return;
+  const float p = fmaxf(cb.prob[e], 1e-6f), c = cb.cost[e];
+  if (cb.cb_type == 0) {
+    UpdateWave(a, a.indptr[r0 + logged], a.indptr[r0 + logged + 1], 0, scores[logged], c, 1.f / p, lane);
+  } else {
+    for (int k = 0; k < A; ++k) {
+      const float lab = cb.cb_type == 1 ? scores[k] + (k == logged ? (c - scores[k]) / p : 0.f)
+                                        : (k == logged ? c / p : 0.f);
+      UpdateWave(a, a.indptr[r0 + k], a.indptr[r0 + k + 1], 0, scores[k], lab, 1.f, lane);
+    }
+  }
+}
+
 // Sync payload per slot: double {w G (adaptive) or w, G} + float N. The weighted sum goes in double: a
 // float w * G underflows (and is flushed) for slots with a tiny gradient mass, which would zero their
 // weight on the average even at world 1.
@@ -475,6 +761,12 @@ struct GpuSgd::Impl {
   uint32_t* idx = nullptr;
   float *val = nullptr, *lab = nullptr, *wt = nullptr, *lo = nullptr, *hi = nullptr, *pred = nullptr, *loss = nullptr;
   size_t cap_rows = 0, cap_nnz = 0;
+  // reductions: csoaa (class, cost) lists; CB multi-line examples
+  int64_t *cptr = nullptr, *aip = nullptr;
+  int32_t *ccls = nullptr, *chosen = nullptr;
+  float *ccost = nullptr, *cbcost = nullptr, *cbprob = nullptr, *best = nullptr;
+  double* cbstats = nullptr;
+  ExpandSpec* spec = nullptr;
   // sync scratch
   int32_t *pos = nullptr, *blocks = nullptr;
   double* sums = nullptr;
@@ -505,6 +797,11 @@ struct GpuSgd::Impl {
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    for (void* q : {static_cast<void*>(cptr), static_cast<void*>(aip), static_cast<void*>(ccls),
+                    static_cast<void*>(chosen), static_cast<void*>(ccost), static_cast<void*>(cbcost),
+                    static_cast<void*>(cbprob), static_cast<void*>(best), static_cast<void*>(cbstats),
+                    static_cast<void*>(spec)})
+      (void)hipFree(q);
     for (void* q : {static_cast<void*>(W), static_cast<void*>(dirty), static_cast<void*>(gs),
                     static_cast<void*>(indptr), static_cast<void*>(idx), static_cast<void*>(val),
                     static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo), static_cast<void*>(hi),
@@ -554,6 +851,8 @@ bool VwGpuAvailable() {
 GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cfg) {
   if (device >= 0) VW_HIP_CHECK(hipSetDevice(device));
   if (cfg.oaa > 256) throw std::runtime_error("GPU oaa supports at most 256 classes");
+  if (cfg.csoaa > 256) throw std::runtime_error("GPU csoaa supports at most 256 classes");
+  if ((cfg.oaa > 0) + (cfg.csoaa > 0) + (cfg.cb >= 0) > 1) throw std::runtime_error("one reduction at a time");
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
   impl_->nw = 1ull << cfg.bits;
@@ -564,6 +863,8 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
   VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, impl_->nblk, impl_->stream));
   VW_HIP_CHECK(hipMalloc(&impl_->gs, 3 * sizeof(double)));
   VW_HIP_CHECK(hipMemsetAsync(impl_->gs, 0, 3 * sizeof(double), impl_->stream));
+  VW_HIP_CHECK(hipMalloc(&impl_->cbstats, 3 * sizeof(double)));
+  VW_HIP_CHECK(hipMemsetAsync(impl_->cbstats, 0, 3 * sizeof(double), impl_->stream));
   VW_HIP_CHECK(hipMalloc(&impl_->loss, sizeof(float)));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), impl_->stream));
   VW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
@@ -577,7 +878,7 @@ SgdArgs BaseArgs(const GpuSgdConfig& c) {
   SgdArgs a{};
   a.lr = c.lr; a.power_t = c.power_t; a.initial_t = c.initial_t; a.l2 = c.l2; a.loss = c.loss;
   a.adaptive = c.adaptive ? 1 : 0; a.normalized = c.normalized ? 1 : 0; a.invariant = c.invariant ? 1 : 0;
-  a.K = c.oaa;
+  a.K = c.oaa > 0 ? c.oaa : c.csoaa;
   return a;
 }
 }  // namespace
@@ -590,7 +891,19 @@ void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
   a.hi = impl_->hi;
   a.n0 = b0; a.n1 = b1; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
   a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = learn ? 1 : 0;
-  if (cfg_.oaa > 0) {
+  if (cfg_.cb >= 0) {
+    a.lo = nullptr;
+    CbArgs cb{impl_->aip, impl_->chosen, impl_->cbcost, impl_->cbprob, cfg_.cb, cfg_.cb_explore ? 1 : 0, cfg_.epsilon,
+              impl_->cbstats, impl_->best};
+    // the widest example of the staged set sizes the score buffer
+    hipLaunchKernelGGL(cb_kernel, dim3(static_cast<unsigned>(b1 - b0)), dim3(64 * kCbWaves),
+                       sizeof(float) * std::max<int64_t>(1, max_actions_), impl_->stream, a, cb);
+  } else if (cfg_.csoaa > 0) {
+    a.lo = nullptr;
+    const int waves = std::min(cfg_.csoaa, kOaaMaxWaves);
+    hipLaunchKernelGGL(csoaa_kernel, dim3(static_cast<unsigned>(b1 - b0)), dim3(64 * waves), sizeof(float) * cfg_.csoaa,
+                       impl_->stream, a, staged_costs_ ? impl_->cptr : nullptr, impl_->ccls, impl_->ccost);
+  } else if (cfg_.oaa > 0) {
     const int waves = std::min(cfg_.oaa, kOaaMaxWaves);
     hipLaunchKernelGGL(oaa_kernel, dim3(static_cast<unsigned>(b1 - b0)), dim3(64 * waves), sizeof(float) * cfg_.oaa,
                        impl_->stream, a);
@@ -721,7 +1034,9 @@ void GpuSgd::Stage(const int64_t* indptr, const uint32_t* indices, const float* 
   VW_HIP_CHECK(hipStreamSynchronize(s));
   staged_labels_.assign(labels, labels + n);
   staged_n_ = n;
+  staged_rows_ = n;
   staged_weights_ = weights != nullptr;
+  staged_costs_ = false;
 }
 
 void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
@@ -730,25 +1045,218 @@ void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
   hipStream_t s = impl_->stream;
   const int64_t m = r1 - r0;
   std::vector<float> lo(m), hi(m);
-  for (int64_t i = 0; i < m; ++i) {
-    if (cfg_.loss != 1 && cfg_.oaa == 0) {
-      min_label_ = std::min<double>(min_label_, staged_labels_[r0 + i]);
-      max_label_ = std::max<double>(max_label_, staged_labels_[r0 + i]);
+  const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0;
+  if (scalar) {
+    for (int64_t i = 0; i < m; ++i) {
+      if (cfg_.loss != 1) {
+        min_label_ = std::min<double>(min_label_, staged_labels_[r0 + i]);
+        max_label_ = std::max<double>(max_label_, staged_labels_[r0 + i]);
+      }
+      lo[i] = static_cast<float>(min_label_);
+      hi[i] = static_cast<float>(max_label_);
     }
-    lo[i] = static_cast<float>(min_label_);
-    hi[i] = static_cast<float>(max_label_);
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->lo + r0, lo.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->hi + r0, hi.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
   }
-  VW_HIP_CHECK(hipMemcpyAsync(impl_->lo + r0, lo.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
-  VW_HIP_CHECK(hipMemcpyAsync(impl_->hi + r0, hi.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), s));
   batch = std::max(1, batch);
   for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, staged_weights_);
   float l = 0;
   VW_HIP_CHECK(hipMemcpyAsync(&l, impl_->loss, sizeof(float), hipMemcpyDeviceToHost, s));
-  if (preds_out) VW_HIP_CHECK(hipMemcpyAsync(preds_out, impl_->pred + r0, m * sizeof(float), hipMemcpyDeviceToHost, s));
+  if (preds_out && cfg_.cb < 0)
+    VW_HIP_CHECK(hipMemcpyAsync(preds_out, impl_->pred + r0, m * sizeof(float), hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
   examples_ += m;
   sum_loss_ += l;
+}
+
+// ---- device featurization
+void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
+  if (plan.ngroups > kMaxGroups) throw std::runtime_error("device featurization: more than 32 namespaces");
+  if (static_cast<int>(plan.inter.size()) > kMaxInter) throw std::runtime_error("device featurization: more than 64 interactions");
+  hipStream_t s = impl_->stream, cs = impl_->copy_stream;
+  ExpandSpec h{};
+  h.ngroups = plan.ngroups;
+  h.ninter = static_cast<int>(plan.inter.size());
+  h.constant = plan.constant ? 1 : 0;
+  for (int q = 0; q < h.ninter; ++q)
+    for (int k = 0; k < 3; ++k) {
+      const int g = plan.inter[q][k];
+      if (g >= plan.ngroups || (k < 2 && g < 0)) throw std::runtime_error("device featurization: bad interaction");
+      h.inter[q][k] = g;
+    }
+  // upload the blocks (pinned staging, parallel host copies) on the copy stream
+  std::vector<void*> tmp;
+  auto dev_copy = [&](const void* src, size_t bytes) -> void* {
+    void* d = nullptr;
+    VW_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 8)));
+    tmp.push_back(d);
+    if (bytes) impl_->stager.Copy(static_cast<char*>(d), static_cast<const char*>(src), bytes, cs);
+    return d;
+  };
+  try {
+    {
+      std::lock_guard<std::mutex> lk(impl_->stager.mu);
+      for (const HostBlock& b : plan.blocks) {
+        if (b.group < 0 || b.group >= plan.ngroups) throw std::runtime_error("device featurization: bad group");
+        const int k = h.gblocks[b.group]++;
+        if (k >= kMaxGroupBlocks) throw std::runtime_error("device featurization: more than 4 blocks in a namespace");
+        if (b.level == 0 && b.rows != n) throw std::runtime_error("device featurization: block rows != examples");
+        const int64_t nnz = b.ip[b.rows] - b.ip[0];
+        std::vector<int64_t> ip(b.ip, b.ip + b.rows + 1);
+        for (auto& v : ip) v -= b.ip[0];
+        DevBlock d;
+        d.ip = static_cast<const int64_t*>(dev_copy(ip.data(), ip.size() * sizeof(int64_t)));
+        d.idx = static_cast<const uint32_t*>(dev_copy(b.idx + b.ip[0], nnz * sizeof(uint32_t)));
+        d.val = static_cast<const float*>(dev_copy(b.val + b.ip[0], nnz * sizeof(float)));
+        d.level = b.level;
+        h.blk[b.group][k] = d;
+      }
+      if (plan.row_map) h.row_map = static_cast<const int64_t*>(dev_copy(plan.row_map, n * sizeof(int64_t)));
+      VW_HIP_CHECK(hipStreamSynchronize(cs));
+    }
+    if (!impl_->spec) VW_HIP_CHECK(hipMalloc(&impl_->spec, sizeof(ExpandSpec)));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->spec, &h, sizeof(ExpandSpec), hipMemcpyHostToDevice, s));
+    impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
+    VW_HIP_CHECK(hipMemsetAsync(impl_->indptr, 0, sizeof(int64_t), s));
+    if (n > 0) {
+      const int grid = static_cast<int>(std::min<int64_t>(65536, (n + 255) / 256));
+      hipLaunchKernelGGL(expand_count_kernel, dim3(grid), dim3(256), 0, s, impl_->spec, n, impl_->indptr + 1);
+      VW_HIP_CHECK(hipGetLastError());
+      size_t tb = 0;
+      VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
+      void* tbuf = dev_copy(nullptr, tb);
+      VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tbuf, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
+    }
+    int64_t nnz = 0;
+    VW_HIP_CHECK(hipMemcpyAsync(&nnz, impl_->indptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    VW_HIP_CHECK(hipStreamSynchronize(s));
+    impl_->Reserve(std::max<int64_t>(1, n), static_cast<size_t>(nnz));
+    if (n > 0) {
+      const int grid = static_cast<int>(std::min<int64_t>(65536, (n + kExpandWaves - 1) / kExpandWaves));
+      hipLaunchKernelGGL(expand_fill_kernel, dim3(grid), dim3(64 * kExpandWaves), 0, s, impl_->spec, n, impl_->indptr,
+                         impl_->idx, impl_->val);
+      VW_HIP_CHECK(hipGetLastError());
+    }
+    VW_HIP_CHECK(hipStreamSynchronize(s));
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(cs);
+    for (void* q : tmp) (void)hipFree(q);
+    throw;
+  }
+  for (void* q : tmp) (void)hipFree(q);
+  staged_rows_ = n;
+}
+
+void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights) {
+  if (n < 0) throw std::runtime_error("negative row count");
+  ExpandToStage(plan, n);
+  hipStream_t s = impl_->stream;
+  if (cfg_.cb < 0 && n) {
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->lab, labels, n * sizeof(float), hipMemcpyHostToDevice, s));
+    if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
+    staged_labels_.assign(labels, labels + n);
+    staged_n_ = n;
+  }
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  staged_weights_ = weights != nullptr;
+  staged_costs_ = false;
+}
+
+void GpuSgd::StageCosts(const int64_t* cptr, const int32_t* cls, const float* cost, int64_t n) {
+  if (n != staged_n_) throw std::runtime_error("StageCosts: rows != staged examples");
+  hipStream_t s = impl_->stream;
+  const int64_t m = cptr[n] - cptr[0];
+  std::vector<int64_t> ip(cptr, cptr + n + 1);
+  for (auto& v : ip) v -= cptr[0];
+  for (void* q : {static_cast<void*>(impl_->cptr), static_cast<void*>(impl_->ccls), static_cast<void*>(impl_->ccost)})
+    (void)hipFree(q);
+  VW_HIP_CHECK(hipMalloc(&impl_->cptr, (n + 1) * sizeof(int64_t)));
+  VW_HIP_CHECK(hipMalloc(&impl_->ccls, std::max<int64_t>(1, m) * sizeof(int32_t)));
+  VW_HIP_CHECK(hipMalloc(&impl_->ccost, std::max<int64_t>(1, m) * sizeof(float)));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->cptr, ip.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  if (m) {
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->ccls, cls + cptr[0], m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->ccost, cost + cptr[0], m * sizeof(float), hipMemcpyHostToDevice, s));
+  }
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  staged_costs_ = true;
+}
+
+void GpuSgd::StageCb(const int64_t* aip, const int32_t* chosen, const float* cost, const float* prob, int64_t ne) {
+  if (cfg_.cb < 0) throw std::runtime_error("StageCb on a learner without --cb_adf");
+  if (aip[ne] - aip[0] != staged_rows_) throw std::runtime_error("StageCb: action rows != staged rows");
+  hipStream_t s = impl_->stream;
+  std::vector<int64_t> ip(aip, aip + ne + 1);
+  for (auto& v : ip) v -= aip[0];
+  max_actions_ = 0;
+  for (int64_t e = 0; e < ne; ++e) max_actions_ = std::max(max_actions_, ip[e + 1] - ip[e]);
+  if (max_actions_ > 4096) throw std::runtime_error("GPU cb_adf supports at most 4096 actions per example");
+  for (void* q : {static_cast<void*>(impl_->aip), static_cast<void*>(impl_->chosen), static_cast<void*>(impl_->cbcost),
+                  static_cast<void*>(impl_->cbprob), static_cast<void*>(impl_->best)})
+    (void)hipFree(q);
+  const size_t m = std::max<int64_t>(1, ne);
+  VW_HIP_CHECK(hipMalloc(&impl_->aip, (ne + 1) * sizeof(int64_t)));
+  VW_HIP_CHECK(hipMalloc(&impl_->chosen, m * sizeof(int32_t)));
+  VW_HIP_CHECK(hipMalloc(&impl_->cbcost, m * sizeof(float)));
+  VW_HIP_CHECK(hipMalloc(&impl_->cbprob, m * sizeof(float)));
+  VW_HIP_CHECK(hipMalloc(&impl_->best, m * sizeof(float)));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->aip, ip.data(), (ne + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  if (ne) {
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->chosen, chosen, ne * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cbcost, cost, ne * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cbprob, prob, ne * sizeof(float), hipMemcpyHostToDevice, s));
+  }
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  staged_n_ = ne;
+  staged_labels_.assign(ne, 0.f);
+  staged_weights_ = false;
+}
+
+void GpuSgd::PredictStaged(float* out, float* best) {
+  hipStream_t s = impl_->stream;
+  const int64_t ne = staged_n_;
+  if (ne <= 0) return;
+  const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0;
+  if (scalar) {
+    std::vector<float> lo(ne, static_cast<float>(min_label_)), hi(ne, static_cast<float>(max_label_));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->lo, lo.data(), ne * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->hi, hi.data(), ne * sizeof(float), hipMemcpyHostToDevice, s));
+  }
+  // prediction launches: the whole staged set at once (no updates, so no ordering to respect)
+  SgdArgs a = BaseArgs(cfg_);
+  a.indptr = impl_->indptr; a.idx = impl_->idx; a.val = impl_->val;
+  a.lo = scalar ? impl_->lo : nullptr; a.hi = impl_->hi;
+  a.n0 = 0; a.n1 = ne; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
+  a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = 0;
+  if (cfg_.cb >= 0) {
+    CbArgs cb{impl_->aip, nullptr, impl_->cbcost, impl_->cbprob, cfg_.cb, cfg_.cb_explore ? 1 : 0, cfg_.epsilon, nullptr,
+              impl_->best};
+    hipLaunchKernelGGL(cb_kernel, dim3(static_cast<unsigned>(ne)), dim3(64 * kCbWaves),
+                       sizeof(float) * std::max<int64_t>(1, max_actions_), s, a, cb);
+  } else if (cfg_.csoaa > 0) {
+    const int waves = std::min(cfg_.csoaa, kOaaMaxWaves);
+    hipLaunchKernelGGL(csoaa_kernel, dim3(static_cast<unsigned>(ne)), dim3(64 * waves), sizeof(float) * cfg_.csoaa, s, a,
+                       static_cast<const int64_t*>(nullptr), static_cast<const int32_t*>(nullptr),
+                       static_cast<const float*>(nullptr));
+  } else if (cfg_.oaa > 0) {
+    const int waves = std::min(cfg_.oaa, kOaaMaxWaves);
+    hipLaunchKernelGGL(oaa_kernel, dim3(static_cast<unsigned>(ne)), dim3(64 * waves), sizeof(float) * cfg_.oaa, s, a);
+  } else {
+    hipLaunchKernelGGL(sgd_kernel, dim3(static_cast<unsigned>((ne + kSgdWaves - 1) / kSgdWaves)), dim3(64 * kSgdWaves), 0,
+                       s, a);
+  }
+  VW_HIP_CHECK(hipGetLastError());
+  VW_HIP_CHECK(hipMemcpyAsync(out, impl_->pred, staged_rows_ * sizeof(float), hipMemcpyDeviceToHost, s));
+  if (best && cfg_.cb >= 0) VW_HIP_CHECK(hipMemcpyAsync(best, impl_->best, ne * sizeof(float), hipMemcpyDeviceToHost, s));
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void GpuSgd::CbStats(double* ips_num, double* snips_den, double* examples) const {
+  double h[3] = {0, 0, 0};
+  VW_HIP_CHECK(hipMemcpy(h, impl_->cbstats, sizeof(h), hipMemcpyDeviceToHost));
+  *ips_num = h[0]; *snips_den = h[1]; *examples = h[2];
 }
 
 void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float* values, int64_t n, float* out) {

@@ -9,7 +9,9 @@ metadata (ML attributes such as categorical slots).
 
 Storage is one numpy array per column. A dense vector column is a 2-D float
 array (rows x width) - the layout the native engines consume without copies;
-sparse/ragged vector columns are object arrays of :class:`SparseVector`.
+sparse/ragged vector columns are object arrays of :class:`SparseVector`, or one
+CSR matrix (:class:`~synapseml_amd.core.linalg.CsrColumn`) that the engines take
+zero-copy.
 """
 from __future__ import annotations
 
@@ -18,7 +20,7 @@ from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence
 
 import numpy as np
 
-from .linalg import DenseVector, SparseVector, Vector
+from .linalg import CsrColumn, DenseVector, SparseVector, Vector
 
 
 class Row(dict):
@@ -35,7 +37,7 @@ class Row(dict):
 
 
 def _as_column(values: Any, n: Optional[int] = None) -> np.ndarray:
-    if isinstance(values, np.ndarray):
+    if isinstance(values, (np.ndarray, CsrColumn)):
         return values
     if isinstance(values, (list, tuple)):
         if values and isinstance(values[0], Vector):
@@ -290,6 +292,10 @@ class DataFrame:
         cols = {}
         for k in names:
             arrs = [p._cols[k] for p in parts]
+            if all(isinstance(a, CsrColumn) for a in arrs):
+                cols[k] = CsrColumn.concat(arrs)
+                continue
+            arrs = [np.asarray(a) if isinstance(a, CsrColumn) else a for a in arrs]
             if any(a.dtype == object for a in arrs) or len({a.ndim for a in arrs}) > 1:
                 out = np.empty(sum(len(a) for a in arrs), dtype=object)
                 i = 0

@@ -97,6 +97,123 @@ class SparseVector(Vector):
         return f"SparseVector({self._size}, {self.indices.tolist()}, {self.values.tolist()})"
 
 
+class CsrColumn:
+    """A column of sparse vectors stored as ONE CSR matrix (indptr int64, indices int32/uint32, values float32 or
+    float64, a common size) instead of an object array of :class:`SparseVector` rows.
+
+    Rows read back as SparseVector (so row-wise code keeps working), while the engines take the CSR arrays
+    without a per-row Python loop: VW's namespace blocks and LightGBM's CSR push are zero-copy views, and
+    slicing a contiguous row range (partitions) only rebases ``indptr``. It supports the subset of the numpy
+    1-D array surface the DataFrame uses (len, ndim / dtype / shape, int / slice / mask / index-array
+    ``__getitem__``, iteration, ``tolist``); ``np.asarray`` materialises the object-array form."""
+
+    ndim = 1
+    dtype = np.dtype(object)
+
+    def __init__(self, indptr, indices, values, size: int):
+        self.indptr = np.asarray(indptr, dtype=np.int64)
+        self.indices = np.asarray(indices)
+        self.values = np.asarray(values)
+        self.size = int(size)
+        if self.indptr.ndim != 1 or len(self.indptr) < 1:
+            raise ValueError("indptr must be a 1-D array of n + 1 offsets")
+        if len(self.indices) != len(self.values):
+            raise ValueError("indices and values must have the same length")
+
+    @property
+    def shape(self):
+        return (len(self.indptr) - 1,)
+
+    def __len__(self) -> int:
+        return len(self.indptr) - 1
+
+    def row(self, i: int) -> SparseVector:
+        a, b = self.indptr[i] - self.indptr[0], self.indptr[i + 1] - self.indptr[0]
+        return SparseVector(self.size, self.indices[a:b].astype(np.int32), self.values[a:b])
+
+    def csr(self):
+        """(indptr rebased to 0, indices, values) of the rows, without copying when already rebased"""
+        base = int(self.indptr[0])
+        ip = self.indptr - base if base else self.indptr
+        return ip, self.indices[: ip[-1]] if len(self.indices) != ip[-1] else self.indices, \
+            self.values[: ip[-1]] if len(self.values) != ip[-1] else self.values
+
+    def __getitem__(self, key):
+        n = len(self)
+        if isinstance(key, (int, np.integer)):
+            k = int(key)
+            if k < 0:
+                k += n
+            if not 0 <= k < n:
+                raise IndexError(key)
+            return self.row(k)
+        if isinstance(key, slice):
+            a, b, step = key.indices(n)
+            if step == 1:
+                b = max(a, b)
+                s, e = int(self.indptr[a]), int(self.indptr[b])
+                base = int(self.indptr[0])
+                return CsrColumn(self.indptr[a:b + 1] - s, self.indices[s - base:e - base],
+                                 self.values[s - base:e - base], self.size)
+            key = np.arange(a, b, step)
+        idx = np.asarray(key)
+        if idx.dtype == bool:
+            if len(idx) != n:
+                raise IndexError("boolean index length mismatch")
+            idx = np.flatnonzero(idx)
+        idx = idx.astype(np.int64)
+        idx[idx < 0] += n
+        ip, ind, val = self.csr()
+        lens = ip[idx + 1] - ip[idx]
+        out_ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        # gather of the selected rows' nonzeros: source position = row start + offset within the row
+        src = np.repeat(ip[idx] - out_ip[:-1], lens) + np.arange(out_ip[-1], dtype=np.int64)
+        return CsrColumn(out_ip, ind[src], val[src], self.size)
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self.row(i)
+
+    def tolist(self) -> list:
+        return list(self)
+
+    def __array__(self, dtype=None, copy=None):
+        out = np.empty(len(self), dtype=object)
+        for i in range(len(self)):
+            out[i] = self.row(i)
+        return out
+
+    @staticmethod
+    def concat(cols) -> "CsrColumn":
+        parts = [c.csr() for c in cols]
+        sizes = {c.size for c in cols}
+        offs = np.cumsum([0] + [p[0][-1] for p in parts])
+        ip = np.concatenate([parts[0][0][:1]] + [p[0][1:] + o for p, o in zip(parts, offs[:-1])])
+        return CsrColumn(ip, np.concatenate([p[1] for p in parts]), np.concatenate([p[2] for p in parts]),
+                         max(sizes) if sizes else 0)
+
+    @staticmethod
+    def from_rows(rows, size: int = 0) -> "CsrColumn":
+        ip, ii, vv = [0], [], []
+        for r in rows:
+            if isinstance(r, SparseVector):
+                ii.append(r.indices)
+                vv.append(r.values)
+                size = max(size, r.size)
+            else:
+                a = np.asarray(r, dtype=np.float64)
+                nz = np.flatnonzero(a)
+                ii.append(nz.astype(np.int32))
+                vv.append(a[nz])
+                size = max(size, len(a))
+            ip.append(ip[-1] + len(ii[-1]))
+        return CsrColumn(np.asarray(ip, np.int64), np.concatenate(ii) if ii else np.zeros(0, np.int32),
+                         np.concatenate(vv) if vv else np.zeros(0), size)
+
+    def __repr__(self) -> str:
+        return f"CsrColumn(rows={len(self)}, size={self.size}, nnz={int(self.indptr[-1] - self.indptr[0])})"
+
+
 class Vectors:
     @staticmethod
     def dense(*values) -> DenseVector:
@@ -133,6 +250,9 @@ def as_matrix(col) -> np.ndarray:
 
 def as_csr(col):
     """Vector column -> (indptr int64, indices int32, values float64, width)."""
+    if isinstance(col, CsrColumn):
+        ip, ind, val = col.csr()
+        return ip, ind.astype(np.int32, copy=False), val.astype(np.float64, copy=False), col.size
     rows = list(col) if not (isinstance(col, np.ndarray) and col.ndim == 2) else None
     if rows is None:
         m = np.asarray(col, dtype=np.float64)
@@ -162,6 +282,8 @@ def as_csr(col):
 
 
 def is_sparse_column(col) -> bool:
+    if isinstance(col, CsrColumn):
+        return True
     if isinstance(col, np.ndarray) and col.ndim == 2:
         return False
     for r in col[:10] if hasattr(col, "__getitem__") else []:

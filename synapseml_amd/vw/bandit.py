@@ -71,12 +71,18 @@ class _CBParams(Params):
 
 class VowpalWabbitContextualBanditModel(VowpalWabbitModelBase, _CBParams):
     def _transform(self, df: DataFrame) -> DataFrame:
-        vw = self._native_model()
         shared = _blocks_rows(df, [self.getSharedCol()] + list(self.getAdditionalSharedFeatures() or []),
                               self.getHashSeed())
         actions, aip = _blocks_actions(df, [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or []),
                                        self.getHashSeed())
         n = df.count()
+        gs = self._gpu_scorer()
+        if gs is not None:  # scored on the device (no host weight table)
+            out = np.empty(n, dtype=object)
+            for i, p in enumerate(gs.predict_cb(actions, shared, aip)):
+                out[i] = p
+            return df.withColumn(self.getPredictionCol(), out)
+        vw = self._native_model()
         res = vw.learn_cb(shared, actions, aip, np.zeros(n, np.int32), np.zeros(n, np.float32),
                           np.ones(n, np.float32), False)
         out = np.empty(n, dtype=object)
@@ -105,9 +111,42 @@ class VowpalWabbitContextualBandit(VowpalWabbitBase, _CBParams):
             sb.appendParamValueIfNotThere("epsilon", self.getEpsilon())
         return sb
 
+    def _train_partition_gpu(self, df: DataFrame, args: str, model_bytes=None):
+        """--cb_explore_adf on the device (vw_gpu.hip cb_kernel): action rows featurized in HBM with their
+        example's shared namespaces, one block per example scores the actions, epsilon-greedy pmf, IPS/SNIPS
+        and the --cb_type (mtr / dr / ips) update; gpuBatchSize=1 is the sequential learner."""
+        import time
+
+        from .learners import _GpuTrainedModel, _device_plan, _gpu_learn_staged, _gpu_learner, _gpu_sync_comm
+
+        t0 = time.perf_counter_ns()
+        vwmod, info, g = _gpu_learner(args, model_bytes)
+        shared = _blocks_rows(df, [self.getSharedCol()] + list(self.getAdditionalSharedFeatures() or []),
+                              self.getHashSeed())
+        actions, aip = _blocks_actions(df, [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or []),
+                                       self.getHashSeed())
+        n = df.count()
+        row_map = np.repeat(np.arange(n, dtype=np.int64), np.diff(aip))
+        gb, ng, inter = _device_plan(actions, info, shared)
+        g.stage_plan(gb, ng, inter, info["constant"] == "1", row_map, int(aip[-1]), None, None)
+        g.stage_cb(aip, np.asarray(df[self.getChosenActionCol()], np.int32) - 1,
+                   np.asarray(df[self.getLabelCol()], np.float32), np.asarray(df[self.getProbabilityCol()], np.float32))
+        t1 = time.perf_counter_ns()
+        _gpu_learn_staged(self, g, _gpu_sync_comm(vwmod), n)
+        t2 = time.perf_counter_ns()
+        ips, snips_den, ex = g.cb_stats
+        st = {"numberOfExamplesPerPass": int(n), "weightedExampleSum": float(ex), "weightedLabelSum": 0.0,
+              "averageLoss": float(ips) / max(ex, 1.0), "bestConstant": 0.0, "totalNumberOfFeatures": 0.0,
+              "passes": int(max(1, self.getNumPasses())), "ipsEstimate": float(ips) / max(ex, 1.0),
+              "snipsEstimate": float(ips) / snips_den if snips_den else 0.0, "syncBytes": 0,
+              "timeTotalNs": t2 - t0, "timeNativeIngestNs": t1 - t0, "timeLearnNs": t2 - t1, "timeMultipassNs": 0}
+        return _GpuTrainedModel(g.export_model(args), args, info), st
+
     def _train_partition(self, df: DataFrame, args: str, model_bytes=None):
         import time
 
+        if (self.getDeviceType() or "cpu").lower() == "gpu":
+            return self._train_partition_gpu(df, args, model_bytes)
         t0 = time.perf_counter_ns()
         vw = _vw().VW(args, model_bytes)
         if D.world_size() > 1:

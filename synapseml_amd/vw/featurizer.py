@@ -11,7 +11,7 @@ import numpy as np
 
 from ..core.contracts import HasInputCols, HasOutputCol
 from ..core.dataframe import DataFrame
-from ..core.linalg import DenseVector, SparseVector
+from ..core.linalg import CsrColumn, DenseVector, SparseVector
 from ..core.params import Param, TypeConverters as T
 from ..core.pipeline import Transformer
 from ..ops import native
@@ -116,32 +116,40 @@ class VowpalWabbitFeaturizer(HasNumBits, HasInputCols, HasOutputCol):
         prefix_on = self.getPrefixStringsWithColumnName()
         split_cols = set(self.getStringSplitInputCols() or [])
         n = df.count()
-        per_row_idx: List[List[np.ndarray]] = [[] for _ in range(n)]
-        per_row_val: List[List[np.ndarray]] = [[] for _ in range(n)]
+        # features accumulate as COO chunks (row, index, value) in column order; one stable sort by row then
+        # keeps each row's features in column order, as the per-row concatenation did
+        R: List[np.ndarray] = []
+        I: List[np.ndarray] = []
+        V: List[np.ndarray] = []
+
+        def add_coo(rows, idx, val):
+            R.append(np.asarray(rows, dtype=np.int64))
+            I.append(np.asarray(idx, dtype=np.int64))
+            V.append(np.asarray(val, dtype=np.float64))
 
         def add(i, idx, val):
-            per_row_idx[i].append(np.asarray(idx, dtype=np.int64))
-            per_row_val[i].append(np.asarray(val, dtype=np.float64))
+            idx = np.asarray(idx, dtype=np.int64)
+            add_coo(np.full(len(idx), i, np.int64), idx, val)
 
         for c in self._all_cols():
             col = df[c]
             pre = c if prefix_on else ""
+            if isinstance(col, CsrColumn):  # columnar sparse vectors: indices kept (masked to the table)
+                ip, ind, val = col.csr()
+                ind = ind.astype(np.int64)
+                add_coo(np.repeat(np.arange(n, dtype=np.int64), np.diff(ip)), ind & mask if col.size >= mask + 1 else ind,
+                        val)
+                continue
             if isinstance(col, np.ndarray) and col.ndim == 2:  # dense vector column
                 width = col.shape[1]
                 idx = np.arange(width, dtype=np.int64) & mask if width >= mask + 1 else np.arange(width)
-                for i in range(n):
-                    add(i, idx, col[i])
+                add_coo(np.repeat(np.arange(n, dtype=np.int64), width), np.tile(idx, n), col.reshape(-1))
                 continue
             if col.dtype.kind in "biuf":
-                if col.dtype.kind == "b":
-                    h = int(vw.murmur3(c.encode(), ns_hash)) & mask
-                    for i in np.nonzero(col)[0]:
-                        add(int(i), [h], [1.0])
-                else:
-                    h = int(vw.murmur3(c.encode(), ns_hash)) & mask
-                    vals = col.astype(np.float64)
-                    for i in np.nonzero(vals)[0]:
-                        add(int(i), [h], [vals[i]])
+                h = int(vw.murmur3(c.encode(), ns_hash)) & mask
+                vals = col.astype(np.float64)
+                nz = np.flatnonzero(vals)
+                add_coo(nz, np.full(len(nz), h, np.int64), np.ones(len(nz)) if col.dtype.kind == "b" else vals[nz])
                 continue
             # object columns: strings, string lists, maps, vectors
             vals = col.tolist()
@@ -151,10 +159,8 @@ class VowpalWabbitFeaturizer(HasNumBits, HasInputCols, HasOutputCol):
                 toks = [vals[i].split() if c in split_cols else [vals[i]] for i in strs]
                 flat = [pre + t for tk in toks for t in tk]
                 hs = hash_strings(flat, ns_hash, mask).astype(np.int64)
-                pos = 0
-                for i, tk in zip(strs, toks):
-                    add(i, hs[pos:pos + len(tk)], np.ones(len(tk)))
-                    pos += len(tk)
+                cnt = np.fromiter((len(tk) for tk in toks), dtype=np.int64, count=len(toks))
+                add_coo(np.repeat(np.asarray(strs, np.int64), cnt), hs, np.ones(len(hs)))
                 continue
             for i, v in enumerate(vals):
                 if v is None:
@@ -168,12 +174,12 @@ class VowpalWabbitFeaturizer(HasNumBits, HasInputCols, HasOutputCol):
                     add(i, hs, np.ones(len(v)))
                 elif isinstance(v, dict):
                     keys = [str(k) for k in v.keys()]
-                    vals = np.asarray([float(x) if not isinstance(x, str) else 1.0 for x in v.values()])
+                    mvals = np.asarray([float(x) if not isinstance(x, str) else 1.0 for x in v.values()])
                     if any(isinstance(x, str) for x in v.values()):
                         keys = [f"{k}{x}" if isinstance(x, str) else k for k, x in v.items()]
                     hs = vw.murmur_batch(keys, ns_hash, c) & mask
-                    nz = vals != 0
-                    add(i, hs[nz], vals[nz])
+                    nz = mvals != 0
+                    add(i, hs[nz], mvals[nz])
                 elif isinstance(v, SparseVector):
                     add(i, v.indices.astype(np.int64) & mask if v.size >= mask + 1 else v.indices, v.values)
                 elif isinstance(v, (DenseVector, np.ndarray, list, tuple)):
@@ -187,17 +193,30 @@ class VowpalWabbitFeaturizer(HasNumBits, HasInputCols, HasOutputCol):
                     if fv != 0:
                         add(i, [int(vw.murmur3(c.encode(), ns_hash)) & mask], [fv])
         size = (1 << 30) if po > 0 else (1 << nb)
-        out = np.empty(n, dtype=object)
-        for i in range(n):
-            idx = np.concatenate(per_row_idx[i]) if per_row_idx[i] else np.zeros(0, np.int64)
-            val = np.concatenate(per_row_val[i]) if per_row_val[i] else np.zeros(0)
-            if po > 0:
-                if len(idx) > (1 << po):
-                    raise ValueError(f"Too many features {len(idx)} for preserveOrderNumBits={po}")
-                idx = idx | (np.arange(len(idx), dtype=np.int64) << (30 - po))
-            si, sv = sort_and_distinct(idx, val, self.getSumCollisions())
-            out[i] = SparseVector(size, si, sv)
-        return df.withColumn(self.getOutputCol(), out)
+        rows = np.concatenate(R) if R else np.zeros(0, np.int64)
+        idx = np.concatenate(I) if I else np.zeros(0, np.int64)
+        val = np.concatenate(V) if V else np.zeros(0)
+        order = np.argsort(rows, kind="stable")
+        rows, idx, val = rows[order], idx[order], val[order]
+        counts = np.bincount(rows, minlength=n) if len(rows) else np.zeros(n, np.int64)
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        if po > 0:
+            if len(counts) and counts.max() > (1 << po):
+                raise ValueError(f"Too many features {int(counts.max())} for preserveOrderNumBits={po}")
+            pos = np.arange(len(rows), dtype=np.int64) - starts[rows]
+            idx = idx | (pos << (30 - po))
+        # VectorUtils.sortAndDistinct per row: sort by index (stable), merge duplicates (sum or keep the first)
+        order = np.lexsort((idx, rows))
+        rows, idx, val = rows[order], idx[order], val[order]
+        first = np.ones(len(rows), dtype=bool)
+        if len(rows) > 1:
+            first[1:] = (rows[1:] != rows[:-1]) | (idx[1:] != idx[:-1])
+        heads = np.flatnonzero(first)
+        out_val = np.add.reduceat(val, heads) if (self.getSumCollisions() and len(heads)) else val[heads]
+        out_rows, out_idx = rows[heads], idx[heads]
+        indptr = np.zeros(n + 1, np.int64)
+        np.cumsum(np.bincount(out_rows, minlength=n) if len(out_rows) else np.zeros(n, np.int64), out=indptr[1:])
+        return df.withColumn(self.getOutputCol(), CsrColumn(indptr, out_idx.astype(np.int32), out_val, size))
 
 
 class VowpalWabbitInteractions(HasNumBits, HasInputCols, HasOutputCol):

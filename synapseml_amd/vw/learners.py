@@ -23,7 +23,7 @@ import numpy as np
 from ..core.contracts import (HasFeaturesCol, HasLabelCol, HasPredictionCol, HasProbabilityCol,
                               HasRawPredictionCol, HasWeightCol)
 from ..core.dataframe import DataFrame
-from ..core.linalg import DenseVector, SparseVector
+from ..core.linalg import CsrColumn, DenseVector, SparseVector
 from ..core.params import Param, TypeConverters as T
 from ..core.pipeline import Estimator, Model, Transformer
 from ..core.utils import ParamsStringBuilder, StopWatch
@@ -108,6 +108,10 @@ def namespace_blocks(df: DataFrame, cols: List[str], hash_seed: int):
         col = df[c]
         ns_hash = murmur_hash(c, hash_seed) & 0xFFFFFFFF
         group = c[0]
+        if isinstance(col, CsrColumn):  # columnar sparse rows: zero-copy (indices are already hashed)
+            ip, ind, val = col.csr()
+            blocks.append((group, ip, ind.astype(np.uint32, copy=False), val.astype(np.float32, copy=False)))
+            continue
         if isinstance(col, np.ndarray) and col.ndim == 2:
             width = col.shape[1]
             nz = col != 0
@@ -245,26 +249,68 @@ class _GpuTrainedModel:
         return self._model
 
 
-def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
-    """Device-resident hogwild mini-batch learner (csrc/vw/vw_gpu.hip, K12).
+def _expand_interactions(specs, chars: List[str]) -> List[tuple]:
+    """VW interaction strings (-q / --cubic / --interactions) -> concrete namespace tuples over `chars` (the
+    namespaces present). A ':' position ranges over the present namespaces in sorted order and each unordered
+    multiset is kept once (its first arrangement: `::` gives ab, never ba), as vw_core.cpp ForEachFeature does
+    per example; explicit namespaces that are absent contribute nothing and are dropped."""
+    present = sorted(chars)
+    out = []
+    for q in specs:
+        if len(q) not in (2, 3):
+            continue
+        if ":" not in q:
+            if all(c in chars for c in q):
+                out.append(tuple(q))
+            continue
+        seen = set()
+        pools = [present if c == ":" else [c] for c in q]
+        import itertools
 
-    Runs VW's update rule - adaptive + normalized + invariant by default, or the subset the command line
-    selects (--sgd / --adaptive / --normalized / --invariant) - for squared / logistic loss, scalar
-    learners and --oaa K, with -q interactions expanded on the host. gpuBatchSize=1 is the exact
-    sequential learner; larger batches update concurrently with atomics (hogwild). csoaa, contextual
-    bandits, CATS, l1, ngrams, ignore and cubic interactions run on the CPU learner and are rejected here
-    rather than silently run elsewhere. Ranks average the blocks they touched at every sync with RCCL
-    (VW's weighted averaging), and the model is exported from the device nonzeros."""
-    vwmod = _vw()
-    info = vwmod.describe_args(args)  # parses + validates the command line without a host table
-    bad = [k for k in ("csoaa", "cats", "ngram") if int(info[k])] + (["cb_adf"] if info["cb_adf"] == "1" else []) + \
-        (["l1"] if float(info["l1"]) else []) + (["ignore"] if info["ignore"] else []) + \
-        (["loss_function " + info["loss_function"]] if info["loss_function"] not in ("squared", "logistic") else []) + \
-        (["cubic interactions"] if any(len(q) > 2 for q in info["interactions"].split(",") if q) else [])
-    if bad:
-        raise ValueError(f"deviceType='gpu' does not run {', '.join(bad)}; use deviceType='cpu' (args: {args})")
-    if not vwmod.gpu_available():
-        raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
+        for combo in itertools.product(*pools):
+            if not all(c in chars for c in combo):
+                continue
+            key = tuple(sorted(combo))
+            if key in seen:
+                continue
+            seen.add(key)
+            out.append(combo)
+    return out
+
+
+def _device_plan(blocks, info, shared_blocks=None):
+    """Namespace blocks -> GpuSgd.stage_plan arguments: (gpu blocks [(group, level, ip, idx, val)], ngroups,
+    interactions as group-id triples). Ignored namespaces are dropped; blocks sharing a first letter form one
+    namespace (the host learner's Example::Get merge); `shared_blocks` (CB) are level-1 blocks read through the
+    row map."""
+    ignore = set(info.get("ignore", ""))
+    chars: List[str] = []
+    gpu_blocks = []
+    for level, bl in ((0, blocks), (1, shared_blocks or [])):
+        for g, ip, ii, vv in bl:
+            if g in ignore:
+                continue
+            if g not in chars:
+                chars.append(g)
+            gpu_blocks.append((chars.index(g), level, np.ascontiguousarray(ip, np.int64),
+                               np.ascontiguousarray(ii, np.uint32), np.ascontiguousarray(vv, np.float32)))
+    specs = [q for q in info.get("interactions", "").split(",") if q]
+    inter = [tuple(chars.index(c) for c in t) + ((-1,) if len(t) == 2 else ()) for t in _expand_interactions(specs, chars)]
+    return gpu_blocks, len(chars), inter
+
+
+def _gpu_refusals(info) -> List[str]:
+    """options the device learner does not run (deviceType='gpu' refuses them rather than silently running
+    something else)"""
+    bad = [k for k in ("cats",) if int(info[k])]
+    bad += ["l1"] if float(info["l1"]) else []
+    bad += ["loss_function " + info["loss_function"]] if info["loss_function"] not in ("squared", "logistic") else []
+    if info["cb_adf"] == "1" and info.get("cb_type", "mtr") not in ("mtr", "dr", "ips"):
+        bad.append("cb_type " + info["cb_type"])
+    return bad
+
+
+def _gpu_config(vwmod, info):
     cfg = vwmod.GpuSgdConfig()
     cfg.bits = int(info["bits"])
     cfg.lr = float(info["learning_rate"])
@@ -274,44 +320,49 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     cfg.loss = 1 if info["loss_function"] == "logistic" else 0
     cfg.adaptive, cfg.normalized, cfg.invariant = (info[k] == "1" for k in ("adaptive", "normalized", "invariant"))
     cfg.oaa = int(info["oaa"])
+    cfg.csoaa = int(info["csoaa"])
+    if info["cb_adf"] == "1":
+        cfg.cb = {"mtr": 0, "dr": 1, "ips": 2}[info.get("cb_type", "mtr")]
+        cfg.cb_explore = info.get("cb_explore", "0") == "1"
+        cfg.epsilon = float(info.get("epsilon", "0.05"))
+    return cfg
+
+
+def _gpu_learner(args: str, model_bytes=None):
+    vwmod = _vw()
+    info = vwmod.describe_args(args)  # parses + validates the command line without a host table
+    bad = _gpu_refusals(info)
+    if bad:
+        raise ValueError(f"deviceType='gpu' does not run {', '.join(bad)}; use deviceType='cpu' (args: {args})")
+    if not vwmod.gpu_available():
+        raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
     import os
 
-    dev = int(os.environ.get("LOCAL_RANK", "0"))
-    g = vwmod.GpuSgd(cfg, dev)
+    g = vwmod.GpuSgd(_gpu_config(vwmod, info), int(os.environ.get("LOCAL_RANK", "0")))
     if model_bytes is not None:  # initialModel: warm start (weights, adaptive / normalizer state, schedule)
         g.import_model(bytes(model_bytes))
-    t0 = time.perf_counter_ns()
-    cols = [est.getFeaturesCol()] + list(est.getAdditionalFeatures() or [])
-    blocks = namespace_blocks(df, cols, est.getHashSeed())
-    labels, multiclass, _ = est._labels(df)
-    if cfg.oaa > 0:
-        if multiclass is None:
-            raise ValueError("--oaa needs integer class labels")
-        labels = np.asarray(multiclass, np.float32)
-    n = df.count()
-    blocks = blocks + [_interaction_block(blocks, pq, n) for pq in _quadratic_pairs(args)]
-    indptr, idx, val = _merged_csr(blocks, n, info["constant"] == "1")
-    wcol = est.getWeightCol()
-    weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
-    t1 = time.perf_counter_ns()
+    return vwmod, info, g
+
+
+def _gpu_sync_comm(vwmod):
     world = D.world_size()
-    comm = None
-    if world > 1:
-        if D.backend() != "nccl":
-            raise RuntimeError("the GPU VW learner averages over RCCL: start the ranks with the nccl backend")
-        key = world
-        if key not in _nccl_cache:
-            uid = vwmod.nccl_unique_id() if D.rank() == 0 else None
-            _nccl_cache[key] = vwmod.nccl_comm(D.broadcast_object(uid, 0), D.rank(), world)
-        comm = _nccl_cache[key]
-    # numSyncsPerPass intermediate weight averages + the end-of-pass one, the same count on every rank
-    # whatever its row count (VowpalWabbitSyncSchedule.scala:36-72)
+    if world <= 1:
+        return None
+    if D.backend() != "nccl":
+        raise RuntimeError("the GPU VW learner averages over RCCL: start the ranks with the nccl backend")
+    if world not in _nccl_cache:
+        uid = vwmod.nccl_unique_id() if D.rank() == 0 else None
+        _nccl_cache[world] = vwmod.nccl_comm(D.broadcast_object(uid, 0), D.rank(), world)
+    return _nccl_cache[world]
+
+
+def _gpu_learn_staged(est, g, comm, n: int):
+    """numSyncsPerPass intermediate weight averages + the end-of-pass one, the same count on every rank
+    whatever its row count (VowpalWabbitSyncSchedule.scala:36-72); the staged rows are re-read from HBM by
+    every pass and segment (VW's cache file)."""
     segs = max(0, int(est.getNumSyncsPerPass() or 0)) + 1
     bounds = np.linspace(0, n, segs + 1).astype(np.int64)
     sync_bytes = []
-    # the partition's CSR goes to HBM once; every pass and sync segment learns from there (VW's cache file)
-    g.stage(indptr, idx, val, np.ascontiguousarray(labels, dtype=np.float32),
-            None if weights is None else np.ascontiguousarray(weights, dtype=np.float32))
     for _ in range(max(1, est.getNumPasses())):
         for s0, s1 in zip(bounds[:-1], bounds[1:]):
             if s1 > s0:
@@ -319,17 +370,105 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
             if comm is not None:
                 g.allreduce_average(comm)
                 sync_bytes.append(int(g.last_sync_bytes))
+    return sync_bytes
+
+
+def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
+    """Device-resident hogwild mini-batch learner (csrc/vw/vw_gpu.hip, K12).
+
+    Runs VW's update rule - adaptive + normalized + invariant by default, or the subset the command line
+    selects (--sgd / --adaptive / --normalized / --invariant) - for squared / logistic loss, scalar learners
+    and --oaa K. The partition's namespace blocks go to HBM as they are and the example rows are built there
+    (device featurization: -q / --cubic / --interactions incl. ':' wildcards, ignored namespaces, the
+    constant). gpuBatchSize=1 is the exact sequential learner; larger batches update concurrently with
+    atomics (hogwild). Ranks average the blocks they touched at every sync with RCCL (VW's weighted
+    averaging), and the model is exported from the device nonzeros."""
+    vwmod, info, g = _gpu_learner(args, model_bytes)
+    if info["cb_adf"] == "1":
+        raise ValueError("deviceType='gpu' runs --cb_adf / --cb_explore_adf through VowpalWabbitContextualBandit or "
+                         "VowpalWabbitGeneric (multi-line examples), not a single-line estimator")
+    t0 = time.perf_counter_ns()
+    cols = [est.getFeaturesCol()] + list(est.getAdditionalFeatures() or [])
+    blocks = namespace_blocks(df, cols, est.getHashSeed())
+    labels, multiclass, costs = est._labels(df)
+    if int(info["oaa"]) > 0:
+        if multiclass is None:
+            raise ValueError("--oaa needs integer class labels")
+        labels = np.asarray(multiclass, np.float32)
+    n = df.count()
+    wcol = est.getWeightCol()
+    weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
+    gb, ng, inter = _device_plan(blocks, info)
+    g.stage_plan(gb, ng, inter, info["constant"] == "1", None, n, np.ascontiguousarray(labels, dtype=np.float32),
+                 None if weights is None else np.ascontiguousarray(weights, dtype=np.float32))
+    if int(info["csoaa"]) > 0:
+        if costs is None:
+            raise ValueError("--csoaa needs per-row (class, cost) lists")
+        cptr = np.concatenate([[0], np.cumsum([len(c) for c in costs])]).astype(np.int64)
+        g.stage_costs(cptr, np.asarray([k for c in costs for k, _ in c], np.int32),
+                      np.asarray([v for c in costs for _, v in c], np.float32))
+    t1 = time.perf_counter_ns()
+    sync_bytes = _gpu_learn_staged(est, g, _gpu_sync_comm(vwmod), n)
     t2 = time.perf_counter_ns()
     lab = np.asarray(labels, np.float64)
     wts = np.ones(n) if weights is None else weights.astype(np.float64)
     wsum = float(wts.sum())
     stats = {"numberOfExamplesPerPass": int(n), "weightedExampleSum": wsum,
              "weightedLabelSum": float((lab * wts).sum()), "averageLoss": float(g.sum_loss) / max(wsum, 1e-300),
-             "bestConstant": float((lab * wts).sum()) / max(wsum, 1e-300), "totalNumberOfFeatures": float(len(idx)),
+             "bestConstant": float((lab * wts).sum()) / max(wsum, 1e-300),
+             "totalNumberOfFeatures": float(sum(len(b[3]) for b in gb)),
              "passes": int(max(1, est.getNumPasses())), "ipsEstimate": 0.0, "snipsEstimate": 0.0,
              "syncBytes": int(sum(sync_bytes)), "timeTotalNs": t2 - t0, "timeNativeIngestNs": t1 - t0,
              "timeLearnNs": t2 - t1, "timeMultipassNs": 0}
     return _GpuTrainedModel(g.export_model(args), args, info), stats
+
+
+class _GpuScorer:
+    """A VW model scored on the MI355X: the model's nonzeros are scattered into an HBM table (no dense host
+    table at any size - a 2^30-slot model is a 16 GiB device allocation, never a host one) and examples are
+    featurized and scored on the device (VowpalWabbitBaseModelSpark.scala:46-60 scores through native VW)."""
+
+    def __init__(self, args: str, model: bytes):
+        vwmod = _vw()
+        self.info = vwmod.describe_args(args)
+        bad = _gpu_refusals(self.info)
+        if bad or int(self.info["ngram"]) or not vwmod.gpu_available():
+            raise ValueError("model not scoreable on the device: " + ", ".join(bad or ["no HIP device / ngram"]))
+        import os
+
+        self.g = vwmod.GpuSgd(_gpu_config(vwmod, self.info), int(os.environ.get("LOCAL_RANK", "0")))
+        self.g.import_model(bytes(model))
+
+    def predict(self, blocks, n: int, shared_blocks=None, row_map=None):
+        gb, ng, inter = _device_plan(blocks, self.info, shared_blocks)
+        self.g.stage_plan(gb, ng, inter, self.info["constant"] == "1", row_map, n, None, None)
+        return self.g.predict_staged()
+
+    def predict_cb(self, action_blocks, shared_blocks, aip):
+        """contextual bandit scoring: per example the action probabilities (cb_explore: epsilon-greedy pmf)
+        or the action scores, in action order"""
+        aip = np.asarray(aip, np.int64)
+        ne = len(aip) - 1
+        counts = np.diff(aip)
+        row_map = np.repeat(np.arange(ne, dtype=np.int64), counts)
+        gb, ng, inter = _device_plan(action_blocks, self.info, shared_blocks)
+        self.g.stage_plan(gb, ng, inter, self.info["constant"] == "1", row_map, int(aip[-1]), None, None)
+        z = np.zeros(ne, np.float32)
+        self.g.stage_cb(aip, np.full(ne, -1, np.int32), z, np.ones(ne, np.float32))
+        scores, best = self.g.predict_staged()
+        out = []
+        eps = float(self.info.get("epsilon", "0.05"))
+        explore = self.info.get("cb_explore", "0") == "1"
+        for e in range(ne):
+            A = int(counts[e])
+            if explore:
+                p = np.full(A, eps / max(A, 1))
+                if A:
+                    p[int(best[e])] += 1.0 - eps
+                out.append(p.tolist())
+            else:
+                out.append([float(x) for x in scores[aip[e]:aip[e + 1]]])
+        return out
 
 
 class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
@@ -360,11 +499,34 @@ class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
         with open(path, "wb") as f:
             f.write(self.getModel())
 
+    def _gpu_scorer(self):
+        """device scorer for deviceType='gpu' models (None: score on the host learner)"""
+        if (self.getDeviceType() or "cpu").lower() != "gpu":
+            return None
+        args = self.getVwArgs() + " --testonly " + (self.getTestArgs() or "")
+        if "--probabilities" in args:
+            return None  # oaa probabilities: host learner
+        key = (id(self.getModel()), args)
+        cache = getattr(self, "_gpu_cache", None)
+        if cache is None or cache[0] != key:
+            try:
+                self._gpu_cache = (key, _GpuScorer(args, self.getModel()))
+            except ValueError:
+                self._gpu_cache = (key, None)
+        return self._gpu_cache[1]
+
     def _predict_raw(self, df: DataFrame, multiclass: bool = False):
-        vw = self._native_model()
         cols = [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or [])
         blocks = namespace_blocks(df, cols, self.getHashSeed())
         n = df.count()
+        gs = self._gpu_scorer()
+        if gs is not None:
+            preds, _ = gs.predict(blocks, n)
+            preds = np.asarray(preds, dtype=np.float64)
+            if gs.info["link_logistic"] == "1":
+                preds = 1.0 / (1.0 + np.exp(-preds))
+            return preds, []
+        vw = self._native_model()
         preds, scores = vw.learn_batch(blocks, np.zeros(n, np.float32), None, None, None, False)
         return np.asarray(preds, dtype=np.float64), scores
 
@@ -586,13 +748,52 @@ class VowpalWabbitGeneric(Estimator, HasPredictionCol):
     inputCol = Param("Column with examples in VW text format", "value", T.toString)
     numPasses = Param("Number of passes over the data", 1, T.toInt)
     initialModel = Param("Initial model to start from", None, complex=True)
+    numSyncsPerPass = Param("Number of times weights should be synchronized within each pass", 0, T.toInt)
+    deviceType = Param("cpu (exact sequential VW semantics) or gpu (hogwild mini-batch SGD on the MI355X: scalar, "
+                       "--oaa, --csoaa and --cb_adf / --cb_explore_adf)", "cpu", T.toString)
+    gpuBatchSize = Param("Mini-batch size of the GPU learner", 1024, T.toInt)
 
     def setInitialModel(self, model):  # noqa: N802
         self.set("initialModel", _initial_model_bytes(model))
         return self
 
+    def _fit_gpu(self, lines: List[str], args: str) -> "VowpalWabbitGenericModel":
+        """Text examples parsed on the host (the learner's hashing / ngrams), then learned on the device:
+        single-line examples (labels, importance weights, --oaa classes, --csoaa cost lists) or blank-line
+        separated ADF groups for --cb_adf / --cb_explore_adf (shared line + one line per action)."""
+        vwmod, info, g = _gpu_learner(args, self.getInitialModel())
+        cb = info["cb_adf"] == "1"
+        d = vwmod.parse_blocks(args, lines, cb)
+        if cb:
+            aip = np.asarray(d["aip"], np.int64)
+            ne = len(aip) - 1
+            row_map = np.repeat(np.arange(ne, dtype=np.int64), np.diff(aip))
+            gb, ng, inter = _device_plan(d["actions"], info, d["shared"])
+            g.stage_plan(gb, ng, inter, info["constant"] == "1", row_map, int(aip[-1]), None, None)
+            g.stage_cb(aip, d["chosen"], d["cost"], d["prob"])
+            n = ne
+        else:
+            n = len(d["labels"])
+            labels = np.asarray(d["multiclass"], np.float32) if int(info["oaa"]) > 0 else d["labels"]
+            weights = np.where(d["has_label"] > 0, d["weights"], 0.0).astype(np.float32)
+            gb, ng, inter = _device_plan(d["blocks"], info)
+            g.stage_plan(gb, ng, inter, info["constant"] == "1", None, n, np.ascontiguousarray(labels, np.float32),
+                         weights)
+            if int(info["csoaa"]) > 0:
+                g.stage_costs(d["cptr"], d["ccls"], d["ccost"])
+        _gpu_learn_staged(self, g, _gpu_sync_comm(vwmod), n)
+        m = VowpalWabbitGenericModel()
+        m.set("model", bytes(g.export_model(args)))
+        m.set("vwArgs", args)
+        m.set("inputCol", self.getInputCol())
+        m.set("predictionCol", self.getPredictionCol())
+        self._gpu_stats = g.cb_stats if cb else None
+        return m
+
     def _fit(self, df: DataFrame):
         args = self.getPassThroughArgs() + (f" --passes {self.getNumPasses()}" if self.getNumPasses() > 1 else "")
+        if (self.getDeviceType() or "cpu").lower() == "gpu":
+            return self._fit_gpu([str(s) for s in df[self.getInputCol()].tolist()], args)
         vw = _vw().VW(args, self.getInitialModel())
         if D.world_size() > 1:
             vw.set_allreduce(D.world_size(), _host_allreduce_f32)

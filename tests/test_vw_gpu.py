@@ -25,9 +25,8 @@ def test_merged_csr_matches_blocks():
     assert idx[2] == 11650396 and idx[4] == 11650396
 
 
-@pytest.mark.parametrize("args", ["--csoaa 3", "--cb_explore_adf", "--cats 4 --bandwidth 1 --min_value 0 --max_value 1",
-                                  "--l1 0.001", "--ngram 2", "--ignore a", "--loss_function hinge",
-                                  "--interactions abc"])
+@pytest.mark.parametrize("args", ["--cats 4 --bandwidth 1 --min_value 0 --max_value 1", "--l1 0.001",
+                                  "--loss_function hinge", "--loss_function quantile"])
 def test_gpu_rejects_reductions_it_does_not_run(args):
     """Reductions the device learner does not implement are refused by name before any GPU work,
     never silently run on the host."""
@@ -140,3 +139,130 @@ def test_gpu_oaa_multiclass():
     acc = lambda m: float(np.mean(m.transform(df)["prediction"] == y))
     ag, ac = acc(g), acc(c)
     assert ag > 0.8 and ag > ac - 0.03, (ag, ac)
+
+
+def _three_ns(n=3000, seed=11):
+    rng = np.random.default_rng(seed)
+    A = rng.normal(size=(n, 3))
+    B = rng.normal(size=(n, 2)) * np.array([1.0, 4.0])
+    C = rng.normal(size=(n, 2)) * 0.5
+    y = A[:, 0] * B[:, 1] - 0.5 * A[:, 2] * C[:, 0] + 0.3 * B[:, 0] * C[:, 1] * A[:, 1] + 0.05 * rng.normal(size=n)
+    return DataFrame({"a": A, "b": B, "c": C, "label": y})
+
+
+def _host_scored(model, df):
+    m = model.copy()
+    m.set("deviceType", "cpu")
+    return m.transform(df)["prediction"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", ["-q ab", "-q ::", "-q a:", "--cubic abc", "--cubic abb", "--cubic :::",
+                                  "-q :: --ignore b", "--interactions cab"])
+def test_gpu_device_featurization_batch1_parity(args):
+    """Device featurization (expand_count / expand_fill kernels: base namespaces, -q / --cubic incl. ':'
+    wildcards with VW's combination semantics, ignored namespaces, the constant): at gpuBatchSize=1 the
+    device learner equals the sequential host learner, and scoring the model on the device equals scoring
+    it on the host."""
+    df = _three_ns()
+    kw = dict(featuresCol="a", additionalFeatures=["b", "c"], passThroughArgs=args, numPasses=1)
+    g = VowpalWabbitRegressor(deviceType="gpu", gpuBatchSize=1, **kw).fit(df)
+    c = VowpalWabbitRegressor(**kw).fit(df)
+    p_dev = g.transform(df)["prediction"]            # device scoring of the device-trained model
+    p_host = _host_scored(g, df)                      # the same model through the host learner
+    p_cpu = c.transform(df)["prediction"]
+    scale = np.abs(p_cpu).max()
+    np.testing.assert_allclose(p_dev, p_host, rtol=1e-5, atol=1e-5 * scale)
+    np.testing.assert_allclose(p_host, p_cpu, rtol=1e-4, atol=1e-4 * scale)
+
+
+def _csoaa_lines(n=1500, seed=3):
+    rng = np.random.default_rng(seed)
+    lines = []
+    for i in range(n):
+        x = rng.normal(size=4)
+        k = int(np.argmax([x[0], x[1] - x[2], 0.3 + x[3]]))
+        costs = " ".join(f"{j + 1}:{0.0 if j == k else 1.0 + 0.1 * j}" for j in range(3))
+        lines.append(f"{costs} |f x0:{x[0]:.4f} x1:{x[1]:.4f} x2:{x[2]:.4f} x3:{x[3]:.4f} |g t{i % 7}")
+    return lines
+
+
+@pytest.mark.gpu
+def test_gpu_csoaa_generic_batch1_parity():
+    """--csoaa on the device (csoaa_kernel): class scores at the oaa offsets, argmin prediction, the example's
+    (class, cost) regressions applied in order. Text examples parsed on the host (VowpalWabbitGeneric
+    deviceType='gpu'); batch 1 equals the host learner's weights."""
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    lines = _csoaa_lines()
+    df = DataFrame({"value": np.asarray(lines, dtype=object)})
+    g = VowpalWabbitGeneric(passThroughArgs="--csoaa 3 -q fg", deviceType="gpu", gpuBatchSize=1).fit(df)
+    c = VowpalWabbitGeneric(passThroughArgs="--csoaa 3 -q fg").fit(df)
+    vw = native.load("_vw")
+    wg = np.asarray(vw.VW("--testonly", g.getModel()).weights())
+    wc = np.asarray(vw.VW("--testonly", c.getModel()).weights())
+    np.testing.assert_allclose(wg, wc, rtol=1e-4, atol=1e-5 * np.abs(wc).max())
+    pg, pc = g.transform(df)["prediction"], c.transform(df)["prediction"]
+    assert np.mean(pg == pc) > 0.999
+
+
+def _cb_frame(n=1200, A=4, seed=9):
+    from synapseml_amd.core.linalg import DenseVector
+
+    rng = np.random.default_rng(seed)
+    shared = rng.normal(size=(n, 3))
+    acts = np.empty(n, dtype=object)
+    chosen = rng.integers(1, A + 1, size=n)
+    cost = np.empty(n)
+    for i in range(n):
+        feats = [DenseVector(rng.normal(size=3)) for _ in range(A)]
+        acts[i] = feats
+        f = feats[chosen[i] - 1].values
+        cost[i] = float(shared[i, 0] * f[0] - f[1] > 0)
+    return DataFrame({"shared": shared, "features": acts, "chosenAction": chosen.astype(np.int32),
+                      "label": cost, "probability": np.full(n, 1.0 / A)})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cb_type", ["mtr", "dr", "ips"])
+def test_gpu_contextual_bandit_batch1_parity(cb_type):
+    """--cb_explore_adf on the device (cb_kernel): action rows featurized with their example's shared
+    namespaces, epsilon-greedy pmf, --cb_type mtr / dr / ips updates. Batch 1 = the host learner: same
+    weights, same action probabilities, same IPS / SNIPS estimates."""
+    from synapseml_amd.vw.bandit import VowpalWabbitContextualBandit
+
+    df = _cb_frame()
+    kw = dict(epsilon=0.1, passThroughArgs=f"--cb_type {cb_type} -q sf")
+    g = VowpalWabbitContextualBandit(deviceType="gpu", gpuBatchSize=1, **kw).fit(df)
+    c = VowpalWabbitContextualBandit(**kw).fit(df)
+    vw = native.load("_vw")
+    wg = np.asarray(vw.VW("--testonly", g.getModel()).weights())
+    wc = np.asarray(vw.VW("--testonly", c.getModel()).weights())
+    np.testing.assert_allclose(wg, wc, rtol=1e-4, atol=1e-5 * max(np.abs(wc).max(), 1e-6))
+    pg = np.stack(g.transform(df)["prediction"])
+    pc = np.stack(c.transform(df)["prediction"])
+    assert np.mean(np.all(np.abs(pg - pc) < 1e-6, axis=1)) > 0.99
+    sg, sc = g.getPerformanceStatistics(), c.getPerformanceStatistics()
+    np.testing.assert_allclose(sg["ipsEstimate"][0], sc["ipsEstimate"][0], rtol=1e-4)
+    np.testing.assert_allclose(sg["snipsEstimate"][0], sc["snipsEstimate"][0], rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_scoring_b30_model_keeps_host_memory_flat():
+    """A 2^30-slot model (16 GiB as a dense table) is transformed on the device from its nonzeros: host RSS
+    stays flat (the host learner would allocate the dense table)."""
+    import psutil
+
+    rng = np.random.default_rng(2)
+    X = rng.normal(size=(20000, 8))
+    y = (X[:, 0] - X[:, 1] > 0).astype(np.float64)
+    df = DataFrame({"features": X, "label": y})
+    m = VowpalWabbitClassifier(deviceType="gpu", numBits=30, labelConversion=True,
+                               passThroughArgs="--loss_function logistic", gpuBatchSize=256).fit(df)
+    proc = psutil.Process()
+    rss0 = proc.memory_info().rss
+    out = m.transform(df)
+    rss1 = proc.memory_info().rss
+    assert rss1 - rss0 < (1 << 30), (rss0, rss1)
+    acc = np.mean(out["prediction"] == y)
+    assert acc > 0.95
