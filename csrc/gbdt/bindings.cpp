@@ -277,6 +277,18 @@ PYBIND11_MODULE(_gbdt, m) {
            py::arg("train"), py::arg("params"), py::arg("comm") = py::none(), py::keep_alive<1, 4>())
       .def_static("from_model_string", [](const std::string& s) { return std::shared_ptr<Booster>(Booster::FromModelString(s)); })
       .def("add_valid", [](Booster& b, PyDataset& d, const std::string& name) { b.AddValidData(d.d, name); })
+      // objective output transform (sigmoid / softmax / exp ...) of raw scores, n x num_model_per_iteration
+      .def("convert_outputs", [](const Booster& b, F64 raw) {
+        const int64_t n = raw.ndim() == 2 ? raw.shape(0) : raw.size();
+        py::array_t<double> out(std::vector<py::ssize_t>(raw.shape(), raw.shape() + raw.ndim()));
+        double* o = out.mutable_data();
+        const double* r = raw.data();
+        {
+          py::gil_scoped_release rel;
+          b.ConvertOutputs(r, n, o);
+        }
+        return out;
+      })
       .def("merge", &Booster::MergeFrom)
       .def("reset_parameter", &Booster::ResetParameter)
       .def("update",
@@ -376,6 +388,26 @@ PYBIND11_MODULE(_gbdt, m) {
              return out;
            },
            py::arg("X"), py::arg("normal") = false)
+      // raw scores of a float32 or float64 row-major batch in ONE device pass (chunked pinned upload overlapped
+      // with the traversal); no dtype conversion of the input on the host
+      .def("predict_raw",
+           [](GpuPredictor& p, py::array X) {
+             if (X.ndim() != 2) throw std::runtime_error("predict_raw: X must be 2-D");
+             const bool f32 = X.dtype().is(py::dtype::of<float>());
+             py::array Xc = f32 ? py::array(py::array_t<float, py::array::c_style | py::array::forcecast>(X))
+                                : py::array(py::array_t<double, py::array::c_style | py::array::forcecast>(X));
+             const int64_t n = Xc.shape(0);
+             const int nc = static_cast<int>(Xc.shape(1));
+             py::array_t<double> out({n, static_cast<int64_t>(p.NumOutputs())});
+             double* o = out.mutable_data();
+             const void* x = Xc.data();
+             {
+               py::gil_scoped_release rel;
+               p.PredictRaw(x, f32, n, nc, o);
+             }
+             return out;
+           },
+           py::arg("X"))
       .def("predict_contrib", [](GpuPredictor& p, const Booster& b, F64 X) -> py::object {
         const int64_t n = X.shape(0);
         py::array_t<double> out({n, static_cast<int64_t>((b.NumFeatures() + 1) * p.NumOutputs())});

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "booster.h"
+#include "dataset.h"
 #include "hip_common.h"
 #include "trace.h"
 #include "predictor.h"
@@ -36,9 +37,10 @@ struct PackedEnsemble {
 };
 
 // child reached from internal node gi (global index) for feature vector `row`
-__device__ __forceinline__ int NodeNext(const PackedEnsemble& e, int gi, const double* row, int ncols) {
+template <typename T>
+__device__ __forceinline__ int NodeNext(const PackedEnsemble& e, int gi, const T* row, int ncols) {
   const int f = e.feat[gi];
-  double x = f < ncols ? row[f] : 0.0;
+  double x = f < ncols ? static_cast<double>(row[f]) : 0.0;
   const int fl = e.flags[gi];
   if (fl & 1) {
     int iv = isnan(x) ? -1 : static_cast<int>(x);
@@ -56,7 +58,8 @@ __device__ __forceinline__ int NodeNext(const PackedEnsemble& e, int gi, const d
   return x <= e.thr[gi] ? e.left[gi] : e.right[gi];
 }
 
-__device__ __forceinline__ int TraverseTree(const PackedEnsemble& e, int t, const double* row, int ncols) {
+template <typename T>
+__device__ __forceinline__ int TraverseTree(const PackedEnsemble& e, int t, const T* row, int ncols) {
   if (e.num_leaves[t] <= 1) return 0;
   const int no = e.node_off[t];
   int node = 0;
@@ -65,23 +68,25 @@ __device__ __forceinline__ int TraverseTree(const PackedEnsemble& e, int t, cons
   return node < 0 ? ~node : 0;
 }
 
-template <bool LEAF>
-__global__ __launch_bounds__(kPredThreads) void predict_kernel(PackedEnsemble e, const double* __restrict__ X,
+// T = double or float: float32 feature rows are scored as they are (a float converts to double exactly, so the
+// threshold comparisons are those of the float64 path) - half the bytes over PCIe and in LDS.
+template <bool LEAF, typename T = double>
+__global__ __launch_bounds__(kPredThreads) void predict_kernel(PackedEnsemble e, const T* __restrict__ X,
                                                               int64_t n, int ncols, double* __restrict__ out,
                                                               int32_t* __restrict__ leaf_out, double avg_div) {
-  __shared__ double tile[kPredThreads * kMaxStagedCols];
+  __shared__ T tile[kPredThreads * kMaxStagedCols];
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kPredThreads;
   const int rows = static_cast<int>(min<int64_t>(kPredThreads, n - row0));
   const bool staged = ncols <= kMaxStagedCols;
   if (staged) {
     const int total = rows * ncols;
-    const double* src = X + row0 * ncols;
+    const T* src = X + row0 * ncols;
     for (int i = threadIdx.x; i < total; i += kPredThreads) tile[i] = src[i];
     __syncthreads();
   }
   const int r = threadIdx.x;
   if (r >= rows) return;
-  const double* row = staged ? tile + r * ncols : X + (row0 + r) * ncols;
+  const T* row = staged ? tile + r * ncols : X + (row0 + r) * ncols;
   const int64_t gi = row0 + r;
   if (LEAF) {
     for (int t = 0; t < e.num_trees; ++t) leaf_out[gi * e.num_trees + t] = TraverseTree(e, t, row, ncols);
@@ -335,6 +340,54 @@ void GpuPredictor::Predict(const double* X, int64_t n, int ncols, bool normal, d
     std::vector<double> raw(out, out + n * num_out_);
     booster_->ConvertOutputs(raw.data(), n, out);
   }
+}
+
+// One device pass over a batch in its own dtype: rows go to HBM through the pinned multi-threaded staging
+// pipeline (UploadPinned) in chunks, chunk c+1's upload overlapping chunk c's traversal, and the raw scores
+// come back once; the transformed outputs (probabilities) are derived from them on the host
+// (Booster::ConvertOutputs), so a transform never runs the ensemble twice.
+void GpuPredictor::PredictRaw(const void* X, bool f32, int64_t n, int ncols, double* out) {
+  TraceRange tr("sml::PredictRaw");
+  if (n <= 0) return;
+  const size_t esz = f32 ? 4 : 8;
+  const int64_t chunk = std::max<int64_t>(kPredThreads, (static_cast<int64_t>(256) << 20) / std::max<int64_t>(1, ncols * esz));
+  const int64_t rows_buf = std::min<int64_t>(n, chunk);
+  impl_->x.alloc((2 * static_cast<size_t>(rows_buf) * ncols * esz + sizeof(double) - 1) / sizeof(double));  // 2 chunk buffers
+  impl_->o.alloc(static_cast<size_t>(n) * num_out_);
+  hipStream_t s = impl_->stream;
+  char* xb[2] = {reinterpret_cast<char*>(impl_->x.get()),
+                 reinterpret_cast<char*>(impl_->x.get()) + static_cast<size_t>(rows_buf) * ncols * esz};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (auto& e : done) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  bool used[2] = {false, false};
+  try {
+    int k = 0;
+    for (int64_t r0 = 0; r0 < n; r0 += chunk, k ^= 1) {
+      const int64_t m = std::min(chunk, n - r0);
+      if (used[k]) SML_HIP_CHECK(hipEventSynchronize(done[k]));  // the traversal that read this buffer finished
+      UploadPinned(static_cast<const char*>(X) + static_cast<size_t>(r0) * ncols * esz, xb[k],
+                   static_cast<size_t>(m) * ncols * esz);
+      const int grid = static_cast<int>((m + kPredThreads - 1) / kPredThreads);
+      if (f32)
+        hipLaunchKernelGGL((predict_kernel<false, float>), dim3(grid), dim3(kPredThreads), 0, s, impl_->e,
+                           reinterpret_cast<const float*>(xb[k]), m, ncols, impl_->o.get() + r0 * num_out_,
+                           static_cast<int32_t*>(nullptr), impl_->avg_div);
+      else
+        hipLaunchKernelGGL((predict_kernel<false, double>), dim3(grid), dim3(kPredThreads), 0, s, impl_->e,
+                           reinterpret_cast<const double*>(xb[k]), m, ncols, impl_->o.get() + r0 * num_out_,
+                           static_cast<int32_t*>(nullptr), impl_->avg_div);
+      SML_HIP_CHECK(hipGetLastError());
+      SML_HIP_CHECK(hipEventRecord(done[k], s));
+      used[k] = true;
+    }
+    SML_HIP_CHECK(hipMemcpyAsync(out, impl_->o.get(), sizeof(double) * n * num_out_, hipMemcpyDeviceToHost, s));
+    SML_HIP_CHECK(hipStreamSynchronize(s));
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    for (auto& e : done) (void)hipEventDestroy(e);
+    throw;
+  }
+  for (auto& e : done) (void)hipEventDestroy(e);
 }
 
 void GpuPredictor::PredictLeaf(const double* X, int64_t n, int ncols, int32_t* out) {

@@ -18,6 +18,8 @@ class GpuPredictor {
   int NumOutputs() const { return num_out_; }
   int NumTrees() const { return num_trees_; }
   void Predict(const double* X, int64_t n, int ncols, bool normal, double* out);
+  // raw scores of float32 (f32) or float64 rows, one chunked upload + traversal pass (n x NumOutputs)
+  void PredictRaw(const void* X, bool f32, int64_t n, int ncols, double* out);
   void PredictLeaf(const double* X, int64_t n, int ncols, int32_t* out);
   // TreeSHAP contributions, layout of Booster::Predict(kPredictContrib);
   // false if a path has more unique features than a wave64 holds

@@ -581,7 +581,16 @@ PYBIND11_MODULE(_vw, m) {
         put(t); put(tw); put(snx);
         put(g.min_label()); put(g.max_label());
         put(static_cast<uint64_t>(idx.size()));
-        for (size_t i = 0; i < idx.size(); ++i) { put(idx[i]); put(val[i]); }
+        // (index, value) records: one resize + a parallel fill (a 2^30-slot model can hold ~1e8 nonzeros)
+        const size_t head = s.size();
+        s.resize(head + idx.size() * 12);
+        char* dst = &s[head];
+        const int64_t m = static_cast<int64_t>(idx.size());
+#pragma omp parallel for schedule(static) if (m > (1 << 16))
+        for (int64_t i = 0; i < m; ++i) {
+          std::memcpy(dst + i * 12, &idx[i], 8);
+          std::memcpy(dst + i * 12 + 8, &val[i], 4);
+        }
         return py::bytes(s);
       })
       // warm start from model bytes of either learner (same format)

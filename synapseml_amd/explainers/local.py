@@ -117,36 +117,97 @@ class LocalExplainer(Transformer, HasOutputCol):
 
 
 # ---------------------------------------------------------------------- KernelSHAP
+def effective_num_samples(num_samples, m: int) -> int:
+    """coalition budget: the numSamples param (default 2 * M + 2048, shap's default) clamped to
+    [M + 2, 2^M] (KernelSHAPBase.scala:132-139)"""
+    value = num_samples if num_samples else 2 * m + 2048
+    return int(min(max(value, m + 2), 2 ** m if m < 63 else value))
+
+
+def shap_sample_sizes(m: int, num_samples: int, kernel_weight) -> List[Tuple[int, float]]:
+    """(number of coalitions, weight) per coalition-size slot, in the reference's order
+    (KernelSHAPSampler.scala generateSampleSizes): sizes k and M - k are paired slots (k < M / 2), the
+    Shapley-kernel size weights (M - 1) / (k (M - k)) (doubled for paired slots) decide how the budget is
+    shared. While a size class fits its share completely it is enumerated exactly (weight kernel_weight(k));
+    the budget left over is then spread over the remaining sizes (paired: ceil(share / 2) each side, or one
+    coalition on the k side when the share is below one) with unit weight."""
+    if not (m > 0 and 0 < num_samples <= 2 ** m - 2):
+        raise ValueError(f"need M > 0 and 0 < numSamples <= 2^M - 2 (M={m}, numSamples={num_samples})")
+    num_subsets, num_paired = m // 2, (m - 1) // 2
+    w = np.array([(m - 1) / (i * (m - i)) for i in range(1, num_subsets + 1)], dtype=np.float64)
+    w[:num_paired] *= 2.0
+
+    def share(k: int) -> float:
+        return float(w[k - 1] / w[k - 1:].sum())
+
+    out: List[Tuple[int, float]] = []
+    left = num_samples
+    k = 1
+    while k <= num_subsets:
+        paired = k <= num_paired
+        combo = comb(m, k) * (2 if paired else 1)
+        if share(k) * left < combo:
+            break
+        sizes = [combo // 2, combo // 2] if paired else [combo]
+        out += [(int(x), kernel_weight(k)) for x in sizes]
+        left -= sum(sizes)
+        if left <= 0:
+            break
+        k += 1
+    remaining = num_samples - sum(x for x, _ in out)
+    if remaining > 0:
+        k, left, rest = len(out) // 2 + 1, remaining, []
+        while True:
+            alloc = share(k) * left
+            if k <= num_paired:
+                sizes = [int(np.ceil(alloc / 2))] * 2 if alloc >= 1 else [1, 0]
+            else:
+                sizes = [int(alloc)]
+            rest += sizes
+            left -= sum(sizes)
+            if left <= 0:
+                break
+            k += 1
+        out += [(x, 1.0) for x in rest]
+    return out
+
+
 def shap_coalitions(m: int, num_samples: int, rng, inf_weight: float) -> Tuple[np.ndarray, np.ndarray]:
-    """Coalitions and Shapley-kernel weights: all 2^M subsets when they fit in the budget (exact SHAP),
-    otherwise the empty/full coalitions (weight infWeight) plus subsets drawn with the kernel's size
-    distribution (unit weights)."""
+    """Coalitions and weights of KernelSHAP (KernelSHAPSampler.scala generateCoalitions): the empty and the
+    full coalition with weight infWeight, then the slots of :func:`shap_sample_sizes` - slot i covers size
+    i / 2 (even i) or M - (i - 1) / 2 (odd i); a slot holding every coalition of its size enumerates them,
+    otherwise its coalitions are drawn uniformly at random. The kernel weight of an enumerated size follows
+    the reference, which uses the sample budget N where the Shapley kernel has M:
+    (N - 1) / (k (N - k)) / C(M, k)."""
+    import itertools
+
     if m == 0:
         return np.zeros((1, 0)), np.ones(1)
-    if (1 << m) <= max(num_samples, 2):
-        Z = ((np.arange(1 << m)[:, None] >> np.arange(m)[None, :]) & 1).astype(np.float64)
-        s = Z.sum(1).astype(int)
-        w = np.array([inf_weight if k in (0, m) else (m - 1) / (comb(m, k) * k * (m - k)) for k in s])
-        return Z, w
-    sizes = np.arange(1, m)
-    p = (m - 1) / (sizes * (m - sizes))
-    p = p / p.sum()
-    n = max(0, num_samples - 2)
-    draws = rng.choice(sizes, size=n, p=p)
-    Z = np.zeros((n + 2, m))
-    Z[1] = 1.0
-    for r, k in enumerate(draws):
-        Z[r + 2, rng.choice(m, size=k, replace=False)] = 1.0
-    w = np.ones(n + 2)
-    w[:2] = inf_weight
-    return Z, w
+    n = effective_num_samples(num_samples, m)
+    kern = lambda k: (n - 1) / (k * (n - k)) / comb(m, k)  # noqa: E731
+    slots = [(1, inf_weight), (1, inf_weight)] + (shap_sample_sizes(m, n - 2, kern) if n > 2 else [])
+    rows, weights = [], []
+    for i, (size, wt) in enumerate(slots):
+        k = i // 2 if i % 2 == 0 else m - (i - 1) // 2
+        if size <= 0:
+            continue
+        if size == comb(m, k):
+            subsets = itertools.combinations(range(m), k)
+        else:
+            subsets = (rng.permutation(m)[:k] for _ in range(size))
+        for sub in subsets:
+            z = np.zeros(m)
+            z[list(sub)] = 1.0
+            rows.append(z)
+            weights.append(wt)
+    return np.asarray(rows), np.asarray(weights, dtype=np.float64)
 
 
 class _KernelSHAPBase(LocalExplainer):
     infWeight = Param("The double value to represent infinite weight. Default: 1E8.", 1e8, T.toFloat)
 
     def _budget(self, m: int) -> int:
-        return self.getNumSamples() or (2 * m + 2048)
+        return effective_num_samples(self.getNumSamples(), m)
 
     def _fit(self, X, y, w):
         r = least_squares(X, y, w, fit_intercept=True)

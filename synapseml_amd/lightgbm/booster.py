@@ -91,8 +91,10 @@ class LightGBMBooster:
         self.numIterations = int(v)
 
     # ------------------------------------------------------------- scoring
-    def _shape(self, X: np.ndarray, disable_shape_check: bool) -> np.ndarray:
-        X = np.ascontiguousarray(X, dtype=np.float64)
+    def _shape(self, X: np.ndarray, disable_shape_check: bool, keep_f32: bool = False) -> np.ndarray:
+        """float64 rows (float32 kept as is when the device path scores them: no host conversion copy)"""
+        X = np.asarray(X)
+        X = np.ascontiguousarray(X) if (keep_f32 and X.dtype == np.float32) else np.ascontiguousarray(X, dtype=np.float64)
         if X.ndim == 1:
             X = X[None, :]
         nf = self.numFeatures
@@ -102,7 +104,7 @@ class LightGBMBooster:
                     f"The number of features in data ({X.shape[1]}) is not the same as it was in training data "
                     f"({nf}). You can set ``predictDisableShapeCheck=true`` to discard this error")
             if X.shape[1] < nf:
-                X = np.concatenate([X, np.zeros((X.shape[0], nf - X.shape[1]))], axis=1)
+                X = np.concatenate([X, np.zeros((X.shape[0], nf - X.shape[1]), dtype=X.dtype)], axis=1)
         return X
 
     def _gpu(self, device: str):
@@ -115,30 +117,47 @@ class LightGBMBooster:
             self._gpu_predictors[key] = p
         return p
 
+    def _gpu_for(self, X, device: str):
+        n = np.shape(X)[0] if np.ndim(X) == 2 else 1
+        return self._gpu(device) if n >= _GPU_BATCH_MIN_ROWS else None
+
     def predict_raw(self, X, disable_shape_check=False, device="gpu") -> np.ndarray:
-        X = self._shape(X, disable_shape_check)
-        gp = self._gpu(device) if X.shape[0] >= _GPU_BATCH_MIN_ROWS else None
-        if gp is not None:
-            return gp.predict(X, False)
-        return self.native.predict(X, 0, self.startIteration, self.numIterations)
+        gp = self._gpu_for(X, device)
+        if gp is not None:  # one device pass over the rows in their own dtype (float32 stays float32)
+            return gp.predict_raw(self._shape(X, disable_shape_check, keep_f32=True))
+        return self.native.predict(self._shape(X, disable_shape_check), 0, self.startIteration, self.numIterations)
 
     def predict_normal(self, X, disable_shape_check=False, device="gpu") -> np.ndarray:
-        X = self._shape(X, disable_shape_check)
-        gp = self._gpu(device) if X.shape[0] >= _GPU_BATCH_MIN_ROWS else None
+        gp = self._gpu_for(X, device)
         if gp is not None:
-            return gp.predict(X, True)
-        return self.native.predict(X, 1, self.startIteration, self.numIterations)
+            return self.native.convert_outputs(gp.predict_raw(self._shape(X, disable_shape_check, keep_f32=True)))
+        return self.native.predict(self._shape(X, disable_shape_check), 1, self.startIteration, self.numIterations)
+
+    def predict_raw_and_normal(self, X, disable_shape_check=False, device="gpu"):
+        """(raw, transformed) outputs from ONE ensemble pass: the device (or host) computes the raw scores
+        and the objective's transform is applied to them (LightGBMBooster.scala:394-405 scores twice)."""
+        raw = self.predict_raw(X, disable_shape_check, device)
+        return raw, self.native.convert_outputs(np.ascontiguousarray(raw))
 
     def score(self, X, raw: bool, classification: bool, disable_shape_check: bool = False,
               device: str = "gpu") -> np.ndarray:
         """Batch version of LightGBMBooster.score (Scala :394-405, :559-575):
         binary classification expands to two columns, [-r, r] or [1-p, p]."""
         out = self.predict_raw(X, disable_shape_check, device) if raw else self.predict_normal(X, disable_shape_check, device)
+        return self._expand(out, raw, classification)
+
+    @staticmethod
+    def _expand(out, raw: bool, classification: bool):
         if classification and out.shape[1] == 1:
             if raw:
                 return np.concatenate([-out, out], axis=1)
             return np.concatenate([1.0 - out, out], axis=1)
         return out
+
+    def score_both(self, X, classification: bool, disable_shape_check: bool = False, device: str = "gpu"):
+        """(rawPrediction, probability) of a batch from a single ensemble pass"""
+        r, p = self.predict_raw_and_normal(X, disable_shape_check, device)
+        return self._expand(r, True, classification), self._expand(p, False, classification)
 
     def predictLeaf(self, X, disable_shape_check=False, device="gpu") -> np.ndarray:  # noqa: N802
         X = self._shape(X, disable_shape_check)

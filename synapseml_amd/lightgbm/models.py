@@ -19,9 +19,11 @@ from .params import LightGBMModelParams
 
 
 def _features_matrix(df: DataFrame, col: str) -> np.ndarray:
+    """the feature rows for scoring: a float32 / float64 dense column as is (no float64 copy of a float32
+    partition: the device scorer reads float32 rows), other layouts densified to float64"""
     c = df[col]
     if isinstance(c, np.ndarray) and c.ndim == 2:
-        return np.ascontiguousarray(c, dtype=np.float64)
+        return np.ascontiguousarray(c) if c.dtype in (np.float32, np.float64) else np.ascontiguousarray(c, np.float64)
     return as_matrix(c)
 
 
@@ -121,11 +123,12 @@ class LightGBMClassificationModel(_LightGBMModelBase, HasRawPredictionCol, HasPr
         dsc = self.getPredictDisableShapeCheck()
         dev = self.getDeviceType()
         raw = prob = None
+        if self.getRawPredictionCol() or self.getProbabilityCol() or self.getPredictionCol():
+            # one ensemble pass yields both the raw scores and the probabilities
+            raw, prob = b.score_both(X, classification=True, disable_shape_check=dsc, device=dev)
         if self.getRawPredictionCol():
-            raw = b.score(X, raw=True, classification=True, disable_shape_check=dsc, device=dev)
             df = df.withColumn(self.getRawPredictionCol(), raw)
         if self.getProbabilityCol():
-            prob = b.score(X, raw=False, classification=True, disable_shape_check=dsc, device=dev)
             df = df.withColumn(self.getProbabilityCol(), prob)
         if self.getPredictionCol():
             th = self.getThresholds()

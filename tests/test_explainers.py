@@ -34,7 +34,7 @@ def test_regression_helpers():
     l1 = lasso(X, y, np.ones(200), alpha=0.1)
     assert abs(l1.coefficients[2]) < 1e-9 and l1.coefficients[0] > 0.7
     Z, w = shap_coalitions(3, 100, rng, 1e8)
-    assert Z.shape == (8, 3) and w[0] == 1e8 and w[-1] == 1e8
+    assert Z.shape == (8, 3) and w[0] == 1e8 and w[1] == 1e8 and Z[1].sum() == 3 and Z[0].sum() == 0
 
 
 def test_tabular_and_vector_shap_exact_for_linear_model():
@@ -136,3 +136,35 @@ def test_ice_pdp_and_feature_importance():
                           categoricalFeatures=[{"name": "c"}]).transform(df)
     assert feat["featureNames"].tolist() == ["c_dependence", "a_dependence"]
     assert feat["pdpBasedDependence"][0].toArray()[0] == pytest.approx(0.25)
+
+
+def test_kernel_shap_coalitions_follow_reference_allocation():
+    """KernelSHAP coalitions (KernelSHAPSampler.scala generateSampleSizes / generateCoalitions, pinned by the
+    reference's KernelSHAPSamplerSupportSuite): exact enumeration when the budget covers every size class,
+    the paired size allocation with random fill otherwise."""
+    import numpy as np
+
+    from synapseml_amd.explainers.local import effective_num_samples, shap_coalitions, shap_sample_sizes
+
+    rng = np.random.default_rng(0)
+    Z, w = shap_coalitions(5, 32, rng, 1e8)
+    s = Z.sum(1)
+    assert len(Z) == 32 and w[0] == 1e8 and w[1] == 1e8
+    assert [int((s == k).sum()) for k in range(6)] == [1, 5, 10, 10, 5, 1]
+    assert len({tuple(r) for r in Z}) == 32  # every subset exactly once
+    Z, w = shap_coalitions(500, 4, rng, 1e8)
+    s = Z.sum(1)
+    assert len(Z) == 4 and list(w) == [1e8, 1e8, 1.0, 1.0]
+    assert [int((s == k).sum()) for k in (0, 500, 1, 2)] == [1, 1, 1, 1]
+    Z, w = shap_coalitions(500, 1000, rng, 1e8)
+    s = Z.sum(1)
+    assert len(Z) == 1000 and (w[:2] == 1e8).all() and (w[2:] == 1.0).all()
+    assert [int((s == k).sum()) for k in (0, 500, 1, 499, 2, 498)] == [1, 1, 74, 74, 37, 37]
+    # budget clamp (KernelSHAPBase.getEffectiveNumSamples) and the kernel weights of enumerated sizes
+    assert effective_num_samples(None, 3) == 8 and effective_num_samples(None, 20) == 2 * 20 + 2048
+    assert effective_num_samples(1, 20) == 22
+    sizes = shap_sample_sizes(6, 62, lambda k: float(k))
+    assert [x for x, _ in sizes] == [6, 6, 15, 15, 20] and [wt for _, wt in sizes] == [1.0, 1.0, 2.0, 2.0, 3.0]
+    for bad in ((5, 0), (5, 31)):
+        with pytest.raises(ValueError):
+            shap_sample_sizes(*bad, lambda k: 1.0)

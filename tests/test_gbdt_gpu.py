@@ -599,3 +599,21 @@ def test_gpu_batched_growth_equals_sequential(extra, spec, monkeypatch):
 
     seq, bat = fit("0"), fit(spec)
     assert bat == seq
+
+
+def test_gpu_single_pass_scoring_float32_rows():
+    """K9 batch scoring: float32 rows are scored as they are (no float64 copy) in one chunked upload +
+    traversal pass; raw and probability come from that single pass and equal the host predictor."""
+    X, y = _data(n=70000, nan_frac=0.03)
+    b = _train(X, y, "objective=binary num_leaves=31 device_type=gpu", 20)
+    from synapseml_amd.lightgbm.booster import LightGBMBooster
+
+    lb = LightGBMBooster(native_booster=b)
+    X32 = X.astype(np.float32)
+    host = b.predict(X32.astype(np.float64), 0, 0, -1)
+    gp = lb._gpu("gpu")
+    np.testing.assert_allclose(gp.predict_raw(X32), host, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(gp.predict_raw(X32.astype(np.float64)), host, rtol=1e-12, atol=1e-12)
+    raw, prob = lb.score_both(X32, classification=True)
+    np.testing.assert_allclose(raw[:, 1], host[:, 0], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(prob[:, 1], b.predict(X32.astype(np.float64), 1, 0, -1)[:, 0], rtol=1e-12, atol=1e-12)

@@ -4,11 +4,12 @@
 
 Per GPU: --rows rows (default 12.5M = 100M / 8, weak scaling) of 28 float
 features in query groups of 20-180 documents with graded relevance 0-4.
-One step = one boosting iteration (lambdarank gradients on the device, K2
-ranking kernel -> 31-leaf tree -> score update). Single GPU:
-``python tools/bench_ranker.py``; N GPUs: ``torchrun --nproc-per-node N
-tools/bench_ranker.py``. Prints one JSON line (rank 0): rows/s over all GPUs
-and NDCG@10 of the trained model on a held-out slice (outside the timing).
+One step = one complete ``LightGBMRanker(numIterations=100).fit(df)`` on the
+rank's DataFrame partition (group prep, sampling, device bin encode, 100
+lambdarank iterations, model). Single GPU: ``python tools/bench_ranker.py``;
+N GPUs: ``python tools/bench_ranker.py --gpus N`` (launches N ranks). Prints
+one JSON line (rank 0): training rows per second of fit wall time over all
+GPUs, a phase breakdown, and NDCG@10 on a held-out slice (outside timing).
 Data is synthetic (no datasets are downloadable here)."""
 from __future__ import annotations
 
@@ -57,65 +58,58 @@ def ndcg_at(scores, labels, sizes, k=10):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--rows", type=int, default=12_500_000, help="rows per GPU (weak scaling)")
     ap.add_argument("--features", type=int, default=28)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=3, help="timed fits")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed fits")
+    ap.add_argument("--iterations", type=int, default=100, help="numIterations per fit (reference default 100)")
     ap.add_argument("--leaves", type=int, default=31)
     ap.add_argument("--device", default="gpu")
     args = ap.parse_args()
-    import torch
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench_ranker: --gpus {args.gpus} but WORLD_SIZE={world}")
+    import torch
+
     use_gpu = args.device == "gpu" and torch.cuda.is_available()
     if use_gpu:
+        if world > torch.cuda.device_count():
+            sys.exit(f"bench_ranker: {world} ranks but {torch.cuda.device_count()} visible GPU(s)")
         torch.cuda.set_device(local_rank)
+    from synapseml_amd.core.dataframe import DataFrame
+    from synapseml_amd.lightgbm import LightGBMRanker
     from synapseml_amd.parallel import distributed as D
 
     if world > 1:
         D.init_from_env("nccl" if use_gpu else "gloo")
-    from synapseml_amd.ops import native
-
-    g = native.gbdt()
     X, y, sizes = ranking_data(args.rows, args.features, seed=77 + rank)
-    params = (f"objective=lambdarank num_iterations={args.warmup + args.steps} learning_rate=0.1 "
-              f"num_leaves={args.leaves} max_bin=255 min_data_in_leaf=20 eval_at=10 "
-              f"device_type={'gpu' if use_gpu else 'cpu'} num_machines={world} tree_learner=data")
-    names = [f"f{i}" for i in range(args.features)]
-    ser = None
-    if rank == 0:
-        idx = np.sort(np.random.default_rng(1).choice(args.rows, size=min(200_000, args.rows), replace=False))
-        ser = bytes(g.DatasetReference.from_sample(X[idx].astype(np.float64), args.rows * world, params, names)
-                    .serialize())
-    ref = g.DatasetReference.deserialize(D.broadcast_object(ser, 0))
-    ds = g.Dataset(ref, args.rows)
-    if use_gpu:
-        ds.push_dense_gpu(X, 0)
-    else:
-        ds.push_dense(X, 0)
-    ds.set_label(y)
-    ds.set_group(sizes)
+    # query ids: contiguous groups, unique across ranks (int64 column of the training DataFrame)
+    qid = np.repeat(np.arange(len(sizes), dtype=np.int64) + (rank << 40), sizes)
+    df = DataFrame({"features": X, "label": y, "query": qid})
     n_hold = min(100_000, args.rows)
     hold_q = int(np.searchsorted(np.cumsum(sizes), n_hold)) + 1
-    Xh, yh, sh = X[: int(sizes[:hold_q].sum())].astype(np.float64), y[: int(sizes[:hold_q].sum())], sizes[:hold_q]
-    del X
-    comm = D.gbdt_comm(use_gpu) if world > 1 else None
-    booster = g.Booster(ds, params, comm)
+    nh = int(sizes[:hold_q].sum())
+    Xh, yh, sh = X[:nh].astype(np.float64), y[:nh], sizes[:hold_q]
+    est = LightGBMRanker(numIterations=args.iterations, learningRate=0.1, numLeaves=args.leaves, maxBin=255,
+                         minDataInLeaf=20, groupCol="query", evalAt=[10], deviceType="gpu" if use_gpu else "cpu")
 
     def sync():
-        booster.synchronize()
         if use_gpu:
             torch.cuda.synchronize()
 
+    model = None
     for _ in range(args.warmup):
-        booster.update()
+        model = est.fit(df)
     sync()
     D.barrier()
     t0 = time.perf_counter()
+    measures = []
     for _ in range(args.steps):
-        booster.update()
+        model = est.fit(df)
+        measures.append(est.getPerformanceMeasures()[0])
     sync()
     D.barrier()
     elapsed = time.perf_counter() - t0
@@ -125,15 +119,23 @@ def main() -> None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    phases = {k: round(float(np.mean([m.get(k, 0.0) for m in measures])), 2)
+              for k in ("sampling_ms", "dataset_creation_ms", "booster_init_ms", "training_iterations_ms", "total_ms")}
     if rank == 0:
-        nd = ndcg_at(booster.predict(Xh, 0, 0, -1)[:, 0], yh, sh)
-        st = booster.stats()
+        nd = ndcg_at(model.getModel().score(Xh, raw=True, classification=False)[:, 0], yh, sh)
+        fit_s = elapsed / args.steps
         print(json.dumps({
-            "bench": "lightgbm_ranker", "metric": "rows/sec LightGBMRanker lambdarank (row-iterations/s, whole job)",
-            "value": round(args.rows * world * args.steps / elapsed, 1), "n_gpus": world if use_gpu else 0,
-            "rows_per_gpu": args.rows, "queries_per_gpu": int(len(sizes)), "steps": args.steps,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ndcg@10_holdout_slice": round(nd, 4),
-            "grad_ms_total": round(st.get("grad_ms", 0.0), 2), "backend": booster.backend,
+            "bench": "lightgbm_ranker_fit", "metric": "rows/sec LightGBMRanker.fit (whole fit, whole job)",
+            "value": round(args.rows * world * args.steps / elapsed, 1), "unit": "training rows / fit wall seconds",
+            "n_gpus": world if use_gpu else 0, "rows_per_gpu": args.rows, "queries_per_gpu": int(len(sizes)),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_fit": round(fit_s * 1e3, 1),
+            "num_iterations": args.iterations, "fit_phases_ms": phases,
+            "group_prep_and_other_ms": round(phases["total_ms"] - phases["sampling_ms"] - phases["dataset_creation_ms"]
+                                             - phases["booster_init_ms"] - phases["training_iterations_ms"], 2),
+            "iteration_ms": round(phases["training_iterations_ms"] / args.iterations, 3),
+            "row_iterations_per_s": round(args.rows * world * args.iterations / (phases["training_iterations_ms"] / 1e3), 1),
+            "ndcg@10_holdout_slice": round(nd, 4), "backend": measures[-1].get("backend"),
+            "timed_region": "LightGBMRanker(numIterations=100).fit(df) end to end (DataFrame built before timing)",
             "data": "synthetic (28 float features, query groups of 20-180 docs, relevance 0-4)"}), flush=True)
     if world > 1:
         import torch.distributed as dist
@@ -142,4 +144,9 @@ def main() -> None:
 
 
 if __name__ == "__main__":
+    sys.path.insert(0, ROOT)
+    from bench import _parse_gpus, launch_ranks
+
+    if "WORLD_SIZE" not in os.environ and _parse_gpus(sys.argv[1:]) > 1:
+        sys.exit(launch_ranks(_parse_gpus(sys.argv[1:]), os.path.abspath(__file__), sys.argv[1:]))
     main()

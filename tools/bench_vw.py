@@ -55,8 +55,71 @@ def make_pass(n, nnz, seed):
     return indptr, idx, val, y
 
 
+def estimator_bench(args, world: int, rank: int) -> None:
+    """One step = one ``VowpalWabbitClassifier(numBits=30, deviceType='gpu').fit(df)`` on the rank's partition:
+    the hashed-feature column is a CSR-backed sparse vector column (zero-copy namespace block), the fit uploads
+    it, builds the example rows on the device (constant feature included), learns one pass of hogwild
+    mini-batches with VW's default update, averages the touched blocks over RCCL (N > 1) and exports the model
+    from the device nonzeros."""
+    import torch
+
+    from synapseml_amd.core.dataframe import DataFrame
+    from synapseml_amd.core.linalg import CsrColumn
+    from synapseml_amd.parallel import distributed as D
+    from synapseml_amd.vw import VowpalWabbitClassifier
+
+    ip, idx, val, y = make_pass(args.rows, args.nnz, seed=1000 * rank)
+    df = DataFrame({"features": CsrColumn(ip, idx, val, 1 << 32), "label": y.astype(np.float64)})
+    hold = make_pass(100_000, args.nnz, seed=999_999)
+    hdf = DataFrame({"features": CsrColumn(hold[0], hold[1], hold[2], 1 << 32), "label": hold[3].astype(np.float64)})
+    est = VowpalWabbitClassifier(numBits=args.bits, deviceType="gpu", gpuBatchSize=args.batch,
+                                 passThroughArgs="--loss_function logistic")
+    model = None
+    for _ in range(args.warmup):
+        model = est.fit(df)
+    torch.cuda.synchronize()
+    D.barrier()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        model = est.fit(df)
+        stats.append({k: float(model.getPerformanceStatistics()[k][0])
+                      for k in ("timeNativeIngestNs", "timeLearnNs", "timeTotalNs", "syncBytes")})
+    torch.cuda.synchronize()
+    D.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        raw = model.transform(hdf)["rawPrediction"]
+        m = hold[3] * raw
+        logloss = float(np.mean(np.log1p(np.exp(-np.clip(m, -50, 50)))))
+        ph = {k: round(float(np.mean([s[k] for s in stats])) / 1e6, 2) for k in stats[0]}
+        fit_ms = elapsed / args.steps * 1e3
+        print(json.dumps({
+            "bench": "vw_classifier_fit", "metric": "examples/sec VowpalWabbitClassifier.fit (whole fit, whole job)",
+            "value": round(args.rows * world * args.steps / elapsed, 1), "unit": "examples / fit wall second",
+            "n_gpus": world, "bits": args.bits, "table_gib": round((2 ** args.bits) * 16 / 2 ** 30, 2),
+            "rows_per_gpu": args.rows, "nnz_per_row": args.nnz, "batch": args.batch, "ms_per_fit": round(fit_ms, 1),
+            "phases_ms": {"ingest_and_device_featurize": ph["timeNativeIngestNs"], "learn_and_sync": ph["timeLearnNs"],
+                          "engine_total": ph["timeTotalNs"],
+                          "export_model_and_other": round(fit_ms - ph["timeTotalNs"], 2)},
+            "sync_mib": round(stats[-1]["syncBytes"] / 2 ** 20, 2), "holdout_logloss": round(logloss, 4),
+            "timed_region": "VowpalWabbitClassifier(numBits, deviceType='gpu').fit(df) end to end (DataFrame built "
+                            "before timing)",
+            "data": "synthetic hashed sparse (Zipf ids from a 2^24 vocabulary, planted linear model)"}), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--api", choices=("estimator", "kernel"), default="estimator",
+                    help="estimator: VowpalWabbitClassifier(deviceType='gpu').fit(df) end to end (default); "
+                         "kernel: the GpuSgd learner alone on a pre-built CSR")
     ap.add_argument("--bits", type=int, default=30)
     ap.add_argument("--rows", type=int, default=2_000_000, help="examples per pass per GPU")
     ap.add_argument("--nnz", type=int, default=64)
@@ -64,21 +127,27 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=16384, help="hogwild mini-batch (examples in flight)")
     ap.add_argument("--resident", action="store_true",
-                    help="multi-pass mode: the pass is staged in HBM once and every step re-learns it from there")
+                    help="kernel mode: the pass is staged in HBM once and every step re-learns it from there")
     args = ap.parse_args()
-    import torch
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench_vw: --gpus {args.gpus} but WORLD_SIZE={world}")
+    import torch
+
     if not torch.cuda.is_available():
         raise SystemExit("bench_vw needs an MI355X")
+    if world > torch.cuda.device_count():
+        sys.exit(f"bench_vw: {world} ranks but {torch.cuda.device_count()} visible GPU(s)")
     torch.cuda.set_device(local_rank)
     from synapseml_amd.ops import native
     from synapseml_amd.parallel import distributed as D
 
     if world > 1:
         D.init_from_env("nccl")
+    if args.api == "estimator":
+        return estimator_bench(args, world, rank)
     vw = native.load("_vw")
     cfg = vw.GpuSgdConfig()
     cfg.bits = args.bits
@@ -133,7 +202,7 @@ def main() -> None:
         m = hold[3] * p
         logloss = float(np.mean(np.log1p(np.exp(-np.clip(m, -50, 50)))))
         print(json.dumps({
-            "bench": "vw_hashed_sgd", "metric": "examples/sec VowpalWabbitClassifier (whole job)",
+            "bench": "vw_hashed_sgd_kernel", "metric": "examples/sec GpuSgd learner (kernel only, whole job)",
             "value": round(args.rows * world * args.steps / elapsed, 1), "n_gpus": world, "bits": args.bits,
             "table_gib": round((2 ** args.bits) * 16 / 2 ** 30, 2), "rows_per_gpu_per_pass": args.rows,
             "nnz_per_row": args.nnz, "batch": args.batch, "ms_per_pass": round(elapsed / args.steps * 1e3, 2),
@@ -148,4 +217,8 @@ def main() -> None:
 
 
 if __name__ == "__main__":
+    from bench import _parse_gpus, launch_ranks
+
+    if "WORLD_SIZE" not in os.environ and _parse_gpus(sys.argv[1:]) > 1:
+        sys.exit(launch_ranks(_parse_gpus(sys.argv[1:]), os.path.abspath(__file__), sys.argv[1:]))
     main()
