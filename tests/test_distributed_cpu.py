@@ -348,3 +348,36 @@ def test_bench_launches_n_ranks_on_cpu():
                           "--rows", "2000", "--iterations", "1", "--steps", "1", "--warmup", "0"],
                          env=env1, capture_output=True, text=True, timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE=1" in bad.stderr
+
+
+def _checksum_task(part, rank, world):
+    from synapseml_amd.core.linalg import CsrColumn
+
+    f = part["f"]
+    csr = part["sv"]
+    return (float(np.asarray(f, np.float64).sum()), str(f.dtype), f.shape, isinstance(csr, CsrColumn),
+            float(csr.values.sum()) if isinstance(csr, CsrColumn) else None, list(part["s"]), float(part["y"].sum()))
+
+
+def test_partitions_reach_workers_through_shared_memory():
+    """Partition hand-off (runtime._share_partition): numeric and CSR columns arrive as shared-memory views with
+    their dtype / shape, object columns pickled; the driver unlinks every segment afterwards."""
+    import glob
+
+    from synapseml_amd.core.linalg import CsrColumn
+
+    before = set(glob.glob("/dev/shm/psm_*"))
+    rng = np.random.default_rng(0)
+    f = rng.standard_normal((1000, 7)).astype(np.float32)
+    ip = np.arange(0, 2001, 2, dtype=np.int64)
+    sv = CsrColumn(ip, rng.integers(0, 50, 2000).astype(np.int32), rng.random(2000), 50)
+    s = np.array([f"r{i}" for i in range(1000)], dtype=object)
+    df = DataFrame({"f": f, "sv": sv, "s": s, "y": np.arange(1000.0)}, num_partitions=2)
+    res = run_partitions(_checksum_task, df, num_workers=2)
+    for r, (a, b) in enumerate(df.partition_bounds()):
+        fs, dt, shape, is_csr, vs, strs, ys = res[r]
+        assert dt == "float32" and shape == (b - a, 7) and is_csr
+        np.testing.assert_allclose(fs, f[a:b].astype(np.float64).sum(), rtol=1e-6)
+        np.testing.assert_allclose(vs, sv[a:b].values.sum())
+        assert strs == list(s[a:b]) and ys == float(np.arange(a, b).sum())
+    assert set(glob.glob("/dev/shm/psm_*")) <= before
