@@ -647,15 +647,42 @@ class InferenceSession:
                 for _ in range(2):
                     self.run_values(static_in, fetch)
             torch.cuda.current_stream(self.device).wait_stream(s)
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=True)
             with torch.cuda.graph(g):
                 static_out = self.run_values(static_in, fetch)
             if not all(isinstance(o, torch.Tensor) for o in static_out):
                 return "eager"
+            # a plan whose work never reached the capture stream (host-computed values, kernels on another
+            # stream) records an empty graph: replaying it would hand back the capture-time buffers, so such a
+            # plan runs eagerly instead
+            if _graph_num_nodes(g) == 0:
+                return "eager"
+            g.instantiate()
             return g, static_in, static_out
         except Exception:
             torch.cuda.synchronize(self.device)
             return "eager"
+
+
+_HIP = None
+
+
+def _graph_num_nodes(g) -> int:
+    """nodes of a captured graph (hipGraphGetNodes on the raw hipGraph_t); -1 when it cannot be queried"""
+    global _HIP
+    import ctypes
+
+    try:
+        if _HIP is None:
+            _HIP = ctypes.CDLL("libamdhip64.so")
+            _HIP.hipGraphGetNodes.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+            _HIP.hipGraphGetNodes.restype = ctypes.c_int
+        n = ctypes.c_size_t(0)
+        if _HIP.hipGraphGetNodes(ctypes.c_void_p(int(g.raw_cuda_graph())), None, ctypes.byref(n)) != 0:
+            return -1
+        return int(n.value)
+    except Exception:  # noqa: BLE001 - no HIP runtime symbol / older torch: treat as unknown
+        return -1
 
 
 # ---------------------------------------------------------------------- fused ops

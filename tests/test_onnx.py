@@ -493,3 +493,35 @@ def test_gpu_featurizer_encoded_bytes_match_decoded_rows():
         return np.stack([v.toArray() for v in f.transform(DataFrame({"image": col}))["features"]])
 
     np.testing.assert_allclose(feats(pngs), feats(rows), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_graph_capture_records_work_or_runs_eager():
+    """HIP-graph replay (session._capture) is only kept when the captured graph has nodes; a plan whose work
+    did not reach the capture stream runs eagerly, so a replay never returns stale capture-time buffers."""
+    from synapseml_amd.onnx.session import _graph_num_nodes
+
+    data, coef, inter = _iris_model()
+    s = InferenceSession(data, device="cuda", use_graph=True)
+    for seed in (0, 1, 2):
+        x = np.random.default_rng(seed).random((64, 4)).astype(np.float32) * 5
+        label = s.run(["output_label"], {"float_input": x})[0]
+        assert np.asarray(label).tolist() == (x @ coef.T + inter).argmax(1).tolist()
+    assert s._graphs
+    for entry in s._graphs.values():
+        assert entry == "eager" or _graph_num_nodes(entry[0]) > 0
+    # a plain tensor graph is replayed from a non-empty capture with fresh results per batch
+    b = GraphBuilder("lin")
+    b.input("x", P.FLOAT32, ["N", 4])
+    w = b.init("w", np.eye(4, dtype=np.float32) * 2)
+    y = b.add("MatMul", ["x", w])
+    b.add("Relu", [y], out="z")
+    b.output("z", P.FLOAT32, ["N", 4])
+    s2 = InferenceSession(b.to_bytes(), device="cuda", use_graph=True)
+    for seed in (3, 4):
+        x = np.random.default_rng(seed).standard_normal((32, 4)).astype(np.float32)
+        out = s2.run(None, {"x": x})[0]
+        out = out.cpu().numpy() if torch.is_tensor(out) else np.asarray(out)
+        np.testing.assert_allclose(out, np.maximum(2 * x, 0), rtol=1e-6)
+    entry = next(iter(s2._graphs.values()))
+    assert entry != "eager" and _graph_num_nodes(entry[0]) > 0

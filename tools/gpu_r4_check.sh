@@ -8,3 +8,9 @@ timeout -k 10 400 python -u -m pytest -v --timeout 120 --timeout-method thread t
 rc=$?
 [ $rc -gt 1 ] && exit $rc
 timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gbdt_gpu.py > "$OUT/pytest_gbdt.log" 2>&1
+rc=$?
+[ $rc -gt 1 ] && exit $rc
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_onnx.py -k "gpu" > "$OUT/pytest_onnx.log" 2>&1
+rc=$?
+[ $rc -gt 1 ] && exit $rc
+timeout -k 10 300 python tools/bench_transform.py > "$OUT/bench_transform.log" 2>&1
