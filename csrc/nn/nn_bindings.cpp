@@ -31,7 +31,7 @@ PYBIND11_MODULE(_nn, m) {
                  dtype, P<void>(sum_out), P<void>(act_out), P<void>(stream));
   });
   m.def("gap_nhwc", [](uintptr_t x, int N, int HW, int C, int dtype, uintptr_t out, uintptr_t stream) {
-    GapNhwc(P<const void>(x), N, HW, C, dtype, P<float>(out), P<void>(stream));
+    GapNhwc(P<const void>(x), N, HW, C, dtype, P<void>(out), P<void>(stream));
   });
   m.def("maxpool_nhwc", [](uintptr_t x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw,
                            int OH, int OW, int dtype, uintptr_t y, uintptr_t stream, uintptr_t shift, int relu) {

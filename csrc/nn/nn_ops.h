@@ -18,7 +18,7 @@ void AddAffineAct(const void* a, const void* b, int64_t n, int C, int HW, int nh
 void MaxPoolNhwc(const void* x, int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw, int OH,
                  int OW, int dtype, void* y, void* stream, const float* shift = nullptr, int relu = 0);
 // NHWC global average pool -> fp32 [N, C]
-void GapNhwc(const void* x, int N, int HW, int C, int dtype, float* out, void* stream);
+void GapNhwc(const void* x, int N, int HW, int C, int dtype, void* out, void* stream);  // out: input dtype
 // Implicit-GEMM MFMA convolution with fused prologue/epilogue (conv_mfma.hip).
 struct ConvArgs {
   const void* x;           // NHWC [B, H, W, C]

@@ -129,18 +129,19 @@ __global__ __launch_bounds__(kThreads) void add_affine_act_kernel(const T* __res
   }
 }
 
-// global average pool over HW of an NHWC tensor -> [N, C] fp32; one thread per
-// (n, c), lanes of a wave on consecutive channels (coalesced rows).
+// K16: global average pool over HW of an NHWC tensor -> [N, C] in the input dtype (fp32 accumulation, one
+// rounding); one thread per (n, c), lanes of a wave on consecutive channels (coalesced rows). The output is
+// the [N, C, 1, 1] tensor the classifier head reads, so no dtype-conversion pass follows it.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void gap_nhwc_kernel(const T* __restrict__ x, int N, int HW, int C,
-                                                            float* __restrict__ out) {
+                                                            T* __restrict__ out) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= static_cast<int64_t>(N) * C) return;
   const int n = static_cast<int>(i / C), c = static_cast<int>(i % C);
   const T* p = x + static_cast<int64_t>(n) * HW * C + c;
   float s = 0.f;
   for (int k = 0; k < HW; ++k) s += ld<T>(p, static_cast<int64_t>(k) * C);
-  out[i] = s / HW;
+  out[i] = cv<T>(s / HW);
 }
 
 // K16: max pool over an NHWC tensor (kh x kw window, stride, symmetric pads, no dilation; padded cells
@@ -294,20 +295,20 @@ void AddAffineAct(const void* a, const void* b, int64_t n, int C, int HW, int nh
   NN_HIP_CHECK(hipGetLastError());
 }
 
-void GapNhwc(const void* x, int N, int HW, int C, int dtype, float* out, void* stream) {
+void GapNhwc(const void* x, int N, int HW, int C, int dtype, void* out, void* stream) {
   const int64_t n = static_cast<int64_t>(N) * C;
   if (n <= 0) return;
   auto s = static_cast<hipStream_t>(stream);
   const int g = Blocks(n, 1);
   if (dtype == 1)
     hipLaunchKernelGGL(gap_nhwc_kernel<__half>, dim3(g), dim3(kThreads), 0, s, static_cast<const __half*>(x), N, HW, C,
-                       out);
+                       static_cast<__half*>(out));
   else if (dtype == 2)
     hipLaunchKernelGGL(gap_nhwc_kernel<__hip_bfloat16>, dim3(g), dim3(kThreads), 0, s,
-                       static_cast<const __hip_bfloat16*>(x), N, HW, C, out);
+                       static_cast<const __hip_bfloat16*>(x), N, HW, C, static_cast<__hip_bfloat16*>(out));
   else
     hipLaunchKernelGGL(gap_nhwc_kernel<float>, dim3(g), dim3(kThreads), 0, s, static_cast<const float*>(x), N, HW, C,
-                       out);
+                       static_cast<float*>(out));
   NN_HIP_CHECK(hipGetLastError());
 }
 

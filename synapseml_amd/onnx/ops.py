@@ -785,6 +785,17 @@ def _lppool(rt, at, x):
 @op("GlobalAveragePool")
 def _gap(rt, at, x):
     t = x[0]
+    nn = getattr(getattr(rt, "session", None), "_nn", None)
+    if (nn is not None and t.is_cuda and t.dim() == 4 and t.dtype in (torch.float16, torch.bfloat16, torch.float32)
+            and t.is_contiguous(memory_format=torch.channels_last)):
+        # K16: NHWC global average pool on the HIP kernel, output in the input dtype ([N, C, 1, 1] is both
+        # layouts at once), fp32 accumulation
+        from .session import _dtype_code, _stream
+
+        N, C, H, W = t.shape
+        y = torch.empty((N, C, 1, 1), dtype=t.dtype, device=t.device)
+        nn.gap_nhwc(t.data_ptr(), N, H * W, C, _dtype_code(t), y.data_ptr(), _stream(t))
+        return [y]
     return [t.mean(dim=tuple(range(2, t.dim())), keepdim=True)]
 
 

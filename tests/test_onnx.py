@@ -525,3 +525,27 @@ def test_gpu_graph_capture_records_work_or_runs_eager():
         np.testing.assert_allclose(out, np.maximum(2 * x, 0), rtol=1e-6)
     entry = next(iter(s2._graphs.values()))
     assert entry != "eager" and _graph_num_nodes(entry[0]) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.bfloat16])
+def test_gpu_global_average_pool_kernel(dt):
+    """GlobalAveragePool on channels-last device tensors runs the HIP kernel (fp32 accumulation, output in the
+    input dtype) and equals an fp32 torch mean."""
+    b = GraphBuilder("gap")
+    b.input("x", P.FLOAT32, ["N", 64, 7, 7])
+    b.add("GlobalAveragePool", ["x"], out="y")
+    b.output("y", P.FLOAT32, ["N", 64, 1, 1])
+    s = InferenceSession(b.to_bytes(), device="cuda", use_graph=False)
+    x = torch.randn(16, 64, 7, 7, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    from synapseml_amd.onnx import ops
+
+    class _RT:
+        session = s
+        node_outputs = ["y"]
+
+    y = ops.OPS["GlobalAveragePool"](_RT(), {}, [x])[0]
+    assert y.dtype == dt and y.shape == (16, 64, 1, 1)
+    ref = x.float().mean(dim=(2, 3), keepdim=True)
+    tol = 1e-6 if dt == torch.float32 else 1e-2
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
