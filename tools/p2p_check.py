@@ -38,6 +38,8 @@ def main():
         out["allreduce_exact"] = bool(np.array_equal(got, exp))
         out["us_per_allreduce_114KB"] = g.comm_device_allreduce_us(c, n, 200)
         out["us_per_allreduce_8KB"] = g.comm_device_allreduce_us(c, 1024, 200)
+        # one round of the batched tree growth: 8 expansions x (histogram + count) = 8 x 114 KB
+        out["us_per_allreduce_917KB"] = g.comm_device_allreduce_us(c, 8 * (28 * 256 + 1) * 2, 100)
         # data-parallel training over P2P vs host comm: identical models
         rng = np.random.default_rng(7 + r)
         X = rng.standard_normal((40000, 8))
