@@ -409,6 +409,8 @@ PYBIND11_MODULE(_vw, m) {
       .def_readwrite("power_t", &GpuSgdConfig::power_t)
       .def_readwrite("initial_t", &GpuSgdConfig::initial_t)
       .def_readwrite("l2", &GpuSgdConfig::l2)
+      .def_readwrite("l1", &GpuSgdConfig::l1)
+      .def_readwrite("tau", &GpuSgdConfig::tau)
       .def_readwrite("loss", &GpuSgdConfig::loss)
       .def_readwrite("adaptive", &GpuSgdConfig::adaptive)
       .def_readwrite("normalized", &GpuSgdConfig::normalized)

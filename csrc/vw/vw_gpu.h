@@ -19,7 +19,9 @@ struct GpuSgdConfig {
   float power_t = 0.5f;
   float initial_t = 0.f;
   float l2 = 0.f;
-  int loss = 0;          // 0 squared, 1 logistic
+  float l1 = 0.f;
+  float tau = 0.5f;      // quantile loss
+  int loss = 0;          // 0 squared, 1 logistic, 2 hinge, 3 quantile
   bool adaptive = true;  // VW's default update: adaptive + normalized + invariant
   bool normalized = true;
   bool invariant = true;

@@ -97,8 +97,8 @@ struct SgdArgs {
   uint64_t mask;
   uint8_t* dirty;
   double* gs;          // [t, total weight, sum of feature norms]
-  float lr, power_t, initial_t, l2;
-  int loss;            // 0 squared, 1 logistic
+  float lr, power_t, initial_t, l2, l1, tau;
+  int loss;            // 0 squared, 1 logistic, 2 hinge, 3 quantile (tau)
   int adaptive, normalized, invariant;
   int K;               // oaa classes (0: scalar learner)
   float* preds;
@@ -147,6 +147,8 @@ __device__ UpdPrep UpdateFirstPass(const SgdArgs& a, int64_t b, int64_t en, uint
   UpdPrep pr;
   float g;
   if (a.loss == 1) g = -y / (1.f + expf(y * raw));
+  else if (a.loss == 2) g = (y * raw < 1.f) ? -y : 0.f;
+  else if (a.loss == 3) g = (y - raw) > 0.f ? -a.tau : (1.f - a.tau);
   else g = 2.f * (raw - y);
   const float grad_sq = g * g * imp;
   float ppu = 0.f, norm_x = 0.f;
@@ -194,7 +196,7 @@ __device__ void UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64
   if (!a.adaptive) eta *= pow(static_cast<double>(a.initial_t) + t, -static_cast<double>(a.power_t));
   const float us = static_cast<float>(eta) * imp;
   float update;
-  if (a.invariant) {
+  if (a.invariant && a.loss <= 1) {
     const float pp = fmaxf(pr.ppu, FLT_MIN);
     if (a.loss == 0) {
       update = us * pp < 1e-6f ? 2.f * (y - raw) * us : (y - raw) * (1.f - expf(-2.f * us * pp)) / pp;
@@ -203,18 +205,23 @@ __device__ void UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64
       update = fabsf(step * pp) > 50.f ? copysignf(50.f / pp, step) : step;
     }
   } else {
-    update = -pr.g * us;
+    update = -pr.g * us;  // hinge / quantile (and non-invariant updates): the plain gradient step
   }
   const float decay = static_cast<float>(eta) * a.l2;
+  const float shrink = static_cast<float>(eta) * a.l1;
   int k = 0;
   for (int64_t p = b + lane; p < en; p += 64, ++k) {
     const uint64_t h = (a.idx[p] + off) & a.mask;
     float4* w = &a.W[h];
     const float x = a.val[p];
     const float rate = k < kRateCache ? pr.rate[k] : Rate(a, a.adaptive ? w->y : 0.f, a.normalized ? w->z : 1.f);
-    if (decay > 0.f) {
-      const float nw = atomicAdd(&w->x, update * x * rate) + update * x * rate;
-      atomicAdd(&w->x, -decay * nw);
+    if (decay > 0.f || shrink > 0.f) {
+      // the host learner's order: w += update; w -= eta l2 w; soft-threshold by eta l1 (as corrections to the
+      // value this update produced: exact at batch 1, hogwild otherwise)
+      float nw = atomicAdd(&w->x, update * x * rate) + update * x * rate;
+      float t = nw - decay * nw;
+      if (shrink > 0.f) t = t > shrink ? t - shrink : (t < -shrink ? t + shrink : 0.f);
+      atomicAdd(&w->x, t - nw);
     } else {
       atomicAdd(&w->x, update * x * rate);  // result unused: a non-returning atomic
     }
@@ -237,8 +244,10 @@ __device__ void UpdateWave(const SgdArgs& a, int64_t b, int64_t en, uint64_t off
   UpdateSecondPass(a, b, en, off, raw, y, imp, lane, pr, t, tw, snx);
 }
 
-__device__ __forceinline__ float LossOf(int loss, float p, float y) {
+__device__ __forceinline__ float LossOf(int loss, float p, float y, float tau = 0.5f) {
   if (loss == 1) return log1pf(expf(-y * p));
+  if (loss == 2) return fmaxf(0.f, 1.f - y * p);
+  if (loss == 3) { const float e = y - p; return e > 0.f ? tau * e : (tau - 1.f) * e; }
   return (p - y) * (p - y);
 }
 
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(64 * kSgdWaves) void sgd_kernel(SgdArgs a) {
     if (a.learn) {
       y = a.lab[e];
       imp = a.wt ? a.wt[e] : 1.f;
-      if (lane == 0) wloss[wid] = LossOf(a.loss, p, y) * imp;
+      if (lane == 0) wloss[wid] = LossOf(a.loss, p, y, a.tau) * imp;
     }
   }
   if (!a.learn) return;  // uniform over the launch
@@ -876,7 +885,8 @@ GpuSgd::~GpuSgd() = default;
 namespace {
 SgdArgs BaseArgs(const GpuSgdConfig& c) {
   SgdArgs a{};
-  a.lr = c.lr; a.power_t = c.power_t; a.initial_t = c.initial_t; a.l2 = c.l2; a.loss = c.loss;
+  a.lr = c.lr; a.power_t = c.power_t; a.initial_t = c.initial_t; a.l2 = c.l2; a.l1 = c.l1; a.tau = c.tau;
+  a.loss = c.loss;
   a.adaptive = c.adaptive ? 1 : 0; a.normalized = c.normalized ? 1 : 0; a.invariant = c.invariant ? 1 : 0;
   a.K = c.oaa > 0 ? c.oaa : c.csoaa;
   return a;

@@ -303,8 +303,8 @@ def _gpu_refusals(info) -> List[str]:
     """options the device learner does not run (deviceType='gpu' refuses them rather than silently running
     something else)"""
     bad = [k for k in ("cats",) if int(info[k])]
-    bad += ["l1"] if float(info["l1"]) else []
-    bad += ["loss_function " + info["loss_function"]] if info["loss_function"] not in ("squared", "logistic") else []
+    bad += ["loss_function " + info["loss_function"]] if info["loss_function"] not in (
+        "squared", "classic", "logistic", "hinge", "quantile") else []
     if info["cb_adf"] == "1" and info.get("cb_type", "mtr") not in ("mtr", "dr", "ips"):
         bad.append("cb_type " + info["cb_type"])
     return bad
@@ -317,7 +317,9 @@ def _gpu_config(vwmod, info):
     cfg.power_t = float(info["power_t"])
     cfg.initial_t = float(info["initial_t"])
     cfg.l2 = float(info["l2"])
-    cfg.loss = 1 if info["loss_function"] == "logistic" else 0
+    cfg.l1 = float(info["l1"])
+    cfg.tau = float(info.get("loss_quantile_tau", "0.5"))
+    cfg.loss = {"logistic": 1, "hinge": 2, "quantile": 3}.get(info["loss_function"], 0)
     cfg.adaptive, cfg.normalized, cfg.invariant = (info[k] == "1" for k in ("adaptive", "normalized", "invariant"))
     cfg.oaa = int(info["oaa"])
     cfg.csoaa = int(info["csoaa"])
