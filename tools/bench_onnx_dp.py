@@ -3,8 +3,8 @@
 config "ONNXModel ResNet-50 batch inference on synthetic 224x224 image
 DataFrame, 8-GPU DP".
 
-Each rank (one per GPU: ``torchrun --nproc-per-node N tools/bench_onnx_dp.py``,
-or plain ``python`` for one GPU) holds its own DataFrame partition of
+Each rank (one per GPU: ``python tools/bench_onnx_dp.py --gpus N`` launches the N
+ranks itself; plain ``python`` for one GPU) holds its own DataFrame partition of
 --images synthetic 3x224x224 float tensors and runs the public
 ``ONNXModel.transform`` (model-zoo ResNet-50 v2 topology, random-init
 weights from our ONNX writer, mini-batch --batch, softmax/argmax post
@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 def main() -> None:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--images", type=int, default=4096, help="images per GPU")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--precisions", default="fp32,fp16")
@@ -37,6 +38,8 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus or world > torch.cuda.device_count():
+        sys.exit(f"bench_onnx_dp: --gpus {a.gpus}, WORLD_SIZE={world}, {torch.cuda.device_count()} visible GPU(s)")
     torch.cuda.set_device(local_rank)
     from synapseml_amd.core.dataframe import DataFrame
     from synapseml_amd.onnx import ONNXModel, writer
@@ -78,4 +81,8 @@ def main() -> None:
 
 
 if __name__ == "__main__":
+    from bench import _parse_gpus, launch_ranks
+
+    if "WORLD_SIZE" not in os.environ and _parse_gpus(sys.argv[1:]) > 1:
+        sys.exit(launch_ranks(_parse_gpus(sys.argv[1:]), os.path.abspath(__file__), sys.argv[1:]))
     main()
