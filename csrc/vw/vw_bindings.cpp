@@ -6,7 +6,9 @@
 #include <pybind11/stl.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <memory>
 #include <stdexcept>
 
@@ -392,15 +394,39 @@ PYBIND11_MODULE(_vw, m) {
     if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
     return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
   });
-  m.def("nccl_comm", [](py::bytes uid, int rank, int world) {
+  // Non-blocking communicator init bounded by timeout_ms: a peer that fails before (or inside) the collective
+  // init cannot leave this rank blocked; on timeout / error the half-built communicator is aborted.
+  m.def("nccl_comm", [](py::bytes uid, int rank, int world, double timeout_ms) {
     std::string s = uid;
+    if (s.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
     std::memcpy(&id, s.data(), sizeof(id));
     auto h = std::make_shared<NcclHandle>();
-    if (ncclCommInitRank(&h->c, world, id, rank) != ncclSuccess) throw std::runtime_error("ncclCommInitRank failed");
+    {
+      py::gil_scoped_release rel;
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      ncclResult_t r = ncclCommInitRankConfig(&h->c, world, id, rank, &cfg);
+      const auto t0 = std::chrono::steady_clock::now();
+      while (r == ncclInProgress) {
+        if (ncclCommGetAsyncError(h->c, &r) != ncclSuccess) r = ncclInternalError;
+        if (r != ncclInProgress) break;
+        if (timeout_ms > 0 &&
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms) {
+          r = ncclInternalError;
+          break;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+      if (r != ncclSuccess) {
+        if (h->c) (void)ncclCommAbort(h->c);
+        h->c = nullptr;
+        throw std::runtime_error(std::string("RCCL communicator init failed or timed out: ") + ncclGetErrorString(r));
+      }
+    }
     h->world = world;
     return h;
-  });
+  }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("timeout_ms") = 120000.0);
 
   py::class_<GpuSgdConfig>(m, "GpuSgdConfig")
       .def(py::init<>())

@@ -1308,7 +1308,11 @@ void GpuSgd::AllReduceAverage(void* comm, int world) {
   if (world < 1 || !comm) return;  // a world-1 communicator still runs the collectives (one-GPU tests)
   hipStream_t s = impl_->stream;
   ncclComm_t c = static_cast<ncclComm_t>(comm);
-  auto nccl = [](ncclResult_t r) {
+  // the communicator is non-blocking (bounded init): an enqueue may answer ncclInProgress, and the next
+  // call must wait for the state to settle
+  auto nccl = [c](ncclResult_t r) {
+    while (r == ncclInProgress)
+      if (ncclCommGetAsyncError(c, &r) != ncclSuccess) r = ncclInternalError;
     if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL allreduce failed: ") + ncclGetErrorString(r));
   };
   const int64_t nblk = impl_->nblk;

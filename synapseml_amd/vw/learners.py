@@ -353,8 +353,13 @@ def _gpu_sync_comm(vwmod):
     if D.backend() != "nccl":
         raise RuntimeError("the GPU VW learner averages over RCCL: start the ranks with the nccl backend")
     if world not in _nccl_cache:
-        uid = vwmod.nccl_unique_id() if D.rank() == 0 else None
-        _nccl_cache[world] = vwmod.nccl_comm(D.broadcast_object(uid, 0), D.rank(), world)
+        import os
+
+        timeout_ms = float(os.environ.get("SML_RCCL_INIT_TIMEOUT_MS", "120000"))
+        # readiness agreement + bounded collective init + abort on any rank's failure (distributed.py)
+        _nccl_cache[world] = D.init_with_retries(
+            lambda uid: vwmod.nccl_comm(uid, D.rank(), world, timeout_ms), "VW RCCL communicator",
+            prepare=lambda: vwmod.nccl_unique_id() if D.rank() == 0 else None)
     return _nccl_cache[world]
 
 

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-4 performance pass: rocprofv3 kernel statistics of the headline fit (batched growth), estimator-level
+# ranker / VW / transform benches, conv roofline table, P2P latency probe. Usage: tools/gpu_r4_perf.sh OUTDIR
+OUT=${1:-gpurun_out/r4p}
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fit" -o fit -- python3 bench.py --steps 2 --warmup 1 > "$OUT/prof_fit.log" 2>&1 || exit 1
+timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker.log" 2>&1 || exit 1
+timeout -k 10 400 python tools/bench_vw.py --steps 2 --warmup 1 > "$OUT/bench_vw_estimator.log" 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_conv.py --dtype fp16 > "$OUT/conv_fp16_roofline.log" 2>&1 || exit 1
+HSA_ENABLE_IPC_MODE_LEGACY=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 --master-port=29541 tools/p2p_check.py > "$OUT/p2p_check_2rank_1gpu.log" 2>&1 || true
