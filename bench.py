@@ -120,10 +120,14 @@ def main() -> None:
 
     use_gpu = args.device == "gpu" and torch.cuda.is_available()
     ndev = torch.cuda.device_count() if use_gpu else 0
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # a launcher that gives every rank its own single visible device (HIP/ROCR/CUDA_VISIBLE_DEVICES per rank)
+    per_rank_vis = ndev == 1 and any(len([x for x in os.environ.get(v, "").split(",") if x.strip()]) == 1
+                                     for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
     # more ranks than GPUs (a rehearsal of the multi-GPU path on a small box): ranks share devices, so the
     # control plane is gloo and histograms go over the one-shot IPC allreduce on a host base communicator
     # (RCCL cannot put two ranks on one device). The driver's N-GPU runs have one GPU per rank.
-    shared = use_gpu and world > ndev
+    shared = use_gpu and local_world > ndev and not per_rank_vis
     if shared and not args.allow_shared_device:
         print(f"bench.py: {world} ranks but only {ndev} visible GPU(s); a {world}-GPU measurement needs {world} "
               "devices (pass --allow-shared-device for a shared-device rehearsal)", file=sys.stderr)
@@ -136,6 +140,17 @@ def main() -> None:
         D.init_from_env("nccl" if use_gpu and not shared else "gloo")
         if shared:
             os.environ["SML_GBDT_SHARED_DEVICE"] = "1"
+    distinct = 0
+    if use_gpu:
+        # the devices really in use, by identity (uuid / PCI location), over every rank
+        pr = torch.cuda.get_device_properties(torch.cuda.current_device())
+        ident = str(getattr(pr, "uuid", "")) + ":%s:%s:%s" % (getattr(pr, "pci_domain_id", ""),
+                                                              getattr(pr, "pci_bus_id", ""), getattr(pr, "pci_device_id", ""))
+        distinct = len(set(D.all_gather_object(ident)))
+        if distinct != world and not args.allow_shared_device:
+            print(f"bench.py: {world} ranks run on {distinct} distinct GPU(s); refusing to report it as a "
+                  f"{world}-GPU measurement", file=sys.stderr)
+            sys.exit(3)
     from synapseml_amd.core.dataframe import DataFrame
     from synapseml_amd.lightgbm import LightGBMClassifier
     from synapseml_amd.ops import native
@@ -207,7 +222,7 @@ def main() -> None:
     if comm_world != world:
         print(f"bench.py: communicator world {comm_world} != {world} ranks", file=sys.stderr)
         sys.exit(4)
-    n_devices = (min(world, ndev) if shared else world) if use_gpu else 0
+    n_devices = distinct if use_gpu else 0
     if rank == 0:
         out = {
             "metric": METRIC,

@@ -44,6 +44,15 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def local_device() -> int:
+    """this rank's GPU index: LOCAL_RANK over the visible devices (a launcher that gives each rank a single
+    visible device maps every rank to its device 0)"""
+    import torch
+
+    n = torch.cuda.device_count()
+    return local_rank() % n if n > 0 else -1
+
+
 def backend() -> Optional[str]:
     d = _dist()
     return d.get_backend() if d and d.is_initialized() else None
@@ -63,7 +72,7 @@ def init_from_env(backend_name: Optional[str] = None, timeout_s: float = 1200.0)
     if backend_name is None:
         backend_name = "nccl" if torch.cuda.is_available() else "gloo"
     if backend_name == "nccl":
-        torch.cuda.set_device(local_rank())
+        torch.cuda.set_device(local_device())
     d.init_process_group(backend=backend_name, timeout=datetime.timedelta(seconds=timeout_s))
     return True
 

@@ -340,7 +340,7 @@ def _gpu_learner(args: str, model_bytes=None):
         raise RuntimeError("deviceType='gpu' requested but no HIP device is visible")
     import os
 
-    g = vwmod.GpuSgd(_gpu_config(vwmod, info), int(os.environ.get("LOCAL_RANK", "0")))
+    g = vwmod.GpuSgd(_gpu_config(vwmod, info), D.local_device())
     if model_bytes is not None:  # initialModel: warm start (weights, adaptive / normalizer state, schedule)
         g.import_model(bytes(model_bytes))
     return vwmod, info, g
@@ -443,7 +443,7 @@ class _GpuScorer:
             raise ValueError("model not scoreable on the device: " + ", ".join(bad or ["no HIP device / ngram"]))
         import os
 
-        self.g = vwmod.GpuSgd(_gpu_config(vwmod, self.info), int(os.environ.get("LOCAL_RANK", "0")))
+        self.g = vwmod.GpuSgd(_gpu_config(vwmod, self.info), D.local_device())
         self.g.import_model(bytes(model))
 
     def predict(self, blocks, n: int, shared_blocks=None, row_map=None):
