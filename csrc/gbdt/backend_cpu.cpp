@@ -1,6 +1,7 @@
 // CPU training backend: OpenMP histogram construction + host split search.
 // It is the numerical oracle for the HIP kernels and the runtime for hosts
 // without an MI355X (BASELINE config 1, "local[2] CPU plumbing").
+#include <emmintrin.h>
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -269,45 +270,59 @@ class CpuBackend : public TrainBackend {
     }
     // row groups x feature slices; one row group unless there are fewer features than threads
     // up to feats_per_slice_ features per thread: the rows are split into row groups (each random row of a
-    // child leaf gathered by one thread per slice), with per-row-group tables summed afterwards
+    // child leaf gathered by one thread per slice), with per-row-group tables summed afterwards.
+    // The tables are accumulated at a padded feature pitch (kPitch = 512 + 8 doubles): at the natural 4 KiB
+    // pitch the same bin of every feature shares its low 12 address bits, and a row whose features sit in
+    // the same (e.g. the most common) bin makes every load look like it aliases the previous feature's store
+    // (4K aliasing): 3.5x slower per update on skewed bins (hb2 microbench, 28 features, 60 % in one bin).
+    constexpr int kPitch = stride + 8;
+    const size_t psz = static_cast<size_t>(F_) * kPitch;
     const int fps = std::max(1, feats_per_slice_);
     const int fs = std::max(1, std::min(nt, (nf + fps - 1) / fps));
     const int rg = std::max(1, nt / fs);
-    if (rg > 1) {
-      if (static_cast<int>(hloc_.size()) < rg) hloc_.resize(rg);
-      for (int gi = 1; gi < rg; ++gi) if (hloc_[gi].size() < hsz) hloc_[gi].resize(hsz);
-    }
+    if (static_cast<int>(hloc_.size()) < rg) hloc_.resize(rg);
+    for (int gi = 0; gi < rg; ++gi) if (hloc_[gi].size() < psz) hloc_[gi].resize(psz);
     double* out = hist->data();
 #pragma omp parallel for num_threads(fs * rg) schedule(static, 1) collapse(2)
     for (int gi = 0; gi < rg; ++gi) {
       for (int si = 0; si < fs; ++si) {
-        double* dst = out;
-        if (rg > 1 && gi > 0) dst = hloc_[gi].data();  // row group 0 writes the output directly
+        double* dst = hloc_[gi].data();
         const int fa = nf * si / fs, fb = nf * (si + 1) / fs;
-        if (rg > 1 && gi > 0)
-          for (int j = fa; j < fb; ++j) std::fill(dst + fl[j] * stride, dst + (fl[j] + 1) * stride, 0.0);
+        for (int j = fa; j < fb; ++j) std::fill(dst + fl[j] * kPitch, dst + fl[j] * kPitch + stride, 0.0);
         const int64_t pa = cnt * gi / rg, pb = cnt * (gi + 1) / rg;
+        // one 16-B (g, h) add per feature (SSE2: one load, add and store instead of two of each)
         for (int64_t p = pa; p < pb; ++p) {
           if (p + 24 < pb) __builtin_prefetch(bins + idx[p + 24] * rs);  // random rows of a child leaf
           const uint8_t* row = bins + idx[p] * rs;
-          const double gv = og[2 * p], hv = og[2 * p + 1];
-          for (int j = fa; j < fb; ++j) {
-            const int f = fl[j];
-            double* c = dst + f * stride + row[f] * 2;
-            c[0] += gv;
-            c[1] += hv;
+          const __m128d gh = _mm_cvtps_pd(_mm_castsi128_ps(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(og + 2 * p))));
+          // four features per step, loads ahead of stores: the four cells are in different features' tables
+          // (never the same address), so the loads need not wait for the stores (2.2x per update, hb3)
+          int j = fa;
+          for (; j + 4 <= fb; j += 4) {
+            double* c0 = dst + fl[j] * kPitch + row[fl[j]] * 2;
+            double* c1 = dst + fl[j + 1] * kPitch + row[fl[j + 1]] * 2;
+            double* c2 = dst + fl[j + 2] * kPitch + row[fl[j + 2]] * 2;
+            double* c3 = dst + fl[j + 3] * kPitch + row[fl[j + 3]] * 2;
+            const __m128d a0 = _mm_load_pd(c0), a1 = _mm_load_pd(c1), a2 = _mm_load_pd(c2), a3 = _mm_load_pd(c3);
+            _mm_store_pd(c0, _mm_add_pd(a0, gh));
+            _mm_store_pd(c1, _mm_add_pd(a1, gh));
+            _mm_store_pd(c2, _mm_add_pd(a2, gh));
+            _mm_store_pd(c3, _mm_add_pd(a3, gh));
+          }
+          for (; j < fb; ++j) {
+            double* c = dst + fl[j] * kPitch + row[fl[j]] * 2;
+            _mm_store_pd(c, _mm_add_pd(_mm_load_pd(c), gh));
           }
         }
       }
     }
-    if (rg > 1) {
-#pragma omp parallel for num_threads(std::min(nt, nf)) schedule(static)
-      for (int j = 0; j < nf; ++j) {
-        double* o = out + fl[j] * stride;
-        for (int gi = 1; gi < rg; ++gi) {
-          const double* src = hloc_[gi].data() + fl[j] * stride;
-          for (int b = 0; b < stride; ++b) o[b] += src[b];
-        }
+#pragma omp parallel for num_threads(std::max(1, std::min(nt, nf))) schedule(static)
+    for (int j = 0; j < nf; ++j) {
+      double* o = out + fl[j] * stride;
+      std::memcpy(o, hloc_[0].data() + fl[j] * kPitch, sizeof(double) * stride);
+      for (int gi = 1; gi < rg; ++gi) {
+        const double* src = hloc_[gi].data() + fl[j] * kPitch;
+        for (int b = 0; b < stride; ++b) o[b] += src[b];
       }
     }
     stats.hist_ms += Ms(t0);

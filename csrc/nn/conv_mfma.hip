@@ -82,11 +82,11 @@ __device__ __forceinline__ T FromF(float v) {
 
 // Epilogue shared by the conv kernels: bias, ReLU, residual add and the optional second output,
 // staged per wave through LDS (lds must hold 4 * (BM/2) * (BN/2 + 8) elements and be free).
-template <class T, int WM, int WN>
+template <class T, int WM, int WN, int kWN = 2>
 __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 16][WN / 16], T* lds, int M, int m0,
                                              int n0, int wid, int lane) {
   constexpr int TM = WM / 16, TN = WN / 16;
-  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
   const int fr = lane & 15;
   // epilogue part 1 (registers): lane holds column n = .. + (lane & 15), rows 4*(lane >> 4) + reg;
   // bias + ReLU in fp32, rounded to T (the unfused graph's conv output), staged per wave through LDS.
@@ -185,13 +185,16 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 // one 16x16x32 step per plane pair instead of eight 16x16x4 f32 MFMAs (1/16 of the bf16 rate on gfx950).
 // kWPre (with kSplit): the weights arrive already split, a.w = [kSplit][Cout][R][S][C] bf16 planes (packed
 // once per model by the executor): no split work for B at staging, 2 B per plane and element from HBM / L2.
+// kWN: waves along N (2, or 1 for the Cout = 64 tiles whose 64x64 wave tiles halve the LDS fragment reads per
+// MFMA against 32x32 ones: at 32x32 a wave issues one ds_read_b128 per 16-cycle MFMA, which is the LDS array's
+// whole rate with a wave per SIMD)
 template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false, int kSplit = 0,
-          bool kWPre = false>
+          bool kWPre = false, int kWN = 2>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
-  constexpr int kWavesM = kThr / 128;           // waves along M (2 along N)
-  constexpr int WM = BM / kWavesM, WN = BN / 2; // wave tile
+  constexpr int kWavesM = kThr / 64 / kWN;        // waves along M
+  constexpr int WM = BM / kWavesM, WN = BN / kWN; // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
   constexpr int AR = BM * kBKBytes / 16 / kThr;  // 16-B A chunks per thread per tile
   constexpr int BR = BN * kBKBytes / 16 / kThr;  // 16-B B chunks per thread per tile
@@ -266,7 +269,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
   const int fr = lane & 15, fk = EPV * (lane >> 4);
   const int nk = K / kBK;
 
@@ -503,10 +506,10 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
-  ConvEpilogue<T, WM, WN>(a, acc, lds, M, m0, n0, wid, lane);
+  ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
-template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false>
+template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false, int kWN = 2>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   // f32 64x64: two register stages when the K loop is long enough and there is no prologue (the prologue
@@ -525,8 +528,8 @@ void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
       return;
     }
   }
-  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit, kWPre>
-                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit, kWPre>;
+  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit, kWPre, kWN>
+                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit, kWPre, kWN>;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
 
@@ -549,6 +552,14 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 128128: LaunchTile<T, 128, 128, kThreads, kSplit, kWPre>(a, M, st); return 0;
     case 128999: LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
     case 64999: LaunchTile<T, 64, 64, 512, kSplit, kWPre>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
+    case 256064:  // 256x64, 4 waves (4x1, 64x64 each)
+    case 128164:  // 128x64, 2 waves (2x1, 64x64 each)
+      if constexpr (sizeof(T) == 2 && kSplit == 0) {
+        if ((a.kernel ? a.kernel : env_tile) == 256064) LaunchTile<T, 256, 64, 256, 0, false, 1>(a, M, st);
+        else LaunchTile<T, 128, 64, 128, 0, false, 1>(a, M, st);
+        return 0;
+      }
+      return -4;
     case 256128:
     case 128256:
       // 8-wave tiles: the f32 epilogue staging would not fit the operand LDS

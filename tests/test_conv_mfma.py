@@ -22,8 +22,9 @@ def _ref(x, w, stride, pad, bias=None, relu=False, pro=None, res=None, post=None
     return y, y2
 
 
-# 0 = shape-chosen tile; BM*1000+BN = forced tile (128999 / 64999: 128x128 / 64x64 with 8 waves)
-KERNELS = [0, 64064, 64999, 128064, 64128, 128128, 128999, 256128, 128256]
+# 0 = shape-chosen tile; BM*1000+BN = forced tile (128999 / 64999: 128x128 / 64x64 with 8 waves; 256064 /
+# 128164: 256x64 / 128x64 with one wave along N, 64x64 wave tiles)
+KERNELS = [0, 64064, 64999, 128064, 64128, 128128, 128999, 256128, 128256, 256064, 128164]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -61,7 +62,7 @@ def test_conv_matches_fp32_reference(dtype, shape):
     bias = torch.randn(Co, device="cuda")
     ref, _ = _ref(x, w, st, pd, bias=bias, relu=True)
     tol = 2e-2 if dtype == torch.float16 else 8e-2
-    for kernel in (0, 128128, 128999, 256128, 128256):
+    for kernel in (0, 128128, 128999, 256128, 128256, 256064, 128164):
         y = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
         torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: f"kernel {kernel}: {m}")
 
