@@ -52,13 +52,47 @@ struct BinMapper {
       if (missing_type == kMissingNaN) return static_cast<uint32_t>(num_bin - 1);
       v = 0.0;
     }
-    // smallest i with v <= upper_bounds[i]
-    int lo = 0, hi = static_cast<int>(upper_bounds.size()) - 1;
-    while (lo < hi) {
-      int mid = (lo + hi) >> 1;
-      if (v <= upper_bounds[mid]) hi = mid; else lo = mid + 1;
+    // smallest i with v <= upper_bounds[i] (the last bound is +inf): a branchless lower bound - the halving
+    // step is a conditional move, so a row of random values costs no branch mispredictions (the branchy
+    // search mispredicted about half of its ~8 steps per value)
+    // (index arithmetic, not a pointer select: g++ turns the select back into a branch; 16.5 vs 66 ns per
+    // value over 255 normal-distributed bounds)
+    const double* b = upper_bounds.data();
+    size_t base = 0, n = upper_bounds.size();
+    while (n > 1) {
+      const size_t half = n >> 1;
+      base += static_cast<size_t>(b[base + half - 1] < v) * half;
+      n -= half;
     }
-    return static_cast<uint32_t>(lo);
+    return static_cast<uint32_t>(base + static_cast<size_t>(b[base] < v));
+  }
+  // ValueToBin of R values of this column at once (v[r * vs] -> o[r * os]): the R searches are interleaved
+  // step by step, so their dependent load chains overlap (8 rows: 8.6 vs 17 ns per value, vb3 microbench)
+  template <int R, class T>
+  inline void ValueToBinN(const T* v, int64_t vs, uint8_t* o, int64_t os) const {
+    if (is_categorical) {
+      for (int r = 0; r < R; ++r) o[r * os] = static_cast<uint8_t>(ValueToBin(static_cast<double>(v[r * vs])));
+      return;
+    }
+    double x[R];
+    size_t base[R];
+    for (int r = 0; r < R; ++r) {
+      const double d = static_cast<double>(v[r * vs]);
+      x[r] = std::isnan(d) ? 0.0 : d;
+      base[r] = 0;
+    }
+    const double* b = upper_bounds.data();
+    size_t n = upper_bounds.size();
+    while (n > 1) {
+      const size_t half = n >> 1;
+      for (int r = 0; r < R; ++r) base[r] += static_cast<size_t>(b[base[r] + half - 1] < x[r]) * half;
+      n -= half;
+    }
+    for (int r = 0; r < R; ++r) {
+      const uint32_t bin = static_cast<uint32_t>(base[r] + static_cast<size_t>(b[base[r]] < x[r]));
+      o[r * os] = static_cast<uint8_t>(missing_type == kMissingNaN && std::isnan(static_cast<double>(v[r * vs]))
+                                           ? static_cast<uint32_t>(num_bin - 1) : bin);
+    }
   }
   double BinToValue(uint32_t bin) const {  // split threshold for "bin <= t"
     return upper_bounds[bin];

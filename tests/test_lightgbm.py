@@ -472,3 +472,34 @@ def test_ranker_group_order_vectorised():
         codes = {}
         ref = np.argsort(np.asarray([codes.setdefault(v, len(codes)) for v in ids.tolist()]), kind="stable")
         assert np.array_equal(_group_order(ids), ref)
+
+
+def test_dense_push_interleaved_bins_match_scalar_and_searchsorted():
+    """Host bin encoding (blocks of 8 rows, interleaved branchless searches) equals the one-row path and a
+    numpy searchsorted oracle, for float32 and float64 rows, NaN / zero-as-missing and a categorical column."""
+    from synapseml_amd import _gbdt as g
+
+    rng = np.random.default_rng(0)
+    n, F = 20011, 6
+    X = rng.normal(size=(n, F))
+    X[rng.random((n, F)) < 0.05] = np.nan
+    X[:, 2] = np.round(X[:, 2] * 3)
+    X[:, 3] = rng.integers(0, 7, n)
+    X[rng.random(n) < 0.3, 4] = 0.0
+    for params in ("max_bin=255 categorical_feature=3", "max_bin=63 use_missing=false",
+                   "max_bin=255 zero_as_missing=true"):
+        ref = g.DatasetReference.from_sample(np.ascontiguousarray(X[:10000]), n, params, [f"f{i}" for i in range(F)])
+        for dt in (np.float64, np.float32):
+            Xd = np.ascontiguousarray(X.astype(dt))
+            ds = g.Dataset(ref, n)
+            ds.push_dense(Xd, 0)
+            b = np.asarray(ds.bins)
+            ds1 = g.Dataset(ref, n)
+            for s in range(0, 300):
+                ds1.push_dense(Xd[s:s + 1], s)
+            assert (b[:300] == np.asarray(ds1.bins)[:300]).all(), params
+            for f in (0, 1, 2, 4, 5):
+                ub = np.asarray(ref.upper_bounds(f))
+                x = Xd[:, f].astype(np.float64)
+                ok = ~np.isnan(x)
+                assert (b[ok, f] == np.searchsorted(ub, x[ok], side="left")).all(), (params, f)
