@@ -509,6 +509,157 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
+// LDS-DMA form (f16 / bf16, no prologue): the A and B tiles go global -> LDS with buffer_load ... lds
+// (16 B per lane, one 1-KiB wave-instruction = 8 tile rows of 128 B), so staging takes no VGPRs and no
+// ds_write (whose 13-cycle wave-instruction transfer, at ~79 B/clk/CU, is as long as the tile's fragment
+// reads). A DMA lands lane-linear, so the rows are unpadded 128-B lines and the bank spread comes from an XOR
+// swizzle applied on the SOURCE side: lane l of an 8-row piece loads chunk (l & 7) ^ row%8 of its row, i.e.
+// chunk c of row r sits at slot c ^ (r & 7); the fragment reads apply the same XOR (conflict-free 16-lane
+// ds_read_b128 groups). Out-of-range rows / padding taps load from an out-of-range buffer offset: zeros.
+// Tile kt+1's DMAs are issued before tile kt's MFMAs; a vmcnt(0) + barrier per K tile retires them.
+template <class T, int BM, int BN, int kThr, int kWN>
+__global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
+  typedef typename Vec<T>::type V8;
+  static_assert(sizeof(T) == 2, "LDS-DMA conv is the f16 / bf16 form");
+  constexpr int kBK = 64, EPV = 8;
+  constexpr int NW = kThr / 64;
+  constexpr int kWavesM = NW / kWN;
+  constexpr int WM = BM / kWavesM, WN = BN / kWN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;  // 8-row DMA pieces per wave and tile
+  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  constexpr int kOpBytes = 2 * (BM + BN) * kBK * 2;
+  constexpr int kEpiBytes = NW * WM * (WN + 8) * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kOpBytes > kEpiBytes ? kOpBytes : kEpiBytes];
+  T* lds = reinterpret_cast<T*>(smem);
+  T* As = lds;                 // [buf][BM][64], swizzled chunks
+  T* Bs = lds + 2 * BM * kBK;  // [buf][BN][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = a.B * a.OH * a.OW;
+  const int K = a.R * a.S * a.C;
+  const int tiles_n = (a.Cout + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int total = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int prow = lane >> 3;                 // row within an 8-row piece (= row % 8)
+  const int kcs = (lane & 7) ^ prow;          // the chunk this lane fetches (source-side swizzle)
+  constexpr uint32_t kOob = 0x80000000u;
+  int abase[AI];
+  uint64_t amask[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + (wid * AI + i) * 8 + prow;
+    const int mm = m < M ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW;
+    const int oh = t2 % a.OH, b = t2 / a.OH;
+    const int ih0 = oh * a.stride_h - a.pad_h, iw0 = ow * a.stride_w - a.pad_w;
+    abase[i] = ((b * a.H + ih0) * a.W + iw0) * a.C + kcs * EPV;
+    uint64_t mk = 0;
+    if (m < M)
+      for (int r = 0, t = 0; r < a.R; ++r)
+        for (int s2 = 0; s2 < a.S; ++s2, ++t) {
+          const int ih = ih0 + r * a.dil_h, iw = iw0 + s2 * a.dil_w;
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) mk |= 1ull << t;
+        }
+    amask[i] = mk;
+  }
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, a.B * a.H * a.W * a.C * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, a.Cout * K * 2, 0x00020000);
+  uint32_t boff[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int n = n0 + (wid * BI + i) * 8 + prow;
+    boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kcs * EPV) * 2) : kOob;
+  }
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
+  const int fr = lane & 15;
+  const int nk = K / kBK;
+
+  int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0, loaded = 0;
+  // DMA of the next K tile into LDS buffer `buf` (wave-uniform destination: 8 rows of 128 B per piece)
+  auto dma_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bool ok = (amask[i] >> lt) & 1ull;
+      const uint32_t vo = ok ? static_cast<uint32_t>((abase[i] + toff) * 2) : kOob;
+      T* dst = As + (buf * BM + (wid * AI + i) * 8) * kBK;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, (__attribute__((address_space(3))) void*)(dst), 16,
+                                               vo, lc0 * 2, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      T* dst = Bs + (buf * BN + (wid * BI + i) * 8) * kBK;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, (__attribute__((address_space(3))) void*)(dst), 16,
+                                               boff[i], lk0 * 2, 0, 0);
+    }
+    if (++loaded < nk) {
+      lk0 += kBK;
+      lc0 += kBK;
+      if (lc0 == a.C) {
+        lc0 = 0;
+        ++lt;
+        if (++ls == a.S) {
+          ls = 0;
+          ++lr;
+        }
+        toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
+      }
+    }
+  };
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < kBK / 32; ++ks) {
+      const int c = ks * 4 + (lane >> 4);  // 16-B chunk of the lane's k range
+      V8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm0 + i * 16 + fr;
+        af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + r) * kBK + ((c ^ (r & 7)) * EPV));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn0 + j * 16 + fr;
+        bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + r) * kBK + ((c ^ (r & 7)) * EPV));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+    }
+  };
+  dma_tile(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) dma_tile(buf ^ 1);
+    compute(buf);
+    __builtin_amdgcn_sched_barrier(0);  // keep the tile's MFMAs ahead of the DMA wait
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
+}
+
+template <class T, int BM, int BN, int kThr, int kWN = 2>
+void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
+  const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
+}
+
 template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false, int kWN = 2>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
@@ -552,6 +703,18 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 128128: LaunchTile<T, 128, 128, kThreads, kSplit, kWPre>(a, M, st); return 0;
     case 128999: LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
     case 64999: LaunchTile<T, 64, 64, 512, kSplit, kWPre>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
+    case 128777:  // LDS-DMA forms (f16 / bf16 without prologue): 128x128 8 waves, 64x64 4 waves, 256x64 4 waves
+    case 64777:
+    case 256777:
+      if constexpr (sizeof(T) == 2 && kSplit == 0) {
+        if (a.in_scale) return -4;
+        const int code = a.kernel ? a.kernel : env_tile;
+        if (code == 128777) LaunchGlds<T, 128, 128, 512>(a, M, st);
+        else if (code == 64777) LaunchGlds<T, 64, 64, 256>(a, M, st);
+        else LaunchGlds<T, 256, 64, 256, 1>(a, M, st);
+        return 0;
+      }
+      return -4;
     case 256064:  // 256x64, 4 waves (4x1, 64x64 each)
     case 128164:  // 128x64, 2 waves (2x1, 64x64 each)
       if constexpr (sizeof(T) == 2 && kSplit == 0) {
@@ -588,6 +751,18 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     if (a.Cout <= 64) LaunchTile<T, 64, 64, kThreads, kSplit, kWPre>(a, M, st);
     else LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st);
     return 0;
+  }
+  // SML_CONV_GLDS=1: the LDS-DMA staged forms for the layers without a prologue (A/B switch)
+  static const bool glds = [] {
+    const char* e = std::getenv("SML_CONV_GLDS");
+    return e && std::atoi(e) != 0;
+  }();
+  if constexpr (sizeof(T) == 2) {
+    if (glds && !a.in_scale) {
+      if (a.Cout <= 64) LaunchGlds<T, 64, 64, 256>(a, M, st);
+      else LaunchGlds<T, 128, 128, 512>(a, M, st);
+      return 0;
+    }
   }
   if (a.Cout <= 64) {
     LaunchTile<T, 64, 64>(a, M, st);

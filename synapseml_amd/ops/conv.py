@@ -80,7 +80,8 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
     (top, left, bottom, right). ``x``: [B, C, H, W] channels_last, fp32/fp16/bf16 (C % 32 == 0 for fp32, % 64 otherwise). ``wp``: packed [Cout, R, S, C]
     (a channels_last [Cout, C, R, S] weight permuted to (0, 2, 3, 1) is exactly that). Returns y (and y2).
     ``kernel``: 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128, 128128, 256128, 128256;
-    128999 / 64999 = 8-wave 128x128 / 64x64; 256064 / 128164 = 256x64 / 128x64 with 64x64 wave tiles).
+    128999 / 64999 = 8-wave 128x128 / 64x64; 256064 / 128164 = 256x64 / 128x64 with 64x64 wave tiles;
+    128777 / 64777 / 256777 = LDS-DMA staged 128x128 / 64x64 / 256x64, f16/bf16 without in_affine).
     ``f32_mode`` (fp32 inputs): "exact" | "bf16x3" | "bf16x6" (see F32_MODES; default SML_CONV_F32 or bf16x6).
     ``w_planes``: split_weight(wp, mode) computed once per weight; the split modes then read the planes instead
     of splitting the weights in every block."""

@@ -23,8 +23,9 @@ def _ref(x, w, stride, pad, bias=None, relu=False, pro=None, res=None, post=None
 
 
 # 0 = shape-chosen tile; BM*1000+BN = forced tile (128999 / 64999: 128x128 / 64x64 with 8 waves; 256064 /
-# 128164: 256x64 / 128x64 with one wave along N, 64x64 wave tiles)
-KERNELS = [0, 64064, 64999, 128064, 64128, 128128, 128999, 256128, 128256, 256064, 128164]
+# 128164: 256x64 / 128x64 with one wave along N, 64x64 wave tiles; 128777 / 64777 / 256777: the LDS-DMA
+# staged 128x128 (8 waves) / 64x64 / 256x64 forms, swizzled unpadded LDS rows)
+KERNELS = [0, 64064, 64999, 128064, 64128, 128128, 128999, 256128, 128256, 256064, 128164, 128777, 64777, 256777]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -62,7 +63,7 @@ def test_conv_matches_fp32_reference(dtype, shape):
     bias = torch.randn(Co, device="cuda")
     ref, _ = _ref(x, w, st, pd, bias=bias, relu=True)
     tol = 2e-2 if dtype == torch.float16 else 8e-2
-    for kernel in (0, 128128, 128999, 256128, 128256, 256064, 128164):
+    for kernel in (0, 128128, 128999, 256128, 128256, 256064, 128164, 128777, 64777, 256777):
         y = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
         torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: f"kernel {kernel}: {m}")
 
