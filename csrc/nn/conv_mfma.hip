@@ -27,6 +27,7 @@
 // Requires C % BK == 0 (every ResNet conv but the 3-channel stem).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -173,6 +174,50 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
   }
 }
 
+// Split-K hand-off (after the K loop, LDS free): every split stores its fp32 partial tile (lane-natural
+// layout, one coalesced 1-KiB store per accumulator and wave), publishes it (vmcnt(0), barrier, agent-scope
+// release, then a relaxed agent-scope ticket add) and the split that draws the last ticket acquires, sums
+// the partial tiles in split order (deterministic whatever the arrival order) and returns true to run the
+// epilogue; the others return false.
+template <int TM, int TN, int kThr>
+__device__ __forceinline__ bool SplitKReduce(const ConvArgs& a, f4 (&acc)[TM][TN], unsigned char* smem, int tile,
+                                             int split, int SK, int tid) {
+  constexpr int kTileF4 = kThr * TM * TN;  // f4 per partial tile
+  f4* mine = reinterpret_cast<f4*>(a.ws) + (static_cast<int64_t>(tile) * SK + split) * kTileF4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) mine[(i * TN + j) * kThr + tid] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(a.ws_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == SK - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __syncthreads();  // the flag's LDS word is reused by the epilogue staging
+  if (!last) return false;
+  const f4* base = reinterpret_cast<const f4*>(a.ws) + static_cast<int64_t>(tile) * SK * kTileF4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      f4 v = base[(i * TN + j) * kThr + tid];
+      for (int s2 = 1; s2 < SK; ++s2) v += base[static_cast<int64_t>(s2) * kTileF4 + (i * TN + j) * kThr + tid];
+      acc[i][j] = v;
+    }
+  return true;
+}
+
 // kThr = 256 (4 waves, 2x2) or 512 (8 waves, 4x2: the 256x128 / 128x256 tiles, one block per CU)
 // kDepth 2: two register stages (tile kt+2's loads in flight during tile kt's MFMAs)
 // kStem: a few-channel stem conv (the 3-channel ResNet stem, input padded to C = 4, weights packed to
@@ -217,9 +262,13 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   const int K = a.R * a.S * a.C;
   const int tiles_n = (a.Cout + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int total = tiles_m * tiles_n;
+  const int SK = kStem ? 1 : a.split_k;  // K splits per tile (a tile's splits are adjacent block ids)
+  const int total = tiles_m * tiles_n * SK;
   int bid = blockIdx.x;
   if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
+  const int split = bid % SK;
+  bid /= SK;
+  const int tile = bid;
   const int tn = bid % tiles_n, tm = bid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -271,7 +320,9 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 
   const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
   const int fr = lane & 15, fk = EPV * (lane >> 4);
-  const int nk = K / kBK;
+  const int nk_all = K / kBK;
+  const int kt0 = split * nk_all / SK;
+  const int nk = (split + 1) * nk_all / SK - kt0;  // K tiles of this split
 
   auto compute = [&](int buf) {
     if constexpr (kSplit > 0) {
@@ -352,6 +403,14 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   };
   // next tile to load: tap (lr, ls) = index lt, channel offset lc0, element offset of the tap toff
   int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0, loaded = 0;
+  if (kt0 > 0) {  // a later split starts inside the (tap, channel) walk
+    lk0 = kt0 * kBK;
+    lt = lk0 / a.C;
+    lc0 = lk0 - lt * a.C;
+    lr = lt / a.S;
+    ls = lt - lr * a.S;
+    toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
+  }
   auto load_tile = [&](Stage& st) {
     st.okm = 0;
     if constexpr (kStem) {
@@ -506,6 +565,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
+  if (SK > 1 && !SplitKReduce<TM, TN, kThr>(a, acc, smem, tile, split, SK, tid)) return;
   ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
@@ -517,6 +577,14 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 // chunk c of row r sits at slot c ^ (r & 7); the fragment reads apply the same XOR (conflict-free 16-lane
 // ds_read_b128 groups). Out-of-range rows / padding taps load from an out-of-range buffer offset: zeros.
 // Tile kt+1's DMAs are issued before tile kt's MFMAs; a vmcnt(0) + barrier per K tile retires them.
+// 16 B per lane from a buffer resource straight into LDS at the wave-uniform dst (+ 16 * lane): the
+// LDS-address-space builtin exists in the device pass only (the host pass just needs the kernel's stub)
+__device__ __forceinline__ void DmaToLds16(__amdgpu_buffer_rsrc_t r, void* dst, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst), 16, voff, soff, 0, 0);
+#endif
+}
+
 template <class T, int BM, int BN, int kThr, int kWN>
 __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
@@ -595,15 +663,11 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
     for (int i = 0; i < AI; ++i) {
       const bool ok = (amask[i] >> lt) & 1ull;
       const uint32_t vo = ok ? static_cast<uint32_t>((abase[i] + toff) * 2) : kOob;
-      T* dst = As + (buf * BM + (wid * AI + i) * 8) * kBK;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, (__attribute__((address_space(3))) void*)(dst), 16,
-                                               vo, lc0 * 2, 0, 0);
+      DmaToLds16(xres, As + (buf * BM + (wid * AI + i) * 8) * kBK, vo, lc0 * 2);
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      T* dst = Bs + (buf * BN + (wid * BI + i) * 8) * kBK;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, (__attribute__((address_space(3))) void*)(dst), 16,
-                                               boff[i], lk0 * 2, 0, 0);
+      DmaToLds16(wres, Bs + (buf * BN + (wid * BI + i) * 8) * kBK, boff[i], lk0 * 2);
     }
     if (++loaded < nk) {
       lk0 += kBK;
@@ -662,7 +726,7 @@ void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
 
 template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false, int kWN = 2>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
-  const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN) * a.split_k;
   // f32 64x64: two register stages when the K loop is long enough and there is no prologue (the prologue
   // variant drops to 3 waves/SIMD at depth 2); r2_convdepth A/B: 2615-2623 -> 2536-2541 us over the 14
   // shapes, the short-K layers (C=64/256 1x1) a little slower. SML_CONV_DEPTH=1/2 forces one.
@@ -684,18 +748,32 @@ void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
 
-template <class T, int kSplit = 0, bool kWPre = false>
-int Launch(const ConvArgs& a, hipStream_t st) {
-  const int M = a.B * a.OH * a.OW;
-  // SML_CONV_TILE=BMxBN forces one register-staged tile shape for the process (tuning sweeps);
-  // ConvArgs::kernel forces a kernel per call (tests)
-  static const int env_tile = [] {
+int EnvTile() {
+  static const int t = [] {
     const char* e = std::getenv("SML_CONV_TILE");
     if (!e) return 0;
     const int bm = std::atoi(e);
     const char* x = std::strchr(e, 'x');
     return x ? bm * 1000 + std::atoi(x + 1) : 0;
   }();
+  return t;
+}
+
+bool EnvGlds() {
+  static const bool g = [] {
+    const char* e = std::getenv("SML_CONV_GLDS");
+    return e && std::atoi(e) != 0;
+  }();
+  return g;
+}
+
+template <class T, int kSplit = 0, bool kWPre = false>
+int Launch(const ConvArgs& a, hipStream_t st) {
+  const int M = a.B * a.OH * a.OW;
+  // SML_CONV_TILE=BMxBN forces one register-staged tile shape for the process (tuning sweeps);
+  // ConvArgs::kernel forces a kernel per call (tests)
+  const int env_tile = EnvTile();
+  if (a.split_k > 1 && (a.kernel || env_tile || !a.ws || !a.ws_cnt)) return -6;  // split-K: planned tiles only
   switch (a.kernel ? a.kernel : env_tile) {
     case 64064: LaunchTile<T, 64, 64, kThreads, kSplit, kWPre>(a, M, st); return 0;
     case 128064: LaunchTile<T, 128, 64, kThreads, kSplit, kWPre>(a, M, st); return 0;
@@ -707,7 +785,7 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 64777:
     case 256777:
       if constexpr (sizeof(T) == 2 && kSplit == 0) {
-        if (a.in_scale) return -4;
+        if (a.in_scale || a.split_k != 1) return -4;
         const int code = a.kernel ? a.kernel : env_tile;
         if (code == 128777) LaunchGlds<T, 128, 128, 512>(a, M, st);
         else if (code == 64777) LaunchGlds<T, 64, 64, 256>(a, M, st);
@@ -753,12 +831,8 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     return 0;
   }
   // SML_CONV_GLDS=1: the LDS-DMA staged forms for the layers without a prologue (A/B switch)
-  static const bool glds = [] {
-    const char* e = std::getenv("SML_CONV_GLDS");
-    return e && std::atoi(e) != 0;
-  }();
   if constexpr (sizeof(T) == 2) {
-    if (glds && !a.in_scale) {
+    if (EnvGlds() && !a.in_scale && a.split_k == 1) {
       if (a.Cout <= 64) LaunchGlds<T, 64, 64, 256>(a, M, st);
       else LaunchGlds<T, 128, 128, 512>(a, M, st);
       return 0;
@@ -793,8 +867,41 @@ bool ConvMfmaSupported(int C, int Cout, int groups, int dtype) {
   return groups == 1 && C > 0 && C % bk == 0 && Cout > 0 && dtype >= 0 && dtype <= 6;
 }
 
+// Split-K for the default tiles when the output has too few tiles to give every CU two blocks (the deep
+// ResNet layers: 7x7 / 14x14 maps at batch 128 make 196-392 tiles of 128x128 for 256 CUs) and the K loop is
+// long: up to 8 splits of >= 4 K tiles each, aiming at >= 512 blocks. SML_CONV_SPLITK=0 disables, =N forces N.
+int ConvSplitPlan(const ConvArgs& a, int dtype, int64_t* ws_floats, int* counters) {
+  *ws_floats = 0;
+  *counters = 0;
+  if (a.kernel != 0 || EnvTile() != 0 || dtype < 0 || dtype > 6 || !ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return 1;
+  const bool half = dtype == 1 || dtype == 2;
+  if (half && EnvGlds() && !a.in_scale) return 1;
+  int bm = 128, bn = 128;
+  if (dtype == 0 || a.Cout <= 64) bm = bn = 64;
+  const int M = a.B * a.OH * a.OW;
+  const int64_t tiles = static_cast<int64_t>((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn);
+  const int nk = a.R * a.S * a.C / (half ? 64 : 32);
+  static const int env = [] {
+    const char* e = std::getenv("SML_CONV_SPLITK");
+    return e ? std::atoi(e) : -1;
+  }();
+  int sk = 1;
+  if (env >= 0) {
+    sk = std::max(1, std::min(env, nk));
+  } else if (tiles < 512 && nk >= 8) {
+    sk = static_cast<int>(std::min<int64_t>({(512 + tiles - 1) / tiles, nk / 4, 8}));
+  }
+  if (sk > 1) {
+    *ws_floats = tiles * sk * bm * bn;
+    *counters = static_cast<int>(tiles);
+  }
+  return std::max(sk, 1);
+}
+
 int ConvMfma(const ConvArgs& a, int dtype, void* stream) {
+  if (a.split_k < 1) return -6;
   if (a.kernel == kConvStem) {  // packed few-channel stem: C = 4, 8 x 8 taps, f16/bf16, no prologue
+    if (a.split_k != 1) return -6;
     if (a.C != 4 || a.R != 8 || a.S != 8 || (dtype != 1 && dtype != 2) || a.in_scale || a.dil_h != 1 || a.dil_w != 1)
       return -1;
     if (a.OH <= 0 || a.OW <= 0 || a.B <= 0) return -2;

@@ -44,18 +44,32 @@ PYBIND11_MODULE(_nn, m) {
   m.def("conv_supported", &ConvMfmaSupported);
   m.def("conv_mfma", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale, uintptr_t in_shift,
                         uintptr_t bias, uintptr_t res, uintptr_t out_scale, uintptr_t out_shift, uintptr_t y2,
-                        std::vector<int> g, int relu, int prologue_relu, int dtype, uintptr_t stream, int kernel) {
+                        std::vector<int> g, int relu, int prologue_relu, int dtype, uintptr_t stream, int kernel,
+                        int split_k, uintptr_t ws, uintptr_t ws_cnt) {
     if (g.size() != 15) throw std::invalid_argument("geometry: B,H,W,C,Cout,R,S,sh,sw,ph,pw,dh,dw,OH,OW");
     ConvArgs a{P<const void>(x), P<const void>(w), P<void>(y), P<const float>(in_scale), P<const float>(in_shift),
                P<const float>(bias), P<const void>(res), P<const float>(out_scale), P<const float>(out_shift),
                P<void>(y2), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13],
-               g[14], relu, prologue_relu, kernel};
+               g[14], relu, prologue_relu, kernel, split_k, P<float>(ws), P<int>(ws_cnt)};
     const int rc = ConvMfma(a, dtype, P<void>(stream));
     if (rc != 0) throw std::runtime_error("conv_mfma failed (rc=" + std::to_string(rc) + ")");
   }, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("in_scale"), pybind11::arg("in_shift"),
      pybind11::arg("bias"), pybind11::arg("res"), pybind11::arg("out_scale"), pybind11::arg("out_shift"),
      pybind11::arg("y2"), pybind11::arg("geom"), pybind11::arg("relu"), pybind11::arg("prologue_relu"),
-     pybind11::arg("dtype"), pybind11::arg("stream"), pybind11::arg("kernel") = 0);
+     pybind11::arg("dtype"), pybind11::arg("stream"), pybind11::arg("kernel") = 0, pybind11::arg("split_k") = 1,
+     pybind11::arg("ws") = 0, pybind11::arg("ws_cnt") = 0);
+  // split-K plan of the default tile: (splits, workspace fp32 floats, int32 counters)
+  m.def("conv_split_plan", [](std::vector<int> g, int dtype, bool has_prologue, int kernel) {
+    if (g.size() != 15) throw std::invalid_argument("geometry: B,H,W,C,Cout,R,S,sh,sw,ph,pw,dh,dw,OH,OW");
+    static const float dummy = 0.f;
+    ConvArgs a{nullptr, nullptr, nullptr, has_prologue ? &dummy : nullptr, nullptr, nullptr, nullptr, nullptr,
+               nullptr, nullptr, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13],
+               g[14], 0, 0, kernel};
+    int64_t wsf = 0;
+    int cnt = 0;
+    const int sk = ConvSplitPlan(a, dtype, &wsf, &cnt);
+    return pybind11::make_tuple(sk, wsf, cnt);
+  }, pybind11::arg("geom"), pybind11::arg("dtype"), pybind11::arg("has_prologue"), pybind11::arg("kernel") = 0);
   // conv: [] or [H, W, C, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, OH, OW] (implicit im2col A)
   m.def("gemm", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int batch, int64_t lda, int64_t ldb,
                    int64_t ldc, int64_t sa, int64_t sb, int64_t sc, int trans_a, int trans_b, float alpha, float beta,

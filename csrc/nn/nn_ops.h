@@ -36,10 +36,18 @@ struct ConvArgs {
   int prologue_relu;   // relu after the prologue affine
   int kernel = 0;      // 0 picks the tile by shape; BM*1000+BN forces one (64064, 128064, 64128,
                        // 128128, 256128, 128256)
+  // split-K (ConvSplitPlan): split_k > 1 K ranges per output tile, fp32 partial tiles in ws, one arrival
+  // counter per tile in ws_cnt (zeroed before the launch); the last arriving split sums and runs the epilogue
+  int split_k = 1;
+  float* ws = nullptr;
+  int* ws_cnt = nullptr;
 };
 constexpr int kConvStem = 1;  // ConvArgs::kernel: the packed few-channel stem form (C = 4, R = S = 8)
 bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);
 int ConvMfma(const ConvArgs& a, int dtype, void* stream);
+// split-K plan of the tile ConvMfma would pick for a (kernel = 0 only): the number of K splits (1: none) and
+// the workspace it needs (fp32 floats, int32 tile counters)
+int ConvSplitPlan(const ConvArgs& a, int dtype, int64_t* ws_floats, int* counters);
 // K17: batched GEMM with fused epilogue (gemm_mfma.hip), dtype 0 fp32 / 1 fp16 / 2 bf16:
 //   C[b] = act(alpha * op(A[b]) * op(B[b]) + beta * (bias[n] | Cin[b]))
 // op(A) is [M][K] (trans_a = 0, lda >= K) or A stored [K][M] (trans_a = 1, lda >= M);

@@ -109,11 +109,19 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
                 or not w_planes.is_contiguous()):
             raise ValueError(f"w_planes must be [{_PLANES[mode]}, {cout}, {r}, {s}, {C}] bf16 contiguous")
         dt, wptr = dt + 2, w_planes.data_ptr()
-    native.load("_nn").conv_mfma(
+    nn = native.load("_nn")
+    # split-K (deep layers with few output tiles): fp32 partial tiles + per-tile arrival counters, allocated
+    # stream-ordered from the caching allocator (so concurrent streams and graph capture each get their own)
+    sk, ws_floats, n_cnt = nn.conv_split_plan(geom, dt, in_affine is not None, int(kernel))
+    ws = cnt = None
+    if sk > 1:
+        ws = torch.empty(ws_floats, device=x.device, dtype=torch.float32)
+        cnt = torch.zeros(n_cnt, device=x.device, dtype=torch.int32)
+    nn.conv_mfma(
         x.data_ptr(), wptr, y.data_ptr(), _ptr(in_affine[0] if in_affine else None),
         _ptr(in_affine[1] if in_affine else None), _ptr(bias), _ptr(res), _ptr(out_affine[0] if out_affine else None),
         _ptr(out_affine[1] if out_affine else None), _ptr(y2), geom, int(relu), int(in_relu), dt,
-        torch.cuda.current_stream(x.device).cuda_stream, int(kernel))
+        torch.cuda.current_stream(x.device).cuda_stream, int(kernel), int(sk), _ptr(ws), _ptr(cnt))
     return (y, y2) if out_affine is not None else y
 
 

@@ -96,6 +96,41 @@ def test_prologue_residual_dual_output():
     torch.testing.assert_close(y3.float(), r3, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("dtype,mode", [(torch.float16, None), (torch.bfloat16, None), (torch.float32, "bf16x6"),
+                                        (torch.float32, "bf16x3")])
+@pytest.mark.parametrize("shape", [(2, 512, 7, 7, 512, 3), (1, 1024, 14, 14, 256, 1), (3, 256, 9, 11, 200, 3)])
+def test_split_k_fused_epilogue(dtype, mode, shape):
+    """Split-K (few output tiles, long K): partial fp32 tiles + arrival counters, the last split sums in split
+    order and runs the fused prologue / bias / ReLU / residual / dual-output epilogue."""
+    from synapseml_amd.ops import native
+    from synapseml_amd.ops.conv import F32_MODES, conv2d_nhwc, pack_weight, out_hw
+
+    B, C, H, W, Co, k = shape
+    pd = k // 2
+    oh, ow = out_hw(H, W, k, k, (1, 1), (pd, pd), (1, 1))
+    geom = [B, H, W, C, Co, k, k, 1, 1, pd, pd, 1, 1, oh, ow]
+    dt_code = F32_MODES[mode] if mode else {torch.float16: 1, torch.bfloat16: 2}[dtype]
+    sk, _, _ = native.load("_nn").conv_split_plan(geom, dt_code, True)
+    assert sk > 1
+    torch.manual_seed(3)
+    x = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)
+    pro = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1)
+    bias = torch.randn(Co, device="cuda")
+    res = torch.randn(B, Co, oh, ow, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    post = (torch.rand(Co, device="cuda") + 0.5, torch.randn(Co, device="cuda") * 0.1)
+    y, y2 = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (1, 1), (pd, pd), bias=bias, relu=True, in_affine=pro,
+                        res=res, out_affine=post, f32_mode=mode)
+    ry, ry2 = _ref(x, w, 1, pd, bias=bias, relu=True, pro=pro, res=res, post=post)
+    tol = {torch.float16: 2e-2, torch.bfloat16: 8e-2, torch.float32: 2e-3}[dtype]
+    torch.testing.assert_close(y.float(), ry, rtol=tol, atol=tol)
+    torch.testing.assert_close(y2.float(), ry2, rtol=tol, atol=1.5 * tol)
+    # repeated calls reuse the caching allocator's workspace: same result (summation order fixed per split)
+    y_again, _ = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (1, 1), (pd, pd), bias=bias, relu=True, in_affine=pro,
+                             res=res, out_affine=post, f32_mode=mode)
+    assert torch.equal(y, y_again)
+
+
 # ---------------------------------------------------------------- fp32 (exact f32-input 16x16x4 MFMA)
 F32_KERNELS = [0, 64064, 64999, 128064, 64128, 128128]
 
