@@ -14,18 +14,3 @@ timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread t
 rc=$?
 [ $rc -gt 1 ] && exit $rc
 timeout -k 10 300 python tools/bench_transform.py > "$OUT/bench_transform.log" 2>&1
-rc=$?
-[ $rc -gt 1 ] && exit $rc
-timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_conv_mfma.py > "$OUT/pytest_conv.log" 2>&1
-rc=$?
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_default.log" 2>&1 || exit 1
-SML_CONV_TILE=256x64 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_256x64.log" 2>&1 || exit 1
-SML_CONV_TILE=128x164 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_128x64w2.log" 2>&1 || exit 1
-SML_CONV_TILE=128x777 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_glds128.log" 2>&1 || exit 1
-SML_CONV_TILE=64x777 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_glds64.log" 2>&1 || exit 1
-SML_CONV_TILE=256x777 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_glds256x64.log" 2>&1 || exit 1
-SML_CONV_SPLITK=0 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_nosplitk.log" 2>&1 || exit 1
-timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16,fp32 > "$OUT/bench_onnx.log" 2>&1 || exit 1
-SML_CONV_SPLITK=0 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_nosplitk.log" 2>&1 || exit 1
-SML_CONV_GLDS=1 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_glds.log" 2>&1 || exit 1
