@@ -16,3 +16,5 @@ SML_CONV_SPLITK=0 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no
 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16,fp32 > "$OUT/bench_onnx.log" 2>&1 || exit 1
 SML_CONV_SPLITK=0 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_nosplitk.log" 2>&1 || exit 1
 SML_CONV_GLDS=1 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_glds.log" 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_onnx" -o onnx -- python3 tools/bench_onnx.py --batches 128 --precisions fp16 --images 0 > "$OUT/prof_onnx.log" 2>&1 || exit 1
