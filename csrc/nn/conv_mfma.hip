@@ -40,6 +40,7 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kBKBytes = 128;  // K extent of a tile row in bytes (8 16-B chunks)
 constexpr int kThreads = 256;
@@ -59,12 +60,18 @@ struct Vec<_Float16> {
   static __device__ __forceinline__ f4 mfma(const h8& a, const h8& b, const f4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
+  static __device__ __forceinline__ f16v mfma32(const h8& a, const h8& b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
 };
 template <>
 struct Vec<__bf16> {
   typedef b8 type;
   static __device__ __forceinline__ f4 mfma(const b8& a, const b8& b, const f4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f16v mfma32(const b8& a, const b8& b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }
 };
 template <>
@@ -79,6 +86,75 @@ __device__ __forceinline__ float ToF(T v) {
 template <class T>
 __device__ __forceinline__ T FromF(float v) {
   return static_cast<T>(v);
+}
+
+// Epilogue part 2, shared by the accumulator layouts: the wave's tile, staged in LDS (Ct, row pitch CL) as T
+// after bias + ReLU, is read back in 16-B row chunks -> residual add, dual output, coalesced 16-B stores.
+template <class T, int WM, int WN, int CL>
+__device__ __forceinline__ void EpilogueStore(const ConvArgs& a, const T* Ct, int M, int m0, int n0, int wm0, int wn0,
+                                              int lane) {
+  T* __restrict__ y = static_cast<T*>(a.y);
+  const T* __restrict__ res = static_cast<const T*>(a.res);
+  T* __restrict__ y2 = static_cast<T*>(a.y2);
+  const bool relu_post = a.relu == 2 && res != nullptr;
+  constexpr int EPV = Tile<T>::EPV;
+  constexpr int CPR = WN / EPV;
+#pragma unroll
+  for (int it = 0; it < WM * CPR / 64; ++it) {
+    const int idx = it * 64 + lane;
+    const int row = idx / CPR, ch = idx % CPR;
+    const int m = m0 + wm0 + row, n = n0 + wn0 + ch * EPV;
+    if (m >= M || n >= a.Cout) continue;
+    uint4 pv = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * EPV);
+    const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
+    if (res) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(res + o);
+      T* pe = reinterpret_cast<T*>(&pv);
+      const T* re = reinterpret_cast<const T*>(&rv);
+#pragma unroll
+      for (int e = 0; e < EPV; ++e) {
+        const float v = ToF(pe[e]) + ToF(re[e]);
+        pe[e] = FromF<T>(relu_post ? fmaxf(v, 0.f) : v);
+      }
+    }
+    *reinterpret_cast<uint4*>(y + o) = pv;
+    if (y2) {
+      uint4 qv;
+      const T* pe = reinterpret_cast<const T*>(&pv);
+      T* qe = reinterpret_cast<T*>(&qv);
+#pragma unroll
+      for (int e = 0; e < EPV; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * a.out_scale[n + e] + a.out_shift[n + e], 0.f));
+      *reinterpret_cast<uint4*>(y2 + o) = qv;
+    }
+  }
+}
+
+// Epilogue of the 32x32x16 MFMA layout (Cout % 8 == 0 only): lane holds column (lane & 31) of each 32x32
+// block and rows 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3) in register r; bias + ReLU, staged through LDS.
+template <class T, int WM, int WN, int kWN>
+__device__ __forceinline__ void ConvEpilogue32(const ConvArgs& a, f16v (&acc)[WM / 32][WN / 32], T* lds, int M, int m0,
+                                               int n0, int wid, int lane) {
+  constexpr int TM = WM / 32, TN = WN / 32;
+  const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
+  const bool relu_pre = a.relu == 1 || (a.relu == 2 && a.res == nullptr);
+  constexpr int CL = WN + 8;
+  T* Ct = lds + wid * WM * CL;
+  const int fc = lane & 31, fh = 4 * (lane >> 5);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + j * 32 + fc;
+    const float bn = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = acc[i][j][r] + bn;
+        if (relu_pre) v = fmaxf(v, 0.f);
+        Ct[(i * 32 + 8 * (r >> 2) + fh + (r & 3)) * CL + j * 32 + fc] = FromF<T>(v);
+      }
+  }
+  __syncthreads();
+  EpilogueStore<T, WM, WN, CL>(a, Ct, M, m0, n0, wm0, wn0, lane);
 }
 
 // Epilogue shared by the conv kernels: bias, ReLU, residual add and the optional second output,
@@ -97,7 +173,6 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
   // relu=1: before the residual add; relu=2: after it (identical without a residual)
   const bool relu_pre = a.relu == 1 || (a.relu == 2 && res == nullptr);
   const bool relu_post = a.relu == 2 && res != nullptr;
-  constexpr int EPV = Tile<T>::EPV;
   if ((a.Cout & 7) == 0) {
     // staged row pitch (elements): 144 B for f16/bf16 (WN=64) and 16 B of padding for f32, so the
     // accumulator rows 4 apart that one 32-lane write group touches land on different banks
@@ -117,36 +192,7 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
         }
     }
     __syncthreads();
-    // part 2: 16-B row chunks -> residual add, dual output, coalesced 16-B stores
-    constexpr int CPR = WN / EPV;
-#pragma unroll
-    for (int it = 0; it < WM * CPR / 64; ++it) {
-      const int idx = it * 64 + lane;
-      const int row = idx / CPR, ch = idx % CPR;
-      const int m = m0 + wm0 + row, n = n0 + wn0 + ch * EPV;
-      if (m >= M || n >= a.Cout) continue;
-      uint4 pv = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * EPV);
-      const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
-      if (res) {
-        const uint4 rv = *reinterpret_cast<const uint4*>(res + o);
-        T* pe = reinterpret_cast<T*>(&pv);
-        const T* re = reinterpret_cast<const T*>(&rv);
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) {
-          const float v = ToF(pe[e]) + ToF(re[e]);
-          pe[e] = FromF<T>(relu_post ? fmaxf(v, 0.f) : v);
-        }
-      }
-      *reinterpret_cast<uint4*>(y + o) = pv;
-      if (y2) {
-        uint4 qv;
-        const T* pe = reinterpret_cast<const T*>(&pv);
-        T* qe = reinterpret_cast<T*>(&qv);
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * a.out_scale[n + e] + a.out_shift[n + e], 0.f));
-        *reinterpret_cast<uint4*>(y2 + o) = qv;
-      }
-    }
+    EpilogueStore<T, WM, WN, CL>(a, Ct, M, m0, n0, wm0, wn0, lane);
     return;
   }
   // generic epilogue (Cout not a multiple of 8): element stores straight from the accumulators
@@ -179,11 +225,11 @@ __device__ __forceinline__ void ConvEpilogue(const ConvArgs& a, f4 (&acc)[WM / 1
 // release, then a relaxed agent-scope ticket add) and the split that draws the last ticket acquires, sums
 // the partial tiles in split order (deterministic whatever the arrival order) and returns true to run the
 // epilogue; the others return false.
-template <int TM, int TN, int kThr>
-__device__ __forceinline__ bool SplitKReduce(const ConvArgs& a, f4 (&acc)[TM][TN], unsigned char* smem, int tile,
+template <class V, int TM, int TN, int kThr>
+__device__ __forceinline__ bool SplitKReduce(const ConvArgs& a, V (&acc)[TM][TN], unsigned char* smem, int tile,
                                              int split, int SK, int tid) {
-  constexpr int kTileF4 = kThr * TM * TN;  // f4 per partial tile
-  f4* mine = reinterpret_cast<f4*>(a.ws) + (static_cast<int64_t>(tile) * SK + split) * kTileF4;
+  constexpr int kTileF4 = kThr * TM * TN;  // accumulator vectors per partial tile
+  V* mine = reinterpret_cast<V*>(a.ws) + (static_cast<int64_t>(tile) * SK + split) * kTileF4;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -206,12 +252,12 @@ __device__ __forceinline__ bool SplitKReduce(const ConvArgs& a, f4 (&acc)[TM][TN
   const bool last = *flag != 0;
   __syncthreads();  // the flag's LDS word is reused by the epilogue staging
   if (!last) return false;
-  const f4* base = reinterpret_cast<const f4*>(a.ws) + static_cast<int64_t>(tile) * SK * kTileF4;
+  const V* base = reinterpret_cast<const V*>(a.ws) + static_cast<int64_t>(tile) * SK * kTileF4;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      f4 v = base[(i * TN + j) * kThr + tid];
+      V v = base[(i * TN + j) * kThr + tid];
       for (int s2 = 1; s2 < SK; ++s2) v += base[static_cast<int64_t>(s2) * kTileF4 + (i * TN + j) * kThr + tid];
       acc[i][j] = v;
     }
@@ -233,14 +279,19 @@ __device__ __forceinline__ bool SplitKReduce(const ConvArgs& a, f4 (&acc)[TM][TN
 // kWN: waves along N (2, or 1 for the Cout = 64 tiles whose 64x64 wave tiles halve the LDS fragment reads per
 // MFMA against 32x32 ones: at 32x32 a wave issues one ds_read_b128 per 16-cycle MFMA, which is the LDS array's
 // whole rate with a wave per SIMD)
+// kM32 (f16 / bf16): 32x32x16 MFMAs (16 accumulators per lane per 32x32 block) instead of 16x16x32 - half the
+// MFMA instructions for the same tile, the same LDS fragment bytes per MFMA FLOP
 template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false, int kSplit = 0,
-          bool kWPre = false, int kWN = 2>
+          bool kWPre = false, int kWN = 2, bool kM32 = false>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
   constexpr int kWavesM = kThr / 64 / kWN;        // waves along M
   constexpr int WM = BM / kWavesM, WN = BN / kWN; // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
+  static_assert(!kM32 || (sizeof(T) == 2 && kSplit == 0 && !kStem && WM % 32 == 0 && WN % 32 == 0),
+                "32x32x16 tiles: f16 / bf16, wave tiles in 32s");
+  constexpr int TM32 = kM32 ? WM / 32 : 1, TN32 = kM32 ? WN / 32 : 1;  // 32x32 MFMA blocks per wave (kM32)
   constexpr int AR = BM * kBKBytes / 16 / kThr;  // 16-B A chunks per thread per tile
   constexpr int BR = BN * kBKBytes / 16 / kThr;  // 16-B B chunks per thread per tile
   constexpr int RS = kThr / 8;                  // tile rows covered by one pass of the block
@@ -317,6 +368,15 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  f16v acc32[TM32][TN32];
+  if constexpr (kM32) {
+#pragma unroll
+    for (int i = 0; i < TM32; ++i)
+#pragma unroll
+      for (int j = 0; j < TN32; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  }
 
   const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
   const int fr = lane & 15, fk = EPV * (lane >> 4);
@@ -371,6 +431,23 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][c], bf[j][c], acc[i][j], 0, 0, 0);
+      }
+    } else if constexpr (kM32) {
+      // 16 k per step; lane holds row / column (lane & 31), k = 8 * (lane >> 5) .. + 7 of the step
+      const int f32r = lane & 31, f32k = 8 * (lane >> 5);
+#pragma unroll
+      for (int ks = 0; ks < kBK / 16; ++ks) {
+        V8 af[TM32], bf[TN32];
+#pragma unroll
+        for (int i = 0; i < TM32; ++i)
+          af[i] = *reinterpret_cast<const V8*>(As + (buf * BM + wm0 + i * 32 + f32r) * kLd + ks * 16 + f32k);
+#pragma unroll
+        for (int j = 0; j < TN32; ++j)
+          bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + wn0 + j * 32 + f32r) * kLd + ks * 16 + f32k);
+#pragma unroll
+        for (int i = 0; i < TM32; ++i)
+#pragma unroll
+          for (int j = 0; j < TN32; ++j) acc32[i][j] = Vec<T>::mfma32(af[i], bf[j], acc32[i][j]);
       }
     } else {
 #pragma unroll
@@ -565,8 +642,13 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
-  if (SK > 1 && !SplitKReduce<TM, TN, kThr>(a, acc, smem, tile, split, SK, tid)) return;
-  ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
+  if constexpr (kM32) {
+    if (SK > 1 && !SplitKReduce<f16v, TM32, TN32, kThr>(a, acc32, smem, tile, split, SK, tid)) return;
+    ConvEpilogue32<T, WM, WN, kWN>(a, acc32, lds, M, m0, n0, wid, lane);
+  } else {
+    if (SK > 1 && !SplitKReduce<f4, TM, TN, kThr>(a, acc, smem, tile, split, SK, tid)) return;
+    ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
+  }
 }
 
 // LDS-DMA form (f16 / bf16, no prologue): the A and B tiles go global -> LDS with buffer_load ... lds
@@ -724,7 +806,8 @@ void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
   hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
 }
 
-template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false, int kWN = 2>
+template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false, int kWN = 2,
+          bool kM32 = false>
 void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN) * a.split_k;
   // f32 64x64: two register stages when the K loop is long enough and there is no prologue (the prologue
@@ -743,8 +826,8 @@ void LaunchTile(const ConvArgs& a, int M, hipStream_t st) {
       return;
     }
   }
-  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit, kWPre, kWN>
-                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit, kWPre, kWN>;
+  auto k = a.in_scale ? conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, kSplit, kWPre, kWN, kM32>
+                      : conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, kSplit, kWPre, kWN, kM32>;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(kThr), 0, st, a);
 }
 
@@ -781,6 +864,18 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 128128: LaunchTile<T, 128, 128, kThreads, kSplit, kWPre>(a, M, st); return 0;
     case 128999: LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
     case 64999: LaunchTile<T, 64, 64, 512, kSplit, kWPre>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
+    case 128932:  // 32x32x16 MFMA forms: 128x128 8 waves (32x64), 256x128 8 waves (64x64), 64x64 4 waves (32x32)
+    case 256932:
+    case 64932:
+      if constexpr (sizeof(T) == 2 && kSplit == 0) {
+        if (a.Cout & 7) return -4;
+        const int code = a.kernel ? a.kernel : env_tile;
+        if (code == 128932) LaunchTile<T, 128, 128, 512, 0, false, 2, true>(a, M, st);
+        else if (code == 256932) LaunchTile<T, 256, 128, 512, 0, false, 2, true>(a, M, st);
+        else LaunchTile<T, 64, 64, 256, 0, false, 2, true>(a, M, st);
+        return 0;
+      }
+      return -4;
     case 128777:  // LDS-DMA forms (f16 / bf16 without prologue): 128x128 8 waves, 64x64 4 waves, 256x64 4 waves
     case 64777:
     case 256777:
