@@ -16,8 +16,8 @@
 // 16x16x32 bf16 MFMAs over operands split into 2 or 3 bf16 planes (kSplit: 3 or 6 products per
 // pair; the 6-product form matches the exact f32 MFMA's error and is the fp32 graphs' default). A and B
 // tiles are staged through registers (the prologue is applied there) into a
-// double-buffered LDS image with a 144-byte row pitch (conflict-free 16-lane
-// ds_read_b128 fragment reads); the next tile's global loads are issued before
+// double-buffered LDS image with a 160-byte row pitch (conflict-free ds_read_b128
+// fragment reads; 144 B for the 32x32 forms); the next tile's global loads are issued before
 // the current tile's MFMAs so HBM latency hides behind matrix work. Blocks are
 // remapped so that each XCD owns a contiguous run of (m, n) tiles: the blocks
 // that share an activation tile (all n for one m) sit on one XCD's L2.
@@ -44,12 +44,11 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kBKBytes = 128;  // K extent of a tile row in bytes (8 16-B chunks)
 constexpr int kThreads = 256;
-// per element type: K elements per tile, elements per 16-B chunk, LDS row pitch (16 B of padding)
+// per element type: K elements per tile, elements per 16-B chunk (the LDS row pitch is set per kernel form)
 template <class T>
 struct Tile {
   static constexpr int BK = kBKBytes / static_cast<int>(sizeof(T));
   static constexpr int EPV = 16 / static_cast<int>(sizeof(T));
-  static constexpr int LD = BK + EPV;
 };
 
 template <class T>
@@ -285,7 +284,12 @@ template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 
           bool kWPre = false, int kWN = 2, bool kM32 = false>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
-  constexpr int kBK = Tile<T>::BK, kLd = Tile<T>::LD, EPV = Tile<T>::EPV;
+  constexpr int kBK = Tile<T>::BK, EPV = Tile<T>::EPV;
+  // LDS row pitch: 160 B (32 B of padding) for the 16x16 fragment reads (row lane & 15, 16-B chunk lane >> 4):
+  // under gfx950's ds_read_b128 lane groups ({0-3,12-15,20-27}, ...) a 144-B pitch puts two lanes of every
+  // group on one bank (2-way, the ~32 % conflict cycles of the r2 PMC pass); 160 B is conflict-free. The
+  // 32x32 fragments (row lane & 31, chunk lane >> 5) are conflict-free at 144 B and 2-way at 160 B.
+  constexpr int kLd = kM32 ? kBK + EPV : kBK + 2 * EPV;
   constexpr int kWavesM = kThr / 64 / kWN;        // waves along M
   constexpr int WM = BM / kWavesM, WN = BN / kWN; // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;     // 16x16 MFMA tiles per wave
@@ -296,7 +300,9 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   constexpr int BR = BN * kBKBytes / 16 / kThr;  // 16-B B chunks per thread per tile
   constexpr int RS = kThr / 8;                  // tile rows covered by one pass of the block
   static_assert(kSplit == 0 || sizeof(T) == 4, "bf16 operand splitting is an f32 mode");
-  constexpr int kLdB = kBK + 8;                 // split planes: bf16 row pitch (80 B: conflict-free b128 reads)
+  // split planes: bf16 row pitch - 96 B is conflict-free for the 16x16 fragment reads (80 B is 2-way); the
+  // 2-plane form keeps 80 B so that its 128x128 tile still fits two blocks per CU
+  constexpr int kLdB = kSplit == 3 ? kBK + 16 : kBK + 8;
   constexpr int kOpBytes = kSplit ? 2 * kSplit * (BM + BN) * kLdB * 2 : 2 * (BM + BN) * kLd * static_cast<int>(sizeof(T));
   // the epilogue re-uses the operand buffers to stage each wave's tile
   constexpr int kEpiBytes = (kThr / 64) * WM * (WN + 8) * static_cast<int>(sizeof(T));

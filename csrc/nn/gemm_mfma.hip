@@ -41,7 +41,8 @@ template <class T>
 struct GTile {
   static constexpr int BK = 128 / static_cast<int>(sizeof(T));  // K elements per tile (128 B per row)
   static constexpr int EPV = 16 / static_cast<int>(sizeof(T));  // elements per 16-B chunk
-  static constexpr int LD = BK + EPV;                            // LDS row pitch (+16 B)
+  static constexpr int LD = BK + 2 * EPV;  // LDS row pitch (+32 B: 160 B rows are bank-conflict-free for the
+                                          // 16x16 fragment reads under gfx950's ds_read_b128 lane groups; 144 B is 2-way)
 };
 
 template <class T>

@@ -3,7 +3,7 @@
 # form, ResNet-50 session A/B (split-K, LDS-DMA). Usage: tools/gpu_r4_conv.sh OUTDIR
 OUT=${1:-gpurun_out/r4conv}
 mkdir -p "$OUT"
-timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_conv_mfma.py > "$OUT/pytest_conv.log" 2>&1
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_conv_mfma.py tests/test_gemm_gpu.py > "$OUT/pytest_conv.log" 2>&1
 rc=$?
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_default.log" 2>&1 || exit 1
