@@ -280,8 +280,11 @@ __device__ __forceinline__ bool SplitKReduce(const ConvArgs& a, V (&acc)[TM][TN]
 // whole rate with a wave per SIMD)
 // kM32 (f16 / bf16): 32x32x16 MFMAs (16 accumulators per lane per 32x32 block) instead of 16x16x32 - half the
 // MFMA instructions for the same tile, the same LDS fragment bytes per MFMA FLOP
+// kPersist: a grid of about one wave of resident blocks, each walking tiles q = blockIdx.x, + gridDim.x, ...;
+// the next tile's first K-tile loads are issued before the current tile's epilogue, so the short-K layers
+// (a 1x1 conv over 64-256 channels is one to four K tiles) keep HBM reads in flight behind their stores.
 template <class T, int BM, int BN, bool kPro, int kThr = kThreads, int kDepth = 1, bool kStem = false, int kSplit = 0,
-          bool kWPre = false, int kWN = 2, bool kM32 = false>
+          bool kWPre = false, int kWN = 2, bool kM32 = false, bool kPersist = false>
 __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kBK = Tile<T>::BK, EPV = Tile<T>::EPV;
@@ -319,15 +322,22 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   const int K = a.R * a.S * a.C;
   const int tiles_n = (a.Cout + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int SK = kStem ? 1 : a.split_k;  // K splits per tile (a tile's splits are adjacent block ids)
+  static_assert(!kPersist || (!kStem && kDepth == 1), "persistent form: register-staged, one stage");
+  const int SK = (kStem || kPersist) ? 1 : a.split_k;  // K splits per tile (a tile's splits are adjacent block ids)
   const int total = tiles_m * tiles_n * SK;
-  int bid = blockIdx.x;
-  if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
-  const int split = bid % SK;
-  bid /= SK;
-  const int tile = bid;
-  const int tn = bid % tiles_n, tm = bid / tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int split = 0, tile = 0, m0 = 0, n0 = 0;
+  auto decode = [&](int q) {
+    int bid = q;
+    if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);  // XCD-contiguous tile runs
+    split = bid % SK;
+    bid /= SK;
+    tile = bid;
+    m0 = (bid / tiles_n) * BM;
+    n0 = (bid % tiles_n) * BN;
+  };
+  int q = blockIdx.x;
+  if (kPersist && q >= total) return;
+  decode(q);
 
   // Operands are read through buffer resources: a lane whose tap falls in the padding (or whose row
   // is past M / channel past Cout) gets an out-of-range offset and the hardware returns zeros, so the
@@ -337,6 +347,9 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   constexpr uint32_t kOob = 0x80000000u;
   int abase[AR];       // element offset of the row's window origin (tap 0, channel kc*8)
   uint64_t amask[AR];  // bit t: tap t = r*S + s is inside the input
+  uint32_t boff[BR];   // byte offset of the thread's weight row chunk (out of range past Cout)
+  constexpr int kWElem = kWPre ? 2 : static_cast<int>(sizeof(T));  // bytes per weight element (per plane)
+  auto setup_rows = [&]() {
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int m = m0 + (tid >> 3) + RS * i;
@@ -354,35 +367,37 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
         }
     amask[i] = mk;
   }
-  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(a.x), 0, a.B * a.H * a.W * a.C * static_cast<int>(sizeof(T)), 0x00020000);
-  constexpr int kWElem = kWPre ? 2 : static_cast<int>(sizeof(T));  // bytes per weight element (per plane)
-  const int wplane = a.Cout * K * kWElem;                             // bytes of one weight plane
-  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(a.w), 0, wplane * (kWPre ? kSplit : 1), 0x00020000);
-  uint32_t boff[BR];  // byte offset of the thread's weight row chunk (out of range past Cout)
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int n = n0 + (tid >> 3) + RS * i;
     boff[i] = n < a.Cout ? static_cast<uint32_t>((n * K + kc * EPV) * kWElem) : kOob;
   }
+  };
+  setup_rows();
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, a.B * a.H * a.W * a.C * static_cast<int>(sizeof(T)), 0x00020000);
+  const int wplane = a.Cout * K * kWElem;                             // bytes of one weight plane
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.w), 0, wplane * (kWPre ? kSplit : 1), 0x00020000);
   constexpr bool pro = kPro;  // prologue affine present (a.in_scale != nullptr): a template
                               // parameter, so no runtime branch sits between loads and their use
 
   f4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   f16v acc32[TM32][TN32];
-  if constexpr (kM32) {
+  auto zero_acc = [&]() {
 #pragma unroll
-    for (int i = 0; i < TM32; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN32; ++j)
+      for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (kM32) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
-  }
+      for (int i = 0; i < TM32; ++i)
+#pragma unroll
+        for (int j = 0; j < TN32; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+    }
+  };
 
   const int wm0 = (wid / kWN) * WM, wn0 = (wid % kWN) * WN;
   const int fr = lane & 15, fk = EPV * (lane >> 4);
@@ -486,14 +501,18 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   };
   // next tile to load: tap (lr, ls) = index lt, channel offset lc0, element offset of the tap toff
   int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0, loaded = 0;
-  if (kt0 > 0) {  // a later split starts inside the (tap, channel) walk
-    lk0 = kt0 * kBK;
-    lt = lk0 / a.C;
-    lc0 = lk0 - lt * a.C;
-    lr = lt / a.S;
-    ls = lt - lr * a.S;
-    toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
-  }
+  auto reset_taps = [&]() {
+    lt = lr = ls = lc0 = lk0 = toff = loaded = 0;
+    if (kt0 > 0) {  // a later split starts inside the (tap, channel) walk
+      lk0 = kt0 * kBK;
+      lt = lk0 / a.C;
+      lc0 = lk0 - lt * a.C;
+      lr = lt / a.S;
+      ls = lt - lr * a.S;
+      toff = (lr * a.dil_h * a.W + ls * a.dil_w) * a.C;
+    }
+  };
+  reset_taps();
   auto load_tile = [&](Stage& st) {
     st.okm = 0;
     if constexpr (kStem) {
@@ -621,6 +640,8 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   };
   Stage s0;
   load_tile(s0);
+  for (;;) {  // one pass unless kPersist
+  zero_acc();
   store_tile(0, s0);
   if constexpr (kDepth == 2) {
     Stage s1;
@@ -648,12 +669,27 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
+  const int em0 = m0, en0 = n0;  // this tile's origin (the prefetch below moves to the next tile)
+  int qn = total;
+  if constexpr (kPersist) {
+    qn = q + static_cast<int>(gridDim.x);
+    if (qn < total) {  // next tile's first K-tile loads in flight behind this tile's epilogue
+      decode(qn);
+      setup_rows();
+      reset_taps();
+      load_tile(s0);
+    }
+  }
   if constexpr (kM32) {
     if (SK > 1 && !SplitKReduce<f16v, TM32, TN32, kThr>(a, acc32, smem, tile, split, SK, tid)) return;
-    ConvEpilogue32<T, WM, WN, kWN>(a, acc32, lds, M, m0, n0, wid, lane);
+    ConvEpilogue32<T, WM, WN, kWN>(a, acc32, lds, M, em0, en0, wid, lane);
   } else {
     if (SK > 1 && !SplitKReduce<f4, TM, TN, kThr>(a, acc, smem, tile, split, SK, tid)) return;
-    ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
+    ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, em0, en0, wid, lane);
+  }
+  if (!kPersist || qn >= total) break;
+  q = qn;
+  __syncthreads();  // the epilogue's LDS staging is read before the next tile's operands land there
   }
 }
 
@@ -806,6 +842,27 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
+// persistent form: about one wave of resident blocks (occupancy x CUs), each walking tiles with the next
+// tile's loads overlapped with the current epilogue
+template <class T, int BM, int BN, int kThr>
+void LaunchPersist(const ConvArgs& a, int M, hipStream_t st) {
+  const int total = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  auto kp = conv_mfma_kernel<T, BM, BN, true, kThr, 1, false, 0, false, 2, false, true>;
+  auto kn = conv_mfma_kernel<T, BM, BN, false, kThr, 1, false, 0, false, 2, false, true>;
+  auto resident = [](decltype(kp) k) {
+    int dev = 0, ncu = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThr, 0) != hipSuccess || nb < 1) nb = 1;
+    return nb * ncu;
+  };
+  static const int res_p = resident(kp), res_n = resident(kn);
+  auto k = a.in_scale ? kp : kn;
+  const int res = a.in_scale ? res_p : res_n;
+  const int grid = total < res ? total : res;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kThr), 0, st, a);
+}
+
 template <class T, int BM, int BN, int kThr, int kWN = 2>
 void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
@@ -848,6 +905,14 @@ int EnvTile() {
   return t;
 }
 
+bool EnvPersist() {
+  static const bool p = [] {
+    const char* e = std::getenv("SML_CONV_PERSIST");
+    return e && std::atoi(e) != 0;
+  }();
+  return p;
+}
+
 bool EnvGlds() {
   static const bool g = [] {
     const char* e = std::getenv("SML_CONV_GLDS");
@@ -870,6 +935,15 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 128128: LaunchTile<T, 128, 128, kThreads, kSplit, kWPre>(a, M, st); return 0;
     case 128999: LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st); return 0;  // 128x128, 8 waves (4x2, 32x64 each)
     case 64999: LaunchTile<T, 64, 64, 512, kSplit, kWPre>(a, M, st); return 0;     // 64x64, 8 waves (4x2, 16x32 each)
+    case 128555:  // persistent forms (tile walk, next tile's loads behind the epilogue): 128x128 8 waves, 64x64
+    case 64555:
+      if constexpr (kSplit == 0 && sizeof(T) == 2) {
+        if (a.split_k != 1) return -4;
+        if ((a.kernel ? a.kernel : env_tile) == 128555) LaunchPersist<T, 128, 128, 512>(a, M, st);
+        else LaunchPersist<T, 64, 64, 256>(a, M, st);
+        return 0;
+      }
+      return -4;
     case 128932:  // 32x32x16 MFMA forms: 128x128 8 waves (32x64), 256x128 8 waves (64x64), 64x64 4 waves (32x32)
     case 256932:
     case 64932:
@@ -931,6 +1005,14 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     else LaunchTile<T, 128, 128, 512, kSplit, kWPre>(a, M, st);
     return 0;
   }
+  // SML_CONV_PERSIST=1: the persistent forms for the short-K layers (<= 4 K tiles; A/B switch)
+  if constexpr (sizeof(T) == 2) {
+    if (EnvPersist() && a.split_k == 1 && a.R * a.S * a.C <= 4 * Tile<T>::BK) {
+      if (a.Cout <= 64) LaunchPersist<T, 64, 64, 256>(a, M, st);
+      else LaunchPersist<T, 128, 128, 512>(a, M, st);
+      return 0;
+    }
+  }
   // SML_CONV_GLDS=1: the LDS-DMA staged forms for the layers without a prologue (A/B switch)
   if constexpr (sizeof(T) == 2) {
     if (EnvGlds() && !a.in_scale && a.split_k == 1) {
@@ -977,6 +1059,7 @@ int ConvSplitPlan(const ConvArgs& a, int dtype, int64_t* ws_floats, int* counter
   if (a.kernel != 0 || EnvTile() != 0 || dtype < 0 || dtype > 6 || !ConvMfmaSupported(a.C, a.Cout, 1, dtype)) return 1;
   const bool half = dtype == 1 || dtype == 2;
   if (half && EnvGlds() && !a.in_scale) return 1;
+  if (half && EnvPersist() && a.R * a.S * a.C <= 4 * 64) return 1;
   int bm = 128, bn = 128;
   if (dtype == 0 || a.Cout <= 64) bm = bn = 64;
   const int M = a.B * a.OH * a.OW;

@@ -26,8 +26,9 @@ def _ref(x, w, stride, pad, bias=None, relu=False, pro=None, res=None, post=None
 # 128164: 256x64 / 128x64 with one wave along N, 64x64 wave tiles; 128777 / 64777 / 256777: the LDS-DMA
 # staged 128x128 (8 waves) / 64x64 / 256x64 forms, swizzled unpadded LDS rows)
 # 128932 / 256932 / 64932: 32x32x16 MFMA forms of 128x128 (8 waves) / 256x128 (8 waves) / 64x64 (4 waves)
+# 128555 / 64555: persistent tile walk (next tile's loads behind the epilogue)
 KERNELS = [0, 64064, 64999, 128064, 64128, 128128, 128999, 256128, 128256, 256064, 128164, 128777, 64777, 256777,
-           128932, 256932, 64932]
+           128932, 256932, 64932, 128555, 64555]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -65,7 +66,8 @@ def test_conv_matches_fp32_reference(dtype, shape):
     bias = torch.randn(Co, device="cuda")
     ref, _ = _ref(x, w, st, pd, bias=bias, relu=True)
     tol = 2e-2 if dtype == torch.float16 else 8e-2
-    for kernel in (0, 128128, 128999, 256128, 128256, 256064, 128164, 128777, 64777, 256777, 128932, 256932, 64932):
+    for kernel in (0, 128128, 128999, 256128, 128256, 256064, 128164, 128777, 64777, 256777, 128932, 256932, 64932,
+                   128555, 64555):
         y = conv2d_nhwc(x, pack_weight(w, dtype), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
         torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: f"kernel {kernel}: {m}")
 
@@ -86,7 +88,7 @@ def test_prologue_residual_dual_output():
     torch.testing.assert_close(y.float(), ry, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(y2.float(), ry2, rtol=2e-2, atol=3e-2)
     # the same through the 8-wave 256x128 tile and the 32x32x16 MFMA forms
-    for kernel in (256128, 128932, 256932, 64932):
+    for kernel in (256128, 128932, 256932, 64932, 128555, 64555):
         yq, yq2 = conv2d_nhwc(x, pack_weight(w, dt), 1, 1, in_affine=pro, res=res, out_affine=post, kernel=kernel)
         torch.testing.assert_close(yq.float(), ry, rtol=2e-2, atol=2e-2)
         torch.testing.assert_close(yq2.float(), ry2, rtol=2e-2, atol=3e-2)

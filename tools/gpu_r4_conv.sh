@@ -15,9 +15,11 @@ SML_CONV_TILE=256x777 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 
 SML_CONV_TILE=128x932 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_m32_128.log" 2>&1 || exit 1
 SML_CONV_TILE=256x932 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_m32_256x128.log" 2>&1 || exit 1
 SML_CONV_TILE=64x932 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_m32_64.log" 2>&1 || exit 1
+SML_CONV_PERSIST=1 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_persist.log" 2>&1 || exit 1
 SML_CONV_SPLITK=0 timeout -k 10 200 python tools/bench_conv.py --dtype fp16 --no-ref > "$OUT/conv_fp16_nosplitk.log" 2>&1 || exit 1
 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16,fp32 > "$OUT/bench_onnx.log" 2>&1 || exit 1
 SML_CONV_SPLITK=0 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_nosplitk.log" 2>&1 || exit 1
+SML_CONV_PERSIST=1 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_persist.log" 2>&1 || exit 1
 SML_CONV_GLDS=1 timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16 > "$OUT/bench_onnx_glds.log" 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_onnx" -o onnx -- python3 tools/bench_onnx.py --batches 128 --precisions fp16 --images 0 > "$OUT/prof_onnx.log" 2>&1 || exit 1
