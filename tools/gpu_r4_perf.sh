@@ -5,6 +5,9 @@ OUT=${1:-gpurun_out/r4p}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fit" -o fit -- python3 bench.py --steps 2 --warmup 1 > "$OUT/prof_fit.log" 2>&1 || exit 1
+SML_GBDT_SPEC=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fit_seq" -o fit -- python3 bench.py --steps 2 --warmup 1 > "$OUT/prof_fit_seq.log" 2>&1 || exit 1
+python3 tools/prof_tree_breakdown.py "$(find "$OUT/prof_fit" -name '*kernel_trace.csv' -print -quit)" > "$OUT/tree_breakdown_batched.txt" 2>&1
+python3 tools/prof_tree_breakdown.py "$(find "$OUT/prof_fit_seq" -name '*kernel_trace.csv' -print -quit)" > "$OUT/tree_breakdown_sequential.txt" 2>&1
 timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker.log" 2>&1 || exit 1
 timeout -k 10 400 python tools/bench_vw.py --steps 2 --warmup 1 > "$OUT/bench_vw_estimator.log" 2>&1 || exit 1
 timeout -k 10 300 python tools/bench_conv.py --dtype fp16 > "$OUT/conv_fp16_roofline.log" 2>&1 || exit 1

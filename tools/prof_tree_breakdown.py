@@ -47,3 +47,25 @@ for t in trees[:-1]:
 allg.sort()
 print('gap count per tree', len(allg)/ (len(trees)-1), 'median', statistics.median(allg), 'p90', allg[int(.9*len(allg))], 'sum<50us per tree', sum(g for g in allg if g<50)/(len(trees)-1))
 big=[g for g in allg if g>=50]; print('big gaps', len(big), sum(big)/(len(trees)-1))
+# batched speculative growth (round 4): per-round kernel times by round position within the tree
+bnames = ('bplan_kernel', 'bpart_kernel', 'bhist_kernel', 'breduce_kernel', 'bfind_kernel')
+rpos = collections.defaultdict(lambda: collections.defaultdict(list))
+nrounds = []
+for t in trees:
+    cnt = collections.Counter()
+    for n, d, s, e in t:
+        for b in bnames:
+            if n.startswith(b):
+                rpos[b][cnt[b]].append(d)
+                cnt[b] += 1
+    if cnt['bplan_kernel']:
+        nrounds.append(cnt['bplan_kernel'])
+if nrounds:
+    print('batched growth: plan launches per tree avg %.2f (min %d max %d)' % (sum(nrounds) / len(nrounds), min(nrounds), max(nrounds)))
+    print('round  ' + ' '.join(f'{b[:-7]:>9s}' for b in bnames) + '   (us, mean over trees)')
+    for r in range(max(nrounds)):
+        cells = []
+        for b in bnames:
+            v = rpos[b].get(r)
+            cells.append(f'{sum(v) / len(v) / 1e3:9.1f}' if v else f'{"-":>9s}')
+        print(f'{r:5d}  ' + ' '.join(cells))
