@@ -7,7 +7,7 @@ SML_GBDT_SPEC=0 timeout -k 10 200 python bench.py --steps 3 --warmup 1 > "$OUT/b
 timeout -k 10 400 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_vw_gpu.py > "$OUT/pytest_vw.log" 2>&1
 rc=$?
 [ $rc -gt 1 ] && exit $rc
-timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gbdt_gpu.py > "$OUT/pytest_gbdt.log" 2>&1
+timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gbdt_gpu.py tests/test_comm_gpu.py > "$OUT/pytest_gbdt.log" 2>&1
 rc=$?
 [ $rc -gt 1 ] && exit $rc
 timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_onnx.py -k "gpu" > "$OUT/pytest_onnx.log" 2>&1
