@@ -549,3 +549,29 @@ def test_gpu_global_average_pool_kernel(dt):
     ref = x.float().mean(dim=(2, 3), keepdim=True)
     tol = 1e-6 if dt == torch.float32 else 1e-2
     torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+
+
+def test_conv_split_k_plan():
+    """Split-K planning (host side of csrc/nn/conv_mfma.hip ConvSplitPlan): the deep few-tile layers of
+    ResNet-50 at batch 128 split K (>= 512 blocks, >= 4 K tiles per split, <= 8 splits), the early
+    many-tile layers and forced tiles do not, and the workspace is one fp32 partial tile per split."""
+    from synapseml_amd.ops import native
+
+    nn = native.load("_nn")
+
+    def plan(C, H, Co, k, B=128, dt=1, kernel=0, pro=False):
+        pd = k // 2
+        g = [B, H, H, C, Co, k, k, 1, 1, pd, pd, 1, 1, H, H]
+        return nn.conv_split_plan(g, dt, pro, kernel)
+
+    assert plan(64, 56, 256, 1) == (1, 0, 0)             # 6272 tiles, one K tile
+    assert plan(256, 14, 256, 3) == (2, 392 * 2 * 128 * 128, 392)
+    assert plan(512, 7, 512, 3) == (3, 196 * 3 * 128 * 128, 196)
+    assert plan(512, 7, 512, 3, kernel=128128)[0] == 1  # forced tiles never split
+    assert plan(512, 7, 2048, 1)[0] == 1                 # 784 tiles
+    sk, wsf, cnt = plan(512, 7, 512, 3, B=1)            # batch 1: 4 tiles, 72 K tiles -> 8 splits
+    assert (sk, cnt) == (8, 4) and wsf == 4 * 8 * 128 * 128
+    sk, wsf, cnt = plan(128, 7, 64, 3, B=1)              # Cout <= 64: 64x64 tiles, 18 K tiles -> 4 splits
+    assert (sk, cnt) == (4, 1) and wsf == 4 * 64 * 64
+    assert plan(64, 7, 64, 1, B=1)[0] == 1               # too short a K loop
+    assert plan(256, 14, 256, 3, dt=4)[0] == 2           # fp32 on bf16 planes: 32-wide K tiles
