@@ -16,7 +16,6 @@ import http.client
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -53,24 +52,40 @@ def main() -> None:
     bodies = [json.dumps({f: float(v) for f, v in zip(fields, row)}).encode() for row in X[:256]]
     srv = serve(pipeline, api="score")
 
-    def client_proc(n, off):
-        """Sequential client in its own process (no GIL sharing with the server)."""
-        import subprocess
-
-        code = (
+    def client_code(n, off):
+        """A sequential client as a program of its own (no GIL shared with the server): prints its
+        latencies and the wall time of its request loop."""
+        return (
             "import http.client, json, sys, time\n"
             f"bodies = {[b.decode() for b in bodies[:64]]!r}\n"
             f"c = http.client.HTTPConnection('{srv.host}', {srv.port})\n"
             "lat = []\n"
+            "t_start = time.perf_counter()\n"
             f"for i in range({n}):\n"
             "    t0 = time.perf_counter()\n"
             f"    c.request('POST', '/score', body=bodies[({off} + i) % len(bodies)].encode(), "
             "headers={'Content-Type': 'application/json'})\n"
             "    r = c.getresponse(); r.read(); assert r.status == 200\n"
             "    lat.append((time.perf_counter() - t0) * 1e3)\n"
-            "print(json.dumps(lat))\n")
-        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout
-        return json.loads(out.strip().splitlines()[-1])
+            "print(json.dumps({'lat': lat, 'wall': time.perf_counter() - t_start}))\n")
+
+    def client_proc(n, off):
+        import subprocess
+
+        out = subprocess.run([sys.executable, "-c", client_code(n, off)], capture_output=True, text=True,
+                             check=True).stdout
+        return json.loads(out.strip().splitlines()[-1])["lat"]
+
+    def client_procs(k, n):
+        """k concurrent client processes of n requests each: (latencies, request-loop wall seconds)"""
+        import subprocess
+
+        ps = [subprocess.Popen([sys.executable, "-c", client_code(n, 13 * j)], stdout=subprocess.PIPE, text=True)
+              for j in range(k)]
+        res = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in ps]
+        if any(p.returncode for p in ps):
+            raise RuntimeError("a serving client failed")
+        return np.concatenate([np.asarray(r["lat"]) for r in res]), max(r["wall"] for r in res)
 
     def client(n, lat, off):
         c = http.client.HTTPConnection(srv.host, srv.port)
@@ -89,18 +104,12 @@ def main() -> None:
         k0 = len(srv.latencies_ms)
         seq = client_proc(a.requests, 7)
         server_side = np.asarray(srv.latencies_ms[k0:])
-        lats = [[] for _ in range(a.clients)]
+        # concurrent clients, each its own process: the throughput is the server's, not the client threads'
+        # share of the server's GIL (r1 ran them as threads of the serving process)
         per = max(1, a.requests // a.clients)
-        th = [threading.Thread(target=client, args=(per, lats[k], k * 13)) for k in range(a.clients)]
-        t0 = time.perf_counter()
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        dt = time.perf_counter() - t0
+        allc, dt = client_procs(a.clients, per)
     finally:
         srv.stop()
-    allc = np.concatenate([np.asarray(x) for x in lats])
     s = np.asarray(seq)
     print(json.dumps({
         "bench": "serving_latency", "model": "LightGBMClassifier 100 trees x 31 leaves, 28 features",
