@@ -187,6 +187,9 @@ class CpuBackend : public TrainBackend {
   void Init(const Dataset* d, const Config& cfg, int K) override {
     d->EnsureHostBins();  // the host learner reads the host bin matrix
     data_ = d; cfg_ = cfg; K_ = K; n_ = d->num_data;
+    if (n_ > static_cast<int64_t>(UINT32_MAX))
+      throw std::runtime_error("the CPU learner indexes rows with 32 bits (at most 4294967295 rows per partition); "
+                               "use more partitions or deviceType=gpu");
     sp_ = MakeSplitParams(cfg);
     score_.assign(static_cast<size_t>(n_) * K, 0.0);
     g_.assign(static_cast<size_t>(n_) * K, 0.f);
@@ -258,7 +261,7 @@ class CpuBackend : public TrainBackend {
     const int* fl = feats.data();
     const int64_t rs = data_->row_stride;
     const uint8_t* bins = data_->bins.data();
-    const int64_t* idx = idx_.data() + leaf.begin;
+    const uint32_t* idx = idx_.data() + leaf.begin;
     const int nt = std::max<int>(1, std::min<int64_t>(nthreads_, cnt / 2048 + 1));
     if (static_cast<int64_t>(ogh_.size()) < 2 * cnt) ogh_.resize(2 * cnt);
     float* og = ogh_.data();
@@ -348,7 +351,7 @@ class CpuBackend : public TrainBackend {
     if (static_cast<int64_t>(part_tmp_.size()) < count) part_tmp_.resize(count);
     if (static_cast<int64_t>(part_flag_.size()) < count) part_flag_.resize(count);
     std::vector<int64_t> nleft(nt + 1, 0);
-    int64_t* idx = idx_.data() + begin;
+    uint32_t* idx = idx_.data() + begin;
     uint8_t* flag = part_flag_.data();
 #pragma omp parallel num_threads(nt)
     {
@@ -371,12 +374,12 @@ class CpuBackend : public TrainBackend {
       for (int i = 0; i < nt; ++i) nleft[i + 1] += nleft[i];
       const int64_t total_left = nleft[nt];
       int64_t lo = nleft[t], ro = total_left + (b - nleft[t]);
-      int64_t* tmp = part_tmp_.data();
+      uint32_t* tmp = part_tmp_.data();
       for (int64_t p = b; p < e; ++p) {
         if (flag[p]) tmp[lo++] = idx[p]; else tmp[ro++] = idx[p];
       }
 #pragma omp barrier
-      std::memcpy(idx + b, tmp + b, sizeof(int64_t) * (e - b));
+      std::memcpy(idx + b, tmp + b, sizeof(uint32_t) * (e - b));
     }
     return nleft[nt];
   }
@@ -559,7 +562,7 @@ class CpuBackend : public TrainBackend {
     Tree tree(L);
     // root
     if (use_bag_) { idx_.assign(bag_.begin(), bag_.end()); }
-    else { idx_.resize(n_); std::iota(idx_.begin(), idx_.end(), 0); }
+    else { idx_.resize(n_); std::iota(idx_.begin(), idx_.end(), 0u); }
     std::vector<LeafInfo> leaves(L);
     std::vector<std::vector<double>> hists(L);
     const float* g = g_.data() + static_cast<size_t>(k) * n_;
@@ -681,7 +684,7 @@ class CpuBackend : public TrainBackend {
     if (use_bag_ || t.num_leaves <= 1) return t;
     const auto t0 = Clock::now();
     double* s = score_.data() + static_cast<size_t>(k) * n_;
-    const int64_t* idx = idx_.data();
+    const uint32_t* idx = idx_.data();
     for (int l = 0; l < t.num_leaves; ++l) {
       const double v = t.leaf_value[l] * shrink;
       const int64_t b = seg_[l].first, e = b + seg_[l].second;
@@ -722,12 +725,12 @@ class CpuBackend : public TrainBackend {
   int64_t n_ = 0;
   std::vector<double> score_;
   std::vector<float> g_, h_;
-  std::vector<int64_t> idx_;
+  std::vector<uint32_t> idx_;  // row indices, grouped by leaf (32-bit: half the bytes the partition moves)
   std::vector<std::pair<int64_t, int64_t>> seg_;  // (begin, count) in idx_ of each leaf of the last tree
   std::vector<std::vector<double>> hloc_;         // per-thread histogram tables (BuildHist)
   int feats_per_slice_ = 32;  // SML_CPU_HIST_FPS (A/B at 1M x 28, 8 threads: 28 -> 2.47 s, 14 -> 2.70, 7 -> 2.99, 1 -> 3.35)
   std::vector<float> ogh_;                        // the leaf's (g, h) in row order (BuildHist)
-  std::vector<int64_t> part_tmp_;                 // partition scratch
+  std::vector<uint32_t> part_tmp_;                // partition scratch
   std::vector<uint8_t> colbins_;                  // bins, column-major (partition decisions)
   std::vector<uint8_t> part_flag_;
   std::vector<int32_t> bag_;
