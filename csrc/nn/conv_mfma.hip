@@ -913,10 +913,13 @@ bool EnvPersist() {
   return p;
 }
 
+// LDS-DMA staging is the default for the f16/bf16 layers without a prologue (r4 per-layer sweep over the 14
+// ResNet-50 shapes: every shape but the 2048->512 1x1 at least as fast as register staging, -10 % in total);
+// SML_CONV_GLDS=0 restores register staging
 bool EnvGlds() {
   static const bool g = [] {
     const char* e = std::getenv("SML_CONV_GLDS");
-    return e && std::atoi(e) != 0;
+    return !e || std::atoi(e) != 0;
   }();
   return g;
 }
@@ -1013,7 +1016,7 @@ int Launch(const ConvArgs& a, hipStream_t st) {
       return 0;
     }
   }
-  // SML_CONV_GLDS=1: the LDS-DMA staged forms for the layers without a prologue (A/B switch)
+  // the LDS-DMA staged forms for the layers without a prologue (SML_CONV_GLDS=0: register staging)
   if constexpr (sizeof(T) == 2) {
     if (EnvGlds() && !a.in_scale && a.split_k == 1) {
       if (a.Cout <= 64) LaunchGlds<T, 64, 64, 256>(a, M, st);
@@ -1031,6 +1034,92 @@ int Launch(const ConvArgs& a, hipStream_t st) {
   return 0;
 }
 
+// ---------------------------------------------------------------- few-channel stem conv
+// The image stem (7x7, stride 2, 3 input channels -> 64 at 224x224: K = 147) has no channel run to tile over:
+// the generic implicit GEMM gathers its A operand 2 bytes at a time (403 us per ResNet-50 fp16 batch of 128,
+// 10 % of the replay). Here a block takes 128 consecutive output pixels and builds their im2col rows in LDS
+// from the input's contiguous runs - for one pixel and filter row r the S * C input values (7 pixels x 3
+// channels = 42 B) are adjacent in NHWC - with K zero-padded to kKP = 160; the [64][160] weight tile (packed
+// once, zero-padded) sits beside it. 4 waves x (32 pixels x 64 channels) of 16x16x32 MFMAs, then the shared
+// LDS-staged bias / ReLU / residual epilogue. Row pitch 176 elements (352 B): conflict-free fragment reads.
+constexpr int kStemKP = 160;              // padded K (5 MFMA k-steps)
+constexpr int kStemLd = kStemKP + 16;     // LDS row pitch
+constexpr int kStemBM = 128, kStemBN = 64;
+
+template <class T>
+__global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
+  typedef typename Vec<T>::type V8;
+  constexpr int kOpElems = (kStemBM + kStemBN) * kStemLd;
+  __shared__ __attribute__((aligned(16))) T lds[kOpElems];
+  T* As = lds;                      // [128][176]: im2col rows
+  T* Bs = lds + kStemBM * kStemLd;  // [64][176]: weights
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = a.B * a.OH * a.OW;
+  const int m0 = blockIdx.x * kStemBM, n0 = blockIdx.y * kStemBN;
+  const int C = a.C, S = a.S, R = a.R, run = S * C, K = R * run;
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const T* __restrict__ w = static_cast<const T*>(a.w);
+  // weights: 64 rows x 160 (already zero-padded by the packer), 16-B chunks
+  for (int q = tid; q < kStemBN * (kStemKP / 8); q += 256) {
+    const int row = q / (kStemKP / 8), ch = q % (kStemKP / 8);
+    const int n = n0 + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < a.Cout) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + ch * 8);
+    *reinterpret_cast<uint4*>(Bs + row * kStemLd + ch * 8) = v;
+  }
+  // the padded K tail of every A row is zero (NaN-free with the zero weight tail)
+  for (int q = tid; q < kStemBM * 4; q += 256) {
+    const int row = q >> 2, ch = q & 3;
+    const int k0 = (K / 8) * 8 + ch * 8;  // 16-B chunks from the last partial one on
+    if (k0 < kStemKP) *reinterpret_cast<uint4*>(As + row * kStemLd + k0) = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  // im2col runs: (pixel, filter row) -> S * C contiguous input values
+  for (int q = tid; q < kStemBM * R; q += 256) {
+    const int ml = q / R, r = q - ml * R;
+    const int m = m0 + ml;
+    T* dst = As + ml * kStemLd + r * run;
+    if (m >= M) continue;
+    const int ow = m % a.OW, t2 = m / a.OW;
+    const int oh = t2 % a.OH, b = t2 / a.OH;
+    const int ih = oh * a.stride_h - a.pad_h + r * a.dil_h;
+    const int iw0 = ow * a.stride_w - a.pad_w;
+    if (ih < 0 || ih >= a.H) {
+      for (int e = 0; e < run; ++e) dst[e] = FromF<T>(0.f);
+      continue;
+    }
+    const T* src = x + (static_cast<int64_t>(b * a.H + ih) * a.W) * C;
+    for (int s2 = 0; s2 < S; ++s2) {
+      const int iw = iw0 + s2 * a.dil_w;
+      const bool ok = iw >= 0 && iw < a.W;
+      for (int c = 0; c < C; ++c) dst[s2 * C + c] = ok ? src[iw * C + c] : FromF<T>(0.f);
+    }
+  }
+  __syncthreads();
+  // 4 waves along M: 32 pixels x 64 channels each
+  constexpr int TM = 2, TN = 4;
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int wm0 = wid * 32, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int ks = 0; ks < kStemKP / 32; ++ks) {
+    V8 af[TM], bf[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const V8*>(As + (wm0 + i * 16 + fr) * kStemLd + ks * 32 + fk);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const V8*>(Bs + (j * 16 + fr) * kStemLd + ks * 32 + fk);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+  }
+  __syncthreads();  // the epilogue stages through the operand LDS
+  ConvEpilogue<T, 32, 64, 1>(a, acc, lds, M, m0, n0, wid, lane);
+}
+
 }  // namespace
 
 template <class T>
@@ -1039,6 +1128,21 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
   const int blocks = ((M + 63) / 64) * ((a.Cout + 63) / 64);
   hipLaunchKernelGGL((conv_mfma_kernel<T, 64, 64, false, kThreads, 1, true>), dim3(blocks), dim3(kThreads), 0, st, a);
   return 0;
+}
+
+// few-channel stem: x NHWC with C <= 4, w packed [Cout][160] (k = (r * S + s) * C + c, zero-padded),
+// R * S * C <= 160, f16 (dtype 1) / bf16 (2)
+int StemConv(const ConvArgs& a, int dtype, void* stream) {
+  if ((dtype != 1 && dtype != 2) || a.C < 1 || a.C > 4 || a.R * a.S * a.C > kStemKP || a.in_scale || a.Cout < 1 ||
+      a.OH <= 0 || a.OW <= 0 || a.B <= 0)
+    return -1;
+  if (static_cast<int64_t>(a.B) * a.OH * a.OW >= (1ll << 31)) return -5;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int M = a.B * a.OH * a.OW;
+  const dim3 grid((M + kStemBM - 1) / kStemBM, (a.Cout + kStemBN - 1) / kStemBN);
+  if (dtype == 1) hipLaunchKernelGGL(stem_conv_kernel<_Float16>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(stem_conv_kernel<__bf16>, grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 // dtype: 0 fp32 (exact f32 MFMAs), 1 fp16, 2 bf16, 3 fp32 on 2 bf16 planes (3 products), 4 fp32 on 3 bf16

@@ -1097,10 +1097,14 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
     }
   // upload the blocks (pinned staging, parallel host copies) on the copy stream
   std::vector<void*> tmp;
-  auto dev_copy = [&](const void* src, size_t bytes) -> void* {
+  auto dev_alloc = [&](size_t bytes) -> void* {  // freed at the end of the staging
     void* d = nullptr;
     VW_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 8)));
     tmp.push_back(d);
+    return d;
+  };
+  auto dev_copy = [&](const void* src, size_t bytes) -> void* {
+    void* d = dev_alloc(bytes);
     if (bytes) impl_->stager.Copy(static_cast<char*>(d), static_cast<const char*>(src), bytes, cs);
     return d;
   };
@@ -1135,7 +1139,7 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
       VW_HIP_CHECK(hipGetLastError());
       size_t tb = 0;
       VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
-      void* tbuf = dev_copy(nullptr, tb);
+      void* tbuf = dev_alloc(tb);  // the scan's temporary storage (no host source)
       VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tbuf, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
     }
     int64_t nnz = 0;

@@ -794,12 +794,44 @@ def _fused_conv(rt, at, x):
                         out_affine=(f32(post[0]), f32(post[1])) if post is not None else None,
                         f32_mode=rt.session.f32_conv_mode)
         return list(y) if post is not None else [y]
+    if _STEM_KERNEL and pro is None and _stem_kernel_ok(rt, at, inp, w):
+        ys = [_stem_kernel_conv(rt, at, inp, w, b, res, act)]
+        if post is not None:
+            return ys + [_affine_act(rt, ys[0], post[0], post[1], None, 1, 0.0)]
+        return ys
     if _STEM_MFMA and pro is None and post is None and _stem_ok(rt, at, inp, w):
         return [_stem_conv(rt, at, inp, w, b, res, act)]
     ys = _fused_conv_fallback(rt, at, inp, w, b, res, pro, act)
     if post is not None:
         return ys + [_affine_act(rt, ys[0], post[0], post[1], None, 1, 0.0)]
     return ys
+
+
+# The few-channel image stem (C <= 4, R * S * C <= 160, f16 / bf16) runs on its dedicated kernel (im2col rows
+# built in LDS from the input's contiguous (s, c) runs, K padded to 160): csrc/nn/conv_mfma.hip
+# stem_conv_kernel. SML_STEM_KERNEL=0 falls back to the generic implicit-GEMM gather.
+_STEM_KERNEL = os.environ.get("SML_STEM_KERNEL", "1") != "0"
+
+
+def _stem_kernel_ok(rt, at, inp, w) -> bool:
+    from ..ops.conv import stem_supported
+
+    return (rt.session._nn is not None and inp.dim() == 4 and inp.dtype == w.dtype and at.get("group", 1) == 1
+            and at.get("__act", 0) in (0, 1) and stem_supported(inp, w)
+            and inp.numel() * inp.element_size() < 2 ** 31)
+
+
+def _stem_kernel_conv(rt, at, inp, w, b, res, act):
+    from ..ops.conv import pack_stem_weight, stem_conv_nhwc
+
+    cache = rt.session.__dict__.setdefault("_stem_wk", {})
+    key = (w.data_ptr(), tuple(w.shape), w.dtype)
+    wk = cache.get(key)
+    if wk is None:
+        wk = cache[key] = pack_stem_weight(w)
+    nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+    return stem_conv_nhwc(inp, wk, w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]), dil,
+                          bias=b, relu=2 if act == 1 else 0, res=res)
 
 
 # SML_STEM_MFMA=1: run the 3-channel stem on the packed MFMA form. Off by default: ResNet-50 fp16 measured

@@ -6,6 +6,7 @@ MFMA; fp32 either on the exact f32-input MFMA (16x16x4, 1/16 of the bf16 rate) o
 split over bf16 planes and the products rebuilt from 16x16x32 MFMAs (F32_MODES)."""
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -13,6 +14,7 @@ import torch
 from . import native
 
 _DT = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+_SPLITK = os.environ.get("SML_CONV_SPLITK", "0") not in ("", "0")
 # fp32 convolution modes: exact f32 MFMAs (16x16x4, 1/16 of the bf16 rate on gfx950), or every f32 operand
 # split into 2 / 3 bf16 planes with the products rebuilt from 3 / 6 bf16 MFMAs (16x16x32): ~16 / ~24
 # significant bits per product (TF32 keeps 11), fp32 accumulation, fp32 in and out.
@@ -111,8 +113,11 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
         dt, wptr = dt + 2, w_planes.data_ptr()
     nn = native.load("_nn")
     # split-K (deep layers with few output tiles): fp32 partial tiles + per-tile arrival counters, allocated
-    # stream-ordered from the caching allocator (so concurrent streams and graph capture each get their own)
-    sk, ws_floats, n_cnt = nn.conv_split_plan(geom, dt, in_affine is not None, int(kernel))
+    # stream-ordered from the caching allocator (so concurrent streams and graph capture each get their own).
+    # Opt-in (SML_CONV_SPLITK=auto or a split count): r4 measured it slower on every ResNet-50 layer it took
+    # (profiles/r4/conv: the partial tiles' agent-scope release per block costs more than the fuller grid).
+    sk, ws_floats, n_cnt = (nn.conv_split_plan(geom, dt, in_affine is not None, int(kernel)) if _SPLITK
+                            else (1, 0, 0))
     ws = cnt = None
     if sk > 1:
         ws = torch.empty(ws_floats, device=x.device, dtype=torch.float32)
@@ -125,7 +130,51 @@ def conv2d_nhwc(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1)
     return (y, y2) if out_affine is not None else y
 
 
-__all__ = ["supported", "pack_weight", "split_weight", "conv2d_nhwc", "out_hw", "F32_MODES"]
+STEM_KP = 160  # padded K of the stem kernel (csrc/nn/conv_mfma.hip stem_conv_kernel)
+
+
+def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """The dedicated few-channel stem kernel takes f16/bf16 NHWC inputs with C <= 4 and R * S * C <= 160."""
+    return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dim() == 4 and 1 <= x.shape[1] <= 4
+            and w.shape[1] == x.shape[1] and w.shape[1] * w.shape[2] * w.shape[3] <= STEM_KP)
+
+
+def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, C, R, S] -> [Cout, 160] with k = (r * S + s) * C + c, zero-padded (packed once per weight)."""
+    cout = w.shape[0]
+    k = w.permute(0, 2, 3, 1).reshape(cout, -1)
+    out = torch.zeros((cout, STEM_KP), dtype=w.dtype, device=w.device)
+    out[:, :k.shape[1]] = k
+    return out
+
+
+def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
+                   bias: Optional[torch.Tensor] = None, relu: int = 0,
+                   res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = relu?(conv(x, w) + bias (+ res)) for a few-channel input (the image stem): ``x`` [B, C, H, W]
+    channels_last f16/bf16 with C <= 4, ``wk`` = pack_stem_weight(w). ``relu``: 0 none, 1 before the residual
+    add, 2 after it. ``pad``: (top, left) or (top, left, bottom, right)."""
+    B, C, H, W = x.shape
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    if wk.dim() != 2 or wk.shape[1] != STEM_KP or wk.dtype != x.dtype or not wk.is_contiguous():
+        raise ValueError("stem weight must be pack_stem_weight(w) in the input dtype")
+    if C * r * s > STEM_KP or C > 4:
+        raise ValueError("stem kernel: C <= 4 and R * S * C <= 160")
+    cout = wk.shape[0]
+    oh, ow = out_hw(H, W, r, s, stride, pad, dil)
+    y = torch.empty((B, cout, oh, ow), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    if res is not None:
+        res = res.to(x.dtype).contiguous(memory_format=torch.channels_last)
+    b32 = None if bias is None else bias.reshape(-1).to(x.device, torch.float32).contiguous()
+    geom = [B, H, W, C, cout, r, s, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], oh, ow]
+    native.load("_nn").stem_conv(x.data_ptr(), wk.data_ptr(), y.data_ptr(), _ptr(b32), _ptr(res), geom, int(relu),
+                                 _DT[x.dtype], torch.cuda.current_stream(x.device).cuda_stream)
+    return y
+
+
+__all__ = ["supported", "pack_weight", "split_weight", "conv2d_nhwc", "out_hw", "F32_MODES", "stem_supported",
+           "pack_stem_weight", "stem_conv_nhwc"]
 
 
 def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),

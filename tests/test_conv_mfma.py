@@ -304,3 +304,34 @@ def test_fp32_presplit_weight_planes_bitwise(mode):
             b = conv2d_nhwc(x, wp, k, k, (1, 1), (k // 2, k // 2), in_affine=ia, f32_mode=mode, kernel=kernel,
                             w_planes=split_weight(wp, mode))
             torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("geom", [
+    # B, C, H, W, Cout, k, stride, pad
+    (4, 3, 224, 224, 64, 7, 2, 3),   # the ResNet-50 stem
+    (3, 3, 37, 29, 64, 7, 2, 3),     # partial pixel tiles, padding on every border
+    (2, 4, 19, 23, 128, 5, 1, 2),    # two 64-channel tiles, C = 4
+    (2, 1, 16, 16, 80, 3, 1, 1),     # a partial channel tile
+])
+def test_stem_kernel_matches_reference(dtype, geom):
+    """Dedicated few-channel stem kernel (im2col rows in LDS, K padded to 160) vs the fp32 reference, with
+    bias + ReLU and a residual; small integers check the layout exactly."""
+    from synapseml_amd.ops.conv import pack_stem_weight, stem_conv_nhwc
+
+    B, C, H, W, Co, k, st, pd = geom
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(-2, 3, (B, C, H, W), generator=g).to(dtype).cuda().contiguous(memory_format=torch.channels_last)
+    w = torch.randint(-2, 3, (Co, C, k, k), generator=g).to(dtype).cuda()
+    y = stem_conv_nhwc(x, pack_stem_weight(w), k, k, (st, st), (pd, pd))
+    ref = F.conv2d(x.float(), w.float(), None, st, pd)
+    torch.testing.assert_close(y.float(), ref.to(dtype).float(), rtol=0, atol=0)  # exact sum, one rounding
+    torch.manual_seed(6)
+    xf = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    wf = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)
+    bias = torch.randn(Co, device="cuda")
+    res = torch.randn_like(ref).to(dtype).contiguous(memory_format=torch.channels_last)
+    y2 = stem_conv_nhwc(xf, pack_stem_weight(wf), k, k, (st, st), (pd, pd), bias=bias, relu=2, res=res)
+    r2 = torch.relu(F.conv2d(xf.float(), wf.float(), bias, st, pd) + res.float())
+    tol = 2e-2 if dtype == torch.float16 else 8e-2
+    torch.testing.assert_close(y2.float(), r2, rtol=tol, atol=tol)

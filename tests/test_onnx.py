@@ -552,14 +552,14 @@ def test_gpu_global_average_pool_kernel(dt):
 
 
 def test_conv_split_k_plan():
-    """Split-K planning (host side of csrc/nn/conv_mfma.hip ConvSplitPlan): the deep few-tile layers of
+    """Split-K planning (host side of csrc/nn/conv_mfma.hip ConvSplitPlan; opt-in, SML_CONV_SPLITK): the deep few-tile layers of
     ResNet-50 at batch 128 split K (>= 512 blocks, >= 4 K tiles per split, <= 8 splits), the early
     many-tile layers and forced tiles do not, and the workspace is one fp32 partial tile per split."""
     from synapseml_amd.ops import native
 
     nn = native.load("_nn")
 
-    def plan(C, H, Co, k, B=128, dt=1, kernel=0, pro=False):
+    def plan(C, H, Co, k, B=128, dt=1, kernel=0, pro=True):  # prologue layers (the others stage by LDS-DMA)
         pd = k // 2
         g = [B, H, H, C, Co, k, k, 1, 1, pd, pd, 1, 1, H, H]
         return nn.conv_split_plan(g, dt, pro, kernel)
@@ -575,3 +575,16 @@ def test_conv_split_k_plan():
     assert (sk, cnt) == (4, 1) and wsf == 4 * 64 * 64
     assert plan(64, 7, 64, 1, B=1)[0] == 1               # too short a K loop
     assert plan(256, 14, 256, 3, dt=4)[0] == 2           # fp32 on bf16 planes: 32-wide K tiles
+    assert plan(256, 14, 256, 3, pro=False)[0] == 1      # f16 without a prologue: the LDS-DMA form, no split
+
+
+def test_stem_weight_packing_order():
+    """pack_stem_weight: k = (r * S + s) * C + c, zero tail to 160 (the stem kernel's im2col order)."""
+    from synapseml_amd.ops.conv import STEM_KP, pack_stem_weight
+
+    w = torch.arange(2 * 3 * 7 * 7, dtype=torch.float32).reshape(2, 3, 7, 7)
+    wk = pack_stem_weight(w)
+    assert wk.shape == (2, STEM_KP)
+    r, s_, c = 4, 5, 2
+    assert wk[1, (r * 7 + s_) * 3 + c] == w[1, c, r, s_]
+    assert torch.all(wk[:, 147:] == 0)

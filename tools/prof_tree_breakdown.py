@@ -2,12 +2,18 @@
 """Per-kernel totals and per-split-position times of GBDT tree growth from a rocprofv3 kernel_trace.csv
 (usage: prof_tree_breakdown.py <kernel_trace.csv>)."""
 import csv, sys, re, collections
-rows=list(csv.DictReader(open(sys.argv[1])))
 def short(n):
     n=n.replace('void ','').replace('sml::(anonymous namespace)::',''); n=re.sub(r'\(.*','',n)
     return n
 tot=collections.defaultdict(lambda:[0,0]); 
-ks=[(short(r['Kernel_Name']),int(r['Start_Timestamp']),int(r['End_Timestamp']),int(r['LDS_Block_Size']),int(r['VGPR_Count']),int(r['Accum_VGPR_Count']),int(r['Scratch_Size'])) for r in rows]
+if sys.argv[1].endswith('.db'):  # rocprofv3's default SQLite output (rocpd schema, `kernels` view)
+    import sqlite3
+    con = sqlite3.connect(sys.argv[1])
+    ks = [(short(n), int(s), int(e), int(l or 0), int(v or 0), int(a or 0), int(sc or 0)) for n, s, e, l, v, a, sc in
+          con.execute('select name, start, end, lds_size, vgpr_count, accum_vgpr_count, scratch_size from kernels')]
+else:
+    rows=list(csv.DictReader(open(sys.argv[1])))
+    ks=[(short(r['Kernel_Name']),int(r['Start_Timestamp']),int(r['End_Timestamp']),int(r['LDS_Block_Size']),int(r['VGPR_Count']),int(r['Accum_VGPR_Count']),int(r['Scratch_Size'])) for r in rows]
 ks.sort(key=lambda x:x[1])
 for n,s,e,*_ in ks: tot[n][0]+=1; tot[n][1]+=e-s
 for n,(c,t) in sorted(tot.items(), key=lambda x:-x[1][1]): print(f"{n:40s} {c:6d} {t/1e6:9.2f} ms {t/c/1e3:8.2f} us")
@@ -19,7 +25,7 @@ for n,s,e,*_ in ks:
     if n=='root_init_kernel':
         cur=[]; trees.append(cur)
     if cur is not None: cur.append((n,e-s,s,e))
-trees=trees[len(trees)//2:]  # timed fit(s)
+trees=trees[len(trees)//3:]  # the timed fits (bench.py: 1 warm-up + 2 timed fits of 100 trees)
 pos=collections.defaultdict(lambda: collections.defaultdict(list))
 for t in trees:
     cnt=collections.Counter()
@@ -30,7 +36,7 @@ for n in ('hist_kernel<2>','hist_reduce_kernel','find_split_kernel','choose_part
 # tree wall: root_init start to next root_init start
 walls=[]
 for t in trees:
-    walls.append((t[-1][3]-t[0][2])/1e3)
+    walls.append((t[-1][3]-t[0][2])/1e3)  # includes the gap to the next fit for a fit's last tree
 busy=[sum(d for _,d,_,_ in t)/1e3 for t in trees]
 print('tree span us avg', sum(walls)/len(walls), 'busy', sum(busy)/len(busy), 'n', len(trees))
 gaps=[]; spans=[]
