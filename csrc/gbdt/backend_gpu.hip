@@ -114,7 +114,14 @@ struct DTree {  // device tree arrays (capacity L)
   int64_t* lcount;      // L
   int32_t* lparent;     // L
   int32_t* ldepth;      // L
+  double out_l1, out_l2, out_mds;  // leaf-output regularisation: the root's value (its internal value once split)
 };
+
+// the root's output as a leaf (LeafOutput of the root totals): the internal value node 0 gets when it splits,
+// as the host learner (backend_cpu.cpp) sets tree.leaf_value[0] before growing
+__device__ __forceinline__ double RootLeafOutput(const DTree& t, double g, double h) {
+  return LeafOutput(g, h, t.out_l1, t.out_l2, t.out_mds);
+}
 
 struct FeatMeta {
   const int32_t* num_bin;
@@ -1379,7 +1386,7 @@ __device__ void ChooseBlock(DState* __restrict__ st, DLeaf* __restrict__ leaves,
       const int bi = sh_best_f[0];
       if (bi >= 0) { lbest[0] = fbest[bi]; lgain[0] = fbest[bi].gain; }
       else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; lgain[0] = -INFINITY; }
-      t.lval[0] = 0.0;
+      t.lval[0] = RootLeafOutput(t, leaves[0].sum_g, leaves[0].sum_h);
       t.lcount[0] = leaves[0].gcount;
       t.lweight[0] = leaves[0].sum_h;
       t.lparent[0] = -1;
@@ -1890,7 +1897,7 @@ __global__ __launch_bounds__(kPartThreads) void choose_part_kernel(
     if (root) {
       if (bf0 >= 0) { lbest[0] = fbest[bf0]; lgain[0] = cg0; }
       else { lbest[0].feature = -1; lbest[0].gain = -INFINITY; lgain[0] = -INFINITY; }
-      t.lval[0] = 0.0;
+      t.lval[0] = RootLeafOutput(t, leaves[0].sum_g, leaves[0].sum_h);
       t.lcount[0] = leaves[0].gcount;
       t.lweight[0] = leaves[0].sum_h;
       t.lparent[0] = -1;
@@ -2111,7 +2118,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       BNode r;
       r.begin = R.begin; r.count = R.count; r.buf = R.buf; r.depth = 0;
       r.gcount = R.gcount; r.sum_g = R.sum_g; r.sum_h = R.sum_h; r.lo = -INFINITY; r.hi = INFINITY;
-      r.out = 0.0; r.c0 = -1; r.c1 = -1;
+      r.out = RootLeafOutput(t, R.sum_g, R.sum_h); r.c0 = -1; r.c1 = -1;
       nodes[0] = r;
       bs->nexp = 0; bs->done = 0; bs->nnodes = 1; bs->expanded = 0; bs->spec_used = 0; bs->ntiles = 0;
       bs->cap_exp = 2 * budget + kMaxSpec;
@@ -2779,8 +2786,11 @@ class GpuBackend : public TrainBackend {
     for (int b = 0; b < 2; ++b) { perm_[b].alloc(n_); ogh_[b].alloc(n_); }
     slab_.alloc(static_cast<size_t>(kMaxHistBlocks) * E_);
     // batched speculative growth (bplan_kernel ..): one-split-at-a-time stays for voting, bynode sampling,
-    // num_leaves > 256 and SML_GBDT_SPEC=0; SML_GBDT_SPEC=k sets the expansions per round (default 8)
-    spec_k_ = 8;
+    // num_leaves > 256 and SML_GBDT_SPEC=0; SML_GBDT_SPEC=k sets the expansions per round (default 4)
+    // 4 expansions per round: r4 A/B at 11M x 28 (profiles/r4/gbdt2): spec 2 231 ms / fit, 4 217 ms, 8 247 ms,
+    // one-split growth 250 ms - wider rounds mostly add never-popped expansions (the rounds follow the
+    // parent -> child dependency chain of the pops, ~15 per tree at 31 leaves)
+    spec_k_ = 4;
     if (const char* e = std::getenv("SML_GBDT_SPEC")) spec_k_ = std::atoi(e);
     batch_ok_ = spec_k_ > 0 && L_ <= kBatchMaxLeaves && !(cfg.tree_learner == "voting" && comm_ && comm_->world() > 1);
     spec_k_ = std::max(1, std::min(kMaxSpec, spec_k_));
@@ -2921,6 +2931,7 @@ class GpuBackend : public TrainBackend {
     dt_.gain = td; dt_.ival = td + NI; dt_.iweight = td + 2 * NI; dt_.lval = td + 3 * NI; dt_.lweight = td + 3 * NI + L_;
     int64_t* tl = reinterpret_cast<int64_t*>(blob_.get() + off_tl_);
     dt_.icount = tl; dt_.lcount = tl + NI;
+    dt_.out_l1 = sp_.lambda_l1; dt_.out_l2 = sp_.lambda_l2; dt_.out_mds = sp_.max_delta_step;
     // score-update tree (uploaded from host trees)
     up_blob_.alloc(static_cast<size_t>(NI + 1) * (16 + 32) + static_cast<size_t>(L_ + 4) * 8);
     leaf_idx_.alloc(n_);
@@ -3772,7 +3783,7 @@ class GpuBackend : public TrainBackend {
   // batched speculative growth
   static constexpr int kBRing = 8;
   bool batch_ok_ = false;
-  int spec_k_ = 8;
+  int spec_k_ = 4;
   int blook_ = 1;
   DevBuf<BState> bstate_;
   DevBuf<BNode> bnodes_;

@@ -1067,11 +1067,14 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
     if (n < a.Cout) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + ch * 8);
     *reinterpret_cast<uint4*>(Bs + row * kStemLd + ch * 8) = v;
   }
-  // the padded K tail of every A row is zero (NaN-free with the zero weight tail)
-  for (int q = tid; q < kStemBM * 4; q += 256) {
-    const int row = q >> 2, ch = q & 3;
-    const int k0 = (K / 8) * 8 + ch * 8;  // 16-B chunks from the last partial one on
-    if (k0 < kStemKP) *reinterpret_cast<uint4*>(As + row * kStemLd + k0) = make_uint4(0, 0, 0, 0);
+  // the padded K tail of every A row is zero (NaN-free with the zero weight tail): every 16-B chunk from the
+  // last partial one to kKP (the im2col runs below overwrite the real part of that first chunk)
+  {
+    const int c0 = K / 8, nch = kStemKP / 8 - c0;
+    for (int q = tid; q < kStemBM * nch; q += 256) {
+      const int row = q / nch, ch = c0 + q % nch;
+      *reinterpret_cast<uint4*>(As + row * kStemLd + ch * 8) = make_uint4(0, 0, 0, 0);
+    }
   }
   __syncthreads();
   // im2col runs: (pixel, filter row) -> S * C contiguous input values
