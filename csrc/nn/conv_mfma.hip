@@ -1046,7 +1046,7 @@ constexpr int kStemKP = 160;              // padded K (5 MFMA k-steps)
 constexpr int kStemLd = kStemKP + 16;     // LDS row pitch
 constexpr int kStemBM = 128, kStemBN = 64;
 
-template <class T>
+template <class T, int C>
 __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kOpElems = (kStemBM + kStemBN) * kStemLd;
@@ -1056,8 +1056,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int M = a.B * a.OH * a.OW;
   const int m0 = blockIdx.x * kStemBM, n0 = blockIdx.y * kStemBN;
-  const int C = a.C, S = a.S, R = a.R, run = S * C, K = R * run;
-  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const int S = a.S, R = a.R, run = S * C, K = R * run;
   const T* __restrict__ w = static_cast<const T*>(a.w);
   // weights: 64 rows x 160 (already zero-padded by the packer), 16-B chunks
   for (int q = tid; q < kStemBN * (kStemKP / 8); q += 256) {
@@ -1077,26 +1076,36 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
     }
   }
   __syncthreads();
-  // im2col runs: (pixel, filter row) -> S * C contiguous input values
+  // im2col runs: (pixel, filter row) -> the S * C contiguous input values of that row. Every value is a 2-byte
+  // buffer load whose offset is out of range for padding (the hardware returns 0): the up-to-32 loads of a run
+  // are independent and issue back to back (C is a template parameter, so the (s, c) of each slot is static).
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, a.B * a.H * a.W * C * static_cast<int>(sizeof(T)), 0x00020000);
+  constexpr uint32_t kOob = 0x80000000u;
+  constexpr int kSlots = 8 * C;  // S <= 8
   for (int q = tid; q < kStemBM * R; q += 256) {
     const int ml = q / R, r = q - ml * R;
     const int m = m0 + ml;
-    T* dst = As + ml * kStemLd + r * run;
     if (m >= M) continue;
     const int ow = m % a.OW, t2 = m / a.OW;
     const int oh = t2 % a.OH, b = t2 / a.OH;
     const int ih = oh * a.stride_h - a.pad_h + r * a.dil_h;
     const int iw0 = ow * a.stride_w - a.pad_w;
-    if (ih < 0 || ih >= a.H) {
-      for (int e = 0; e < run; ++e) dst[e] = FromF<T>(0.f);
-      continue;
-    }
-    const T* src = x + (static_cast<int64_t>(b * a.H + ih) * a.W) * C;
-    for (int s2 = 0; s2 < S; ++s2) {
+    const bool row_ok = ih >= 0 && ih < a.H;
+    const int rowbase = (b * a.H + ih) * a.W;
+    unsigned short v[kSlots];
+#pragma unroll
+    for (int e = 0; e < kSlots; ++e) {
+      const int s2 = e / C, c = e % C;
       const int iw = iw0 + s2 * a.dil_w;
-      const bool ok = iw >= 0 && iw < a.W;
-      for (int c = 0; c < C; ++c) dst[s2 * C + c] = ok ? src[iw * C + c] : FromF<T>(0.f);
+      const bool ok = row_ok && s2 < S && iw >= 0 && iw < a.W;
+      const uint32_t off = ok ? static_cast<uint32_t>(((rowbase + iw) * C + c) * static_cast<int>(sizeof(T))) : kOob;
+      v[e] = __builtin_amdgcn_raw_buffer_load_b16(xres, off, 0, 0);
     }
+    T* dst = As + ml * kStemLd + r * run;
+#pragma unroll
+    for (int e = 0; e < kSlots; ++e)
+      if (e < run) dst[e] = __builtin_bit_cast(T, v[e]);
   }
   __syncthreads();
   // 4 waves along M: 32 pixels x 64 channels each
@@ -1143,8 +1152,24 @@ int StemConv(const ConvArgs& a, int dtype, void* stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int M = a.B * a.OH * a.OW;
   const dim3 grid((M + kStemBM - 1) / kStemBM, (a.Cout + kStemBN - 1) / kStemBN);
-  if (dtype == 1) hipLaunchKernelGGL(stem_conv_kernel<_Float16>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(stem_conv_kernel<__bf16>, grid, dim3(256), 0, st, a);
+  if (a.S > 8) return -1;
+  if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * 2 >= (1ll << 31)) return -5;
+  auto launch = [&](auto k) { hipLaunchKernelGGL(k, grid, dim3(256), 0, st, a); };
+  if (dtype == 1) {
+    switch (a.C) {
+      case 1: launch(stem_conv_kernel<_Float16, 1>); break;
+      case 2: launch(stem_conv_kernel<_Float16, 2>); break;
+      case 3: launch(stem_conv_kernel<_Float16, 3>); break;
+      default: launch(stem_conv_kernel<_Float16, 4>); break;
+    }
+  } else {
+    switch (a.C) {
+      case 1: launch(stem_conv_kernel<__bf16, 1>); break;
+      case 2: launch(stem_conv_kernel<__bf16, 2>); break;
+      case 3: launch(stem_conv_kernel<__bf16, 3>); break;
+      default: launch(stem_conv_kernel<__bf16, 4>); break;
+    }
+  }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -136,7 +136,7 @@ STEM_KP = 160  # padded K of the stem kernel (csrc/nn/conv_mfma.hip stem_conv_ke
 def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
     """The dedicated few-channel stem kernel takes f16/bf16 NHWC inputs with C <= 4 and R * S * C <= 160."""
     return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dim() == 4 and 1 <= x.shape[1] <= 4
-            and w.shape[1] == x.shape[1] and w.shape[1] * w.shape[2] * w.shape[3] <= STEM_KP)
+            and w.shape[1] == x.shape[1] and w.shape[3] <= 8 and w.shape[1] * w.shape[2] * w.shape[3] <= STEM_KP)
 
 
 def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
