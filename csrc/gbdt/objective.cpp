@@ -63,14 +63,23 @@ void Objective::Init(const float* label, const float* weight, int64_t n, const s
   }
   if (p_.kind == kObjLambdarank) {
     if (qb_.size() < 2) throw std::runtime_error("lambdarank requires query/group information");
+    // ideal DCG per query: the labels in descending order are a counting sort over the (clipped) gain index -
+    // labels are small non-negative integers - so a query costs one pass, not a sort (125k queries of ~100
+    // documents: the serial sort loop was ~130 ms of LightGBMRanker's booster init)
     inv_max_dcg_.assign(qb_.size() - 1, 0.0);
-    for (size_t q = 0; q + 1 < qb_.size(); ++q) {
-      std::vector<int> labs;
-      for (int32_t i = qb_[q]; i < qb_[q + 1]; ++i) labs.push_back(static_cast<int>(label[i]));
-      std::sort(labs.begin(), labs.end(), std::greater<int>());
+    const int ng = static_cast<int>(label_gain_.size());
+    const int64_t nq = static_cast<int64_t>(qb_.size()) - 1;
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t q = 0; q < nq; ++q) {
+      std::vector<int32_t> cnt(ng, 0);
+      for (int32_t i = qb_[q]; i < qb_[q + 1]; ++i) {
+        const int l = static_cast<int>(label[i]);
+        ++cnt[std::max(0, std::min(l, ng - 1))];
+      }
       double dcg = 0;
-      for (int k = 0; k < static_cast<int>(labs.size()) && k < max_position_; ++k)
-        dcg += label_gain_[std::min<int>(labs[k], static_cast<int>(label_gain_.size()) - 1)] / std::log2(2.0 + k);
+      int k = 0;
+      for (int gi = ng - 1; gi >= 0 && k < max_position_; --gi)
+        for (int32_t c = 0; c < cnt[gi] && k < max_position_; ++c, ++k) dcg += label_gain_[gi] / std::log2(2.0 + k);
       inv_max_dcg_[q] = dcg > 0 ? 1.0 / dcg : 0.0;
     }
   }
