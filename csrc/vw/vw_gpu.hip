@@ -140,11 +140,17 @@ constexpr int kRateCache = 4;
 struct UpdPrep {
   float g, ppu, norm_x;
   float rate[kRateCache];
+  float hot_x2, hot_x, hot_ax;  // the example's occurrences of the block-aggregated slot: sum x^2, sum x, max |x|
 };
 
+// slot index meaning "no aggregated slot"
+constexpr uint64_t kNoHot = ~0ull;
+constexpr uint32_t kVwConstantHash = 11650396u;  // VW's constant feature (the featurizer writes it as kConstantIdx)
+
 __device__ UpdPrep UpdateFirstPass(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y,
-                                   float imp, int lane) {
+                                   float imp, int lane, uint64_t hot = kNoHot) {
   UpdPrep pr;
+  float hx2 = 0.f, hx = 0.f, hax = 0.f;
   float g;
   if (a.loss == 1) g = -y / (1.f + expf(y * raw));
   else if (a.loss == 2) g = (y * raw < 1.f) ? -y : 0.f;
@@ -159,6 +165,12 @@ __device__ UpdPrep UpdateFirstPass(const SgdArgs& a, int64_t b, int64_t en, uint
     const float x = a.val[p];
     float x2 = x * x;
     if (x2 < FLT_MIN) x2 = FLT_MIN;
+    if (h == hot) {  // the block-aggregated slot (sgd_kernel): its G / N / weight updates are done per block
+      hx2 += x2;
+      hx += x;
+      hax = fmaxf(hax, fabsf(x));
+      continue;
+    }
     float G = 0.f, N = 1.f;
     // G and N come back from returning atomics: in a hogwild batch of examples sharing dense features, each
     // update must see the accumulators of the updates serialized before it (a plain load would hand every
@@ -182,12 +194,20 @@ __device__ UpdPrep UpdateFirstPass(const SgdArgs& a, int64_t b, int64_t en, uint
   pr.g = g;
   pr.ppu = WaveSum(ppu);
   pr.norm_x = WaveSum(norm_x);
+  pr.hot_x2 = hot == kNoHot ? 0.f : WaveSum(hx2);
+  pr.hot_x = hot == kNoHot ? 0.f : WaveSum(hx);
+  if (hot != kNoHot) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hax = fmaxf(hax, __shfl_xor(hax, o, 64));
+  }
+  pr.hot_ax = hax;
   return pr;
 }
 
 // t, tw, snx: the global state including this update (what the sequential learner sees)
-__device__ void UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y,
-                                 float imp, int lane, const UpdPrep& pr, double t, double tw, double snx) {
+__device__ float UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64_t off, float raw, float y,
+                                  float imp, int lane, const UpdPrep& pr, double t, double tw, double snx,
+                                  uint64_t hot = kNoHot) {
   double eta = a.lr;
   if (a.normalized && snx > 0.0) {
     const double avg = tw / snx;
@@ -212,6 +232,7 @@ __device__ void UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64
   int k = 0;
   for (int64_t p = b + lane; p < en; p += 64, ++k) {
     const uint64_t h = (a.idx[p] + off) & a.mask;
+    if (h == hot) continue;  // applied per block by the caller
     float4* w = &a.W[h];
     const float x = a.val[p];
     const float rate = k < kRateCache ? pr.rate[k] : Rate(a, a.adaptive ? w->y : 0.f, a.normalized ? w->z : 1.f);
@@ -227,6 +248,7 @@ __device__ void UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint64
     }
     a.dirty[h >> kDirtyShift] = 1;
   }
+  return update;
 }
 
 // whole update with its own global-state step (oaa: one per class update)
@@ -280,8 +302,53 @@ __global__ __launch_bounds__(64 * kSgdWaves) void sgd_kernel(SgdArgs a) {
   }
   if (!a.learn) return;  // uniform over the launch
   const bool upd = act && imp > 0.f;
+  // VW's constant feature is in every example: per-example returning atomics on its slot serialize every
+  // example of a hogwild batch on one address (769 vs 303 us per 16384-example batch at 2^30, r4 trace). Its
+  // G / N / weight updates are aggregated per block instead: one returning atomic for the block's G, each
+  // example taking G_base + the inclusive prefix of the block's contributions in wave order (the serialized
+  // order the per-example atomics would have produced, up to the order among the block's examples), one
+  // atomicMax for N, one atomicAdd for the summed weight deltas. Not with l1 / l2 (their per-update
+  // corrections need the running value).
+  const uint64_t hot = (a.l1 > 0.f || a.l2 > 0.f) ? kNoHot : (static_cast<uint64_t>(kVwConstantHash) & a.mask);
+  __shared__ float s_hg[kSgdWaves], s_hax[kSgdWaves], s_hd[kSgdWaves], s_hot[2];
   UpdPrep pr{0.f, 0.f, 0.f};
-  if (upd) pr = UpdateFirstPass(a, b, en, 0, raw, y, imp, lane);
+  if (upd) pr = UpdateFirstPass(a, b, en, 0, raw, y, imp, lane, hot);
+  float hot_rate = 0.f;
+  if (hot != kNoHot) {
+    if (lane == 0) {
+      s_hg[wid] = upd ? pr.g * pr.g * imp * pr.hot_x2 : 0.f;
+      s_hax[wid] = upd ? pr.hot_ax : 0.f;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tot = 0.f, mx = 0.f;
+      for (int w = 0; w < kSgdWaves; ++w) { tot += s_hg[w]; mx = fmaxf(mx, s_hax[w]); }
+      float gb = 0.f, nn = 1.f;
+      if (mx > 0.f) {
+        float4* wh = &a.W[hot];
+        if (a.adaptive) gb = atomicAdd(&wh->y, tot);
+        if (a.normalized) {
+          const float old = __uint_as_float(atomicMax(reinterpret_cast<unsigned int*>(&wh->z), __float_as_uint(mx)));
+          if (mx > old && old > 0.f) {
+            const float r = old / mx;
+            wh->x *= a.adaptive ? r : r * r;
+          }
+          nn = fmaxf(old, mx);
+        }
+      }
+      s_hot[0] = gb;
+      s_hot[1] = nn;
+    }
+    __syncthreads();
+    if (upd && pr.hot_x2 > 0.f) {
+      float pre = 0.f;
+      for (int w = 0; w <= wid; ++w) pre += s_hg[w];
+      const float N = s_hot[1];
+      hot_rate = Rate(a, s_hot[0] + pre, N);
+      pr.ppu += pr.hot_x2 * hot_rate;
+      if (a.normalized) pr.norm_x += pr.hot_x2 / (N * N);
+    }
+  }
   if (lane == 0) {
     s_imp[wid] = upd ? static_cast<double>(imp) : 0.0;
     s_nx[wid] = upd ? static_cast<double>(imp) * pr.norm_x : 0.0;
@@ -297,10 +364,25 @@ __global__ __launch_bounds__(64 * kSgdWaves) void sgd_kernel(SgdArgs a) {
     atomicAdd(a.loss_acc, sl);
   }
   __syncthreads();
-  if (!upd) return;
-  double pi = 0.0, pn = 0.0;
-  for (int w = 0; w <= wid; ++w) { pi += s_imp[w]; pn += s_nx[w]; }
-  UpdateSecondPass(a, b, en, 0, raw, y, imp, lane, pr, s_base[0] + pi, s_base[1] + pi, s_base[2] + pn);
+  float upd_scalar = 0.f;
+  if (upd) {
+    double pi = 0.0, pn = 0.0;
+    for (int w = 0; w <= wid; ++w) { pi += s_imp[w]; pn += s_nx[w]; }
+    upd_scalar = UpdateSecondPass(a, b, en, 0, raw, y, imp, lane, pr, s_base[0] + pi, s_base[1] + pi, s_base[2] + pn,
+                                  hot);
+  }
+  if (hot != kNoHot) {  // the aggregated slot's weight: one atomic for the block's summed deltas
+    if (lane == 0) s_hd[wid] = (upd && pr.hot_x2 > 0.f) ? upd_scalar * pr.hot_x * hot_rate : 0.f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float d = 0.f, mx = 0.f;
+      for (int w = 0; w < kSgdWaves; ++w) { d += s_hd[w]; mx = fmaxf(mx, s_hax[w]); }
+      if (mx > 0.f) {
+        atomicAdd(&a.W[hot].x, d);
+        a.dirty[hot >> kDirtyShift] = 1;
+      }
+    }
+  }
 }
 
 // --oaa K: one block per example, wave c handles classes c, c + waves, ...: scores (predict), then the
@@ -347,7 +429,7 @@ constexpr int kMaxGroups = 32;
 constexpr int kMaxGroupBlocks = 4;
 constexpr int kMaxInter = 64;
 constexpr uint32_t kFnv = 16777619u;
-constexpr uint32_t kConstantIdx = 11650396u;
+constexpr uint32_t kConstantIdx = kVwConstantHash;
 
 struct DevBlock {
   const int64_t* ip;
@@ -679,17 +761,30 @@ __global__ void count_nz_kernel(const float4* __restrict__ W, uint64_t nw, uint6
   if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-__global__ void write_nz_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per, const int64_t* __restrict__ base,
-                                uint64_t* __restrict__ oidx, float* __restrict__ oval) {
-  // one thread per block keeps the records in slot order (the host model's order) - blocks are small
-  if (threadIdx.x != 0) return;
+// one wave per block of `per` slots, 64 slots per step: a wave prefix sum of the step's nonzero counts gives
+// every lane its output offset, so the records stay in slot order (the host model's order) while all lanes
+// work (the one-thread-per-block form took 36 ms over a 2^30-slot table)
+__global__ __launch_bounds__(64) void write_nz_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per,
+                                                      const int64_t* __restrict__ base, uint64_t* __restrict__ oidx,
+                                                      float* __restrict__ oval) {
+  const int lane = threadIdx.x & 63;
   const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * per, s1 = min(nw, s0 + per);
   int64_t o = base[blockIdx.x];
-  for (uint64_t s = s0; s < s1; ++s) {
-    const float4 v = W[s];
-    if (v.x != 0.f) { oidx[o] = 4 * s; oval[o++] = v.x; }
-    if (v.y != 0.f) { oidx[o] = 4 * s + 1; oval[o++] = v.y; }
-    if (v.z != 0.f) { oidx[o] = 4 * s + 2; oval[o++] = v.z; }
+  for (uint64_t s = s0; s < s1; s += 64) {
+    const uint64_t my = s + lane;
+    const float4 v = my < s1 ? W[my] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int c = (v.x != 0.f) + (v.y != 0.f) + (v.z != 0.f);
+    int inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += t;
+    }
+    int64_t p = o + (inc - c);
+    if (v.x != 0.f) { oidx[p] = 4 * my; oval[p++] = v.x; }
+    if (v.y != 0.f) { oidx[p] = 4 * my + 1; oval[p++] = v.y; }
+    if (v.z != 0.f) { oidx[p] = 4 * my + 2; oval[p] = v.z; }
+    o += __shfl(inc, 63, 64);
   }
 }
 
