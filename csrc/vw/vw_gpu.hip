@@ -4,6 +4,7 @@
 // scatter AdaGrad updates back with float atomics (conflicts are rare in a
 // 2^b table, which is what makes hogwild converge like sequential SGD).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
@@ -104,6 +105,7 @@ struct SgdArgs {
   float* preds;
   float* loss_acc;
   int learn;
+  int hot_agg;         // block-aggregate the constant feature's slot (sgd_kernel; SML_VW_HOT_AGG=0 disables)
 };
 
 __device__ __forceinline__ float WaveSum(float v) {
@@ -309,7 +311,8 @@ __global__ __launch_bounds__(64 * kSgdWaves) void sgd_kernel(SgdArgs a) {
   // order the per-example atomics would have produced, up to the order among the block's examples), one
   // atomicMax for N, one atomicAdd for the summed weight deltas. Not with l1 / l2 (their per-update
   // corrections need the running value).
-  const uint64_t hot = (a.l1 > 0.f || a.l2 > 0.f) ? kNoHot : (static_cast<uint64_t>(kVwConstantHash) & a.mask);
+  const uint64_t hot = (!a.hot_agg || a.l1 > 0.f || a.l2 > 0.f) ? kNoHot
+                                                                 : (static_cast<uint64_t>(kVwConstantHash) & a.mask);
   __shared__ float s_hg[kSgdWaves], s_hax[kSgdWaves], s_hd[kSgdWaves], s_hot[2];
   UpdPrep pr{0.f, 0.f, 0.f};
   if (upd) pr = UpdateFirstPass(a, b, en, 0, raw, y, imp, lane, hot);
@@ -984,6 +987,11 @@ SgdArgs BaseArgs(const GpuSgdConfig& c) {
   a.loss = c.loss;
   a.adaptive = c.adaptive ? 1 : 0; a.normalized = c.normalized ? 1 : 0; a.invariant = c.invariant ? 1 : 0;
   a.K = c.oaa > 0 ? c.oaa : c.csoaa;
+  static const int hot_agg = [] {
+    const char* e = std::getenv("SML_VW_HOT_AGG");
+    return e ? std::atoi(e) : 1;
+  }();
+  a.hot_agg = hot_agg;
   return a;
 }
 }  // namespace
