@@ -1078,36 +1078,49 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   __syncthreads();
   // im2col runs: (pixel, filter row) -> the S * C contiguous input values of that row (21 for the 7x7 x 3 stem).
   // A wave takes floor(64 / run) runs per step with lane l on element l % run of run l / run, so one
-  // wave-instruction reads a few contiguous 42-B stretches (a per-lane-run form issued one cache line per lane:
-  // 313 us per batch). Padding comes from out-of-range buffer offsets (the hardware returns 0).
+  // wave-instruction reads a few contiguous 42-B stretches (one run per lane issued a cache line per lane:
+  // 313 us per batch). The pixels' window origins come from an LDS table (no divisions in the loop), a lane's
+  // (pixel, row) advances by a fixed step, and padding comes from out-of-range buffer offsets (zeros).
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.x), 0, a.B * a.H * a.W * C * static_cast<int>(sizeof(T)), 0x00020000);
   constexpr uint32_t kOob = 0x80000000u;
+  __shared__ int s_ih0[kStemBM], s_iw0[kStemBM], s_img[kStemBM];
+  if (tid < kStemBM) {
+    const int m = m0 + tid;
+    const int mm = m < M ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW;
+    const int oh = t2 % a.OH, b = t2 / a.OH;
+    s_ih0[tid] = m < M ? oh * a.stride_h - a.pad_h : -(1 << 29);  // rows past M read nothing (zeros)
+    s_iw0[tid] = ow * a.stride_w - a.pad_w;
+    s_img[tid] = b * a.H;
+  }
+  __syncthreads();
   {
     const int rpw = 64 / run;                  // runs per wave-step (>= 2: run <= 32)
     const int lr = lane / run, e = lane - lr * run;
     const int s2 = e / C, c = e - s2 * C;
     const bool lane_on = lr < rpw;
     const int nruns = kStemBM * R, step = 4 * rpw;
+    const int dml = step / R, dr = step - dml * R;
+    int q = wid * rpw + lr;
+    int ml = q / R, r = q - ml * R;
+    const int sdw = s2 * a.dil_w;
     constexpr int U = 8;  // runs in flight per lane: offsets first, then the loads, then the LDS writes
-    for (int q0 = wid * rpw; q0 < nruns; q0 += step * U) {
+    for (; q - lr < nruns; ) {
       uint32_t off[U];
       int dst[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int q = q0 + u * step + lr;
         const bool on = lane_on && q < nruns;
-        const int qq = on ? q : 0;
-        const int ml = qq / R, r = qq - ml * R;
-        const int m = m0 + ml;
-        const int mm = m < M ? m : 0;
-        const int ow = mm % a.OW, t2 = mm / a.OW;
-        const int oh = t2 % a.OH, b = t2 / a.OH;
-        const int ih = oh * a.stride_h - a.pad_h + r * a.dil_h;
-        const int iw = ow * a.stride_w - a.pad_w + s2 * a.dil_w;
-        const bool ok = on && m < M && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-        off[u] = ok ? static_cast<uint32_t>((((b * a.H + ih) * a.W + iw) * C + c) * static_cast<int>(sizeof(T))) : kOob;
+        const int mlc = on ? ml : 0;
+        const int ih = s_ih0[mlc] + r * a.dil_h, iw = s_iw0[mlc] + sdw;
+        const bool ok = on && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+        off[u] = ok ? static_cast<uint32_t>((((s_img[mlc] + ih) * a.W + iw) * C + c) * static_cast<int>(sizeof(T))) : kOob;
         dst[u] = on ? ml * kStemLd + r * run + e : -1;
+        q += step;
+        ml += dml;
+        r += dr;
+        if (r >= R) { r -= R; ++ml; }
       }
       unsigned short v[U];
 #pragma unroll
