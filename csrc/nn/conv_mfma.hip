@@ -1076,59 +1076,36 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
     }
   }
   __syncthreads();
-  // im2col runs: (pixel, filter row) -> the S * C contiguous input values of that row (21 for the 7x7 x 3 stem).
-  // A wave takes floor(64 / run) runs per step with lane l on element l % run of run l / run, so one
-  // wave-instruction reads a few contiguous 42-B stretches (one run per lane issued a cache line per lane:
-  // 313 us per batch). The pixels' window origins come from an LDS table (no divisions in the loop), a lane's
-  // (pixel, row) advances by a fixed step, and padding comes from out-of-range buffer offsets (zeros).
+  // im2col runs: (pixel, filter row) -> the S * C contiguous input values of that row. Every value is a 2-byte
+  // buffer load whose offset is out of range for padding (the hardware returns 0): the up-to-32 loads of a run
+  // are independent and issue back to back (C is a template parameter, so the (s, c) of each slot is static).
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.x), 0, a.B * a.H * a.W * C * static_cast<int>(sizeof(T)), 0x00020000);
   constexpr uint32_t kOob = 0x80000000u;
-  __shared__ int s_ih0[kStemBM], s_iw0[kStemBM], s_img[kStemBM];
-  if (tid < kStemBM) {
-    const int m = m0 + tid;
-    const int mm = m < M ? m : 0;
-    const int ow = mm % a.OW, t2 = mm / a.OW;
+  constexpr int kSlots = 8 * C;  // S <= 8
+  for (int q = tid; q < kStemBM * R; q += 256) {
+    const int ml = q / R, r = q - ml * R;
+    const int m = m0 + ml;
+    if (m >= M) continue;
+    const int ow = m % a.OW, t2 = m / a.OW;
     const int oh = t2 % a.OH, b = t2 / a.OH;
-    s_ih0[tid] = m < M ? oh * a.stride_h - a.pad_h : -(1 << 29);  // rows past M read nothing (zeros)
-    s_iw0[tid] = ow * a.stride_w - a.pad_w;
-    s_img[tid] = b * a.H;
-  }
-  __syncthreads();
-  {
-    const int rpw = 64 / run;                  // runs per wave-step (>= 2: run <= 32)
-    const int lr = lane / run, e = lane - lr * run;
-    const int s2 = e / C, c = e - s2 * C;
-    const bool lane_on = lr < rpw;
-    const int nruns = kStemBM * R, step = 4 * rpw;
-    const int dml = step / R, dr = step - dml * R;
-    int q = wid * rpw + lr;
-    int ml = q / R, r = q - ml * R;
-    const int sdw = s2 * a.dil_w;
-    constexpr int U = 8;  // runs in flight per lane: offsets first, then the loads, then the LDS writes
-    for (; q - lr < nruns; ) {
-      uint32_t off[U];
-      int dst[U];
+    const int ih = oh * a.stride_h - a.pad_h + r * a.dil_h;
+    const int iw0 = ow * a.stride_w - a.pad_w;
+    const bool row_ok = ih >= 0 && ih < a.H;
+    const int rowbase = (b * a.H + ih) * a.W;
+    unsigned short v[kSlots];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool on = lane_on && q < nruns;
-        const int mlc = on ? ml : 0;
-        const int ih = s_ih0[mlc] + r * a.dil_h, iw = s_iw0[mlc] + sdw;
-        const bool ok = on && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-        off[u] = ok ? static_cast<uint32_t>((((s_img[mlc] + ih) * a.W + iw) * C + c) * static_cast<int>(sizeof(T))) : kOob;
-        dst[u] = on ? ml * kStemLd + r * run + e : -1;
-        q += step;
-        ml += dml;
-        r += dr;
-        if (r >= R) { r -= R; ++ml; }
-      }
-      unsigned short v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b16(xres, off[u], 0, 0);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (dst[u] >= 0) As[dst[u]] = __builtin_bit_cast(T, v[u]);
+    for (int e = 0; e < kSlots; ++e) {
+      const int s2 = e / C, c = e % C;
+      const int iw = iw0 + s2 * a.dil_w;
+      const bool ok = row_ok && s2 < S && iw >= 0 && iw < a.W;
+      const uint32_t off = ok ? static_cast<uint32_t>(((rowbase + iw) * C + c) * static_cast<int>(sizeof(T))) : kOob;
+      v[e] = __builtin_amdgcn_raw_buffer_load_b16(xres, off, 0, 0);
     }
+    T* dst = As + ml * kStemLd + r * run;
+#pragma unroll
+    for (int e = 0; e < kSlots; ++e)
+      if (e < run) dst[e] = __builtin_bit_cast(T, v[e]);
   }
   __syncthreads();
   // 4 waves along M: 32 pixels x 64 channels each
