@@ -936,7 +936,7 @@ __device__ __forceinline__ void SlabWrite(ulonglong2* out, const unsigned long l
 // One block's share of a leaf histogram: rows [begin, begin + count) of ping-pong buffer `buf` (-1 =
 // physical rows) are cut into nb_active chunks; this block (chunk lb, feature group blockIdx.y) accumulates
 // its chunk into LDS and writes its slab.
-template <int kUnroll, int kFPG>
+template <int kUnroll, int kFPG, bool kPipe = false>
 __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_active, int lb, const uint4* __restrict__ bins4,
                                          int W4, int F, const int32_t* __restrict__ perm0,
                                          const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
@@ -959,6 +959,55 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
   const int32_t* __restrict__ perm = buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = buf == 0 ? ogh0 : ogh1;
   const bool phys = buf < 0;
+  const int rot = tid & 15;
+  if constexpr (kPipe) {
+    // Software pipeline, two stages deep: while the rows of step i go into the LDS histogram, the bins /
+    // (g, h) of step i + 1 and the row ids of step i + 2 are in flight, so a wave's memory latency hides
+    // behind its own atomics instead of only behind the other 15 waves' (the plain loop issues the next
+    // loads only after the atomics). Positions past p1 load row 0 / position p0 and are never accumulated.
+    constexpr int kStep = kHistBlockThreads * kUnroll;
+    auto rows_at = [&](int base, int* r) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int pos = base + u * kHistBlockThreads;
+        r[u] = pos < p1 ? (phys ? pos : perm[pos]) : 0;
+      }
+    };
+    auto data_at = [&](int base, const int* r, uint4* b0, uint4* b1, float2* v) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int pos = base + u * kHistBlockThreads;
+        const size_t rb = static_cast<size_t>(r[u]) * W4 + col;
+        b0[u] = bins4[rb];
+        b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
+        v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : (pos < p1 ? ogh[pos] : make_float2(0.f, 0.f));
+      }
+    };
+    int r1[kUnroll], r2[kUnroll];
+    uint4 b0[kUnroll], b1[kUnroll];
+    float2 v[kUnroll];
+    int base = p0 + tid;
+    rows_at(base, r1);
+    data_at(base, r1, b0, b1, v);
+    rows_at(base + kStep, r1);
+    for (; base < p1; base += kStep) {
+      rows_at(base + 2 * kStep, r2);
+      uint4 n0[kUnroll], n1[kUnroll];
+      float2 nv[kUnroll];
+      data_at(base + kStep, r1, n0, n1, nv);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        if (base + u * kHistBlockThreads < p1) {
+          if (kFPG > 16 && two) hist_accumulate_rot<(kFPG > 16 ? 32 : 16), kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
+          else hist_accumulate_rot<16, kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
+        }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) { b0[u] = n0[u]; b1[u] = n1[u]; v[u] = nv[u]; r1[u] = r2[u]; }
+    }
+    __syncthreads();
+    SlabWrite<kFPG, kHistBlockThreads>(slab_out, shg, shh, F, grp * kFPG, Fg, tid);
+    return;
+  }
   for (int base = p0 + tid; base < p1; base += kHistBlockThreads * kUnroll) {
     int r[kUnroll];
     bool ok[kUnroll];
@@ -978,7 +1027,6 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
       b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
       v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : (ok[u] ? ogh[pos] : make_float2(0.f, 0.f));
     }
-    const int rot = tid & 15;
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
       if (ok[u]) {
@@ -992,7 +1040,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
 
 // kFPG features per block (blockIdx.y = feature group): 32 = one 128 KB LDS histogram per CU; 16 halves
 // the LDS (two blocks per CU) at the price of reading every row's perm / g / h once per group
-template <int kUnroll, int kFPG>
+template <int kUnroll, int kFPG, bool kPipe = false>
 __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
@@ -1002,7 +1050,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
   const DLeaf L = HistSeg(st, leaves);
   const int nb_active = HistBlocks(L.count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  HistBody<kUnroll, kFPG>(L.begin, L.count, L.buf, nb_active, blockIdx.x, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
+  HistBody<kUnroll, kFPG, kPipe>(L.begin, L.count, L.buf, nb_active, blockIdx.x, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
                           ghmax, slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature);
 }
 
@@ -2382,7 +2430,7 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   }
 }
 
-template <int kUnroll, int kFPG>
+template <int kUnroll, int kFPG, bool kPipe = false>
 __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
     const BState* __restrict__ bs, const uint4* __restrict__ bins4, int W4, int F, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
@@ -2403,7 +2451,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   const BExp& x = bs->exp[j];
   const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
   const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
-  HistBody<kUnroll, kFPG>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
+  HistBody<kUnroll, kFPG, kPipe>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
                           ogh1, g, h, ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature);
 }
 
@@ -2635,7 +2683,7 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
 // Replaces score_kernel + grad_kernel + the root hist_kernel (150 + 54 + 131
 // us at 11M x 28 on MI355X, three full passes over rows).
 
-template <int kUnroll>
+template <int kUnroll, bool kPipe = false>
 __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
@@ -2666,7 +2714,57 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   const bool two = F > 16;
   const int rot = tid & 15;
   float mg = 0.f, mh = 0.f;
-  for (int base = p0 + tid; base < p1; base += kThreads * kUnroll) {
+  // one row of the pass: walk the tree, update the score, gradients, histogram
+  auto row = [&](int i, const uint4& r0, const uint4& r1, double sv, float yv, float wv) {
+    int node = ni > 0 ? 0 : ~0;
+    for (int guard = 0; node >= 0 && guard < num_leaves; ++guard) {
+      const int4 nd = snodes[node];
+      node = NodeStep(nd, ByteOfRow(r0, r1, nd.x & 0xFFFF), cat_bits, node);
+    }
+    const double sn = sv + scale * slval[ni > 0 ? ~node : 0];
+    score[i] = sn;
+    float gg, hh;
+    PointGradient(p, sn, yv, wv, &gg, &hh);
+    g[i] = gg;
+    h[i] = hh;
+    mg = fmaxf(mg, fabsf(gg));
+    mh = fmaxf(mh, fabsf(hh));
+    hist_accumulate_rot<32, kFeatPerGroup>(shg, shh, r0, r1, QuantGH(make_float2(gg, hh), sc), rot);
+  };
+  if constexpr (kPipe) {
+    // the next step's bins / score / label / weight are loaded before this step's rows are processed
+    constexpr int kStep = kThreads * kUnroll;
+    auto load = [&](int base, uint4* b0, uint4* b1, double* s, float* y, float* w) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int i = base + u * kThreads;
+        const bool ok = i < p1;
+        const size_t rb = static_cast<size_t>(ok ? i : p0) * W4;
+        b0[u] = bins4[rb];
+        b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
+        s[u] = ok ? score[i] : 0.0;
+        y[u] = ok ? label[i] : 0.f;
+        w[u] = ok && weight ? weight[i] : 1.f;
+      }
+    };
+    uint4 b0[kUnroll], b1[kUnroll];
+    double s[kUnroll];
+    float y[kUnroll], w[kUnroll];
+    int base = p0 + tid;
+    load(base, b0, b1, s, y, w);
+    for (; base < p1; base += kStep) {
+      uint4 n0[kUnroll], n1[kUnroll];
+      double ns[kUnroll];
+      float ny[kUnroll], nw[kUnroll];
+      load(base + kStep, n0, n1, ns, ny, nw);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u]);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) { b0[u] = n0[u]; b1[u] = n1[u]; s[u] = ns[u]; y[u] = ny[u]; w[u] = nw[u]; }
+    }
+  }
+  for (int base = kPipe ? p1 : p0 + tid; base < p1; base += kThreads * kUnroll) {
     uint4 b0[kUnroll], b1[kUnroll];
     double s[kUnroll];
     float y[kUnroll], w[kUnroll];
@@ -2681,26 +2779,10 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
       y[u] = ok ? label[i] : 0.f;
       w[u] = ok && weight ? weight[i] : 1.f;
     }
+    // all 32 slots (b1 = 0 when F <= 16: bin 0 of unused slots): one code path keeps this kernel unspilled
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int i = base + u * kThreads;
-      if (i >= p1) continue;
-      int node = ni > 0 ? 0 : ~0;
-      for (int guard = 0; node >= 0 && guard < num_leaves; ++guard) {
-        const int4 nd = snodes[node];
-        node = NodeStep(nd, ByteOfRow(b0[u], b1[u], nd.x & 0xFFFF), cat_bits, node);
-      }
-      const double sn = s[u] + scale * slval[ni > 0 ? ~node : 0];
-      score[i] = sn;
-      float gg, hh;
-      PointGradient(p, sn, y[u], w[u], &gg, &hh);
-      g[i] = gg;
-      h[i] = hh;
-      mg = fmaxf(mg, fabsf(gg));
-      mh = fmaxf(mh, fabsf(hh));
-      // all 32 slots (b1 = 0 when F <= 16: bin 0 of unused slots): one code path keeps this kernel unspilled
-      hist_accumulate_rot<32, kFeatPerGroup>(shg, shh, b0[u], b1[u], QuantGH(make_float2(gg, hh), sc), rot);
-    }
+    for (int u = 0; u < kUnroll; ++u)
+      if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u]);
   }
   BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
   __syncthreads();
@@ -2826,6 +2908,7 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_GBDT_COMM_WORLD1")) comm_world1_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
     if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
+    if (const char* e = std::getenv("SML_GBDT_HIST_PIPE")) hist_pipe_ = std::atoi(e) != 0;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -3259,7 +3342,9 @@ class GpuBackend : public TrainBackend {
     const int max_rounds = budget + 2;
     auto bp = part_rows_ == 16 ? bpart_kernel<16> : (part_rows_ == 4 ? bpart_kernel<4> : bpart_kernel<8>);
     auto bh = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16>
-              : (hist_unroll4_ ? bhist_kernel<4, kFeatPerGroup> : bhist_kernel<kHistUnroll, kFeatPerGroup>);
+              : (hist_unroll4_ ? bhist_kernel<4, kFeatPerGroup>
+                               : (hist_pipe_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, true>
+                                             : bhist_kernel<kHistUnroll, kFeatPerGroup>));
     int r = 0;
     for (; r <= max_rounds; ++r) {
       if (r >= blook_) {
@@ -3402,7 +3487,8 @@ class GpuBackend : public TrainBackend {
   // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
   void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
     if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    hipLaunchKernelGGL(score_grad_hist_kernel<kHistUnroll>, dim3(kMaxHistBlocks), dim3(kHistBlockThreads), 0, stream_, tv, src,
+    auto sgk = hist_pipe_ ? score_grad_hist_kernel<kHistUnroll, true> : score_grad_hist_kernel<kHistUnroll>;
+    hipLaunchKernelGGL(sgk, dim3(kMaxHistBlocks), dim3(kHistBlockThreads), 0, stream_, tv, src,
                        reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, static_cast<int32_t>(n_), scale,
                        score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
                        reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
@@ -3507,7 +3593,9 @@ class GpuBackend : public TrainBackend {
   void EnqueueHistogram(const float* g, const float* h) {
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
     auto hk = hist_fpg_ == 16 ? hist_kernel<kHistUnroll, 16>
-              : (hist_unroll4_ ? hist_kernel<4, kFeatPerGroup> : hist_kernel<kHistUnroll, kFeatPerGroup>);
+              : (hist_unroll4_ ? hist_kernel<4, kFeatPerGroup>
+                               : (hist_pipe_ ? hist_kernel<kHistUnroll, kFeatPerGroup, true>
+                                             : hist_kernel<kHistUnroll, kFeatPerGroup>));
     hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
                        perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
@@ -3701,6 +3789,7 @@ class GpuBackend : public TrainBackend {
   int K_ = 1, F_ = 0, S_ = 4, W_ = 1, E_ = 0, L_ = 2, FG_ = 1;
   int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
   bool hist_unroll4_ = false;     // SML_HIST_UNROLL=4: 4 gathered rows in flight per thread (A/B knob)
+  bool hist_pipe_ = false;        // SML_GBDT_HIST_PIPE=1: software-pipelined histogram loops (A/B knob)
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
   DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident

@@ -923,13 +923,36 @@ def _post(kind, s):
     return s
 
 
+def _attr_const(at, dev, key, make):
+    """A device tensor built once per (node attributes, device) and kept in the attribute dict (like the
+    compiled tree ensembles): no host->device copy per run, so the op can sit inside a HIP-graph capture."""
+    cache = at.setdefault("__dev_consts__", {})
+    k = (key, str(dev))
+    t = cache.get(k)
+    if t is None:
+        t = make()
+        cache[k] = t
+    return t
+
+
+def _labels_of(at, dev, labels, idx):
+    """class labels for argmax indices: on the device for integer labels, host objects for strings"""
+    if isinstance(labels[0], str):
+        return np.asarray(labels)[idx.cpu().numpy()].astype(object)
+    lt = _attr_const(at, dev, "labels", lambda: torch.tensor([int(v) for v in labels], dtype=torch.int64, device=dev))
+    return lt[idx]
+
+
 @op("LinearClassifier")
 def _linclf(rt, at, x):
     X = x[0].to(torch.float32)
     labels = at.get("classlabels_ints") or at.get("classlabels_strings")
     nc = len(labels)
-    coef = torch.tensor(at["coefficients"], dtype=torch.float32, device=X.device).reshape(-1, X.shape[1])
-    inter = torch.tensor(at.get("intercepts", [0.0] * coef.shape[0]), dtype=torch.float32, device=X.device)
+    dev = X.device
+    coef = _attr_const(at, dev, "coef", lambda: torch.tensor(at["coefficients"], dtype=torch.float32,
+                                                             device=dev).reshape(-1, X.shape[1]))
+    inter = _attr_const(at, dev, "inter", lambda: torch.tensor(at.get("intercepts", [0.0] * coef.shape[0]),
+                                                               dtype=torch.float32, device=dev))
     s = X @ coef.t() + inter
     if coef.shape[0] == 1 and nc == 2:
         s = torch.cat([-s, s], dim=1)
@@ -941,18 +964,17 @@ def _linclf(rt, at, x):
             post = _post(at.get("post_transform", "NONE"), s)
     else:
         post = _post(at.get("post_transform", "NONE"), s)
-    idx = torch.argmax(s, dim=1).cpu().numpy()
-    lab = np.asarray(labels)[idx]
-    lab_t = torch.from_numpy(lab.astype(np.int64)) if not isinstance(labels[0], str) else lab.astype(object)
-    return [lab_t, post]
+    return [_labels_of(at, dev, labels, torch.argmax(s, dim=1)), post]
 
 
 @op("LinearRegressor")
 def _linreg(rt, at, x):
     X = x[0].to(torch.float32)
     t = at.get("targets", 1)
-    coef = torch.tensor(at["coefficients"], dtype=torch.float32, device=X.device).reshape(t, -1)
-    inter = torch.tensor(at.get("intercepts", [0.0] * t), dtype=torch.float32, device=X.device)
+    coef = _attr_const(at, X.device, "coef", lambda: torch.tensor(at["coefficients"], dtype=torch.float32,
+                                                                  device=X.device).reshape(t, -1))
+    inter = _attr_const(at, X.device, "inter", lambda: torch.tensor(at.get("intercepts", [0.0] * t),
+                                                                    dtype=torch.float32, device=X.device))
     return [_post(at.get("post_transform", "NONE"), X @ coef.t() + inter)]
 
 
@@ -972,8 +994,10 @@ def _normalizer(rt, at, x):
 @op("Scaler")
 def _scaler(rt, at, x):
     X = x[0].to(torch.float32)
-    off = torch.tensor(at.get("offset", [0.0]), dtype=torch.float32, device=X.device)
-    sc = torch.tensor(at.get("scale", [1.0]), dtype=torch.float32, device=X.device)
+    off = _attr_const(at, X.device, "off", lambda: torch.tensor(at.get("offset", [0.0]), dtype=torch.float32,
+                                                                device=X.device))
+    sc = _attr_const(at, X.device, "sc", lambda: torch.tensor(at.get("scale", [1.0]), dtype=torch.float32,
+                                                              device=X.device))
     return [(X - off) * sc]
 
 
@@ -983,7 +1007,8 @@ def _afe(rt, at, x):
     ind = _ints(x[1])
     if isinstance(data, np.ndarray):
         return [data[..., ind]]
-    return [data[..., torch.tensor(ind, device=data.device)]]
+    key = ("ind",) + tuple(int(i) for i in np.ravel(ind))
+    return [data[..., _attr_const(at, data.device, key, lambda: torch.tensor(ind, device=data.device))]]
 
 
 @op("Binarizer")
@@ -1022,8 +1047,8 @@ def _ohe(rt, at, x):
 @op("Imputer")
 def _imputer(rt, at, x):
     X = x[0]
-    vals = torch.tensor(at.get("imputed_value_floats") or at.get("imputed_value_int64s"), device=X.device,
-                        dtype=X.dtype)
+    vals = _attr_const(at, X.device, ("vals", str(X.dtype)), lambda: torch.tensor(
+        at.get("imputed_value_floats") or at.get("imputed_value_int64s"), device=X.device, dtype=X.dtype))
     rep = at.get("replaced_value_float", float("nan"))
     mask = torch.isnan(X) if math.isnan(rep) else (X == rep)
     return [torch.where(mask, vals.expand_as(X) if vals.numel() > 1 else vals, X)]

@@ -42,7 +42,9 @@ HOST_SYNC_OPS = {"Loop", "Scan", "If", "NonZero", "Compress", "Unique", "NonMaxS
                  "DynamicQuantizeLinear", "MatMulInteger", "ConvInteger", "QLinearMatMul", "QLinearConv",
                  "LSTM", "GRU", "RNN", "Bernoulli", "Multinomial", "RandomNormal", "RandomUniform",
                  "RandomNormalLike", "RandomUniformLike", "StringNormalizer", "StringConcat", "StringSplit",
-                 "RegexFullMatch", "CategoryMapper", "DictVectorizer", "FeatureVectorizer"}
+                 "RegexFullMatch", "CategoryMapper", "DictVectorizer", "FeatureVectorizer",
+                 # ai.onnx.ml ops evaluated on the host (numpy maps / dicts): a capture would record nothing
+                 "ZipMap", "LabelEncoder", "OneHotEncoder", "TfIdfVectorizer"}
 
 
 def _t(v, device=None, dtype=None) -> torch.Tensor:

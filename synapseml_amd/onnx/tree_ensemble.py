@@ -90,7 +90,9 @@ def run_tree_ensemble(rt, at, x):
         scores = scores / T
     base = at.get("base_values")
     if base:
-        scores = scores + torch.tensor(base, dtype=torch.float32, device=dev)
+        if "base" not in c:
+            c["base"] = torch.tensor(base, dtype=torch.float32, device=dev)
+        scores = scores + c["base"]
     post = at.get("post_transform", "NONE")
     if not classifier:
         if post == "LOGISTIC":
@@ -113,6 +115,8 @@ def run_tree_ensemble(rt, at, x):
         else:
             probs = scores
         idx = torch.argmax(scores, dim=1)
-    lab = np.asarray(labels)[idx.cpu().numpy()]
-    lab_t = lab.astype(object) if isinstance(labels[0], str) else torch.from_numpy(lab.astype(np.int64))
-    return [lab_t, probs]
+    if isinstance(labels[0], str):
+        return [np.asarray(labels)[idx.cpu().numpy()].astype(object), probs]
+    if "labels_t" not in c:
+        c["labels_t"] = torch.tensor([int(v) for v in labels], dtype=torch.int64, device=dev)
+    return [c["labels_t"][idx], probs]

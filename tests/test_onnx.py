@@ -507,9 +507,27 @@ def test_gpu_graph_capture_records_work_or_runs_eager():
         x = np.random.default_rng(seed).random((64, 4)).astype(np.float32) * 5
         label = s.run(["output_label"], {"float_input": x})[0]
         assert np.asarray(label).tolist() == (x @ coef.T + inter).argmax(1).tolist()
-    assert s._graphs
-    for entry in s._graphs.values():
-        assert entry == "eager" or _graph_num_nodes(entry[0]) > 0
+    # the ZipMap output (a sequence of host dicts) makes the plan non-graphable: it never captures
+    assert not s._graphable({"float_input": x}) and not s._graphs
+    # LinearClassifier alone (integer labels gathered on the device, coefficients cached on the device)
+    # captures a non-empty graph whose replays track new inputs
+    b = GraphBuilder("lc")
+    b.input("float_input", P.FLOAT32, [None, 4])
+    b.add("LinearClassifier", ["float_input"], {"coefficients": [float(v) for v in np.ravel(coef)],
+                                                "intercepts": [float(v) for v in inter],
+                                                "classlabels_ints": [0, 1, 2], "post_transform": "SOFTMAX"},
+          n_out=2, domain="ai.onnx.ml", out="lc")
+    b.nodes[-1].outputs = ["output_label", "probabilities"]
+    b.output("output_label", P.INT64, [None])
+    b.output("probabilities", P.FLOAT32, [None, 3])
+    s1 = InferenceSession(b.to_bytes({"": 13, "ai.onnx.ml": 1}), device="cuda", use_graph=True)
+    for seed in (5, 6, 7):
+        x = np.random.default_rng(seed).random((64, 4)).astype(np.float32) * 5
+        label = s1.run(["output_label"], {"float_input": x})[0]
+        label = label.cpu().numpy() if torch.is_tensor(label) else np.asarray(label)
+        assert label.tolist() == (x @ coef.T + inter).argmax(1).tolist()
+    entry = next(iter(s1._graphs.values()))
+    assert entry != "eager" and _graph_num_nodes(entry[0]) > 0
     # a plain tensor graph is replayed from a non-empty capture with fresh results per batch
     b = GraphBuilder("lin")
     b.input("x", P.FLOAT32, ["N", 4])
