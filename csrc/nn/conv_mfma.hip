@@ -693,7 +693,7 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
   }
 }
 
-// LDS-DMA form (f16 / bf16, no prologue): the A and B tiles go global -> LDS with buffer_load ... lds
+// LDS-DMA form (f16 / bf16): the A and B tiles go global -> LDS with buffer_load ... lds
 // (16 B per lane, one 1-KiB wave-instruction = 8 tile rows of 128 B), so staging takes no VGPRs and no
 // ds_write (whose 13-cycle wave-instruction transfer, at ~79 B/clk/CU, is as long as the tile's fragment
 // reads). A DMA lands lane-linear, so the rows are unpadded 128-B lines and the bank spread comes from an XOR
@@ -701,6 +701,9 @@ __global__ __launch_bounds__(kThr) void conv_mfma_kernel(ConvArgs a) {
 // chunk c of row r sits at slot c ^ (r & 7); the fragment reads apply the same XOR (conflict-free 16-lane
 // ds_read_b128 groups). Out-of-range rows / padding taps load from an out-of-range buffer offset: zeros.
 // Tile kt+1's DMAs are issued before tile kt's MFMAs; a vmcnt(0) + barrier per K tile retires them.
+// kPro (1x1, unpadded layers only: no padding tap must stay 0): the pre-activation BN + ReLU of the input
+// is applied to the A fragments as they leave LDS (each A element is read by the kWN waves of its row
+// band); the tile's 64 channels of scale / shift ride the same DMA into a 2 x 2 KiB side buffer.
 // 16 B per lane from a buffer resource straight into LDS at the wave-uniform dst (+ 16 * lane): the
 // LDS-address-space builtin exists in the device pass only (the host pass just needs the kernel's stub)
 __device__ __forceinline__ void DmaToLds16(__amdgpu_buffer_rsrc_t r, void* dst, uint32_t voff, uint32_t soff) {
@@ -709,7 +712,7 @@ __device__ __forceinline__ void DmaToLds16(__amdgpu_buffer_rsrc_t r, void* dst, 
 #endif
 }
 
-template <class T, int BM, int BN, int kThr, int kWN>
+template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false>
 __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   static_assert(sizeof(T) == 2, "LDS-DMA conv is the f16 / bf16 form");
@@ -721,11 +724,14 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;  // 8-row DMA pieces per wave and tile
   static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
   constexpr int kOpBytes = 2 * (BM + BN) * kBK * 2;
+  constexpr int kProBytes = kPro ? 2 * 2 * 1024 : 0;  // [buf][scale | shift][256 floats]: one DMA each
   constexpr int kEpiBytes = NW * WM * (WN + 8) * 2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kOpBytes > kEpiBytes ? kOpBytes : kEpiBytes];
+  __shared__ __attribute__((aligned(16)))
+  unsigned char smem[kOpBytes + kProBytes > kEpiBytes ? kOpBytes + kProBytes : kEpiBytes];
   T* lds = reinterpret_cast<T*>(smem);
   T* As = lds;                 // [buf][BM][64], swizzled chunks
   T* Bs = lds + 2 * BM * kBK;  // [buf][BN][64]
+  float* Ps = reinterpret_cast<float*>(smem + kOpBytes);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int M = a.B * a.OH * a.OW;
@@ -763,6 +769,9 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.x), 0, a.B * a.H * a.W * a.C * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, a.Cout * K * 2, 0x00020000);
+  // prologue scale / shift (unused, and dropped by the compiler, without kPro)
+  const __amdgpu_buffer_rsrc_t sres = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in_scale), 0, a.C * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t hres = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in_shift), 0, a.C * 4, 0x00020000);
   uint32_t boff[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
@@ -793,6 +802,13 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
     for (int i = 0; i < BI; ++i) {
       DmaToLds16(wres, Bs + (buf * BN + (wid * BI + i) * 8) * kBK, boff[i], lk0 * 2);
     }
+    if constexpr (kPro) {
+      if (wid == 0) {  // lanes 0-15: the tile's 64 channels (1x1: channel = k); the rest land zeros
+        const uint32_t po = lane < 16 ? static_cast<uint32_t>(lane * 16) : kOob;
+        DmaToLds16(sres, Ps + buf * 512, po, lc0 * 4);
+        DmaToLds16(hres, Ps + buf * 512 + 256, po, lc0 * 4);
+      }
+    }
     if (++loaded < nk) {
       lk0 += kBK;
       lc0 += kBK;
@@ -821,6 +837,22 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
       for (int j = 0; j < TN; ++j) {
         const int r = wn0 + j * 16 + fr;
         bf[j] = *reinterpret_cast<const V8*>(Bs + (buf * BN + r) * kBK + ((c ^ (r & 7)) * EPV));
+      }
+      if constexpr (kPro) {
+        // channels c * 8 .. c * 8 + 7 of the tile (16 lanes share them: broadcast reads)
+        const float4* ps = reinterpret_cast<const float4*>(Ps + buf * 512 + c * EPV);
+        const float4 s0 = ps[0], s1 = ps[1], h0 = ps[64], h1 = ps[65];
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          T* e = reinterpret_cast<T*>(&af[i]);
+#pragma unroll
+          for (int j = 0; j < EPV; ++j) {
+            const float t = ToF(e[j]) * sc[j] + sh[j];
+            e[j] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
+          }
+        }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -866,7 +898,13 @@ void LaunchPersist(const ConvArgs& a, int M, hipStream_t st) {
 template <class T, int BM, int BN, int kThr, int kWN = 2>
 void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
+  if (a.in_scale) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, true>), dim3(blocks), dim3(kThr), 0, st, a);
+  else hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
+}
+
+// the LDS-DMA form applies a prologue only where no padding tap exists (1x1, unpadded)
+inline bool GldsProOk(const ConvArgs& a) {
+  return !a.in_scale || (a.R == 1 && a.S == 1 && a.pad_h == 0 && a.pad_w == 0);
 }
 
 template <class T, int BM, int BN, int kThr = kThreads, int kSplit = 0, bool kWPre = false, int kWN = 2,
@@ -924,6 +962,14 @@ bool EnvGlds() {
   return g;
 }
 
+bool EnvGldsPro() {
+  static const bool g = [] {
+    const char* e = std::getenv("SML_CONV_GLDS_PRO");
+    return !e || std::atoi(e) != 0;
+  }();
+  return g;
+}
+
 template <class T, int kSplit = 0, bool kWPre = false>
 int Launch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.OH * a.OW;
@@ -963,7 +1009,7 @@ int Launch(const ConvArgs& a, hipStream_t st) {
     case 64777:
     case 256777:
       if constexpr (sizeof(T) == 2 && kSplit == 0) {
-        if (a.in_scale || a.split_k != 1) return -4;
+        if (!GldsProOk(a) || a.split_k != 1) return -4;
         const int code = a.kernel ? a.kernel : env_tile;
         if (code == 128777) LaunchGlds<T, 128, 128, 512>(a, M, st);
         else if (code == 64777) LaunchGlds<T, 64, 64, 256>(a, M, st);
@@ -1016,9 +1062,10 @@ int Launch(const ConvArgs& a, hipStream_t st) {
       return 0;
     }
   }
-  // the LDS-DMA staged forms for the layers without a prologue (SML_CONV_GLDS=0: register staging)
+  // the LDS-DMA staged forms for the layers without a prologue, and (SML_CONV_GLDS_PRO, default on) for the
+  // 1x1 pre-activation layers with one (SML_CONV_GLDS=0: register staging for all)
   if constexpr (sizeof(T) == 2) {
-    if (EnvGlds() && !a.in_scale && a.split_k == 1) {
+    if (EnvGlds() && (!a.in_scale || (EnvGldsPro() && GldsProOk(a))) && a.split_k == 1) {
       if (a.Cout <= 64) LaunchGlds<T, 64, 64, 256>(a, M, st);
       else LaunchGlds<T, 128, 128, 512>(a, M, st);
       return 0;

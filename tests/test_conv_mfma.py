@@ -101,6 +101,29 @@ def test_prologue_residual_dual_output():
     torch.testing.assert_close(y3.float(), r3, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 256, 14, 14, 64, 1), (2, 128, 15, 13, 200, 1), (3, 512, 14, 14, 1024, 2)])
+def test_glds_prologue_matches_register_path(dtype, shape):
+    """The LDS-DMA form's fragment-time prologue (1x1 pre-activation layers, stride 1 or 2) against the fp32
+    reference and against the register-staged tile that applies the same affine + ReLU at its LDS write."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
+
+    B, C, H, W, Co, st = shape
+    torch.manual_seed(4)
+    x = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 1, 1, device="cuda") / C ** 0.5).to(dtype)
+    pro = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.5)
+    bias = torch.randn(Co, device="cuda")
+    ref, _ = _ref(x, w, st, 0, bias=bias, relu=True, pro=pro)
+    tol = 2e-2 if dtype == torch.float16 else 8e-2
+    wp = pack_weight(w, dtype)
+    yr = conv2d_nhwc(x, wp, 1, 1, (st, st), (0, 0), bias=bias, relu=True, in_affine=pro, kernel=128999)
+    for kernel in (0, 128777, 64777, 256777):
+        y = conv2d_nhwc(x, wp, 1, 1, (st, st), (0, 0), bias=bias, relu=True, in_affine=pro, kernel=kernel)
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol, msg=lambda m: f"kernel {kernel}: {m}")
+        torch.testing.assert_close(y.float(), yr.float(), rtol=1e-2, atol=1e-2, msg=lambda m: f"kernel {kernel}: {m}")
+
+
 @pytest.mark.parametrize("dtype,mode", [(torch.float16, None), (torch.bfloat16, None), (torch.float32, "bf16x6"),
                                         (torch.float32, "bf16x3")])
 @pytest.mark.parametrize("shape", [(2, 512, 7, 7, 512, 3), (1, 1024, 14, 14, 256, 1), (3, 256, 9, 11, 200, 3)])
