@@ -962,10 +962,14 @@ bool EnvGlds() {
   return g;
 }
 
+// SML_CONV_GLDS_PRO=1: the LDS-DMA form for the 1x1 prologue layers too (off: r4 pass 9, ResNet-50 fp16
+// b128, the 20 prologue convs took 1112 us on it vs 1028 us register-staged - the affine at fragment read
+// runs kWN times per element plus the scale / shift reads, against once per element at the register
+// path's LDS write; session 39.7k vs 40.4k img/s)
 bool EnvGldsPro() {
   static const bool g = [] {
     const char* e = std::getenv("SML_CONV_GLDS_PRO");
-    return !e || std::atoi(e) != 0;
+    return e && std::atoi(e) != 0;
   }();
   return g;
 }
@@ -1062,8 +1066,8 @@ int Launch(const ConvArgs& a, hipStream_t st) {
       return 0;
     }
   }
-  // the LDS-DMA staged forms for the layers without a prologue, and (SML_CONV_GLDS_PRO, default on) for the
-  // 1x1 pre-activation layers with one (SML_CONV_GLDS=0: register staging for all)
+  // the LDS-DMA staged forms for the layers without a prologue, and (SML_CONV_GLDS_PRO=1) for the 1x1
+  // pre-activation layers with one (SML_CONV_GLDS=0: register staging for all)
   if constexpr (sizeof(T) == 2) {
     if (EnvGlds() && (!a.in_scale || (EnvGldsPro() && GldsProOk(a))) && a.split_k == 1) {
       if (a.Cout <= 64) LaunchGlds<T, 64, 64, 256>(a, M, st);
@@ -1093,7 +1097,7 @@ constexpr int kStemKP = 160;              // padded K (5 MFMA k-steps)
 constexpr int kStemLd = kStemKP + 16;     // LDS row pitch
 constexpr int kStemBM = 128, kStemBN = 64;
 
-template <class T, int C>
+template <class T, int C, bool kPro = false>
 __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   constexpr int kOpElems = (kStemBM + kStemBN) * kStemLd;
@@ -1126,33 +1130,62 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   // im2col runs: (pixel, filter row) -> the S * C contiguous input values of that row. Every value is a 2-byte
   // buffer load whose offset is out of range for padding (the hardware returns 0): the up-to-32 loads of a run
   // are independent and issue back to back (C is a template parameter, so the (s, c) of each slot is static).
+  // The kernel is bound by how many of these gathers are in flight (2 blocks per CU, 8 waves).
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.x), 0, a.B * a.H * a.W * C * static_cast<int>(sizeof(T)), 0x00020000);
   constexpr uint32_t kOob = 0x80000000u;
   constexpr int kSlots = 8 * C;  // S <= 8
-  for (int q = tid; q < kStemBM * R; q += 256) {
+  // a thread's (up to 4) runs are all in flight before any is written to LDS: ~4 x 8C loads per lane
+  // outstanding instead of one run's (the one-run loop waited out a full load latency per run)
+  constexpr int kRunsPerThread = (kStemBM * 8 + 255) / 256;  // R <= 8
+  unsigned short v[kRunsPerThread][kSlots];
+  int dsto[kRunsPerThread];
+  uint32_t okm[kRunsPerThread];  // kPro: in-range slots (padding stays 0 after the affine)
+  float psc[C], psh[C];
+  if constexpr (kPro) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+  }
+#pragma unroll
+  for (int u = 0; u < kRunsPerThread; ++u) {
+    const int q = tid + u * 256;
     const int ml = q / R, r = q - ml * R;
     const int m = m0 + ml;
-    if (m >= M) continue;
-    const int ow = m % a.OW, t2 = m / a.OW;
+    const bool live = q < kStemBM * R && m < M;
+    dsto[u] = live ? ml * kStemLd + r * run : -1;
+    const int mm = live ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW;
     const int oh = t2 % a.OH, b = t2 / a.OH;
     const int ih = oh * a.stride_h - a.pad_h + r * a.dil_h;
     const int iw0 = ow * a.stride_w - a.pad_w;
-    const bool row_ok = ih >= 0 && ih < a.H;
+    const bool row_ok = live && ih >= 0 && ih < a.H;
     const int rowbase = (b * a.H + ih) * a.W;
-    unsigned short v[kSlots];
+    okm[u] = 0u;
 #pragma unroll
     for (int e = 0; e < kSlots; ++e) {
       const int s2 = e / C, c = e % C;
       const int iw = iw0 + s2 * a.dil_w;
       const bool ok = row_ok && s2 < S && iw >= 0 && iw < a.W;
+      okm[u] |= ok ? (1u << e) : 0u;
       const uint32_t off = ok ? static_cast<uint32_t>(((rowbase + iw) * C + c) * static_cast<int>(sizeof(T))) : kOob;
-      v[e] = __builtin_amdgcn_raw_buffer_load_b16(xres, off, 0, 0);
+      v[u][e] = __builtin_amdgcn_raw_buffer_load_b16(xres, off, 0, 0);
     }
-    T* dst = As + ml * kStemLd + r * run;
+  }
 #pragma unroll
-    for (int e = 0; e < kSlots; ++e)
-      if (e < run) dst[e] = __builtin_bit_cast(T, v[e]);
+  for (int u = 0; u < kRunsPerThread; ++u) {
+    if (dsto[u] < 0) continue;
+    T* dst = As + dsto[u];
+#pragma unroll
+    for (int e = 0; e < kSlots; ++e) {
+      if (e >= run) continue;
+      if constexpr (kPro) {
+        const int c = e % C;
+        const float t = ToF(__builtin_bit_cast(T, v[u][e])) * psc[c] + psh[c];
+        dst[e] = (okm[u] >> e) & 1u ? FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t) : FromF<T>(0.f);
+      } else {
+        dst[e] = __builtin_bit_cast(T, v[u][e]);
+      }
+    }
   }
   __syncthreads();
   // 4 waves along M: 32 pixels x 64 channels each
@@ -1192,30 +1225,32 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
 // few-channel stem: x NHWC with C <= 4, w packed [Cout][160] (k = (r * S + s) * C + c, zero-padded),
 // R * S * C <= 160, f16 (dtype 1) / bf16 (2)
 int StemConv(const ConvArgs& a, int dtype, void* stream) {
-  if ((dtype != 1 && dtype != 2) || a.C < 1 || a.C > 4 || a.R * a.S * a.C > kStemKP || a.in_scale || a.Cout < 1 ||
+  if ((dtype != 1 && dtype != 2) || a.C < 1 || a.C > 4 || a.R * a.S * a.C > kStemKP || a.Cout < 1 ||
       a.OH <= 0 || a.OW <= 0 || a.B <= 0)
     return -1;
   if (static_cast<int64_t>(a.B) * a.OH * a.OW >= (1ll << 31)) return -5;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int M = a.B * a.OH * a.OW;
   const dim3 grid((M + kStemBM - 1) / kStemBM, (a.Cout + kStemBN - 1) / kStemBN);
-  if (a.S > 8) return -1;
+  if (a.S > 8 || a.R > 8) return -1;  // <= 8 x 8 taps: at most 4 (pixel, row) runs per thread
   if (static_cast<int64_t>(a.B) * a.H * a.W * a.C * 2 >= (1ll << 31)) return -5;
   auto launch = [&](auto k) { hipLaunchKernelGGL(k, grid, dim3(256), 0, st, a); };
+  auto by_c = [&](auto tag, auto pro) {
+    using T = decltype(tag);
+    constexpr bool P = decltype(pro)::value;
+    switch (a.C) {
+      case 1: launch(stem_conv_kernel<T, 1, P>); break;
+      case 2: launch(stem_conv_kernel<T, 2, P>); break;
+      case 3: launch(stem_conv_kernel<T, 3, P>); break;
+      default: launch(stem_conv_kernel<T, 4, P>); break;
+    }
+  };
   if (dtype == 1) {
-    switch (a.C) {
-      case 1: launch(stem_conv_kernel<_Float16, 1>); break;
-      case 2: launch(stem_conv_kernel<_Float16, 2>); break;
-      case 3: launch(stem_conv_kernel<_Float16, 3>); break;
-      default: launch(stem_conv_kernel<_Float16, 4>); break;
-    }
+    if (a.in_scale) by_c(_Float16{}, std::true_type{});
+    else by_c(_Float16{}, std::false_type{});
   } else {
-    switch (a.C) {
-      case 1: launch(stem_conv_kernel<__bf16, 1>); break;
-      case 2: launch(stem_conv_kernel<__bf16, 2>); break;
-      case 3: launch(stem_conv_kernel<__bf16, 3>); break;
-      default: launch(stem_conv_kernel<__bf16, 4>); break;
-    }
+    if (a.in_scale) by_c(__bf16{}, std::true_type{});
+    else by_c(__bf16{}, std::false_type{});
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

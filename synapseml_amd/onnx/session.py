@@ -329,6 +329,17 @@ class InferenceSession:
             out_nodes.append(n)
         return self._reorder([n for n in out_nodes if id(n) not in drop])
 
+    def _stem_conv_node(self, n: Node) -> bool:
+        """A _FusedConv the few-channel stem kernel runs (f16 / bf16 GPU session, C <= 4, R, S <= 8,
+        R * S * C <= 160, one group): its input affine can ride the kernel's im2col (padding stays 0)."""
+        if (not _STEM_KERNEL or n.op_type != "_FusedConv" or n.inputs[1] not in self._consts or not self.gpu
+                or self.compute_dtype not in (torch.float16, torch.bfloat16)):
+            return False
+        w = self._consts[n.inputs[1]]
+        return (isinstance(w, torch.Tensor) and w.dim() == 4 and n.attrs.get("group", 1) == 1
+                and 1 <= w.shape[1] <= 4 and w.shape[2] <= 8 and w.shape[3] <= 8
+                and w.shape[1] * w.shape[2] * w.shape[3] <= 160 and n.attrs.get("__act", 0) in (0, 1))
+
     def _mfma_conv(self, n: Node) -> bool:
         """A _FusedConv the MFMA implicit-GEMM kernel runs (2-D, one group, C % 64 == 0, relu-or-none act)."""
         if n.op_type != "_FusedConv" or n.inputs[1] not in self._consts:
@@ -355,7 +366,7 @@ class InferenceSession:
 
         def absorb(value: str, src: str, scale: str, shift: str, relu: bool) -> bool:
             cs = by_input.get(value, [])
-            if value in outs or not cs or not all(self._mfma_conv(c) and c.inputs[0] == value and
+            if value in outs or not cs or not all((self._mfma_conv(c) or self._stem_conv_node(c)) and c.inputs[0] == value and
                                                   c.inputs[1:].count(value) == 0 and len(c.inputs) <= 4
                                                   for c in cs):
                 return False
@@ -794,8 +805,8 @@ def _fused_conv(rt, at, x):
                         out_affine=(f32(post[0]), f32(post[1])) if post is not None else None,
                         f32_mode=rt.session.f32_conv_mode)
         return list(y) if post is not None else [y]
-    if _STEM_KERNEL and pro is None and _stem_kernel_ok(rt, at, inp, w):
-        ys = [_stem_kernel_conv(rt, at, inp, w, b, res, act)]
+    if _STEM_KERNEL and _stem_kernel_ok(rt, at, inp, w):
+        ys = [_stem_kernel_conv(rt, at, inp, w, b, res, act, pro)]
         if post is not None:
             return ys + [_affine_act(rt, ys[0], post[0], post[1], None, 1, 0.0)]
         return ys
@@ -821,7 +832,7 @@ def _stem_kernel_ok(rt, at, inp, w) -> bool:
             and inp.numel() * inp.element_size() < 2 ** 31)
 
 
-def _stem_kernel_conv(rt, at, inp, w, b, res, act):
+def _stem_kernel_conv(rt, at, inp, w, b, res, act, pro=None):
     from ..ops.conv import pack_stem_weight, stem_conv_nhwc
 
     cache = rt.session.__dict__.setdefault("_stem_wk", {})
@@ -831,7 +842,8 @@ def _stem_kernel_conv(rt, at, inp, w, b, res, act):
         wk = cache[key] = pack_stem_weight(w)
     nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
     return stem_conv_nhwc(inp, wk, w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]), dil,
-                          bias=b, relu=2 if act == 1 else 0, res=res)
+                          bias=b, relu=2 if act == 1 else 0, res=res, in_affine=pro,
+                          in_relu=bool(at.get("__pro_relu", 1)))
 
 
 # SML_STEM_MFMA=1: run the 3-channel stem on the packed MFMA form. Off by default: ResNet-50 fp16 measured

@@ -134,9 +134,11 @@ STEM_KP = 160  # padded K of the stem kernel (csrc/nn/conv_mfma.hip stem_conv_ke
 
 
 def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
-    """The dedicated few-channel stem kernel takes f16/bf16 NHWC inputs with C <= 4 and R * S * C <= 160."""
+    """The dedicated few-channel stem kernel takes f16/bf16 NHWC inputs with C <= 4, R, S <= 8 and
+    R * S * C <= 160."""
     return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dim() == 4 and 1 <= x.shape[1] <= 4
-            and w.shape[1] == x.shape[1] and w.shape[3] <= 8 and w.shape[1] * w.shape[2] * w.shape[3] <= STEM_KP)
+            and w.shape[1] == x.shape[1] and w.shape[2] <= 8 and w.shape[3] <= 8
+            and w.shape[1] * w.shape[2] * w.shape[3] <= STEM_KP)
 
 
 def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
@@ -150,10 +152,12 @@ def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
 
 def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
                    bias: Optional[torch.Tensor] = None, relu: int = 0,
-                   res: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = relu?(conv(x, w) + bias (+ res)) for a few-channel input (the image stem): ``x`` [B, C, H, W]
+                   res: Optional[torch.Tensor] = None, in_affine=None, in_relu: bool = False) -> torch.Tensor:
+    """y = relu?(conv(x', w) + bias (+ res)) for a few-channel input (the image stem): ``x`` [B, C, H, W]
     channels_last f16/bf16 with C <= 4, ``wk`` = pack_stem_weight(w). ``relu``: 0 none, 1 before the residual
-    add, 2 after it. ``pad``: (top, left) or (top, left, bottom, right)."""
+    add, 2 after it. ``pad``: (top, left) or (top, left, bottom, right). ``in_affine`` = (scale, shift) per
+    input channel: x' = x * scale + shift (ReLU'd with ``in_relu``) inside the kernel, padding taps 0 - an
+    input BatchNormalization without its own pass."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         x = x.contiguous(memory_format=torch.channels_last)
@@ -168,8 +172,15 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
         res = res.to(x.dtype).contiguous(memory_format=torch.channels_last)
     b32 = None if bias is None else bias.reshape(-1).to(x.device, torch.float32).contiguous()
     geom = [B, H, W, C, cout, r, s, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], oh, ow]
+    sc = sh = None
+    if in_affine is not None:
+        sc = in_affine[0].reshape(-1).to(x.device, torch.float32).contiguous()
+        sh = in_affine[1].reshape(-1).to(x.device, torch.float32).contiguous()
+        if sc.numel() != C or sh.numel() != C:
+            raise ValueError("stem in_affine: one scale / shift per input channel")
     native.load("_nn").stem_conv(x.data_ptr(), wk.data_ptr(), y.data_ptr(), _ptr(b32), _ptr(res), geom, int(relu),
-                                 _DT[x.dtype], torch.cuda.current_stream(x.device).cuda_stream)
+                                 _DT[x.dtype], torch.cuda.current_stream(x.device).cuda_stream, _ptr(sc), _ptr(sh),
+                                 int(bool(in_relu)))
     return y
 
 

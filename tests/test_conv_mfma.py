@@ -358,3 +358,13 @@ def test_stem_kernel_matches_reference(dtype, geom):
     r2 = torch.relu(F.conv2d(xf.float(), wf.float(), bias, st, pd) + res.float())
     tol = 2e-2 if dtype == torch.float16 else 8e-2
     torch.testing.assert_close(y2.float(), r2, rtol=tol, atol=tol)
+    # input affine (+ ReLU) inside the im2col: padding taps stay 0 (the affine of the padded input is not)
+    sc = torch.rand(C, device="cuda") + 0.5
+    sh = torch.randn(C, device="cuda")
+    for in_relu in (False, True):
+        y3 = stem_conv_nhwc(xf, pack_stem_weight(wf), k, k, (st, st), (pd, pd), bias=bias, in_affine=(sc, sh),
+                            in_relu=in_relu)
+        xa = xf.float() * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+        xa = (torch.relu(xa) if in_relu else xa).to(dtype).float()
+        r3 = F.conv2d(xa, wf.float(), bias, st, pd)
+        torch.testing.assert_close(y3.float(), r3, rtol=tol, atol=tol)

@@ -411,6 +411,9 @@ def test_gpu_mfma_fused_resnet_matches_cpu(prec):
     sess = InferenceSession(data, device="cuda", precision=prec)
     fused = [n for n in sess.nodes if n.op_type == "_FusedConv" and len(n.inputs) > 5]
     assert len(fused) >= 16  # pre-activations folded into MFMA conv prologues
+    # the input BatchNormalization rides the stem kernel's im2col (no separate affine pass over the images)
+    stem = [n for n in sess.nodes if sess._stem_conv_node(n)]
+    assert len(stem) == 1 and stem[0].inputs[0] == "data" and len(stem[0].inputs) == 6
     out = sess.run(None, {"data": x})[0].astype(np.float64)
     # relative L2 error of the logits vs the fp32 host graph: measured 7.3e-4 (fp16) / 5.4e-3 (bf16) on
     # MI355X, i.e. the rounding of the storage format; a wrong fusion (dropped bias, BN or residual) is O(1)
