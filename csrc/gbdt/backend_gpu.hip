@@ -486,6 +486,12 @@ __device__ void LambdarankQuery(const RankTables& t, int q, const double* __rest
   __syncthreads();  // LDS reuse by the next query
 }
 
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ double ReadLaneD(double v, int l) {
   const long long x = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
@@ -503,8 +509,10 @@ __device__ __forceinline__ double ReadLaneD(double v, int l) {
 template <int NU>  // documents per lane: cnt <= 64 * NU
 __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __restrict__ score,
                                     const float* __restrict__ label, const float* __restrict__ weight,
-                                    float* __restrict__ g, float* __restrict__ h, const double* s_disc) {
-  const int lane = threadIdx.x;
+                                    float* __restrict__ g, float* __restrict__ h, const double* s_disc,
+                                    int* s_doc_of_rank) {
+  // one wave per query (its own 64-entry rank -> doc map; wave-level syncs only)
+  const int lane = threadIdx.x & 63;
   const int b = t.qb[q], cnt = t.qb[q + 1] - b;
   const int ntop = min(cnt, t.max_position);
   double sc[NU];
@@ -558,18 +566,17 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   int tlab = 0, tdoc = 0;
   float tgn = 0.f;
   {
-    __shared__ int s_doc_of_rank[64];
 #pragma unroll
     for (int u = 0; u < NU; ++u)
       if (u * 64 + lane < cnt && rk[u] < ntop) s_doc_of_rank[rk[u]] = u * 64 + lane;
-    __syncthreads();
+    WaveSync();
     if (lane < ntop) {
       tdoc = s_doc_of_rank[lane];
       tsc = score[b + tdoc];
       tlab = static_cast<int>(label[b + tdoc]);
       tgn = static_cast<float>(t.gain[min(static_cast<unsigned>(tlab), gtop)]);
     }
-    __syncthreads();
+    WaveSync();  // the map is read before the next query of this wave rewrites it
   }
   const float tdc = static_cast<float>(s_disc[lane]);  // discount of rank `lane` (valid for lane < ntop)
   const float sig = static_cast<float>(t.sigma);
@@ -636,25 +643,30 @@ __device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
   return cnt <= kRankLds && t.max_position <= 64;
 }
 
-// The common case on its own kernel: its LDS is the discount table and the
-// 64-entry rank->doc map (2.3 KB instead of the LDS path's 11.5 KB), so the
-// one-wave blocks are VGPR-limited (4 waves/SIMD) rather than LDS-limited.
-__global__ __launch_bounds__(64) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
-                                                             const float* __restrict__ label,
-                                                             const float* __restrict__ weight, float* __restrict__ g,
-                                                             float* __restrict__ h) {
+// The common case on its own kernel: its LDS is the discount table and one 64-entry rank->doc map per
+// wave (2 KB + 256 B per wave instead of the LDS path's 11.5 KB). kWaves independent waves per block, each
+// walking its own queries: a CU holds at most 16 workgroups, so one-wave blocks capped the kernel at 4
+// waves per SIMD although its 48 VGPRs allow 10 - and every wave here is latency-bound (readlane
+// broadcasts, cross-lane sums), so resident waves are its throughput.
+template <int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
+                                                                      const float* __restrict__ label,
+                                                                      const float* __restrict__ weight,
+                                                                      float* __restrict__ g, float* __restrict__ h) {
   __shared__ double s_disc[kRankLds];
-  for (int r = threadIdx.x; r < kRankLds; r += 64) s_disc[r] = 1.0 / log2(2.0 + r);
+  __shared__ int s_map[kWaves][64];
+  for (int r = threadIdx.x; r < kRankLds; r += 64 * kWaves) s_disc[r] = 1.0 / log2(2.0 + r);
   __syncthreads();
+  const int wid = threadIdx.x >> 6;
   // documents per lane sized to the query: the pair loops run NU-wide, so a 100-document query
   // costs half of what the kRankLds-wide form would
-  for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
+  for (int q = blockIdx.x * kWaves + wid; q < t.nq; q += gridDim.x * kWaves) {
     const int cnt = t.qb[q + 1] - t.qb[q];
     if (cnt <= 0 || !RegsEligible(t, cnt)) continue;
-    if (cnt <= 64) LambdarankQueryRegs<1>(t, q, score, label, weight, g, h, s_disc);
-    else if (cnt <= 128) LambdarankQueryRegs<2>(t, q, score, label, weight, g, h, s_disc);
-    else if (cnt <= 192) LambdarankQueryRegs<3>(t, q, score, label, weight, g, h, s_disc);
-    else LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc);
+    if (cnt <= 64) LambdarankQueryRegs<1>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    else if (cnt <= 128) LambdarankQueryRegs<2>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    else if (cnt <= 192) LambdarankQueryRegs<3>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    else LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
   }
 }
 
@@ -2123,12 +2135,6 @@ __device__ __forceinline__ int BatchSmallCount(const BState* bs, int j) {
   return x.left_small ? lt : x.pcount - lt;
 }
 
-__device__ __forceinline__ void WaveSync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 struct SimKey {  // frontier entry order: larger gain, then smaller leaf index (the sequential argmax)
   double gain;
   int li, idx;
@@ -2909,6 +2915,7 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
     if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
     if (const char* e = std::getenv("SML_GBDT_HIST_PIPE")) hist_pipe_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SML_RANK_WAVES")) rank_waves_ = std::atoi(e) == 1 ? 1 : 4;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -3074,8 +3081,14 @@ class GpuBackend : public TrainBackend {
       if (rank_.nq > 0) {
         const int grid = std::min(rank_.nq, 65536);
         if (rank_regs_) {
-          hipLaunchKernelGGL(lambdarank_regs_kernel, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(),
-                             label_.get(), weight_.get(), g_.get(), h_.get());
+          if (rank_waves_ == 1) {
+            hipLaunchKernelGGL(lambdarank_regs_kernel<1>, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(),
+                               label_.get(), weight_.get(), g_.get(), h_.get());
+          } else {
+            const int g4 = std::max(1, std::min((rank_.nq + 3) / 4, 16384));
+            hipLaunchKernelGGL(lambdarank_regs_kernel<4>, dim3(g4), dim3(256), 0, stream_, rank_, score_.get(),
+                               label_.get(), weight_.get(), g_.get(), h_.get());
+          }
           SML_HIP_CHECK(hipGetLastError());
         }
         if (rank_lds_) {
@@ -3790,6 +3803,7 @@ class GpuBackend : public TrainBackend {
   int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
   bool hist_unroll4_ = false;     // SML_HIST_UNROLL=4: 4 gathered rows in flight per thread (A/B knob)
   bool hist_pipe_ = false;        // SML_GBDT_HIST_PIPE=1: software-pipelined histogram loops (A/B knob)
+  int rank_waves_ = 4;            // lambdarank register kernel: waves per block (SML_RANK_WAVES=1: one)
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
   DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident

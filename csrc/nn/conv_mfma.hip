@@ -1212,6 +1212,147 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   ConvEpilogue<T, 32, 64, 1>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
+// Row-run form of the stem (C = 3, S * C <= 24, R <= 8: the 7x7 RGB stem). The b16 gathers above keep the
+// texture path busy ~33 cycles per 64-lane load (r4 pass 10 counters: TA 75 %, TD 84 % busy over the
+// kernel, 105 load instructions per wave), so here every (pixel, filter row) run is fetched as the
+// enclosing 64 aligned bytes (4 x 16-B buffer loads, 5x fewer instructions, 8x the bytes each) and
+// shifted into place in registers (dword selects + v_alignbyte). K is packed per filter row to RP = 24
+// (k = r * 24 + s * 3 + c, weights zero in slots s * 3 + c >= S * C), so each run lands as 3 aligned
+// 16-B LDS stores; K = R * 24 padded to 192 (6 MFMA k-steps; the MFMAs are ~5 % of the kernel).
+// Row pitch 208 elements (416 B: the 16 rows x 2 chunks of a b128 fragment group hit 16 distinct slots).
+constexpr int kWideRP = 24, kWideKP = 192, kWideLd = kWideKP + 16;
+
+template <class T, bool kPro>
+__global__ __launch_bounds__(256) void stem_wide_kernel(ConvArgs a) {
+  typedef typename Vec<T>::type V8;
+  constexpr int C = 3;
+  constexpr int kOpElems = (kStemBM + kStemBN) * kWideLd;
+  __shared__ __attribute__((aligned(16))) T lds[kOpElems];
+  T* As = lds;                      // [128][208]: im2col rows, run r at r * 24
+  T* Bs = lds + kStemBM * kWideLd;  // [64][208]: weights
+  const int tid = threadIdx.x;
+  const int M = a.B * a.OH * a.OW;
+  const int m0 = blockIdx.x * kStemBM, n0 = blockIdx.y * kStemBN;
+  const int S = a.S, R = a.R, SC = S * C, K = R * kWideRP;
+  const T* __restrict__ w = static_cast<const T*>(a.w);
+  for (int q = tid; q < kStemBN * (kWideKP / 8); q += 256) {
+    const int row = q / (kWideKP / 8), ch = q % (kWideKP / 8);
+    const int n = n0 + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < a.Cout) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kWideKP + ch * 8);
+    *reinterpret_cast<uint4*>(Bs + row * kWideLd + ch * 8) = v;
+  }
+  // K tail beyond R * 24 (whole 16-B chunks: 24 is a multiple of 8)
+  {
+    const int c0 = K / 8, nch = kWideKP / 8 - c0;
+    for (int q = tid; q < kStemBM * nch; q += 256) {
+      const int row = q / nch, ch = c0 + q % nch;
+      *reinterpret_cast<uint4*>(As + row * kWideLd + ch * 8) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  // records rounded up to the 16-B chunk: a chunk holding the input's last bytes loads whole (the few bytes
+  // past the end land in masked slots; the caching allocator's blocks are 512-B granular)
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, (a.B * a.H * a.W * C * static_cast<int>(sizeof(T)) + 15) & ~15, 0x00020000);
+  constexpr uint32_t kOob = 0x80000000u;
+  float psc[C], psh[C];
+  if constexpr (kPro) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+  }
+  constexpr int kRuns = (kStemBM * 8 + 255) / 256;  // R <= 8
+  uint32_t win[kRuns][16];
+  int dsto[kRuns], iw0s[kRuns], shs[kRuns];
+  bool rows_ok[kRuns];
+#pragma unroll
+  for (int u = 0; u < kRuns; ++u) {
+    const int q = tid + u * 256;
+    const int ml = q / R, r = q - ml * R;
+    const int m = m0 + ml;
+    const bool live = q < kStemBM * R && m < M;
+    dsto[u] = live ? ml * kWideLd + r * kWideRP : -1;
+    const int mm = live ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW;
+    const int oh = t2 % a.OH, b = t2 / a.OH;
+    const int ih = oh * a.stride_h - a.pad_h + r * a.dil_h;
+    const int iw0 = ow * a.stride_w - a.pad_w;
+    rows_ok[u] = live && ih >= 0 && ih < a.H;
+    iw0s[u] = iw0;
+    const int byte0 = (((b * a.H + ih) * a.W + iw0) * C) * static_cast<int>(sizeof(T));  // may be < 0 at the border
+    const int base = byte0 & ~15;
+    shs[u] = byte0 - base;  // 0..14, even
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = base + 16 * k;
+      const uint32_t off = rows_ok[u] && o >= 0 ? static_cast<uint32_t>(o) : kOob;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xres, off, 0, 0);
+      win[u][4 * k] = v[0]; win[u][4 * k + 1] = v[1]; win[u][4 * k + 2] = v[2]; win[u][4 * k + 3] = v[3];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kRuns; ++u) {
+    if (dsto[u] < 0) continue;
+    // shift the window left by shs bytes: dword rotation by shs >> 2 (two select levels), then 0 / 2 bytes
+    const int dsh = shs[u] >> 2;
+    const uint32_t sb = static_cast<uint32_t>(shs[u] & 3);
+    uint32_t v1[15], v2[13], o[12];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) v1[k] = (dsh & 1) ? win[u][k + 1] : win[u][k];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) v2[k] = (dsh & 2) ? v1[k + 2] : v1[k];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) o[i] = __builtin_amdgcn_alignbyte(v2[i + 1], v2[i], sb);
+    // element e = s * 3 + c of the run: real iff e < S * C, the row is in range and 0 <= iw0 + s < W
+    const int iw0 = iw0s[u];
+    const bool rok = rows_ok[u];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      uint32_t outw = 0;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int e = 2 * i + hh;
+        const int iw = iw0 + e / C;
+        const bool ok = rok && e < SC && iw >= 0 && iw < a.W;
+        const uint32_t bits = (o[i] >> (16 * hh)) & 0xFFFFu;
+        uint32_t val = ok ? bits : 0u;
+        if constexpr (kPro) {
+          const float t = ToF(__builtin_bit_cast(T, static_cast<unsigned short>(bits))) * psc[e % C] + psh[e % C];
+          val = ok ? static_cast<uint32_t>(__builtin_bit_cast(unsigned short, FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t))) : 0u;
+        }
+        outw |= val << (16 * hh);
+      }
+      o[i] = outw;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(As + dsto[u]);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    dst[2] = make_uint4(o[8], o[9], o[10], o[11]);
+  }
+  __syncthreads();
+  const int lane = tid & 63, wid = tid >> 6;
+  constexpr int TM = 2, TN = 4;
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int wm0 = wid * 32, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int ks = 0; ks < kWideKP / 32; ++ks) {
+    V8 af[TM], bf[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const V8*>(As + (wm0 + i * 16 + fr) * kWideLd + ks * 32 + fk);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const V8*>(Bs + (j * 16 + fr) * kWideLd + ks * 32 + fk);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+  }
+  __syncthreads();
+  ConvEpilogue<T, 32, 64, 1>(a, acc, lds, M, m0, n0, wid, lane);
+}
+
 }  // namespace
 
 template <class T>
@@ -1224,7 +1365,26 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
 
 // few-channel stem: x NHWC with C <= 4, w packed [Cout][160] (k = (r * S + s) * C + c, zero-padded),
 // R * S * C <= 160, f16 (dtype 1) / bf16 (2)
-int StemConv(const ConvArgs& a, int dtype, void* stream) {
+int StemConv(const ConvArgs& a, int dtype, void* stream, int kp) {
+  if (kp == kWideKP) {  // row-run form: weights packed [Cout][192], k = r * 24 + s * 3 + c
+    if ((dtype != 1 && dtype != 2) || a.C != 3 || a.S * 3 > kWideRP || a.R > 8 || a.Cout < 1 || a.OH <= 0 ||
+        a.OW <= 0 || a.B <= 0)
+      return -1;
+    if (static_cast<int64_t>(a.B) * a.OH * a.OW >= (1ll << 31)) return -5;
+    if (static_cast<int64_t>(a.B) * a.H * a.W * 3 * 2 >= (1ll << 31) - 64) return -5;
+    const int M = a.B * a.OH * a.OW;
+    const dim3 grid((M + kStemBM - 1) / kStemBM, (a.Cout + kStemBN - 1) / kStemBN);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (dtype == 1) {
+      if (a.in_scale) hipLaunchKernelGGL((stem_wide_kernel<_Float16, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((stem_wide_kernel<_Float16, false>), grid, dim3(256), 0, st, a);
+    } else {
+      if (a.in_scale) hipLaunchKernelGGL((stem_wide_kernel<__bf16, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((stem_wide_kernel<__bf16, false>), grid, dim3(256), 0, st, a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
+  if (kp != kStemKP) return -1;
   if ((dtype != 1 && dtype != 2) || a.C < 1 || a.C > 4 || a.R * a.S * a.C > kStemKP || a.Cout < 1 ||
       a.OH <= 0 || a.OW <= 0 || a.B <= 0)
     return -1;

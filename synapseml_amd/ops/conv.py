@@ -141,9 +141,31 @@ def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[1] * w.shape[2] * w.shape[3] <= STEM_KP)
 
 
-def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
-    """[Cout, C, R, S] -> [Cout, 160] with k = (r * S + s) * C + c, zero-padded (packed once per weight)."""
+STEM_WIDE_KP, STEM_WIDE_RP = 192, 24  # the row-run stem form (C = 3, S * 3 <= 24, R <= 8)
+
+
+def stem_wide(w: torch.Tensor) -> bool:
+    """The 3-channel stems (7x7 RGB) run on the row-run kernel: each (pixel, filter row) run of S * 3 input
+    values is fetched as aligned 16-B chunks instead of 2-byte gathers."""
+    return w.shape[1] == 3 and w.shape[3] * 3 <= STEM_WIDE_RP and w.shape[2] <= 8
+
+
+def pack_stem_weight(w: torch.Tensor, wide: Optional[bool] = None) -> torch.Tensor:
+    """[Cout, C, R, S] -> [Cout, 160] with k = (r * S + s) * C + c, zero-padded; for the row-run form
+    (``stem_wide``) [Cout, 192] with k = r * 24 + s * 3 + c, zero in every slot s * 3 + c >= S * 3 and past
+    R * 24 (packed once per weight)."""
     cout = w.shape[0]
+    if wide is None:
+        wide = stem_wide(w)
+    if wide:
+        if not stem_wide(w):
+            raise ValueError("row-run stem packing: C = 3, S * 3 <= 24, R <= 8")
+        R, S = w.shape[2], w.shape[3]
+        out = torch.zeros((cout, R, STEM_WIDE_RP), dtype=w.dtype, device=w.device)
+        out[:, :, :S * 3] = w.permute(0, 2, 3, 1).reshape(cout, R, S * 3)
+        full = torch.zeros((cout, STEM_WIDE_KP), dtype=w.dtype, device=w.device)
+        full[:, :R * STEM_WIDE_RP] = out.reshape(cout, -1)
+        return full
     k = w.permute(0, 2, 3, 1).reshape(cout, -1)
     out = torch.zeros((cout, STEM_KP), dtype=w.dtype, device=w.device)
     out[:, :k.shape[1]] = k
@@ -161,8 +183,10 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         x = x.contiguous(memory_format=torch.channels_last)
-    if wk.dim() != 2 or wk.shape[1] != STEM_KP or wk.dtype != x.dtype or not wk.is_contiguous():
+    if wk.dim() != 2 or wk.shape[1] not in (STEM_KP, STEM_WIDE_KP) or wk.dtype != x.dtype or not wk.is_contiguous():
         raise ValueError("stem weight must be pack_stem_weight(w) in the input dtype")
+    if wk.shape[1] == STEM_WIDE_KP and (C != 3 or s * 3 > STEM_WIDE_RP or r > 8):
+        raise ValueError("row-run stem weight for a different filter shape")
     if C * r * s > STEM_KP or C > 4:
         raise ValueError("stem kernel: C <= 4 and R * S * C <= 160")
     cout = wk.shape[0]
@@ -180,12 +204,12 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
             raise ValueError("stem in_affine: one scale / shift per input channel")
     native.load("_nn").stem_conv(x.data_ptr(), wk.data_ptr(), y.data_ptr(), _ptr(b32), _ptr(res), geom, int(relu),
                                  _DT[x.dtype], torch.cuda.current_stream(x.device).cuda_stream, _ptr(sc), _ptr(sh),
-                                 int(bool(in_relu)))
+                                 int(bool(in_relu)), int(wk.shape[1]))
     return y
 
 
 __all__ = ["supported", "pack_weight", "split_weight", "conv2d_nhwc", "out_hw", "F32_MODES", "stem_supported",
-           "pack_stem_weight", "stem_conv_nhwc"]
+           "pack_stem_weight", "stem_conv_nhwc", "stem_wide"]
 
 
 def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),

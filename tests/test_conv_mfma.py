@@ -336,6 +336,8 @@ def test_fp32_presplit_weight_planes_bitwise(mode):
     (3, 3, 37, 29, 64, 7, 2, 3),     # partial pixel tiles, padding on every border
     (2, 4, 19, 23, 128, 5, 1, 2),    # two 64-channel tiles, C = 4
     (2, 1, 16, 16, 80, 3, 1, 1),     # a partial channel tile
+    (2, 3, 33, 31, 64, 5, 1, 2),     # 3 channels, 5x5 stride 1: row runs of 15 values, odd row byte offsets
+    (1, 3, 17, 9, 64, 3, 3, 0),      # 3x3 stride 3 unpadded
 ])
 def test_stem_kernel_matches_reference(dtype, geom):
     """Dedicated few-channel stem kernel (im2col rows in LDS, K padded to 160) vs the fp32 reference, with
@@ -349,6 +351,9 @@ def test_stem_kernel_matches_reference(dtype, geom):
     y = stem_conv_nhwc(x, pack_stem_weight(w), k, k, (st, st), (pd, pd))
     ref = F.conv2d(x.float(), w.float(), None, st, pd)
     torch.testing.assert_close(y.float(), ref.to(dtype).float(), rtol=0, atol=0)  # exact sum, one rounding
+    if C == 3:  # the row-run form (default for 3 channels) and the 2-byte gather form agree exactly
+        yn = stem_conv_nhwc(x, pack_stem_weight(w, wide=False), k, k, (st, st), (pd, pd))
+        torch.testing.assert_close(yn.float(), ref.to(dtype).float(), rtol=0, atol=0)
     torch.manual_seed(6)
     xf = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
     wf = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)

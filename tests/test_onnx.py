@@ -600,12 +600,23 @@ def test_conv_split_k_plan():
 
 
 def test_stem_weight_packing_order():
-    """pack_stem_weight: k = (r * S + s) * C + c, zero tail to 160 (the stem kernel's im2col order)."""
-    from synapseml_amd.ops.conv import STEM_KP, pack_stem_weight
+    """pack_stem_weight: k = (r * S + s) * C + c, zero tail to 160 (the stem kernel's im2col order); the
+    3-channel row-run form: k = r * 24 + s * 3 + c, zero in the slots past S * 3 and past R * 24."""
+    from synapseml_amd.ops.conv import STEM_KP, STEM_WIDE_KP, pack_stem_weight, stem_wide
 
-    w = torch.arange(2 * 3 * 7 * 7, dtype=torch.float32).reshape(2, 3, 7, 7)
+    w = torch.arange(2 * 4 * 5 * 5, dtype=torch.float32).reshape(2, 4, 5, 5)
+    assert not stem_wide(w)
     wk = pack_stem_weight(w)
     assert wk.shape == (2, STEM_KP)
-    r, s_, c = 4, 5, 2
-    assert wk[1, (r * 7 + s_) * 3 + c] == w[1, c, r, s_]
-    assert torch.all(wk[:, 147:] == 0)
+    r, s_, c = 4, 3, 2
+    assert wk[1, (r * 5 + s_) * 4 + c] == w[1, c, r, s_]
+    assert torch.all(wk[:, 100:] == 0)
+    w7 = torch.arange(2 * 3 * 7 * 7, dtype=torch.float32).reshape(2, 3, 7, 7) + 1
+    assert stem_wide(w7)
+    wk7 = pack_stem_weight(w7)
+    assert wk7.shape == (2, STEM_WIDE_KP)
+    for (r, s_, c) in ((0, 0, 0), (4, 5, 2), (6, 6, 1)):
+        assert wk7[1, r * 24 + s_ * 3 + c] == w7[1, c, r, s_]
+    lay = wk7.reshape(2, 8, 24)
+    assert torch.all(lay[:, :7, 21:] == 0) and torch.all(lay[:, 7:] == 0)
+    assert int((wk7 != 0).sum()) == w7.numel()
