@@ -645,9 +645,8 @@ __device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
 
 // The common case on its own kernel: its LDS is the discount table and one 64-entry rank->doc map per
 // wave (2 KB + 256 B per wave instead of the LDS path's 11.5 KB). kWaves independent waves per block, each
-// walking its own queries: a CU holds at most 16 workgroups, so one-wave blocks capped the kernel at 4
-// waves per SIMD although its 48 VGPRs allow 10 - and every wave here is latency-bound (readlane
-// broadcasts, cross-lane sums), so resident waves are its throughput.
+// walking its own queries (a CU holds at most 16 workgroups, so one-wave blocks cap residency at 4 waves
+// per SIMD; kWaves = 4 lifts that, but measured slower - see rank_waves_).
 template <int kWaves>
 __global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
                                                                       const float* __restrict__ label,
@@ -2915,7 +2914,7 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
     if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
     if (const char* e = std::getenv("SML_GBDT_HIST_PIPE")) hist_pipe_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SML_RANK_WAVES")) rank_waves_ = std::atoi(e) == 1 ? 1 : 4;
+    if (const char* e = std::getenv("SML_RANK_WAVES")) rank_waves_ = std::atoi(e) == 4 ? 4 : 1;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -3803,7 +3802,10 @@ class GpuBackend : public TrainBackend {
   int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
   bool hist_unroll4_ = false;     // SML_HIST_UNROLL=4: 4 gathered rows in flight per thread (A/B knob)
   bool hist_pipe_ = false;        // SML_GBDT_HIST_PIPE=1: software-pipelined histogram loops (A/B knob)
-  int rank_waves_ = 4;            // lambdarank register kernel: waves per block (SML_RANK_WAVES=1: one)
+  // lambdarank register kernel: waves per block. SML_RANK_WAVES=4 packs 4 independent waves per block (up
+  // to 10 resident per SIMD instead of 4): r4 pass 11 measured it slower (949 vs 860 us per call, ranker
+  // fit 33.6M vs 34.0M rows/s), so one-wave blocks stay the default
+  int rank_waves_ = 1;
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
   DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident

@@ -142,11 +142,15 @@ def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 STEM_WIDE_KP, STEM_WIDE_RP = 192, 24  # the row-run stem form (C = 3, S * 3 <= 24, R <= 8)
+# SML_STEM_ROWRUN=1 makes the row-run form the default for 3-channel stems. Off: r4 pass 11 measured it at
+# 426 us per ResNet-50 batch of 128 against 330 us for the 2-byte gathers - the texture path moves ~4 B per
+# clock per CU for these scattered accesses whatever the width, and the 64-B windows fetch 1.5x the bytes.
+_STEM_ROWRUN = os.environ.get("SML_STEM_ROWRUN", "0") == "1"
 
 
 def stem_wide(w: torch.Tensor) -> bool:
-    """The 3-channel stems (7x7 RGB) run on the row-run kernel: each (pixel, filter row) run of S * 3 input
-    values is fetched as aligned 16-B chunks instead of 2-byte gathers."""
+    """Whether a stem weight fits the row-run kernel (C = 3, S * 3 <= 24, R <= 8): each (pixel, filter row)
+    run of S * 3 input values fetched as aligned 16-B chunks instead of 2-byte gathers."""
     return w.shape[1] == 3 and w.shape[3] * 3 <= STEM_WIDE_RP and w.shape[2] <= 8
 
 
@@ -156,7 +160,7 @@ def pack_stem_weight(w: torch.Tensor, wide: Optional[bool] = None) -> torch.Tens
     R * 24 (packed once per weight)."""
     cout = w.shape[0]
     if wide is None:
-        wide = stem_wide(w)
+        wide = _STEM_ROWRUN and stem_wide(w)
     if wide:
         if not stem_wide(w):
             raise ValueError("row-run stem packing: C = 3, S * 3 <= 24, R <= 8")

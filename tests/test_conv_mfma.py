@@ -351,9 +351,9 @@ def test_stem_kernel_matches_reference(dtype, geom):
     y = stem_conv_nhwc(x, pack_stem_weight(w), k, k, (st, st), (pd, pd))
     ref = F.conv2d(x.float(), w.float(), None, st, pd)
     torch.testing.assert_close(y.float(), ref.to(dtype).float(), rtol=0, atol=0)  # exact sum, one rounding
-    if C == 3:  # the row-run form (default for 3 channels) and the 2-byte gather form agree exactly
-        yn = stem_conv_nhwc(x, pack_stem_weight(w, wide=False), k, k, (st, st), (pd, pd))
-        torch.testing.assert_close(yn.float(), ref.to(dtype).float(), rtol=0, atol=0)
+    if C == 3:  # the row-run form (SML_STEM_ROWRUN) and the 2-byte gather form agree exactly
+        yw = stem_conv_nhwc(x, pack_stem_weight(w, wide=True), k, k, (st, st), (pd, pd))
+        torch.testing.assert_close(yw.float(), ref.to(dtype).float(), rtol=0, atol=0)
     torch.manual_seed(6)
     xf = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
     wf = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)

@@ -613,7 +613,8 @@ def test_stem_weight_packing_order():
     assert torch.all(wk[:, 100:] == 0)
     w7 = torch.arange(2 * 3 * 7 * 7, dtype=torch.float32).reshape(2, 3, 7, 7) + 1
     assert stem_wide(w7)
-    wk7 = pack_stem_weight(w7)
+    assert pack_stem_weight(w7).shape == (2, STEM_KP)  # the gather form unless SML_STEM_ROWRUN=1
+    wk7 = pack_stem_weight(w7, wide=True)
     assert wk7.shape == (2, STEM_WIDE_KP)
     for (r, s_, c) in ((0, 0, 0), (4, 5, 2), (6, 6, 1)):
         assert wk7[1, r * 24 + s_ * 3 + c] == w7[1, c, r, s_]

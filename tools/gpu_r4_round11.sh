@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest -v --timeout 120 --timeout-method thread t
 rc=$?
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python tools/stem_probe.py 128 20 > "$OUT/stem_probe.log" 2>&1 || exit 1
-timeout -k 10 300 python tools/bench_onnx.py --batches 128 --precisions fp16,bf16 --images 0 > "$OUT/bench_onnx.log" 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_onnx.py --batches 128,256 --precisions fp16,bf16 --images 0 > "$OUT/bench_onnx.log" 2>&1 || exit 1
 timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker.log" 2>&1 || exit 1
 SML_RANK_WAVES=1 timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker_w1.log" 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
