@@ -1212,6 +1212,120 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   ConvEpilogue<T, 32, 64, 1>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
+// Row-staged form of the stem: one block per output row (OW <= 128 pixels, C = 3, dilation 1). The R input
+// rows the block reads are staged once in LDS by coalesced 16-B loads (zero columns of padding either side,
+// zero rows out of range), and the im2col runs are built from LDS. The 2-byte gather form moves every input
+// value ~R * S / (sh * sw) = 12 times through the texture path, which runs at ~4 B per clock per CU for
+// scattered accesses (r4 passes 10-11: TA 75 % busy, 33 cycles per 64-lane gather); here each value
+// crosses it once per block and the replication happens in LDS. With kPro the input affine (+ ReLU) is
+// applied once per staged value; padding stays 0. Weights and the K order are the gather form's
+// ([Cout][160], k = (r * S + s) * 3 + c); M rows past OW are computed and not stored.
+constexpr int kRowPad = 8;  // zero columns staged either side of an input row (pad_w <= 8)
+
+template <class T, bool kPro>
+__global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
+  typedef typename Vec<T>::type V8;
+  constexpr int C = 3;
+  __shared__ __attribute__((aligned(16))) T lds[(kStemBM + kStemBN) * kStemLd];
+  extern __shared__ __attribute__((aligned(16))) unsigned char stem_dyn_smem[];
+  T* rowbuf = reinterpret_cast<T*>(stem_dyn_smem);  // [R][(W + 16) * 3], dynamic LDS
+  T* As = lds;
+  T* Bs = lds + kStemBM * kStemLd;
+  const int tid = threadIdx.x;
+  const int orow = blockIdx.x;  // b * OH + oh
+  const int oh = orow % a.OH, b = orow / a.OH;
+  const int m0 = orow * a.OW, n0 = blockIdx.y * kStemBN;
+  const int S = a.S, R = a.R, run = S * C, K = R * run;
+  const int SP = (a.W + 2 * kRowPad) * C;  // slot pitch (halfs), a multiple of 8
+  const T* __restrict__ w = static_cast<const T*>(a.w);
+  for (int q = tid; q < kStemBN * (kStemKP / 8); q += 256) {
+    const int row = q / (kStemKP / 8), ch = q % (kStemKP / 8);
+    const int n = n0 + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < a.Cout) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + ch * 8);
+    *reinterpret_cast<uint4*>(Bs + row * kStemLd + ch * 8) = v;
+  }
+  {
+    const int c0 = K / 8, nch = kStemKP / 8 - c0;
+    for (int q = tid; q < kStemBM * nch; q += 256) {
+      const int row = q / nch, ch = c0 + q % nch;
+      *reinterpret_cast<uint4*>(As + row * kStemLd + ch * 8) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  // stage the R input rows: chunk j of slot r holds halfs [8j, 8j + 8) = columns (8j + i) / 3 - kRowPad
+  {
+    const T* __restrict__ x = static_cast<const T*>(a.x);
+    const int cps = SP / 8, d0 = kRowPad * C / 8, d1 = d0 + a.W * C / 8;  // data chunks [d0, d1)
+    float psc[C], psh[C];
+    if constexpr (kPro) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+    }
+    for (int q = tid; q < R * cps; q += 256) {
+      const int r = q / cps, j = q - r * cps;
+      const int ih = oh * a.stride_h - a.pad_h + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ih >= 0 && ih < a.H && j >= d0 && j < d1) {
+        v = *reinterpret_cast<const uint4*>(x + (static_cast<int64_t>(b) * a.H + ih) * a.W * C + (j - d0) * 8);
+        if constexpr (kPro) {
+          T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int c = (j * 8 + i) % C;
+            const float t = ToF(e[i]) * psc[c] + psh[c];
+            e[i] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
+          }
+        }
+      }
+      *reinterpret_cast<uint4*>(rowbuf + r * SP + j * 8) = v;
+    }
+  }
+  __syncthreads();
+  // im2col runs from LDS: thread -> (filter row r, pixel ml), consecutive lanes on consecutive pixels
+  for (int q = tid; q < R * kStemBM; q += 256) {
+    const int r = q >> 7, ml = q & (kStemBM - 1);
+    if (ml >= a.OW) continue;
+    const int h0 = (ml * a.stride_w - a.pad_w + kRowPad) * C;
+    const unsigned short* src = reinterpret_cast<const unsigned short*>(rowbuf + r * SP + h0);
+    unsigned short* dst = reinterpret_cast<unsigned short*>(As + ml * kStemLd + r * run);
+#pragma unroll
+    for (int e = 0; e < 8 * C; ++e)
+      if (e < run) dst[e] = src[e];
+  }
+  __syncthreads();
+  const int lane = tid & 63, wid = tid >> 6;
+  constexpr int TM = 2, TN = 4;
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int wm0 = wid * 32, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int ks = 0; ks < kStemKP / 32; ++ks) {
+    V8 af[TM], bf[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const V8*>(As + (wm0 + i * 16 + fr) * kStemLd + ks * 32 + fk);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const V8*>(Bs + (j * 16 + fr) * kStemLd + ks * 32 + fk);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+  }
+  __syncthreads();
+  ConvEpilogue<T, 32, 64, 1>(a, acc, lds, m0 + a.OW, m0, n0, wid, lane);  // rows past OW are not stored
+}
+
+// the row-staged form's shapes: 3 channels, one block per output row, 16-B aligned input rows, padding and
+// dilation it stages, and its LDS (static operand tiles + R staged rows) within two blocks per CU
+inline int RowbufLds(const ConvArgs& a) { return a.R * (a.W + 2 * kRowPad) * 3 * 2; }
+inline bool RowbufOk(const ConvArgs& a) {
+  return a.C == 3 && a.OW <= kStemBM && a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= kRowPad && a.R <= 8 && a.S <= 8 &&
+         (a.W * 3 * 2) % 16 == 0 && (a.OW - 1) * a.stride_w - a.pad_w + a.S <= a.W + kRowPad &&
+         RowbufLds(a) <= 12 * 1024;
+}
+
 // Row-run form of the stem (C = 3, S * C <= 24, R <= 8: the 7x7 RGB stem). The b16 gathers above keep the
 // texture path busy ~33 cycles per 64-lane load (r4 pass 10 counters: TA 75 %, TD 84 % busy over the
 // kernel, 105 load instructions per wave), so here every (pixel, filter row) run is fetched as the
@@ -1365,7 +1479,7 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
 
 // few-channel stem: x NHWC with C <= 4, w packed [Cout][160] (k = (r * S + s) * C + c, zero-padded),
 // R * S * C <= 160, f16 (dtype 1) / bf16 (2)
-int StemConv(const ConvArgs& a, int dtype, void* stream, int kp) {
+int StemConv(const ConvArgs& a, int dtype, void* stream, int kp, int form) {
   if (kp == kWideKP) {  // row-run form: weights packed [Cout][192], k = r * 24 + s * 3 + c
     if ((dtype != 1 && dtype != 2) || a.C != 3 || a.S * 3 > kWideRP || a.R > 8 || a.Cout < 1 || a.OH <= 0 ||
         a.OW <= 0 || a.B <= 0)
@@ -1385,6 +1499,22 @@ int StemConv(const ConvArgs& a, int dtype, void* stream, int kp) {
     return hipGetLastError() == hipSuccess ? 0 : -3;
   }
   if (kp != kStemKP) return -1;
+  // the row-staged form where it applies (form 0 = auto, 1 = 2-byte gathers, 2 = row-staged)
+  if (form != 1 && RowbufOk(a) && (dtype == 1 || dtype == 2) && a.Cout >= 1 && a.B > 0 && a.OH > 0 &&
+      static_cast<int64_t>(a.B) * a.OH * a.OW < (1ll << 31) && static_cast<int64_t>(a.B) * a.H * a.W * 3 < (1ll << 31)) {
+    const dim3 grid(a.B * a.OH, (a.Cout + kStemBN - 1) / kStemBN);
+    const size_t dyn = static_cast<size_t>(RowbufLds(a));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (dtype == 1) {
+      if (a.in_scale) hipLaunchKernelGGL((stem_rowbuf_kernel<_Float16, true>), grid, dim3(256), dyn, st, a);
+      else hipLaunchKernelGGL((stem_rowbuf_kernel<_Float16, false>), grid, dim3(256), dyn, st, a);
+    } else {
+      if (a.in_scale) hipLaunchKernelGGL((stem_rowbuf_kernel<__bf16, true>), grid, dim3(256), dyn, st, a);
+      else hipLaunchKernelGGL((stem_rowbuf_kernel<__bf16, false>), grid, dim3(256), dyn, st, a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
+  if (form == 2) return -4;  // row-staged form forced on a shape it does not take
   if ((dtype != 1 && dtype != 2) || a.C < 1 || a.C > 4 || a.R * a.S * a.C > kStemKP || a.Cout < 1 ||
       a.OH <= 0 || a.OW <= 0 || a.B <= 0)
     return -1;

@@ -63,18 +63,18 @@ PYBIND11_MODULE(_nn, m) {
   // taps stay 0 - the input BatchNormalization of an image model)
   m.def("stem_conv", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t bias, uintptr_t res, std::vector<int> g,
                         int relu, int dtype, uintptr_t stream, uintptr_t in_scale, uintptr_t in_shift, int pro_relu,
-                        int kp) {
+                        int kp, int form) {
     if (g.size() != 15) throw std::invalid_argument("geometry: B,H,W,C,Cout,R,S,sh,sw,ph,pw,dh,dw,OH,OW");
     if ((in_scale == 0) != (in_shift == 0)) throw std::invalid_argument("in_scale and in_shift go together");
     ConvArgs a{P<const void>(x), P<const void>(w), P<void>(y), P<const float>(in_scale), P<const float>(in_shift),
                P<const float>(bias), P<const void>(res), nullptr, nullptr, nullptr, g[0], g[1], g[2], g[3], g[4], g[5],
                g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], relu, pro_relu, 0};
-    const int rc = StemConv(a, dtype, P<void>(stream), kp);
+    const int rc = StemConv(a, dtype, P<void>(stream), kp, form);
     if (rc != 0) throw std::runtime_error("stem_conv failed (rc=" + std::to_string(rc) + ")");
   }, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("bias"), pybind11::arg("res"),
      pybind11::arg("geom"), pybind11::arg("relu"), pybind11::arg("dtype"), pybind11::arg("stream"),
      pybind11::arg("in_scale") = 0, pybind11::arg("in_shift") = 0, pybind11::arg("pro_relu") = 0,
-     pybind11::arg("kp") = 160);
+     pybind11::arg("kp") = 160, pybind11::arg("form") = 0);
   // split-K plan of the default tile: (splits, workspace fp32 floats, int32 counters)
   m.def("conv_split_plan", [](std::vector<int> g, int dtype, bool has_prologue, int kernel) {
     if (g.size() != 15) throw std::invalid_argument("geometry: B,H,W,C,Cout,R,S,sh,sw,ph,pw,dh,dw,OH,OW");

@@ -47,7 +47,8 @@ bool ConvMfmaSupported(int C, int Cout, int groups, int dtype);
 int ConvMfma(const ConvArgs& a, int dtype, void* stream);
 // few-channel (C <= 4) stem conv, K = R * S * C <= 160, weights packed [Cout][160] zero-padded; f16 / bf16
 // kp = packed K width: 160 (k = (r * S + s) * C + c) or 192 (C = 3, S * 3 <= 24: k = r * 24 + s * 3 + c)
-int StemConv(const ConvArgs& a, int dtype, void* stream, int kp = 160);
+// form: 0 auto (the row-staged kernel where it applies), 1 the 2-byte gather kernel, 2 row-staged only
+int StemConv(const ConvArgs& a, int dtype, void* stream, int kp = 160, int form = 0);
 // split-K plan of the tile ConvMfma would pick for a (kernel = 0 only): the number of K splits (1: none) and
 // the workspace it needs (fp32 floats, int32 tile counters)
 int ConvSplitPlan(const ConvArgs& a, int dtype, int64_t* ws_floats, int* counters);

@@ -178,12 +178,15 @@ def pack_stem_weight(w: torch.Tensor, wide: Optional[bool] = None) -> torch.Tens
 
 def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
                    bias: Optional[torch.Tensor] = None, relu: int = 0,
-                   res: Optional[torch.Tensor] = None, in_affine=None, in_relu: bool = False) -> torch.Tensor:
+                   res: Optional[torch.Tensor] = None, in_affine=None, in_relu: bool = False,
+                   form: int = 0) -> torch.Tensor:
     """y = relu?(conv(x', w) + bias (+ res)) for a few-channel input (the image stem): ``x`` [B, C, H, W]
     channels_last f16/bf16 with C <= 4, ``wk`` = pack_stem_weight(w). ``relu``: 0 none, 1 before the residual
     add, 2 after it. ``pad``: (top, left) or (top, left, bottom, right). ``in_affine`` = (scale, shift) per
     input channel: x' = x * scale + shift (ReLU'd with ``in_relu``) inside the kernel, padding taps 0 - an
-    input BatchNormalization without its own pass."""
+    input BatchNormalization without its own pass. ``form`` (160-wide weights): 0 picks the row-staged kernel
+    where it applies (3 channels, one block per output row of <= 128 pixels), 1 forces the 2-byte gather
+    kernel, 2 the row-staged one."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         x = x.contiguous(memory_format=torch.channels_last)
@@ -208,7 +211,7 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
             raise ValueError("stem in_affine: one scale / shift per input channel")
     native.load("_nn").stem_conv(x.data_ptr(), wk.data_ptr(), y.data_ptr(), _ptr(b32), _ptr(res), geom, int(relu),
                                  _DT[x.dtype], torch.cuda.current_stream(x.device).cuda_stream, _ptr(sc), _ptr(sh),
-                                 int(bool(in_relu)), int(wk.shape[1]))
+                                 int(bool(in_relu)), int(wk.shape[1]), int(form))
     return y
 
 

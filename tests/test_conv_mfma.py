@@ -338,6 +338,8 @@ def test_fp32_presplit_weight_planes_bitwise(mode):
     (2, 1, 16, 16, 80, 3, 1, 1),     # a partial channel tile
     (2, 3, 33, 31, 64, 5, 1, 2),     # 3 channels, 5x5 stride 1: row runs of 15 values, odd row byte offsets
     (1, 3, 17, 9, 64, 3, 3, 0),      # 3x3 stride 3 unpadded
+    (2, 3, 40, 48, 64, 7, 2, 3),     # row-staged form: 24-pixel output rows, padding both sides
+    (3, 3, 24, 16, 80, 5, 1, 2),     # row-staged form, stride 1, a partial channel tile
 ])
 def test_stem_kernel_matches_reference(dtype, geom):
     """Dedicated few-channel stem kernel (im2col rows in LDS, K padded to 160) vs the fp32 reference, with
@@ -354,6 +356,11 @@ def test_stem_kernel_matches_reference(dtype, geom):
     if C == 3:  # the row-run form (SML_STEM_ROWRUN) and the 2-byte gather form agree exactly
         yw = stem_conv_nhwc(x, pack_stem_weight(w, wide=True), k, k, (st, st), (pd, pd))
         torch.testing.assert_close(yw.float(), ref.to(dtype).float(), rtol=0, atol=0)
+        yg = stem_conv_nhwc(x, pack_stem_weight(w), k, k, (st, st), (pd, pd), form=1)
+        torch.testing.assert_close(yg.float(), ref.to(dtype).float(), rtol=0, atol=0)
+        if W % 8 == 0 and ref.shape[3] <= 128:  # the row-staged form (the default where it applies)
+            yr = stem_conv_nhwc(x, pack_stem_weight(w), k, k, (st, st), (pd, pd), form=2)
+            torch.testing.assert_close(yr.float(), ref.to(dtype).float(), rtol=0, atol=0)
     torch.manual_seed(6)
     xf = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
     wf = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dtype)

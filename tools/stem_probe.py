@@ -12,10 +12,11 @@ from synapseml_amd.ops.conv import pack_stem_weight, stem_conv_nhwc  # noqa: E40
 def main(batch=128, iters=20):
     x = torch.randn(batch, 3, 224, 224, device="cuda").half().contiguous(memory_format=torch.channels_last)
     w = (torch.randn(64, 3, 7, 7, device="cuda") / 12).half()
-    wk, wn = pack_stem_weight(w), pack_stem_weight(w, wide=False)
+    wk, wn = pack_stem_weight(w, wide=True), pack_stem_weight(w, wide=False)
     bias = torch.randn(64, device="cuda")
     aff = (torch.rand(3, device="cuda") + 0.5, torch.randn(3, device="cuda"))
-    for name, wq, kw in (("gather", wn, {}), ("rowrun", wk, {}), ("rowrun_affine", wk, {"in_affine": aff})):
+    for name, wq, kw in (("gather", wn, {"form": 1}), ("rowstaged", wn, {"form": 2}),
+                         ("rowstaged_affine", wn, {"form": 2, "in_affine": aff}), ("rowrun", wk, {})):
         for _ in range(3):
             stem_conv_nhwc(x, wq, 7, 7, (2, 2), (3, 3), bias=bias, relu=2, **kw)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
