@@ -1237,13 +1237,29 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
   const int m0 = orow * a.OW, n0 = blockIdx.y * kStemBN;
   const int S = a.S, R = a.R, run = S * C, K = R * run;
   const int SP = (a.W + 2 * kRowPad) * C;  // slot pitch (halfs), a multiple of 8
+  const int cps = SP / 8, d0 = kRowPad * C / 8, d1 = d0 + a.W * C / 8;  // data chunks [d0, d1) of a slot
+  // every global load of the prologue is issued before the first LDS store: one memory latency, not one
+  // per loop trip (weights: 1280 16-B chunks = 5 per thread; staged rows: <= 768 chunks = 3 per thread)
+  constexpr int kWIt = kStemBN * (kStemKP / 8) / 256, kRIt = 3;
   const T* __restrict__ w = static_cast<const T*>(a.w);
-  for (int q = tid; q < kStemBN * (kStemKP / 8); q += 256) {
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  uint4 wv[kWIt], rv[kRIt];
+#pragma unroll
+  for (int i = 0; i < kWIt; ++i) {
+    const int q = tid + i * 256;
     const int row = q / (kStemKP / 8), ch = q % (kStemKP / 8);
     const int n = n0 + row;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (n < a.Cout) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + ch * 8);
-    *reinterpret_cast<uint4*>(Bs + row * kStemLd + ch * 8) = v;
+    wv[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + ch * 8)
+                       : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < kRIt; ++i) {
+    const int q = tid + i * 256;
+    const int r = q / cps, j = q - r * cps;
+    const int ih = oh * a.stride_h - a.pad_h + r;
+    rv[i] = make_uint4(0, 0, 0, 0);
+    if (q < R * cps && ih >= 0 && ih < a.H && j >= d0 && j < d1)
+      rv[i] = *reinterpret_cast<const uint4*>(x + (static_cast<int64_t>(b) * a.H + ih) * a.W * C + (j - d0) * 8);
   }
   {
     const int c0 = K / 8, nch = kStemKP / 8 - c0;
@@ -1252,45 +1268,69 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
       *reinterpret_cast<uint4*>(As + row * kStemLd + ch * 8) = make_uint4(0, 0, 0, 0);
     }
   }
-  // stage the R input rows: chunk j of slot r holds halfs [8j, 8j + 8) = columns (8j + i) / 3 - kRowPad
-  {
-    const T* __restrict__ x = static_cast<const T*>(a.x);
-    const int cps = SP / 8, d0 = kRowPad * C / 8, d1 = d0 + a.W * C / 8;  // data chunks [d0, d1)
-    float psc[C], psh[C];
-    if constexpr (kPro) {
 #pragma unroll
-      for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
-    }
-    for (int q = tid; q < R * cps; q += 256) {
-      const int r = q / cps, j = q - r * cps;
+  for (int i = 0; i < kWIt; ++i) {
+    const int q = tid + i * 256;
+    *reinterpret_cast<uint4*>(Bs + (q / (kStemKP / 8)) * kStemLd + (q % (kStemKP / 8)) * 8) = wv[i];
+  }
+  float psc[C], psh[C];
+  if constexpr (kPro) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+  }
+#pragma unroll
+  for (int i = 0; i < kRIt; ++i) {
+    const int q = tid + i * 256;
+    if (q >= R * cps) continue;
+    const int r = q / cps, j = q - r * cps;
+    uint4 v = rv[i];
+    if constexpr (kPro) {  // the affine of real values only: padding columns / rows stay 0
       const int ih = oh * a.stride_h - a.pad_h + r;
-      uint4 v = make_uint4(0, 0, 0, 0);
       if (ih >= 0 && ih < a.H && j >= d0 && j < d1) {
-        v = *reinterpret_cast<const uint4*>(x + (static_cast<int64_t>(b) * a.H + ih) * a.W * C + (j - d0) * 8);
-        if constexpr (kPro) {
-          T* e = reinterpret_cast<T*>(&v);
+        T* e = reinterpret_cast<T*>(&v);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int c = (j * 8 + i) % C;
-            const float t = ToF(e[i]) * psc[c] + psh[c];
-            e[i] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
-          }
+        for (int k = 0; k < 8; ++k) {
+          const int c = (j * 8 + k) % C;
+          const float t = ToF(e[k]) * psc[c] + psh[c];
+          e[k] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
         }
       }
-      *reinterpret_cast<uint4*>(rowbuf + r * SP + j * 8) = v;
     }
+    *reinterpret_cast<uint4*>(rowbuf + r * SP + j * 8) = v;
   }
   __syncthreads();
-  // im2col runs from LDS: thread -> (filter row r, pixel ml), consecutive lanes on consecutive pixels
+  // im2col runs from LDS, a dword at a time: thread -> (filter row r, pixel ml), a wave = 64 pixels of one r.
+  // The run's S * 3 halves start at any half (h0) and land at any half (dst): read 12 dwords from h0's dword,
+  // shift by h0's parity (v_alignbyte), store as dwords shifted by dst's parity (wave-uniform: r * run).
   for (int q = tid; q < R * kStemBM; q += 256) {
     const int r = q >> 7, ml = q & (kStemBM - 1);
     if (ml >= a.OW) continue;
-    const int h0 = (ml * a.stride_w - a.pad_w + kRowPad) * C;
-    const unsigned short* src = reinterpret_cast<const unsigned short*>(rowbuf + r * SP + h0);
-    unsigned short* dst = reinterpret_cast<unsigned short*>(As + ml * kStemLd + r * run);
+    const int h0 = r * SP + (ml * a.stride_w - a.pad_w + kRowPad) * C;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(rowbuf) + (h0 >> 1);
+    uint32_t d[12], o[11];
 #pragma unroll
-    for (int e = 0; e < 8 * C; ++e)
-      if (e < run) dst[e] = src[e];
+    for (int k = 0; k < 12; ++k) d[k] = src[k];
+    const uint32_t sb = static_cast<uint32_t>(h0 & 1) * 2u;
+#pragma unroll
+    for (int k = 0; k < 11; ++k) o[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sb);  // halves 2k, 2k + 1
+    const int dst = ml * kStemLd + r * run;  // half index in As
+    uint32_t* A32 = reinterpret_cast<uint32_t*>(As);
+    unsigned short* A16 = reinterpret_cast<unsigned short*>(As);
+    if ((dst & 1) == 0) {
+#pragma unroll
+      for (int k = 0; k < 11; ++k) {
+        if (2 * k + 1 < run) A32[(dst >> 1) + k] = o[k];
+        else if (2 * k < run) A16[dst + 2 * k] = static_cast<unsigned short>(o[k] & 0xFFFFu);
+      }
+    } else {
+      A16[dst] = static_cast<unsigned short>(o[0] & 0xFFFFu);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {  // halves (2k + 1, 2k + 2)
+        const uint32_t pr = __builtin_amdgcn_alignbyte(o[k + 1], o[k], 2u);
+        if (2 * k + 2 < run) A32[((dst + 1) >> 1) + k] = pr;
+        else if (2 * k + 1 < run) A16[dst + 2 * k + 1] = static_cast<unsigned short>(pr & 0xFFFFu);
+      }
+    }
   }
   __syncthreads();
   const int lane = tid & 63, wid = tid >> 6;
@@ -1321,7 +1361,7 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
 // dilation it stages, and its LDS (static operand tiles + R staged rows) within two blocks per CU
 inline int RowbufLds(const ConvArgs& a) { return a.R * (a.W + 2 * kRowPad) * 3 * 2; }
 inline bool RowbufOk(const ConvArgs& a) {
-  return a.C == 3 && a.OW <= kStemBM && a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= kRowPad && a.R <= 8 && a.S <= 8 &&
+  return a.C == 3 && a.S * 3 <= 21 && a.OW <= kStemBM && a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= kRowPad && a.R <= 8 && a.S <= 8 &&
          (a.W * 3 * 2) % 16 == 0 && (a.OW - 1) * a.stride_w - a.pad_w + a.S <= a.W + kRowPad &&
          RowbufLds(a) <= 12 * 1024;
 }
