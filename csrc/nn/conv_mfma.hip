@@ -1243,6 +1243,11 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
   constexpr int kWIt = kStemBN * (kStemKP / 8) / 256, kRIt = 3;
   const T* __restrict__ w = static_cast<const T*>(a.w);
   const T* __restrict__ x = static_cast<const T*>(a.x);
+  float psc[C], psh[C];  // the input affine's 3 scale / shift pairs, in flight with the tiles below
+  if constexpr (kPro) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+  }
   uint4 wv[kWIt], rv[kRIt];
 #pragma unroll
   for (int i = 0; i < kWIt; ++i) {
@@ -1273,11 +1278,6 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
     const int q = tid + i * 256;
     *reinterpret_cast<uint4*>(Bs + (q / (kStemKP / 8)) * kStemLd + (q % (kStemKP / 8)) * 8) = wv[i];
   }
-  float psc[C], psh[C];
-  if constexpr (kPro) {
-#pragma unroll
-    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
-  }
 #pragma unroll
   for (int i = 0; i < kRIt; ++i) {
     const int q = tid + i * 256;
@@ -1288,9 +1288,10 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
       const int ih = oh * a.stride_h - a.pad_h + r;
       if (ih >= 0 && ih < a.H && j >= d0 && j < d1) {
         T* e = reinterpret_cast<T*>(&v);
+        const int c0 = (j * 8) % C;  // channel of the chunk's first value (rows are C-aligned in the slot)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int c = (j * 8 + k) % C;
+          const int c = (c0 + k) % C;
           const float t = ToF(e[k]) * psc[c] + psh[c];
           e[k] = FromF<T>(a.prologue_relu ? fmaxf(t, 0.f) : t);
         }
