@@ -232,6 +232,8 @@ struct RankTables {
   const int32_t* qb;
   const double* inv_max_dcg;
   const double* gain;
+  const double* disc;  // 1 / log2(2 + r) for r < kRankLds, computed once on the host (std::log2, as the
+                       // host objective): each block copies 2 KB instead of evaluating 256 fp64 log2 + div
   int32_t* rank_scratch;
   double* lam_scratch;
   double* hes_scratch;
@@ -654,7 +656,7 @@ __global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables
                                                                       float* __restrict__ g, float* __restrict__ h) {
   __shared__ double s_disc[kRankLds];
   __shared__ int s_map[kWaves][64];
-  for (int r = threadIdx.x; r < kRankLds; r += 64 * kWaves) s_disc[r] = 1.0 / log2(2.0 + r);
+  for (int r = threadIdx.x; r < kRankLds; r += 64 * kWaves) s_disc[r] = t.disc[r];
   __syncthreads();
   const int wid = threadIdx.x >> 6;
   // documents per lane sized to the query: the pair loops run NU-wide, so a 100-document query
@@ -679,7 +681,7 @@ __global__ __launch_bounds__(64) void lambdarank_kernel(RankTables t, const doub
   __shared__ int s_rk[kRankLds];
   __shared__ int s_top[kRankLds];
   __shared__ double s_tlam[kRankLds], s_thes[kRankLds];
-  for (int r = threadIdx.x; r < kRankLds; r += 64) s_disc[r] = 1.0 / log2(2.0 + r);
+  for (int r = threadIdx.x; r < kRankLds; r += 64) s_disc[r] = t.disc[r];
   __syncthreads();
   for (int q = blockIdx.x; q < t.nq; q += gridDim.x) {
     const int cnt = t.qb[q + 1] - t.qb[q];
@@ -3536,6 +3538,12 @@ class GpuBackend : public TrainBackend {
     SML_HIP_CHECK(hipMemcpy(rank_qb_.get(), qb.data(), sizeof(int32_t) * qb.size(), hipMemcpyHostToDevice));
     SML_HIP_CHECK(hipMemcpy(rank_imd_.get(), imd.data(), sizeof(double) * imd.size(), hipMemcpyHostToDevice));
     SML_HIP_CHECK(hipMemcpy(rank_gain_.get(), gain.data(), sizeof(double) * gain.size(), hipMemcpyHostToDevice));
+    {
+      std::vector<double> disc(kRankLds);
+      for (int r = 0; r < kRankLds; ++r) disc[r] = 1.0 / std::log2(2.0 + r);
+      rank_disc_.alloc(kRankLds);
+      SML_HIP_CHECK(hipMemcpy(rank_disc_.get(), disc.data(), sizeof(double) * kRankLds, hipMemcpyHostToDevice));
+    }
     int max_q = 0;
     rank_regs_ = rank_lds_ = false;
     const bool regs_pos = obj.max_position() <= 64;  // RegsEligible, host side: which kernels have work
@@ -3561,6 +3569,7 @@ class GpuBackend : public TrainBackend {
     rank_.qb = rank_qb_.get();
     rank_.inv_max_dcg = rank_imd_.get();
     rank_.gain = rank_gain_.get();
+    rank_.disc = rank_disc_.get();
     rank_.nq = static_cast<int>(qb.size()) - 1;
     rank_.ngain = static_cast<int>(gain.size());
     rank_.max_position = obj.max_position();
@@ -3883,7 +3892,7 @@ class GpuBackend : public TrainBackend {
   RankTables rank_{};
   DevBuf<int32_t> rank_qb_, rank_scratch_;
   std::vector<std::unique_ptr<DeviceValidSet>> vsets_;
-  DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_;
+  DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_, rank_disc_;
   int32_t* flags_ = nullptr;
   // batched speculative growth
   static constexpr int kBRing = 8;
