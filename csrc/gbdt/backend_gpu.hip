@@ -508,7 +508,7 @@ __device__ __forceinline__ double ReadLaneD(double v, int l) {
 // lanes 0..ntop-1 and is broadcast the same way. Pairs: (a) every top
 // document with every document, spread over the lanes and wave-reduced;
 // (b) every other document with the top list, one lane per document.
-template <int NU>  // documents per lane: cnt <= 64 * NU
+template <int NU, bool kTR>  // documents per lane: cnt <= 64 * NU; kTR: transpose-reduced top sums
 __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __restrict__ score,
                                     const float* __restrict__ label, const float* __restrict__ weight,
                                     float* __restrict__ g, float* __restrict__ h, const double* s_disc,
@@ -596,7 +596,8 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   // normaliser sum takes such a pair's term from both ends. Grouping four top documents so their wave
   // sums interleave measured no faster (1.44 vs 1.35 ms per call): not shuffle-latency bound.
   float top_la = 0.f, top_he = 0.f;  // lane r keeps the reduced lambdas of top document r
-  for (int r = 0; r < ntop; ++r) {
+  // this lane's terms of top document r against its partners (and the partners' mirrored terms)
+  auto top_terms = [&](int r, float* la_out, float* he_out) {
     const double si = ReadLaneD(tsc, r);
     const int li = __builtin_amdgcn_readlane(tlab, r);
     const int di = __builtin_amdgcn_readlane(tdoc, r);
@@ -619,9 +620,55 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
         }
       }
     }
-    la = WaveSumF(la);
-    he = WaveSumF(he);
-    if (lane == r) { top_la = la; top_he = he; }
+    *la_out = la;
+    *he_out = he;
+  };
+  if constexpr (kTR) {
+    // Eight top documents per round of cross-lane sums: their 16 partial sums are transpose-reduced (each
+    // xor step keeps half of the values, 8 + 4 + 2 + 1 + 1 + 1 = 17 shuffles instead of 16 x 6). The shuffles
+    // are ds_bpermute through the CU's one LDS pipe, which the 12 per top document saturated (4-wave blocks
+    // measured slower, not faster). Same xor pairing as WaveSumF: every sum is bitwise the same.
+    for (int r0 = 0; r0 < ntop; r0 += 8) {
+      float v[16];
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        v[rr] = 0.f;
+        v[8 + rr] = 0.f;
+        if (r0 + rr < ntop) top_terms(r0 + rr, &v[rr], &v[8 + rr]);
+      }
+      const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+      float a8[8], a4[4], a2[2];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float mine = b5 ? v[8 + k] : v[k], oth = b5 ? v[k] : v[8 + k];
+        a8[k] = mine + __shfl_xor(oth, 32, 64);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float mine = b4 ? a8[4 + k] : a8[k], oth = b4 ? a8[k] : a8[4 + k];
+        a4[k] = mine + __shfl_xor(oth, 16, 64);
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float mine = b3 ? a4[2 + k] : a4[k], oth = b3 ? a4[k] : a4[2 + k];
+        a2[k] = mine + __shfl_xor(oth, 8, 64);
+      }
+      float a1 = (b2 ? a2[1] : a2[0]) + __shfl_xor(b2 ? a2[0] : a2[1], 4, 64);
+      a1 += __shfl_xor(a1, 2, 64);
+      a1 += __shfl_xor(a1, 1, 64);
+      // lane l now holds value (l >> 2): la of top document r0 + i at lane 4i, he at lane 32 + 4i
+      const int rr = lane - r0;
+      const float tla = __shfl(a1, (rr & 7) * 4, 64), the = __shfl(a1, 32 + (rr & 7) * 4, 64);
+      if (rr >= 0 && rr < 8) { top_la = tla; top_he = the; }
+    }
+  } else {
+    for (int r = 0; r < ntop; ++r) {
+      float la, he;
+      top_terms(r, &la, &he);
+      la = WaveSumF(la);
+      he = WaveSumF(he);
+      if (lane == r) { top_la = la; top_he = he; }
+    }
   }
   const double sumd = WaveSumF(suml);
   const double nf = (t.norm && sumd > 0) ? log2(1.0 + sumd) / sumd : 1.0;
@@ -649,7 +696,7 @@ __device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
 // wave (2 KB + 256 B per wave instead of the LDS path's 11.5 KB). kWaves independent waves per block, each
 // walking its own queries (a CU holds at most 16 workgroups, so one-wave blocks cap residency at 4 waves
 // per SIMD; kWaves = 4 lifts that, but measured slower - see rank_waves_).
-template <int kWaves>
+template <int kWaves, bool kTR = true>
 __global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
                                                                       const float* __restrict__ label,
                                                                       const float* __restrict__ weight,
@@ -664,10 +711,10 @@ __global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables
   for (int q = blockIdx.x * kWaves + wid; q < t.nq; q += gridDim.x * kWaves) {
     const int cnt = t.qb[q + 1] - t.qb[q];
     if (cnt <= 0 || !RegsEligible(t, cnt)) continue;
-    if (cnt <= 64) LambdarankQueryRegs<1>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
-    else if (cnt <= 128) LambdarankQueryRegs<2>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
-    else if (cnt <= 192) LambdarankQueryRegs<3>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
-    else LambdarankQueryRegs<kRankPerLane>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    if (cnt <= 64) LambdarankQueryRegs<1, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    else if (cnt <= 128) LambdarankQueryRegs<2, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    else if (cnt <= 192) LambdarankQueryRegs<3, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    else LambdarankQueryRegs<kRankPerLane, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
   }
 }
 
@@ -2917,6 +2964,7 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
     if (const char* e = std::getenv("SML_GBDT_HIST_PIPE")) hist_pipe_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_RANK_WAVES")) rank_waves_ = std::atoi(e) == 4 ? 4 : 1;
+    if (const char* e = std::getenv("SML_RANK_TREDUCE")) rank_treduce_ = std::atoi(e) != 0;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -3083,7 +3131,8 @@ class GpuBackend : public TrainBackend {
         const int grid = std::min(rank_.nq, 65536);
         if (rank_regs_) {
           if (rank_waves_ == 1) {
-            hipLaunchKernelGGL(lambdarank_regs_kernel<1>, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(),
+            auto lk = rank_treduce_ ? lambdarank_regs_kernel<1, true> : lambdarank_regs_kernel<1, false>;
+            hipLaunchKernelGGL(lk, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(),
                                label_.get(), weight_.get(), g_.get(), h_.get());
           } else {
             const int g4 = std::max(1, std::min((rank_.nq + 3) / 4, 16384));
@@ -3815,6 +3864,7 @@ class GpuBackend : public TrainBackend {
   // to 10 resident per SIMD instead of 4): r4 pass 11 measured it slower (949 vs 860 us per call, ranker
   // fit 33.6M vs 34.0M rows/s), so one-wave blocks stay the default
   int rank_waves_ = 1;
+  bool rank_treduce_ = true;  // SML_RANK_TREDUCE=0: one pair of wave sums per top document (A/B knob)
   int64_t n_ = 0;
   int32_t bag_n_ = -1;
   DevBuf<uint8_t> bins_, cbins_;           // bins_: own upload when the dataset is not device-resident

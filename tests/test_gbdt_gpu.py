@@ -297,6 +297,22 @@ def test_gpu_lambdarank_gradients_match_host(maxpos):
     np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
 
 
+def test_gpu_lambdarank_transpose_reduce_is_bitwise(monkeypatch):
+    """The lambdarank register kernel's transpose-reduced top-document sums (eight documents per round of
+    shuffles) use WaveSumF's xor pairing: gradients bitwise equal to one wave sum per top document."""
+    X, y, sizes = _rank_data()
+    p = "objective=lambdarank num_leaves=15 min_data_in_leaf=5 eval_at=5 max_position=20 device_type=gpu"
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("SML_RANK_TREDUCE", v)
+        b = _train_rank(X, y, sizes, p, 3)
+        out[v] = (b.gradients(), b.save_model_string())
+    (g0, h0), m0 = out["0"]
+    (g1, h1), m1 = out["1"]
+    assert np.array_equal(g0, g1) and np.array_equal(h0, h1)
+    assert m0 == m1
+
+
 def test_gpu_bagging_draws_the_host_bag():
     """K8: device bagging draws the same rows as the host (counter-based RNG), so trees match the CPU oracle."""
     X, y = _data(n=50000)
