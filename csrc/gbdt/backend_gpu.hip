@@ -2194,6 +2194,7 @@ __device__ __forceinline__ bool SimBetter(const SimKey& x, const SimKey& y) {
 }
 
 constexpr int kPlanThreads = 1024;
+constexpr int kPlanFm = 1024;  // features whose split metadata the plan stages in LDS
 
 // round outcome for the host (coherent pinned memory, read after the plan's event): system-scope vector store
 __device__ __forceinline__ void SetHostFlag(int* f, int v) {
@@ -2241,6 +2242,18 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   // counts and row segments. One wave per child; lanes stride over features (ties: smaller feature).
   const int nchild = first ? 1 : 2 * nexp;
   for (int c = wid; c < nchild; c += kWaves) {
+    // the expansion record, its cursor and the smaller child's count do not depend on the argmax below:
+    // loaded first, so their latency overlaps the feature records' (one memory round trip, not two)
+    int x_node = 0, x_c0 = 0, x_c1 = 0, x_ls = 0, x_pb = 0, x_pc = 0, x_buf = 0, lt = 0;
+    int64_t small_cnt = 0;
+    if (!first && lane == 0) {
+      const int j = c >> 1;
+      const BExp& x = bs->exp[j];
+      x_node = x.node; x_c0 = x.c0; x_c1 = x.c1; x_ls = x.left_small;
+      x_pb = x.pbegin; x_pc = x.pcount; x_buf = x.pbuf;
+      lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+      small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
+    }
     KeyG k{-INFINITY, 1 << 30, 0};
     for (int f = lane; f < F; f += 64) {
       const SplitResult& r = fbest[c * F + f];
@@ -2254,18 +2267,14 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       if (first) {
         id = 0;
       } else {
-        const int j = c >> 1;
-        const BExp& x = bs->exp[j];
-        const int small = x.left_small ? x.c0 : x.c1;
-        id = (c & 1) ? (small == x.c0 ? x.c1 : x.c0) : small;
-        const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
-        const int64_t small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
+        const int small = x_ls ? x_c0 : x_c1;
+        id = (c & 1) ? (small == x_c0 ? x_c1 : x_c0) : small;
         BNode& nd = nodes[id];
-        const bool is_left = id == x.c0;
-        nd.begin = is_left ? x.pbegin : x.pbegin + lt;
-        nd.count = is_left ? lt : x.pcount - lt;
-        nd.buf = x.pbuf == 0 ? 1 : 0;
-        nd.gcount = (c & 1) ? nodes[x.node].gcount - small_cnt : small_cnt;
+        const bool is_left = id == x_c0;
+        nd.begin = is_left ? x_pb : x_pb + lt;
+        nd.count = is_left ? lt : x_pc - lt;
+        nd.buf = x_buf == 0 ? 1 : 0;
+        nd.gcount = (c & 1) ? nodes[x_node].gcount - small_cnt : small_cnt;
       }
       if (k.gain == -INFINITY) {
         nbest[id].feature = -1;
@@ -2276,13 +2285,29 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     }
   }
   __syncthreads();
-  // ---- node gains and expansion links into LDS (the replay's dependent reads stay on chip)
+  // ---- node gains and expansion links into LDS (the replay's dependent reads stay on chip); in the same
+  // pass the committed replay prefix and (F <= kPlanFm) the split features' metadata, so the one-wave
+  // replay and plan below start without a memory round trip of their own
+  __shared__ int s_rp[2];
+  __shared__ int s_nb[kPlanFm], s_mt[kPlanFm], s_db[kPlanFm];
   for (int i = tid; i < nnodes; i += kPlanThreads) {
     const SplitResult& r = nbest[i];
     s_gain[i] = r.feature >= 0 ? r.gain : -INFINITY;
     s_c0[i] = nodes[i].c0;
     s_c1[i] = nodes[i].c1;
     s_pop[i] = -1;
+  }
+  const bool fm_lds = F <= kPlanFm;
+  if (fm_lds)
+    for (int f = tid; f < F; f += kPlanThreads) { s_nb[f] = fm.num_bin[f]; s_mt[f] = fm.missing[f]; s_db[f] = fm.default_bin[f]; }
+  if (!first) {
+    if (tid == 0) { s_rp[0] = bs->rp_nf; s_rp[1] = bs->rp_pops; }
+    // the prefix arrays are read whole-capacity-bounded by the stored counts after the barrier; loading
+    // kBatchMaxLeaves entries regardless keeps this pass free of a dependent count load
+    for (int i = tid; i < kBatchMaxLeaves + 1; i += kPlanThreads) {
+      f_node[i] = bs->rp_fnode[i]; f_li[i] = bs->rp_fli[i]; f_gain[i] = bs->rp_fgain[i];
+      if (i < kBatchMaxLeaves) { p_node[i] = bs->rp_pnode[i]; p_li[i] = bs->rp_pli[i]; }
+    }
   }
   __syncthreads();
   if (wid != 0) return;
@@ -2291,15 +2316,9 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   if (first) {
     if (lane == 0) { f_node[0] = 0; f_li[0] = 0; f_gain[0] = s_gain[0]; }
   } else {
-    nf = bs->rp_nf;
-    pops = bs->rp_pops;
-    for (int i = lane; i < nf; i += 64) { f_node[i] = bs->rp_fnode[i]; f_li[i] = bs->rp_fli[i]; f_gain[i] = bs->rp_fgain[i]; }
-    for (int i = lane; i < pops; i += 64) {
-      const int v = bs->rp_pnode[i];
-      p_node[i] = v;
-      p_li[i] = bs->rp_pli[i];
-      s_pop[v] = i;
-    }
+    nf = s_rp[0];
+    pops = s_rp[1];
+    for (int i = lane; i < pops; i += 64) s_pop[p_node[i]] = i;
   }
   const int committed = pops;
   WaveSync();
@@ -2432,9 +2451,9 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     x.ps.is_cat = sr.is_cat;
     x.ps.dleft = sr.default_left;
     x.ps.thr = sr.threshold;
-    x.ps.nb = fm.num_bin[sr.feature];
-    x.ps.mt = fm.missing[sr.feature];
-    x.ps.dbin = fm.default_bin[sr.feature];
+    x.ps.nb = fm_lds ? s_nb[sr.feature] : fm.num_bin[sr.feature];
+    x.ps.mt = fm_lds ? s_mt[sr.feature] : fm.missing[sr.feature];
+    x.ps.dbin = fm_lds ? s_db[sr.feature] : fm.default_bin[sr.feature];
     for (int w = 0; w < 8; ++w) x.cat[w] = sr.is_cat ? sr.cat_bits[w] : 0u;
     // first global tile: prefix over the expansions' tile counts
     const int nt = (P.count + part_tile - 1) / part_tile;
