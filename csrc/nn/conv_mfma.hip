@@ -98,32 +98,54 @@ __device__ __forceinline__ void EpilogueStore(const ConvArgs& a, const T* Ct, in
   const bool relu_post = a.relu == 2 && res != nullptr;
   constexpr int EPV = Tile<T>::EPV;
   constexpr int CPR = WN / EPV;
+  constexpr int NIT = WM * CPR / 64;
+  static_assert(64 % CPR == 0, "a lane keeps one channel chunk across the row iterations");
+  // Every global load of the tile's epilogue (residual rows, second-output affine) is issued before the
+  // first store: the plain per-row loop waited out one memory latency per row iteration (the compiler
+  // cannot move a residual load above the previous row's output store), which memory-bound 1x1 layers
+  // with a residual paid NIT times per tile.
+  const int ch = lane % CPR;  // idx = it * 64 + lane: the chunk is the same in every iteration
+  const int n = n0 + wn0 + ch * EPV;
+  const bool n_ok = n < a.Cout;
+  uint4 pv[NIT], rv[NIT];
+  int64_t o[NIT];
+  bool ok[NIT];
 #pragma unroll
-  for (int it = 0; it < WM * CPR / 64; ++it) {
-    const int idx = it * 64 + lane;
-    const int row = idx / CPR, ch = idx % CPR;
-    const int m = m0 + wm0 + row, n = n0 + wn0 + ch * EPV;
-    if (m >= M || n >= a.Cout) continue;
-    uint4 pv = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * EPV);
-    const int64_t o = static_cast<int64_t>(m) * a.Cout + n;
+  for (int it = 0; it < NIT; ++it) {
+    const int row = (it * 64 + lane) / CPR;
+    const int m = m0 + wm0 + row;
+    ok[it] = m < M && n_ok;
+    o[it] = static_cast<int64_t>(ok[it] ? m : 0) * a.Cout + (n_ok ? n : 0);
+    pv[it] = *reinterpret_cast<const uint4*>(Ct + row * CL + ch * EPV);
+    rv[it] = make_uint4(0, 0, 0, 0);
+    if (res && ok[it]) rv[it] = *reinterpret_cast<const uint4*>(res + o[it]);
+  }
+  float os[EPV], ob[EPV];
+  if (y2 && n_ok) {
+#pragma unroll
+    for (int e = 0; e < EPV; ++e) { os[e] = a.out_scale[n + e]; ob[e] = a.out_shift[n + e]; }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    if (!ok[it]) continue;
+    uint4 v = pv[it];
     if (res) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(res + o);
-      T* pe = reinterpret_cast<T*>(&pv);
-      const T* re = reinterpret_cast<const T*>(&rv);
+      T* pe = reinterpret_cast<T*>(&v);
+      const T* re = reinterpret_cast<const T*>(&rv[it]);
 #pragma unroll
       for (int e = 0; e < EPV; ++e) {
-        const float v = ToF(pe[e]) + ToF(re[e]);
-        pe[e] = FromF<T>(relu_post ? fmaxf(v, 0.f) : v);
+        const float t = ToF(pe[e]) + ToF(re[e]);
+        pe[e] = FromF<T>(relu_post ? fmaxf(t, 0.f) : t);
       }
     }
-    *reinterpret_cast<uint4*>(y + o) = pv;
+    *reinterpret_cast<uint4*>(y + o[it]) = v;
     if (y2) {
       uint4 qv;
-      const T* pe = reinterpret_cast<const T*>(&pv);
+      const T* pe = reinterpret_cast<const T*>(&v);
       T* qe = reinterpret_cast<T*>(&qv);
 #pragma unroll
-      for (int e = 0; e < EPV; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * a.out_scale[n + e] + a.out_shift[n + e], 0.f));
-      *reinterpret_cast<uint4*>(y2 + o) = qv;
+      for (int e = 0; e < EPV; ++e) qe[e] = FromF<T>(fmaxf(ToF(pe[e]) * os[e] + ob[e], 0.f));
+      *reinterpret_cast<uint4*>(y2 + o[it]) = qv;
     }
   }
 }
