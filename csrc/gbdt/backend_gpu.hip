@@ -1826,25 +1826,38 @@ __device__ __forceinline__ void PartitionTile(
   {
     const int t0 = pbegin + tile * kPartTile;
     const int tv = min(kPartTile, pbegin + pcount - t0);
+    // Branch-free loads, every row of the tile in flight at once: rows past the segment read position t0
+    // (always valid) and are masked afterwards. (Guarding each load with k < tv put every load in its own
+    // branch, and the compiler waited out one memory latency per row - 8 serial bin-byte gathers per tile.)
     int r[kPartRows];
     float2 v[kPartRows];
+    if (pbuf < 0) {
 #pragma unroll
-    for (int u = 0; u < kPartRows; ++u) {
-      const int k = u * kPartThreads + tid;
-      r[u] = 0;
-      v[u] = make_float2(0.f, 0.f);
-      if (k < tv) {
-        const int p = t0 + k;
-        if (pbuf < 0) { r[u] = p; v[u] = make_float2(g[p], h[p]); }
-        else { r[u] = perm[p]; v[u] = ogh[p]; }
+      for (int u = 0; u < kPartRows; ++u) {
+        const int k = u * kPartThreads + tid;
+        const int p = t0 + (k < tv ? k : 0);
+        r[u] = p;
+        v[u] = make_float2(g[p], h[p]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPartRows; ++u) {
+        const int k = u * kPartThreads + tid;
+        const int p = t0 + (k < tv ? k : 0);
+        r[u] = perm[p];
+        v[u] = ogh[p];
       }
     }
+    uint32_t bin[kPartRows];
+    const uint8_t* __restrict__ col = cbins + static_cast<size_t>(ps.feature) * n;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) bin[u] = col[r[u]];
     int rl[kPartRows];
     unsigned lmask = 0;
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       const int k = u * kPartThreads + tid;
-      const bool left = k < tv && RowGoesLeft(cbins, n, r[u], ps, s_cat);
+      const bool left = k < tv && DeviceGoesLeft(bin[u], ps.nb, ps.mt, ps.dbin, ps.is_cat, ps.thr, ps.dleft, s_cat);
       lmask |= left ? (1u << u) : 0u;
       const unsigned long long bl = __ballot(left);
       rl[u] = __popcll(bl & below);
