@@ -1069,23 +1069,26 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
     return;
   }
   for (int base = p0 + tid; base < p1; base += kHistBlockThreads * kUnroll) {
-    int r[kUnroll];
+    // branch-free loads (positions past p1 read position p0, a valid row, and are never accumulated): a
+    // guarded load is a branch, and the compiler waits out each one before the next row's
+    int r[kUnroll], pq[kUnroll];
     bool ok[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int pos = base + u * kHistBlockThreads;
       ok[u] = pos < p1;
-      r[u] = ok[u] ? (phys ? pos : perm[pos]) : 0;
+      pq[u] = ok[u] ? pos : p0;
+      r[u] = phys ? pq[u] : perm[pq[u]];
     }
     uint4 b0[kUnroll], b1[kUnroll];
     float2 v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const int pos = base + u * kHistBlockThreads;
       const size_t rb = static_cast<size_t>(r[u]) * W4 + col;
       b0[u] = bins4[rb];
-      b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
-      v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : (ok[u] ? ogh[pos] : make_float2(0.f, 0.f));
+      b1[u] = bins4[two ? rb + 1 : rb];
+      if (!two) b1[u] = make_uint4(0, 0, 0, 0);
+      v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : ogh[pq[u]];
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
@@ -2854,16 +2857,23 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     uint4 b0[kUnroll], b1[kUnroll];
     double s[kUnroll];
     float y[kUnroll], w[kUnroll];
+    int iq[kUnroll];
+    // branch-free loads: rows past p1 read row p0 and are skipped below (no guarded load to wait out)
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int i = base + u * kThreads;
-      const bool ok = i < p1;
-      const size_t rb = static_cast<size_t>(ok ? i : p0) * W4;
+      iq[u] = i < p1 ? i : p0;
+      const size_t rb = static_cast<size_t>(iq[u]) * W4;
       b0[u] = bins4[rb];
-      b1[u] = two ? bins4[rb + 1] : make_uint4(0, 0, 0, 0);
-      s[u] = ok ? score[i] : 0.0;
-      y[u] = ok ? label[i] : 0.f;
-      w[u] = ok && weight ? weight[i] : 1.f;
+      b1[u] = bins4[two ? rb + 1 : rb];
+      if (!two) b1[u] = make_uint4(0, 0, 0, 0);
+      s[u] = score[iq[u]];
+      y[u] = label[iq[u]];
+      w[u] = 1.f;
+    }
+    if (weight) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) w[u] = weight[iq[u]];
     }
     // all 32 slots (b1 = 0 when F <= 16: bin 0 of unused slots): one code path keeps this kernel unspilled
 #pragma unroll
