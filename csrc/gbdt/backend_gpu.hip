@@ -2713,15 +2713,18 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
   int leaf[kScoreRows];
   if (packed) {
     uint4 ra[kScoreRows], rb[kScoreRows];
+    if (ni > 0) {  // branch-free row loads (rows past n read row 0; their results are not stored)
 #pragma unroll
-    for (int u = 0; u < kScoreRows; ++u) {
-      const int64_t i = i0 + u * stride;
-      ra[u] = make_uint4(0, 0, 0, 0);
-      rb[u] = ra[u];
-      if (i < n && ni > 0) {
-        ra[u] = bins4[i * W4];
-        if (F > 16) rb[u] = bins4[i * W4 + 1];
+      for (int u = 0; u < kScoreRows; ++u) {
+        const int64_t i = i0 + u * stride;
+        const int64_t iq = i < n ? i : 0;
+        ra[u] = bins4[iq * W4];
+        rb[u] = bins4[F > 16 ? iq * W4 + 1 : iq * W4];
+        if (F <= 16) rb[u] = make_uint4(0, 0, 0, 0);
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kScoreRows; ++u) { ra[u] = make_uint4(0, 0, 0, 0); rb[u] = ra[u]; }
     }
 #pragma unroll
     for (int u = 0; u < kScoreRows; ++u) {
