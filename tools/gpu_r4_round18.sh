@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 eighteenth GPU pass: partition tiles with branch-free batched loads (GBDT GPU tests,
+# Round-4 eighteenth GPU pass: branch-free batched loads in partition / histogram / score kernels (GBDT GPU tests,
 # headline fit x2, kernel trace with the per-round breakdown). Usage: tools/gpu_r4_round18.sh OUTDIR
 OUT=${1:-gpurun_out/r4r18}
 ROOT=$(pwd)
@@ -10,5 +10,6 @@ rc=$?
 [ $rc -eq 1 ] && exit 1
 timeout -k 10 300 python bench.py > "$OUT/bench.log" 2>&1 || exit 1
 timeout -k 10 300 python bench.py > "$OUT/bench2.log" 2>&1 || exit 1
+timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker.log" 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/prof_fit" -o fit -- python3 bench.py --steps 2 --warmup 1 > "$OUT/prof_fit.log" 2>&1
