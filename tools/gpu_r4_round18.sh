@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-4 eighteenth GPU pass: branch-free batched loads in partition / histogram / score kernels (GBDT GPU tests,
-# headline fit x2, kernel trace with the per-round breakdown). Usage: tools/gpu_r4_round18.sh OUTDIR
+# Round-4 eighteenth GPU pass: the root pass's tree walks interleaved across its unrolled rows. The whole GPU
+# suite in one process, smoke(), headline fit x2, ranker fit, fit trace. Usage: tools/gpu_r4_round18.sh OUTDIR
 OUT=${1:-gpurun_out/r4r18}
 ROOT=$(pwd)
 mkdir -p "$OUT"
-timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gbdt_gpu.py tests/test_lightgbm.py -m gpu > "$OUT/pytest_gbdt.log" 2>&1
+timeout -k 10 900 python -u -m pytest -v --timeout 120 --timeout-method thread tests -m gpu > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
-[ $rc -gt 1 ] && exit $rc
-[ $rc -eq 1 ] && exit 1
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
 timeout -k 10 300 python bench.py > "$OUT/bench.log" 2>&1 || exit 1
 timeout -k 10 300 python bench.py > "$OUT/bench2.log" 2>&1 || exit 1
 timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker.log" 2>&1 || exit 1
