@@ -920,9 +920,13 @@ __device__ __forceinline__ int ScaleExp(int count, float vmax) {
   return max(-1000, min(1000, ilogb(r)));
 }
 
-__device__ __forceinline__ HScale HistScale(int count, const float* ghmax) {
-  const int eg = ScaleExp(count, ghmax[0]), eh = ScaleExp(count, ghmax[1]);
+__device__ __forceinline__ HScale HistScaleV(int count, float gmax, float hmax) {
+  const int eg = ScaleExp(count, gmax), eh = ScaleExp(count, hmax);
   return HScale{ldexp(1.0, eg), ldexp(1.0, eh), ldexp(1.0, -eg), ldexp(1.0, -eh)};
+}
+
+__device__ __forceinline__ HScale HistScale(int count, const float* ghmax) {
+  return HistScaleV(count, ghmax[0], ghmax[1]);
 }
 
 struct QGH {
@@ -1006,6 +1010,8 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
   constexpr int kWords = kFPG * kBinsPerFeature;
   __shared__ unsigned long long shg[kWords], shh[kWords];
   const int tid = threadIdx.x;
+  // the fixed-point scale's inputs load while the LDS histogram is zeroed (not after the barrier)
+  const float gmax_g = ghmax[0], gmax_h = ghmax[1];
   for (int i = tid; i < kWords; i += kHistBlockThreads) { shg[i] = 0ull; shh[i] = 0ull; }
   __syncthreads();
   const int grp = blockIdx.y;
@@ -1015,7 +1021,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
   const int chunk = ceil_div_i(count, nb_active);
   const int p0 = begin + lb * chunk;
   const int p1 = min(begin + count, p0 + chunk);
-  const HScale sc = HistScale(count, ghmax);
+  const HScale sc = HistScaleV(count, gmax_g, gmax_h);
   const int32_t* __restrict__ perm = buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = buf == 0 ? ogh0 : ogh1;
   const bool phys = buf < 0;
@@ -2503,18 +2509,23 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   if (nexp == 0) return;
   const int ntiles = bs->ntiles;
   if (static_cast<int>(blockIdx.x) >= ntiles) return;
-  __shared__ int s_tile0[kMaxSpec];
+  __shared__ int s_tile0[kMaxSpec], s_pb[kMaxSpec], s_pc[kMaxSpec], s_pbuf[kMaxSpec];
+  __shared__ PartSplit s_ps[kMaxSpec];
   __shared__ uint32_t s_cat[kMaxSpec][8];
   const int tid = threadIdx.x;
-  if (tid < nexp) s_tile0[tid] = bs->exp[tid].tile0;
+  // every expansion's partition parameters staged once (the tile loop then starts its row loads without a
+  // dependent read of the expansion record)
+  if (tid < nexp) {
+    const BExp& x = bs->exp[tid];
+    s_tile0[tid] = x.tile0; s_pb[tid] = x.pbegin; s_pc[tid] = x.pcount; s_pbuf[tid] = x.pbuf; s_ps[tid] = x.ps;
+  }
   if (tid < nexp * 8) s_cat[tid >> 3][tid & 7] = bs->exp[tid >> 3].cat[tid & 7];
   __syncthreads();
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     int j = 0;
     while (j + 1 < nexp && s_tile0[j + 1] <= tile) ++j;
-    const BExp& x = bs->exp[j];
-    const PartSplit ps = x.ps;
-    PartitionTile<kPartRows>(ps, s_cat[j], tile - s_tile0[j], x.pbegin, x.pcount, x.pbuf, &bs->cursor[j], cbins, n,
+    const PartSplit ps = s_ps[j];
+    PartitionTile<kPartRows>(ps, s_cat[j], tile - s_tile0[j], s_pb[j], s_pc[j], s_pbuf[j], &bs->cursor[j], cbins, n,
                              perm0, perm1, ogh0, ogh1, wperm0, wperm1, wogh0, wogh1, g, h);
   }
 }
@@ -2528,10 +2539,10 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   const int nexp = bs->nexp;
   if (nexp == 0) return;
   __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
-  if (threadIdx.x == 0) {
-    for (int q = 0; q < nexp; ++q) s_cnt[q] = BatchSmallCount(bs, q);
-    BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
-  }
+  // the expansions' counts load in parallel (one thread each: one memory latency, not nexp in a row)
+  if (threadIdx.x < nexp) s_cnt[threadIdx.x] = BatchSmallCount(bs, threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
   __syncthreads();
   const int bx = blockIdx.x;
   int j = -1;
@@ -2554,10 +2565,9 @@ __global__ __launch_bounds__(kRedE * kRedG) void breduce_kernel(const BState* __
   if (j >= nexp) return;
   const int tid = threadIdx.x, le = tid % kRedE, grp = tid / kRedE;
   __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
-  if (tid == 0) {
-    for (int q = 0; q < nexp; ++q) s_cnt[q] = BatchSmallCount(bs, q);
-    BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
-  }
+  if (tid < nexp) s_cnt[tid] = BatchSmallCount(bs, tid);  // in parallel, as in bhist_kernel
+  __syncthreads();
+  if (tid == 0) BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
   __syncthreads();
   const int count = s_cnt[j];
   const int nbj = s_nb[j], offj = s_off[j];
@@ -2598,14 +2608,17 @@ __global__ __launch_bounds__(256) void bfind_kernel(const BState* __restrict__ b
                                                     double2* __restrict__ hist_pool, FeatMeta fm, SplitParams sp,
                                                     SplitResult* __restrict__ fbest, int F) {
   const int j = blockIdx.y >> 1, c = blockIdx.y & 1;
-  if (j >= bs->nexp) return;
   const int f = blockIdx.x, tid = threadIdx.x;
-  const BExp& x = bs->exp[j];
-  const int small = x.left_small ? x.c0 : x.c1;
-  const int child = c == 0 ? small : (small == x.c0 ? x.c1 : x.c0);
+  // the expansion record and this feature's reduced bins load together with the expansion count (all
+  // within their buffers for any j < spec_k); the guard comes after, so the loads are not serialized behind it
+  const int nexp = bs->nexp;
+  const BExp x = bs->exp[j];
   const double2* pj = part + static_cast<size_t>(j) * (E + 1);
   const int e = f * kBinsPerFeature + tid;
   const double2 sm = pj[e];
+  if (j >= nexp) return;
+  const int small = x.left_small ? x.c0 : x.c1;
+  const int child = c == 0 ? small : (small == x.c0 ? x.c1 : x.c0);
   double2 mine = sm;
   if (c == 1) {
     const double2 par = hist_pool[static_cast<size_t>(x.node) * E + e];
