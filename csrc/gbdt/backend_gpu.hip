@@ -2891,38 +2891,12 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) w[u] = weight[iq[u]];
     }
-    // the kUnroll rows' tree walks step together: each level's node reads (LDS) of the rows are independent,
-    // so their latencies overlap instead of one walk finishing before the next starts
-    int node[kUnroll];
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) node[u] = (ni > 0 && base + u * kThreads < p1) ? 0 : ~0;
-    for (int guard = 0; guard < num_leaves; ++guard) {
-      bool live = false;
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        if (node[u] >= 0) {
-          const int4 nd = snodes[node[u]];
-          node[u] = NodeStep(nd, ByteOfRow(b0[u], b1[u], nd.x & 0xFFFF), cat_bits, node[u]);
-          live = true;
-        }
-      }
-      if (!live) break;
-    }
+    // (stepping the kUnroll rows' tree walks together measured slower - 274.8 -> 281.9 us, r4 pass 18 - the
+    // extra live state spills at this kernel's 128-VGPR cap)
     // all 32 slots (b1 = 0 when F <= 16: bin 0 of unused slots): one code path keeps this kernel unspilled
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int i = base + u * kThreads;
-      if (i >= p1) continue;
-      const double sn = s[u] + scale * slval[ni > 0 ? ~node[u] : 0];
-      score[i] = sn;
-      float gg, hh;
-      PointGradient(p, sn, y[u], w[u], &gg, &hh);
-      g[i] = gg;
-      h[i] = hh;
-      mg = fmaxf(mg, fabsf(gg));
-      mh = fmaxf(mh, fabsf(hh));
-      hist_accumulate_rot<32, kFeatPerGroup>(shg, shh, b0[u], b1[u], QuantGH(make_float2(gg, hh), sc), rot);
-    }
+    for (int u = 0; u < kUnroll; ++u)
+      if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u]);
   }
   BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
   __syncthreads();
