@@ -734,7 +734,7 @@ __device__ __forceinline__ void DmaToLds16(__amdgpu_buffer_rsrc_t r, void* dst, 
 #endif
 }
 
-template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false>
+template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false, int kNB = 2>
 __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   static_assert(sizeof(T) == 2, "LDS-DMA conv is the f16 / bf16 form");
@@ -745,14 +745,16 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;  // 8-row DMA pieces per wave and tile
   static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
-  constexpr int kOpBytes = 2 * (BM + BN) * kBK * 2;
+  // kNB LDS buffers: 2 (tile kt + 1 lands while kt computes), 1 for a single-K-tile layer (the 1x1 layers on
+  // 64 channels): half the LDS, twice the resident blocks to hide their memory-bound epilogue
+  constexpr int kOpBytes = kNB * (BM + BN) * kBK * 2;
   constexpr int kProBytes = kPro ? 2 * 2 * 1024 : 0;  // [buf][scale | shift][256 floats]: one DMA each
   constexpr int kEpiBytes = NW * WM * (WN + 8) * 2;
   __shared__ __attribute__((aligned(16)))
   unsigned char smem[kOpBytes + kProBytes > kEpiBytes ? kOpBytes + kProBytes : kEpiBytes];
   T* lds = reinterpret_cast<T*>(smem);
   T* As = lds;                 // [buf][BM][64], swizzled chunks
-  T* Bs = lds + 2 * BM * kBK;  // [buf][BN][64]
+  T* Bs = lds + kNB * BM * kBK;  // [buf][BN][64]
   float* Ps = reinterpret_cast<float*>(smem + kOpBytes);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -920,7 +922,13 @@ void LaunchPersist(const ConvArgs& a, int M, hipStream_t st) {
 template <class T, int BM, int BN, int kThr, int kWN = 2>
 void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
   const int blocks = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  static const bool single = [] {
+    const char* e = std::getenv("SML_CONV_GLDS_SINGLE");
+    return !e || std::atoi(e) != 0;
+  }();
   if (a.in_scale) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, true>), dim3(blocks), dim3(kThr), 0, st, a);
+  else if (single && a.R * a.S * a.C == 64)  // one K tile: no second buffer to fill (SML_CONV_GLDS_SINGLE=0: off)
+    hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 1>), dim3(blocks), dim3(kThr), 0, st, a);
   else hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
 }
 
