@@ -1392,7 +1392,7 @@ __global__ __launch_bounds__(256) void stem_rowbuf_kernel(ConvArgs a) {
 // dilation it stages, and its LDS (static operand tiles + R staged rows) within two blocks per CU
 inline int RowbufLds(const ConvArgs& a) { return a.R * (a.W + 2 * kRowPad) * 3 * 2; }
 inline bool RowbufOk(const ConvArgs& a) {
-  return a.C == 3 && a.S * 3 <= 21 && a.OW <= kStemBM && a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= kRowPad && a.R <= 8 && a.S <= 8 &&
+  return reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && a.C == 3 && a.S * 3 <= 21 && a.OW <= kStemBM && a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= kRowPad && a.R <= 8 && a.S <= 8 &&
          (a.W * 3 * 2) % 16 == 0 && (a.OW - 1) * a.stride_w - a.pad_w + a.S <= a.W + kRowPad &&
          RowbufLds(a) <= 12 * 1024;
 }
