@@ -2571,6 +2571,7 @@ __global__ __launch_bounds__(kRedE * kRedG) void breduce_kernel(const BState* __
                                                                  const float* __restrict__ ghmax,
                                                                  double2* __restrict__ part) {
   const int nexp = bs->nexp;
+  const float gmax_g = ghmax[0], gmax_h = ghmax[1];  // with the count: not a late dependent load
   const int j = blockIdx.y;
   if (j >= nexp) return;
   const int tid = threadIdx.x, le = tid % kRedE, grp = tid / kRedE;
@@ -2602,7 +2603,7 @@ __global__ __launch_bounds__(kRedE * kRedG) void breduce_kernel(const BState* __
     unsigned long long tg = 0, th = 0;
 #pragma unroll
     for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
-    const HScale s = HistScale(count, ghmax);
+    const HScale s = HistScaleV(count, gmax_g, gmax_h);
     const int F = E / kBinsPerFeature;
     const int bin = e / F, f = e - bin * F;
     out[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
