@@ -1139,13 +1139,23 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(ConvArgs a) {
   const int m0 = blockIdx.x * kStemBM, n0 = blockIdx.y * kStemBN;
   const int S = a.S, R = a.R, run = S * C, K = R * run;
   const T* __restrict__ w = static_cast<const T*>(a.w);
-  // weights: 64 rows x 160 (already zero-padded by the packer), 16-B chunks
-  for (int q = tid; q < kStemBN * (kStemKP / 8); q += 256) {
-    const int row = q / (kStemKP / 8), ch = q % (kStemKP / 8);
-    const int n = n0 + row;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (n < a.Cout) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + ch * 8);
-    *reinterpret_cast<uint4*>(Bs + row * kStemLd + ch * 8) = v;
+  // weights: 64 rows x 160 (already zero-padded by the packer), 16-B chunks - all 5 per thread in flight
+  // before the first LDS store (the row-staged form's measured fix: one memory latency, not five)
+  {
+    constexpr int kWIt = kStemBN * (kStemKP / 8) / 256;
+    uint4 wv[kWIt];
+#pragma unroll
+    for (int i = 0; i < kWIt; ++i) {
+      const int q = tid + i * 256;
+      const int n = n0 + q / (kStemKP / 8);
+      wv[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(n) * kStemKP + (q % (kStemKP / 8)) * 8)
+                         : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kWIt; ++i) {
+      const int q = tid + i * 256;
+      *reinterpret_cast<uint4*>(Bs + (q / (kStemKP / 8)) * kStemLd + (q % (kStemKP / 8)) * 8) = wv[i];
+    }
   }
   // the padded K tail of every A row is zero (NaN-free with the zero weight tail): every 16-B chunk from the
   // last partial one to kKP (the im2col runs below overwrite the real part of that first chunk)
