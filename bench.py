@@ -127,7 +127,9 @@ def main() -> None:
     # more ranks than GPUs (a rehearsal of the multi-GPU path on a small box): ranks share devices, so the
     # control plane is gloo and histograms go over the one-shot IPC allreduce on a host base communicator
     # (RCCL cannot put two ranks on one device). The driver's N-GPU runs have one GPU per rank.
-    shared = use_gpu and local_world > ndev and not per_rank_vis
+    # (--allow-shared-device asks for the rehearsal outright: a 1-GPU box may export its one device in
+    # HIP_VISIBLE_DEVICES for every rank, which looks like per-rank visibility but is one shared device)
+    shared = use_gpu and local_world > ndev and (args.allow_shared_device or not per_rank_vis)
     if shared and not args.allow_shared_device:
         print(f"bench.py: {world} ranks but only {ndev} visible GPU(s); a {world}-GPU measurement needs {world} "
               "devices (pass --allow-shared-device for a shared-device rehearsal)", file=sys.stderr)
