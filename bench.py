@@ -10,11 +10,12 @@ The timed region is everything the reference's ``LightGBMBase.train``
 (lightgbm/.../LightGBMBase.scala:36-65,396-447) does after the DataFrame
 exists: column extraction, row sampling + bin boundaries (reference dataset),
 dataset construction (K1 device bin encode), booster creation, 100 boosting
-iterations, and the returned LightGBMClassificationModel (model string).
+iterations, and the returned LightGBMClassificationModel with its model
+string (forced inside the timed loop: the engine builds the text lazily).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
 N > 1 it runs under torch.distributed.run with one rank per GPU (RCCL
-histogram allreduce inside the engine). Started WITHOUT a torchrun
+histogram allreduce inside the engine; gloo control plane). Started WITHOUT a torchrun
 environment and ``--gpus N > 1``, this script launches
 ``python -m torch.distributed.run --nproc-per-node N bench.py ...`` as a child
 process before anything touches the GPU (the parent never imports torch),
@@ -119,40 +120,35 @@ def main() -> None:
     import torch
 
     use_gpu = args.device == "gpu" and torch.cuda.is_available()
-    ndev = torch.cuda.device_count() if use_gpu else 0
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    # a launcher that gives every rank its own single visible device (HIP/ROCR/CUDA_VISIBLE_DEVICES per rank)
-    per_rank_vis = ndev == 1 and any(len([x for x in os.environ.get(v, "").split(",") if x.strip()]) == 1
-                                     for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
-    # more ranks than GPUs (a rehearsal of the multi-GPU path on a small box): ranks share devices, so the
-    # control plane is gloo and histograms go over the one-shot IPC allreduce on a host base communicator
-    # (RCCL cannot put two ranks on one device). The driver's N-GPU runs have one GPU per rank.
-    # (--allow-shared-device asks for the rehearsal outright: a 1-GPU box may export its one device in
-    # HIP_VISIBLE_DEVICES for every rank, which looks like per-rank visibility but is one shared device)
-    shared = use_gpu and local_world > ndev and (args.allow_shared_device or not per_rank_vis)
-    if shared and not args.allow_shared_device:
-        print(f"bench.py: {world} ranks but only {ndev} visible GPU(s); a {world}-GPU measurement needs {world} "
-              "devices (pass --allow-shared-device for a shared-device rehearsal)", file=sys.stderr)
-        sys.exit(3)
     if use_gpu:
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
     from synapseml_amd.parallel import distributed as D
 
+    # Control plane: gloo over TCP for every world size. The histogram data plane is the engine's own RCCL
+    # communicator (ncclUniqueId handed out over this control plane, P2P one-shot over xGMI on top), so
+    # nothing needs an NCCL default group - and the device identities below are agreed on BEFORE any RCCL
+    # object exists: ranks that share a GPU are refused (or run the rehearsal) with a clear message instead of
+    # RCCL's "Duplicate GPU detected" crash.
     if world > 1:
-        D.init_from_env("nccl" if use_gpu and not shared else "gloo")
-        if shared:
-            os.environ["SML_GBDT_SHARED_DEVICE"] = "1"
+        D.init_from_env("gloo")
     distinct = 0
+    shared = False
     if use_gpu:
         # the devices really in use, by identity (uuid / PCI location), over every rank
         pr = torch.cuda.get_device_properties(torch.cuda.current_device())
         ident = str(getattr(pr, "uuid", "")) + ":%s:%s:%s" % (getattr(pr, "pci_domain_id", ""),
                                                               getattr(pr, "pci_bus_id", ""), getattr(pr, "pci_device_id", ""))
         distinct = len(set(D.all_gather_object(ident)))
-        if distinct != world and not args.allow_shared_device:
+        shared = distinct < world
+        if shared and not args.allow_shared_device:
             print(f"bench.py: {world} ranks run on {distinct} distinct GPU(s); refusing to report it as a "
-                  f"{world}-GPU measurement", file=sys.stderr)
+                  f"{world}-GPU measurement (pass --allow-shared-device for a shared-device rehearsal)",
+                  file=sys.stderr)
             sys.exit(3)
+        if shared:
+            # ranks share devices: RCCL cannot put two ranks on one device, so histograms go over the one-shot
+            # IPC allreduce on a host base communicator
+            os.environ["SML_GBDT_SHARED_DEVICE"] = "1"
     from synapseml_amd.core.dataframe import DataFrame
     from synapseml_amd.lightgbm import LightGBMClassifier
     from synapseml_amd.ops import native
@@ -163,8 +159,6 @@ def main() -> None:
     # this rank's partition of the training DataFrame (one process per GPU = one Spark executor)
     df = DataFrame({"features": X, "label": y})
     gen_s = time.perf_counter() - t_gen
-    n_hold = min(200_000, args.rows)
-    X_hold, y_hold = X[:n_hold].astype(np.float64), y[:n_hold]
     del X
 
     est = LightGBMClassifier(numIterations=args.iterations, learningRate=0.1, numLeaves=args.leaves, maxBin=255,
@@ -178,6 +172,7 @@ def main() -> None:
     model = None
     for _ in range(args.warmup):
         model = est.fit(df)
+        model.getNativeModel()
     sync()
     D.barrier()
     sync()
@@ -185,6 +180,9 @@ def main() -> None:
     measures = []
     for _ in range(args.steps):
         model = est.fit(df)
+        # the returned model's LightGBM text, as the reference's fit serialises the booster before it returns
+        # (BasePartitionTask.scala:450-461); this engine builds the text lazily, so it is forced here
+        model.getNativeModel()
         measures.append(est.getPerformanceMeasures()[0])
     sync()
     D.barrier()
@@ -193,7 +191,7 @@ def main() -> None:
     if world > 1:
         import torch.distributed as dist
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu and not shared else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -204,13 +202,16 @@ def main() -> None:
         phases[k] = round(float(np.mean(vals)), 2) if vals else None
     native_stats = measures[-1].get("native_stats", {}) if measures else {}
     iter_s = (phases["training_iterations_ms"] or 0.0) / 1e3
-    # sanity (outside the timed region): holdout AUC of the last model on this rank's first rows
+    # sanity (outside the timed region): AUC of the last model on 200k fresh rows of the same distribution
+    # (a different seed from every rank's training rows: a real holdout, not a train AUC)
     auc = None
+    n_hold = min(200_000, args.rows)
     if rank == 0 and model is not None:
         try:
             from sklearn.metrics import roc_auc_score
 
-            p = model.getModel().score(X_hold, raw=False, classification=True)[:, 1]
+            X_hold, y_hold = higgs_like(n_hold, args.features, seed=987_654)
+            p = model.getModel().score(X_hold.astype(np.float64), raw=False, classification=True)[:, 1]
             auc = float(roc_auc_score(y_hold, p))
         except Exception:  # pragma: no cover
             auc = None
@@ -253,16 +254,19 @@ def main() -> None:
                 "distinct_devices": n_devices,
                 "shared_device_rehearsal": bool(shared),
                 "data_plane_world": comm_world,
+                "control_plane": "gloo" if world > 1 else None,
                 "data_plane": (None if world == 1 else type(comm).__name__ if comm is None else
                                ("rccl" if use_gpu and not shared else "host") +
                                ("+p2p-ipc" if D.p2p_status.get("active") else "")),
-                "timed_region": "LightGBMClassifier.fit(df) end to end (DataFrame built before timing)",
+                "timed_region": "LightGBMClassifier.fit(df) end to end + the model's LightGBM text "
+                                "(DataFrame built before timing)",
                 "fit_phases_ms": phases,
                 "iteration_loop_row_iters_per_s": round(total_rows * args.iterations / iter_s, 1) if iter_s else None,
                 "iteration_ms": round(phases["training_iterations_ms"] / args.iterations, 3)
                 if phases["training_iterations_ms"] else None,
                 "backend": measures[-1].get("backend") if measures else None,
-                "holdout_auc_first_rows": auc,
+                "holdout_auc": auc,
+                "holdout_rows": n_hold,
                 "datagen_s": round(gen_s, 2),
                 "native_comm_ms": native_stats.get("comm_ms"),
                 "histogram_accumulation": "int64 fixed point per (feature, bin), exact int64 block reduce -> fp64",

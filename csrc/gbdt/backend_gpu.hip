@@ -949,28 +949,81 @@ __device__ __forceinline__ QGH QuantGH(float2 v, const HScale& s) {
 // pass of profiles/r2_pmc.) The row is rotated once in registers (two dword-rotation selects + alignbyte),
 // so every step extracts a fixed byte. Slots f >= Fg of a partial group collect the row's padding bytes
 // (always < 256) and are never read.
-template <int S, int kFPG>
+// All-ones when bit `B` of x is set, else 0 (v_bfe_i32 x, B, 1). Kept opaque to the optimiser on purpose: a
+// plain `cond ? a : b` over the row's dwords was turned into a dynamically indexed select - a 7-deep
+// v_cmp / v_cndmask / s_nop chain per dword (~170 VALU per row in the root pass's ISA); with an opaque mask
+// each select is one v_bfi_b32.
+template <int B>
+__device__ __forceinline__ uint32_t BitMask(uint32_t x) {
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(x), "i"(B));
+  return m;
+}
+
+__device__ __forceinline__ uint32_t SelBits(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
+// The row rotated by `rot` bytes (0..S-1 lanes' residues): r byte j = row byte (j + rot) mod S, S = 4 * NW
+template <int NW>
+__device__ __forceinline__ void RotateRow(const uint4& b0, const uint4& b1, uint32_t rot, uint32_t* r) {
+  const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  const uint32_t m1 = BitMask<2>(rot), m2 = BitMask<3>(rot);
+  uint32_t v[NW], u[NW];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = SelBits(m1, w[(k + 1) % NW], w[k]);
+#pragma unroll
+  for (int k = 0; k < NW; ++k) u[k] = SelBits(m2, v[(k + 2) % NW], v[k]);
+#pragma unroll
+  for (int k = 0; k < NW; ++k) r[k] = __builtin_amdgcn_alignbyte(u[(k + 1) % NW], u[k], rot & 3u);
+}
+
+// Per-thread table for the 32-slot bin-major histogram (kFPG = 32, 8-B slots: byte address of slot (b, f) =
+// b * 256 + f * 8): byte k of fo[q] = 8 * ((4q + k + rot) mod 32), the slot offset of step j = 4q + k. One
+// v_perm_b32 per step then builds the LDS byte address from it and the rotated row's byte:
+// perm(fo[q], r[q], 0x0C0C'k'(4+k)) = (row byte << 8) | fo byte.
+__device__ __forceinline__ void SlotOffsets32(uint32_t rot, uint32_t* fo) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x |= (((4u * q + k + rot) & 31u) * 8u) << (8 * k);
+    fo[q] = x;
+  }
+}
+
+// h plane base (bytes from the g plane) when every real feature of the group is below slot 28: the g plane's
+// slots (bin 255, f 28..31) then coincide with the h plane's (bin 0, f 0..3) and are never written (padding
+// bytes are 0, so padding slots only ever receive bin 0) nor read - and the h atomic's address fits the DS
+// instruction's 16-bit offset (no add per step). Otherwise the planes are 64 KiB apart.
+constexpr uint32_t kHPlaneTight = 65536u - 32u;
+constexpr uint32_t kHPlaneApart = 65536u;
+
+template <int S, int kFPG, uint32_t kHOff = kHPlaneApart>
 __device__ __forceinline__ void hist_accumulate_rot(unsigned long long* shg, unsigned long long* shh,
-                                                    const uint4& b0, const uint4& b1, const QGH& q, int rot) {
+                                                    const uint4& b0, const uint4& b1, const QGH& q, int rot,
+                                                    const uint32_t* fo = nullptr) {
   static_assert(S == 16 || S == 32, "16 or 32 features per rotated row");
   static_assert(kFPG % 16 == 0 && S <= kFPG, "slots per bin");
   constexpr int NW = S / 4;
-  uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-  const int qd = rot >> 2, rb = rot & 3;
-  uint32_t v[NW], u[NW], r[NW];
+  uint32_t r[NW];
+  RotateRow<NW>(b0, b1, static_cast<uint32_t>(rot), r);
+  if constexpr (S == 32 && kFPG == 32) {
+    // shg / shh are kHOff bytes apart (caller's layout); one perm per step gives the slot's byte address
+    char* base = reinterpret_cast<char*>(shg);
 #pragma unroll
-  for (int k = 0; k < NW; ++k) v[k] = (qd & 1) ? w[(k + 1) % NW] : w[k];
+    for (int j = 0; j < S; ++j) {
+      const uint32_t sel = 0x0C0C0000u | ((j & 3u) << 8) | (4u + (j & 3u));
+      const uint32_t a = __builtin_amdgcn_perm(fo[j >> 2], r[j >> 2], sel);
+      atomicAdd(reinterpret_cast<unsigned long long*>(base + a), q.g);
+      atomicAdd(reinterpret_cast<unsigned long long*>(base + a + kHOff), q.h);
+    }
+  } else {
 #pragma unroll
-  for (int k = 0; k < NW; ++k) u[k] = (qd & 2) ? v[(k + 2) % NW] : v[k];
-  // r byte j = row byte (j + rot) mod S
-#pragma unroll
-  for (int k = 0; k < NW; ++k) r[k] = __builtin_amdgcn_alignbyte(u[(k + 1) % NW], u[k], static_cast<uint32_t>(rb));
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const int f = (j + rot) & (S - 1);
-    const int i = static_cast<int>((r[j >> 2] >> (8 * (j & 3))) & 255u) * kFPG + f;
-    atomicAdd(&shg[i], q.g);
-    atomicAdd(&shh[i], q.h);
+    for (int j = 0; j < S; ++j) {
+      const int f = (j + rot) & (S - 1);
+      const int i = static_cast<int>((r[j >> 2] >> (8 * (j & 3))) & 255u) * kFPG + f;
+      atomicAdd(&shg[i], q.g);
+      atomicAdd(&shh[i], q.h);
+    }
   }
 }
 
@@ -1000,7 +1053,7 @@ __device__ __forceinline__ void SlabWrite(ulonglong2* out, const unsigned long l
 // One block's share of a leaf histogram: rows [begin, begin + count) of ping-pong buffer `buf` (-1 =
 // physical rows) are cut into nb_active chunks; this block (chunk lb, feature group blockIdx.y) accumulates
 // its chunk into LDS and writes its slab.
-template <int kUnroll, int kFPG, bool kPipe = false>
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false>
 __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_active, int lb, const uint4* __restrict__ bins4,
                                          int W4, int F, const int32_t* __restrict__ perm0,
                                          const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
@@ -1008,11 +1061,18 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
                                          const float* __restrict__ h, const float* __restrict__ ghmax,
                                          ulonglong2* __restrict__ slab_out) {
   constexpr int kWords = kFPG * kBinsPerFeature;
-  __shared__ unsigned long long shg[kWords], shh[kWords];
+  // g plane at 0, h plane kHOff bytes above it (kTight: F <= 28, see kHPlaneTight)
+  constexpr uint32_t kHOff = kFPG == 32 ? (kTight ? kHPlaneTight : kHPlaneApart) : kWords * 8u;
+  constexpr int kShWords = static_cast<int>(kHOff / 8) + kWords;
+  __shared__ unsigned long long sh[kShWords];
+  unsigned long long* shg = sh;
+  unsigned long long* shh = sh + kHOff / 8;
   const int tid = threadIdx.x;
   // the fixed-point scale's inputs load while the LDS histogram is zeroed (not after the barrier)
   const float gmax_g = ghmax[0], gmax_h = ghmax[1];
-  for (int i = tid; i < kWords; i += kHistBlockThreads) { shg[i] = 0ull; shh[i] = 0ull; }
+  for (int i = tid; i < kShWords; i += kHistBlockThreads) sh[i] = 0ull;
+  uint32_t fo[8];
+  if constexpr (kFPG == 32) SlotOffsets32(static_cast<uint32_t>(tid & 15), fo);
   __syncthreads();
   const int grp = blockIdx.y;
   const int Fg = min(kFPG, F - grp * kFPG);
@@ -1064,7 +1124,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)
         if (base + u * kHistBlockThreads < p1) {
-          if (kFPG > 16 && two) hist_accumulate_rot<(kFPG > 16 ? 32 : 16), kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
+          if (kFPG > 16 && two) hist_accumulate_rot<(kFPG > 16 ? 32 : 16), kFPG, kHOff>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot, fo);
           else hist_accumulate_rot<16, kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
         }
 #pragma unroll
@@ -1099,7 +1159,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
       if (ok[u]) {
-        if (kFPG > 16 && two) hist_accumulate_rot<(kFPG > 16 ? 32 : 16), kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
+        if (kFPG > 16 && two) hist_accumulate_rot<(kFPG > 16 ? 32 : 16), kFPG, kHOff>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot, fo);
         else hist_accumulate_rot<16, kFPG>(shg, shh, b0[u], b1[u], QuantGH(v[u], sc), rot);
       }
   }
@@ -1109,7 +1169,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
 
 // kFPG features per block (blockIdx.y = feature group): 32 = one 128 KB LDS histogram per CU; 16 halves
 // the LDS (two blocks per CU) at the price of reading every row's perm / g / h once per group
-template <int kUnroll, int kFPG, bool kPipe = false>
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false>
 __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
@@ -1119,7 +1179,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
   const DLeaf L = HistSeg(st, leaves);
   const int nb_active = HistBlocks(L.count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  HistBody<kUnroll, kFPG, kPipe>(L.begin, L.count, L.buf, nb_active, blockIdx.x, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
+  HistBody<kUnroll, kFPG, kPipe, kTight>(L.begin, L.count, L.buf, nb_active, blockIdx.x, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
                           ghmax, slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature);
 }
 
@@ -2540,7 +2600,7 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   }
 }
 
-template <int kUnroll, int kFPG, bool kPipe = false>
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false>
 __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
     const BState* __restrict__ bs, const uint4* __restrict__ bins4, int W4, int F, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
@@ -2561,7 +2621,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   const BExp& x = bs->exp[j];
   const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
   const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
-  HistBody<kUnroll, kFPG, kPipe>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
+  HistBody<kUnroll, kFPG, kPipe, kTight>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
                           ogh1, g, h, ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature);
 }
 
@@ -2690,10 +2750,17 @@ __device__ __forceinline__ void StageDeviceTree(const DevTreeSrc& src, int num_l
   for (int i = tid; i < num_leaves; i += nthreads) slval[i] = src.t.lval[i] * src.shrink;
 }
 
+// Byte f (0..31) of a 32-byte row held in registers: one v_perm_b32 per dword pair picks byte f & 7 of that
+// pair, and two levels of opaque-mask selects (bits 3 and 4 of f) pick the pair - 10 VALU, no VCC hazards
+// (the nested ternary compiled to a 7-deep compare / cndmask / s_nop chain per tree-walk step).
 __device__ __forceinline__ uint32_t ByteOfRow(const uint4& a, const uint4& b, int f) {
-  const int w = f >> 2;
-  uint32_t x = w == 0 ? a.x : w == 1 ? a.y : w == 2 ? a.z : w == 3 ? a.w : w == 4 ? b.x : w == 5 ? b.y : w == 6 ? b.z : b.w;
-  return (x >> (8 * (f & 3))) & 255u;
+  const uint32_t sel = 0x0C0C0C00u | (static_cast<uint32_t>(f) & 7u);
+  const uint32_t p0 = __builtin_amdgcn_perm(a.y, a.x, sel);
+  const uint32_t p1 = __builtin_amdgcn_perm(a.w, a.z, sel);
+  const uint32_t p2 = __builtin_amdgcn_perm(b.y, b.x, sel);
+  const uint32_t p3 = __builtin_amdgcn_perm(b.w, b.z, sel);
+  const uint32_t m3 = BitMask<3>(static_cast<uint32_t>(f)), m4 = BitMask<4>(static_cast<uint32_t>(f));
+  return SelBits(m4, SelBits(m3, p3, p2), SelBits(m3, p1, p0));
 }
 
 __device__ __forceinline__ int NodeStep(const int4& nd, uint32_t b, const uint32_t* cat_bits, int node) {
@@ -2799,7 +2866,7 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
 // Replaces score_kernel + grad_kernel + the root hist_kernel (150 + 54 + 131
 // us at 11M x 28 on MI355X, three full passes over rows).
 
-template <int kUnroll, bool kPipe = false>
+template <int kUnroll, bool kPipe = false, bool kTight = false>
 __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
@@ -2808,14 +2875,20 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   constexpr int kThreads = kHistBlockThreads;
   const int nb_active = HistBlocks(n);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
-  __shared__ unsigned long long shg[kHistWords], shh[kHistWords];
+  constexpr uint32_t kHOff = kTight ? kHPlaneTight : kHPlaneApart;  // h plane above the g plane (HistBody)
+  constexpr int kShWords = static_cast<int>(kHOff / 8) + kHistWords;
+  __shared__ unsigned long long sh[kShWords];
+  unsigned long long* shg = sh;
+  unsigned long long* shh = sh + kHOff / 8;
   __shared__ int4 snodes[kPrepMaxNodes];
   __shared__ double slval[kPrepMaxNodes + 1];
   const int tid = threadIdx.x;
   const int num_leaves = src.st ? src.st->num_leaves : tv.num_leaves;
   const int ni = num_leaves - 1;
   const uint32_t* cat_bits = src.st ? src.t.cat_bits : tv.cat_bits;
-  for (int i = tid; i < kHistWords; i += kThreads) { shg[i] = 0ull; shh[i] = 0ull; }
+  for (int i = tid; i < kShWords; i += kThreads) sh[i] = 0ull;
+  uint32_t fo[8];
+  SlotOffsets32(static_cast<uint32_t>(tid & 15), fo);
   if (src.st) {
     StageDeviceTree(src, num_leaves, snodes, slval, tid, kThreads);
   } else {
@@ -2845,7 +2918,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     h[i] = hh;
     mg = fmaxf(mg, fabsf(gg));
     mh = fmaxf(mh, fabsf(hh));
-    hist_accumulate_rot<32, kFeatPerGroup>(shg, shh, r0, r1, QuantGH(make_float2(gg, hh), sc), rot);
+    hist_accumulate_rot<32, kFeatPerGroup, kHOff>(shg, shh, r0, r1, QuantGH(make_float2(gg, hh), sc), rot, fo);
   };
   if constexpr (kPipe) {
     // the next step's bins / score / label / weight are loaded before this step's rows are processed
@@ -3034,6 +3107,9 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
     if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
     if (const char* e = std::getenv("SML_GBDT_HIST_PIPE")) hist_pipe_ = std::atoi(e) != 0;
+    // overlapped LDS planes (kHPlaneTight) need every group's features below slot 28
+    tight_ = F_ <= 28;
+    if (const char* e = std::getenv("SML_HIST_TIGHT")) tight_ = tight_ && std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_RANK_WAVES")) rank_waves_ = std::atoi(e) == 4 ? 4 : 1;
     if (const char* e = std::getenv("SML_RANK_TREDUCE")) rank_treduce_ = std::atoi(e) != 0;
     voting_ = cfg.tree_learner == "voting" && Distributed();
@@ -3478,7 +3554,8 @@ class GpuBackend : public TrainBackend {
     auto bh = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16>
               : (hist_unroll4_ ? bhist_kernel<4, kFeatPerGroup>
                                : (hist_pipe_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, true>
-                                             : bhist_kernel<kHistUnroll, kFeatPerGroup>));
+                                             : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true>
+                                                       : bhist_kernel<kHistUnroll, kFeatPerGroup>)));
     int r = 0;
     for (; r <= max_rounds; ++r) {
       if (r >= blook_) {
@@ -3621,7 +3698,8 @@ class GpuBackend : public TrainBackend {
   // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
   void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
     if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    auto sgk = hist_pipe_ ? score_grad_hist_kernel<kHistUnroll, true> : score_grad_hist_kernel<kHistUnroll>;
+    auto sgk = hist_pipe_ ? score_grad_hist_kernel<kHistUnroll, true>
+                          : (tight_ ? score_grad_hist_kernel<kHistUnroll, false, true> : score_grad_hist_kernel<kHistUnroll>);
     hipLaunchKernelGGL(sgk, dim3(kMaxHistBlocks), dim3(kHistBlockThreads), 0, stream_, tv, src,
                        reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, static_cast<int32_t>(n_), scale,
                        score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
@@ -3736,7 +3814,8 @@ class GpuBackend : public TrainBackend {
     auto hk = hist_fpg_ == 16 ? hist_kernel<kHistUnroll, 16>
               : (hist_unroll4_ ? hist_kernel<4, kFeatPerGroup>
                                : (hist_pipe_ ? hist_kernel<kHistUnroll, kFeatPerGroup, true>
-                                             : hist_kernel<kHistUnroll, kFeatPerGroup>));
+                                             : (tight_ ? hist_kernel<kHistUnroll, kFeatPerGroup, false, true>
+                                                       : hist_kernel<kHistUnroll, kFeatPerGroup>)));
     hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
                        perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
@@ -3931,6 +4010,7 @@ class GpuBackend : public TrainBackend {
   int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
   bool hist_unroll4_ = false;     // SML_HIST_UNROLL=4: 4 gathered rows in flight per thread (A/B knob)
   bool hist_pipe_ = false;        // SML_GBDT_HIST_PIPE=1: software-pipelined histogram loops (A/B knob)
+  bool tight_ = false;            // h LDS plane inside the DS offset range of the g plane (F <= 28; SML_HIST_TIGHT=0 off)
   // lambdarank register kernel: waves per block. SML_RANK_WAVES=4 packs 4 independent waves per block (up
   // to 10 resident per SIMD instead of 4): r4 pass 11 measured it slower (949 vs 860 us per call, ranker
   // fit 33.6M vs 34.0M rows/s), so one-wave blocks stay the default

@@ -53,10 +53,20 @@ void FillExample(Example* ex, const std::vector<Block>& blocks, int64_t row) {
   }
 }
 
+// RCCL communicator of the device learner's weight averaging. A collective that failed or timed out (a peer
+// died) aborts it: ncclCommAbort unblocks kernels of pending collectives, and the broken group is never
+// destroyed collectively (ncclCommDestroy on it could wait for the dead peer).
 struct NcclHandle {
   ncclComm_t c = nullptr;
   int world = 1;
-  ~NcclHandle() { if (c) ncclCommDestroy(c); }
+  double timeout_ms = 0;
+  bool aborted = false;
+  void Abort() {
+    if (c && !aborted) (void)ncclCommAbort(c);
+    aborted = true;
+    c = nullptr;
+  }
+  ~NcclHandle() { if (c && !aborted) ncclCommDestroy(c); }
 };
 }  // namespace
 
@@ -388,7 +398,10 @@ PYBIND11_MODULE(_vw, m) {
     return std::shared_ptr<VW>(VW::Merge(v));
   });
 
-  py::class_<NcclHandle, std::shared_ptr<NcclHandle>>(m, "NcclComm");
+  m.def("_stager_rejects_null", &StagerRejectsNull);
+  py::class_<NcclHandle, std::shared_ptr<NcclHandle>>(m, "NcclComm")
+      .def("abort", &NcclHandle::Abort)
+      .def_property_readonly("aborted", [](const NcclHandle& h) { return h.aborted; });
   m.def("nccl_unique_id", []() {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
@@ -425,6 +438,7 @@ PYBIND11_MODULE(_vw, m) {
       }
     }
     h->world = world;
+    h->timeout_ms = timeout_ms;
     return h;
   }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("timeout_ms") = 120000.0);
 
@@ -585,8 +599,14 @@ PYBIND11_MODULE(_vw, m) {
              return out;
            })
       .def("allreduce_average", [](GpuSgd& g, std::shared_ptr<NcclHandle> h) {
+        if (h->aborted) throw std::runtime_error("VW RCCL communicator was aborted by an earlier failure");
         py::gil_scoped_release rel;
-        g.AllReduceAverage(h->c, h->world);
+        try {
+          g.AllReduceAverage(h->c, h->world, h->timeout_ms);
+        } catch (...) {
+          h->Abort();
+          throw;
+        }
       })
       // model bytes in the host learner's format (vw_core.cpp VW::SaveModel), built from the device nonzeros
       .def("export_model", [](const GpuSgd& g, const std::string& args) {

@@ -79,7 +79,8 @@ class GpuSgd {
   int64_t staged_examples() const { return staged_n_; }
   void CbStats(double* ips_num, double* snips_den, double* examples) const;
   // weighted average over ranks of the blocks touched since the last sync (RCCL on the learner's stream)
-  void AllReduceAverage(void* nccl_comm_handle, int world);
+  // timeout_ms > 0 bounds each collective's settling (a dead peer): past it the call throws
+  void AllReduceAverage(void* nccl_comm_handle, int world, double timeout_ms = 0);
   uint64_t NumWeights() const;
   // the table's nonzero components as (stride-4 index, value) - the host model format's records
   void ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val) const;
@@ -114,6 +115,8 @@ class GpuSgd {
 };
 
 bool VwGpuAvailable();
+// the pinned stager refuses a null source / destination (host-only; no HIP call is reached)
+bool StagerRejectsNull();
 // K13: murmur3_32(bytes[offsets[i]:offsets[i+1]], seed) & mask for every i, on the device
 void MurmurBatchGpu(const uint8_t* bytes, int64_t nbytes, const int64_t* offsets, int64_t n, uint32_t seed,
                     uint32_t mask, uint32_t* out);

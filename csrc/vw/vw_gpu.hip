@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -827,6 +828,10 @@ struct Stager {
   }
   // queue `bytes` from pageable `src` to device `dst` on stream s (caller holds mu)
   void Copy(char* dst, const char* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    // a null source or destination is a caller bug (round 4: a device scratch buffer "copied" from a null host
+    // pointer segfaulted the staging threads) - refuse it here instead of faulting in a memcpy thread
+    if (!src || !dst) throw std::invalid_argument("Stager::Copy: null source or destination for a non-empty copy");
     for (size_t off = 0; off < bytes; off += kStageBytes) {
       const int k = next;
       next = (next + 1) % kStage;
@@ -854,6 +859,18 @@ struct Stager {
   }
 };
 }  // namespace
+
+// Host-only check of the staging guard (it throws before any HIP call, so it runs without a GPU).
+bool StagerRejectsNull() {
+  Stager st;
+  char d[16];
+  try {
+    st.Copy(d, nullptr, sizeof(d), nullptr);
+  } catch (const std::invalid_argument&) {
+    return true;
+  }
+  return false;
+}
 
 struct GpuSgd::Impl {
   hipStream_t stream = nullptr, copy_stream = nullptr;
@@ -1411,15 +1428,24 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
 // Average the table over ranks: only the 64 KB blocks some rank touched since the last sync (the union
 // of the dirty maps, one small max-allreduce) are packed, reduced (fp64 sums of {wG or w, G}, max of N) and
 // unpacked with VW's weighted averaging - no host staging, and a sparse pass moves a fraction of the table.
-void GpuSgd::AllReduceAverage(void* comm, int world) {
+void GpuSgd::AllReduceAverage(void* comm, int world, double timeout_ms) {
   if (world < 1 || !comm) return;  // a world-1 communicator still runs the collectives (one-GPU tests)
   hipStream_t s = impl_->stream;
   ncclComm_t c = static_cast<ncclComm_t>(comm);
-  // the communicator is non-blocking (bounded init): an enqueue may answer ncclInProgress, and the next
-  // call must wait for the state to settle
-  auto nccl = [c](ncclResult_t r) {
-    while (r == ncclInProgress)
+  // the communicator is non-blocking (bounded init): an enqueue may answer ncclInProgress (the lazy peer
+  // connection of a first collective), and the next call must wait for the state to settle - bounded by
+  // timeout_ms, so a peer that died cannot leave this rank spinning (the caller then aborts the communicator)
+  auto nccl = [c, timeout_ms](ncclResult_t r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
       if (ncclCommGetAsyncError(c, &r) != ncclSuccess) r = ncclInternalError;
+      if (r != ncclInProgress) break;
+      if (timeout_ms > 0 &&
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms)
+        throw std::runtime_error("RCCL allreduce did not settle within " + std::to_string(timeout_ms) +
+                                 " ms (a peer rank failed)");
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
     if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL allreduce failed: ") + ncclGetErrorString(r));
   };
   const int64_t nblk = impl_->nblk;

@@ -459,6 +459,14 @@ class DataFrame:
             if pa.types.is_fixed_size_list(t) and (pa.types.is_floating(t.value_type) or pa.types.is_integer(t.value_type)):
                 flat = col.combine_chunks().flatten().to_numpy(zero_copy_only=False)
                 cols[name] = flat.reshape(len(col), t.list_size)
+            elif ((pa.types.is_list(t) or pa.types.is_large_list(t)) and
+                  (pa.types.is_floating(t.value_type) or pa.types.is_integer(t.value_type)) and col.null_count == 0
+                  and _uniform_list_width(col) is not None):
+                # array<double> (Spark's vector_to_array): equal-length rows become a 2-D array from the flat
+                # values buffer, with no per-row Python objects
+                w = _uniform_list_width(col)
+                flat = col.combine_chunks().flatten().to_numpy(zero_copy_only=False)
+                cols[name] = flat.reshape(len(col), w)
             elif pa.types.is_floating(t) or pa.types.is_integer(t) or pa.types.is_boolean(t):
                 cols[name] = col.to_numpy()
             else:
@@ -475,6 +483,16 @@ class DataFrame:
 
     def __repr__(self) -> str:
         return f"DataFrame[{', '.join(f'{k}: {t}' for k, t in self.dtypes)}] ({self._n} rows, {self.getNumPartitions()} partitions)"
+
+
+def _uniform_list_width(col):
+    """Common length of every row of a list column, or None when the lengths differ."""
+    arr = col.combine_chunks()
+    off = arr.offsets.to_numpy(zero_copy_only=False)
+    if len(off) < 2:
+        return 0
+    d = np.diff(off)
+    return int(d[0]) if (d == d[0]).all() else None
 
 
 def _arrow_value(x):

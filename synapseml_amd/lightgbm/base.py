@@ -357,7 +357,66 @@ class LightGBMBase(Estimator, LightGBMParams):
             json.dump(meta, f)
         os.replace(tmp, os.path.join(d, "latest.json"))
 
+    # Params of the reference's JVM data-transfer path. Here partitions reach HBM as columnar blocks through one
+    # path whatever their value, so an explicit setting is reported instead of silently ignored.
+    _INERT_PARAMS = {
+        "dataTransferMode": "partitions are always pushed as columnar blocks (the streaming and bulk JVM paths "
+                            "do not exist here)",
+        "executionMode": "deprecated in the reference; partitions are always pushed as columnar blocks",
+        "useSingleDatasetMode": "each task (one process per MI355X) always builds exactly one Dataset",
+        "microBatchSize": "rows are pushed in whole columnar blocks, not JVM micro-batches",
+        "chunkSize": "rows are pushed in whole columnar blocks, not JVM chunked arrays",
+        "maxStreamingOMPThreads": "the host encoder sizes its own thread pool",
+        "repartitionByGroupingColumn": "ranker rows are grouped inside each task instead of by a Spark shuffle",
+    }
+
+    def _warn_inert_params(self) -> None:
+        for name, why in self._INERT_PARAMS.items():
+            if self.hasParam(name) and self.isSet(name):
+                log.warning("%s=%r has no effect: %s", name, self.getOrDefault(name), why)
+
     def _fit(self, df: DataFrame):
+        from ..parallel import runtime as R
+
+        self._warn_inert_params()
+        if not R.in_partition_task():
+            from ..utils.cluster import _device_count
+
+            # counting devices does not initialise HIP in this (driver) process, which only spawns the tasks
+            use_gpu = self.getDeviceType() == "gpu" and _device_count() > 0
+            ntasks = R.determine_num_tasks(self.getNumTasks(), df, use_gpu)
+            if ntasks > 1:
+                return self._fit_tasks(df, ntasks, use_gpu)
+        return self._fit_local(df)
+
+    def _fit_tasks(self, df: DataFrame, ntasks: int, use_gpu: bool):
+        """Fan the fit out over ``ntasks`` partition tasks, one process (and one MI355X) each, as the
+        reference's fit does with barrier / plain mapPartitions (LightGBMBase.scala:608-628); the tasks
+        rendezvous on driverListenPort / defaultListenPort, train data-parallel (histogram allreduce over
+        RCCL) and the main task's model is returned (BasePartitionTask.scala:450-461)."""
+        from ..parallel import runtime as R
+
+        kw = {"timeout_s": max(60.0, float(self.getTimeout()))}
+        dp = int(self.getDriverListenPort() or 0)
+        if dp > 0:
+            kw["port"] = R.rendezvous_port(dp)
+        else:
+            kw["default_listen_port"] = int(self.getDefaultListenPort() or 0)
+        log.info("fit: %d partition tasks (%s)", ntasks, "gpu" if use_gpu else "cpu")
+        est = self.copy()
+        res = R.fan_out(R._FitTask(est, barrier=bool(self.getUseBarrierExecutionMode()), with_measures=True), df,
+                        ntasks, use_gpu, **kw)
+        model = res[0][0]
+        self._measures = list(res[0][1] or [])
+        self._task_measures = [r[1] for r in res]
+        return model
+
+    def getTaskMeasures(self) -> list:  # noqa: N802
+        """Per-task instrumentation of the last fanned-out fit, in task order
+        (LightGBMPerformance.setTaskMeasures)."""
+        return list(getattr(self, "_task_measures", []))
+
+    def _fit_local(self, df: DataFrame):
         self._measures = []
         nb = self.getNumBatches()
         batches = df.randomSplit([1.0] * nb, seed=self.getSeed() or 0) if nb and nb > 0 else [df]

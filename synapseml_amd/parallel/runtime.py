@@ -94,6 +94,19 @@ def _injected_fault(rank: int) -> Optional[str]:
 # no second copy on the worker side (an 11M x 28 float32 partition was a 1.2 GB pickle per rank). Object
 # columns (strings, vector objects) still travel pickled inside the small descriptor.
 _SHM_ALIGN = 64
+_SHM_DIR = "/dev/shm"
+
+
+def _shm_fits(nbytes: int) -> bool:
+    """True when /dev/shm has room for a segment of ``nbytes`` (plus 64 MiB of headroom for the other
+    segments of this job and the rest of the host); ``SML_SHM_HANDOFF=0`` forces the pickled hand-off."""
+    if os.environ.get("SML_SHM_HANDOFF", "1") == "0":
+        return False
+    try:
+        st = os.statvfs(_SHM_DIR)
+    except OSError:
+        return False
+    return st.f_bavail * st.f_frsize >= nbytes + (64 << 20)
 
 
 def _share_partition(df: DataFrame):
@@ -120,6 +133,12 @@ def _share_partition(df: DataFrame):
             plan.append((name, "shm", place(col)))
         else:
             plan.append((name, "pickle", pickle.dumps(col)))
+    if total and not _shm_fits(total):
+        # a small /dev/shm (Docker's 64 MB default, k8s without a Memory emptyDir): filling a segment past its
+        # free space raises SIGBUS inside the driver, so the partition travels pickled instead
+        desc = {"n": df.count(), "meta": {k: df.metadata(k) for k in df.columns}, "shm": None,
+                "cols": [(name, "pickle", pickle.dumps(df[name])) for name in df.columns]}
+        return pickle.dumps(desc), None
     shm = shared_memory.SharedMemory(create=True, size=max(total, 1)) if total else None
     if shm is not None:
         for off, a in arrays:
@@ -162,9 +181,11 @@ def _attach_partition(desc_bytes: bytes):
     return df, shm
 
 def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, parts_bytes: bytes, out_dir: str,
-            use_gpu: bool, attempt: int = 0) -> None:
+            use_gpu: bool, attempt: int = 0, env: Optional[dict] = None) -> None:
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      MASTER_PORT=str(port), SML_PARTITION_TASK="1")
+    if env:
+        os.environ.update({k: str(v) for k, v in env.items()})
     result: Any
     fault = _injected_fault(rank)
     if fault == "crash_before":
@@ -217,11 +238,13 @@ def _init_timeout():
 def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_workers: Optional[int] = None,
                    backend: Optional[str] = None, use_gpu: bool = False, timeout_s: float = 1200.0,
                    fail_fast: bool = True, port: Optional[int] = None, default_listen_port: int = 0,
-                   network_retries: int = NETWORK_RETRIES, initial_delay_s: float = INITIAL_DELAY_S) -> List[Any]:
+                   network_retries: int = NETWORK_RETRIES, initial_delay_s: float = INITIAL_DELAY_S,
+                   env: Optional[dict] = None) -> List[Any]:
     """Run ``fn(partition_df, rank, world)`` in ``num_workers`` processes.
 
     Partitions are grouped contiguously onto workers (coalesce). Returns the
-    per-rank results in rank order.
+    per-rank results in rank order. ``env`` is exported in every worker before
+    it imports anything (e.g. ``SML_GBDT_SHARED_DEVICE``).
 
     Network initialisation follows the reference's NetworkInit retry (NetworkManager.scala:195-218): when
     any rank fails to join the rendezvous, every rank of that attempt is stopped and the job is relaunched
@@ -236,7 +259,7 @@ def run_partitions(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_
     for attempt in range(network_retries + 1):
         p = pinned if pinned else (find_open_port(default_listen_port) if default_listen_port > 0 else _free_port())
         try:
-            return _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, p, attempt)
+            return _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, p, attempt, env)
         except _NetworkInitError as e:
             if attempt == network_retries:
                 raise RuntimeError(f"network init failed after {network_retries} retries: {e}") from None
@@ -251,7 +274,7 @@ class _NetworkInitError(RuntimeError):
     pass
 
 
-def _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, port, attempt) -> List[Any]:
+def _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, port, attempt, env=None) -> List[Any]:
     import tempfile
 
     import torch.multiprocessing as mp
@@ -266,9 +289,17 @@ def _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, port,
     ctx = mp.get_context("spawn")
     shared = []
     try:
+        # every partition is placed before any worker starts: a hand-off that fails leaves no started worker
+        # waiting in the rendezvous
+        descs = []
+        for r in range(world):
+            desc, shm = _share_partition(parts[r])
+            if shm is not None:
+                shared.append(shm)
+            descs.append(desc)
         with tempfile.TemporaryDirectory() as d:
-            return _run_procs(ctx, fn_bytes, parts, world, port, backend, use_gpu, attempt, timeout_s, fail_fast, d,
-                              shared)
+            return _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, timeout_s, fail_fast, d,
+                              env)
     finally:
         for shm in shared:
             try:
@@ -278,16 +309,19 @@ def _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, port,
                 pass
 
 
-def _run_procs(ctx, fn_bytes, parts, world, port, backend, use_gpu, attempt, timeout_s, fail_fast, d, shared):
+def _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, timeout_s, fail_fast, d, env):
     procs = []
-    for r in range(world):
-        desc, shm = _share_partition(parts[r])
-        if shm is not None:
-            shared.append(shm)
-        p = ctx.Process(target=_worker,
-                        args=(r, world, port, backend, fn_bytes, desc, d, use_gpu, attempt))
-        p.start()
-        procs.append(p)
+    try:
+        for r in range(world):
+            p = ctx.Process(target=_worker,
+                            args=(r, world, port, backend, fn_bytes, descs[r], d, use_gpu, attempt, env))
+            p.start()
+            procs.append(p)
+    except BaseException:
+        for p in procs:  # a worker that failed to start: the started ones would wait in the rendezvous
+            p.terminate()
+            p.join(10)
+        raise
     # fail fast: a rank that exits with an error (or dies) aborts the job instead of leaving the others
     # blocked in collectives until the timeout (the reference waits for the Spark task timeout)
     import time as _time
@@ -361,12 +395,70 @@ def _run_procs(ctx, fn_bytes, parts, world, port, backend, use_gpu, attempt, tim
 
 
 class _FitTask:
-    def __init__(self, estimator):
+    def __init__(self, estimator, barrier: bool = False, with_measures: bool = False):
         self.estimator = estimator
+        self.barrier = barrier
+        self.with_measures = with_measures
 
     def __call__(self, part: DataFrame, rank: int, world: int):
+        if self.barrier:
+            from . import distributed as D
+
+            D.barrier()  # barrier execution mode: every task starts its fit together
         model = self.estimator.fit(part)
+        if self.with_measures:
+            get = getattr(self.estimator, "getPerformanceMeasures", None)
+            return (model if rank == 0 else None, get() if get else None)
         return model if rank == 0 else None
+
+
+# ---------------------------------------------------------------- estimator-driven fan-out
+def in_partition_task() -> bool:
+    """True inside a distributed task: a worker this runtime started, a torchrun rank, or any process whose
+    default process group is up. A fit there trains its own partition and joins the group's collectives;
+    it never fans out again."""
+    from . import distributed as D
+
+    return os.environ.get("SML_PARTITION_TASK") == "1" or D.is_initialized()
+
+
+def executor_tasks(use_gpu: bool) -> int:
+    """Tasks the local "cluster" runs at once (ClusterUtil.getNumExecutorTasks, ClusterUtil.scala:92-140):
+    one per visible MI355X for a GPU job; a CPU job runs one task unless ``SML_EXECUTOR_TASKS`` says how many
+    CPU executors to use (the reference's executor cores)."""
+    env = os.environ.get("SML_EXECUTOR_TASKS")
+    if env:
+        return max(1, int(env))
+    if use_gpu:
+        from ..utils.cluster import _device_count
+
+        return max(1, _device_count())
+    return 1
+
+
+def determine_num_tasks(config_num_tasks: int, df: DataFrame, use_gpu: bool) -> int:
+    """LightGBMBase.determineNumTasks (LightGBMBase.scala:449-456): ``numTasks > 0`` wins, otherwise
+    min(executor tasks, the DataFrame's partitions)."""
+    if config_num_tasks and int(config_num_tasks) > 0:
+        return int(config_num_tasks)
+    return max(1, min(executor_tasks(use_gpu), df.getNumPartitions()))
+
+
+def fan_out(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_tasks: int, use_gpu: bool, **kw) -> List[Any]:
+    """Run ``fn`` over ``num_tasks`` partition tasks, one process each (Spark's mapPartitions over the
+    coalesced / repartitioned DataFrame, LightGBMBase.scala:608-628). GPU tasks take one MI355X each over
+    RCCL; with more tasks than visible devices the ranks share devices (gloo control plane, the engines'
+    shared-device communicators - a rehearsal mode, not a scaling configuration)."""
+    env = dict(kw.pop("env", None) or {})
+    backend = kw.pop("backend", None)
+    if use_gpu:
+        from ..utils.cluster import _device_count
+
+        ndev = _device_count()
+        if num_tasks > max(1, ndev):
+            backend = backend or "gloo"
+            env.setdefault("SML_GBDT_SHARED_DEVICE", "1")
+    return run_partitions(fn, df, num_workers=num_tasks, backend=backend, use_gpu=use_gpu, env=env, **kw)
 
 
 def distributed_fit(estimator, df: DataFrame, num_workers: Optional[int] = None, use_gpu: bool = False,

@@ -330,6 +330,26 @@ def _gpu_config(vwmod, info):
     return cfg
 
 
+def _vw_fan_out(est, df: DataFrame):
+    """The reference's VW fit runs one task per partition, min(executor tasks, partitions) of them
+    (VowpalWabbitBase.scala:124-137, VowpalWabbitBaseLearner.scala:180-211), the tasks averaging their weights
+    through VW's allreduce, and keeps the first partition's model. Returns that model when this fit fans out
+    (GPU: one rank per visible MI355X - the device learner averages over RCCL), else None."""
+    from ..parallel import runtime as R
+    from ..utils.cluster import _device_count
+
+    if R.in_partition_task():
+        return None
+    use_gpu = (est.getOrDefault("deviceType") or "cpu").lower() == "gpu" and _device_count() > 0
+    n = R.determine_num_tasks(0, df, use_gpu)
+    if use_gpu:
+        n = min(n, max(1, _device_count()))
+    if n <= 1:
+        return None
+    barrier = bool(est.getOrDefault("useBarrierExecutionMode")) if est.hasParam("useBarrierExecutionMode") else False
+    return R.fan_out(R._FitTask(est.copy(), barrier=barrier), df, n, use_gpu)[0]
+
+
 def _gpu_learner(args: str, model_bytes=None):
     vwmod = _vw()
     info = vwmod.describe_args(args)  # parses + validates the command line without a host table
@@ -350,8 +370,10 @@ def _gpu_sync_comm(vwmod):
     world = D.world_size()
     if world <= 1:
         return None
-    if D.backend() != "nccl":
-        raise RuntimeError("the GPU VW learner averages over RCCL: start the ranks with the nccl backend")
+    # (the control plane may be gloo or nccl: the averaging runs on the learner's own RCCL communicator,
+    # whose unique id travels over the control plane)
+    if world in _nccl_cache and getattr(_nccl_cache[world], "aborted", False):
+        del _nccl_cache[world]  # aborted by a failed sync of an earlier fit: rebuild
     if world not in _nccl_cache:
         import os
 
@@ -361,6 +383,15 @@ def _gpu_sync_comm(vwmod):
             lambda uid: vwmod.nccl_comm(uid, D.rank(), world, timeout_ms), "VW RCCL communicator",
             prepare=lambda: vwmod.nccl_unique_id() if D.rank() == 0 else None)
     return _nccl_cache[world]
+
+
+def _evict_nccl(comm) -> None:
+    for k, v in list(_nccl_cache.items()):
+        if v is comm:
+            del _nccl_cache[k]
+    abort = getattr(comm, "abort", None)
+    if abort is not None:
+        abort()
 
 
 def _gpu_learn_staged(est, g, comm, n: int):
@@ -375,7 +406,13 @@ def _gpu_learn_staged(est, g, comm, n: int):
             if s1 > s0:
                 g.learn_staged(int(s0), int(s1), int(est.getGpuBatchSize()))
             if comm is not None:
-                g.allreduce_average(comm)
+                try:
+                    g.allreduce_average(comm)
+                except RuntimeError:
+                    # the native call aborted the communicator (a peer died / the sync timed out): drop it so a
+                    # later fit in this process builds a fresh one, and fail this fit on every rank
+                    _evict_nccl(comm)
+                    raise
                 sync_bytes.append(int(g.last_sync_bytes))
     return sync_bytes
 
@@ -489,12 +526,14 @@ class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
     vwArgs = Param("Arguments the model was trained with", "", T.toString)
 
     def _native_model(self):
+        # keyed on the model object itself (held by the cache, compared with `is`): an id() key can be reused by
+        # a new bytes object once the old model is garbage-collected, and would then score with stale weights
         cache = getattr(self, "_vw_cache", None)
-        key = (id(self.getModel()), self.getTestArgs())
-        if cache is None or cache[0] != key:
-            m = _vw().VW(self.getVwArgs() + " --testonly " + (self.getTestArgs() or ""), self.getModel())
-            self._vw_cache = (key, m)
-        return self._vw_cache[1]
+        model, targs = self.getModel(), self.getTestArgs()
+        if cache is None or cache[0] is not model or cache[1] != targs:
+            m = _vw().VW(self.getVwArgs() + " --testonly " + (targs or ""), model)
+            self._vw_cache = (model, targs, m)
+        return self._vw_cache[2]
 
     def getPerformanceStatistics(self) -> DataFrame:  # noqa: N802
         return self.getOrDefault("performanceStatistics")
@@ -513,14 +552,14 @@ class VowpalWabbitModelBase(Model, VowpalWabbitBaseParams, HasPredictionCol):
         args = self.getVwArgs() + " --testonly " + (self.getTestArgs() or "")
         if "--probabilities" in args:
             return None  # oaa probabilities: host learner
-        key = (id(self.getModel()), args)
+        model = self.getModel()
         cache = getattr(self, "_gpu_cache", None)
-        if cache is None or cache[0] != key:
+        if cache is None or cache[0] is not model or cache[1] != args:
             try:
-                self._gpu_cache = (key, _GpuScorer(args, self.getModel()))
+                self._gpu_cache = (model, args, _GpuScorer(args, model))
             except ValueError:
-                self._gpu_cache = (key, None)
-        return self._gpu_cache[1]
+                self._gpu_cache = (model, args, None)
+        return self._gpu_cache[2]
 
     def _predict_raw(self, df: DataFrame, multiclass: bool = False):
         cols = [self.getFeaturesCol()] + list(self.getAdditionalFeatures() or [])
@@ -608,6 +647,10 @@ class VowpalWabbitBase(Estimator, VowpalWabbitBaseParams, HasLabelCol, HasWeight
         return DataFrame({k: [v] for k, v in row.items()})
 
     def _fit(self, df: DataFrame):
+        if not self.getSplitCol():
+            fanned = _vw_fan_out(self, df)
+            if fanned is not None:
+                return fanned
         args = build_args(self, self._extra_args())
         init = self.getInitialModel()
         if self.getSplitCol():
@@ -798,6 +841,9 @@ class VowpalWabbitGeneric(Estimator, HasPredictionCol):
         return m
 
     def _fit(self, df: DataFrame):
+        fanned = _vw_fan_out(self, df)
+        if fanned is not None:
+            return fanned
         args = self.getPassThroughArgs() + (f" --passes {self.getNumPasses()}" if self.getNumPasses() > 1 else "")
         if (self.getDeviceType() or "cpu").lower() == "gpu":
             return self._fit_gpu([str(s) for s in df[self.getInputCol()].tolist()], args)

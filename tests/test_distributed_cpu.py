@@ -381,3 +381,91 @@ def test_partitions_reach_workers_through_shared_memory():
         np.testing.assert_allclose(vs, sv[a:b].values.sum())
         assert strs == list(s[a:b]) and ys == float(np.arange(a, b).sum())
     assert set(glob.glob("/dev/shm/psm_*")) <= before
+
+
+def test_partitions_fall_back_to_pickle_when_shm_is_small(monkeypatch):
+    """A /dev/shm without room for the partition (Docker's 64 MB default) must not SIGBUS the driver: the
+    partition travels pickled, with the same contents."""
+    from synapseml_amd.parallel import runtime as R
+
+    monkeypatch.setenv("SML_SHM_HANDOFF", "0")
+    assert not R._shm_fits(1)
+    rng = np.random.default_rng(1)
+    f = rng.standard_normal((400, 3)).astype(np.float32)
+    from synapseml_amd.core.linalg import CsrColumn
+
+    ip = np.arange(0, 801, 2, dtype=np.int64)
+    sv = CsrColumn(ip, rng.integers(0, 9, 800).astype(np.int32), rng.random(800), 9)
+    s = np.array([f"r{i}" for i in range(400)], dtype=object)
+    df = DataFrame({"f": f, "sv": sv, "s": s, "y": np.arange(400.0)}, num_partitions=2)
+    desc, shm = R._share_partition(df.partitions()[0])
+    assert shm is None
+    res = run_partitions(_checksum_task, df, num_workers=2)
+    a, b = df.partition_bounds()[1]
+    assert res[1][1] == "float32" and res[1][2] == (b - a, 3) and res[1][6] == float(np.arange(a, b).sum())
+
+
+def _lgbm_df(n=4000, parts=2, seed=3):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, 6))
+    y = (X[:, 0] - X[:, 1] * X[:, 2] > 0).astype(float)
+    return DataFrame({"features": X, "label": y}, num_partitions=parts)
+
+
+def _splits(m):
+    return [l for l in m.getNativeModel().splitlines() if l.startswith(("split_feature=", "threshold=", "leaf_value="))]
+
+
+def test_num_tasks_fans_out_like_distributed_fit():
+    """LightGBMClassifier(numTasks=2).fit(df) runs 2 partition tasks itself (LightGBMBase.scala:449-456,
+    608-628) and returns the main task's model: the same model as an explicit distributed_fit."""
+    df = _lgbm_df()
+    base = LightGBMClassifier(deviceType="cpu", numIterations=6, numThreads=1)
+    base.fit(df.coalesce(1))
+    ref = base._last_reference
+    est = LightGBMClassifier(deviceType="cpu", numIterations=6, numThreads=1, referenceDataset=ref, numTasks=2,
+                             useBarrierExecutionMode=True)
+    fanned = est.fit(df)
+    explicit = distributed_fit(LightGBMClassifier(deviceType="cpu", numIterations=6, numThreads=1,
+                                                  referenceDataset=ref), df, num_workers=2)
+    assert _splits(fanned) == _splits(explicit)
+    tm = est.getTaskMeasures()
+    assert len(tm) == 2 and all(t and "training_iterations_ms" in t[0] for t in tm)
+    np.testing.assert_allclose(fanned.transform(df)["probability"], explicit.transform(df)["probability"])
+
+
+def test_num_tasks_default_uses_executor_tasks(monkeypatch):
+    """numTasks=0: min(executor tasks, partitions) (determineNumTasks); one executor task keeps the fit in
+    this process, SML_EXECUTOR_TASKS=2 (two CPU executors) fans a 3-partition DataFrame out to 2 tasks."""
+    from synapseml_amd.parallel import runtime as R
+
+    df = _lgbm_df(parts=3)
+    assert R.determine_num_tasks(0, df, use_gpu=False) == 1
+    assert R.determine_num_tasks(5, df, use_gpu=False) == 5
+    monkeypatch.setenv("SML_EXECUTOR_TASKS", "2")
+    assert R.determine_num_tasks(0, df, use_gpu=False) == 2
+    assert R.determine_num_tasks(0, df.coalesce(1), use_gpu=False) == 1
+    calls = []
+    real = R.fan_out
+
+    def spy(fn, d, n, use_gpu, **kw):
+        calls.append(n)
+        return real(fn, d, n, use_gpu, **kw)
+
+    monkeypatch.setattr(R, "fan_out", spy)
+    m = LightGBMClassifier(deviceType="cpu", numIterations=3, numThreads=1).fit(df)
+    assert calls == [2] and m.transform(df)["probability"].shape[0] == len(df)
+
+
+def test_inert_params_warn(caplog):
+    import logging
+
+    df = _lgbm_df(n=600, parts=1)
+    with caplog.at_level(logging.WARNING, logger="synapseml_amd.lightgbm"):
+        LightGBMClassifier(deviceType="cpu", numIterations=2, dataTransferMode="bulk", chunkSize=5).fit(df)
+    msgs = " ".join(r.getMessage() for r in caplog.records)
+    assert "dataTransferMode" in msgs and "chunkSize" in msgs
+    caplog.clear()
+    with caplog.at_level(logging.WARNING, logger="synapseml_amd.lightgbm"):
+        LightGBMClassifier(deviceType="cpu", numIterations=2).fit(df)
+    assert not any("has no effect" in r.getMessage() for r in caplog.records)

@@ -80,13 +80,27 @@ class _RDD:
         return _Barrier(self.parts)
 
 
+class _Batches(list):
+    """mapInArrow's result: the output batches; collect() gives their rows (a Spark DataFrame's collect)."""
+
+    def collect(self):
+        return [row for b in self for row in b.to_pylist()]
+
+
 class _SparkDF:
-    def __init__(self, rows, arrow_table):
+    def __init__(self, rows, arrow_table, arrow_barrier=True):
         self.rdd = _RDD([rows])
         self.table = arrow_table
+        self.arrow_barrier = arrow_barrier
+        self.arrow_fit_calls = 0
 
-    def mapInArrow(self, fn, schema):  # noqa: N802
-        return list(fn(iter(self.table.to_batches(max_chunksize=256))))
+    def mapInArrow(self, fn, schema, barrier=False):  # noqa: N802
+        if barrier:
+            if not self.arrow_barrier:  # Spark < 3.5
+                raise TypeError("mapInArrow() got an unexpected keyword argument 'barrier'")
+            self.arrow_fit_calls += 1
+            _Ctx.current = _Ctx(0, 1)
+        return _Batches(fn(iter(self.table.to_batches(max_chunksize=256))))
 
 
 @pytest.fixture
@@ -106,10 +120,20 @@ def test_fit_and_transform_through_pyspark_surface(fake_pyspark):
     X = rng.standard_normal((1000, 4))
     y = (X[:, 0] - X[:, 1] > 0).astype(float)
     rows = [_Row(features=_Vec(x), label=float(t)) for x, t in zip(X, y)]
+    import pyarrow as pa
+
+    # the training partition as Spark ships it after vector_to_array: array<double> features + a label column
+    train_table = pa.table({"features": pa.array([list(x) for x in X], type=pa.list_(pa.float64())), "label": y})
     table = DataFrame({"features": X}).toArrow()
-    sdf = _SparkDF(rows, table)
-    model = fit_on_spark(LightGBMClassifier(deviceType="cpu", numIterations=10), sdf, use_gpu=False)
     local = LightGBMClassifier(deviceType="cpu", numIterations=10).fit(DataFrame({"features": X, "label": y}))
+    # Spark >= 3.5: barrier mapInArrow, the partition arrives as Arrow (no Row objects)
+    sdf_arrow = _SparkDF(None, train_table)
+    model = fit_on_spark(LightGBMClassifier(deviceType="cpu", numIterations=10), sdf_arrow, use_gpu=False)
+    assert sdf_arrow.arrow_fit_calls == 1
+    assert model.getNativeModel().split("parameters:")[0] == local.getNativeModel().split("parameters:")[0]
+    # Spark < 3.5: the Row path, same model
+    sdf = _SparkDF(rows, table, arrow_barrier=False)
+    model = fit_on_spark(LightGBMClassifier(deviceType="cpu", numIterations=10), sdf, use_gpu=False)
     assert model.getNativeModel().split("parameters:")[0] == local.getNativeModel().split("parameters:")[0]
     batches = transform_on_spark(model, sdf, schema=None)
     out = DataFrame.fromArrow(batches)

@@ -572,3 +572,41 @@ def test_wildcard_and_cubic_interactions_vw_semantics():
     assert _touched("--cubic aab", blocks) == {x & M for x in base | cub(A, A, B, True, False)}
     # an explicit pair is NOT canonicalised: -q ba hashes b first
     assert _touched("-q ba", blocks) == {x & M for x in base | q(B, A, 0)}
+
+
+def test_fit_fans_out_over_executor_tasks(monkeypatch):
+    """VowpalWabbitClassifier.fit runs min(executor tasks, partitions) tasks itself
+    (VowpalWabbitBase.scala:124-137, VowpalWabbitBaseLearner.scala:180-211) and keeps the first partition's
+    model - the model every rank holds after the end-of-pass average."""
+    from synapseml_amd.parallel.runtime import run_partitions
+    from synapseml_amd.vw import VowpalWabbitClassifier as C
+
+    df, X, y = _binary_df(n=2000, parts=2)
+    explicit = run_partitions(_vw_rank_fn, df, num_workers=2)[0]
+    monkeypatch.setenv("SML_EXECUTOR_TASKS", "2")
+    m = C(labelConversion=True, passThroughArgs="--loss_function logistic", numPasses=2, numSyncsPerPass=1).fit(df)
+    vw = native.load("_vw")
+    np.testing.assert_allclose(np.asarray(vw.VW("--testonly", m.getModel()).weights()),
+                               np.asarray(vw.VW("--testonly", explicit).weights()), rtol=1e-6, atol=1e-7)
+    assert m.transform(df)["prediction"].shape[0] == 2000
+
+
+def test_stager_rejects_null_source():
+    """The pinned host->HBM stager refuses a null source before any copy thread runs (the round-4 segfault)."""
+    assert native.load("_vw")._stager_rejects_null()
+
+
+def test_model_cache_is_keyed_on_the_model_object():
+    """Replacing the model bytes always rebuilds the cached scorer, even if the new object reuses the old id."""
+    from synapseml_amd.vw import VowpalWabbitRegressor
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((200, 4))
+    df = DataFrame({"features": X, "label": X[:, 0] * 2.0})
+    m = VowpalWabbitRegressor().fit(df)
+    p1 = m.transform(df)["prediction"]
+    m2 = VowpalWabbitRegressor(passThroughArgs="-l 0.01").fit(df)
+    m.set("model", bytes(m2.getModel()))
+    p2 = m.transform(df)["prediction"]
+    np.testing.assert_allclose(p2, m2.transform(df)["prediction"])
+    assert not np.allclose(p1, p2)
