@@ -243,11 +243,15 @@ class CpuBackend : public TrainBackend {
     if (rows) { bag_ = *rows; use_bag_ = true; } else { bag_.clear(); use_bag_ = false; }
   }
 
-  // Histogram of one leaf: the leaf's (g, h) are gathered once into a contiguous ordered buffer, then the
-  // threads split the work into row groups x feature slices; each accumulates in fp64 into its row group's
-  // table (group 0 writes the output directly), and the tables are summed per feature afterwards.
+  // Histogram of one leaf in 64-bit fixed point (the device engine's K3 representation): the leaf's (g, h)
+  // are quantised once into a contiguous ordered buffer of int64 pairs with the tree's GLOBAL scale (the
+  // global row count bound and the global max |g| / max h, see TreeScale), then the threads split the work
+  // into row groups x feature slices, each adding into its row group's int64 table, and the tables are summed.
+  // Integer sums are associative: the histogram is bitwise independent of threads, row order and - summed
+  // over ranks as int64 - of how the rows are partitioned, so an N-rank model is the 1-rank model. The
+  // returned fp64 histogram is the int64 sums x 2^-e. `tot` (optional) receives the leaf's exact (g, h) sums.
   void BuildHist(int k, const LeafInfo& leaf, const std::vector<char>& fmask, std::vector<double>* hist,
-                 bool reduce = true) {
+                 bool reduce = true, int64_t* tot = nullptr) {
     const auto t0 = Clock::now();
     const int stride = 256 * 2;
     const size_t hsz = static_cast<size_t>(F_) * stride;
@@ -264,17 +268,23 @@ class CpuBackend : public TrainBackend {
     const uint32_t* idx = idx_.data() + leaf.begin;
     const int nt = std::max<int>(1, std::min<int64_t>(nthreads_, cnt / 2048 + 1));
     if (static_cast<int64_t>(ogh_.size()) < 2 * cnt) ogh_.resize(2 * cnt);
-    float* og = ogh_.data();
-#pragma omp parallel for num_threads(nt) schedule(static)
+    int64_t* og = ogh_.data();
+    const double sg = scale_g_, sh = scale_h_;
+    int64_t tg = 0, th = 0;
+#pragma omp parallel for num_threads(nt) schedule(static) reduction(+ : tg, th)
     for (int64_t p = 0; p < cnt; ++p) {
       const int64_t r = idx[p];
-      og[2 * p] = g[r];
-      og[2 * p + 1] = h[r];
+      const int64_t qg = static_cast<int64_t>(std::nearbyint(static_cast<double>(g[r]) * sg));
+      const int64_t qh = static_cast<int64_t>(std::nearbyint(static_cast<double>(std::max(h[r], 0.f)) * sh));
+      og[2 * p] = qg;
+      og[2 * p + 1] = qh;
+      tg += qg;
+      th += qh;
     }
     // row groups x feature slices; one row group unless there are fewer features than threads
     // up to feats_per_slice_ features per thread: the rows are split into row groups (each random row of a
     // child leaf gathered by one thread per slice), with per-row-group tables summed afterwards.
-    // The tables are accumulated at a padded feature pitch (kPitch = 512 + 8 doubles): at the natural 4 KiB
+    // The tables are accumulated at a padded feature pitch (kPitch = 512 + 8 words): at the natural 4 KiB
     // pitch the same bin of every feature shares its low 12 address bits, and a row whose features sit in
     // the same (e.g. the most common) bin makes every load look like it aliases the previous feature's store
     // (4K aliasing): 3.5x slower per update on skewed bins (hb2 microbench, 28 features, 60 % in one bin).
@@ -285,61 +295,103 @@ class CpuBackend : public TrainBackend {
     const int rg = std::max(1, nt / fs);
     if (static_cast<int>(hloc_.size()) < rg) hloc_.resize(rg);
     for (int gi = 0; gi < rg; ++gi) if (hloc_[gi].size() < psz) hloc_[gi].resize(psz);
-    double* out = hist->data();
 #pragma omp parallel for num_threads(fs * rg) schedule(static, 1) collapse(2)
     for (int gi = 0; gi < rg; ++gi) {
       for (int si = 0; si < fs; ++si) {
-        double* dst = hloc_[gi].data();
+        int64_t* dst = hloc_[gi].data();
         const int fa = nf * si / fs, fb = nf * (si + 1) / fs;
-        for (int j = fa; j < fb; ++j) std::fill(dst + fl[j] * kPitch, dst + fl[j] * kPitch + stride, 0.0);
+        for (int j = fa; j < fb; ++j) std::fill(dst + fl[j] * kPitch, dst + fl[j] * kPitch + stride, int64_t{0});
         const int64_t pa = cnt * gi / rg, pb = cnt * (gi + 1) / rg;
-        // one 16-B (g, h) add per feature (SSE2: one load, add and store instead of two of each)
+        // one 16-B (g, h) integer add per feature (SSE2: one load, add and store instead of two of each)
         for (int64_t p = pa; p < pb; ++p) {
           if (p + 24 < pb) __builtin_prefetch(bins + idx[p + 24] * rs);  // random rows of a child leaf
           const uint8_t* row = bins + idx[p] * rs;
-          const __m128d gh = _mm_cvtps_pd(_mm_castsi128_ps(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(og + 2 * p))));
+          const __m128i gh = _mm_loadu_si128(reinterpret_cast<const __m128i*>(og + 2 * p));
           // four features per step, loads ahead of stores: the four cells are in different features' tables
           // (never the same address), so the loads need not wait for the stores (2.2x per update, hb3)
           int j = fa;
           for (; j + 4 <= fb; j += 4) {
-            double* c0 = dst + fl[j] * kPitch + row[fl[j]] * 2;
-            double* c1 = dst + fl[j + 1] * kPitch + row[fl[j + 1]] * 2;
-            double* c2 = dst + fl[j + 2] * kPitch + row[fl[j + 2]] * 2;
-            double* c3 = dst + fl[j + 3] * kPitch + row[fl[j + 3]] * 2;
-            const __m128d a0 = _mm_load_pd(c0), a1 = _mm_load_pd(c1), a2 = _mm_load_pd(c2), a3 = _mm_load_pd(c3);
-            _mm_store_pd(c0, _mm_add_pd(a0, gh));
-            _mm_store_pd(c1, _mm_add_pd(a1, gh));
-            _mm_store_pd(c2, _mm_add_pd(a2, gh));
-            _mm_store_pd(c3, _mm_add_pd(a3, gh));
+            __m128i* c0 = reinterpret_cast<__m128i*>(dst + fl[j] * kPitch + row[fl[j]] * 2);
+            __m128i* c1 = reinterpret_cast<__m128i*>(dst + fl[j + 1] * kPitch + row[fl[j + 1]] * 2);
+            __m128i* c2 = reinterpret_cast<__m128i*>(dst + fl[j + 2] * kPitch + row[fl[j + 2]] * 2);
+            __m128i* c3 = reinterpret_cast<__m128i*>(dst + fl[j + 3] * kPitch + row[fl[j + 3]] * 2);
+            const __m128i a0 = _mm_load_si128(c0), a1 = _mm_load_si128(c1), a2 = _mm_load_si128(c2),
+                          a3 = _mm_load_si128(c3);
+            _mm_store_si128(c0, _mm_add_epi64(a0, gh));
+            _mm_store_si128(c1, _mm_add_epi64(a1, gh));
+            _mm_store_si128(c2, _mm_add_epi64(a2, gh));
+            _mm_store_si128(c3, _mm_add_epi64(a3, gh));
           }
           for (; j < fb; ++j) {
-            double* c = dst + fl[j] * kPitch + row[fl[j]] * 2;
-            _mm_store_pd(c, _mm_add_pd(_mm_load_pd(c), gh));
+            __m128i* c = reinterpret_cast<__m128i*>(dst + fl[j] * kPitch + row[fl[j]] * 2);
+            _mm_store_si128(c, _mm_add_epi64(_mm_load_si128(c), gh));
           }
         }
       }
     }
+    // int64 histogram (+ the leaf's exact sums and row count): summed tables, then over ranks
+    std::vector<int64_t>& acc = hsum_;
+    acc.assign(hsz + 3, 0);
 #pragma omp parallel for num_threads(std::max(1, std::min(nt, nf))) schedule(static)
     for (int j = 0; j < nf; ++j) {
-      double* o = out + fl[j] * stride;
-      std::memcpy(o, hloc_[0].data() + fl[j] * kPitch, sizeof(double) * stride);
+      int64_t* o = acc.data() + fl[j] * stride;
+      std::memcpy(o, hloc_[0].data() + fl[j] * kPitch, sizeof(int64_t) * stride);
       for (int gi = 1; gi < rg; ++gi) {
-        const double* src = hloc_[gi].data() + fl[j] * kPitch;
+        const int64_t* src = hloc_[gi].data() + fl[j] * kPitch;
         for (int b = 0; b < stride; ++b) o[b] += src[b];
       }
     }
+    acc[hsz] = tg;
+    acc[hsz + 1] = th;
+    acc[hsz + 2] = leaf.count;
     stats.hist_ms += Ms(t0);
     if (reduce && comm_ && comm_->world() > 1) {
       const auto tc = Clock::now();
-      hist->push_back(static_cast<double>(leaf.count));
-      comm_->AllReduceHost(hist->data(), static_cast<int64_t>(hist->size()));
-      last_gcount_ = static_cast<int64_t>(hist->back());
-      hist->pop_back();
+      comm_->AllReduceHostI64(acc.data(), static_cast<int64_t>(acc.size()));
+      last_gcount_ = acc[hsz + 2];
       stats.comm_ms += Ms(tc);
       ++stats.comm_calls;
     } else {
       last_gcount_ = leaf.count;
     }
+    double* out = hist->data();
+    for (int j = 0; j < nf; ++j) {
+      const int64_t* a = acc.data() + fl[j] * stride;
+      double* o = out + fl[j] * stride;
+      for (int b = 0; b < stride; b += 2) {
+        o[b] = static_cast<double>(a[b]) * inv_g_;
+        o[b + 1] = static_cast<double>(a[b + 1]) * inv_h_;
+      }
+    }
+    if (tot) { tot[0] = acc[hsz]; tot[1] = acc[hsz + 1]; tot[2] = acc[hsz + 2]; }
+  }
+
+  // The tree's fixed-point scale (the device engine's HistScaleV): 2^e with e the largest exponent such that
+  // scale_n * max * 2^e <= 2^62, from the global row count and the global max |g| / max h of class k.
+  void TreeScale(int k) {
+    if (scale_n_ == 0) {
+      double c = static_cast<double>(n_);
+      if (comm_ && comm_->world() > 1) comm_->AllReduceHost(&c, 1);
+      scale_n_ = static_cast<int64_t>(c);
+    }
+    const float* g = g_.data() + static_cast<size_t>(k) * n_;
+    const float* h = h_.data() + static_cast<size_t>(k) * n_;
+    float mg = 0.f, mh = 0.f;
+#pragma omp parallel for num_threads(nthreads_) reduction(max : mg, mh)
+    for (int64_t i = 0; i < n_; ++i) {
+      mg = std::max(mg, std::fabs(g[i]));
+      mh = std::max(mh, std::fabs(h[i]));
+    }
+    double m[2] = {mg, mh};
+    if (comm_ && comm_->world() > 1) comm_->AllReduceHostMax(m, 2);
+    auto ex = [&](double vmax) {
+      const double r = 4.611686018427387904e18 / (static_cast<double>(std::max<int64_t>(1, scale_n_)) *
+                                                  std::max(static_cast<double>(static_cast<float>(vmax)), 1e-300));
+      return std::max(-1000, std::min(1000, std::ilogb(r)));
+    };
+    const int eg = ex(m[0]), eh = ex(m[1]);
+    scale_g_ = std::ldexp(1.0, eg); inv_g_ = std::ldexp(1.0, -eg);
+    scale_h_ = std::ldexp(1.0, eh); inv_h_ = std::ldexp(1.0, -eh);
   }
 
   // Stable partition of idx_[begin, begin + count) by `left(r)`: every thread flags and counts its chunk,
@@ -568,20 +620,19 @@ class CpuBackend : public TrainBackend {
     const float* g = g_.data() + static_cast<size_t>(k) * n_;
     const float* h = h_.data() + static_cast<size_t>(k) * n_;
     leaves[0].begin = 0; leaves[0].count = static_cast<int64_t>(idx_.size());
-    double G = 0, H = 0;
-#pragma omp parallel for reduction(+ : G, H)
-    for (int64_t p = 0; p < leaves[0].count; ++p) { G += g[idx_[p]]; H += h[idx_[p]]; }
-    {
-      double st[3] = {G, H, static_cast<double>(leaves[0].count)};
-      if (comm_) comm_->AllReduceHost(st, 3);
-      G = st[0]; H = st[1]; leaves[0].gcount = static_cast<int64_t>(st[2]);
-    }
+    TreeScale(k);
+    const bool voting = cfg_.tree_learner == "voting" && comm_ && comm_->world() > 1;
+    // root totals: the exact int64 sums of the quantised (g, h) (global: summed with the histogram, or on
+    // their own when voting keeps the histograms local)
+    int64_t tot[3];
+    BuildHist(k, leaves[0], fmask, &hists[0], !voting, tot);
+    if (voting) comm_->AllReduceHostI64(tot, 3);
+    const double G = static_cast<double>(tot[0]) * inv_g_, H = static_cast<double>(tot[1]) * inv_h_;
+    leaves[0].gcount = tot[2];
     leaves[0].sum_g = G; leaves[0].sum_h = H;
     tree.leaf_value[0] = LeafOutput(G, H, sp_.lambda_l1, sp_.lambda_l2, sp_.max_delta_step);
     tree.leaf_count[0] = leaves[0].gcount;
     tree.leaf_weight[0] = H;
-    const bool voting = cfg_.tree_learner == "voting" && comm_ && comm_->world() > 1;
-    BuildHist(k, leaves[0], fmask, &hists[0], !voting);
     if (voting) VotingFind({&leaves[0]}, {&hists[0]}, fmask, leaves[0].gcount);
     else FindBest(hists[0], &leaves[0], fmask);
     for (int s = 1; s < L; ++s) {
@@ -727,9 +778,12 @@ class CpuBackend : public TrainBackend {
   std::vector<float> g_, h_;
   std::vector<uint32_t> idx_;  // row indices, grouped by leaf (32-bit: half the bytes the partition moves)
   std::vector<std::pair<int64_t, int64_t>> seg_;  // (begin, count) in idx_ of each leaf of the last tree
-  std::vector<std::vector<double>> hloc_;         // per-thread histogram tables (BuildHist)
+  std::vector<std::vector<int64_t>> hloc_;        // per-thread int64 histogram tables (BuildHist)
+  std::vector<int64_t> hsum_;                     // summed int64 histogram + leaf sums + count (BuildHist)
+  int64_t scale_n_ = 0;                           // global row count (the histogram scale's count bound)
+  double scale_g_ = 1, scale_h_ = 1, inv_g_ = 1, inv_h_ = 1;  // this tree's fixed-point scales
   int feats_per_slice_ = 32;  // SML_CPU_HIST_FPS (A/B at 1M x 28, 8 threads: 28 -> 2.47 s, 14 -> 2.70, 7 -> 2.99, 1 -> 3.35)
-  std::vector<float> ogh_;                        // the leaf's (g, h) in row order (BuildHist)
+  std::vector<int64_t> ogh_;                      // the leaf's quantised (g, h) in row order (BuildHist)
   std::vector<uint32_t> part_tmp_;                // partition scratch
   std::vector<uint8_t> colbins_;                  // bins, column-major (partition decisions)
   std::vector<uint8_t> part_flag_;

@@ -914,19 +914,24 @@ struct HScale {
   double ig, ih;  // 2^-eg, 2^-eh: conversion back
 };
 
-__device__ __forceinline__ int ScaleExp(int count, float vmax) {
+// The fixed-point scale of every histogram of a tree is a function of GLOBAL quantities only: the bound
+// `scale_n` = the training set's global row count (>= any leaf's global count, so every sum of the tree fits
+// 2^62) and the global max |g| / max h (or the objective's a-priori bound). It does not depend on how the
+// rows are spread over ranks, so per-rank int64 histograms summed over ranks are bitwise the 1-rank
+// histogram: an N-rank model is the 1-rank model (VerifyLightGBMClassifierStream.scala:95-101).
+__device__ __forceinline__ int ScaleExp(int64_t count, float vmax) {
   // largest e with count * vmax * 2^e <= 2^62
-  const double r = 4.611686018427387904e18 / (static_cast<double>(max(1, count)) * fmax(static_cast<double>(vmax), 1e-300));
+  const double r = 4.611686018427387904e18 / (static_cast<double>(max(int64_t{1}, count)) * fmax(static_cast<double>(vmax), 1e-300));
   return max(-1000, min(1000, ilogb(r)));
 }
 
-__device__ __forceinline__ HScale HistScaleV(int count, float gmax, float hmax) {
-  const int eg = ScaleExp(count, gmax), eh = ScaleExp(count, hmax);
+__device__ __forceinline__ HScale HistScaleV(int64_t scale_n, float gmax, float hmax) {
+  const int eg = ScaleExp(scale_n, gmax), eh = ScaleExp(scale_n, hmax);
   return HScale{ldexp(1.0, eg), ldexp(1.0, eh), ldexp(1.0, -eg), ldexp(1.0, -eh)};
 }
 
-__device__ __forceinline__ HScale HistScale(int count, const float* ghmax) {
-  return HistScaleV(count, ghmax[0], ghmax[1]);
+__device__ __forceinline__ HScale HistScale(int64_t scale_n, const float* ghmax) {
+  return HistScaleV(scale_n, ghmax[0], ghmax[1]);
 }
 
 struct QGH {
@@ -1059,7 +1064,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
                                          const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
                                          const float2* __restrict__ ogh1, const float* __restrict__ g,
                                          const float* __restrict__ h, const float* __restrict__ ghmax,
-                                         ulonglong2* __restrict__ slab_out) {
+                                         ulonglong2* __restrict__ slab_out, int64_t scale_n) {
   constexpr int kWords = kFPG * kBinsPerFeature;
   // g plane at 0, h plane kHOff bytes above it (kTight: F <= 28, see kHPlaneTight)
   constexpr uint32_t kHOff = kFPG == 32 ? (kTight ? kHPlaneTight : kHPlaneApart) : kWords * 8u;
@@ -1081,7 +1086,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
   const int chunk = ceil_div_i(count, nb_active);
   const int p0 = begin + lb * chunk;
   const int p1 = min(begin + count, p0 + chunk);
-  const HScale sc = HistScaleV(count, gmax_g, gmax_h);
+  const HScale sc = HistScaleV(scale_n, gmax_g, gmax_h);
   const int32_t* __restrict__ perm = buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = buf == 0 ? ogh0 : ogh1;
   const bool phys = buf < 0;
@@ -1174,13 +1179,13 @@ __global__ __launch_bounds__(kHistBlockThreads) void hist_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const uint4* __restrict__ bins4,
     int W4, int F, const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1,
     const float2* __restrict__ ogh0, const float2* __restrict__ ogh1, const float* __restrict__ g,
-    const float* __restrict__ h, const float* __restrict__ ghmax, ulonglong2* __restrict__ slab) {
+    const float* __restrict__ h, const float* __restrict__ ghmax, ulonglong2* __restrict__ slab, int64_t scale_n) {
   if (st->done) return;
   const DLeaf L = HistSeg(st, leaves);
   const int nb_active = HistBlocks(L.count);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
   HistBody<kUnroll, kFPG, kPipe, kTight>(L.begin, L.count, L.buf, nb_active, blockIdx.x, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
-                          ghmax, slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature);
+                          ghmax, slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature, scale_n);
 }
 
 // max |g|, max h of one class when the gradients did not come from grad_kernel
@@ -1205,9 +1210,11 @@ __global__ __launch_bounds__(256) void ghmax_kernel(const float* __restrict__ g,
 constexpr int kRedE = 32;
 constexpr int kRedG = 16;
 
+// i64_out (data-parallel): the int64 sums and the row count are written as int64 for the exact cross-rank
+// allreduce; hist_convert_kernel then turns them into the fp64 histogram exactly as the 1-rank path does here.
 __global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
     const DState* __restrict__ st, const DLeaf* __restrict__ leaves, const ulonglong2* __restrict__ slab, int E,
-    const float* __restrict__ ghmax, double2* __restrict__ hist) {
+    const float* __restrict__ ghmax, double2* __restrict__ hist, int64_t scale_n, int i64_out) {
   if (st->done) return;
   const int count = HistSeg(st, leaves).count;
   const int nb_active = HistBlocks(count);
@@ -1231,13 +1238,53 @@ __global__ __launch_bounds__(kRedE * kRedG) void hist_reduce_kernel(
     unsigned long long tg = 0, th = 0;
 #pragma unroll
     for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
-    const HScale s = HistScale(count, ghmax);
     const int F = E / kBinsPerFeature;  // slab element e = b * F + f -> histogram [f][b]
     const int bin = e / F, f = e - bin * F;
-    hist[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
-                           static_cast<double>(static_cast<long long>(th)) * s.ih);
+    if (i64_out) {
+      reinterpret_cast<ulonglong2*>(hist)[f * kBinsPerFeature + bin] = make_ulonglong2(tg, th);
+    } else {
+      const HScale s = HistScale(scale_n, ghmax);
+      hist[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
+                             static_cast<double>(static_cast<long long>(th)) * s.ih);
+    }
   }
-  if (blockIdx.x == 0 && tid == 0) hist[E] = make_double2(static_cast<double>(count), 0.0);
+  if (blockIdx.x == 0 && tid == 0) {
+    if (i64_out) reinterpret_cast<ulonglong2*>(hist)[E] = make_ulonglong2(static_cast<unsigned long long>(count), 0ull);
+    else hist[E] = make_double2(static_cast<double>(count), 0.0);
+  }
+}
+
+// Data-parallel histograms after the int64 allreduce: (E + 1) int64 pairs per histogram (blockIdx.y) -> fp64
+// with the tree's global scale, the same conversion the 1-rank reduce applies; slot E = the global row count.
+__global__ __launch_bounds__(256) void hist_convert_kernel(double2* __restrict__ part, int E, int64_t scale_n,
+                                                           const float* __restrict__ ghmax) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e > E) return;
+  double2* p = part + static_cast<size_t>(blockIdx.y) * (E + 1);
+  const ulonglong2 v = reinterpret_cast<const ulonglong2*>(p)[e];
+  if (e == E) {
+    p[e] = make_double2(static_cast<double>(static_cast<long long>(v.x)), 0.0);
+    return;
+  }
+  const HScale s = HistScale(scale_n, ghmax);
+  p[e] = make_double2(static_cast<double>(static_cast<long long>(v.x)) * s.ig,
+                      static_cast<double>(static_cast<long long>(v.y)) * s.ih);
+}
+
+// Global max |g| / max h over ranks (the histogram scale's inputs): every rank writes its maxima into its slot
+// of a zeroed world-sized buffer, the buffer is sum-allreduced (exact: the other slots are zeros) and
+// gh_slot_fold_kernel takes the max back into ghmax.
+__global__ void gh_slot_fill_kernel(const unsigned int* __restrict__ ghmax, float* __restrict__ slots, int rank,
+                                    int world) {
+  for (int i = threadIdx.x; i < 2 * world; i += blockDim.x)
+    slots[i] = (i >> 1) == rank ? __uint_as_float(ghmax[i & 1]) : 0.f;
+}
+__global__ void gh_slot_fold_kernel(const float* __restrict__ slots, int world, unsigned int* __restrict__ ghmax) {
+  if (threadIdx.x < 2) {
+    float m = 0.f;
+    for (int q = 0; q < world; ++q) m = fmaxf(m, slots[2 * q + threadIdx.x]);
+    ghmax[threadIdx.x] = __float_as_uint(m);
+  }
 }
 
 // ---------------------------------------------------------------- K4 + K5
@@ -2605,7 +2652,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
     const BState* __restrict__ bs, const uint4* __restrict__ bins4, int W4, int F, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
     const float* __restrict__ g, const float* __restrict__ h, const float* __restrict__ ghmax,
-    ulonglong2* __restrict__ slab) {
+    ulonglong2* __restrict__ slab, int64_t scale_n) {
   const int nexp = bs->nexp;
   if (nexp == 0) return;
   __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
@@ -2622,14 +2669,15 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
   const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
   HistBody<kUnroll, kFPG, kPipe, kTight>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
-                          ogh1, g, h, ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature);
+                          ogh1, g, h, ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n);
 }
 
 // grid (ceil(E / kRedE), spec_k): block (x, j) reduces the slabs of expansion j into part[j * (E + 1) ..]
 __global__ __launch_bounds__(kRedE * kRedG) void breduce_kernel(const BState* __restrict__ bs,
                                                                  const ulonglong2* __restrict__ slab, int E,
                                                                  const float* __restrict__ ghmax,
-                                                                 double2* __restrict__ part) {
+                                                                 double2* __restrict__ part, int64_t scale_n,
+                                                                 int i64_out) {
   const int nexp = bs->nexp;
   const float gmax_g = ghmax[0], gmax_h = ghmax[1];  // with the count: not a late dependent load
   const int j = blockIdx.y;
@@ -2663,13 +2711,20 @@ __global__ __launch_bounds__(kRedE * kRedG) void breduce_kernel(const BState* __
     unsigned long long tg = 0, th = 0;
 #pragma unroll
     for (int k = 0; k < kRedG; ++k) { tg += rg[k][le]; th += rh[k][le]; }
-    const HScale s = HistScaleV(count, gmax_g, gmax_h);
     const int F = E / kBinsPerFeature;
     const int bin = e / F, f = e - bin * F;
-    out[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
-                                                  static_cast<double>(static_cast<long long>(th)) * s.ih);
+    if (i64_out) {
+      reinterpret_cast<ulonglong2*>(out)[f * kBinsPerFeature + bin] = make_ulonglong2(tg, th);
+    } else {
+      const HScale s = HistScaleV(scale_n, gmax_g, gmax_h);
+      out[f * kBinsPerFeature + bin] = make_double2(static_cast<double>(static_cast<long long>(tg)) * s.ig,
+                                                    static_cast<double>(static_cast<long long>(th)) * s.ih);
+    }
   }
-  if (blockIdx.x == 0 && tid == 0) out[E] = make_double2(static_cast<double>(count), 0.0);
+  if (blockIdx.x == 0 && tid == 0) {
+    if (i64_out) reinterpret_cast<ulonglong2*>(out)[E] = make_ulonglong2(static_cast<unsigned long long>(count), 0ull);
+    else out[E] = make_double2(static_cast<double>(count), 0.0);
+  }
 }
 
 // grid (F, 2 * spec_k): block (f, 2j + c) searches feature f of expansion j's smaller (c = 0) or larger (c = 1)
@@ -2763,18 +2818,20 @@ __device__ __forceinline__ uint32_t ByteOfRow(const uint4& a, const uint4& b, in
   return SelBits(m4, SelBits(m3, p3, p2), SelBits(m3, p1, p0));
 }
 
+// One tree-walk step. Numerical nodes are decided branch-free (the missing-bin test folded in with masks: a
+// nested if / else if compiled to exec-mask juggling around every step); only categorical nodes, whose bitset
+// lives in global memory, take a branch.
 __device__ __forceinline__ int NodeStep(const int4& nd, uint32_t b, const uint32_t* cat_bits, int node) {
-  const int x = nd.x;
-  const int mt = (x >> 16) & 3, dl = (x >> 18) & 1, ic = (x >> 19) & 1;
-  const uint32_t mbin = static_cast<uint32_t>(x >> 20) & 511u;
-  bool left;
-  if (ic) {
+  const uint32_t x = static_cast<uint32_t>(nd.x);
+  uint32_t left;
+  if (__builtin_expect((x >> 19) & 1u, 0)) {
     const uint32_t* cb = cat_bits + node * 8;
     left = (cb[b >> 5] >> (b & 31)) & 1u;
-  } else if (mt != kMissingNone && b == mbin) {
-    left = dl != 0;
   } else {
-    left = b <= static_cast<uint32_t>(nd.y);
+    const uint32_t miss = static_cast<uint32_t>(((x >> 16) & 3u) != kMissingNone) &
+                          static_cast<uint32_t>(b == ((x >> 20) & 511u));
+    const uint32_t le = static_cast<uint32_t>(b <= static_cast<uint32_t>(nd.y));
+    left = (le & (miss ^ 1u)) | ((x >> 18) & miss);
   }
   return left ? nd.z : nd.w;
 }
@@ -2871,7 +2928,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
     float* __restrict__ g, float* __restrict__ h, const float* __restrict__ bound, float* __restrict__ partial,
-    ulonglong2* __restrict__ slab) {
+    ulonglong2* __restrict__ slab, int64_t scale_n) {
   constexpr int kThreads = kHistBlockThreads;
   const int nb_active = HistBlocks(n);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
@@ -2899,7 +2956,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   const int chunk = ceil_div_i(n, nb_active);
   const int p0 = blockIdx.x * chunk;
   const int p1 = min(n, p0 + chunk);
-  const HScale sc = HistScale(n, bound);
+  const HScale sc = HistScale(scale_n, bound);
   const bool two = F > 16;
   const int rot = tid & 15;
   float mg = 0.f, mh = 0.f;
@@ -3107,6 +3164,7 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_HIST_FPG")) hist_fpg_ = std::atoi(e) == 16 ? 16 : kFeatPerGroup;
     if (const char* e = std::getenv("SML_HIST_UNROLL")) hist_unroll4_ = std::atoi(e) == 4;
     if (const char* e = std::getenv("SML_GBDT_HIST_PIPE")) hist_pipe_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SML_GBDT_ROOT_PIPE")) root_pipe_ = std::atoi(e) != 0;
     // overlapped LDS planes (kHPlaneTight) need every group's features below slot 28
     tight_ = F_ <= 28;
     if (const char* e = std::getenv("SML_HIST_TIGHT")) tight_ = tight_ && std::atoi(e) != 0;
@@ -3161,6 +3219,15 @@ class GpuBackend : public TrainBackend {
       }
       ymax_ = -1.0;  // max |label|: computed when a cross-entropy prep pass first needs it
       ghbound_.alloc(2);
+    }
+    // global quantities of the histogram scale (HistScaleV): the row-count bound and the objective bound's
+    // max |weight| are the same on every rank, so the fixed-point histograms do not depend on the partitioning
+    scale_n_ = n_;
+    if (comm_ && comm_->world() > 1) {
+      double c = static_cast<double>(n_);
+      comm_->AllReduceHost(&c, 1);
+      scale_n_ = static_cast<int64_t>(c);
+      comm_->AllReduceHostMax(&wmax_, 1);
     }
     fbest_.alloc(static_cast<size_t>(2) * F_ * (batch_ok_ ? kMaxSpec : 1));
     lbest_.alloc(L_);
@@ -3502,6 +3569,7 @@ class GpuBackend : public TrainBackend {
                        ghmax_partial_.get(), pending_parts_, ghmax_.get());
     SML_HIP_CHECK(hipGetLastError());
     pending_parts_ = 0;
+    GlobalGhmax();
     // root histogram (slabs already built by score_grad_hist_kernel, or built here) + split search
     const float* root_scale = nullptr;
     if (root_prepared) {
@@ -3552,8 +3620,9 @@ class GpuBackend : public TrainBackend {
     const int max_rounds = budget + 2;
     auto bp = part_rows_ == 16 ? bpart_kernel<16> : (part_rows_ == 4 ? bpart_kernel<4> : bpart_kernel<8>);
     auto bh = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16>
-              : (hist_unroll4_ ? bhist_kernel<4, kFeatPerGroup>
-                               : (hist_pipe_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, true>
+              : (hist_unroll4_ ? (tight_ ? bhist_kernel<4, kFeatPerGroup, false, true> : bhist_kernel<4, kFeatPerGroup>)
+                               : (hist_pipe_ ? (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, true, true>
+                                                       : bhist_kernel<kHistUnroll, kFeatPerGroup, true>)
                                              : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true>
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup>)));
     int r = 0;
@@ -3576,13 +3645,13 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL(bh, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_,
                          bstate_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
-                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
+                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get(), scale_n_);
       SML_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL(breduce_kernel, dim3((E_ + kRedE - 1) / kRedE, spec_k_), dim3(kRedE * kRedG), 0, stream_,
-                         bstate_.get(), slab_.get(), E_, ghmax, part_.get());
+                         bstate_.get(), slab_.get(), E_, ghmax, part_.get(), scale_n_, Distributed() ? 1 : 0);
       SML_HIP_CHECK(hipGetLastError());
-      // every expansion's smaller-child histogram + row count in ONE collective per round
-      if (Distributed()) TimedAllReduce(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_ + 1) * 2 * spec_k_);
+      // every expansion's smaller-child histogram + row count in ONE exact int64 collective per round
+      if (Distributed()) ExactAllReduce(spec_k_, ghmax);
       hipLaunchKernelGGL(bfind_kernel, dim3(F_, 2 * spec_k_), dim3(256), 0, stream_, bstate_.get(), bnodes_.get(),
                          part_.get(), E_, hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
       SML_HIP_CHECK(hipGetLastError());
@@ -3698,12 +3767,12 @@ class GpuBackend : public TrainBackend {
   // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
   void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
     if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    auto sgk = hist_pipe_ ? score_grad_hist_kernel<kHistUnroll, true>
+    auto sgk = root_pipe_ ? score_grad_hist_kernel<kHistUnroll, true>
                           : (tight_ ? score_grad_hist_kernel<kHistUnroll, false, true> : score_grad_hist_kernel<kHistUnroll>);
     hipLaunchKernelGGL(sgk, dim3(kMaxHistBlocks), dim3(kHistBlockThreads), 0, stream_, tv, src,
                        reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, static_cast<int32_t>(n_), scale,
                        score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
-                       reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get());
+                       reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get(), scale_n_);
     SML_HIP_CHECK(hipGetLastError());
     if (src.st) {
       SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
@@ -3790,6 +3859,7 @@ class GpuBackend : public TrainBackend {
       if (ymax_ < 0.0) {
         ymax_ = 0.0;
         for (float y : data_->label) ymax_ = std::max(ymax_, static_cast<double>(std::fabs(y)));
+        if (comm_ && comm_->world() > 1) comm_->AllReduceHostMax(&ymax_, 1);
       }
       gb = (1.0 + ymax_) * wmax_;
       hb = 0.25 * wmax_;
@@ -3818,19 +3888,47 @@ class GpuBackend : public TrainBackend {
                                                        : hist_kernel<kHistUnroll, kFeatPerGroup>)));
     hipLaunchKernelGGL(hk, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_, st_cur_,
                        leaves_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
-                       perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get());
+                       perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get(), scale_n_);
     SML_HIP_CHECK(hipGetLastError());
     EnqueueReduce(ghmax);
   }
 
   // slab reduce with the scale the slabs were built with (+ the data-parallel allreduce)
   void EnqueueReduce(const float* ghmax) {
+    const bool exact = Distributed() && !voting_;
     hipLaunchKernelGGL(hist_reduce_kernel, dim3((E_ + kRedE - 1) / kRedE), dim3(kRedE * kRedG), 0, stream_, st_cur_,
-                       leaves_.get(), slab_.get(), E_, ghmax, part_.get());
+                       leaves_.get(), slab_.get(), E_, ghmax, part_.get(), scale_n_, exact ? 1 : 0);
     SML_HIP_CHECK(hipGetLastError());
-    // smaller child's histogram and its row count: one allreduce of 2E+2 doubles over RCCL / P2P, timed on
-    // the device (hipEvents around the collective on the engine stream). Voting keeps them local.
-    if (Distributed() && !voting_) TimedAllReduce(reinterpret_cast<double*>(part_.get()), static_cast<int64_t>(E_) * 2 + 2);
+    // smaller child's histogram and its row count: one exact int64 allreduce of 2E+2 words over RCCL / P2P,
+    // timed on the device (hipEvents around the collective on the engine stream). Voting keeps them local.
+    if (exact) ExactAllReduce(1, ghmax);
+  }
+
+  // int64 histograms (+ counts) of `nh` histograms in part_ summed over ranks, then converted to fp64 with the
+  // tree's global scale: bitwise the 1-rank histograms of the union of the partitions
+  void ExactAllReduce(int nh, const float* ghmax) {
+    EnsureCommEvents();
+    const bool timed = comm_used_ < static_cast<int>(comm_ev_.size()) / 2;
+    if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_], stream_));
+    comm_->AllReduceDeviceI64(reinterpret_cast<int64_t*>(part_.get()), static_cast<int64_t>(E_ + 1) * 2 * nh, stream_);
+    if (timed) SML_HIP_CHECK(hipEventRecord(comm_ev_[2 * comm_used_ + 1], stream_));
+    comm_used_ += timed ? 1 : 0;
+    ++stats.comm_calls;
+    hipLaunchKernelGGL(hist_convert_kernel, dim3((E_ + 1 + 255) / 256, nh), dim3(256), 0, stream_, part_.get(), E_,
+                       scale_n_, ghmax);
+    SML_HIP_CHECK(hipGetLastError());
+  }
+
+  // ghmax_ = max over ranks (data-parallel), on the stream: the scale of this tree's histograms
+  void GlobalGhmax() {
+    if (!Distributed() || comm_->world() <= 1) return;
+    const int w = comm_->world();
+    ghslot_.alloc(2 * w);
+    hipLaunchKernelGGL(gh_slot_fill_kernel, dim3(1), dim3(64), 0, stream_, ghmax_.get(), ghslot_.get(), comm_->rank(), w);
+    SML_HIP_CHECK(hipGetLastError());
+    comm_->AllReduceDeviceF32(ghslot_.get(), 2 * w, stream_);
+    hipLaunchKernelGGL(gh_slot_fold_kernel, dim3(1), dim3(64), 0, stream_, ghslot_.get(), w, ghmax_.get());
+    SML_HIP_CHECK(hipGetLastError());
   }
 
   // SML_GBDT_COMM_WORLD1=1 (tests): a world-1 communicator runs the full data-parallel path (allreduce per
@@ -4010,6 +4108,7 @@ class GpuBackend : public TrainBackend {
   int hist_fpg_ = kFeatPerGroup;  // SML_HIST_FPG=16: half-width feature groups for the per-split histogram
   bool hist_unroll4_ = false;     // SML_HIST_UNROLL=4: 4 gathered rows in flight per thread (A/B knob)
   bool hist_pipe_ = false;        // SML_GBDT_HIST_PIPE=1: software-pipelined histogram loops (A/B knob)
+  bool root_pipe_ = false;        // SML_GBDT_ROOT_PIPE=1: software-pipelined root pass (A/B knob)
   bool tight_ = false;            // h LDS plane inside the DS offset range of the g plane (F <= 28; SML_HIST_TIGHT=0 off)
   // lambdarank register kernel: waves per block. SML_RANK_WAVES=4 packs 4 independent waves per block (up
   // to 10 resident per SIMD instead of 4): r4 pass 11 measured it slower (949 vs 860 us per call, ranker
@@ -4033,6 +4132,8 @@ class GpuBackend : public TrainBackend {
   DevBuf<int32_t> meta_i_, bag_;
   DevBuf<int8_t> mask_, mono_;
   DevBuf<unsigned int> ghmax_;
+  DevBuf<float> ghslot_;   // data-parallel: per-rank slots of the global max |g| / max h
+  int64_t scale_n_ = 0;    // global row count: the histogram scale's count bound
   // Fusing reduce / find / choose into one launch (F blocks, slab reduce inside) measured slower on MI355X
   // (2.05 vs 1.97 ms/iter: 28 blocks cannot pull the slabs fast enough; profiles/README, round 2)
   bool skip_last_ = true;  // SML_SKIP_LAST_SPLIT=0: histogram + search the last split's children too

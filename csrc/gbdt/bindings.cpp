@@ -10,6 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <stdexcept>
+#include <type_traits>
 
 #include "backend.h"
 #include "booster.h"
@@ -225,18 +226,26 @@ PYBIND11_MODULE(_gbdt, m) {
       .def("allreduce_host", [](PyComm& c, py::array_t<double> a) {
         auto b = a.request();
         c.c->AllReduceHost(static_cast<double*>(b.ptr), b.size);
+      })
+      .def("allreduce_host_i64", [](PyComm& c, py::array_t<int64_t> a) {
+        auto b = a.request();
+        c.c->AllReduceHostI64(static_cast<int64_t*>(b.ptr), b.size);
       });
-  m.def("host_comm", [](int rank, int world, std::function<void(py::array_t<double>)> fn) {
+  // fn(array) sums a float64 or int64 host array in place over the ranks (the Python control plane)
+  m.def("host_comm", [](int rank, int world, py::function fn) {
     PyComm c;
-    c.c = std::make_shared<HostComm>(rank, world, [fn](double* buf, int64_t n) {
+    auto call = [fn](auto* buf, int64_t n) {
+      using T = std::remove_pointer_t<decltype(buf)>;
       py::gil_scoped_acquire acq;
-      py::array_t<double> a({n}, {sizeof(double)}, buf, py::none());
+      py::array_t<T> a({n}, {static_cast<py::ssize_t>(sizeof(T))}, buf, py::none());
       try {
         fn(a);
       } catch (py::error_already_set& e) {  // gloo / TCP failure of the host collective (peer died, timeout)
         throw CommError(std::string("host allreduce failed: ") + e.what());
       }
-    });
+    };
+    c.c = std::make_shared<HostComm>(rank, world, [call](double* buf, int64_t n) { call(buf, n); },
+                                     [call](int64_t* buf, int64_t n) { call(buf, n); });
     return c;
   });
   m.def("p2p_comm", [](PyComm& base, int device, int64_t cap_bytes, double timeout_ms) {

@@ -106,13 +106,7 @@ void Booster::InitTraining() {
     if (cfg_.boost_from_average && objective_->params().kind != kObjLambdarank &&
         objective_->params().kind != kObjCustom) {
       for (int k = 0; k < K; ++k) {
-        double v = objective_->BoostFromScore(k);
-        if (comm_ && comm_->world() > 1) {
-          double buf[2] = {v * n, static_cast<double>(n)};
-          comm_->AllReduceHost(buf, 2);
-          v = buf[1] > 0 ? buf[0] / buf[1] : 0.0;
-        }
-        init_scores_[k] = v;
+        init_scores_[k] = objective_->BoostFromScore(k, comm_);
       }
     }
     backend_->FillScores(init_scores_, n);  // constant start scores, written where the scores live

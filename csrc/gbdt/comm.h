@@ -6,6 +6,7 @@
 //   * HostComm: a host-buffer allreduce supplied by the Python runtime (gloo /
 //     TCP) for the CPU backend and for tests without GPUs.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -31,6 +32,23 @@ class Comm {
   // in-place sum over ranks of a DEVICE buffer on `stream` (hipStream_t)
   virtual void AllReduceDeviceF32(float* buf, int64_t n, void* stream) = 0;
   virtual void AllReduceDeviceF64(double* buf, int64_t n, void* stream) = 0;
+  // exact (associative) sums: the fixed-point histograms of data-parallel training travel as int64, so an
+  // N-rank histogram is bitwise the 1-rank histogram of the union of the partitions
+  virtual void AllReduceHostI64(int64_t* buf, int64_t n) = 0;
+  virtual void AllReduceDeviceI64(int64_t* buf, int64_t n, void* stream) = 0;
+  // element-wise max over ranks of a small HOST buffer, built on the sum: every rank contributes its values in
+  // its own slot of a world-sized buffer (exact - the other slots are zeros) and takes the max locally
+  void AllReduceHostMax(double* buf, int64_t n) {
+    if (world() <= 1) return;
+    std::vector<double> all(static_cast<size_t>(n) * world(), 0.0);
+    for (int64_t i = 0; i < n; ++i) all[static_cast<size_t>(rank()) * n + i] = buf[i];
+    AllReduceHost(all.data(), static_cast<int64_t>(all.size()));
+    for (int64_t i = 0; i < n; ++i) {
+      double m = all[i];
+      for (int q = 1; q < world(); ++q) m = std::max(m, all[static_cast<size_t>(q) * n + i]);
+      buf[i] = m;
+    }
+  }
   virtual bool is_device() const { return false; }
   // raise CommError if an asynchronous collective failed; polled while the backend waits on the device
   virtual void Check() {}
@@ -43,16 +61,21 @@ class Comm {
 class HostComm : public Comm {
  public:
   using Fn = std::function<void(double*, int64_t)>;
-  HostComm(int rank, int world, Fn fn) : rank_(rank), world_(world), fn_(std::move(fn)) {}
+  using FnI64 = std::function<void(int64_t*, int64_t)>;
+  HostComm(int rank, int world, Fn fn, FnI64 fn_i64 = nullptr)
+      : rank_(rank), world_(world), fn_(std::move(fn)), fn_i64_(std::move(fn_i64)) {}
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   void AllReduceHost(double* buf, int64_t n) override { if (world_ > 1) fn_(buf, n); }
+  void AllReduceHostI64(int64_t* buf, int64_t n) override;
   void AllReduceDeviceF32(float*, int64_t, void*) override;
   void AllReduceDeviceF64(double*, int64_t, void*) override;
+  void AllReduceDeviceI64(int64_t*, int64_t, void*) override;
 
  private:
   int rank_, world_;
   Fn fn_;
+  FnI64 fn_i64_;
 };
 
 // RCCL communicator (defined in comm_rccl.cpp)

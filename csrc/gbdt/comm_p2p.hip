@@ -168,6 +168,11 @@ class P2pComm : public Comm {
   const std::string& reason() const { return reason_; }
 
   void AllReduceHost(double* buf, int64_t n) override { base_->AllReduceHost(buf, n); }
+  void AllReduceHostI64(int64_t* buf, int64_t n) override { base_->AllReduceHostI64(buf, n); }
+  void AllReduceDeviceI64(int64_t* buf, int64_t n, void* stream) override {
+    if (!Use(n * 8)) return base_->AllReduceDeviceI64(buf, n, stream);
+    Launch(reinterpret_cast<long long*>(buf), n, static_cast<hipStream_t>(stream));
+  }
   void AllReduceDeviceF32(float* buf, int64_t n, void* stream) override {
     if (!Use(n * 4)) return base_->AllReduceDeviceF32(buf, n, stream);
     Launch(buf, n, static_cast<hipStream_t>(stream));

@@ -38,6 +38,41 @@ void HostComm::AllReduceDeviceF32(float* buf, int64_t n, void* stream) {
   SML_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void HostComm::AllReduceHostI64(int64_t* buf, int64_t n) {
+  if (world_ <= 1) return;
+  if (fn_i64_) {
+    fn_i64_(buf, n);
+    return;
+  }
+  // no integer collective was supplied: exact through the double one in 26-bit limbs (every partial sum of
+  // a limb stays far below 2^53 for any realistic world size)
+  constexpr int kLimbs = 3;
+  std::vector<double> d(static_cast<size_t>(n) * kLimbs);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t u = static_cast<uint64_t>(buf[i]);
+    d[i * kLimbs] = static_cast<double>(u & ((1ull << 26) - 1));
+    d[i * kLimbs + 1] = static_cast<double>((u >> 26) & ((1ull << 26) - 1));
+    d[i * kLimbs + 2] = static_cast<double>(u >> 52);
+  }
+  fn_(d.data(), static_cast<int64_t>(d.size()));
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t a = static_cast<uint64_t>(d[i * kLimbs]), b = static_cast<uint64_t>(d[i * kLimbs + 1]),
+                   c = static_cast<uint64_t>(d[i * kLimbs + 2]);
+    buf[i] = static_cast<int64_t>(a + (b << 26) + (c << 52));  // modulo 2^64: two's complement sums wrap exactly
+  }
+}
+
+void HostComm::AllReduceDeviceI64(int64_t* buf, int64_t n, void* stream) {
+  if (world_ <= 1) return;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::vector<int64_t> h(n);
+  SML_HIP_CHECK(hipMemcpyAsync(h.data(), buf, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
+  SML_HIP_CHECK(hipStreamSynchronize(s));
+  AllReduceHostI64(h.data(), n);
+  SML_HIP_CHECK(hipMemcpyAsync(buf, h.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
+  SML_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 void HostComm::AllReduceDeviceF64(double* buf, int64_t n, void* stream) {
   if (world_ <= 1) return;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -120,6 +155,20 @@ class RcclComm : public Comm {
   void AllReduceDeviceF64(double* buf, int64_t n, void* stream) override {
     if (!comm_) throw CommError("RCCL communicator was aborted");
     Settle(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm_, static_cast<hipStream_t>(stream)), "ncclAllReduce");
+  }
+  void AllReduceDeviceI64(int64_t* buf, int64_t n, void* stream) override {
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    Settle(ncclAllReduce(buf, buf, n, ncclInt64, ncclSum, comm_, static_cast<hipStream_t>(stream)), "ncclAllReduce");
+  }
+  void AllReduceHostI64(int64_t* buf, int64_t n) override {
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    int64_t* d = nullptr;
+    SML_HIP_CHECK(hipMalloc(&d, sizeof(int64_t) * n));
+    SML_HIP_CHECK(hipMemcpy(d, buf, sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    Settle(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm_, nullptr), "ncclAllReduce");
+    SML_HIP_CHECK(hipStreamSynchronize(nullptr));
+    SML_HIP_CHECK(hipMemcpy(buf, d, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    SML_HIP_CHECK(hipFree(d));
   }
 
  private:

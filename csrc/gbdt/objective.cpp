@@ -1,4 +1,5 @@
 #include "objective.h"
+#include "comm.h"
 
 #include <algorithm>
 #include <cmath>
@@ -188,7 +189,46 @@ double WeightedPercentile(std::vector<std::pair<double, double>> v, double alpha
 }
 }  // namespace
 
-double Objective::BoostFromScore(int class_id) const {
+// Sums of y(i) * w(i) and w(i) over the rows of EVERY rank, exactly: values are quantised to int64 with a
+// scale from global quantities (row count, max |y w|, max |w|) and summed as integers, so the result does not
+// depend on thread count or on how rows are spread over ranks (LightGBM reduces these sums over machines,
+// GlobalSyncUpBySum in BoostFromScore; averaging per-rank log-odds, as this engine did before, is not the
+// log-odds of the global mean).
+template <class Y, class W>
+static void GlobalSums(int64_t n, Y y, W w, Comm* comm, double* sum_yw, double* sum_w) {
+  double m0 = 0.0, m1 = 0.0;
+#pragma omp parallel for schedule(static) reduction(max : m0, m1)
+  for (int64_t i = 0; i < n; ++i) {
+    m0 = std::max(m0, std::fabs(y(i) * w(i)));
+    m1 = std::max(m1, std::fabs(w(i)));
+  }
+  double mx[2] = {m0, m1};
+  double nn = static_cast<double>(n);
+  const bool dist = comm && comm->world() > 1;
+  if (dist) {
+    comm->AllReduceHostMax(mx, 2);
+    comm->AllReduceHost(&nn, 1);
+  }
+  auto ex = [&](double vmax) {
+    const double r = 4.611686018427387904e18 / (std::max(1.0, nn) * std::max(vmax, 1e-300));
+    return std::max(-1000, std::min(1000, std::ilogb(r)));
+  };
+  const double s0 = std::ldexp(1.0, ex(mx[0])), s1 = std::ldexp(1.0, ex(mx[1]));
+  int64_t q[2] = {0, 0};
+  int64_t a = 0, b = 0;
+#pragma omp parallel for schedule(static) reduction(+ : a, b)
+  for (int64_t i = 0; i < n; ++i) {
+    a += static_cast<int64_t>(std::nearbyint(y(i) * w(i) * s0));
+    b += static_cast<int64_t>(std::nearbyint(w(i) * s1));
+  }
+  q[0] = a;
+  q[1] = b;
+  if (dist) comm->AllReduceHostI64(q, 2);
+  *sum_yw = static_cast<double>(q[0]) / s0;
+  *sum_w = static_cast<double>(q[1]) / s1;
+}
+
+double Objective::BoostFromScore(int class_id, Comm* comm) const {
   if (!boost_from_average_) return 0.0;
   const int64_t n = n_;
   auto W = [&](int64_t i) { return weight_ ? static_cast<double>(weight_[i]) : 1.0; };
@@ -197,12 +237,11 @@ double Objective::BoostFromScore(int class_id) const {
     case kObjMulticlassOVA:
     case kObjCrossEntropy: {
       double sl = 0, sw = 0;
-#pragma omp parallel for schedule(static) reduction(+ : sl, sw)
-      for (int64_t i = 0; i < n; ++i) {
-        double y = p_.kind == kObjMulticlassOVA ? (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0)
-                                               : (p_.kind == kObjBinary ? (label_[i] > 0 ? 1.0 : 0.0) : label_[i]);
-        sl += y * W(i); sw += W(i);
-      }
+      GlobalSums(n, [&](int64_t i) {
+        return p_.kind == kObjMulticlassOVA ? (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0)
+                                           : (p_.kind == kObjBinary ? (label_[i] > 0 ? 1.0 : 0.0)
+                                                                    : static_cast<double>(label_[i]));
+      }, W, comm, &sl, &sw);
       double pavg = sw > 0 ? sl / sw : 0.5;
       pavg = std::min(std::max(pavg, kEpsilon), 1.0 - kEpsilon);
       double init = std::log(pavg / (1.0 - pavg));
@@ -211,8 +250,7 @@ double Objective::BoostFromScore(int class_id) const {
     }
     case kObjMulticlass: {
       double sl = 0, sw = 0;
-#pragma omp parallel for schedule(static) reduction(+ : sl, sw)
-      for (int64_t i = 0; i < n; ++i) { sl += (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0) * W(i); sw += W(i); }
+      GlobalSums(n, [&](int64_t i) { return static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0; }, W, comm, &sl, &sw);
       double p = sw > 0 ? sl / sw : 1.0 / p_.num_class;
       return std::log(std::max(kEpsilon, p));
     }
@@ -220,27 +258,34 @@ double Objective::BoostFromScore(int class_id) const {
     case kObjHuber:
     case kObjFair: {
       double s = 0, sw = 0;
-      for (int64_t i = 0; i < n; ++i) { s += label_[i] * W(i); sw += W(i); }
+      GlobalSums(n, [&](int64_t i) { return static_cast<double>(label_[i]); }, W, comm, &s, &sw);
       return sw > 0 ? s / sw : 0.0;
     }
     case kObjPoisson:
     case kObjGamma:
     case kObjTweedie: {
       double s = 0, sw = 0;
-      for (int64_t i = 0; i < n; ++i) { s += label_[i] * W(i); sw += W(i); }
+      GlobalSums(n, [&](int64_t i) { return static_cast<double>(label_[i]); }, W, comm, &s, &sw);
       double m = sw > 0 ? s / sw : 1.0;
       return std::log(std::max(m, kEpsilon));
     }
     case kObjL1:
-    case kObjQuantile: {
-      std::vector<std::pair<double, double>> v(n);
-      for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i)};
-      return WeightedPercentile(std::move(v), p_.kind == kObjL1 ? 0.5 : p_.alpha);
-    }
+    case kObjQuantile:
     case kObjMape: {
+      // a weighted percentile of the local rows; over ranks the row-count-weighted mean of them (as LightGBM's
+      // distributed L1 / quantile start: an approximation of the global percentile)
       std::vector<std::pair<double, double>> v(n);
-      for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i) / std::max(1.0, std::fabs(static_cast<double>(label_[i])))};
-      return WeightedPercentile(std::move(v), 0.5);
+      if (p_.kind == kObjMape)
+        for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i) / std::max(1.0, std::fabs(static_cast<double>(label_[i])))};
+      else
+        for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i)};
+      double r = WeightedPercentile(std::move(v), p_.kind == kObjQuantile ? p_.alpha : 0.5);
+      if (comm && comm->world() > 1) {
+        double buf[2] = {r * n, static_cast<double>(n)};
+        comm->AllReduceHost(buf, 2);
+        r = buf[1] > 0 ? buf[0] / buf[1] : 0.0;
+      }
+      return r;
     }
     default: return 0.0;
   }

@@ -103,7 +103,8 @@ class Objective {
   void Init(const float* label, const float* weight, int64_t n, const std::vector<int32_t>& qb);
   // score layout: class-major, score[k * n + i]
   void GetGradients(const double* score, float* g, float* h) const;
-  double BoostFromScore(int class_id) const;
+  // the start score over every rank's rows (comm: the data-parallel group, or nullptr)
+  double BoostFromScore(int class_id, class Comm* comm = nullptr) const;
   void ConvertOutput(const double* raw, double* out) const;  // one row, num_out values
   int NumModelPerIteration() const { return num_tree_per_iter_; }
   bool NeedRenewTreeOutput() const { return p_.kind == kObjL1 || p_.kind == kObjQuantile || p_.kind == kObjMape; }

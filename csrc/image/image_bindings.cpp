@@ -155,8 +155,11 @@ PYBIND11_MODULE(_image, m) {
   m.def("preprocess_batch_device",
         [](uintptr_t src, uintptr_t offsets, uintptr_t dims, int B, int out_h, int out_w, int resize_h, int resize_w,
            int crop_y, int crop_x, std::vector<int> chan_map, double scale, std::vector<double> mean,
-           std::vector<double> stdv, int out_dtype, int nhwc, uintptr_t out, uintptr_t stream) {
+           std::vector<double> stdv, int out_dtype, int nhwc, uintptr_t out, uintptr_t stream,
+           std::vector<int32_t> host_dims) {
           PrepParams p{};
+          if (resize_h > 0 && host_dims.size() != static_cast<size_t>(3) * B)
+            throw std::invalid_argument("preprocess: resize needs host_dims = 3 ints per image");
           p.out_h = out_h; p.out_w = out_w; p.resize_h = resize_h; p.resize_w = resize_w;
           p.crop_y = crop_y; p.crop_x = crop_x;
           p.cout = static_cast<int>(chan_map.size());
@@ -164,9 +167,17 @@ PYBIND11_MODULE(_image, m) {
             throw std::invalid_argument("preprocess: bad channel map / mean / std");
           for (int k = 0; k < p.cout; ++k) { p.chan_map[k] = chan_map[k]; p.mean[k] = mean[k]; p.stdv[k] = stdv[k]; }
           p.scale = scale; p.out_dtype = out_dtype; p.nhwc = nhwc;
+          p.host_dims = host_dims.empty() ? nullptr : host_dims.data();
           PreprocessBatchDevice(Ptr<const uint8_t>(src), Ptr<const int64_t>(offsets), Ptr<const int32_t>(dims), B, p,
                                 Ptr<void>(out), Ptr<void>(stream));
-        });
+        }, py::arg("src"), py::arg("offsets"), py::arg("dims"), py::arg("B"), py::arg("out_h"), py::arg("out_w"),
+        py::arg("resize_h"), py::arg("resize_w"), py::arg("crop_y"), py::arg("crop_x"), py::arg("chan_map"),
+        py::arg("scale"), py::arg("mean"), py::arg("stdv"), py::arg("out_dtype"), py::arg("nhwc"), py::arg("out"),
+        py::arg("stream"), py::arg("host_dims") = std::vector<int32_t>{});
+  m.def("crop_flip_batch_device", [](uintptr_t src, int B, int sh, int sw, int c, uintptr_t dst, int dh, int dw, int cy,
+                                     int cx, int flip, uintptr_t stream) {
+    CropFlipBatchDevice(Ptr<const uint8_t>(src), B, sh, sw, c, Ptr<uint8_t>(dst), dh, dw, cy, cx, flip, Ptr<void>(stream));
+  });
   m.def("resize_batch_device", [](uintptr_t src, int B, int sh, int sw, int c, uintptr_t dst, int dh, int dw,
                                   uintptr_t stream) {
     ResizeBatchDevice(Ptr<const uint8_t>(src), B, sh, sw, c, Ptr<uint8_t>(dst), dh, dw, Ptr<void>(stream));

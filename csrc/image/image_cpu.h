@@ -29,6 +29,7 @@ struct PrepParams {
   double mean[4], stdv[4];
   int out_dtype;          // 0 f32, 1 f16, 2 bf16
   int nhwc;               // 0 = NCHW (ONNX layout), 1 = NHWC
+  const int32_t* host_dims = nullptr;  // HOST copy of dims (the resize taps are built per image on the host)
 };
 
 // K19: batched decode-free preprocess. Images are packed HWC uint8 at
@@ -45,6 +46,9 @@ void ColumnFilterBatchDevice(const uint8_t* src, int B, int h, int w, int c, uin
                              void* stream);
 void ThresholdDevice(const uint8_t* src, int64_t n, uint8_t* dst, double thr, double maxval, int type, void* stream);
 void FlipBatchDevice(const uint8_t* src, int B, int h, int w, int c, uint8_t* dst, int code, void* stream);
+// crop window (cy, cx, dh x dw) of every image, optionally flipped (0 up-down, 1 left-right, 2 both, -1 none)
+void CropFlipBatchDevice(const uint8_t* src, int B, int sh, int sw, int c, uint8_t* dst, int dh, int dw, int cy, int cx,
+                         int flip, void* stream);
 void CvtColorDevice(const uint8_t* src, int64_t npx, int cin, int code, uint8_t* dst, void* stream);
 bool ImageGpuAvailable();
 

@@ -8,8 +8,12 @@ core/.../image/UnrollImage.scala:27-250.
 Execution: stage semantics are the OpenCV ones (csrc/image/image_ops.h). On
 the MI355X the common inference pipeline — decode → resize → (center)crop →
 channel reorder → normalize → CHW tensor — runs as ONE batched HIP kernel
-(K19, csrc/image/image_gpu.hip) over a packed host→device upload; other stage
-lists run stage by stage through the native host kernels.
+(K19, csrc/image/image_gpu.hip) over a packed host→device upload. Every other
+stage list (resize incl. keepAspectRatio, crop, centerCrop, colorFormat, flip,
+blur, threshold, gaussianKernel, optionally followed by toTensor) runs on the
+device too, as batched K20 launches over images of one shape that stay
+resident in HBM from the upload to the last stage; results are bit-identical
+to the host kernels (deviceType="cpu").
 """
 from __future__ import annotations
 
@@ -344,12 +348,144 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         _img().preprocess_batch_device(src.data_ptr(), off_d.data_ptr(), dims_d.data_ptr(), B, ch, cw, rh, rw, cy, cx,
                                        cmap, scale, mean, std, {torch.float32: 0, torch.float16: 1,
                                                                 torch.bfloat16: 2}[tdt], int(nhwc), out.data_ptr(),
-                                       torch.cuda.current_stream(dev).cuda_stream)
+                                       torch.cuda.current_stream(dev).cuda_stream, [int(v) for v in dims])
         if nhwc:
             out = out.permute(0, 3, 1, 2)  # logical NCHW view, channels-last memory
         # keep the upload buffers alive until the kernel has consumed them
         out._sml_keepalive = (host, src, off_d, dims_d)
         return out
+
+    # ---- K20: any stage list on the device, one uniform-shape batch at a time
+    _DEVICE_STAGES = ("resize", "crop", "centercrop", "colorformat", "flip", "blur", "threshold", "gaussiankernel")
+
+    def run_stages_device(self, batch: np.ndarray):
+        """The stage list on a batch of equally shaped HWC uint8 images ([B, h, w, c] numpy) on the MI355X;
+        returns the resident device result [B, h', w', c'] (torch uint8) or None when a stage has no device
+        form for this shape (the host path then runs)."""
+        import torch
+
+        stages = list(self.getStages() or [])
+        if any(stage_action(st) not in self._DEVICE_STAGES for st in stages) or batch.ndim != 4:
+            return None
+        lib = _img()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        x = torch.from_numpy(np.ascontiguousarray(batch)).pin_memory().to(dev, non_blocking=True)
+        keep = [x]
+        for st in stages:
+            B, h, w, c = x.shape
+            name = stage_action(st)
+            if c not in (1, 3, 4) and name in ("resize", "crop", "centercrop", "flip"):
+                return None
+            if name == "resize":
+                th, tw = resize_target(st, h, w)
+                y = torch.empty((B, th, tw, c), dtype=torch.uint8, device=dev)
+                lib.resize_batch_device(x.data_ptr(), B, h, w, c, y.data_ptr(), th, tw, stream)
+            elif name in ("crop", "centercrop"):
+                if name == "crop":
+                    cy, cx, ch, cw = int(st["y"]), int(st["x"]), int(st["height"]), int(st["width"])
+                    if cx + cw > w or cy + ch > h:
+                        raise ValueError("crop rectangle outside the image")
+                else:
+                    cy, cx, ch, cw = center_crop_rect(st, h, w)
+                y = torch.empty((B, ch, cw, c), dtype=torch.uint8, device=dev)
+                lib.crop_flip_batch_device(x.data_ptr(), B, h, w, c, y.data_ptr(), ch, cw, cy, cx, -1, stream)
+            elif name == "colorformat":
+                code = int(st["format"])
+                cout = lib.cvt_channels_out(code, c)
+                y = torch.empty((B, h, w, cout), dtype=torch.uint8, device=dev)
+                lib.cvt_color_device(x.data_ptr(), B * h * w, c, code, y.data_ptr(), stream)
+            elif name == "flip":
+                y = torch.empty_like(x)
+                lib.flip_batch_device(x.data_ptr(), B, h, w, c, y.data_ptr(), int(st.get("flipCode", 1)), stream)
+            elif name == "blur":
+                y = torch.empty_like(x)
+                # Imgproc.blur(image, dst, new Size(height, width)): Size(width=height, height=width)
+                lib.box_blur_batch_device(x.data_ptr(), B, h, w, c, y.data_ptr(), int(st["height"]), int(st["width"]),
+                                          stream)
+            elif name == "threshold":
+                y = torch.empty_like(x)
+                lib.threshold_device(x.data_ptr(), x.numel(), y.data_ptr(), float(st["threshold"]), float(st["maxVal"]),
+                                     int(st["type"]), stream)
+            else:  # gaussiankernel
+                k = lib.gaussian_kernel(int(st["apertureSize"]), float(st["sigma"]))
+                y = torch.empty_like(x)
+                lib.column_filter_batch_device(x.data_ptr(), B, h, w, c, y.data_ptr(), list(k), stream)
+            keep.append(y)
+            x = y
+        x._sml_keepalive = keep
+        return x
+
+    def tensors_from_device_images(self, x, dtype: str = "float32"):
+        """toTensor of a resident [B, h, w, c] uint8 batch: the K19 kernel with no resize / crop."""
+        import torch
+
+        B, h, w, c = x.shape
+        cmap = channel_map(c, self.getTensorChannelOrder(), self.getAutoConvertToColor())
+        mean, std, scale = self._norm_params(len(cmap))
+        dev = x.device
+        offsets = torch.arange(B, dtype=torch.int64, device=dev) * (h * w * c)
+        dims = torch.tensor([h, w, c] * B, dtype=torch.int32, device=dev)
+        tdt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[dtype]
+        out = torch.empty((B, len(cmap), h, w), dtype=tdt, device=dev)
+        _img().preprocess_batch_device(x.data_ptr(), offsets.data_ptr(), dims.data_ptr(), B, h, w, 0, 0, 0, 0, cmap,
+                                       scale, mean, std, {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[tdt],
+                                       0, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        out._sml_keepalive = (x, offsets, dims)
+        return out
+
+    def _transform_device(self, arrays: List[Optional[np.ndarray]], valid: List[int], out: np.ndarray,
+                          origins: List[str]) -> set:
+        """Device execution of the stage list (K19 fused when it applies, else K20 stage kernels over
+        uniform-shape batches). Returns the row indices it produced."""
+        done = set()
+        bs = max(1, self.getBatchSize())
+        to_tensor = self.getToTensor()
+        fused = to_tensor and self._fused_plan([arrays[i].shape for i in valid]) is not None
+        if fused:
+            for s in range(0, len(valid), bs):
+                idx = valid[s:s + bs]
+                t = self.device_tensors([arrays[i] for i in idx])
+                if t is None:
+                    return done
+                host = t.float().cpu().numpy()
+                for j, i in enumerate(idx):
+                    out[i] = host[j]
+                    done.add(i)
+            return done
+        groups: Dict[tuple, List[int]] = {}
+        for i in valid:
+            groups.setdefault(arrays[i].shape, []).append(i)
+        float_tensor = to_tensor and self.getTensorElementType().lower() == "float"
+        for shape, members in groups.items():
+            if len(shape) != 3:
+                continue
+            for s in range(0, len(members), bs):
+                idx = members[s:s + bs]
+                x = self.run_stages_device(np.stack([arrays[i] for i in idx]))
+                if x is None:
+                    break
+                if float_tensor:
+                    host = self.tensors_from_device_images(x).cpu().numpy()
+                    for j, i in enumerate(idx):
+                        out[i] = host[j]
+                        done.add(i)
+                    continue
+                host = x.cpu().numpy()
+                for j, i in enumerate(idx):
+                    a = host[j]
+                    out[i] = self._finish_host(a) if to_tensor else make_image_row(a, origins[i])
+                    done.add(i)
+        return done
+
+    def _finish_host(self, a: np.ndarray):
+        """toTensor of one processed image on the host (tensorElementType double: the reference's fp64)."""
+        cmap = channel_map(a.shape[2], self.getTensorChannelOrder(), self.getAutoConvertToColor())
+        mean, std, scale = self._norm_params(len(cmap))
+        if self.getTensorElementType().lower() == "double":
+            src = a[:, :, cmap].astype(np.float64).transpose(2, 0, 1)
+            return (src * scale - np.asarray(mean)[:, None, None]) / np.asarray(std)[:, None, None]
+        return _img().to_tensor(np.ascontiguousarray(a), cmap, scale, mean, std)
 
     def process_host(self, a: np.ndarray):
         for st in self.getStages() or []:
@@ -378,30 +514,16 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         n = len(arrays)
         out = np.empty(n, dtype=object)
         valid = [i for i, a in enumerate(arrays) if a is not None]
+        col = df[self.getInputCol()]
+        origins = [(v.get("origin", "") if isinstance(v, dict) else "") for v in (col.tolist() if valid else [])]
         done = set()
-        if self.getToTensor() and valid and _gpu_ok(self.getDeviceType()):
-            bs = max(1, self.getBatchSize())
-            for s in range(0, len(valid), bs):
-                idx = valid[s:s + bs]
-                t = self.device_tensors([arrays[i] for i in idx])
-                if t is None:
-                    break
-                host = t.float().cpu().numpy()
-                for j, i in enumerate(idx):
-                    out[i] = host[j]
-                    done.add(i)
+        if valid and _gpu_ok(self.getDeviceType()):
+            done = self._transform_device(arrays, valid, out, origins)
         for i in valid:
             if i in done:
                 continue
             r = self.process_host(arrays[i])
-            if self.getToTensor():
-                out[i] = r
-            else:
-                origin = ""
-                v = df[self.getInputCol()][i]
-                if isinstance(v, dict):
-                    origin = v.get("origin", "")
-                out[i] = make_image_row(r, origin)
+            out[i] = r if self.getToTensor() else make_image_row(r, origins[i])
         return df.withColumn(self.getOutputCol(), out)
 
 

@@ -107,7 +107,7 @@ def all_gather_object(obj: Any) -> List[Any]:
 
 
 def allreduce_numpy(a: np.ndarray) -> None:
-    """In-place sum of a float64 host array over the default group."""
+    """In-place sum of a float64 or int64 host array over the default group (int64: exact)."""
     if not is_initialized() or world_size() == 1:
         return
     import torch

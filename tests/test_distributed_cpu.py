@@ -469,3 +469,38 @@ def test_inert_params_warn(caplog):
     with caplog.at_level(logging.WARNING, logger="synapseml_amd.lightgbm"):
         LightGBMClassifier(deviceType="cpu", numIterations=2).fit(df)
     assert not any("has no effect" in r.getMessage() for r in caplog.records)
+
+
+
+
+class _ModelText:
+    def __init__(self, est):
+        self.est = est
+
+    def __call__(self, part, rank, world):
+        m = self.est.fit(part)
+        return m.getNativeModel().split("parameters:")[0] if rank == 0 else None
+
+
+@pytest.mark.parametrize("est_cls,extra", [(LightGBMClassifier, {}),
+                                           (LightGBMRegressor, {"lambdaL2": 1.0}),
+                                           (LightGBMClassifier, {"numLeaves": 63, "minDataInLeaf": 5})])
+def test_n_ranks_give_the_1_rank_model_bitwise(est_cls, extra):
+    """The fixed-point histograms travel as int64 with a scale built from global quantities only (global row
+    count, global max |g| / max h), so 1, 2 and 4 ranks train byte-identical models on the same rows and bin
+    boundaries (VerifyLightGBMClassifierStream.scala:95-101 checks the same for streaming vs bulk)."""
+    rng = np.random.default_rng(5)
+    n = 8000
+    X = rng.standard_normal((n, 7))
+    y = (X[:, 0] + X[:, 1] * X[:, 2] - 0.5 * X[:, 3] > 0).astype(float)
+    if est_cls is LightGBMRegressor:
+        y = X[:, 0] * 2 + X[:, 1] ** 2 + 0.1 * rng.standard_normal(n)
+    kw = dict(deviceType="cpu", numIterations=6, numThreads=2, **extra)
+    base = est_cls(**kw)
+    df1 = DataFrame({"features": X, "label": y})
+    one = base.fit(df1).getNativeModel().split("parameters:")[0]
+    ref = base._last_reference
+    for world in (2, 4):
+        df = DataFrame({"features": X, "label": y}, num_partitions=world)
+        txt = run_partitions(_ModelText(est_cls(referenceDataset=ref, **kw)), df, num_workers=world)[0]
+        assert txt == one, f"world {world} model differs from the 1-rank model"

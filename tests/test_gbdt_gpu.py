@@ -633,3 +633,22 @@ def test_gpu_single_pass_scoring_float32_rows():
     raw, prob = lb.score_both(X32, classification=True)
     np.testing.assert_allclose(raw[:, 1], host[:, 0], rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(prob[:, 1], b.predict(X32.astype(np.float64), 1, 0, -1)[:, 0], rtol=1e-12, atol=1e-12)
+
+
+def test_num_tasks_fit_fans_out_on_gpu():
+    """LightGBMClassifier(numTasks=2).fit(df) on the device runs 2 partition tasks itself (LightGBMBase.scala:
+    449-456, 608-628). On a one-GPU box the tasks share the device (gloo control plane, shared-device
+    histogram allreduce); the model is byte-identical to the one-task model on the same data and bins."""
+    from synapseml_amd.core import DataFrame
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    X, y = _data(n=40000, f=10)
+    df = DataFrame({"features": X, "label": y}, num_partitions=2)
+    one = LightGBMClassifier(deviceType="gpu", numIterations=5, numTasks=1)
+    m1 = one.fit(df)
+    ref = one._last_reference
+    est = LightGBMClassifier(deviceType="gpu", numIterations=5, numTasks=2, referenceDataset=ref)
+    m2 = est.fit(df)
+    assert len(est.getTaskMeasures()) == 2
+    # int64 histograms under a global scale: the 2-task model is bitwise the 1-task model
+    assert m2.getNativeModel().split("parameters:")[0] == m1.getNativeModel().split("parameters:")[0]
