@@ -413,8 +413,16 @@ void VW::Update(const Example& ex, uint64_t offset, float pred, float label, flo
       // first-order implicit step, bounded so the margin cannot overshoot
       const float step = label * update_scale / (1.f + std::exp(label * pred));
       update = std::abs(step * ppu) > 50.f ? std::copysign(50.f / ppu, step) : step;
+    } else if (loss_ == "hinge") {
+      // the step stops at the margin (VW's hingeloss::getUpdate)
+      const float err = 1.f - label * pred;
+      update = err <= 0.f ? 0.f : label * std::min(update_scale, err / ppu);
     } else {
-      update = -g * update_scale;
+      // quantile: the step stops at the label (VW's quantileloss::getUpdate)
+      const float err = label - pred;
+      update = err == 0.f ? 0.f
+                          : (err > 0.f ? std::min(quantile_tau_ * update_scale, err / ppu)
+                                       : std::max(-(1.f - quantile_tau_) * update_scale, err / ppu));
     }
   } else {
     update = -g * update_scale;

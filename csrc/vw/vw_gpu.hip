@@ -219,16 +219,24 @@ __device__ float UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint6
   if (!a.adaptive) eta *= pow(static_cast<double>(a.initial_t) + t, -static_cast<double>(a.power_t));
   const float us = static_cast<float>(eta) * imp;
   float update;
-  if (a.invariant && a.loss <= 1) {
+  if (a.invariant) {
     const float pp = fmaxf(pr.ppu, FLT_MIN);
     if (a.loss == 0) {
       update = us * pp < 1e-6f ? 2.f * (y - raw) * us : (y - raw) * (1.f - expf(-2.f * us * pp)) / pp;
-    } else {
+    } else if (a.loss == 1) {
       const float step = y * us / (1.f + expf(y * raw));
       update = fabsf(step * pp) > 50.f ? copysignf(50.f / pp, step) : step;
+    } else if (a.loss == 2) {
+      // hinge: the step stops at the margin (VW's hingeloss::getUpdate)
+      const float err = 1.f - y * raw;
+      update = err <= 0.f ? 0.f : y * fminf(us, err / pp);
+    } else {
+      // quantile: the step stops at the label (VW's quantileloss::getUpdate)
+      const float err = y - raw;
+      update = err == 0.f ? 0.f : (err > 0.f ? fminf(a.tau * us, err / pp) : fmaxf(-(1.f - a.tau) * us, err / pp));
     }
   } else {
-    update = -pr.g * us;  // hinge / quantile (and non-invariant updates): the plain gradient step
+    update = -pr.g * us;  // the plain gradient step
   }
   const float decay = static_cast<float>(eta) * a.l2;
   const float shrink = static_cast<float>(eta) * a.l1;

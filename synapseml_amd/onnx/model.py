@@ -241,7 +241,25 @@ class ONNXModel(Transformer):
         return get_session(self.getModelPayload(), outputs, _device_for(self.getDeviceType()),
                            self.getPrecision(), self.getOptimizationLevel())
 
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_graph", None)  # parsed lazily from the payload again (tasks receive the payload, not the graph)
+        return st
+
+    def _fan_out(self, df: DataFrame) -> Optional[DataFrame]:
+        """Partition-parallel transform over the visible MI355Xs (one task per device, ONNXModel.scala:242-251);
+        None when one task does it all."""
+        from ..parallel import runtime as R
+        from ..utils.cluster import _device_count
+
+        use_gpu = (self.getDeviceType() or "").upper() != "CPU" and _device_count() > 0
+        nt = R.transform_tasks(df, use_gpu)
+        return R.fan_out_transform(self, df, nt, use_gpu) if nt > 1 else None
+
     def _transform(self, df: DataFrame) -> DataFrame:
+        fanned = self._fan_out(df)
+        if fanned is not None:
+            return fanned
         self._validate(df)
         fetch = dict(self.getFetchDict() or {})
         requested = sorted(fetch.values())
@@ -533,8 +551,14 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
 
     def _transform(self, df: DataFrame) -> DataFrame:
         from ..core.utils import find_unused_column_name
+        from ..parallel import runtime as R
+        from ..utils.cluster import _device_count
 
         model = self.getOnnxModel()
+        use_gpu = (model.getDeviceType() or "").upper() != "CPU" and _device_count() > 0
+        nt = R.transform_tasks(df, use_gpu)
+        if nt > 1:  # one task per MI355X, as the reference's per-partition sessions
+            return R.fan_out_transform(self, df, nt, use_gpu)
         out_name = self.getFeatureTensorName() if self.getHeadless() else self.getOutputTensorName()
         if not out_name:
             raise ValueError("featureTensorName / outputTensorName must be set")

@@ -24,10 +24,12 @@ F32_MODES = {"exact": 0, "bf16x3": 3, "bf16x6": 4}
 def f32_mode_default() -> str:
     import os
 
-    # bf16x6 by default: its error against an fp64 convolution measured at or below the exact f32 MFMA's
-    # (0.2-1.0e-6 vs 0.3-1.4e-6 of max |y| on four ResNet shapes) and ResNet-50 fp32 runs 4 % faster;
-    # bf16x3 (~3e-6) is the fast opt-in (+60 %: 11.9k -> 18.3k img/s at batch 128; profiles/r3/conv_f32_modes)
-    m = os.environ.get("SML_CONV_F32", "bf16x6")
+    # bf16x3 by default: ~16 significant bits per product, 2.9-4.3e-6 of max |y| against an fp64 convolution
+    # and gated at <= 1e-5 on all 14 ResNet-50 layer shapes (tests/test_conv_mfma.py) - two orders of magnitude
+    # tighter than TF32 (11 bits, ~1e-3), the fp32 conv math ORT's CUDA provider uses on tensor cores - at
+    # +60 % ResNet-50 fp32 throughput over bf16x6 (11.9k -> 18.3k img/s at batch 128, profiles/r3/
+    # conv_f32_modes). bf16x6 (error at the exact f32 MFMA's level) and exact stay selectable.
+    m = os.environ.get("SML_CONV_F32", "bf16x3")
     if m not in F32_MODES:
         raise ValueError(f"SML_CONV_F32={m!r}: expected one of {sorted(F32_MODES)}")
     return m

@@ -214,19 +214,24 @@ def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, par
             os._exit(18)  # dies while the other ranks wait in collectives
         if fault == "empty":
             part = part.slice(0, 0)
-        result = ("ok", fn(part, rank, world))
+        # serialised while the partition is still mapped: a result may view the shared-memory columns (a
+        # transformed partition keeps its input columns), and numpy views do not pin the mapping - closing it
+        # first left them dangling (the pickling then read unmapped memory)
+        payload = pickle.dumps(("ok", fn(part, rank, world)))
         del part
         dist.barrier()
         dist.destroy_process_group()
         if shm is not None:
             try:
                 shm.close()
-            except BufferError:  # a result still views the partition: the mapping goes with the process
+            except BufferError:
                 pass
     except BaseException as e:  # noqa: BLE001 - report to the driver
-        result = ("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}")
-    with open(os.path.join(out_dir, f"result_{rank}.pkl"), "wb") as f:
-        pickle.dump(result, f)
+        payload = pickle.dumps(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+    tmp = os.path.join(out_dir, f"result_{rank}.pkl.tmp")
+    with open(tmp, "wb") as f:
+        f.write(payload)
+    os.replace(tmp, os.path.join(out_dir, f"result_{rank}.pkl"))  # the driver never sees a partial file
 
 
 def _init_timeout():
@@ -352,6 +357,12 @@ def _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, tim
             if p.is_alive():
                 p.kill()
                 p.join()
+    if failed is None:
+        # every worker had exited by the last poll: a crash after its result file (or a missing file) is a failure
+        for r, p in enumerate(procs):
+            if p.exitcode != 0 or not os.path.exists(os.path.join(d, f"result_{r}.pkl")):
+                failed = (r, f"exit code {p.exitcode}")
+                break
     if failed is not None and failed[1] == "netinit":
         with open(os.path.join(d, f"result_{failed[0]}.pkl"), "rb") as f:
             msg = pickle.load(f)[1]  # written by our own worker process
@@ -459,6 +470,29 @@ def fan_out(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_tasks: 
             backend = backend or "gloo"
             env.setdefault("SML_GBDT_SHARED_DEVICE", "1")
     return run_partitions(fn, df, num_workers=num_tasks, backend=backend, use_gpu=use_gpu, env=env, **kw)
+
+
+class _TransformTask:
+    def __init__(self, transformer):
+        self.transformer = transformer
+
+    def __call__(self, part: DataFrame, rank: int, world: int):
+        return self.transformer.transform(part)
+
+
+def transform_tasks(df: DataFrame, use_gpu: bool) -> int:
+    """Partition tasks of a model's transform (ONNXModel.scala:242-251 maps the partitions, each task on its
+    executor's device): min(executor tasks, partitions); 1 inside a task."""
+    if in_partition_task():
+        return 1
+    return max(1, min(executor_tasks(use_gpu), df.getNumPartitions()))
+
+
+def fan_out_transform(transformer, df: DataFrame, num_tasks: int, use_gpu: bool) -> DataFrame:
+    """``transformer.transform`` of every partition in its own task (one MI355X each), the results
+    concatenated in partition order."""
+    parts = fan_out(_TransformTask(transformer), df, num_tasks, use_gpu)
+    return DataFrame.union_all(parts, keep_partitions=True)
 
 
 def distributed_fit(estimator, df: DataFrame, num_workers: Optional[int] = None, use_gpu: bool = False,

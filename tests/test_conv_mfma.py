@@ -380,3 +380,30 @@ def test_stem_kernel_matches_reference(dtype, geom):
         xa = (torch.relu(xa) if in_relu else xa).to(dtype).float()
         r3 = F.conv2d(xa, wf.float(), bias, st, pd)
         torch.testing.assert_close(y3.float(), r3, rtol=tol, atol=tol)
+
+
+_RESNET50_SHAPES = [  # C, H, Cout, k, stride (tools/bench_conv.py SHAPES: the 14 bottleneck layer shapes)
+    (64, 56, 64, 1, 1), (64, 56, 64, 3, 1), (64, 56, 256, 1, 1), (256, 56, 64, 1, 1),
+    (128, 28, 128, 3, 1), (128, 28, 512, 1, 1), (512, 28, 128, 1, 1), (256, 56, 512, 1, 2),
+    (256, 14, 256, 3, 1), (256, 14, 1024, 1, 1), (1024, 14, 256, 1, 1),
+    (512, 7, 512, 3, 1), (512, 7, 2048, 1, 1), (2048, 7, 512, 1, 1),
+]
+
+
+@pytest.mark.parametrize("shape", _RESNET50_SHAPES)
+def test_fp32_default_mode_error_gate_resnet50(shape):
+    """The default fp32 conv mode (bf16x3 unless SML_CONV_F32 says otherwise) stays within 1e-5 of max |y| of
+    an fp64 convolution on every ResNet-50 layer shape (TF32 would be ~1e-3)."""
+    from synapseml_amd.ops.conv import conv2d_nhwc, f32_mode_default, pack_weight
+
+    C, H, Co, k, st = shape
+    torch.manual_seed(sum(shape))
+    x = torch.randn(2, C, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5
+    bias = torch.randn(Co, device="cuda")
+    pd = k // 2
+    ref = torch.relu(F.conv2d(x.cpu().double(), w.cpu().double(), bias.cpu().double(), st, pd))
+    y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), bias=bias, relu=True)
+    err = float((y.cpu().double() - ref).abs().max()) / float(ref.abs().max())
+    print(f1 := f"{f32_mode_default()} {shape}: max |err| / max |y| = {err:.2e}")
+    assert err <= 1e-5, f1

@@ -504,3 +504,17 @@ def test_n_ranks_give_the_1_rank_model_bitwise(est_cls, extra):
         df = DataFrame({"features": X, "label": y}, num_partitions=world)
         txt = run_partitions(_ModelText(est_cls(referenceDataset=ref, **kw)), df, num_workers=world)[0]
         assert txt == one, f"world {world} model differs from the 1-rank model"
+
+
+def _return_partition(part, rank, world):
+    return part.withColumn("twice", np.asarray(part["id"]) * 2)
+
+
+def test_worker_result_may_view_the_shared_partition():
+    """A task result that keeps the partition's shared-memory columns (a transformed partition) is serialised
+    before the worker unmaps the segment (it used to read unmapped memory and die after an empty result file,
+    which the driver then reported as an unpickling error)."""
+    df = DataFrame({"features": np.ones((60, 4), np.float32), "id": np.arange(60.0)}, num_partitions=3)
+    res = run_partitions(_return_partition, df, num_workers=2)
+    assert [r.count() for r in res] == [20, 40]
+    assert np.concatenate([r["twice"] for r in res]).tolist() == (np.arange(60.0) * 2).tolist()

@@ -288,3 +288,63 @@ def test_pack_decoded_mixed_batch():
     assert shapes[6] == (12, 8, 1)
     with pytest.raises(Exception):
         pack_decoded([b"garbage"], ignore_errors=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [1, 3, 4])
+def test_gpu_stage_pipeline_matches_host(c):
+    """Every image-output stage list runs on the device (batched K20 launches on resident images) and is
+    bit-identical to the host path (deviceType="cpu"): odd widths (row tails not a multiple of 4 bytes),
+    1 / 3 / 4 channels, keepAspectRatio resize, reflected large blur / gaussian windows, threshold types,
+    all flip codes, colour conversion and toTensor after the stages."""
+    from synapseml_amd.image import ImageTransformer
+    from synapseml_amd.image.schema import make_image_row
+
+    rng = np.random.default_rng(11)
+    imgs = [rng.integers(0, 256, (37, 53, c), dtype=np.uint8) for _ in range(5)] + \
+           [rng.integers(0, 256, (64, 48, c), dtype=np.uint8) for _ in range(3)]
+    df = DataFrame({"image": [make_image_row(a, f"o{i}") for i, a in enumerate(imgs)]})
+    conv = {1: 8, 3: 6, 4: 3}[c]  # GRAY2BGR / BGR2GRAY / BGRA2BGR
+    lists = [
+        lambda t: t.resize(height=29, width=31).centerCrop(17, 19).flip(1),
+        lambda t: t.resize(size=40, keep_aspect_ratio=True).crop(3, 2, 21, 23).flip(0),
+        lambda t: t.blur(9, 5).threshold(100.7, 250, 1).flip(-1),
+        lambda t: t.gaussianKernel(9, 2.1).threshold(90, 200, 4),
+        lambda t: t.colorFormat(conv).resize(height=22, width=27),
+        lambda t: t.resize(height=30, width=30).blur(3, 3).normalize([0.5] * (3 if c != 1 else 1),
+                                                                     [0.25] * (3 if c != 1 else 1), 1 / 255.0),
+    ]
+    for build in lists:
+        g = build(ImageTransformer(inputCol="image", outputCol="o", deviceType="gpu")).transform(df)["o"]
+        h = build(ImageTransformer(inputCol="image", outputCol="o", deviceType="cpu")).transform(df)["o"]
+        for x, y in zip(g, h):
+            if isinstance(x, dict):
+                assert (x["height"], x["width"], x["nChannels"]) == (y["height"], y["width"], y["nChannels"])
+                assert x["data"] == y["data"] and x["origin"] == y["origin"]
+            else:
+                np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+
+
+@pytest.mark.gpu
+def test_gpu_stage_kernels_reflect_and_tails():
+    """The K20 kernels on shapes that stress their tables: blur / gaussian windows larger than the image
+    (repeated BORDER_REFLECT_101), 1-pixel images, row lengths with 1-3 byte tails."""
+    import torch
+
+    img = native.load("_image")
+    rng = np.random.default_rng(7)
+    stream = torch.cuda.current_stream().cuda_stream
+    for (h, w, c) in [(1, 1, 3), (2, 3, 1), (5, 7, 3), (9, 2, 4)]:
+        a = rng.integers(0, 256, (2, h, w, c), dtype=np.uint8)
+        src = torch.from_numpy(a).cuda()
+        bl = torch.empty_like(src)
+        img.box_blur_batch_device(src.data_ptr(), 2, h, w, c, bl.data_ptr(), 11, 7, stream)
+        np.testing.assert_array_equal(bl.cpu().numpy(), np.stack([img.box_blur(x, 11, 7).reshape(h, w, c) for x in a]))
+        k = img.gaussian_kernel(13, 3.0)
+        gs = torch.empty_like(src)
+        img.column_filter_batch_device(src.data_ptr(), 2, h, w, c, gs.data_ptr(), k, stream)
+        np.testing.assert_array_equal(gs.cpu().numpy(),
+                                      np.stack([img.column_filter(x, k).reshape(h, w, c) for x in a]))
+        rs = torch.empty((2, 3, 5, c), dtype=torch.uint8, device="cuda")
+        img.resize_batch_device(src.data_ptr(), 2, h, w, c, rs.data_ptr(), 3, 5, stream)
+        np.testing.assert_array_equal(rs.cpu().numpy(), np.stack([img.resize(x, 3, 5).reshape(3, 5, c) for x in a]))

@@ -621,3 +621,25 @@ def test_stem_weight_packing_order():
     lay = wk7.reshape(2, 8, 24)
     assert torch.all(lay[:, :7, 21:] == 0) and torch.all(lay[:, 7:] == 0)
     assert int((wk7 != 0).sum()) == w7.numel()
+
+
+def test_onnx_model_transform_fans_out_over_partitions(monkeypatch):
+    """ONNXModel.transform maps the partitions, one task per executor (ONNXModel.scala:242-251): with two
+    executor tasks a 3-partition DataFrame is transformed in 2 processes, rows in order, same outputs."""
+    data, coef, inter = _iris_model()
+    rng = np.random.default_rng(3)
+    feats = rng.normal(4, 2, (60, 4)).astype(np.float32)
+    df = DataFrame({"features": feats, "id": np.arange(60.0)}, num_partitions=3)
+    m = (ONNXModel().setModelPayload(data).setFeedDict({"float_input": "features"})
+         .setFetchDict({"prediction": "output_label"}).setDeviceType("CPU"))
+    single = m.transform(df)
+    from synapseml_amd.parallel import runtime as R
+
+    monkeypatch.setenv("SML_EXECUTOR_TASKS", "2")
+    calls = []
+    real = R.fan_out_transform
+    monkeypatch.setattr(R, "fan_out_transform", lambda *a, **k: calls.append(a[2]) or real(*a, **k))
+    out = m.transform(df)
+    assert calls == [2]
+    assert out["id"].tolist() == list(range(60))
+    assert out["prediction"].tolist() == single["prediction"].tolist() == (feats @ coef.T + inter).argmax(1).tolist()

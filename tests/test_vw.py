@@ -610,3 +610,18 @@ def test_model_cache_is_keyed_on_the_model_object():
     p2 = m.transform(df)["prediction"]
     np.testing.assert_allclose(p2, m2.transform(df)["prediction"])
     assert not np.allclose(p1, p2)
+
+
+@pytest.mark.parametrize("loss,label", [("hinge", 1.0), ("quantile", 3.0)])
+def test_invariant_update_does_not_overshoot(loss, label):
+    """Importance-invariant updates for hinge / quantile (VW's getUpdate): one example with a huge importance
+    weight moves the prediction up to the margin / the label, never past it (the plain gradient step of
+    earlier builds overshot by orders of magnitude)."""
+    from synapseml_amd.vw import VowpalWabbitRegressor
+
+    X = np.array([[1.0, 0.5, -0.25]])
+    df = DataFrame({"features": X, "label": np.array([label]), "w": np.array([1e4])})
+    m = VowpalWabbitRegressor(passThroughArgs=f"--loss_function {loss}", weightCol="w").fit(df)
+    p = float(m.transform(df)["prediction"][0])
+    bound = 1.0 if loss == "hinge" else label
+    assert 0.0 < p <= bound * (1 + 1e-4), p

@@ -1,14 +1,14 @@
 #!/bin/bash
 # Round-5 pass 2: PMC counters of the GBDT root pass and batched histogram / partition kernels (one rocprofv3
 # run per counter set, kernel trace only), 20-iteration fits.
-OUT=${1:-gpurun_out/r5p2}
+OUT=${1:-gpurun_out/r5p7}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 GB="python3 bench.py --steps 1 --warmup 0 --iterations 20"
 run() {
   local name=$1; shift
-  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex 'score_grad|bhist|bpart|bplan' \
+  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex "score_grad|bhist" \
     -d "$OUT/$name" -o "$name" "$@" -- $GB > "$OUT/$name.log" 2>&1
 }
 run valu --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_WR && \
