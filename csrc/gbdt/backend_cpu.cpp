@@ -274,8 +274,8 @@ class CpuBackend : public TrainBackend {
 #pragma omp parallel for num_threads(nt) schedule(static) reduction(+ : tg, th)
     for (int64_t p = 0; p < cnt; ++p) {
       const int64_t r = idx[p];
-      const int64_t qg = static_cast<int64_t>(std::nearbyint(static_cast<double>(g[r]) * sg));
-      const int64_t qh = static_cast<int64_t>(std::nearbyint(static_cast<double>(std::max(h[r], 0.f)) * sh));
+      const int64_t qg = static_cast<int64_t>(RintFast(static_cast<double>(g[r]) * sg));
+      const int64_t qh = static_cast<int64_t>(RintFast(static_cast<double>(std::max(h[r], 0.f)) * sh));
       og[2 * p] = qg;
       og[2 * p + 1] = qh;
       tg += qg;

@@ -58,6 +58,7 @@ __constant__ int c_max_hist_blocks = kMaxHistBlocks;
 __constant__ int c_slab_wt = 1;
 // SML_PART_WT=1: partition outputs (perm, ordered g/h) written through L2 (A/B: 1.96 -> 1.99 ms/iter, slower)
 __constant__ int c_part_wt = 0;
+__constant__ int c_part_pipe = 1;  // software-pipelined batched partition (SML_PART_PIPE=0: the plain tile loop)
 
 constexpr int kPartThreads = 512;
 constexpr int kMaxPartBlocks = 2048;
@@ -2616,6 +2617,151 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   }
 }
 
+// One tile's rows in registers (the software-pipelined batched partition below keeps two).
+template <int kPartRows>
+struct PartRegs {
+  int r[kPartRows];
+  float2 v[kPartRows];
+  uint32_t bin[kPartRows];
+};
+
+// Issue the loads of a tile: row ids + (g, h) (physical or ordered), then the split feature's bins. Branch-free
+// as PartitionTile's (rows past the segment read its first position and are masked later).
+template <int kPartRows>
+__device__ __forceinline__ void PartLoad(PartRegs<kPartRows>& t, int feature, int t0, int tv, int pbuf,
+                                         const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
+                                         const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
+                                         const float2* __restrict__ ogh1, const float* __restrict__ g,
+                                         const float* __restrict__ h) {
+  const int tid = threadIdx.x;
+  if (pbuf < 0) {
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const int k = u * kPartThreads + tid;
+      const int p = t0 + (k < tv ? k : 0);
+      t.r[u] = p;
+      t.v[u] = make_float2(g[p], h[p]);
+    }
+  } else {
+    const int32_t* perm = pbuf == 0 ? perm0 : perm1;
+    const float2* ogh = pbuf == 0 ? ogh0 : ogh1;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const int k = u * kPartThreads + tid;
+      const int p = t0 + (k < tv ? k : 0);
+      t.r[u] = perm[p];
+      t.v[u] = ogh[p];
+    }
+  }
+  const uint8_t* __restrict__ col = cbins + static_cast<size_t>(feature) * n;
+#pragma unroll
+  for (int u = 0; u < kPartRows; ++u) t.bin[u] = col[t.r[u]];
+}
+
+// Batched partition with the tile loop software-pipelined: the next tile's row / gradient / bin loads are
+// issued before this tile claims its output ranges (the block-wide ballot count -> one returning atomic on
+// the expansion's cursor -> barrier), so their memory latency overlaps the atomic's round trip and the
+// scatter instead of following it. Output order inside a child is still the claim order (histograms are
+// exact integer sums: nothing downstream depends on it).
+template <int kPartRows>
+__device__ __forceinline__ void BatchedPartitionPipelined(
+    BState* __restrict__ bs, int nexp, int ntiles, const int* s_tile0, const int* s_pb, const int* s_pc,
+    const int* s_pbuf, const PartSplit* s_ps, const uint32_t (*s_cat)[8], const uint8_t* __restrict__ cbins, int64_t n,
+    const int32_t* __restrict__ perm0, const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
+    const float2* __restrict__ ogh1, int32_t* __restrict__ wperm0, int32_t* __restrict__ wperm1,
+    float2* __restrict__ wogh0, float2* __restrict__ wogh1, const float* __restrict__ g, const float* __restrict__ h) {
+  constexpr int kPartTile = kPartThreads * kPartRows;
+  constexpr int kWaves = kPartThreads / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ int wl[kPartRows][kWaves];
+  __shared__ int bases[2];
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  auto locate = [&](int tile, int* j, int* t0, int* tv) {
+    int q = 0;
+    while (q + 1 < nexp && s_tile0[q + 1] <= tile) ++q;
+    *j = q;
+    *t0 = s_pb[q] + (tile - s_tile0[q]) * kPartTile;
+    *tv = min(kPartTile, s_pb[q] + s_pc[q] - *t0);
+  };
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  PartRegs<kPartRows> cur, nxt;
+  int j, t0, tv;
+  locate(tile, &j, &t0, &tv);
+  PartLoad<kPartRows>(cur, s_ps[j].feature, t0, tv, s_pbuf[j], cbins, n, perm0, perm1, ogh0, ogh1, g, h);
+  for (;;) {
+    const PartSplit ps = s_ps[j];
+    int rl[kPartRows];
+    unsigned lmask = 0;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const int k = u * kPartThreads + tid;
+      const bool left = k < tv && DeviceGoesLeft(cur.bin[u], ps.nb, ps.mt, ps.dbin, ps.is_cat, ps.thr, ps.dleft, s_cat[j]);
+      lmask |= left ? (1u << u) : 0u;
+      const unsigned long long bl = __ballot(left);
+      rl[u] = __popcll(bl & below);
+      if (lane == 0) wl[u][wid] = __popcll(bl);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int tl = 0;
+      for (int u = 0; u < kPartRows; ++u)
+        for (int w = 0; w < kWaves; ++w) tl += wl[u][w];
+      const int tr = tv - tl;
+      const unsigned long long old = atomicAdd(&bs->cursor[j], static_cast<unsigned long long>(tl) |
+                                                                   (static_cast<unsigned long long>(tr) << 32));
+      bases[0] = s_pb[j] + static_cast<int>(old & 0xFFFFFFFFull);
+      bases[1] = s_pb[j] + s_pc[j] - static_cast<int>(old >> 32) - tr;
+    }
+    // the next tile's loads go out while thread 0's atomic is in flight
+    const int ntile = tile + static_cast<int>(gridDim.x);
+    int nj = j, nt0 = 0, ntv = 0;
+    if (ntile < ntiles) {
+      locate(ntile, &nj, &nt0, &ntv);
+      PartLoad<kPartRows>(nxt, s_ps[nj].feature, nt0, ntv, s_pbuf[nj], cbins, n, perm0, perm1, ogh0, ogh1, g, h);
+    }
+    __syncthreads();
+    const int lb = bases[0], rb = bases[1];
+    const int pbuf = s_pbuf[j];
+    int32_t* operm = pbuf == 0 ? wperm1 : wperm0;
+    float2* oogh = pbuf == 0 ? wogh1 : wogh0;
+    int run = 0;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      int wb = 0, ut = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const int c = wl[u][w];
+        wb += w < wid ? c : 0;
+        ut += c;
+      }
+      const int k = u * kPartThreads + tid;
+      if (k < tv) {
+        const int lbefore = run + wb + rl[u];
+        const int dst = (lmask >> u) & 1u ? lb + lbefore : rb + (k - lbefore);
+        if (c_part_wt) {
+          __hip_atomic_store(operm + dst, cur.r[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(oogh + dst),
+                             (static_cast<unsigned long long>(__float_as_uint(cur.v[u].y)) << 32) |
+                                 __float_as_uint(cur.v[u].x),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          operm[dst] = cur.r[u];
+          oogh[dst] = cur.v[u];
+        }
+      }
+      run += ut;
+    }
+    if (ntile >= ntiles) break;
+    __syncthreads();  // wl / bases are rewritten by the next tile
+    tile = ntile;
+    j = nj;
+    t0 = nt0;
+    tv = ntv;
+    cur = nxt;
+  }
+}
+
 template <int kPartRows>
 __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
     BState* __restrict__ bs, const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
@@ -2638,6 +2784,11 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   }
   if (tid < nexp * 8) s_cat[tid >> 3][tid & 7] = bs->exp[tid >> 3].cat[tid & 7];
   __syncthreads();
+  if (c_part_pipe) {
+    BatchedPartitionPipelined<kPartRows>(bs, nexp, ntiles, s_tile0, s_pb, s_pc, s_pbuf, s_ps, s_cat, cbins, n, perm0,
+                                         perm1, ogh0, ogh1, wperm0, wperm1, wogh0, wogh1, g, h);
+    return;
+  }
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     int j = 0;
     while (j + 1 < nexp && s_tile0[j + 1] <= tile) ++j;
@@ -3154,6 +3305,10 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_PART_WT")) {
       const int v = std::atoi(e) != 0 ? 1 : 0;
       SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_part_wt), &v, sizeof(int)));
+    }
+    if (const char* e = std::getenv("SML_PART_PIPE")) {
+      const int v = std::atoi(e) != 0 ? 1 : 0;
+      SML_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_part_pipe), &v, sizeof(int)));
     }
     if (const char* e = std::getenv("SML_SLAB_WT")) {
       const int v = std::atoi(e) != 0 ? 1 : 0;

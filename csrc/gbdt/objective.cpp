@@ -218,8 +218,8 @@ static void GlobalSums(int64_t n, Y y, W w, Comm* comm, double* sum_yw, double* 
   int64_t a = 0, b = 0;
 #pragma omp parallel for schedule(static) reduction(+ : a, b)
   for (int64_t i = 0; i < n; ++i) {
-    a += static_cast<int64_t>(std::nearbyint(y(i) * w(i) * s0));
-    b += static_cast<int64_t>(std::nearbyint(w(i) * s1));
+    a += static_cast<int64_t>(RintFast(y(i) * w(i) * s0));
+    b += static_cast<int64_t>(RintFast(w(i) * s1));
   }
   q[0] = a;
   q[1] = b;

@@ -14,6 +14,17 @@
 
 namespace sml {
 
+// Round half to even (the default FP rounding mode, what rint / nearbyint return) without a libm call:
+// |x| + 2^52 lands where doubles are spaced 1 apart, so the FPU's addition rounds it (SSE2 double; the pair is
+// not folded without -ffast-math); |x| >= 2^52 is integral already. Used where a quantised value per row is
+// computed on the host (fixed-point histograms and label sums).
+inline double RintFast(double x) {
+  constexpr double kTwo52 = 4503599627370496.0;
+  const double a = std::fabs(x);
+  if (!(a < kTwo52)) return x;  // integral already (or nan / inf)
+  return std::copysign((a + kTwo52) - kTwo52, x);
+}
+
 constexpr double kEpsilon = 1e-15;
 
 struct SplitParams {

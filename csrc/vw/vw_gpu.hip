@@ -18,9 +18,11 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "vw_gpu.h"
+#include "../gbdt/hip_common.h"  // sml::DevPoolAlloc / DevPoolFree: the process-wide caching device allocator
 
 #define VW_HIP_CHECK(e)                                                                          \
   do {                                                                                           \
@@ -30,6 +32,41 @@
 
 namespace smlvw {
 namespace {
+
+// The learner's large buffers (the 2^bits weight table - 16 GiB at b=30 -, the staged example rows and the
+// featurization's temporary blocks) come from the caching pool: a fit frees them at its end and the next fit
+// of the same shape gets them back without a hipMalloc / hipFree of gigabytes (the table is still zeroed per
+// learner). Small buffers stay on plain hipMalloc.
+std::mutex g_pool_mu;
+std::unordered_map<void*, size_t> g_pool_granted;
+
+template <class T>
+void PoolMalloc(T** p, size_t bytes) {
+  size_t granted = 0;
+  void* q = sml::DevPoolAlloc(std::max<size_t>(bytes, 16), &granted);
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool_granted[q] = granted;
+  }
+  *p = static_cast<T*>(q);
+}
+
+void PoolFree(void* p) {
+  if (!p) return;
+  size_t granted = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool_granted.find(p);
+    if (it == g_pool_granted.end()) {
+      (void)hipFree(p);
+      return;
+    }
+    granted = it->second;
+    g_pool_granted.erase(it);
+  }
+  sml::DevPoolFree(p, granted);
+}
+
 
 constexpr int kWavesPerBlock = 4;
 
@@ -908,19 +945,19 @@ struct GpuSgd::Impl {
     if (rows > cap_rows) {
       for (void* q : {static_cast<void*>(indptr), static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo),
                       static_cast<void*>(hi), static_cast<void*>(pred)})
-        (void)hipFree(q);
-      VW_HIP_CHECK(hipMalloc(&indptr, (rows + 1) * sizeof(int64_t)));
-      VW_HIP_CHECK(hipMalloc(&lab, rows * sizeof(float)));
-      VW_HIP_CHECK(hipMalloc(&wt, rows * sizeof(float)));
-      VW_HIP_CHECK(hipMalloc(&lo, rows * sizeof(float)));
-      VW_HIP_CHECK(hipMalloc(&hi, rows * sizeof(float)));
-      VW_HIP_CHECK(hipMalloc(&pred, rows * sizeof(float)));
+        PoolFree(q);
+      PoolMalloc(&indptr, (rows + 1) * sizeof(int64_t));
+      PoolMalloc(&lab, rows * sizeof(float));
+      PoolMalloc(&wt, rows * sizeof(float));
+      PoolMalloc(&lo, rows * sizeof(float));
+      PoolMalloc(&hi, rows * sizeof(float));
+      PoolMalloc(&pred, rows * sizeof(float));
       cap_rows = rows;
     }
     if (nnz > cap_nnz) {
-      (void)hipFree(idx); (void)hipFree(val);
-      VW_HIP_CHECK(hipMalloc(&idx, std::max<size_t>(1, nnz) * sizeof(uint32_t)));
-      VW_HIP_CHECK(hipMalloc(&val, std::max<size_t>(1, nnz) * sizeof(float)));
+      PoolFree(idx); PoolFree(val);
+      PoolMalloc(&idx, std::max<size_t>(1, nnz) * sizeof(uint32_t));
+      PoolMalloc(&val, std::max<size_t>(1, nnz) * sizeof(float));
       cap_nnz = nnz;
     }
   }
@@ -934,10 +971,11 @@ struct GpuSgd::Impl {
                     static_cast<void*>(cbprob), static_cast<void*>(best), static_cast<void*>(cbstats),
                     static_cast<void*>(spec)})
       (void)hipFree(q);
-    for (void* q : {static_cast<void*>(W), static_cast<void*>(dirty), static_cast<void*>(gs),
-                    static_cast<void*>(indptr), static_cast<void*>(idx), static_cast<void*>(val),
+    for (void* q : {static_cast<void*>(W), static_cast<void*>(indptr), static_cast<void*>(idx), static_cast<void*>(val),
                     static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo), static_cast<void*>(hi),
-                    static_cast<void*>(pred), static_cast<void*>(loss), static_cast<void*>(pos),
+                    static_cast<void*>(pred)})
+      PoolFree(q);
+    for (void* q : {static_cast<void*>(dirty), static_cast<void*>(gs), static_cast<void*>(loss), static_cast<void*>(pos),
                     static_cast<void*>(blocks), static_cast<void*>(sums), static_cast<void*>(nmax)})
       (void)hipFree(q);
     if (stream) (void)hipStreamDestroy(stream);
@@ -988,7 +1026,7 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
   impl_->nw = 1ull << cfg.bits;
-  VW_HIP_CHECK(hipMalloc(&impl_->W, impl_->nw * sizeof(float4)));
+  PoolMalloc(&impl_->W, impl_->nw * sizeof(float4));
   VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), impl_->stream));
   impl_->nblk = static_cast<int64_t>((impl_->nw + (1ull << kDirtyShift) - 1) >> kDirtyShift);
   VW_HIP_CHECK(hipMalloc(&impl_->dirty, impl_->nblk));
@@ -1227,7 +1265,7 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
   std::vector<void*> tmp;
   auto dev_alloc = [&](size_t bytes) -> void* {  // freed at the end of the staging
     void* d = nullptr;
-    VW_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 8)));
+    PoolMalloc(&d, std::max<size_t>(bytes, 8));
     tmp.push_back(d);
     return d;
   };
@@ -1284,10 +1322,10 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
   } catch (...) {
     (void)hipStreamSynchronize(s);
     (void)hipStreamSynchronize(cs);
-    for (void* q : tmp) (void)hipFree(q);
+    for (void* q : tmp) PoolFree(q);
     throw;
   }
-  for (void* q : tmp) (void)hipFree(q);
+  for (void* q : tmp) PoolFree(q);
   staged_rows_ = n;
 }
 

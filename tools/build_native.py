@@ -66,7 +66,7 @@ MODULES = {
     ),
     "_vw": (
         "csrc/vw",
-        ["vw_core.cpp", "vw_bindings.cpp", "vw_gpu.hip"],
+        ["vw_core.cpp", "vw_bindings.cpp", "vw_gpu.hip", "../gbdt/dev_pool.cpp"],
         ["-lrccl"],
     ),
     "_image": (

@@ -40,6 +40,8 @@ def main():
         out["us_per_allreduce_8KB"] = g.comm_device_allreduce_us(c, 1024, 200)
         # one round of the batched tree growth: 8 expansions x (histogram + count) = 8 x 114 KB
         out["us_per_allreduce_917KB"] = g.comm_device_allreduce_us(c, 8 * (28 * 256 + 1) * 2, 100)
+        # the default batched round: 4 expansions x (E + 1) int64 (g, h) pairs, E = 28 x 256 -> 459 KB
+        out["us_per_allreduce_459KB_round"] = g.comm_device_allreduce_us(c, 4 * (28 * 256 + 1) * 2, 100)
         # data-parallel training over P2P vs host comm: identical models
         rng = np.random.default_rng(7 + r)
         X = rng.standard_normal((40000, 8))
