@@ -753,14 +753,14 @@ __global__ __launch_bounds__(64 * kCbWaves) void cb_kernel(SgdArgs a, CbArgs cb)
 // float w * G underflows (and is flushed) for slots with a tiny gradient mass, which would zero their
 // weight on the average even at world 1.
 __global__ void pack_kernel(const float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk,
-                            uint64_t nw, int adaptive, double* __restrict__ sums, float* __restrict__ nmax) {
+                            uint64_t nw, int adaptive, float* __restrict__ sums, float* __restrict__ nmax) {
   constexpr int64_t B = int64_t(1) << kDirtyShift;
   const int64_t m = nblk * B;
   for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < m;
        j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
     const float4 v = slot < nw ? W[slot] : make_float4(0.f, 0.f, 0.f, 0.f);
-    sums[2 * j] = adaptive ? static_cast<double>(v.x) * v.y : static_cast<double>(v.x);
+    sums[2 * j] = adaptive ? v.x * v.y : v.x;
     sums[2 * j + 1] = v.y;
     nmax[j] = v.z;
   }
@@ -768,9 +768,10 @@ __global__ void pack_kernel(const float4* __restrict__ W, const int32_t* __restr
 
 // VW's weighted averaging: with adaptive state w = sum(w G) / sum(G) (a slot no rank has gradient mass
 // on was never updated and keeps its value), G = sum(G) / world; N = max(N); without adaptive
-// w = sum(w) / world
+// w = sum(w) / world. The sums are fp32, as VW's own allreduce of its float weight buffers (half the bytes
+// of the fp64 sums earlier builds sent).
 __global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk, uint64_t nw,
-                              int adaptive, double inv_world, const double* __restrict__ sums,
+                              int adaptive, float inv_world, const float* __restrict__ sums,
                               const float* __restrict__ nmax) {
   constexpr int64_t B = int64_t(1) << kDirtyShift;
   const int64_t m = nblk * B;
@@ -779,10 +780,10 @@ __global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict_
     const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
     if (slot >= nw) continue;
     float4 v = W[slot];
-    const double s0 = sums[2 * j], sg = sums[2 * j + 1];
-    if (!adaptive) v.x = static_cast<float>(s0 * inv_world);
-    else if (sg > 0.0) v.x = static_cast<float>(s0 / sg);
-    v.y = static_cast<float>(sg * inv_world);
+    const float s0 = sums[2 * j], sg = sums[2 * j + 1];
+    if (!adaptive) v.x = s0 * inv_world;
+    else if (sg > 0.f) v.x = s0 / sg;
+    v.y = sg * inv_world;
     v.z = nmax[j];
     W[slot] = v;
   }
@@ -938,7 +939,7 @@ struct GpuSgd::Impl {
   ExpandSpec* spec = nullptr;
   // sync scratch
   int32_t *pos = nullptr, *blocks = nullptr;
-  double* sums = nullptr;
+  float* sums = nullptr;  // per-slot (w or wG, G) sync sums, fp32 as VW's allreduce
   float* nmax = nullptr;
   size_t cap_sync = 0;
   void Reserve(size_t rows, size_t nnz) {
@@ -1509,7 +1510,7 @@ void GpuSgd::AllReduceAverage(void* comm, int world, double timeout_ms) {
     if (slots > impl_->cap_sync) {
       (void)hipFree(impl_->blocks); (void)hipFree(impl_->sums); (void)hipFree(impl_->nmax);
       VW_HIP_CHECK(hipMalloc(&impl_->blocks, nblk * sizeof(int32_t)));
-      VW_HIP_CHECK(hipMalloc(&impl_->sums, slots * 2 * sizeof(double)));
+      VW_HIP_CHECK(hipMalloc(&impl_->sums, slots * 2 * sizeof(float)));
       VW_HIP_CHECK(hipMalloc(&impl_->nmax, slots * sizeof(float)));
       impl_->cap_sync = slots;
     }
@@ -1519,12 +1520,12 @@ void GpuSgd::AllReduceAverage(void* comm, int world, double timeout_ms) {
     hipLaunchKernelGGL(pack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
                        impl_->sums, impl_->nmax);
     VW_HIP_CHECK(hipGetLastError());
-    nccl(ncclAllReduce(impl_->sums, impl_->sums, slots * 2, ncclDouble, ncclSum, c, s));
+    nccl(ncclAllReduce(impl_->sums, impl_->sums, slots * 2, ncclFloat, ncclSum, c, s));
     nccl(ncclAllReduce(impl_->nmax, impl_->nmax, slots, ncclFloat, ncclMax, c, s));
     hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
-                       1.0 / world, impl_->sums, impl_->nmax);
+                       1.0f / world, impl_->sums, impl_->nmax);
     VW_HIP_CHECK(hipGetLastError());
-    last_sync_bytes_ = static_cast<int64_t>(slots) * (2 * sizeof(double) + sizeof(float)) + nblk;
+    last_sync_bytes_ = static_cast<int64_t>(slots) * (2 * sizeof(float) + sizeof(float)) + nblk;
   }
   VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, nblk, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
