@@ -336,6 +336,28 @@ __device__ __forceinline__ void PairTermsPre(float sig, float imd, bool use_norm
   *pl_out = pl;
 }
 
+// The register path's form of PairTermsPre, branch-free: the top document i (wave-uniform si / li / gi /
+// di) against this lane's partner j. Both orientations of a difference are exact negations of one another
+// (round-to-nearest is sign-symmetric), so ds and gap take one subtraction and a sign flip; an ineligible
+// partner (same label, itself, padding lane) gets dn = 0, which zeroes all three terms (p stays finite for
+// any ds, infinities included); the two quotients are hardware reciprocals (v_rcp_f32, 1 ulp) instead of
+// IEEE divides (~11 VALU instructions each, 40 % of the pair's instructions). sl2e = sigma * log2(e).
+__device__ __forceinline__ void PairTermsFast(float sig, float sl2e, float imd, bool use_norm, bool ok, double si,
+                                              int li, float gi, float di, double sj, int lj, float gj, float dj,
+                                              float* c, float* ph_out, float* pl_out) {
+  const unsigned flip = li > lj ? 0u : 0x80000000u;  // i is the higher-labelled document: no flip
+  const float ds = __uint_as_float(__float_as_uint(static_cast<float>(si - sj)) ^ flip);
+  const float gap = __uint_as_float(__float_as_uint(gi - gj) ^ flip);
+  const float pd = fabsf(di - dj);
+  float dn = ok ? gap * pd * imd : 0.f;
+  if (use_norm) dn *= __builtin_amdgcn_rcpf(0.01f + fabsf(ds));
+  const float p = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(sl2e * ds));
+  const float pl = p * (-sig * dn);
+  *ph_out = p * (1.0f - p) * (sig * sig * dn);
+  *pl_out = pl;
+  *c = __uint_as_float(__float_as_uint(pl) ^ flip);
+}
+
 // All pairs of doc i: a doc ranked below max_position only pairs with the
 // top max_position documents (s_top, by rank), a top document with every
 // other document.
@@ -545,8 +567,12 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   for (int v = 0; v < NU; ++v) {
     if (v * 64 >= cnt) break;
     const int jn = min(64, cnt - v * 64);
+    // wave-uniform partner scores through the constant address space: s_load into SGPRs (read-only data),
+    // no v_readlane pair + hazard per partner
+    const __attribute__((address_space(4))) double* sv =
+        (const __attribute__((address_space(4))) double*)(score + b + v * 64);
     for (int jj = 0; jj < jn; ++jj) {
-      const double sj = ReadLaneD(sc[v], jj);
+      const double sj = sv[jj];
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         if (u < v) rk[u] += sj >= sup[u] ? 1 : 0;         // every j of slot v is after i
@@ -583,12 +609,17 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   }
   const float tdc = static_cast<float>(s_disc[lane]);  // discount of rank `lane` (valid for lane < ntop)
   const float sig = static_cast<float>(t.sigma);
+  const float sl2e = sig * 1.4426950408889634f;
   const float fimd = static_cast<float>(t.inv_max_dcg[q]);
   const bool use_norm = t.norm && mx != mn;
   // fp32 accumulators: a document sums at most max_position + cnt pair terms, each already fp32
-  float lam[NU], hes[NU];
+  float lam[NU], hes[NU], ntf[NU];
 #pragma unroll
-  for (int u = 0; u < NU; ++u) { lam[u] = 0.f; hes[u] = 0.f; }
+  for (int u = 0; u < NU; ++u) {
+    lam[u] = 0.f;
+    hes[u] = 0.f;
+    ntf[u] = u * 64 + lane < cnt && rk[u] >= ntop ? 1.f : 0.f;  // a non-top document mirrors its pair terms
+  }
   float suml = 0.f;
   // Top document r against every document (partners on the lanes), each pair evaluated once: the
   // top document's terms are wave-reduced, a non-top partner (which pairs with the top list only) takes
@@ -607,19 +638,18 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
     float la = 0.f, he = 0.f;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
+      // branch-free: an ineligible pair adds signed zeros (bitwise a no-op on these sums), a top partner
+      // takes no mirrored terms (ntf = 0: fma(-0, c, x) = x)
       const int j = u * 64 + lane;
-      if (j < cnt && j != di && lab[u] != li) {
-        float c, ph, pl;
-        PairTermsPre(sig, fimd, use_norm, si, li, gi, dci, sc[u], lab[u], gn[u], dc[u], &c, &ph, &pl);
-        la += c;
-        he += ph;
-        suml -= pl;
-        if (rk[u] >= ntop) {
-          lam[u] -= c;
-          hes[u] += ph;
-          suml -= pl;
-        }
-      }
+      float c, ph, pl;
+      PairTermsFast(sig, sl2e, fimd, use_norm, j < cnt && j != di && lab[u] != li, si, li, gi, dci, sc[u], lab[u],
+                    gn[u], dc[u], &c, &ph, &pl);
+      la += c;
+      he += ph;
+      suml -= pl;
+      lam[u] = fmaf(-ntf[u], c, lam[u]);
+      hes[u] = fmaf(ntf[u], ph, hes[u]);
+      suml = fmaf(-ntf[u], pl, suml);
     }
     *la_out = la;
     *he_out = he;
@@ -698,7 +728,7 @@ __device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
 // walking its own queries (a CU holds at most 16 workgroups, so one-wave blocks cap residency at 4 waves
 // per SIMD; kWaves = 4 lifts that, but measured slower - see rank_waves_).
 template <int kWaves, bool kTR = true>
-__global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
+__global__ __launch_bounds__(64 * kWaves, 4) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
                                                                       const float* __restrict__ label,
                                                                       const float* __restrict__ weight,
                                                                       float* __restrict__ g, float* __restrict__ h) {
@@ -706,7 +736,7 @@ __global__ __launch_bounds__(64 * kWaves) void lambdarank_regs_kernel(RankTables
   __shared__ int s_map[kWaves][64];
   for (int r = threadIdx.x; r < kRankLds; r += 64 * kWaves) s_disc[r] = t.disc[r];
   __syncthreads();
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform to the compiler: q, b, cnt in SGPRs
   // documents per lane sized to the query: the pair loops run NU-wide, so a 100-document query
   // costs half of what the kRankLds-wide form would
   for (int q = blockIdx.x * kWaves + wid; q < t.nq; q += gridDim.x * kWaves) {

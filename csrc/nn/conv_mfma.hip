@@ -884,16 +884,39 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
     }
   };
-  dma_tile(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) dma_tile(buf ^ 1);
-    compute(buf);
-    __builtin_amdgcn_sched_barrier(0);  // keep the tile's MFMAs ahead of the DMA wait
+  if constexpr (kNB == 3) {
+    // Three buffers, two tiles in flight across the barrier: at step kt a wave retires only its own DMAs of
+    // tile kt (counted vmcnt: the kPieces of tile kt + 1 may stay outstanding), the raw s_barrier then makes
+    // every wave's tile kt visible AND proves every wave is past compute(kt - 1), so tile kt + 2 may land in
+    // that buffer. No __syncthreads() in the loop: its fence would drain the DMA queue (vmcnt(0)).
+    constexpr int kPieces = AI + BI;
+    static_assert(!kPro, "the 3-buffer form has no prologue side buffer");
+    dma_tile(0);
+    if (nk > 1) dma_tile(1);
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kPieces) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 < nk) dma_tile(buf == 0 ? 2 : buf - 1);
+      compute(buf);
+      buf = buf == 2 ? 0 : buf + 1;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();  // the epilogue's LDS staging overwrites the operand buffers
+  } else {
+    dma_tile(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) dma_tile(buf ^ 1);
+      compute(buf);
+      __builtin_amdgcn_sched_barrier(0);  // keep the tile's MFMAs ahead of the DMA wait
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
   ConvEpilogue<T, WM, WN, kWN>(a, acc, lds, M, m0, n0, wid, lane);
 }
@@ -926,7 +949,25 @@ void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
     const char* e = std::getenv("SML_CONV_GLDS_SINGLE");
     return !e || std::atoi(e) != 0;
   }();
+  // SML_CONV_GLDS_NB=2 / 3 forces a depth; unset: three buffers only for launches of at most two blocks per CU.
+  // r5 pass 10, ResNet-50 b128 per layer: the 3-buffer form halves the resident 128x128 blocks (96 KB of
+  // LDS), which costs the many-block layers 10-40 % (occupancy hid more than the pipeline does), and wins
+  // where the grid is below two blocks per CU anyway (512 3x3 at 7x7: 52.9 -> 46.7 us; 2048 -> 512 1x1:
+  // 27.9 -> 23.1 us)
+  static const int nb = [] {
+    const char* e = std::getenv("SML_CONV_GLDS_NB");
+    return e ? std::atoi(e) : 0;
+  }();
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n;
+  }();
+  const bool deep = nb == 3 || (nb == 0 && blocks <= 2 * ncu);
   if (a.in_scale) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, true>), dim3(blocks), dim3(kThr), 0, st, a);
+  else if (deep && a.R * a.S * a.C >= 3 * 64)  // two K tiles in flight across the barrier
+    hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 3>), dim3(blocks), dim3(kThr), 0, st, a);
   else if (single && a.R * a.S * a.C == 64)  // one K tile: no second buffer to fill (SML_CONV_GLDS_SINGLE=0: off)
     hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 1>), dim3(blocks), dim3(kThr), 0, st, a);
   else hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);

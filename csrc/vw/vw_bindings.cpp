@@ -494,7 +494,7 @@ PYBIND11_MODULE(_vw, m) {
       // (namespace group ids, c = -1 for pairs), row_map (n int64) for level-1 blocks
       .def("stage_plan",
            [](GpuSgd& g, py::list blocks, int ngroups, py::list inter, bool constant, py::object row_map, int64_t n,
-              py::object labels, py::object weights) {
+              py::object labels, py::object weights, int64_t learn_r1, int batch) {
              FeatPlan plan;
              std::vector<I64> keep_i;
              std::vector<U32> keep_u;
@@ -539,10 +539,12 @@ PYBIND11_MODULE(_vw, m) {
              std::vector<float> zeros;
              if (labels.is_none()) zeros.assign(static_cast<size_t>(std::max<int64_t>(0, n)), 0.f);
              py::gil_scoped_release rel;
-             g.StagePlan(plan, n, labels.is_none() ? zeros.data() : lab.data(), weights.is_none() ? nullptr : w.data());
+             g.StagePlan(plan, n, labels.is_none() ? zeros.data() : lab.data(), weights.is_none() ? nullptr : w.data(),
+                         learn_r1, batch);
            },
            py::arg("blocks"), py::arg("ngroups"), py::arg("interactions"), py::arg("constant"), py::arg("row_map"),
-           py::arg("n"), py::arg("labels") = py::none(), py::arg("weights") = py::none())
+           py::arg("n"), py::arg("labels") = py::none(), py::arg("weights") = py::none(), py::arg("learn_r1") = 0,
+           py::arg("batch") = 1)
       .def("stage_costs",
            [](GpuSgd& g, I64 cptr, py::array_t<int32_t, py::array::c_style | py::array::forcecast> cls, F32 cost) {
              const int64_t n = cptr.size() - 1;

@@ -69,7 +69,11 @@ class GpuSgd {
   // Device featurization: the plan's namespace blocks -> the staged example CSR (interactions and the
   // constant expanded on the device). Then optionally the per-example label extras of the reductions:
   // csoaa (class, cost) lists, or the CB multi-line structure (rows of the plan = action rows).
-  void StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights);
+  // learn_r1 > 0: rows [0, learn_r1) are also learned (batch examples per launch) while the pass stages -
+  // the blocks go up in chunks on the copy stream and each chunk is expanded and learned as soon as it has
+  // landed (LearnStaged(0, learn_r1, batch) after a plain StagePlan, without the serial upload before it)
+  void StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights, int64_t learn_r1 = 0,
+                 int batch = 1);
   void StageCosts(const int64_t* cptr, const int32_t* cls, const float* cost, int64_t n);
   void StageCb(const int64_t* aip, const int32_t* chosen, const float* cost, const float* prob, int64_t n_examples);
   // predictions of every staged row (scalar: clamped score; oaa / csoaa: 1-based class; cb: action scores,
@@ -111,7 +115,10 @@ class GpuSgd {
   bool staged_weights_ = false;
   bool staged_costs_ = false;
   int64_t max_actions_ = 0;
-  void ExpandToStage(const FeatPlan& plan, int64_t n);
+  void ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1 = 0, int batch = 1);
+  // per-row clamp bounds + loss reset before learning rows [r0, r1); loss read-back (and predictions) after
+  void PrepLearn(int64_t r0, int64_t r1);
+  void FinishLearn(int64_t r0, int64_t r1, float* preds_out);
 };
 
 bool VwGpuAvailable();

@@ -554,14 +554,15 @@ __device__ __forceinline__ void GroupFeat(const ExpandSpec& s, const RowExt& e, 
   *x = 0.f;
 }
 
-__global__ __launch_bounds__(64 * kExpandWaves) void expand_fill_kernel(const ExpandSpec* __restrict__ sp, int64_t n,
-                                                                         const int64_t* __restrict__ indptr,
+// rows [r0, r1) (the staging pipeline fills the pass chunk by chunk as its blocks arrive)
+__global__ __launch_bounds__(64 * kExpandWaves) void expand_fill_kernel(const ExpandSpec* __restrict__ sp, int64_t r0,
+                                                                         int64_t r1, const int64_t* __restrict__ indptr,
                                                                          uint32_t* __restrict__ oidx,
                                                                          float* __restrict__ oval) {
   const ExpandSpec& s = *sp;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __shared__ RowExt ext[kExpandWaves][kMaxGroups];
-  for (int64_t r = blockIdx.x * static_cast<int64_t>(kExpandWaves) + wid; r < n;
+  for (int64_t r = r0 + blockIdx.x * static_cast<int64_t>(kExpandWaves) + wid; r < r1;
        r += static_cast<int64_t>(gridDim.x) * kExpandWaves) {
     const int64_t rm = s.row_map ? s.row_map[r] : r;
     RowExt* E = ext[wid];
@@ -749,9 +750,13 @@ __global__ __launch_bounds__(64 * kCbWaves) void cb_kernel(SgdArgs a, CbArgs cb)
   }
 }
 
-// Sync payload per slot: double {w G (adaptive) or w, G} + float N. The weighted sum goes in double: a
-// float w * G underflows (and is flushed) for slots with a tiny gradient mass, which would zero their
-// weight on the average even at world 1.
+// Sync payload per slot: float {w G (adaptive) or w, G} + float N. A plain float w * G underflows for slots
+// with a tiny gradient mass (G ~ 1e-44 after a few updates on a well-classified logistic example), which
+// would zero their weight on the average even at world 1; both adaptive sums therefore carry G scaled by
+// 2^32 (exact: a power of two), which keeps w G representable for any w above ~1e-10 (G down to the
+// smallest denormal) and G up to ~8e28 finite, and leaves the ratio sum(w G) / sum(G) unchanged.
+constexpr float kSyncScale = 4294967296.0f;              // 2^32
+constexpr float kSyncUnscale = 2.3283064365386963e-10f;  // 2^-32
 __global__ void pack_kernel(const float4* __restrict__ W, const int32_t* __restrict__ blocks, int64_t nblk,
                             uint64_t nw, int adaptive, float* __restrict__ sums, float* __restrict__ nmax) {
   constexpr int64_t B = int64_t(1) << kDirtyShift;
@@ -760,8 +765,9 @@ __global__ void pack_kernel(const float4* __restrict__ W, const int32_t* __restr
        j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const uint64_t slot = static_cast<uint64_t>(blocks[j >> kDirtyShift]) * B + (j & (B - 1));
     const float4 v = slot < nw ? W[slot] : make_float4(0.f, 0.f, 0.f, 0.f);
-    sums[2 * j] = adaptive ? v.x * v.y : v.x;
-    sums[2 * j + 1] = v.y;
+    const float g = v.y * kSyncScale;
+    sums[2 * j] = adaptive ? v.x * g : v.x;
+    sums[2 * j + 1] = g;
     nmax[j] = v.z;
   }
 }
@@ -783,7 +789,7 @@ __global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict_
     const float s0 = sums[2 * j], sg = sums[2 * j + 1];
     if (!adaptive) v.x = s0 * inv_world;
     else if (sg > 0.f) v.x = s0 / sg;
-    v.y = sg * inv_world;
+    v.y = sg * kSyncUnscale * inv_world;
     v.z = nmax[j];
     W[slot] = v;
   }
@@ -1216,39 +1222,52 @@ void GpuSgd::Stage(const int64_t* indptr, const uint32_t* indices, const float* 
   staged_costs_ = false;
 }
 
-void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
-  if (r0 < 0 || r1 > staged_n_ || r0 > r1) throw std::runtime_error("LearnStaged: rows outside the staged set");
-  if (r1 == r0) return;
+void GpuSgd::PrepLearn(int64_t r0, int64_t r1) {
   hipStream_t s = impl_->stream;
   const int64_t m = r1 - r0;
-  std::vector<float> lo(m), hi(m);
   const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0;
-  if (scalar) {
-    for (int64_t i = 0; i < m; ++i) {
-      if (cfg_.loss != 1) {
+  if (scalar && m > 0) {
+    std::vector<float> lo(m), hi(m);
+    if (cfg_.loss == 1) {  // logistic: the fixed [-50, 50] range
+      std::fill(lo.begin(), lo.end(), static_cast<float>(min_label_));
+      std::fill(hi.begin(), hi.end(), static_cast<float>(max_label_));
+    } else {
+      for (int64_t i = 0; i < m; ++i) {
         min_label_ = std::min<double>(min_label_, staged_labels_[r0 + i]);
         max_label_ = std::max<double>(max_label_, staged_labels_[r0 + i]);
+        lo[i] = static_cast<float>(min_label_);
+        hi[i] = static_cast<float>(max_label_);
       }
-      lo[i] = static_cast<float>(min_label_);
-      hi[i] = static_cast<float>(max_label_);
     }
     VW_HIP_CHECK(hipMemcpyAsync(impl_->lo + r0, lo.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
     VW_HIP_CHECK(hipMemcpyAsync(impl_->hi + r0, hi.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipStreamSynchronize(s));  // lo / hi are locals: the copies must be done before they go
   }
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), s));
-  batch = std::max(1, batch);
-  for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, staged_weights_);
+}
+
+void GpuSgd::FinishLearn(int64_t r0, int64_t r1, float* preds_out) {
+  hipStream_t s = impl_->stream;
   float l = 0;
   VW_HIP_CHECK(hipMemcpyAsync(&l, impl_->loss, sizeof(float), hipMemcpyDeviceToHost, s));
   if (preds_out && cfg_.cb < 0)
-    VW_HIP_CHECK(hipMemcpyAsync(preds_out, impl_->pred + r0, m * sizeof(float), hipMemcpyDeviceToHost, s));
+    VW_HIP_CHECK(hipMemcpyAsync(preds_out, impl_->pred + r0, (r1 - r0) * sizeof(float), hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
-  examples_ += m;
+  examples_ += r1 - r0;
   sum_loss_ += l;
 }
 
+void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
+  if (r0 < 0 || r1 > staged_n_ || r0 > r1) throw std::runtime_error("LearnStaged: rows outside the staged set");
+  if (r1 == r0) return;
+  PrepLearn(r0, r1);
+  batch = std::max(1, batch);
+  for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, staged_weights_);
+  FinishLearn(r0, r1, preds_out);
+}
+
 // ---- device featurization
-void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
+void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, int batch) {
   if (plan.ngroups > kMaxGroups) throw std::runtime_error("device featurization: more than 32 namespaces");
   if (static_cast<int>(plan.inter.size()) > kMaxInter) throw std::runtime_error("device featurization: more than 64 interactions");
   hipStream_t s = impl_->stream, cs = impl_->copy_stream;
@@ -1262,7 +1281,6 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
       if (g >= plan.ngroups || (k < 2 && g < 0)) throw std::runtime_error("device featurization: bad interaction");
       h.inter[q][k] = g;
     }
-  // upload the blocks (pinned staging, parallel host copies) on the copy stream
   std::vector<void*> tmp;
   auto dev_alloc = [&](size_t bytes) -> void* {  // freed at the end of the staging
     void* d = nullptr;
@@ -1275,6 +1293,24 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
     if (bytes) impl_->stager.Copy(static_cast<char*>(d), static_cast<const char*>(src), bytes, cs);
     return d;
   };
+  // Block feature ids / values are the pass's bulk (8 B per nonzero): they go up after the small per-row
+  // arrays, in row chunks when learning rides along (a chunk's rows are expanded and learned while the next
+  // chunk's bytes cross PCIe), else in one piece.
+  struct Bulk {
+    uint32_t* idx;
+    float* val;
+    const HostBlock* b;
+  };
+  std::vector<Bulk> bulk;
+  const int64_t lr1 = std::min<int64_t>(std::max<int64_t>(0, learn_r1), n);
+  batch = std::max(1, batch);
+  // whole batches per chunk (the launches match the unchunked LearnStaged's), >= 64k rows
+  // (SML_VW_STAGE_CHUNK_ROWS: another floor, read per call - the tests cut a small pass into many chunks)
+  const char* ce = std::getenv("SML_VW_STAGE_CHUNK_ROWS");
+  const int64_t floor_rows = ce && std::atoll(ce) > 0 ? std::atoll(ce) : 65536;
+  const int64_t chunk_rows =
+      lr1 > 0 ? std::max<int64_t>(1, (floor_rows + batch - 1) / batch) * batch : std::max<int64_t>(1, n);
+  const int64_t nchunks = n > 0 ? (n + chunk_rows - 1) / chunk_rows : 0;
   try {
     {
       std::lock_guard<std::mutex> lk(impl_->stager.mu);
@@ -1284,14 +1320,21 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
         if (k >= kMaxGroupBlocks) throw std::runtime_error("device featurization: more than 4 blocks in a namespace");
         if (b.level == 0 && b.rows != n) throw std::runtime_error("device featurization: block rows != examples");
         const int64_t nnz = b.ip[b.rows] - b.ip[0];
-        std::vector<int64_t> ip(b.ip, b.ip + b.rows + 1);
-        for (auto& v : ip) v -= b.ip[0];
         DevBlock d;
-        d.ip = static_cast<const int64_t*>(dev_copy(ip.data(), ip.size() * sizeof(int64_t)));
-        d.idx = static_cast<const uint32_t*>(dev_copy(b.idx + b.ip[0], nnz * sizeof(uint32_t)));
-        d.val = static_cast<const float*>(dev_copy(b.val + b.ip[0], nnz * sizeof(float)));
+        if (b.ip[0] == 0) {
+          d.ip = static_cast<const int64_t*>(dev_copy(b.ip, (b.rows + 1) * sizeof(int64_t)));
+        } else {  // a row slice of a larger CSR: rebase its offsets
+          std::vector<int64_t> ip(b.ip, b.ip + b.rows + 1);
+          for (auto& v : ip) v -= b.ip[0];
+          d.ip = static_cast<const int64_t*>(dev_copy(ip.data(), ip.size() * sizeof(int64_t)));
+        }
+        auto* di = static_cast<uint32_t*>(dev_alloc(nnz * sizeof(uint32_t)));
+        auto* dv = static_cast<float*>(dev_alloc(nnz * sizeof(float)));
+        d.idx = di;
+        d.val = dv;
         d.level = b.level;
         h.blk[b.group][k] = d;
+        bulk.push_back({di, dv, &b});
       }
       if (plan.row_map) h.row_map = static_cast<const int64_t*>(dev_copy(plan.row_map, n * sizeof(int64_t)));
       VW_HIP_CHECK(hipStreamSynchronize(cs));
@@ -1300,7 +1343,7 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
     VW_HIP_CHECK(hipMemcpyAsync(impl_->spec, &h, sizeof(ExpandSpec), hipMemcpyHostToDevice, s));
     impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
     VW_HIP_CHECK(hipMemsetAsync(impl_->indptr, 0, sizeof(int64_t), s));
-    if (n > 0) {
+    if (n > 0) {  // row lengths need only the offsets: the whole pass's CSR layout before any bulk byte lands
       const int grid = static_cast<int>(std::min<int64_t>(65536, (n + 255) / 256));
       hipLaunchKernelGGL(expand_count_kernel, dim3(grid), dim3(256), 0, s, impl_->spec, n, impl_->indptr + 1);
       VW_HIP_CHECK(hipGetLastError());
@@ -1313,12 +1356,78 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
     VW_HIP_CHECK(hipMemcpyAsync(&nnz, impl_->indptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     VW_HIP_CHECK(hipStreamSynchronize(s));
     impl_->Reserve(std::max<int64_t>(1, n), static_cast<size_t>(nnz));
-    if (n > 0) {
-      const int grid = static_cast<int>(std::min<int64_t>(65536, (n + kExpandWaves - 1) / kExpandWaves));
-      hipLaunchKernelGGL(expand_fill_kernel, dim3(grid), dim3(64 * kExpandWaves), 0, s, impl_->spec, n, impl_->indptr,
-                         impl_->idx, impl_->val);
-      VW_HIP_CHECK(hipGetLastError());
+    for (size_t i = impl_->events.size(); i < static_cast<size_t>(nchunks); ++i) {
+      hipEvent_t e;
+      VW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      impl_->events.push_back(e);
     }
+    if (lr1 > 0) PrepLearn(0, lr1);
+    std::mutex rmu;
+    std::condition_variable rcv;
+    int64_t recorded = 0;
+    std::string upload_error;
+    const int dev = [] { int d = 0; (void)hipGetDevice(&d); return d; }();
+    std::thread uploader([&]() {
+      try {
+        VW_HIP_CHECK(hipSetDevice(dev));
+        Stager& st = impl_->stager;
+        std::lock_guard<std::mutex> lk(st.mu);
+        for (int64_t c = 0; c < nchunks; ++c) {
+          const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
+          for (const Bulk& u : bulk) {
+            const HostBlock& b = *u.b;
+            // per-example blocks go up row range by row range; row-mapped (level 1) blocks whole, first
+            int64_t p0, p1;
+            if (b.level == 0) {
+              p0 = b.ip[r0] - b.ip[0];
+              p1 = b.ip[r1] - b.ip[0];
+            } else if (c == 0) {
+              p0 = 0;
+              p1 = b.ip[b.rows] - b.ip[0];
+            } else {
+              continue;
+            }
+            if (p1 > p0) {
+              st.Copy(reinterpret_cast<char*>(u.idx + p0), reinterpret_cast<const char*>(b.idx + b.ip[0] + p0),
+                      (p1 - p0) * sizeof(uint32_t), cs);
+              st.Copy(reinterpret_cast<char*>(u.val + p0), reinterpret_cast<const char*>(b.val + b.ip[0] + p0),
+                      (p1 - p0) * sizeof(float), cs);
+            }
+          }
+          VW_HIP_CHECK(hipEventRecord(impl_->events[c], cs));
+          std::lock_guard<std::mutex> g(rmu);
+          recorded = c + 1;
+          rcv.notify_all();
+        }
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(rmu);
+        upload_error = e.what();
+        recorded = nchunks;  // release the expand loop; it rethrows
+        rcv.notify_all();
+      }
+    });
+    try {
+      for (int64_t c = 0; c < nchunks; ++c) {
+        {
+          std::unique_lock<std::mutex> g(rmu);
+          rcv.wait(g, [&] { return recorded > c; });
+          if (!upload_error.empty()) break;
+        }
+        VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
+        const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
+        const int grid = static_cast<int>(std::min<int64_t>(65536, (r1 - r0 + kExpandWaves - 1) / kExpandWaves));
+        hipLaunchKernelGGL(expand_fill_kernel, dim3(grid), dim3(64 * kExpandWaves), 0, s, impl_->spec, r0, r1,
+                           impl_->indptr, impl_->idx, impl_->val);
+        VW_HIP_CHECK(hipGetLastError());
+        for (int64_t b0 = r0; b0 < std::min(r1, lr1); b0 += batch)
+          Launch(b0, std::min<int64_t>(std::min(r1, lr1), b0 + batch), true, staged_weights_);
+      }
+    } catch (...) {
+      uploader.join();
+      throw;
+    }
+    uploader.join();
+    if (!upload_error.empty()) throw std::runtime_error("VW pass upload failed: " + upload_error);
     VW_HIP_CHECK(hipStreamSynchronize(s));
   } catch (...) {
     (void)hipStreamSynchronize(s);
@@ -1328,21 +1437,27 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n) {
   }
   for (void* q : tmp) PoolFree(q);
   staged_rows_ = n;
+  if (lr1 > 0) FinishLearn(0, lr1, nullptr);
 }
 
-void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights) {
+void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights, int64_t learn_r1,
+                       int batch) {
   if (n < 0) throw std::runtime_error("negative row count");
-  ExpandToStage(plan, n);
   hipStream_t s = impl_->stream;
+  if (learn_r1 > 0 && (cfg_.cb >= 0 || cfg_.csoaa > 0))  // their label extras are staged after the plan
+    throw std::runtime_error("StagePlan: learning while staging is for the scalar / oaa learners");
+  // labels / weights first: a pipelined stage learns as the chunks land
+  impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
   if (cfg_.cb < 0 && n) {
     VW_HIP_CHECK(hipMemcpyAsync(impl_->lab, labels, n * sizeof(float), hipMemcpyHostToDevice, s));
     if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
     staged_labels_.assign(labels, labels + n);
     staged_n_ = n;
   }
-  VW_HIP_CHECK(hipStreamSynchronize(s));
   staged_weights_ = weights != nullptr;
   staged_costs_ = false;
+  ExpandToStage(plan, n, learn_r1, batch);
+  VW_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 void GpuSgd::StageCosts(const int64_t* cptr, const int32_t* cls, const float* cost, int64_t n) {
@@ -1542,8 +1657,8 @@ void GpuSgd::ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val)
   const int64_t nb = static_cast<int64_t>((impl_->nw + per - 1) / per);
   int32_t* cnt = nullptr;
   int64_t* base = nullptr;
-  VW_HIP_CHECK(hipMalloc(&cnt, nb * sizeof(int32_t)));
-  VW_HIP_CHECK(hipMalloc(&base, nb * sizeof(int64_t)));
+  PoolMalloc(&cnt, nb * sizeof(int32_t));  // caching pool: no hipMalloc / hipFree device syncs per export
+  PoolMalloc(&base, nb * sizeof(int64_t));
   hipLaunchKernelGGL(count_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, s, impl_->W, impl_->nw, per, cnt);
   std::vector<int32_t> hc(nb);
   VW_HIP_CHECK(hipMemcpyAsync(hc.data(), cnt, nb * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1556,19 +1671,19 @@ void GpuSgd::ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val)
   if (tot > 0) {
     uint64_t* di = nullptr;
     float* dv = nullptr;
-    VW_HIP_CHECK(hipMalloc(&di, tot * sizeof(uint64_t)));
-    VW_HIP_CHECK(hipMalloc(&dv, tot * sizeof(float)));
+    PoolMalloc(&di, tot * sizeof(uint64_t));
+    PoolMalloc(&dv, tot * sizeof(float));
     VW_HIP_CHECK(hipMemcpyAsync(base, hb.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(write_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw, per, base,
                        di, dv);
     VW_HIP_CHECK(hipMemcpyAsync(idx->data(), di, tot * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     VW_HIP_CHECK(hipMemcpyAsync(val->data(), dv, tot * sizeof(float), hipMemcpyDeviceToHost, s));
     VW_HIP_CHECK(hipStreamSynchronize(s));
-    (void)hipFree(di);
-    (void)hipFree(dv);
+    PoolFree(di);
+    PoolFree(dv);
   }
-  (void)hipFree(cnt);
-  (void)hipFree(base);
+  PoolFree(cnt);
+  PoolFree(base);
 }
 
 void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val) {

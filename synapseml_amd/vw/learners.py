@@ -14,6 +14,7 @@ training broadcasts the model per split and averages (mergeModels).
 """
 from __future__ import annotations
 
+import os
 import re
 import time
 from typing import List, Optional
@@ -394,16 +395,22 @@ def _evict_nccl(comm) -> None:
         abort()
 
 
-def _gpu_learn_staged(est, g, comm, n: int):
-    """numSyncsPerPass intermediate weight averages + the end-of-pass one, the same count on every rank
-    whatever its row count (VowpalWabbitSyncSchedule.scala:36-72); the staged rows are re-read from HBM by
-    every pass and segment (VW's cache file)."""
+def _sync_bounds(est, n: int) -> np.ndarray:
+    """row bounds of the sync segments of one pass: numSyncsPerPass intermediate averages + the end-of-pass
+    one, the same count on every rank whatever its row count (VowpalWabbitSyncSchedule.scala:36-72)"""
     segs = max(0, int(est.getNumSyncsPerPass() or 0)) + 1
-    bounds = np.linspace(0, n, segs + 1).astype(np.int64)
+    return np.linspace(0, n, segs + 1).astype(np.int64)
+
+
+def _gpu_learn_staged(est, g, comm, n: int, first_learned: bool = False):
+    """The sync schedule over the staged rows, re-read from HBM by every pass and segment (VW's cache file).
+    ``first_learned``: pass 0's first segment was already learned while the pass staged (stage_plan's
+    learn_r1); its sync still runs here."""
+    bounds = _sync_bounds(est, n)
     sync_bytes = []
-    for _ in range(max(1, est.getNumPasses())):
-        for s0, s1 in zip(bounds[:-1], bounds[1:]):
-            if s1 > s0:
+    for p in range(max(1, est.getNumPasses())):
+        for k, (s0, s1) in enumerate(zip(bounds[:-1], bounds[1:])):
+            if s1 > s0 and not (first_learned and p == 0 and k == 0):
                 g.learn_staged(int(s0), int(s1), int(est.getGpuBatchSize()))
             if comm is not None:
                 try:
@@ -443,8 +450,13 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     wcol = est.getWeightCol()
     weights = np.asarray(df[wcol], np.float32) if wcol and wcol in df else None
     gb, ng, inter = _device_plan(blocks, info)
+    # scalar / oaa learners learn pass 0's first sync segment while the pass's blocks cross PCIe (chunked
+    # upload on the copy stream, each chunk expanded and learned as it lands); csoaa stages its cost lists
+    # after the plan, so it stages first
+    fused = int(info["csoaa"]) == 0 and os.environ.get("SML_VW_STAGE_LEARN", "1") != "0"
     g.stage_plan(gb, ng, inter, info["constant"] == "1", None, n, np.ascontiguousarray(labels, dtype=np.float32),
-                 None if weights is None else np.ascontiguousarray(weights, dtype=np.float32))
+                 None if weights is None else np.ascontiguousarray(weights, dtype=np.float32),
+                 learn_r1=int(_sync_bounds(est, n)[1]) if fused else 0, batch=int(est.getGpuBatchSize()))
     if int(info["csoaa"]) > 0:
         if costs is None:
             raise ValueError("--csoaa needs per-row (class, cost) lists")
@@ -452,7 +464,7 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
         g.stage_costs(cptr, np.asarray([k for c in costs for k, _ in c], np.int32),
                       np.asarray([v for c in costs for _, v in c], np.float32))
     t1 = time.perf_counter_ns()
-    sync_bytes = _gpu_learn_staged(est, g, _gpu_sync_comm(vwmod), n)
+    sync_bytes = _gpu_learn_staged(est, g, _gpu_sync_comm(vwmod), n, first_learned=fused)
     t2 = time.perf_counter_ns()
     lab = np.asarray(labels, np.float64)
     wts = np.ones(n) if weights is None else weights.astype(np.float64)
@@ -464,7 +476,9 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
              "passes": int(max(1, est.getNumPasses())), "ipsEstimate": 0.0, "snipsEstimate": 0.0,
              "syncBytes": int(sum(sync_bytes)), "timeTotalNs": t2 - t0, "timeNativeIngestNs": t1 - t0,
              "timeLearnNs": t2 - t1, "timeMultipassNs": 0}
-    return _GpuTrainedModel(g.export_model(args), args, info), stats
+    model = g.export_model(args)
+    stats["timeExportNs"] = time.perf_counter_ns() - t2  # device nonzeros -> model bytes
+    return _GpuTrainedModel(model, args, info), stats
 
 
 class _GpuScorer:

@@ -185,7 +185,8 @@ def test_fp32_exact_integer_layout(kernel):
     (1, 2048, 7, 7, 512, 1, 1, 0),
 ])
 def test_fp32_conv_matches_fp64_reference(shape):
-    """fp32 MFMA conv (+bias, ReLU) against an fp64 host convolution: fp32-level error, no reduced-precision path."""
+    """fp32 MFMA conv (+bias, ReLU) against an fp64 host convolution: fp32-level error, no reduced-precision path
+    (the exact f32 MFMA mode; the bf16x3 default has its own error gate below)."""
     from synapseml_amd.ops.conv import conv2d_nhwc, pack_weight
 
     B, C, H, W, Co, k, st, pd = shape
@@ -195,10 +196,11 @@ def test_fp32_conv_matches_fp64_reference(shape):
     bias = torch.randn(Co, device="cuda")
     ref = torch.relu(F.conv2d(x.cpu().double(), w.cpu().double(), bias.cpu().double(), st, pd))
     for kernel in (0, 64064, 128128, 64128):
-        y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel)
+        y = conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), bias=bias, relu=True, kernel=kernel,
+                        f32_mode="exact")
         torch.testing.assert_close(y.cpu().double(), ref, rtol=1e-5, atol=2e-5, msg=lambda m: f"kernel {kernel}: {m}")
     with pytest.raises(RuntimeError):  # the 8-wave tiles are f16/bf16 only
-        conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), kernel=256128)
+        conv2d_nhwc(x, pack_weight(w, torch.float32), k, k, (st, st), (pd, pd), kernel=256128, f32_mode="exact")
 
 
 def test_fp32_prologue_residual_dual_output():

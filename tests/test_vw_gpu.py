@@ -268,3 +268,36 @@ def test_gpu_scoring_b30_model_keeps_host_memory_flat():
     assert rss1 - rss0 < (1 << 30), (rss0, rss1)
     acc = np.mean(out["prediction"] == y)
     assert acc > 0.95
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args,syncs", [("", 0), ("-q ab --loss_function logistic", 2), ("--oaa 3", 0)])
+def test_gpu_fused_stage_learn_equals_stage_then_learn(monkeypatch, args, syncs):
+    """The estimator learns pass 0's first sync segment while the pass's blocks upload (chunk by chunk, each
+    chunk expanded and learned as it lands): at gpuBatchSize=1 the scalar learners (one wave per example,
+    deterministic) give bitwise the model of staging everything first and learning after, with the pass cut
+    into many chunks. --oaa runs one wave per class whose global-state atomics land in any order, so its
+    models agree to rounding."""
+    df = _three_ns(n=2500)
+    y = df["label"]
+    if "logistic" in args:
+        df = DataFrame({"a": df["a"], "b": df["b"], "c": df["c"], "label": np.where(y > 0, 1.0, -1.0)})
+    elif "oaa" in args:
+        df = DataFrame({"a": df["a"], "b": df["b"], "c": df["c"], "label": (np.digitize(y, [-0.5, 0.5]) + 1.0)})
+    kw = dict(featuresCol="a", additionalFeatures=["b", "c"], passThroughArgs=args, numPasses=2,
+              numSyncsPerPass=syncs, deviceType="gpu", gpuBatchSize=1)
+    if "oaa" in args:
+        kw["numClasses"] = 3
+    cls = VowpalWabbitClassifier if ("logistic" in args or "oaa" in args) else VowpalWabbitRegressor
+    monkeypatch.setenv("SML_VW_STAGE_CHUNK_ROWS", "300")
+    monkeypatch.setenv("SML_VW_STAGE_LEARN", "1")
+    fused = cls(**kw).fit(df)
+    monkeypatch.setenv("SML_VW_STAGE_LEARN", "0")
+    plain = cls(**kw).fit(df)
+    sf, sp = fused.getPerformanceStatistics(), plain.getPerformanceStatistics()
+    if "oaa" in args:
+        assert np.mean(fused.transform(df)["prediction"] == plain.transform(df)["prediction"]) > 0.99
+        assert float(sf["averageLoss"][0]) == pytest.approx(float(sp["averageLoss"][0]), rel=1e-3)
+        return
+    assert fused.getNativeModel() == plain.getNativeModel()
+    assert float(sf["averageLoss"][0]) == float(sp["averageLoss"][0])

@@ -84,7 +84,8 @@ def estimator_bench(args, world: int, rank: int) -> None:
     for _ in range(args.steps):
         model = est.fit(df)
         stats.append({k: float(model.getPerformanceStatistics()[k][0])
-                      for k in ("timeNativeIngestNs", "timeLearnNs", "timeTotalNs", "syncBytes")})
+                      for k in ("timeNativeIngestNs", "timeLearnNs", "timeTotalNs", "syncBytes", "timeExportNs")
+                      if k in model.getPerformanceStatistics()})
     torch.cuda.synchronize()
     D.barrier()
     elapsed = time.perf_counter() - t0
@@ -105,8 +106,9 @@ def estimator_bench(args, world: int, rank: int) -> None:
             "value": round(args.rows * world * args.steps / elapsed, 1), "unit": "examples / fit wall second",
             "n_gpus": world, "bits": args.bits, "table_gib": round((2 ** args.bits) * 16 / 2 ** 30, 2),
             "rows_per_gpu": args.rows, "nnz_per_row": args.nnz, "batch": args.batch, "ms_per_fit": round(fit_ms, 1),
-            "phases_ms": {"ingest_and_device_featurize": ph["timeNativeIngestNs"], "learn_and_sync": ph["timeLearnNs"],
-                          "engine_total": ph["timeTotalNs"],
+            "phases_ms": {"stage_and_first_segment_learn": ph["timeNativeIngestNs"],
+                          "remaining_learn_and_sync": ph["timeLearnNs"], "engine_total": ph["timeTotalNs"],
+                          "export_model": ph.get("timeExportNs"),
                           "export_model_and_other": round(fit_ms - ph["timeTotalNs"], 2)},
             "sync_mib": round(stats[-1]["syncBytes"] / 2 ** 20, 2), "holdout_logloss": round(logloss, 4),
             "timed_region": "VowpalWabbitClassifier(numBits, deviceType='gpu').fit(df) end to end (DataFrame built "

@@ -11,3 +11,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 timeout -k 10 300 python tools/bench_onnx.py --batches 128,256 --precisions fp32,fp16 --images 0 > "$OUT/bench_onnx.log" 2>&1 || exit 1
 timeout -k 10 400 python tools/bench_ranker.py --steps 2 --warmup 1 > "$OUT/bench_ranker.log" 2>&1 || exit 1
 timeout -k 10 400 python tools/bench_vw.py --steps 3 --warmup 1 > "$OUT/bench_vw_estimator.log" 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rank" -o rank -- python3 tools/bench_ranker.py --steps 1 --warmup 0 > "$OUT/prof_rank.log" 2>&1 || exit 1
