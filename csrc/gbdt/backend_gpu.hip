@@ -238,9 +238,13 @@ struct RankTables {
   int32_t* rank_scratch;
   double* lam_scratch;
   double* hes_scratch;
+  const int32_t* order;  // register-path queries, largest first (longest-processing-time order), nreg of them
   int nq, ngain, max_position, norm;
+  int gain_mono;  // label gains strictly increasing (the register kernel's kMono form)
+  int nreg;
   double sigma;
 };
+constexpr int kGainLds = 64;  // label gains staged in LDS by the register kernel (longer tables: global)
 
 __device__ __forceinline__ double WaveSumD(double v) {
 #pragma unroll
@@ -338,18 +342,23 @@ __device__ __forceinline__ void PairTermsPre(float sig, float imd, bool use_norm
 
 // The register path's form of PairTermsPre, branch-free: the top document i (wave-uniform si / li / gi /
 // di) against this lane's partner j. Both orientations of a difference are exact negations of one another
-// (round-to-nearest is sign-symmetric), so ds and gap take one subtraction and a sign flip; an ineligible
-// partner (same label, itself, padding lane) gets dn = 0, which zeroes all three terms (p stays finite for
-// any ds, infinities included); the two quotients are hardware reciprocals (v_rcp_f32, 1 ulp) instead of
-// IEEE divides (~11 VALU instructions each, 40 % of the pair's instructions). sl2e = sigma * log2(e).
-__device__ __forceinline__ void PairTermsFast(float sig, float sl2e, float imd, bool use_norm, bool ok, double si,
-                                              int li, float gi, float di, double sj, int lj, float gj, float dj,
-                                              float* c, float* ph_out, float* pl_out) {
-  const unsigned flip = li > lj ? 0u : 0x80000000u;  // i is the higher-labelled document: no flip
+// (round-to-nearest is sign-symmetric), so ds and gap take one subtraction and a sign flip. No eligibility
+// test: a same-label partner (the top document itself included) has gap = 0 and a padding lane imdv = 0,
+// so dn = 0 zeroes all three terms (p stays finite for any ds, infinities included), exactly what skipping
+// the pair adds to these sums. kMono (label gains strictly increasing - LightGBM's default 2^l - 1 table):
+// i is the higher-labelled document iff gi > gj, so the flip is the sign bit of gi - gj and gap its
+// magnitude (no label compare / select). The two quotients are hardware reciprocals (v_rcp_f32, 1 ulp)
+// instead of IEEE divides (~11 VALU instructions each). sl2e = sigma * log2(e).
+template <bool kMono>
+__device__ __forceinline__ void PairTermsFast(float sig, float sl2e, float imdv, bool use_norm, double si, int li,
+                                              float gi, float di, double sj, int lj, float gj, float dj, float* c,
+                                              float* ph_out, float* pl_out) {
+  const float dg = gi - gj;
+  const unsigned flip = kMono ? (__float_as_uint(dg) & 0x80000000u) : (li > lj ? 0u : 0x80000000u);
   const float ds = __uint_as_float(__float_as_uint(static_cast<float>(si - sj)) ^ flip);
-  const float gap = __uint_as_float(__float_as_uint(gi - gj) ^ flip);
+  const float gap = kMono ? fabsf(dg) : __uint_as_float(__float_as_uint(dg) ^ flip);
   const float pd = fabsf(di - dj);
-  float dn = ok ? gap * pd * imd : 0.f;
+  float dn = gap * pd * imdv;
   if (use_norm) dn *= __builtin_amdgcn_rcpf(0.01f + fabsf(ds));
   const float p = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(sl2e * ds));
   const float pl = p * (-sig * dn);
@@ -531,12 +540,20 @@ __device__ __forceinline__ double ReadLaneD(double v, int l) {
 // lanes 0..ntop-1 and is broadcast the same way. Pairs: (a) every top
 // document with every document, spread over the lanes and wave-reduced;
 // (b) every other document with the top list, one lane per document.
-template <int NU, bool kTR>  // documents per lane: cnt <= 64 * NU; kTR: transpose-reduced top sums
+// the top list's per-document values, staged by rank in LDS by their owning lanes (lane r of the wave reads
+// rank r's; no second global load of the top documents' scores / labels)
+struct RankTop {
+  double sc[64];
+  float gn[64];
+  int lab[64];
+};
+
+template <int NU, bool kTR, bool kMono>  // documents per lane: cnt <= 64 * NU; kTR: transpose-reduced top sums
 __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __restrict__ score,
                                     const float* __restrict__ label, const float* __restrict__ weight,
                                     float* __restrict__ g, float* __restrict__ h, const double* s_disc,
-                                    int* s_doc_of_rank) {
-  // one wave per query (its own 64-entry rank -> doc map; wave-level syncs only)
+                                    const float* s_gain, int* s_doc_of_rank, RankTop& top) {
+  // one wave per query (its own kRankLds-entry rank -> doc map; wave-level syncs only)
   const int lane = threadIdx.x & 63;
   const int b = t.qb[q], cnt = t.qb[q + 1] - b;
   const int ntop = min(cnt, t.max_position);
@@ -556,69 +573,106 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
     mx = fmax(mx, __shfl_xor(mx, off, 64));
     mn = fmin(mn, __shfl_xor(mn, off, 64));
   }
-  // ranks: number of documents scoring higher, ties by index (stable sort):
-  // rank(i) = #{j: sj > si || (sj == si && j < i)} = #{j < i: sj >= si} + #{j > i: sj >= next_up(si)},
-  // one fp64 compare per pair. Whether j < i is static for documents in different lane slots
-  // (u != v) and jj < lane within one; the document itself (sj < next_up(sj)) counts 0.
+  // ranks: number of documents scoring higher, ties by index (stable sort). First the strict count
+  // #{j: sj > si} = #{j: sj >= next_up(si)} - one fp64 compare per pair and no per-partner index test; without
+  // ties it IS the stable rank (a permutation), which the wave checks by scattering doc -> rank slot: a
+  // shared slot means tied scores (every document of a query ties on the first iteration), and only then
+  // the tie-aware count runs: rank(i) = #{j < i: sj >= si} + #{j > i: sj >= next_up(si)} (whether j < i is
+  // static for documents in different lane slots (u != v) and jj < lane within one).
   double sup[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) sup[u] = nextafter(sc[u], INFINITY);
+  auto count_ranks = [&](bool ties) {
 #pragma unroll
-  for (int v = 0; v < NU; ++v) {
-    if (v * 64 >= cnt) break;
-    const int jn = min(64, cnt - v * 64);
-    // wave-uniform partner scores through the constant address space: s_load into SGPRs (read-only data),
-    // no v_readlane pair + hazard per partner
-    const __attribute__((address_space(4))) double* sv =
-        (const __attribute__((address_space(4))) double*)(score + b + v * 64);
-    for (int jj = 0; jj < jn; ++jj) {
-      const double sj = sv[jj];
+    for (int v = 0; v < NU; ++v) {
+      if (v * 64 >= cnt) break;
+      const int jn = min(64, cnt - v * 64);
+      // wave-uniform partner scores through the constant address space: s_load into SGPRs (read-only data),
+      // no v_readlane pair + hazard per partner
+      const __attribute__((address_space(4))) double* sv =
+          (const __attribute__((address_space(4))) double*)(score + b + v * 64);
+      if (!ties) {
+        for (int jj = 0; jj < jn; ++jj) {
+          const double sj = sv[jj];
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        if (u < v) rk[u] += sj >= sup[u] ? 1 : 0;         // every j of slot v is after i
-        else if (u > v) rk[u] += sj >= sc[u] ? 1 : 0;     // every j of slot v is before i
-        else rk[u] += sj >= (jj < lane ? sc[u] : sup[u]) ? 1 : 0;
+          for (int u = 0; u < NU; ++u) rk[u] += sj >= sup[u] ? 1 : 0;
+        }
+      } else {
+        for (int jj = 0; jj < jn; ++jj) {
+          const double sj = sv[jj];
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            if (u < v) rk[u] += sj >= sup[u] ? 1 : 0;         // every j of slot v is after i
+            else if (u > v) rk[u] += sj >= sc[u] ? 1 : 0;     // every j of slot v is before i
+            else rk[u] += sj >= (jj < lane ? sc[u] : sup[u]) ? 1 : 0;
+          }
+        }
       }
     }
+  };
+  auto scatter = [&]() {  // rank -> doc map (every document's slot)
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      if (u * 64 + lane < cnt) s_doc_of_rank[rk[u]] = u * 64 + lane;
+    WaveSync();
+  };
+  count_ranks(false);
+  scatter();
+  bool clash = false;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) clash |= u * 64 + lane < cnt && s_doc_of_rank[rk[u]] != u * 64 + lane;
+  if (__builtin_amdgcn_ballot_w64(clash)) {  // tied scores: the exact, tie-aware ranks
+    WaveSync();                               // every lane has read the map before it is rewritten
+#pragma unroll
+    for (int u = 0; u < NU; ++u) rk[u] = 0;
+    count_ranks(true);
+    scatter();
   }
-  // per-document label gain and rank discount (ranks < cnt <= kRankLds: table hit)
+  // per-document label gain (LDS table up to kGainLds labels) and rank discount (ranks < cnt <= kRankLds)
   const unsigned gtop = static_cast<unsigned>(t.ngain - 1);
+  const bool gain_lds = t.ngain <= kGainLds;
   float gn[NU], dc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const bool ok = u * 64 + lane < cnt;
-    gn[u] = ok ? static_cast<float>(t.gain[min(static_cast<unsigned>(lab[u]), gtop)]) : 0.f;
+    const unsigned gi = min(static_cast<unsigned>(lab[u]), gtop);
+    gn[u] = ok ? (gain_lds ? s_gain[gi] : static_cast<float>(t.gain[gi])) : 0.f;
     dc[u] = ok ? static_cast<float>(s_disc[rk[u]]) : 0.f;
   }
-  // top list: lane r holds the document of rank r (ranks are a permutation)
+  // top list: lane r holds the document of rank r (ranks are a permutation; the map is already written),
+  // its score / label / gain staged by rank by the owning lane
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    if (u * 64 + lane < cnt && rk[u] < ntop) {
+      top.sc[rk[u]] = sc[u];
+      top.gn[rk[u]] = gn[u];
+      top.lab[rk[u]] = lab[u];
+    }
+  }
+  WaveSync();
   double tsc = 0.0;
   int tlab = 0, tdoc = 0;
   float tgn = 0.f;
-  {
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-      if (u * 64 + lane < cnt && rk[u] < ntop) s_doc_of_rank[rk[u]] = u * 64 + lane;
-    WaveSync();
-    if (lane < ntop) {
-      tdoc = s_doc_of_rank[lane];
-      tsc = score[b + tdoc];
-      tlab = static_cast<int>(label[b + tdoc]);
-      tgn = static_cast<float>(t.gain[min(static_cast<unsigned>(tlab), gtop)]);
-    }
-    WaveSync();  // the map is read before the next query of this wave rewrites it
+  if (lane < ntop) {
+    tdoc = s_doc_of_rank[lane];
+    tsc = top.sc[lane];
+    tlab = top.lab[lane];
+    tgn = top.gn[lane];
   }
+  WaveSync();  // the map and the top slots are read before the next query of this wave rewrites them
   const float tdc = static_cast<float>(s_disc[lane]);  // discount of rank `lane` (valid for lane < ntop)
   const float sig = static_cast<float>(t.sigma);
   const float sl2e = sig * 1.4426950408889634f;
   const float fimd = static_cast<float>(t.inv_max_dcg[q]);
   const bool use_norm = t.norm && mx != mn;
   // fp32 accumulators: a document sums at most max_position + cnt pair terms, each already fp32
-  float lam[NU], hes[NU], ntf[NU];
+  float lam[NU], hes[NU], ntf[NU], imdv[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     lam[u] = 0.f;
     hes[u] = 0.f;
     ntf[u] = u * 64 + lane < cnt && rk[u] >= ntop ? 1.f : 0.f;  // a non-top document mirrors its pair terms
+    imdv[u] = u * 64 + lane < cnt ? fimd : 0.f;                  // padding lanes: dn = 0
   }
   float suml = 0.f;
   // Top document r against every document (partners on the lanes), each pair evaluated once: the
@@ -631,8 +685,7 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   // this lane's terms of top document r against its partners (and the partners' mirrored terms)
   auto top_terms = [&](int r, float* la_out, float* he_out) {
     const double si = ReadLaneD(tsc, r);
-    const int li = __builtin_amdgcn_readlane(tlab, r);
-    const int di = __builtin_amdgcn_readlane(tdoc, r);
+    const int li = kMono ? 0 : __builtin_amdgcn_readlane(tlab, r);
     const float gi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tgn), r));
     const float dci = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tdc), r));
     float la = 0.f, he = 0.f;
@@ -640,10 +693,8 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
     for (int u = 0; u < NU; ++u) {
       // branch-free: an ineligible pair adds signed zeros (bitwise a no-op on these sums), a top partner
       // takes no mirrored terms (ntf = 0: fma(-0, c, x) = x)
-      const int j = u * 64 + lane;
       float c, ph, pl;
-      PairTermsFast(sig, sl2e, fimd, use_norm, j < cnt && j != di && lab[u] != li, si, li, gi, dci, sc[u], lab[u],
-                    gn[u], dc[u], &c, &ph, &pl);
+      PairTermsFast<kMono>(sig, sl2e, imdv[u], use_norm, si, li, gi, dci, sc[u], lab[u], gn[u], dc[u], &c, &ph, &pl);
       la += c;
       he += ph;
       suml -= pl;
@@ -727,25 +778,29 @@ __device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
 // wave (2 KB + 256 B per wave instead of the LDS path's 11.5 KB). kWaves independent waves per block, each
 // walking its own queries (a CU holds at most 16 workgroups, so one-wave blocks cap residency at 4 waves
 // per SIMD; kWaves = 4 lifts that, but measured slower - see rank_waves_).
-template <int kWaves, bool kTR = true>
+template <int kWaves, bool kTR = true, bool kMono = true>
 __global__ __launch_bounds__(64 * kWaves, 4) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
                                                                       const float* __restrict__ label,
                                                                       const float* __restrict__ weight,
                                                                       float* __restrict__ g, float* __restrict__ h) {
   __shared__ double s_disc[kRankLds];
-  __shared__ int s_map[kWaves][64];
+  __shared__ float s_gain[kGainLds];
+  __shared__ int s_map[kWaves][kRankLds];
+  __shared__ RankTop s_top[kWaves];
   for (int r = threadIdx.x; r < kRankLds; r += 64 * kWaves) s_disc[r] = t.disc[r];
+  for (int r = threadIdx.x; r < kGainLds; r += 64 * kWaves) s_gain[r] = r < t.ngain ? static_cast<float>(t.gain[r]) : 0.f;
   __syncthreads();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform to the compiler: q, b, cnt in SGPRs
   // documents per lane sized to the query: the pair loops run NU-wide, so a 100-document query
   // costs half of what the kRankLds-wide form would
-  for (int q = blockIdx.x * kWaves + wid; q < t.nq; q += gridDim.x * kWaves) {
+  for (int k = blockIdx.x * kWaves + wid; k < t.nreg; k += gridDim.x * kWaves) {
+    const int q = t.order[k];
     const int cnt = t.qb[q + 1] - t.qb[q];
     if (cnt <= 0 || !RegsEligible(t, cnt)) continue;
-    if (cnt <= 64) LambdarankQueryRegs<1, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
-    else if (cnt <= 128) LambdarankQueryRegs<2, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
-    else if (cnt <= 192) LambdarankQueryRegs<3, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
-    else LambdarankQueryRegs<kRankPerLane, kTR>(t, q, score, label, weight, g, h, s_disc, s_map[wid]);
+    if (cnt <= 64) LambdarankQueryRegs<1, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
+    else if (cnt <= 128) LambdarankQueryRegs<2, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
+    else if (cnt <= 192) LambdarankQueryRegs<3, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
+    else LambdarankQueryRegs<kRankPerLane, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
   }
 }
 
@@ -3529,13 +3584,18 @@ class GpuBackend : public TrainBackend {
       if (rank_.nq > 0) {
         const int grid = std::min(rank_.nq, 65536);
         if (rank_regs_) {
+          const int rgrid = std::max(1, std::min(rank_.nreg, 1 << 20));  // one wave per query
           if (rank_waves_ == 1) {
-            auto lk = rank_treduce_ ? lambdarank_regs_kernel<1, true> : lambdarank_regs_kernel<1, false>;
-            hipLaunchKernelGGL(lk, dim3(grid), dim3(64), 0, stream_, rank_, score_.get(),
+            auto lk = rank_treduce_ ? (rank_.gain_mono ? lambdarank_regs_kernel<1, true, true>
+                                                       : lambdarank_regs_kernel<1, true, false>)
+                                    : (rank_.gain_mono ? lambdarank_regs_kernel<1, false, true>
+                                                       : lambdarank_regs_kernel<1, false, false>);
+            hipLaunchKernelGGL(lk, dim3(rgrid), dim3(64), 0, stream_, rank_, score_.get(),
                                label_.get(), weight_.get(), g_.get(), h_.get());
           } else {
-            const int g4 = std::max(1, std::min((rank_.nq + 3) / 4, 16384));
-            hipLaunchKernelGGL(lambdarank_regs_kernel<4>, dim3(g4), dim3(256), 0, stream_, rank_, score_.get(),
+            const int g4 = std::max(1, std::min((rank_.nreg + 3) / 4, 1 << 18));
+            auto l4 = rank_.gain_mono ? lambdarank_regs_kernel<4, true, true> : lambdarank_regs_kernel<4, true, false>;
+            hipLaunchKernelGGL(l4, dim3(g4), dim3(256), 0, stream_, rank_, score_.get(),
                                label_.get(), weight_.get(), g_.get(), h_.get());
           }
           SML_HIP_CHECK(hipGetLastError());
@@ -3999,13 +4059,29 @@ class GpuBackend : public TrainBackend {
     int max_q = 0;
     rank_regs_ = rank_lds_ = false;
     const bool regs_pos = obj.max_position() <= 64;  // RegsEligible, host side: which kernels have work
+    std::vector<int32_t> reg_q;
     for (size_t q = 0; q + 1 < qb.size(); ++q) {
       const int c = qb[q + 1] - qb[q];
       max_q = std::max(max_q, c);
       if (c <= 0) continue;
-      if (regs_pos && c <= kRankLds) rank_regs_ = true; else rank_lds_ = true;
+      if (regs_pos && c <= kRankLds) {
+        rank_regs_ = true;
+        reg_q.push_back(static_cast<int32_t>(q));
+      } else {
+        rank_lds_ = true;
+      }
     }
+    // the register kernel walks its queries largest first, one wave each (a query's cost grows with its
+    // documents - NU lane slots of pair terms and ranks - and 20..180-document queries in index order left
+    // a tail of long queries on a few waves)
+    std::stable_sort(reg_q.begin(), reg_q.end(),
+                     [&qb](int32_t a, int32_t b) { return qb[a + 1] - qb[a] > qb[b + 1] - qb[b]; });
+    rank_order_.alloc(std::max<size_t>(1, reg_q.size()));
+    if (!reg_q.empty())
+      SML_HIP_CHECK(hipMemcpy(rank_order_.get(), reg_q.data(), sizeof(int32_t) * reg_q.size(), hipMemcpyHostToDevice));
     rank_ = RankTables{};
+    rank_.order = rank_order_.get();
+    rank_.nreg = static_cast<int>(reg_q.size());
     if (max_q > kRankLds) {  // long queries stream ranks / lambdas through global scratch
       rank_scratch_.alloc(n_);
       rank_lam_.alloc(n_);
@@ -4027,6 +4103,20 @@ class GpuBackend : public TrainBackend {
     rank_.max_position = obj.max_position();
     rank_.norm = obj.lambdarank_norm() ? 1 : 0;
     rank_.sigma = obj.params().sigmoid;
+    // kMono: the higher label of a pair is the one with the larger gain - true when the gains (as the fp32
+    // the kernel compares) strictly increase and no label is negative (a negative label clamps to the top gain)
+    bool mono = true;
+    for (size_t k = 0; k + 1 < gain.size(); ++k) mono &= static_cast<float>(gain[k + 1]) > static_cast<float>(gain[k]);
+    if (mono && obj.labels()) {
+      const float* lab = obj.labels();
+      const int64_t nl = obj.num_rows();
+      bool neg = false;
+#pragma omp parallel for reduction(|| : neg) schedule(static)
+      for (int64_t i = 0; i < nl; ++i) neg = neg || lab[i] < 0.f;
+      mono = !neg;
+    }
+    const char* me = std::getenv("SML_RANK_MONO");  // 0: the label-compare form (A/B and tests), read per booster
+    rank_.gain_mono = me && std::atoi(me) == 0 ? 0 : (mono ? 1 : 0);
     rank_ready_ = true;
   }
 
@@ -4377,7 +4467,7 @@ class GpuBackend : public TrainBackend {
   // lambdarank (K2 ranking)
   bool rank_ready_ = false, rank_regs_ = false, rank_lds_ = false;
   RankTables rank_{};
-  DevBuf<int32_t> rank_qb_, rank_scratch_;
+  DevBuf<int32_t> rank_qb_, rank_scratch_, rank_order_;
   std::vector<std::unique_ptr<DeviceValidSet>> vsets_;
   DevBuf<double> rank_imd_, rank_gain_, rank_lam_, rank_hes_, rank_disc_;
   int32_t* flags_ = nullptr;

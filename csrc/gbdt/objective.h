@@ -119,6 +119,8 @@ class Objective {
   const std::vector<int32_t>& query_boundaries() const { return qb_; }
   const std::vector<double>& inv_max_dcg() const { return inv_max_dcg_; }
   const std::vector<double>& label_gain() const { return label_gain_; }
+  const float* labels() const { return label_; }
+  int64_t num_rows() const { return n_; }
   int max_position() const { return max_position_; }
   bool lambdarank_norm() const { return lambdarank_norm_; }
 

@@ -734,7 +734,10 @@ __device__ __forceinline__ void DmaToLds16(__amdgpu_buffer_rsrc_t r, void* dst, 
 #endif
 }
 
-template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false, int kNB = 2>
+// kSched (2-buffer form): 0 issues tile kt + 1's DMA pieces ahead of tile kt's MFMAs; 1 splits them, the A
+// pieces before k-step 0 and the B pieces before k-step 1, so each piece's issue cost lands between MFMA
+// groups; 2 is 1 with the MFMA groups at raised wave priority (s_setprio 1)
+template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false, int kNB = 2, int kSched = 0>
 __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   static_assert(sizeof(T) == 2, "LDS-DMA conv is the f16 / bf16 form");
@@ -815,13 +818,15 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
 
   int lt = 0, lr = 0, ls = 0, lc0 = 0, lk0 = 0, toff = 0, loaded = 0;
   // DMA of the next K tile into LDS buffer `buf` (wave-uniform destination: 8 rows of 128 B per piece)
-  auto dma_tile = [&](int buf) {
+  auto dma_a = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bool ok = (amask[i] >> lt) & 1ull;
       const uint32_t vo = ok ? static_cast<uint32_t>((abase[i] + toff) * 2) : kOob;
       DmaToLds16(xres, As + (buf * BM + (wid * AI + i) * 8) * kBK, vo, lc0 * 2);
     }
+  };
+  auto dma_b = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       DmaToLds16(wres, Bs + (buf * BN + (wid * BI + i) * 8) * kBK, boff[i], lk0 * 2);
@@ -833,6 +838,8 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
         DmaToLds16(hres, Ps + buf * 512 + 256, po, lc0 * 4);
       }
     }
+  };
+  auto advance = [&]() {
     if (++loaded < nk) {
       lk0 += kBK;
       lc0 += kBK;
@@ -847,9 +854,13 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
       }
     }
   };
-  auto compute = [&](int buf) {
-#pragma unroll
-    for (int ks = 0; ks < kBK / 32; ++ks) {
+  auto dma_tile = [&](int buf) {
+    dma_a(buf);
+    dma_b(buf);
+    advance();
+  };
+  auto compute_ks = [&](int buf, int ks) {
+    {
       const int c = ks * 4 + (lane >> 4);  // 16-B chunk of the lane's k range
       V8 af[TM], bf[TN];
 #pragma unroll
@@ -878,11 +889,17 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
           }
         }
       }
+      if constexpr (kSched == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
+      if constexpr (kSched == 2) __builtin_amdgcn_s_setprio(0);
     }
+  };
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < kBK / 32; ++ks) compute_ks(buf, ks);
   };
   if constexpr (kNB == 3) {
     // Three buffers, two tiles in flight across the barrier: at step kt a wave retires only its own DMAs of
@@ -911,8 +928,20 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nk) dma_tile(buf ^ 1);
-      compute(buf);
+      if (kSched > 0 && kt + 1 < nk) {
+        static_assert(kBK / 32 == 2, "the split schedule interleaves two k-steps");
+        dma_a(buf ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_ks(buf, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        dma_b(buf ^ 1);
+        advance();
+        __builtin_amdgcn_sched_barrier(0);
+        compute_ks(buf, 1);
+      } else {
+        if (kt + 1 < nk) dma_tile(buf ^ 1);
+        compute(buf);
+      }
       __builtin_amdgcn_sched_barrier(0);  // keep the tile's MFMAs ahead of the DMA wait
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -965,11 +994,17 @@ void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
     return n;
   }();
   const bool deep = nb == 3 || (nb == 0 && blocks <= 2 * ncu);
+  static const int sched = [] {
+    const char* e = std::getenv("SML_CONV_GLDS_SCHED");
+    return e ? std::atoi(e) : 0;
+  }();
   if (a.in_scale) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, true>), dim3(blocks), dim3(kThr), 0, st, a);
   else if (deep && a.R * a.S * a.C >= 3 * 64)  // two K tiles in flight across the barrier
     hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 3>), dim3(blocks), dim3(kThr), 0, st, a);
   else if (single && a.R * a.S * a.C == 64)  // one K tile: no second buffer to fill (SML_CONV_GLDS_SINGLE=0: off)
     hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 1>), dim3(blocks), dim3(kThr), 0, st, a);
+  else if (sched == 1) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 2, 1>), dim3(blocks), dim3(kThr), 0, st, a);
+  else if (sched == 2) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 2, 2>), dim3(blocks), dim3(kThr), 0, st, a);
   else hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
 }
 

@@ -612,12 +612,11 @@ PYBIND11_MODULE(_vw, m) {
       })
       // model bytes in the host learner's format (vw_core.cpp VW::SaveModel), built from the device nonzeros
       .def("export_model", [](const GpuSgd& g, const std::string& args) {
-        std::vector<uint64_t> idx;
-        std::vector<float> val;
+        int64_t m = 0;
         double t, tw, snx;
         {
           py::gil_scoped_release rel;
-          g.ExportNonzeros(&idx, &val);
+          m = g.CountNonzeros();
           g.GlobalState(&t, &tw, &snx);
         }
         std::string s = "SMLVW001";
@@ -630,18 +629,21 @@ PYBIND11_MODULE(_vw, m) {
         put(static_cast<uint32_t>(4));
         put(t); put(tw); put(snx);
         put(g.min_label()); put(g.max_label());
-        put(static_cast<uint64_t>(idx.size()));
-        // (index, value) records: one resize + a parallel fill (a 2^30-slot model can hold ~1e8 nonzeros)
-        const size_t head = s.size();
-        s.resize(head + idx.size() * 12);
-        char* dst = &s[head];
-        const int64_t m = static_cast<int64_t>(idx.size());
-#pragma omp parallel for schedule(static) if (m > (1 << 16))
-        for (int64_t i = 0; i < m; ++i) {
-          std::memcpy(dst + i * 12, &idx[i], 8);
-          std::memcpy(dst + i * 12 + 8, &val[i], 4);
+        put(static_cast<uint64_t>(m));
+        // the (index, value) records go from the device straight into the bytes object (a 2^30-slot model
+        // can hold ~1e8 nonzeros: no host vectors, no second copy)
+        PyObject* out = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(s.size() + 12 * static_cast<size_t>(m)));
+        if (!out) throw py::error_already_set();
+        char* dst = PyBytes_AS_STRING(out);
+        std::memcpy(dst, s.data(), s.size());
+        try {
+          py::gil_scoped_release rel;
+          g.WriteRecords(dst + s.size());
+        } catch (...) {
+          Py_DECREF(out);
+          throw;
         }
-        return py::bytes(s);
+        return py::reinterpret_steal<py::bytes>(out);
       })
       // warm start from model bytes of either learner (same format)
       .def("import_model", [](GpuSgd& g, const std::string& bytes) {

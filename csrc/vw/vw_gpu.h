@@ -88,6 +88,10 @@ class GpuSgd {
   uint64_t NumWeights() const;
   // the table's nonzero components as (stride-4 index, value) - the host model format's records
   void ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val) const;
+  // the same records in the host model's byte layout: CountNonzeros() sizes the export, WriteRecords(dst)
+  // fills 12 * count bytes at dst (u64 stride-4 index + f32 value each, slot order)
+  int64_t CountNonzeros() const;
+  void WriteRecords(char* dst) const;
   void ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val);
   void GlobalState(double* t, double* total_weight, double* sum_norm_x) const;
   void SetGlobalState(double t, double total_weight, double sum_norm_x);
@@ -115,6 +119,8 @@ class GpuSgd {
   bool staged_weights_ = false;
   bool staged_costs_ = false;
   int64_t max_actions_ = 0;
+  mutable std::vector<int64_t> export_base_;  // per-4096-slot record offsets of the last CountNonzeros()
+  mutable int64_t export_count_ = 0;
   void ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1 = 0, int batch = 1);
   // per-row clamp bounds + loss reset before learning rows [r0, r1); loss read-back (and predictions) after
   void PrepLearn(int64_t r0, int64_t r1);

@@ -795,6 +795,40 @@ __global__ void unpack_kernel(float4* __restrict__ W, const int32_t* __restrict_
   }
 }
 
+// The same walk writing the host model's 12-byte records (u64 stride-4 index, f32 value; little-endian, so
+// three dword stores) straight into one device buffer: the export then moves each byte across PCIe once,
+// into the Python bytes object, with no per-field host vectors to interleave.
+__global__ __launch_bounds__(64) void write_rec_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per,
+                                                       const int64_t* __restrict__ base, uint32_t* __restrict__ rec) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * per, s1 = min(nw, s0 + per);
+  int64_t o = base[blockIdx.x];
+  for (uint64_t s = s0; s < s1; s += 64) {
+    const uint64_t my = s + lane;
+    const float4 v = my < s1 ? W[my] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int c = (v.x != 0.f) + (v.y != 0.f) + (v.z != 0.f);
+    int inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += t;
+    }
+    int64_t p = o + (inc - c);
+    const float vals[3] = {v.x, v.y, v.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (vals[k] != 0.f) {
+        const uint64_t ix = 4 * my + k;
+        uint32_t* r = rec + 3 * p++;
+        r[0] = static_cast<uint32_t>(ix);
+        r[1] = static_cast<uint32_t>(ix >> 32);
+        r[2] = __float_as_uint(vals[k]);
+      }
+    }
+    o += __shfl(inc, 63, 64);
+  }
+}
+
 __global__ void dirty_list_kernel(const uint8_t* __restrict__ dirty, int64_t nblk, const int32_t* __restrict__ pos,
                                   int32_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < nblk;
@@ -865,7 +899,10 @@ constexpr int kStage = 4;
 constexpr size_t kStageBytes = 32ull << 20;
 constexpr int kStageThreads = 8;
 
-// One per learner (its events are recorded on that learner's copy stream only), buffers allocated on first use.
+// One per process (SharedStager), buffers allocated on first use: 4 x 32 MiB of pinned memory cost ~4 ms per
+// hipHostMalloc, which a per-learner stager paid again on every fit (the first chunk of a pass waited
+// ~17 ms for them, r5 pass 11 trace). Callers hold `mu` for a whole copy sequence; a buffer's event may
+// have been recorded on another learner's copy stream, and waiting on it is still correct.
 struct Stager {
   std::mutex mu;
   char* buf[kStage] = {};
@@ -888,7 +925,7 @@ struct Stager {
       const int k = next;
       next = (next + 1) % kStage;
       if (!buf[k]) {
-        VW_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&buf[k]), kStageBytes, hipHostMallocDefault));
+        VW_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&buf[k]), kStageBytes, hipHostMallocPortable));
         VW_HIP_CHECK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
       }
       if (used[k]) VW_HIP_CHECK(hipEventSynchronize(ev[k]));
@@ -912,6 +949,11 @@ struct Stager {
 };
 }  // namespace
 
+static Stager& SharedStager() {
+  static Stager* st = new Stager();  // never destroyed: pinned buffers live for the process
+  return *st;
+}
+
 // Host-only check of the staging guard (it throws before any HIP call, so it runs without a GPU).
 bool StagerRejectsNull() {
   Stager st;
@@ -926,7 +968,7 @@ bool StagerRejectsNull() {
 
 struct GpuSgd::Impl {
   hipStream_t stream = nullptr, copy_stream = nullptr;
-  Stager stager;  // pinned host->device staging of pass data (copy_stream)
+  Stager& stager = SharedStager();  // pinned host->device staging of pass data (on this learner's copy_stream)
   std::vector<hipEvent_t> events;
   float4* W = nullptr;
   uint64_t nw = 0;
@@ -1684,6 +1726,79 @@ void GpuSgd::ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val)
   }
   PoolFree(cnt);
   PoolFree(base);
+}
+
+int64_t GpuSgd::CountNonzeros() const {
+  hipStream_t s = impl_->stream;
+  const uint64_t per = 4096;
+  const int64_t nb = static_cast<int64_t>((impl_->nw + per - 1) / per);
+  int32_t* cnt = nullptr;
+  PoolMalloc(&cnt, nb * sizeof(int32_t));
+  hipLaunchKernelGGL(count_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, s, impl_->W, impl_->nw, per, cnt);
+  std::vector<int32_t> hc(nb);
+  VW_HIP_CHECK(hipMemcpyAsync(hc.data(), cnt, nb * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  PoolFree(cnt);
+  export_base_.resize(nb);
+  int64_t tot = 0;
+  for (int64_t i = 0; i < nb; ++i) { export_base_[i] = tot; tot += hc[i]; }
+  export_count_ = tot;
+  return tot;
+}
+
+void GpuSgd::WriteRecords(char* dst) const {
+  const int64_t tot = export_count_;
+  if (tot <= 0) return;
+  hipStream_t s = impl_->stream;
+  const uint64_t per = 4096;
+  const int64_t nb = static_cast<int64_t>(export_base_.size());
+  int64_t* base = nullptr;
+  uint32_t* rec = nullptr;
+  PoolMalloc(&base, nb * sizeof(int64_t));
+  PoolMalloc(&rec, static_cast<size_t>(tot) * 12);
+  VW_HIP_CHECK(hipMemcpyAsync(base, export_base_.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(write_rec_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw, per, base,
+                     rec);
+  VW_HIP_CHECK(hipGetLastError());
+  // device -> pinned ring (the shared stager's buffers) -> dst, the host copy of piece k overlapping the DMA
+  // of piece k + 1 (a pageable D2H would bounce through the runtime's own staging at a fraction of the rate)
+  Stager& st = impl_->stager;
+  std::lock_guard<std::mutex> lk(st.mu);
+  const size_t bytes = static_cast<size_t>(tot) * 12;
+  const char* src = reinterpret_cast<const char*>(rec);
+  struct Piece { int k; size_t off, n; };
+  std::vector<Piece> inflight;
+  auto drain_one = [&]() {
+    const Piece pc = inflight.front();
+    inflight.erase(inflight.begin());
+    VW_HIP_CHECK(hipEventSynchronize(st.ev[pc.k]));
+    const size_t per_t = (pc.n + kStageThreads - 1) / kStageThreads;
+    std::vector<std::thread> th;
+    for (int t = 0; t < kStageThreads && t * per_t < pc.n; ++t) {
+      const size_t a0 = t * per_t, a1 = std::min(pc.n, a0 + per_t);
+      th.emplace_back([=, &st]() { std::memcpy(dst + pc.off + a0, st.buf[pc.k] + a0, a1 - a0); });
+    }
+    for (auto& x : th) x.join();
+  };
+  for (size_t off = 0; off < bytes; off += kStageBytes) {
+    const int k = st.next;
+    st.next = (st.next + 1) % kStage;
+    if (!st.buf[k]) {
+      VW_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st.buf[k]), kStageBytes, hipHostMallocPortable));
+      VW_HIP_CHECK(hipEventCreateWithFlags(&st.ev[k], hipEventDisableTiming));
+    }
+    if (st.used[k]) VW_HIP_CHECK(hipEventSynchronize(st.ev[k]));
+    const size_t n = std::min(kStageBytes, bytes - off);
+    VW_HIP_CHECK(hipMemcpyAsync(st.buf[k], src + off, n, hipMemcpyDeviceToHost, s));
+    VW_HIP_CHECK(hipEventRecord(st.ev[k], s));
+    st.used[k] = true;
+    inflight.push_back({k, off, n});
+    if (inflight.size() >= 2) drain_one();
+  }
+  while (!inflight.empty()) drain_one();
+  VW_HIP_CHECK(hipStreamSynchronize(s));
+  PoolFree(base);
+  PoolFree(rec);
 }
 
 void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val) {

@@ -297,6 +297,88 @@ def test_gpu_lambdarank_gradients_match_host(maxpos):
     np.testing.assert_allclose(bg.train_scores(), pg, rtol=1e-5, atol=1e-5)
 
 
+def test_gpu_lambdarank_monotone_gain_form_is_bitwise(monkeypatch):
+    """With strictly increasing label gains the register kernel takes the pair's orientation from the sign
+    of the gain difference (no label compare); it must give bitwise the gradients and trees of the
+    label-compare form, through the all-tied first iteration (exact tie-aware ranks) and the later ones
+    (strict ranks, checked for ties by the rank -> document scatter)."""
+    X, y, sizes = _rank_data(long_queries=False)
+    p = "objective=lambdarank num_leaves=15 min_data_in_leaf=5 eval_at=5 max_position=20 device_type=gpu"
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("SML_RANK_MONO", v)
+        b = _train_rank(X, y, sizes, p, 4)
+        out[v] = (b.gradients(), b.save_model_string())
+    (g0, h0), m0 = out["0"]
+    (g1, h1), m1 = out["1"]
+    assert np.array_equal(g0, g1) and np.array_equal(h0, h1)
+    assert m0 == m1
+
+
+def _lambdarank_oracle(score, label, sizes, max_position=20, sigma=1.0, norm=True):
+    """numpy LambdaRank gradients (LightGBM's rank_objective: stable-sort ranks with ties by index, pairs of
+    different labels with min(rank) < max_position, |delta DCG| scaled by 1 / (0.01 + |ds|) when the query's
+    scores differ, log2(1 + sum) / sum normalisation), fp64 throughout"""
+    gain = 2.0 ** np.arange(31) - 1.0
+    g = np.zeros(len(score))
+    h = np.zeros(len(score))
+    b = 0
+    for c in sizes:
+        sc, lb = score[b:b + c], label[b:b + c].astype(int)
+        order = np.argsort(-sc, kind="stable")
+        rk = np.empty(c, int)
+        rk[order] = np.arange(c)
+        disc = 1.0 / np.log2(2.0 + rk)
+        ideal = np.sort(gain[np.minimum(lb, 30)])[::-1][:max_position]
+        mdcg = (ideal / np.log2(2.0 + np.arange(len(ideal)))).sum()
+        imd = 1.0 / mdcg if mdcg > 0 else 0.0
+        use_norm = norm and sc.max() != sc.min()
+        lam = np.zeros(c)
+        hes = np.zeros(c)
+        suml = 0.0
+        for i in range(c):
+            for j in range(i + 1, c):
+                if lb[i] == lb[j] or min(rk[i], rk[j]) >= max_position:
+                    continue
+                hi, lo = (i, j) if lb[i] > lb[j] else (j, i)
+                ds = sc[hi] - sc[lo]
+                dn = (gain[min(lb[hi], 30)] - gain[min(lb[lo], 30)]) * abs(disc[hi] - disc[lo]) * imd
+                if use_norm:
+                    dn /= 0.01 + abs(ds)
+                p = 1.0 / (1.0 + np.exp(sigma * ds))
+                pl = -sigma * dn * p
+                ph = sigma * sigma * dn * p * (1.0 - p)
+                lam[hi] += pl
+                lam[lo] -= pl
+                hes[hi] += ph
+                hes[lo] += ph
+                suml -= 2.0 * pl
+        nf = np.log2(1.0 + suml) / suml if (norm and suml > 0) else 1.0
+        g[b:b + c] = lam * nf
+        h[b:b + c] = hes * nf
+        b += c
+    return g, h
+
+
+def test_gpu_lambdarank_ties_after_first_iteration():
+    """Duplicate documents keep tied scores on every iteration: the strict-rank fast path must detect the
+    ties (rank -> document scatter) and fall back to the index-ordered ranks. The kernel's gradients at
+    iteration 3 against a numpy LambdaRank oracle evaluated on the same (tied) scores."""
+    X, y, sizes = _rank_data(long_queries=False)
+    X = X.copy()
+    X[1::2] = X[0::2][: len(X[1::2])]  # every odd row duplicates its predecessor's features
+    p = "objective=lambdarank num_leaves=15 min_data_in_leaf=5 eval_at=5 max_position=20 device_type=gpu"
+    bg = _train_rank(X, y, sizes, p, 2)
+    s2 = np.asarray(bg.train_scores(), np.float64).reshape(-1)
+    assert len(np.unique(s2)) < len(s2) - len(s2) // 4  # ties survive training
+    bg.update()
+    gg, hg = bg.gradients()
+    go, ho = _lambdarank_oracle(s2, y, sizes)
+    scale = np.abs(go).max()
+    np.testing.assert_allclose(gg, go, rtol=1e-4, atol=1e-5 * scale)
+    np.testing.assert_allclose(hg, ho, rtol=1e-4, atol=1e-5 * np.abs(ho).max())
+
+
 def test_gpu_lambdarank_transpose_reduce_is_bitwise(monkeypatch):
     """The lambdarank register kernel's transpose-reduced top-document sums (eight documents per round of
     shuffles) use WaveSumF's xor pairing: gradients bitwise equal to one wave sum per top document."""

@@ -50,7 +50,10 @@ def main():
         dt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[sys.argv[sys.argv.index("--dtype") + 1]]
     print(f"dtype {dt}")
     tot_m, tot_t, tot_floor = 0.0, 0.0, 0.0
-    for C, H, Co, k, st in (SHAPES[:4] if quick else SHAPES):
+    shapes = SHAPES[:4] if quick else SHAPES
+    if "--only" in sys.argv:  # e.g. --only 1,4,8: the ResNet-50 3x3 layers (profiling runs)
+        shapes = [SHAPES[int(i)] for i in sys.argv[sys.argv.index("--only") + 1].split(",")]
+    for C, H, Co, k, st in shapes:
         x = torch.randn(B, C, H, H, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
         w = (torch.randn(Co, C, k, k, device="cuda") / (C * k * k) ** 0.5).to(dt)
         wp = pack_weight(w, dt)

@@ -89,6 +89,15 @@ def estimator_bench(args, world: int, rank: int) -> None:
     torch.cuda.synchronize()
     D.barrier()
     elapsed = time.perf_counter() - t0
+    if args.profile and rank == 0:  # host-side breakdown of one more fit (outside the timed region)
+        import cProfile
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        est.fit(df)
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
     if world > 1:
         import torch.distributed as dist
 
@@ -111,6 +120,7 @@ def estimator_bench(args, world: int, rank: int) -> None:
                           "export_model": ph.get("timeExportNs"),
                           "export_model_and_other": round(fit_ms - ph["timeTotalNs"], 2)},
             "sync_mib": round(stats[-1]["syncBytes"] / 2 ** 20, 2), "holdout_logloss": round(logloss, 4),
+            "model_mib": round(len(model.getNativeModel()) / 2 ** 20, 2),
             "timed_region": "VowpalWabbitClassifier(numBits, deviceType='gpu').fit(df) end to end (DataFrame built "
                             "before timing)",
             "data": "synthetic hashed sparse (Zipf ids from a 2^24 vocabulary, planted linear model)"}), flush=True)
@@ -128,6 +138,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=16384, help="hogwild mini-batch (examples in flight)")
+    ap.add_argument("--profile", action="store_true", help="estimator mode: cProfile one extra fit (stderr)")
     ap.add_argument("--resident", action="store_true",
                     help="kernel mode: the pass is staged in HBM once and every step re-learns it from there")
     args = ap.parse_args()
