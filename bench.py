@@ -105,6 +105,7 @@ def main() -> None:
     ap.add_argument("--iterations", type=int, default=100, help="numIterations of each fit (reference default 100)")
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--save-model", default=None, help="write the last model's text here (after timing)")
+    ap.add_argument("--profile", action="store_true", help="cProfile one more fit after timing (stderr, host side)")
     ap.add_argument("--allow-shared-device", action="store_true",
                     help="rehearsal only: allow more ranks than visible GPUs (ranks share devices)")
     args = ap.parse_args()
@@ -188,6 +189,16 @@ def main() -> None:
     D.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    if args.profile and world == 1:  # outside the timed region (one rank: a fit is collective)
+        import cProfile
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        est.fit(df).getNativeModel()
+        sync()
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(35)
     if world > 1:
         import torch.distributed as dist
 

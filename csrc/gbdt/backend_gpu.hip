@@ -242,6 +242,7 @@ struct RankTables {
   int nq, ngain, max_position, norm;
   int gain_mono;  // label gains strictly increasing (the register kernel's kMono form)
   int nreg;
+  int rank_src;   // where the rank loop reads partner scores (LambdarankQueryRegs)
   double sigma;
 };
 constexpr int kGainLds = 64;  // label gains staged in LDS by the register kernel (longer tables: global)
@@ -543,6 +544,7 @@ __device__ __forceinline__ double ReadLaneD(double v, int l) {
 // the top list's per-document values, staged by rank in LDS by their owning lanes (lane r of the wave reads
 // rank r's; no second global load of the top documents' scores / labels)
 struct RankTop {
+  double all[kRankLds];  // every document's score (the rank loop's broadcast partner reads)
   double sc[64];
   float gn[64];
   int lab[64];
@@ -582,24 +584,31 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   double sup[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) sup[u] = nextafter(sc[u], INFINITY);
-  auto count_ranks = [&](bool ties) {
+  // Partner scores (t.rank_src, A/B): 0 scalar loads through the constant address space (8 partners per
+  // s_load_dwordx16), 1 a v_readlane pair from the owning lane, 2 broadcast reads of the wave's LDS copy
+  // (r5 pass 14: 660 vs 600 us for the scalar loads)
+  const int src = t.rank_src;
+  if (src == 2) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      if (u * 64 + lane < cnt) top.all[u * 64 + lane] = sc[u];
+    WaveSync();
+  }
+  // the rank loop, instantiated per partner source (the switch stays outside the partner loop)
+  auto rank_loop = [&](auto get, bool ties) {
 #pragma unroll
     for (int v = 0; v < NU; ++v) {
       if (v * 64 >= cnt) break;
       const int jn = min(64, cnt - v * 64);
-      // wave-uniform partner scores through the constant address space: s_load into SGPRs (read-only data),
-      // no v_readlane pair + hazard per partner
-      const __attribute__((address_space(4))) double* sv =
-          (const __attribute__((address_space(4))) double*)(score + b + v * 64);
       if (!ties) {
         for (int jj = 0; jj < jn; ++jj) {
-          const double sj = sv[jj];
+          const double sj = get(v, jj);
 #pragma unroll
           for (int u = 0; u < NU; ++u) rk[u] += sj >= sup[u] ? 1 : 0;
         }
       } else {
         for (int jj = 0; jj < jn; ++jj) {
-          const double sj = sv[jj];
+          const double sj = get(v, jj);
 #pragma unroll
           for (int u = 0; u < NU; ++u) {
             if (u < v) rk[u] += sj >= sup[u] ? 1 : 0;         // every j of slot v is after i
@@ -608,6 +617,17 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
           }
         }
       }
+    }
+  };
+  auto count_ranks = [&](bool ties) {
+    if (src == 1) {
+      rank_loop([&](int v, int jj) { return ReadLaneD(sc[v], jj); }, ties);
+    } else if (src == 2) {
+      rank_loop([&](int v, int jj) { return top.all[v * 64 + jj]; }, ties);
+    } else {
+      const __attribute__((address_space(4))) double* sv =
+          (const __attribute__((address_space(4))) double*)(score + b);
+      rank_loop([&](int v, int jj) { return sv[v * 64 + jj]; }, ties);
     }
   };
   auto scatter = [&]() {  // rank -> doc map (every document's slot)
@@ -4117,6 +4137,8 @@ class GpuBackend : public TrainBackend {
     }
     const char* me = std::getenv("SML_RANK_MONO");  // 0: the label-compare form (A/B and tests), read per booster
     rank_.gain_mono = me && std::atoi(me) == 0 ? 0 : (mono ? 1 : 0);
+    const char* se = std::getenv("SML_RANK_SRC");  // partner scores of the rank loop: 0 s_load, 1 readlane, 2 LDS
+    rank_.rank_src = se ? std::atoi(se) : 0;
     rank_ready_ = true;
   }
 

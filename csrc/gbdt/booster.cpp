@@ -571,8 +571,11 @@ std::string Booster::SaveModelToString(int start_iteration, int num_iteration, i
   for (size_t i = 0; i < feature_infos_.size(); ++i) o << (i ? " " : "") << feature_infos_[i];
   o << "\n";
   auto r = TreeRange(start_iteration, num_iteration);
-  std::vector<std::string> blocks;
-  for (int t = r.first; t < r.second; ++t) blocks.push_back(trees_[t].ToString(t - r.first));
+  // the trees' text blocks are independent: one per thread (a 100-tree model took ~5 ms serially, inside
+  // every timed fit that returns the model text)
+  std::vector<std::string> blocks(static_cast<size_t>(std::max(0, r.second - r.first)));
+#pragma omp parallel for schedule(dynamic, 4) if (blocks.size() > 8)
+  for (int t = r.first; t < r.second; ++t) blocks[t - r.first] = trees_[t].ToString(t - r.first);
   o << "tree_sizes=";
   for (size_t i = 0; i < blocks.size(); ++i) o << (i ? " " : "") << blocks[i].size();
   o << "\n\n";

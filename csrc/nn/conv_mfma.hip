@@ -734,10 +734,10 @@ __device__ __forceinline__ void DmaToLds16(__amdgpu_buffer_rsrc_t r, void* dst, 
 #endif
 }
 
-// kSched (2-buffer form): 0 issues tile kt + 1's DMA pieces ahead of tile kt's MFMAs; 1 splits them, the A
-// pieces before k-step 0 and the B pieces before k-step 1, so each piece's issue cost lands between MFMA
-// groups; 2 is 1 with the MFMA groups at raised wave priority (s_setprio 1)
-template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false, int kNB = 2, int kSched = 0>
+// (r5 pass 13 A/B, ResNet-50 b128 per layer: issuing the next tile's A pieces before k-step 0 and its B pieces
+// before k-step 1 - with or without s_setprio around the MFMA groups - measured 2-10 % slower than issuing
+// them all ahead of the tile's MFMAs, so the pieces stay together)
+template <class T, int BM, int BN, int kThr, int kWN, bool kPro = false, int kNB = 2>
 __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
   typedef typename Vec<T>::type V8;
   static_assert(sizeof(T) == 2, "LDS-DMA conv is the f16 / bf16 form");
@@ -889,12 +889,10 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
           }
         }
       }
-      if constexpr (kSched == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = Vec<T>::mfma(af[i], bf[j], acc[i][j]);
-      if constexpr (kSched == 2) __builtin_amdgcn_s_setprio(0);
     }
   };
   auto compute = [&](int buf) {
@@ -928,20 +926,8 @@ __global__ __launch_bounds__(kThr) void conv_glds_kernel(ConvArgs a) {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      if (kSched > 0 && kt + 1 < nk) {
-        static_assert(kBK / 32 == 2, "the split schedule interleaves two k-steps");
-        dma_a(buf ^ 1);
-        __builtin_amdgcn_sched_barrier(0);
-        compute_ks(buf, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        dma_b(buf ^ 1);
-        advance();
-        __builtin_amdgcn_sched_barrier(0);
-        compute_ks(buf, 1);
-      } else {
-        if (kt + 1 < nk) dma_tile(buf ^ 1);
-        compute(buf);
-      }
+      if (kt + 1 < nk) dma_tile(buf ^ 1);
+      compute(buf);
       __builtin_amdgcn_sched_barrier(0);  // keep the tile's MFMAs ahead of the DMA wait
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -978,11 +964,11 @@ void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
     const char* e = std::getenv("SML_CONV_GLDS_SINGLE");
     return !e || std::atoi(e) != 0;
   }();
-  // SML_CONV_GLDS_NB=2 / 3 forces a depth; unset: three buffers only for launches of at most two blocks per CU.
-  // r5 pass 10, ResNet-50 b128 per layer: the 3-buffer form halves the resident 128x128 blocks (96 KB of
-  // LDS), which costs the many-block layers 10-40 % (occupancy hid more than the pipeline does), and wins
-  // where the grid is below two blocks per CU anyway (512 3x3 at 7x7: 52.9 -> 46.7 us; 2048 -> 512 1x1:
-  // 27.9 -> 23.1 us)
+  // SML_CONV_GLDS_NB=2 / 3 forces a depth; unset: three buffers only for launches of at most one block per CU.
+  // r5 passes 10 / 13, ResNet-50 b128 per layer: the 3-buffer form halves the resident 128x128 blocks (96 KB
+  // of LDS), which costs every layer with more blocks than CUs 10-40 % (occupancy hid more than the pipeline
+  // does; the 392-block 256 3x3 at 14x14: 39.6 -> 52-56 us), and wins where the grid is below one block per
+  // CU anyway (the 196-block 512 3x3 at 7x7: 52.9 -> 46.7 us; 2048 -> 512 1x1: 27.9 -> 23.1 us)
   static const int nb = [] {
     const char* e = std::getenv("SML_CONV_GLDS_NB");
     return e ? std::atoi(e) : 0;
@@ -993,18 +979,13 @@ void LaunchGlds(const ConvArgs& a, int M, hipStream_t st) {
       n = 256;
     return n;
   }();
-  const bool deep = nb == 3 || (nb == 0 && blocks <= 2 * ncu);
-  static const int sched = [] {
-    const char* e = std::getenv("SML_CONV_GLDS_SCHED");
-    return e ? std::atoi(e) : 0;
-  }();
+  const bool deep = nb == 3 || (nb == 0 && blocks <= ncu);
+
   if (a.in_scale) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, true>), dim3(blocks), dim3(kThr), 0, st, a);
   else if (deep && a.R * a.S * a.C >= 3 * 64)  // two K tiles in flight across the barrier
     hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 3>), dim3(blocks), dim3(kThr), 0, st, a);
   else if (single && a.R * a.S * a.C == 64)  // one K tile: no second buffer to fill (SML_CONV_GLDS_SINGLE=0: off)
     hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 1>), dim3(blocks), dim3(kThr), 0, st, a);
-  else if (sched == 1) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 2, 1>), dim3(blocks), dim3(kThr), 0, st, a);
-  else if (sched == 2) hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN, false, 2, 2>), dim3(blocks), dim3(kThr), 0, st, a);
   else hipLaunchKernelGGL((conv_glds_kernel<T, BM, BN, kThr, kWN>), dim3(blocks), dim3(kThr), 0, st, a);
 }
 

@@ -151,11 +151,16 @@ PYBIND11_MODULE(_vw, m) {
       std::vector<uint8_t> has;
       std::vector<int32_t> mc, ccls;
       std::vector<int64_t> cptr{0};
-      std::vector<float> ccost;
+      std::vector<float> ccost, cact, ccst, cpdf;
+      std::vector<uint8_t> chas;
       for (const auto& e : exs) {
         rows.push_back(&e);
         lab.push_back(e.l.label);
         w.push_back(e.l.weight);
+        cact.push_back(e.l.cats_action);
+        ccst.push_back(e.l.cats_cost);
+        cpdf.push_back(e.l.cats_pdf);
+        chas.push_back(e.l.cats_has ? 1 : 0);
         has.push_back(e.l.has_label || e.l.multiclass > 0 || !e.l.costs.empty() ? 1 : 0);
         mc.push_back(e.l.multiclass);
         for (const auto& c : e.l.costs) { ccls.push_back(c.first); ccost.push_back(c.second); }
@@ -169,6 +174,10 @@ PYBIND11_MODULE(_vw, m) {
       d["cptr"] = py::array_t<int64_t>(cptr.size(), cptr.data());
       d["ccls"] = py::array_t<int32_t>(ccls.size(), ccls.data());
       d["ccost"] = py::array_t<float>(ccost.size(), ccost.data());
+      d["cats_action"] = py::array_t<float>(cact.size(), cact.data());
+      d["cats_cost"] = py::array_t<float>(ccst.size(), ccst.data());
+      d["cats_pdf"] = py::array_t<float>(cpdf.size(), cpdf.data());
+      d["cats_has"] = py::array_t<uint8_t>(chas.size(), chas.data());
       return d;
     }
     std::vector<const Example*> shared, actions;
@@ -459,7 +468,11 @@ PYBIND11_MODULE(_vw, m) {
       .def_readwrite("csoaa", &GpuSgdConfig::csoaa)
       .def_readwrite("cb", &GpuSgdConfig::cb)
       .def_readwrite("cb_explore", &GpuSgdConfig::cb_explore)
-      .def_readwrite("epsilon", &GpuSgdConfig::epsilon);
+      .def_readwrite("epsilon", &GpuSgdConfig::epsilon)
+      .def_readwrite("cats", &GpuSgdConfig::cats)
+      .def_readwrite("cats_min", &GpuSgdConfig::cats_min)
+      .def_readwrite("cats_max", &GpuSgdConfig::cats_max)
+      .def_readwrite("cats_bw", &GpuSgdConfig::cats_bw);
   py::class_<GpuSgd, std::shared_ptr<GpuSgd>>(m, "GpuSgd")
       .def(py::init([](const GpuSgdConfig& c, int dev) { return std::make_shared<GpuSgd>(c, dev); }),
            py::arg("config"), py::arg("device") = -1)
@@ -551,6 +564,14 @@ PYBIND11_MODULE(_vw, m) {
              if (cls.size() < cptr.data()[n] || cost.size() < cptr.data()[n]) throw std::runtime_error("cost lists too short");
              py::gil_scoped_release rel;
              g.StageCosts(cptr.data(), cls.data(), cost.data(), n);
+           })
+      .def("stage_cats",
+           [](GpuSgd& g, F32 action, F32 cost, F32 pdf, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> has) {
+             const int64_t n = has.size();
+             if (action.size() != n || cost.size() != n || pdf.size() != n)
+               throw std::runtime_error("action / cost / pdf / has need one entry per row");
+             py::gil_scoped_release rel;
+             g.StageCats(action.data(), cost.data(), pdf.data(), has.data(), n);
            })
       .def("stage_cb",
            [](GpuSgd& g, I64 aip, py::array_t<int32_t, py::array::c_style | py::array::forcecast> chosen, F32 cost,

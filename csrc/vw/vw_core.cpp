@@ -213,6 +213,9 @@ std::map<std::string, std::string> VW::DescribeArgs(const std::string& args) {
   d["csoaa"] = std::to_string(v.csoaa_);
   d["cb_adf"] = v.cb_adf_ ? "1" : "0";
   d["cats"] = std::to_string(v.cats_k_);
+  d["min_value"] = f(v.min_value_);
+  d["max_value"] = f(v.max_value_);
+  d["bandwidth"] = f(v.bandwidth_);
   int ng = v.ngram_;
   for (int g : v.ngram_ns_) ng = std::max(ng, g);
   d["ngram"] = std::to_string(ng);

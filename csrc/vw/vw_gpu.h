@@ -28,6 +28,8 @@ struct GpuSgdConfig {
   int oaa = 0;           // one-against-all classes (0: scalar learner)
   int csoaa = 0;         // cost-sensitive one-against-all classes (0: off)
   int cb = -1;           // contextual bandit with action-dependent features: -1 off, 0 mtr, 1 dr, 2 ips
+  int cats = 0;          // --cats_pdf / --cats K discretized actions (0: off): the filter tree of K leaves
+  float cats_min = 0.f, cats_max = 1.f, cats_bw = 1.f;  // --min_value / --max_value / --bandwidth
   bool cb_explore = false;
   float epsilon = 0.05f;
 };
@@ -76,6 +78,8 @@ class GpuSgd {
                  int batch = 1);
   void StageCosts(const int64_t* cptr, const int32_t* cls, const float* cost, int64_t n);
   void StageCb(const int64_t* aip, const int32_t* chosen, const float* cost, const float* prob, int64_t n_examples);
+  // CATS labels of the staged rows (action, cost, logged pdf; has = 0: no label, prediction only)
+  void StageCats(const float* action, const float* cost, const float* pdf, const uint8_t* has, int64_t n);
   // predictions of every staged row (scalar: clamped score; oaa / csoaa: 1-based class; cb: action scores,
   // plus the greedy action per example in *best)
   void PredictStaged(float* out, float* best);
@@ -119,8 +123,13 @@ class GpuSgd {
   bool staged_weights_ = false;
   bool staged_costs_ = false;
   int64_t max_actions_ = 0;
+  std::vector<float> cats_cost_;   // staged CATS costs / label flags: the host builds each example's
+  std::vector<uint8_t> cats_has_;  // control-variate baseline (a running mean over the labelled examples)
+  double cats_cost_sum_ = 0, cats_cost_n_ = 0;
   mutable std::vector<int64_t> export_base_;  // per-4096-slot record offsets of the last CountNonzeros()
   mutable int64_t export_count_ = 0;
+  mutable uint32_t* export_reg_ = nullptr;  // one-scan export: per-block record regions + counts (device)
+  mutable int32_t* export_cnt_ = nullptr;
   void ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1 = 0, int batch = 1);
   // per-row clamp bounds + loss reset before learning rows [r0, r1); loss read-back (and predictions) after
   void PrepLearn(int64_t r0, int64_t r1);

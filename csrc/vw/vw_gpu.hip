@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -464,6 +465,87 @@ __global__ __launch_bounds__(64 * kOaaMaxWaves) void oaa_kernel(SgdArgs a) {
                                                  k + 1 == y ? 1.f : -1.f, imp, lane);
 }
 
+// ---------------------------------------------------------------- CATS (--cats_pdf / --cats)
+// Continuous actions over [min, max] discretized into K centroids, a filter tree of 2^depth leaves whose
+// internal nodes are binary learners at their own table offsets (vw_core.cpp CatsPredictLeaf / CatsLearn).
+// One wave per example: the leaf its current routing reaches (the progressive prediction), then - labelled
+// examples - the IPS estimate of every leaf's smoothed cost with the control-variate baseline (the running
+// mean cost, from the host: `base`) and the bottom-up tournament, each node with both children real learning
+// which child's winner is cheaper, weighted by the difference, in the host learner's node order.
+struct CatsArgs {
+  const float* act;
+  const float* cost;
+  const float* pdf;
+  const float* base;
+  const uint8_t* has;
+  int k, depth;
+  float vmin, vmax, bw;
+};
+
+__device__ __forceinline__ uint64_t CatsOff(int node) { return static_cast<uint64_t>(node + 1) * 2654435761ull; }
+
+__global__ __launch_bounds__(64) void cats_kernel(SgdArgs a, CatsArgs c) {
+  const int lane = threadIdx.x;
+  const int64_t e = a.n0 + blockIdx.x;
+  if (e >= a.n1) return;
+  extern __shared__ float cats_lds[];  // win[2L - 1], then valid[2L - 1] (0 / 1)
+  const int L = 1 << c.depth;
+  float* win = cats_lds;
+  float* valid = cats_lds + (2 * L - 1);
+  const int64_t b = a.indptr[e], en = a.indptr[e + 1];
+  if (a.preds) {
+    int node = 0;
+    for (int d = 0; d < c.depth; ++d) {
+      // right only when its subtree holds a real action (K need not be a power of two)
+      const int right = 2 * node + 2;
+      int fl = right;
+      while (fl < L - 1) fl = 2 * fl + 1;
+      const bool right_ok = fl - (L - 1) < c.k;
+      const float sc = Dot(a, b, en, CatsOff(node), lane);
+      node = (sc > 0.f && right_ok) ? right : 2 * node + 1;
+    }
+    if (lane == 0) a.preds[e] = static_cast<float>(node - (L - 1));  // leaf: the host maps it to the pdf / action
+  }
+  if (!a.learn || !c.has[e]) return;
+  const float bb = c.base[e];
+  const float unit = (c.vmax - c.vmin) / c.k;
+  const float p = fmaxf(c.pdf[e], 1e-12f);
+  const float act = c.act[e], cost = c.cost[e];
+  for (int i = lane; i < 2 * L - 1; i += 64) {
+    win[i] = bb;
+    valid[i] = 0.f;
+  }
+  __syncthreads();
+  for (int k = lane; k < c.k; k += 64) {
+    const float ctr = c.vmin + (k + 0.5f) * unit;
+    const float lo = fmaxf(c.vmin, ctr - c.bw), hi = fminf(c.vmax, ctr + c.bw);
+    valid[L - 1 + k] = 1.f;
+    if (act >= lo && act <= hi) win[L - 1 + k] = bb + (cost - bb) / ((hi - lo) * p);
+  }
+  __syncthreads();
+  if (lane == 0) atomicAdd(a.loss_acc, cost);
+  for (int node = L - 2; node >= 0; --node) {
+    const int l = 2 * node + 1, r = 2 * node + 2;
+    const bool vl = valid[l] != 0.f, vr = valid[r] != 0.f;
+    const float wl = win[l], wr = win[r];
+    float wn;
+    if (!vl || !vr) {
+      wn = vl ? wl : wr;
+    } else {
+      const float sc = Dot(a, b, en, CatsOff(node), lane);
+      const float imp = fabsf(wl - wr);
+      if (imp > 0.f) UpdateWave(a, b, en, CatsOff(node), sc, wr < wl ? 1.f : -1.f, imp, lane);
+      wn = sc > 0.f ? wr : wl;
+    }
+    __syncthreads();  // every lane has read the children before lane 0 writes the node
+    if (lane == 0) {
+      valid[node] = (vl || vr) ? 1.f : 0.f;
+      win[node] = wn;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- device featurization
 // The learner's example CSR is built on the device from the namespace blocks (one CSR per feature column,
 // already hashed): base features of every namespace, then each interaction's crosses, then VW's constant.
@@ -829,6 +911,59 @@ __global__ __launch_bounds__(64) void write_rec_kernel(const float4* __restrict_
   }
 }
 
+// One-scan export: block b (one per `per` slots) writes its records into its own region of `cap` records
+// (any order of blocks, slot order within one) and its count; a block past `cap` records stops writing and
+// reports the count, and the host then takes the two-scan path. rec_compact_kernel packs the regions.
+__global__ __launch_bounds__(64) void write_rec_region_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per,
+                                                              int cap, uint32_t* __restrict__ reg,
+                                                              int32_t* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * per, s1 = min(nw, s0 + per);
+  uint32_t* rec = reg + static_cast<uint64_t>(blockIdx.x) * cap * 3;
+  int64_t o = 0;
+  for (uint64_t s = s0; s < s1; s += 64) {
+    const uint64_t my = s + lane;
+    const float4 v = my < s1 ? W[my] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int c = (v.x != 0.f) + (v.y != 0.f) + (v.z != 0.f);
+    int inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += t;
+    }
+    int64_t p = o + (inc - c);
+    const float vals[3] = {v.x, v.y, v.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (vals[k] != 0.f) {
+        if (p < cap) {
+          const uint64_t ix = 4 * my + k;
+          uint32_t* r = rec + 3 * p;
+          r[0] = static_cast<uint32_t>(ix);
+          r[1] = static_cast<uint32_t>(ix >> 32);
+          r[2] = __float_as_uint(vals[k]);
+        }
+        ++p;
+      }
+    }
+    o += __shfl(inc, 63, 64);
+  }
+  if (lane == 0) cnt[blockIdx.x] = static_cast<int32_t>(o);
+}
+
+// region b's records -> out at base[b] (12-byte records as dwords)
+__global__ __launch_bounds__(256) void rec_compact_kernel(const uint32_t* __restrict__ reg, int cap,
+                                                          const int32_t* __restrict__ cnt,
+                                                          const int64_t* __restrict__ base, int64_t nb,
+                                                          uint32_t* __restrict__ out) {
+  for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const int n3 = cnt[b] * 3;
+    const uint32_t* src = reg + static_cast<uint64_t>(b) * cap * 3;
+    uint32_t* dst = out + base[b] * 3;
+    for (int i = threadIdx.x; i < n3; i += blockDim.x) dst[i] = src[i];
+  }
+}
+
 __global__ void dirty_list_kernel(const uint8_t* __restrict__ dirty, int64_t nblk, const int32_t* __restrict__ pos,
                                   int32_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < nblk;
@@ -983,6 +1118,8 @@ struct GpuSgd::Impl {
   int64_t *cptr = nullptr, *aip = nullptr;
   int32_t *ccls = nullptr, *chosen = nullptr;
   float *ccost = nullptr, *cbcost = nullptr, *cbprob = nullptr, *best = nullptr;
+  float *cats_act = nullptr, *cats_cost = nullptr, *cats_pdf = nullptr, *cats_base = nullptr;
+  uint8_t* cats_has = nullptr;
   double* cbstats = nullptr;
   ExpandSpec* spec = nullptr;
   // sync scratch
@@ -1020,6 +1157,9 @@ struct GpuSgd::Impl {
                     static_cast<void*>(cbprob), static_cast<void*>(best), static_cast<void*>(cbstats),
                     static_cast<void*>(spec)})
       (void)hipFree(q);
+    for (void* q : {static_cast<void*>(cats_act), static_cast<void*>(cats_cost), static_cast<void*>(cats_pdf),
+                    static_cast<void*>(cats_base), static_cast<void*>(cats_has)})
+      PoolFree(q);
     for (void* q : {static_cast<void*>(W), static_cast<void*>(indptr), static_cast<void*>(idx), static_cast<void*>(val),
                     static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo), static_cast<void*>(hi),
                     static_cast<void*>(pred)})
@@ -1071,7 +1211,10 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
   if (device >= 0) VW_HIP_CHECK(hipSetDevice(device));
   if (cfg.oaa > 256) throw std::runtime_error("GPU oaa supports at most 256 classes");
   if (cfg.csoaa > 256) throw std::runtime_error("GPU csoaa supports at most 256 classes");
-  if ((cfg.oaa > 0) + (cfg.csoaa > 0) + (cfg.cb >= 0) > 1) throw std::runtime_error("one reduction at a time");
+  if ((cfg.oaa > 0) + (cfg.csoaa > 0) + (cfg.cb >= 0) + (cfg.cats > 0) > 1) throw std::runtime_error("one reduction at a time");
+  if (cfg.cats == 1 || cfg.cats > 4096) throw std::runtime_error("GPU CATS supports 2..4096 discrete actions");
+  if (cfg.cats > 0 && !(cfg.cats_max > cfg.cats_min && cfg.cats_bw > 0.f))
+    throw std::runtime_error("GPU CATS needs min_value < max_value and bandwidth > 0");
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
   impl_->nw = 1ull << cfg.bits;
@@ -1086,11 +1229,15 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
   VW_HIP_CHECK(hipMemsetAsync(impl_->cbstats, 0, 3 * sizeof(double), impl_->stream));
   VW_HIP_CHECK(hipMalloc(&impl_->loss, sizeof(float)));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), impl_->stream));
-  VW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
+  // no wait here: every later use of the table is ordered behind the zeroing on this stream, and the
+  // caller's host work (featurization, labels) overlaps the 16 GiB memset of a 2^30 table (~2.8 ms)
   if (cfg.loss == 1) { min_label_ = -50.0; max_label_ = 50.0; }
 }
 
-GpuSgd::~GpuSgd() = default;
+GpuSgd::~GpuSgd() {
+  PoolFree(export_reg_);  // an export counted but never written
+  PoolFree(export_cnt_);
+}
 
 namespace {
 SgdArgs BaseArgs(const GpuSgdConfig& c) {
@@ -1116,7 +1263,16 @@ void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
   a.hi = impl_->hi;
   a.n0 = b0; a.n1 = b1; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
   a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = learn ? 1 : 0;
-  if (cfg_.cb >= 0) {
+  if (cfg_.cats > 0) {
+    a.lo = nullptr;
+    if (learn && !impl_->cats_has) throw std::runtime_error("CATS learning needs StageCats first");
+    int depth = 0;
+    while ((1 << depth) < cfg_.cats) ++depth;
+    CatsArgs c{impl_->cats_act, impl_->cats_cost, impl_->cats_pdf, impl_->cats_base, impl_->cats_has, cfg_.cats, depth,
+               cfg_.cats_min, cfg_.cats_max, cfg_.cats_bw};
+    const size_t lds = sizeof(float) * 2 * (2 * (size_t(1) << depth) - 1);
+    hipLaunchKernelGGL(cats_kernel, dim3(static_cast<unsigned>(b1 - b0)), dim3(64), lds, impl_->stream, a, c);
+  } else if (cfg_.cb >= 0) {
     a.lo = nullptr;
     CbArgs cb{impl_->aip, impl_->chosen, impl_->cbcost, impl_->cbprob, cfg_.cb, cfg_.cb_explore ? 1 : 0, cfg_.epsilon,
               impl_->cbstats, impl_->best};
@@ -1267,7 +1423,22 @@ void GpuSgd::Stage(const int64_t* indptr, const uint32_t* indices, const float* 
 void GpuSgd::PrepLearn(int64_t r0, int64_t r1) {
   hipStream_t s = impl_->stream;
   const int64_t m = r1 - r0;
-  const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0;
+  if (cfg_.cats > 0 && m > 0) {
+    // CATS control variate: the running mean cost over the labelled examples so far, this one included (the
+    // learner state carries across passes and segments, as the host learner's)
+    if (static_cast<int64_t>(cats_has_.size()) < r1) throw std::runtime_error("CATS learning needs StageCats first");
+    std::vector<float> base(m);
+    for (int64_t i = 0; i < m; ++i) {
+      if (cats_has_[r0 + i]) {
+        cats_cost_sum_ += cats_cost_[r0 + i];
+        cats_cost_n_ += 1.0;
+      }
+      base[i] = cats_cost_n_ > 0 ? static_cast<float>(cats_cost_sum_ / cats_cost_n_) : 0.f;
+    }
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cats_base + r0, base.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipStreamSynchronize(s));  // base is a local
+  }
+  const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0 && cfg_.cats == 0;
   if (scalar && m > 0) {
     std::vector<float> lo(m), hi(m);
     if (cfg_.loss == 1) {  // logistic: the fixed [-50, 50] range
@@ -1486,7 +1657,7 @@ void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, con
                        int batch) {
   if (n < 0) throw std::runtime_error("negative row count");
   hipStream_t s = impl_->stream;
-  if (learn_r1 > 0 && (cfg_.cb >= 0 || cfg_.csoaa > 0))  // their label extras are staged after the plan
+  if (learn_r1 > 0 && (cfg_.cb >= 0 || cfg_.csoaa > 0 || cfg_.cats > 0))  // label extras staged after the plan
     throw std::runtime_error("StagePlan: learning while staging is for the scalar / oaa learners");
   // labels / weights first: a pipelined stage learns as the chunks land
   impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
@@ -1520,6 +1691,31 @@ void GpuSgd::StageCosts(const int64_t* cptr, const int32_t* cls, const float* co
   }
   VW_HIP_CHECK(hipStreamSynchronize(s));
   staged_costs_ = true;
+}
+
+void GpuSgd::StageCats(const float* action, const float* cost, const float* pdf, const uint8_t* has, int64_t n) {
+  if (cfg_.cats <= 0) throw std::runtime_error("StageCats: the learner is not a CATS learner");
+  if (n != staged_n_) throw std::runtime_error("StageCats: rows != staged examples");
+  hipStream_t s = impl_->stream;
+  for (void* q : {static_cast<void*>(impl_->cats_act), static_cast<void*>(impl_->cats_cost),
+                  static_cast<void*>(impl_->cats_pdf), static_cast<void*>(impl_->cats_base),
+                  static_cast<void*>(impl_->cats_has)})
+    PoolFree(q);
+  const size_t m = static_cast<size_t>(std::max<int64_t>(1, n));
+  PoolMalloc(&impl_->cats_act, m * sizeof(float));
+  PoolMalloc(&impl_->cats_cost, m * sizeof(float));
+  PoolMalloc(&impl_->cats_pdf, m * sizeof(float));
+  PoolMalloc(&impl_->cats_base, m * sizeof(float));
+  PoolMalloc(&impl_->cats_has, m);
+  if (n > 0) {
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cats_act, action, n * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cats_cost, cost, n * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cats_pdf, pdf, n * sizeof(float), hipMemcpyHostToDevice, s));
+    VW_HIP_CHECK(hipMemcpyAsync(impl_->cats_has, has, n, hipMemcpyHostToDevice, s));
+  }
+  cats_cost_.assign(cost, cost + n);
+  cats_has_.assign(has, has + n);
+  VW_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 void GpuSgd::StageCb(const int64_t* aip, const int32_t* chosen, const float* cost, const float* prob, int64_t ne) {
@@ -1556,9 +1752,14 @@ void GpuSgd::PredictStaged(float* out, float* best) {
   hipStream_t s = impl_->stream;
   const int64_t ne = staged_n_;
   if (ne <= 0) return;
-  const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0;
+  const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0 && cfg_.cats == 0;
+  // the clamp bounds' host copies live until the stream is drained below: an async copy from pageable memory
+  // may still be reading them after the call returns (these were block-scoped, freed under a pending copy:
+  // intermittently garbage clamps and scores)
+  std::vector<float> lo, hi;
   if (scalar) {
-    std::vector<float> lo(ne, static_cast<float>(min_label_)), hi(ne, static_cast<float>(max_label_));
+    lo.assign(ne, static_cast<float>(min_label_));
+    hi.assign(ne, static_cast<float>(max_label_));
     VW_HIP_CHECK(hipMemcpyAsync(impl_->lo, lo.data(), ne * sizeof(float), hipMemcpyHostToDevice, s));
     VW_HIP_CHECK(hipMemcpyAsync(impl_->hi, hi.data(), ne * sizeof(float), hipMemcpyHostToDevice, s));
   }
@@ -1568,7 +1769,13 @@ void GpuSgd::PredictStaged(float* out, float* best) {
   a.lo = scalar ? impl_->lo : nullptr; a.hi = impl_->hi;
   a.n0 = 0; a.n1 = ne; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
   a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = 0;
-  if (cfg_.cb >= 0) {
+  if (cfg_.cats > 0) {
+    int depth = 0;
+    while ((1 << depth) < cfg_.cats) ++depth;
+    CatsArgs c{nullptr, nullptr, nullptr, nullptr, nullptr, cfg_.cats, depth, cfg_.cats_min, cfg_.cats_max, cfg_.cats_bw};
+    const size_t lds = sizeof(float) * 2 * (2 * (size_t(1) << depth) - 1);
+    hipLaunchKernelGGL(cats_kernel, dim3(static_cast<unsigned>(ne)), dim3(64), lds, s, a, c);
+  } else if (cfg_.cb >= 0) {
     CbArgs cb{impl_->aip, nullptr, impl_->cbcost, impl_->cbprob, cfg_.cb, cfg_.cb_explore ? 1 : 0, cfg_.epsilon, nullptr,
               impl_->best};
     hipLaunchKernelGGL(cb_kernel, dim3(static_cast<unsigned>(ne)), dim3(64 * kCbWaves),
@@ -1593,7 +1800,8 @@ void GpuSgd::PredictStaged(float* out, float* best) {
 
 void GpuSgd::CbStats(double* ips_num, double* snips_den, double* examples) const {
   double h[3] = {0, 0, 0};
-  VW_HIP_CHECK(hipMemcpy(h, impl_->cbstats, sizeof(h), hipMemcpyDeviceToHost));
+  VW_HIP_CHECK(hipMemcpyAsync(h, impl_->cbstats, sizeof(h), hipMemcpyDeviceToHost, impl_->stream));
+  VW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
   *ips_num = h[0]; *snips_den = h[1]; *examples = h[2];
 }
 
@@ -1728,27 +1936,77 @@ void GpuSgd::ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val)
   PoolFree(base);
 }
 
+// The export scans the table once when no 4096-slot block holds more than kRegionCap records (a hashed
+// table's nonzeros spread evenly: ~8 per block for a 2M-example pass at 2^30), writing each block's records
+// into its own region; a denser table (a small -b, a long training) takes the count scan + write scan.
+constexpr int kRegionCap = 256;
+
+// SML_VW_EXPORT_TIMING=1: per-phase export timings on stderr (profiling runs)
+struct ExportClock {
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  ExportClock() : on(std::getenv("SML_VW_EXPORT_TIMING") != nullptr), t0(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[vw export] %-24s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+
 int64_t GpuSgd::CountNonzeros() const {
   hipStream_t s = impl_->stream;
   const uint64_t per = 4096;
   const int64_t nb = static_cast<int64_t>((impl_->nw + per - 1) / per);
   int32_t* cnt = nullptr;
   PoolMalloc(&cnt, nb * sizeof(int32_t));
-  hipLaunchKernelGGL(count_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, s, impl_->W, impl_->nw, per, cnt);
+  ExportClock clk;
+  const char* re = std::getenv("SML_VW_EXPORT_REGIONS");  // 0: the two-scan export (A/B, tests)
+  const bool regions = !(re && std::atoi(re) == 0);
+  if (regions) {
+    PoolMalloc(&export_reg_, static_cast<size_t>(nb) * kRegionCap * 12);
+    hipLaunchKernelGGL(write_rec_region_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw,
+                       per, kRegionCap, export_reg_, cnt);
+  } else {
+    hipLaunchKernelGGL(count_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, s, impl_->W, impl_->nw, per, cnt);
+  }
+  VW_HIP_CHECK(hipGetLastError());
   std::vector<int32_t> hc(nb);
   VW_HIP_CHECK(hipMemcpyAsync(hc.data(), cnt, nb * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
-  PoolFree(cnt);
+  clk.mark(regions ? "region scan + counts" : "count scan");
   export_base_.resize(nb);
   int64_t tot = 0;
-  for (int64_t i = 0; i < nb; ++i) { export_base_[i] = tot; tot += hc[i]; }
+  int32_t mx = 0;
+  for (int64_t i = 0; i < nb; ++i) {
+    export_base_[i] = tot;
+    tot += hc[i];
+    mx = std::max(mx, hc[i]);
+  }
+  if (regions && mx > kRegionCap) {  // too dense for the regions: the write scan runs in WriteRecords
+    PoolFree(export_reg_);
+    export_reg_ = nullptr;
+  }
+  if (export_reg_) {
+    export_cnt_ = cnt;  // the region counts stay on the device for the compaction
+  } else {
+    PoolFree(cnt);
+  }
   export_count_ = tot;
+  clk.mark("host prefix");
   return tot;
 }
 
 void GpuSgd::WriteRecords(char* dst) const {
   const int64_t tot = export_count_;
-  if (tot <= 0) return;
+  if (tot <= 0) {
+    PoolFree(export_reg_);
+    PoolFree(export_cnt_);
+    export_reg_ = nullptr;
+    export_cnt_ = nullptr;
+    return;
+  }
+  ExportClock clk;
   hipStream_t s = impl_->stream;
   const uint64_t per = 4096;
   const int64_t nb = static_cast<int64_t>(export_base_.size());
@@ -1757,9 +2015,16 @@ void GpuSgd::WriteRecords(char* dst) const {
   PoolMalloc(&base, nb * sizeof(int64_t));
   PoolMalloc(&rec, static_cast<size_t>(tot) * 12);
   VW_HIP_CHECK(hipMemcpyAsync(base, export_base_.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(write_rec_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw, per, base,
-                     rec);
+  if (export_reg_) {
+    const int grid = static_cast<int>(std::min<int64_t>(nb, 65536));
+    hipLaunchKernelGGL(rec_compact_kernel, dim3(grid), dim3(256), 0, s, export_reg_, kRegionCap, export_cnt_, base, nb,
+                       rec);
+  } else {
+    hipLaunchKernelGGL(write_rec_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw, per,
+                       base, rec);
+  }
   VW_HIP_CHECK(hipGetLastError());
+  clk.mark("records queued");
   // device -> pinned ring (the shared stager's buffers) -> dst, the host copy of piece k overlapping the DMA
   // of piece k + 1 (a pageable D2H would bounce through the runtime's own staging at a fraction of the rate)
   Stager& st = impl_->stager;
@@ -1797,8 +2062,14 @@ void GpuSgd::WriteRecords(char* dst) const {
   }
   while (!inflight.empty()) drain_one();
   VW_HIP_CHECK(hipStreamSynchronize(s));
+  clk.mark("d2h + host copy");
   PoolFree(base);
   PoolFree(rec);
+  PoolFree(export_reg_);
+  PoolFree(export_cnt_);
+  export_reg_ = nullptr;
+  export_cnt_ = nullptr;
+  clk.mark("frees");
 }
 
 void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val) {
@@ -1823,13 +2094,17 @@ void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<
 
 void GpuSgd::GlobalState(double* t, double* total_weight, double* sum_norm_x) const {
   double h[3] = {0, 0, 0};
-  VW_HIP_CHECK(hipMemcpy(h, impl_->gs, sizeof(h), hipMemcpyDeviceToHost));
+  VW_HIP_CHECK(hipMemcpyAsync(h, impl_->gs, sizeof(h), hipMemcpyDeviceToHost, impl_->stream));
+  VW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
   *t = h[0]; *total_weight = h[1]; *sum_norm_x = h[2];
 }
 
+// on the learner's (non-blocking) stream: a plain hipMemcpy runs on the null stream, which does not wait for
+// the constructor's still-queued zeroing of gs on this stream and could be overwritten by it
 void GpuSgd::SetGlobalState(double t, double total_weight, double sum_norm_x) {
   const double h[3] = {t, total_weight, sum_norm_x};
-  VW_HIP_CHECK(hipMemcpy(impl_->gs, h, sizeof(h), hipMemcpyHostToDevice));
+  VW_HIP_CHECK(hipMemcpyAsync(impl_->gs, h, sizeof(h), hipMemcpyHostToDevice, impl_->stream));
+  VW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
 }
 
 void* GpuSgd::weights_device() { return impl_->W; }

@@ -303,8 +303,7 @@ def _device_plan(blocks, info, shared_blocks=None):
 def _gpu_refusals(info) -> List[str]:
     """options the device learner does not run (deviceType='gpu' refuses them rather than silently running
     something else)"""
-    bad = [k for k in ("cats",) if int(info[k])]
-    bad += ["loss_function " + info["loss_function"]] if info["loss_function"] not in (
+    bad = ["loss_function " + info["loss_function"]] if info["loss_function"] not in (
         "squared", "classic", "logistic", "hinge", "quantile") else []
     if info["cb_adf"] == "1" and info.get("cb_type", "mtr") not in ("mtr", "dr", "ips"):
         bad.append("cb_type " + info["cb_type"])
@@ -324,6 +323,9 @@ def _gpu_config(vwmod, info):
     cfg.adaptive, cfg.normalized, cfg.invariant = (info[k] == "1" for k in ("adaptive", "normalized", "invariant"))
     cfg.oaa = int(info["oaa"])
     cfg.csoaa = int(info["csoaa"])
+    if int(info.get("cats", "0")) > 0:
+        cfg.cats = int(info["cats"])
+        cfg.cats_min, cfg.cats_max, cfg.cats_bw = (float(info[k]) for k in ("min_value", "max_value", "bandwidth"))
     if info["cb_adf"] == "1":
         cfg.cb = {"mtr": 0, "dr": 1, "ips": 2}[info.get("cb_type", "mtr")]
         cfg.cb_explore = info.get("cb_explore", "0") == "1"
@@ -434,6 +436,9 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     constant). gpuBatchSize=1 is the exact sequential learner; larger batches update concurrently with
     atomics (hogwild). Ranks average the blocks they touched at every sync with RCCL (VW's weighted
     averaging), and the model is exported from the device nonzeros."""
+    if int(_vw().describe_args(args).get("cats", "0")) > 0:  # CATS labels ("ca action:cost:pdf") are VW text
+        raise ValueError(f"deviceType='gpu' does not run cats in a vector-column estimator; use VowpalWabbitGeneric "
+                         f"(args: {args})")
     vwmod, info, g = _gpu_learner(args, model_bytes)
     if info["cb_adf"] == "1":
         raise ValueError("deviceType='gpu' runs --cb_adf / --cb_explore_adf through VowpalWabbitContextualBandit or "
@@ -466,18 +471,23 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     t1 = time.perf_counter_ns()
     sync_bytes = _gpu_learn_staged(est, g, _gpu_sync_comm(vwmod), n, first_learned=fused)
     t2 = time.perf_counter_ns()
-    lab = np.asarray(labels, np.float64)
-    wts = np.ones(n) if weights is None else weights.astype(np.float64)
-    wsum = float(wts.sum())
+    model = g.export_model(args)
+    t3 = time.perf_counter_ns()
+    lab = np.asarray(labels)
+    if weights is None:  # unit weights: no n-long ones / product arrays
+        wsum = float(n)
+        lsum = float(lab.sum(dtype=np.float64))
+    else:
+        w64 = np.asarray(weights, np.float64)
+        wsum = float(w64.sum())
+        lsum = float(np.dot(lab.astype(np.float64), w64))
     stats = {"numberOfExamplesPerPass": int(n), "weightedExampleSum": wsum,
-             "weightedLabelSum": float((lab * wts).sum()), "averageLoss": float(g.sum_loss) / max(wsum, 1e-300),
-             "bestConstant": float((lab * wts).sum()) / max(wsum, 1e-300),
+             "weightedLabelSum": lsum, "averageLoss": float(g.sum_loss) / max(wsum, 1e-300),
+             "bestConstant": lsum / max(wsum, 1e-300),
              "totalNumberOfFeatures": float(sum(len(b[3]) for b in gb)),
              "passes": int(max(1, est.getNumPasses())), "ipsEstimate": 0.0, "snipsEstimate": 0.0,
              "syncBytes": int(sum(sync_bytes)), "timeTotalNs": t2 - t0, "timeNativeIngestNs": t1 - t0,
-             "timeLearnNs": t2 - t1, "timeMultipassNs": 0}
-    model = g.export_model(args)
-    stats["timeExportNs"] = time.perf_counter_ns() - t2  # device nonzeros -> model bytes
+             "timeLearnNs": t2 - t1, "timeMultipassNs": 0, "timeExportNs": t3 - t2}  # export: nonzeros -> bytes
     return _GpuTrainedModel(model, args, info), stats
 
 
@@ -814,7 +824,7 @@ class VowpalWabbitGeneric(Estimator, HasPredictionCol):
     initialModel = Param("Initial model to start from", None, complex=True)
     numSyncsPerPass = Param("Number of times weights should be synchronized within each pass", 0, T.toInt)
     deviceType = Param("cpu (exact sequential VW semantics) or gpu (hogwild mini-batch SGD on the MI355X: scalar, "
-                       "--oaa, --csoaa and --cb_adf / --cb_explore_adf)", "cpu", T.toString)
+                       "--oaa, --csoaa, --cb_adf / --cb_explore_adf and --cats_pdf / --cats)", "cpu", T.toString)
     gpuBatchSize = Param("Mini-batch size of the GPU learner", 1024, T.toInt)
 
     def setInitialModel(self, model):  # noqa: N802
@@ -845,6 +855,8 @@ class VowpalWabbitGeneric(Estimator, HasPredictionCol):
                          weights)
             if int(info["csoaa"]) > 0:
                 g.stage_costs(d["cptr"], d["ccls"], d["ccost"])
+            if int(info.get("cats", "0")) > 0:  # --cats_pdf / --cats: "ca action:cost:pdf" labels
+                g.stage_cats(d["cats_action"], d["cats_cost"], d["cats_pdf"], d["cats_has"])
         _gpu_learn_staged(self, g, _gpu_sync_comm(vwmod), n)
         m = VowpalWabbitGenericModel()
         m.set("model", bytes(g.export_model(args)))

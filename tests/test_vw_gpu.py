@@ -28,8 +28,9 @@ def test_merged_csr_matches_blocks():
 @pytest.mark.parametrize("args", ["--cats 4 --bandwidth 1 --min_value 0 --max_value 1",
                                   "--cats_pdf 4 --bandwidth 1 --min_value 0 --max_value 1"])
 def test_gpu_rejects_reductions_it_does_not_run(args):
-    """Reductions the device learner does not implement are refused by name before any GPU work,
-    never silently run on the host."""
+    """Reductions a vector-column estimator cannot feed on the device (CATS labels are VW text: the device
+    CATS learner runs through VowpalWabbitGeneric) are refused by name before any GPU work, never silently run
+    on the host."""
     df, _ = _binary(n=50)
     with pytest.raises(ValueError, match="deviceType='gpu' does not run"):
         VowpalWabbitRegressor(deviceType="gpu", passThroughArgs=args).fit(df)
@@ -301,3 +302,71 @@ def test_gpu_fused_stage_learn_equals_stage_then_learn(monkeypatch, args, syncs)
         return
     assert fused.getNativeModel() == plain.getNativeModel()
     assert float(sf["averageLoss"][0]) == float(sp["averageLoss"][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [12, 22])
+def test_gpu_export_one_scan_regions_match_two_scans(monkeypatch, bits):
+    """The model export's one-scan form (per-4096-slot record regions, then a compaction) writes the same
+    bytes as the count-scan + write-scan form; a table too dense for the regions (2^12 slots) falls back."""
+    vw = native.load("_vw")
+    cfg = vw.GpuSgdConfig()
+    cfg.bits = bits
+    cfg.loss = 1
+    sgd = vw.GpuSgd(cfg, 0)
+    rng = np.random.default_rng(3)
+    n, k = 20000, 16
+    idx = rng.integers(0, 1 << 32, size=n * k, dtype=np.uint64).astype(np.uint32)
+    val = rng.standard_normal(n * k).astype(np.float32)
+    ip = np.arange(0, n * k + 1, k, dtype=np.int64)
+    lab = (rng.random(n) > 0.5).astype(np.float32) * 2 - 1
+    sgd.learn(ip, idx, val, lab, None, 256)
+    args = f"--loss_function logistic -b {bits}"
+    monkeypatch.setenv("SML_VW_EXPORT_REGIONS", "1")
+    m1 = sgd.export_model(args)
+    monkeypatch.setenv("SML_VW_EXPORT_REGIONS", "0")
+    m0 = sgd.export_model(args)
+    assert len(m1) > 200 and m1 == m0
+
+
+def _cats_lines(n=2000, seed=0, x_informative=True):
+    rng = np.random.default_rng(seed)
+    lines = []
+    for _ in range(n):
+        a = rng.uniform(0, 20000)
+        f = rng.integers(0, 2)
+        lo, hi = (12000, 18000) if (f == 0 or not x_informative) else (2000, 8000)
+        cost = 0.0 if lo < a < hi else 1.0
+        lines.append(f"ca {a:.2f}:{cost}:{1 / 20000:.8f} | f{f} x")
+    return DataFrame({"value": np.array(lines, dtype=object)})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", ["--cats_pdf 4 --bandwidth 2500 --min_value 0 --max_value 20000",
+                                  "--cats_pdf 6 --bandwidth 1500 --min_value 0 --max_value 20000 --loss_function logistic",
+                                  "--cats 8 --bandwidth 1000 --min_value 0 --max_value 20000"])
+def test_gpu_cats_batch1_parity(args):
+    """--cats_pdf / --cats on the device (filter tree of binary node learners, IPS leaf costs with the running-
+    mean baseline, bottom-up tournament): at gpuBatchSize=1 the device-trained model routes like the host
+    learner's - the same leaf for the examples (host scoring of both models, compared through the pdf's peak
+    window or the sampled action's window) - and it learned the context-dependent cheap regions."""
+    from synapseml_amd.vw import VowpalWabbitGeneric
+
+    df = _cats_lines()
+    g = VowpalWabbitGeneric(passThroughArgs=args, deviceType="gpu", gpuBatchSize=1).fit(df)
+    c = VowpalWabbitGeneric(passThroughArgs=args).fit(df)
+    og, oc = g.transform(df), c.transform(df)
+    if "--cats_pdf" in args:
+        peak = lambda seg: max(seg, key=lambda s: s["pdfValue"])["left"]  # noqa: E731
+        pg = np.array([peak(s) for s in og["segments"]])
+        pc = np.array([peak(s) for s in oc["segments"]])
+        assert np.mean(pg == pc) > 0.97, np.mean(pg == pc)
+        # context f0 -> cheap near 15000, f1 -> near 5000 (the peak window's centre)
+        lines = df["value"].tolist()
+        ctr = np.array([(max(s, key=lambda t: t["pdfValue"])["left"] + max(s, key=lambda t: t["pdfValue"])["right"]) / 2
+                        for s in og["segments"]])
+        f1 = np.array(["f1" in l for l in lines])
+        assert np.median(ctr[~f1]) > 10000 and np.median(ctr[f1]) < 10000
+    else:
+        a = np.asarray(og["action"])
+        assert ((a >= 0) & (a <= 20000)).all() and np.all(np.asarray(og["pdf"]) > 0)
