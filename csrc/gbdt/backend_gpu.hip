@@ -242,7 +242,6 @@ struct RankTables {
   int nq, ngain, max_position, norm;
   int gain_mono;  // label gains strictly increasing (the register kernel's kMono form)
   int nreg;
-  int rank_src;   // where the rank loop reads partner scores (LambdarankQueryRegs)
   double sigma;
 };
 constexpr int kGainLds = 64;  // label gains staged in LDS by the register kernel (longer tables: global)
@@ -544,7 +543,6 @@ __device__ __forceinline__ double ReadLaneD(double v, int l) {
 // the top list's per-document values, staged by rank in LDS by their owning lanes (lane r of the wave reads
 // rank r's; no second global load of the top documents' scores / labels)
 struct RankTop {
-  double all[kRankLds];  // every document's score (the rank loop's broadcast partner reads)
   double sc[64];
   float gn[64];
   int lab[64];
@@ -584,31 +582,24 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
   double sup[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) sup[u] = nextafter(sc[u], INFINITY);
-  // Partner scores (t.rank_src, A/B): 0 scalar loads through the constant address space (8 partners per
-  // s_load_dwordx16), 1 a v_readlane pair from the owning lane, 2 broadcast reads of the wave's LDS copy
-  // (r5 pass 14: 660 vs 600 us for the scalar loads)
-  const int src = t.rank_src;
-  if (src == 2) {
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-      if (u * 64 + lane < cnt) top.all[u * 64 + lane] = sc[u];
-    WaveSync();
-  }
-  // the rank loop, instantiated per partner source (the switch stays outside the partner loop)
-  auto rank_loop = [&](auto get, bool ties) {
+  // Partner scores: scalar loads through the constant address space (8 partners per s_load_dwordx16). r5 pass
+  // 15 A/B on one box: 635 us per call, v_readlane pairs 727 us, broadcast reads of an LDS copy 635 us.
+  const __attribute__((address_space(4))) double* sv =
+      (const __attribute__((address_space(4))) double*)(score + b);
+  auto count_ranks = [&](bool ties) {
 #pragma unroll
     for (int v = 0; v < NU; ++v) {
       if (v * 64 >= cnt) break;
       const int jn = min(64, cnt - v * 64);
       if (!ties) {
         for (int jj = 0; jj < jn; ++jj) {
-          const double sj = get(v, jj);
+          const double sj = sv[v * 64 + jj];
 #pragma unroll
           for (int u = 0; u < NU; ++u) rk[u] += sj >= sup[u] ? 1 : 0;
         }
       } else {
         for (int jj = 0; jj < jn; ++jj) {
-          const double sj = get(v, jj);
+          const double sj = sv[v * 64 + jj];
 #pragma unroll
           for (int u = 0; u < NU; ++u) {
             if (u < v) rk[u] += sj >= sup[u] ? 1 : 0;         // every j of slot v is after i
@@ -617,17 +608,6 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
           }
         }
       }
-    }
-  };
-  auto count_ranks = [&](bool ties) {
-    if (src == 1) {
-      rank_loop([&](int v, int jj) { return ReadLaneD(sc[v], jj); }, ties);
-    } else if (src == 2) {
-      rank_loop([&](int v, int jj) { return top.all[v * 64 + jj]; }, ties);
-    } else {
-      const __attribute__((address_space(4))) double* sv =
-          (const __attribute__((address_space(4))) double*)(score + b);
-      rank_loop([&](int v, int jj) { return sv[v * 64 + jj]; }, ties);
     }
   };
   auto scatter = [&]() {  // rank -> doc map (every document's slot)
@@ -798,11 +778,14 @@ __device__ __forceinline__ bool RegsEligible(const RankTables& t, int cnt) {
 // wave (2 KB + 256 B per wave instead of the LDS path's 11.5 KB). kWaves independent waves per block, each
 // walking its own queries (a CU holds at most 16 workgroups, so one-wave blocks cap residency at 4 waves
 // per SIMD; kWaves = 4 lifts that, but measured slower - see rank_waves_).
-template <int kWaves, bool kTR = true, bool kMono = true>
-__global__ __launch_bounds__(64 * kWaves, 4) void lambdarank_regs_kernel(RankTables t, const double* __restrict__ score,
-                                                                      const float* __restrict__ label,
-                                                                      const float* __restrict__ weight,
-                                                                      float* __restrict__ g, float* __restrict__ h) {
+// kSmall: the queries of <= 128 documents only (NU 1 / 2): without the NU 3 / 4 code paths the kernel needs
+// fewer VGPRs, so more waves per SIMD hide the per-query latency chains; the host launches the > 128-document
+// queries (the front of the largest-first order) on a kSmall = false launch first. [k0, k1) = the launch's
+// slice of t.order.
+template <int kWaves, bool kTR = true, bool kMono = true, bool kSmall = false>
+__global__ __launch_bounds__(64 * kWaves, kSmall ? 5 : 4) void lambdarank_regs_kernel(
+    RankTables t, const double* __restrict__ score, const float* __restrict__ label, const float* __restrict__ weight,
+    float* __restrict__ g, float* __restrict__ h, int k0, int k1) {
   __shared__ double s_disc[kRankLds];
   __shared__ float s_gain[kGainLds];
   __shared__ int s_map[kWaves][kRankLds];
@@ -813,14 +796,16 @@ __global__ __launch_bounds__(64 * kWaves, 4) void lambdarank_regs_kernel(RankTab
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform to the compiler: q, b, cnt in SGPRs
   // documents per lane sized to the query: the pair loops run NU-wide, so a 100-document query
   // costs half of what the kRankLds-wide form would
-  for (int k = blockIdx.x * kWaves + wid; k < t.nreg; k += gridDim.x * kWaves) {
+  for (int k = k0 + blockIdx.x * kWaves + wid; k < k1; k += gridDim.x * kWaves) {
     const int q = t.order[k];
     const int cnt = t.qb[q + 1] - t.qb[q];
     if (cnt <= 0 || !RegsEligible(t, cnt)) continue;
     if (cnt <= 64) LambdarankQueryRegs<1, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
     else if (cnt <= 128) LambdarankQueryRegs<2, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
-    else if (cnt <= 192) LambdarankQueryRegs<3, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
-    else LambdarankQueryRegs<kRankPerLane, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
+    else if constexpr (!kSmall) {
+      if (cnt <= 192) LambdarankQueryRegs<3, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
+      else LambdarankQueryRegs<kRankPerLane, kTR, kMono>(t, q, score, label, weight, g, h, s_disc, s_gain, s_map[wid], s_top[wid]);
+    }
   }
 }
 
@@ -3430,6 +3415,8 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_HIST_TIGHT")) tight_ = tight_ && std::atoi(e) != 0;
     if (const char* e = std::getenv("SML_RANK_WAVES")) rank_waves_ = std::atoi(e) == 4 ? 4 : 1;
     if (const char* e = std::getenv("SML_RANK_TREDUCE")) rank_treduce_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SML_RANK_SPLIT")) rank_split_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SML_RANK_SMALL_WAVES")) rank_small_waves_ = std::atoi(e) == 4 ? 4 : 1;
     voting_ = cfg.tree_learner == "voting" && Distributed();
     if (voting_) {
       if (F_ > kVoteMaxF) throw std::runtime_error("GPU voting_parallel: more than 8192 features");
@@ -3604,19 +3591,38 @@ class GpuBackend : public TrainBackend {
       if (rank_.nq > 0) {
         const int grid = std::min(rank_.nq, 65536);
         if (rank_regs_) {
-          const int rgrid = std::max(1, std::min(rank_.nreg, 1 << 20));  // one wave per query
           if (rank_waves_ == 1) {
+            // the > 128-document queries (first in the largest-first order) on the full kernel, then the rest
+            // on the NU <= 2 form (fewer VGPRs: more resident waves); SML_RANK_SPLIT=0: one launch
+            const int k_split = rank_split_ ? rank_nbig_ : rank_.nreg;
             auto lk = rank_treduce_ ? (rank_.gain_mono ? lambdarank_regs_kernel<1, true, true>
                                                        : lambdarank_regs_kernel<1, true, false>)
                                     : (rank_.gain_mono ? lambdarank_regs_kernel<1, false, true>
                                                        : lambdarank_regs_kernel<1, false, false>);
-            hipLaunchKernelGGL(lk, dim3(rgrid), dim3(64), 0, stream_, rank_, score_.get(),
-                               label_.get(), weight_.get(), g_.get(), h_.get());
+            if (k_split > 0)
+              hipLaunchKernelGGL(lk, dim3(std::min(k_split, 1 << 20)), dim3(64), 0, stream_, rank_, score_.get(),
+                                 label_.get(), weight_.get(), g_.get(), h_.get(), 0, k_split);
+            if (k_split < rank_.nreg) {
+              const int nsmall = rank_.nreg - k_split;
+              if (rank_small_waves_ == 4) {  // 4-wave blocks: past the per-CU workgroup cap of one-wave blocks
+                auto ls = rank_.gain_mono ? lambdarank_regs_kernel<4, true, true, true>
+                                          : lambdarank_regs_kernel<4, true, false, true>;
+                hipLaunchKernelGGL(ls, dim3(std::min((nsmall + 3) / 4, 1 << 18)), dim3(256), 0, stream_, rank_,
+                                   score_.get(), label_.get(), weight_.get(), g_.get(), h_.get(), k_split, rank_.nreg);
+              } else {
+                auto ls = rank_treduce_ ? (rank_.gain_mono ? lambdarank_regs_kernel<1, true, true, true>
+                                                           : lambdarank_regs_kernel<1, true, false, true>)
+                                        : (rank_.gain_mono ? lambdarank_regs_kernel<1, false, true, true>
+                                                           : lambdarank_regs_kernel<1, false, false, true>);
+                hipLaunchKernelGGL(ls, dim3(std::min(nsmall, 1 << 20)), dim3(64), 0, stream_, rank_, score_.get(),
+                                   label_.get(), weight_.get(), g_.get(), h_.get(), k_split, rank_.nreg);
+              }
+            }
           } else {
             const int g4 = std::max(1, std::min((rank_.nreg + 3) / 4, 1 << 18));
             auto l4 = rank_.gain_mono ? lambdarank_regs_kernel<4, true, true> : lambdarank_regs_kernel<4, true, false>;
             hipLaunchKernelGGL(l4, dim3(g4), dim3(256), 0, stream_, rank_, score_.get(),
-                               label_.get(), weight_.get(), g_.get(), h_.get());
+                               label_.get(), weight_.get(), g_.get(), h_.get(), 0, rank_.nreg);
           }
           SML_HIP_CHECK(hipGetLastError());
         }
@@ -4096,6 +4102,9 @@ class GpuBackend : public TrainBackend {
     // a tail of long queries on a few waves)
     std::stable_sort(reg_q.begin(), reg_q.end(),
                      [&qb](int32_t a, int32_t b) { return qb[a + 1] - qb[a] > qb[b + 1] - qb[b]; });
+    rank_nbig_ = 0;
+    while (rank_nbig_ < static_cast<int>(reg_q.size()) && qb[reg_q[rank_nbig_] + 1] - qb[reg_q[rank_nbig_]] > 128)
+      ++rank_nbig_;
     rank_order_.alloc(std::max<size_t>(1, reg_q.size()));
     if (!reg_q.empty())
       SML_HIP_CHECK(hipMemcpy(rank_order_.get(), reg_q.data(), sizeof(int32_t) * reg_q.size(), hipMemcpyHostToDevice));
@@ -4137,8 +4146,6 @@ class GpuBackend : public TrainBackend {
     }
     const char* me = std::getenv("SML_RANK_MONO");  // 0: the label-compare form (A/B and tests), read per booster
     rank_.gain_mono = me && std::atoi(me) == 0 ? 0 : (mono ? 1 : 0);
-    const char* se = std::getenv("SML_RANK_SRC");  // partner scores of the rank loop: 0 s_load, 1 readlane, 2 LDS
-    rank_.rank_src = se ? std::atoi(se) : 0;
     rank_ready_ = true;
   }
 
@@ -4411,6 +4418,9 @@ class GpuBackend : public TrainBackend {
   // to 10 resident per SIMD instead of 4): r4 pass 11 measured it slower (949 vs 860 us per call, ranker
   // fit 33.6M vs 34.0M rows/s), so one-wave blocks stay the default
   int rank_waves_ = 1;
+  int rank_nbig_ = 0;       // register-path queries of > 128 documents (the front of rank_order_)
+  bool rank_split_ = true;  // SML_RANK_SPLIT=0: one launch of the full kernel for all register-path queries
+  int rank_small_waves_ = 1;  // SML_RANK_SMALL_WAVES=4: the small-query launch in 4-wave blocks
   bool rank_treduce_ = true;  // SML_RANK_TREDUCE=0: one pair of wave sums per top document (A/B knob)
   int64_t n_ = 0;
   int32_t bag_n_ = -1;

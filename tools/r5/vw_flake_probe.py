@@ -21,11 +21,12 @@ def binary(n=20000, d=20, seed=0):
 
 
 df, y = binary()
+BATCH = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     for fused in ("1", "0"):
         os.environ["SML_VW_STAGE_LEARN"] = fused
         m = VowpalWabbitClassifier(deviceType="gpu", labelConversion=True, passThroughArgs="--loss_function logistic",
-                                   numPasses=3, gpuBatchSize=256).fit(df)
+                                   numPasses=3, gpuBatchSize=BATCH).fit(df)
         a_dev = roc_auc_score(y, m.transform(df)["probability"][:, 1])
         h = m.copy()
         h.set("deviceType", "cpu")
