@@ -2,7 +2,10 @@
 #include "valid_gpu.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <map>
@@ -80,8 +83,18 @@ Booster::Booster(std::shared_ptr<Dataset> train, const std::string& params, Comm
 }
 
 void Booster::InitTraining() {
+  // SML_GBDT_INIT_TIMING=1: the phases of the booster construction on stderr (profiling runs)
+  const bool timing = std::getenv("SML_GBDT_INIT_TIMING") != nullptr;
+  auto tick = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[booster init] %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tick).count());
+    tick = now;
+  };
   objective_.reset(new Objective(cfg_));
   objective_->Init(*train_);
+  mark("objective init");
   num_tree_per_iter_ = objective_->NumModelPerIteration();
   num_class_ = cfg_.IsClassification() && cfg_.objective != "binary" ? cfg_.num_class : 1;
   objective_str_ = objective_->ToString();
@@ -94,7 +107,9 @@ void Booster::InitTraining() {
   if (want_gpu && GpuAvailable()) backend_ = MakeGpuBackend(cfg_.gpu_device_id);
   if (!backend_) backend_ = MakeCpuBackend();
   if (comm_) backend_->SetComm(comm_);
+  mark("backend create");
   backend_->Init(train_.get(), cfg_, num_tree_per_iter_);
+  mark("backend init");
   const int64_t n = train_->num_data;
   const int K = num_tree_per_iter_;
   init_scores_.assign(K, 0.0);
@@ -109,7 +124,9 @@ void Booster::InitTraining() {
         init_scores_[k] = objective_->BoostFromScore(k, comm_);
       }
     }
+    mark("boost from score");
     backend_->FillScores(init_scores_, n);  // constant start scores, written where the scores live
+    mark("fill scores");
   }
   bag_rng_.seed(cfg_.bagging_seed);
   feat_rng_.seed(cfg_.feature_fraction_seed);

@@ -228,6 +228,20 @@ static void GlobalSums(int64_t n, Y y, W w, Comm* comm, double* sum_yw, double* 
   *sum_w = static_cast<double>(q[1]) / s1;
 }
 
+// Unweighted 0 / 1 indicators (binary, one-vs-all, multiclass start scores): the sums are integer counts, so
+// one integer pass gives exactly what the quantised sums would (r5: the two floating passes over 11M labels
+// were 6 ms of a 210 ms fit).
+template <class Ind>
+static void GlobalCounts(int64_t n, Ind ind, Comm* comm, double* sum_yw, double* sum_w) {
+  int64_t c = 0;
+#pragma omp parallel for schedule(static) reduction(+ : c)
+  for (int64_t i = 0; i < n; ++i) c += ind(i) ? 1 : 0;
+  int64_t q[2] = {c, n};
+  if (comm && comm->world() > 1) comm->AllReduceHostI64(q, 2);
+  *sum_yw = static_cast<double>(q[0]);
+  *sum_w = static_cast<double>(q[1]);
+}
+
 double Objective::BoostFromScore(int class_id, Comm* comm) const {
   if (!boost_from_average_) return 0.0;
   const int64_t n = n_;
@@ -237,6 +251,11 @@ double Objective::BoostFromScore(int class_id, Comm* comm) const {
     case kObjMulticlassOVA:
     case kObjCrossEntropy: {
       double sl = 0, sw = 0;
+      if (!weight_ && p_.kind == kObjBinary)
+        GlobalCounts(n, [&](int64_t i) { return label_[i] > 0; }, comm, &sl, &sw);
+      else if (!weight_ && p_.kind == kObjMulticlassOVA)
+        GlobalCounts(n, [&](int64_t i) { return static_cast<int>(label_[i]) == class_id; }, comm, &sl, &sw);
+      else
       GlobalSums(n, [&](int64_t i) {
         return p_.kind == kObjMulticlassOVA ? (static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0)
                                            : (p_.kind == kObjBinary ? (label_[i] > 0 ? 1.0 : 0.0)
@@ -250,7 +269,10 @@ double Objective::BoostFromScore(int class_id, Comm* comm) const {
     }
     case kObjMulticlass: {
       double sl = 0, sw = 0;
-      GlobalSums(n, [&](int64_t i) { return static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0; }, W, comm, &sl, &sw);
+      if (!weight_)
+        GlobalCounts(n, [&](int64_t i) { return static_cast<int>(label_[i]) == class_id; }, comm, &sl, &sw);
+      else
+        GlobalSums(n, [&](int64_t i) { return static_cast<int>(label_[i]) == class_id ? 1.0 : 0.0; }, W, comm, &sl, &sw);
       double p = sw > 0 ? sl / sw : 1.0 / p_.num_class;
       return std::log(std::max(kEpsilon, p));
     }

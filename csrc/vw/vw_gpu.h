@@ -111,6 +111,8 @@ class GpuSgd {
 
  private:
   void Launch(int64_t b0, int64_t b1, bool learn, bool have_weights);
+  // end of the launch starting at row b0 of the range [r0, r1) being learned (warm-up sizes, then `batch`)
+  int64_t NextLaunch(int64_t b0, int64_t r0, int64_t r1, int batch) const;
   struct Impl;
   std::unique_ptr<Impl> impl_;
   GpuSgdConfig cfg_;

@@ -1295,6 +1295,22 @@ void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
   VW_HIP_CHECK(hipGetLastError());
 }
 
+// Hogwild warm-up: the learner's first examples run in launches of 1, 1, 2, 4, ... examples (doubling up to
+// `batch`), so the adaptive / normalized state (every slot's G and N, the global t / weight / norm sums) forms
+// near-sequentially before wide concurrency. Without it, `batch` examples of a fresh table all take their large
+// first-step rates at once: on dense features (every example updating the same slots) their summed steps
+// overshoot, and 1-2 fits in 14 diverged at batch 64 / 256 (progressive loss 3-9, AUC 0.87-0.98; r5 passes
+// 18-19). Launch sizes depend only on how many examples the learner has seen, so runs stay reproducible.
+int64_t GpuSgd::NextLaunch(int64_t b0, int64_t r0, int64_t r1, int batch) const {
+  const int64_t seen = static_cast<int64_t>(examples_) + (b0 - r0);
+  int64_t bs = batch;
+  if (seen < batch) {
+    bs = 1;
+    while (bs * 2 <= seen) bs *= 2;
+  }
+  return std::min<int64_t>(r1, b0 + bs);
+}
+
 void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
                    const float* weights, int64_t n, int batch, float* preds_out) {
   if (n <= 0) return;
@@ -1371,7 +1387,10 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
       }
       VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
       const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
-      for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, weights != nullptr);
+      for (int64_t b0 = r0, b1; b0 < r1; b0 = b1) {
+        b1 = NextLaunch(b0, 0, r1, batch);
+        Launch(b0, b1, true, weights != nullptr);
+      }
     }
   } catch (...) {
     uploader.join();
@@ -1475,7 +1494,10 @@ void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
   if (r1 == r0) return;
   PrepLearn(r0, r1);
   batch = std::max(1, batch);
-  for (int64_t b0 = r0; b0 < r1; b0 += batch) Launch(b0, std::min<int64_t>(r1, b0 + batch), true, staged_weights_);
+  for (int64_t b0 = r0, b1; b0 < r1; b0 = b1) {
+    b1 = NextLaunch(b0, r0, r1, batch);
+    Launch(b0, b1, true, staged_weights_);
+  }
   FinishLearn(r0, r1, preds_out);
 }
 
@@ -1632,8 +1654,10 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
         hipLaunchKernelGGL(expand_fill_kernel, dim3(grid), dim3(64 * kExpandWaves), 0, s, impl_->spec, r0, r1,
                            impl_->indptr, impl_->idx, impl_->val);
         VW_HIP_CHECK(hipGetLastError());
-        for (int64_t b0 = r0; b0 < std::min(r1, lr1); b0 += batch)
-          Launch(b0, std::min<int64_t>(std::min(r1, lr1), b0 + batch), true, staged_weights_);
+        for (int64_t b0 = r0, b1; b0 < std::min(r1, lr1); b0 = b1) {
+          b1 = NextLaunch(b0, 0, std::min(r1, lr1), batch);
+          Launch(b0, b1, true, staged_weights_);
+        }
       }
     } catch (...) {
       uploader.join();
