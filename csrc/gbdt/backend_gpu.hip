@@ -29,6 +29,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstddef>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -2366,6 +2367,7 @@ struct BExp {
   int32_t pbegin, pcount, pbuf, tile0;  // parent segment; first global partition tile of this expansion
   PartSplit ps;
   uint32_t cat[8];
+  int64_t pgcount;  // the parent's global rows (the larger child's count = pgcount - the smaller's)
 };
 
 struct BState {
@@ -2378,7 +2380,6 @@ struct BState {
   // replaying the whole tree again (the replay cost ~1 us per pop: 7.6 us at round 0, 36 us at round 29)
   int32_t rp_nf, rp_pops;
   int32_t rp_fnode[kBatchMaxLeaves + 1], rp_fli[kBatchMaxLeaves + 1];
-  double rp_fgain[kBatchMaxLeaves + 1];
   int32_t rp_pnode[kBatchMaxLeaves], rp_pli[kBatchMaxLeaves];
 };
 
@@ -2403,16 +2404,6 @@ __device__ __forceinline__ int BatchSmallCount(const BState* bs, int j) {
   return x.left_small ? lt : x.pcount - lt;
 }
 
-struct SimKey {  // frontier entry order: larger gain, then smaller leaf index (the sequential argmax)
-  double gain;
-  int li, idx;
-};
-
-__device__ __forceinline__ bool SimBetter(const SimKey& x, const SimKey& y) {
-  if (x.gain != y.gain) return x.gain > y.gain;
-  return x.li < y.li;
-}
-
 constexpr int kPlanThreads = 1024;
 constexpr int kPlanFm = 1024;  // features whose split metadata the plan stages in LDS
 
@@ -2421,20 +2412,92 @@ __device__ __forceinline__ void SetHostFlag(int* f, int v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Wave-wide maximum of a 64-bit key: DPP exchanges inside each row of 16 lanes (quad swaps, half-row and row
+// mirrors: VALU, no LDS round trip), then the four rows' maxima read into scalars. Every lane must be active.
+template <int kCtrl>
+__device__ __forceinline__ unsigned long long DppMaxU64(unsigned long long x) {
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), kCtrl, 0xF, 0xF, false));
+  const unsigned hi =
+      static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x >> 32), kCtrl, 0xF, 0xF, false));
+  const unsigned long long y = (static_cast<unsigned long long>(hi) << 32) | lo;
+  return y > x ? y : x;
+}
+
+__device__ __forceinline__ unsigned long long WaveMaxU64(unsigned long long x) {
+  x = DppMaxU64<0xB1>(x);   // quad_perm [1,0,3,2]
+  x = DppMaxU64<0x4E>(x);   // quad_perm [2,3,0,1]
+  x = DppMaxU64<0x141>(x);  // row_half_mirror
+  x = DppMaxU64<0x140>(x);  // row_mirror
+  unsigned long long m = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x), 16 * r));
+    const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x >> 32), 16 * r));
+    const unsigned long long y = (static_cast<unsigned long long>(hi) << 32) | lo;
+    m = y > m ? y : m;
+  }
+  return m;
+}
+
+__device__ __forceinline__ int WaveMinI32(int x) {
+  x = min(x, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));
+  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+             min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+}
+
+// a double's bits as an unsigned key with the same order (larger gain -> larger key; +0 -> 2^63)
+__device__ __forceinline__ unsigned long long GainKey(double g) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(g));
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// entry `s` of a per-lane register array picked by a wave-uniform slot (a select chain, no scratch)
+template <int kSlots, typename T>
+__device__ __forceinline__ T SlotSel(const T (&a)[kSlots], int s) {
+  T v = a[0];
+#pragma unroll
+  for (int i = 1; i < kSlots; ++i) v = s == i ? a[i] : v;
+  return v;
+}
+
+// kSlots: frontier entries per lane (entry e lives in lane e % 64, slot e / 64): 1 for num_leaves <= 64
+template <int kSlots>
 __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     BState* __restrict__ bs, BNode* __restrict__ nodes, SplitResult* __restrict__ nbest,
     const SplitResult* __restrict__ fbest, int F, const double2* __restrict__ part, int E,
     const DLeaf* __restrict__ leaves, DState* __restrict__ st, DTree t, FeatMeta fm, const int8_t* __restrict__ mono,
-    int has_mono, int first, int spec_k, int budget, int part_tile, int* __restrict__ host_flag) {
+    int has_mono, int first, int spec_k, int budget, int part_tile, int cap_nodes, int* __restrict__ host_flag,
+    long long* __restrict__ prof) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int kWaves = kPlanThreads / 64;
+  // SML_BPLAN_PROF: thread 0 stamps the real-time clock at the phase boundaries (entry, absorbed, staged,
+  // replayed, end) into prof[0..4]; prof[5] = pops replayed this round
+  auto stamp = [&](int k) { if (prof != nullptr && tid == 0) prof[k] = static_cast<long long>(wall_clock64()); };
+  stamp(0);
   __shared__ double s_gain[kBatchMaxNodes];
   __shared__ int s_c0[kBatchMaxNodes], s_c1[kBatchMaxNodes], s_pop[kBatchMaxNodes];
-  __shared__ int f_node[kBatchMaxLeaves + 1], f_li[kBatchMaxLeaves + 1];
-  __shared__ double f_gain[kBatchMaxLeaves + 1];
   __shared__ int p_node[kBatchMaxLeaves], p_li[kBatchMaxLeaves];
   __shared__ int ch_node[kMaxSpec];
-  __shared__ int s_nnodes, s_nexp_prev;
+  __shared__ int s_rp[2], s_hdr[3];
+  __shared__ int s_nb[kPlanFm], s_mt[kPlanFm], s_db[kPlanFm];
+  // ---- phase 0: every load that does not depend on this round's header (done / nnodes / nexp) goes out
+  // together - the header, the last round's expansion records and their children's per-feature best splits
+  // (F <= 64 and 2 spec_k <= waves: one wave per child, lane f holding feature f's record in registers),
+  // every node's gain and links up to the allocation's capacity, the committed replay prefix and the split
+  // features' metadata - so the plan pays one memory round trip before the replay instead of four
+  // (header -> records -> parent count / record copy -> node gains; r5 pass 22: absorb 3.0 + stage 1.9 us)
+  // children go to waves 1.. (wave 0 replays right after the barrier; the others copy the winning records
+  // into nbest after it, off the replay's path - the plan reads a child absorbed this round from fbest)
+  const bool fast = F <= 64 && 2 * spec_k < kWaves;
+  const int cw = wid - 1;  // fast path: the child this wave absorbs
+  __shared__ int s_src[kBatchMaxNodes];  // fbest record of a node absorbed this round (fast path), else -1
+  int x_c0 = 0, x_c1 = 0, x_ls = 0, x_pb = 0, x_pc = 0, x_buf = 0, lt = 0;
+  int64_t x_pg = 0, small_cnt = 0;
+  int rfeat = -1;
+  double rgain = -INFINITY;
   if (first) {
     if (tid == 0) {
       const DLeaf R = leaves[0];
@@ -2446,157 +2509,223 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       bs->nexp = 0; bs->done = 0; bs->nnodes = 1; bs->expanded = 0; bs->spec_used = 0; bs->ntiles = 0;
       bs->cap_exp = 2 * budget + kMaxSpec;
       bs->cap_nodes = min(kBatchMaxNodes, 1 + 2 * bs->cap_exp);
-      s_nnodes = 1;
-      s_nexp_prev = 0;
+      s_hdr[0] = 0; s_hdr[1] = 1; s_hdr[2] = 0;
+      s_c0[0] = -1; s_c1[0] = -1; s_pop[0] = -1; s_src[0] = -1;
     }
+    if (fast && cw == 0 && lane < F) { rfeat = fbest[lane].feature; rgain = fbest[lane].gain; }
   } else {
-    if (bs->done) {
-      if (tid == 0) { bs->nexp = 0; SetHostFlag(host_flag, 1); }
-      return;
-    }
-    if (tid == 0) { s_nnodes = bs->nnodes; s_nexp_prev = bs->nexp; }
-  }
-  __syncthreads();
-  const int nnodes = s_nnodes, nexp = s_nexp_prev;
-  // ---- absorb: the children of last round's expansions (first: the root) get their best splits, global
-  // counts and row segments. One wave per child; lanes stride over features (ties: smaller feature).
-  const int nchild = first ? 1 : 2 * nexp;
-  for (int c = wid; c < nchild; c += kWaves) {
-    // the expansion record, its cursor and the smaller child's count do not depend on the argmax below:
-    // loaded first, so their latency overlaps the feature records' (one memory round trip, not two)
-    int x_node = 0, x_c0 = 0, x_c1 = 0, x_ls = 0, x_pb = 0, x_pc = 0, x_buf = 0, lt = 0;
-    int64_t small_cnt = 0;
-    if (!first && lane == 0) {
-      const int j = c >> 1;
-      const BExp& x = bs->exp[j];
-      x_node = x.node; x_c0 = x.c0; x_c1 = x.c1; x_ls = x.left_small;
-      x_pb = x.pbegin; x_pc = x.pcount; x_buf = x.pbuf;
-      lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
-      small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
-    }
-    KeyG k{-INFINITY, 1 << 30, 0};
-    for (int f = lane; f < F; f += 64) {
-      const SplitResult& r = fbest[c * F + f];
-      if (r.feature < 0) continue;
-      KeyG cand{r.gain, f, 0};
-      if (KeyBetter(cand, k)) k = cand;
-    }
-    k = WaveArgmax(k);
-    if (lane == 0) {
-      int id;
-      if (first) {
-        id = 0;
-      } else {
-        const int small = x_ls ? x_c0 : x_c1;
-        id = (c & 1) ? (small == x_c0 ? x_c1 : x_c0) : small;
-        BNode& nd = nodes[id];
-        const bool is_left = id == x_c0;
-        nd.begin = is_left ? x_pb : x_pb + lt;
-        nd.count = is_left ? lt : x_pc - lt;
-        nd.buf = x_buf == 0 ? 1 : 0;
-        nd.gcount = (c & 1) ? nodes[x_node].gcount - small_cnt : small_cnt;
+    if (tid == 0) { s_hdr[0] = bs->done; s_hdr[1] = bs->nnodes; s_hdr[2] = bs->nexp; }
+    if (fast && cw >= 0 && cw < 2 * spec_k) {
+      const int j = cw >> 1;
+      if (lane == 0) {
+        const BExp& x = bs->exp[j];
+        x_c0 = x.c0; x_c1 = x.c1; x_ls = x.left_small;
+        x_pb = x.pbegin; x_pc = x.pcount; x_buf = x.pbuf; x_pg = x.pgcount;
+        lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+        small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
       }
-      if (k.gain == -INFINITY) {
-        nbest[id].feature = -1;
-        nbest[id].gain = -INFINITY;
-      } else {
-        nbest[id] = fbest[c * F + k.a];
-      }
+      if (lane < F) { rfeat = fbest[cw * F + lane].feature; rgain = fbest[cw * F + lane].gain; }
     }
-  }
-  __syncthreads();
-  // ---- node gains and expansion links into LDS (the replay's dependent reads stay on chip); in the same
-  // pass the committed replay prefix and (F <= kPlanFm) the split features' metadata, so the one-wave
-  // replay and plan below start without a memory round trip of their own
-  __shared__ int s_rp[2];
-  __shared__ int s_nb[kPlanFm], s_mt[kPlanFm], s_db[kPlanFm];
-  for (int i = tid; i < nnodes; i += kPlanThreads) {
-    const SplitResult& r = nbest[i];
-    s_gain[i] = r.feature >= 0 ? r.gain : -INFINITY;
-    s_c0[i] = nodes[i].c0;
-    s_c1[i] = nodes[i].c1;
-    s_pop[i] = -1;
+    for (int i = tid; i < cap_nodes; i += kPlanThreads) {
+      const SplitResult& r = nbest[i];
+      s_gain[i] = r.feature >= 0 ? r.gain : -INFINITY;
+      s_c0[i] = nodes[i].c0;
+      s_c1[i] = nodes[i].c1;
+      s_pop[i] = -1;
+      s_src[i] = -1;
+    }
   }
   const bool fm_lds = F <= kPlanFm;
   if (fm_lds)
     for (int f = tid; f < F; f += kPlanThreads) { s_nb[f] = fm.num_bin[f]; s_mt[f] = fm.missing[f]; s_db[f] = fm.default_bin[f]; }
+  // the committed frontier (node, leaf index) goes straight into wave 0's registers
+  int fn[kSlots], fl[kSlots];
+#pragma unroll
+  for (int q = 0; q < kSlots; ++q) { fn[q] = -1; fl[q] = 0; }
   if (!first) {
     if (tid == 0) { s_rp[0] = bs->rp_nf; s_rp[1] = bs->rp_pops; }
     // the prefix arrays are read whole-capacity-bounded by the stored counts after the barrier; loading
     // kBatchMaxLeaves entries regardless keeps this pass free of a dependent count load
-    for (int i = tid; i < kBatchMaxLeaves + 1; i += kPlanThreads) {
-      f_node[i] = bs->rp_fnode[i]; f_li[i] = bs->rp_fli[i]; f_gain[i] = bs->rp_fgain[i];
-      if (i < kBatchMaxLeaves) { p_node[i] = bs->rp_pnode[i]; p_li[i] = bs->rp_pli[i]; }
+    for (int i = tid; i < kBatchMaxLeaves; i += kPlanThreads) { p_node[i] = bs->rp_pnode[i]; p_li[i] = bs->rp_pli[i]; }
+    if (wid == 0) {
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) { fn[q] = bs->rp_fnode[q * 64 + lane]; fl[q] = bs->rp_fli[q * 64 + lane]; }
     }
+  } else if (lane == 0) {
+    fn[0] = 0;  // the root, leaf 0
   }
   __syncthreads();
-  if (wid != 0) return;
-  // ---- replay of the sequential best-first growth (one wave), resumed at the committed prefix
-  int nf = 1, pops = 0, nch = 0;
-  if (first) {
-    if (lane == 0) { f_node[0] = 0; f_li[0] = 0; f_gain[0] = s_gain[0]; }
+  if (s_hdr[0]) {
+    if (tid == 0) { bs->nexp = 0; SetHostFlag(host_flag, 1); }
+    return;
+  }
+  const int nnodes = s_hdr[1], nexp = s_hdr[2];
+  // ---- absorb: the children of last round's expansions (first: the root) get their best splits, global
+  // counts and row segments (ties: smaller feature); their gains go to the staged LDS table
+  const int nchild = first ? 1 : 2 * nexp;
+  auto child_id = [&](int c) {
+    const int small = x_ls ? x_c0 : x_c1;
+    return (c & 1) ? (small == x_c0 ? x_c1 : x_c0) : small;
+  };
+  auto write_node = [&](int c, int id) {
+    BNode& nd = nodes[id];
+    const bool is_left = id == x_c0;
+    nd.begin = is_left ? x_pb : x_pb + lt;
+    nd.count = is_left ? lt : x_pc - lt;
+    nd.buf = x_buf == 0 ? 1 : 0;
+    nd.gcount = (c & 1) ? x_pg - small_cnt : small_cnt;
+  };
+  int copy_src = -1, copy_id = 0;  // fast path: the record this wave copies into nbest after the barrier
+  if (fast) {
+    if (cw >= 0 && cw < nchild) {
+      // DPP argmax of the gain keys; equal gains -> the lowest lane = the smaller feature
+      const bool valid = lane < F && rfeat >= 0 && rgain > -INFINITY;
+      const unsigned long long key = valid ? GainKey(rgain) : 0ull;
+      const unsigned long long m = WaveMaxU64(key);
+      const unsigned long long win = __ballot(valid && key == m);
+      const int id = __builtin_amdgcn_readlane(first ? 0 : child_id(cw), 0);  // x_* sit in lane 0
+      if (lane == 0) {
+        if (!first) write_node(cw, id);
+        if (m == 0) { nbest[id].feature = -1; nbest[id].gain = -INFINITY; s_gain[id] = -INFINITY; }
+      }
+      if (m != 0) {
+        const int wl = static_cast<int>(__builtin_ctzll(win));
+        if (lane == wl) { s_gain[id] = rgain; s_src[id] = cw * F + wl; }
+        copy_src = cw * F + wl;
+        copy_id = id;
+      }
+    }
   } else {
+    for (int c = wid; c < nchild; c += kWaves) {
+      if (!first && lane == 0) {
+        const int j = c >> 1;
+        const BExp& x = bs->exp[j];
+        x_c0 = x.c0; x_c1 = x.c1; x_ls = x.left_small;
+        x_pb = x.pbegin; x_pc = x.pcount; x_buf = x.pbuf; x_pg = x.pgcount;
+        lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+        small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
+      }
+      KeyG k{-INFINITY, 1 << 30, 0};
+      for (int f = lane; f < F; f += 64) {
+        const SplitResult& r = fbest[c * F + f];
+        if (r.feature < 0) continue;
+        KeyG cand{r.gain, f, 0};
+        if (KeyBetter(cand, k)) k = cand;
+      }
+      k = WaveArgmax(k);
+      if (lane == 0) {
+        const int id = first ? 0 : child_id(c);
+        if (!first) write_node(c, id);
+        if (k.gain == -INFINITY) {
+          nbest[id].feature = -1;
+          nbest[id].gain = -INFINITY;
+        } else {
+          nbest[id] = fbest[c * F + k.a];
+        }
+        s_gain[id] = k.gain;
+      }
+    }
+  }
+  stamp(1);
+  __syncthreads();
+  stamp(2);
+  if (wid != 0) {
+    if (copy_src >= 0 && lane < static_cast<int>(sizeof(SplitResult) / 4)) {
+      static_assert(sizeof(SplitResult) % 4 == 0, "SplitResult copied as dwords");
+      reinterpret_cast<uint32_t*>(nbest + copy_id)[lane] = reinterpret_cast<const uint32_t*>(fbest + copy_src)[lane];
+    }
+    return;
+  }
+  // ---- replay of the sequential best-first growth (one wave), resumed at the committed prefix. The frontier
+  // lives in registers (entry e: lane e % 64, slot e / 64) with each entry's gain and children, so a pop is
+  // a DPP argmax + v_readlane of the winner and one broadcast LDS read of its children - no LDS round trip
+  // for the frontier itself (the LDS-array replay cost ~1.1 us per pop, 8 us of a 15.6 us plan; r5 pass 22)
+  int nf = 1, pops = 0, nch = 0;
+  if (!first) {
     nf = s_rp[0];
     pops = s_rp[1];
     for (int i = lane; i < pops; i += 64) s_pop[p_node[i]] = i;
+  }
+  double fg[kSlots];
+  int fc0[kSlots], fc1[kSlots];
+#pragma unroll
+  for (int q = 0; q < kSlots; ++q) {
+    const bool in = q * 64 + lane < nf;
+    const int v = in && fn[q] >= 0 && fn[q] < nnodes ? fn[q] : 0;  // out-of-range ids are caught when popped
+    fg[q] = in ? s_gain[v] : -INFINITY;
+    fc0[q] = s_c0[v];
+    fc1[q] = s_c1[v];
   }
   const int committed = pops;
   WaveSync();
   const int spec_room = max(1, min(spec_k, bs->cap_exp - bs->expanded));
   const bool may_spec = bs->spec_used < budget && nnodes + 2 * spec_k <= bs->cap_nodes;
+  constexpr int kFrontCap = kSlots * 64 < kBatchMaxLeaves ? kSlots * 64 : kBatchMaxLeaves;
   while (pops < budget) {
-    SimKey k{-INFINITY, 1 << 30, -1};
-    for (int i = lane; i < nf; i += 64) {
-      SimKey c{f_gain[i], f_li[i], i};
-      if (c.gain > -INFINITY && SimBetter(c, k)) k = c;
-    }
-    // entries sit in lanes < nf: the xor steps above the highest occupied lane are skipped and lane 0's
-    // result broadcast with v_readlane (the same winner - the maximum over the same entries - for a
-    // frontier of <= 32 entries in 5 dependent shuffle rounds instead of 6, <= 16 in 4)
-    const int top = nf <= 16 ? 8 : (nf <= 32 ? 16 : 32);
+    // the sequential argmax: larger gain, then smaller leaf index (leaf indices are distinct)
+    unsigned long long key = 0;
+    int bli = INT_MAX, bsl = 0;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      if (off > top) continue;
-      SimKey o;
-      o.gain = __shfl_xor(k.gain, off, 64);
-      o.li = __shfl_xor(k.li, off, 64);
-      o.idx = __shfl_xor(k.idx, off, 64);
-      if (SimBetter(o, k)) k = o;
+    for (int q = 0; q < kSlots; ++q) {
+      if (q * 64 + lane < nf && fg[q] > -INFINITY) {
+        const unsigned long long kq = GainKey(fg[q]);
+        if (kq > key || (kq == key && fl[q] < bli)) { key = kq; bli = fl[q]; bsl = q; }
+      }
     }
-    if (top < 32) {
-      k.gain = ReadLaneD(k.gain, 0);
-      k.li = __builtin_amdgcn_readlane(k.li, 0);
-      k.idx = __builtin_amdgcn_readlane(k.idx, 0);
+    const unsigned long long m = WaveMaxU64(key);
+    if (m <= 0x8000000000000000ull) break;  // no entry, or the best gain is not > 0
+    const unsigned long long tied = __ballot(key == m);
+    int w;
+    if (__popcll(tied) == 1) {
+      w = static_cast<int>(__builtin_ctzll(tied));
+    } else {  // equal gains: the smallest leaf index among them
+      const int mli = WaveMinI32(key == m ? bli : INT_MAX);
+      w = static_cast<int>(__builtin_ctzll(__ballot(key == m && bli == mli)));
     }
-    if (k.idx < 0 || !(k.gain > 0.0)) break;
-    const int v = f_node[k.idx];
-    if (v < 0 || v >= nnodes || nf > kBatchMaxLeaves - 1) {  // invariant broken: stop (host raises), never fault
+    const int ws = __builtin_amdgcn_readlane(bsl, w);
+    const int v = __builtin_amdgcn_readlane(SlotSel(fn, ws), w);
+    const int li = __builtin_amdgcn_readlane(SlotSel(fl, ws), w);
+    const int a = __builtin_amdgcn_readlane(SlotSel(fc0, ws), w);
+    const int b = __builtin_amdgcn_readlane(SlotSel(fc1, ws), w);
+    if (v < 0 || v >= nnodes || nf > kFrontCap - 1) {  // invariant broken: stop (host raises), never fault
       if (lane == 0) { bs->done = 1; bs->nexp = 0; SetHostFlag(host_flag, 2); }
       return;
     }
-    const bool explored = s_c0[v] >= 0;
+    const bool explored = a >= 0;
     if (!explored && nch == 0) {
       // the first unexplored pop: everything before it is final, so commit the frontier and the pops
-      for (int i = lane; i < nf; i += 64) { bs->rp_fnode[i] = f_node[i]; bs->rp_fli[i] = f_li[i]; bs->rp_fgain[i] = f_gain[i]; }
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q)
+        if (q * 64 + lane < nf) { bs->rp_fnode[q * 64 + lane] = fn[q]; bs->rp_fli[q * 64 + lane] = fl[q]; }
       for (int i = committed + lane; i < pops; i += 64) { bs->rp_pnode[i] = p_node[i]; bs->rp_pli[i] = p_li[i]; }
       if (lane == 0) { bs->rp_nf = nf; bs->rp_pops = pops; }
-      WaveSync();  // the lanes' reads of the frontier happen before lane 0 edits it below
     }
-    if (lane == 0) {
-      const int last = nf - 1;  // the popped entry is replaced by the last one
-      f_node[k.idx] = f_node[last]; f_li[k.idx] = f_li[last]; f_gain[k.idx] = f_gain[last];
-      if (explored) {
-        const int a = s_c0[v], b = s_c1[v];
-        f_node[last] = a; f_li[last] = k.li; f_gain[last] = s_gain[a];
-        f_node[last + 1] = b; f_li[last + 1] = pops + 1; f_gain[last + 1] = s_gain[b];
-        p_node[pops] = v; p_li[pops] = k.li;
-        s_pop[v] = pops;
-      } else {
-        ch_node[nch] = v;
+    if (explored) {
+      // the popped entry becomes child a (it keeps the leaf index), child b is appended with leaf pops + 1
+      const int ua = a < nnodes ? a : 0, ub = b >= 0 && b < nnodes ? b : 0;
+      const double ga = s_gain[ua], gb = s_gain[ub];
+      const int a0 = s_c0[ua], a1 = s_c1[ua], b0 = s_c0[ub], b1 = s_c1[ub];
+      const int nl = nf & 63, ns = nf >> 6;
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) {
+        if (q == ws && lane == w) { fn[q] = a; fg[q] = ga; fc0[q] = a0; fc1[q] = a1; }
+        if (q == ns && lane == nl) { fn[q] = b; fl[q] = pops + 1; fg[q] = gb; fc0[q] = b0; fc1[q] = b1; }
       }
-    }
-    nf = explored ? nf + 1 : nf - 1;
-    if (!explored) {
+      if (lane == 0) { p_node[pops] = v; p_li[pops] = li; s_pop[v] = pops; }
+      ++nf;
+    } else {
+      // the popped entry is replaced by the last one
+      const int ll = (nf - 1) & 63, ls = (nf - 1) >> 6;
+      const int xn = __builtin_amdgcn_readlane(SlotSel(fn, ls), ll);
+      const int xl = __builtin_amdgcn_readlane(SlotSel(fl, ls), ll);
+      const double xg = ReadLaneD(SlotSel(fg, ls), ll);
+      const int x0 = __builtin_amdgcn_readlane(SlotSel(fc0, ls), ll);
+      const int x1 = __builtin_amdgcn_readlane(SlotSel(fc1, ls), ll);
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q)
+        if (q == ws && lane == w) { fn[q] = xn; fl[q] = xl; fg[q] = xg; fc0[q] = x0; fc1[q] = x1; }
+      if (lane == 0) ch_node[nch] = v;
+      --nf;
       ++nch;
       if (nch >= spec_room || !may_spec) { ++pops; break; }
     }
@@ -2604,6 +2733,8 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     WaveSync();
   }
   WaveSync();
+  stamp(3);
+  if (prof != nullptr && tid == 0) prof[5] = pops - committed;
   if (nch == 0) {
     // ---- the tree is final: write it in sequential numbering. Pop i = internal node i; its left child
     // keeps the popped leaf's index, its right child gets leaf index i + 1.
@@ -2626,8 +2757,10 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       t.icount[i] = P.gcount;
     }
     // leaves: the final frontier (every entry is a node never popped) plus, for a stump, the root
-    for (int i = lane; i < nf; i += 64) {
-      const int v = f_node[i], li = f_li[i];
+#pragma unroll
+    for (int q = 0; q < kSlots; ++q) {
+      if (q * 64 + lane >= nf) continue;
+      const int v = fn[q], li = fl[q];
       const BNode L = nodes[v];
       t.lval[li] = L.out;
       t.lweight[li] = L.sum_h;
@@ -2648,6 +2781,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       bs->nexp = 0;
       SetHostFlag(host_flag, 1);
     }
+    stamp(4);
     return;
   }
   // ---- plan this round's expansions: ch_node[0] is the sequential learner's next split, the rest are
@@ -2655,7 +2789,8 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   const int base = nnodes;
   if (lane < nch) {
     const int j = lane, v = ch_node[j];
-    const SplitResult sr = nbest[v];
+    const int src = s_src[v];  // absorbed this round: its record is still being copied into nbest
+    const SplitResult sr = src >= 0 ? fbest[src] : nbest[v];
     const BNode P = nodes[v];
     const int a = base + 2 * j, b = a + 1;
     BNode L = P, R = P;
@@ -2676,7 +2811,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     BExp x;
     x.node = v; x.c0 = a; x.c1 = b;
     x.left_small = sr.left_cnt <= sr.right_cnt ? 1 : 0;
-    x.pbegin = P.begin; x.pcount = P.count; x.pbuf = P.buf;
+    x.pbegin = P.begin; x.pcount = P.count; x.pbuf = P.buf; x.pgcount = P.gcount;
     x.ps.feature = sr.feature;
     x.ps.is_cat = sr.is_cat;
     x.ps.dleft = sr.default_left;
@@ -2705,6 +2840,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     bs->spec_used += nch - 1;
     SetHostFlag(host_flag, 0);
   }
+  stamp(4);
 }
 
 // One tile's rows in registers (the software-pipelined batched partition below keeps two).
@@ -3318,6 +3454,14 @@ class GpuBackend : public TrainBackend {
     if (pinned_) (void)hipHostFree(pinned_);
     for (hipEvent_t e : bev_) if (e) (void)hipEventDestroy(e);
     if (bflag_host_) (void)hipHostFree(bflag_host_);
+    if (bprof_) {
+      if (bprof_n_ > 0) {  // wall_clock64 ticks at 100 MHz: 10 ns
+        std::fprintf(stderr, "bplan phases (us/round over %lld rounds): absorb %.2f stage %.2f replay %.2f plan %.2f "
+                     "pops/round %.2f\n", bprof_n_, bprof_sum_[0] / bprof_n_ * 1e-2, bprof_sum_[1] / bprof_n_ * 1e-2,
+                     bprof_sum_[2] / bprof_n_ * 1e-2, bprof_sum_[3] / bprof_n_ * 1e-2, bprof_sum_[4] / bprof_n_);
+      }
+      (void)hipFree(bprof_);
+    }
   }
   std::string Name() const override { return "hip"; }
 
@@ -3380,9 +3524,15 @@ class GpuBackend : public TrainBackend {
     if (batch_ok_) {
       bstate_.alloc(1);
       bnodes_.alloc(cap_nodes);
+      plan_cap_ = cap_nodes;
       nbest_.alloc(cap_nodes);
       SML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&bflag_host_), sizeof(int) * kBRing, hipHostMallocMapped | hipHostMallocCoherent));
       SML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&bflag_dev_), bflag_host_, 0));
+      if (const char* e = std::getenv("SML_BPLAN_PROF"); e != nullptr && std::atoi(e) != 0) {
+        const size_t nb = sizeof(long long) * 8 * (cfg.num_leaves + 3);
+        SML_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&bprof_), nb));
+        SML_HIP_CHECK(hipMemset(bprof_, 0, nb));
+      }
       for (hipEvent_t& e : bev_) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     // launch-shape knobs for A/B runs (defaults are the measured best)
@@ -3896,6 +4046,7 @@ class GpuBackend : public TrainBackend {
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup, true>)
                                              : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true>
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup>)));
+    if (bprof_) SML_HIP_CHECK(hipMemsetAsync(bprof_, 0, sizeof(long long) * 8 * (max_rounds + 1), stream_));
     int r = 0;
     for (; r <= max_rounds; ++r) {
       if (r >= blook_) {
@@ -3905,9 +4056,10 @@ class GpuBackend : public TrainBackend {
         if (fl == 2) throw std::runtime_error("batched tree growth: device replay invariant violated");
         if (fl) break;
       }
-      hipLaunchKernelGGL(bplan_kernel, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
+      hipLaunchKernelGGL(L_ <= 64 ? bplan_kernel<1> : bplan_kernel<4>, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
                          nbest_.get(), fbest_.get(), F_, part_.get(), E_, leaves_.get(), state_, dt_, fm_, mono_.get(),
-                         sp_.has_mono, r == 0 ? 1 : 0, spec_k_, budget, part_tile, bflag_dev_ + r % kBRing);
+                         sp_.has_mono, r == 0 ? 1 : 0, spec_k_, budget, part_tile, plan_cap_, bflag_dev_ + r % kBRing,
+                         bprof_ ? bprof_ + 8 * r : nullptr);
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(bev_[r % kBRing], stream_));
       hipLaunchKernelGGL(bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
@@ -3928,6 +4080,18 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipGetLastError());
     }
     if (r > max_rounds) throw std::runtime_error("batched tree growth did not finish within num_leaves rounds");
+    if (bprof_) {  // SML_BPLAN_PROF: the rounds' phase stamps (profiling only: a blocking copy per tree)
+      std::vector<long long> p(8 * (max_rounds + 1));
+      SML_HIP_CHECK(hipMemcpyAsync(p.data(), bprof_, p.size() * sizeof(long long), hipMemcpyDeviceToHost, stream_));
+      SML_HIP_CHECK(hipStreamSynchronize(stream_));
+      for (int q = 0; q < r; ++q) {
+        const long long* s = p.data() + 8 * q;
+        if (s[4] == 0) continue;  // a round queued behind the final plan (it returned at entry)
+        for (int k = 0; k < 4; ++k) bprof_sum_[k] += static_cast<double>(s[k + 1] - s[k]);
+        bprof_sum_[4] += static_cast<double>(s[5]);
+        ++bprof_n_;
+      }
+    }
   }
 
   // spin on an event (a blocking sync can sleep through the few microseconds the batched growth waits);
@@ -4513,6 +4677,10 @@ class GpuBackend : public TrainBackend {
   DevBuf<SplitResult> nbest_;
   int* bflag_host_ = nullptr;
   int* bflag_dev_ = nullptr;
+  int plan_cap_ = 0;            // node records allocated for the batched growth (the plan stages them all)
+  long long* bprof_ = nullptr;  // SML_BPLAN_PROF phase stamps, 8 per round
+  double bprof_sum_[5] = {0, 0, 0, 0, 0};
+  long long bprof_n_ = 0;
   hipEvent_t bev_[kBRing] = {};
   DTree dt_{};
   FeatMeta fm_{};

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-5 pass 22: bplan phase stamps (SML_BPLAN_PROF) next to its rocprof kernel time (tree breakdown).
+OUT=${1:-gpurun_out/r5p22}
+ROOT=$(pwd)
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
+SML_BPLAN_PROF=1 timeout -k 10 300 python bench.py --steps 3 --warmup 1 > "$OUT/bench_prof.log" 2> "$OUT/bplan_phases.txt" || exit 1
+tail -3 "$OUT/bplan_phases.txt"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_fit" -o fit -- python3 bench.py --steps 2 --warmup 1 > "$OUT/prof_fit.log" 2>&1 || exit 1
+python3 tools/prof_tree_breakdown.py "$(find "$OUT/prof_fit" -name '*kernel_trace.csv' -print -quit)" > "$OUT/tree_breakdown.txt" 2>&1
+rm -rf "$OUT/prof_fit"
+head -30 "$OUT/tree_breakdown.txt"
