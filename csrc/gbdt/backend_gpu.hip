@@ -527,6 +527,12 @@ __device__ __forceinline__ void WaveSync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ unsigned long long ReadLaneU64(unsigned long long v, int l) {
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v >> 32), l));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
 __device__ __forceinline__ double ReadLaneD(double v, int l) {
   const long long x = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
@@ -2405,6 +2411,7 @@ __device__ __forceinline__ int BatchSmallCount(const BState* bs, int j) {
 }
 
 constexpr int kPlanThreads = 1024;
+constexpr int kPlanProfStride = 16;  // SML_BPLAN_PROF slots per round
 constexpr int kPlanFm = 1024;  // features whose split metadata the plan stages in LDS
 
 // round outcome for the host (coherent pinned memory, read after the plan's event): system-scope vector store
@@ -2423,20 +2430,26 @@ __device__ __forceinline__ unsigned long long DppMaxU64(unsigned long long x) {
   return y > x ? y : x;
 }
 
+// rows not in kRowMask keep x (the DPP write is masked off for them)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ unsigned long long DppMaxRowsU64(unsigned long long x) {
+  const int xl = static_cast<int>(x), xh = static_cast<int>(x >> 32);
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_update_dpp(xl, xl, kCtrl, kRowMask, 0xF, false));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_update_dpp(xh, xh, kCtrl, kRowMask, 0xF, false));
+  const unsigned long long y = (static_cast<unsigned long long>(hi) << 32) | lo;
+  return y > x ? y : x;
+}
+
 __device__ __forceinline__ unsigned long long WaveMaxU64(unsigned long long x) {
   x = DppMaxU64<0xB1>(x);   // quad_perm [1,0,3,2]
   x = DppMaxU64<0x4E>(x);   // quad_perm [2,3,0,1]
   x = DppMaxU64<0x141>(x);  // row_half_mirror
-  x = DppMaxU64<0x140>(x);  // row_mirror
-  unsigned long long m = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x), 16 * r));
-    const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x >> 32), 16 * r));
-    const unsigned long long y = (static_cast<unsigned long long>(hi) << 32) | lo;
-    m = y > m ? y : m;
-  }
-  return m;
+  x = DppMaxU64<0x140>(x);  // row_mirror: every lane holds its row's maximum
+  x = DppMaxRowsU64<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3 fold in rows 0, 2
+  x = DppMaxRowsU64<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3 fold in row 1: lane 63 holds the maximum
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x >> 32), 63));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
 }
 
 __device__ __forceinline__ int WaveMinI32(int x) {
@@ -2481,7 +2494,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   __shared__ int s_c0[kBatchMaxNodes], s_c1[kBatchMaxNodes], s_pop[kBatchMaxNodes];
   __shared__ int p_node[kBatchMaxLeaves], p_li[kBatchMaxLeaves];
   __shared__ int ch_node[kMaxSpec];
-  __shared__ int s_rp[2], s_hdr[3];
+  __shared__ int s_rp[2], s_hdr[7];  // done, nnodes, nexp, cap_exp, expanded, spec_used, cap_nodes
   __shared__ int s_nb[kPlanFm], s_mt[kPlanFm], s_db[kPlanFm];
   // ---- phase 0: every load that does not depend on this round's header (done / nnodes / nexp) goes out
   // together - the header, the last round's expansion records and their children's per-feature best splits
@@ -2510,11 +2523,16 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       bs->cap_exp = 2 * budget + kMaxSpec;
       bs->cap_nodes = min(kBatchMaxNodes, 1 + 2 * bs->cap_exp);
       s_hdr[0] = 0; s_hdr[1] = 1; s_hdr[2] = 0;
+      s_hdr[3] = 2 * budget + kMaxSpec; s_hdr[4] = 0; s_hdr[5] = 0;
+      s_hdr[6] = min(kBatchMaxNodes, 1 + 2 * s_hdr[3]);
       s_c0[0] = -1; s_c1[0] = -1; s_pop[0] = -1; s_src[0] = -1;
     }
     if (fast && cw == 0 && lane < F) { rfeat = fbest[lane].feature; rgain = fbest[lane].gain; }
   } else {
-    if (tid == 0) { s_hdr[0] = bs->done; s_hdr[1] = bs->nnodes; s_hdr[2] = bs->nexp; }
+    if (tid == 0) {
+      s_hdr[0] = bs->done; s_hdr[1] = bs->nnodes; s_hdr[2] = bs->nexp;
+      s_hdr[3] = bs->cap_exp; s_hdr[4] = bs->expanded; s_hdr[5] = bs->spec_used; s_hdr[6] = bs->cap_nodes;
+    }
     if (fast && cw >= 0 && cw < 2 * spec_k) {
       const int j = cw >> 1;
       if (lane == 0) {
@@ -2646,31 +2664,33 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     pops = s_rp[1];
     for (int i = lane; i < pops; i += 64) s_pop[p_node[i]] = i;
   }
-  double fg[kSlots];
+  // fk: the entry's gain as an order-preserving key (GainKey), 0 for no candidate (-inf / NaN gain, or a slot
+  // past the frontier), so the argmax needs no per-pop validity test
+  unsigned long long fk[kSlots];
   int fc0[kSlots], fc1[kSlots];
+  auto gkey = [](double g) { return g > -INFINITY ? GainKey(g) : 0ull; };
 #pragma unroll
   for (int q = 0; q < kSlots; ++q) {
     const bool in = q * 64 + lane < nf;
     const int v = in && fn[q] >= 0 && fn[q] < nnodes ? fn[q] : 0;  // out-of-range ids are caught when popped
-    fg[q] = in ? s_gain[v] : -INFINITY;
+    fk[q] = in ? gkey(s_gain[v]) : 0ull;
     fc0[q] = s_c0[v];
     fc1[q] = s_c1[v];
   }
   const int committed = pops;
   WaveSync();
-  const int spec_room = max(1, min(spec_k, bs->cap_exp - bs->expanded));
-  const bool may_spec = bs->spec_used < budget && nnodes + 2 * spec_k <= bs->cap_nodes;
+  const long long c_start = prof != nullptr ? static_cast<long long>(__builtin_amdgcn_s_memtime()) : 0;
+  const int spec_room = max(1, min(spec_k, s_hdr[3] - s_hdr[4]));
+  const bool may_spec = s_hdr[5] < budget && nnodes + 2 * spec_k <= s_hdr[6];
   constexpr int kFrontCap = kSlots * 64 < kBatchMaxLeaves ? kSlots * 64 : kBatchMaxLeaves;
   while (pops < budget) {
     // the sequential argmax: larger gain, then smaller leaf index (leaf indices are distinct)
-    unsigned long long key = 0;
-    int bli = INT_MAX, bsl = 0;
+    unsigned long long key = fk[0];
+    int bli = fl[0], bsl = 0;
 #pragma unroll
-    for (int q = 0; q < kSlots; ++q) {
-      if (q * 64 + lane < nf && fg[q] > -INFINITY) {
-        const unsigned long long kq = GainKey(fg[q]);
-        if (kq > key || (kq == key && fl[q] < bli)) { key = kq; bli = fl[q]; bsl = q; }
-      }
+    for (int q = 1; q < kSlots; ++q) {
+      const unsigned long long kq = fk[q];
+      if (kq > key || (kq == key && fl[q] < bli)) { key = kq; bli = fl[q]; bsl = q; }
     }
     const unsigned long long m = WaveMaxU64(key);
     if (m <= 0x8000000000000000ull) break;  // no entry, or the best gain is not > 0
@@ -2703,13 +2723,13 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     if (explored) {
       // the popped entry becomes child a (it keeps the leaf index), child b is appended with leaf pops + 1
       const int ua = a < nnodes ? a : 0, ub = b >= 0 && b < nnodes ? b : 0;
-      const double ga = s_gain[ua], gb = s_gain[ub];
+      const unsigned long long ka = gkey(s_gain[ua]), kb = gkey(s_gain[ub]);
       const int a0 = s_c0[ua], a1 = s_c1[ua], b0 = s_c0[ub], b1 = s_c1[ub];
       const int nl = nf & 63, ns = nf >> 6;
 #pragma unroll
       for (int q = 0; q < kSlots; ++q) {
-        if (q == ws && lane == w) { fn[q] = a; fg[q] = ga; fc0[q] = a0; fc1[q] = a1; }
-        if (q == ns && lane == nl) { fn[q] = b; fl[q] = pops + 1; fg[q] = gb; fc0[q] = b0; fc1[q] = b1; }
+        if (q == ws && lane == w) { fn[q] = a; fk[q] = ka; fc0[q] = a0; fc1[q] = a1; }
+        if (q == ns && lane == nl) { fn[q] = b; fl[q] = pops + 1; fk[q] = kb; fc0[q] = b0; fc1[q] = b1; }
       }
       if (lane == 0) { p_node[pops] = v; p_li[pops] = li; s_pop[v] = pops; }
       ++nf;
@@ -2718,12 +2738,14 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       const int ll = (nf - 1) & 63, ls = (nf - 1) >> 6;
       const int xn = __builtin_amdgcn_readlane(SlotSel(fn, ls), ll);
       const int xl = __builtin_amdgcn_readlane(SlotSel(fl, ls), ll);
-      const double xg = ReadLaneD(SlotSel(fg, ls), ll);
+      const unsigned long long xk = ReadLaneU64(SlotSel(fk, ls), ll);
       const int x0 = __builtin_amdgcn_readlane(SlotSel(fc0, ls), ll);
       const int x1 = __builtin_amdgcn_readlane(SlotSel(fc1, ls), ll);
 #pragma unroll
-      for (int q = 0; q < kSlots; ++q)
-        if (q == ws && lane == w) { fn[q] = xn; fl[q] = xl; fg[q] = xg; fc0[q] = x0; fc1[q] = x1; }
+      for (int q = 0; q < kSlots; ++q) {
+        if (q == ws && lane == w) { fn[q] = xn; fl[q] = xl; fk[q] = xk; fc0[q] = x0; fc1[q] = x1; }
+        if (q == ls && lane == ll) fk[q] = 0;  // after the move: the last slot leaves the frontier
+      }
       if (lane == 0) ch_node[nch] = v;
       --nf;
       ++nch;
@@ -2734,7 +2756,26 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   }
   WaveSync();
   stamp(3);
-  if (prof != nullptr && tid == 0) prof[5] = pops - committed;
+  if (prof != nullptr && tid == 0) {
+    prof[5] = pops - committed;
+    prof[6] = static_cast<long long>(__builtin_amdgcn_s_memtime()) - c_start;  // shader clocks of the pop loop
+  }
+  if (nch == 0 && prof != nullptr) {
+    // profiling: every expanded node (children allocated) and the ones the sequential order never popped
+    long long er = 0, wr = 0;
+    int ec = 0, wc = 0;
+    for (int i = lane; i < nnodes; i += 64) {
+      if (s_c0[i] < 0) continue;
+      const int cnt = nodes[i].count;
+      er += cnt; ++ec;
+      if (s_pop[i] < 0) { wr += cnt; ++wc; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      er += __shfl_xor(er, off, 64); wr += __shfl_xor(wr, off, 64);
+      ec += __shfl_xor(ec, off, 64); wc += __shfl_xor(wc, off, 64);
+    }
+    if (lane == 0) { prof[7] = er; prof[8] = wr; prof[9] = ec; prof[10] = wc; }
+  }
   if (nch == 0) {
     // ---- the tree is final: write it in sequential numbering. Pop i = internal node i; its left child
     // keeps the popped leaf's index, its right child gets leaf index i + 1.
@@ -2836,8 +2877,8 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   if (lane == 0) {
     bs->nexp = nch;
     bs->nnodes = base + 2 * nch;
-    bs->expanded += nch;
-    bs->spec_used += nch - 1;
+    bs->expanded = s_hdr[4] + nch;
+    bs->spec_used = s_hdr[5] + nch - 1;
     SetHostFlag(host_flag, 0);
   }
   stamp(4);
@@ -3457,8 +3498,15 @@ class GpuBackend : public TrainBackend {
     if (bprof_) {
       if (bprof_n_ > 0) {  // wall_clock64 ticks at 100 MHz: 10 ns
         std::fprintf(stderr, "bplan phases (us/round over %lld rounds): absorb %.2f stage %.2f replay %.2f plan %.2f "
-                     "pops/round %.2f\n", bprof_n_, bprof_sum_[0] / bprof_n_ * 1e-2, bprof_sum_[1] / bprof_n_ * 1e-2,
-                     bprof_sum_[2] / bprof_n_ * 1e-2, bprof_sum_[3] / bprof_n_ * 1e-2, bprof_sum_[4] / bprof_n_);
+                     "pops/round %.2f pop-loop clocks/round %.0f\n", bprof_n_, bprof_sum_[0] / bprof_n_ * 1e-2,
+                     bprof_sum_[1] / bprof_n_ * 1e-2, bprof_sum_[2] / bprof_n_ * 1e-2, bprof_sum_[3] / bprof_n_ * 1e-2,
+                     bprof_sum_[4] / bprof_n_, bprof_sum_[5] / bprof_n_);
+      }
+      if (bprof_trees_ > 0) {
+        const double t = static_cast<double>(bprof_trees_);
+        std::fprintf(stderr, "bplan trees %lld: expansions/tree %.2f (never popped %.2f), partitioned rows/tree %.0f "
+                     "(in never-popped nodes %.0f)\n", bprof_trees_, bprof_tree_[2] / t, bprof_tree_[3] / t,
+                     bprof_tree_[0] / t, bprof_tree_[1] / t);
       }
       (void)hipFree(bprof_);
     }
@@ -3529,7 +3577,7 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&bflag_host_), sizeof(int) * kBRing, hipHostMallocMapped | hipHostMallocCoherent));
       SML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&bflag_dev_), bflag_host_, 0));
       if (const char* e = std::getenv("SML_BPLAN_PROF"); e != nullptr && std::atoi(e) != 0) {
-        const size_t nb = sizeof(long long) * 8 * (cfg.num_leaves + 3);
+        const size_t nb = sizeof(long long) * kPlanProfStride * (cfg.num_leaves + 3);
         SML_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&bprof_), nb));
         SML_HIP_CHECK(hipMemset(bprof_, 0, nb));
       }
@@ -4046,7 +4094,7 @@ class GpuBackend : public TrainBackend {
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup, true>)
                                              : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true>
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup>)));
-    if (bprof_) SML_HIP_CHECK(hipMemsetAsync(bprof_, 0, sizeof(long long) * 8 * (max_rounds + 1), stream_));
+    if (bprof_) SML_HIP_CHECK(hipMemsetAsync(bprof_, 0, sizeof(long long) * kPlanProfStride * (max_rounds + 1), stream_));
     int r = 0;
     for (; r <= max_rounds; ++r) {
       if (r >= blook_) {
@@ -4059,7 +4107,7 @@ class GpuBackend : public TrainBackend {
       hipLaunchKernelGGL(L_ <= 64 ? bplan_kernel<1> : bplan_kernel<4>, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
                          nbest_.get(), fbest_.get(), F_, part_.get(), E_, leaves_.get(), state_, dt_, fm_, mono_.get(),
                          sp_.has_mono, r == 0 ? 1 : 0, spec_k_, budget, part_tile, plan_cap_, bflag_dev_ + r % kBRing,
-                         bprof_ ? bprof_ + 8 * r : nullptr);
+                         bprof_ ? bprof_ + kPlanProfStride * r : nullptr);
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(bev_[r % kBRing], stream_));
       hipLaunchKernelGGL(bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
@@ -4081,14 +4129,19 @@ class GpuBackend : public TrainBackend {
     }
     if (r > max_rounds) throw std::runtime_error("batched tree growth did not finish within num_leaves rounds");
     if (bprof_) {  // SML_BPLAN_PROF: the rounds' phase stamps (profiling only: a blocking copy per tree)
-      std::vector<long long> p(8 * (max_rounds + 1));
+      std::vector<long long> p(kPlanProfStride * (max_rounds + 1));
       SML_HIP_CHECK(hipMemcpyAsync(p.data(), bprof_, p.size() * sizeof(long long), hipMemcpyDeviceToHost, stream_));
       SML_HIP_CHECK(hipStreamSynchronize(stream_));
       for (int q = 0; q < r; ++q) {
-        const long long* s = p.data() + 8 * q;
+        const long long* s = p.data() + kPlanProfStride * q;
+        if (s[9] > 0) {  // the final round: the tree's expansions and the ones never popped
+          for (int k = 0; k < 4; ++k) bprof_tree_[k] += static_cast<double>(s[7 + k]);
+          ++bprof_trees_;
+        }
         if (s[4] == 0) continue;  // a round queued behind the final plan (it returned at entry)
         for (int k = 0; k < 4; ++k) bprof_sum_[k] += static_cast<double>(s[k + 1] - s[k]);
         bprof_sum_[4] += static_cast<double>(s[5]);
+        bprof_sum_[5] += static_cast<double>(s[6]);
         ++bprof_n_;
       }
     }
@@ -4678,8 +4731,10 @@ class GpuBackend : public TrainBackend {
   int* bflag_host_ = nullptr;
   int* bflag_dev_ = nullptr;
   int plan_cap_ = 0;            // node records allocated for the batched growth (the plan stages them all)
-  long long* bprof_ = nullptr;  // SML_BPLAN_PROF phase stamps, 8 per round
-  double bprof_sum_[5] = {0, 0, 0, 0, 0};
+  long long* bprof_ = nullptr;  // SML_BPLAN_PROF phase stamps, kPlanProfStride per round
+  double bprof_sum_[6] = {0, 0, 0, 0, 0, 0};
+  double bprof_tree_[4] = {0, 0, 0, 0};  // rows partitioned, of them in never-popped nodes; expansions, wasted
+  long long bprof_trees_ = 0;
   long long bprof_n_ = 0;
   hipEvent_t bev_[kBRing] = {};
   DTree dt_{};
