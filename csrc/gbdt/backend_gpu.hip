@@ -3171,7 +3171,7 @@ __global__ __launch_bounds__(256) void bfind_kernel(const BState* __restrict__ b
   hist_pool[static_cast<size_t>(child) * E + e] = mine;
   const BNode nd = nodes[child];
   const int64_t small_cnt = static_cast<int64_t>(pj[E].x);
-  const int64_t cnt = c == 0 ? small_cnt : nodes[x.node].gcount - small_cnt;
+  const int64_t cnt = c == 0 ? small_cnt : x.pgcount - small_cnt;
   SearchFeatureBlock(mine, nd.sum_g, nd.sum_h, cnt, nd.depth, 0, nd.lo, nd.hi, f, F, fm, sp,
                      fbest + static_cast<size_t>(blockIdx.y) * F + f, true);
 }
