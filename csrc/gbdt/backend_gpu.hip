@@ -243,6 +243,7 @@ struct RankTables {
   int nq, ngain, max_position, norm;
   int gain_mono;  // label gains strictly increasing (the register kernel's kMono form)
   int nreg;
+  int prof_phase;  // SML_RANK_PROF_PHASE (timing only, gradients wrong): 1 = identity ranks (no rank count)
   double sigma;
 };
 constexpr int kGainLds = 64;  // label gains staged in LDS by the register kernel (longer tables: global)
@@ -623,7 +624,12 @@ __device__ void LambdarankQueryRegs(const RankTables& t, int q, const double* __
       if (u * 64 + lane < cnt) s_doc_of_rank[rk[u]] = u * 64 + lane;
     WaveSync();
   };
-  count_ranks(false);
+  if (t.prof_phase == 1) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) rk[u] = u * 64 + lane;
+  } else {
+    count_ranks(false);
+  }
   scatter();
   bool clash = false;
 #pragma unroll
@@ -4363,6 +4369,8 @@ class GpuBackend : public TrainBackend {
     }
     const char* me = std::getenv("SML_RANK_MONO");  // 0: the label-compare form (A/B and tests), read per booster
     rank_.gain_mono = me && std::atoi(me) == 0 ? 0 : (mono ? 1 : 0);
+    const char* pp = std::getenv("SML_RANK_PROF_PHASE");
+    rank_.prof_phase = pp ? std::atoi(pp) : 0;
     rank_ready_ = true;
   }
 
