@@ -2473,12 +2473,28 @@ __device__ __forceinline__ unsigned long long GainKey(double g) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
-// entry `s` of a per-lane register array picked by a wave-uniform slot (a select chain, no scratch)
-template <int kSlots, typename T>
-__device__ __forceinline__ T SlotSel(const T (&a)[kSlots], int s) {
-  T v = a[0];
+// lane l's entry `s` of a per-lane register array, `s` wave-uniform: every slot is read with v_readlane and
+// the scalar results selected (a select over the register array itself was turned back into an indexed
+// scratch load for kSlots = 4)
+template <int kSlots>
+__device__ __forceinline__ int SlotReadLane(const int (&a)[kSlots], int s, int l) {
+  int v = __builtin_amdgcn_readlane(a[0], l);
 #pragma unroll
-  for (int i = 1; i < kSlots; ++i) v = s == i ? a[i] : v;
+  for (int i = 1; i < kSlots; ++i) {
+    const int x = __builtin_amdgcn_readlane(a[i], l);
+    v = s == i ? x : v;
+  }
+  return v;
+}
+
+template <int kSlots>
+__device__ __forceinline__ unsigned long long SlotReadLaneU64(const unsigned long long (&a)[kSlots], int s, int l) {
+  unsigned long long v = ReadLaneU64(a[0], l);
+#pragma unroll
+  for (int i = 1; i < kSlots; ++i) {
+    const unsigned long long x = ReadLaneU64(a[i], l);
+    v = s == i ? x : v;
+  }
   return v;
 }
 
@@ -2709,10 +2725,10 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       w = static_cast<int>(__builtin_ctzll(__ballot(key == m && bli == mli)));
     }
     const int ws = __builtin_amdgcn_readlane(bsl, w);
-    const int v = __builtin_amdgcn_readlane(SlotSel(fn, ws), w);
-    const int li = __builtin_amdgcn_readlane(SlotSel(fl, ws), w);
-    const int a = __builtin_amdgcn_readlane(SlotSel(fc0, ws), w);
-    const int b = __builtin_amdgcn_readlane(SlotSel(fc1, ws), w);
+    const int v = SlotReadLane(fn, ws, w);
+    const int li = SlotReadLane(fl, ws, w);
+    const int a = SlotReadLane(fc0, ws, w);
+    const int b = SlotReadLane(fc1, ws, w);
     if (v < 0 || v >= nnodes || nf > kFrontCap - 1) {  // invariant broken: stop (host raises), never fault
       if (lane == 0) { bs->done = 1; bs->nexp = 0; SetHostFlag(host_flag, 2); }
       return;
@@ -2742,11 +2758,11 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     } else {
       // the popped entry is replaced by the last one
       const int ll = (nf - 1) & 63, ls = (nf - 1) >> 6;
-      const int xn = __builtin_amdgcn_readlane(SlotSel(fn, ls), ll);
-      const int xl = __builtin_amdgcn_readlane(SlotSel(fl, ls), ll);
-      const unsigned long long xk = ReadLaneU64(SlotSel(fk, ls), ll);
-      const int x0 = __builtin_amdgcn_readlane(SlotSel(fc0, ls), ll);
-      const int x1 = __builtin_amdgcn_readlane(SlotSel(fc1, ls), ll);
+      const int xn = SlotReadLane(fn, ls, ll);
+      const int xl = SlotReadLane(fl, ls, ll);
+      const unsigned long long xk = SlotReadLaneU64(fk, ls, ll);
+      const int x0 = SlotReadLane(fc0, ls, ll);
+      const int x1 = SlotReadLane(fc1, ls, ll);
 #pragma unroll
       for (int q = 0; q < kSlots; ++q) {
         if (q == ws && lane == w) { fn[q] = xn; fl[q] = xl; fk[q] = xk; fc0[q] = x0; fc1[q] = x1; }
