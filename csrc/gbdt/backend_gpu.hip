@@ -3582,7 +3582,10 @@ class GpuBackend : public TrainBackend {
     // 4 expansions per round: r4 A/B at 11M x 28 (profiles/r4/gbdt2): spec 2 231 ms / fit, 4 217 ms, 8 247 ms,
     // one-split growth 250 ms - wider rounds mostly add never-popped expansions (the rounds follow the
     // parent -> child dependency chain of the pops, ~15 per tree at 31 leaves)
-    spec_k_ = 4;
+    // more leaves, wider rounds: r5 pass 48 (11M x 28, ms per iteration at spec 4 / 8 / 16): 63 leaves 2.10 /
+    // 2.16 / 2.84, 127 leaves 3.24 / 2.94 / 3.77, 255 leaves 5.28 / 4.39 / 4.48 (the per-round fixed cost -
+    // plan, reduce, split search, launch gaps - over ~L / 3.8 rounds outweighs the extra speculation)
+    spec_k_ = L_ > 64 ? 8 : 4;
     if (const char* e = std::getenv("SML_GBDT_SPEC")) spec_k_ = std::atoi(e);
     batch_ok_ = spec_k_ > 0 && L_ <= kBatchMaxLeaves && !(cfg.tree_learner == "voting" && comm_ && comm_->world() > 1);
     spec_k_ = std::max(1, std::min(kMaxSpec, spec_k_));
