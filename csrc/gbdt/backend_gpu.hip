@@ -2498,7 +2498,8 @@ __device__ __forceinline__ unsigned long long SlotReadLaneU64(const unsigned lon
   return v;
 }
 
-// kSlots: frontier entries per lane (entry e lives in lane e % 64, slot e / 64): 1 for num_leaves <= 64
+// kSlots: frontier entries per lane (entry e lives in lane e % 64, slot e / 64): 1 for num_leaves <= 64,
+// 2 up to 128, 4 up to 256
 template <int kSlots>
 __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     BState* __restrict__ bs, BNode* __restrict__ nodes, SplitResult* __restrict__ nbest,
@@ -4129,7 +4130,9 @@ class GpuBackend : public TrainBackend {
         if (fl == 2) throw std::runtime_error("batched tree growth: device replay invariant violated");
         if (fl) break;
       }
-      hipLaunchKernelGGL(L_ <= 64 ? bplan_kernel<1> : bplan_kernel<4>, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
+      // frontier slots per lane: a tree of L leaves has at most L frontier entries
+      auto plan = L_ <= 64 ? bplan_kernel<1> : (L_ <= 128 ? bplan_kernel<2> : bplan_kernel<4>);
+      hipLaunchKernelGGL(plan, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
                          nbest_.get(), fbest_.get(), F_, part_.get(), E_, leaves_.get(), state_, dt_, fm_, mono_.get(),
                          sp_.has_mono, r == 0 ? 1 : 0, spec_k_, budget, part_tile, plan_cap_, bflag_dev_ + r % kBRing,
                          bprof_ ? bprof_ + kPlanProfStride * r : nullptr);

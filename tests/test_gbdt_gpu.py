@@ -678,6 +678,7 @@ def test_gpu_ranking_metrics_on_device():
 
 
 @pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5", "num_leaves=63 max_depth=5",
+                                   "num_leaves=127 min_data_in_leaf=5",
                                    "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
                                    "num_leaves=2", "num_leaves=31 min_gain_to_split=5.0",
                                    "num_leaves=31 objective=multiclass num_class=3"])
@@ -685,7 +686,8 @@ def test_gpu_ranking_metrics_on_device():
 def test_gpu_batched_growth_equals_sequential(extra, spec, monkeypatch):
     """Batched speculative growth (bplan_kernel ..; SML_GBDT_SPEC=k expansions per round) builds exactly the
     trees of the one-split-at-a-time growth (SML_GBDT_SPEC=0): byte-identical model text, for small / deep /
-    depth-capped / categorical + monotone / stump-like / gain-limited / multiclass trees."""
+    depth-capped / categorical + monotone / stump-like / gain-limited / multiclass trees (31 / 63 / 127 / 255
+    leaves: the plan kernel's one, two and four frontier slots per lane)."""
     X, y = _data(n=80000, nan_frac=0.02, cat="categorical" in extra)
     if "multiclass" in extra:
         y = (np.digitize(np.nan_to_num(X[:, 0] + X[:, 1]), [-0.5, 0.5])).astype(np.float32)
