@@ -2527,13 +2527,24 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   // (header -> records -> parent count / record copy -> node gains; r5 pass 22: absorb 3.0 + stage 1.9 us)
   // children go to waves 1.. (wave 0 replays right after the barrier; the others copy the winning records
   // into nbest after it, off the replay's path - the plan reads a child absorbed this round from fbest)
-  const bool fast = F <= 64 && 2 * spec_k < kWaves;
-  const int cw = wid - 1;  // fast path: the child this wave absorbs
+  // absorbing waves 1 .. kWaves - 1 take children cw and cw + kAbs (two each at 8 expansions per round)
+  constexpr int kAbs = kWaves - 1;
+  const bool fast = F <= 64 && 2 * spec_k <= 2 * kAbs;
+  const int cw = wid - 1;  // fast path: this wave's first child
   __shared__ int s_src[kBatchMaxNodes];  // fbest record of a node absorbed this round (fast path), else -1
-  int x_c0 = 0, x_c1 = 0, x_ls = 0, x_pb = 0, x_pc = 0, x_buf = 0, lt = 0;
-  int64_t x_pg = 0, small_cnt = 0;
-  int rfeat = -1;
-  double rgain = -INFINITY;
+  int x_c0[2] = {0, 0}, x_c1[2] = {0, 0}, x_ls[2] = {0, 0}, x_pb[2] = {0, 0}, x_pc[2] = {0, 0};
+  int x_buf[2] = {0, 0}, lt[2] = {0, 0};
+  int64_t x_pg[2] = {0, 0}, small_cnt[2] = {0, 0};
+  int rfeat[2] = {-1, -1};
+  double rgain[2] = {-INFINITY, -INFINITY};
+  auto load_exp = [&](int c, int q) {  // lane 0: child c's expansion record, cursor and smaller-child count
+    const int j = c >> 1;
+    const BExp& x = bs->exp[j];
+    x_c0[q] = x.c0; x_c1[q] = x.c1; x_ls[q] = x.left_small;
+    x_pb[q] = x.pbegin; x_pc[q] = x.pcount; x_buf[q] = x.pbuf; x_pg[q] = x.pgcount;
+    lt[q] = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+    small_cnt[q] = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
+  };
   if (first) {
     if (tid == 0) {
       const DLeaf R = leaves[0];
@@ -2550,22 +2561,19 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       s_hdr[6] = min(kBatchMaxNodes, 1 + 2 * s_hdr[3]);
       s_c0[0] = -1; s_c1[0] = -1; s_pop[0] = -1; s_src[0] = -1;
     }
-    if (fast && cw == 0 && lane < F) { rfeat = fbest[lane].feature; rgain = fbest[lane].gain; }
+    if (fast && cw == 0 && lane < F) { rfeat[0] = fbest[lane].feature; rgain[0] = fbest[lane].gain; }
   } else {
     if (tid == 0) {
       s_hdr[0] = bs->done; s_hdr[1] = bs->nnodes; s_hdr[2] = bs->nexp;
       s_hdr[3] = bs->cap_exp; s_hdr[4] = bs->expanded; s_hdr[5] = bs->spec_used; s_hdr[6] = bs->cap_nodes;
     }
-    if (fast && cw >= 0 && cw < 2 * spec_k) {
-      const int j = cw >> 1;
-      if (lane == 0) {
-        const BExp& x = bs->exp[j];
-        x_c0 = x.c0; x_c1 = x.c1; x_ls = x.left_small;
-        x_pb = x.pbegin; x_pc = x.pcount; x_buf = x.pbuf; x_pg = x.pgcount;
-        lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
-        small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = cw + q * kAbs;
+      if (fast && cw >= 0 && c < 2 * spec_k) {
+        if (lane == 0) load_exp(c, q);
+        if (lane < F) { rfeat[q] = fbest[c * F + lane].feature; rgain[q] = fbest[c * F + lane].gain; }
       }
-      if (lane < F) { rfeat = fbest[cw * F + lane].feature; rgain = fbest[cw * F + lane].gain; }
     }
     for (int i = tid; i < cap_nodes; i += kPlanThreads) {
       const SplitResult& r = nbest[i];
@@ -2604,48 +2612,45 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   // ---- absorb: the children of last round's expansions (first: the root) get their best splits, global
   // counts and row segments (ties: smaller feature); their gains go to the staged LDS table
   const int nchild = first ? 1 : 2 * nexp;
-  auto child_id = [&](int c) {
-    const int small = x_ls ? x_c0 : x_c1;
-    return (c & 1) ? (small == x_c0 ? x_c1 : x_c0) : small;
+  auto child_id = [&](int c, int q) {
+    const int small = x_ls[q] ? x_c0[q] : x_c1[q];
+    return (c & 1) ? (small == x_c0[q] ? x_c1[q] : x_c0[q]) : small;
   };
-  auto write_node = [&](int c, int id) {
+  auto write_node = [&](int c, int id, int q) {
     BNode& nd = nodes[id];
-    const bool is_left = id == x_c0;
-    nd.begin = is_left ? x_pb : x_pb + lt;
-    nd.count = is_left ? lt : x_pc - lt;
-    nd.buf = x_buf == 0 ? 1 : 0;
-    nd.gcount = (c & 1) ? x_pg - small_cnt : small_cnt;
+    const bool is_left = id == x_c0[q];
+    nd.begin = is_left ? x_pb[q] : x_pb[q] + lt[q];
+    nd.count = is_left ? lt[q] : x_pc[q] - lt[q];
+    nd.buf = x_buf[q] == 0 ? 1 : 0;
+    nd.gcount = (c & 1) ? x_pg[q] - small_cnt[q] : small_cnt[q];
   };
-  int copy_src = -1, copy_id = 0;  // fast path: the record this wave copies into nbest after the barrier
+  // fast path: the records this wave copies into nbest after the barrier
+  int copy_src[2] = {-1, -1}, copy_id[2] = {0, 0};
   if (fast) {
-    if (cw >= 0 && cw < nchild) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = cw + q * kAbs;
+      if (cw < 0 || c >= nchild) continue;
       // DPP argmax of the gain keys; equal gains -> the lowest lane = the smaller feature
-      const bool valid = lane < F && rfeat >= 0 && rgain > -INFINITY;
-      const unsigned long long key = valid ? GainKey(rgain) : 0ull;
+      const bool valid = lane < F && rfeat[q] >= 0 && rgain[q] > -INFINITY;
+      const unsigned long long key = valid ? GainKey(rgain[q]) : 0ull;
       const unsigned long long m = WaveMaxU64(key);
       const unsigned long long win = __ballot(valid && key == m);
-      const int id = __builtin_amdgcn_readlane(first ? 0 : child_id(cw), 0);  // x_* sit in lane 0
+      const int id = __builtin_amdgcn_readlane(first ? 0 : child_id(c, q), 0);  // x_* sit in lane 0
       if (lane == 0) {
-        if (!first) write_node(cw, id);
+        if (!first) write_node(c, id, q);
         if (m == 0) { nbest[id].feature = -1; nbest[id].gain = -INFINITY; s_gain[id] = -INFINITY; }
       }
       if (m != 0) {
         const int wl = static_cast<int>(__builtin_ctzll(win));
-        if (lane == wl) { s_gain[id] = rgain; s_src[id] = cw * F + wl; }
-        copy_src = cw * F + wl;
-        copy_id = id;
+        if (lane == wl) { s_gain[id] = rgain[q]; s_src[id] = c * F + wl; }
+        copy_src[q] = c * F + wl;
+        copy_id[q] = id;
       }
     }
   } else {
     for (int c = wid; c < nchild; c += kWaves) {
-      if (!first && lane == 0) {
-        const int j = c >> 1;
-        const BExp& x = bs->exp[j];
-        x_c0 = x.c0; x_c1 = x.c1; x_ls = x.left_small;
-        x_pb = x.pbegin; x_pc = x.pcount; x_buf = x.pbuf; x_pg = x.pgcount;
-        lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
-        small_cnt = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
-      }
+      if (!first && lane == 0) load_exp(c, 0);
       KeyG k{-INFINITY, 1 << 30, 0};
       for (int f = lane; f < F; f += 64) {
         const SplitResult& r = fbest[c * F + f];
@@ -2655,8 +2660,8 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       }
       k = WaveArgmax(k);
       if (lane == 0) {
-        const int id = first ? 0 : child_id(c);
-        if (!first) write_node(c, id);
+        const int id = first ? 0 : child_id(c, 0);
+        if (!first) write_node(c, id, 0);
         if (k.gain == -INFINITY) {
           nbest[id].feature = -1;
           nbest[id].gain = -INFINITY;
@@ -2671,10 +2676,12 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   __syncthreads();
   stamp(2);
   if (wid != 0) {
-    if (copy_src >= 0 && lane < static_cast<int>(sizeof(SplitResult) / 4)) {
-      static_assert(sizeof(SplitResult) % 4 == 0, "SplitResult copied as dwords");
-      reinterpret_cast<uint32_t*>(nbest + copy_id)[lane] = reinterpret_cast<const uint32_t*>(fbest + copy_src)[lane];
-    }
+    static_assert(sizeof(SplitResult) % 4 == 0, "SplitResult copied as dwords");
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (copy_src[q] >= 0 && lane < static_cast<int>(sizeof(SplitResult) / 4))
+        reinterpret_cast<uint32_t*>(nbest + copy_id[q])[lane] =
+            reinterpret_cast<const uint32_t*>(fbest + copy_src[q])[lane];
     return;
   }
   // ---- replay of the sequential best-first growth (one wave), resumed at the committed prefix. The frontier
