@@ -2753,8 +2753,15 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     if (explored) {
       // the popped entry becomes child a (it keeps the leaf index), child b is appended with leaf pops + 1
       const int ua = a < nnodes ? a : 0, ub = b >= 0 && b < nnodes ? b : 0;
-      const unsigned long long ka = gkey(s_gain[ua]), kb = gkey(s_gain[ub]);
-      const int a0 = s_c0[ua], a1 = s_c1[ua], b0 = s_c0[ub], b1 = s_c1[ub];
+      // both children's gain and links in one LDS round trip: lanes < 32 read a's, the others b's (lane-varying
+      // addresses keep the three reads vector and in flight together; wave-uniform ones were scalarized and
+      // read one after the other), then v_readlane from lanes 0 and 32
+      const int ux = lane < 32 ? ua : ub;
+      const double gx = s_gain[ux];
+      const int cx0 = s_c0[ux], cx1 = s_c1[ux];
+      const unsigned long long ka = gkey(ReadLaneD(gx, 0)), kb = gkey(ReadLaneD(gx, 32));
+      const int a0 = __builtin_amdgcn_readlane(cx0, 0), a1 = __builtin_amdgcn_readlane(cx1, 0);
+      const int b0 = __builtin_amdgcn_readlane(cx0, 32), b1 = __builtin_amdgcn_readlane(cx1, 32);
       const int nl = nf & 63, ns = nf >> 6;
 #pragma unroll
       for (int q = 0; q < kSlots; ++q) {
