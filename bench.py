@@ -14,8 +14,9 @@ iterations, and the returned LightGBMClassificationModel with its model
 string (forced inside the timed loop: the engine builds the text lazily).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
-N > 1 it runs under torch.distributed.run with one rank per GPU (RCCL
-histogram allreduce inside the engine; gloo control plane). Started WITHOUT a torchrun
+N > 1 it runs under torch.distributed.run with one rank per GPU (exact int64
+histogram allreduce inside the engine, one per batched round: the one-shot P2P
+allreduce over xGMI for messages up to 1 MB, RCCL above; gloo control plane). Started WITHOUT a torchrun
 environment and ``--gpus N > 1``, this script launches
 ``python -m torch.distributed.run --nproc-per-node N bench.py ...`` as a child
 process before anything touches the GPU (the parent never imports torch),
