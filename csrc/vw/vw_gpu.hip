@@ -1105,6 +1105,7 @@ struct GpuSgd::Impl {
   hipStream_t stream = nullptr, copy_stream = nullptr;
   Stager& stager = SharedStager();  // pinned host->device staging of pass data (on this learner's copy_stream)
   std::vector<hipEvent_t> events;
+  hipEvent_t ev_ip = nullptr;  // ExpandToStage: the offsets' upload, ordered before the count kernel
   float4* W = nullptr;
   uint64_t nw = 0;
   uint8_t* dirty = nullptr;
@@ -1151,6 +1152,7 @@ struct GpuSgd::Impl {
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    if (ev_ip) (void)hipEventDestroy(ev_ip);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     for (void* q : {static_cast<void*>(cptr), static_cast<void*>(aip), static_cast<void*>(ccls),
                     static_cast<void*>(chosen), static_cast<void*>(ccost), static_cast<void*>(cbcost),
@@ -1572,31 +1574,18 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
         bulk.push_back({di, dv, &b});
       }
       if (plan.row_map) h.row_map = static_cast<const int64_t*>(dev_copy(plan.row_map, n * sizeof(int64_t)));
-      VW_HIP_CHECK(hipStreamSynchronize(cs));
     }
-    if (!impl_->spec) VW_HIP_CHECK(hipMalloc(&impl_->spec, sizeof(ExpandSpec)));
-    VW_HIP_CHECK(hipMemcpyAsync(impl_->spec, &h, sizeof(ExpandSpec), hipMemcpyHostToDevice, s));
-    impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
-    VW_HIP_CHECK(hipMemsetAsync(impl_->indptr, 0, sizeof(int64_t), s));
-    if (n > 0) {  // row lengths need only the offsets: the whole pass's CSR layout before any bulk byte lands
-      const int grid = static_cast<int>(std::min<int64_t>(65536, (n + 255) / 256));
-      hipLaunchKernelGGL(expand_count_kernel, dim3(grid), dim3(256), 0, s, impl_->spec, n, impl_->indptr + 1);
-      VW_HIP_CHECK(hipGetLastError());
-      size_t tb = 0;
-      VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
-      void* tbuf = dev_alloc(tb);  // the scan's temporary storage (no host source)
-      VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tbuf, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
-    }
-    int64_t nnz = 0;
-    VW_HIP_CHECK(hipMemcpyAsync(&nnz, impl_->indptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    VW_HIP_CHECK(hipStreamSynchronize(s));
-    impl_->Reserve(std::max<int64_t>(1, n), static_cast<size_t>(nnz));
+    // the offsets (and row map) are ordered before the count kernel by an event, not a host wait, and the
+    // bulk uploader starts now: its chunks cross PCIe while the table is zeroed and the layout is counted
+    // (r5 pass 54: the host waits put ~8 ms between the fit's start and the first chunk)
+    if (!impl_->ev_ip) VW_HIP_CHECK(hipEventCreateWithFlags(&impl_->ev_ip, hipEventDisableTiming));
+    VW_HIP_CHECK(hipEventRecord(impl_->ev_ip, cs));
+    VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->ev_ip, 0));
     for (size_t i = impl_->events.size(); i < static_cast<size_t>(nchunks); ++i) {
       hipEvent_t e;
       VW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       impl_->events.push_back(e);
     }
-    if (lr1 > 0) PrepLearn(0, lr1);
     std::mutex rmu;
     std::condition_variable rcv;
     int64_t recorded = 0;
@@ -1642,6 +1631,24 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
       }
     });
     try {
+      if (!impl_->spec) VW_HIP_CHECK(hipMalloc(&impl_->spec, sizeof(ExpandSpec)));
+      VW_HIP_CHECK(hipMemcpyAsync(impl_->spec, &h, sizeof(ExpandSpec), hipMemcpyHostToDevice, s));
+      impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
+      VW_HIP_CHECK(hipMemsetAsync(impl_->indptr, 0, sizeof(int64_t), s));
+      if (n > 0) {  // row lengths need only the offsets: the whole pass's CSR layout before any bulk byte lands
+        const int grid = static_cast<int>(std::min<int64_t>(65536, (n + 255) / 256));
+        hipLaunchKernelGGL(expand_count_kernel, dim3(grid), dim3(256), 0, s, impl_->spec, n, impl_->indptr + 1);
+        VW_HIP_CHECK(hipGetLastError());
+        size_t tb = 0;
+        VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
+        void* tbuf = dev_alloc(tb);  // the scan's temporary storage (no host source)
+        VW_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tbuf, tb, impl_->indptr + 1, impl_->indptr + 1, n, s));
+      }
+      int64_t nnz = 0;
+      VW_HIP_CHECK(hipMemcpyAsync(&nnz, impl_->indptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      VW_HIP_CHECK(hipStreamSynchronize(s));
+      impl_->Reserve(std::max<int64_t>(1, n), static_cast<size_t>(nnz));
+      if (lr1 > 0) PrepLearn(0, lr1);
       for (int64_t c = 0; c < nchunks; ++c) {
         {
           std::unique_lock<std::mutex> g(rmu);
@@ -1686,8 +1693,15 @@ void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, con
   // labels / weights first: a pipelined stage learns as the chunks land
   impl_->Reserve(std::max<int64_t>(1, n), impl_->cap_nnz);
   if (cfg_.cb < 0 && n) {
-    VW_HIP_CHECK(hipMemcpyAsync(impl_->lab, labels, n * sizeof(float), hipMemcpyHostToDevice, s));
-    if (weights) VW_HIP_CHECK(hipMemcpyAsync(impl_->wt, weights, n * sizeof(float), hipMemcpyHostToDevice, s));
+    // through the pinned stager on the copy stream: a pageable copy on the compute stream queued behind the
+    // table's zeroing and held the host until it had run; ExpandToStage orders the copy stream before any
+    // kernel that reads the labels (its offsets event)
+    std::lock_guard<std::mutex> lk(impl_->stager.mu);
+    impl_->stager.Copy(reinterpret_cast<char*>(impl_->lab), reinterpret_cast<const char*>(labels), n * sizeof(float),
+                       impl_->copy_stream);
+    if (weights)
+      impl_->stager.Copy(reinterpret_cast<char*>(impl_->wt), reinterpret_cast<const char*>(weights),
+                         n * sizeof(float), impl_->copy_stream);
     staged_labels_.assign(labels, labels + n);
     staged_n_ = n;
   }
