@@ -120,6 +120,7 @@ class GpuSgd {
   double min_label_ = 0, max_label_ = 0;
   int64_t last_sync_bytes_ = 0, last_sync_blocks_ = 0;
   std::vector<float> staged_labels_;
+  bool clamp_const_ = false;  // the learning launches clamp to the fixed [min_label_, max_label_] (logistic)
   int64_t staged_n_ = 0;       // examples
   int64_t staged_rows_ = 0;    // CSR rows (= examples, or action rows under cb)
   bool staged_weights_ = false;
