@@ -211,9 +211,10 @@ class ContinuousServingServer(ServingServer):
                 self._finish(rid, rep if isinstance(rep, dict) and "statusLine" in rep else make_response(rep))
             except Exception as e:  # noqa: BLE001 - the task "crashes" and is restarted at the same epoch
                 self._failures[rid] += 1
+                # counted before the reply: a client that sees the 500 also sees every attempt
+                self.task_attempts[pid] += 1
                 if self._failures[rid] >= self.max_task_failures:
                     self._finish(rid, make_response(f"{type(e).__name__}: {e}", 500, "Internal Server Error"))
-                self.task_attempts[pid] += 1
                 with self._cond:
                     e_now = self._task_epoch[pid]
                     replay = collections.deque(x for x in self._history.get((e_now, pid), ())
