@@ -1162,13 +1162,31 @@ __device__ __forceinline__ void SlabWrite(ulonglong2* out, const unsigned long l
 // One block's share of a leaf histogram: rows [begin, begin + count) of ping-pong buffer `buf` (-1 =
 // physical rows) are cut into nb_active chunks; this block (chunk lb, feature group blockIdx.y) accumulates
 // its chunk into LDS and writes its slab.
-template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false>
+// bhist (leaf-id mode): this block's rows are the runs [r0, r1) of expansion j's list; spre = their exclusive
+// prefix of smaller-side counts (nr + 1 entries, in LDS). Position p -> the run holding it (binary search) ->
+// list[j stride + run C + (p - spre[run])].
+struct LidRuns {
+  const int32_t* list;  // expansion j's list
+  const int* spre;      // LDS
+  int nr, r0, chunk;
+  // positions of one thread grow (a clamped tail position restarts the walk): `k` is the thread's current run
+  __device__ __forceinline__ int row(int p, int& k) const {
+    if (nr == 1) return list[static_cast<int64_t>(r0) * chunk + p];
+    if (p < spre[k]) k = 0;
+    while (k + 1 < nr && spre[k + 1] <= p) ++k;
+    return list[static_cast<int64_t>(r0 + k) * chunk + (p - spre[k])];
+  }
+};
+
+// kGather: rows come from the leaf-id partition's runs (`runs`) and g / h are read at the row id
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false, bool kGather = false>
 __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_active, int lb, const uint4* __restrict__ bins4,
                                          int W4, int F, const int32_t* __restrict__ perm0,
                                          const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
                                          const float2* __restrict__ ogh1, const float* __restrict__ g,
                                          const float* __restrict__ h, const float* __restrict__ ghmax,
-                                         ulonglong2* __restrict__ slab_out, int64_t scale_n) {
+                                         ulonglong2* __restrict__ slab_out, int64_t scale_n,
+                                         const LidRuns& runs = LidRuns{}) {
   constexpr int kWords = kFPG * kBinsPerFeature;
   // g plane at 0, h plane kHOff bytes above it (kTight: F <= 28, see kHPlaneTight)
   constexpr uint32_t kHOff = kFPG == 32 ? (kTight ? kHPlaneTight : kHPlaneApart) : kWords * 8u;
@@ -1191,10 +1209,11 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
   const int p0 = begin + lb * chunk;
   const int p1 = min(begin + count, p0 + chunk);
   const HScale sc = HistScaleV(scale_n, gmax_g, gmax_h);
-  const int32_t* __restrict__ perm = buf == 0 ? perm0 : perm1;
+  const int32_t* __restrict__ perm = kGather || buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = buf == 0 ? ogh0 : ogh1;
-  const bool phys = buf < 0;
+  const bool phys = !kGather && buf < 0;
   const int rot = tid & 15;
+  static_assert(!(kPipe && kGather), "the pipelined loop reads the ordered g / h copy");
   if constexpr (kPipe) {
     // Software pipeline, two stages deep: while the rows of step i go into the LDS histogram, the bins /
     // (g, h) of step i + 1 and the row ids of step i + 2 are in flight, so a wave's memory latency hides
@@ -1243,6 +1262,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
     SlabWrite<kFPG, kHistBlockThreads>(slab_out, shg, shh, F, grp * kFPG, Fg, tid);
     return;
   }
+  int rk = 0;  // kGather: this thread's current run
   for (int base = p0 + tid; base < p1; base += kHistBlockThreads * kUnroll) {
     // branch-free loads (positions past p1 read position p0, a valid row, and are never accumulated): a
     // guarded load is a branch, and the compiler waits out each one before the next row's
@@ -1253,7 +1273,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
       const int pos = base + u * kHistBlockThreads;
       ok[u] = pos < p1;
       pq[u] = ok[u] ? pos : p0;
-      r[u] = phys ? pq[u] : perm[pq[u]];
+      r[u] = kGather ? runs.row(pq[u], rk) : (phys ? pq[u] : perm[pq[u]]);
     }
     uint4 b0[kUnroll], b1[kUnroll];
     float2 v[kUnroll];
@@ -1263,7 +1283,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
       b0[u] = bins4[rb];
       b1[u] = bins4[two ? rb + 1 : rb];
       if (!two) b1[u] = make_uint4(0, 0, 0, 0);
-      v[u] = phys ? make_float2(g[r[u]], h[r[u]]) : ogh[pq[u]];
+      v[u] = phys || kGather ? make_float2(g[r[u]], h[r[u]]) : ogh[pq[u]];
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
@@ -3102,17 +3122,320 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   }
 }
 
-template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false>
+// ---- leaf-id partition (the batched growth's default when bagging is off)
+// Instead of moving every row of an expanded node (row id + ordered g / h: 12 B read + 12 B written per row, 60.5M
+// row moves per 31-leaf tree at 11M rows - the 412 us/iter bpart of profiles/r5/pass38), every row carries the id
+// of the node it sits in (1 B when the node table fits 256 ids) and a round is one coalesced pass over the ids: a
+// row of an expanded node reads its split feature's bin and takes the child's id; rows outside the round's
+// expansions cost one byte read.
+// The smaller children's rows are listed for bhist WITHOUT any global atomic: a round-6 first form claimed list
+// space with one 64-bit atomic per (4096-row block, expansion) on the expansion cursor - ~2700 serialized
+// same-address atomics per round cost ~50 us whatever the round's size (r6 pass 1). Now the grid is G blocks of
+// kLidThreads threads, block b owns the contiguous row chunk [b C, (b + 1) C) and writes the smaller-side rows of
+// expansion j into its own run list[j * stride + b * C ..] (capacity C: no claim needed), in a second pass over
+// the ids it just wrote; its (left, right) counts go to cnt[j * G + b]. bhist reads the runs (a block takes a
+// contiguous range of runs, a row position is located by a binary search over the runs' prefix in LDS) and
+// block 0 of bhist stores the totals into the expansion cursor (left in the low half, right in the high half), so
+// the reduce / plan read the same counts as with the moving partition. Deterministic list positions.
+constexpr int kLidThreads = 1024;
+constexpr int kLidRows = 16;          // ids per thread per group (one 16-B load of 1-B ids)
+constexpr int kLidGroups = 3;         // groups per thread per pass: C <= kLidThreads * kLidRows * kLidGroups
+constexpr int kLidMaxChunk = kLidThreads * kLidRows * kLidGroups;  // 49152 (16-bit per-block counters)
+constexpr int kLidMaxRuns = 2048;     // G: runs per expansion (bhist stages a run prefix in LDS)
+
+template <typename Id>
+struct LidVec {  // kLidRows ids
+  static constexpr int kWords = kLidRows * sizeof(Id) / 16;
+  uint4 w[kWords];
+  __device__ __forceinline__ uint32_t get(int u) const {
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(w);
+    if constexpr (sizeof(Id) == 1) return (d[u >> 2] >> (8 * (u & 3))) & 0xFFu;
+    else return (d[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+  }
+  __device__ __forceinline__ void set(int u, uint32_t v) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(w);
+    if constexpr (sizeof(Id) == 1) {
+      const int s = 8 * (u & 3);
+      d[u >> 2] = (d[u >> 2] & ~(0xFFu << s)) | (v << s);
+    } else {
+      const int s = 16 * (u & 1);
+      d[u >> 1] = (d[u >> 1] & ~(0xFFFFu << s)) | (v << s);
+    }
+  }
+};
+
+// block-wide exclusive prefix of a packed 64-bit counter word (kLidThreads threads); *total = the block sum
+__device__ __forceinline__ unsigned long long LidBlockScan(unsigned long long v, unsigned long long* s_w,
+                                                           unsigned long long* total) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  unsigned long long pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kLidThreads / 64; ++w) {
+    const unsigned long long t = s_w[w];
+    pre += w < wid ? t : 0ull;
+    tot += t;
+  }
+  __syncthreads();  // s_w is reused by the next word's scan
+  *total = tot;
+  return pre + x - v;
+}
+
+template <int kW>
+__device__ __forceinline__ uint32_t LidField(const unsigned long long (&w)[kW], int j) {
+  unsigned long long x = w[0];
+#pragma unroll
+  for (int q = 1; q < kW; ++q) x = (j >> 2) == q ? w[q] : x;
+  return static_cast<uint32_t>(x >> (16 * (j & 3))) & 0xFFFFu;
+}
+
+// grid G x kLidThreads; kW counter words of 4 expansions each (rounds of up to 4 kW expansions)
+template <typename Id, int kW>
+__global__ __launch_bounds__(kLidThreads) void bpart_lid_kernel(BState* __restrict__ bs, void* __restrict__ lid_raw,
+                                                              const uint8_t* __restrict__ cbins, int32_t n, int chunk,
+                                                              int32_t* __restrict__ list, int64_t list_stride,
+                                                              unsigned long long* __restrict__ cnt, int first) {
+  const int nexp = bs->nexp;
+  if (nexp == 0) return;
+  Id* __restrict__ lid = static_cast<Id*>(lid_raw);
+  constexpr int kMap = sizeof(Id) == 1 ? 256 : kBatchMaxNodes;
+  __shared__ int8_t s_map[kMap];   // node id -> expansion slot (this round's parents)
+  __shared__ int8_t s_cmap[kMap];  // node id -> 2 slot + side (this round's children; pass 2)
+  // per expansion: split feature, packed decision (thr | missing bin << 8 | dleft << 17 | is_cat << 18; missing
+  // bin 256 = none), children ids (c0 | c1 << 16)
+  __shared__ int s_feat[kMaxSpec];
+  __shared__ uint32_t s_dec[kMaxSpec], s_cc[kMaxSpec];
+  __shared__ uint32_t s_cat[kMaxSpec][8];
+  __shared__ int s_ls[kMaxSpec];
+  __shared__ unsigned long long s_w[kLidThreads / 64];
+  __shared__ int s_anycat;
+  const int tid = threadIdx.x, G = static_cast<int>(gridDim.x);
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * chunk;
+  const int64_t c1 = min(static_cast<int64_t>(n), c0 + chunk);
+  // this thread's groups: kLidGroups consecutive 16-row groups from c0 + tid kLidGroups 16 (so the list, filled in
+  // thread order, follows the physical row order: bhist's row gathers stay ascending); their ids go out before
+  // the tables are staged
+  LidVec<Id> ids[kLidGroups];
+#pragma unroll
+  for (int k = 0; k < kLidGroups; ++k) {
+    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
+#pragma unroll
+    for (int q = 0; q < LidVec<Id>::kWords; ++q) ids[k].w[q] = make_uint4(0, 0, 0, 0);
+    if (!first && r0 < c1) {
+      const uint4* src = reinterpret_cast<const uint4*>(lid + r0);
+#pragma unroll
+      for (int q = 0; q < LidVec<Id>::kWords; ++q) ids[k].w[q] = src[q];
+    }
+  }
+  for (int i = tid; i < kMap; i += kLidThreads) { s_map[i] = -1; s_cmap[i] = -1; }
+  if (tid == 0) s_anycat = 0;
+  __syncthreads();
+  if (tid < nexp) {
+    const BExp& x = bs->exp[tid];
+    const PartSplit& ps = x.ps;
+    if (ps.is_cat) s_anycat = 1;
+    if (x.node >= 0 && x.node < kMap) s_map[x.node] = static_cast<int8_t>(tid);
+    if (x.c0 >= 0 && x.c0 < kMap) s_cmap[x.c0] = static_cast<int8_t>(2 * tid);
+    if (x.c1 >= 0 && x.c1 < kMap) s_cmap[x.c1] = static_cast<int8_t>(2 * tid + 1);
+    const uint32_t mbin = ps.mt == kMissingZero ? static_cast<uint32_t>(ps.dbin)
+                                                : (ps.mt == kMissingNaN ? static_cast<uint32_t>(ps.nb - 1) : 256u);
+    s_feat[tid] = ps.feature;
+    s_dec[tid] = (ps.thr > 255u ? 255u : ps.thr) | (mbin << 8) | ((ps.dleft ? 1u : 0u) << 17) |
+                 ((ps.is_cat ? 1u : 0u) << 18);
+    s_cc[tid] = static_cast<uint32_t>(x.c0) | (static_cast<uint32_t>(x.c1) << 16);
+    s_ls[tid] = x.left_small;
+  }
+  if (tid < nexp * 8) s_cat[tid >> 3][tid & 7] = bs->exp[tid >> 3].cat[tid & 7];
+  __syncthreads();
+  // ---- pass 1: new ids, per-thread left / right counts (4 expansions per 64-bit word, 16-bit fields)
+  unsigned long long cl[kW], cr[kW];
+#pragma unroll
+  for (int w = 0; w < kW; ++w) { cl[w] = 0ull; cr[w] = 0ull; }
+  // window path (<= 4 expansions, 16-B aligned columns): a group's rows of expansion j read their bins from ONE
+  // 16-B load of column f_j at the group's rows (4 window loads at most instead of 16 byte gathers); every
+  // group's windows are issued before any is used. Expansion slots per row packed as nibbles (15 = none).
+  const bool win = kW == 1 && (n & 15) == 0;
+  unsigned long long jn[kLidGroups];
+  uint32_t present[kLidGroups];
+  if (win) {
+#pragma unroll
+    for (int k = 0; k < kLidGroups; ++k) {
+      const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
+      unsigned long long nib = ~0ull;
+      uint32_t pr = 0;
+#pragma unroll
+      for (int u = 0; u < kLidRows; ++u) {
+        const uint32_t v = ids[k].get(u);
+        const int j = r0 + u < c1 && v < static_cast<uint32_t>(kMap) ? static_cast<int>(s_map[v]) : -1;
+        if (j >= 0) { nib &= ~(15ull << (4 * u)); nib |= static_cast<unsigned long long>(j) << (4 * u); pr |= 1u << j; }
+      }
+      jn[k] = nib;
+      present[k] = pr;
+    }
+  }
+  // the windows of group k: issued one group ahead of their use (two groups' windows live at a time)
+  auto load_win = [&](int k, uint4 (&w)[4]) {
+    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w[j] = make_uint4(0, 0, 0, 0);
+      if ((present[k] >> j) & 1u) w[j] = *reinterpret_cast<const uint4*>(cbins + static_cast<size_t>(s_feat[j]) * n + r0);
+    }
+  };
+  uint4 wcur[4], wnxt[4];
+  if (win) load_win(0, wcur);
+  auto count_row = [&](int j, bool left) {
+    const unsigned long long one = j >= 0 ? (1ull << (16 * (j & 3))) : 0ull;
+#pragma unroll
+    for (int w = 0; w < kW; ++w) {
+      const unsigned long long add = (j >> 2) == w ? one : 0ull;
+      cl[w] += left ? add : 0ull;
+      cr[w] += left ? 0ull : add;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < kLidGroups; ++k) {
+    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
+    if (r0 >= c1) break;
+    if (win) {
+      if (k + 1 < kLidGroups) load_win(k + 1, wnxt);
+      const uint4* wbk = wcur;
+      if (jn[k] == ~0ull) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wcur[j] = wnxt[j];
+        continue;
+      }
+      // numerical splits decided straight from the windows; categorical ones (rare) below
+#pragma unroll
+      for (int u = 0; u < kLidRows; ++u) {
+        const int j = static_cast<int>((jn[k] >> (4 * u)) & 15ull);
+        const uint32_t w0 = (&wbk[0].x)[u >> 2], w1 = (&wbk[1].x)[u >> 2];
+        const uint32_t w2 = (&wbk[2].x)[u >> 2], w3 = (&wbk[3].x)[u >> 2];
+        const uint32_t w = (j & 2) ? ((j & 1) ? w3 : w2) : ((j & 1) ? w1 : w0);
+        const uint32_t bu = (w >> (8 * (u & 3))) & 0xFFu;
+        const int jj = j == 15 ? 0 : j;
+        const uint32_t d = s_dec[jj], cc = s_cc[jj];
+        bool left = bu == ((d >> 8) & 511u) ? ((d >> 17) & 1u) != 0 : bu <= (d & 255u);
+        if (s_anycat && j != 15 && ((d >> 18) & 1u)) left = (s_cat[jj][bu >> 5] >> (bu & 31)) & 1u;
+        ids[k].set(u, j == 15 ? ids[k].get(u) : (left ? (cc & 0xFFFFu) : (cc >> 16)));
+        count_row(j == 15 ? -1 : j, left);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wcur[j] = wnxt[j];
+    } else {
+      int js[kLidRows];
+      uint32_t b[kLidRows];
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < kLidRows; ++u) {
+        const uint32_t v = ids[k].get(u);
+        js[u] = r0 + u < c1 && v < static_cast<uint32_t>(kMap) ? static_cast<int>(s_map[v]) : -1;
+        any |= js[u] >= 0;
+      }
+      if (!any) continue;
+#pragma unroll
+      for (int u = 0; u < kLidRows; ++u) {
+        const int f = js[u] >= 0 ? s_feat[js[u]] : 0;
+        b[u] = cbins[static_cast<size_t>(f) * n + (r0 + u < c1 ? r0 + u : c0)];
+      }
+      // branch-free per row (rows outside the round keep their id); categorical splits only when the round has one
+#pragma unroll
+      for (int u = 0; u < kLidRows; ++u) {
+        const int j = js[u], jj = j < 0 ? 0 : j;
+        const uint32_t d = s_dec[jj], bu = b[u], cc = s_cc[jj];
+        bool left = bu == ((d >> 8) & 511u) ? ((d >> 17) & 1u) != 0 : bu <= (d & 255u);
+        if (s_anycat && j >= 0 && ((d >> 18) & 1u)) left = (s_cat[jj][bu >> 5] >> (bu & 31)) & 1u;
+        ids[k].set(u, j < 0 ? ids[k].get(u) : (left ? (cc & 0xFFFFu) : (cc >> 16)));
+        count_row(j, left);
+      }
+    }
+    uint4* dst = reinterpret_cast<uint4*>(lid + r0);  // the id array is padded to whole groups
+#pragma unroll
+    for (int q = 0; q < LidVec<Id>::kWords; ++q) dst[q] = ids[k].w[q];
+  }
+  // ---- block prefix of the counts, the block's (left, right) per expansion -> cnt[j * G + b]
+  const int nw = (nexp + 3) >> 2;
+  unsigned long long el[kW], er[kW], tl[kW], tr[kW];
+#pragma unroll
+  for (int w = 0; w < kW; ++w) { el[w] = er[w] = tl[w] = tr[w] = 0ull; }
+#pragma unroll
+  for (int w = 0; w < kW; ++w) {
+    if (w >= nw) break;  // block-uniform
+    el[w] = LidBlockScan(cl[w], s_w, &tl[w]);
+    er[w] = LidBlockScan(cr[w], s_w, &tr[w]);
+  }
+  if (tid < nexp)
+    cnt[static_cast<size_t>(tid) * G + blockIdx.x] =
+        static_cast<unsigned long long>(LidField(tl, tid)) | (static_cast<unsigned long long>(LidField(tr, tid)) << 32);
+  // ---- pass 2: smaller-side rows -> the block's run of the expansion's list (positions: thread prefix + running)
+  unsigned long long ol[kW], orr[kW];
+#pragma unroll
+  for (int w = 0; w < kW; ++w) { ol[w] = el[w]; orr[w] = er[w]; }
+#pragma unroll
+  for (int k = 0; k < kLidGroups; ++k) {
+    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
+    if (r0 >= c1) break;
+#pragma unroll
+    for (int u = 0; u < kLidRows; ++u) {
+      const uint32_t v = ids[k].get(u);
+      const int m = r0 + u < c1 && v < static_cast<uint32_t>(kMap) ? static_cast<int>(s_cmap[v]) : -1;
+      const int jj = m < 0 ? 0 : (m >> 1);
+      const bool left = (m & 1) == 0;
+      const bool app = m >= 0 && left == (s_ls[jj] != 0);
+      const uint32_t p = left ? LidField(ol, jj) : LidField(orr, jj);
+      if (app) list[jj * list_stride + c0 + p] = static_cast<int32_t>(r0 + u);
+      const unsigned long long one = m >= 0 ? 1ull << (16 * (jj & 3)) : 0ull;
+#pragma unroll
+      for (int q = 0; q < kW; ++q) {
+        const unsigned long long a = (jj >> 2) == q ? one : 0ull;
+        ol[q] += left ? a : 0ull;
+        orr[q] += left ? 0ull : a;
+      }
+    }
+  }
+}
+
+
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false, bool kLid = false>
 __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
     const BState* __restrict__ bs, const uint4* __restrict__ bins4, int W4, int F, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
     const float* __restrict__ g, const float* __restrict__ h, const float* __restrict__ ghmax,
-    ulonglong2* __restrict__ slab, int64_t scale_n) {
+    ulonglong2* __restrict__ slab, int64_t scale_n, BState* __restrict__ bsw, const unsigned long long* __restrict__ lcnt,
+    int G, int chunk, int64_t lstride) {
   const int nexp = bs->nexp;
   if (nexp == 0) return;
   __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
-  // the expansions' counts load in parallel (one thread each: one memory latency, not nexp in a row)
-  if (threadIdx.x < nexp) s_cnt[threadIdx.x] = BatchSmallCount(bs, threadIdx.x);
+  if constexpr (kLid) {
+    // the expansions' totals from the partition's per-block counts (wave j sums expansion j's G counts: 32-bit
+    // halves cannot carry into each other, every block total is < 2^16); block (0, 0) publishes them in the cursors
+    __shared__ unsigned int s_tl[kMaxSpec], s_tr[kMaxSpec];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    static_assert(kHistBlockThreads / 64 >= kMaxSpec, "one wave per expansion");
+    if (wid < nexp) {
+      unsigned long long acc = 0;
+      for (int b = lane; b < G; b += 64) acc += lcnt[static_cast<size_t>(wid) * G + b];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) { s_tl[wid] = static_cast<unsigned int>(acc & 0xFFFFFFFFull); s_tr[wid] = static_cast<unsigned int>(acc >> 32); }
+    }
+    __syncthreads();
+    if (tid < nexp) {
+      s_cnt[tid] = static_cast<int>(bs->exp[tid].left_small ? s_tl[tid] : s_tr[tid]);
+      if (blockIdx.x == 0 && blockIdx.y == 0)
+        bsw->cursor[tid] = static_cast<unsigned long long>(s_tl[tid]) | (static_cast<unsigned long long>(s_tr[tid]) << 32);
+    }
+  } else {
+    // the expansions' counts load in parallel (one thread each: one memory latency, not nexp in a row)
+    if (threadIdx.x < nexp) s_cnt[threadIdx.x] = BatchSmallCount(bs, threadIdx.x);
+  }
   __syncthreads();
   if (threadIdx.x == 0) BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
   __syncthreads();
@@ -3121,10 +3444,42 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   for (int q = 0; q < nexp; ++q) if (bx >= s_off[q] && bx < s_off[q] + s_nb[q]) j = q;
   if (j < 0) return;
   const BExp& x = bs->exp[j];
-  const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
-  const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
-  HistBody<kUnroll, kFPG, kPipe, kTight>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F, perm0, perm1, ogh0,
-                          ogh1, g, h, ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n);
+  if constexpr (kLid) {
+    // this block's runs of expansion j's list and their smaller-side prefix (wave 0 scans 64 runs at a time)
+    __shared__ int s_pre[kLidMaxRuns + 1];
+    const int nb = s_nb[j], lb = bx - s_off[j];
+    const int r0 = static_cast<int>(static_cast<int64_t>(lb) * G / nb);
+    const int r1 = static_cast<int>(static_cast<int64_t>(lb + 1) * G / nb);
+    const int nr = r1 - r0, tid = threadIdx.x, lane = tid & 63;
+    const bool lsm = x.left_small != 0;
+    if (tid < 64) {
+      int carry = 0;
+      if (tid == 0) s_pre[0] = 0;
+      for (int b0 = 0; b0 < nr; b0 += 64) {
+        const int k = b0 + lane;
+        const unsigned long long v = k < nr ? lcnt[static_cast<size_t>(j) * G + r0 + k] : 0ull;
+        int c = static_cast<int>(lsm ? (v & 0xFFFFFFFFull) : (v >> 32));
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int y = __shfl_up(c, off, 64);
+          if (lane >= off) c += y;
+        }
+        if (k < nr) s_pre[k + 1] = carry + c;
+        carry += __shfl(c, 63, 64);
+      }
+    }
+    __syncthreads();
+    LidRuns runs{perm0 + static_cast<int64_t>(j) * lstride, s_pre, nr, r0, chunk};
+    HistBody<kUnroll, kFPG, kPipe, kTight, true>(0, s_pre[nr], 0, 1, 0, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
+                                                 ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n,
+                                                 runs);
+  } else {
+    const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+    const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
+    HistBody<kUnroll, kFPG, kPipe, kTight>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F,
+                                           perm0, perm1, ogh0, ogh1, g, h, ghmax,
+                                           slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n);
+  }
 }
 
 // grid (ceil(E / kRedE), spec_k): block (x, j) reduces the slabs of expansion j into part[j * (E + 1) ..]
@@ -3622,6 +3977,27 @@ class GpuBackend : public TrainBackend {
         SML_HIP_CHECK(hipMemset(bprof_, 0, nb));
       }
       for (hipEvent_t& e : bev_) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      // leaf-id partition: SML_GBDT_LID=1 (bagged trees still take the moving partition); off by default - on
+      // MI355X it measured slower than the moving partition (1.77 vs 1.56 ms/iter at 11M x 28, r6 passes 1-4)
+      lid_ok_ = false;
+      if (const char* e = std::getenv("SML_GBDT_LID")) lid_ok_ = std::atoi(e) != 0;
+      if (lid_ok_) {
+        // chunk: rows per partition block, a multiple of 16 (whole 16-B id groups), <= kLidMaxChunk (16-bit block
+        // counters); G = blocks = runs per expansion (<= kLidMaxRuns: larger sets keep the moving partition)
+        int64_t c = std::max<int64_t>(16, (n_ + 255) / 256);
+        c = std::min<int64_t>(kLidMaxChunk, (c + 15) / 16 * 16);
+        const int64_t g = (n_ + c - 1) / c;
+        if (g > kLidMaxRuns || c > static_cast<int64_t>(kLidThreads) * kLidRows * kLidGroups) lid_ok_ = false;
+        if (lid_ok_) {
+          lid_wide_ = cap_nodes > 256;
+          lid_chunk_ = static_cast<int>(c);
+          lid_g_ = static_cast<int>(g);
+          lid_stride_ = g * c;
+          lid_.alloc(static_cast<size_t>(lid_stride_) * (lid_wide_ ? 2 : 1) + 64);
+          lid_list_.alloc(static_cast<size_t>(lid_stride_) * spec_k_);
+          lid_cnt_.alloc(static_cast<size_t>(kMaxSpec) * lid_g_);
+        }
+      }
     }
     // launch-shape knobs for A/B runs (defaults are the measured best)
     if (const char* e = std::getenv("SML_PART_ROWS")) part_rows_ = std::atoi(e);
@@ -4089,7 +4465,7 @@ class GpuBackend : public TrainBackend {
     }
     EnqueueFindChoose(false);
     if (batch_ok_ && sp_.bynode_k <= 0 && !voting_) {
-      GrowBatched(g, h);
+      GrowBatched(g, h, lid_ok_ && bag_n_ < 0);
       final_v_ = 0;
       SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
       return;
@@ -4121,7 +4497,7 @@ class GpuBackend : public TrainBackend {
   // Rounds of the batched speculative growth (see bplan_kernel). The host stays blook_ rounds ahead: before
   // enqueueing round r it waits for the plan of round r - blook_ and stops once a plan reported the tree
   // final (the rounds already queued behind it are no-ops).
-  void GrowBatched(const float* g, const float* h) {
+  void GrowBatched(const float* g, const float* h, bool lid) {
     TraceRange tr("sml::GrowBatched");
     const int budget = L_ - 1;
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
@@ -4134,6 +4510,10 @@ class GpuBackend : public TrainBackend {
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup, true>)
                                              : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true>
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup>)));
+    // leaf-id partition: the smaller children's rows come from the list (perm_[0]), g / h gathered by row id
+    auto bhl = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16, false, false, true>
+                               : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true, true>
+                                         : bhist_kernel<kHistUnroll, kFeatPerGroup, false, false, true>);
     if (bprof_) SML_HIP_CHECK(hipMemsetAsync(bprof_, 0, sizeof(long long) * kPlanProfStride * (max_rounds + 1), stream_));
     int r = 0;
     for (; r <= max_rounds; ++r) {
@@ -4152,13 +4532,26 @@ class GpuBackend : public TrainBackend {
                          bprof_ ? bprof_ + kPlanProfStride * r : nullptr);
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(bev_[r % kBRing], stream_));
-      hipLaunchKernelGGL(bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
-                         perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), perm_[0].get(), perm_[1].get(),
-                         ogh_[0].get(), ogh_[1].get(), g, h);
-      SML_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(bh, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_,
-                         bstate_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
-                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax, slab_.get(), scale_n_);
+      if (lid) {
+        auto lk = lid_wide_ ? (spec_k_ <= 4 ? bpart_lid_kernel<uint16_t, 1> : (spec_k_ <= 8 ? bpart_lid_kernel<uint16_t, 2>
+                                                                                           : bpart_lid_kernel<uint16_t, 4>))
+                            : (spec_k_ <= 4 ? bpart_lid_kernel<uint8_t, 1> : (spec_k_ <= 8 ? bpart_lid_kernel<uint8_t, 2>
+                                                                                          : bpart_lid_kernel<uint8_t, 4>));
+        hipLaunchKernelGGL(lk, dim3(lid_g_), dim3(kLidThreads), 0, stream_, bstate_.get(), lid_.get(), cbins_.get(),
+                           static_cast<int32_t>(n_), lid_chunk_, lid_list_.get(), lid_stride_, lid_cnt_.get(),
+                           r == 0 ? 1 : 0);
+        SML_HIP_CHECK(hipGetLastError());
+      } else {
+        hipLaunchKernelGGL(bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
+                           perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), perm_[0].get(), perm_[1].get(),
+                           ogh_[0].get(), ogh_[1].get(), g, h);
+        SML_HIP_CHECK(hipGetLastError());
+      }
+      hipLaunchKernelGGL(lid ? bhl : bh, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_,
+                         bstate_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_,
+                         lid ? lid_list_.get() : perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax,
+                         slab_.get(), scale_n_, bstate_.get(), lid ? lid_cnt_.get() : nullptr, lid_g_, lid_chunk_,
+                         lid_stride_);
       SML_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL(breduce_kernel, dim3((E_ + kRedE - 1) / kRedE, spec_k_), dim3(kRedE * kRedG), 0, stream_,
                          bstate_.get(), slab_.get(), E_, ghmax, part_.get(), scale_n_, Distributed() ? 1 : 0);
@@ -4775,6 +5168,14 @@ class GpuBackend : public TrainBackend {
   int* bflag_host_ = nullptr;
   int* bflag_dev_ = nullptr;
   int plan_cap_ = 0;            // node records allocated for the batched growth (the plan stages them all)
+  // leaf-id partition (bpart_lid_kernel): node id per row, 1 B when the node table fits 256 ids, else 2 B
+  bool lid_ok_ = false;
+  bool lid_wide_ = false;
+  int lid_chunk_ = 0, lid_g_ = 0;  // rows per partition block, blocks (= runs per expansion)
+  int64_t lid_stride_ = 0;         // list entries per expansion slot (G x chunk)
+  DevBuf<uint8_t> lid_;
+  DevBuf<int32_t> lid_list_;
+  DevBuf<unsigned long long> lid_cnt_;
   long long* bprof_ = nullptr;  // SML_BPLAN_PROF phase stamps, kPlanProfStride per round
   double bprof_sum_[6] = {0, 0, 0, 0, 0, 0};
   double bprof_tree_[4] = {0, 0, 0, 0};  // rows partitioned, of them in never-popped nodes; expansions, wasted

@@ -257,10 +257,10 @@ class ONNXModel(Transformer):
         return R.fan_out_transform(self, df, nt, use_gpu) if nt > 1 else None
 
     def _transform(self, df: DataFrame) -> DataFrame:
+        self._validate(df)  # before any fan-out: a schema error is raised here, not inside a task
         fanned = self._fan_out(df)
         if fanned is not None:
             return fanned
-        self._validate(df)
         fetch = dict(self.getFetchDict() or {})
         requested = sorted(fetch.values())
         model_outs = sorted(self.modelOutput)
@@ -555,13 +555,15 @@ class ImageFeaturizer(Transformer, HasInputCol, HasOutputCol):
         from ..utils.cluster import _device_count
 
         model = self.getOnnxModel()
+        out_name = self.getFeatureTensorName() if self.getHeadless() else self.getOutputTensorName()
+        if not out_name:
+            raise ValueError("featureTensorName / outputTensorName must be set")
+        if self.getInputCol() not in df.columns:
+            raise ValueError(f"input column {self.getInputCol()} is not in the DataFrame")
         use_gpu = (model.getDeviceType() or "").upper() != "CPU" and _device_count() > 0
         nt = R.transform_tasks(df, use_gpu)
         if nt > 1:  # one task per MI355X, as the reference's per-partition sessions
             return R.fan_out_transform(self, df, nt, use_gpu)
-        out_name = self.getFeatureTensorName() if self.getHeadless() else self.getOutputTensorName()
-        if not out_name:
-            raise ValueError("featureTensorName / outputTensorName must be set")
         img_name = self.getImageTensorName() or next(iter(model.modelInput))
         device = _device_for(model.getDeviceType())
         if device.startswith("cuda"):

@@ -106,6 +106,156 @@ def all_gather_object(obj: Any) -> List[Any]:
     return out
 
 
+class _ShmReducer:
+    """Host allreduce for ranks that share one machine (the local executors, the shared-device rehearsal): the
+    ranks meet in one POSIX shared-memory segment instead of gloo's loopback TCP (~0.8 ms per call for a 24 KB
+    histogram on this host; ~150 calls per small 5-iteration fit). Rank r writes its array into its slot of the
+    call's half (calls alternate halves), then publishes the call number in its flag; every rank waits for all
+    flags and sums the slots in rank order - the same bits on every rank, exact for int64. A rank can reuse a
+    half only after every rank entered the next call, i.e. finished reading this one. Flags are written after
+    the data (x86 stores are not reordered with other stores)."""
+
+    _SLOT = 1 << 20  # bytes per rank per half (larger arrays go in pieces)
+
+    def __init__(self, world: int, rk: int, name: Optional[str]):
+        from .executor import attach_shm
+
+        self.world, self.rank = world, rk
+        size = 64 * world + 2 * world * self._SLOT
+        if name is None:
+            from multiprocessing import shared_memory
+
+            self.shm = shared_memory.SharedMemory(create=True, size=size)
+            self.owner = True
+        else:
+            self.shm = attach_shm(name)
+            self.owner = False
+        self.flags = np.ndarray((world, 8), dtype=np.int64, buffer=self.shm.buf)  # one 64-B line per rank
+        self.calls = 0
+        if self.owner:
+            self.flags[:] = 0
+
+    def publish_pid(self) -> None:
+        self.flags[self.rank, 1] = os.getpid()
+
+    def _dead_peer(self, k: int) -> Optional[int]:
+        """a rank that has not arrived at call k and whose process is gone (or a zombie)"""
+        for r in range(self.world):
+            if r == self.rank or int(self.flags[r, 0]) >= k:
+                continue
+            pid = int(self.flags[r, 1])
+            if pid > 0 and not _pid_alive(pid):
+                return r
+        return None
+
+    def allreduce(self, a: np.ndarray) -> None:
+        flat = a.reshape(-1)
+        per = self._SLOT // flat.itemsize
+        for s in range(0, max(1, flat.size), per):
+            self._one(flat[s:s + per])
+
+    def _one(self, x: np.ndarray) -> None:
+        import time
+
+        self.calls += 1
+        k = self.calls
+        half = k & 1
+        base = 64 * self.world + half * self.world * self._SLOT
+        n = x.size
+
+        def slot(r):
+            return np.ndarray(n, dtype=x.dtype, buffer=self.shm.buf, offset=base + r * self._SLOT)
+
+        slot(self.rank)[...] = x
+        self.flags[self.rank, 0] = k
+        spins, t0, tcheck = 0, None, 0.0
+        while int(self.flags[:, 0].min()) < k:
+            spins += 1
+            if spins > 2000:
+                now = time.monotonic()
+                if t0 is None:
+                    t0 = now
+                elif now - t0 > _SHM_TIMEOUT_S:
+                    raise TimeoutError(f"shared-memory allreduce: a peer did not arrive within {_SHM_TIMEOUT_S}s")
+                if now - tcheck > 0.01:  # a dead peer fails the collective (gloo would see its socket close)
+                    tcheck = now
+                    dead = self._dead_peer(k)
+                    if dead is not None:
+                        raise RuntimeError(f"shared-memory allreduce: rank {dead} died")
+                time.sleep(20e-6)
+        acc = slot(0).copy()
+        for r in range(1, self.world):
+            acc += slot(r)
+        x[...] = acc
+
+    def close(self) -> None:
+        try:
+            self.shm.close()
+            if self.owner:
+                self.shm.unlink()
+        except Exception:  # noqa: BLE001 - already gone
+            pass
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return True
+
+
+_SHM_TIMEOUT_S = float(os.environ.get("SML_SHM_ALLREDUCE_TIMEOUT_S", "1200"))
+_shm_reducer: Optional[_ShmReducer] = None
+_shm_key = None
+
+
+def _same_host_reducer() -> Optional[_ShmReducer]:
+    """The shared-memory reducer of the default group when every rank runs on this host (gloo groups only;
+    SML_SHM_ALLREDUCE=0 keeps gloo). Built collectively on first use, rebuilt when the group changes."""
+    global _shm_reducer, _shm_key
+    if os.environ.get("SML_SHM_ALLREDUCE", "1") == "0":
+        return None
+    d = _dist()
+    key = (id(d.group.WORLD), world_size(), rank())
+    if _shm_key == key:
+        return _shm_reducer
+    import socket
+
+    if _shm_reducer is not None:
+        _shm_reducer.close()
+    hosts = all_gather_object(socket.gethostname())
+    red = None
+    if len(set(hosts)) == 1:
+        if rank() == 0:
+            red = _ShmReducer(world_size(), 0, None)
+            broadcast_object(red.shm.name)
+        else:
+            red = _ShmReducer(world_size(), rank(), broadcast_object(None))
+        red.publish_pid()
+        barrier()  # every rank attached (and its pid published) before any reduces or rank 0 may unlink at exit
+        # multiprocessing's exit hook runs in spawned children too (they end in os._exit: atexit does not)
+        from multiprocessing import util
+
+        util.Finalize(red, red.close, exitpriority=10)
+    _shm_reducer, _shm_key = red, key
+    return red
+
+
+def close_shm_reducer() -> None:
+    """Release the shared-memory reducer (a task process calls this before its group goes away)."""
+    global _shm_reducer, _shm_key
+    if _shm_reducer is not None:
+        _shm_reducer.close()
+    _shm_reducer, _shm_key = None, None
+
+
 def allreduce_numpy(a: np.ndarray) -> None:
     """In-place sum of a float64 or int64 host array over the default group (int64: exact)."""
     if not is_initialized() or world_size() == 1:
@@ -113,6 +263,11 @@ def allreduce_numpy(a: np.ndarray) -> None:
     import torch
 
     d = _dist()
+    if backend() != "nccl" and a.flags.c_contiguous and a.dtype in (np.float64, np.int64):
+        red = _same_host_reducer()
+        if red is not None:
+            red.allreduce(a)
+            return
     if backend() == "nccl":
         t = torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{torch.cuda.current_device()}")
         d.all_reduce(t)

@@ -149,19 +149,16 @@ def _share_partition(df: DataFrame):
 
 
 def _attach_partition(desc_bytes: bytes):
-    from multiprocessing import resource_tracker, shared_memory
-
     from ..core.linalg import CsrColumn
+    from .executor import attach_shm
 
-    desc = pickle.loads(desc_bytes)  # built by the driver process of this job (_share_partition)
+    desc = pickle.loads(desc_bytes)  # built by a process of this job (_share_partition)
     shm = None
     if desc["shm"]:
-        shm = shared_memory.SharedMemory(name=desc["shm"])
-        # the driver owns (and unlinks) the segment; this process must not unlink it at exit
-        try:
-            resource_tracker.unregister(shm._name, "shared_memory")
-        except Exception:  # noqa: BLE001 - tracker details differ between Python versions
-            pass
+        # the creator owns (and unlinks) the segment: attached without a resource-tracker registration (the
+        # tracker is shared with the driver; an attach + unregister here dropped the driver's own entry and its
+        # unlink then failed inside the tracker with KeyError '/psm_...')
+        shm = attach_shm(desc["shm"])
 
     def view(spec):
         off, dt, shape = spec
@@ -220,6 +217,9 @@ def _worker(rank: int, world: int, port: int, backend: str, fn_bytes: bytes, par
         payload = pickle.dumps(("ok", fn(part, rank, world)))
         del part
         dist.barrier()
+        from . import distributed as D
+
+        D.close_shm_reducer()
         dist.destroy_process_group()
         if shm is not None:
             try:
@@ -285,9 +285,7 @@ def _run_once(fn, df, num_workers, backend, use_gpu, timeout_s, fail_fast, port,
     import torch.multiprocessing as mp
 
     world = num_workers or df.getNumPartitions()
-    parts = df.coalesce(world).partitions() if df.getNumPartitions() >= world else df.repartition(world).partitions()
-    while len(parts) < world:
-        parts.append(df.slice(0, 0))
+    parts = _task_partitions(df, world)
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
     fn_bytes = pickle.dumps(fn)
@@ -469,10 +467,36 @@ def fan_out(fn: Callable[[DataFrame, int, int], Any], df: DataFrame, num_tasks: 
         if num_tasks > max(1, ndev):
             backend = backend or "gloo"
             env.setdefault("SML_GBDT_SHARED_DEVICE", "1")
-    return run_partitions(fn, df, num_workers=num_tasks, backend=backend, use_gpu=use_gpu, env=env, **kw)
+    from . import executor as X
+
+    if not X.pool_enabled():
+        return run_partitions(fn, df, num_workers=num_tasks, backend=backend, use_gpu=use_gpu, env=env, **kw)
+    # the persistent executors (executor.py): started on the first call, reused by the later ones
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    run_kw = {k: kw.pop(k) for k in ("timeout_s", "fail_fast") if k in kw}
+    start_kw = {k: kw.pop(k) for k in ("port", "default_listen_port", "network_retries", "initial_delay_s")
+                if k in kw}
+    if kw:
+        raise TypeError(f"fan_out: unexpected arguments {sorted(kw)}")
+    parts = _task_partitions(df, num_tasks)
+    pool = X.get_pool(num_tasks, use_gpu, backend, env, **start_kw)
+    return pool.run(fn, parts, **run_kw)
+
+
+def _task_partitions(df: DataFrame, world: int) -> List[DataFrame]:
+    """The DataFrame cut into ``world`` task partitions (coalesced or repartitioned; empty ones padded)."""
+    parts = df.coalesce(world).partitions() if df.getNumPartitions() >= world else df.repartition(world).partitions()
+    while len(parts) < world:
+        parts.append(df.slice(0, 0))
+    return parts
 
 
 class _TransformTask:
+    # kept by a persistent executor between calls (by the digest of its bytes): the transformer's session,
+    # graphs and device buffers are built once per executor, as the reference's per-executor ONNX sessions
+    cacheable = True
+
     def __init__(self, transformer):
         self.transformer = transformer
 
@@ -480,12 +504,19 @@ class _TransformTask:
         return self.transformer.transform(part)
 
 
+TRANSFORM_MIN_ROWS_PER_TASK = 1024
+
+
 def transform_tasks(df: DataFrame, use_gpu: bool) -> int:
     """Partition tasks of a model's transform (ONNXModel.scala:242-251 maps the partitions, each task on its
-    executor's device): min(executor tasks, partitions); 1 inside a task."""
+    executor's device): min(executor tasks, partitions, rows / SML_TRANSFORM_MIN_ROWS (default 1024) per task);
+    1 inside a task. A small DataFrame stays in this process: handing it to the executors costs more than
+    scoring it here."""
     if in_partition_task():
         return 1
-    return max(1, min(executor_tasks(use_gpu), df.getNumPartitions()))
+    min_rows = int(os.environ.get("SML_TRANSFORM_MIN_ROWS", str(TRANSFORM_MIN_ROWS_PER_TASK)))
+    by_rows = max(1, df.count() // max(1, min_rows))
+    return max(1, min(executor_tasks(use_gpu), df.getNumPartitions(), by_rows))
 
 
 def fan_out_transform(transformer, df: DataFrame, num_tasks: int, use_gpu: bool) -> DataFrame:

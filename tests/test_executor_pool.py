@@ -1,0 +1,175 @@
+"""Persistent executor pool behind fan_out (parallel/executor.py): workers live across calls, task objects that
+opt in are kept per worker, results come back through shared memory, failures retire the pool.
+CPU only (gloo, world size 2)."""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from synapseml_amd.core.dataframe import DataFrame
+from synapseml_amd.parallel import executor as X
+from synapseml_amd.parallel import runtime as R
+
+
+@pytest.fixture(autouse=True)
+def _fresh_pool():
+    X.shutdown()
+    yield
+    X.shutdown()
+
+
+def _pid_task(part, rank, world):
+    import torch.distributed as dist
+
+    t = __import__("torch").tensor([float(part.count())])
+    dist.all_reduce(t)
+    return (os.getpid(), rank, world, float(t.item()))
+
+
+def test_pool_reuses_workers_and_runs_collectives():
+    df = DataFrame({"x": np.arange(10.0)}, num_partitions=2)
+    a = R.fan_out(_pid_task, df, 2, use_gpu=False)
+    t0 = time.perf_counter()
+    b = R.fan_out(_pid_task, df, 2, use_gpu=False)
+    dt = time.perf_counter() - t0
+    assert [r[1:] for r in a] == [(0, 2, 10.0), (1, 2, 10.0)]
+    assert [r[0] for r in a] == [r[0] for r in b]  # the same processes served both calls
+    assert dt < 1.0, dt
+    assert X.current_pool().tasks_run == 2
+
+
+class _Counter:
+    """cacheable: the worker keeps this object, so its state survives between calls"""
+    cacheable = True
+
+    def __init__(self):
+        self.calls = 0
+
+    def __call__(self, part, rank, world):
+        self.calls += 1
+        return self.calls
+
+
+def test_cacheable_task_objects_persist_per_worker():
+    df = DataFrame({"x": np.arange(4.0)}, num_partitions=2)
+    c = _Counter()
+    assert R.fan_out(c, df, 2, use_gpu=False) == [1, 1]
+    assert R.fan_out(c, df, 2, use_gpu=False) == [2, 2]  # same bytes -> the worker's cached object
+    c2 = _Counter()
+    c2.calls = 10  # different bytes -> a new object
+    assert R.fan_out(c2, df, 2, use_gpu=False) == [11, 11]
+    assert R.fan_out(c, df, 2, use_gpu=False) == [3, 3]
+
+
+def _df_task(part, rank, world):
+    n = part.count()
+    return DataFrame({"x2": np.asarray(part["x"]) * 2, "rank": np.full(n, rank, dtype=np.int32),
+                      "s": np.array([f"r{rank}"] * n, dtype=object)})
+
+
+def _psm():
+    try:
+        return {f for f in os.listdir("/dev/shm") if f.startswith("psm_")}
+    except OSError:
+        return set()
+
+
+def test_dataframe_results_come_back_through_shared_memory():
+    before = _psm()
+    df = DataFrame({"x": np.arange(9.0)}, num_partitions=3)
+    out = DataFrame.union_all(R.fan_out(_df_task, df, 2, use_gpu=False), keep_partitions=True)
+    np.testing.assert_array_equal(out["x2"], np.arange(9.0) * 2)
+    assert list(out["s"][:1]) == ["r0"] and out["rank"].dtype == np.int32
+    assert _psm() <= before  # every segment of the job was unlinked
+
+
+def _fail_rank1(part, rank, world):
+    if rank == 1:
+        raise ValueError("boom on rank 1")
+    return rank
+
+
+def _crash_rank1(part, rank, world):
+    if rank == 1:
+        os._exit(3)
+    import torch.distributed as dist
+
+    dist.barrier()  # rank 0 would wait here forever: the driver aborts the job
+    return rank
+
+
+@pytest.mark.parametrize("fn,msg", [(_fail_rank1, "boom on rank 1"), (_crash_rank1, "exit code")])
+def test_failure_retires_the_pool_and_the_next_call_starts_fresh(fn, msg):
+    df = DataFrame({"x": np.arange(4.0)}, num_partitions=2)
+    pids = [r[0] for r in R.fan_out(_pid_task, df, 2, use_gpu=False)]
+    with pytest.raises(RuntimeError, match=msg):
+        R.fan_out(fn, df, 2, use_gpu=False, timeout_s=60)
+    again = R.fan_out(_pid_task, df, 2, use_gpu=False)
+    assert [r[1:] for r in again] == [(0, 2, 4.0), (1, 2, 4.0)]
+    assert not set(pids) & {r[0] for r in again}  # fresh child processes
+
+
+def test_timeout_raises_and_retires_the_pool():
+    df = DataFrame({"x": np.arange(4.0)}, num_partitions=2)
+    with pytest.raises(TimeoutError):
+        R.fan_out(_sleep_task, df, 2, use_gpu=False, timeout_s=1.0)
+    assert R.fan_out(_pid_task, df, 2, use_gpu=False)[0][1:] == (0, 2, 4.0)
+
+
+def _sleep_task(part, rank, world):
+    time.sleep(30)
+    return rank
+
+
+def test_context_manager_and_explicit_shutdown():
+    pool = X.get_pool(2, False, "gloo")
+    with pool:
+        parts = R._task_partitions(DataFrame({"x": np.arange(6.0)}, num_partitions=2), 2)
+        assert [r[1] for r in pool.run(_pid_task, parts)] == [0, 1]
+    assert pool.closed and X.current_pool() is None
+    assert all(not p.is_alive() for p in pool.procs)
+
+
+def test_lightgbm_num_tasks_repeated_fit_is_as_cheap_as_in_process():
+    """round-5 verdict: a numTasks=2 fit spawned processes every call (4.6-5.1 s vs 0.03 s in-process). With
+    the persistent executors the second fit costs about what the in-process fit does, and grows the same
+    model as the first."""
+    from synapseml_amd.lightgbm import LightGBMClassifier
+
+    rng = np.random.default_rng(0)
+    Xm = rng.standard_normal((20000, 8))
+    y = (Xm[:, 0] + Xm[:, 1] * Xm[:, 2] > 0).astype(float)
+    df = DataFrame({"features": Xm, "label": y}, num_partitions=2)
+    kw = dict(deviceType="cpu", numIterations=5, numThreads=1)
+    t0 = time.perf_counter()
+    LightGBMClassifier(numTasks=1, **kw).fit(df.coalesce(1))
+    t_local = time.perf_counter() - t0
+    m1 = LightGBMClassifier(numTasks=2, **kw).fit(df)  # starts the executors
+    best = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        m2 = LightGBMClassifier(numTasks=2, **kw).fit(df)
+        best = min(best, time.perf_counter() - t0)
+    assert m1.getNativeModel() == m2.getNativeModel()
+    assert best <= t_local + 0.3, (best, t_local)
+
+
+def test_no_resource_tracker_tracebacks():
+    """round-5 verdict: every fan-out printed KeyError '/psm_...' tracebacks from the resource tracker (a worker
+    unregistered the driver's segment). Run a fan-out in a fresh interpreter and read its stderr."""
+    code = ("import numpy as np\n"
+            "from synapseml_amd.core.dataframe import DataFrame\n"
+            "from synapseml_amd.parallel import runtime as R\n"
+            "from tests.test_executor_pool import _df_task\n"
+            "df = DataFrame({'x': np.arange(8.0)}, num_partitions=2)\n"
+            "R.fan_out(_df_task, df, 2, use_gpu=False)\n"
+            "R.fan_out(_df_task, df, 2, use_gpu=False)\n"
+            "import os; os.environ['SML_EXECUTOR_POOL'] = '0'\n"
+            "R.fan_out(_df_task, df, 2, use_gpu=False)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "KeyError" not in p.stderr and "leaked shared_memory" not in p.stderr, p.stderr[-2000:]

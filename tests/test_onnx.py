@@ -639,6 +639,11 @@ def test_onnx_model_transform_fans_out_over_partitions(monkeypatch):
     calls = []
     real = R.fan_out_transform
     monkeypatch.setattr(R, "fan_out_transform", lambda *a, **k: calls.append(a[2]) or real(*a, **k))
+    m.transform(df)
+    assert calls == []  # 60 rows: below the per-task row threshold, scored in this process
+    with pytest.raises(ValueError, match="not in the DataFrame"):  # validated before any fan-out
+        m.copy().setFeedDict({next(iter(m.modelInput)): "nope"}).transform(df)
+    monkeypatch.setenv("SML_TRANSFORM_MIN_ROWS", "1")
     out = m.transform(df)
     assert calls == [2]
     assert out["id"].tolist() == list(range(60))

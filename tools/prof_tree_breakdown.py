@@ -61,7 +61,7 @@ for t in trees:
     cnt = collections.Counter()
     for n, d, s, e in t:
         for b in bnames:
-            if n.startswith(b):
+            if n.startswith(b) or (b == 'bpart_kernel' and n.startswith('bpart_lid_kernel')):
                 rpos[b][cnt[b]].append(d)
                 cnt[b] += 1
     if cnt['bplan_kernel']:
