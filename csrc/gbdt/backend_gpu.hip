@@ -1162,31 +1162,15 @@ __device__ __forceinline__ void SlabWrite(ulonglong2* out, const unsigned long l
 // One block's share of a leaf histogram: rows [begin, begin + count) of ping-pong buffer `buf` (-1 =
 // physical rows) are cut into nb_active chunks; this block (chunk lb, feature group blockIdx.y) accumulates
 // its chunk into LDS and writes its slab.
-// bhist (leaf-id mode): this block's rows are the runs [r0, r1) of expansion j's list; spre = their exclusive
-// prefix of smaller-side counts (nr + 1 entries, in LDS). Position p -> the run holding it (binary search) ->
-// list[j stride + run C + (p - spre[run])].
-struct LidRuns {
-  const int32_t* list;  // expansion j's list
-  const int* spre;      // LDS
-  int nr, r0, chunk;
-  // positions of one thread grow (a clamped tail position restarts the walk): `k` is the thread's current run
-  __device__ __forceinline__ int row(int p, int& k) const {
-    if (nr == 1) return list[static_cast<int64_t>(r0) * chunk + p];
-    if (p < spre[k]) k = 0;
-    while (k + 1 < nr && spre[k + 1] <= p) ++k;
-    return list[static_cast<int64_t>(r0 + k) * chunk + (p - spre[k])];
-  }
-};
-
-// kGather: rows come from the leaf-id partition's runs (`runs`) and g / h are read at the row id
-template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false, bool kGather = false>
+// kGH2: the index-only partition - the segment holds row ids only and each row's (g, h) is gathered from the
+// interleaved physical copy `g` points to (float2 per row)
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false, bool kGH2 = false>
 __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_active, int lb, const uint4* __restrict__ bins4,
                                          int W4, int F, const int32_t* __restrict__ perm0,
                                          const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
                                          const float2* __restrict__ ogh1, const float* __restrict__ g,
                                          const float* __restrict__ h, const float* __restrict__ ghmax,
-                                         ulonglong2* __restrict__ slab_out, int64_t scale_n,
-                                         const LidRuns& runs = LidRuns{}) {
+                                         ulonglong2* __restrict__ slab_out, int64_t scale_n) {
   constexpr int kWords = kFPG * kBinsPerFeature;
   // g plane at 0, h plane kHOff bytes above it (kTight: F <= 28, see kHPlaneTight)
   constexpr uint32_t kHOff = kFPG == 32 ? (kTight ? kHPlaneTight : kHPlaneApart) : kWords * 8u;
@@ -1209,11 +1193,12 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
   const int p0 = begin + lb * chunk;
   const int p1 = min(begin + count, p0 + chunk);
   const HScale sc = HistScaleV(scale_n, gmax_g, gmax_h);
-  const int32_t* __restrict__ perm = kGather || buf == 0 ? perm0 : perm1;
+  const int32_t* __restrict__ perm = buf == 0 ? perm0 : perm1;
   const float2* __restrict__ ogh = buf == 0 ? ogh0 : ogh1;
-  const bool phys = !kGather && buf < 0;
+  const float2* __restrict__ gh2 = reinterpret_cast<const float2*>(g);
+  const bool phys = buf < 0;
   const int rot = tid & 15;
-  static_assert(!(kPipe && kGather), "the pipelined loop reads the ordered g / h copy");
+  static_assert(!(kPipe && kGH2), "the pipelined loop reads the ordered g / h copy");
   if constexpr (kPipe) {
     // Software pipeline, two stages deep: while the rows of step i go into the LDS histogram, the bins /
     // (g, h) of step i + 1 and the row ids of step i + 2 are in flight, so a wave's memory latency hides
@@ -1262,7 +1247,6 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
     SlabWrite<kFPG, kHistBlockThreads>(slab_out, shg, shh, F, grp * kFPG, Fg, tid);
     return;
   }
-  int rk = 0;  // kGather: this thread's current run
   for (int base = p0 + tid; base < p1; base += kHistBlockThreads * kUnroll) {
     // branch-free loads (positions past p1 read position p0, a valid row, and are never accumulated): a
     // guarded load is a branch, and the compiler waits out each one before the next row's
@@ -1273,7 +1257,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
       const int pos = base + u * kHistBlockThreads;
       ok[u] = pos < p1;
       pq[u] = ok[u] ? pos : p0;
-      r[u] = kGather ? runs.row(pq[u], rk) : (phys ? pq[u] : perm[pq[u]]);
+      r[u] = phys ? pq[u] : perm[pq[u]];
     }
     uint4 b0[kUnroll], b1[kUnroll];
     float2 v[kUnroll];
@@ -1283,7 +1267,7 @@ __device__ __forceinline__ void HistBody(int begin, int count, int buf, int nb_a
       b0[u] = bins4[rb];
       b1[u] = bins4[two ? rb + 1 : rb];
       if (!two) b1[u] = make_uint4(0, 0, 0, 0);
-      v[u] = phys || kGather ? make_float2(g[r[u]], h[r[u]]) : ogh[pq[u]];
+      v[u] = kGH2 ? gh2[r[u]] : (phys ? make_float2(g[r[u]], h[r[u]]) : ogh[pq[u]]);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
@@ -2951,7 +2935,8 @@ struct PartRegs {
 
 // Issue the loads of a tile: row ids + (g, h) (physical or ordered), then the split feature's bins. Branch-free
 // as PartitionTile's (rows past the segment read its first position and are masked later).
-template <int kPartRows>
+// kIdx: the index-only partition (row ids move, g / h stay in the interleaved physical copy bhist gathers from)
+template <int kPartRows, bool kIdx = false>
 __device__ __forceinline__ void PartLoad(PartRegs<kPartRows>& t, int feature, int t0, int tv, int pbuf,
                                          const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
                                          const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0,
@@ -2964,7 +2949,7 @@ __device__ __forceinline__ void PartLoad(PartRegs<kPartRows>& t, int feature, in
       const int k = u * kPartThreads + tid;
       const int p = t0 + (k < tv ? k : 0);
       t.r[u] = p;
-      t.v[u] = make_float2(g[p], h[p]);
+      if (!kIdx) t.v[u] = make_float2(g[p], h[p]);
     }
   } else {
     const int32_t* perm = pbuf == 0 ? perm0 : perm1;
@@ -2974,7 +2959,7 @@ __device__ __forceinline__ void PartLoad(PartRegs<kPartRows>& t, int feature, in
       const int k = u * kPartThreads + tid;
       const int p = t0 + (k < tv ? k : 0);
       t.r[u] = perm[p];
-      t.v[u] = ogh[p];
+      if (!kIdx) t.v[u] = ogh[p];
     }
   }
   const uint8_t* __restrict__ col = cbins + static_cast<size_t>(feature) * n;
@@ -2987,7 +2972,7 @@ __device__ __forceinline__ void PartLoad(PartRegs<kPartRows>& t, int feature, in
 // the expansion's cursor -> barrier), so their memory latency overlaps the atomic's round trip and the
 // scatter instead of following it. Output order inside a child is still the claim order (histograms are
 // exact integer sums: nothing downstream depends on it).
-template <int kPartRows>
+template <int kPartRows, bool kIdx = false>
 __device__ __forceinline__ void BatchedPartitionPipelined(
     BState* __restrict__ bs, int nexp, int ntiles, const int* s_tile0, const int* s_pb, const int* s_pc,
     const int* s_pbuf, const PartSplit* s_ps, const uint32_t (*s_cat)[8], const uint8_t* __restrict__ cbins, int64_t n,
@@ -3012,7 +2997,7 @@ __device__ __forceinline__ void BatchedPartitionPipelined(
   PartRegs<kPartRows> cur, nxt;
   int j, t0, tv;
   locate(tile, &j, &t0, &tv);
-  PartLoad<kPartRows>(cur, s_ps[j].feature, t0, tv, s_pbuf[j], cbins, n, perm0, perm1, ogh0, ogh1, g, h);
+  PartLoad<kPartRows, kIdx>(cur, s_ps[j].feature, t0, tv, s_pbuf[j], cbins, n, perm0, perm1, ogh0, ogh1, g, h);
   for (;;) {
     const PartSplit ps = s_ps[j];
     int rl[kPartRows];
@@ -3042,7 +3027,7 @@ __device__ __forceinline__ void BatchedPartitionPipelined(
     int nj = j, nt0 = 0, ntv = 0;
     if (ntile < ntiles) {
       locate(ntile, &nj, &nt0, &ntv);
-      PartLoad<kPartRows>(nxt, s_ps[nj].feature, nt0, ntv, s_pbuf[nj], cbins, n, perm0, perm1, ogh0, ogh1, g, h);
+      PartLoad<kPartRows, kIdx>(nxt, s_ps[nj].feature, nt0, ntv, s_pbuf[nj], cbins, n, perm0, perm1, ogh0, ogh1, g, h);
     }
     __syncthreads();
     const int lb = bases[0], rb = bases[1];
@@ -3063,7 +3048,9 @@ __device__ __forceinline__ void BatchedPartitionPipelined(
       if (k < tv) {
         const int lbefore = run + wb + rl[u];
         const int dst = (lmask >> u) & 1u ? lb + lbefore : rb + (k - lbefore);
-        if (c_part_wt) {
+        if (kIdx) {
+          operm[dst] = cur.r[u];
+        } else if (c_part_wt) {
           __hip_atomic_store(operm + dst, cur.r[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(reinterpret_cast<unsigned long long*>(oogh + dst),
                              (static_cast<unsigned long long>(__float_as_uint(cur.v[u].y)) << 32) |
@@ -3086,7 +3073,7 @@ __device__ __forceinline__ void BatchedPartitionPipelined(
   }
 }
 
-template <int kPartRows>
+template <int kPartRows, bool kIdx = false>
 __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
     BState* __restrict__ bs, const uint8_t* __restrict__ cbins, int64_t n, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
@@ -3108,9 +3095,9 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   }
   if (tid < nexp * 8) s_cat[tid >> 3][tid & 7] = bs->exp[tid >> 3].cat[tid & 7];
   __syncthreads();
-  if (c_part_pipe) {
-    BatchedPartitionPipelined<kPartRows>(bs, nexp, ntiles, s_tile0, s_pb, s_pc, s_pbuf, s_ps, s_cat, cbins, n, perm0,
-                                         perm1, ogh0, ogh1, wperm0, wperm1, wogh0, wogh1, g, h);
+  if (kIdx || c_part_pipe) {  // the index-only partition has the pipelined form only
+    BatchedPartitionPipelined<kPartRows, kIdx>(bs, nexp, ntiles, s_tile0, s_pb, s_pc, s_pbuf, s_ps, s_cat, cbins, n,
+                                               perm0, perm1, ogh0, ogh1, wperm0, wperm1, wogh0, wogh1, g, h);
     return;
   }
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -3122,320 +3109,18 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
   }
 }
 
-// ---- leaf-id partition (the batched growth's default when bagging is off)
-// Instead of moving every row of an expanded node (row id + ordered g / h: 12 B read + 12 B written per row, 60.5M
-// row moves per 31-leaf tree at 11M rows - the 412 us/iter bpart of profiles/r5/pass38), every row carries the id
-// of the node it sits in (1 B when the node table fits 256 ids) and a round is one coalesced pass over the ids: a
-// row of an expanded node reads its split feature's bin and takes the child's id; rows outside the round's
-// expansions cost one byte read.
-// The smaller children's rows are listed for bhist WITHOUT any global atomic: a round-6 first form claimed list
-// space with one 64-bit atomic per (4096-row block, expansion) on the expansion cursor - ~2700 serialized
-// same-address atomics per round cost ~50 us whatever the round's size (r6 pass 1). Now the grid is G blocks of
-// kLidThreads threads, block b owns the contiguous row chunk [b C, (b + 1) C) and writes the smaller-side rows of
-// expansion j into its own run list[j * stride + b * C ..] (capacity C: no claim needed), in a second pass over
-// the ids it just wrote; its (left, right) counts go to cnt[j * G + b]. bhist reads the runs (a block takes a
-// contiguous range of runs, a row position is located by a binary search over the runs' prefix in LDS) and
-// block 0 of bhist stores the totals into the expansion cursor (left in the low half, right in the high half), so
-// the reduce / plan read the same counts as with the moving partition. Deterministic list positions.
-constexpr int kLidThreads = 1024;
-constexpr int kLidRows = 16;          // ids per thread per group (one 16-B load of 1-B ids)
-constexpr int kLidGroups = 3;         // groups per thread per pass: C <= kLidThreads * kLidRows * kLidGroups
-constexpr int kLidMaxChunk = kLidThreads * kLidRows * kLidGroups;  // 49152 (16-bit per-block counters)
-constexpr int kLidMaxRuns = 2048;     // G: runs per expansion (bhist stages a run prefix in LDS)
-
-template <typename Id>
-struct LidVec {  // kLidRows ids
-  static constexpr int kWords = kLidRows * sizeof(Id) / 16;
-  uint4 w[kWords];
-  __device__ __forceinline__ uint32_t get(int u) const {
-    const uint32_t* d = reinterpret_cast<const uint32_t*>(w);
-    if constexpr (sizeof(Id) == 1) return (d[u >> 2] >> (8 * (u & 3))) & 0xFFu;
-    else return (d[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-  }
-  __device__ __forceinline__ void set(int u, uint32_t v) {
-    uint32_t* d = reinterpret_cast<uint32_t*>(w);
-    if constexpr (sizeof(Id) == 1) {
-      const int s = 8 * (u & 3);
-      d[u >> 2] = (d[u >> 2] & ~(0xFFu << s)) | (v << s);
-    } else {
-      const int s = 16 * (u & 1);
-      d[u >> 1] = (d[u >> 1] & ~(0xFFFFu << s)) | (v << s);
-    }
-  }
-};
-
-// block-wide exclusive prefix of a packed 64-bit counter word (kLidThreads threads); *total = the block sum
-__device__ __forceinline__ unsigned long long LidBlockScan(unsigned long long v, unsigned long long* s_w,
-                                                           unsigned long long* total) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  unsigned long long x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned long long y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) s_w[wid] = x;
-  __syncthreads();
-  unsigned long long pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kLidThreads / 64; ++w) {
-    const unsigned long long t = s_w[w];
-    pre += w < wid ? t : 0ull;
-    tot += t;
-  }
-  __syncthreads();  // s_w is reused by the next word's scan
-  *total = tot;
-  return pre + x - v;
-}
-
-template <int kW>
-__device__ __forceinline__ uint32_t LidField(const unsigned long long (&w)[kW], int j) {
-  unsigned long long x = w[0];
-#pragma unroll
-  for (int q = 1; q < kW; ++q) x = (j >> 2) == q ? w[q] : x;
-  return static_cast<uint32_t>(x >> (16 * (j & 3))) & 0xFFFFu;
-}
-
-// grid G x kLidThreads; kW counter words of 4 expansions each (rounds of up to 4 kW expansions)
-template <typename Id, int kW>
-__global__ __launch_bounds__(kLidThreads) void bpart_lid_kernel(BState* __restrict__ bs, void* __restrict__ lid_raw,
-                                                              const uint8_t* __restrict__ cbins, int32_t n, int chunk,
-                                                              int32_t* __restrict__ list, int64_t list_stride,
-                                                              unsigned long long* __restrict__ cnt, int first) {
-  const int nexp = bs->nexp;
-  if (nexp == 0) return;
-  Id* __restrict__ lid = static_cast<Id*>(lid_raw);
-  constexpr int kMap = sizeof(Id) == 1 ? 256 : kBatchMaxNodes;
-  __shared__ int8_t s_map[kMap];   // node id -> expansion slot (this round's parents)
-  __shared__ int8_t s_cmap[kMap];  // node id -> 2 slot + side (this round's children; pass 2)
-  // per expansion: split feature, packed decision (thr | missing bin << 8 | dleft << 17 | is_cat << 18; missing
-  // bin 256 = none), children ids (c0 | c1 << 16)
-  __shared__ int s_feat[kMaxSpec];
-  __shared__ uint32_t s_dec[kMaxSpec], s_cc[kMaxSpec];
-  __shared__ uint32_t s_cat[kMaxSpec][8];
-  __shared__ int s_ls[kMaxSpec];
-  __shared__ unsigned long long s_w[kLidThreads / 64];
-  __shared__ int s_anycat;
-  const int tid = threadIdx.x, G = static_cast<int>(gridDim.x);
-  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * chunk;
-  const int64_t c1 = min(static_cast<int64_t>(n), c0 + chunk);
-  // this thread's groups: kLidGroups consecutive 16-row groups from c0 + tid kLidGroups 16 (so the list, filled in
-  // thread order, follows the physical row order: bhist's row gathers stay ascending); their ids go out before
-  // the tables are staged
-  LidVec<Id> ids[kLidGroups];
-#pragma unroll
-  for (int k = 0; k < kLidGroups; ++k) {
-    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
-#pragma unroll
-    for (int q = 0; q < LidVec<Id>::kWords; ++q) ids[k].w[q] = make_uint4(0, 0, 0, 0);
-    if (!first && r0 < c1) {
-      const uint4* src = reinterpret_cast<const uint4*>(lid + r0);
-#pragma unroll
-      for (int q = 0; q < LidVec<Id>::kWords; ++q) ids[k].w[q] = src[q];
-    }
-  }
-  for (int i = tid; i < kMap; i += kLidThreads) { s_map[i] = -1; s_cmap[i] = -1; }
-  if (tid == 0) s_anycat = 0;
-  __syncthreads();
-  if (tid < nexp) {
-    const BExp& x = bs->exp[tid];
-    const PartSplit& ps = x.ps;
-    if (ps.is_cat) s_anycat = 1;
-    if (x.node >= 0 && x.node < kMap) s_map[x.node] = static_cast<int8_t>(tid);
-    if (x.c0 >= 0 && x.c0 < kMap) s_cmap[x.c0] = static_cast<int8_t>(2 * tid);
-    if (x.c1 >= 0 && x.c1 < kMap) s_cmap[x.c1] = static_cast<int8_t>(2 * tid + 1);
-    const uint32_t mbin = ps.mt == kMissingZero ? static_cast<uint32_t>(ps.dbin)
-                                                : (ps.mt == kMissingNaN ? static_cast<uint32_t>(ps.nb - 1) : 256u);
-    s_feat[tid] = ps.feature;
-    s_dec[tid] = (ps.thr > 255u ? 255u : ps.thr) | (mbin << 8) | ((ps.dleft ? 1u : 0u) << 17) |
-                 ((ps.is_cat ? 1u : 0u) << 18);
-    s_cc[tid] = static_cast<uint32_t>(x.c0) | (static_cast<uint32_t>(x.c1) << 16);
-    s_ls[tid] = x.left_small;
-  }
-  if (tid < nexp * 8) s_cat[tid >> 3][tid & 7] = bs->exp[tid >> 3].cat[tid & 7];
-  __syncthreads();
-  // ---- pass 1: new ids, per-thread left / right counts (4 expansions per 64-bit word, 16-bit fields)
-  unsigned long long cl[kW], cr[kW];
-#pragma unroll
-  for (int w = 0; w < kW; ++w) { cl[w] = 0ull; cr[w] = 0ull; }
-  // window path (<= 4 expansions, 16-B aligned columns): a group's rows of expansion j read their bins from ONE
-  // 16-B load of column f_j at the group's rows (4 window loads at most instead of 16 byte gathers); every
-  // group's windows are issued before any is used. Expansion slots per row packed as nibbles (15 = none).
-  const bool win = kW == 1 && (n & 15) == 0;
-  unsigned long long jn[kLidGroups];
-  uint32_t present[kLidGroups];
-  if (win) {
-#pragma unroll
-    for (int k = 0; k < kLidGroups; ++k) {
-      const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
-      unsigned long long nib = ~0ull;
-      uint32_t pr = 0;
-#pragma unroll
-      for (int u = 0; u < kLidRows; ++u) {
-        const uint32_t v = ids[k].get(u);
-        const int j = r0 + u < c1 && v < static_cast<uint32_t>(kMap) ? static_cast<int>(s_map[v]) : -1;
-        if (j >= 0) { nib &= ~(15ull << (4 * u)); nib |= static_cast<unsigned long long>(j) << (4 * u); pr |= 1u << j; }
-      }
-      jn[k] = nib;
-      present[k] = pr;
-    }
-  }
-  // the windows of group k: issued one group ahead of their use (two groups' windows live at a time)
-  auto load_win = [&](int k, uint4 (&w)[4]) {
-    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      w[j] = make_uint4(0, 0, 0, 0);
-      if ((present[k] >> j) & 1u) w[j] = *reinterpret_cast<const uint4*>(cbins + static_cast<size_t>(s_feat[j]) * n + r0);
-    }
-  };
-  uint4 wcur[4], wnxt[4];
-  if (win) load_win(0, wcur);
-  auto count_row = [&](int j, bool left) {
-    const unsigned long long one = j >= 0 ? (1ull << (16 * (j & 3))) : 0ull;
-#pragma unroll
-    for (int w = 0; w < kW; ++w) {
-      const unsigned long long add = (j >> 2) == w ? one : 0ull;
-      cl[w] += left ? add : 0ull;
-      cr[w] += left ? 0ull : add;
-    }
-  };
-#pragma unroll
-  for (int k = 0; k < kLidGroups; ++k) {
-    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
-    if (r0 >= c1) break;
-    if (win) {
-      if (k + 1 < kLidGroups) load_win(k + 1, wnxt);
-      const uint4* wbk = wcur;
-      if (jn[k] == ~0ull) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wcur[j] = wnxt[j];
-        continue;
-      }
-      // numerical splits decided straight from the windows; categorical ones (rare) below
-#pragma unroll
-      for (int u = 0; u < kLidRows; ++u) {
-        const int j = static_cast<int>((jn[k] >> (4 * u)) & 15ull);
-        const uint32_t w0 = (&wbk[0].x)[u >> 2], w1 = (&wbk[1].x)[u >> 2];
-        const uint32_t w2 = (&wbk[2].x)[u >> 2], w3 = (&wbk[3].x)[u >> 2];
-        const uint32_t w = (j & 2) ? ((j & 1) ? w3 : w2) : ((j & 1) ? w1 : w0);
-        const uint32_t bu = (w >> (8 * (u & 3))) & 0xFFu;
-        const int jj = j == 15 ? 0 : j;
-        const uint32_t d = s_dec[jj], cc = s_cc[jj];
-        bool left = bu == ((d >> 8) & 511u) ? ((d >> 17) & 1u) != 0 : bu <= (d & 255u);
-        if (s_anycat && j != 15 && ((d >> 18) & 1u)) left = (s_cat[jj][bu >> 5] >> (bu & 31)) & 1u;
-        ids[k].set(u, j == 15 ? ids[k].get(u) : (left ? (cc & 0xFFFFu) : (cc >> 16)));
-        count_row(j == 15 ? -1 : j, left);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wcur[j] = wnxt[j];
-    } else {
-      int js[kLidRows];
-      uint32_t b[kLidRows];
-      bool any = false;
-#pragma unroll
-      for (int u = 0; u < kLidRows; ++u) {
-        const uint32_t v = ids[k].get(u);
-        js[u] = r0 + u < c1 && v < static_cast<uint32_t>(kMap) ? static_cast<int>(s_map[v]) : -1;
-        any |= js[u] >= 0;
-      }
-      if (!any) continue;
-#pragma unroll
-      for (int u = 0; u < kLidRows; ++u) {
-        const int f = js[u] >= 0 ? s_feat[js[u]] : 0;
-        b[u] = cbins[static_cast<size_t>(f) * n + (r0 + u < c1 ? r0 + u : c0)];
-      }
-      // branch-free per row (rows outside the round keep their id); categorical splits only when the round has one
-#pragma unroll
-      for (int u = 0; u < kLidRows; ++u) {
-        const int j = js[u], jj = j < 0 ? 0 : j;
-        const uint32_t d = s_dec[jj], bu = b[u], cc = s_cc[jj];
-        bool left = bu == ((d >> 8) & 511u) ? ((d >> 17) & 1u) != 0 : bu <= (d & 255u);
-        if (s_anycat && j >= 0 && ((d >> 18) & 1u)) left = (s_cat[jj][bu >> 5] >> (bu & 31)) & 1u;
-        ids[k].set(u, j < 0 ? ids[k].get(u) : (left ? (cc & 0xFFFFu) : (cc >> 16)));
-        count_row(j, left);
-      }
-    }
-    uint4* dst = reinterpret_cast<uint4*>(lid + r0);  // the id array is padded to whole groups
-#pragma unroll
-    for (int q = 0; q < LidVec<Id>::kWords; ++q) dst[q] = ids[k].w[q];
-  }
-  // ---- block prefix of the counts, the block's (left, right) per expansion -> cnt[j * G + b]
-  const int nw = (nexp + 3) >> 2;
-  unsigned long long el[kW], er[kW], tl[kW], tr[kW];
-#pragma unroll
-  for (int w = 0; w < kW; ++w) { el[w] = er[w] = tl[w] = tr[w] = 0ull; }
-#pragma unroll
-  for (int w = 0; w < kW; ++w) {
-    if (w >= nw) break;  // block-uniform
-    el[w] = LidBlockScan(cl[w], s_w, &tl[w]);
-    er[w] = LidBlockScan(cr[w], s_w, &tr[w]);
-  }
-  if (tid < nexp)
-    cnt[static_cast<size_t>(tid) * G + blockIdx.x] =
-        static_cast<unsigned long long>(LidField(tl, tid)) | (static_cast<unsigned long long>(LidField(tr, tid)) << 32);
-  // ---- pass 2: smaller-side rows -> the block's run of the expansion's list (positions: thread prefix + running)
-  unsigned long long ol[kW], orr[kW];
-#pragma unroll
-  for (int w = 0; w < kW; ++w) { ol[w] = el[w]; orr[w] = er[w]; }
-#pragma unroll
-  for (int k = 0; k < kLidGroups; ++k) {
-    const int64_t r0 = c0 + static_cast<int64_t>(tid * kLidGroups + k) * kLidRows;
-    if (r0 >= c1) break;
-#pragma unroll
-    for (int u = 0; u < kLidRows; ++u) {
-      const uint32_t v = ids[k].get(u);
-      const int m = r0 + u < c1 && v < static_cast<uint32_t>(kMap) ? static_cast<int>(s_cmap[v]) : -1;
-      const int jj = m < 0 ? 0 : (m >> 1);
-      const bool left = (m & 1) == 0;
-      const bool app = m >= 0 && left == (s_ls[jj] != 0);
-      const uint32_t p = left ? LidField(ol, jj) : LidField(orr, jj);
-      if (app) list[jj * list_stride + c0 + p] = static_cast<int32_t>(r0 + u);
-      const unsigned long long one = m >= 0 ? 1ull << (16 * (jj & 3)) : 0ull;
-#pragma unroll
-      for (int q = 0; q < kW; ++q) {
-        const unsigned long long a = (jj >> 2) == q ? one : 0ull;
-        ol[q] += left ? a : 0ull;
-        orr[q] += left ? 0ull : a;
-      }
-    }
-  }
-}
-
-
-template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false, bool kLid = false>
+// kIdx: the index-only partition (row ids in the segments; `g` = the interleaved (g, h) copy, gathered per row)
+template <int kUnroll, int kFPG, bool kPipe = false, bool kTight = false, bool kIdx = false>
 __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
     const BState* __restrict__ bs, const uint4* __restrict__ bins4, int W4, int F, const int32_t* __restrict__ perm0,
     const int32_t* __restrict__ perm1, const float2* __restrict__ ogh0, const float2* __restrict__ ogh1,
     const float* __restrict__ g, const float* __restrict__ h, const float* __restrict__ ghmax,
-    ulonglong2* __restrict__ slab, int64_t scale_n, BState* __restrict__ bsw, const unsigned long long* __restrict__ lcnt,
-    int G, int chunk, int64_t lstride) {
+    ulonglong2* __restrict__ slab, int64_t scale_n) {
   const int nexp = bs->nexp;
   if (nexp == 0) return;
   __shared__ int s_cnt[kMaxSpec], s_nb[kMaxSpec], s_off[kMaxSpec];
-  if constexpr (kLid) {
-    // the expansions' totals from the partition's per-block counts (wave j sums expansion j's G counts: 32-bit
-    // halves cannot carry into each other, every block total is < 2^16); block (0, 0) publishes them in the cursors
-    __shared__ unsigned int s_tl[kMaxSpec], s_tr[kMaxSpec];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    static_assert(kHistBlockThreads / 64 >= kMaxSpec, "one wave per expansion");
-    if (wid < nexp) {
-      unsigned long long acc = 0;
-      for (int b = lane; b < G; b += 64) acc += lcnt[static_cast<size_t>(wid) * G + b];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) { s_tl[wid] = static_cast<unsigned int>(acc & 0xFFFFFFFFull); s_tr[wid] = static_cast<unsigned int>(acc >> 32); }
-    }
-    __syncthreads();
-    if (tid < nexp) {
-      s_cnt[tid] = static_cast<int>(bs->exp[tid].left_small ? s_tl[tid] : s_tr[tid]);
-      if (blockIdx.x == 0 && blockIdx.y == 0)
-        bsw->cursor[tid] = static_cast<unsigned long long>(s_tl[tid]) | (static_cast<unsigned long long>(s_tr[tid]) << 32);
-    }
-  } else {
-    // the expansions' counts load in parallel (one thread each: one memory latency, not nexp in a row)
-    if (threadIdx.x < nexp) s_cnt[threadIdx.x] = BatchSmallCount(bs, threadIdx.x);
-  }
+  // the expansions' counts load in parallel (one thread each: one memory latency, not nexp in a row)
+  if (threadIdx.x < nexp) s_cnt[threadIdx.x] = BatchSmallCount(bs, threadIdx.x);
   __syncthreads();
   if (threadIdx.x == 0) BatchHistAlloc(s_cnt, nexp, s_nb, s_off);
   __syncthreads();
@@ -3444,42 +3129,11 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   for (int q = 0; q < nexp; ++q) if (bx >= s_off[q] && bx < s_off[q] + s_nb[q]) j = q;
   if (j < 0) return;
   const BExp& x = bs->exp[j];
-  if constexpr (kLid) {
-    // this block's runs of expansion j's list and their smaller-side prefix (wave 0 scans 64 runs at a time)
-    __shared__ int s_pre[kLidMaxRuns + 1];
-    const int nb = s_nb[j], lb = bx - s_off[j];
-    const int r0 = static_cast<int>(static_cast<int64_t>(lb) * G / nb);
-    const int r1 = static_cast<int>(static_cast<int64_t>(lb + 1) * G / nb);
-    const int nr = r1 - r0, tid = threadIdx.x, lane = tid & 63;
-    const bool lsm = x.left_small != 0;
-    if (tid < 64) {
-      int carry = 0;
-      if (tid == 0) s_pre[0] = 0;
-      for (int b0 = 0; b0 < nr; b0 += 64) {
-        const int k = b0 + lane;
-        const unsigned long long v = k < nr ? lcnt[static_cast<size_t>(j) * G + r0 + k] : 0ull;
-        int c = static_cast<int>(lsm ? (v & 0xFFFFFFFFull) : (v >> 32));
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int y = __shfl_up(c, off, 64);
-          if (lane >= off) c += y;
-        }
-        if (k < nr) s_pre[k + 1] = carry + c;
-        carry += __shfl(c, 63, 64);
-      }
-    }
-    __syncthreads();
-    LidRuns runs{perm0 + static_cast<int64_t>(j) * lstride, s_pre, nr, r0, chunk};
-    HistBody<kUnroll, kFPG, kPipe, kTight, true>(0, s_pre[nr], 0, 1, 0, bins4, W4, F, perm0, perm1, ogh0, ogh1, g, h,
-                                                 ghmax, slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n,
-                                                 runs);
-  } else {
-    const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
-    const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
-    HistBody<kUnroll, kFPG, kPipe, kTight>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F,
-                                           perm0, perm1, ogh0, ogh1, g, h, ghmax,
-                                           slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n);
-  }
+  const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+  const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
+  HistBody<kUnroll, kFPG, kPipe, kTight, kIdx>(begin, s_cnt[j], x.pbuf == 0 ? 1 : 0, s_nb[j], bx - s_off[j], bins4, W4, F,
+                                               perm0, perm1, ogh0, ogh1, g, h, ghmax,
+                                               slab + static_cast<size_t>(bx) * F * kBinsPerFeature, scale_n);
 }
 
 // grid (ceil(E / kRedE), spec_k): block (x, j) reduces the slabs of expansion j into part[j * (E + 1) ..]
@@ -3733,7 +3387,8 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
 // Replaces score_kernel + grad_kernel + the root hist_kernel (150 + 54 + 131
 // us at 11M x 28 on MI355X, three full passes over rows).
 
-template <int kUnroll, bool kPipe = false, bool kTight = false>
+// kGH2: the gradients go to one interleaved (g, h) array (`g`, float2 per row) for the index-only partition
+template <int kUnroll, bool kPipe = false, bool kTight = false, bool kGH2 = false>
 __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
@@ -3781,8 +3436,12 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     score[i] = sn;
     float gg, hh;
     PointGradient(p, sn, yv, wv, &gg, &hh);
-    g[i] = gg;
-    h[i] = hh;
+    if (kGH2) {
+      reinterpret_cast<float2*>(g)[i] = make_float2(gg, hh);
+    } else {
+      g[i] = gg;
+      h[i] = hh;
+    }
     mg = fmaxf(mg, fabsf(gg));
     mh = fmaxf(mh, fabsf(hh));
     hist_accumulate_rot<32, kFeatPerGroup, kHOff>(shg, shh, r0, r1, QuantGH(make_float2(gg, hh), sc), rot, fo);
@@ -3853,6 +3512,22 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   __syncthreads();
   SlabWrite<kFeatPerGroup, kThreads>(slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature, shg, shh, F, 0, F,
                                      tid);
+}
+
+// (g, h) <-> the interleaved copy the index-only partition's histograms gather from
+__global__ void pack_gh_kernel(const float* __restrict__ g, const float* __restrict__ h, int64_t n,
+                               float2* __restrict__ gh) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gh[i] = make_float2(g[i], h[i]);
+}
+
+__global__ void unpack_gh_kernel(const float2* __restrict__ gh, int64_t n, float* __restrict__ g,
+                                 float* __restrict__ h) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float2 v = gh[i];
+    g[i] = v.x;
+    h[i] = v.y;
+  }
 }
 
 // row-major -> column-major bin copy (once per dataset)
@@ -3977,27 +3652,13 @@ class GpuBackend : public TrainBackend {
         SML_HIP_CHECK(hipMemset(bprof_, 0, nb));
       }
       for (hipEvent_t& e : bev_) SML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      // leaf-id partition: SML_GBDT_LID=1 (bagged trees still take the moving partition); off by default - on
-      // MI355X it measured slower than the moving partition (1.77 vs 1.56 ms/iter at 11M x 28, r6 passes 1-4)
-      lid_ok_ = false;
-      if (const char* e = std::getenv("SML_GBDT_LID")) lid_ok_ = std::atoi(e) != 0;
-      if (lid_ok_) {
-        // chunk: rows per partition block, a multiple of 16 (whole 16-B id groups), <= kLidMaxChunk (16-bit block
-        // counters); G = blocks = runs per expansion (<= kLidMaxRuns: larger sets keep the moving partition)
-        int64_t c = std::max<int64_t>(16, (n_ + 255) / 256);
-        c = std::min<int64_t>(kLidMaxChunk, (c + 15) / 16 * 16);
-        const int64_t g = (n_ + c - 1) / c;
-        if (g > kLidMaxRuns || c > static_cast<int64_t>(kLidThreads) * kLidRows * kLidGroups) lid_ok_ = false;
-        if (lid_ok_) {
-          lid_wide_ = cap_nodes > 256;
-          lid_chunk_ = static_cast<int>(c);
-          lid_g_ = static_cast<int>(g);
-          lid_stride_ = g * c;
-          lid_.alloc(static_cast<size_t>(lid_stride_) * (lid_wide_ ? 2 : 1) + 64);
-          lid_list_.alloc(static_cast<size_t>(lid_stride_) * spec_k_);
-          lid_cnt_.alloc(static_cast<size_t>(kMaxSpec) * lid_g_);
-        }
-      }
+      // index-only partition (bpart_kernel<.., true>): the batched partition moves row ids only (4 + 4 B per row
+      // instead of 12 + 12 with the ordered g / h) and bhist gathers each row's (g, h) from one interleaved
+      // physical copy (gh2_, written by the fused score / gradient pass or packed once per tree); one class, no
+      // bagging. SML_GBDT_IDX=0: the ordered-gradient partition.
+      idx_ok_ = K == 1;
+      if (const char* e = std::getenv("SML_GBDT_IDX")) idx_ok_ = idx_ok_ && std::atoi(e) != 0;
+      if (idx_ok_) gh2_.alloc(n_);
     }
     // launch-shape knobs for A/B runs (defaults are the measured best)
     if (const char* e = std::getenv("SML_PART_ROWS")) part_rows_ = std::atoi(e);
@@ -4199,6 +3860,7 @@ class GpuBackend : public TrainBackend {
     }
     prep_valid_ = false;
     root_ready_ = false;
+    gh2_valid_ = g_stale_ = false;  // g_ / h_ are rewritten below
     if (p.kind == kObjLambdarank && K_ == 1) {
       auto t0 = std::chrono::steady_clock::now();
       EnsureRankTables(obj);
@@ -4277,12 +3939,21 @@ class GpuBackend : public TrainBackend {
   void SetGradients(const float* g, const float* h) override {
     ghmax_valid_ = false;
     prep_valid_ = root_ready_ = false;
+    gh2_valid_ = g_stale_ = false;
     pending_parts_ = 0;
     SML_HIP_CHECK(hipMemcpyAsync(g_.get(), g, sizeof(float) * n_ * K_, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipMemcpyAsync(h_.get(), h, sizeof(float) * n_ * K_, hipMemcpyHostToDevice, stream_));
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
   }
+  // g_ / h_ made current when the fused pass wrote only the interleaved copy
+  void EnsureGH() {
+    if (!g_stale_) return;
+    hipLaunchKernelGGL(unpack_gh_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, gh2_.get(), n_, g_.get(), h_.get());
+    SML_HIP_CHECK(hipGetLastError());
+    g_stale_ = false;
+  }
   void GetGradients(std::vector<float>* g, std::vector<float>* h) override {
+    EnsureGH();
     g->resize(static_cast<size_t>(n_) * K_); h->resize(g->size());
     SML_HIP_CHECK(hipMemcpyAsync(g->data(), g_.get(), sizeof(float) * g->size(), hipMemcpyDeviceToHost, stream_));
     SML_HIP_CHECK(hipMemcpyAsync(h->data(), h_.get(), sizeof(float) * h->size(), hipMemcpyDeviceToHost, stream_));
@@ -4298,6 +3969,8 @@ class GpuBackend : public TrainBackend {
 
   bool SampleRows(const RowSampleSpec& spec) override {
     if (spec.kind != kSampleBagging && spec.kind != kSampleGoss) return false;
+    EnsureGH();
+    gh2_valid_ = false;  // GOSS rescales g_ / h_
     roctxRangePushA("sml::SampleRows");
     bag_.alloc(static_cast<size_t>(std::max<int64_t>(1, n_)));
     sel_.alloc(1);
@@ -4430,6 +4103,8 @@ class GpuBackend : public TrainBackend {
     const float* g = g_.get() + static_cast<size_t>(k) * n_;
     const float* h = h_.get() + static_cast<size_t>(k) * n_;
     const bool root_prepared = root_ready_ && bag_n_ < 0 && k == 0;
+    const bool idx = idx_ok_ && batch_ok_ && sp_.bynode_k <= 0 && !voting_ && bag_n_ < 0 && k == 0;
+    if (!idx || !root_prepared) EnsureGH();  // the physical g / h are read below
     root_ready_ = false;
     int32_t root_count = static_cast<int32_t>(n_);
     int root_buf = -1;
@@ -4465,7 +4140,12 @@ class GpuBackend : public TrainBackend {
     }
     EnqueueFindChoose(false);
     if (batch_ok_ && sp_.bynode_k <= 0 && !voting_) {
-      GrowBatched(g, h, lid_ok_ && bag_n_ < 0);
+      if (idx && !gh2_valid_) {
+        hipLaunchKernelGGL(pack_gh_kernel, dim3(GridFor(n_)), dim3(256), 0, stream_, g, h, n_, gh2_.get());
+        SML_HIP_CHECK(hipGetLastError());
+        gh2_valid_ = true;
+      }
+      GrowBatched(g, h, idx);
       final_v_ = 0;
       SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
       return;
@@ -4497,7 +4177,7 @@ class GpuBackend : public TrainBackend {
   // Rounds of the batched speculative growth (see bplan_kernel). The host stays blook_ rounds ahead: before
   // enqueueing round r it waits for the plan of round r - blook_ and stops once a plan reported the tree
   // final (the rounds already queued behind it are no-ops).
-  void GrowBatched(const float* g, const float* h, bool lid) {
+  void GrowBatched(const float* g, const float* h, bool idx) {
     TraceRange tr("sml::GrowBatched");
     const int budget = L_ - 1;
     const float* ghmax = reinterpret_cast<const float*>(ghmax_.get());
@@ -4510,10 +4190,12 @@ class GpuBackend : public TrainBackend {
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup, true>)
                                              : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true>
                                                        : bhist_kernel<kHistUnroll, kFeatPerGroup>)));
-    // leaf-id partition: the smaller children's rows come from the list (perm_[0]), g / h gathered by row id
-    auto bhl = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16, false, false, true>
+    // index-only partition: row ids in the segments, (g, h) gathered from gh2_
+    auto bhi = hist_fpg_ == 16 ? bhist_kernel<kHistUnroll, 16, false, false, true>
                                : (tight_ ? bhist_kernel<kHistUnroll, kFeatPerGroup, false, true, true>
                                          : bhist_kernel<kHistUnroll, kFeatPerGroup, false, false, true>);
+    auto bpi = part_rows_ == 16 ? bpart_kernel<16, true> : (part_rows_ == 4 ? bpart_kernel<4, true> : bpart_kernel<8, true>);
+    const float* hg = idx ? reinterpret_cast<const float*>(gh2_.get()) : g;
     if (bprof_) SML_HIP_CHECK(hipMemsetAsync(bprof_, 0, sizeof(long long) * kPlanProfStride * (max_rounds + 1), stream_));
     int r = 0;
     for (; r <= max_rounds; ++r) {
@@ -4532,26 +4214,13 @@ class GpuBackend : public TrainBackend {
                          bprof_ ? bprof_ + kPlanProfStride * r : nullptr);
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(bev_[r % kBRing], stream_));
-      if (lid) {
-        auto lk = lid_wide_ ? (spec_k_ <= 4 ? bpart_lid_kernel<uint16_t, 1> : (spec_k_ <= 8 ? bpart_lid_kernel<uint16_t, 2>
-                                                                                           : bpart_lid_kernel<uint16_t, 4>))
-                            : (spec_k_ <= 4 ? bpart_lid_kernel<uint8_t, 1> : (spec_k_ <= 8 ? bpart_lid_kernel<uint8_t, 2>
-                                                                                          : bpart_lid_kernel<uint8_t, 4>));
-        hipLaunchKernelGGL(lk, dim3(lid_g_), dim3(kLidThreads), 0, stream_, bstate_.get(), lid_.get(), cbins_.get(),
-                           static_cast<int32_t>(n_), lid_chunk_, lid_list_.get(), lid_stride_, lid_cnt_.get(),
-                           r == 0 ? 1 : 0);
-        SML_HIP_CHECK(hipGetLastError());
-      } else {
-        hipLaunchKernelGGL(bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
-                           perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), perm_[0].get(), perm_[1].get(),
-                           ogh_[0].get(), ogh_[1].get(), g, h);
-        SML_HIP_CHECK(hipGetLastError());
-      }
-      hipLaunchKernelGGL(lid ? bhl : bh, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_,
-                         bstate_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_,
-                         lid ? lid_list_.get() : perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), g, h, ghmax,
-                         slab_.get(), scale_n_, bstate_.get(), lid ? lid_cnt_.get() : nullptr, lid_g_, lid_chunk_,
-                         lid_stride_);
+      hipLaunchKernelGGL(idx ? bpi : bp, dim3(part_grid_), dim3(kPartThreads), 0, stream_, bstate_.get(), cbins_.get(), n_,
+                         perm_[0].get(), perm_[1].get(), ogh_[0].get(), ogh_[1].get(), perm_[0].get(), perm_[1].get(),
+                         ogh_[0].get(), ogh_[1].get(), g, h);
+      SML_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(idx ? bhi : bh, dim3(kMaxHistBlocks, (F_ + hist_fpg_ - 1) / hist_fpg_), dim3(kHistBlockThreads), 0, stream_,
+                         bstate_.get(), reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, perm_[0].get(),
+                         perm_[1].get(), ogh_[0].get(), ogh_[1].get(), hg, h, ghmax, slab_.get(), scale_n_);
       SML_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL(breduce_kernel, dim3((E_ + kRedE - 1) / kRedE, spec_k_), dim3(kRedE * kRedG), 0, stream_,
                          bstate_.get(), slab_.get(), E_, ghmax, part_.get(), scale_n_, Distributed() ? 1 : 0);
@@ -4690,13 +4359,21 @@ class GpuBackend : public TrainBackend {
   // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
   void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
     if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    auto sgk = root_pipe_ ? score_grad_hist_kernel<kHistUnroll, true>
-                          : (tight_ ? score_grad_hist_kernel<kHistUnroll, false, true> : score_grad_hist_kernel<kHistUnroll>);
+    // index-only partition: the pass writes the interleaved (g, h) copy instead of g_ / h_ (same bytes)
+    const bool gh2 = idx_ok_ && batch_ok_;
+    auto sgk = gh2 ? (root_pipe_ ? score_grad_hist_kernel<kHistUnroll, true, false, true>
+                                 : (tight_ ? score_grad_hist_kernel<kHistUnroll, false, true, true>
+                                           : score_grad_hist_kernel<kHistUnroll, false, false, true>))
+                   : (root_pipe_ ? score_grad_hist_kernel<kHistUnroll, true>
+                                 : (tight_ ? score_grad_hist_kernel<kHistUnroll, false, true> : score_grad_hist_kernel<kHistUnroll>));
     hipLaunchKernelGGL(sgk, dim3(kMaxHistBlocks), dim3(kHistBlockThreads), 0, stream_, tv, src,
                        reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, static_cast<int32_t>(n_), scale,
-                       score_.get(), prep_params_, label_.get(), weight_.get(), g_.get(), h_.get(),
+                       score_.get(), prep_params_, label_.get(), weight_.get(),
+                       gh2 ? reinterpret_cast<float*>(gh2_.get()) : g_.get(), h_.get(),
                        reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get(), scale_n_);
     SML_HIP_CHECK(hipGetLastError());
+    gh2_valid_ = gh2;
+    g_stale_ = gh2;
     if (src.st) {
       SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
       score_pending_ = true;
@@ -5168,14 +4845,12 @@ class GpuBackend : public TrainBackend {
   int* bflag_host_ = nullptr;
   int* bflag_dev_ = nullptr;
   int plan_cap_ = 0;            // node records allocated for the batched growth (the plan stages them all)
-  // leaf-id partition (bpart_lid_kernel): node id per row, 1 B when the node table fits 256 ids, else 2 B
-  bool lid_ok_ = false;
-  bool lid_wide_ = false;
-  int lid_chunk_ = 0, lid_g_ = 0;  // rows per partition block, blocks (= runs per expansion)
-  int64_t lid_stride_ = 0;         // list entries per expansion slot (G x chunk)
-  DevBuf<uint8_t> lid_;
-  DevBuf<int32_t> lid_list_;
-  DevBuf<unsigned long long> lid_cnt_;
+  // index-only partition: interleaved (g, h) of class 0; gh2_valid_: it holds the current gradients; g_stale_:
+  // g_ / h_ do not (the fused pass wrote only gh2_) - EnsureGH unpacks before anything reads them
+  bool idx_ok_ = false;
+  bool gh2_valid_ = false;
+  bool g_stale_ = false;
+  DevBuf<float2> gh2_;
   long long* bprof_ = nullptr;  // SML_BPLAN_PROF phase stamps, kPlanProfStride per round
   double bprof_sum_[6] = {0, 0, 0, 0, 0, 0};
   double bprof_tree_[4] = {0, 0, 0, 0};  // rows partitioned, of them in never-popped nodes; expansions, wasted

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -110,11 +111,14 @@ class RcclComm : public Comm {
       throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r) + " (ncclCommInitRankConfig)");
     }
     Settle(r, "ncclCommInitRankConfig");
-    SML_HIP_CHECK(hipMalloc(&scratch_, 64));
+    SML_HIP_CHECK(hipStreamCreateWithFlags(&host_stream_, hipStreamNonBlocking));
   }
   ~RcclComm() override {
     if (comm_) ncclCommDestroy(comm_);  // (null after an abort)
+    if (host_stream_) (void)hipStreamSynchronize(host_stream_);
     if (scratch_) (void)hipFree(scratch_);
+    if (pinned_) (void)hipHostFree(pinned_);
+    if (host_stream_) (void)hipStreamDestroy(host_stream_);
   }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
@@ -122,15 +126,9 @@ class RcclComm : public Comm {
   // (a world-1 communicator still runs every collective: that is how the one-GPU tests execute this path)
   void AllReduceHost(double* buf, int64_t n) override {
     TraceRange tr("sml::AllReduceHost");
-    // small host reductions (root sums, init scores): stage through the device
-    if (!comm_) throw CommError("RCCL communicator was aborted");
-    double* d = nullptr;
-    SML_HIP_CHECK(hipMalloc(&d, sizeof(double) * n));
-    SML_HIP_CHECK(hipMemcpy(d, buf, sizeof(double) * n, hipMemcpyHostToDevice));
-    Settle(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm_, nullptr), "ncclAllReduce");
-    SML_HIP_CHECK(hipStreamSynchronize(nullptr));
-    SML_HIP_CHECK(hipMemcpy(buf, d, sizeof(double) * n, hipMemcpyDeviceToHost));
-    SML_HIP_CHECK(hipFree(d));
+    // small host reductions (root sums, init scores): staged through a persistent device scratch and pinned
+    // buffer on the communicator's own stream (no per-call allocation, no device-wide null-stream sync)
+    HostReduce(buf, n, ncclDouble);
   }
   void AllReduceDeviceF32(float* buf, int64_t n, void* stream) override {
     if (!comm_) throw CommError("RCCL communicator was aborted");
@@ -160,18 +158,34 @@ class RcclComm : public Comm {
     if (!comm_) throw CommError("RCCL communicator was aborted");
     Settle(ncclAllReduce(buf, buf, n, ncclInt64, ncclSum, comm_, static_cast<hipStream_t>(stream)), "ncclAllReduce");
   }
-  void AllReduceHostI64(int64_t* buf, int64_t n) override {
-    if (!comm_) throw CommError("RCCL communicator was aborted");
-    int64_t* d = nullptr;
-    SML_HIP_CHECK(hipMalloc(&d, sizeof(int64_t) * n));
-    SML_HIP_CHECK(hipMemcpy(d, buf, sizeof(int64_t) * n, hipMemcpyHostToDevice));
-    Settle(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm_, nullptr), "ncclAllReduce");
-    SML_HIP_CHECK(hipStreamSynchronize(nullptr));
-    SML_HIP_CHECK(hipMemcpy(buf, d, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
-    SML_HIP_CHECK(hipFree(d));
-  }
+  void AllReduceHostI64(int64_t* buf, int64_t n) override { HostReduce(buf, n, ncclInt64); }
 
  private:
+  // host array -> pinned -> device scratch -> allreduce -> back, all on host_stream_ (8-byte elements)
+  void HostReduce(void* buf, int64_t n, ncclDataType_t type) {
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    if (n <= 0) return;
+    const size_t bytes = sizeof(double) * static_cast<size_t>(n);
+    if (bytes > cap_) {
+      size_t c = std::max<size_t>(4096, cap_);
+      while (c < bytes) c *= 2;
+      if (scratch_) SML_HIP_CHECK(hipFree(scratch_));
+      if (pinned_) SML_HIP_CHECK(hipHostFree(pinned_));
+      scratch_ = nullptr;
+      pinned_ = nullptr;
+      cap_ = 0;
+      SML_HIP_CHECK(hipMalloc(&scratch_, c));
+      SML_HIP_CHECK(hipHostMalloc(&pinned_, c, hipHostMallocDefault));
+      cap_ = c;
+    }
+    std::memcpy(pinned_, buf, bytes);
+    SML_HIP_CHECK(hipMemcpyAsync(scratch_, pinned_, bytes, hipMemcpyHostToDevice, host_stream_));
+    Settle(ncclAllReduce(scratch_, scratch_, n, type, ncclSum, comm_, host_stream_), "ncclAllReduce");
+    SML_HIP_CHECK(hipMemcpyAsync(pinned_, scratch_, bytes, hipMemcpyDeviceToHost, host_stream_));
+    SML_HIP_CHECK(hipStreamSynchronize(host_stream_));
+    std::memcpy(buf, pinned_, bytes);
+  }
+
   // Non-blocking communicators may answer ncclInProgress (init, and the lazy peer connection of a first
   // collective); the next call on the communicator must wait until the state settles. Bounded by the
   // timeout: past it the communicator is aborted and the call fails with CommError.
@@ -199,7 +213,10 @@ class RcclComm : public Comm {
   int rank_, world_;
   double timeout_ms_;
   ncclComm_t comm_ = nullptr;
-  void* scratch_ = nullptr;
+  hipStream_t host_stream_ = nullptr;  // the host-array reductions' stream
+  void* scratch_ = nullptr;            // their device scratch and pinned staging (cap_ bytes each, grow-only)
+  void* pinned_ = nullptr;
+  size_t cap_ = 0;
 };
 
 }  // namespace

@@ -294,8 +294,10 @@ double Objective::BoostFromScore(int class_id, Comm* comm) const {
     case kObjL1:
     case kObjQuantile:
     case kObjMape: {
-      // a weighted percentile of the local rows; over ranks the row-count-weighted mean of them (as LightGBM's
-      // distributed L1 / quantile start: an approximation of the global percentile)
+      // a weighted percentile of the local rows; over ranks the unweighted mean of the per-rank percentiles - the
+      // form of LightGBM's GlobalSyncUpByMean for its distributed L1 / quantile / MAPE start (not a global
+      // percentile). Deliberate difference: a rank without rows has no percentile and is left out of the mean.
+      // (The reference ships no LightGBM source: this form is unpinned against it.)
       std::vector<std::pair<double, double>> v(n);
       if (p_.kind == kObjMape)
         for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i) / std::max(1.0, std::fabs(static_cast<double>(label_[i])))};
@@ -303,7 +305,7 @@ double Objective::BoostFromScore(int class_id, Comm* comm) const {
         for (int64_t i = 0; i < n; ++i) v[i] = {label_[i], W(i)};
       double r = WeightedPercentile(std::move(v), p_.kind == kObjQuantile ? p_.alpha : 0.5);
       if (comm && comm->world() > 1) {
-        double buf[2] = {r * n, static_cast<double>(n)};
+        double buf[2] = {n > 0 ? r : 0.0, n > 0 ? 1.0 : 0.0};
         comm->AllReduceHost(buf, 2);
         r = buf[1] > 0 ? buf[0] / buf[1] : 0.0;
       }

@@ -1390,6 +1390,9 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
     }
   });
   try {
+    // launches follow the unchunked boundary sequence (the warm-up's 1, 1, 2, 4, ... then `batch`): one that runs
+    // past the chunk that has landed waits for the next chunk instead of being cut at the chunk boundary
+    int64_t lb0 = 0;
     for (int64_t c = 0; c < nchunks; ++c) {
       {
         std::unique_lock<std::mutex> g(rmu);
@@ -1397,10 +1400,12 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
         if (!upload_error.empty()) break;
       }
       VW_HIP_CHECK(hipStreamWaitEvent(s, impl_->events[c], 0));
-      const int64_t r0 = c * chunk_rows, r1 = std::min<int64_t>(n, r0 + chunk_rows);
-      for (int64_t b0 = r0, b1; b0 < r1; b0 = b1) {
-        b1 = NextLaunch(b0, 0, r1, batch);
-        Launch(b0, b1, true, weights != nullptr);
+      const int64_t r1 = std::min<int64_t>(n, (c + 1) * chunk_rows);
+      while (lb0 < r1) {
+        const int64_t b1 = NextLaunch(lb0, 0, n, batch);
+        if (b1 > r1) break;
+        Launch(lb0, b1, true, weights != nullptr);
+        lb0 = b1;
       }
     }
   } catch (...) {
@@ -1548,7 +1553,8 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
   std::vector<Bulk> bulk;
   const int64_t lr1 = std::min<int64_t>(std::max<int64_t>(0, learn_r1), n);
   batch = std::max(1, batch);
-  // whole batches per chunk (the launches match the unchunked LearnStaged's), >= 64k rows
+  // whole batches per chunk, >= 64k rows; the launches follow the unchunked LearnStaged's boundaries (a launch
+  // that straddles a chunk boundary runs once the next chunk is expanded)
   // (SML_VW_STAGE_CHUNK_ROWS: another floor, read per call - the tests cut a small pass into many chunks)
   const char* ce = std::getenv("SML_VW_STAGE_CHUNK_ROWS");
   const int64_t floor_rows = ce && std::atoll(ce) > 0 ? std::atoll(ce) : 65536;
@@ -1656,6 +1662,7 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
       VW_HIP_CHECK(hipStreamSynchronize(s));
       impl_->Reserve(std::max<int64_t>(1, n), static_cast<size_t>(nnz));
       if (lr1 > 0) PrepLearn(0, lr1);
+      int64_t lb0 = 0;
       for (int64_t c = 0; c < nchunks; ++c) {
         {
           std::unique_lock<std::mutex> g(rmu);
@@ -1668,9 +1675,11 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
         hipLaunchKernelGGL(expand_fill_kernel, dim3(grid), dim3(64 * kExpandWaves), 0, s, impl_->spec, r0, r1,
                            impl_->indptr, impl_->idx, impl_->val);
         VW_HIP_CHECK(hipGetLastError());
-        for (int64_t b0 = r0, b1; b0 < std::min(r1, lr1); b0 = b1) {
-          b1 = NextLaunch(b0, 0, std::min(r1, lr1), batch);
-          Launch(b0, b1, true, staged_weights_);
+        while (lb0 < std::min(r1, lr1)) {
+          const int64_t b1 = NextLaunch(lb0, 0, lr1, batch);
+          if (b1 > r1) break;
+          Launch(lb0, b1, true, staged_weights_);
+          lb0 = b1;
         }
       }
     } catch (...) {

@@ -331,6 +331,7 @@ def _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, tim
 
     deadline = _time.monotonic() + timeout_s
     failed = None
+    timed_out = False
     while any(p.is_alive() for p in procs):
         for r, p in enumerate(procs):
             if p.is_alive():
@@ -345,7 +346,10 @@ def _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, tim
                     failed = failed or (r, "netinit")
                 elif st != "ok":
                     failed = failed or (r, "task error")
-        if (failed and (fail_fast or failed[1] == "netinit")) or _time.monotonic() > deadline:
+        if failed and (fail_fast or failed[1] == "netinit"):
+            break
+        if _time.monotonic() > deadline:
+            timed_out = True
             break
         _time.sleep(0.05)
     for p in procs:
@@ -355,6 +359,9 @@ def _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, tim
             if p.is_alive():
                 p.kill()
                 p.join()
+    if timed_out and failed is None:
+        # the ranks still running at the deadline were terminated (exit code -15): a timeout, not a task failure
+        raise TimeoutError(f"partition tasks did not finish within {timeout_s}s")
     if failed is None:
         # every worker had exited by the last poll: a crash after its result file (or a missing file) is a failure
         for r, p in enumerate(procs):
@@ -387,8 +394,6 @@ def _run_procs(ctx, fn_bytes, descs, world, port, backend, use_gpu, attempt, tim
             if st != "ok":
                 why = val
         raise RuntimeError(f"worker {r} failed ({why}); the job was aborted on the remaining ranks")
-    if _time.monotonic() > deadline:
-        raise TimeoutError(f"partition tasks did not finish within {timeout_s}s")
     results = []
     for r in range(world):
         path = os.path.join(d, f"result_{r}.pkl")

@@ -173,3 +173,11 @@ def test_no_resource_tracker_tracebacks():
     p = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "KeyError" not in p.stderr and "leaked shared_memory" not in p.stderr, p.stderr[-2000:]
+
+
+def test_spawned_run_partitions_times_out_as_timeout():
+    """ranks still running at the deadline are terminated (exit code -15); that is reported as a
+    TimeoutError, not as a worker failure."""
+    df = DataFrame({"x": np.arange(4.0)}, num_partitions=2)
+    with pytest.raises(TimeoutError):
+        R.run_partitions(_sleep_task, df, num_workers=2, timeout_s=3.0)

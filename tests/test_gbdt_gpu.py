@@ -703,25 +703,27 @@ def test_gpu_batched_growth_equals_sequential(extra, spec, monkeypatch):
 
 @pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5",
                                    "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
-                                   "num_leaves=31 objective=multiclass num_class=3"])
-@pytest.mark.parametrize("spec", ["4", "8", "16"])
-def test_gpu_leaf_id_partition_equals_sequential(extra, spec, monkeypatch):
-    """SML_GBDT_LID=1: the batched growth on the leaf-id partition (bpart_lid_kernel: node ids per row, per-block
-    runs of the smaller children, bhist over the runs) grows the byte-identical model of one-split growth - 1-byte
-    and 2-byte ids, 1 / 2 / 4 counter words, categorical splits, an n that is not a multiple of 16 (byte-gather
-    path) and one that is (16-B window path)."""
-    for n in (80000, 80003):
-        X, y = _data(n=n, nan_frac=0.02, cat="categorical" in extra)
-        if "multiclass" in extra:
-            y = (np.digitize(np.nan_to_num(X[:, 0] + X[:, 1]), [-0.5, 0.5])).astype(np.float32)
-        p = ("objective=binary " if "objective" not in extra else "") + f"learning_rate=0.2 {extra} device_type=gpu"
+                                   "num_leaves=31 objective=cross_entropy", "num_leaves=31 objective=regression"])
+def test_gpu_index_only_partition_equals_ordered_gradients(extra, monkeypatch):
+    """SML_GBDT_IDX=1 (the default): the batched partition moves row ids only and bhist gathers (g, h) from the
+    interleaved copy the fused score / gradient pass writes (or packed once per tree for objectives without the
+    fused pass) - byte-identical models to the ordered-gradient partition (SML_GBDT_IDX=0) and to one-split
+    growth; the host still reads the current gradients (unpacked on demand)."""
+    X, y = _data(n=80000, nan_frac=0.02, cat="categorical" in extra)
+    if "regression" in extra:
+        y = (X[:, 0] + np.nan_to_num(X[:, 1]) * 0.5).astype(np.float32)
+    p = ("objective=binary " if "objective" not in extra else "") + f"learning_rate=0.2 {extra} device_type=gpu"
 
-        def fit(k, lid):
-            monkeypatch.setenv("SML_GBDT_SPEC", k)
-            monkeypatch.setenv("SML_GBDT_LID", lid)
-            return _train(X, y, p, 5).save_model_string()
+    def fit(idx, spec="4"):
+        monkeypatch.setenv("SML_GBDT_IDX", idx)
+        monkeypatch.setenv("SML_GBDT_SPEC", spec)
+        return _train(X, y, p, 6)
 
-        assert fit(spec, "1") == fit("0", "0")
+    b1, b0 = fit("1"), fit("0")
+    assert b1.save_model_string() == b0.save_model_string() == fit("0", "0").save_model_string()
+    (g1, h1), (g0, h0) = b1.gradients(), b0.gradients()
+    np.testing.assert_array_equal(g1, g0)
+    np.testing.assert_array_equal(h1, h0)
 
 
 def test_gpu_single_pass_scoring_float32_rows():

@@ -309,6 +309,25 @@ def test_gpu_fused_stage_learn_equals_stage_then_learn(monkeypatch, args, syncs)
 
 
 @pytest.mark.gpu
+def test_gpu_fused_stage_learn_non_power_of_two_batch(monkeypatch):
+    """after the hogwild warm-up (launches of 1, 1, 2, 4, ... examples) the launch boundaries of a
+    non-power-of-two batch are offset from the chunk boundaries (multiples of the batch); the fused staging
+    now carries a straddling launch into the next chunk instead of cutting it, so both paths launch the same
+    example ranges (batch > 1 is hogwild: models agree to rounding)."""
+    df = _three_ns(n=2500)
+    kw = dict(featuresCol="a", additionalFeatures=["b", "c"], numPasses=2, deviceType="gpu", gpuBatchSize=7)
+    monkeypatch.setenv("SML_VW_STAGE_CHUNK_ROWS", "300")
+    monkeypatch.setenv("SML_VW_STAGE_LEARN", "1")
+    fused = VowpalWabbitRegressor(**kw).fit(df)
+    monkeypatch.setenv("SML_VW_STAGE_LEARN", "0")
+    plain = VowpalWabbitRegressor(**kw).fit(df)
+    pf, pp = fused.transform(df)["prediction"], plain.transform(df)["prediction"]
+    np.testing.assert_allclose(pf, pp, rtol=2e-3, atol=2e-3)
+    assert float(fused.getPerformanceStatistics()["averageLoss"][0]) == pytest.approx(
+        float(plain.getPerformanceStatistics()["averageLoss"][0]), rel=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bits", [12, 22])
 def test_gpu_export_one_scan_regions_match_two_scans(monkeypatch, bits):
     """The model export's one-scan form (per-4096-slot record regions, then a compaction) writes the same
