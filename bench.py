@@ -281,6 +281,11 @@ def main() -> None:
                 "holdout_rows": n_hold,
                 "datagen_s": round(gen_s, 2),
                 "native_comm_ms": native_stats.get("comm_ms"),
+                "native_comm_calls": native_stats.get("comm_calls"),
+                # histogram bytes: the host-side bound (every expansion slot of every round) and what this rank
+                # actually pushed through the device-sized P2P transport (only each round's expansions)
+                "comm_bytes_bound": native_stats.get("comm_bytes_max"),
+                "comm_bytes_pushed": native_stats.get("comm_dev_bytes"),
                 "histogram_accumulation": "int64 fixed point per (feature, bin), exact int64 block reduce -> fp64",
                 "histogram_allreduce": (None if world == 1 else "host (gloo)" if not use_gpu else
                                         "p2p-ipc one-shot" if D.p2p_status.get("active") else

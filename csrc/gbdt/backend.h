@@ -22,6 +22,9 @@ namespace sml {
 struct TrainStats {
   double hist_ms = 0, split_ms = 0, partition_ms = 0, grad_ms = 0, score_ms = 0, comm_ms = 0;
   int64_t comm_calls = 0;  // device histogram allreduces issued
+  int64_t comm_dyn_calls = 0;   // of which sized on the device (only the round's expansions travel)
+  double comm_bytes_max = 0;    // host-side upper bound of the histogram bytes reduced
+  int64_t comm_dev_bytes = 0;   // bytes this rank pushed through the device-driven transport (P2P)
   // device-side (hipEvent) time of whole tree growths and score updates; device memory in use after Init
   double device_tree_ms = 0, device_score_ms = 0, device_mem_mb = 0;
   int64_t trees = 0;

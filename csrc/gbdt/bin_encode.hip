@@ -212,7 +212,8 @@ class Encoder {
 
   // Encode rows already resident in HBM (DeviceRows): one launch over all rows.
   template <class T>
-  void EncodeResident(const T* dev_rows, int64_t nrows, int ncols, uint8_t* dev_out, hipStream_t ks) {
+  void EncodeResident(const T* dev_rows, int64_t nrows, int ncols, uint8_t* dev_out, hipStream_t ks,
+                      bool sync = true) {
     if (nrows <= 0) return;
     const size_t lds = EncodeLds<T>(m_);
     const int64_t words = nrows * (m_.stride / 4);
@@ -220,7 +221,7 @@ class Encoder {
     hipLaunchKernelGGL(encode_kernel<T>, dim3(grid), dim3(kEncThreads), lds, ks, m_, dev_rows, nrows, ncols,
                        reinterpret_cast<uint32_t*>(dev_out));
     SML_HIP_CHECK(hipGetLastError());
-    SML_HIP_CHECK(hipStreamSynchronize(ks));
+    if (sync) SML_HIP_CHECK(hipStreamSynchronize(ks));
   }
 
   Encoder(const Encoder&) = delete;
@@ -333,7 +334,6 @@ void PushDenseDeviceImpl(Dataset* d, const T* rows, int64_t nrows, int num_cols,
 template <class T>
 void PushResidentImpl(Dataset* d, DeviceRows* src, int64_t start) {
   TraceRange tr("sml::EncodeResidentRows");
-  src->Wait();
   const int64_t nrows = src->nrows;
   if (start < 0 || start + nrows > d->num_data) throw std::runtime_error("push_device_rows out of range");
   if (d->row_stride % 4 != 0) throw std::runtime_error("device bin encode needs a 4-byte aligned row stride");
@@ -344,8 +344,34 @@ void PushResidentImpl(Dataset* d, DeviceRows* src, int64_t start) {
     EnsureDeviceBins(d, src->device, ks);
     uint8_t* dst = d->dev->rows + static_cast<size_t>(start) * d->row_stride;
     {
+      // the encode follows the upload: rows already in HBM are encoded at once, the rest chunk by chunk as
+      // their copies land (a device-side wait on each chunk's event), so the bin matrix is ready ~one chunk
+      // after the last byte arrives instead of one whole-matrix encode after the upload (r6)
       Encoder enc(d->ref, d->row_stride);
-      enc.EncodeResident(static_cast<const T*>(src->ptr), nrows, src->ncols, dst, ks);
+      const T* rows = static_cast<const T*>(src->ptr);
+      const size_t row_bytes = static_cast<size_t>(src->ncols) * sizeof(T);
+      int64_t r_done = 0;
+      for (size_t c = 0;; ++c) {
+        hipEvent_t e = nullptr;
+        size_t end = 0;
+        {
+          std::unique_lock<std::mutex> lk(src->mu);
+          src->cv.wait(lk, [&] { return src->chunk_ev.size() > c || src->finished; });
+          if (src->chunk_ev.size() <= c) break;
+          e = static_cast<hipEvent_t>(src->chunk_ev[c]);
+          end = src->chunk_end[c];
+        }
+        const int64_t r_end = std::min<int64_t>(nrows, static_cast<int64_t>(end / row_bytes));
+        if (r_end <= r_done) continue;
+        SML_HIP_CHECK(hipStreamWaitEvent(ks, e, 0));
+        enc.EncodeResident(rows + r_done * src->ncols, r_end - r_done, src->ncols, dst + r_done * d->row_stride, ks,
+                           false);
+        r_done = r_end;
+      }
+      src->Wait();  // the copy thread is done (raises if it failed)
+      enc.EncodeResident(rows + r_done * src->ncols, nrows - r_done, src->ncols, dst + r_done * d->row_stride, ks,
+                         false);
+      SML_HIP_CHECK(hipStreamSynchronize(ks));
     }
     if (d->host_valid)
       SML_HIP_CHECK(hipMemcpy(d->bins.data() + static_cast<size_t>(start) * d->row_stride, dst,
@@ -403,7 +429,7 @@ void ParallelCopy(char* dst, const char* src, size_t bytes, int threads) {
 }
 }  // namespace
 
-void UploadPinned(const char* host, char* dev, size_t bytes) {
+void UploadPinned(const char* host, char* dev, size_t bytes, DeviceRows* progress) {
   TraceRange tr("sml::UploadPinned");
   StagePool& sp = Stage();
   std::lock_guard<std::mutex> lk(sp.mu);  // one pinned pipeline at a time per process
@@ -424,6 +450,15 @@ void UploadPinned(const char* host, char* dev, size_t bytes) {
       SML_HIP_CHECK(hipMemcpyAsync(dev + off, sp.buf[k], n, hipMemcpyHostToDevice, s));
       SML_HIP_CHECK(hipEventRecord(ev[k], s));
       used[k] = true;
+      if (progress) {  // the encode may start on these rows as soon as this copy lands
+        hipEvent_t ce = nullptr;
+        SML_HIP_CHECK(hipEventCreateWithFlags(&ce, hipEventDisableTiming));
+        SML_HIP_CHECK(hipEventRecord(ce, s));
+        std::lock_guard<std::mutex> g(progress->mu);
+        progress->chunk_ev.push_back(ce);
+        progress->chunk_end.push_back(off + n);
+        progress->cv.notify_all();
+      }
     }
     SML_HIP_CHECK(hipStreamSynchronize(s));
   } catch (...) {
@@ -448,10 +483,13 @@ DeviceRows::DeviceRows(const void* host, int64_t nrows_, int ncols_, int elem_by
   worker = std::thread([this, host, bytes]() {
     try {
       SML_HIP_CHECK(hipSetDevice(device));
-      UploadPinned(static_cast<const char*>(host), static_cast<char*>(ptr), bytes);
+      UploadPinned(static_cast<const char*>(host), static_cast<char*>(ptr), bytes, this);
     } catch (const std::exception& e) {
       error = e.what();
     }
+    std::lock_guard<std::mutex> g(mu);
+    finished = true;
+    cv.notify_all();
   });
 }
 
@@ -462,6 +500,7 @@ void DeviceRows::Wait() {
 
 DeviceRows::~DeviceRows() {
   if (worker.joinable()) worker.join();
+  for (void* e : chunk_ev) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
   if (ptr) DevPoolFree(ptr, granted);
 }
 

@@ -370,6 +370,8 @@ PYBIND11_MODULE(_gbdt, m) {
         if (s) {
           d["grad_ms"] = s->grad_ms; d["hist_ms"] = s->hist_ms; d["split_ms"] = s->split_ms;
           d["partition_ms"] = s->partition_ms; d["score_ms"] = s->score_ms; d["comm_ms"] = s->comm_ms; d["comm_calls"] = s->comm_calls;
+          d["comm_dyn_calls"] = s->comm_dyn_calls; d["comm_bytes_max"] = s->comm_bytes_max;
+          d["comm_dev_bytes"] = s->comm_dev_bytes;
           d["trees"] = s->trees;
           d["device_tree_ms"] = s->device_tree_ms; d["device_score_ms"] = s->device_score_ms;
           d["device_mem_mb"] = s->device_mem_mb;

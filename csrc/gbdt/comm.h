@@ -36,6 +36,18 @@ class Comm {
   // N-rank histogram is bitwise the 1-rank histogram of the union of the partitions
   virtual void AllReduceHostI64(int64_t* buf, int64_t n) = 0;
   virtual void AllReduceDeviceI64(int64_t* buf, int64_t n, void* stream) = 0;
+  // the same over the first min(n_max, *units * per_unit) elements, `units` a device int the preceding kernels
+  // wrote (the batched growth's expansion count): a device-driven transport moves only those; the default
+  // (host-sized collectives) reduces all n_max. Returns true if the size was applied on the device.
+  virtual bool AllReduceDeviceI64Active(int64_t* buf, int64_t n_max, const int32_t* units, int64_t per_unit,
+                                        void* stream) {
+    (void)units;
+    (void)per_unit;
+    AllReduceDeviceI64(buf, n_max, stream);
+    return false;
+  }
+  // bytes this rank moved through a device-driven transport so far (0 if it does not count)
+  virtual int64_t DeviceBytes() const { return 0; }
   // element-wise max over ranks of a small HOST buffer, built on the sum: every rank contributes its values in
   // its own slot of a world-sized buffer (exact - the other slots are zeros) and takes the max locally
   void AllReduceHostMax(double* buf, int64_t n) {

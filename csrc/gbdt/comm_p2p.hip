@@ -60,12 +60,18 @@ struct VecOf {
   T v[VW];
 };
 
+// units != nullptr: only the first min(n, *units * per_unit) elements travel (every block still signals, so the
+// epochs stay in step); bytes (when set) counts what this rank pushed
 template <class T, int VW>
 __global__ __launch_bounds__(kP2pThreads) void p2p_allreduce_kernel(PeerPtrs peers, const T* in, T* out, int64_t n,
                                                                     int64_t chunk, int64_t cap_bytes, int rank,
                                                                     int world, uint32_t epoch, long long timeout_ticks,
-                                                                    int* err) {
+                                                                    int* err, const int32_t* units, int64_t per_unit,
+                                                                    unsigned long long* bytes) {
   using V = VecOf<T, VW>;
+  if (units) n = min(n, static_cast<int64_t>(max(0, *units)) * per_unit);
+  if (bytes && blockIdx.x == 0 && threadIdx.x == 0)
+    atomicAdd(bytes, static_cast<unsigned long long>(n) * sizeof(T) * static_cast<unsigned long long>(world - 1));
   const int b = blockIdx.x;
   const int64_t lo = static_cast<int64_t>(b) * chunk;  // chunk is a multiple of VW
   const int64_t hi = min(n, lo + chunk);
@@ -173,6 +179,18 @@ class P2pComm : public Comm {
     if (!Use(n * 8)) return base_->AllReduceDeviceI64(buf, n, stream);
     Launch(reinterpret_cast<long long*>(buf), n, static_cast<hipStream_t>(stream));
   }
+  bool AllReduceDeviceI64Active(int64_t* buf, int64_t n_max, const int32_t* units, int64_t per_unit,
+                                void* stream) override {
+    if (!Use(n_max * 8)) return base_->AllReduceDeviceI64Active(buf, n_max, units, per_unit, stream);
+    Launch(reinterpret_cast<long long*>(buf), n_max, static_cast<hipStream_t>(stream), units, per_unit);
+    return true;
+  }
+  // (a blocking read of the device counter: stats time only)
+  int64_t DeviceBytes() const override {
+    unsigned long long v = 0;
+    if (bytes_) SML_HIP_CHECK(hipMemcpy(&v, bytes_, sizeof(v), hipMemcpyDeviceToHost));
+    return static_cast<int64_t>(v);
+  }
   void AllReduceDeviceF32(float* buf, int64_t n, void* stream) override {
     if (!Use(n * 4)) return base_->AllReduceDeviceF32(buf, n, stream);
     Launch(buf, n, static_cast<hipStream_t>(stream));
@@ -193,7 +211,7 @@ class P2pComm : public Comm {
   bool Use(int64_t bytes) const { return active_ && world_ > 1 && bytes <= cap_; }
 
   template <class T>
-  void Launch(T* buf, int64_t n, hipStream_t s) {
+  void Launch(T* buf, int64_t n, hipStream_t s, const int32_t* units = nullptr, int64_t per_unit = 0) {
     if (n <= 0) return;
     constexpr int VW = 16 / sizeof(T);
     const bool vec = reinterpret_cast<uintptr_t>(buf) % 16 == 0;
@@ -204,10 +222,10 @@ class P2pComm : public Comm {
     ++epoch_;
     if (vec)
       hipLaunchKernelGGL((p2p_allreduce_kernel<T, VW>), dim3(blocks), dim3(kP2pThreads), 0, s, peers_, buf, buf, n,
-                         chunk, cap_, rank_, world_, epoch_, timeout_ticks_, err_);
+                         chunk, cap_, rank_, world_, epoch_, timeout_ticks_, err_, units, per_unit, bytes_);
     else
       hipLaunchKernelGGL((p2p_allreduce_kernel<T, 1>), dim3(blocks), dim3(kP2pThreads), 0, s, peers_, buf, buf, n,
-                         chunk, cap_, rank_, world_, epoch_, timeout_ticks_, err_);
+                         chunk, cap_, rank_, world_, epoch_, timeout_ticks_, err_, units, per_unit, bytes_);
     SML_HIP_CHECK(hipGetLastError());
   }
 
@@ -236,6 +254,8 @@ class P2pComm : public Comm {
     SML_HIP_CHECK(hipMemset(sig_, 0, sig_bytes));
     SML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), sizeof(int), hipHostMallocCoherent));
     *err_ = 0;
+    SML_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&bytes_), sizeof(unsigned long long)));
+    SML_HIP_CHECK(hipMemset(bytes_, 0, sizeof(unsigned long long)));
     SML_HIP_CHECK(hipDeviceSynchronize());
     hipIpcMemHandle_t h[2];
     SML_HIP_CHECK(hipIpcGetMemHandle(&h[0], recv_));
@@ -302,6 +322,8 @@ class P2pComm : public Comm {
     if (recv_) (void)hipFree(recv_);
     if (sig_) (void)hipFree(sig_);
     if (err_) (void)hipHostFree(err_);
+    if (bytes_) (void)hipFree(bytes_);
+    bytes_ = nullptr;
     recv_ = nullptr;
     sig_ = nullptr;
     err_ = nullptr;
@@ -316,6 +338,7 @@ class P2pComm : public Comm {
   char* recv_ = nullptr;
   uint32_t* sig_ = nullptr;
   int* err_ = nullptr;
+  unsigned long long* bytes_ = nullptr;  // pushed bytes (device memory, bumped by the kernels' block 0)
   uint32_t epoch_ = 0;
   PeerPtrs peers_{};
   std::vector<void*> opened_;

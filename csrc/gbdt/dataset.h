@@ -11,6 +11,7 @@
 #pragma once
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
 #include <limits>
 #include <memory>
@@ -188,10 +189,18 @@ struct DeviceRows {
   size_t granted = 0;
   std::thread worker;
   std::string error;
+  // upload progress, for an encode that follows the copy chunk by chunk: chunk_ev[i] (a hipEvent_t) completes
+  // when the first chunk_end[i] bytes are in HBM; `finished` once no more chunks come (done or failed)
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<void*> chunk_ev;
+  std::vector<size_t> chunk_end;
+  bool finished = false;
 };
 void DatasetPushDeviceRows(Dataset* d, DeviceRows* src, int64_t start);
 // host (pageable) -> device copy through pinned staging buffers filled by parallel CPU threads (bin_encode.hip)
-void UploadPinned(const char* host, char* dev, size_t bytes);
+// `progress`: optional - each chunk's completion event is published there as the copy is queued
+void UploadPinned(const char* host, char* dev, size_t bytes, DeviceRows* progress = nullptr);
 
 // device -> host copy of a device-resident bin matrix (bin_encode.hip)
 void DatasetDownloadBins(const Dataset& d, uint8_t* host);

@@ -221,8 +221,12 @@ __device__ UpdPrep UpdateFirstPass(const SgdArgs& a, int64_t b, int64_t en, uint
     if (a.adaptive) G = atomicAdd(&w->y, grad_sq * x2) + grad_sq * x2;
     if (a.normalized) {
       const float ax = fabsf(x);
-      // N only grows: the float bits of non-negative values order like unsigned integers
-      const float old = __uint_as_float(atomicMax(reinterpret_cast<unsigned int*>(&w->z), __float_as_uint(ax)));
+      // N only grows: the float bits of non-negative values order like unsigned integers. A plain load first:
+      // once a slot's N covers |x| (the steady state: every later example of the slot) the atomicMax would be a
+      // no-op, so it is issued only when this update may raise N - one returning atomic fewer per feature on the
+      // hot slots (identical at batch 1; under hogwild N is read as of the load instead of the atomic)
+      float old = w->z;
+      if (ax > old) old = __uint_as_float(atomicMax(reinterpret_cast<unsigned int*>(&w->z), __float_as_uint(ax)));
       if (ax > old && old > 0.f) {
         const float r = old / ax;
         w->x *= a.adaptive ? r : r * r;  // hogwild rescale of this slot's weight
@@ -297,7 +301,10 @@ __device__ float UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint6
     } else {
       atomicAdd(&w->x, update * x * rate);  // result unused: a non-returning atomic
     }
-    a.dirty[h >> kDirtyShift] = 1;
+    // the touched-block flag: written only when still clear (most updates hit blocks already marked; a plain
+    // byte load instead of a store that takes the line from the other XCDs' caches)
+    uint8_t* dflag = a.dirty + (h >> kDirtyShift);
+    if (*dflag == 0) *dflag = 1;
   }
   return update;
 }

@@ -107,12 +107,19 @@ def _parallel_copy(dst_views, srcs) -> None:
             d[...] = a
         return
     if _COPY_POOL is None:
-        _COPY_POOL = ThreadPoolExecutor(max_workers=8)
+        _COPY_POOL = ThreadPoolExecutor(max_workers=16)
 
     def put(k):
         dst_views[k][...] = srcs[k]
 
     list(_COPY_POOL.map(put, range(len(srcs))))
+
+
+def _bulk_copy(host: np.ndarray, n: int) -> np.ndarray:
+    """The first n images of a (reused) pinned slot copied into a fresh array, in parallel."""
+    fresh = np.empty((n,) + host.shape[1:], dtype=host.dtype)
+    _parallel_copy([fresh[j] for j in range(n)], [host[j] for j in range(n)])
+    return fresh
 
 
 def _gpu_ok(device_type: str) -> bool:
@@ -458,49 +465,98 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
     def _transform_device(self, arrays: List[Optional[np.ndarray]], valid: List[int], out: np.ndarray,
                           origins: List[str]) -> set:
         """Device execution of the stage list (K19 fused when it applies, else K20 stage kernels over
-        uniform-shape batches). Returns the row indices it produced."""
+        uniform-shape batches). Returns the row indices it produced.
+
+        Two-slot pipeline per batch: the host fills pinned input slot k % 2 while the device runs batch k - 1
+        (H2D, kernels, D2H into pinned output slot), and the rows of batch k - 1 are built while batch k runs
+        on the device; a slot is refilled only after its event (batch k - 2's D2H) has completed. The pinned
+        slots come from torch's caching host allocator, so repeated calls reuse them."""
+        import torch
+
         done = set()
         bs = max(1, self.getBatchSize())
         to_tensor = self.getToTensor()
+        float_tensor = to_tensor and self.getTensorElementType().lower() == "float"
         fused = to_tensor and self._fused_plan([arrays[i].shape for i in valid]) is not None
         if fused:
-            for s in range(0, len(valid), bs):
-                idx = valid[s:s + bs]
-                t = self.device_tensors([arrays[i] for i in idx])
-                if t is None:
-                    return done
-                host = t.float().cpu().numpy()
-                for j, i in enumerate(idx):
-                    out[i] = host[j]
-                    done.add(i)
+            def launch_fused(idx, slot):
+                return self.device_tensors([arrays[i] for i in idx])
+
+            self._pipeline(valid, bs, launch_fused, None, lambda host, idx: self._emit_float(host, idx, out, done),
+                           out, done)
             return done
         groups: Dict[tuple, List[int]] = {}
         for i in valid:
             groups.setdefault(arrays[i].shape, []).append(i)
-        float_tensor = to_tensor and self.getTensorElementType().lower() == "float"
-        import torch
+
+        def emit(host, idx):
+            if float_tensor:  # one bulk copy out of the reused pinned slot; the rows are views of it
+                host = _bulk_copy(host, len(idx))
+            for j, i in enumerate(idx):
+                a = host[j]
+                out[i] = a if float_tensor else (self._finish_host(a) if to_tensor else make_image_row(a, origins[i]))
+                done.add(i)
 
         for shape, members in groups.items():
             if len(shape) != 3:
                 continue
-            # one pinned staging buffer per shape group, filled in parallel and reused by every batch
-            stage_in = torch.empty((min(bs, len(members)),) + tuple(shape), dtype=torch.uint8, pin_memory=True)
-            sv = stage_in.numpy()
-            for s in range(0, len(members), bs):
-                idx = members[s:s + bs]
+            nb = min(bs, len(members))
+            ins = [torch.empty((nb,) + tuple(shape), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+
+            def launch(idx, slot, ins=ins):
+                sv = ins[slot].numpy()
                 _parallel_copy([sv[j] for j in range(len(idx))], [arrays[i] for i in idx])
-                x = self.run_stages_device(stage_in[:len(idx)])
+                x = self.run_stages_device(ins[slot][:len(idx)])
                 if x is None:
-                    break
-                res = self.tensors_from_device_images(x) if float_tensor else x
-                host_t = torch.empty(res.shape, dtype=res.dtype, pin_memory=True)
-                host_t.copy_(res)  # D2H into pinned memory (also orders the staging buffer's reuse)
-                host = host_t.numpy()
-                for j, i in enumerate(idx):
-                    a = host[j]
-                    out[i] = a if float_tensor else (self._finish_host(a) if to_tensor else make_image_row(a, origins[i]))
-                    done.add(i)
+                    return None
+                return self.tensors_from_device_images(x) if float_tensor else x
+
+            if not self._pipeline(members, bs, launch, ins, emit, out, done):
+                break
         return done
+
+    @staticmethod
+    def _pipeline(members, bs, launch, ins, emit, out, done) -> bool:
+        """Batches of `members` through launch(idx, slot) -> device result (None: not on the device), D2H into
+        pinned output slot (slot = batch % 2), emit(host, idx) one batch behind. False if a launch declined."""
+        import torch
+
+        outs = [None, None]
+        ev = [None, None]
+        pending = None
+
+        def finish(slot, idx):
+            ev[slot].synchronize()
+            emit(outs[slot].numpy(), idx)
+
+        ok = True
+        for k, s in enumerate(range(0, len(members), bs)):
+            slot = k & 1
+            idx = members[s:s + bs]
+            if ev[slot] is not None:
+                ev[slot].synchronize()  # batch k - 2 left both slots (its rows were built at step k - 1)
+            res = launch(idx, slot)
+            if res is None:
+                ok = False
+                break
+            shp = (min(bs, len(members)),) + tuple(res.shape[1:])
+            if outs[slot] is None or tuple(outs[slot].shape) != shp or outs[slot].dtype != res.dtype:
+                outs[slot] = torch.empty(shp, dtype=res.dtype, pin_memory=True)
+            outs[slot][:len(idx)].copy_(res, non_blocking=True)
+            ev[slot] = torch.cuda.Event()
+            ev[slot].record()
+            if pending is not None:
+                finish(*pending)
+            pending = (slot, idx)
+        if pending is not None:
+            finish(*pending)
+        return ok
+
+    def _emit_float(self, host, idx, out, done) -> None:
+        fresh = _bulk_copy(host, len(idx))  # the pinned slot is reused by the batch after next
+        for j, i in enumerate(idx):
+            out[i] = fresh[j]
+            done.add(i)
 
     def _finish_host(self, a: np.ndarray):
         """toTensor of one processed image on the host (tensorElementType double: the reference's fp64)."""

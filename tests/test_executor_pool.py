@@ -181,3 +181,35 @@ def test_spawned_run_partitions_times_out_as_timeout():
     df = DataFrame({"x": np.arange(4.0)}, num_partitions=2)
     with pytest.raises(TimeoutError):
         R.run_partitions(_sleep_task, df, num_workers=2, timeout_s=3.0)
+
+
+def _shm_reduce_task(part, rank, world):
+    from synapseml_amd.parallel import distributed as D
+
+    rng = np.random.default_rng(rank)
+    big = rng.standard_normal(300_000)  # 2.4 MB: three pieces of the 1 MiB slot
+    ints = rng.integers(-2**40, 2**40, size=5000, dtype=np.int64)
+    D.allreduce_numpy(big)
+    D.allreduce_numpy(ints)
+    red = D._same_host_reducer()
+    return big, ints, red is not None
+
+
+def test_same_host_shared_memory_allreduce_three_ranks():
+    """allreduce_numpy on a same-host gloo group goes through one shared-memory segment: every rank gets the
+    bitwise-identical float64 result (slots summed in rank order, chunked past the slot size) and exact int64
+    sums."""
+    df = DataFrame({"x": np.arange(6.0)}, num_partitions=3)
+    res = R.run_partitions(_shm_reduce_task, df, num_workers=3)
+    assert all(r[2] for r in res)
+    exp_f = sum(np.random.default_rng(r).standard_normal(300_000) for r in range(3))
+    for big, ints, _ in res:
+        np.testing.assert_array_equal(big, res[0][0])
+        np.testing.assert_array_equal(ints, res[0][1])
+    np.testing.assert_allclose(res[0][0], exp_f, rtol=1e-12, atol=1e-12)
+    want = np.zeros(5000, dtype=np.int64)
+    for r in range(3):
+        rng = np.random.default_rng(r)
+        rng.standard_normal(300_000)
+        want += rng.integers(-2**40, 2**40, size=5000, dtype=np.int64)
+    np.testing.assert_array_equal(res[0][1], want)
