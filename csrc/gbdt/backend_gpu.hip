@@ -2397,10 +2397,14 @@ struct BExp {
   int64_t pgcount;  // the parent's global rows (the larger child's count = pgcount - the smaller's)
 };
 
+constexpr int kCurStride = 32;  // 8-byte words between two expansions' cursors (256 B)
+
 struct BState {
   int32_t nexp, done, nnodes, expanded;
   int32_t spec_used, ntiles, cap_nodes, cap_exp;
-  unsigned long long cursor[kMaxSpec];
+  // expansion j's partition cursor is cursor[j * kCurStride]: each on its own 256-byte line, so the per-tile
+  // claims of different expansions do not serialise on one cache line
+  unsigned long long cursor[kMaxSpec * kCurStride];
   BExp exp[kMaxSpec];
   // the replay's committed prefix (every pop before the first unexplored one, which later rounds can only
   // confirm): the frontier at that point and the pops so far, so the next round resumes there instead of
@@ -2427,7 +2431,7 @@ __device__ __forceinline__ void BatchHistAlloc(const int* cnt, int nexp, int* nb
 
 __device__ __forceinline__ int BatchSmallCount(const BState* bs, int j) {
   const BExp& x = bs->exp[j];
-  const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+  const int lt = static_cast<int>(bs->cursor[j * kCurStride] & 0xFFFFFFFFull);
   return x.left_small ? lt : x.pcount - lt;
 }
 
@@ -2557,7 +2561,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     const BExp& x = bs->exp[j];
     x_c0[q] = x.c0; x_c1[q] = x.c1; x_ls[q] = x.left_small;
     x_pb[q] = x.pbegin; x_pc[q] = x.pcount; x_buf[q] = x.pbuf; x_pg[q] = x.pgcount;
-    lt[q] = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+    lt[q] = static_cast<int>(bs->cursor[j * kCurStride] & 0xFFFFFFFFull);
     small_cnt[q] = static_cast<int64_t>(part[static_cast<size_t>(j) * (E + 1) + E].x);
   };
   if (first) {
@@ -2923,7 +2927,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     }
     x.tile0 = pre - nt;
     bs->exp[j] = x;
-    bs->cursor[j] = 0ull;
+    bs->cursor[j * kCurStride] = 0ull;
     if (j == nch - 1) bs->ntiles = pre;
   }
   if (lane == 0) {
@@ -3028,7 +3032,7 @@ __device__ __forceinline__ void BatchedPartitionPipelined(
       for (int u = 0; u < kPartRows; ++u)
         for (int w = 0; w < kWaves; ++w) tl += wl[u][w];
       const int tr = tv - tl;
-      const unsigned long long old = atomicAdd(&bs->cursor[j], static_cast<unsigned long long>(tl) |
+      const unsigned long long old = atomicAdd(&bs->cursor[j * kCurStride], static_cast<unsigned long long>(tl) |
                                                                    (static_cast<unsigned long long>(tr) << 32));
       bases[0] = s_pb[j] + static_cast<int>(old & 0xFFFFFFFFull);
       bases[1] = s_pb[j] + s_pc[j] - static_cast<int>(old >> 32) - tr;
@@ -3118,7 +3122,7 @@ __global__ __launch_bounds__(kPartThreads) void bpart_kernel(
     int j = 0;
     while (j + 1 < nexp && s_tile0[j + 1] <= tile) ++j;
     const PartSplit ps = s_ps[j];
-    PartitionTile<kPartRows>(ps, s_cat[j], tile - s_tile0[j], s_pb[j], s_pc[j], s_pbuf[j], &bs->cursor[j], cbins, n,
+    PartitionTile<kPartRows>(ps, s_cat[j], tile - s_tile0[j], s_pb[j], s_pc[j], s_pbuf[j], &bs->cursor[j * kCurStride], cbins, n,
                              perm0, perm1, ogh0, ogh1, wperm0, wperm1, wogh0, wogh1, g, h);
   }
 }
@@ -3147,7 +3151,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void bhist_kernel(
   if (q < 0) return;
   const int j = j0 + q;
   const BExp& x = bs->exp[j];
-  const int lt = static_cast<int>(bs->cursor[j] & 0xFFFFFFFFull);
+  const int lt = static_cast<int>(bs->cursor[j * kCurStride] & 0xFFFFFFFFull);
   const int begin = x.left_small ? x.pbegin : x.pbegin + lt;
   HistBody<kUnroll, kFPG, kPipe, kTight, kIdx>(begin, s_cnt[q], x.pbuf == 0 ? 1 : 0, s_nb[q], bx - s_off[q], bins4, W4, F,
                                                perm0, perm1, ogh0, ogh1, g, h, ghmax,
@@ -3768,6 +3772,7 @@ class GpuBackend : public TrainBackend {
     // global quantities of the histogram scale (HistScaleV): the row-count bound and the objective bound's
     // max |weight| are the same on every rank, so the fixed-point histograms do not depend on the partitioning
     scale_n_ = n_;
+    comm_bytes0_ = comm_ ? comm_->DeviceBytes() : 0;  // the (cached) communicator's count so far
     if (comm_ && comm_->world() > 1) {
       double c = static_cast<double>(n_);
       comm_->AllReduceHost(&c, 1);
@@ -4075,7 +4080,7 @@ class GpuBackend : public TrainBackend {
     }
     SML_HIP_CHECK(hipStreamSynchronize(stream_));
     AccountScoreTime();
-    if (comm_) stats.comm_dev_bytes = comm_->DeviceBytes();
+    if (comm_) stats.comm_dev_bytes = comm_->DeviceBytes() - comm_bytes0_;  // this booster's share
   }
 
   Tree TrainTree(int k, const std::vector<char>& fmask_in) override {
@@ -4891,6 +4896,7 @@ class GpuBackend : public TrainBackend {
   int plan_cap_ = 0;            // node records allocated for the batched growth (the plan stages them all)
   // index-only partition: interleaved (g, h) of class 0; gh2_valid_: it holds the current gradients; g_stale_:
   // g_ / h_ do not (the fused pass wrote only gh2_) - EnsureGH unpacks before anything reads them
+  int64_t comm_bytes0_ = 0;
   bool idx_ok_ = false;
   bool gh2_valid_ = false;
   bool g_stale_ = false;
