@@ -33,8 +33,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <numeric>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -3576,19 +3578,66 @@ __global__ void axpby_kernel(double* __restrict__ s, int64_t n, double a, double
 }
 
 // ---------------------------------------------------------------- backend
+// Per-device cache of the backend's runtime objects that cost milliseconds to make and free (the stream, the
+// 4 MB pinned readback buffer, the mapped flag ring): a process that fits repeatedly hands them from one
+// backend to the next (create + destroy measured at ~1.5 ms + ~1.8 ms per fit; r6 pass 15).
+struct BackendObjects {
+  std::mutex mu;
+  std::unordered_map<int, std::vector<hipStream_t>> streams;
+  std::unordered_map<int, std::vector<void*>> pinned, flags;
+  static constexpr size_t kKeep = 4;  // per device and kind
+
+  static BackendObjects& Get() {
+    static BackendObjects* p = new BackendObjects();  // never destroyed (teardown order)
+    return *p;
+  }
+  template <class T>
+  bool Take(std::unordered_map<int, std::vector<T>>& m, int dev, T* out) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto& v = m[dev];
+    if (v.empty()) return false;
+    *out = v.back();
+    v.pop_back();
+    return true;
+  }
+  template <class T>
+  bool Give(std::unordered_map<int, std::vector<T>>& m, int dev, T x) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto& v = m[dev];
+    if (v.size() >= kKeep) return false;
+    v.push_back(x);
+    return true;
+  }
+};
+
 class GpuBackend : public TrainBackend {
  public:
   explicit GpuBackend(int dev) : dev_(dev) {}
   ~GpuBackend() override {
+    static const bool prof = std::getenv("SML_RELEASE_PROF") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto t0 = now();
+    BackendObjects& cache = BackendObjects::Get();
     vsets_.clear();  // they sync on stream_ before it goes
-    if (stream_) { (void)hipStreamSynchronize(stream_); (void)hipStreamDestroy(stream_); }
+    const auto t1 = now();
+    if (stream_) {
+      const bool idle = hipStreamSynchronize(stream_) == hipSuccess;
+      if (!idle || !cache.Give(cache.streams, dev_, stream_)) (void)hipStreamDestroy(stream_);
+    }
+    const auto t2 = now();
     for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
     if (ev_copy_) (void)hipEventDestroy(ev_copy_);
     if (ev_sync_) (void)hipEventDestroy(ev_sync_);
     for (hipEvent_t e : comm_ev_) if (e) (void)hipEventDestroy(e);
-    if (pinned_) (void)hipHostFree(pinned_);
+    const auto t3 = now();
+    if (pinned_ && !cache.Give(cache.pinned, dev_, pinned_)) (void)hipHostFree(pinned_);
+    const auto t4 = now();
     for (hipEvent_t e : bev_) if (e) (void)hipEventDestroy(e);
-    if (bflag_host_) (void)hipHostFree(bflag_host_);
+    if (bflag_host_ && !cache.Give(cache.flags, dev_, static_cast<void*>(bflag_host_))) (void)hipHostFree(bflag_host_);
+    if (prof)
+      std::fprintf(stderr, "~GpuBackend: vsets %.3f stream %.3f events %.3f pinned %.3f bflag %.3f ms\n", ms(t0, t1),
+                   ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, now()));
     if (bprof_) {
       if (bprof_n_ > 0) {  // wall_clock64 ticks at 100 MHz: 10 ns
         std::fprintf(stderr, "bplan phases (us/round over %lld rounds): absorb %.2f stage %.2f replay %.2f plan %.2f "
@@ -3614,7 +3663,8 @@ class GpuBackend : public TrainBackend {
     if (cfg.num_leaves > 4096) throw std::runtime_error("GPU backend: num_leaves > 4096");
     if (dev_ >= 0) SML_HIP_CHECK(hipSetDevice(dev_));
     SML_HIP_CHECK(hipGetDevice(&dev_));
-    SML_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (!BackendObjects::Get().Take(BackendObjects::Get().streams, dev_, &stream_))
+      SML_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     sp_ = MakeSplitParams(cfg);
     ghmax_.alloc(2);  // max |g|, max h (float bits)
     ghmax_partial_.alloc(2 * kGhmaxBlocks);
@@ -3671,7 +3721,11 @@ class GpuBackend : public TrainBackend {
       bnodes_.alloc(cap_nodes);
       plan_cap_ = cap_nodes;
       nbest_.alloc(cap_nodes);
-      SML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&bflag_host_), sizeof(int) * kBRing, hipHostMallocMapped | hipHostMallocCoherent));
+      if (void* f = nullptr; BackendObjects::Get().Take(BackendObjects::Get().flags, dev_, &f))
+        bflag_host_ = static_cast<int*>(f);
+      else
+        SML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&bflag_host_), sizeof(int) * kBRing,
+                                    hipHostMallocMapped | hipHostMallocCoherent));
       SML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&bflag_dev_), bflag_host_, 0));
       if (const char* e = std::getenv("SML_BPLAN_PROF"); e != nullptr && std::atoi(e) != 0) {
         const size_t nb = sizeof(long long) * kPlanProfStride * (cfg.num_leaves + 3);
@@ -3838,7 +3892,8 @@ class GpuBackend : public TrainBackend {
     // score-update tree (uploaded from host trees)
     up_blob_.alloc(static_cast<size_t>(NI + 1) * (16 + 32) + static_cast<size_t>(L_ + 4) * 8);
     leaf_idx_.alloc(n_);
-    SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
+    if (!BackendObjects::Get().Take(BackendObjects::Get().pinned, dev_, &pinned_))
+      SML_HIP_CHECK(hipHostMalloc(&pinned_, kPinnedBytes, hipHostMallocDefault));
     for (hipEvent_t& e : ev_) SML_HIP_CHECK(hipEventCreate(&e));
     SML_HIP_CHECK(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming));
     SML_HIP_CHECK(hipEventCreateWithFlags(&ev_sync_, hipEventDisableTiming));

@@ -198,7 +198,8 @@ PYBIND11_MODULE(_gbdt, m) {
            })
       .def("set_label", [](PyDataset& p, F32 y) {
         if (y.size() != p.d->num_data) throw std::runtime_error("label size mismatch");
-        p.d->label.assign(y.data(), y.data() + y.size());
+        py::gil_scoped_release rel;
+        p.d->SetLabel(y.data(), y.size());
       })
       .def("set_weight", [](PyDataset& p, F32 w) {
         if (w.size() != p.d->num_data) throw std::runtime_error("weight size mismatch");
@@ -211,7 +212,10 @@ PYBIND11_MODULE(_gbdt, m) {
       })
       .def_property_readonly("num_data", [](const PyDataset& p) { return p.d->num_data; })
       .def_property_readonly("num_features", [](const PyDataset& p) { return p.d->ref.num_total_features; })
-      .def("get_label", [](const PyDataset& p) { return py::array_t<float>(p.d->label.size(), p.d->label.data()); })
+      .def("get_label", [](const PyDataset& p) {
+        p.d->FinalizeLabel();
+        return py::array_t<float>(p.d->label.size(), p.d->label.data());
+      })
       .def("get_bins", [](const PyDataset& p) {
         p.d->EnsureHostBins();
         return py::array_t<uint8_t>({p.d->num_data, static_cast<int64_t>(p.d->row_stride)}, p.d->bins.data());
@@ -352,6 +356,12 @@ PYBIND11_MODULE(_gbdt, m) {
       .def_property_readonly("current_iteration", &Booster::CurrentIteration)
       .def_property_readonly("feature_names", &Booster::FeatureNames)
       .def_property_readonly("backend", &Booster::BackendName)
+      .def("release_training", [](Booster& b) {
+        auto d = b.DetachTraining();  // the booster's own state changes under the GIL
+        py::gil_scoped_release rel;
+        d->Free();
+      })
+      .def_property_readonly("training_released", &Booster::training_released)
       .def("gradients", [](Booster& b) {
         std::vector<float> g, h;
         {

@@ -92,6 +92,7 @@ void Booster::InitTraining() {
     std::fprintf(stderr, "[booster init] %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tick).count());
     tick = now;
   };
+  train_->FinalizeLabel();
   objective_.reset(new Objective(cfg_));
   objective_->Init(*train_);
   mark("objective init");
@@ -136,6 +137,7 @@ void Booster::InitTraining() {
 
 void Booster::AddValidData(std::shared_ptr<Dataset> valid, const std::string& name) {
   const int K = num_tree_per_iter_;
+  valid->FinalizeLabel();
   std::vector<double> s(static_cast<size_t>(valid->num_data) * K, 0.0);
   if (!valid->init_score.empty()) s = valid->init_score;
   else for (int k = 0; k < K; ++k) for (int64_t i = 0; i < valid->num_data; ++i) s[k * valid->num_data + i] += (trees_.empty() ? init_scores_[k] : 0.0);
@@ -423,6 +425,29 @@ void Booster::RollbackOneIter() {
   --iter_;
 }
 
+void Booster::ReleaseTraining() { DetachTraining()->Free(); }
+
+std::unique_ptr<DetachedTraining> Booster::DetachTraining() {
+  auto d = std::make_unique<DetachedTraining>();
+  if (train_) loaded_parameters_ = cfg_.ToParametersSection();  // the model text's parameters section
+  if (backend_) released_backend_ = backend_->Name();
+  d->backend = std::move(backend_);
+  d->train = std::move(train_);
+  d->valid = std::move(valid_);
+  d->valid_objectives = std::move(valid_objectives_);
+  d->valid_scores = std::move(valid_scores_);
+  backend_.reset();
+  train_.reset();
+  valid_.clear();
+  valid_objectives_.clear();
+  valid_scores_.clear();
+  valid_dev_.clear();
+  bag_rows_.clear();
+  bag_rows_.shrink_to_fit();
+  released_ = true;
+  return d;
+}
+
 void Booster::Truncate(int num_iteration) {
   const size_t keep = static_cast<size_t>(std::max(0, num_iteration)) * num_tree_per_iter_;
   if (keep < trees_.size()) trees_.resize(keep);
@@ -451,6 +476,7 @@ std::vector<std::string> Booster::EvalNames() const {
 }
 
 std::vector<std::pair<std::string, double>> Booster::Eval(int idx, bool device) {
+  Backend();  // raises once the training state was released
   std::vector<std::pair<std::string, double>> out;
   const Dataset* d;
   const Objective* obj;
@@ -483,7 +509,7 @@ std::vector<std::pair<std::string, double>> Booster::Eval(int idx, bool device) 
   return out;
 }
 
-void Booster::GetTrainScores(std::vector<double>* s) { backend_->GetScores(s); }
+void Booster::GetTrainScores(std::vector<double>* s) { Backend()->GetScores(s); }
 void Booster::GetPredictForValid(int idx, std::vector<double>* s) const {
   if (valid_dev_.at(idx)) backend_->GetValidScores(idx, s);
   else *s = valid_scores_.at(idx);

@@ -6,8 +6,12 @@
 // SaveModelToString 276, DumpModel 481, PredictFor* 520-557,
 // FeatureImportance 504, ResetParameter 320).
 #pragma once
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>
@@ -22,6 +26,35 @@
 namespace sml {
 
 enum PredictType { kPredictRaw = 0, kPredictNormal = 1, kPredictLeaf = 2, kPredictContrib = 3 };
+
+// What Booster::DetachTraining takes out of a fitted booster: freed by whoever holds it (Free() / destructor),
+// e.g. on a background thread, while the booster keeps serving predictions.
+struct DetachedTraining {
+  std::unique_ptr<TrainBackend> backend;
+  std::shared_ptr<Dataset> train;
+  std::vector<std::shared_ptr<Dataset>> valid;
+  std::vector<std::unique_ptr<Objective>> valid_objectives;
+  std::vector<std::vector<double>> valid_scores;
+  void Free() {
+    static const bool prof = std::getenv("SML_RELEASE_PROF") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto t0 = now();
+    if (backend) backend->Synchronize();
+    const auto t1 = now();
+    backend.reset();
+    const auto t2 = now();
+    train.reset();
+    const auto t3 = now();
+    valid.clear();
+    valid_objectives.clear();
+    valid_scores.clear();
+    if (prof && (t3 - t0) > std::chrono::microseconds(50))
+      std::fprintf(stderr, "release: sync %.3f backend %.3f train %.3f valid %.3f ms\n", ms(t0, t1), ms(t1, t2),
+                   ms(t2, t3), ms(t3, now()));
+  }
+  ~DetachedTraining() { Free(); }
+};
 
 class Booster {
  public:
@@ -64,13 +97,21 @@ class Booster {
   int CurrentIteration() const { return static_cast<int>(trees_.size()) / std::max(1, num_tree_per_iter_); }
   const std::vector<std::string>& FeatureNames() const { return feature_names_; }
   const Config& config() const { return cfg_; }
-  std::string BackendName() const { return backend_ ? backend_->Name() : "none"; }
+  // the backend that trained this booster (kept after ReleaseTraining)
+  std::string BackendName() const { return backend_ ? backend_->Name() : (released_ ? released_backend_ : "none"); }
   TrainStats* stats() { return backend_ ? &backend_->stats : nullptr; }
   void Synchronize() { if (backend_) backend_->Synchronize(); }
   // gradients / hessians of the last iteration (class-major n*K; after GOSS rescaling)
-  void GetGradients(std::vector<float>* g, std::vector<float>* h) { backend_->GetGradients(g, h); }
+  void GetGradients(std::vector<float>* g, std::vector<float>* h) { Backend()->GetGradients(g, h); }
   // Keep only the first `num_iteration` iterations (early stopping).
   void Truncate(int num_iteration);
+  // Free everything only training needs (backend with its device buffers, datasets, validation state); the
+  // trees, objective and feature metadata stay, so prediction / model text / importance keep working and
+  // training calls raise. A fitted model's booster is released off the fit's critical path.
+  void ReleaseTraining();
+  // the same, but the released state is handed back instead of freed here (quick: pointer moves only)
+  std::unique_ptr<DetachedTraining> DetachTraining();
+  bool training_released() const { return released_; }
   const Objective* objective() const { return objective_.get(); }
 
  private:
@@ -112,6 +153,12 @@ class Booster {
   std::vector<int32_t> bag_rows_;
   // rf: per-class running sums of tree outputs are kept as scores/iter count
   int rf_trees_ = 0;
+  bool released_ = false;
+  std::string released_backend_;
+  TrainBackend* Backend() const {
+    if (!backend_) throw std::runtime_error(released_ ? "booster training state was released" : "booster has no backend");
+    return backend_.get();
+  }
 };
 
 }  // namespace sml

@@ -76,7 +76,7 @@ int SML_DatasetCreateFromMat(const void* data, int data_type, int32_t nrow, int3
     h->d = std::make_shared<Dataset>();
     h->d->Init(ref, nrow);
     h->d->PushDense(x.data(), nrow, ncol, 0);
-    h->d->label.assign(label, label + nrow);
+    h->d->SetLabel(label, nrow);
     *out = h.release();
   });
 }

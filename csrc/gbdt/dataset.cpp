@@ -391,7 +391,21 @@ void Dataset::Init(const DatasetReference& r, int64_t n) {
   host_valid = false;
   dev.reset();
   dev_valid = false;
-  label.assign(n, 0.f);
+  label.resize(static_cast<size_t>(n));  // default-initialised: SetLabel or FinalizeLabel writes it
+  label_set = false;
+}
+
+void Dataset::SetLabel(const float* y, int64_t n) {
+  if (n != num_data) throw std::runtime_error("label size mismatch");
+  label.resize(static_cast<size_t>(n));
+  std::copy(y, y + n, label.begin());
+  label_set = true;
+}
+
+void Dataset::FinalizeLabel() {
+  if (label_set) return;
+  std::fill(label.begin(), label.end(), 0.f);
+  label_set = true;
 }
 
 std::vector<uint8_t> Dataset::DefaultRow() const {

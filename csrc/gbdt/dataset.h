@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "config.h"
+#include "host_pool.h"
 
 namespace sml {
 
@@ -150,9 +151,15 @@ struct Dataset {
   mutable bool host_valid = false;    // `bins` holds every pushed row
   std::shared_ptr<DeviceBins> dev;    // device copy, current when dev_valid
   bool dev_valid = false;
-  std::vector<float> label;
-  std::vector<float> weight;          // empty = unweighted
+  // per-row vectors on the host block pool (host_pool.h): a repeated fit reuses the previous fit's blocks
+  PooledVector<float> label;          // num_data entries; zeros unless set (see FinalizeLabel)
+  PooledVector<float> weight;         // empty = unweighted
   std::vector<double> init_score;     // empty or num_data * num_tree_per_iteration
+  // Init leaves the labels unwritten (the caller's set_label overwrites them all - one pass over a 44 MB
+  // vector instead of two); consumers call FinalizeLabel, which zero-fills labels nobody set
+  bool label_set = false;
+  void SetLabel(const float* y, int64_t n);
+  void FinalizeLabel();
   std::vector<int32_t> query_boundaries;  // ranking: size num_queries+1
 
   void Init(const DatasetReference& r, int64_t n);

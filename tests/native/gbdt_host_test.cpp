@@ -58,14 +58,14 @@ static void run(const std::string& params, bool csr) {
   } else {
     ds->PushDense(X.data(), n, F, 0);
   }
-  ds->label = y;
+  ds->SetLabel(y.data(), static_cast<int64_t>(y.size()));
   Booster b(ds, params);
   // a validation set (the first 1000 rows): its incrementally folded scores equal the model's raw predictions
   const int nv = 1000;
   auto vd = std::make_shared<Dataset>();
   vd->Init(ref, nv);
   vd->PushDense(X.data(), nv, F, 0);
-  vd->label.assign(y.begin(), y.begin() + nv);
+  vd->SetLabel(y.data(), nv);
   b.AddValidData(vd, "valid_0");
   for (int it = 0; it < 15; ++it)
     if (b.TrainOneIter()) break;
@@ -119,7 +119,7 @@ static void malformed_models() {
   auto ds = std::make_shared<Dataset>();
   ds->Init(ref, n);
   ds->PushDense(X.data(), n, F, 0);
-  ds->label = y;
+  ds->SetLabel(y.data(), static_cast<int64_t>(y.size()));
   Booster b(ds, params);
   b.TrainOneIter();
   b.TrainOneIter();
@@ -218,7 +218,7 @@ static void concurrent_push_and_predict() {
     for (auto& t : th) t.join();
     if (mode != 1) CHECK(ds->bins == serial->bins);  // f32 rounding may move a bin edge: compare f64 pushes
     if (mode == 0) {
-      ds->label = y;
+      ds->SetLabel(y.data(), static_cast<int64_t>(y.size()));
       Booster b(ds, params);
       for (int it = 0; it < 8; ++it) b.TrainOneIter();
       std::vector<double> ref_pred(n), par(n);

@@ -1,5 +1,7 @@
 """Data-parallel training across 2 processes (gloo) must match one process on
 the union of the shards when both use the same bin boundaries."""
+import os
+
 import numpy as np
 import pytest
 
@@ -380,7 +382,8 @@ def test_partitions_reach_workers_through_shared_memory():
         np.testing.assert_allclose(fs, f[a:b].astype(np.float64).sum(), rtol=1e-6)
         np.testing.assert_allclose(vs, sv[a:b].values.sum())
         assert strs == list(s[a:b]) and ys == float(np.arange(a, b).sum())
-    assert set(glob.glob("/dev/shm/psm_*")) <= before
+    if not os.environ.get("PYTEST_XDIST_WORKER"):  # (other workers' jobs create segments concurrently)
+        assert set(glob.glob("/dev/shm/psm_*")) <= before
 
 
 def test_partitions_fall_back_to_pickle_when_shm_is_small(monkeypatch):

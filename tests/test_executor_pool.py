@@ -83,7 +83,8 @@ def test_dataframe_results_come_back_through_shared_memory():
     out = DataFrame.union_all(R.fan_out(_df_task, df, 2, use_gpu=False), keep_partitions=True)
     np.testing.assert_array_equal(out["x2"], np.arange(9.0) * 2)
     assert list(out["s"][:1]) == ["r0"] and out["rank"].dtype == np.int32
-    assert _psm() <= before  # every segment of the job was unlinked
+    if not os.environ.get("PYTEST_XDIST_WORKER"):  # (other workers' jobs create segments concurrently)
+        assert _psm() <= before  # every segment of the job was unlinked
 
 
 def _fail_rank1(part, rank, world):

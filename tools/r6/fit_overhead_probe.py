@@ -43,6 +43,28 @@ def main():
                           "text_ms": round((t2 - t1) * 1e3, 2), "del_prev_ms": round((t3a - t2) * 1e3, 2),
                           "gc_ms": round((t3 - t3a) * 1e3, 2),
                           "sync_ms": round((t4 - t3) * 1e3, 2)}), flush=True)
+    # the bench's loop (no explicit collection): time the interpreter's own cyclic collections inside each fit
+    gcs = []
+    t_start = [0.0]
+
+    def cb(phase, info):
+        if phase == "start":
+            t_start[0] = time.perf_counter()
+        else:
+            gcs.append((info["generation"], (time.perf_counter() - t_start[0]) * 1e3))
+
+    gc.callbacks.append(cb)
+    for step in range(5):
+        gcs.clear()
+        t0 = time.perf_counter()
+        model = est.fit(df)
+        model.getNativeModel()
+        t1 = time.perf_counter()
+        m = est.getPerformanceMeasures()[0]
+        print(json.dumps({"autogc_step": step, "step_ms": round((t1 - t0) * 1e3, 2), "total_ms": m.get("total_ms"),
+                          "gc_gen2_ms": round(sum(t for g, t in gcs if g == 2), 2),
+                          "gc_other_ms": round(sum(t for g, t in gcs if g < 2), 2), "n_gc": len(gcs)}), flush=True)
+    gc.callbacks.remove(cb)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-6 pass 15: host-side reuse across fits (label vectors on a host block pool, backend stream / pinned
+# staging / flag ring cached per device, synchronous release) - GBDT GPU suite, headline x3, fault probe.
+OUT=${1:-gpurun_out/r6p15}
+ROOT=$(pwd)
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
+timeout -k 10 600 python -u -m pytest -q --timeout 180 --timeout-method thread tests/test_gbdt_gpu.py tests/test_comm_gpu.py -m gpu > "$OUT/pytest_gbdt.log" 2>&1
+rc=$?; tail -2 "$OUT/pytest_gbdt.log"; [ $rc -ne 0 ] && { grep -E "FAILED|Error" "$OUT/pytest_gbdt.log" | head -20; exit $rc; }
+for i in 1 2 3; do
+  timeout -k 10 400 python bench.py --steps 5 --warmup 1 > "$OUT/bench_$i.log" 2>&1 || exit 1
+  tail -1 "$OUT/bench_$i.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['config']['iteration_ms'], d['config']['fit_phases_ms'])"
+done
+SML_RELEASE_PROF=1 timeout -k 10 400 python tools/r6/fit_fault_probe.py > "$OUT/faults.log" 2>&1 || exit 1
+grep -E "step|thp" "$OUT/faults.log"
