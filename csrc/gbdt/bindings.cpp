@@ -94,6 +94,16 @@ PYBIND11_MODULE(_gbdt, m) {
       .def("upper_bounds", [](const DatasetReference& r, int f) { return r.mappers.at(f).upper_bounds; })
       .def("value_to_bin", [](const DatasetReference& r, int f, double v) { return r.mappers.at(f).ValueToBin(v); });
 
+  m.def("group_runs", [](I64 ids) {
+    std::vector<int64_t> starts;
+    bool grouped;
+    {
+      py::gil_scoped_release rel;
+      grouped = GroupRuns(ids.data(), ids.size(), &starts);
+    }
+    return py::make_tuple(py::array_t<int64_t>(starts.size(), starts.data()), grouped);
+  }, "first row of every run of equal ids, and whether each id forms one run");
+
   // K1 input staging: the raw rows go up on a native thread while Python samples / builds bin boundaries
   m.def("sample_dense_rows",
         [](py::array X, int64_t count, uint64_t seed) -> py::array {

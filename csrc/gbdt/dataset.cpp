@@ -395,6 +395,39 @@ void Dataset::Init(const DatasetReference& r, int64_t n) {
   label_set = false;
 }
 
+bool GroupRuns(const int64_t* a, int64_t n, std::vector<int64_t>* starts) {
+  starts->clear();
+  if (n <= 0) return true;
+  // one pass over the column in parallel chunks (12.5M ids: ~8 ms as two numpy passes), then the run ids
+  const int nt = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(omp_get_max_threads(), n >> 16)));
+  std::vector<std::vector<int64_t>> part(nt);
+#pragma omp parallel for schedule(static) num_threads(nt)
+  for (int t = 0; t < nt; ++t) {
+    const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    auto& v = part[t];
+    for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
+      if (a[i] != a[i - 1]) v.push_back(i);
+  }
+  size_t total = 1;
+  for (auto& v : part) total += v.size();
+  starts->reserve(total);
+  starts->push_back(0);
+  for (auto& v : part) starts->insert(starts->end(), v.begin(), v.end());
+  // grouped iff the run ids are distinct: monotone run ids (the usual layout) are, otherwise sort and look
+  const size_t r = starts->size();
+  bool inc = true, dec = true;
+  for (size_t k = 1; k < r && (inc || dec); ++k) {
+    const int64_t x = a[(*starts)[k - 1]], y = a[(*starts)[k]];
+    inc &= x < y;
+    dec &= x > y;
+  }
+  if (inc || dec) return true;
+  std::vector<int64_t> ids(r);
+  for (size_t k = 0; k < r; ++k) ids[k] = a[(*starts)[k]];
+  std::sort(ids.begin(), ids.end());
+  return std::adjacent_find(ids.begin(), ids.end()) == ids.end();
+}
+
 void Dataset::SetLabel(const float* y, int64_t n) {
   if (n != num_data) throw std::runtime_error("label size mismatch");
   label.resize(static_cast<size_t>(n));

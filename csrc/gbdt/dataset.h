@@ -212,6 +212,10 @@ void UploadPinned(const char* host, char* dev, size_t bytes, DeviceRows* progres
 // device -> host copy of a device-resident bin matrix (bin_encode.hip)
 void DatasetDownloadBins(const Dataset& d, uint8_t* host);
 
+// Runs of equal ids in a query-group column (LightGBMRanker): *starts gets the first row of every run (in
+// row order); returns true when no id starts two runs (the rows are grouped, no reorder needed). Parallel scan.
+bool GroupRuns(const int64_t* ids, int64_t n, std::vector<int64_t>* starts);
+
 // k distinct row indices of [0, n), sorted, drawn from the seed (bin-boundary sampling, K1's host side)
 std::vector<int64_t> SampleRowIndices(int64_t n, int64_t k, uint64_t seed);
 

@@ -64,23 +64,33 @@ void Objective::Init(const float* label, const float* weight, int64_t n, const s
   }
   if (p_.kind == kObjLambdarank) {
     if (qb_.size() < 2) throw std::runtime_error("lambdarank requires query/group information");
-    // ideal DCG per query: the labels in descending order are a counting sort over the (clipped) gain index -
-    // labels are small non-negative integers - so a query costs one pass, not a sort (125k queries of ~100
-    // documents: the serial sort loop was ~130 ms of LightGBMRanker's booster init)
+    // ideal DCG per query. Labels are small non-negative integers: from the query's largest (clipped) label down, count the documents
+    // of that label (a vectorised compare-and-count over the query) until max_position places are filled; a
+    // run of c documents of gain G at places [k, k + c) adds G * (P[k + c] - P[k]), P the prefix sums of
+    // 1 / log2(2 + k). (125k queries of ~100 documents: 3.6 ms of the ranker's booster init with a per-document
+    // counting sort and a per-place divide, ~2.4x less this way; the serial sort loop before that was ~130 ms.)
     inv_max_dcg_.assign(qb_.size() - 1, 0.0);
     const int ng = static_cast<int>(label_gain_.size());
     const int64_t nq = static_cast<int64_t>(qb_.size()) - 1;
+    const int mp = std::max(0, max_position_);
+    std::vector<double> pre(mp + 1, 0.0);
+    for (int k = 0; k < mp; ++k) pre[k + 1] = pre[k] + 1.0 / std::log2(2.0 + k);
+    auto gidx = [ng](float x) { return std::max(0, std::min(static_cast<int>(x), ng - 1)); };
 #pragma omp parallel for schedule(dynamic, 256)
     for (int64_t q = 0; q < nq; ++q) {
-      std::vector<int32_t> cnt(ng, 0);
-      for (int32_t i = qb_[q]; i < qb_[q + 1]; ++i) {
-        const int l = static_cast<int>(label[i]);
-        ++cnt[std::max(0, std::min(l, ng - 1))];
-      }
+      const int32_t b = qb_[q], e = qb_[q + 1];
+      int mx = 0;
+      for (int32_t i = b; i < e; ++i) mx = std::max(mx, gidx(label[i]));
       double dcg = 0;
       int k = 0;
-      for (int gi = ng - 1; gi >= 0 && k < max_position_; --gi)
-        for (int32_t c = 0; c < cnt[gi] && k < max_position_; ++c, ++k) dcg += label_gain_[gi] / std::log2(2.0 + k);
+      for (int v = mx; v >= 0 && k < mp; --v) {
+        int c = 0;
+        for (int32_t i = b; i < e; ++i) c += gidx(label[i]) == v;
+        if (c == 0) continue;
+        const int take = std::min(c, mp - k);
+        dcg += label_gain_[v] * (pre[k + take] - pre[k]);
+        k += take;
+      }
       inv_max_dcg_[q] = dcg > 0 ? 1.0 / dcg : 0.0;
     }
   }

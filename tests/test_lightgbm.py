@@ -474,6 +474,24 @@ def test_ranker_group_order_vectorised():
         assert np.array_equal(_group_order(ids), ref)
 
 
+def test_group_runs_native_matches_numpy():
+    """The parallel native run scan (integer group ids) gives numpy's run starts and grouped flag: sorted,
+    decreasing, unsorted-but-contiguous and scattered ids, runs across the scan's chunk boundaries."""
+    from synapseml_amd.lightgbm.base import _group_runs
+
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(1, 300, 3000)
+    cases = [np.repeat(np.arange(len(sizes)), sizes), np.repeat(np.arange(len(sizes))[::-1], sizes),
+             np.repeat(rng.permutation(len(sizes)), sizes), rng.integers(0, 50, 400_000),
+             np.repeat(np.array([4, 1, 4]), [70000, 5, 70000]), np.repeat(np.arange(3, dtype=np.int32), 100000)]
+    for ids in cases:
+        starts, grouped = _group_runs(ids)
+        ref = np.concatenate(([0], np.flatnonzero(ids[1:] != ids[:-1]) + 1))
+        assert np.array_equal(starts, ref)
+        assert grouped == (len(np.unique(ids[ref])) == len(ref))
+    assert not _group_runs(cases[3])[1] and not _group_runs(cases[4])[1] and _group_runs(cases[2])[1]
+
+
 def test_dense_push_interleaved_bins_match_scalar_and_searchsorted():
     """Host bin encoding (blocks of 8 rows, interleaved branchless searches) equals the one-row path and a
     numpy searchsorted oracle, for float32 and float64 rows, NaN / zero-as-missing and a categorical column."""

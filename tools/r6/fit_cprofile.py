@@ -16,10 +16,23 @@ def main():
     from synapseml_amd.core.dataframe import DataFrame
     from synapseml_amd.lightgbm import LightGBMClassifier
 
-    X, y = higgs_like(11_000_000, 28, seed=1234)
-    df = DataFrame({"features": X, "label": y})
-    est = LightGBMClassifier(numIterations=100, learningRate=0.1, numLeaves=31, maxBin=255, binSampleCount=200000,
-                             minDataInLeaf=20, objective="binary", deviceType="gpu", metric="auc")
+    if "--ranker" in sys.argv:  # tools/bench_ranker.py's data and estimator
+        import numpy as np
+
+        from synapseml_amd.lightgbm import LightGBMRanker
+        from tools.bench_ranker import ranking_data
+
+        X, y, sizes = ranking_data(12_500_000, 28, seed=77)
+        qid = np.repeat(np.arange(len(sizes), dtype=np.int64), sizes)
+        df = DataFrame({"features": X, "label": y, "query": qid})
+        est = LightGBMRanker(numIterations=100, learningRate=0.1, numLeaves=31, maxBin=255, minDataInLeaf=20,
+                             groupCol="query", evalAt=[10], deviceType="gpu")
+    else:
+        X, y = higgs_like(11_000_000, 28, seed=1234)
+        df = DataFrame({"features": X, "label": y})
+        est = LightGBMClassifier(numIterations=100, learningRate=0.1, numLeaves=31, maxBin=255,
+                                 binSampleCount=200000, minDataInLeaf=20, objective="binary", deviceType="gpu",
+                                 metric="auc")
     model = est.fit(df)
     model.getNativeModel()
     torch.cuda.synchronize()
