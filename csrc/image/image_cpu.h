@@ -30,6 +30,7 @@ struct PrepParams {
   int out_dtype;          // 0 f32, 1 f16, 2 bf16
   int nhwc;               // 0 = NCHW (ONNX layout), 1 = NHWC
   const int32_t* host_dims = nullptr;  // HOST copy of dims (the resize taps are built per image on the host)
+  int taps_uniform = 0;   // device path: every image has the same (h, w), one set of resize taps for the batch
 };
 
 // K19: batched decode-free preprocess. Images are packed HWC uint8 at

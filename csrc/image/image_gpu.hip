@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(const uint8_t* __r
   const bool rs = p.resize_h > 0;
   int4 ty = make_int4(ry, ry, 0, 0), tx = make_int4(rx, rx, 0, 0);
   if (rs) {
-    const int4* tb = taps + static_cast<size_t>(b) * (p.resize_h + p.resize_w);
+    const int4* tb = taps + (p.taps_uniform ? size_t(0) : static_cast<size_t>(b) * (p.resize_h + p.resize_w));
     ty = tb[ry];
     tx = tb[p.resize_h + rx];
   }
@@ -281,10 +281,18 @@ void PreprocessBatchDevice(const uint8_t* src, const int64_t* offsets, const int
     for (int v = 0; v < 256; ++v)
       lut[k * 256 + v] = static_cast<float>((static_cast<double>(v) * p.scale - p.mean[k]) / p.stdv[k]);
   std::vector<int4> taps;
+  PrepParams q = p;
   if (p.resize_h > 0) {
     if (!p.host_dims) throw std::invalid_argument("preprocess: resize needs the images' host dims");
-    taps.reserve(static_cast<size_t>(B) * (p.resize_h + p.resize_w));
-    for (int b = 0; b < B; ++b) {
+    // one set of taps when every image has the same size (a 256-image batch's per-image tables were 2 MB of
+    // pageable upload, which waited for the batch's own H2D before returning: r6 pass 19)
+    bool uniform = true;
+    for (int b = 1; b < B && uniform; ++b)
+      uniform = p.host_dims[3 * b] == p.host_dims[0] && p.host_dims[3 * b + 1] == p.host_dims[1];
+    q.taps_uniform = uniform ? 1 : 0;
+    const int nb = uniform ? 1 : B;
+    taps.reserve(static_cast<size_t>(nb) * (p.resize_h + p.resize_w));
+    for (int b = 0; b < nb; ++b) {
       const auto ty = AxisTaps(p.resize_h, p.host_dims[3 * b]), tx = AxisTaps(p.resize_w, p.host_dims[3 * b + 1]);
       taps.insert(taps.end(), ty.begin(), ty.end());
       taps.insert(taps.end(), tx.begin(), tx.end());
@@ -294,13 +302,13 @@ void PreprocessBatchDevice(const uint8_t* src, const int64_t* offsets, const int
   int4* d_taps = UploadTable(taps, s);
   dim3 grid((p.out_h * p.out_w + kThreads - 1) / kThreads, B);
   if (p.out_dtype == 1)
-    hipLaunchKernelGGL(preprocess_kernel<__half>, grid, dim3(kThreads), 0, s, src, offsets, dims, p, d_taps, d_lut,
+    hipLaunchKernelGGL(preprocess_kernel<__half>, grid, dim3(kThreads), 0, s, src, offsets, dims, q, d_taps, d_lut,
                        static_cast<__half*>(out));
   else if (p.out_dtype == 2)
-    hipLaunchKernelGGL(preprocess_kernel<__hip_bfloat16>, grid, dim3(kThreads), 0, s, src, offsets, dims, p, d_taps,
+    hipLaunchKernelGGL(preprocess_kernel<__hip_bfloat16>, grid, dim3(kThreads), 0, s, src, offsets, dims, q, d_taps,
                        d_lut, static_cast<__hip_bfloat16*>(out));
   else
-    hipLaunchKernelGGL(preprocess_kernel<float>, grid, dim3(kThreads), 0, s, src, offsets, dims, p, d_taps, d_lut,
+    hipLaunchKernelGGL(preprocess_kernel<float>, grid, dim3(kThreads), 0, s, src, offsets, dims, q, d_taps, d_lut,
                        static_cast<float*>(out));
   IMG_HIP_CHECK(hipGetLastError());
   IMG_HIP_CHECK(hipFreeAsync(d_lut, s));

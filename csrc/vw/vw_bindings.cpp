@@ -408,6 +408,7 @@ PYBIND11_MODULE(_vw, m) {
   });
 
   m.def("_stager_rejects_null", &StagerRejectsNull);
+  m.def("_stager_unit_pieces", &StagerUnitPieces);
   py::class_<NcclHandle, std::shared_ptr<NcclHandle>>(m, "NcclComm")
       .def("abort", &NcclHandle::Abort)
       .def_property_readonly("aborted", [](const NcclHandle& h) { return h.aborted; });

@@ -142,6 +142,8 @@ class GpuSgd {
 bool VwGpuAvailable();
 // the pinned stager refuses a null source / destination (host-only; no HIP call is reached)
 bool StagerRejectsNull();
+// value pieces the shared stager sent as a device fill of 1.0f instead of their bytes (since process start)
+int64_t StagerUnitPieces();
 // K13: murmur3_32(bytes[offsets[i]:offsets[i+1]], seed) & mask for every i, on the device
 void MurmurBatchGpu(const uint8_t* bytes, int64_t nbytes, const int64_t* offsets, int64_t n, uint32_t seed,
                     uint32_t mask, uint32_t* out);

@@ -9,12 +9,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <chrono>
 #include <cstdio>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -1048,24 +1050,127 @@ constexpr int kStageThreads = 8;
 // hipHostMalloc, which a per-learner stager paid again on every fit (the first chunk of a pass waited
 // ~17 ms for them, r5 pass 11 trace). Callers hold `mu` for a whole copy sequence; a buffer's event may
 // have been recorded on another learner's copy stream, and waiting on it is still correct.
+// A fixed team of kStageThreads - 1 helper threads (the caller is member 0) for the staging copies: a 32 MiB
+// piece used to start and join 8 std::threads, ~32 pieces per 1 GiB pass.
+class CopyTeam {
+ public:
+  CopyTeam() {
+    for (int t = 1; t < kStageThreads; ++t) th_.emplace_back([this, t] { Loop(t); });
+  }
+  ~CopyTeam() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  // fn(t) for t in [0, kStageThreads), t = 0 on the calling thread; returns when all have run
+  template <class F>
+  void Run(F&& fn) {
+    std::function<void(int)> job(std::forward<F>(fn));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &job;
+      pending_ = kStageThreads - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    job(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void Loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        job = job_;
+      }
+      (*job)(t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(int)>* job_ = nullptr;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 struct Stager {
   std::mutex mu;
   char* buf[kStage] = {};
   hipEvent_t ev[kStage] = {};
   bool used[kStage] = {};
   int next = 0;
+  CopyTeam* team = nullptr;  // made on the first large copy
+  int64_t unit_pieces = 0;   // value pieces sent as a device fill (all 1.0f), for the tests
   ~Stager() {
     for (int k = 0; k < kStage; ++k) {
       if (ev[k]) { (void)hipEventSynchronize(ev[k]); (void)hipEventDestroy(ev[k]); }
       if (buf[k]) (void)hipHostFree(buf[k]);
     }
+    delete team;
   }
-  // queue `bytes` from pageable `src` to device `dst` on stream s (caller holds mu)
-  void Copy(char* dst, const char* src, size_t bytes, hipStream_t s) {
+  CopyTeam& Team() {
+    if (!team) team = new CopyTeam();
+    return *team;
+  }
+  // true when every float of src[0, n) is 1.0f (bit pattern 0x3F800000); the team scans slices and stops at
+  // the first other value (non-unit data: after a few cache lines)
+  bool AllOnes(const float* src, size_t n) {
+    auto scan = [](const float* p, size_t m) {
+      const uint32_t* u = reinterpret_cast<const uint32_t*>(p);
+      size_t i = 0;
+      for (; i + 16 <= m; i += 16) {
+        uint32_t x = 0;
+        for (int j = 0; j < 16; ++j) x |= u[i + j] ^ 0x3F800000u;
+        if (x) return false;
+      }
+      for (; i < m; ++i)
+        if (u[i] != 0x3F800000u) return false;
+      return true;
+    };
+    if (n == 0) return true;
+    if (!scan(src, std::min<size_t>(n, 4096))) return false;  // the common non-unit case, on this thread
+    if (n < (size_t(1) << 18)) return scan(src, n);
+    std::atomic<bool> ok{true};
+    const size_t per = (n + kStageThreads - 1) / kStageThreads;
+    Team().Run([&](int t) {
+      const size_t a0 = t * per, a1 = std::min(n, a0 + per);
+      if (a0 < a1 && ok.load(std::memory_order_relaxed) && !scan(src + a0, a1 - a0)) ok = false;
+    });
+    return ok.load();
+  }
+  // queue `bytes` from pageable `src` to device `dst` on stream s (caller holds mu). unit_floats: the bytes are
+  // float values that are very often all 1.0f (binary hashed features): such a piece crosses PCIe as a device
+  // fill instead of its bytes.
+  void Copy(char* dst, const char* src, size_t bytes, hipStream_t s, bool unit_floats = false) {
     if (bytes == 0) return;
     // a null source or destination is a caller bug (round 4: a device scratch buffer "copied" from a null host
     // pointer segfaulted the staging threads) - refuse it here instead of faulting in a memcpy thread
     if (!src || !dst) throw std::invalid_argument("Stager::Copy: null source or destination for a non-empty copy");
+    if (unit_floats) {  // SML_VW_UNIT_FILL=0: always send the bytes (read per call: the tests A/B it)
+      const char* e = std::getenv("SML_VW_UNIT_FILL");
+      unit_floats = !(e && e[0] == '0');
+    }
+    if (unit_floats && bytes % sizeof(float) == 0 &&
+        AllOnes(reinterpret_cast<const float*>(src), bytes / sizeof(float))) {
+      VW_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dst), 0x3F800000, bytes / sizeof(float), s));
+      ++unit_pieces;
+      return;
+    }
     for (size_t off = 0; off < bytes; off += kStageBytes) {
       const int k = next;
       next = (next + 1) % kStage;
@@ -1079,12 +1184,12 @@ struct Stager {
         std::memcpy(buf[k], src + off, n);  // small pieces: a thread team costs more than the copy
       } else {
         const size_t per = (n + kStageThreads - 1) / kStageThreads;
-        std::vector<std::thread> th;
-        for (int t = 0; t < kStageThreads && t * per < n; ++t) {
+        char* b = buf[k];
+        const char* from = src + off;
+        Team().Run([=](int t) {
           const size_t a0 = t * per, a1 = std::min(n, a0 + per);
-          th.emplace_back([=]() { std::memcpy(buf[k] + a0, src + off + a0, a1 - a0); });
-        }
-        for (auto& x : th) x.join();
+          if (a0 < a1) std::memcpy(b + a0, from + a0, a1 - a0);
+        });
       }
       VW_HIP_CHECK(hipMemcpyAsync(dst + off, buf[k], n, hipMemcpyHostToDevice, s));
       VW_HIP_CHECK(hipEventRecord(ev[k], s));
@@ -1097,6 +1202,12 @@ struct Stager {
 static Stager& SharedStager() {
   static Stager* st = new Stager();  // never destroyed: pinned buffers live for the process
   return *st;
+}
+
+int64_t StagerUnitPieces() {
+  Stager& st = SharedStager();
+  std::lock_guard<std::mutex> lk(st.mu);
+  return st.unit_pieces;
 }
 
 // Host-only check of the staging guard (it throws before any HIP call, so it runs without a GPU).
@@ -1382,7 +1493,7 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
           st.Copy(reinterpret_cast<char*>(impl_->idx + p0), reinterpret_cast<const char*>(indices + indptr[0] + p0),
                   (p1 - p0) * sizeof(uint32_t), cs);
           st.Copy(reinterpret_cast<char*>(impl_->val + p0), reinterpret_cast<const char*>(values + indptr[0] + p0),
-                  (p1 - p0) * sizeof(float), cs);
+                  (p1 - p0) * sizeof(float), cs, /*unit_floats=*/true);
         }
         VW_HIP_CHECK(hipEventRecord(impl_->events[c], cs));
         std::lock_guard<std::mutex> g(rmu);
@@ -1451,7 +1562,7 @@ void GpuSgd::Stage(const int64_t* indptr, const uint32_t* indices, const float* 
     st.Copy(reinterpret_cast<char*>(impl_->idx), reinterpret_cast<const char*>(indices + indptr[0]),
             nnz * sizeof(uint32_t), cs);
     st.Copy(reinterpret_cast<char*>(impl_->val), reinterpret_cast<const char*>(values + indptr[0]), nnz * sizeof(float),
-            cs);
+            cs, /*unit_floats=*/true);
     VW_HIP_CHECK(hipStreamSynchronize(cs));
   }
   VW_HIP_CHECK(hipStreamSynchronize(s));
@@ -1635,7 +1746,7 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
               st.Copy(reinterpret_cast<char*>(u.idx + p0), reinterpret_cast<const char*>(b.idx + b.ip[0] + p0),
                       (p1 - p0) * sizeof(uint32_t), cs);
               st.Copy(reinterpret_cast<char*>(u.val + p0), reinterpret_cast<const char*>(b.val + b.ip[0] + p0),
-                      (p1 - p0) * sizeof(float), cs);
+                      (p1 - p0) * sizeof(float), cs, /*unit_floats=*/true);
             }
           }
           VW_HIP_CHECK(hipEventRecord(impl_->events[c], cs));

@@ -99,27 +99,57 @@ _COPY_POOL: Optional[ThreadPoolExecutor] = None
 
 
 def _parallel_copy(dst_views, srcs) -> None:
-    """dst_views[i][...] = srcs[i] on a small thread pool (numpy releases the GIL for plain copies): the host
-    side of a device batch is memory-bandwidth work, one core moves ~1-2 GB/s of fresh pages."""
+    """dst_views[i][...] = srcs[i] on a small thread pool (numpy releases the GIL for plain copies), in at most
+    16 tasks of consecutive images (a task per image cost more than its copy: r6 pass 19)."""
     global _COPY_POOL
-    if len(srcs) < 8:
+    n = len(srcs)
+    if n < 8:
         for d, a in zip(dst_views, srcs):
             d[...] = a
         return
     if _COPY_POOL is None:
         _COPY_POOL = ThreadPoolExecutor(max_workers=16)
+    nt = min(16, n)
 
-    def put(k):
-        dst_views[k][...] = srcs[k]
+    def put(t):
+        for k in range(n * t // nt, n * (t + 1) // nt):
+            dst_views[k][...] = srcs[k]
 
-    list(_COPY_POOL.map(put, range(len(srcs))))
+    list(_COPY_POOL.map(put, range(nt)))
+
+
+def _gather_images(dst: np.ndarray, arrays) -> None:
+    """dst[j] = arrays[j] for equally shaped uint8 images: one native call, copies spread over a thread team
+    with the GIL released (falls back to the pool for non-contiguous sources)."""
+    try:
+        if dst.dtype != np.uint8 or any(a.dtype != np.uint8 for a in arrays):
+            raise TypeError("non-uint8 image")
+        _img().gather_into(list(arrays), dst.ctypes.data, int(dst[0].nbytes))
+    except (ValueError, TypeError):
+        _parallel_copy([dst[j] for j in range(len(arrays))], list(arrays))
 
 
 def _bulk_copy(host: np.ndarray, n: int) -> np.ndarray:
-    """The first n images of a (reused) pinned slot copied into a fresh array, in parallel."""
+    """The first n images of a (reused) pinned slot copied into a fresh array, in parallel (native team)."""
     fresh = np.empty((n,) + host.shape[1:], dtype=host.dtype)
-    _parallel_copy([fresh[j] for j in range(n)], [host[j] for j in range(n)])
+    if n:
+        _img().copy_parallel(fresh.ctypes.data, host.ctypes.data, int(fresh.nbytes))
     return fresh
+
+
+def _image_rows(host: np.ndarray, n: int, origins) -> list:
+    """Image rows of the first n HWC images of a (reused) pinned slot: the rows' data bytes are made and
+    filled in parallel by one native call (numpy's tobytes per row held the GIL: ~27 us per 150 KB row)."""
+    if n == 0:
+        return []
+    h, w = int(host.shape[1]), int(host.shape[2])
+    c = int(host.shape[3]) if host.ndim == 4 else 1
+    if c not in (1, 3, 4):
+        return [make_image_row(host[j], origins[j]) for j in range(n)]
+    datas = _img().split_bytes(host.ctypes.data, n, h * w * c)
+    mode = {1: 0, 3: 16, 4: 24}[c]
+    return [{"origin": origins[j], "height": h, "width": w, "nChannels": c, "mode": mode, "data": datas[j]}
+            for j in range(n)]
 
 
 def _gpu_ok(device_type: str) -> bool:
@@ -341,7 +371,12 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         offsets[1:] = np.cumsum(sizes)[:-1]
         host = torch.empty(int(sum(sizes)), dtype=torch.uint8, pin_memory=True)
         hv = host.numpy()
-        _parallel_copy([hv[o:o + a.size] for a, o in zip(arrays, offsets)], [a.reshape(-1) for a in arrays])
+        try:  # back to back, one native call (the offsets are the running sizes)
+            if any(a.dtype != np.uint8 for a in arrays):
+                raise TypeError("non-uint8 image")
+            _img().gather_into(list(arrays), hv.ctypes.data, 0)
+        except (ValueError, TypeError):
+            _parallel_copy([hv[o:o + a.size] for a, o in zip(arrays, offsets)], [a.reshape(-1) for a in arrays])
         return self.device_tensors_packed(host, offsets, shapes, dtype, nhwc, src_rgb)
 
     def device_tensors_packed(self, host, offsets: np.ndarray, shapes: List[tuple], dtype: str = "float32",
@@ -492,9 +527,15 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
         def emit(host, idx):
             if float_tensor:  # one bulk copy out of the reused pinned slot; the rows are views of it
                 host = _bulk_copy(host, len(idx))
+            elif not to_tensor:  # image rows: their data bytes filled in parallel
+                rows = _image_rows(host, len(idx), [origins[i] for i in idx])
+                for j, i in enumerate(idx):
+                    out[i] = rows[j]
+                    done.add(i)
+                return
             for j, i in enumerate(idx):
                 a = host[j]
-                out[i] = a if float_tensor else (self._finish_host(a) if to_tensor else make_image_row(a, origins[i]))
+                out[i] = a if float_tensor else self._finish_host(a)
                 done.add(i)
 
         for shape, members in groups.items():
@@ -505,7 +546,7 @@ class ImageTransformer(Transformer, HasInputCol, HasOutputCol):
 
             def launch(idx, slot, ins=ins):
                 sv = ins[slot].numpy()
-                _parallel_copy([sv[j] for j in range(len(idx))], [arrays[i] for i in idx])
+                _gather_images(sv, [arrays[i] for i in idx])
                 x = self.run_stages_device(ins[slot][:len(idx)])
                 if x is None:
                     return None

@@ -348,3 +348,32 @@ def test_gpu_stage_kernels_reflect_and_tails():
         rs = torch.empty((2, 3, 5, c), dtype=torch.uint8, device="cuda")
         img.resize_batch_device(src.data_ptr(), 2, h, w, c, rs.data_ptr(), 3, 5, stream)
         np.testing.assert_array_equal(rs.cpu().numpy(), np.stack([img.resize(x, 3, 5).reshape(3, 5, c) for x in a]))
+
+
+def test_native_batch_copy_helpers():
+    """The host side of a device batch (transformer.py): images gathered into one buffer, per-row bytes split
+    out of it and a bulk copy, by the native thread team - the same bytes as the numpy copies they replace."""
+    import numpy as np
+
+    from synapseml_amd.image.transformer import _bulk_copy, _gather_images, _image_rows
+    from synapseml_amd.image.schema import make_image_row
+
+    rng = np.random.default_rng(4)
+    imgs = [rng.integers(0, 256, (61, 47, 3), dtype=np.uint8) for _ in range(40)]
+    srcs = [im if k % 2 else im.tobytes() for k, im in enumerate(imgs)]  # arrays and row bytes
+    dst = np.zeros((48, 61, 47, 3), np.uint8)
+    _gather_images(dst, [np.frombuffer(s, np.uint8).reshape(61, 47, 3) if isinstance(s, bytes) else s
+                         for s in srcs])
+    assert np.array_equal(dst[:40], np.stack(imgs)) and not dst[40:].any()
+    strided = [im[:, ::-1] for im in imgs[:9]]  # non-contiguous: the pool fallback
+    _gather_images(dst, strided)
+    assert np.array_equal(dst[:9], np.stack(strided))
+    _gather_images(dst, imgs)
+    rows = _image_rows(dst, 40, [f"o{k}" for k in range(40)])
+    for k in range(40):
+        assert rows[k] == make_image_row(imgs[k], f"o{k}")
+    gray = rng.integers(0, 256, (5, 33, 20), dtype=np.uint8)
+    assert _image_rows(gray, 5, list("abcde"))[3] == make_image_row(gray[3], "d")
+    big = rng.standard_normal((7, 3, 224, 224)).astype(np.float32)
+    out = _bulk_copy(big, 6)
+    assert np.array_equal(out, big[:6]) and not np.shares_memory(out, big)

@@ -397,3 +397,38 @@ def test_gpu_cats_batch1_parity(args):
     else:
         a = np.asarray(og["action"])
         assert ((a >= 0) & (a <= 20000)).all() and np.all(np.asarray(og["pdf"]) > 0)
+
+
+@pytest.mark.gpu
+def test_gpu_unit_values_cross_as_device_fill(monkeypatch):
+    """Binary hashed features (every value 1.0): the stager sends such value pieces as a device fill instead of
+    their bytes. Batch-1 fits with and without the fill give the same model bytes; a block with one other
+    value is sent as bytes."""
+    from synapseml_amd.core.linalg import CsrColumn
+
+    vw = native.load("_vw")
+    rng = np.random.default_rng(21)
+    n, k = 6000, 12
+    ip = np.arange(0, n * k + 1, k, dtype=np.int64)
+    idx = rng.integers(0, 1 << 20, size=n * k, dtype=np.int64).astype(np.uint32)
+    w = rng.standard_normal(1 << 20)
+    y = np.where(w[idx.reshape(n, k)].sum(1) > 0, 1.0, -1.0)
+    kw = dict(numBits=20, deviceType="gpu", gpuBatchSize=1, passThroughArgs="--loss_function logistic")
+    monkeypatch.setenv("SML_VW_STAGE_CHUNK_ROWS", "1000")
+    out = {}
+    for fill in ("1", "0"):
+        monkeypatch.setenv("SML_VW_UNIT_FILL", fill)
+        before = vw._stager_unit_pieces()
+        df = DataFrame({"features": CsrColumn(ip, idx, np.ones(n * k, np.float32), 1 << 32), "label": y})
+        m = VowpalWabbitClassifier(**kw).fit(df)
+        out[fill] = (m.getNativeModel(), vw._stager_unit_pieces() - before)
+    assert out["1"][1] > 0 and out["0"][1] == 0
+    assert bytes(out["1"][0]) == bytes(out["0"][0])
+    val = np.ones(n * k, np.float32)
+    val[-1] = 2.0  # the last piece is not all ones
+    monkeypatch.setenv("SML_VW_UNIT_FILL", "1")
+    df = DataFrame({"features": CsrColumn(ip, idx, val, 1 << 32), "label": y})
+    a = VowpalWabbitClassifier(**kw).fit(df)
+    monkeypatch.setenv("SML_VW_UNIT_FILL", "0")
+    b = VowpalWabbitClassifier(**kw).fit(df)
+    assert bytes(a.getNativeModel()) == bytes(b.getNativeModel())
