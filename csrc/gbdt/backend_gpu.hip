@@ -2526,8 +2526,8 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     BState* __restrict__ bs, BNode* __restrict__ nodes, SplitResult* __restrict__ nbest,
     const SplitResult* __restrict__ fbest, int F, const double2* __restrict__ part, int E,
     const DLeaf* __restrict__ leaves, DState* __restrict__ st, DTree t, FeatMeta fm, const int8_t* __restrict__ mono,
-    int has_mono, int first, int spec_k, int budget, int part_tile, int cap_nodes, int* __restrict__ host_flag,
-    long long* __restrict__ prof) {
+    int has_mono, int first, int spec_k, int spec_max, int wide_div, int budget, int part_tile, int cap_nodes,
+    int* __restrict__ host_flag, long long* __restrict__ prof) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int kWaves = kPlanThreads / 64;
   // SML_BPLAN_PROF: thread 0 stamps the real-time clock at the phase boundaries (entry, absorbed, staged,
@@ -2538,6 +2538,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   __shared__ int s_c0[kBatchMaxNodes], s_c1[kBatchMaxNodes], s_pop[kBatchMaxNodes];
   __shared__ int p_node[kBatchMaxLeaves], p_li[kBatchMaxLeaves];
   __shared__ int ch_node[kMaxSpec];
+  __shared__ long long s_cnt[kBatchMaxNodes];  // every node's global row count (the adaptive round width)
   __shared__ int s_rp[2], s_hdr[7];  // done, nnodes, nexp, cap_exp, expanded, spec_used, cap_nodes
   __shared__ int s_nb[kPlanFm], s_mt[kPlanFm], s_db[kPlanFm];
   // ---- phase 0: every load that does not depend on this round's header (done / nnodes / nexp) goes out
@@ -2550,7 +2551,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   // into nbest after it, off the replay's path - the plan reads a child absorbed this round from fbest)
   // absorbing waves 1 .. kWaves - 1 take children cw and cw + kAbs (two each at 8 expansions per round)
   constexpr int kAbs = kWaves - 1;
-  const bool fast = F <= 64 && 2 * spec_k <= 2 * kAbs;
+  const bool fast = F <= 64 && spec_max <= kAbs;
   const int cw = wid - 1;  // fast path: this wave's first child
   __shared__ int s_src[kBatchMaxNodes];  // fbest record of a node absorbed this round (fast path), else -1
   int x_c0[2] = {0, 0}, x_c1[2] = {0, 0}, x_ls[2] = {0, 0}, x_pb[2] = {0, 0}, x_pc[2] = {0, 0};
@@ -2581,6 +2582,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       s_hdr[3] = 2 * budget + kMaxSpec; s_hdr[4] = 0; s_hdr[5] = 0;
       s_hdr[6] = min(kBatchMaxNodes, 1 + 2 * s_hdr[3]);
       s_c0[0] = -1; s_c1[0] = -1; s_pop[0] = -1; s_src[0] = -1;
+      s_cnt[0] = R.gcount;
     }
     if (fast && cw == 0 && lane < F) { rfeat[0] = fbest[lane].feature; rgain[0] = fbest[lane].gain; }
   } else {
@@ -2591,7 +2593,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = cw + q * kAbs;
-      if (fast && cw >= 0 && c < 2 * spec_k) {
+      if (fast && cw >= 0 && c < 2 * spec_max) {
         if (lane == 0) load_exp(c, q);
         if (lane < F) { rfeat[q] = fbest[c * F + lane].feature; rgain[q] = fbest[c * F + lane].gain; }
       }
@@ -2601,6 +2603,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       s_gain[i] = r.feature >= 0 ? r.gain : -INFINITY;
       s_c0[i] = nodes[i].c0;
       s_c1[i] = nodes[i].c1;
+      s_cnt[i] = nodes[i].gcount;
       s_pop[i] = -1;
       s_src[i] = -1;
     }
@@ -2644,6 +2647,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
     nd.count = is_left ? lt[q] : x_pc[q] - lt[q];
     nd.buf = x_buf[q] == 0 ? 1 : 0;
     nd.gcount = (c & 1) ? x_pg[q] - small_cnt[q] : small_cnt[q];
+    s_cnt[id] = nd.gcount;
   };
   // fast path: the records this wave copies into nbest after the barrier
   int copy_src[2] = {-1, -1}, copy_id[2] = {0, 0};
@@ -2733,6 +2737,13 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
   const long long c_start = prof != nullptr ? static_cast<long long>(__builtin_amdgcn_s_memtime()) : 0;
   const int spec_room = max(1, min(spec_k, s_hdr[3] - s_hdr[4]));
   const bool may_spec = s_hdr[5] < budget && nnodes + 2 * spec_k <= s_hdr[6];
+  // adaptive width: past spec_k, keep taking the replay's next unexplored nodes (up to spec_max) while the
+  // round's expansions hold at most 1 / wide_div of the rows - late rounds are latency-bound (5-40 us per
+  // kernel whatever their size), so a wider round costs little and saves whole rounds
+  const int wide_room = max(1, min(spec_max, s_hdr[3] - s_hdr[4]));
+  const bool may_wide = wide_div > 0 && may_spec && nnodes + 2 * spec_max <= s_hdr[6];
+  const long long wide_rows = wide_div > 0 ? s_cnt[0] / wide_div : 0;
+  long long srows = 0;
   constexpr int kFrontCap = kSlots * 64 < kBatchMaxLeaves ? kSlots * 64 : kBatchMaxLeaves;
   while (pops < budget) {
     // the sequential argmax: larger gain, then smaller leaf index (leaf indices are distinct)
@@ -2807,7 +2818,9 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       if (lane == 0) ch_node[nch] = v;
       --nf;
       ++nch;
-      if (nch >= spec_room || !may_spec) { ++pops; break; }
+      srows += s_cnt[v];
+      const bool wide = may_wide && nch < wide_room && srows <= wide_rows;
+      if ((nch >= spec_room && !wide) || !may_spec) { ++pops; break; }
     }
     ++pops;
     WaveSync();
@@ -3711,6 +3724,14 @@ class GpuBackend : public TrainBackend {
     if (const char* e = std::getenv("SML_GBDT_SPEC")) spec_k_ = std::atoi(e);
     batch_ok_ = spec_k_ > 0 && L_ <= kBatchMaxLeaves && !(cfg.tree_learner == "voting" && comm_ && comm_->world() > 1);
     spec_k_ = std::max(1, std::min(kMaxSpec, spec_k_));
+    // adaptive round width (bplan_kernel): rounds whose expansions hold <= 1 / wide_div of the rows may take up
+    // to spec_max expansions (SML_GBDT_WIDE=<divisor>, 0 = fixed width; SML_GBDT_SPEC_MAX caps it; <= 15, the
+    // plan's absorbing waves)
+    wide_div_ = 0;
+    if (const char* e = std::getenv("SML_GBDT_WIDE")) wide_div_ = std::max(0, std::atoi(e));
+    spec_max_ = wide_div_ > 0 ? 2 * spec_k_ : spec_k_;
+    if (const char* e = std::getenv("SML_GBDT_SPEC_MAX")) spec_max_ = std::atoi(e);
+    spec_max_ = std::max(spec_k_, std::min(std::min(kMaxSpec, kPlanThreads / 64 - 1), spec_max_));
     if (const char* e = std::getenv("SML_GBDT_LOOKAHEAD")) blook_ = std::max(1, std::min(4, std::atoi(e)));
     const int cap_nodes = std::min(kBatchMaxNodes, 1 + 2 * (2 * (L_ - 1) + kMaxSpec));
     // histogram + (row count, 0) per expansion of a round
@@ -4297,7 +4318,8 @@ class GpuBackend : public TrainBackend {
       auto plan = L_ <= 64 ? bplan_kernel<1> : (L_ <= 128 ? bplan_kernel<2> : bplan_kernel<4>);
       hipLaunchKernelGGL(plan, dim3(1), dim3(kPlanThreads), 0, stream_, bstate_.get(), bnodes_.get(),
                          nbest_.get(), fbest_.get(), F_, part_.get(), E_, leaves_.get(), state_, dt_, fm_, mono_.get(),
-                         sp_.has_mono, r == 0 ? 1 : 0, spec_k_, budget, part_tile, plan_cap_, bflag_dev_ + r % kBRing,
+                         sp_.has_mono, r == 0 ? 1 : 0, spec_k_, spec_max_, wide_div_, budget, part_tile, plan_cap_,
+                         bflag_dev_ + r % kBRing,
                          bprof_ ? bprof_ + kPlanProfStride * r : nullptr);
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(bev_[r % kBRing], stream_));
@@ -4317,12 +4339,12 @@ class GpuBackend : public TrainBackend {
       // build - measured 1.86-1.91 ms/iter against 1.51 on one stream: the cross-stream event waits of every
       // round cost more than the overlap gains; r6 pass 8)
       part_hist(0, kMaxSpec, stream_, 0);
-      hipLaunchKernelGGL(breduce_kernel, dim3((E_ + kRedE - 1) / kRedE, spec_k_), dim3(kRedE * kRedG), 0, stream_,
+      hipLaunchKernelGGL(breduce_kernel, dim3((E_ + kRedE - 1) / kRedE, spec_max_), dim3(kRedE * kRedG), 0, stream_,
                          bstate_.get(), slab_.get(), E_, ghmax, part_.get(), scale_n_, Distributed() ? 1 : 0, 0);
       SML_HIP_CHECK(hipGetLastError());
       // every expansion's smaller-child histogram + row count in ONE exact int64 collective per round
-      if (Distributed()) ExactAllReduce(spec_k_, ghmax, &bstate_.get()->nexp);
-      hipLaunchKernelGGL(bfind_kernel, dim3(F_, 2 * spec_k_), dim3(256), 0, stream_, bstate_.get(), bnodes_.get(),
+      if (Distributed()) ExactAllReduce(spec_max_, ghmax, &bstate_.get()->nexp);
+      hipLaunchKernelGGL(bfind_kernel, dim3(F_, 2 * spec_max_), dim3(256), 0, stream_, bstate_.get(), bnodes_.get(),
                          part_.get(), E_, hist_pool_.get(), fm_, sp_, fbest_.get(), F_);
       SML_HIP_CHECK(hipGetLastError());
     }
@@ -4942,6 +4964,7 @@ class GpuBackend : public TrainBackend {
   static constexpr int kBRing = 8;
   bool batch_ok_ = false;
   int spec_k_ = 4;
+  int spec_max_ = 4, wide_div_ = 0;  // adaptive round width (bplan_kernel)
   int blook_ = 1;
   DevBuf<BState> bstate_;
   DevBuf<BNode> bnodes_;

@@ -703,6 +703,26 @@ def test_gpu_batched_growth_equals_sequential(extra, spec, monkeypatch):
 
 @pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5",
                                    "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
+                                   "num_leaves=31 objective=multiclass num_class=3"])
+@pytest.mark.parametrize("wide,spec_max", [("16", "8"), ("1", "15"), ("4", "6")])
+def test_gpu_adaptive_round_width_equals_sequential(extra, wide, spec_max, monkeypatch):
+    """Adaptive round width (SML_GBDT_WIDE=d: a round whose expansions hold <= 1/d of the rows keeps
+    speculating up to SML_GBDT_SPEC_MAX expansions; d = 1 widens every round): byte-identical models to
+    one-split growth, through the plan's slow absorb path (more than 15 children) and the fast one."""
+    X, y = _data(n=80000, nan_frac=0.02, cat="categorical" in extra)
+    if "multiclass" in extra:
+        y = (np.digitize(np.nan_to_num(X[:, 0] + X[:, 1]), [-0.5, 0.5])).astype(np.float32)
+    p = ("objective=binary " if "objective" not in extra else "") + f"learning_rate=0.2 {extra} device_type=gpu"
+    monkeypatch.setenv("SML_GBDT_SPEC", "0")
+    seq = _train(X, y, p, 6).save_model_string()
+    monkeypatch.setenv("SML_GBDT_SPEC", "4")
+    monkeypatch.setenv("SML_GBDT_WIDE", wide)
+    monkeypatch.setenv("SML_GBDT_SPEC_MAX", spec_max)
+    assert _train(X, y, p, 6).save_model_string() == seq
+
+
+@pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5",
+                                   "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
                                    "num_leaves=31 objective=cross_entropy", "num_leaves=31 objective=regression"])
 def test_gpu_index_only_partition_equals_ordered_gradients(extra, monkeypatch):
     """SML_GBDT_IDX=1 (the default): the batched partition moves row ids only and bhist gathers (g, h) from the
