@@ -781,3 +781,11 @@ def test_num_tasks_fit_fans_out_on_gpu():
     assert len(est.getTaskMeasures()) == 2
     # int64 histograms under a global scale: the 2-task model is bitwise the 1-task model
     assert m2.getNativeModel().split("parameters:")[0] == m1.getNativeModel().split("parameters:")[0]
+
+
+def test_gpu_small_hessian_leaves_match_fp64():
+    """The device histograms' fixed-point scale on confident binary predictions: leaf values equal
+    the fp64 sums over the routed rows (tests/test_lightgbm.py::_small_hessian_leaf_check)."""
+    from tests.test_lightgbm import _small_hessian_leaf_check
+
+    _small_hessian_leaf_check("gpu")
