@@ -431,7 +431,17 @@ bool GroupRuns(const int64_t* a, int64_t n, std::vector<int64_t>* starts) {
 void Dataset::SetLabel(const float* y, int64_t n) {
   if (n != num_data) throw std::runtime_error("label size mismatch");
   label.resize(static_cast<size_t>(n));
-  std::copy(y, y + n, label.begin());
+  float* dst = label.data();
+  if (n >= (int64_t(1) << 20)) {  // 11M labels: ~4 ms on one thread
+    const int nt = std::min<int>(8, omp_get_max_threads());
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int t = 0; t < nt; ++t) {
+      const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+      std::memcpy(dst + a, y + a, sizeof(float) * (b - a));
+    }
+  } else {
+    std::copy(y, y + n, dst);
+  }
   label_set = true;
 }
 

@@ -602,20 +602,8 @@ class LightGBMBase(Estimator, LightGBMParams):
 
     def _build_dataset(self, g, ref, df: DataFrame, kind, data, n, num_class, upload=None):
         ds = g.Dataset(ref, n)
-        if kind == "dense":
-            # K1: large dense partitions are bin-encoded on the MI355X (bit-identical with the host encoder)
-            on_gpu = n >= (1 << 16) and self.getDeviceType() == "gpu" and native.gpu_available()
-            if upload is not None:
-                ds.push_device_rows(upload, 0)
-            elif on_gpu:
-                ds.push_dense_gpu(data, 0)
-            else:
-                chunk = 1 << 20
-                for s in range(0, n, chunk):
-                    ds.push_dense(data[s: s + chunk], s)
-        else:
-            indptr, indices, values, _ = data
-            ds.push_csr(indptr, indices, values, 0)
+        # the per-row columns first: with a background upload in flight (K1 staging) their host copies run
+        # while the feature bytes cross PCIe instead of after the encode (~4 ms for 11M labels)
         ds.set_label(self._labels(df))
         wcol = self.getWeightCol()
         if wcol and wcol in df:
@@ -637,6 +625,20 @@ class LightGBMBase(Estimator, LightGBMParams):
             starts = _group_runs(vals)[0] if len(vals) else np.zeros(0, np.int64)
             sizes = np.diff(np.append(starts, len(vals)))
             ds.set_group(np.asarray(sizes, dtype=np.int32))
+        if kind == "dense":
+            # K1: large dense partitions are bin-encoded on the MI355X (bit-identical with the host encoder)
+            on_gpu = n >= (1 << 16) and self.getDeviceType() == "gpu" and native.gpu_available()
+            if upload is not None:
+                ds.push_device_rows(upload, 0)
+            elif on_gpu:
+                ds.push_dense_gpu(data, 0)
+            else:
+                chunk = 1 << 20
+                for s in range(0, n, chunk):
+                    ds.push_dense(data[s: s + chunk], s)
+        else:
+            indptr, indices, values, _ = data
+            ds.push_csr(indptr, indices, values, 0)
         return ds
 
     def _labels(self, df: DataFrame) -> np.ndarray:

@@ -543,9 +543,12 @@ def _small_hessian_leaf_check(device: str):
     ds.push_dense(X, 0)
     ds.set_label(y)
     b = g.Booster(ds, p, None)
-    for _ in range(25):
+    for _ in range(24):
         b.update()
-    gg, hh = b.gradients()  # the gradients the 25th tree was grown from
+    # the 25th tree from explicit float32 gradients of the current (confident) scores, on either backend
+    prob = 1.0 / (1.0 + np.exp(-np.asarray(b.train_scores(), np.float64)))
+    gg, hh = (prob - y).astype(np.float32), (prob * (1.0 - prob)).astype(np.float32)
+    b.update(gg, hh)
     leaf = b.predict(X, 2, 24, 1)[:, 0].astype(int)
     vals = {}
 
