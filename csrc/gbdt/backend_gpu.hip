@@ -118,6 +118,7 @@ struct DTree {  // device tree arrays (capacity L)
   int64_t* lcount;      // L
   int32_t* lparent;     // L
   int32_t* ldepth;      // L
+  int4* lseg;           // L (batched growth, may be null): leaf li's node (w) and row segment (begin, count, buffer)
   double out_l1, out_l2, out_mds;  // leaf-output regularisation: the root's value (its internal value once split)
 };
 
@@ -2878,6 +2879,7 @@ __global__ __launch_bounds__(kPlanThreads) void bplan_kernel(
       t.lweight[li] = L.sum_h;
       t.lcount[li] = L.gcount;
       t.ldepth[li] = L.depth;
+      if (t.lseg) t.lseg[li] = make_int4(L.begin, L.count, L.buf, v);
     }
     // parent of each leaf: the pop that created it (leaf index li of a child of pop i: left = p_li[i], right = i+1)
     for (int i = lane; i < pops; i += 64) {
@@ -3435,7 +3437,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     DevTreeView tv, DevTreeSrc src, const uint4* __restrict__ bins4, int W4, int F, int32_t n, double scale,
     double* __restrict__ score, ObjParams p, const float* __restrict__ label, const float* __restrict__ weight,
     float* __restrict__ g, float* __restrict__ h, const float* __restrict__ bound, float* __restrict__ partial,
-    ulonglong2* __restrict__ slab, int64_t scale_n) {
+    ulonglong2* __restrict__ slab, int64_t scale_n, const uint8_t* __restrict__ row_leaf) {
   constexpr int kThreads = kHistBlockThreads;
   const int nb_active = HistBlocks(n);
   if (static_cast<int>(blockIdx.x) >= nb_active) return;
@@ -3468,13 +3470,20 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   const int rot = tid & 15;
   float mg = 0.f, mh = 0.f;
   // one row of the pass: walk the tree, update the score, gradients, histogram
-  auto row = [&](int i, const uint4& r0, const uint4& r1, double sv, float yv, float wv) {
-    int node = ni > 0 ? 0 : ~0;
-    for (int guard = 0; node >= 0 && guard < num_leaves; ++guard) {
-      const int4 nd = snodes[node];
-      node = NodeStep(nd, ByteOfRow(r0, r1, nd.x & 0xFFFF), cat_bits, node);
+  // row_leaf (batched growth, no bagging): every row's leaf in the tree just grown, scattered from the final
+  // leaves' row segments by leaf_scatter_kernel - no per-row walk (the walk was ~68 of this pass's 236 us at
+  // 11M x 28: a divergent loop of dependent LDS node reads; r6 pass 23)
+  auto row = [&](int i, const uint4& r0, const uint4& r1, double sv, float yv, float wv, int lf) {
+    int li = lf;
+    if (!row_leaf) {
+      int node = ni > 0 ? 0 : ~0;
+      for (int guard = 0; node >= 0 && guard < num_leaves; ++guard) {
+        const int4 nd = snodes[node];
+        node = NodeStep(nd, ByteOfRow(r0, r1, nd.x & 0xFFFF), cat_bits, node);
+      }
+      li = ni > 0 ? ~node : 0;
     }
-    const double sn = sv + scale * slval[ni > 0 ? ~node : 0];
+    const double sn = sv + scale * slval[li];
     score[i] = sn;
     float gg, hh;
     PointGradient(p, sn, yv, wv, &gg, &hh);
@@ -3491,7 +3500,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
   if constexpr (kPipe) {
     // the next step's bins / score / label / weight are loaded before this step's rows are processed
     constexpr int kStep = kThreads * kUnroll;
-    auto load = [&](int base, uint4* b0, uint4* b1, double* s, float* y, float* w) {
+    auto load = [&](int base, uint4* b0, uint4* b1, double* s, float* y, float* w, int* lf) {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int i = base + u * kThreads;
@@ -3502,30 +3511,35 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
         s[u] = ok ? score[i] : 0.0;
         y[u] = ok ? label[i] : 0.f;
         w[u] = ok && weight ? weight[i] : 1.f;
+        lf[u] = ok && row_leaf ? row_leaf[i] : 0;
       }
     };
     uint4 b0[kUnroll], b1[kUnroll];
     double s[kUnroll];
     float y[kUnroll], w[kUnroll];
+    int lf[kUnroll];
     int base = p0 + tid;
-    load(base, b0, b1, s, y, w);
+    load(base, b0, b1, s, y, w, lf);
     for (; base < p1; base += kStep) {
       uint4 n0[kUnroll], n1[kUnroll];
       double ns[kUnroll];
       float ny[kUnroll], nw[kUnroll];
-      load(base + kStep, n0, n1, ns, ny, nw);
+      int nl[kUnroll];
+      load(base + kStep, n0, n1, ns, ny, nw, nl);
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)
-        if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u]);
+        if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u], lf[u]);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) { b0[u] = n0[u]; b1[u] = n1[u]; s[u] = ns[u]; y[u] = ny[u]; w[u] = nw[u]; }
+      for (int u = 0; u < kUnroll; ++u) {
+        b0[u] = n0[u]; b1[u] = n1[u]; s[u] = ns[u]; y[u] = ny[u]; w[u] = nw[u]; lf[u] = nl[u];
+      }
     }
   }
   for (int base = kPipe ? p1 : p0 + tid; base < p1; base += kThreads * kUnroll) {
     uint4 b0[kUnroll], b1[kUnroll];
     double s[kUnroll];
     float y[kUnroll], w[kUnroll];
-    int iq[kUnroll];
+    int iq[kUnroll], lf[kUnroll];
     // branch-free loads: rows past p1 read row p0 and are skipped below (no guarded load to wait out)
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
@@ -3538,6 +3552,7 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
       s[u] = score[iq[u]];
       y[u] = label[iq[u]];
       w[u] = 1.f;
+      lf[u] = row_leaf ? row_leaf[iq[u]] : 0;
     }
     if (weight) {
 #pragma unroll
@@ -3548,12 +3563,91 @@ __global__ __launch_bounds__(kHistBlockThreads) void score_grad_hist_kernel(
     // all 32 slots (b1 = 0 when F <= 16: bin 0 of unused slots): one code path keeps this kernel unspilled
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
-      if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u]);
+      if (base + u * kThreads < p1) row(base + u * kThreads, b0[u], b1[u], s[u], y[u], w[u], lf[u]);
   }
   BlockMaxPartial(mg, mh, partial);  // ends with a block barrier before thread 0 stores
   __syncthreads();
   SlabWrite<kFeatPerGroup, kThreads>(slab + static_cast<size_t>(blockIdx.x) * F * kBinsPerFeature, shg, shh, F, 0, F,
                                      tid);
+}
+
+// Every row's leaf in the tree batched growth just finished, for the fused score pass. A node's row segment is
+// intact only while it has no descendants (a descendant's partition rewrites part of its range in the node's
+// own buffer), and a final leaf may have some: the speculative continuation of a round's replay can pop an
+// explored node and expand its children, and that node can still end up a leaf. The nodes never expanded
+// are the finest partition - their segments tile [0, n) and are intact - so each of them is labelled with the
+// final leaf it lies under (climbing parent links to the first node that is a final leaf), and the table is
+// sorted by segment begin for leaf_scatter_kernel.
+constexpr int kLeafTableThreads = 1024;
+__global__ __launch_bounds__(kLeafTableThreads) void leaf_table_kernel(const BState* __restrict__ bs,
+                                                                      const BNode* __restrict__ nodes,
+                                                                      const DState* __restrict__ st,
+                                                                      const int4* __restrict__ lseg,
+                                                                      int4* __restrict__ rtab, int* __restrict__ rcount) {
+  __shared__ int s_par[kBatchMaxNodes], s_lab[kBatchMaxNodes];
+  __shared__ int4 s_ent[kBatchMaxNodes];
+  __shared__ int s_m;
+  const int tid = threadIdx.x;
+  const int nn = min(bs->nnodes, kBatchMaxNodes);
+  const int nl = min(st->num_leaves, kBatchMaxLeaves);
+  if (tid == 0) s_m = 0;
+  for (int x = tid; x < nn; x += kLeafTableThreads) { s_par[x] = -1; s_lab[x] = -1; }
+  __syncthreads();
+  for (int x = tid; x < nn; x += kLeafTableThreads) {
+    const int c0 = nodes[x].c0, c1 = nodes[x].c1;
+    if (c0 >= 0 && c0 < nn) s_par[c0] = x;
+    if (c1 >= 0 && c1 < nn) s_par[c1] = x;
+  }
+  for (int li = tid; li < nl; li += kLeafTableThreads) {
+    const int v = lseg[li].w;
+    if (v >= 0 && v < nn) s_lab[v] = li;
+  }
+  __syncthreads();
+  for (int y = tid; y < nn; y += kLeafTableThreads) {
+    const BNode b = nodes[y];
+    if (b.c0 >= 0 || b.count <= 0) continue;  // expanded, or no local rows
+    int z = y, guard = 0;
+    while (z >= 0 && s_lab[z] < 0 && guard++ < kBatchMaxNodes) z = s_par[z];
+    if (z < 0 || s_lab[z] < 0) continue;  // (a subtree of no final leaf: not reachable for a finished tree)
+    const int k = atomicAdd(&s_m, 1);
+    s_ent[k] = make_int4(b.begin, b.count, b.buf, s_lab[z]);
+  }
+  __syncthreads();
+  const int m = s_m;
+  for (int k = tid; k < m; k += kLeafTableThreads) {  // rank by begin (distinct: the segments tile [0, n))
+    const int bk = s_ent[k].x;
+    int r = 0;
+    for (int q = 0; q < m; ++q) r += s_ent[q].x < bk ? 1 : 0;
+    rtab[r] = s_ent[k];
+  }
+  if (tid == 0) *rcount = m;
+}
+
+// row_leaf[perm[buf][k]] = label of the table segment holding position k (buf < 0: the root's physical order)
+__global__ __launch_bounds__(256) void leaf_scatter_kernel(const int4* __restrict__ rtab, const int* __restrict__ rcount,
+                                                           const int32_t* __restrict__ perm0,
+                                                           const int32_t* __restrict__ perm1, int32_t n,
+                                                           uint8_t* __restrict__ row_leaf) {
+  __shared__ int s_beg[kBatchMaxNodes], s_buf[kBatchMaxNodes], s_lab[kBatchMaxNodes];
+  const int m = min(*rcount, kBatchMaxNodes);
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    const int4 e = rtab[i];
+    s_beg[i] = e.x;
+    s_buf[i] = e.z;
+    s_lab[i] = e.w;
+  }
+  __syncthreads();
+  if (m == 0) return;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    int lo = 0, hi = m - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_beg[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    const int buf = s_buf[lo];
+    const int row = buf < 0 ? k : (buf == 0 ? perm0[k] : perm1[k]);
+    row_leaf[row] = static_cast<uint8_t>(s_lab[lo]);
+  }
 }
 
 // (g, h) <-> the interleaved copy the index-only partition's histograms gather from
@@ -3910,6 +4004,13 @@ class GpuBackend : public TrainBackend {
     int64_t* tl = reinterpret_cast<int64_t*>(blob_.get() + off_tl_);
     dt_.icount = tl; dt_.lcount = tl + NI;
     dt_.out_l1 = sp_.lambda_l1; dt_.out_l2 = sp_.lambda_l2; dt_.out_mds = sp_.max_delta_step;
+    dt_.lseg = nullptr;
+    if (batch_ok_ && L_ <= kBatchMaxLeaves && row_leaf_on_) {
+      lseg_.alloc(L_);
+      row_leaf_.alloc(n_);
+      rtab_.alloc(kBatchMaxNodes + 1);  // the sorted segment table, then its length
+      dt_.lseg = lseg_.get();
+    }
     // score-update tree (uploaded from host trees)
     up_blob_.alloc(static_cast<size_t>(NI + 1) * (16 + 32) + static_cast<size_t>(L_ + 4) * 8);
     leaf_idx_.alloc(n_);
@@ -4180,7 +4281,20 @@ class GpuBackend : public TrainBackend {
     AccountScoreTime();  // the previous pass (done before this growth) frees the event pair
     DevTreeSrc src{dt_, state_ + final_v_, fm_.num_bin, fm_.missing, fm_.default_bin, shrink};
     if (prep_armed_ && k == 0 && K_ == 1) {
-      LaunchPrep(DevTreeView{}, src, 1.0);
+      // every row was partitioned (no bag): its leaf comes from the final leaves' segments, not a tree walk
+      const uint8_t* rl = nullptr;
+      if (grew_batched_ && bag_n_ < 0 && dt_.lseg) {
+        hipLaunchKernelGGL(leaf_table_kernel, dim3(1), dim3(kLeafTableThreads), 0, stream_, bstate_.get(),
+                           bnodes_.get(), state_ + final_v_, dt_.lseg, rtab_.get(), rtab_.get() == nullptr ? nullptr
+                           : reinterpret_cast<int*>(rtab_.get() + kBatchMaxNodes));
+        SML_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(leaf_scatter_kernel, dim3(std::min(GridFor(n_), 2048)), dim3(256), 0, stream_, rtab_.get(),
+                           reinterpret_cast<const int*>(rtab_.get() + kBatchMaxNodes), perm_[0].get(), perm_[1].get(),
+                           static_cast<int32_t>(n_), row_leaf_.get());
+        SML_HIP_CHECK(hipGetLastError());
+        rl = row_leaf_.get();
+      }
+      LaunchPrep(DevTreeView{}, src, 1.0, rl);
     } else {
       // any other objective: the plain score update, still without the host round trip
       prep_valid_ = root_ready_ = false;
@@ -4200,6 +4314,7 @@ class GpuBackend : public TrainBackend {
 
   void GrowTree(int k, const std::vector<char>& fmask_in) {
     SML_HIP_CHECK(hipEventRecord(ev_[0], stream_));
+    grew_batched_ = false;
     std::vector<int8_t> fmask(F_, 1);
     for (int f = 0; f < F_ && f < static_cast<int>(fmask_in.size()); ++f) fmask[f] = fmask_in[f] ? 1 : 0;
     sp_.tree_seq = tree_seq_++;
@@ -4254,6 +4369,7 @@ class GpuBackend : public TrainBackend {
         gh2_valid_ = true;
       }
       GrowBatched(g, h, idx);
+      grew_batched_ = true;
       final_v_ = 0;
       SML_HIP_CHECK(hipEventRecord(ev_[1], stream_));
       return;
@@ -4474,7 +4590,7 @@ class GpuBackend : public TrainBackend {
   // device time of the last score update; call only after a stream sync
   // score update + next gradients + next root histogram in one pass (score_grad_hist_kernel) with
   // the uploaded host tree `tv` or, when src.st is set, the device tree just grown
-  void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale) {
+  void LaunchPrep(const DevTreeView& tv, const DevTreeSrc& src, double scale, const uint8_t* row_leaf = nullptr) {
     if (src.st) SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
     // index-only partition: the pass writes the interleaved (g, h) copy instead of g_ / h_ (same bytes)
     const bool gh2 = idx_ok_ && batch_ok_;
@@ -4487,7 +4603,8 @@ class GpuBackend : public TrainBackend {
                        reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, static_cast<int32_t>(n_), scale,
                        score_.get(), prep_params_, label_.get(), weight_.get(),
                        gh2 ? reinterpret_cast<float*>(gh2_.get()) : g_.get(), h_.get(),
-                       reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get(), scale_n_);
+                       reinterpret_cast<const float*>(ghbound_.get()), ghmax_partial_.get(), slab_.get(), scale_n_,
+                       row_leaf);
     SML_HIP_CHECK(hipGetLastError());
     gh2_valid_ = gh2;
     g_stale_ = gh2;
@@ -4965,6 +5082,12 @@ class GpuBackend : public TrainBackend {
   bool batch_ok_ = false;
   int spec_k_ = 4;
   int spec_max_ = 4, wide_div_ = 0;  // adaptive round width (bplan_kernel)
+  // the fused score pass reads every row's leaf from row_leaf_ (leaf_scatter_kernel) after batched growth;
+  // SML_GBDT_ROW_LEAF=0 walks the tree per row instead
+  bool row_leaf_on_ = !(std::getenv("SML_GBDT_ROW_LEAF") && std::atoi(std::getenv("SML_GBDT_ROW_LEAF")) == 0);
+  bool grew_batched_ = false;
+  DevBuf<int4> lseg_, rtab_;
+  DevBuf<uint8_t> row_leaf_;
   int blook_ = 1;
   DevBuf<BState> bstate_;
   DevBuf<BNode> bnodes_;

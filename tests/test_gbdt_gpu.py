@@ -789,3 +789,26 @@ def test_gpu_small_hessian_leaves_match_fp64():
     from tests.test_lightgbm import _small_hessian_leaf_check
 
     _small_hessian_leaf_check("gpu")
+
+
+@pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5", "num_leaves=2",
+                                   "num_leaves=31 objective=cross_entropy",
+                                   "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
+                                   "num_leaves=31 bagging_fraction=0.7 bagging_freq=1"])
+def test_gpu_row_leaf_scatter_equals_tree_walk(extra, monkeypatch):
+    """After batched growth the fused score pass reads every row's leaf from the final leaves' row segments
+    (leaf_scatter_kernel) instead of walking the tree per row: bitwise the same scores, gradients and models
+    (SML_GBDT_ROW_LEAF=0 walks); bagged trees keep the walk (out-of-bag rows are not partitioned)."""
+    X, y = _data(n=80000, nan_frac=0.02, cat="categorical" in extra)
+    p = ("objective=binary " if "objective" not in extra else "") + f"learning_rate=0.2 {extra} device_type=gpu"
+
+    def fit(v):
+        monkeypatch.setenv("SML_GBDT_ROW_LEAF", v)
+        return _train(X, y, p, 8)
+
+    a, b = fit("1"), fit("0")
+    assert a.save_model_string() == b.save_model_string()
+    np.testing.assert_array_equal(a.train_scores(), b.train_scores())
+    (ga, ha), (gb, hb) = a.gradients(), b.gradients()
+    np.testing.assert_array_equal(ga, gb)
+    np.testing.assert_array_equal(ha, hb)
