@@ -633,7 +633,8 @@ PYBIND11_MODULE(_vw, m) {
         }
       })
       // model bytes in the host learner's format (vw_core.cpp VW::SaveModel), built from the device nonzeros
-      .def("export_model", [](const GpuSgd& g, const std::string& args) {
+      .def("export_model", [](GpuSgd& g, const std::string& args, bool final) {
+        g.SetFinalExport(final);
         int64_t m = 0;
         double t, tw, snx;
         {
@@ -666,7 +667,8 @@ PYBIND11_MODULE(_vw, m) {
           throw;
         }
         return py::reinterpret_steal<py::bytes>(out);
-      })
+      }, py::arg("args"), py::arg("final") = false,
+         "final=True: the fit's last use - the table is cleared as it is exported (reused clean by the next learner)")
       // warm start from model bytes of either learner (same format)
       .def("import_model", [](GpuSgd& g, const std::string& bytes) {
         if (bytes.size() < 12 || bytes.compare(0, 8, "SMLVW001") != 0) throw std::runtime_error("not a VW model");

@@ -96,6 +96,11 @@ class GpuSgd {
   // fills 12 * count bytes at dst (u64 stride-4 index + f32 value each, slot order)
   int64_t CountNonzeros() const;
   void WriteRecords(char* dst) const;
+  // final export (a fit's last use of the learner): WriteRecords also zeroes every exported component in place,
+  // so at destruction the table goes to the process's clean-table cache and the next learner of that size
+  // skips its 16 GiB memset (2^30); the learner refuses further learning / import / syncs afterwards
+  void SetFinalExport(bool on) { final_export_ = on; }
+  bool retired() const { return retired_; }
   void ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val);
   void GlobalState(double* t, double* total_weight, double* sum_norm_x) const;
   void SetGlobalState(double t, double total_weight, double sum_norm_x);
@@ -133,6 +138,9 @@ class GpuSgd {
   mutable int64_t export_count_ = 0;
   mutable uint32_t* export_reg_ = nullptr;  // one-scan export: per-block record regions + counts (device)
   mutable int32_t* export_cnt_ = nullptr;
+  bool final_export_ = false;
+  mutable bool retired_ = false;
+  void CheckLive() const;
   void ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1 = 0, int batch = 1);
   // per-row clamp bounds + loss reset before learning rows [r0, r1); loss read-back (and predictions) after
   void PrepLearn(int64_t r0, int64_t r1);

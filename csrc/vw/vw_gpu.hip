@@ -963,6 +963,15 @@ __global__ __launch_bounds__(64) void write_rec_region_kernel(const float4* __re
   if (lane == 0) cnt[blockIdx.x] = static_cast<int32_t>(o);
 }
 
+// final export: every exported component (record index = the component's float index in the table) back to 0
+__global__ void clear_records_kernel(const uint32_t* __restrict__ rec, int64_t n, float* __restrict__ W) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t ix = static_cast<uint64_t>(rec[3 * i]) | (static_cast<uint64_t>(rec[3 * i + 1]) << 32);
+    W[ix] = 0.f;
+  }
+}
+
 // region b's records -> out at base[b] (12-byte records as dwords)
 __global__ __launch_bounds__(256) void rec_compact_kernel(const uint32_t* __restrict__ reg, int cap,
                                                           const int32_t* __restrict__ cnt,
@@ -1222,8 +1231,36 @@ bool StagerRejectsNull() {
   return false;
 }
 
+// Tables a final export left all-zero (clear_records_kernel), per device: the next learner of the same size
+// takes one instead of allocating and zeroing 16 GiB (a 2^30 table's memset was ~3 ms of every fit, and the
+// staging's layout count waited behind it). One kept per device; never destroyed (teardown order).
+struct CleanTables {
+  std::mutex mu;
+  std::unordered_map<int, std::pair<void*, size_t>> t;
+  static CleanTables& Get() {
+    static CleanTables* c = new CleanTables();
+    return *c;
+  }
+  bool Take(int dev, size_t bytes, void** out) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = t.find(dev);
+    if (it == t.end() || it->second.second != bytes) return false;
+    *out = it->second.first;
+    t.erase(it);
+    return true;
+  }
+  bool Give(int dev, void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (t.count(dev)) return false;
+    t[dev] = {p, bytes};
+    return true;
+  }
+};
+
 struct GpuSgd::Impl {
   hipStream_t stream = nullptr, copy_stream = nullptr;
+  int dev = 0;
+  bool clean = false;  // W is all zeros again (a final export cleared it)
   Stager& stager = SharedStager();  // pinned host->device staging of pass data (on this learner's copy_stream)
   std::vector<hipEvent_t> events;
   hipEvent_t ev_ip = nullptr;  // ExpandToStage: the offsets' upload, ordered before the count kernel
@@ -1283,6 +1320,7 @@ struct GpuSgd::Impl {
     for (void* q : {static_cast<void*>(cats_act), static_cast<void*>(cats_cost), static_cast<void*>(cats_pdf),
                     static_cast<void*>(cats_base), static_cast<void*>(cats_has)})
       PoolFree(q);
+    if (W && clean && CleanTables::Get().Give(dev, W, nw * sizeof(float4))) W = nullptr;
     for (void* q : {static_cast<void*>(W), static_cast<void*>(indptr), static_cast<void*>(idx), static_cast<void*>(val),
                     static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo), static_cast<void*>(hi),
                     static_cast<void*>(pred)})
@@ -1341,8 +1379,17 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
   VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
   impl_->nw = 1ull << cfg.bits;
-  PoolMalloc(&impl_->W, impl_->nw * sizeof(float4));
-  VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), impl_->stream));
+  VW_HIP_CHECK(hipGetDevice(&impl_->dev));
+  void* clean = nullptr;
+  if (std::getenv("SML_VW_CLEAN_TABLES") && std::atoi(std::getenv("SML_VW_CLEAN_TABLES")) == 0) {
+    // (A/B: every learner zeroes its own table)
+  } else if (CleanTables::Get().Take(impl_->dev, impl_->nw * sizeof(float4), &clean)) {
+    impl_->W = static_cast<float4*>(clean);
+  }
+  if (!impl_->W) {
+    PoolMalloc(&impl_->W, impl_->nw * sizeof(float4));
+    VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), impl_->stream));
+  }
   impl_->nblk = static_cast<int64_t>((impl_->nw + (1ull << kDirtyShift) - 1) >> kDirtyShift);
   VW_HIP_CHECK(hipMalloc(&impl_->dirty, impl_->nblk));
   VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, impl_->nblk, impl_->stream));
@@ -1379,6 +1426,7 @@ SgdArgs BaseArgs(const GpuSgdConfig& c) {
 }  // namespace
 
 void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
+  CheckLive();
   SgdArgs a = BaseArgs(cfg_);
   a.indptr = impl_->indptr; a.idx = impl_->idx; a.val = impl_->val; a.lab = impl_->lab;
   a.wt = have_weights ? impl_->wt : nullptr;
@@ -1442,6 +1490,7 @@ int64_t GpuSgd::NextLaunch(int64_t b0, int64_t r0, int64_t r1, int batch) const 
 
 void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
                    const float* weights, int64_t n, int batch, float* preds_out) {
+  CheckLive();
   if (n <= 0) return;
   const size_t nnz = static_cast<size_t>(indptr[n] - indptr[0]);
   impl_->Reserve(n, nnz);
@@ -1545,6 +1594,7 @@ void GpuSgd::Learn(const int64_t* indptr, const uint32_t* indices, const float* 
 // over PCIe. Only the per-row label-range clamp bounds of the rows being learned move (8 B / row).
 void GpuSgd::Stage(const int64_t* indptr, const uint32_t* indices, const float* values, const float* labels,
                    const float* weights, int64_t n) {
+  CheckLive();
   if (n < 0) throw std::runtime_error("negative row count");
   const size_t nnz = static_cast<size_t>(n ? indptr[n] - indptr[0] : 0);
   impl_->Reserve(std::max<int64_t>(1, n), nnz);
@@ -1622,6 +1672,7 @@ void GpuSgd::FinishLearn(int64_t r0, int64_t r1, float* preds_out) {
 }
 
 void GpuSgd::LearnStaged(int64_t r0, int64_t r1, int batch, float* preds_out) {
+  CheckLive();
   if (r0 < 0 || r1 > staged_n_ || r0 > r1) throw std::runtime_error("LearnStaged: rows outside the staged set");
   if (r1 == r0) return;
   PrepLearn(r0, r1);
@@ -1820,6 +1871,7 @@ void GpuSgd::ExpandToStage(const FeatPlan& plan, int64_t n, int64_t learn_r1, in
 
 void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, const float* weights, int64_t learn_r1,
                        int batch) {
+  CheckLive();
   if (n < 0) throw std::runtime_error("negative row count");
   hipStream_t s = impl_->stream;
   if (learn_r1 > 0 && (cfg_.cb >= 0 || cfg_.csoaa > 0 || cfg_.cats > 0))  // label extras staged after the plan
@@ -1846,6 +1898,7 @@ void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, con
 }
 
 void GpuSgd::StageCosts(const int64_t* cptr, const int32_t* cls, const float* cost, int64_t n) {
+  CheckLive();
   if (n != staged_n_) throw std::runtime_error("StageCosts: rows != staged examples");
   hipStream_t s = impl_->stream;
   const int64_t m = cptr[n] - cptr[0];
@@ -1866,6 +1919,7 @@ void GpuSgd::StageCosts(const int64_t* cptr, const int32_t* cls, const float* co
 }
 
 void GpuSgd::StageCats(const float* action, const float* cost, const float* pdf, const uint8_t* has, int64_t n) {
+  CheckLive();
   if (cfg_.cats <= 0) throw std::runtime_error("StageCats: the learner is not a CATS learner");
   if (n != staged_n_) throw std::runtime_error("StageCats: rows != staged examples");
   hipStream_t s = impl_->stream;
@@ -1891,6 +1945,7 @@ void GpuSgd::StageCats(const float* action, const float* cost, const float* pdf,
 }
 
 void GpuSgd::StageCb(const int64_t* aip, const int32_t* chosen, const float* cost, const float* prob, int64_t ne) {
+  CheckLive();
   if (cfg_.cb < 0) throw std::runtime_error("StageCb on a learner without --cb_adf");
   if (aip[ne] - aip[0] != staged_rows_) throw std::runtime_error("StageCb: action rows != staged rows");
   hipStream_t s = impl_->stream;
@@ -1921,6 +1976,7 @@ void GpuSgd::StageCb(const int64_t* aip, const int32_t* chosen, const float* cos
 }
 
 void GpuSgd::PredictStaged(float* out, float* best) {
+  CheckLive();
   hipStream_t s = impl_->stream;
   const int64_t ne = staged_n_;
   if (ne <= 0) return;
@@ -1978,6 +2034,7 @@ void GpuSgd::CbStats(double* ips_num, double* snips_den, double* examples) const
 }
 
 void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float* values, int64_t n, float* out) {
+  CheckLive();
   if (n <= 0) return;
   const size_t nnz = static_cast<size_t>(indptr[n] - indptr[0]);
   impl_->Reserve(n, nnz);
@@ -2013,6 +2070,7 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
 // of the dirty maps, one small max-allreduce) are packed, reduced (fp64 sums of {wG or w, G}, max of N) and
 // unpacked with VW's weighted averaging - no host staging, and a sparse pass moves a fraction of the table.
 void GpuSgd::AllReduceAverage(void* comm, int world, double timeout_ms) {
+  CheckLive();
   if (world < 1 || !comm) return;  // a world-1 communicator still runs the collectives (one-GPU tests)
   hipStream_t s = impl_->stream;
   ncclComm_t c = static_cast<ncclComm_t>(comm);
@@ -2074,6 +2132,7 @@ uint64_t GpuSgd::NumWeights() const { return impl_->nw; }
 // Nonzero table components as (stride-4 index, value), compacted on the device: the host only ever holds
 // the nonzeros (a 2^30-slot table never crosses PCIe whole)
 void GpuSgd::ExportNonzeros(std::vector<uint64_t>* idx, std::vector<float>* val) const {
+  CheckLive();
   hipStream_t s = impl_->stream;
   const uint64_t per = 4096;
   const int64_t nb = static_cast<int64_t>((impl_->nw + per - 1) / per);
@@ -2127,6 +2186,7 @@ struct ExportClock {
 };
 
 int64_t GpuSgd::CountNonzeros() const {
+  CheckLive();
   hipStream_t s = impl_->stream;
   const uint64_t per = 4096;
   const int64_t nb = static_cast<int64_t>((impl_->nw + per - 1) / per);
@@ -2169,9 +2229,17 @@ int64_t GpuSgd::CountNonzeros() const {
   return tot;
 }
 
+void GpuSgd::CheckLive() const {
+  if (retired_) throw std::runtime_error("GPU VW learner: its table was cleared by the final export");
+}
+
 void GpuSgd::WriteRecords(char* dst) const {
   const int64_t tot = export_count_;
   if (tot <= 0) {
+    if (final_export_) {  // nothing nonzero: the table is clean as it is
+      impl_->clean = true;
+      retired_ = true;
+    }
     PoolFree(export_reg_);
     PoolFree(export_cnt_);
     export_reg_ = nullptr;
@@ -2196,6 +2264,11 @@ void GpuSgd::WriteRecords(char* dst) const {
                        base, rec);
   }
   VW_HIP_CHECK(hipGetLastError());
+  if (final_export_) {  // the records name every nonzero component: zero them behind the D2H copies below
+    hipLaunchKernelGGL(clear_records_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(65536, (tot + 255) / 256))),
+                       dim3(256), 0, s, rec, tot, reinterpret_cast<float*>(impl_->W));
+    VW_HIP_CHECK(hipGetLastError());
+  }
   clk.mark("records queued");
   // device -> pinned ring (the shared stager's buffers) -> dst, the host copy of piece k overlapping the DMA
   // of piece k + 1 (a pageable D2H would bounce through the runtime's own staging at a fraction of the rate)
@@ -2234,6 +2307,10 @@ void GpuSgd::WriteRecords(char* dst) const {
   }
   while (!inflight.empty()) drain_one();
   VW_HIP_CHECK(hipStreamSynchronize(s));
+  if (final_export_) {
+    impl_->clean = true;
+    retired_ = true;
+  }
   clk.mark("d2h + host copy");
   PoolFree(base);
   PoolFree(rec);
@@ -2245,6 +2322,7 @@ void GpuSgd::WriteRecords(char* dst) const {
 }
 
 void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<float>& val) {
+  CheckLive();
   hipStream_t s = impl_->stream;
   VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), s));
   const int64_t n = static_cast<int64_t>(idx.size());

@@ -471,7 +471,7 @@ def _train_partition_gpu(est, df: DataFrame, args: str, model_bytes=None):
     t1 = time.perf_counter_ns()
     sync_bytes = _gpu_learn_staged(est, g, _gpu_sync_comm(vwmod), n, first_learned=fused)
     t2 = time.perf_counter_ns()
-    model = g.export_model(args)
+    model = g.export_model(args, final=True)  # the learner's last use: its table is cleared for reuse
     t3 = time.perf_counter_ns()
     lab = np.asarray(labels)
     if weights is None:  # unit weights: no n-long ones / product arrays

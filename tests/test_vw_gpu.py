@@ -432,3 +432,34 @@ def test_gpu_unit_values_cross_as_device_fill(monkeypatch):
     monkeypatch.setenv("SML_VW_UNIT_FILL", "0")
     b = VowpalWabbitClassifier(**kw).fit(df)
     assert bytes(a.getNativeModel()) == bytes(b.getNativeModel())
+
+
+@pytest.mark.gpu
+def test_gpu_final_export_leaves_a_clean_table_for_the_next_fit(monkeypatch):
+    """A fit's final export clears the exported components in place; the next learner of that size takes the
+    table without its memset (SML_VW_CLEAN_TABLES=0: always zero a fresh one). Batch-1 fits in a row give the
+    same model bytes either way, and a retired learner refuses further work."""
+    from synapseml_amd.core.linalg import CsrColumn
+
+    rng = np.random.default_rng(8)
+    n, k = 5000, 10
+    ip = np.arange(0, n * k + 1, k, dtype=np.int64)
+    idx = rng.integers(0, 1 << 20, size=n * k, dtype=np.int64).astype(np.uint32)
+    val = rng.standard_normal(n * k).astype(np.float32)
+    y = np.where(rng.standard_normal(n) > 0, 1.0, -1.0)
+    df = DataFrame({"features": CsrColumn(ip, idx, val, 1 << 32), "label": y})
+    kw = dict(numBits=18, deviceType="gpu", gpuBatchSize=1, passThroughArgs="--loss_function logistic")
+    models = {}
+    for clean in ("1", "0"):
+        monkeypatch.setenv("SML_VW_CLEAN_TABLES", clean)
+        models[clean] = [VowpalWabbitClassifier(**kw).fit(df).getNativeModel() for _ in range(3)]
+    assert len({bytes(m) for m in models["1"] + models["0"]}) == 1
+    vw = native.load("_vw")
+    cfg = vw.GpuSgdConfig()
+    cfg.bits = 18
+    cfg.loss = 1
+    g = vw.GpuSgd(cfg, 0)
+    g.learn(ip, idx, val, y.astype(np.float32), None, 1)
+    assert len(g.export_model("--loss_function logistic -b 18", final=True)) > 100
+    with pytest.raises(RuntimeError, match="cleared by the final export"):
+        g.learn(ip, idx, val, y.astype(np.float32), None, 1)
