@@ -38,8 +38,9 @@ namespace {
 
 // The learner's large buffers (the 2^bits weight table - 16 GiB at b=30 -, the staged example rows and the
 // featurization's temporary blocks) come from the caching pool: a fit frees them at its end and the next fit
-// of the same shape gets them back without a hipMalloc / hipFree of gigabytes (the table is still zeroed per
-// learner). Small buffers stay on plain hipMalloc.
+// of the same shape gets them back without a hipMalloc / hipFree of gigabytes; the per-learner small buffers
+// (touched-block flags, global state, loss) too (a hipFree per buffer at every learner's end). A table a final
+// export cleared skips even its memset (CleanTables).
 std::mutex g_pool_mu;
 std::unordered_map<void*, size_t> g_pool_granted;
 
@@ -1255,6 +1256,33 @@ struct CleanTables {
     t[dev] = {p, bytes};
     return true;
   }
+  // the learners' two streams, kept per device (create + destroy cost ~0.8 ms per learner)
+  std::unordered_map<int, std::vector<hipStream_t>> streams;
+  hipStream_t TakeStream(int dev) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto& v = streams[dev];
+      if (!v.empty()) {
+        hipStream_t s = v.back();
+        v.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    VW_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+  }
+  void GiveStream(int dev, hipStream_t s) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto& v = streams[dev];
+      if (v.size() < 4) {
+        v.push_back(s);
+        return;
+      }
+    }
+    (void)hipStreamDestroy(s);
+  }
 };
 
 struct GpuSgd::Impl {
@@ -1307,16 +1335,27 @@ struct GpuSgd::Impl {
     }
   }
   ~Impl() {
+    static const bool prof = std::getenv("SML_VW_LIFE_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Done {
+      bool on;
+      std::chrono::steady_clock::time_point t0;
+      ~Done() {
+        if (on)
+          std::fprintf(stderr, "[vw learner] destroy %.3f ms\n",
+                       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      }
+    } done{prof, t0};
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
     if (ev_ip) (void)hipEventDestroy(ev_ip);
-    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (copy_stream) CleanTables::Get().GiveStream(dev, copy_stream);
     for (void* q : {static_cast<void*>(cptr), static_cast<void*>(aip), static_cast<void*>(ccls),
                     static_cast<void*>(chosen), static_cast<void*>(ccost), static_cast<void*>(cbcost),
-                    static_cast<void*>(cbprob), static_cast<void*>(best), static_cast<void*>(cbstats),
-                    static_cast<void*>(spec)})
+                    static_cast<void*>(cbprob), static_cast<void*>(best), static_cast<void*>(spec)})
       (void)hipFree(q);
+    PoolFree(cbstats);
     for (void* q : {static_cast<void*>(cats_act), static_cast<void*>(cats_cost), static_cast<void*>(cats_pdf),
                     static_cast<void*>(cats_base), static_cast<void*>(cats_has)})
       PoolFree(q);
@@ -1325,10 +1364,12 @@ struct GpuSgd::Impl {
                     static_cast<void*>(lab), static_cast<void*>(wt), static_cast<void*>(lo), static_cast<void*>(hi),
                     static_cast<void*>(pred)})
       PoolFree(q);
-    for (void* q : {static_cast<void*>(dirty), static_cast<void*>(gs), static_cast<void*>(loss), static_cast<void*>(pos),
-                    static_cast<void*>(blocks), static_cast<void*>(sums), static_cast<void*>(nmax)})
+    PoolFree(dirty);
+    PoolFree(gs);
+    PoolFree(loss);
+    for (void* q : {static_cast<void*>(pos), static_cast<void*>(blocks), static_cast<void*>(sums), static_cast<void*>(nmax)})
       (void)hipFree(q);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream) CleanTables::Get().GiveStream(dev, stream);
   }
 };
 
@@ -1369,6 +1410,8 @@ bool VwGpuAvailable() {
 }
 
 GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cfg) {
+  static const bool prof = std::getenv("SML_VW_LIFE_TIMING") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
   if (device >= 0) VW_HIP_CHECK(hipSetDevice(device));
   if (cfg.oaa > 256) throw std::runtime_error("GPU oaa supports at most 256 classes");
   if (cfg.csoaa > 256) throw std::runtime_error("GPU csoaa supports at most 256 classes");
@@ -1376,10 +1419,10 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
   if (cfg.cats == 1 || cfg.cats > 4096) throw std::runtime_error("GPU CATS supports 2..4096 discrete actions");
   if (cfg.cats > 0 && !(cfg.cats_max > cfg.cats_min && cfg.cats_bw > 0.f))
     throw std::runtime_error("GPU CATS needs min_value < max_value and bandwidth > 0");
-  VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
-  VW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->copy_stream, hipStreamNonBlocking));
-  impl_->nw = 1ull << cfg.bits;
   VW_HIP_CHECK(hipGetDevice(&impl_->dev));
+  impl_->stream = CleanTables::Get().TakeStream(impl_->dev);
+  impl_->copy_stream = CleanTables::Get().TakeStream(impl_->dev);
+  impl_->nw = 1ull << cfg.bits;
   void* clean = nullptr;
   if (std::getenv("SML_VW_CLEAN_TABLES") && std::atoi(std::getenv("SML_VW_CLEAN_TABLES")) == 0) {
     // (A/B: every learner zeroes its own table)
@@ -1391,17 +1434,20 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
     VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), impl_->stream));
   }
   impl_->nblk = static_cast<int64_t>((impl_->nw + (1ull << kDirtyShift) - 1) >> kDirtyShift);
-  VW_HIP_CHECK(hipMalloc(&impl_->dirty, impl_->nblk));
+  PoolMalloc(&impl_->dirty, impl_->nblk);
   VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, impl_->nblk, impl_->stream));
-  VW_HIP_CHECK(hipMalloc(&impl_->gs, 3 * sizeof(double)));
+  PoolMalloc(&impl_->gs, 3 * sizeof(double));
   VW_HIP_CHECK(hipMemsetAsync(impl_->gs, 0, 3 * sizeof(double), impl_->stream));
-  VW_HIP_CHECK(hipMalloc(&impl_->cbstats, 3 * sizeof(double)));
+  PoolMalloc(&impl_->cbstats, 3 * sizeof(double));
   VW_HIP_CHECK(hipMemsetAsync(impl_->cbstats, 0, 3 * sizeof(double), impl_->stream));
-  VW_HIP_CHECK(hipMalloc(&impl_->loss, sizeof(float)));
+  PoolMalloc(&impl_->loss, sizeof(float));
   VW_HIP_CHECK(hipMemsetAsync(impl_->loss, 0, sizeof(float), impl_->stream));
   // no wait here: every later use of the table is ordered behind the zeroing on this stream, and the
   // caller's host work (featurization, labels) overlaps the 16 GiB memset of a 2^30 table (~2.8 ms)
   if (cfg.loss == 1) { min_label_ = -50.0; max_label_ = 50.0; }
+  if (prof)
+    std::fprintf(stderr, "[vw learner] create %.3f ms\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
 }
 
 GpuSgd::~GpuSgd() {
