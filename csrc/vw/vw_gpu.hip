@@ -125,7 +125,14 @@ __global__ __launch_bounds__(256) void murmur_batch_kernel(const uint8_t* __rest
 //   pass 2: w += update * x * rate (+ l2), and the slot's 16 K-slot block is marked dirty for the sync.
 // Hogwild: examples of a mini-batch run concurrently on atomics (conflicts are rare in a 2^b table);
 // batch = 1 is the exact sequential learner.
-constexpr int kDirtyShift = 12;  // dirty-tracking granularity: 4096 slots (64 KB) per block
+constexpr int kDirtyShift = 12;  // sync granularity: 4096 slots (64 KB) per block
+// Touch map (one byte per 256 slots, 4 MB at 2^30): the sync epoch in which a 4 KB sub-block was last written
+// (0 = never). The sync derives its 64 KB "touched since the last sync" blocks from it (coarsen_kernel) and the
+// export scans only the sub-blocks ever written (a 2M-example pass writes ~16 % of them: the 16 GiB export scan
+// was ~3 ms of every fit). One byte per feature update as before (the old map was 64 KB-granular and cleared at
+// every sync, so it could not serve the export).
+constexpr int kTouchShift = 8;
+constexpr int kTouchPerBlock = 1 << (kDirtyShift - kTouchShift);
 
 struct SgdArgs {
   const int64_t* indptr;
@@ -140,7 +147,7 @@ struct SgdArgs {
   int64_t n0, n1;
   float4* W;
   uint64_t mask;
-  uint8_t* dirty;
+  uint8_t* dirty;      // the touch map (kTouchShift granularity; epoch of the last write)
   double* gs;          // [t, total weight, sum of feature norms]
   float lr, power_t, initial_t, l2, l1, tau;
   int loss;            // 0 squared, 1 logistic, 2 hinge, 3 quantile (tau)
@@ -150,6 +157,7 @@ struct SgdArgs {
   float* loss_acc;
   int learn;
   int hot_agg;         // block-aggregate the constant feature's slot (sgd_kernel; SML_VW_HOT_AGG=0 disables)
+  int epoch;           // the current sync epoch (1..255) written into the touch map
 };
 
 __device__ __forceinline__ float WaveSum(float v) {
@@ -306,8 +314,8 @@ __device__ float UpdateSecondPass(const SgdArgs& a, int64_t b, int64_t en, uint6
     }
     // the touched-block flag: written only when still clear (most updates hit blocks already marked; a plain
     // byte load instead of a store that takes the line from the other XCDs' caches)
-    uint8_t* dflag = a.dirty + (h >> kDirtyShift);
-    if (*dflag == 0) *dflag = 1;
+    uint8_t* dflag = a.dirty + (h >> kTouchShift);
+    if (*dflag != static_cast<uint8_t>(a.epoch)) *dflag = static_cast<uint8_t>(a.epoch);
   }
   return update;
 }
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(64 * kSgdWaves) void sgd_kernel(SgdArgs a) {
       for (int w = 0; w < kSgdWaves; ++w) { d += s_hd[w]; mx = fmaxf(mx, s_hax[w]); }
       if (mx > 0.f) {
         atomicAdd(&a.W[hot].x, d);
-        a.dirty[hot >> kDirtyShift] = 1;
+        a.dirty[hot >> kTouchShift] = static_cast<uint8_t>(a.epoch);
       }
     }
   }
@@ -929,12 +937,15 @@ __global__ __launch_bounds__(64) void write_rec_kernel(const float4* __restrict_
 // reports the count, and the host then takes the two-scan path. rec_compact_kernel packs the regions.
 __global__ __launch_bounds__(64) void write_rec_region_kernel(const float4* __restrict__ W, uint64_t nw, uint64_t per,
                                                               int cap, uint32_t* __restrict__ reg,
-                                                              int32_t* __restrict__ cnt) {
+                                                              int32_t* __restrict__ cnt,
+                                                              const uint8_t* __restrict__ touch) {
   const int lane = threadIdx.x & 63;
   const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * per, s1 = min(nw, s0 + per);
   uint32_t* rec = reg + static_cast<uint64_t>(blockIdx.x) * cap * 3;
   int64_t o = 0;
   for (uint64_t s = s0; s < s1; s += 64) {
+    // (touch map: a never-written 256-slot sub-block is all zeros - the 64 slots of this step lie in one)
+    if (touch && touch[s >> kTouchShift] == 0) continue;
     const uint64_t my = s + lane;
     const float4 v = my < s1 ? W[my] : make_float4(0.f, 0.f, 0.f, 0.f);
     const int c = (v.x != 0.f) + (v.y != 0.f) + (v.z != 0.f);
@@ -986,6 +997,34 @@ __global__ __launch_bounds__(256) void rec_compact_kernel(const uint32_t* __rest
   }
 }
 
+// sync: 64 KB block b was written this epoch if any of its 16 touch bytes holds the epoch
+__global__ void coarsen_kernel(const uint8_t* __restrict__ touch, int64_t nblk, int epoch, uint8_t* __restrict__ coarse) {
+  for (int64_t b = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; b < nblk;
+       b += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint8_t* t = touch + b * kTouchPerBlock;
+    uint8_t any = 0;
+#pragma unroll
+    for (int j = 0; j < kTouchPerBlock; ++j) any |= t[j] == static_cast<uint8_t>(epoch) ? 1 : 0;
+    coarse[b] = any;
+  }
+}
+
+// sync: the averaged blocks were written on every rank (a block another rank touched gets values here too)
+__global__ void mark_blocks_kernel(const int32_t* __restrict__ blocks, int64_t m, int epoch, uint8_t* __restrict__ touch) {
+  const int64_t n = m * kTouchPerBlock;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    touch[static_cast<int64_t>(blocks[i / kTouchPerBlock]) * kTouchPerBlock + i % kTouchPerBlock] =
+        static_cast<uint8_t>(epoch);
+}
+
+// epoch wrap (255 syncs): every written sub-block back to epoch 1
+__global__ void touch_renorm_kernel(uint8_t* __restrict__ touch, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    if (touch[i]) touch[i] = 1;
+}
+
 __global__ void dirty_list_kernel(const uint8_t* __restrict__ dirty, int64_t nblk, const int32_t* __restrict__ pos,
                                   int32_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < nblk;
@@ -1035,13 +1074,17 @@ __global__ __launch_bounds__(64) void write_nz_kernel(const float4* __restrict__
   }
 }
 
-__global__ void scatter_kernel(float4* __restrict__ W, uint64_t nw, const uint64_t* __restrict__ idx,
+__global__ void scatter_kernel(float4* __restrict__ W, uint64_t nw, uint8_t* __restrict__ touch, int epoch,
+                               const uint64_t* __restrict__ idx,
                                const float* __restrict__ val, int64_t n) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const uint64_t s = idx[i] >> 2;
     const int c = static_cast<int>(idx[i] & 3);
-    if (s < nw && c < 3) reinterpret_cast<float*>(&W[s])[c] = val[i];
+    if (s < nw && c < 3) {
+      reinterpret_cast<float*>(&W[s])[c] = val[i];
+      touch[s >> kTouchShift] = static_cast<uint8_t>(epoch);
+    }
   }
 }
 
@@ -1294,8 +1337,10 @@ struct GpuSgd::Impl {
   hipEvent_t ev_ip = nullptr;  // ExpandToStage: the offsets' upload, ordered before the count kernel
   float4* W = nullptr;
   uint64_t nw = 0;
-  uint8_t* dirty = nullptr;
-  int64_t nblk = 0;
+  uint8_t* dirty = nullptr;   // the touch map (nfine bytes)
+  uint8_t* coarse = nullptr;  // sync: 64 KB blocks written this epoch (nblk bytes)
+  int64_t nblk = 0, nfine = 0;
+  int epoch = 1;
   double* gs = nullptr;
   int64_t* indptr = nullptr;
   uint32_t* idx = nullptr;
@@ -1365,6 +1410,7 @@ struct GpuSgd::Impl {
                     static_cast<void*>(pred)})
       PoolFree(q);
     PoolFree(dirty);
+    PoolFree(coarse);
     PoolFree(gs);
     PoolFree(loss);
     for (void* q : {static_cast<void*>(pos), static_cast<void*>(blocks), static_cast<void*>(sums), static_cast<void*>(nmax)})
@@ -1434,8 +1480,10 @@ GpuSgd::GpuSgd(const GpuSgdConfig& cfg, int device) : impl_(new Impl()), cfg_(cf
     VW_HIP_CHECK(hipMemsetAsync(impl_->W, 0, impl_->nw * sizeof(float4), impl_->stream));
   }
   impl_->nblk = static_cast<int64_t>((impl_->nw + (1ull << kDirtyShift) - 1) >> kDirtyShift);
-  PoolMalloc(&impl_->dirty, impl_->nblk);
-  VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, impl_->nblk, impl_->stream));
+  impl_->nfine = static_cast<int64_t>(impl_->nblk) * kTouchPerBlock;
+  PoolMalloc(&impl_->dirty, impl_->nfine);
+  VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, impl_->nfine, impl_->stream));
+  PoolMalloc(&impl_->coarse, impl_->nblk);
   PoolMalloc(&impl_->gs, 3 * sizeof(double));
   VW_HIP_CHECK(hipMemsetAsync(impl_->gs, 0, 3 * sizeof(double), impl_->stream));
   PoolMalloc(&impl_->cbstats, 3 * sizeof(double));
@@ -1484,7 +1532,7 @@ void GpuSgd::Launch(int64_t b0, int64_t b1, bool learn, bool have_weights) {
     a.clo = static_cast<float>(min_label_);
     a.chi = static_cast<float>(max_label_);
   }
-  a.n0 = b0; a.n1 = b1; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
+  a.n0 = b0; a.n1 = b1; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.epoch = impl_->epoch; a.gs = impl_->gs;
   a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = learn ? 1 : 0;
   if (cfg_.cats > 0) {
     a.lo = nullptr;
@@ -2041,7 +2089,7 @@ void GpuSgd::PredictStaged(float* out, float* best) {
   SgdArgs a = BaseArgs(cfg_);
   a.indptr = impl_->indptr; a.idx = impl_->idx; a.val = impl_->val;
   a.lo = scalar ? impl_->lo : nullptr; a.hi = impl_->hi;
-  a.n0 = 0; a.n1 = ne; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
+  a.n0 = 0; a.n1 = ne; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.epoch = impl_->epoch; a.gs = impl_->gs;
   a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = 0;
   if (cfg_.cats > 0) {
     int depth = 0;
@@ -2098,7 +2146,7 @@ void GpuSgd::Predict(const int64_t* indptr, const uint32_t* indices, const float
   SgdArgs a = BaseArgs(cfg_);
   a.indptr = impl_->indptr; a.idx = impl_->idx; a.val = impl_->val;
   a.lo = cfg_.oaa == 0 ? impl_->lo : nullptr; a.hi = impl_->hi;
-  a.n0 = 0; a.n1 = n; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.gs = impl_->gs;
+  a.n0 = 0; a.n1 = n; a.W = impl_->W; a.mask = impl_->nw - 1; a.dirty = impl_->dirty; a.epoch = impl_->epoch; a.gs = impl_->gs;
   a.preds = impl_->pred; a.loss_acc = impl_->loss; a.learn = 0;
   if (cfg_.oaa > 0) {
     const int waves = std::min(cfg_.oaa, kOaaMaxWaves);
@@ -2137,10 +2185,13 @@ void GpuSgd::AllReduceAverage(void* comm, int world, double timeout_ms) {
     if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL allreduce failed: ") + ncclGetErrorString(r));
   };
   const int64_t nblk = impl_->nblk;
-  nccl(ncclAllReduce(impl_->dirty, impl_->dirty, nblk, ncclUint8, ncclMax, c, s));
+  hipLaunchKernelGGL(coarsen_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(65536, (nblk + 255) / 256))), dim3(256),
+                     0, s, impl_->dirty, nblk, impl_->epoch, impl_->coarse);
+  VW_HIP_CHECK(hipGetLastError());
+  nccl(ncclAllReduce(impl_->coarse, impl_->coarse, nblk, ncclUint8, ncclMax, c, s));
   // deterministic compaction (every rank packs the same blocks in the same order): host prefix over the map
   std::vector<uint8_t> hd(nblk);
-  VW_HIP_CHECK(hipMemcpyAsync(hd.data(), impl_->dirty, nblk, hipMemcpyDeviceToHost, s));
+  VW_HIP_CHECK(hipMemcpyAsync(hd.data(), impl_->coarse, nblk, hipMemcpyDeviceToHost, s));
   VW_HIP_CHECK(hipStreamSynchronize(s));
   std::vector<int32_t> list;
   for (int64_t i = 0; i < nblk; ++i) if (hd[i]) list.push_back(static_cast<int32_t>(i));
@@ -2166,9 +2217,20 @@ void GpuSgd::AllReduceAverage(void* comm, int world, double timeout_ms) {
     hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, impl_->W, impl_->blocks, m, impl_->nw, adaptive,
                        1.0f / world, impl_->sums, impl_->nmax);
     VW_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(mark_blocks_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(65536, (m * kTouchPerBlock + 255) / 256))),
+                       dim3(256), 0, s, impl_->blocks, m, impl_->epoch, impl_->dirty);
+    VW_HIP_CHECK(hipGetLastError());
     last_sync_bytes_ = static_cast<int64_t>(slots) * (2 * sizeof(float) + sizeof(float)) + nblk;
   }
-  VW_HIP_CHECK(hipMemsetAsync(impl_->dirty, 0, nblk, s));
+  // the next epoch (the touch map keeps every write for the export; 255 epochs fit a byte)
+  if (impl_->epoch >= 255) {
+    hipLaunchKernelGGL(touch_renorm_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(65536, (impl_->nfine + 255) / 256))),
+                       dim3(256), 0, s, impl_->dirty, impl_->nfine);
+    VW_HIP_CHECK(hipGetLastError());
+    impl_->epoch = 2;
+  } else {
+    ++impl_->epoch;
+  }
   VW_HIP_CHECK(hipStreamSynchronize(s));
   last_sync_blocks_ = m;
 }
@@ -2243,8 +2305,10 @@ int64_t GpuSgd::CountNonzeros() const {
   const bool regions = !(re && std::atoi(re) == 0);
   if (regions) {
     PoolMalloc(&export_reg_, static_cast<size_t>(nb) * kRegionCap * 12);
+    const char* sk = std::getenv("SML_VW_EXPORT_SKIP");  // 0: scan every sub-block (A/B, tests)
+    const uint8_t* touch = (sk && std::atoi(sk) == 0) ? nullptr : impl_->dirty;
     hipLaunchKernelGGL(write_rec_region_kernel, dim3(static_cast<unsigned>(nb)), dim3(64), 0, s, impl_->W, impl_->nw,
-                       per, kRegionCap, export_reg_, cnt);
+                       per, kRegionCap, export_reg_, cnt, touch);
   } else {
     hipLaunchKernelGGL(count_nz_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, s, impl_->W, impl_->nw, per, cnt);
   }
@@ -2329,12 +2393,12 @@ void GpuSgd::WriteRecords(char* dst) const {
     inflight.erase(inflight.begin());
     VW_HIP_CHECK(hipEventSynchronize(st.ev[pc.k]));
     const size_t per_t = (pc.n + kStageThreads - 1) / kStageThreads;
-    std::vector<std::thread> th;
-    for (int t = 0; t < kStageThreads && t * per_t < pc.n; ++t) {
+    const char* from = st.buf[pc.k];
+    char* to = dst + pc.off;
+    st.Team().Run([=](int t) {  // the stager's persistent copy team (the bytes object's pages fault in here)
       const size_t a0 = t * per_t, a1 = std::min(pc.n, a0 + per_t);
-      th.emplace_back([=, &st]() { std::memcpy(dst + pc.off + a0, st.buf[pc.k] + a0, a1 - a0); });
-    }
-    for (auto& x : th) x.join();
+      if (a0 < a1) std::memcpy(to + a0, from + a0, a1 - a0);
+    });
   };
   for (size_t off = 0; off < bytes; off += kStageBytes) {
     const int k = st.next;
@@ -2380,7 +2444,7 @@ void GpuSgd::ImportNonzeros(const std::vector<uint64_t>& idx, const std::vector<
     VW_HIP_CHECK(hipMemcpyAsync(di, idx.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     VW_HIP_CHECK(hipMemcpyAsync(dv, val.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(scatter_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(65536, (n + 255) / 256))), dim3(256),
-                       0, s, impl_->W, impl_->nw, di, dv, n);
+                       0, s, impl_->W, impl_->nw, impl_->dirty, impl_->epoch, di, dv, n);
     VW_HIP_CHECK(hipStreamSynchronize(s));
     (void)hipFree(di);
     (void)hipFree(dv);

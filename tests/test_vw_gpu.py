@@ -463,3 +463,45 @@ def test_gpu_final_export_leaves_a_clean_table_for_the_next_fit(monkeypatch):
     assert len(g.export_model("--loss_function logistic -b 18", final=True)) > 100
     with pytest.raises(RuntimeError, match="cleared by the final export"):
         g.learn(ip, idx, val, y.astype(np.float32), None, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [14, 24])
+def test_gpu_export_touch_map_skip_matches_full_scan(monkeypatch, bits):
+    """The export scans only the 256-slot sub-blocks the touch map says were ever written: same bytes as the
+    full scan (SML_VW_EXPORT_SKIP=0) after learning, after syncs (a world-1 communicator still runs them; the
+    sync epochs advance and the touch map keeps every write) and for a warm-started learner (the import marks
+    the sub-blocks it fills)."""
+    vw = native.load("_vw")
+    cfg = vw.GpuSgdConfig()
+    cfg.bits = bits
+    cfg.loss = 1
+    rng = np.random.default_rng(5)
+    n, k = 20000, 12
+    idx = rng.integers(0, 1 << 32, size=n * k, dtype=np.uint64).astype(np.uint32)
+    val = rng.standard_normal(n * k).astype(np.float32)
+    ip = np.arange(0, n * k + 1, k, dtype=np.int64)
+    lab = (rng.random(n) > 0.5).astype(np.float32) * 2 - 1
+    args = f"--loss_function logistic -b {bits}"
+
+    def both(g):
+        monkeypatch.setenv("SML_VW_EXPORT_SKIP", "1")
+        a = g.export_model(args)
+        monkeypatch.setenv("SML_VW_EXPORT_SKIP", "0")
+        b = g.export_model(args)
+        assert a == b
+        return a
+
+    g = vw.GpuSgd(cfg, 0)
+    g.learn(ip[: n // 2 + 1], idx[: ip[n // 2]], val[: ip[n // 2]], lab[: n // 2], None, 64)
+    m_half = both(g)
+    comm = vw.nccl_comm(vw.nccl_unique_id(), 0, 1, 60000.0)
+    for _ in range(3):
+        g.allreduce_average(comm)
+    g.learn(ip[n // 2:] - ip[n // 2], idx[ip[n // 2]:], val[ip[n // 2]:], lab[n // 2:], None, 64)
+    g.allreduce_average(comm)
+    m_full = both(g)
+    assert len(m_full) > len(m_half) > 200
+    g2 = vw.GpuSgd(cfg, 0)
+    g2.import_model(bytes(m_full))
+    assert len(both(g2)) == len(m_full)  # every imported record found by the skipping scan
