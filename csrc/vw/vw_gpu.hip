@@ -1982,7 +1982,11 @@ void GpuSgd::StagePlan(const FeatPlan& plan, int64_t n, const float* labels, con
     if (weights)
       impl_->stager.Copy(reinterpret_cast<char*>(impl_->wt), reinterpret_cast<const char*>(weights),
                          n * sizeof(float), impl_->copy_stream);
-    staged_labels_.assign(labels, labels + n);
+    // the host copy feeds only the running label range of non-logistic scalar learners (PrepLearn); a logistic
+    // learner clamps to fixed bounds, so its 8 MB per 2M-example pass is not copied (fresh pages every fit)
+    const bool scalar = cfg_.oaa == 0 && cfg_.csoaa == 0 && cfg_.cb < 0 && cfg_.cats == 0;
+    if (scalar && cfg_.loss == 1) staged_labels_.clear();
+    else staged_labels_.assign(labels, labels + n);
     staged_n_ = n;
   }
   staged_weights_ = weights != nullptr;
