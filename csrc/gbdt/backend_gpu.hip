@@ -3667,11 +3667,42 @@ __global__ void unpack_gh_kernel(const float2* __restrict__ gh, int64_t n, float
 }
 
 // row-major -> column-major bin copy (once per dataset)
+// Four rows per thread: each 16-byte chunk of the four rows is read as one dwordx4 per row and every feature of
+// the chunk leaves as one dword (the four rows' bins) - a byte load + byte store per (row, feature) ran at
+// ~1.1 TB/s (606 us at 11M x 28, r6 pass 24). n % 4 != 0 (dword stores misaligned) takes the byte form.
 __global__ void transpose_bins_kernel(const uint8_t* __restrict__ bins, int S, int F, int64_t n,
                                       uint8_t* __restrict__ cbins) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint8_t* row = bins + i * S;
-    for (int f = 0; f < F; ++f) cbins[static_cast<size_t>(f) * n + i] = row[f];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if ((n & 3) != 0 || (S & 15) != 0) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+      const uint8_t* row = bins + i * S;
+      for (int f = 0; f < F; ++f) cbins[static_cast<size_t>(f) * n + i] = row[f];
+    }
+    return;
+  }
+  const int64_t nq = n >> 2;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq; q += stride) {
+    const int64_t i0 = q << 2;
+    const uint4* r = reinterpret_cast<const uint4*>(bins + i0 * S);
+    const int cs = S >> 4;  // 16-byte chunks per row
+    for (int c = 0; c * 16 < F; ++c) {
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = r[k * cs + c];
+      const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&v[0]);
+      const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&v[1]);
+      const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&v[2]);
+      const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&v[3]);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int f = c * 16 + j;
+        if (f >= F) break;
+        const int d = j >> 2, sh = (j & 3) * 8;
+        const uint32_t out = ((w0[d] >> sh) & 0xFFu) | (((w1[d] >> sh) & 0xFFu) << 8) |
+                             (((w2[d] >> sh) & 0xFFu) << 16) | (((w3[d] >> sh) & 0xFFu) << 24);
+        *reinterpret_cast<uint32_t*>(cbins + static_cast<size_t>(f) * n + i0) = out;
+      }
+    }
   }
 }
 
