@@ -3348,7 +3348,8 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
                                                               const uint4* __restrict__ bins4, int W4,
                                                               int F, const uint8_t* __restrict__ cbins, int64_t n,
                                                               double scale, double* __restrict__ score,
-                                                              int32_t* __restrict__ leaf_out) {
+                                                              int32_t* __restrict__ leaf_out,
+                                                              const uint8_t* __restrict__ row_leaf = nullptr) {
   __shared__ int4 snodes[kScoreLdsNodes];
   __shared__ double slv[kPrepMaxNodes + 1];
   if (src.st) {  // the tree just grown, straight from the device arrays (TrainTreeAndUpdateScore)
@@ -3367,7 +3368,13 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(DevTreeView tv, De
   const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kScoreThreads + threadIdx.x;
   const bool packed = F <= 32;
   int leaf[kScoreRows];
-  if (packed) {
+  if (row_leaf) {  // every row's leaf from the scattered map (batched growth, no bag): no walk, no bin loads
+#pragma unroll
+    for (int u = 0; u < kScoreRows; ++u) {
+      const int64_t i = i0 + u * stride;
+      leaf[u] = i < n ? row_leaf[i] : 0;
+    }
+  } else if (packed) {
     uint4 ra[kScoreRows], rb[kScoreRows];
     if (ni > 0) {  // branch-free row loads (rows past n read row 0; their results are not stored)
 #pragma unroll
@@ -4311,20 +4318,21 @@ class GpuBackend : public TrainBackend {
     EnqueueTreeCopy();
     AccountScoreTime();  // the previous pass (done before this growth) frees the event pair
     DevTreeSrc src{dt_, state_ + final_v_, fm_.num_bin, fm_.missing, fm_.default_bin, shrink};
+    // every row was partitioned (batched growth, no bag): its leaf comes from the finest segments' labels
+    // (leaf_table_kernel + leaf_scatter_kernel), not a per-row tree walk
+    const uint8_t* rl = nullptr;
+    if (grew_batched_ && bag_n_ < 0 && dt_.lseg) {
+      hipLaunchKernelGGL(leaf_table_kernel, dim3(1), dim3(kLeafTableThreads), 0, stream_, bstate_.get(),
+                         bnodes_.get(), state_ + final_v_, dt_.lseg, rtab_.get(),
+                         reinterpret_cast<int*>(rtab_.get() + kBatchMaxNodes));
+      SML_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(leaf_scatter_kernel, dim3(std::min(GridFor(n_), 2048)), dim3(256), 0, stream_, rtab_.get(),
+                         reinterpret_cast<const int*>(rtab_.get() + kBatchMaxNodes), perm_[0].get(), perm_[1].get(),
+                         static_cast<int32_t>(n_), row_leaf_.get());
+      SML_HIP_CHECK(hipGetLastError());
+      rl = row_leaf_.get();
+    }
     if (prep_armed_ && k == 0 && K_ == 1) {
-      // every row was partitioned (no bag): its leaf comes from the final leaves' segments, not a tree walk
-      const uint8_t* rl = nullptr;
-      if (grew_batched_ && bag_n_ < 0 && dt_.lseg) {
-        hipLaunchKernelGGL(leaf_table_kernel, dim3(1), dim3(kLeafTableThreads), 0, stream_, bstate_.get(),
-                           bnodes_.get(), state_ + final_v_, dt_.lseg, rtab_.get(), rtab_.get() == nullptr ? nullptr
-                           : reinterpret_cast<int*>(rtab_.get() + kBatchMaxNodes));
-        SML_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(leaf_scatter_kernel, dim3(std::min(GridFor(n_), 2048)), dim3(256), 0, stream_, rtab_.get(),
-                           reinterpret_cast<const int*>(rtab_.get() + kBatchMaxNodes), perm_[0].get(), perm_[1].get(),
-                           static_cast<int32_t>(n_), row_leaf_.get());
-        SML_HIP_CHECK(hipGetLastError());
-        rl = row_leaf_.get();
-      }
       LaunchPrep(DevTreeView{}, src, 1.0, rl);
     } else {
       // any other objective: the plain score update, still without the host round trip
@@ -4332,7 +4340,7 @@ class GpuBackend : public TrainBackend {
       SML_HIP_CHECK(hipEventRecord(ev_[2], stream_));
       hipLaunchKernelGGL(score_kernel, dim3(ScoreGrid()), dim3(kScoreThreads), 0, stream_, DevTreeView{}, src,
                          reinterpret_cast<const uint4*>(bins_ptr_), S_ / 16, F_, cbins_.get(), n_, 1.0,
-                         score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr));
+                         score_.get() + static_cast<size_t>(k) * n_, static_cast<int32_t*>(nullptr), rl);
       SML_HIP_CHECK(hipGetLastError());
       SML_HIP_CHECK(hipEventRecord(ev_[3], stream_));
       score_pending_ = true;

@@ -794,7 +794,8 @@ def test_gpu_small_hessian_leaves_match_fp64():
 @pytest.mark.parametrize("extra", ["num_leaves=31", "num_leaves=255 min_data_in_leaf=5", "num_leaves=2",
                                    "num_leaves=31 objective=cross_entropy",
                                    "num_leaves=31 categorical_feature=0 monotone_constraints=0,1,-1",
-                                   "num_leaves=31 bagging_fraction=0.7 bagging_freq=1"])
+                                   "num_leaves=31 bagging_fraction=0.7 bagging_freq=1",
+                                   "num_leaves=31 objective=multiclass num_class=3", "num_leaves=63 objective=regression"])
 def test_gpu_row_leaf_scatter_equals_tree_walk(extra, monkeypatch):
     """After batched growth the fused score pass reads every row's leaf from the final leaves' row segments
     (leaf_scatter_kernel) instead of walking the tree per row: bitwise the same scores, gradients and models
@@ -812,3 +813,17 @@ def test_gpu_row_leaf_scatter_equals_tree_walk(extra, monkeypatch):
     (ga, ha), (gb, hb) = a.gradients(), b.gradients()
     np.testing.assert_array_equal(ga, gb)
     np.testing.assert_array_equal(ha, hb)
+
+
+def test_gpu_row_leaf_map_ranker_equals_tree_walk(monkeypatch):
+    """The plain score kernel (objectives without the fused pass: lambdarank here) reads the row -> leaf map
+    too: bitwise the walk's scores and models."""
+    X, y, sizes = _rank_data()
+    p = "objective=lambdarank num_leaves=31 min_data_in_leaf=5 eval_at=5 device_type=gpu"
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SML_GBDT_ROW_LEAF", v)
+        b = _train_rank(X, y, sizes, p, 5)
+        out[v] = (b.save_model_string(), np.asarray(b.train_scores()))
+    assert out["1"][0] == out["0"][0]
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
