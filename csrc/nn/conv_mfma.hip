@@ -1605,6 +1605,171 @@ __global__ __launch_bounds__(256) void stem_wide_kernel(ConvArgs a) {
   ConvEpilogue<T, 32, 64, 1>(a, acc, lds, M, m0, n0, wid, lane);
 }
 
+// fp32 stem on bf16 planes (the fp32 graphs' bf16x3 / bf16x6 modes, kP = 2 / 3 planes, 3 / 6 products per
+// pair as in the tiled kernel's kSplit): the row-staged form above with fp32 input rows. Each staged value is
+// (affine'd, then) split once into kP RNE bf16 planes (x = x0 + x1 (+ x2) up to the last plane's rounding),
+// the im2col rows of one plane at a time are built in LDS from that plane's rows, and the products (xp, wq)
+// with p + q < kP are accumulated in fp32 by 16x16x32 bf16 MFMAs. The weight planes ([kP][Cout][160] bf16,
+// split once per model) live in registers: waves split 2 (pixels) x 2 (channels), 64 x 32 per wave, so a
+// wave's B fragments are loaded once per block. Replaces the generic exact-f32 gather GEMM for the 3-channel
+// stem of an fp32 graph (r6 pass 25: 954 us per ResNet-50 batch of 256, plus the input affine's own pass).
+// LDS: one A plane [128][176] bf16 (45 KB, the fp32 epilogue staging reuses it) + kP staged row planes.
+template <int kP, bool kPro>
+__global__ __launch_bounds__(256) void stem_f32_kernel(ConvArgs a) {
+  typedef __bf16 bt;
+  constexpr int C = 3, TM = 4, TN = 2, kKS = kStemKP / 32, kRIt = 8;
+  __shared__ __attribute__((aligned(16))) bt As[kStemBM * kStemLd];
+  extern __shared__ __attribute__((aligned(16))) unsigned char stem_f32_smem[];
+  bt* rowbuf = reinterpret_cast<bt*>(stem_f32_smem);  // [kP][R][SP]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int orow = blockIdx.x;  // b * OH + oh
+  const int oh = orow % a.OH, b = orow / a.OH;
+  const int m0 = orow * a.OW, n0 = blockIdx.y * kStemBN;
+  const int S = a.S, R = a.R, run = S * C, K = R * run;
+  const int SP = (a.W + 2 * kRowPad) * C;  // plane row pitch (elements), a multiple of 4
+  const int cps = SP / 4, d0 = kRowPad * C / 4, d1 = d0 + a.W * C / 4;  // 4-value chunks; data in [d0, d1)
+  const int plane = R * SP;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  // every global load first: the wave's weight fragments (kP planes x 5 k-steps x 2 channel tiles) and the
+  // block's input rows (<= 8 float4 per thread), one memory latency for all of them
+  const bt* __restrict__ w = static_cast<const bt*>(a.w);
+  b8 bfr[kP][kKS][TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * 32 + j * 16 + fr;
+#pragma unroll
+    for (int q = 0; q < kP; ++q)
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks) {
+        if (n < a.Cout) {
+          bfr[q][ks][j] = *reinterpret_cast<const b8*>(w + (static_cast<int64_t>(q) * a.Cout + n) * kStemKP + ks * 32 + fk);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[q][ks][j][e] = static_cast<bt>(0.f);
+        }
+      }
+  }
+  const float* __restrict__ x = static_cast<const float*>(a.x);
+  float psc[C], psh[C];
+  if constexpr (kPro) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+  }
+  f4 rv[kRIt];
+  bool rok[kRIt];
+#pragma unroll
+  for (int i = 0; i < kRIt; ++i) {
+    const int q = tid + i * 256;
+    const int r = q / cps, j = q - r * cps;
+    const int ih = oh * a.stride_h - a.pad_h + r;
+    rok[i] = q < R * cps && ih >= 0 && ih < a.H && j >= d0 && j < d1;
+    rv[i] = f4{0.f, 0.f, 0.f, 0.f};
+    if (rok[i]) rv[i] = *reinterpret_cast<const f4*>(x + (static_cast<int64_t>(b) * a.H + ih) * a.W * C + (j - d0) * 4);
+  }
+  {  // the padded K tail of every A row is zero in every plane (the im2col below writes only [0, K))
+    const int c0 = K / 8, nch = kStemKP / 8 - c0;
+    for (int q = tid; q < kStemBM * nch; q += 256) {
+      const int row = q / nch, ch = c0 + q % nch;
+      *reinterpret_cast<uint4*>(As + row * kStemLd + ch * 8) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  // stage: affine (real values only: padding stays 0), then the plane split, 8 B per plane and chunk
+#pragma unroll
+  for (int i = 0; i < kRIt; ++i) {
+    const int q = tid + i * 256;
+    if (q >= R * cps) continue;
+    const int r = q / cps, j = q - r * cps;
+    float v[4] = {rv[i][0], rv[i][1], rv[i][2], rv[i][3]};
+    if constexpr (kPro) {
+      if (rok[i]) {
+        const int c0 = (j * 4) % C;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = (c0 + k) % C;
+          const float t = v[k] * psc[c] + psh[c];
+          v[k] = a.prologue_relu ? fmaxf(t, 0.f) : t;
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      bt h[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        h[k] = static_cast<bt>(v[k]);
+        v[k] -= static_cast<float>(h[k]);
+      }
+      *reinterpret_cast<uint2*>(rowbuf + p * plane + r * SP + j * 4) = *reinterpret_cast<const uint2*>(h);
+    }
+  }
+  __syncthreads();
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < kP; ++p) {
+    // im2col rows of plane p from its staged rows (the f16 row-staged form's dword shifts)
+    const bt* rb = rowbuf + p * plane;
+    for (int q = tid; q < R * kStemBM; q += 256) {
+      const int r = q >> 7, ml = q & (kStemBM - 1);
+      if (ml >= a.OW) continue;
+      const int h0 = r * SP + (ml * a.stride_w - a.pad_w + kRowPad) * C;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(rb) + (h0 >> 1);
+      uint32_t d[12], o[11];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) d[k] = src[k];
+      const uint32_t sb = static_cast<uint32_t>(h0 & 1) * 2u;
+#pragma unroll
+      for (int k = 0; k < 11; ++k) o[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sb);
+      const int dst = ml * kStemLd + r * run;
+      uint32_t* A32 = reinterpret_cast<uint32_t*>(As);
+      unsigned short* A16 = reinterpret_cast<unsigned short*>(As);
+      if ((dst & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+          if (2 * k + 1 < run) A32[(dst >> 1) + k] = o[k];
+          else if (2 * k < run) A16[dst + 2 * k] = static_cast<unsigned short>(o[k] & 0xFFFFu);
+        }
+      } else {
+        A16[dst] = static_cast<unsigned short>(o[0] & 0xFFFFu);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          const uint32_t pr = __builtin_amdgcn_alignbyte(o[k + 1], o[k], 2u);
+          if (2 * k + 2 < run) A32[((dst + 1) >> 1) + k] = pr;
+          else if (2 * k + 1 < run) A16[dst + 2 * k + 1] = static_cast<unsigned short>(pr & 0xFFFFu);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if ((wm * TM + i) * 16 >= a.OW) continue;  // wave-uniform: pixel tiles past the output row
+        const b8 af = *reinterpret_cast<const b8*>(As + (wm * 64 + i * 16 + fr) * kStemLd + ks * 32 + fk);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < kP - p; ++q) acc[i][j] = Vec<bt>::mfma(af, bfr[q][ks][j], acc[i][j]);
+      }
+    }
+    __syncthreads();  // the next plane's im2col (or the epilogue staging) overwrites As
+  }
+  ConvEpilogue<float, 64, 32, 2>(a, acc, reinterpret_cast<float*>(As), m0 + a.OW, m0, n0, wid, lane);
+}
+
+inline int StemF32Lds(const ConvArgs& a, int planes) { return planes * a.R * (a.W + 2 * kRowPad) * 3 * 2; }
+inline bool StemF32Ok(const ConvArgs& a, int planes) {
+  return reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && a.C == 3 && a.S * 3 <= 21 && a.R <= 8 && a.R * a.S * 3 <= kStemKP &&
+         a.OW <= kStemBM && a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= kRowPad && a.W % 4 == 0 &&
+         (a.OW - 1) * a.stride_w - a.pad_w + a.S <= a.W + kRowPad && a.R * (a.W + 2 * kRowPad) * 3 / 4 <= 8 * 256 &&
+         StemF32Lds(a, planes) <= 34 * 1024 && a.B > 0 && a.OH > 0 && a.Cout >= 1 &&
+         static_cast<int64_t>(a.B) * a.OH * a.OW * a.Cout < (1ll << 31) && static_cast<int64_t>(a.B) * a.H * a.W * 3 < (1ll << 31);
+}
+
 }  // namespace
 
 template <class T>
@@ -1618,6 +1783,22 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
 // few-channel stem: x NHWC with C <= 4, w packed [Cout][160] (k = (r * S + s) * C + c, zero-padded),
 // R * S * C <= 160, f16 (dtype 1) / bf16 (2)
 int StemConv(const ConvArgs& a, int dtype, void* stream, int kp, int form) {
+  if (dtype == 3 || dtype == 4) {  // fp32 input, weights [planes][Cout][160] bf16 (ops.conv.pack_stem_weight_f32)
+    const int planes = dtype == 3 ? 2 : 3;
+    if (kp != kStemKP || form == 1) return -1;
+    if (!StemF32Ok(a, planes)) return -4;
+    const dim3 grid(a.B * a.OH, (a.Cout + kStemBN - 1) / kStemBN);
+    const size_t dyn = static_cast<size_t>(StemF32Lds(a, planes));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (planes == 2) {
+      if (a.in_scale) hipLaunchKernelGGL((stem_f32_kernel<2, true>), grid, dim3(256), dyn, st, a);
+      else hipLaunchKernelGGL((stem_f32_kernel<2, false>), grid, dim3(256), dyn, st, a);
+    } else {
+      if (a.in_scale) hipLaunchKernelGGL((stem_f32_kernel<3, true>), grid, dim3(256), dyn, st, a);
+      else hipLaunchKernelGGL((stem_f32_kernel<3, false>), grid, dim3(256), dyn, st, a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
   if (kp == kWideKP) {  // row-run form: weights packed [Cout][192], k = r * 24 + s * 3 + c
     if ((dtype != 1 && dtype != 2) || a.C != 3 || a.S * 3 > kWideRP || a.R > 8 || a.Cout < 1 || a.OH <= 0 ||
         a.OW <= 0 || a.B <= 0)

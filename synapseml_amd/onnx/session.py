@@ -333,9 +333,15 @@ class InferenceSession:
         """A _FusedConv the few-channel stem kernel runs (f16 / bf16 GPU session, C <= 4, R, S <= 8,
         R * S * C <= 160, one group): its input affine can ride the kernel's im2col (padding stays 0)."""
         if (not _STEM_KERNEL or n.op_type != "_FusedConv" or n.inputs[1] not in self._consts or not self.gpu
-                or self.compute_dtype not in (torch.float16, torch.bfloat16)):
+                or self.compute_dtype not in (torch.float16, torch.bfloat16, torch.float32)):
             return False
         w = self._consts[n.inputs[1]]
+        if self.compute_dtype == torch.float32:  # the bf16-plane fp32 stem kernel: 3 channels, S <= 7
+            from ..ops.conv import f32_mode_default
+
+            if (self.f32_conv_mode or f32_mode_default()) == "exact" or not isinstance(w, torch.Tensor) \
+                    or w.dim() != 4 or w.shape[1] != 3 or w.shape[3] > 7:
+                return False
         return (isinstance(w, torch.Tensor) and w.dim() == 4 and n.attrs.get("group", 1) == 1
                 and 1 <= w.shape[1] <= 4 and w.shape[2] <= 8 and w.shape[3] <= 8
                 and w.shape[1] * w.shape[2] * w.shape[3] <= 160 and n.attrs.get("__act", 0) in (0, 1))
@@ -805,7 +811,7 @@ def _fused_conv(rt, at, x):
                         out_affine=(f32(post[0]), f32(post[1])) if post is not None else None,
                         f32_mode=rt.session.f32_conv_mode)
         return list(y) if post is not None else [y]
-    if _STEM_KERNEL and _stem_kernel_ok(rt, at, inp, w):
+    if _STEM_KERNEL and (_stem_kernel_ok(rt, at, inp, w) or _stem_f32_ok(rt, at, inp, w)):
         ys = [_stem_kernel_conv(rt, at, inp, w, b, res, act, pro)]
         if post is not None:
             return ys + [_affine_act(rt, ys[0], post[0], post[1], None, 1, 0.0)]
@@ -832,14 +838,40 @@ def _stem_kernel_ok(rt, at, inp, w) -> bool:
             and inp.numel() * inp.element_size() < 2 ** 31)
 
 
+def _stem_f32_mode(rt) -> str:
+    from ..ops.conv import f32_mode_default
+
+    return rt.session.f32_conv_mode or f32_mode_default()
+
+
+def _stem_f32_ok(rt, at, inp, w) -> bool:
+    """The 3-channel stem of an fp32 graph in a bf16-plane mode (bf16x3 / bf16x6; "exact" keeps the exact-f32
+    gather GEMM): csrc/nn/conv_mfma.hip stem_f32_kernel, the input affine fused, for the row-staged geometry."""
+    if rt.session._nn is None or inp.dtype != torch.float32 or w.dtype != torch.float32 or inp.dim() != 4:
+        return False
+    if at.get("group", 1) != 1 or at.get("__act", 0) not in (0, 1) or w.dim() != 4:
+        return False
+    mode = _stem_f32_mode(rt)
+    if mode == "exact":
+        return False
+    from ..ops.conv import stem_f32_supported
+
+    if not inp.is_contiguous(memory_format=torch.channels_last):
+        return False
+    nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+    return stem_f32_supported(inp, w, strides, (pb[0], pb[1], pe[0], pe[1]), dil, mode)
+
+
 def _stem_kernel_conv(rt, at, inp, w, b, res, act, pro=None):
-    from ..ops.conv import pack_stem_weight, stem_conv_nhwc
+    from ..ops.conv import pack_stem_weight, pack_stem_weight_f32, stem_conv_nhwc
 
     cache = rt.session.__dict__.setdefault("_stem_wk", {})
-    key = (w.data_ptr(), tuple(w.shape), w.dtype)
+    f32 = inp.dtype == torch.float32
+    mode = _stem_f32_mode(rt) if f32 else None
+    key = (w.data_ptr(), tuple(w.shape), w.dtype, mode)
     wk = cache.get(key)
-    if wk is None:
-        wk = cache[key] = pack_stem_weight(w)
+    if wk is None:  # packed (fp32: and split into bf16 planes) once per weight
+        wk = cache[key] = pack_stem_weight_f32(w, mode) if f32 else pack_stem_weight(w)
     nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
     return stem_conv_nhwc(inp, wk, w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]), dil,
                           bias=b, relu=2 if act == 1 else 0, res=res, in_affine=pro,

@@ -178,6 +178,29 @@ def pack_stem_weight(w: torch.Tensor, wide: Optional[bool] = None) -> torch.Tens
     return out
 
 
+def stem_f32_supported(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), pad=(0, 0), dil=(1, 1),
+                       mode: str = "bf16x3") -> bool:
+    """The fp32 stem kernel (bf16-plane products, csrc/nn/conv_mfma.hip stem_f32_kernel): fp32 NHWC input with
+    3 channels, R <= 8, S <= 7, W % 4 == 0, output rows of <= 128 pixels, no dilation, pad_w <= 8, 16-B
+    aligned rows (the row-staged geometry; the native launcher re-checks and refuses other shapes)."""
+    if mode not in _PLANES or not (
+            x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and w.dim() == 4 and x.shape[1] == 3
+            and w.shape[1] == 3 and w.shape[2] <= 8 and w.shape[3] <= 7 and x.shape[3] % 4 == 0
+            and tuple(dil) == (1, 1) and pad[1] <= 8 and x.data_ptr() % 16 == 0):
+        return False
+    H, W = x.shape[2], x.shape[3]
+    r, s = w.shape[2], w.shape[3]
+    oh, ow = out_hw(H, W, r, s, stride, pad, dil)
+    return (0 < ow <= 128 and oh > 0 and (ow - 1) * stride[1] - pad[1] + s <= W + 8
+            and _PLANES[mode] * r * (W + 16) * 3 * 2 <= 34 * 1024 and r * (W + 16) * 3 // 4 <= 2048)
+
+
+def pack_stem_weight_f32(w: torch.Tensor, mode: str = "bf16x3") -> torch.Tensor:
+    """fp32 [Cout, 3, R, S] -> [planes, Cout, 160] bf16 (pack_stem_weight, then split_weight's RNE planes:
+    2 for bf16x3, 3 for bf16x6) - the fp32 stem kernel's weight operand, made once per model."""
+    return split_weight(pack_stem_weight(w.float(), wide=False), mode)
+
+
 def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
                    bias: Optional[torch.Tensor] = None, relu: int = 0,
                    res: Optional[torch.Tensor] = None, in_affine=None, in_relu: bool = False,
@@ -188,17 +211,26 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
     input channel: x' = x * scale + shift (ReLU'd with ``in_relu``) inside the kernel, padding taps 0 - an
     input BatchNormalization without its own pass. ``form`` (160-wide weights): 0 picks the row-staged kernel
     where it applies (3 channels, one block per output row of <= 128 pixels), 1 forces the 2-byte gather
-    kernel, 2 the row-staged one."""
+    kernel, 2 the row-staged one. fp32 ``x``: ``wk`` = pack_stem_weight_f32(w, mode), the bf16-plane kernel
+    (2 planes: 3 products per pair, 3 planes: 6), 3 channels and the row-staged geometry only."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         x = x.contiguous(memory_format=torch.channels_last)
-    if wk.dim() != 2 or wk.shape[1] not in (STEM_KP, STEM_WIDE_KP) or wk.dtype != x.dtype or not wk.is_contiguous():
+    if x.dtype == torch.float32:
+        if wk.dim() != 3 or wk.shape[0] not in (2, 3) or wk.shape[2] != STEM_KP or wk.dtype != torch.bfloat16 \
+                or not wk.is_contiguous():
+            raise ValueError("fp32 stem weight must be pack_stem_weight_f32(w, mode)")
+        cout = wk.shape[1]
+        dt = 3 if wk.shape[0] == 2 else 4
+    elif wk.dim() != 2 or wk.shape[1] not in (STEM_KP, STEM_WIDE_KP) or wk.dtype != x.dtype or not wk.is_contiguous():
         raise ValueError("stem weight must be pack_stem_weight(w) in the input dtype")
-    if wk.shape[1] == STEM_WIDE_KP and (C != 3 or s * 3 > STEM_WIDE_RP or r > 8):
+    else:
+        cout = wk.shape[0]
+        dt = _DT[x.dtype]
+    if wk.shape[-1] == STEM_WIDE_KP and (C != 3 or s * 3 > STEM_WIDE_RP or r > 8):
         raise ValueError("row-run stem weight for a different filter shape")
     if C * r * s > STEM_KP or C > 4:
         raise ValueError("stem kernel: C <= 4 and R * S * C <= 160")
-    cout = wk.shape[0]
     oh, ow = out_hw(H, W, r, s, stride, pad, dil)
     y = torch.empty((B, cout, oh, ow), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
     if res is not None:
@@ -212,13 +244,13 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
         if sc.numel() != C or sh.numel() != C:
             raise ValueError("stem in_affine: one scale / shift per input channel")
     native.load("_nn").stem_conv(x.data_ptr(), wk.data_ptr(), y.data_ptr(), _ptr(b32), _ptr(res), geom, int(relu),
-                                 _DT[x.dtype], torch.cuda.current_stream(x.device).cuda_stream, _ptr(sc), _ptr(sh),
-                                 int(bool(in_relu)), int(wk.shape[1]), int(form))
+                                 dt, torch.cuda.current_stream(x.device).cuda_stream, _ptr(sc), _ptr(sh),
+                                 int(bool(in_relu)), int(wk.shape[-1]), int(form))
     return y
 
 
 __all__ = ["supported", "pack_weight", "split_weight", "conv2d_nhwc", "out_hw", "F32_MODES", "stem_supported",
-           "pack_stem_weight", "stem_conv_nhwc", "stem_wide"]
+           "pack_stem_weight", "stem_conv_nhwc", "stem_wide", "stem_f32_supported", "pack_stem_weight_f32"]
 
 
 def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),

@@ -384,6 +384,82 @@ def test_stem_kernel_matches_reference(dtype, geom):
         torch.testing.assert_close(y3.float(), r3, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("mode", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("geom", [
+    # B, H, W, Cout, k, stride, pad
+    (3, 224, 224, 64, 7, 2, 3),   # the ResNet-50 stem
+    (2, 40, 48, 64, 7, 2, 3),     # 24-pixel output rows: a partial pixel tile per wave pair
+    (3, 24, 16, 80, 5, 1, 2),     # stride 1, a partial channel tile (Cout % 8 == 0)
+    (2, 20, 36, 36, 3, 1, 1),     # Cout % 8 != 0: the element-store epilogue
+    (1, 17, 12, 64, 3, 3, 0),     # 3x3 stride 3 unpadded
+])
+def test_stem_f32_kernel_matches_fp64(mode, geom):
+    """fp32 stem on bf16 planes (stem_f32_kernel) vs an fp64 convolution: small integers (exact in one plane)
+    check the layout bit for bit; random data stays within the tiled fp32 modes' error gate (bf16x3: 1e-5
+    of max |y|; bf16x6: 1e-6), with bias + ReLU + residual and with the fused input affine (+ ReLU)."""
+    from synapseml_amd.ops.conv import pack_stem_weight_f32, stem_conv_nhwc, stem_f32_supported
+
+    B, H, W, Co, k, st, pd = geom
+    g = torch.Generator().manual_seed(7)
+    x = torch.randint(-3, 4, (B, 3, H, W), generator=g).float().cuda().contiguous(memory_format=torch.channels_last)
+    w = torch.randint(-3, 4, (Co, 3, k, k), generator=g).float().cuda()
+    assert stem_f32_supported(x, w, (st, st), (pd, pd), (1, 1), mode)
+    y = stem_conv_nhwc(x, pack_stem_weight_f32(w, mode), k, k, (st, st), (pd, pd))
+    ref = F.conv2d(x.double(), w.double(), None, st, pd)
+    torch.testing.assert_close(y.double(), ref, rtol=0, atol=0)
+    torch.manual_seed(8)
+    xf = torch.randn(B, 3, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    wf = torch.randn(Co, 3, k, k, device="cuda") / (3 * k * k) ** 0.5
+    bias = torch.randn(Co, device="cuda")
+    res = torch.randn_like(ref.float()).contiguous(memory_format=torch.channels_last)
+    gate = 1e-5 if mode == "bf16x3" else 1e-6
+    wk = pack_stem_weight_f32(wf, mode)
+    y2 = stem_conv_nhwc(xf, wk, k, k, (st, st), (pd, pd), bias=bias, relu=2, res=res)
+    r2 = torch.relu(F.conv2d(xf.double(), wf.double(), bias.double(), st, pd) + res.double())
+    assert (y2.double() - r2).abs().max().item() <= gate * r2.abs().max().item()
+    sc = torch.rand(3, device="cuda") + 0.5
+    sh = torch.randn(3, device="cuda")
+    for in_relu in (False, True):
+        y3 = stem_conv_nhwc(xf, wk, k, k, (st, st), (pd, pd), bias=bias, relu=1, in_affine=(sc, sh), in_relu=in_relu)
+        xa = xf.double() * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1)
+        xa = torch.relu(xa) if in_relu else xa
+        r3 = torch.relu(F.conv2d(xa, wf.double(), bias.double(), st, pd))
+        assert (y3.double() - r3).abs().max().item() <= gate * r3.abs().max().item()
+
+
+def test_resnet_fp32_session_stem_uses_f32_kernel():
+    """An fp32 graph's 3-channel stem with its input BatchNormalization: the BN rides the bf16-plane stem
+    kernel (no separate affine pass), and the output matches an fp64 reference within the fp32 conv gate."""
+    import numpy as np
+
+    from synapseml_amd.onnx import InferenceSession, proto as P
+    from synapseml_amd.onnx.writer import GraphBuilder
+
+    rng = np.random.default_rng(3)
+    gb = GraphBuilder("stem32")
+    gb.input("x", P.FLOAT32, ["N", 3, 64, 64])
+    prm = [gb.init("s", (rng.random(3) + 0.5).astype(np.float32)),
+           gb.init("t", rng.standard_normal(3).astype(np.float32)),
+           gb.init("m", (rng.standard_normal(3) * 0.1).astype(np.float32)),
+           gb.init("v", (rng.random(3) + 0.5).astype(np.float32))]
+    xb = gb.add("BatchNormalization", ["x"] + prm, {"epsilon": 1e-5})
+    w = gb.init("w", (rng.standard_normal((64, 3, 7, 7)) / 12).astype(np.float32))
+    bb = gb.init("b", rng.standard_normal(64).astype(np.float32))
+    c = gb.add("Conv", [xb, w, bb], {"kernel_shape": [7, 7], "pads": [3, 3, 3, 3], "strides": [2, 2]})
+    gb.add("Relu", [c], out="y")
+    gb.output("y", P.FLOAT32, None)
+    sess = InferenceSession(gb.to_bytes(), device="cuda", precision="fp32")
+    stem = [n for n in sess.nodes if sess._stem_conv_node(n)]
+    assert len(stem) == 1 and stem[0].inputs[0] == "x" and len(stem[0].inputs) == 6  # the BN is the prologue
+    xin = rng.standard_normal((2, 3, 64, 64)).astype(np.float32)
+    y = np.asarray(sess.run(None, {"x": xin})[0], dtype=np.float64)
+    it = {k: torch.from_numpy(gb.inits[k]).double().view(1, -1, 1, 1) for k in ("s", "t", "m", "v")}
+    xr = (torch.from_numpy(xin).double() - it["m"]) / torch.sqrt(it["v"] + 1e-5) * it["s"] + it["t"]
+    ref = torch.relu(F.conv2d(xr, torch.from_numpy(gb.inits["w"]).double(),
+                              torch.from_numpy(gb.inits["b"]).double(), 2, 3)).numpy()
+    assert np.abs(y - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
 _RESNET50_SHAPES = [  # C, H, Cout, k, stride (tools/bench_conv.py SHAPES: the 14 bottleneck layer shapes)
     (64, 56, 64, 1, 1), (64, 56, 64, 3, 1), (64, 56, 256, 1, 1), (256, 56, 64, 1, 1),
     (128, 28, 128, 3, 1), (128, 28, 512, 1, 1), (512, 28, 128, 1, 1), (256, 56, 512, 1, 2),

@@ -462,7 +462,12 @@ def test_gpu_stem_epilogue_moves_past_maxpool():
     x = np.random.default_rng(8).random((2, 3, 224, 224), dtype=np.float32)
     gpu = InferenceSession(data, device="cuda")
     pools = [n for n in gpu.nodes if n.op_type == "MaxPool"]
-    assert pools and len(pools[0].inputs) == 2 and pools[0].attrs.get("__act") == 1
+    stem = [n for n in gpu.nodes if gpu._stem_conv_node(n)]
+    if stem:  # fp32 on bf16 planes: the stem kernel takes the input BN as its prologue, bias + ReLU in its epilogue
+        assert len(stem) == 1 and stem[0].inputs[0] == "data" and len(stem[0].inputs) == 6
+        assert stem[0].attrs.get("__act") == 1 and pools and len(pools[0].inputs) == 1
+    else:
+        assert pools and len(pools[0].inputs) == 2 and pools[0].attrs.get("__act") == 1
     # the last block's residual add + post-activation BN + ReLU: the final conv's second output
     assert any(n.op_type == "_FusedConv" and len(n.outputs) == 2 and len(n.inputs) == 8 for n in gpu.nodes)
     cpu = InferenceSession(data, device="cpu").run(None, {"data": x})[0]
