@@ -31,6 +31,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "nn_ops.h"
 
@@ -1761,6 +1762,206 @@ __global__ __launch_bounds__(256) void stem_f32_kernel(ConvArgs a) {
   ConvEpilogue<float, 64, 32, 2>(a, acc, reinterpret_cast<float*>(As), m0 + a.OW, m0, n0, wid, lane);
 }
 
+// Strip form of the stride-2 RGB stem (f16 / bf16 with one plane, fp32 on kP bf16 planes): a block walks
+// kRingOut consecutive output rows of one image. The input rows live in an LDS ring of R + stride_h rows
+// (per plane); an output row needs only its stride_h new input rows, loaded into registers while the previous
+// row's MFMAs run and written to the ring slots that row no longer reads. No im2col buffer: with the row-run
+// K order (k = r * 24 + s * 3 + c, weights zero in slots s * 3 + c >= S * 3) a fragment's 8 consecutive k are 8
+// consecutive values of one staged row, and stride_w * 3 even with the row staged pad_w zero pixels in keeps
+// every fragment's first value at an even slot offset: 4 aligned dword reads per fragment. The weight planes
+// sit in registers for the whole strip (waves 2 pixels x 2 channels, 64 x 32 each), the epilogue stages
+// through its own LDS area (the shared bias / ReLU / residual / 16-B store path).
+constexpr int kRingOut = 8;  // output rows per block
+
+template <class T, int kP, bool kPro>
+__global__ __launch_bounds__(256) void stem_ring_kernel(ConvArgs a, int SP, int nstrip) {
+  typedef typename std::conditional<sizeof(T) == 4, __bf16, T>::type MT;  // MFMA operand type
+  typedef typename Vec<MT>::type V8;
+  constexpr int C = 3, TM = 4, TN = 2, kKS = kWideKP / 32, EPC = 16 / static_cast<int>(sizeof(T));
+  constexpr int kEpiL = 32 + (sizeof(T) == 4 ? 4 : 8);  // ConvEpilogue<T, 64, 32, 2>'s staged row pitch
+  constexpr int kItInit = 8, kItPre = 2;
+  __shared__ __attribute__((aligned(16))) T epi[4 * 64 * kEpiL];
+  extern __shared__ __attribute__((aligned(16))) unsigned char stem_ring_smem[];
+  MT* ring = reinterpret_cast<MT*>(stem_ring_smem);  // [kP][NR][SP] (+ one slack row)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int b = blockIdx.x / nstrip, oh0 = (blockIdx.x - b * nstrip) * kRingOut;
+  const int nout = min(kRingOut, a.OH - oh0);
+  const int n0 = blockIdx.y * kStemBN;
+  const int R = a.R, sh = a.stride_h, NR = R + sh, plane = NR * SP;
+  const int cpr = a.W * C / EPC;  // 16-B input chunks per row
+  const int d0 = a.pad_w * C;     // slot offset of the row's first value (the row is staged pad_w pixels in)
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const MT* __restrict__ w = static_cast<const MT*>(a.w);
+  V8 bfr[kP][kKS][TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * 32 + j * 16 + fr;
+#pragma unroll
+    for (int q = 0; q < kP; ++q)
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks) {
+        if (n < a.Cout) {
+          bfr[q][ks][j] = *reinterpret_cast<const V8*>(w + (static_cast<int64_t>(q) * a.Cout + n) * kWideKP + ks * 32 + fk);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[q][ks][j][e] = static_cast<MT>(0.f);
+        }
+      }
+  }
+  float psc[C], psh[C];
+  if constexpr (kPro) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { psc[c] = a.in_scale[c]; psh[c] = a.in_shift[c]; }
+  }
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const int64_t img = static_cast<int64_t>(b) * a.H;
+  auto slot_of = [&](int ih) { return (ih + 16 * NR) % NR; };
+  // one 16-B input chunk: row ih (zero outside the image), chunk j
+  auto load = [&](int ih, int j) -> uint4 {
+    if (ih < 0 || ih >= a.H) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(x + (img + ih) * a.W * C + j * EPC);
+  };
+  // affine (real rows only), plane split, and the chunk's values written at slot offset d0 + j * EPC: dword
+  // stores from the first even offset, a 2-byte store at an odd end
+  auto commit = [&](int ih, int j, uint4 raw) {
+    float v[EPC];
+    const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) v[k] = ToF(e[k]);
+    if constexpr (kPro) {
+      if (ih >= 0 && ih < a.H) {
+        const int c0 = (j * EPC) % C;
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) {
+          const int c = (c0 + k) % C;
+          const float t = v[k] * psc[c] + psh[c];
+          v[k] = a.prologue_relu ? fmaxf(t, 0.f) : t;
+        }
+      }
+    }
+    const int off = slot_of(ih) * SP + d0 + j * EPC;
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      MT h[EPC];
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        h[k] = static_cast<MT>(v[k]);
+        if constexpr (kP > 1) v[k] -= static_cast<float>(h[k]);
+      }
+      unsigned short* r16 = reinterpret_cast<unsigned short*>(ring + p * plane + off);
+      const unsigned short* hs = reinterpret_cast<const unsigned short*>(h);
+      if ((off & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < EPC; k += 2)
+          *reinterpret_cast<uint32_t*>(r16 + k) = static_cast<uint32_t>(hs[k]) | (static_cast<uint32_t>(hs[k + 1]) << 16);
+      } else {
+        r16[0] = hs[0];
+#pragma unroll
+        for (int k = 1; k + 1 < EPC; k += 2)
+          *reinterpret_cast<uint32_t*>(r16 + k) = static_cast<uint32_t>(hs[k]) | (static_cast<uint32_t>(hs[k + 1]) << 16);
+        r16[EPC - 1] = hs[EPC - 1];
+      }
+    }
+  };
+  // the whole ring zero (padding columns stay zero for the strip), then the first output row's R input rows
+  {
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(ring);
+    const int nd = (kP * plane + SP) / 2;
+    for (int q = tid; q < nd; q += 256) r32[q] = 0u;
+  }
+  __syncthreads();
+  {
+    const int ih0 = oh0 * sh - a.pad_h;
+    uint4 rv[kItInit];
+#pragma unroll
+    for (int i = 0; i < kItInit; ++i) {
+      const int q = tid + i * 256;
+      rv[i] = q < R * cpr ? load(ih0 + q / cpr, q % cpr) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kItInit; ++i) {
+      const int q = tid + i * 256;
+      if (q < R * cpr) commit(ih0 + q / cpr, q % cpr, rv[i]);
+    }
+  }
+  // per lane: the filter row and slot offset of its 8 k of every k-step (rows >= R carry zero weights: read row
+  // R - 1 instead of a slot being refilled)
+  for (int k = 0; k < nout; ++k) {
+    __syncthreads();  // this row's input rows staged; the previous epilogue's staging reads done
+    const int oh = oh0 + k;
+    const bool more = k + 1 < nout;
+    const int ihn = oh * sh - a.pad_h + R;  // the next output row's new input rows: [ihn, ihn + sh)
+    uint4 pv[kItPre];
+#pragma unroll
+    for (int i = 0; i < kItPre; ++i) {
+      const int q = tid + i * 256;
+      pv[i] = (more && q < sh * cpr) ? load(ihn + q / cpr, q % cpr) : make_uint4(0, 0, 0, 0);
+    }
+    f4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int ihb = oh * sh - a.pad_h;
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) {
+      const int k0 = ks * 32 + fk;
+      const int r = min(k0 / kWideRP, R - 1), jj = k0 % kWideRP;
+      const int rowoff = slot_of(ihb + r) * SP + jj;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if ((wm * TM + i) * 16 >= a.OW) continue;  // wave-uniform: pixel tiles past the output row
+        const int ow = wm * 64 + i * 16 + fr;
+        const int e0 = rowoff + ow * a.stride_w * C;  // even: stride_w * 3 even, pad_w cancels
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(ring + p * plane + e0);
+          uint4 u;
+          u.x = src[0];
+          u.y = src[1];
+          u.z = src[2];
+          u.w = src[3];
+          const V8 af = __builtin_bit_cast(V8, u);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < kP - p; ++q) acc[i][j] = Vec<MT>::mfma(af, bfr[q][ks][j], acc[i][j]);
+        }
+      }
+    }
+    if (more) {  // slots of the rows output row oh - 1 read (done before the barrier above), not row oh's
+#pragma unroll
+      for (int i = 0; i < kItPre; ++i) {
+        const int q = tid + i * 256;
+        if (q < sh * cpr) commit(ihn + q / cpr, q % cpr, pv[i]);
+      }
+    }
+    const int m0 = (b * a.OH + oh) * a.OW;
+    ConvEpilogue<T, 64, 32, 2>(a, acc, epi, m0 + a.OW, m0, n0, wid, lane);
+  }
+}
+
+// slot pitch (elements) of the strip form's ring: the staged row (pad_w zero pixels, the row, zeros) and
+// the farthest 24-value run a stored output pixel reads, rounded up to 8 values
+inline int RingSP(const ConvArgs& a) {
+  const int data_end = (a.pad_w + a.W) * 3;
+  const int run_end = ((a.OW - 1) * a.stride_w) * 3 + kWideRP;
+  return (std::max(data_end, run_end) + 8 + 7) / 8 * 8;
+}
+inline int RingLds(const ConvArgs& a, int planes) { return (planes * (a.R + a.stride_h) + 1) * RingSP(a) * 2; }
+inline bool RingOk(const ConvArgs& a, int planes, int esize) {
+  const int epc = 16 / esize;
+  return reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && a.C == 3 && (a.stride_w % 2) == 0 && a.stride_w <= 4 &&
+         a.S * 3 <= kWideRP &&
+         a.R <= 8 && a.R >= 1 && a.stride_h >= 1 && a.stride_h <= 4 && a.OW <= kStemBM && a.OW > 0 && a.OH > 0 &&
+         a.dil_h == 1 && a.dil_w == 1 && a.pad_w <= 8 && (a.W * 3) % epc == 0 &&
+         a.R * (a.W * 3 / epc) <= 8 * 256 && a.stride_h * (a.W * 3 / epc) <= 2 * 256 &&
+         RingLds(a, planes) <= 44 * 1024 && a.B > 0 && a.Cout >= 1 &&
+         static_cast<int64_t>(a.B) * a.OH * a.OW * a.Cout < (1ll << 31) &&
+         static_cast<int64_t>(a.B) * a.H * a.W * 3 < (1ll << 31);
+}
+
 inline int StemF32Lds(const ConvArgs& a, int planes) { return planes * a.R * (a.W + 2 * kRowPad) * 3 * 2; }
 inline bool StemF32Ok(const ConvArgs& a, int planes) {
   return reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && a.C == 3 && a.S * 3 <= 21 && a.R <= 8 && a.R * a.S * 3 <= kStemKP &&
@@ -1782,7 +1983,35 @@ int LaunchStem(const ConvArgs& a, hipStream_t st) {
 
 // few-channel stem: x NHWC with C <= 4, w packed [Cout][160] (k = (r * S + s) * C + c, zero-padded),
 // R * S * C <= 160, f16 (dtype 1) / bf16 (2)
+namespace {
+template <class T, int kP>
+void LaunchRing(const ConvArgs& a, hipStream_t st) {
+  const int nstrip = (a.OH + kRingOut - 1) / kRingOut;
+  const dim3 grid(a.B * nstrip, (a.Cout + kStemBN - 1) / kStemBN);
+  const size_t dyn = static_cast<size_t>(RingLds(a, kP));
+  const int SP = RingSP(a);
+  if (a.in_scale) hipLaunchKernelGGL((stem_ring_kernel<T, kP, true>), grid, dim3(256), dyn, st, a, SP, nstrip);
+  else hipLaunchKernelGGL((stem_ring_kernel<T, kP, false>), grid, dim3(256), dyn, st, a, SP, nstrip);
+}
+}  // namespace
+
 int StemConv(const ConvArgs& a, int dtype, void* stream, int kp, int form) {
+  hipStream_t rst = static_cast<hipStream_t>(stream);
+  if ((dtype == 3 || dtype == 4) && kp == kWideKP) {  // fp32 strip form: weights [planes][Cout][192] bf16
+    const int planes = dtype == 3 ? 2 : 3;
+    if (form == 1 || !RingOk(a, planes, 4)) return -4;
+    if (planes == 2) LaunchRing<float, 2>(a, rst);
+    else LaunchRing<float, 3>(a, rst);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
+  // f16 / bf16 row-run weights: form 0 = the strip form where it applies, else the row-run kernel; 1 = the
+  // row-run kernel only; 3 = the strip form only
+  if ((dtype == 1 || dtype == 2) && kp == kWideKP && form != 1 && RingOk(a, 1, 2)) {
+    if (dtype == 1) LaunchRing<_Float16, 1>(a, rst);
+    else LaunchRing<__bf16, 1>(a, rst);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
+  if (form == 3) return -4;
   if (dtype == 3 || dtype == 4) {  // fp32 input, weights [planes][Cout][160] bf16 (ops.conv.pack_stem_weight_f32)
     const int planes = dtype == 3 ? 2 : 3;
     if (kp != kStemKP || form == 1) return -1;

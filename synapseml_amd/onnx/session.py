@@ -863,16 +863,20 @@ def _stem_f32_ok(rt, at, inp, w) -> bool:
 
 
 def _stem_kernel_conv(rt, at, inp, w, b, res, act, pro=None):
-    from ..ops.conv import pack_stem_weight, pack_stem_weight_f32, stem_conv_nhwc
+    from ..ops.conv import _PLANES, pack_stem_weight, pack_stem_weight_f32, stem_conv_nhwc, stem_ring_ok
 
     cache = rt.session.__dict__.setdefault("_stem_wk", {})
     f32 = inp.dtype == torch.float32
     mode = _stem_f32_mode(rt) if f32 else None
-    key = (w.data_ptr(), tuple(w.shape), w.dtype, mode)
+    nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+    if not inp.is_contiguous(memory_format=torch.channels_last):
+        inp = inp.contiguous(memory_format=torch.channels_last)
+    # the strip form (row-run K order) where it applies: stride-2 RGB stems
+    wide = stem_ring_ok(inp, w, strides, (pb[0], pb[1], pe[0], pe[1]), dil, _PLANES[mode] if f32 else 1)
+    key = (w.data_ptr(), tuple(w.shape), w.dtype, mode, wide)
     wk = cache.get(key)
     if wk is None:  # packed (fp32: and split into bf16 planes) once per weight
-        wk = cache[key] = pack_stem_weight_f32(w, mode) if f32 else pack_stem_weight(w)
-    nd, strides, dil, pb, pe = conv_args(at, inp.shape, w.shape)
+        wk = cache[key] = pack_stem_weight_f32(w, mode, wide) if f32 else pack_stem_weight(w, wide=True if wide else None)
     return stem_conv_nhwc(inp, wk, w.shape[2], w.shape[3], strides, (pb[0], pb[1], pe[0], pe[1]), dil,
                           bias=b, relu=2 if act == 1 else 0, res=res, in_affine=pro,
                           in_relu=bool(at.get("__pro_relu", 1)))

@@ -195,10 +195,37 @@ def stem_f32_supported(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), pad=(0, 
             and _PLANES[mode] * r * (W + 16) * 3 * 2 <= 34 * 1024 and r * (W + 16) * 3 // 4 <= 2048)
 
 
-def pack_stem_weight_f32(w: torch.Tensor, mode: str = "bf16x3") -> torch.Tensor:
+def pack_stem_weight_f32(w: torch.Tensor, mode: str = "bf16x3", wide: bool = False) -> torch.Tensor:
     """fp32 [Cout, 3, R, S] -> [planes, Cout, 160] bf16 (pack_stem_weight, then split_weight's RNE planes:
-    2 for bf16x3, 3 for bf16x6) - the fp32 stem kernel's weight operand, made once per model."""
-    return split_weight(pack_stem_weight(w.float(), wide=False), mode)
+    2 for bf16x3, 3 for bf16x6) - the fp32 stem kernel's weight operand, made once per model; ``wide``: the
+    row-run K order [planes, Cout, 192] of the strip form (``stem_ring_ok``)."""
+    return split_weight(pack_stem_weight(w.float(), wide=wide), mode)
+
+
+# SML_STEM_RING=0: the row-staged stem forms instead of the strip form (one block per 8 output rows, input rows
+# in an LDS ring, the weights in registers) for the stride-2 RGB stems
+_STEM_RING = os.environ.get("SML_STEM_RING", "1") != "0"
+
+
+def stem_ring_ok(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), pad=(0, 0), dil=(1, 1), planes: int = 1) -> bool:
+    """Whether the strip form of the stem (csrc/nn/conv_mfma.hip stem_ring_kernel, mirrors RingOk) takes this
+    conv: 3 channels, an even horizontal stride <= 4, R <= 8, S * 3 <= 24, pad_w <= 8, no dilation, output
+    rows of <= 128 pixels, 16-B aligned input rows and its LDS ring within 44 KB."""
+    if not _STEM_RING or x.dim() != 4 or w.dim() != 4 or x.shape[1] != 3 or w.shape[1] != 3:
+        return False
+    esize = x.element_size()
+    epc = 16 // esize
+    H, W = x.shape[2], x.shape[3]
+    r, s = w.shape[2], w.shape[3]
+    sh, sw = stride
+    if (sw % 2 or sw > 4 or s * 3 > STEM_WIDE_RP or not 1 <= r <= 8 or not 1 <= sh <= 4 or tuple(dil) != (1, 1)
+            or pad[1] > 8 or (W * 3) % epc or x.data_ptr() % 16):
+        return False
+    oh, ow = out_hw(H, W, r, s, stride, pad, dil)
+    cpr = W * 3 // epc
+    sp = (max((pad[1] + W) * 3, (ow - 1) * sw * 3 + STEM_WIDE_RP) + 15) // 8 * 8
+    return (0 < ow <= 128 and oh > 0 and r * cpr <= 2048 and sh * cpr <= 512
+            and (planes * (r + sh) + 1) * sp * 2 <= 44 * 1024)
 
 
 def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0), dil=(1, 1),
@@ -211,13 +238,16 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
     input channel: x' = x * scale + shift (ReLU'd with ``in_relu``) inside the kernel, padding taps 0 - an
     input BatchNormalization without its own pass. ``form`` (160-wide weights): 0 picks the row-staged kernel
     where it applies (3 channels, one block per output row of <= 128 pixels), 1 forces the 2-byte gather
-    kernel, 2 the row-staged one. fp32 ``x``: ``wk`` = pack_stem_weight_f32(w, mode), the bf16-plane kernel
-    (2 planes: 3 products per pair, 3 planes: 6), 3 channels and the row-staged geometry only."""
+    kernel, 2 the row-staged one; 192-wide weights: 0 picks the strip form (``stem_ring_ok``) where it applies,
+    1 forces the row-run kernel, 3 the strip form. fp32 ``x``: ``wk`` = pack_stem_weight_f32(w, mode), the bf16-plane kernel
+    (2 planes: 3 products per pair, 3 planes: 6), 3 channels and the row-staged geometry only (192-wide planes:
+    the strip form)."""
     B, C, H, W = x.shape
     if not x.is_contiguous(memory_format=torch.channels_last):
         x = x.contiguous(memory_format=torch.channels_last)
     if x.dtype == torch.float32:
-        if wk.dim() != 3 or wk.shape[0] not in (2, 3) or wk.shape[2] != STEM_KP or wk.dtype != torch.bfloat16 \
+        if wk.dim() != 3 or wk.shape[0] not in (2, 3) or wk.shape[2] not in (STEM_KP, STEM_WIDE_KP) \
+                or wk.dtype != torch.bfloat16 \
                 or not wk.is_contiguous():
             raise ValueError("fp32 stem weight must be pack_stem_weight_f32(w, mode)")
         cout = wk.shape[1]
@@ -250,7 +280,8 @@ def stem_conv_nhwc(x: torch.Tensor, wk: torch.Tensor, r: int, s: int, stride=(1,
 
 
 __all__ = ["supported", "pack_weight", "split_weight", "conv2d_nhwc", "out_hw", "F32_MODES", "stem_supported",
-           "pack_stem_weight", "stem_conv_nhwc", "stem_wide", "stem_f32_supported", "pack_stem_weight_f32"]
+           "pack_stem_weight", "stem_conv_nhwc", "stem_wide", "stem_f32_supported", "pack_stem_weight_f32",
+           "stem_ring_ok"]
 
 
 def conv2d_nhwc_general(x: torch.Tensor, wp: torch.Tensor, r: int, s: int, stride=(1, 1), pad=(0, 0, 0, 0),

@@ -356,7 +356,7 @@ def test_stem_kernel_matches_reference(dtype, geom):
     ref = F.conv2d(x.float(), w.float(), None, st, pd)
     torch.testing.assert_close(y.float(), ref.to(dtype).float(), rtol=0, atol=0)  # exact sum, one rounding
     if C == 3:  # the row-run form (SML_STEM_ROWRUN) and the 2-byte gather form agree exactly
-        yw = stem_conv_nhwc(x, pack_stem_weight(w, wide=True), k, k, (st, st), (pd, pd))
+        yw = stem_conv_nhwc(x, pack_stem_weight(w, wide=True), k, k, (st, st), (pd, pd), form=1)
         torch.testing.assert_close(yw.float(), ref.to(dtype).float(), rtol=0, atol=0)
         yg = stem_conv_nhwc(x, pack_stem_weight(w), k, k, (st, st), (pd, pd), form=1)
         torch.testing.assert_close(yg.float(), ref.to(dtype).float(), rtol=0, atol=0)
@@ -425,6 +425,69 @@ def test_stem_f32_kernel_matches_fp64(mode, geom):
         xa = torch.relu(xa) if in_relu else xa
         r3 = torch.relu(F.conv2d(xa, wf.double(), bias.double(), st, pd))
         assert (y3.double() - r3).abs().max().item() <= gate * r3.abs().max().item()
+
+
+_RING_GEOMS = [
+    # B, H, W, Cout, k, stride, pad
+    (3, 224, 224, 64, 7, 2, 3),   # the ResNet-50 stem: 14 strips of 8 output rows
+    (2, 40, 48, 64, 7, 2, 3),     # a partial last strip (OH = 20), a partial pixel tile
+    (2, 36, 40, 80, 5, 2, 2),     # a partial channel tile, even pad
+    (2, 21, 24, 36, 3, 2, 1),     # Cout % 8 != 0 (element-store epilogue), odd H
+    (1, 30, 32, 64, 8, 2, 3),     # 8 x 8 taps: K = 192, every run slot real
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("geom", _RING_GEOMS)
+def test_stem_ring_kernel_matches_reference(dtype, geom):
+    """The strip form of the stride-2 RGB stem (input rows in an LDS ring, fragments read straight from the
+    staged rows): small integers exact against the reference (f16 / bf16, and fp32 on bf16 planes), random data
+    within each precision's gate, with bias + ReLU + residual and the fused input affine (+ ReLU)."""
+    from synapseml_amd.ops.conv import pack_stem_weight, pack_stem_weight_f32, stem_conv_nhwc, stem_ring_ok
+
+    B, H, W, Co, k, st, pd = geom
+    f32 = dtype == torch.float32
+    pack = (lambda t: pack_stem_weight_f32(t, "bf16x3", wide=True)) if f32 else (lambda t: pack_stem_weight(t, wide=True))
+    g = torch.Generator().manual_seed(11)
+    x = torch.randint(-3, 4, (B, 3, H, W), generator=g).to(dtype).cuda().contiguous(memory_format=torch.channels_last)
+    w = torch.randint(-3, 4, (Co, 3, k, k), generator=g).to(dtype).cuda()
+    assert stem_ring_ok(x, w, (st, st), (pd, pd), (1, 1), 2 if f32 else 1)
+    if k * k * 3 > 160:  # the Python front end's K bound (the strip form itself takes R * 24 <= 192)
+        with pytest.raises(ValueError):
+            stem_conv_nhwc(x, pack(w), k, k, (st, st), (pd, pd), form=3)
+        return
+    y = stem_conv_nhwc(x, pack(w), k, k, (st, st), (pd, pd), form=3)
+    ref = F.conv2d(x.double(), w.double(), None, st, pd)
+    torch.testing.assert_close(y.double(), ref.to(dtype).double(), rtol=0, atol=0)
+    torch.manual_seed(12)
+    xf = torch.randn(B, 3, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    wf = (torch.randn(Co, 3, k, k, device="cuda") / (3 * k * k) ** 0.5).to(dtype)
+    bias = torch.randn(Co, device="cuda")
+    res = torch.randn(ref.shape, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    wk = pack(wf)
+    y2 = stem_conv_nhwc(xf, wk, k, k, (st, st), (pd, pd), bias=bias, relu=2, res=res, form=3)
+    r2 = torch.relu(F.conv2d(xf.double(), wf.double(), bias.double(), st, pd) + res.double())
+    sc = torch.rand(3, device="cuda") + 0.5
+    sh = torch.randn(3, device="cuda")
+    outs = [(y2, r2)]
+    for in_relu in (False, True):
+        y3 = stem_conv_nhwc(xf, wk, k, k, (st, st), (pd, pd), bias=bias, relu=1, in_affine=(sc, sh), in_relu=in_relu,
+                            form=3)
+        xa = xf.double() * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1)
+        xa = torch.relu(xa) if in_relu else xa
+        if not f32:
+            xa = xa.to(dtype).double()  # the kernel rounds the affine'd input to the storage type
+        outs.append((y3, torch.relu(F.conv2d(xa, wf.double(), bias.double(), st, pd))))
+    for yy, rr in outs:
+        if f32:
+            assert (yy.double() - rr).abs().max().item() <= 1e-5 * rr.abs().max().item()
+        else:
+            tol = 2e-2 if dtype == torch.float16 else 8e-2
+            torch.testing.assert_close(yy.double(), rr, rtol=tol, atol=tol)
+    # the strip form and the row-staged form agree (f16 / bf16: both one rounding of an fp32 sum)
+    if not f32 and W % 8 == 0 and ref.shape[3] <= 128 and k * k * 3 <= 160:
+        yr = stem_conv_nhwc(xf, pack_stem_weight(wf), k, k, (st, st), (pd, pd), bias=bias, relu=2, res=res, form=2)
+        torch.testing.assert_close(y2.float(), yr.float(), rtol=1e-2, atol=1e-2)
 
 
 def test_resnet_fp32_session_stem_uses_f32_kernel():
