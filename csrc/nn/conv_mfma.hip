@@ -1774,7 +1774,8 @@ __global__ __launch_bounds__(256) void stem_f32_kernel(ConvArgs a) {
 constexpr int kRingOut = 8;  // output rows per block
 
 template <class T, int kP, bool kPro>
-__global__ __launch_bounds__(256) void stem_ring_kernel(ConvArgs a, int SP, int nstrip) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kP > 2 ? 1 : 2, 2))) void stem_ring_kernel(ConvArgs a, int SP,
+                                                                                         int nstrip) {
   typedef typename std::conditional<sizeof(T) == 4, __bf16, T>::type MT;  // MFMA operand type
   typedef typename Vec<MT>::type V8;
   constexpr int C = 3, TM = 4, TN = 2, kKS = kWideKP / 32, EPC = 16 / static_cast<int>(sizeof(T));
