@@ -10,6 +10,7 @@
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <algorithm>
 #include <cstdint>
@@ -149,7 +150,10 @@ __global__ __launch_bounds__(kThreads) void gap_nhwc_kernel(const T* __restrict_
 // of consecutive channels for fp16 / bf16. C % 8 == 0 (the host checks).
 // Optional epilogue y = relu?(max + shift[c]): the producing conv's bias + ReLU moved past the pool
 // (x -> round(x + b), ReLU are monotone, so max commutes with them exactly) - a quarter of the writes.
-template <typename T>
+// KH / KW > 0: a compile-time window (the 3x3 image-stem pool): every tap's load is issued before the first max
+// (row / column clamped into the image, out-of-range taps masked), instead of one load latency per tap of the
+// runtime loop.
+template <typename T, int KH = 0, int KW = 0>
 __global__ __launch_bounds__(kThreads) void maxpool_nhwc_kernel(const T* __restrict__ x, int N, int H, int W, int C,
                                                                 int kh, int kw, int sh, int sw, int ph, int pw,
                                                                 int OH, int OW, const float* __restrict__ shift,
@@ -167,7 +171,25 @@ __global__ __launch_bounds__(kThreads) void maxpool_nhwc_kernel(const T* __restr
 #pragma unroll
     for (int j = 0; j < kVec; ++j) m[j] = -INFINITY;
     const int h0 = oh * sh - ph, w0 = ow * sw - pw;
-    for (int i = 0; i < kh; ++i) {
+    if constexpr (KH > 0 && KW > 0) {
+      Vec8<T> v[KH][KW];
+#pragma unroll
+      for (int i = 0; i < KH; ++i)
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+          const int hh = min(max(h0 + i, 0), H - 1), ww = min(max(w0 + k, 0), W - 1);
+          v[i][k] = *reinterpret_cast<const Vec8<T>*>(x + ((static_cast<int64_t>(n) * H + hh) * W + ww) * C + cg * kVec);
+        }
+#pragma unroll
+      for (int i = 0; i < KH; ++i)
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+          if (h0 + i < 0 || h0 + i >= H || w0 + k < 0 || w0 + k >= W) continue;
+#pragma unroll
+          for (int j = 0; j < kVec; ++j) m[j] = fmaxf(m[j], ld<T>(v[i][k].v, j));
+        }
+    }
+    for (int i = 0; i < (KH > 0 ? 0 : kh); ++i) {
       const int hh = h0 + i;
       if (hh < 0 || hh >= H) continue;
       for (int k = 0; k < kw; ++k) {
@@ -237,16 +259,23 @@ void MaxPoolNhwc(const void* x, int N, int H, int W, int C, int kh, int kw, int 
   if (total <= 0) return;
   auto s = static_cast<hipStream_t>(stream);
   const int g = static_cast<int>(std::min<int64_t>((total + kThreads - 1) / kThreads, 1 << 20));
-  if (dtype == 1)
-    hipLaunchKernelGGL(maxpool_nhwc_kernel<__half>, dim3(g), dim3(kThreads), 0, s, static_cast<const __half*>(x), N, H,
-                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu, static_cast<__half*>(y));
-  else if (dtype == 2)
-    hipLaunchKernelGGL(maxpool_nhwc_kernel<__hip_bfloat16>, dim3(g), dim3(kThreads), 0, s,
-                       static_cast<const __hip_bfloat16*>(x), N, H, W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu,
-                       static_cast<__hip_bfloat16*>(y));
-  else
-    hipLaunchKernelGGL(maxpool_nhwc_kernel<float>, dim3(g), dim3(kThreads), 0, s, static_cast<const float*>(x), N, H,
-                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu, static_cast<float*>(y));
+  auto launch = [&](auto tag, auto win) {
+    using TT = decltype(tag);
+    constexpr int K = decltype(win)::value;
+    hipLaunchKernelGGL((maxpool_nhwc_kernel<TT, K, K>), dim3(g), dim3(kThreads), 0, s, static_cast<const TT*>(x), N, H,
+                       W, C, kh, kw, sh, sw, ph, pw, OH, OW, shift, relu, static_cast<TT*>(y));
+  };
+  const bool k3 = kh == 3 && kw == 3;
+  if (dtype == 1) {
+    if (k3) launch(__half{}, std::integral_constant<int, 3>{});
+    else launch(__half{}, std::integral_constant<int, 0>{});
+  } else if (dtype == 2) {
+    if (k3) launch(__hip_bfloat16{}, std::integral_constant<int, 3>{});
+    else launch(__hip_bfloat16{}, std::integral_constant<int, 0>{});
+  } else {
+    if (k3) launch(float{}, std::integral_constant<int, 3>{});
+    else launch(float{}, std::integral_constant<int, 0>{});
+  }
   NN_HIP_CHECK(hipGetLastError());
 }
 
